@@ -1,0 +1,192 @@
+"""bench.py - images/sec of the YOLO-SOD inference step on MI355X (BASELINE.json metric), one process per GPU.
+
+step = one predictor pass over one batch of synthetic 640x640 images already resident in HBM:
+       backbone/neck convs (PyTorch-ROCm) + HIP MAFN operators + HIP Detect decode + HIP batched NMS
+       (+ for N > 1 the RCCL all-gather of the padded detections: the path's single exchange step).
+Weak scaling: every rank processes its own batch of 32 images; value = N * 32 * K / max-over-ranks(time of K steps).
+
+Usage: python bench.py [--gpus N --steps K --warmup W]; for N > 1 launch with
+       python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 --master-port P \
+              bench.py --gpus N --steps K --warmup W
+Rank 0 prints ONE JSON line (plus `roofline` of the dominant HIP operator, measured live with HIP events inside
+the timed region, and `cpu_baseline` = the oracle CPU model timed on the host cores, rank 0 at N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import torch
+import torch.distributed as dist
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+import yolosod_import  # noqa: E402,F401
+
+from yolosod_amd import _hip, perf  # noqa: E402
+from yolosod_amd.engine.predictor import DetectionPredictor, gather_detections  # noqa: E402
+from yolosod_amd.nn.tasks import build_model  # noqa: E402
+
+METRIC = "images/sec @640×640 bs=32, 1→8 MI355X; mAP@0.5:0.95 parity vs CPU ref"
+CONFIGS = {
+    # name: (yaml, imgsz, batch per GPU)
+    "n640": ("yolov12-sod-fusion-v5-simple.yaml", 640, 32),
+    "n1280": ("yolov12-sod-fusion-v5-simple.yaml", 1280, 8),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(cfg_yaml, imgsz, n_images, threads):
+    """Oracle CPU model (fp32 PyTorch-CPU restatement + C NMS) on a bounded sample of the same workload."""
+    from oracle.model_ref import build_cpu_model
+    from oracle.nms import non_max_suppression_ref
+    torch.set_num_threads(threads)
+    m = build_cpu_model(cfg_yaml)
+    g = torch.Generator().manual_seed(0)
+    x = torch.rand(n_images, 3, imgsz, imgsz, generator=g)
+    with torch.inference_mode():
+        m(x[:1])  # warm-up
+        t0 = time.perf_counter()
+        done = 0
+        for i in range(0, n_images, 8):
+            y = m(x[i:i + 8])[0]
+            non_max_suppression_ref(y.numpy().copy(), 0.25, 0.7, max_det=300)
+            done += y.shape[0]
+        dt = time.perf_counter() - t0
+    return {"value": round(done / dt, 3), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"{done} images {imgsz}x{imgsz} (forward+decode+NMS, oracle fp32 CPU model, "
+                      f"torch threads={threads}), {dt:.1f}s"}
+
+
+def load_traffic():
+    p = ROOT / "profiles" / "traffic.json"
+    if p.exists():
+        try:
+            return json.loads(p.read_text())
+        except Exception:
+            return None
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="n640", choices=list(CONFIGS))
+    ap.add_argument("--conf", type=float, default=0.25)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-images", type=int, default=16)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    cfg_yaml, imgsz, bs = CONFIGS[args.config]
+    model = build_model(cfg_yaml, seed=0, device=dev)
+    predictor = DetectionPredictor(model, conf=args.conf, iou=0.7, max_det=300)
+    g = torch.Generator().manual_seed(1000 + rank)
+    x = torch.rand(bs, 3, imgsz, imgsz, generator=g).to(dev)
+
+    def step():
+        out, counts, _ = predictor.predict_padded(x)
+        if world > 1:
+            gather_detections(out, counts)
+        return counts
+
+    t_w = time.perf_counter()
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    log(f"[rank {rank}] warmup {args.warmup} steps {time.perf_counter() - t_w:.2f}s")
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    with _hip.op_timer() as timer:
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t1 = time.perf_counter()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    elapsed = float(elapsed.item())
+    durs = timer.durations_ms()
+
+    # per-operator live timings (HIP events on the launch stream) -> roofline of the dominant operator
+    agg = {}
+    for key, ms in durs:
+        a = agg.setdefault(key, [0.0, 0])
+        a[0] += ms
+        a[1] += 1
+    ops = []
+    for key, (tot, n) in agg.items():
+        nbytes, flops = perf.op_cost(key)
+        avg = tot / n
+        ops.append({"op": key[0], "shape": list(key[1]), "launches": n, "avg_ms": round(avg, 4),
+                    "total_ms_per_step": round(tot / args.steps, 4),
+                    "GBps": round(nbytes / (avg * 1e-3) / 1e9, 1),
+                    "TFLOPs": round(flops / (avg * 1e-3) / 1e12, 2), "bytes": nbytes, "flops": flops})
+    ops.sort(key=lambda o: -o["total_ms_per_step"])
+    dom = ops[0]
+    bound = perf.bound_of(dom["op"])
+    if bound == "mfma":
+        achieved, peak, unit = dom["TFLOPs"], perf.PEAK_FP32_MFMA_TFLOPS, "TFLOP/s"
+    else:
+        achieved, peak, unit = dom["GBps"], perf.PEAK_HBM_GBS, "GB/s"
+    traffic = load_traffic()
+    roofline = {"bound": bound, "achieved": achieved, "peak": peak, "unit": unit,
+                "frac": round(achieved / peak, 4),
+                "traffic": (traffic or {}).get(f"{dom['op']}:{'x'.join(map(str, dom['shape']))}"),
+                "kernel": f"{dom['op']}{tuple(dom['shape'])} (one C-ABI call = its launch sequence)",
+                "algorithmic_per_launch": dom["flops"] if bound == "mfma" else dom["bytes"]}
+
+    total_imgs = world * bs * args.steps
+    value = total_imgs / elapsed
+    hip_ms = sum(o["total_ms_per_step"] for o in ops)
+    result = {
+        "metric": METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic: torch.rand images in HBM, seed-0 random-init weights of the paper model",
+        "config": {"workload": f"yolov12n-sod (paper YAML) {imgsz}x{imgsz}, {bs} images per GPU, fused fp32 "
+                               f"forward + decode + NMS(conf={args.conf}, iou=0.7)",
+                   "imgsz": imgsz, "batch_per_gpu": bs, "global_batch": bs * world, "parallelism": f"dp{world}"},
+        "roofline": roofline,
+        "hip_ops_ms_per_step": round(hip_ms, 3),
+        "hip_ops": [{k: v for k, v in o.items() if k not in ("bytes", "flops")} for o in ops],
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        threads = min(int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)), 16)
+        try:
+            result["cpu_baseline"] = cpu_baseline(cfg_yaml, imgsz, args.cpu_images, threads)
+        except Exception as e:  # report, never hide
+            result["cpu_baseline"] = {"error": repr(e)}
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,100 @@
+/*
+ * yolosod_hip.h - C ABI of the MI355X (gfx950) hot path of YOLO-SOD inference.
+ *
+ * Library: yolo-sod_amd/lib/libyolosod_hip.so  (built by `python -m yolosod_amd.build` / __graft_entry__.build()).
+ *
+ * Conventions (every entry point):
+ *   - all tensor arguments are DEVICE pointers to contiguous fp32 (or int32) buffers in the reference's layout
+ *     (NCHW feature maps, PyTorch Linear/Conv weight layouts), allocated and owned by the caller;
+ *   - `workspace` is a caller-owned device buffer of at least yolosod_<op>_workspace(...) bytes;
+ *   - `stream` is a hipStream_t; launches are stream-ordered, nothing synchronises the host;
+ *   - return 0 on success, nonzero on error (message in yolosod_last_error(), thread-local).
+ *   - outputs never alias inputs, except yolosod_nms with in_place=1 which rewrites pred[:, 0:4] to xyxy,
+ *     mirroring non_max_suppression(in_place=True).
+ *
+ * Each entry point replaces one reference interface (quitedob/yolo-sod, file:line):
+ */
+#ifndef YOLOSOD_HIP_H
+#define YOLOSOD_HIP_H
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+int yolosod_abi_version(void);
+const char* yolosod_last_error(void);
+
+/* SE / SE_Block.forward            ultralytics/nn/modules/smallobj_modules.py:84-92
+ * y = x * sigmoid(fc2(relu(fc1(mean_hw(x)))));  fc1: [hidden,C]+[hidden], fc2: [C,hidden]+[C]. */
+size_t yolosod_se_workspace(int B, int C, int H, int W);
+int yolosod_se_forward(const float* x, float* y, int B, int C, int H, int W, const float* fc1_w, const float* fc1_b,
+                       const float* fc2_w, const float* fc2_b, int hidden, void* workspace, size_t workspace_bytes,
+                       void* stream);
+
+/* CBAM_Block.forward               ultralytics/nn/modules/cbam_block.py:52-55 (ChannelAttention :19-23,
+ * SpatialAttention :32-37).  fc0: [hidden,C] (channel_attention.fc.0), fc2: [C,hidden] (fc.2), sa_w: [1,2,7,7]. */
+size_t yolosod_cbam_workspace(int B, int C, int H, int W);
+int yolosod_cbam_forward(const float* x, float* y, int B, int C, int H, int W, const float* fc0_w,
+                         const float* fc2_w, int hidden, const float* sa_w, void* workspace, size_t workspace_bytes,
+                         void* stream);
+
+/* CA_Block.forward                 ultralytics/nn/modules/ca_block.py:38-59 (bn1 in eval mode, not fused). */
+size_t yolosod_ca_workspace(int B, int C, int H, int W);
+int yolosod_ca_forward(const float* x, float* y, int B, int C, int H, int W, const float* conv1_w,
+                       const float* conv1_b, int mip, const float* bn_w, const float* bn_b, const float* bn_mean,
+                       const float* bn_var, float bn_eps, const float* convh_w, const float* convh_b,
+                       const float* convw_w, const float* convw_b, void* workspace, size_t workspace_bytes,
+                       void* stream);
+
+/* A2_Attn.forward (Conv layers in fused form, nn/tasks.py:227-255)   ultralytics/nn/modules/a2_attn.py:35-69
+ * proj / oproj: [C,C] fused conv weight + bias (SiLU), MHA: in_proj [3C,C]+[3C], out_proj [C,C]+[C]. */
+size_t yolosod_a2_workspace(int B, int C, int H, int W, int num_areas);
+int yolosod_a2_forward(const float* x, float* y, int B, int C, int H, int W, int num_areas, int num_heads,
+                       const float* proj_w, const float* proj_b, const float* ln_w, const float* ln_b, float ln_eps,
+                       const float* in_proj_w, const float* in_proj_b, const float* mha_out_w,
+                       const float* mha_out_b, const float* oproj_w, const float* oproj_b, void* workspace,
+                       size_t workspace_bytes, void* stream);
+
+/* SwinBlock.forward                ultralytics/nn/modules/blocks_transformer.py:150-171 (WindowAttention
+ * :100-131, window_partition :8-47, window_reverse :49-79).  dw: [C,1,3,3]; in_proj [3C,C]; mlp1 [hid,C];
+ * mlp2 [C,hid]; pw [C,C,1,1]; bn in eval mode (not fused by fuse()). */
+size_t yolosod_swin_workspace(int B, int C, int H, int W, int window, int mlp_hidden);
+int yolosod_swin_forward(const float* x, float* y, int B, int C, int H, int W, int num_heads, int window,
+                         const float* dw_w, const float* ln1_w, const float* ln1_b, float ln1_eps,
+                         const float* in_proj_w, const float* in_proj_b, const float* out_proj_w,
+                         const float* out_proj_b, const float* ln2_w, const float* ln2_b, float ln2_eps,
+                         const float* mlp1_w, const float* mlp1_b, int mlp_hidden, const float* mlp2_w,
+                         const float* mlp2_b, const float* pw_w, const float* bn_w, const float* bn_b,
+                         const float* bn_mean, const float* bn_var, float bn_eps, void* workspace,
+                         size_t workspace_bytes, void* stream);
+
+/* Detect._inference (decode)       ultralytics/nn/modules/head.py:100-131, DFL block.py:79-82,
+ * make_anchors / dist2bbox utils/tal.py:333-357.
+ * maps: host array of nl device pointers, map i = [B, 4*reg_max+nc, heights[i], widths[i]];
+ * y: [B, 4+nc, A] (xywh * stride, sigmoid scores), A = sum_i heights[i]*widths[i]. */
+int yolosod_detect_decode(int nl, const float* const* maps, const int* heights, const int* widths,
+                          const float* strides, int B, int nc, int reg_max, float* y, void* stream);
+
+/* non_max_suppression + torchvision.ops.nms   ultralytics/utils/ops.py:167-316 (nms call :296).
+ * pred: [B, 4+nc, A] xywh (rewritten to xyxy in place when in_place); classes: device int32[n_classes] or NULL;
+ * out: [B, max_det, 6] rows (x1,y1,x2,y2,conf,cls) in kept order, zero padded; counts: [B];
+ * out_index: [B, max_det] anchor index of each kept row (-1 padded). */
+size_t yolosod_nms_workspace(int B, int nc, int A, int multi_label);
+int yolosod_nms(float* pred, int B, int nc, int A, float conf_thres, double iou_thres, const int* classes,
+                int n_classes, int agnostic, int multi_label, int max_det, int max_nms, float max_wh, int in_place,
+                float* out, int* counts, int* out_index, void* workspace, size_t workspace_bytes, void* stream);
+
+/* Building blocks, exported for unit tests (no single reference interface):
+ * C(b,m,n) = act(sum_k A(b,m,k) B(b,k,n) + bias) + res;  A K-contiguous; B K- or N-contiguous. */
+int yolosod_gemm_f32(const float* A, long a_bs, int lda, const float* B, long b_bs, int ldb, int b_kcontig, float* C,
+                     long c_bs, int ldc, int M, int N, int K, int batch, const float* bias, int bias_mode, int act,
+                     const float* res, void* stream);
+int yolosod_layernorm(const float* x, float* y, long rows, int C, const float* w, const float* b, float eps,
+                      void* stream);
+int yolosod_attention(const float* qkv, float* out, long n_seq, int L, int C, int heads, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* YOLOSOD_HIP_H */

@@ -1,0 +1,83 @@
+"""ORACLE - TEST INFRASTRUCTURE ONLY (see oracle/ops_ref.py header for the rules).
+
+Whole-model CPU reference: the product's graph builder (``yolosod_amd.nn.tasks.parse_model``, pinned by the
+seed-0 state_dict hash in tests/golden/model_manifest.json) instantiated with CPU operator classes whose forward
+is the restatement in ``oracle/ops_ref.py``. Same parameter names, same RNG order, so a product model's
+``state_dict`` loads unchanged. Used for end-to-end parity and as bench.py's ``cpu_baseline``.
+"""
+from __future__ import annotations
+
+import torch
+
+from yolosod_import import yolosod_amd  # noqa: F401
+from yolosod_amd.nn import modules as M
+from yolosod_amd.nn import tasks as T
+
+from . import ops_ref as R
+
+
+def _d(t):
+    return t.detach()
+
+
+class SE_CPU(M.SE):
+    def forward(self, x):
+        b, c, h, w = x.shape
+        self._maybe_build(c, x.device)
+        return R.se_ref(x, _d(self.fc1.weight), _d(self.fc1.bias), _d(self.fc2.weight), _d(self.fc2.bias))
+
+
+class CBAM_CPU(M.CBAM_Block):
+    def forward(self, x):
+        fc = self.channel_attention.fc
+        return R.cbam_ref(x, _d(fc[0].weight), _d(fc[2].weight), _d(self.spatial_attention.conv1.weight))
+
+
+class CA_CPU(M.CA_Block):
+    def forward(self, x):
+        bn = self.bn1
+        return R.ca_ref(x, _d(self.conv1.weight), _d(self.conv1.bias), _d(bn.weight), _d(bn.bias),
+                        _d(bn.running_mean), _d(bn.running_var), bn.eps, _d(self.conv_h.weight),
+                        _d(self.conv_h.bias), _d(self.conv_w.weight), _d(self.conv_w.bias))
+
+
+class A2_CPU(M.A2_Attn):
+    def forward(self, x):
+        pw, pb = M.conv_weight_bias(self.proj)
+        ow, ob = M.conv_weight_bias(self.out_proj)
+        at = self.attention
+        return R.a2_ref(x, self.num_areas, self.num_heads, pw, pb, _d(self.layer_norm.weight),
+                        _d(self.layer_norm.bias), self.layer_norm.eps, _d(at.in_proj_weight), _d(at.in_proj_bias),
+                        _d(at.out_proj.weight), _d(at.out_proj.bias), ow, ob)
+
+
+class Swin_CPU(M.SwinBlock):
+    def forward(self, x):
+        wa = self.window_attn
+        return R.swin_ref(x, wa.attn.num_heads, wa.window_size, _d(self.dw.weight), _d(wa.norm1.weight),
+                          _d(wa.norm1.bias), wa.norm1.eps, _d(wa.attn.in_proj_weight), _d(wa.attn.in_proj_bias),
+                          _d(wa.attn.out_proj.weight), _d(wa.attn.out_proj.bias), _d(wa.norm2.weight),
+                          _d(wa.norm2.bias), wa.norm2.eps, _d(wa.mlp[0].weight), _d(wa.mlp[0].bias),
+                          _d(wa.mlp[2].weight), _d(wa.mlp[2].bias), _d(self.pw.weight), _d(self.bn.weight),
+                          _d(self.bn.bias), _d(self.bn.running_mean), _d(self.bn.running_var), self.bn.eps)
+
+
+class Detect_CPU(M.Detect):
+    def _inference(self, x):
+        return R.decode_ref(x, [float(s) for s in self.stride], self.nc, self.reg_max)
+
+
+REGISTRY = {"SE": SE_CPU, "SE_Block": SE_CPU, "CBAM_Block": CBAM_CPU, "CA_Block": CA_CPU, "A2_Attn": A2_CPU,
+            "SwinBlock": Swin_CPU, "Detect": Detect_CPU}
+
+OP_CLASSES = {"SE_Block": SE_CPU, "CBAM_Block": CBAM_CPU, "CA_Block": CA_CPU, "A2_Attn": A2_CPU,
+              "SwinBlock": Swin_CPU}
+
+
+def build_cpu_model(cfg="yolov12-sod-fusion-v5-simple.yaml", seed=0, fuse=True, dtype=torch.float32):
+    """Seed-0 model with oracle operators on the CPU (eval, fused like AutoBackend)."""
+    torch.manual_seed(seed)
+    m = T.DetectionModel(cfg, registry=REGISTRY)
+    if fuse:
+        m.fuse()
+    return m.to(dtype).eval()

@@ -1,0 +1,55 @@
+"""GPU end-to-end: the seed-0 paper model (backbone on PyTorch-ROCm + HIP hot path) against the reference's fused
+fp32 CPU forward (golden) and against the oracle CPU model; batch-size invariance at the BASELINE batch (bs=32)."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from oplib import tol_close
+
+pytestmark = pytest.mark.gpu
+
+ATOL = 1e-3
+
+
+@pytest.fixture(scope="module")
+def gpu_model(cuda):
+    from yolosod_amd.nn.tasks import build_model
+    return build_model("yolov12-sod-fusion-v5-simple.yaml", seed=0, device=cuda)
+
+
+def test_model_matches_reference_golden(gpu_model, cuda):
+    g = torch.Generator().manual_seed(0)
+    x = torch.rand(2, 3, 256, 256, generator=g)
+    with torch.inference_mode():
+        y = gpu_model(x.to(cuda))[0].cpu()
+    ok, err, _ = tol_close(y, torch.from_numpy(golden("model_out_256")["y"]), ATOL, 0.0)
+    assert ok, f"max abs err {err:.3g}"
+
+
+def test_model_640_matches_oracle(gpu_model, cuda):
+    from oracle.model_ref import build_cpu_model
+    cpu = build_cpu_model()
+    cpu.load_state_dict({k: v.cpu() for k, v in gpu_model.state_dict().items()})
+    g = torch.Generator().manual_seed(1)
+    x = torch.rand(1, 3, 640, 640, generator=g)
+    with torch.inference_mode():
+        y = gpu_model(x.to(cuda))[0].cpu()
+        ref = cpu(x)[0]
+    ok, err, _ = tol_close(y, ref, ATOL, 0.0)
+    assert ok, f"max abs err {err:.3g}"
+
+
+def test_predictor_bs32_batch_invariance(gpu_model, cuda):
+    from yolosod_amd.engine.predictor import DetectionPredictor
+    pred = DetectionPredictor(gpu_model, conf=0.0005, iou=0.7)
+    g = torch.Generator().manual_seed(2)
+    x = torch.rand(32, 3, 640, 640, generator=g).to(cuda)
+    with torch.inference_mode():
+        y32 = gpu_model(x)[0]
+        y1 = torch.cat([gpu_model(x[i:i + 1])[0] for i in (0, 17, 31)])
+    ok, err, _ = tol_close(y32[[0, 17, 31]].cpu(), y1.cpu(), ATOL, 0.0)
+    assert ok, err
+    out, counts, index = pred.predict_padded(x)
+    assert out.shape == (32, 300, 6) and counts.shape == (32,)
+    assert int(counts.min()) >= 0 and int(counts.max()) <= 300

@@ -1,0 +1,59 @@
+"""GPU NMS: bit-exact kept rows, counts, anchor indices and in-place rewrite vs the reference fixtures and the
+oracle (including ties, class filter, agnostic, multi-label, max_nms / max_det cuts, empty, IoU threshold 0)."""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+import recipes
+from conftest import golden
+from oracle.nms import non_max_suppression_ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _run_gpu(pred_np, cuda, **kw):
+    from yolosod_amd.utils.ops import non_max_suppression_padded
+    p = torch.from_numpy(pred_np.copy()).to(cuda)
+    out, counts, index = non_max_suppression_padded(p, **kw)
+    return p.cpu().numpy(), out.cpu().numpy(), counts.cpu().numpy(), index.cpu().numpy()
+
+
+@pytest.mark.parametrize("name", list(recipes.NMS_CASES))
+def test_nms_matches_reference_fixture(name, cuda):
+    z = golden(name)
+    kw = json.loads(str(z["kwargs"]))
+    p_after, out, counts, index = _run_gpu(z["pred"], cuda, **kw)
+    assert np.array_equal(p_after, z["pred_after"]), "in-place xyxy rewrite differs"
+    assert counts.tolist() == z["counts"].tolist()
+    rows = np.concatenate([out[b, :c] for b, c in enumerate(counts)]) if counts.sum() else np.zeros((0, 6))
+    idx = np.concatenate([index[b, :c] for b, c in enumerate(counts)]) if counts.sum() else np.zeros((0,))
+    assert np.array_equal(rows, z["rows"]), "kept rows differ (must be bit-exact)"
+    assert np.array_equal(idx, z["index"]), "kept anchor indices differ"
+
+
+def test_nms_list_api(cuda):
+    from yolosod_amd.utils.ops import non_max_suppression
+    z = golden("nms_predict")
+    res = non_max_suppression(torch.from_numpy(z["pred"].copy()).to(cuda), 0.25, 0.7)
+    assert [len(r) for r in res] == z["counts"].tolist()
+    assert np.array_equal(torch.cat(res).cpu().numpy(), z["rows"])
+
+
+@pytest.mark.parametrize("B,A,clusters,kw", [
+    (8, 34000, 200, dict(conf_thres=0.25, iou_thres=0.7)),
+    (4, 34000, 60, dict(conf_thres=0.001, iou_thres=0.7, multi_label=True)),
+    (2, 34000, 3000, dict(conf_thres=0.05, iou_thres=0.5, max_det=1000)),
+    (2, 136000, 400, dict(conf_thres=0.25, iou_thres=0.7)),
+])
+def test_nms_full_size_vs_oracle(B, A, clusters, kw, cuda):
+    pred = recipes.synthetic_predictions(1000 + B + A, B, A, 10, n_clusters=clusters)
+    p_after, out, counts, index = _run_gpu(pred, cuda, **kw)
+    ref = pred.copy()
+    rows, idx = non_max_suppression_ref(ref, **kw)
+    assert np.array_equal(p_after, ref)
+    assert counts.tolist() == [len(r) for r in rows]
+    for b in range(B):
+        assert np.array_equal(out[b, :counts[b]], rows[b]), b
+        assert np.array_equal(index[b, :counts[b]], idx[b]), b

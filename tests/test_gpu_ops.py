@@ -1,0 +1,150 @@
+"""GPU parity of the HIP MAFN operators and Detect decode.
+
+Every HIP output is compared with (a) the golden output of the reference module on the same inputs / parameters
+(tests/golden, produced by the reference in fp32 on CPU) and (b) the oracle restatement evaluated in float64 on
+the CPU. Tolerance: BASELINE.json north star, |y - ref| <= 1e-3 absolute (fp32), plus a relative 1e-4 check
+against the fp64 oracle that keeps the test meaningful where outputs are large.
+"""
+import numpy as np
+import pytest
+import torch
+
+import recipes
+from conftest import golden
+from oplib import build_fixture_module, tol_close
+from oracle import ops_ref as R
+from oracle.model_ref import OP_CLASSES
+
+pytestmark = pytest.mark.gpu
+
+ATOL = 1e-3  # north-star fp32 tolerance
+
+
+def _oracle64(name, x):
+    m, _ = build_fixture_module(name, OP_CLASSES)
+    with torch.inference_mode():
+        return m.double()(x.double())
+
+
+@pytest.mark.parametrize("name", list(recipes.OPS))
+def test_op_matches_reference_fixture(name, cuda):
+    z = golden(f"ops_{name}")
+    m, sha = build_fixture_module(name)
+    assert sha == str(z["params_sha256"])
+    x = torch.from_numpy(z["x"])
+    with torch.inference_mode():
+        y = m.to(cuda)(x.to(cuda)).cpu()
+    ok, err, _ = tol_close(y, torch.from_numpy(z["y"]), ATOL, 0.0)
+    assert ok, f"{name}: max abs err vs reference {err:.3g}"
+    y64 = _oracle64(name, x)
+    ok, err, ratio = tol_close(y, y64, 1e-5, 1e-4)
+    assert ok, f"{name}: vs fp64 oracle max abs err {err:.3g} (ratio {ratio:.2f})"
+
+
+# real-model shapes (one image; the batch dimension is exercised by the model tests)
+REAL = {
+    "se_L1": ("SE_Block", (64,), (1, 32, 320, 320)),
+    "cbam_L4": ("CBAM_Block", (64, 128, 16), (1, 64, 160, 160)),
+    "swin_L9": ("SwinBlock", (256, 4, 7), (1, 256, 40, 40)),
+    "a2_L12": ("A2_Attn", (512, None, 8, 8), (2, 512, 20, 20)),
+    "cbam_L18": ("CBAM_Block", (256, 512, 16), (1, 256, 40, 40)),
+    "se_L23": ("SE_Block", (256,), (2, 128, 80, 80)),
+    "swin_L28": ("SwinBlock", (64, 2, 7), (1, 64, 160, 160)),
+    "ca_L32": ("CA_Block", (128, 256, 32), (2, 128, 80, 80)),
+    "swin_L28_1280": ("SwinBlock", (64, 2, 7), (1, 64, 320, 320)),
+    "a2_L12_1280": ("A2_Attn", (512, None, 8, 8), (1, 512, 40, 40)),
+}
+
+
+@pytest.mark.parametrize("name", list(REAL))
+def test_op_real_shapes_vs_oracle(name, cuda, monkeypatch):
+    monkeypatch.setitem(recipes.OPS, name, REAL[name])
+    m, _ = build_fixture_module(name)
+    x = recipes.make_input(name, REAL[name][2])
+    with torch.inference_mode():
+        y = m.to(cuda)(x.to(cuda)).cpu()
+    ref = _oracle64(name, x)
+    ok, err, ratio = tol_close(y, ref, ATOL, 0.0)
+    assert ok, f"{name}: max abs err {err:.3g}"
+    ok, err, ratio = tol_close(y, ref, 1e-5, 1e-4)
+    assert ok, f"{name}: rel check max abs err {err:.3g} ratio {ratio:.2f}"
+
+
+def test_se_chunked_equals_unchunked(cuda):
+    """The Infinity-Cache image chunking of the channel-attention ops must not change results (bitwise)."""
+    import importlib
+    import os
+    name = "se_c32_r64"
+    m, _ = build_fixture_module(name)
+    m = m.to(cuda)
+    x = torch.randn(9, 32, 64, 64, device=cuda)
+    with torch.inference_mode():
+        a = m(x)
+        b = torch.cat([m(x[i:i + 1]) for i in range(9)])
+    assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("M_,N,K,bkc", [(300, 192, 64, True), (1000, 64, 128, True), (129, 768, 256, True),
+                                         (512, 400, 512, False), (64, 1600, 64, False), (130, 13, 16, True),
+                                         (70, 150, 32, False)])
+def test_gemm_f32(M_, N, K, bkc, cuda):
+    from yolosod_amd import _hip
+    g = torch.Generator().manual_seed(M_ * 7 + N)
+    A = torch.randn(M_, K, generator=g)
+    B = torch.randn(N, K, generator=g) if bkc else torch.randn(K, N, generator=g)
+    bias = torch.randn(N, generator=g)
+    res = torch.randn(M_, N, generator=g)
+    ref = (A.double() @ (B.double().t() if bkc else B.double())) + bias.double()
+    ref = torch.nn.functional.silu(ref) + res.double()
+    C = _hip.gemm_f32(A.to(cuda), B.to(cuda), bkc, bias=bias.to(cuda), bias_mode=2, act=1, res=res.to(cuda)).cpu()
+    ok, err, _ = tol_close(C, ref, 1e-4, 1e-5)
+    assert ok, err
+
+
+@pytest.mark.parametrize("L,C,heads", [(49, 64, 2), (49, 256, 4), (36, 64, 2), (160, 512, 8), (160, 64, 8),
+                                        (320, 512, 8), (35, 64, 4), (7, 128, 1), (100, 256, 2)])
+def test_attention(L, C, heads, cuda):
+    from yolosod_amd import _hip
+    nseq = 5
+    g = torch.Generator().manual_seed(L * 31 + C)
+    qkv = torch.randn(nseq * L, 3 * C, generator=g)
+    q, k, v = qkv.double().view(nseq, L, 3, heads, C // heads).permute(2, 0, 3, 1, 4)
+    p = torch.softmax(q @ k.transpose(-1, -2) / (C // heads) ** 0.5, -1)
+    ref = (p @ v).transpose(1, 2).reshape(nseq * L, C)
+    out = _hip.attention(qkv.to(cuda), nseq, L, C, heads).cpu()
+    ok, err, _ = tol_close(out, ref, 1e-5, 1e-4)
+    assert ok, err
+
+
+@pytest.mark.parametrize("C", [64, 256, 512, 1000])
+def test_layernorm(C, cuda):
+    from yolosod_amd import _hip
+    x = torch.randn(333, C) * 3 + 1
+    w, b = torch.randn(C), torch.randn(C)
+    ref = torch.nn.functional.layer_norm(x.double(), (C,), w.double(), b.double(), 1e-5)
+    y = _hip.layernorm(x.to(cuda), w.to(cuda), b.to(cuda), 1e-5).cpu()
+    ok, err, _ = tol_close(y, ref, 1e-5, 1e-5)
+    assert ok, err
+
+
+def test_decode_matches_reference_fixture(cuda):
+    from yolosod_amd import _hip
+    z = golden("decode_128")
+    maps = [torch.from_numpy(z[f"map{i}"]).to(cuda) for i in range(4)]
+    y = _hip.detect_decode(maps, recipes.DECODE["strides"], recipes.DECODE["nc"]).cpu()
+    ok, err, _ = tol_close(y, torch.from_numpy(z["y"]), ATOL, 0.0)
+    assert ok, err
+    y64 = R.decode_ref([m.cpu().double() for m in maps], recipes.DECODE["strides"], recipes.DECODE["nc"])
+    ok, err, _ = tol_close(y, y64, 1e-5, 1e-6)
+    assert ok, err
+
+
+def test_decode_real_shapes(cuda):
+    from yolosod_amd import _hip
+    g = torch.Generator().manual_seed(5)
+    maps = [torch.randn(2, 74, s, s, generator=g) * 3 for s in (160, 80, 40, 20)]
+    y = _hip.detect_decode([m.to(cuda) for m in maps], [4.0, 8.0, 16.0, 32.0], 10).cpu()
+    ref = R.decode_ref([m.double() for m in maps], [4.0, 8.0, 16.0, 32.0], 10)
+    assert y.shape == (2, 14, 34000)
+    ok, err, _ = tol_close(y, ref, ATOL, 0.0)
+    assert ok, err

@@ -1,0 +1,77 @@
+"""CPU: the oracle (oracle/) and the host graph builder against golden fixtures produced by the reference."""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+import recipes
+from conftest import GOLDEN, golden
+from oplib import build_fixture_module, tol_close
+from oracle import ops_ref as R
+from oracle.model_ref import OP_CLASSES, build_cpu_model
+from oracle.nms import non_max_suppression_ref
+
+# the oracle restates the reference in the same fp32 CPU math; differences are op-ordering rounding only
+ATOL, RTOL = 2e-5, 2e-5
+
+
+@pytest.mark.parametrize("name", list(recipes.OPS))
+def test_oracle_op_matches_reference(name):
+    z = golden(f"ops_{name}")
+    m, sha = build_fixture_module(name, OP_CLASSES)
+    assert sha == str(z["params_sha256"]), "parameter recipe drifted from the fixture"
+    x = torch.from_numpy(z["x"])
+    with torch.inference_mode():
+        y = m(x)
+    ok, err, ratio = tol_close(y, torch.from_numpy(z["y"]), ATOL, RTOL)
+    assert ok, f"{name}: max abs err {err:.3g} (ratio {ratio:.2f})"
+
+
+def test_oracle_decode_matches_reference():
+    z = golden("decode_128")
+    maps = [torch.from_numpy(z[f"map{i}"]) for i in range(4)]
+    for i, m in enumerate(recipes.decode_maps()):
+        assert torch.equal(m, maps[i])
+    y = R.decode_ref(maps, recipes.DECODE["strides"], recipes.DECODE["nc"])
+    ok, err, _ = tol_close(y, torch.from_numpy(z["y"]), 1e-4, 1e-6)
+    assert ok, err
+
+
+@pytest.mark.parametrize("name", list(recipes.NMS_CASES))
+def test_oracle_nms_matches_reference(name):
+    z = golden(name)
+    seed, B, A, nc, kw = recipes.NMS_CASES[name]
+    kw = dict(kw)
+    tie = kw.pop("tie", False)
+    pred = recipes.synthetic_predictions(seed, B, A, nc, tie_scores=tie)
+    assert np.array_equal(pred, z["pred"])
+    p = pred.copy()
+    rows, idx = non_max_suppression_ref(p, **kw)
+    assert np.array_equal(p, z["pred_after"]), "in-place xywh->xyxy rewrite differs"
+    assert [len(r) for r in rows] == z["counts"].tolist()
+    assert np.array_equal(np.concatenate(rows), z["rows"])
+    assert np.array_equal(np.concatenate(idx), z["index"])
+
+
+def test_model_weights_match_reference_manifest():
+    from yolosod_amd.nn.tasks import DetectionModel, state_dict_sha256
+    man = json.loads((GOLDEN / "model_manifest.json").read_text())
+    for cfg in ("yolov12-sod-fusion-v5-simple", "yolov12m-sod"):
+        torch.manual_seed(0)
+        m = DetectionModel(cfg + ".yaml")
+        assert sum(p.numel() for p in m.parameters()) == man[cfg]["n_params"]
+        assert len(m.state_dict()) == man[cfg]["n_state"]
+        assert state_dict_sha256(m) == man[cfg]["state_dict_sha256"], cfg
+
+
+def test_oracle_model_forward_matches_reference():
+    torch.set_num_threads(min(8, torch.get_num_threads()))
+    m = build_cpu_model()
+    g = torch.Generator().manual_seed(0)
+    x = torch.rand(2, 3, 256, 256, generator=g)
+    with torch.inference_mode():
+        y = m(x)[0]
+    ref = torch.from_numpy(golden("model_out_256")["y"])
+    ok, err, _ = tol_close(y, ref, 1e-3, 1e-6)
+    assert ok, err

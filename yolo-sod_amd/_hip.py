@@ -1,0 +1,311 @@
+"""ctypes binding of the C ABI in ``include/yolosod_hip.h`` (``lib/libyolosod_hip.so``).
+
+PyTorch is only plumbing here: it owns device memory (caching allocator) and the current HIP stream. Every
+wrapper checks device / dtype / contiguity / shapes on the host before launching (a kernel never sees a shape it
+was not written for) and raises ``RuntimeError`` with the library's message on failure. There is no CPU
+fallback: calling an op on a CPU tensor, or without the built library, raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import torch
+
+LIB_PATH = Path(__file__).resolve().parent / "lib" / "libyolosod_hip.so"
+
+_c_float_p = ctypes.c_void_p
+_vp = ctypes.c_void_p
+_i = ctypes.c_int
+_l = ctypes.c_long
+_f = ctypes.c_float
+_d = ctypes.c_double
+_sz = ctypes.c_size_t
+
+# name -> (restype, argtypes)
+SIGNATURES = {
+    "yolosod_abi_version": (_i, []),
+    "yolosod_last_error": (ctypes.c_char_p, []),
+    "yolosod_se_workspace": (_sz, [_i, _i, _i, _i]),
+    "yolosod_se_forward": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _i, _vp, _sz, _vp]),
+    "yolosod_cbam_workspace": (_sz, [_i, _i, _i, _i]),
+    "yolosod_cbam_forward": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _sz, _vp]),
+    "yolosod_ca_workspace": (_sz, [_i, _i, _i, _i]),
+    "yolosod_ca_forward": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp,
+                                _vp, _vp, _sz, _vp]),
+    "yolosod_a2_workspace": (_sz, [_i, _i, _i, _i, _i]),
+    "yolosod_a2_forward": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp, _vp,
+                                _vp, _vp, _sz, _vp]),
+    "yolosod_swin_workspace": (_sz, [_i, _i, _i, _i, _i, _i]),
+    "yolosod_swin_forward": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp, _vp, _vp,
+                                  _f, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f, _vp, _sz, _vp]),
+    "yolosod_detect_decode": (_i, [_i, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp]),
+    "yolosod_nms_workspace": (_sz, [_i, _i, _i, _i]),
+    "yolosod_nms": (_i, [_vp, _i, _i, _i, _f, _d, _vp, _i, _i, _i, _i, _i, _f, _i, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "yolosod_gemm_f32": (_i, [_vp, _l, _i, _vp, _l, _i, _i, _vp, _l, _i, _i, _i, _i, _i, _vp, _i, _i, _vp, _vp]),
+    "yolosod_layernorm": (_i, [_vp, _vp, _l, _i, _vp, _vp, _f, _vp]),
+    "yolosod_attention": (_i, [_vp, _vp, _l, _i, _i, _i, _vp]),
+}
+
+_LIB = None
+
+
+def load_library() -> ctypes.CDLL:
+    """Load (once) the in-tree HIP library; raises if it has not been built."""
+    global _LIB
+    if _LIB is None:
+        if not LIB_PATH.exists():
+            raise RuntimeError(
+                f"yolosod_amd: HIP library {LIB_PATH} is missing - run __graft_entry__.build() "
+                "(or python yolo-sod_amd/build.py). There is no CPU fallback.")
+        lib = ctypes.CDLL(str(LIB_PATH))
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _LIB = lib
+    return _LIB
+
+
+class _OpTimer:
+    """Records HIP events around every C-ABI launch sequence (on the launch stream) while active."""
+
+    def __init__(self):
+        self.records = []
+
+    def durations_ms(self):
+        torch.cuda.synchronize()
+        out = []
+        for key, e0, e1 in self.records:
+            out.append((key, e0.elapsed_time(e1)))
+        return out
+
+
+_TIMER: _OpTimer | None = None
+
+
+class op_timer:
+    """``with op_timer() as t: ...`` -> ``t.durations_ms()`` = [((op, shape, extra), ms), ...] per launch."""
+
+    def __enter__(self):
+        global _TIMER
+        self.t = _OpTimer()
+        _TIMER = self.t
+        return self.t
+
+    def __exit__(self, *exc):
+        global _TIMER
+        _TIMER = None
+        return False
+
+
+def _launch(key, fn, *args):
+    t = _TIMER
+    if t is None:
+        return fn(*args)
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record()
+    rc = fn(*args)
+    e1.record()
+    t.records.append((key, e0, e1))
+    return rc
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load_library().yolosod_last_error().decode(errors="replace")
+        raise RuntimeError(f"yolosod_amd.{what} failed (rc={rc}): {msg}")
+
+
+def _dev(t: torch.Tensor, name: str) -> int:
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name}: expected a tensor")
+    if t.device.type != "cuda":
+        raise RuntimeError(f"{name}: HIP kernel requires a GPU tensor (got device {t.device}); no CPU fallback")
+    if t.dtype != torch.float32:
+        raise RuntimeError(f"{name}: expected float32, got {t.dtype}")
+    if not t.is_contiguous():
+        raise RuntimeError(f"{name}: expected a contiguous tensor")
+    return t.data_ptr()
+
+
+def _p(t: torch.Tensor, name: str, numel: int | None = None) -> int:
+    """Pointer of a (parameter) tensor, made fp32-contiguous on the caller's device if needed."""
+    if numel is not None and t.numel() != numel:
+        raise RuntimeError(f"{name}: expected {numel} elements, got {t.numel()}")
+    return _dev(t, name)
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _workspace(nbytes: int, device) -> torch.Tensor:
+    return torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+
+
+def _c(t: torch.Tensor) -> torch.Tensor:
+    return t.detach().float().contiguous()
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# operator wrappers (parameters are passed as tensors already on the input's device)
+# ---------------------------------------------------------------------------------------------------------------
+def se_forward(x, fc1_w, fc1_b, fc2_w, fc2_b):
+    lib = load_library()
+    B, C, H, W = x.shape
+    hid = fc1_w.shape[0]
+    y = torch.empty_like(x)
+    ws = _workspace(lib.yolosod_se_workspace(B, C, H, W), x.device)
+    _check(_launch(("se", tuple(x.shape), hid), lib.yolosod_se_forward, _dev(x, "x"), _dev(y, "y"), B, C, H, W, _p(fc1_w, "fc1.weight", hid * C),
+                                  _p(fc1_b, "fc1.bias", hid), _p(fc2_w, "fc2.weight", C * hid),
+                                  _p(fc2_b, "fc2.bias", C), hid, ws.data_ptr(), ws.numel(), _stream()), "se_forward")
+    return y
+
+
+def cbam_forward(x, fc0_w, fc2_w, sa_w):
+    lib = load_library()
+    B, C, H, W = x.shape
+    hid = fc0_w.shape[0]
+    y = torch.empty_like(x)
+    ws = _workspace(lib.yolosod_cbam_workspace(B, C, H, W), x.device)
+    _check(_launch(("cbam", tuple(x.shape), hid), lib.yolosod_cbam_forward, _dev(x, "x"), _dev(y, "y"), B, C, H, W, _p(fc0_w, "fc.0.weight", hid * C),
+                                    _p(fc2_w, "fc.2.weight", C * hid), hid, _p(sa_w, "conv1.weight", 98),
+                                    ws.data_ptr(), ws.numel(), _stream()), "cbam_forward")
+    return y
+
+
+def ca_forward(x, conv1_w, conv1_b, bn_w, bn_b, bn_mean, bn_var, bn_eps, convh_w, convh_b, convw_w, convw_b):
+    lib = load_library()
+    B, C, H, W = x.shape
+    mip = conv1_w.shape[0]
+    y = torch.empty_like(x)
+    ws = _workspace(lib.yolosod_ca_workspace(B, C, H, W), x.device)
+    _check(_launch(("ca", tuple(x.shape), mip), lib.yolosod_ca_forward, _dev(x, "x"), _dev(y, "y"), B, C, H, W, _p(conv1_w, "conv1.weight", mip * C),
+                                  _p(conv1_b, "conv1.bias", mip), mip, _p(bn_w, "bn1.weight", mip),
+                                  _p(bn_b, "bn1.bias", mip), _p(bn_mean, "bn1.running_mean", mip),
+                                  _p(bn_var, "bn1.running_var", mip), float(bn_eps),
+                                  _p(convh_w, "conv_h.weight", C * mip), _p(convh_b, "conv_h.bias", C),
+                                  _p(convw_w, "conv_w.weight", C * mip), _p(convw_b, "conv_w.bias", C),
+                                  ws.data_ptr(), ws.numel(), _stream()), "ca_forward")
+    return y
+
+
+def a2_forward(x, num_areas, num_heads, proj_w, proj_b, ln_w, ln_b, ln_eps, in_w, in_b, mo_w, mo_b, op_w, op_b):
+    lib = load_library()
+    B, C, H, W = x.shape
+    if C % num_heads:
+        raise RuntimeError(f"A2_Attn: C={C} not divisible by num_heads={num_heads}")
+    if num_areas * W > 320:
+        raise RuntimeError(f"A2_Attn: sequence length {num_areas * W} > 320 unsupported")
+    y = torch.empty_like(x)
+    ws = _workspace(lib.yolosod_a2_workspace(B, C, H, W, num_areas), x.device)
+    _check(_launch(("a2", tuple(x.shape), (num_areas, num_heads)), lib.yolosod_a2_forward, _dev(x, "x"), _dev(y, "y"), B, C, H, W, num_areas, num_heads,
+                                  _p(proj_w, "proj.weight", C * C), _p(proj_b, "proj.bias", C),
+                                  _p(ln_w, "layer_norm.weight", C), _p(ln_b, "layer_norm.bias", C), float(ln_eps),
+                                  _p(in_w, "in_proj_weight", 3 * C * C), _p(in_b, "in_proj_bias", 3 * C),
+                                  _p(mo_w, "attention.out_proj.weight", C * C),
+                                  _p(mo_b, "attention.out_proj.bias", C), _p(op_w, "out_proj.weight", C * C),
+                                  _p(op_b, "out_proj.bias", C), ws.data_ptr(), ws.numel(), _stream()),
+           "a2_forward")
+    return y
+
+
+def swin_forward(x, num_heads, window, dw_w, ln1_w, ln1_b, ln1_eps, in_w, in_b, out_w, out_b, ln2_w, ln2_b,
+                 ln2_eps, m1_w, m1_b, m2_w, m2_b, pw_w, bn_w, bn_b, bn_mean, bn_var, bn_eps):
+    lib = load_library()
+    B, C, H, W = x.shape
+    hid = m1_w.shape[0]
+    wh = H if (H <= window and W <= window) else min(window, H)
+    ww = W if (H <= window and W <= window) else min(window, W)
+    if wh * ww > 320:
+        raise RuntimeError(f"SwinBlock: window of {wh}x{ww} tokens unsupported")
+    if C % num_heads or (C // num_heads) not in (8, 16, 32, 64, 128):
+        raise RuntimeError(f"SwinBlock: head dim {C}/{num_heads} unsupported")
+    y = torch.empty_like(x)
+    ws = _workspace(lib.yolosod_swin_workspace(B, C, H, W, window, hid), x.device)
+    _check(_launch(("swin", tuple(x.shape), (num_heads, window, hid)), lib.yolosod_swin_forward,
+        _dev(x, "x"), _dev(y, "y"), B, C, H, W, num_heads, window, _p(dw_w, "dw.weight", C * 9),
+        _p(ln1_w, "norm1.weight", C), _p(ln1_b, "norm1.bias", C), float(ln1_eps),
+        _p(in_w, "in_proj_weight", 3 * C * C), _p(in_b, "in_proj_bias", 3 * C),
+        _p(out_w, "out_proj.weight", C * C), _p(out_b, "out_proj.bias", C),
+        _p(ln2_w, "norm2.weight", C), _p(ln2_b, "norm2.bias", C), float(ln2_eps),
+        _p(m1_w, "mlp.0.weight", hid * C), _p(m1_b, "mlp.0.bias", hid), hid,
+        _p(m2_w, "mlp.2.weight", C * hid), _p(m2_b, "mlp.2.bias", C), _p(pw_w, "pw.weight", C * C),
+        _p(bn_w, "bn.weight", C), _p(bn_b, "bn.bias", C), _p(bn_mean, "bn.running_mean", C),
+        _p(bn_var, "bn.running_var", C), float(bn_eps), ws.data_ptr(), ws.numel(), _stream()), "swin_forward")
+    return y
+
+
+def detect_decode(maps, strides, nc, reg_max=16):
+    """maps: list of [B, 4*reg_max+nc, Hi, Wi] fp32 -> y [B, 4+nc, A]."""
+    lib = load_library()
+    nl = len(maps)
+    B = maps[0].shape[0]
+    no = 4 * reg_max + nc
+    for i, m in enumerate(maps):
+        if m.dim() != 4 or m.shape[0] != B or m.shape[1] != no:
+            raise RuntimeError(f"detect_decode: map {i} has shape {tuple(m.shape)}, expected [B,{no},H,W]")
+    A = sum(m.shape[2] * m.shape[3] for m in maps)
+    y = torch.empty((B, 4 + nc, A), dtype=torch.float32, device=maps[0].device)
+    ptrs = (ctypes.c_void_p * nl)(*[_dev(m, f"maps[{i}]") for i, m in enumerate(maps)])
+    hs = (ctypes.c_int * nl)(*[m.shape[2] for m in maps])
+    wsz = (ctypes.c_int * nl)(*[m.shape[3] for m in maps])
+    st = (ctypes.c_float * nl)(*[float(s) for s in strides])
+    _check(_launch(("decode", (B, A), nc), lib.yolosod_detect_decode, nl, ctypes.cast(ptrs, ctypes.c_void_p), ctypes.cast(hs, ctypes.c_void_p),
+                                     ctypes.cast(wsz, ctypes.c_void_p), ctypes.cast(st, ctypes.c_void_p), B, nc,
+                                     reg_max, _dev(y, "y"), _stream()), "detect_decode")
+    return y
+
+
+def nms(pred, conf_thres, iou_thres, classes, agnostic, multi_label, max_det, max_nms, max_wh, in_place):
+    """Batched NMS on pred [B, 4+nc, A] (GPU). Returns (out [B,max_det,6], counts [B] int32, index [B,max_det])."""
+    lib = load_library()
+    B, no, A = pred.shape
+    nc = no - 4
+    dev = pred.device
+    if not in_place:
+        pred = pred.clone()
+    out = torch.empty((B, max_det, 6), dtype=torch.float32, device=dev)
+    counts = torch.empty((B,), dtype=torch.int32, device=dev)
+    index = torch.empty((B, max_det), dtype=torch.int32, device=dev)
+    ws = _workspace(lib.yolosod_nms_workspace(B, nc, A, int(multi_label)), dev)
+    cls_ptr, ncls = None, 0
+    if classes is not None:
+        ct = torch.as_tensor(classes, dtype=torch.int32, device=dev).reshape(-1).contiguous()
+        cls_ptr, ncls = ct.data_ptr(), ct.numel()
+    _check(_launch(("nms", (B, nc, A), int(multi_label)), lib.yolosod_nms, _dev(pred, "prediction"), B, nc, A, float(conf_thres), float(iou_thres), cls_ptr, ncls,
+                           int(bool(agnostic)), int(bool(multi_label)), int(max_det), int(max_nms), float(max_wh),
+                           1, out.data_ptr(), counts.data_ptr(), index.data_ptr(), ws.data_ptr(), ws.numel(),
+                           _stream()), "nms")
+    return out, counts, index
+
+
+def gemm_f32(A, B, b_kcontig, bias=None, bias_mode=0, act=0, res=None):
+    """Test hook: A [M,K]; B [N,K] (b_kcontig) or [K,N]; returns C [M,N]."""
+    lib = load_library()
+    M, K = A.shape
+    N = B.shape[0] if b_kcontig else B.shape[1]
+    C = torch.empty((M, N), dtype=torch.float32, device=A.device)
+    _check(lib.yolosod_gemm_f32(_dev(A, "A"), 0, K, _dev(B, "B"), 0, B.shape[1], int(b_kcontig), _dev(C, "C"), 0, N,
+                                M, N, K, 1, None if bias is None else _dev(bias, "bias"), bias_mode, act,
+                                None if res is None else _dev(res, "res"), _stream()), "gemm_f32")
+    return C
+
+
+def layernorm(x, w, b, eps):
+    lib = load_library()
+    rows, C = x.shape
+    y = torch.empty_like(x)
+    _check(lib.yolosod_layernorm(_dev(x, "x"), _dev(y, "y"), rows, C, _dev(w, "w"), _dev(b, "b"), float(eps),
+                                 _stream()), "layernorm")
+    return y
+
+
+def attention(qkv, n_seq, L, C, heads):
+    lib = load_library()
+    out = torch.empty((n_seq * L, C), dtype=torch.float32, device=qkv.device)
+    _check(lib.yolosod_attention(_dev(qkv, "qkv"), _dev(out, "out"), n_seq, L, C, heads, _stream()), "attention")
+    return out

@@ -1,0 +1,769 @@
+// Transformer-shaped MAFN operators on gfx950: SwinBlock (window attention at P4/P2) and A2_Attn (area attention
+// at P5), built from four device primitives:
+//   * gemm_f32      - LDS-tiled GEMM on the exact-fp32 matrix cores (v_mfma_f32_32x32x2_f32), 128xBN x16 tiles,
+//                     4 waves, fused epilogues (bias / folded-BN / SiLU / GELU / residual / Swin window-reverse).
+//   * attn_f32      - per-(sequence, head, 64-query block) attention on v_mfma_f32_16x16x4_f32: Q in registers,
+//                     K and V staged through LDS in 64-key chunks, scores for the whole (<=320-key) row kept in
+//                     registers, softmax via 16-lane shuffles, P transposed through LDS for the P.V product.
+//   * layernorm     - one wave per token row.
+//   * swin_partition (depthwise 3x3 + zero pad + window partition, token-major out) / a2 pool + upsample.
+// Numerics: fp32 in / fp32 accumulate everywhere (the MFMA f32 form is an exact f32 fma chain), matching the
+// reference's fp32 PyTorch-CPU math to rounding.
+//
+// Reference semantics:
+//   SwinBlock  ultralytics/nn/modules/blocks_transformer.py:8-171 (window_partition :8-47, window_reverse :49-79,
+//              WindowAttention.forward :100-131, SwinBlock.forward :150-171)
+//   A2_Attn    ultralytics/nn/modules/a2_attn.py:35-69
+#include "common.h"
+#include <math.h>
+
+namespace ys {
+
+// =================================================================================================
+// GEMM:  out(b, m, n) = epilogue( sum_k A(b, m, k) * B(b, k, n) )
+//   A(b,m,k) = A[b*a_bs + m*lda + k]                        (always K-contiguous)
+//   B_KC:  B(b,k,n) = B[b*b_bs + n*ldb + k]                  (K-contiguous: Linear weights / token-major acts)
+//   !B_KC: B(b,k,n) = B[b*b_bs + k*ldb + n]                  (N-contiguous: NCHW activations)
+// Requires K % 16 == 0, lda % 4 == 0, ldb % 4 == 0, 16-byte aligned bases.
+// =================================================================================================
+struct Epi {
+  const float* bias;   // bias_mode 1: per-row m, 2: per-col n
+  int bias_mode;
+  const float* scale;  // folded BN:  v = v*scale + shift, bn_mode 1: per-row, 2: per-col
+  const float* shift;
+  int bn_mode;
+  int act;             // 0 none, 1 SiLU, 2 GELU(erf), 3 ReLU
+  const float* res;    // residual added after activation (same indexing as out)
+  long res_bs;
+  int ldr;
+  float* out;
+  long out_bs;
+  int ldc;
+  // window-reverse output (SwinBlock): n = global token, m = channel; out/res are NCHW [img][M][H][W]
+  int swin;
+  int sw_H, sw_W, sw_wh, sw_ww, sw_nWx, sw_nWin;
+};
+
+struct GemmArgs {
+  const float* A;
+  long a_bs;
+  int lda;
+  const float* B;
+  long b_bs;
+  int ldb;
+  int M, N, K;
+  Epi epi;
+};
+
+__device__ __forceinline__ float apply_act(float v, int act) {
+  if (act == 1) return siluf_(v);
+  if (act == 2) return geluf_(v);
+  if (act == 3) return fmaxf(v, 0.f);
+  return v;
+}
+
+__device__ __forceinline__ void epi_store(const Epi& e, int bz, int m, int n, float v) {
+  if (e.bias_mode == 1) v += e.bias[m];
+  else if (e.bias_mode == 2) v += e.bias[n];
+  if (e.bn_mode == 1) v = v * e.scale[m] + e.shift[m];
+  else if (e.bn_mode == 2) v = v * e.scale[n] + e.shift[n];
+  v = apply_act(v, e.act);
+  if (!e.swin) {
+    const long o = (long)bz * e.out_bs + (long)m * e.ldc + n;
+    if (e.res) v += e.res[(long)bz * e.res_bs + (long)m * e.ldr + n];
+    e.out[o] = v;
+  } else {
+    const int L = e.sw_wh * e.sw_ww;
+    const int per_img = e.sw_nWin * L;
+    const int img = n / per_img;
+    const int r = n - img * per_img;
+    const int win = r / L, tok = r - (r / L) * L;
+    const int wy = win / e.sw_nWx, wx = win - wy * e.sw_nWx;
+    const int iy = tok / e.sw_ww, ix = tok - iy * e.sw_ww;
+    const int h = wy * e.sw_wh + iy, w = wx * e.sw_ww + ix;
+    if (h >= e.sw_H || w >= e.sw_W) return;  // crop of the zero-padded border (blocks_transformer.py:125-129)
+    const long o = (((long)img * e.ldc + m) * e.sw_H + h) * e.sw_W + w;  // ldc = channels here
+    if (e.res) v += e.res[o];
+    e.out[o] = v;
+  }
+}
+
+template <int WM, int WN, int MI, int NI, bool B_KC>
+__global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
+  constexpr int BM = WM * MI * 32;
+  constexpr int BN = WN * NI * 32;
+  constexpr int BK = 16;
+  constexpr int SA = BM + 2;                  // transposed (k-major) A image; +2 keeps the 4-way k-scatter
+  constexpr int SB = B_KC ? BN + 2 : BN + 4;  // conflict-free; +4 keeps b128 stores aligned
+  constexpr int NA = BM / 64;                 // float4 loads per thread for the A tile
+  constexpr int NB = BN / 64;
+  static_assert(WM * WN == 4, "4 waves");
+  __shared__ float As[BK * SA];
+  __shared__ float Bs[BK * SB];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int bz = blockIdx.z;
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const float* A = g.A + (long)bz * g.a_bs;
+  const float* B = g.B + (long)bz * g.b_bs;
+  const int M = g.M, N = g.N, K = g.K;
+
+  float4 ra[NA], rb[NB];
+  auto load_tiles = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int idx = tid + 256 * i;
+      const int ml = idx >> 2, kq = (idx & 3) * 4;
+      const int m = m0 + ml;
+      ra[i] = (m < M) ? *reinterpret_cast<const float4*>(A + (long)m * g.lda + k0 + kq) : make_float4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int idx = tid + 256 * i;
+      if (B_KC) {
+        const int nl = idx >> 2, kq = (idx & 3) * 4;
+        const int n = n0 + nl;
+        rb[i] = (n < N) ? *reinterpret_cast<const float4*>(B + (long)n * g.ldb + k0 + kq) : make_float4(0, 0, 0, 0);
+      } else {
+        const int kl = idx / (BN / 4), nq = (idx % (BN / 4)) * 4;
+        const int n = n0 + nq;
+        const float* src = B + (long)(k0 + kl) * g.ldb + n;
+        if (n + 3 < N) {
+          rb[i] = *reinterpret_cast<const float4*>(src);
+        } else {
+          rb[i].x = (n < N) ? src[0] : 0.f;
+          rb[i].y = (n + 1 < N) ? src[1] : 0.f;
+          rb[i].z = (n + 2 < N) ? src[2] : 0.f;
+          rb[i].w = (n + 3 < N) ? src[3] : 0.f;
+        }
+      }
+    }
+  };
+  auto store_tiles = [&]() {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int idx = tid + 256 * i;
+      const int ml = idx >> 2, kq = (idx & 3) * 4;
+      As[(kq + 0) * SA + ml] = ra[i].x;
+      As[(kq + 1) * SA + ml] = ra[i].y;
+      As[(kq + 2) * SA + ml] = ra[i].z;
+      As[(kq + 3) * SA + ml] = ra[i].w;
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int idx = tid + 256 * i;
+      if (B_KC) {
+        const int nl = idx >> 2, kq = (idx & 3) * 4;
+        Bs[(kq + 0) * SB + nl] = rb[i].x;
+        Bs[(kq + 1) * SB + nl] = rb[i].y;
+        Bs[(kq + 2) * SB + nl] = rb[i].z;
+        Bs[(kq + 3) * SB + nl] = rb[i].w;
+      } else {
+        const int kl = idx / (BN / 4), nq = (idx % (BN / 4)) * 4;
+        *reinterpret_cast<float4*>(&Bs[kl * SB + nq]) = rb[i];
+      }
+    }
+  };
+
+  f32x16 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int nk = K / BK;
+  load_tiles(0);
+  const int lr = lane & 31, lk = lane >> 5;
+  for (int kb = 0; kb < nk; ++kb) {
+    __syncthreads();
+    store_tiles();
+    __syncthreads();
+    if (kb + 1 < nk) load_tiles((kb + 1) * BK);
+#pragma unroll
+    for (int kk = 0; kk < BK / 2; ++kk) {
+      const int kr = kk * 2 + lk;
+      float a[MI], b[NI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) a[i] = As[kr * SA + wm * (MI * 32) + i * 32 + lr];
+#pragma unroll
+      for (int j = 0; j < NI; ++j) b[j] = Bs[kr * SB + wn * (NI * 32) + j * 32 + lr];
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+  }
+
+  // epilogue: C/D map of 32x32: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int n = n0 + wn * (NI * 32) + j * 32 + lr;
+      if (n >= N) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * (MI * 32) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
+        if (m < M) epi_store(g.epi, bz, m, n, acc[i][j][r]);
+      }
+    }
+}
+
+static int launch_gemm(const GemmArgs& g, int batch, bool b_kc, hipStream_t st) {
+  YS_CHECK_ARG(g.K % 16 == 0, "gemm: K=%d must be a multiple of 16", g.K);
+  YS_CHECK_ARG(g.lda % 4 == 0 && g.ldb % 4 == 0, "gemm: lda/ldb must be multiples of 4");
+  YS_CHECK_ARG(((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.B & 15) == 0, "gemm: A/B must be 16-byte aligned");
+  if (g.M == 0 || g.N == 0 || batch == 0) return 0;
+  const bool wide = (g.N % 128 == 0) || g.N > 256;
+  if (wide) {
+    dim3 grid((g.N + 127) / 128, (g.M + 127) / 128, batch);
+    if (b_kc) hipLaunchKernelGGL((gemm_f32_kernel<2, 2, 2, 2, true>), grid, dim3(256), 0, st, g);
+    else hipLaunchKernelGGL((gemm_f32_kernel<2, 2, 2, 2, false>), grid, dim3(256), 0, st, g);
+  } else {
+    dim3 grid((g.N + 63) / 64, (g.M + 127) / 128, batch);
+    if (b_kc) hipLaunchKernelGGL((gemm_f32_kernel<4, 1, 1, 2, true>), grid, dim3(256), 0, st, g);
+    else hipLaunchKernelGGL((gemm_f32_kernel<4, 1, 1, 2, false>), grid, dim3(256), 0, st, g);
+  }
+  YS_CHECK_LAUNCH("gemm_f32");
+  return 0;
+}
+
+static Epi epi_plain(float* out, long out_bs, int ldc) {
+  Epi e{};
+  e.out = out;
+  e.out_bs = out_bs;
+  e.ldc = ldc;
+  return e;
+}
+
+// =================================================================================================
+// LayerNorm over rows of C (token-major), one wave per row. y = (x-mean)*rstd*w + b, biased variance.
+// =================================================================================================
+template <int VPL>  // values per lane, C <= 64*VPL
+__global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, float* __restrict__ y, long rows,
+                                                        int C, const float* __restrict__ w,
+                                                        const float* __restrict__ b, float eps) {
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const float* xr = x + row * C;
+  float v[VPL];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int c = lane + 64 * i;
+    v[i] = (c < C) ? xr[c] : 0.f;
+    s += v[i];
+  }
+  const float mean = wave_sum(s) / (float)C;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int c = lane + 64 * i;
+    const float d = (c < C) ? v[i] - mean : 0.f;
+    q += d * d;
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)C + eps);
+  float* yr = y + row * C;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int c = lane + 64 * i;
+    if (c < C) yr[c] = (v[i] - mean) * rstd * w[c] + b[c];
+  }
+}
+
+static int launch_layernorm(const float* x, float* y, long rows, int C, const float* w, const float* b, float eps,
+                            hipStream_t st) {
+  YS_CHECK_ARG(C > 0 && C <= 1024, "layernorm: C=%d unsupported", C);
+  if (rows == 0) return 0;
+  dim3 grid((unsigned)((rows + 3) / 4));
+  if (C <= 64) hipLaunchKernelGGL((layernorm_kernel<1>), grid, dim3(256), 0, st, x, y, rows, C, w, b, eps);
+  else if (C <= 128) hipLaunchKernelGGL((layernorm_kernel<2>), grid, dim3(256), 0, st, x, y, rows, C, w, b, eps);
+  else if (C <= 256) hipLaunchKernelGGL((layernorm_kernel<4>), grid, dim3(256), 0, st, x, y, rows, C, w, b, eps);
+  else if (C <= 512) hipLaunchKernelGGL((layernorm_kernel<8>), grid, dim3(256), 0, st, x, y, rows, C, w, b, eps);
+  else hipLaunchKernelGGL((layernorm_kernel<16>), grid, dim3(256), 0, st, x, y, rows, C, w, b, eps);
+  YS_CHECK_LAUNCH("layernorm");
+  return 0;
+}
+
+// =================================================================================================
+// Attention over packed QKV rows: qkv[(s*L + t)*ld + {0,C,2C} + h*hd + d]; out[(s*L + t)*ldo + h*hd + d].
+// grid = (ceil(L/64), heads, n_seq). Each wave owns 16 query rows; the full score row (NKB*16 keys) lives in
+// registers (NKB f32x4 accumulators), so softmax needs no rescaling.
+// =================================================================================================
+template <int HD, int NKB>
+__global__ __launch_bounds__(256) void attn_f32_kernel(const float* __restrict__ qkv, int ld, int C,
+                                                       float* __restrict__ out, int ldo, int L, float scale) {
+  constexpr int HDP = HD < 16 ? 16 : HD;  // padded head dim for the P.V output blocks
+  constexpr int KS = HDP + 1;             // LDS row stride of the K / V chunk
+  constexpr int NK = NKB * 16;            // keys covered
+  constexpr int PS = NK + 1;              // LDS row stride of P
+  __shared__ float KV[64 * KS];
+  __shared__ float Ps[4 * 16 * PS];
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int h = blockIdx.y;
+  const long seq_row0 = (long)blockIdx.z * L;
+  const int q0 = blockIdx.x * 64 + wv * 16;
+  const int l15 = lane & 15, l4 = lane >> 4;
+
+  // Q fragment: A[i = l&15][k = l>>4] over k-steps of 4 (scaled once, as q*scale in the MHA math path)
+  float qf[(HD + 3) / 4];
+  {
+    const int qrow = q0 + l15;
+#pragma unroll
+    for (int s = 0; s < (HD + 3) / 4; ++s) {
+      const int d = 4 * s + l4;
+      qf[s] = (qrow < L && d < HD) ? qkv[(seq_row0 + qrow) * ld + h * HD + d] * scale : 0.f;
+    }
+  }
+
+  f32x4 sacc[NKB];
+#pragma unroll
+  for (int kb = 0; kb < NKB; ++kb) sacc[kb] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // ---- S = Q K^T, K staged in 64-key chunks ----
+#pragma unroll
+  for (int ch = 0; ch < (NKB + 3) / 4; ++ch) {
+    __syncthreads();
+    for (int e = tid; e < 64 * HD; e += 256) {
+      const int kr = e / HD, d = e % HD;
+      const int key = ch * 64 + kr;
+      KV[kr * KS + d] = (key < L) ? qkv[(seq_row0 + key) * ld + C + h * HD + d] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kb4 = 0; kb4 < 4; ++kb4) {
+      const int kb = ch * 4 + kb4;
+      if (kb < NKB) {
+#pragma unroll
+        for (int s = 0; s < (HD + 3) / 4; ++s) {
+          const int d = 4 * s + l4;
+          const float bk = (d < HD) ? KV[(kb4 * 16 + l15) * KS + d] : 0.f;
+          sacc[kb] = __builtin_amdgcn_mfma_f32_16x16x4f32(qf[s], bk, sacc[kb], 0, 0, 0);
+        }
+      }
+    }
+  }
+
+  // ---- softmax over keys; lane holds S[row = l4*4 + r][key = kb*16 + l15] ----
+  float rmax[4], rsum[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) rmax[r] = -INFINITY;
+#pragma unroll
+  for (int kb = 0; kb < NKB; ++kb) {
+    const bool valid = (kb * 16 + l15) < L;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (!valid) sacc[kb][r] = -INFINITY;
+      rmax[r] = fmaxf(rmax[r], sacc[kb][r]);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) rmax[r] = fmaxf(rmax[r], __shfl_xor(rmax[r], o, 64));
+    rsum[r] = 0.f;
+  }
+#pragma unroll
+  for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float e = expf(sacc[kb][r] - rmax[r]);
+      sacc[kb][r] = e;
+      rsum[r] += e;
+    }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) rsum[r] += __shfl_xor(rsum[r], o, 64);
+    rsum[r] = 1.0f / rsum[r];
+  }
+  float* Pw = Ps + wv * 16 * PS;
+#pragma unroll
+  for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) Pw[(l4 * 4 + r) * PS + kb * 16 + l15] = sacc[kb][r] * rsum[r];
+
+  // ---- O = P V, V staged in 64-key chunks ----
+  f32x4 oacc[HDP / 16];
+#pragma unroll
+  for (int nb = 0; nb < HDP / 16; ++nb) oacc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ch = 0; ch < (NKB + 3) / 4; ++ch) {
+    __syncthreads();
+    for (int e = tid; e < 64 * HDP; e += 256) {
+      const int kr = e / HDP, d = e % HDP;
+      const int key = ch * 64 + kr;
+      KV[kr * KS + d] = (key < L && d < HD) ? qkv[(seq_row0 + key) * ld + 2 * C + h * HD + d] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int key = ch * 64 + 4 * s + l4;  // k index of this k-step for this lane
+      if (ch * 64 + 4 * s < NK) {
+        const float pa = Pw[l15 * PS + key];
+#pragma unroll
+        for (int nb = 0; nb < HDP / 16; ++nb) {
+          const float vb = KV[(4 * s + l4) * KS + nb * 16 + l15];
+          oacc[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(pa, vb, oacc[nb], 0, 0, 0);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int nb = 0; nb < HDP / 16; ++nb) {
+    const int d = nb * 16 + l15;
+    if (d >= HD) continue;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int qrow = q0 + l4 * 4 + r;
+      if (qrow < L) out[(seq_row0 + qrow) * ldo + h * HD + d] = oacc[nb][r];
+    }
+  }
+}
+
+template <int HD>
+static void launch_attn_hd(int nkb, dim3 grid, hipStream_t st, const float* qkv, int ld, int C, float* out, int ldo,
+                           int L, float scale) {
+#define YS_ATTN_CASE(NKBV)                                                                                   \
+  if (nkb <= NKBV) {                                                                                         \
+    hipLaunchKernelGGL((attn_f32_kernel<HD, NKBV>), grid, dim3(256), 0, st, qkv, ld, C, out, ldo, L, scale); \
+    return;                                                                                                  \
+  }
+  YS_ATTN_CASE(4)
+  YS_ATTN_CASE(8)
+  YS_ATTN_CASE(10)
+  YS_ATTN_CASE(12)
+  YS_ATTN_CASE(16)
+  YS_ATTN_CASE(20)
+#undef YS_ATTN_CASE
+}
+
+static int launch_attention(const float* qkv, float* out, long n_seq, int L, int C, int heads, hipStream_t st) {
+  YS_CHECK_ARG(heads > 0 && C % heads == 0, "attention: C=%d not divisible by heads=%d", C, heads);
+  const int hd = C / heads;
+  YS_CHECK_ARG(L > 0 && L <= 320, "attention: sequence length %d unsupported (1..320)", L);
+  YS_CHECK_ARG(n_seq < 65536, "attention: too many sequences (%ld)", n_seq);
+  const int nkb = (L + 15) / 16;
+  const float scale = 1.0f / sqrtf((float)hd);
+  dim3 grid((L + 63) / 64, heads, (unsigned)n_seq);
+  switch (hd) {
+    case 8: launch_attn_hd<8>(nkb, grid, st, qkv, 3 * C, C, out, C, L, scale); break;
+    case 16: launch_attn_hd<16>(nkb, grid, st, qkv, 3 * C, C, out, C, L, scale); break;
+    case 32: launch_attn_hd<32>(nkb, grid, st, qkv, 3 * C, C, out, C, L, scale); break;
+    case 64: launch_attn_hd<64>(nkb, grid, st, qkv, 3 * C, C, out, C, L, scale); break;
+    case 128: launch_attn_hd<128>(nkb, grid, st, qkv, 3 * C, C, out, C, L, scale); break;
+    default: YS_CHECK_ARG(false, "attention: head dim %d unsupported (8,16,32,64,128)", hd);
+  }
+  YS_CHECK_LAUNCH("attention");
+  return 0;
+}
+
+// =================================================================================================
+// Swin: depthwise 3x3 (pad 1, no bias) + bottom/right zero pad + window partition -> token-major T[tok][C].
+// Token order (img, wy, wx, iy, ix) as window_partition's permute(0,2,4,3,5,1) (blocks_transformer.py:43-46).
+// grid = (nWin_total, ceil(C/64)); a 64-channel slab of the (wh+2)x(ww+2) halo patch is staged in LDS.
+// =================================================================================================
+__global__ __launch_bounds__(256) void swin_partition_kernel(const float* __restrict__ x, const float* __restrict__ dw,
+                                                             float* __restrict__ T, int C, int H, int W, int wh,
+                                                             int ww, int nWx, int nWin) {
+  extern __shared__ float patch[];  // [64][(wh+2)*(ww+2)]
+  const int PH = wh + 2, PW = ww + 2, PP = PH * PW;
+  const long gw = blockIdx.x;
+  const int img = (int)(gw / nWin), win = (int)(gw % nWin);
+  const int wy = win / nWx, wx = win % nWx;
+  const int c0 = blockIdx.y * 64;
+  const int nc = (C - c0 < 64) ? C - c0 : 64;
+  const int h0 = wy * wh - 1, w0 = wx * ww - 1;
+  const float* xb = x + ((long)img * C + c0) * H * W;
+  for (int e = threadIdx.x; e < nc * PP; e += 256) {
+    const int c = e / PP, r = e % PP;
+    const int py = r / PW, px = r % PW;
+    const int hh = h0 + py, ww_ = w0 + px;
+    patch[e] = (hh >= 0 && hh < H && ww_ >= 0 && ww_ < W) ? xb[((long)c * H + hh) * W + ww_] : 0.f;
+  }
+  __syncthreads();
+  const int L = wh * ww;
+  float* Tw = T + (gw * L) * C + c0;
+  for (int e = threadIdx.x; e < L * nc; e += 256) {
+    const int tok = e / nc, c = e % nc;
+    const int iy = tok / ww, ix = tok % ww;
+    const int hh = wy * wh + iy, ww_ = wx * ww + ix;
+    float v = 0.f;
+    if (hh < H && ww_ < W) {
+      const float* pc = patch + c * PP + iy * PW + ix;
+      const float* k = dw + (long)(c0 + c) * 9;
+      v = k[0] * pc[0] + k[1] * pc[1] + k[2] * pc[2] + k[3] * pc[PW] + k[4] * pc[PW + 1] + k[5] * pc[PW + 2] +
+          k[6] * pc[2 * PW] + k[7] * pc[2 * PW + 1] + k[8] * pc[2 * PW + 2];
+    }
+    Tw[(long)tok * C + c] = v;
+  }
+}
+
+// =================================================================================================
+// A2: adaptive-avg-pool over rows to `A` areas (overlapping bins [floor(a*H/A), ceil((a+1)*H/A))), emitted
+// token-major S[(img*A + a)*W + w][c]  (a2_attn.py:44-48).  grid = (B*A), 256 threads.
+// =================================================================================================
+__global__ __launch_bounds__(256) void a2_pool_tokens_kernel(const float* __restrict__ xp, float* __restrict__ S, int C,
+                                                             int H, int W, int A) {
+  const int img = blockIdx.x / A, a = blockIdx.x % A;
+  const int r0 = (a * H) / A, r1 = ((a + 1) * H + A - 1) / A;
+  const float inv = (float)(r1 - r0);
+  const float* xb = xp + (long)img * C * H * W;
+  float* Sb = S + ((long)img * A + a) * W * C;
+  for (int e = threadIdx.x; e < W * C; e += 256) {
+    const int w = e / C, c = e % C;
+    float s = 0.f;
+    for (int r = r0; r < r1; ++r) s += xb[((long)c * H + r) * W + w];
+    Sb[(long)w * C + c] = s / inv;
+  }
+}
+
+// A2 tail: y = x + SiLU(up_h(T) + b), T = out_proj_conv(Z) laid out [img][C][A][W]; bilinear along H with
+// align_corners=False (a2_attn.py:60), identity along W (same size). Upsampling commutes with the 1x1 conv.
+__global__ __launch_bounds__(256) void a2_upsample_out_kernel(const float* __restrict__ x, const float* __restrict__ T,
+                                                              const float* __restrict__ bias, float* __restrict__ y,
+                                                              int C, int H, int W, int A, long total) {
+  const float sc = (float)A / (float)H;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    const int w = (int)(e % W);
+    const long t = e / W;
+    const int h = (int)(t % H);
+    const long pc = t / H;  // img*C + c
+    const int c = (int)(pc % C);
+    float src = sc * ((float)h + 0.5f) - 0.5f;
+    if (src < 0.f) src = 0.f;
+    const int y0 = (int)src;
+    const int y1 = y0 + ((y0 < A - 1) ? 1 : 0);
+    const float l1 = src - (float)y0, l0 = 1.0f - l1;
+    const float* Tp = T + pc * A * W;
+    const float u = l0 * Tp[y0 * W + w] + l1 * Tp[y1 * W + w];
+    y[e] = x[e] + siluf_(u + bias[c]);
+  }
+}
+
+static int gs_blocks(long n) {
+  long b = (n + 255) / 256;
+  if (b > 4096) b = 4096;
+  return (int)(b < 1 ? 1 : b);
+}
+
+struct SwinGeom {
+  int wh, ww, Hp, Wp, nWy, nWx, nWin, L;
+  long ntok;
+};
+static SwinGeom swin_geom(int B, int H, int W, int ws) {
+  SwinGeom g;
+  g.wh = H < ws ? H : ws;
+  g.ww = W < ws ? W : ws;
+  if (H <= ws && W <= ws) {  // single global window, no pad (blocks_transformer.py:25-28)
+    g.wh = H;
+    g.ww = W;
+  }
+  g.Hp = H + (g.wh - H % g.wh) % g.wh;
+  g.Wp = W + (g.ww - W % g.ww) % g.ww;
+  g.nWy = g.Hp / g.wh;
+  g.nWx = g.Wp / g.ww;
+  g.nWin = g.nWy * g.nWx;
+  g.L = g.wh * g.ww;
+  g.ntok = (long)B * g.nWin * g.L;
+  return g;
+}
+
+}  // namespace ys
+
+using namespace ys;
+
+// =================================================================================================
+// C ABI
+// =================================================================================================
+YS_EXPORT int yolosod_gemm_f32(const float* A, long a_bs, int lda, const float* B, long b_bs, int ldb, int b_kcontig,
+                               float* C, long c_bs, int ldc, int M, int N, int K, int batch, const float* bias,
+                               int bias_mode, int act, const float* res, void* stream) {
+  GemmArgs g{};
+  g.A = A; g.a_bs = a_bs; g.lda = lda;
+  g.B = B; g.b_bs = b_bs; g.ldb = ldb;
+  g.M = M; g.N = N; g.K = K;
+  g.epi = epi_plain(C, c_bs, ldc);
+  g.epi.bias = bias; g.epi.bias_mode = bias ? bias_mode : 0;
+  g.epi.act = act;
+  g.epi.res = res; g.epi.res_bs = c_bs; g.epi.ldr = ldc;
+  return launch_gemm(g, batch, b_kcontig != 0, (hipStream_t)stream);
+}
+
+YS_EXPORT int yolosod_layernorm(const float* x, float* y, long rows, int C, const float* w, const float* b, float eps,
+                                void* stream) {
+  return launch_layernorm(x, y, rows, C, w, b, eps, (hipStream_t)stream);
+}
+
+YS_EXPORT int yolosod_attention(const float* qkv, float* out, long n_seq, int L, int C, int heads, void* stream) {
+  return launch_attention(qkv, out, n_seq, L, C, heads, (hipStream_t)stream);
+}
+
+YS_EXPORT size_t yolosod_swin_workspace(int B, int C, int H, int W, int window, int mlp_hidden) {
+  SwinGeom g = swin_geom(B, H, W, window);
+  Sizer s;
+  s.take<float>((size_t)g.ntok * C);  // T (residual stream)
+  s.take<float>((size_t)g.ntok * C);  // U (LN out / attention out)
+  const int wide = (3 * C > mlp_hidden) ? 3 * C : mlp_hidden;
+  s.take<float>((size_t)g.ntok * wide);  // QKV / MLP hidden
+  s.take<float>((size_t)C * 2);          // folded BN
+  return s.off;
+}
+
+__global__ void fold_bn_kernel(const float* w, const float* b, const float* m, const float* v, float eps, int C,
+                               float* scale, float* shift) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  const float inv = 1.0f / sqrtf(v[c] + eps);
+  const float sc = w[c] * inv;
+  scale[c] = sc;
+  shift[c] = b[c] - m[c] * sc;
+}
+
+YS_EXPORT int yolosod_swin_forward(const float* x, float* y, int B, int C, int H, int W, int num_heads, int window,
+                                   const float* dw_w, const float* ln1_w, const float* ln1_b, float ln1_eps,
+                                   const float* in_proj_w, const float* in_proj_b, const float* out_proj_w,
+                                   const float* out_proj_b, const float* ln2_w, const float* ln2_b, float ln2_eps,
+                                   const float* mlp1_w, const float* mlp1_b, int mlp_hidden, const float* mlp2_w,
+                                   const float* mlp2_b, const float* pw_w, const float* bn_w, const float* bn_b,
+                                   const float* bn_mean, const float* bn_var, float bn_eps, void* workspace,
+                                   size_t workspace_bytes, void* stream) {
+  YS_CHECK_ARG(x && y && dw_w && ln1_w && ln1_b && in_proj_w && in_proj_b && out_proj_w && out_proj_b && ln2_w &&
+                   ln2_b && mlp1_w && mlp1_b && mlp2_w && mlp2_b && pw_w && bn_w && bn_b && bn_mean && bn_var,
+               "swin: null pointer");
+  YS_CHECK_ARG(B >= 0 && C > 0 && H > 0 && W > 0 && window > 0, "swin: bad shape");
+  YS_CHECK_ARG(C % 16 == 0 && mlp_hidden % 16 == 0, "swin: C and mlp_hidden must be multiples of 16");
+  if (B == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  SwinGeom g = swin_geom(B, H, W, window);
+  YS_CHECK_ARG(g.L <= 320, "swin: window of %d tokens unsupported", g.L);
+  Carver cv(workspace, workspace_bytes);
+  float* T = cv.take<float>((size_t)g.ntok * C);
+  float* U = cv.take<float>((size_t)g.ntok * C);
+  const int wide = (3 * C > mlp_hidden) ? 3 * C : mlp_hidden;
+  float* Q = cv.take<float>((size_t)g.ntok * wide);
+  float* bn_fold = cv.take<float>((size_t)C * 2);
+  YS_CHECK_ARG(bn_fold, "swin: workspace too small (%zu)", workspace_bytes);
+  int rc;
+
+  const size_t lds = (size_t)64 * (g.wh + 2) * (g.ww + 2) * sizeof(float);
+  YS_CHECK_ARG(lds <= 64 * 1024, "swin: window %dx%d too large for the partition kernel", g.wh, g.ww);
+  hipLaunchKernelGGL(swin_partition_kernel, dim3((unsigned)((long)B * g.nWin), (C + 63) / 64), dim3(256), lds, st, x,
+                     dw_w, T, C, H, W, g.wh, g.ww, g.nWx, g.nWin);
+  YS_CHECK_LAUNCH("swin_partition");
+  if ((rc = launch_layernorm(T, U, g.ntok, C, ln1_w, ln1_b, ln1_eps, st))) return rc;
+
+  GemmArgs ga{};
+  // QKV = U Win^T + b_in
+  ga.A = U; ga.lda = C; ga.B = in_proj_w; ga.ldb = C; ga.M = (int)g.ntok; ga.N = 3 * C; ga.K = C;
+  ga.epi = epi_plain(Q, 0, 3 * C);
+  ga.epi.bias = in_proj_b; ga.epi.bias_mode = 2;
+  if ((rc = launch_gemm(ga, 1, true, st))) return rc;
+  if ((rc = launch_attention(Q, U, (long)B * g.nWin, g.L, C, num_heads, st))) return rc;
+  // T = T + (O Wo^T + bo)
+  ga = GemmArgs{};
+  ga.A = U; ga.lda = C; ga.B = out_proj_w; ga.ldb = C; ga.M = (int)g.ntok; ga.N = C; ga.K = C;
+  ga.epi = epi_plain(T, 0, C);
+  ga.epi.bias = out_proj_b; ga.epi.bias_mode = 2; ga.epi.res = T; ga.epi.ldr = C;
+  if ((rc = launch_gemm(ga, 1, true, st))) return rc;
+  if ((rc = launch_layernorm(T, U, g.ntok, C, ln2_w, ln2_b, ln2_eps, st))) return rc;
+  // Hd = GELU(U2 W1^T + b1)
+  ga = GemmArgs{};
+  ga.A = U; ga.lda = C; ga.B = mlp1_w; ga.ldb = C; ga.M = (int)g.ntok; ga.N = mlp_hidden; ga.K = C;
+  ga.epi = epi_plain(Q, 0, mlp_hidden);
+  ga.epi.bias = mlp1_b; ga.epi.bias_mode = 2; ga.epi.act = 2;
+  if ((rc = launch_gemm(ga, 1, true, st))) return rc;
+  // T = T + (Hd W2^T + b2)
+  ga = GemmArgs{};
+  ga.A = Q; ga.lda = mlp_hidden; ga.B = mlp2_w; ga.ldb = mlp_hidden; ga.M = (int)g.ntok; ga.N = C; ga.K = mlp_hidden;
+  ga.epi = epi_plain(T, 0, C);
+  ga.epi.bias = mlp2_b; ga.epi.bias_mode = 2; ga.epi.res = T; ga.epi.ldr = C;
+  if ((rc = launch_gemm(ga, 1, true, st))) return rc;
+  // y = x + SiLU(BN(pw . T)) with window reverse + crop: M = out channel, N = token
+  float* bn_scale = bn_fold;
+  float* bn_shift = bn_fold + C;
+  hipLaunchKernelGGL(fold_bn_kernel, dim3((C + 255) / 256), dim3(256), 0, st, bn_w, bn_b, bn_mean, bn_var, bn_eps, C,
+                     bn_scale, bn_shift);
+  ga = GemmArgs{};
+  ga.A = pw_w; ga.lda = C; ga.B = T; ga.ldb = C; ga.M = C; ga.N = (int)g.ntok; ga.K = C;
+  ga.epi = epi_plain(y, 0, C);
+  ga.epi.scale = bn_scale; ga.epi.shift = bn_shift; ga.epi.bn_mode = 1; ga.epi.act = 1;
+  ga.epi.res = x;
+  ga.epi.swin = 1; ga.epi.sw_H = H; ga.epi.sw_W = W; ga.epi.sw_wh = g.wh; ga.epi.sw_ww = g.ww;
+  ga.epi.sw_nWx = g.nWx; ga.epi.sw_nWin = g.nWin;
+  if ((rc = launch_gemm(ga, 1, true, st))) return rc;
+  return 0;
+}
+
+YS_EXPORT size_t yolosod_a2_workspace(int B, int C, int H, int W, int num_areas) {
+  const long ntok = (long)B * num_areas * W;
+  Sizer s;
+  s.take<float>((size_t)B * C * H * W);  // proj output
+  s.take<float>((size_t)ntok * C);       // S
+  s.take<float>((size_t)ntok * C);       // U / O
+  s.take<float>((size_t)ntok * 3 * C);   // QKV
+  s.take<float>((size_t)ntok * C);       // Z
+  return s.off;
+}
+
+YS_EXPORT int yolosod_a2_forward(const float* x, float* y, int B, int C, int H, int W, int num_areas, int num_heads,
+                                 const float* proj_w, const float* proj_b, const float* ln_w, const float* ln_b,
+                                 float ln_eps, const float* in_proj_w, const float* in_proj_b,
+                                 const float* mha_out_w, const float* mha_out_b, const float* oproj_w,
+                                 const float* oproj_b, void* workspace, size_t workspace_bytes, void* stream) {
+  YS_CHECK_ARG(x && y && proj_w && proj_b && ln_w && ln_b && in_proj_w && in_proj_b && mha_out_w && mha_out_b &&
+                   oproj_w && oproj_b,
+               "a2: null pointer");
+  YS_CHECK_ARG(B >= 0 && C > 0 && H > 0 && W > 0 && num_areas > 0, "a2: bad shape");
+  YS_CHECK_ARG(C % 16 == 0, "a2: C must be a multiple of 16");
+  if (B == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  const int A = num_areas;
+  const long HW = (long)H * W;
+  const long ntok = (long)B * A * W;
+  Carver cv(workspace, workspace_bytes);
+  float* XP = cv.take<float>((size_t)B * C * HW);
+  float* S = cv.take<float>((size_t)ntok * C);
+  float* U = cv.take<float>((size_t)ntok * C);
+  float* Q = cv.take<float>((size_t)ntok * 3 * C);
+  float* Z = cv.take<float>((size_t)ntok * C);
+  YS_CHECK_ARG(Z, "a2: workspace too small (%zu)", workspace_bytes);
+  int rc;
+  YS_CHECK_ARG(HW % 4 == 0, "a2: H*W must be a multiple of 4");
+  // XP = SiLU(Wp x + bp)  (Conv with folded BN, a2_attn.py:39): M = Cout, N = HW, batched over images
+  GemmArgs ga{};
+  ga.A = proj_w; ga.lda = C; ga.B = x; ga.b_bs = C * HW; ga.ldb = (int)HW; ga.M = C; ga.N = (int)HW; ga.K = C;
+  ga.epi = epi_plain(XP, C * HW, (int)HW);
+  ga.epi.bias = proj_b; ga.epi.bias_mode = 1; ga.epi.act = 1;
+  if ((rc = launch_gemm(ga, B, false, st))) return rc;
+  hipLaunchKernelGGL(a2_pool_tokens_kernel, dim3(B * A), dim3(256), 0, st, XP, S, C, H, W, A);
+  YS_CHECK_LAUNCH("a2_pool");
+  if ((rc = launch_layernorm(S, U, ntok, C, ln_w, ln_b, ln_eps, st))) return rc;
+  ga = GemmArgs{};
+  ga.A = U; ga.lda = C; ga.B = in_proj_w; ga.ldb = C; ga.M = (int)ntok; ga.N = 3 * C; ga.K = C;
+  ga.epi = epi_plain(Q, 0, 3 * C);
+  ga.epi.bias = in_proj_b; ga.epi.bias_mode = 2;
+  if ((rc = launch_gemm(ga, 1, true, st))) return rc;
+  if ((rc = launch_attention(Q, U, B, A * W, C, num_heads, st))) return rc;
+  ga = GemmArgs{};
+  ga.A = U; ga.lda = C; ga.B = mha_out_w; ga.ldb = C; ga.M = (int)ntok; ga.N = C; ga.K = C;
+  ga.epi = epi_plain(Z, 0, C);
+  ga.epi.bias = mha_out_b; ga.epi.bias_mode = 2;
+  if ((rc = launch_gemm(ga, 1, true, st))) return rc;
+  // T[img][n][t] = sum_c Wout[n][c] Z[img*AW + t][c]   (reuse S as T: B*C*A*W floats == ntok*C)
+  float* T = S;
+  ga = GemmArgs{};
+  ga.A = oproj_w; ga.lda = C; ga.B = Z; ga.b_bs = (long)A * W * C; ga.ldb = C; ga.M = C; ga.N = A * W; ga.K = C;
+  ga.epi = epi_plain(T, (long)C * A * W, A * W);
+  if ((rc = launch_gemm(ga, B, true, st))) return rc;
+  const long total = (long)B * C * HW;
+  hipLaunchKernelGGL(a2_upsample_out_kernel, dim3(gs_blocks(total)), dim3(256), 0, st, x, T, oproj_b, y, C, H, W, A,
+                     total);
+  YS_CHECK_LAUNCH("a2_upsample");
+  return 0;
+}

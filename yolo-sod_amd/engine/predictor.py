@@ -1,0 +1,77 @@
+"""Inference driver for tensor batches (the reference's predictor hot loop, minus the absent ``ultralytics/data``).
+
+Reference flow (``engine/predictor.py:116-143, 219-304`` and ``models/yolo/detect/predict.py:23-41``):
+``preprocess`` (tensor input: ``.to(device).float()``, no /255, no letterbox) -> ``AutoBackend`` forward of the
+fused model -> ``postprocess`` = ``non_max_suppression`` + ``scale_boxes`` (same-shape input: clip to the image).
+
+MI355X additions:
+* :meth:`DetectionPredictor.predict_padded` never syncs the host: NMS returns fixed-shape ``[B, max_det, 6]``
+  rows + counts, so a batch is one stream-ordered sequence of launches (graph-capturable).
+* Data parallel inference: one process per GPU; :func:`shard_bounds` splits images across ranks (no data-path
+  collective), :func:`gather_detections` is the single exchange step - an all-gather of the padded detections and
+  counts (RCCL over xGMI with backend ``nccl``; ``gloo`` on CPU for tests).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+from ..utils import ops
+
+
+@dataclass
+class Detections:
+    """Per-image result: ``boxes`` [n, 6] = (x1, y1, x2, y2, conf, cls) clipped to the image, ``index`` anchors."""
+
+    boxes: torch.Tensor
+    index: torch.Tensor
+    orig_shape: tuple
+
+
+class DetectionPredictor:
+    def __init__(self, model, conf=0.25, iou=0.7, max_det=300, classes=None, agnostic_nms=False,
+                 multi_label=False):
+        self.model = model
+        self.conf, self.iou, self.max_det = conf, iou, max_det
+        self.classes, self.agnostic, self.multi_label = classes, agnostic_nms, multi_label
+        self.device = next(model.parameters()).device
+
+    def preprocess(self, im: torch.Tensor) -> torch.Tensor:
+        return im.to(self.device, non_blocking=True).float()
+
+    @torch.inference_mode()
+    def predict_padded(self, im: torch.Tensor):
+        """(out [B, max_det, 6] clipped, counts [B] int32, index [B, max_det] int32) without host sync."""
+        x = self.preprocess(im)
+        preds = self.model(x)
+        y = preds[0] if isinstance(preds, (list, tuple)) else preds
+        out, counts, index = ops.non_max_suppression_padded(
+            y, self.conf, self.iou, classes=self.classes, agnostic=self.agnostic, multi_label=self.multi_label,
+            max_det=self.max_det)
+        ops.clip_boxes(out[..., :4], x.shape[2:])  # scale_boxes with gain 1 / pad 0 (same-shape tensor input)
+        return out, counts, index
+
+    def __call__(self, im: torch.Tensor):
+        out, counts, index = self.predict_padded(im)
+        n = counts.cpu().tolist()
+        shape = tuple(im.shape[2:])
+        return [Detections(out[i, : n[i]], index[i, : n[i]], shape) for i in range(len(n))]
+
+
+def shard_bounds(n: int, rank: int, world: int):
+    """Contiguous, balanced image shard [lo, hi) of rank ``rank``."""
+    base, rem = divmod(n, world)
+    lo = rank * base + min(rank, rem)
+    return lo, lo + base + (1 if rank < rem else 0)
+
+
+def gather_detections(out: torch.Tensor, counts: torch.Tensor, group=None):
+    """All-gather padded detections of equal-size shards: [B_local, D, 6] + [B_local] -> [world*B_local, ...]."""
+    world = dist.get_world_size(group)
+    g_out = torch.empty((world * out.shape[0], *out.shape[1:]), dtype=out.dtype, device=out.device)
+    g_cnt = torch.empty((world * counts.shape[0],), dtype=counts.dtype, device=counts.device)
+    dist.all_gather_into_tensor(g_out, out.contiguous(), group=group)
+    dist.all_gather_into_tensor(g_cnt, counts.contiguous(), group=group)
+    return g_out, g_cnt

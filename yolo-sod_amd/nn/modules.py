@@ -1,0 +1,389 @@
+"""Operator library resolved by YAML name (the reference's ``ultralytics.nn.modules`` API surface for this path).
+
+Classes keep the reference's names, constructor signatures, attribute names (hence ``state_dict`` keys) and the
+order in which they create parameters (hence seed-for-seed identical random init).
+
+* Backbone / neck building blocks (``Conv``, ``C2f``, ``Bottleneck``, ``SPPF``, ``Concat``) are ordinary PyTorch
+  modules: their convolutions run on PyTorch-ROCm (MIOpen). Reference: ``ultralytics/nn/modules/conv.py:37-55,
+  102-107, 323-333`` and ``block.py:178-197, 233-255, 343-356``.
+* The hot-path operators - ``SE``/``SE_Block``, ``CBAM_Block``, ``CA_Block``, ``A2_Attn``, ``SwinBlock`` and the
+  decode of ``Detect`` - run exclusively through the gfx950 HIP library (``yolosod_amd._hip``). They have no CPU
+  compute path: a CPU tensor raises. On the ``meta`` device they only propagate shapes (used for the stride probe
+  of :class:`~yolosod_amd.nn.tasks.DetectionModel`).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+
+from .. import _hip
+
+__all__ = (
+    "Conv", "DWConv", "Concat", "Bottleneck", "C2f", "SPPF", "DFL", "SE", "SE_Block", "CBAM_Block",
+    "ChannelAttention", "SpatialAttention", "CA_Block", "h_sigmoid", "A2_Attn", "WindowAttention", "SwinBlock",
+    "Detect",
+)
+
+
+def autopad(k, p=None, d=1):
+    """'same' padding (conv.py:28-34)."""
+    if d > 1:
+        k = d * (k - 1) + 1 if isinstance(k, int) else [d * (x - 1) + 1 for x in k]
+    if p is None:
+        p = k // 2 if isinstance(k, int) else [x // 2 for x in k]
+    return p
+
+
+def _is_meta(x: torch.Tensor) -> bool:
+    return x.device.type == "meta"
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# host PyTorch blocks
+# ---------------------------------------------------------------------------------------------------------------
+class Conv(nn.Module):
+    """Conv2d(no bias) + BatchNorm2d + SiLU; after ``fuse()`` the BN is folded into the conv (conv.py:37-55)."""
+
+    default_act = nn.SiLU()
+
+    def __init__(self, c1, c2, k=1, s=1, p=None, g=1, d=1, act=True):
+        super().__init__()
+        self.conv = nn.Conv2d(c1, c2, k, s, autopad(k, p, d), groups=g, dilation=d, bias=False)
+        self.bn = nn.BatchNorm2d(c2)
+        self.act = self.default_act if act is True else act if isinstance(act, nn.Module) else nn.Identity()
+
+    def forward(self, x):
+        return self.act(self.bn(self.conv(x)))
+
+    def forward_fuse(self, x):
+        return self.act(self.conv(x))
+
+
+class DWConv(Conv):
+    """Depth-wise Conv (conv.py:102-107)."""
+
+    def __init__(self, c1, c2, k=1, s=1, d=1, act=True):
+        super().__init__(c1, c2, k, s, g=math.gcd(c1, c2), d=d, act=act)
+
+
+class Concat(nn.Module):
+    def __init__(self, dimension=1):
+        super().__init__()
+        self.d = dimension
+
+    def forward(self, x):
+        return torch.cat(x, self.d)
+
+
+class Bottleneck(nn.Module):
+    def __init__(self, c1, c2, shortcut=True, g=1, k=(3, 3), e=0.5):
+        super().__init__()
+        c_ = int(c2 * e)
+        self.cv1 = Conv(c1, c_, k[0], 1)
+        self.cv2 = Conv(c_, c2, k[1], 1, g=g)
+        self.add = shortcut and c1 == c2
+
+    def forward(self, x):
+        return x + self.cv2(self.cv1(x)) if self.add else self.cv2(self.cv1(x))
+
+
+class C2f(nn.Module):
+    def __init__(self, c1, c2, n=1, shortcut=False, g=1, e=0.5):
+        super().__init__()
+        self.c = int(c2 * e)
+        self.cv1 = Conv(c1, 2 * self.c, 1, 1)
+        self.cv2 = Conv((2 + n) * self.c, c2, 1)
+        self.m = nn.ModuleList(Bottleneck(self.c, self.c, shortcut, g, k=((3, 3), (3, 3)), e=1.0) for _ in range(n))
+
+    def forward(self, x):
+        y = list(self.cv1(x).chunk(2, 1))
+        y.extend(m(y[-1]) for m in self.m)
+        return self.cv2(torch.cat(y, 1))
+
+
+class SPPF(nn.Module):
+    def __init__(self, c1, c2, k=5):
+        super().__init__()
+        c_ = c1 // 2
+        self.cv1 = Conv(c1, c_, 1, 1)
+        self.cv2 = Conv(c_ * 4, c2, 1, 1)
+        self.m = nn.MaxPool2d(kernel_size=k, stride=1, padding=k // 2)
+
+    def forward(self, x):
+        y = [self.cv1(x)]
+        y.extend(self.m(y[-1]) for _ in range(3))
+        return self.cv2(torch.cat(y, 1))
+
+
+class DFL(nn.Module):
+    """Distribution Focal Loss integral (block.py:64-83): fixed 1x1 conv with weights 0..c1-1.
+
+    Kept for the state_dict (``dfl.conv.weight``); the decode itself runs in ``yolosod_detect_decode``."""
+
+    def __init__(self, c1=16):
+        super().__init__()
+        self.conv = nn.Conv2d(c1, 1, 1, bias=False).requires_grad_(False)
+        x = torch.arange(c1, dtype=torch.float)
+        self.conv.weight.data[:] = nn.Parameter(x.view(1, c1, 1, 1))
+        self.c1 = c1
+
+
+def fold_conv_bn(conv: nn.Conv2d, bn: nn.BatchNorm2d):
+    """(weight, bias) of conv followed by eval-mode BN, with the reference's arithmetic (torch_utils.py:238-265)."""
+    w_conv = conv.weight.view(conv.out_channels, -1)
+    w_bn = torch.diag(bn.weight.div(torch.sqrt(bn.eps + bn.running_var)))
+    w = torch.mm(w_bn, w_conv).view(conv.weight.shape)
+    b_conv = torch.zeros(conv.weight.shape[0], device=conv.weight.device) if conv.bias is None else conv.bias
+    b_bn = bn.bias - bn.weight.mul(bn.running_mean).div(torch.sqrt(bn.running_var + bn.eps))
+    b = torch.mm(w_bn, b_conv.reshape(-1, 1)).reshape(-1) + b_bn
+    return w, b
+
+
+def conv_weight_bias(m: Conv):
+    """Folded (weight [c2, c1*k*k], bias [c2]) of a Conv whether or not ``fuse()`` has run."""
+    if hasattr(m, "bn"):
+        w, b = fold_conv_bn(m.conv, m.bn)
+    else:
+        w, b = m.conv.weight, m.conv.bias
+    return w.detach().reshape(w.shape[0], -1).contiguous(), b.detach().contiguous()
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# MAFN operators (HIP)
+# ---------------------------------------------------------------------------------------------------------------
+class SE(nn.Module):
+    """Squeeze-Excitation with lazily created fc1/fc2 (smallobj_modules.py:57-92).
+
+    The YAML argument is the *reduction*: hidden = max(C // reduction, 4). fc1/fc2 are created on first use for
+    the observed channel count; ``DetectionModel`` materialises them right after graph construction in layer order,
+    which reproduces the reference's RNG order (they are built during its stride probe)."""
+
+    def __init__(self, reduction: int = 16) -> None:
+        super().__init__()
+        self.reduction = reduction
+        self.fc1: nn.Conv2d | None = None
+        self.fc2: nn.Conv2d | None = None
+        self.in_channels: int | None = None
+
+    def _maybe_build(self, c: int, device):
+        hidden = max(c // self.reduction, 4)
+        if (self.fc1 is None) or (self.in_channels != c):
+            self.fc1 = nn.Conv2d(c, hidden, 1, bias=True)
+            self.fc2 = nn.Conv2d(hidden, c, 1, bias=True)
+            self.in_channels = c
+        if device is not None and torch.device(device).type != "meta":
+            self.fc1.to(device=device, dtype=torch.float32)
+            self.fc2.to(device=device, dtype=torch.float32)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        b, c, h, w = x.shape
+        if _is_meta(x):
+            if self.fc1 is None or self.in_channels != c:
+                raise RuntimeError("SE: lazy weights must be materialised before a meta shape probe")
+            return torch.empty_like(x)
+        self._maybe_build(c, x.device)
+        return _hip.se_forward(x, self.fc1.weight.detach(), self.fc1.bias.detach(), self.fc2.weight.detach(),
+                               self.fc2.bias.detach())
+
+
+SE_Block = SE
+
+
+class ChannelAttention(nn.Module):
+    """CBAM channel branch parameters (cbam_block.py:8-23)."""
+
+    def __init__(self, in_planes, ratio=16):
+        super().__init__()
+        self.avg_pool = nn.AdaptiveAvgPool2d(1)
+        self.max_pool = nn.AdaptiveMaxPool2d(1)
+        self.fc = nn.Sequential(nn.Conv2d(in_planes, in_planes // ratio, 1, bias=False), nn.ReLU(),
+                                nn.Conv2d(in_planes // ratio, in_planes, 1, bias=False))
+        self.sigmoid = nn.Sigmoid()
+
+
+class SpatialAttention(nn.Module):
+    """CBAM spatial branch parameters (cbam_block.py:25-37)."""
+
+    def __init__(self, kernel_size=7):
+        super().__init__()
+        self.conv1 = nn.Conv2d(2, 1, kernel_size, padding=kernel_size // 2, bias=False)
+        self.sigmoid = nn.Sigmoid()
+
+
+class CBAM_Block(nn.Module):
+    """CBAM (cbam_block.py:39-55): y = (x * ca) * sa."""
+
+    def __init__(self, c1, c2=None, reduction=16):
+        super().__init__()
+        self.channel_attention = ChannelAttention(c1, reduction)
+        self.spatial_attention = SpatialAttention()
+
+    def forward(self, x):
+        if _is_meta(x):
+            return torch.empty_like(x)
+        fc = self.channel_attention.fc
+        if self.spatial_attention.conv1.kernel_size != (7, 7):
+            raise RuntimeError("CBAM_Block: only the 7x7 spatial kernel is implemented")
+        return _hip.cbam_forward(x, fc[0].weight.detach(), fc[2].weight.detach(),
+                                 self.spatial_attention.conv1.weight.detach())
+
+
+class h_sigmoid(nn.Module):
+    def __init__(self, inplace=True):
+        super().__init__()
+        self.relu = nn.ReLU6(inplace=inplace)
+
+    def forward(self, x):
+        return self.relu(x + 3) / 6
+
+
+class CA_Block(nn.Module):
+    """Coordinate attention (ca_block.py:16-59): y = (x * a_w) * a_h."""
+
+    def __init__(self, c1, c2=None, reduction=32):
+        super().__init__()
+        self.pool_h = nn.AdaptiveAvgPool2d((None, 1))
+        self.pool_w = nn.AdaptiveAvgPool2d((1, None))
+        mip = max(8, c1 // reduction)
+        self.conv1 = nn.Conv2d(c1, mip, kernel_size=1, stride=1, padding=0)
+        self.bn1 = nn.BatchNorm2d(mip)
+        self.act = h_sigmoid()
+        self.conv_h = nn.Conv2d(mip, c1, kernel_size=1, stride=1, padding=0)
+        self.conv_w = nn.Conv2d(mip, c1, kernel_size=1, stride=1, padding=0)
+
+    def forward(self, x):
+        if _is_meta(x):
+            return torch.empty_like(x)
+        if self.training:
+            raise RuntimeError("CA_Block: HIP path is inference-only (eval-mode BatchNorm)")
+        d = lambda t: t.detach()  # noqa: E731
+        return _hip.ca_forward(x, d(self.conv1.weight), d(self.conv1.bias), d(self.bn1.weight), d(self.bn1.bias),
+                               d(self.bn1.running_mean), d(self.bn1.running_var), self.bn1.eps,
+                               d(self.conv_h.weight), d(self.conv_h.bias), d(self.conv_w.weight),
+                               d(self.conv_w.bias))
+
+
+class A2_Attn(nn.Module):
+    """Area attention (a2_attn.py:9-69): proj -> pool to areas -> LN -> MHA -> bilinear up -> out_proj -> +x."""
+
+    def __init__(self, c1, c2=None, num_areas=4, num_heads=4):
+        super().__init__()
+        if c2 is None:
+            c2 = c1
+        self.num_areas = num_areas
+        self.num_heads = num_heads
+        assert c1 % num_heads == 0, f"Input channels {c1} must be divisible by num_heads {num_heads}"
+        self.proj = Conv(c1, c1, 1)
+        self.attention = nn.MultiheadAttention(embed_dim=c1, num_heads=num_heads, batch_first=True)
+        self.out_proj = Conv(c1, c2, 1)
+        self.layer_norm = nn.LayerNorm(c1)
+
+    def forward(self, x):
+        if _is_meta(x):
+            return torch.empty((x.shape[0], self.out_proj.conv.out_channels, *x.shape[2:]), device="meta")
+        if self.training:
+            raise RuntimeError("A2_Attn: HIP path is inference-only")
+        if self.out_proj.conv.out_channels != x.shape[1]:
+            raise RuntimeError("A2_Attn: HIP path implements the residual (c2 == c1) form only")
+        pw, pb = conv_weight_bias(self.proj)
+        ow, ob = conv_weight_bias(self.out_proj)
+        at = self.attention
+        return _hip.a2_forward(x, self.num_areas, self.num_heads, pw, pb, self.layer_norm.weight.detach(),
+                               self.layer_norm.bias.detach(), self.layer_norm.eps, at.in_proj_weight.detach(),
+                               at.in_proj_bias.detach(), at.out_proj.weight.detach(), at.out_proj.bias.detach(),
+                               ow, ob)
+
+
+class WindowAttention(nn.Module):
+    """Parameters of the window attention (blocks_transformer.py:81-131)."""
+
+    def __init__(self, dim: int, num_heads: int = 4, window_size: int = 7, mlp_ratio: float = 2.0):
+        super().__init__()
+        self.window_size = window_size
+        self.dim = dim
+        self.norm1 = nn.LayerNorm(dim)
+        self.attn = nn.MultiheadAttention(dim, num_heads, batch_first=True)
+        self.norm2 = nn.LayerNorm(dim)
+        self.mlp = nn.Sequential(nn.Linear(dim, int(dim * mlp_ratio)), nn.GELU(), nn.Linear(int(dim * mlp_ratio), dim))
+
+
+class SwinBlock(nn.Module):
+    """dw3x3 -> window attention (pad, LN, MHA, MLP) -> pw1x1 -> BN -> SiLU -> +x (blocks_transformer.py:133-171)."""
+
+    def __init__(self, c: int, num_heads: int = 4, window_size: int = 7):
+        super().__init__()
+        self.dw = nn.Conv2d(c, c, 3, padding=1, groups=c, bias=False)
+        self.window_attn = WindowAttention(c, num_heads=num_heads, window_size=window_size)
+        self.pw = nn.Conv2d(c, c, 1, bias=False)
+        self.bn = nn.BatchNorm2d(c)
+        self.act = nn.SiLU(inplace=True)
+
+    def forward(self, x):
+        if _is_meta(x):
+            return torch.empty_like(x)
+        if self.training:
+            raise RuntimeError("SwinBlock: HIP path is inference-only (eval-mode BatchNorm)")
+        wa = self.window_attn
+        d = lambda t: t.detach()  # noqa: E731
+        return _hip.swin_forward(
+            x, wa.attn.num_heads, wa.window_size, d(self.dw.weight), d(wa.norm1.weight), d(wa.norm1.bias),
+            wa.norm1.eps, d(wa.attn.in_proj_weight), d(wa.attn.in_proj_bias), d(wa.attn.out_proj.weight),
+            d(wa.attn.out_proj.bias), d(wa.norm2.weight), d(wa.norm2.bias), wa.norm2.eps, d(wa.mlp[0].weight),
+            d(wa.mlp[0].bias), d(wa.mlp[2].weight), d(wa.mlp[2].bias), d(self.pw.weight), d(self.bn.weight),
+            d(self.bn.bias), d(self.bn.running_mean), d(self.bn.running_var), self.bn.eps)
+
+
+class Detect(nn.Module):
+    """YOLO Detect head (head.py:21-172). Towers stay PyTorch; ``_inference`` (DFL decode, anchors, stride,
+    class sigmoid) is one HIP kernel."""
+
+    dynamic = False
+    export = False
+    format = None
+    end2end = False
+    max_det = 300
+    shape = None
+    anchors = torch.empty(0)
+    strides = torch.empty(0)
+    legacy = False
+
+    def __init__(self, nc=80, ch=()):
+        super().__init__()
+        self.nc = nc
+        self.nl = len(ch)
+        self.reg_max = 16
+        self.no = nc + self.reg_max * 4
+        self.stride = torch.zeros(self.nl)
+        c2, c3 = max((16, ch[0] // 4, self.reg_max * 4)), max(ch[0], min(self.nc, 100))
+        self.cv2 = nn.ModuleList(
+            nn.Sequential(Conv(x, c2, 3), Conv(c2, c2, 3), nn.Conv2d(c2, 4 * self.reg_max, 1)) for x in ch)
+        self.cv3 = (
+            nn.ModuleList(nn.Sequential(Conv(x, c3, 3), Conv(c3, c3, 3), nn.Conv2d(c3, self.nc, 1)) for x in ch)
+            if self.legacy
+            else nn.ModuleList(
+                nn.Sequential(nn.Sequential(DWConv(x, x, 3), Conv(x, c3, 1)),
+                              nn.Sequential(DWConv(c3, c3, 3), Conv(c3, c3, 1)), nn.Conv2d(c3, self.nc, 1))
+                for x in ch))
+        self.dfl = DFL(self.reg_max) if self.reg_max > 1 else nn.Identity()
+
+    def forward(self, x):
+        for i in range(self.nl):
+            x[i] = torch.cat((self.cv2[i](x[i]), self.cv3[i](x[i])), 1)
+        if self.training:
+            return x
+        y = self._inference(x)
+        return y if self.export else (y, x)
+
+    def _inference(self, x):
+        if x[0].device.type == "meta":
+            a = sum(t.shape[2] * t.shape[3] for t in x)
+            return torch.empty((x[0].shape[0], 4 + self.nc, a), device="meta")
+        return _hip.detect_decode(x, [float(s) for s in self.stride], self.nc, self.reg_max)
+
+    def bias_init(self):
+        """Detect biases (head.py:133-144)."""
+        for a, b, s in zip(self.cv2, self.cv3, self.stride):
+            a[-1].bias.data[:] = 1.0
+            b[-1].bias.data[: self.nc] = math.log(5 / self.nc / (640 / s) ** 2)

@@ -1,0 +1,273 @@
+"""Graph builder / executor for the reference's model YAMLs (``ultralytics/nn/tasks.py`` semantics).
+
+* :func:`parse_model` - ``tasks.py:967-1169``: YAML rows ``[from, n, module, args]`` -> ``nn.Sequential``, with the
+  reference's depth/width scaling (``make_divisible(min(c2, max_channels) * width, 8)``), ``scales`` support and
+  the channel-injection rules of the MAFN operators (``tasks.py:1122-1146``). Modules are resolved **by name**
+  through a registry, so a caller (e.g. the CPU oracle in ``oracle/``) can substitute implementations while
+  keeping parameter layout and RNG order.
+* :class:`DetectionModel` - ``tasks.py:336-379``: builds the graph, materialises the lazy SE weights in layer
+  order, probes strides (shape-only, on the ``meta`` device), applies ``Detect.bias_init`` and
+  ``initialize_weights`` (every BatchNorm2d: eps=1e-3, momentum=0.03) and loads the BatchNorm running statistics
+  that the reference's *train-mode* 256x256 stride probe leaves behind (shipped per config as
+  ``cfg/<name>.probe.npz``, recorded from the reference by ``tests/golden/make_golden.py``).
+* :meth:`BaseModel.fuse` - ``tasks.py:227-255``: folds BN into ``Conv``/``DWConv`` (SwinBlock.bn and CA.bn1 stay
+  unfused, as in the reference).
+"""
+from __future__ import annotations
+
+import ast
+import contextlib
+import copy
+import hashlib
+import math
+import re
+from pathlib import Path
+
+import numpy as np
+import torch
+import torch.nn as nn
+import yaml
+
+from . import modules as M
+
+CFG_DIR = Path(__file__).resolve().parent.parent / "cfg"
+
+# name -> class; the YAML resolves module strings through this (tasks.py:995-1002)
+DEFAULT_REGISTRY = {
+    "Conv": M.Conv, "DWConv": M.DWConv, "Concat": M.Concat, "Bottleneck": M.Bottleneck, "C2f": M.C2f,
+    "SPPF": M.SPPF, "DFL": M.DFL, "SE": M.SE, "SE_Block": M.SE_Block, "CBAM_Block": M.CBAM_Block,
+    "CA_Block": M.CA_Block, "A2_Attn": M.A2_Attn, "SwinBlock": M.SwinBlock, "Detect": M.Detect,
+}
+
+# channel-injection classes of the reference parse_model (by name)
+_SCALED_C1C2 = {"Conv", "DWConv", "Bottleneck", "C2f", "SPPF"}
+_REPEAT_INSERT = {"C2f"}
+_KEEP_CH = {"SE", "SE_Block", "SwinBlock", "CA_Block", "A2_Attn", "CBAM_Block"}
+_DETECT = {"Detect"}
+
+
+def make_divisible(x, divisor):
+    """ops.py:130-143."""
+    if isinstance(divisor, torch.Tensor):
+        divisor = int(divisor.max())
+    return math.ceil(x / divisor) * divisor
+
+
+def guess_model_scale(model_path) -> str:
+    """tasks.py guess_model_scale: the n/s/m/l/x letter after 'yolov<digits>' in the file stem, else ''."""
+    m = re.search(r"yolov\d+([nslmx])", Path(model_path).stem)
+    return m.group(1) if m else ""
+
+
+def yaml_model_load(path) -> dict:
+    """Load a model YAML (tasks.py:1172-1185 minus the unified-name lookup; ``scale`` from the YAML wins)."""
+    path = Path(path)
+    if not path.exists() and (CFG_DIR / path.name).exists():
+        path = CFG_DIR / path.name
+    d = yaml.safe_load(path.read_text())
+    d.setdefault("scale", guess_model_scale(path))
+    d["yaml_file"] = str(path)
+    return d
+
+
+def parse_model(d: dict, ch: int, verbose: bool = False, registry: dict | None = None):
+    """YAML dict -> (nn.Sequential, sorted save list). Mirrors tasks.py:967-1169 for the operators of this path."""
+    reg = dict(DEFAULT_REGISTRY)
+    if registry:
+        reg.update(registry)
+    legacy = True
+    max_channels = float("inf")
+    nc, act, scales = (d.get(x) for x in ("nc", "activation", "scales"))
+    depth, width, kpt_shape = (d.get(x, 1.0) for x in ("depth_multiple", "width_multiple", "kpt_shape"))
+    if scales:
+        scale = d.get("scale")
+        if not scale:
+            scale = tuple(scales.keys())[0]
+        depth, width, max_channels = scales[scale]
+    if act:
+        raise NotImplementedError("custom 'activation' is not supported on this path")
+
+    ch = [ch]
+    layers, save, c2 = [], [], ch[-1]
+    for i, (f, n, m, args) in enumerate(d.get("backbone", []) + d.get("neck", []) + d.get("head", [])):
+        name = m
+        if m.startswith("nn."):
+            cls = getattr(torch.nn, m[3:])
+        else:
+            if m not in reg:
+                raise KeyError(f"module '{m}' (layer {i}) is not provided by yolosod_amd")
+            cls = reg[m]
+        args = list(args)
+        for j, a in enumerate(args):
+            if isinstance(a, str):
+                with contextlib.suppress(ValueError):
+                    args[j] = locals()[a] if a in locals() else ast.literal_eval(a)
+        n = n_ = max(round(n * depth), 1) if n > 1 else n
+        if name in _SCALED_C1C2:
+            c1, c2 = ch[f], args[0]
+            if c2 != nc:
+                c2 = make_divisible(min(c2, max_channels) * width, 8)
+            args = [c1, c2, *args[1:]]
+            if name in _REPEAT_INSERT:
+                args.insert(2, n)
+                n = 1
+        elif name == "Concat":
+            c2 = sum(ch[x] for x in f)
+        elif name in _KEEP_CH:
+            c2 = ch[f]
+            if name in {"SwinBlock", "CA_Block", "CBAM_Block"}:
+                args = [ch[f], *args]
+            elif name == "A2_Attn":
+                args = [ch[f], None, *args]
+        elif name in _DETECT:
+            f_list = f if isinstance(f, (list, tuple)) else [f]
+            args.append([ch[x] for x in f_list])
+            cls.legacy = legacy
+        else:
+            c2 = ch[f]
+
+        m_ = nn.Sequential(*(cls(*args) for _ in range(n))) if n > 1 else cls(*args)
+        t = name if not name.startswith("nn.") else f"torch.nn.modules.{name[3:]}"
+        m_.np = sum(x.numel() for x in m_.parameters())
+        m_.i, m_.f, m_.type = i, f, t
+        m_.c_in = ch[f] if isinstance(f, int) else [ch[x] for x in f]
+        if verbose:
+            print(f"{i:>3}{str(f):>20}{n_:>3}{m_.np:10.0f}  {t:<45}{str(args):<30}")
+        save.extend(x % i for x in ([f] if isinstance(f, int) else f) if x != -1)
+        layers.append(m_)
+        if i == 0:
+            ch = []
+        ch.append(c2)
+    return nn.Sequential(*layers), sorted(save)
+
+
+def initialize_weights(model: nn.Module) -> None:
+    """torch_utils.py:410-420."""
+    for m in model.modules():
+        t = type(m)
+        if t is nn.BatchNorm2d:
+            m.eps = 1e-3
+            m.momentum = 0.03
+        elif t in {nn.Hardswish, nn.LeakyReLU, nn.ReLU, nn.ReLU6, nn.SiLU}:
+            m.inplace = True
+
+
+def state_dict_sha256(model: nn.Module) -> str:
+    """Hash over (key, float tensor bytes) in state_dict order - the manifest identity of seeded weights."""
+    h = hashlib.sha256()
+    for k, v in model.state_dict().items():
+        h.update(k.encode())
+        h.update(v.detach().cpu().contiguous().numpy().tobytes())
+    return h.hexdigest()
+
+
+class BaseModel(nn.Module):
+    def forward(self, x, *args, **kwargs):
+        return self.predict(x, *args, **kwargs)
+
+    def predict(self, x, profile=False, visualize=False, augment=False, embed=None):
+        return self._predict_once(x)
+
+    def _predict_once(self, x):
+        """tasks.py:165-192: run layers in YAML order, keeping the outputs other layers read."""
+        y = []
+        for m in self.model:
+            if m.f != -1:
+                x = y[m.f] if isinstance(m.f, int) else [x if j == -1 else y[j] for j in m.f]
+            x = m(x)
+            y.append(x if m.i in self.save else None)
+        return x
+
+    def is_fused(self, thresh=10):
+        bn = tuple(v for k, v in nn.__dict__.items() if "Norm" in k)
+        return sum(isinstance(v, bn) for v in self.modules()) < thresh
+
+    def fuse(self, verbose=False):
+        """Fold BN into Conv/DWConv (tasks.py:227-255 + torch_utils.fuse_conv_and_bn :238-265)."""
+        if not self.is_fused():
+            for m in self.model.modules():
+                if isinstance(m, M.Conv) and hasattr(m, "bn"):
+                    m.conv = _fuse_conv_and_bn(m.conv, m.bn)
+                    delattr(m, "bn")
+                    m.forward = m.forward_fuse
+        return self
+
+
+def _fuse_conv_and_bn(conv: nn.Conv2d, bn: nn.BatchNorm2d) -> nn.Conv2d:
+    fused = nn.Conv2d(conv.in_channels, conv.out_channels, kernel_size=conv.kernel_size, stride=conv.stride,
+                      padding=conv.padding, dilation=conv.dilation, groups=conv.groups,
+                      bias=True).requires_grad_(False).to(conv.weight.device)
+    with torch.no_grad():
+        w, b = M.fold_conv_bn(conv, bn)
+        fused.weight.copy_(w)
+        fused.bias.copy_(b)
+    return fused
+
+
+def probe_manifest_path(yaml_file) -> Path:
+    return CFG_DIR / (Path(yaml_file).stem + ".probe.npz")
+
+
+class DetectionModel(BaseModel):
+    """Detection model (tasks.py:336-379) for the YOLO-SOD YAMLs."""
+
+    def __init__(self, cfg="yolov12-sod-fusion-v5-simple.yaml", ch=3, nc=None, verbose=False, registry=None,
+                 probe_stats: bool = True):
+        super().__init__()
+        self.yaml = cfg if isinstance(cfg, dict) else yaml_model_load(cfg)
+        ch = self.yaml["ch"] = self.yaml.get("ch", ch)
+        if nc and nc != self.yaml["nc"]:
+            self.yaml["nc"] = nc
+        self.model, self.save = parse_model(copy.deepcopy(self.yaml), ch=ch, verbose=verbose, registry=registry)
+        self.names = {i: f"{i}" for i in range(self.yaml["nc"])}
+        self.inplace = self.yaml.get("inplace", True)
+
+        # lazy SE weights: the reference creates them during the stride probe, in forward (= layer) order,
+        # after every eager module -> same RNG stream position here.
+        for m in self.model:
+            if isinstance(m, M.SE):
+                m._maybe_build(m.c_in, None)
+
+        det = self.model[-1]
+        if not isinstance(det, M.Detect):
+            raise NotImplementedError("only Detect-headed models are supported")
+        det.stride = self._probe_strides(ch)
+        self.stride = det.stride
+        det.bias_init()
+        initialize_weights(self)
+        if probe_stats:
+            self._load_probe_stats()
+
+    def _probe_strides(self, ch: int, s: int = 256) -> torch.Tensor:
+        """Shape-only replica of the reference's 256x256 stride probe (tasks.py:369), on the meta device."""
+        meta = copy.deepcopy(self).to("meta")
+        meta.train()
+        with torch.no_grad():
+            out = meta._predict_once(torch.zeros(1, ch, s, s, device="meta"))
+        return torch.tensor([s / x.shape[-2] for x in out])
+
+    def _load_probe_stats(self) -> None:
+        """BatchNorm running stats produced by the reference's train-mode stride probe (not re-derivable from the
+        seed alone: they depend on that forward's arithmetic). Recorded from the reference, see module doc."""
+        p = probe_manifest_path(self.yaml.get("yaml_file", ""))
+        if not p.exists():
+            import warnings
+            warnings.warn(f"no stride-probe BatchNorm manifest {p.name}; running stats keep their init values")
+            return
+        z = np.load(p, allow_pickle=False)
+        sd = self.state_dict()
+        with torch.no_grad():
+            for k in z.files:
+                if k not in sd:
+                    raise KeyError(f"probe manifest key {k} not in model")
+                sd[k].copy_(torch.from_numpy(z[k]).to(sd[k].dtype))
+
+
+def build_model(cfg="yolov12-sod-fusion-v5-simple.yaml", seed: int = 0, device="cuda", fuse: bool = True,
+                registry=None) -> DetectionModel:
+    """Seeded construction -> (fused) eval model on ``device`` (autobackend.py:145-156 semantics)."""
+    torch.manual_seed(seed)
+    m = DetectionModel(cfg, registry=registry)
+    if fuse:
+        m.fuse()
+    return m.to(device).eval()

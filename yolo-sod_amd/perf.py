@@ -1,0 +1,64 @@
+"""Analytic cost model of the hot-path operators: algorithmic HBM bytes and FLOPs per call.
+
+Bytes count compulsory traffic only - each activation tensor read once and written once, weights once; FLOPs
+count multiply-adds as 2. These are the numerators of ``roofline.achieved`` in bench.py.
+"""
+from __future__ import annotations
+
+F32 = 4
+
+# MI355X peaks (MI355X_MICROARCH.md "Chip-level parameters")
+PEAK_HBM_GBS = 8000.0
+PEAK_FP32_MFMA_TFLOPS = 157.3
+
+
+def swin_geom(H, W, ws=7):
+    if H <= ws and W <= ws:
+        return H, W, H, W
+    wh, ww = min(ws, H), min(ws, W)
+    return wh, ww, H + (wh - H % wh) % wh, W + (ww - W % ww) % ww
+
+
+def op_cost(key):
+    """key = (op, shape, extra) as recorded by yolosod_amd._hip.op_timer -> (bytes, flops)."""
+    op, shape, extra = key
+    if op in ("se", "cbam", "ca"):
+        B, C, H, W = shape
+        hid = extra
+        act = 2 * B * C * H * W * F32
+        w = (2 * C * hid + C + hid) * F32
+        flops = B * C * H * W * (2 if op == "se" else 6)
+        return act + w, flops
+    if op == "a2":
+        B, C, H, W = shape
+        A, heads = extra
+        L = A * W
+        act = 2 * B * C * H * W * F32
+        w = (2 * (C * C + C) + 4 * C * C + 4 * C + 2 * C) * F32
+        conv = 2 * 2 * C * C * H * W  # proj + out_proj (1x1 convs on the full map)
+        mha = 2 * L * C * 3 * C + 2 * L * C * C + 2 * 2 * L * L * C
+        return act + w, B * (conv + mha)
+    if op == "swin":
+        B, C, H, W = shape
+        heads, ws, hid = extra
+        wh, ww, Hp, Wp = swin_geom(H, W, ws)
+        L = wh * ww
+        tok_p = Hp * Wp
+        act = 2 * B * C * H * W * F32
+        w = (9 * C + 4 * C * C + 3 * C + C + 2 * C * hid + hid + C + C * C + 6 * C) * F32
+        dense = tok_p * (2 * C * 3 * C + 2 * C * C + 2 * 2 * C * hid) + H * W * 2 * C * C
+        attn = tok_p * 2 * 2 * L * C
+        dw = H * W * 2 * 9 * C
+        return act + w, B * (dense + attn + dw)
+    if op == "decode":
+        B, A = shape
+        nc = extra
+        return B * A * ((64 + nc) + (4 + nc)) * F32, B * A * (64 * 4 + nc * 4)
+    if op == "nms":
+        B, nc, A = shape
+        return B * A * (4 + nc) * F32, 0
+    raise KeyError(op)
+
+
+def bound_of(op):
+    return "mfma" if op in ("swin", "a2") else "hbm"
