@@ -84,7 +84,10 @@ def main():
     ap.add_argument("--conf", type=float, default=0.25)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-images", type=int, default=16)
+    ap.add_argument("--miopen-benchmark", action="store_true", help="torch.backends.cudnn.benchmark (MIOpen find)")
     args = ap.parse_args()
+    if args.miopen_benchmark:
+        torch.backends.cudnn.benchmark = True
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

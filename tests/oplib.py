@@ -11,13 +11,18 @@ from yolosod_amd.nn import modules as M
 
 
 def build_fixture_module(name: str, classes: dict | None = None):
-    """(module, fixture args) for recipes.OPS[name]; ``classes`` overrides op-name -> class."""
+    """(module, sha256 of the recipe parameters before any BN folding) for recipes.OPS[name].
+
+    ``classes`` overrides op-name -> class. The pre-fold hash is platform independent (seeded CPU generator);
+    the folded A2 weights can differ by an ulp across host CPUs (BLAS kernel of the fold), which the output
+    tolerance absorbs."""
     op, args, shape = recipes.OPS[name]
     cls = (classes or {}).get(op) or getattr(M, op)
     m = cls(*args)
     if op == "SE_Block":
         m._maybe_build(shape[1], None)
     recipes.perturb_(m, recipes.seed_of(name))
+    sha = recipes.params_sha256(m)
     if op == "A2_Attn":  # fixtures use the fused Conv form (AutoBackend fuse=True)
         for c in (m.proj, m.out_proj):
             w, b = M.fold_conv_bn(c.conv, c.bn)
@@ -28,7 +33,7 @@ def build_fixture_module(name: str, classes: dict | None = None):
             c.conv = conv
             delattr(c, "bn")
             c.forward = c.forward_fuse
-    return m.eval(), recipes.params_sha256(m)
+    return m.eval(), sha
 
 
 def tol_close(y, ref, atol, rtol):

@@ -20,7 +20,7 @@ ATOL, RTOL = 2e-5, 2e-5
 def test_oracle_op_matches_reference(name):
     z = golden(f"ops_{name}")
     m, sha = build_fixture_module(name, OP_CLASSES)
-    assert sha == str(z["params_sha256"]), "parameter recipe drifted from the fixture"
+    assert sha == str(z["params_sha256_unfused"]), "parameter recipe drifted from the fixture"
     x = torch.from_numpy(z["x"])
     with torch.inference_mode():
         y = m(x)

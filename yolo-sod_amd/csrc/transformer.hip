@@ -108,6 +108,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
   const float* A = g.A + (long)bz * g.a_bs;
   const float* B = g.B + (long)bz * g.b_bs;
   const int M = g.M, N = g.N, K = g.K;
+  const bool vec_b = (g.ldb & 3) == 0 && (g.b_bs & 3) == 0;  // float4 rows of an N-contiguous B
 
   float4 ra[NA], rb[NB];
   auto load_tiles = [&](int k0) {
@@ -129,7 +130,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
         const int kl = idx / (BN / 4), nq = (idx % (BN / 4)) * 4;
         const int n = n0 + nq;
         const float* src = B + (long)(k0 + kl) * g.ldb + n;
-        if (n + 3 < N) {
+        if (n + 3 < N && vec_b) {
           rb[i] = *reinterpret_cast<const float4*>(src);
         } else {
           rb[i].x = (n < N) ? src[0] : 0.f;
@@ -214,7 +215,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
 
 static int launch_gemm(const GemmArgs& g, int batch, bool b_kc, hipStream_t st) {
   YS_CHECK_ARG(g.K % 16 == 0, "gemm: K=%d must be a multiple of 16", g.K);
-  YS_CHECK_ARG(g.lda % 4 == 0 && g.ldb % 4 == 0, "gemm: lda/ldb must be multiples of 4");
+  YS_CHECK_ARG(g.lda % 4 == 0 && (!b_kc || g.ldb % 4 == 0), "gemm: lda (and ldb of a K-contiguous B) must be multiples of 4");
   YS_CHECK_ARG(((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.B & 15) == 0, "gemm: A/B must be 16-byte aligned");
   if (g.M == 0 || g.N == 0 || batch == 0) return 0;
   const bool wide = (g.N % 128 == 0) || g.N > 256;
@@ -734,7 +735,6 @@ YS_EXPORT int yolosod_a2_forward(const float* x, float* y, int B, int C, int H, 
   float* Z = cv.take<float>((size_t)ntok * C);
   YS_CHECK_ARG(Z, "a2: workspace too small (%zu)", workspace_bytes);
   int rc;
-  YS_CHECK_ARG(HW % 4 == 0, "a2: H*W must be a multiple of 4");
   // XP = SiLU(Wp x + bp)  (Conv with folded BN, a2_attn.py:39): M = Cout, N = HW, batched over images
   GemmArgs ga{};
   ga.A = proj_w; ga.lda = C; ga.B = x; ga.b_bs = C * HW; ga.ldb = (int)HW; ga.M = C; ga.N = (int)HW; ga.K = C;
