@@ -60,6 +60,8 @@ int yolosod_a2_forward(const float* x, float* y, int B, int C, int H, int W, int
  * :100-131, window_partition :8-47, window_reverse :49-79).  dw: [C,1,3,3]; in_proj [3C,C]; mlp1 [hid,C];
  * mlp2 [C,hid]; pw [C,C,1,1]; bn in eval mode (not fused by fuse()). */
 size_t yolosod_swin_workspace(int B, int C, int H, int W, int window, int mlp_hidden);
+/* heads-aware query: small when the fused per-window kernel handles the shape (C in {32,64,128}, <=49 tokens) */
+size_t yolosod_swin_workspace_v2(int B, int C, int H, int W, int num_heads, int window, int mlp_hidden);
 int yolosod_swin_forward(const float* x, float* y, int B, int C, int H, int W, int num_heads, int window,
                          const float* dw_w, const float* ln1_w, const float* ln1_b, float ln1_eps,
                          const float* in_proj_w, const float* in_proj_b, const float* out_proj_w,

@@ -1,0 +1,53 @@
+"""Micro-benchmark of individual HIP operators at the bs=32 640x640 shapes (GPU only; for rocprof A/B work)."""
+import sys
+import time
+from pathlib import Path
+
+import torch
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "tests"))
+sys.path.insert(0, str(ROOT / "tests" / "golden"))
+import yolosod_import  # noqa: E402,F401
+import recipes  # noqa: E402
+from yolosod_amd import _hip, perf  # noqa: E402
+from yolosod_amd.nn import modules as M  # noqa: E402
+
+CASES = {
+    "swin_L28": ("SwinBlock", (64, 2, 7), (32, 64, 160, 160)),
+    "swin_L9": ("SwinBlock", (256, 4, 7), (32, 256, 40, 40)),
+    "a2_L12": ("A2_Attn", (512, None, 8, 8), (32, 512, 20, 20)),
+    "se_L1": ("SE_Block", (64,), (32, 32, 320, 320)),
+    "cbam_L4": ("CBAM_Block", (64, 128, 16), (32, 64, 160, 160)),
+    "ca_L32": ("CA_Block", (128, 256, 32), (32, 128, 80, 80)),
+}
+
+
+def main():
+    names = sys.argv[1:] or list(CASES)
+    dev = torch.device("cuda")
+    for name in names:
+        op, args, shape = CASES[name]
+        m = getattr(M, op)(*args)
+        if op == "SE_Block":
+            m._maybe_build(shape[1], None)
+        recipes.perturb_(m, 1)
+        m = m.to(dev).eval()
+        x = torch.randn(shape, device=dev)
+        with torch.inference_mode():
+            for _ in range(3):
+                m(x)
+            torch.cuda.synchronize()
+            with _hip.op_timer() as t:
+                for _ in range(10):
+                    m(x)
+            d = t.durations_ms()
+        key = d[0][0]
+        ms = sum(v for _, v in d) / len(d)
+        b, f = perf.op_cost(key)
+        print(f"{name:10s} {ms:8.3f} ms  {b / ms / 1e6:8.1f} GB/s  {f / ms / 1e9:7.2f} TFLOP/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -85,7 +85,7 @@ def test_se_chunked_equals_unchunked(cuda):
 
 
 @pytest.mark.parametrize("M_,N,K,bkc", [(300, 192, 64, True), (1000, 64, 128, True), (129, 768, 256, True),
-                                         (512, 400, 512, False), (64, 1600, 64, False), (130, 13, 16, True),
+                                         (512, 400, 512, False), (64, 1600, 64, False), (130, 13, 32, True),
                                          (70, 150, 32, False)])
 def test_gemm_f32(M_, N, K, bkc, cuda):
     from yolosod_amd import _hip

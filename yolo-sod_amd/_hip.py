@@ -38,6 +38,7 @@ SIGNATURES = {
     "yolosod_a2_forward": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp, _vp,
                                 _vp, _vp, _sz, _vp]),
     "yolosod_swin_workspace": (_sz, [_i, _i, _i, _i, _i, _i]),
+    "yolosod_swin_workspace_v2": (_sz, [_i, _i, _i, _i, _i, _i, _i]),
     "yolosod_swin_forward": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp, _vp, _vp,
                                   _f, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f, _vp, _sz, _vp]),
     "yolosod_detect_decode": (_i, [_i, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp]),
@@ -225,7 +226,7 @@ def swin_forward(x, num_heads, window, dw_w, ln1_w, ln1_b, ln1_eps, in_w, in_b, 
     if C % num_heads or (C // num_heads) not in (8, 16, 32, 64, 128):
         raise RuntimeError(f"SwinBlock: head dim {C}/{num_heads} unsupported")
     y = torch.empty_like(x)
-    ws = _workspace(lib.yolosod_swin_workspace(B, C, H, W, window, hid), x.device)
+    ws = _workspace(lib.yolosod_swin_workspace_v2(B, C, H, W, num_heads, window, hid), x.device)
     _check(_launch(("swin", tuple(x.shape), (num_heads, window, hid)), lib.yolosod_swin_forward,
         _dev(x, "x"), _dev(y, "y"), B, C, H, W, num_heads, window, _p(dw_w, "dw.weight", C * 9),
         _p(ln1_w, "norm1.weight", C), _p(ln1_b, "norm1.bias", C), float(ln1_eps),

@@ -1,0 +1,335 @@
+// Exact-fp32 MFMA GEMM for gfx950 with fused prologue / epilogue (used by the Swin and A2 drivers).
+//
+//   out(b, m, n) = epilogue( sum_k A'(b, m, k) * B(b, k, n) )
+//   A(b,m,k) = A[b*a_bs + m*lda + k]       (K-contiguous)
+//   A'      = A, or LayerNorm_k(A) when ln_w != nullptr (row statistics over the full K computed in the block
+//             prologue, normalisation applied while staging the tile -> no separate LN pass over HBM)
+//   B_KC:  B(b,k,n) = B[b*b_bs + n*ldb + k]  (K-contiguous: nn.Linear / 1x1-conv weights, token-major acts)
+//   !B_KC: B(b,k,n) = B[b*b_bs + k*ldb + n]  (N-contiguous: NCHW activations)
+//
+// Tiling: 4 waves, each an (MI*32)x(NI*32) output block of v_mfma_f32_32x32x2_f32 accumulators (128x128 tiles with
+// 2x2 per wave, or 128x64 with 1x2 for narrow N); block tile x BK=32; LDS double-buffered with register prefetch (one barrier per K block).
+// The MFMA's k index is permuted: lane half h takes k = h*16 + s (s = 0..15) of each 32-deep block, so the A and
+// K-contiguous B fragments are 16-byte ds_read_b128 along k from a [row][k] LDS image whose 36-float row stride
+// keeps each 16-lane read group conflict-free. The summation order differs from a plain k loop only by rounding.
+#pragma once
+#include "common.h"
+
+namespace ys {
+
+struct Epi {
+  const float* bias;   // bias_mode 1: per-row m, 2: per-col n
+  int bias_mode;
+  const float* scale;  // folded BN:  v = v*scale + shift, bn_mode 1: per-row, 2: per-col
+  const float* shift;
+  int bn_mode;
+  int act;             // 0 none, 1 SiLU, 2 GELU(erf), 3 ReLU
+  const float* res;    // residual added after activation (same indexing as out)
+  long res_bs;
+  int ldr;
+  float* out;
+  long out_bs;
+  int ldc;
+  // window-reverse output (SwinBlock): n = global token, m = channel; out/res are NCHW [img][M][H][W]
+  int swin;
+  int sw_H, sw_W, sw_wh, sw_ww, sw_nWx, sw_nWin;
+};
+
+struct GemmArgs {
+  const float* A;
+  long a_bs;
+  int lda;
+  const float* B;
+  long b_bs;
+  int ldb;
+  int M, N, K;
+  const float* ln_w;  // optional LayerNorm of A rows
+  const float* ln_b;
+  float ln_eps;
+  Epi epi;
+};
+
+__device__ __forceinline__ float apply_act(float v, int act) {
+  if (act == 1) return siluf_(v);
+  if (act == 2) return geluf_(v);
+  if (act == 3) return fmaxf(v, 0.f);
+  return v;
+}
+
+__device__ __forceinline__ float epi_value(const Epi& e, int m, int n, float v) {
+  if (e.bias_mode == 1) v += e.bias[m];
+  else if (e.bias_mode == 2) v += e.bias[n];
+  if (e.bn_mode == 1) v = v * e.scale[m] + e.shift[m];
+  else if (e.bn_mode == 2) v = v * e.scale[n] + e.shift[n];
+  return apply_act(v, e.act);
+}
+
+template <int WM, int WN, int MI, int NI, bool B_KC, bool A_LN>
+__global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
+  constexpr int BM = WM * MI * 32;
+  constexpr int BN = WN * NI * 32;
+  constexpr int BK = 32;
+  constexpr int SK = BK + 4;                     // [row][k] images
+  constexpr int SBN = BN + 4;                    // [k][n] image (N-contiguous B)
+  constexpr int A_ELEMS = BM * SK;
+  constexpr int B_ELEMS = B_KC ? BN * SK : BK * SBN;
+  constexpr int NA = BM * BK / 4 / 256;          // float4 per thread per A tile
+  constexpr int NB = BN * BK / 4 / 256;
+  static_assert(WM * WN == 4, "4 waves");
+  __shared__ __attribute__((aligned(16))) float smem[2 * A_ELEMS + 2 * B_ELEMS + (A_LN ? 2 * BM : 0)];
+  float* As = smem;
+  float* Bs = smem + 2 * A_ELEMS;
+  float* s_mean = smem + 2 * A_ELEMS + 2 * B_ELEMS;
+  float* s_rstd = s_mean + BM;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int bz = blockIdx.z;
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const float* A = g.A + (long)bz * g.a_bs;
+  const float* B = g.B + (long)bz * g.b_bs;
+  const int M = g.M, N = g.N, K = g.K;
+  const bool vec_b = (g.ldb & 3) == 0 && (g.b_bs & 3) == 0;
+
+  if (A_LN) {
+    // Row statistics over the full K: TPR threads per row, each streaming a strided share of the row with
+    // 8 float4 loads in flight, two-pass (mean, M2) per chunk combined with Chan's formula, then across the
+    // row's threads with shuffles. Rows >= M get (0, 0).
+    constexpr int TPR = 256 / BM;  // 2 (BM=128)
+    const int r = tid / TPR, part = tid % TPR;
+    const int m = m0 + r;
+    float cnt = 0.f, mean = 0.f, m2 = 0.f;
+    if (m < M) {
+      const float4* ar = reinterpret_cast<const float4*>(A + (long)m * g.lda);
+      const int K4 = K >> 2;
+      for (int c0 = part * 8; c0 < K4; c0 += TPR * 8) {
+        float4 v[8];
+        int nv = 0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (c0 + u < K4) { v[u] = ar[c0 + u]; nv = u + 1; }
+        float s = 0.f;
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (u < nv) s += (v[u].x + v[u].y) + (v[u].z + v[u].w);
+        const float n_b = 4.0f * nv, mu_b = s / n_b;
+        float q = 0.f;
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (u < nv) {
+            const float a0 = v[u].x - mu_b, a1 = v[u].y - mu_b, a2 = v[u].z - mu_b, a3 = v[u].w - mu_b;
+            q += (a0 * a0 + a1 * a1) + (a2 * a2 + a3 * a3);
+          }
+        const float n_ab = cnt + n_b, d = mu_b - mean;
+        mean += d * (n_b / n_ab);
+        m2 += q + d * d * (cnt * n_b / n_ab);
+        cnt = n_ab;
+      }
+    }
+#pragma unroll
+    for (int o = 1; o < TPR; o <<= 1) {
+      const float c2 = __shfl_xor(cnt, o, 64), mu2 = __shfl_xor(mean, o, 64), q2 = __shfl_xor(m2, o, 64);
+      const float n_ab = cnt + c2;
+      if (n_ab > 0.f) {
+        const float d = mu2 - mean;
+        mean += d * (c2 / n_ab);
+        m2 += q2 + d * d * (cnt * c2 / n_ab);
+      }
+      cnt = n_ab;
+    }
+    if (part == 0) {
+      s_mean[r] = mean;
+      s_rstd[r] = (m < M) ? 1.0f / sqrtf(m2 / (float)K + g.ln_eps) : 0.f;
+    }
+    __syncthreads();
+  }
+
+  float4 ra[NA], rb[NB];
+  auto load_tiles = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int idx = tid + 256 * i;
+      const int r = idx >> 3, kq = (idx & 7) * 4;
+      const int m = m0 + r;
+      ra[i] = (m < M) ? *reinterpret_cast<const float4*>(A + (long)m * g.lda + k0 + kq) : make_float4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int idx = tid + 256 * i;
+      if (B_KC) {
+        const int r = idx >> 3, kq = (idx & 7) * 4;
+        const int n = n0 + r;
+        rb[i] = (n < N) ? *reinterpret_cast<const float4*>(B + (long)n * g.ldb + k0 + kq) : make_float4(0, 0, 0, 0);
+      } else {
+        const int kl = idx / (BN / 4), nq = (idx % (BN / 4)) * 4;
+        const int n = n0 + nq;
+        const float* src = B + (long)(k0 + kl) * g.ldb + n;
+        if (n + 3 < N && vec_b) {
+          rb[i] = *reinterpret_cast<const float4*>(src);
+        } else {
+          rb[i].x = (n < N) ? src[0] : 0.f;
+          rb[i].y = (n + 1 < N) ? src[1] : 0.f;
+          rb[i].z = (n + 2 < N) ? src[2] : 0.f;
+          rb[i].w = (n + 3 < N) ? src[3] : 0.f;
+        }
+      }
+    }
+  };
+  auto store_tiles = [&](int buf, int k0) {
+    float* Ab = As + buf * A_ELEMS;
+    float* Bb = Bs + buf * B_ELEMS;
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int idx = tid + 256 * i;
+      const int r = idx >> 3, kq = (idx & 7) * 4;
+      float4 v = ra[i];
+      if (A_LN) {
+        const float mu = s_mean[r], rs = s_rstd[r];
+        const float4 w = *reinterpret_cast<const float4*>(g.ln_w + k0 + kq);
+        const float4 b = *reinterpret_cast<const float4*>(g.ln_b + k0 + kq);
+        v.x = (v.x - mu) * rs * w.x + b.x;
+        v.y = (v.y - mu) * rs * w.y + b.y;
+        v.z = (v.z - mu) * rs * w.z + b.z;
+        v.w = (v.w - mu) * rs * w.w + b.w;
+      }
+      *reinterpret_cast<float4*>(&Ab[r * SK + kq]) = v;
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int idx = tid + 256 * i;
+      if (B_KC) {
+        const int r = idx >> 3, kq = (idx & 7) * 4;
+        *reinterpret_cast<float4*>(&Bb[r * SK + kq]) = rb[i];
+      } else {
+        const int kl = idx / (BN / 4), nq = (idx % (BN / 4)) * 4;
+        *reinterpret_cast<float4*>(&Bb[kl * SBN + nq]) = rb[i];
+      }
+    }
+  };
+
+  f32x16 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int nk = K / BK;
+  const int lr = lane & 31, lh = lane >> 5;
+  load_tiles(0);
+  store_tiles(0, 0);
+  __syncthreads();
+  for (int kb = 0; kb < nk; ++kb) {
+    const int buf = kb & 1;
+    if (kb + 1 < nk) load_tiles((kb + 1) * BK);
+    const float* Ab = As + buf * A_ELEMS + (wm * MI * 32 + lr) * SK + lh * 16;
+    const float* Bb = Bs + buf * B_ELEMS;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      float4 a[MI], b[NI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) a[i] = *reinterpret_cast<const float4*>(Ab + i * 32 * SK + 4 * t);
+      if (B_KC) {
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          b[j] = *reinterpret_cast<const float4*>(Bb + (wn * NI * 32 + j * 32 + lr) * SK + lh * 16 + 4 * t);
+      } else {
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          const float* col = Bb + (lh * 16 + 4 * t) * SBN + wn * NI * 32 + j * 32 + lr;
+          b[j] = make_float4(col[0], col[SBN], col[2 * SBN], col[3 * SBN]);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].x, b[j].x, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].y, b[j].y, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].z, b[j].z, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].w, b[j].w, acc[i][j], 0, 0, 0);
+        }
+    }
+    if (kb + 1 < nk) store_tiles(buf ^ 1, (kb + 1) * BK);
+    __syncthreads();
+  }
+
+  // epilogue: C/D map of 32x32: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+  const Epi& e = g.epi;
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int n = n0 + wn * NI * 32 + j * 32 + lr;
+    if (n >= N) continue;
+    long col_off;  // output offset of (m = 0, n)
+    long m_stride;
+    if (!e.swin) {
+      col_off = (long)bz * e.out_bs + n;
+      m_stride = e.ldc;
+    } else {
+      const int L = e.sw_wh * e.sw_ww;
+      const int per_img = e.sw_nWin * L;
+      const int img = n / per_img;
+      const int rr = n - img * per_img;
+      const int win = rr / L, tok = rr - win * L;
+      const int wy = win / e.sw_nWx, wx = win - wy * e.sw_nWx;
+      const int iy = tok / e.sw_ww, ix = tok - iy * e.sw_ww;
+      const int h = wy * e.sw_wh + iy, w = wx * e.sw_ww + ix;
+      if (h >= e.sw_H || w >= e.sw_W) continue;  // crop of the zero-padded border (blocks_transformer.py:125-129)
+      m_stride = (long)e.sw_H * e.sw_W;
+      col_off = (long)img * e.ldc * m_stride + (long)h * e.sw_W + w;  // ldc = channels
+    }
+    const long rcol_off = e.swin ? col_off : (long)bz * e.res_bs + n;
+    const long r_stride = e.swin ? m_stride : e.ldr;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * MI * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (m >= M) continue;
+        float v = epi_value(e, m, n, acc[i][j][r]);
+        if (e.res) v += e.res[rcol_off + (long)m * r_stride];
+        e.out[col_off + (long)m * m_stride] = v;
+      }
+  }
+}
+
+static inline int launch_gemm(const GemmArgs& g, int batch, bool b_kc, hipStream_t st) {
+  YS_CHECK_ARG(g.K % 32 == 0, "gemm: K=%d must be a multiple of 32", g.K);
+  YS_CHECK_ARG(g.lda % 4 == 0 && (!b_kc || g.ldb % 4 == 0),
+               "gemm: lda (and ldb of a K-contiguous B) must be multiples of 4");
+  YS_CHECK_ARG(((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.B & 15) == 0, "gemm: A/B must be 16-byte aligned");
+  YS_CHECK_ARG(!g.ln_w || (((uintptr_t)g.ln_w & 15) == 0 && ((uintptr_t)g.ln_b & 15) == 0),
+               "gemm: LN params must be 16-byte aligned");
+  if (g.M == 0 || g.N == 0 || batch == 0) return 0;
+  const bool ln = g.ln_w != nullptr;
+  // N tiles of 64 when N is not a multiple of 128 (e.g. 3C = 192) or small; 128 otherwise
+  const bool narrow = (g.N % 128 != 0) && (g.N <= 256);
+#define YS_GEMM_LAUNCH(WM_, WN_, MI_, NI_)                                                                     \
+  do {                                                                                                         \
+    constexpr int bm = WM_ * MI_ * 32, bn = WN_ * NI_ * 32;                                                    \
+    dim3 grid((g.N + bn - 1) / bn, (g.M + bm - 1) / bm, batch);                                               \
+    if (b_kc) {                                                                                                \
+      if (ln) hipLaunchKernelGGL((gemm_f32_kernel<WM_, WN_, MI_, NI_, true, true>), grid, dim3(256), 0, st, g); \
+      else hipLaunchKernelGGL((gemm_f32_kernel<WM_, WN_, MI_, NI_, true, false>), grid, dim3(256), 0, st, g);  \
+    } else {                                                                                                   \
+      if (ln) hipLaunchKernelGGL((gemm_f32_kernel<WM_, WN_, MI_, NI_, false, true>), grid, dim3(256), 0, st, g); \
+      else hipLaunchKernelGGL((gemm_f32_kernel<WM_, WN_, MI_, NI_, false, false>), grid, dim3(256), 0, st, g); \
+    }                                                                                                          \
+  } while (0)
+  if (narrow) YS_GEMM_LAUNCH(4, 1, 1, 2);
+  else YS_GEMM_LAUNCH(2, 2, 2, 2);
+#undef YS_GEMM_LAUNCH
+  YS_CHECK_LAUNCH("gemm_f32");
+  return 0;
+}
+
+static inline Epi epi_plain(float* out, long out_bs, int ldc) {
+  Epi e{};
+  e.out = out;
+  e.out_bs = out_bs;
+  e.ldc = ldc;
+  return e;
+}
+
+}  // namespace ys

@@ -15,230 +15,11 @@
 //              WindowAttention.forward :100-131, SwinBlock.forward :150-171)
 //   A2_Attn    ultralytics/nn/modules/a2_attn.py:35-69
 #include "common.h"
+#include "gemm_f32.h"
 #include <math.h>
+#include <stdlib.h>
 
 namespace ys {
-
-// =================================================================================================
-// GEMM:  out(b, m, n) = epilogue( sum_k A(b, m, k) * B(b, k, n) )
-//   A(b,m,k) = A[b*a_bs + m*lda + k]                        (always K-contiguous)
-//   B_KC:  B(b,k,n) = B[b*b_bs + n*ldb + k]                  (K-contiguous: Linear weights / token-major acts)
-//   !B_KC: B(b,k,n) = B[b*b_bs + k*ldb + n]                  (N-contiguous: NCHW activations)
-// Requires K % 16 == 0, lda % 4 == 0, ldb % 4 == 0, 16-byte aligned bases.
-// =================================================================================================
-struct Epi {
-  const float* bias;   // bias_mode 1: per-row m, 2: per-col n
-  int bias_mode;
-  const float* scale;  // folded BN:  v = v*scale + shift, bn_mode 1: per-row, 2: per-col
-  const float* shift;
-  int bn_mode;
-  int act;             // 0 none, 1 SiLU, 2 GELU(erf), 3 ReLU
-  const float* res;    // residual added after activation (same indexing as out)
-  long res_bs;
-  int ldr;
-  float* out;
-  long out_bs;
-  int ldc;
-  // window-reverse output (SwinBlock): n = global token, m = channel; out/res are NCHW [img][M][H][W]
-  int swin;
-  int sw_H, sw_W, sw_wh, sw_ww, sw_nWx, sw_nWin;
-};
-
-struct GemmArgs {
-  const float* A;
-  long a_bs;
-  int lda;
-  const float* B;
-  long b_bs;
-  int ldb;
-  int M, N, K;
-  Epi epi;
-};
-
-__device__ __forceinline__ float apply_act(float v, int act) {
-  if (act == 1) return siluf_(v);
-  if (act == 2) return geluf_(v);
-  if (act == 3) return fmaxf(v, 0.f);
-  return v;
-}
-
-__device__ __forceinline__ void epi_store(const Epi& e, int bz, int m, int n, float v) {
-  if (e.bias_mode == 1) v += e.bias[m];
-  else if (e.bias_mode == 2) v += e.bias[n];
-  if (e.bn_mode == 1) v = v * e.scale[m] + e.shift[m];
-  else if (e.bn_mode == 2) v = v * e.scale[n] + e.shift[n];
-  v = apply_act(v, e.act);
-  if (!e.swin) {
-    const long o = (long)bz * e.out_bs + (long)m * e.ldc + n;
-    if (e.res) v += e.res[(long)bz * e.res_bs + (long)m * e.ldr + n];
-    e.out[o] = v;
-  } else {
-    const int L = e.sw_wh * e.sw_ww;
-    const int per_img = e.sw_nWin * L;
-    const int img = n / per_img;
-    const int r = n - img * per_img;
-    const int win = r / L, tok = r - (r / L) * L;
-    const int wy = win / e.sw_nWx, wx = win - wy * e.sw_nWx;
-    const int iy = tok / e.sw_ww, ix = tok - iy * e.sw_ww;
-    const int h = wy * e.sw_wh + iy, w = wx * e.sw_ww + ix;
-    if (h >= e.sw_H || w >= e.sw_W) return;  // crop of the zero-padded border (blocks_transformer.py:125-129)
-    const long o = (((long)img * e.ldc + m) * e.sw_H + h) * e.sw_W + w;  // ldc = channels here
-    if (e.res) v += e.res[o];
-    e.out[o] = v;
-  }
-}
-
-template <int WM, int WN, int MI, int NI, bool B_KC>
-__global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
-  constexpr int BM = WM * MI * 32;
-  constexpr int BN = WN * NI * 32;
-  constexpr int BK = 16;
-  constexpr int SA = BM + 2;                  // transposed (k-major) A image; +2 keeps the 4-way k-scatter
-  constexpr int SB = B_KC ? BN + 2 : BN + 4;  // conflict-free; +4 keeps b128 stores aligned
-  constexpr int NA = BM / 64;                 // float4 loads per thread for the A tile
-  constexpr int NB = BN / 64;
-  static_assert(WM * WN == 4, "4 waves");
-  __shared__ float As[BK * SA];
-  __shared__ float Bs[BK * SB];
-
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid / WN, wn = wid % WN;
-  const int bz = blockIdx.z;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-  const float* A = g.A + (long)bz * g.a_bs;
-  const float* B = g.B + (long)bz * g.b_bs;
-  const int M = g.M, N = g.N, K = g.K;
-  const bool vec_b = (g.ldb & 3) == 0 && (g.b_bs & 3) == 0;  // float4 rows of an N-contiguous B
-
-  float4 ra[NA], rb[NB];
-  auto load_tiles = [&](int k0) {
-#pragma unroll
-    for (int i = 0; i < NA; ++i) {
-      const int idx = tid + 256 * i;
-      const int ml = idx >> 2, kq = (idx & 3) * 4;
-      const int m = m0 + ml;
-      ra[i] = (m < M) ? *reinterpret_cast<const float4*>(A + (long)m * g.lda + k0 + kq) : make_float4(0, 0, 0, 0);
-    }
-#pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      const int idx = tid + 256 * i;
-      if (B_KC) {
-        const int nl = idx >> 2, kq = (idx & 3) * 4;
-        const int n = n0 + nl;
-        rb[i] = (n < N) ? *reinterpret_cast<const float4*>(B + (long)n * g.ldb + k0 + kq) : make_float4(0, 0, 0, 0);
-      } else {
-        const int kl = idx / (BN / 4), nq = (idx % (BN / 4)) * 4;
-        const int n = n0 + nq;
-        const float* src = B + (long)(k0 + kl) * g.ldb + n;
-        if (n + 3 < N && vec_b) {
-          rb[i] = *reinterpret_cast<const float4*>(src);
-        } else {
-          rb[i].x = (n < N) ? src[0] : 0.f;
-          rb[i].y = (n + 1 < N) ? src[1] : 0.f;
-          rb[i].z = (n + 2 < N) ? src[2] : 0.f;
-          rb[i].w = (n + 3 < N) ? src[3] : 0.f;
-        }
-      }
-    }
-  };
-  auto store_tiles = [&]() {
-#pragma unroll
-    for (int i = 0; i < NA; ++i) {
-      const int idx = tid + 256 * i;
-      const int ml = idx >> 2, kq = (idx & 3) * 4;
-      As[(kq + 0) * SA + ml] = ra[i].x;
-      As[(kq + 1) * SA + ml] = ra[i].y;
-      As[(kq + 2) * SA + ml] = ra[i].z;
-      As[(kq + 3) * SA + ml] = ra[i].w;
-    }
-#pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      const int idx = tid + 256 * i;
-      if (B_KC) {
-        const int nl = idx >> 2, kq = (idx & 3) * 4;
-        Bs[(kq + 0) * SB + nl] = rb[i].x;
-        Bs[(kq + 1) * SB + nl] = rb[i].y;
-        Bs[(kq + 2) * SB + nl] = rb[i].z;
-        Bs[(kq + 3) * SB + nl] = rb[i].w;
-      } else {
-        const int kl = idx / (BN / 4), nq = (idx % (BN / 4)) * 4;
-        *reinterpret_cast<float4*>(&Bs[kl * SB + nq]) = rb[i];
-      }
-    }
-  };
-
-  f32x16 acc[MI][NI];
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < NI; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  const int nk = K / BK;
-  load_tiles(0);
-  const int lr = lane & 31, lk = lane >> 5;
-  for (int kb = 0; kb < nk; ++kb) {
-    __syncthreads();
-    store_tiles();
-    __syncthreads();
-    if (kb + 1 < nk) load_tiles((kb + 1) * BK);
-#pragma unroll
-    for (int kk = 0; kk < BK / 2; ++kk) {
-      const int kr = kk * 2 + lk;
-      float a[MI], b[NI];
-#pragma unroll
-      for (int i = 0; i < MI; ++i) a[i] = As[kr * SA + wm * (MI * 32) + i * 32 + lr];
-#pragma unroll
-      for (int j = 0; j < NI; ++j) b[j] = Bs[kr * SB + wn * (NI * 32) + j * 32 + lr];
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NI; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
-    }
-  }
-
-  // epilogue: C/D map of 32x32: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      const int n = n0 + wn * (NI * 32) + j * 32 + lr;
-      if (n >= N) continue;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * (MI * 32) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
-        if (m < M) epi_store(g.epi, bz, m, n, acc[i][j][r]);
-      }
-    }
-}
-
-static int launch_gemm(const GemmArgs& g, int batch, bool b_kc, hipStream_t st) {
-  YS_CHECK_ARG(g.K % 16 == 0, "gemm: K=%d must be a multiple of 16", g.K);
-  YS_CHECK_ARG(g.lda % 4 == 0 && (!b_kc || g.ldb % 4 == 0), "gemm: lda (and ldb of a K-contiguous B) must be multiples of 4");
-  YS_CHECK_ARG(((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.B & 15) == 0, "gemm: A/B must be 16-byte aligned");
-  if (g.M == 0 || g.N == 0 || batch == 0) return 0;
-  const bool wide = (g.N % 128 == 0) || g.N > 256;
-  if (wide) {
-    dim3 grid((g.N + 127) / 128, (g.M + 127) / 128, batch);
-    if (b_kc) hipLaunchKernelGGL((gemm_f32_kernel<2, 2, 2, 2, true>), grid, dim3(256), 0, st, g);
-    else hipLaunchKernelGGL((gemm_f32_kernel<2, 2, 2, 2, false>), grid, dim3(256), 0, st, g);
-  } else {
-    dim3 grid((g.N + 63) / 64, (g.M + 127) / 128, batch);
-    if (b_kc) hipLaunchKernelGGL((gemm_f32_kernel<4, 1, 1, 2, true>), grid, dim3(256), 0, st, g);
-    else hipLaunchKernelGGL((gemm_f32_kernel<4, 1, 1, 2, false>), grid, dim3(256), 0, st, g);
-  }
-  YS_CHECK_LAUNCH("gemm_f32");
-  return 0;
-}
-
-static Epi epi_plain(float* out, long out_bs, int ldc) {
-  Epi e{};
-  e.out = out;
-  e.out_bs = out_bs;
-  e.ldc = ldc;
-  return e;
-}
 
 // =================================================================================================
 // LayerNorm over rows of C (token-major), one wave per row. y = (x-mean)*rstd*w + b, biased variance.
@@ -579,6 +360,28 @@ static SwinGeom swin_geom(int B, int H, int W, int ws) {
 
 using namespace ys;
 
+int yolosod_swin_fused_launch(const float* x, float* y, int B, int C, int H, int W, int num_heads, int wh, int ww,
+                              int nWx, int nWin, const float* dw_w, const float* ln1_w, const float* ln1_b,
+                              float ln1_eps, const float* in_proj_w, const float* in_proj_b, const float* out_proj_w,
+                              const float* out_proj_b, const float* ln2_w, const float* ln2_b, float ln2_eps,
+                              const float* mlp1_w, const float* mlp1_b, int mlp_hidden, const float* mlp2_w,
+                              const float* mlp2_b, const float* pw_w, const float* bn_scale, const float* bn_shift,
+                              hipStream_t st);
+
+static bool swin_fused_enabled() {
+  static int v = [] {
+    const char* e = getenv("YOLOSOD_SWIN_FUSED");
+    return e ? atoi(e) : 1;
+  }();
+  return v != 0;
+}
+
+// shapes the fused per-window kernel (swin_fused.hip) handles
+static bool swin_fused_ok(int C, int heads, int L, int mlp_hidden) {
+  if (!swin_fused_enabled() || L > 49 || mlp_hidden != 2 * C) return false;
+  return (C == 64 && (heads == 2 || heads == 4)) || (C == 128 && (heads == 2 || heads == 4));
+}
+
 // =================================================================================================
 // C ABI
 // =================================================================================================
@@ -626,6 +429,17 @@ __global__ void fold_bn_kernel(const float* w, const float* b, const float* m, c
   shift[c] = b[c] - m[c] * sc;
 }
 
+YS_EXPORT size_t yolosod_swin_workspace_v2(int B, int C, int H, int W, int num_heads, int window,
+                                           int mlp_hidden) {
+  SwinGeom g = swin_geom(B, H, W, window);
+  if (swin_fused_ok(C, num_heads, g.L, mlp_hidden)) {
+    Sizer s;
+    s.take<float>((size_t)C * 2);
+    return s.off;
+  }
+  return yolosod_swin_workspace(B, C, H, W, window, mlp_hidden);
+}
+
 YS_EXPORT int yolosod_swin_forward(const float* x, float* y, int B, int C, int H, int W, int num_heads, int window,
                                    const float* dw_w, const float* ln1_w, const float* ln1_b, float ln1_eps,
                                    const float* in_proj_w, const float* in_proj_b, const float* out_proj_w,
@@ -638,11 +452,24 @@ YS_EXPORT int yolosod_swin_forward(const float* x, float* y, int B, int C, int H
                    ln2_b && mlp1_w && mlp1_b && mlp2_w && mlp2_b && pw_w && bn_w && bn_b && bn_mean && bn_var,
                "swin: null pointer");
   YS_CHECK_ARG(B >= 0 && C > 0 && H > 0 && W > 0 && window > 0, "swin: bad shape");
-  YS_CHECK_ARG(C % 16 == 0 && mlp_hidden % 16 == 0, "swin: C and mlp_hidden must be multiples of 16");
+  YS_CHECK_ARG(C % 32 == 0 && mlp_hidden % 32 == 0, "swin: C and mlp_hidden must be multiples of 32");
   if (B == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   SwinGeom g = swin_geom(B, H, W, window);
   YS_CHECK_ARG(g.L <= 320, "swin: window of %d tokens unsupported", g.L);
+  if (swin_fused_ok(C, num_heads, g.L, mlp_hidden)) {
+    Carver cf(workspace, workspace_bytes);
+    float* fold = cf.take<float>((size_t)C * 2);
+    YS_CHECK_ARG(fold, "swin: workspace too small (%zu)", workspace_bytes);
+    hipLaunchKernelGGL(fold_bn_kernel, dim3((C + 255) / 256), dim3(256), 0, st, bn_w, bn_b, bn_mean, bn_var, bn_eps,
+                       C, fold, fold + C);
+    const int r = yolosod_swin_fused_launch(x, y, B, C, H, W, num_heads, g.wh, g.ww, g.nWx, g.nWin, dw_w, ln1_w,
+                                            ln1_b, ln1_eps, in_proj_w, in_proj_b, out_proj_w, out_proj_b, ln2_w,
+                                            ln2_b, ln2_eps, mlp1_w, mlp1_b, mlp_hidden, mlp2_w, mlp2_b, pw_w, fold,
+                                            fold + C, st);
+    if (r < 0) return -1;
+    if (r == 1) return 0;
+  }
   Carver cv(workspace, workspace_bytes);
   float* T = cv.take<float>((size_t)g.ntok * C);
   float* U = cv.take<float>((size_t)g.ntok * C);
@@ -657,11 +484,10 @@ YS_EXPORT int yolosod_swin_forward(const float* x, float* y, int B, int C, int H
   hipLaunchKernelGGL(swin_partition_kernel, dim3((unsigned)((long)B * g.nWin), (C + 63) / 64), dim3(256), lds, st, x,
                      dw_w, T, C, H, W, g.wh, g.ww, g.nWx, g.nWin);
   YS_CHECK_LAUNCH("swin_partition");
-  if ((rc = launch_layernorm(T, U, g.ntok, C, ln1_w, ln1_b, ln1_eps, st))) return rc;
-
   GemmArgs ga{};
-  // QKV = U Win^T + b_in
-  ga.A = U; ga.lda = C; ga.B = in_proj_w; ga.ldb = C; ga.M = (int)g.ntok; ga.N = 3 * C; ga.K = C;
+  // QKV = LN1(T) Win^T + b_in   (LN fused into the A staging)
+  ga.A = T; ga.lda = C; ga.B = in_proj_w; ga.ldb = C; ga.M = (int)g.ntok; ga.N = 3 * C; ga.K = C;
+  ga.ln_w = ln1_w; ga.ln_b = ln1_b; ga.ln_eps = ln1_eps;
   ga.epi = epi_plain(Q, 0, 3 * C);
   ga.epi.bias = in_proj_b; ga.epi.bias_mode = 2;
   if ((rc = launch_gemm(ga, 1, true, st))) return rc;
@@ -672,10 +498,10 @@ YS_EXPORT int yolosod_swin_forward(const float* x, float* y, int B, int C, int H
   ga.epi = epi_plain(T, 0, C);
   ga.epi.bias = out_proj_b; ga.epi.bias_mode = 2; ga.epi.res = T; ga.epi.ldr = C;
   if ((rc = launch_gemm(ga, 1, true, st))) return rc;
-  if ((rc = launch_layernorm(T, U, g.ntok, C, ln2_w, ln2_b, ln2_eps, st))) return rc;
-  // Hd = GELU(U2 W1^T + b1)
+  // Hd = GELU(LN2(T) W1^T + b1)
   ga = GemmArgs{};
-  ga.A = U; ga.lda = C; ga.B = mlp1_w; ga.ldb = C; ga.M = (int)g.ntok; ga.N = mlp_hidden; ga.K = C;
+  ga.A = T; ga.lda = C; ga.B = mlp1_w; ga.ldb = C; ga.M = (int)g.ntok; ga.N = mlp_hidden; ga.K = C;
+  ga.ln_w = ln2_w; ga.ln_b = ln2_b; ga.ln_eps = ln2_eps;
   ga.epi = epi_plain(Q, 0, mlp_hidden);
   ga.epi.bias = mlp1_b; ga.epi.bias_mode = 2; ga.epi.act = 2;
   if ((rc = launch_gemm(ga, 1, true, st))) return rc;
@@ -721,7 +547,7 @@ YS_EXPORT int yolosod_a2_forward(const float* x, float* y, int B, int C, int H, 
                    oproj_w && oproj_b,
                "a2: null pointer");
   YS_CHECK_ARG(B >= 0 && C > 0 && H > 0 && W > 0 && num_areas > 0, "a2: bad shape");
-  YS_CHECK_ARG(C % 16 == 0, "a2: C must be a multiple of 16");
+  YS_CHECK_ARG(C % 32 == 0, "a2: C must be a multiple of 32");
   if (B == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   const int A = num_areas;
@@ -743,9 +569,9 @@ YS_EXPORT int yolosod_a2_forward(const float* x, float* y, int B, int C, int H, 
   if ((rc = launch_gemm(ga, B, false, st))) return rc;
   hipLaunchKernelGGL(a2_pool_tokens_kernel, dim3(B * A), dim3(256), 0, st, XP, S, C, H, W, A);
   YS_CHECK_LAUNCH("a2_pool");
-  if ((rc = launch_layernorm(S, U, ntok, C, ln_w, ln_b, ln_eps, st))) return rc;
   ga = GemmArgs{};
-  ga.A = U; ga.lda = C; ga.B = in_proj_w; ga.ldb = C; ga.M = (int)ntok; ga.N = 3 * C; ga.K = C;
+  ga.A = S; ga.lda = C; ga.B = in_proj_w; ga.ldb = C; ga.M = (int)ntok; ga.N = 3 * C; ga.K = C;
+  ga.ln_w = ln_w; ga.ln_b = ln_b; ga.ln_eps = ln_eps;
   ga.epi = epi_plain(Q, 0, 3 * C);
   ga.epi.bias = in_proj_b; ga.epi.bias_mode = 2;
   if ((rc = launch_gemm(ga, 1, true, st))) return rc;
