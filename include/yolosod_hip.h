@@ -87,6 +87,12 @@ int yolosod_nms(float* pred, int B, int nc, int A, float conf_thres, double iou_
                 int n_classes, int agnostic, int multi_label, int max_det, int max_nms, float max_wh, int in_place,
                 float* out, int* counts, int* out_index, void* workspace, size_t workspace_bytes, void* stream);
 
+/* Conv epilogue for the PyTorch-ROCm backbone convs (not a reference hot-path op; conv.py:37-55 + block.py:343-356
+ * + Concat): out[b*out_bstride + c*HW + p] = act(y[b*y_bstride + c*HW + p] + bias[c]) (+ res[...]); act 0 id, 1 SiLU.
+ * Writes into channel slices of a concat buffer via out_bstride; in place allowed. */
+int yolosod_bias_act(const float* y, long y_bstride, float* out, long out_bstride, const float* bias,
+                     const float* res, long res_bstride, int B, int C, long HW, int act, void* stream);
+
 /* Building blocks, exported for unit tests (no single reference interface):
  * C(b,m,n) = act(sum_k A(b,m,k) B(b,k,n) + bias) + res;  A K-contiguous; B K- or N-contiguous. */
 int yolosod_gemm_f32(const float* A, long a_bs, int lda, const float* B, long b_bs, int ldb, int b_kcontig, float* C,

@@ -1,0 +1,38 @@
+"""Micro-benchmark of the fp32 MFMA GEMM (C-ABI test hook) at the Swin-L9 / A2 shapes."""
+import sys
+from pathlib import Path
+
+import torch
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+import yolosod_import  # noqa: E402,F401
+from yolosod_amd import _hip  # noqa: E402
+
+SHAPES = [(56448, 768, 256), (56448, 512, 256), (56448, 256, 512), (56448, 256, 256), (5120, 1536, 512),
+          (829472, 192, 64), (4096, 4096, 4096)]
+
+
+def main():
+    dev = torch.device("cuda")
+    for (M, N, K) in SHAPES:
+        A = torch.randn(M, K, device=dev)
+        B = torch.randn(N, K, device=dev)
+        bias = torch.randn(N, device=dev)
+        for _ in range(3):
+            _hip.gemm_f32(A, B, True, bias=bias, bias_mode=2)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        n = 10
+        e0.record()
+        for _ in range(n):
+            _hip.gemm_f32(A, B, True, bias=bias, bias_mode=2)
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / n
+        tf = 2 * M * N * K / ms / 1e9
+        print(f"M={M:7d} N={N:5d} K={K:5d}  {ms:8.3f} ms  {tf:7.1f} TFLOP/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()

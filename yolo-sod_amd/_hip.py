@@ -47,6 +47,7 @@ SIGNATURES = {
     "yolosod_gemm_f32": (_i, [_vp, _l, _i, _vp, _l, _i, _i, _vp, _l, _i, _i, _i, _i, _i, _vp, _i, _i, _vp, _vp]),
     "yolosod_layernorm": (_i, [_vp, _vp, _l, _i, _vp, _vp, _f, _vp]),
     "yolosod_attention": (_i, [_vp, _vp, _l, _i, _i, _i, _vp]),
+    "yolosod_bias_act": (_i, [_vp, _l, _vp, _l, _vp, _vp, _l, _i, _i, _l, _i, _vp]),
 }
 
 _LIB = None
@@ -282,6 +283,31 @@ def nms(pred, conf_thres, iou_thres, classes, agnostic, multi_label, max_det, ma
                            1, out.data_ptr(), counts.data_ptr(), index.data_ptr(), ws.data_ptr(), ws.numel(),
                            _stream()), "nms")
     return out, counts, index
+
+
+def bias_act(y, bias, act, out=None, res=None):
+    """Backbone conv epilogue: out = act(y + bias[c]) (+ res). ``out`` may be a channel slice [B, C, H, W] of a
+    larger contiguous concat buffer (batch stride > C*H*W); ``res`` likewise. In place when out is None."""
+    lib = load_library()
+    B, C, H, W = y.shape
+    HW = H * W
+    if out is None:
+        out = y
+
+    def bstride(t, name):
+        if t.device.type != "cuda" or t.dtype != torch.float32:
+            raise RuntimeError(f"bias_act: {name} must be a float32 GPU tensor")
+        if t.shape != y.shape or t.stride(3) != 1 or t.stride(2) != W or t.stride(1) != HW:
+            raise RuntimeError(f"bias_act: {name} must be [B,C,H,W] with contiguous channels (got {t.stride()})")
+        return t.stride(0)
+
+    yb = bstride(y, "y")
+    ob = bstride(out, "out")
+    rb = bstride(res, "res") if res is not None else 0
+    _check(lib.yolosod_bias_act(y.data_ptr(), yb, out.data_ptr(), ob, _dev(bias, "bias"),
+                                None if res is None else res.data_ptr(), rb, B, C, HW, int(act), _stream()),
+           "bias_act")
+    return out
 
 
 def gemm_f32(A, B, b_kcontig, bias=None, bias_mode=0, act=0, res=None):

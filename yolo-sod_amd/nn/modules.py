@@ -17,6 +17,7 @@ import math
 
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
 
 from .. import _hip
 
@@ -43,8 +44,37 @@ def _is_meta(x: torch.Tensor) -> bool:
 # ---------------------------------------------------------------------------------------------------------------
 # host PyTorch blocks
 # ---------------------------------------------------------------------------------------------------------------
+def _act_code(act):
+    if isinstance(act, nn.SiLU):
+        return 1
+    if isinstance(act, nn.Identity):
+        return 0
+    return None
+
+
+def conv_epilogue(conv: nn.Conv2d, act_code, x, out=None, res=None):
+    """GPU fast path of ``act(conv(x)) (+ res)``: MIOpen conv without bias, then one HIP pass for bias +
+    activation (+ shortcut), optionally written straight into a channel slice ``out`` of a concat buffer.
+    Returns None when the fast path does not apply (CPU tensor, no bias, unsupported activation / shape)."""
+    if x.device.type != "cuda" or conv.bias is None or act_code is None or x.dtype != torch.float32:
+        return None
+    y = F.conv2d(x, conv.weight, None, conv.stride, conv.padding, conv.dilation, conv.groups)
+    if (y.shape[2] * y.shape[3]) % 4:
+        y = y + conv.bias.view(1, -1, 1, 1)
+        y = F.silu(y) if act_code == 1 else y
+        if res is not None:
+            y = y + res
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
+    return _hip.bias_act(y, conv.bias.detach(), act_code, out=out, res=res)
+
+
 class Conv(nn.Module):
-    """Conv2d(no bias) + BatchNorm2d + SiLU; after ``fuse()`` the BN is folded into the conv (conv.py:37-55)."""
+    """Conv2d(no bias) + BatchNorm2d + SiLU; after ``fuse()`` the BN is folded into the conv (conv.py:37-55).
+
+    Fused form on GPU: MIOpen conv + one HIP epilogue pass (bias + SiLU, optional shortcut / concat slice)."""
 
     default_act = nn.SiLU()
 
@@ -57,8 +87,20 @@ class Conv(nn.Module):
     def forward(self, x):
         return self.act(self.bn(self.conv(x)))
 
-    def forward_fuse(self, x):
-        return self.act(self.conv(x))
+    def forward_fuse(self, x, out=None, res=None):
+        y = conv_epilogue(self.conv, _act_code(self.act), x, out, res)
+        if y is not None:
+            return y
+        y = self.act(self.conv(x))
+        if res is not None:
+            y = y + res
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
+
+    def is_fused(self):
+        return not hasattr(self, "bn")
 
 
 class DWConv(Conv):
@@ -85,8 +127,14 @@ class Bottleneck(nn.Module):
         self.cv2 = Conv(c_, c2, k[1], 1, g=g)
         self.add = shortcut and c1 == c2
 
-    def forward(self, x):
-        return x + self.cv2(self.cv1(x)) if self.add else self.cv2(self.cv1(x))
+    def forward(self, x, out=None):
+        if self.cv2.is_fused():  # shortcut fused into cv2's epilogue, output optionally into a concat slice
+            return self.cv2.forward_fuse(self.cv1(x), out=out, res=x if self.add else None)
+        y = x + self.cv2(self.cv1(x)) if self.add else self.cv2(self.cv1(x))
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
 
 
 class C2f(nn.Module):
@@ -98,6 +146,15 @@ class C2f(nn.Module):
         self.m = nn.ModuleList(Bottleneck(self.c, self.c, shortcut, g, k=((3, 3), (3, 3)), e=1.0) for _ in range(n))
 
     def forward(self, x):
+        if x.device.type == "cuda" and self.cv1.is_fused():
+            # every branch writes its channel slice of one buffer: no torch.cat copy (block.py:249-253 semantics)
+            B, _, H, W = x.shape
+            n, c = len(self.m), self.c
+            z = torch.empty((B, (2 + n) * c, H, W), dtype=x.dtype, device=x.device)
+            self.cv1.forward_fuse(x, out=z[:, : 2 * c])
+            for i, m in enumerate(self.m):
+                m(z[:, (1 + i) * c:(2 + i) * c], out=z[:, (2 + i) * c:(3 + i) * c])
+            return self.cv2(z)
         y = list(self.cv1(x).chunk(2, 1))
         y.extend(m(y[-1]) for m in self.m)
         return self.cv2(torch.cat(y, 1))
@@ -370,11 +427,27 @@ class Detect(nn.Module):
 
     def forward(self, x):
         for i in range(self.nl):
-            x[i] = torch.cat((self.cv2[i](x[i]), self.cv3[i](x[i])), 1)
+            x[i] = self._tower(i, x[i])
         if self.training:
             return x
         y = self._inference(x)
         return y if self.export else (y, x)
+
+    def _tower(self, i, xi):
+        """torch.cat((cv2[i](x), cv3[i](x)), 1) (head.py:70); on GPU the two final 1x1 convs write their slices of
+        the [B, 4*reg_max+nc, H, W] map directly (bias in the HIP epilogue)."""
+        b2, b3 = self.cv2[i], self.cv3[i]
+        if xi.device.type == "cuda" and not self.training and b2[-1].bias is not None and b3[-1].bias is not None:
+            h2 = b2[:-1](xi)
+            h3 = b3[:-1](xi)
+            B, _, H, W = h2.shape
+            if (H * W) % 4 == 0:
+                z = torch.empty((B, self.no, H, W), dtype=h2.dtype, device=h2.device)
+                conv_epilogue(b2[-1], 0, h2, out=z[:, : 4 * self.reg_max])
+                conv_epilogue(b3[-1], 0, h3, out=z[:, 4 * self.reg_max:])
+                return z
+            return torch.cat((b2[-1](h2), b3[-1](h3)), 1)
+        return torch.cat((b2(xi), b3(xi)), 1)
 
     def _inference(self, x):
         if x[0].device.type == "meta":
