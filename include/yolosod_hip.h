@@ -93,6 +93,11 @@ int yolosod_nms(float* pred, int B, int nc, int A, float conf_thres, double iou_
 int yolosod_bias_act(const float* y, long y_bstride, float* out, long out_bstride, const float* bias,
                      const float* res, long res_bstride, int B, int C, long HW, int act, void* stream);
 
+/* 1x1 convolution (stride 1, groups 1) of the backbone as an fp32 MFMA GEMM with the epilogue fused:
+ * out[b*out_bs + m*HW + p] = act(sum_k w[m][k] x[b*x_bs + k*HW + p] + bias[m]) (+ res[...]); Cin % 32 == 0. */
+int yolosod_conv1x1(const float* x, long x_bs, const float* w, const float* bias, float* out, long out_bs,
+                    const float* res, long res_bs, int B, int Cin, int Cout, long HW, int act, void* stream);
+
 /* Building blocks, exported for unit tests (no single reference interface):
  * C(b,m,n) = act(sum_k A(b,m,k) B(b,k,n) + bias) + res;  A K-contiguous; B K- or N-contiguous. */
 int yolosod_gemm_f32(const float* A, long a_bs, int lda, const float* B, long b_bs, int ldb, int b_kcontig, float* C,

@@ -21,6 +21,8 @@ CASES = {
     "se_L1": ("SE_Block", (64,), (32, 32, 320, 320)),
     "cbam_L4": ("CBAM_Block", (64, 128, 16), (32, 64, 160, 160)),
     "ca_L32": ("CA_Block", (128, 256, 32), (32, 128, 80, 80)),
+    "cbam_L18": ("CBAM_Block", (256, 512, 16), (32, 256, 40, 40)),
+    "se_L23": ("SE_Block", (256,), (32, 128, 80, 80)),
 }
 
 

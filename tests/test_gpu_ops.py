@@ -70,17 +70,18 @@ def test_op_real_shapes_vs_oracle(name, cuda, monkeypatch):
     assert ok, f"{name}: rel check max abs err {err:.3g} ratio {ratio:.2f}"
 
 
-def test_se_chunked_equals_unchunked(cuda):
-    """The Infinity-Cache image chunking of the channel-attention ops must not change results (bitwise)."""
-    import importlib
-    import os
-    name = "se_c32_r64"
+@pytest.mark.parametrize("name,shape", [("se_c32_r64", (9, 32, 64, 64)), ("se_c64_r4_odd", (5, 64, 9, 7)),
+                                        ("cbam_c64", (9, 64, 48, 40)), ("cbam_c32_odd", (5, 32, 13, 11)),
+                                        ("ca_c128", (9, 128, 24, 20)), ("ca_c64_odd", (5, 64, 9, 7))])
+def test_channel_ops_batch_invariant(name, shape, cuda):
+    """Partial-reduction plans depend on the plane shape only, so a batch, its Infinity-Cache chunks and any
+    shard of it give bitwise identical results."""
     m, _ = build_fixture_module(name)
     m = m.to(cuda)
-    x = torch.randn(9, 32, 64, 64, device=cuda)
+    x = torch.randn(*shape, device=cuda)
     with torch.inference_mode():
         a = m(x)
-        b = torch.cat([m(x[i:i + 1]) for i in range(9)])
+        b = torch.cat([m(x[i:i + 1]) for i in range(shape[0])])
     assert torch.equal(a, b)
 
 
@@ -148,4 +149,39 @@ def test_decode_real_shapes(cuda):
     ref = R.decode_ref([m.double() for m in maps], [4.0, 8.0, 16.0, 32.0], 10)
     assert y.shape == (2, 14, 34000)
     ok, err, _ = tol_close(y, ref, ATOL, 0.0)
+    assert ok, err
+
+
+@pytest.mark.parametrize("B,Cin,Cout,H,W,act,res", [(2, 64, 64, 40, 40, 1, True), (3, 96, 256, 20, 20, 1, False),
+                                                     (2, 1024, 512, 20, 20, 1, False), (1, 64, 10, 16, 16, 0, False),
+                                                     (2, 128, 32, 80, 80, 1, True)])
+def test_conv1x1_epilogue(B, Cin, Cout, H, W, act, res, cuda):
+    """Backbone 1x1 conv as fused GEMM: act(conv(x) + b) (+ res), written into a channel slice."""
+    from yolosod_amd import _hip
+    g = torch.Generator().manual_seed(Cin + Cout)
+    x = torch.randn(B, Cin, H, W, generator=g)
+    w = torch.randn(Cout, Cin, generator=g) / Cin ** 0.5
+    b = torch.randn(Cout, generator=g)
+    r = torch.randn(B, Cout, H, W, generator=g) if res else None
+    ref = torch.nn.functional.conv2d(x.double(), w.double().view(Cout, Cin, 1, 1), b.double())
+    ref = torch.nn.functional.silu(ref) if act else ref
+    if res:
+        ref = ref + r.double()
+    buf = torch.zeros(B, Cout + 8, H, W, device=cuda)  # write into a channel slice of a concat buffer
+    out = _hip.conv1x1(x.to(cuda), w.to(cuda), b.to(cuda), act, out=buf[:, 4:4 + Cout],
+                       res=None if r is None else r.to(cuda))
+    ok, err, _ = tol_close(out.cpu(), ref, 1e-4, 1e-5)
+    assert ok, err
+    assert float(buf[:, :4].abs().max()) == 0.0 and float(buf[:, 4 + Cout:].abs().max()) == 0.0
+
+
+def test_bias_act_slice(cuda):
+    from yolosod_amd import _hip
+    y = torch.randn(2, 16, 12, 12)
+    b = torch.randn(16)
+    r = torch.randn(2, 16, 12, 12)
+    buf = torch.zeros(2, 40, 12, 12, device=cuda)
+    out = _hip.bias_act(y.to(cuda), b.to(cuda), 1, out=buf[:, 8:24], res=r.to(cuda))
+    ref = torch.nn.functional.silu(y.double() + b.double().view(1, -1, 1, 1)) + r.double()
+    ok, err, _ = tol_close(out.cpu(), ref, 1e-5, 1e-6)
     assert ok, err

@@ -48,6 +48,7 @@ SIGNATURES = {
     "yolosod_layernorm": (_i, [_vp, _vp, _l, _i, _vp, _vp, _f, _vp]),
     "yolosod_attention": (_i, [_vp, _vp, _l, _i, _i, _i, _vp]),
     "yolosod_bias_act": (_i, [_vp, _l, _vp, _l, _vp, _vp, _l, _i, _i, _l, _i, _vp]),
+    "yolosod_conv1x1": (_i, [_vp, _l, _vp, _vp, _vp, _l, _vp, _l, _i, _i, _i, _l, _i, _vp]),
 }
 
 _LIB = None
@@ -307,6 +308,32 @@ def bias_act(y, bias, act, out=None, res=None):
     _check(lib.yolosod_bias_act(y.data_ptr(), yb, out.data_ptr(), ob, _dev(bias, "bias"),
                                 None if res is None else res.data_ptr(), rb, B, C, HW, int(act), _stream()),
            "bias_act")
+    return out
+
+
+def conv1x1(x, w, bias, act, out=None, res=None):
+    """1x1 conv (stride 1, groups 1) + bias + act (+ res) as one fused GEMM; ``x``/``out``/``res`` may be
+    channel slices of concat buffers (contiguous channels, any batch stride)."""
+    lib = load_library()
+    B, Cin, H, W = x.shape
+    Cout = w.shape[0]
+    HW = H * W
+    if out is None:
+        out = torch.empty((B, Cout, H, W), dtype=torch.float32, device=x.device)
+
+    def bstride(t, name, C):
+        if t.device.type != "cuda" or t.dtype != torch.float32:
+            raise RuntimeError(f"conv1x1: {name} must be a float32 GPU tensor")
+        if tuple(t.shape) != (B, C, H, W) or t.stride(3) != 1 or t.stride(2) != W or t.stride(1) != HW:
+            raise RuntimeError(f"conv1x1: {name} must be [B,{C},H,W] with contiguous channels")
+        return t.stride(0)
+
+    xb = bstride(x, "x", Cin)
+    ob = bstride(out, "out", Cout)
+    rb = bstride(res, "res", Cout) if res is not None else 0
+    _check(lib.yolosod_conv1x1(x.data_ptr(), xb, _dev(w, "weight"), None if bias is None else _dev(bias, "bias"),
+                               out.data_ptr(), ob, None if res is None else res.data_ptr(), rb, B, Cin, Cout, HW,
+                               int(act), _stream()), "conv1x1")
     return out
 
 

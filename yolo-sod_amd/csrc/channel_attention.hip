@@ -1,11 +1,16 @@
 // Channel / spatial / coordinate attention of the Multi-Attention Fusion Neck: SE_Block, CBAM_Block, CA_Block.
 //
 // All three are HBM-bound (a few FLOPs per byte). Layout is the reference's NCHW fp32. Each op is split into
-//   (1) a per-(b,c)-plane reduction pass (global-avg / global-max / row+column means),
-//   (2) a tiny per-image gate computation folded into the prologue of the next pass, and
-//   (3) one streaming apply pass that reads x once and writes y once (float4, coalesced).
-// To keep the apply pass' re-read of x out of HBM, the host driver walks the batch in image chunks sized to
-// stay resident in the 256 MiB Infinity Cache between the reduction pass and the apply pass.
+//   (1) a reduction pass over x (per-plane sum/max split over several workgroups per plane, or row+column
+//       means), writing small partials,
+//   (2) a tiny per-image gate kernel (the SE / CBAM channel MLP, the CA conv1+BN+h_sigmoid+conv_h/w gates),
+//   (3) one streaming apply pass that reads x once and writes y once (float4, coalesced, every lane busy).
+// CBAM has one more reduction (per-pixel channel mean/max, split over channel groups) and a 16x16-tiled 7x7
+// conv for the spatial gate between (2) and (3).
+// Optionally (YOLOSOD_MALL_CHUNK_MB > 0) the host driver walks the batch in image chunks sized to stay resident
+// in the 256 MiB Infinity Cache between the passes. Measured on MI355X at the bs=32 640x640 shapes, the apply
+// pass' re-read does hit on-die (7.3 TB/s) but the extra launch boundaries and the smaller grids cost more
+// (SE L1 0.269 vs 0.243 ms, CBAM L4 0.199 vs 0.163, CA L32 0.090 vs 0.073), so the default is one chunk.
 //
 // Reference semantics (file:line in quitedob/yolo-sod):
 //   SE     ultralytics/nn/modules/smallobj_modules.py:84-92  (x * sigmoid(fc2(relu(fc1(mean_hw x)))))
@@ -20,7 +25,7 @@ namespace ys {
 static size_t mall_chunk_bytes() {
   static size_t v = [] {
     const char* e = getenv("YOLOSOD_MALL_CHUNK_MB");
-    long mb = e ? atol(e) : 96;
+    long mb = e ? atol(e) : 0;
     return (size_t)(mb < 0 ? 0 : mb) << 20;
   }();
   return v;
@@ -35,19 +40,43 @@ static int images_per_chunk(int B, size_t bytes_per_image) {
   return (int)n;
 }
 
+constexpr int kMaxParts = 64;
+
+// How many workgroups reduce one plane: one per 8192 floats (32 KiB), so the big early planes (SE at 320x320,
+// CBAM at 160x160) still launch thousands of workgroups per chunk. Depends on the plane size only, never on
+// the batch, so results are bitwise independent of batch size, chunking and sharding.
+struct PartPlan {
+  int parts;
+  long seg;
+};
+static PartPlan part_plan(long HW) {
+  long p = HW / 8192;
+  if (p > kMaxParts) p = kMaxParts;
+  if (p < 1) p = 1;
+  long seg = (HW + p - 1) / p;
+  if ((HW & 3) == 0) seg = (seg + 3) & ~3L;
+  p = (HW + seg - 1) / seg;
+  return {(int)p, seg};
+}
+
 // ------------------------------------------------------------------------------------------------
-// (1) per-plane sum (+max): one 256-thread workgroup per (b,c) plane, float4 streaming, 4 loads in flight.
+// (1) per-plane partial sum (+max): workgroup (plane, k) reduces x[plane][k*seg, (k+1)*seg) with four 16-B
+// loads in flight per lane; partials land in psum/pmax[plane * parts + k].
 // ------------------------------------------------------------------------------------------------
 template <bool WITH_MAX>
-__global__ __launch_bounds__(256) void plane_stats_kernel(const float* __restrict__ x, long HW,
-                                                          float* __restrict__ mean, float* __restrict__ mx) {
-  const long plane = blockIdx.x;
+__global__ __launch_bounds__(256) void plane_part_stats_kernel(const float* __restrict__ x, long HW, int parts,
+                                                               long seg, float* __restrict__ psum,
+                                                               float* __restrict__ pmax) {
+  const long plane = blockIdx.x / parts;
+  const int k = blockIdx.x % parts;
+  const long s0 = k * seg;
+  const long s1 = (s0 + seg < HW) ? s0 + seg : HW;
   const float* p = x + plane * HW;
   float s = 0.f, m = -INFINITY;
   const int tid = threadIdx.x;
   if ((HW & 3) == 0) {
-    const float4* p4 = reinterpret_cast<const float4*>(p);
-    const long n4 = HW >> 2;
+    const float4* p4 = reinterpret_cast<const float4*>(p + s0);
+    const long n4 = (s1 - s0) >> 2;
     long i = tid;
     for (; i + 3 * 256 < n4; i += 4 * 256) {
       float4 a = p4[i], b = p4[i + 256], c = p4[i + 512], d = p4[i + 768];
@@ -64,7 +93,7 @@ __global__ __launch_bounds__(256) void plane_stats_kernel(const float* __restric
       if (WITH_MAX) m = fmaxf(m, fmaxf(fmaxf(a.x, a.y), fmaxf(a.z, a.w)));
     }
   } else {
-    for (long i = tid; i < HW; i += 256) {
+    for (long i = s0 + tid; i < s1; i += 256) {
       float v = p[i];
       s += v;
       if (WITH_MAX) m = fmaxf(m, v);
@@ -80,88 +109,50 @@ __global__ __launch_bounds__(256) void plane_stats_kernel(const float* __restric
   }
   __syncthreads();
   if (tid == 0) {
-    float t = (ss[0] + ss[1]) + (ss[2] + ss[3]);
-    mean[plane] = t / (float)HW;
-    if (WITH_MAX) mx[plane] = fmaxf(fmaxf(sm[0], sm[1]), fmaxf(sm[2], sm[3]));
+    psum[blockIdx.x] = (ss[0] + ss[1]) + (ss[2] + ss[3]);
+    if (WITH_MAX) pmax[blockIdx.x] = fmaxf(fmaxf(sm[0], sm[1]), fmaxf(sm[2], sm[3]));
   }
 }
 
 // ------------------------------------------------------------------------------------------------
-// SE apply: gate a[b,c] = sigmoid(W2 relu(W1 m + b1) + b2) recomputed in the block prologue (hidden <= 64,
-// C <= 4096), then y = x * a over a chunk of the plane. grid.x = planes * chunks_per_plane.
+// (2) per-image channel gates. grid = images, 256 threads, dynamic LDS = (2*C + 128) floats.
+//   SE:   gate[c] = sigmoid(W2 relu(W1 mean + b1) + b2)
+//   CBAM: gate[c] = sigmoid(W2 relu(W1 avg) + W2 relu(W1 max))     (no biases, cbam_block.py:14-17)
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void se_apply_kernel(const float* __restrict__ x, float* __restrict__ y,
-                                                       const float* __restrict__ mean, int C, long HW,
-                                                       int chunks, const float* __restrict__ w1,
-                                                       const float* __restrict__ b1, const float* __restrict__ w2,
-                                                       const float* __restrict__ b2, int hid) {
-  const long plane = blockIdx.x / chunks;
-  const int chunk = blockIdx.x % chunks;
-  const int b = (int)(plane / C), c = (int)(plane % C);
-  __shared__ float hsh[64];
-  __shared__ float gate;
+template <bool CBAM>
+__global__ __launch_bounds__(256) void channel_gate_kernel(const float* __restrict__ psum,
+                                                           const float* __restrict__ pmax, int parts, int C,
+                                                           float inv_hw, const float* __restrict__ w1,
+                                                           const float* __restrict__ b1, const float* __restrict__ w2,
+                                                           const float* __restrict__ b2, int hid,
+                                                           float* __restrict__ gate) {
+  extern __shared__ float sh[];
+  float* avg = sh;            // [C]
+  float* mx = sh + C;         // [C]   (CBAM)
+  float* hsh = sh + 2 * C;    // [128] hidden of both branches
+  const int b = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const float* mb = mean + (long)b * C;
-  for (int j = wv; j < hid; j += 4) {
-    float acc = 0.f;
-    for (int k = lane; k < C; k += 64) acc += w1[(long)j * C + k] * mb[k];
-    acc = wave_sum(acc);
-    if (lane == 0) hsh[j] = fmaxf(acc + b1[j], 0.f);
-  }
-  __syncthreads();
-  if (tid == 0) {
-    float z = 0.f;
-    for (int j = 0; j < hid; ++j) z += w2[(long)c * hid + j] * hsh[j];
-    gate = sigmoidf_(z + b2[c]);
-  }
-  __syncthreads();
-  const float a = gate;
-  const float* p = x + plane * HW;
-  float* q = y + plane * HW;
-  const long per = (HW + chunks - 1) / chunks;
-  long s0 = chunk * per, s1 = s0 + per;
-  if (s1 > HW) s1 = HW;
-  if ((HW & 3) == 0 && (per & 3) == 0) {
-    const float4* p4 = reinterpret_cast<const float4*>(p + s0);
-    float4* q4 = reinterpret_cast<float4*>(q + s0);
-    const long n4 = (s1 - s0) >> 2;
-    for (long i = tid; i < n4; i += 256) {
-      float4 v = p4[i];
-      v.x *= a; v.y *= a; v.z *= a; v.w *= a;
-      q4[i] = v;
+  for (int c = tid; c < C; c += 256) {
+    const float* ps = psum + ((long)b * C + c) * parts;
+    float s = 0.f;
+    for (int k = 0; k < parts; ++k) s += ps[k];
+    avg[c] = s * inv_hw;
+    if (CBAM) {
+      const float* pm = pmax + ((long)b * C + c) * parts;
+      float m = -INFINITY;
+      for (int k = 0; k < parts; ++k) m = fmaxf(m, pm[k]);
+      mx[c] = m;
     }
-  } else {
-    for (long i = s0 + tid; i < s1; i += 256) q[i] = p[i] * a;
   }
-}
-
-static int chunks_for_plane(long HW) {
-  // ~16 KiB of x per workgroup keeps >= 8 waves/CU busy even for the smallest planes.
-  long c = HW / 4096;
-  if (c < 1) c = 1;
-  if (c > 64) c = 64;
-  // keep chunk length a multiple of 4 floats when possible
-  while (c > 1 && ((HW + c - 1) / c) % 4 != 0) --c;
-  return (int)c;
-}
-
-// ------------------------------------------------------------------------------------------------
-// CBAM pass 2: per-pixel channel mean / max of o = ca[c] * x  ->  map[b][0|1][p].
-// The block prologue computes ca[b, :] = sigmoid(fc(avg) + fc(max)) into LDS (fc = W2 relu(W1 .), no bias);
-// block (0, b) also publishes ca to global for pass 3.
-// ------------------------------------------------------------------------------------------------
-template <int MAXC>
-__device__ void cbam_channel_gate(const float* avg, const float* mx, const float* w1, const float* w2, int C, int hid,
-                                  float* ca_sh, float* hsh) {
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  // hidden activations of both branches: hsh[j] (avg), hsh[64+j] (max)
-  for (int j = wv; j < 2 * hid; j += 4) {
+  __syncthreads();
+  const int nh = CBAM ? 2 * hid : hid;
+  for (int j = wv; j < nh; j += 4) {
     const int jj = j % hid;
     const float* v = (j < hid) ? avg : mx;
     float acc = 0.f;
     for (int k = lane; k < C; k += 64) acc += w1[(long)jj * C + k] * v[k];
     acc = wave_sum(acc);
-    if (lane == 0) hsh[(j < hid ? 0 : 64) + jj] = fmaxf(acc, 0.f);
+    if (lane == 0) hsh[(j < hid ? 0 : 64) + jj] = fmaxf(CBAM ? acc : acc + b1[jj], 0.f);
   }
   __syncthreads();
   for (int c = tid; c < C; c += 256) {
@@ -169,115 +160,232 @@ __device__ void cbam_channel_gate(const float* avg, const float* mx, const float
     for (int j = 0; j < hid; ++j) {
       const float wcj = w2[(long)c * hid + j];
       za += wcj * hsh[j];
-      zm += wcj * hsh[64 + j];
+      if (CBAM) zm += wcj * hsh[64 + j];
     }
-    ca_sh[c] = sigmoidf_(za + zm);
+    gate[(long)b * C + c] = CBAM ? sigmoidf_(za + zm) : sigmoidf_(za + b2[c]);
   }
-  __syncthreads();
 }
 
-__global__ __launch_bounds__(256) void cbam_pixel_stats_kernel(const float* __restrict__ x, const float* __restrict__ avg,
-                                                               const float* __restrict__ mx, const float* __restrict__ w1,
-                                                               const float* __restrict__ w2, int C, int hid, long HW,
-                                                               float* __restrict__ ca_out, float* __restrict__ map) {
-  __shared__ float ca_sh[4096];
-  __shared__ float hsh[128];
-  const int b = blockIdx.y;
-  cbam_channel_gate<4096>(avg + (long)b * C, mx + (long)b * C, w1, w2, C, hid, ca_sh, hsh);
-  if (blockIdx.x == 0)
-    for (int c = threadIdx.x; c < C; c += 256) ca_out[(long)b * C + c] = ca_sh[c];
-  const long p = (long)blockIdx.x * 256 + threadIdx.x;
+// ------------------------------------------------------------------------------------------------
+// (3a) SE apply: y = x * gate[plane]. grid = (planes, ceil(HW / 4096)); each lane issues its four 16-B loads
+// before the first store.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void plane_scale_kernel(const float* __restrict__ x, float* __restrict__ y,
+                                                          const float* __restrict__ gate, long HW) {
+  const long plane = blockIdx.x;
+  const float a = gate[plane];
+  const int tid = threadIdx.x;
+  if ((HW & 3) == 0) {
+    const float4* p4 = reinterpret_cast<const float4*>(x + plane * HW);
+    float4* q4 = reinterpret_cast<float4*>(y + plane * HW);
+    const long n4 = HW >> 2;
+    const long base = (long)blockIdx.y * 1024 + tid;
+    float4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (base + u * 256 < n4) v[u] = p4[base + u * 256];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (base + u * 256 < n4) {
+        float4 o = v[u];
+        o.x *= a; o.y *= a; o.z *= a; o.w *= a;
+        q4[base + u * 256] = o;
+      }
+  } else {
+    const float* p = x + plane * HW;
+    float* q = y + plane * HW;
+    const long base = (long)blockIdx.y * 4096 + tid;
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+      if (base + u * 256 < HW) q[base + u * 256] = p[base + u * 256] * a;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// CBAM pass 2: per-pixel channel sum / max of o = ca[c] * x over channel group g -> mpart[b][g][0|1][HW].
+// grid = (ceil(HW / (256*V)), G, images); V = 4 (float4 pixels) when HW % 4 == 0.
+// ------------------------------------------------------------------------------------------------
+template <int V>
+__global__ __launch_bounds__(256) void cbam_pixel_stats_kernel(const float* __restrict__ x,
+                                                               const float* __restrict__ ca, int C, int CG, long HW,
+                                                               float* __restrict__ mpart) {
+  const int b = blockIdx.z, g = blockIdx.y, G = gridDim.y;
+  const long p = ((long)blockIdx.x * 256 + threadIdx.x) * V;
   if (p >= HW) return;
-  const float* xb = x + (long)b * C * HW + p;
-  float s = 0.f, m = -INFINITY;
-  int c = 0;
-  for (; c + 8 <= C; c += 8) {
-    float v[8];
+  const int c0 = g * CG;
+  const int c1 = (c0 + CG < C) ? c0 + CG : C;
+  const float* xb = x + ((long)b * C) * HW + p;
+  const float* cab = ca + (long)b * C;
+  float* sp = mpart + ((long)(b * G + g) * 2) * HW + p;
+  if (V == 4) {
+    f32x4 s = {0.f, 0.f, 0.f, 0.f}, m = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    int c = c0;
+    for (; c + 8 <= c1; c += 8) {
+      f32x4 v[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = xb[(long)(c + u) * HW];
+      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const f32x4*>(xb + (long)(c + u) * HW);
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const float o = ca_sh[c + u] * v[u];
+      for (int u = 0; u < 8; ++u) {
+        const f32x4 o = cab[c + u] * v[u];
+        s += o;
+        m.x = fmaxf(m.x, o.x); m.y = fmaxf(m.y, o.y); m.z = fmaxf(m.z, o.z); m.w = fmaxf(m.w, o.w);
+      }
+    }
+    for (; c < c1; ++c) {
+      const f32x4 o = cab[c] * *reinterpret_cast<const f32x4*>(xb + (long)c * HW);
+      s += o;
+      m.x = fmaxf(m.x, o.x); m.y = fmaxf(m.y, o.y); m.z = fmaxf(m.z, o.z); m.w = fmaxf(m.w, o.w);
+    }
+    *reinterpret_cast<f32x4*>(sp) = s;
+    *reinterpret_cast<f32x4*>(sp + HW) = m;
+  } else {
+    float s = 0.f, m = -INFINITY;
+    int c = c0;
+    for (; c + 8 <= c1; c += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = xb[(long)(c + u) * HW];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const float o = cab[c + u] * v[u];
+        s += o;
+        m = fmaxf(m, o);
+      }
+    }
+    for (; c < c1; ++c) {
+      const float o = cab[c] * xb[(long)c * HW];
       s += o;
       m = fmaxf(m, o);
     }
+    sp[0] = s;
+    sp[HW] = m;
   }
-  for (; c < C; ++c) {
-    const float o = ca_sh[c] * xb[(long)c * HW];
-    s += o;
-    m = fmaxf(m, o);
-  }
-  float* mp = map + (long)b * 2 * HW;
-  mp[p] = s / (float)C;
-  mp[HW + p] = m;
 }
 
-// CBAM pass 3: sa = sigmoid(conv7x7([mean;max]), pad 3, no bias); y = sa * (ca[c] * x).
-__global__ __launch_bounds__(256) void cbam_apply_kernel(const float* __restrict__ x, float* __restrict__ y,
-                                                         const float* __restrict__ ca, const float* __restrict__ map,
-                                                         const float* __restrict__ wsa, int C, int H, int W) {
+// CBAM pass 2b: sa = sigmoid(conv7x7([mean_c o ; max_c o]), zero pad 3, no bias) on 16x16 output tiles, the
+// 22x22 halo of both maps (combined over the G channel groups) staged in LDS. grid = (tiles_x, tiles_y, images).
+__global__ __launch_bounds__(256) void cbam_sa_kernel(const float* __restrict__ mpart, int G, int C, int H, int W,
+                                                      const float* __restrict__ wsa, float* __restrict__ sa) {
+  __shared__ float mm[2][22][23];
   __shared__ float wk[98];
-  if (threadIdx.x < 98) wk[threadIdx.x] = wsa[threadIdx.x];
-  __syncthreads();
-  const int b = blockIdx.y;
+  const int b = blockIdx.z;
   const long HW = (long)H * W;
-  const long p = (long)blockIdx.x * 256 + threadIdx.x;
-  if (p >= HW) return;
-  const int py = (int)(p / W), px = (int)(p % W);
-  const float* mp = map + (long)b * 2 * HW;
-  float z = 0.f;
-  for (int ci = 0; ci < 2; ++ci) {
-    const float* m = mp + ci * HW;
-    for (int ky = 0; ky < 7; ++ky) {
-      const int yy = py + ky - 3;
-      if (yy < 0 || yy >= H) continue;
-      for (int kx = 0; kx < 7; ++kx) {
-        const int xx = px + kx - 3;
-        if (xx < 0 || xx >= W) continue;
-        z += wk[ci * 49 + ky * 7 + kx] * m[(long)yy * W + xx];
+  const int tid = threadIdx.x;
+  if (tid < 98) wk[tid] = wsa[tid];
+  const int oy = blockIdx.y * 16 - 3, ox = blockIdx.x * 16 - 3;
+  const float invC = 1.0f / (float)C;
+  for (int i = tid; i < 22 * 22; i += 256) {
+    const int ty = i / 22, tx = i % 22;
+    const int yy = oy + ty, xx = ox + tx;
+    float s = 0.f, m = 0.f;
+    if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
+      const float* q = mpart + (long)b * G * 2 * HW + (long)yy * W + xx;
+      m = -INFINITY;
+      for (int g = 0; g < G; ++g) {
+        s += q[(long)(2 * g) * HW];
+        m = fmaxf(m, q[(long)(2 * g + 1) * HW]);
       }
+      s *= invC;
     }
+    mm[0][ty][tx] = s;
+    mm[1][ty][tx] = m;
   }
-  const float sa = sigmoidf_(z);
-  const float* xb = x + (long)b * C * HW + p;
-  float* yb = y + (long)b * C * HW + p;
-  const float* cab = ca + (long)b * C;
-  int c = 0;
-  for (; c + 8 <= C; c += 8) {
-    float v[8];
+  __syncthreads();
+  const int ly = tid >> 4, lx = tid & 15;
+  const int py = blockIdx.y * 16 + ly, px = blockIdx.x * 16 + lx;
+  if (py >= H || px >= W) return;
+  float z = 0.f;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = xb[(long)(c + u) * HW];
+  for (int ci = 0; ci < 2; ++ci)
 #pragma unroll
-    for (int u = 0; u < 8; ++u) yb[(long)(c + u) * HW] = sa * (cab[c + u] * v[u]);
+    for (int ky = 0; ky < 7; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < 7; ++kx) z += wk[ci * 49 + ky * 7 + kx] * mm[ci][ly + ky][lx + kx];
+  sa[(long)b * HW + (long)py * W + px] = sigmoidf_(z);
+}
+
+// CBAM pass 3: y = sa[p] * (ca[c] * x). grid = (ceil(HW / (256*V)), ceil(C / 8), images).
+template <int V>
+__global__ __launch_bounds__(256) void cbam_apply_kernel(const float* __restrict__ x, float* __restrict__ y,
+                                                         const float* __restrict__ ca, const float* __restrict__ sa,
+                                                         int C, long HW) {
+  const int b = blockIdx.z;
+  const long p = ((long)blockIdx.x * 256 + threadIdx.x) * V;
+  if (p >= HW) return;
+  const int c0 = blockIdx.y * 8;
+  const int n = (C - c0 < 8) ? C - c0 : 8;
+  const float* xb = x + ((long)b * C + c0) * HW + p;
+  float* yb = y + ((long)b * C + c0) * HW + p;
+  const float* cab = ca + (long)b * C + c0;
+  if (V == 4) {
+    const f32x4 s4 = *reinterpret_cast<const f32x4*>(sa + (long)b * HW + p);
+    if (n == 8) {
+      f32x4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const f32x4*>(xb + (long)u * HW);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) *reinterpret_cast<f32x4*>(yb + (long)u * HW) = s4 * (cab[u] * v[u]);
+    } else {
+      for (int u = 0; u < n; ++u)
+        *reinterpret_cast<f32x4*>(yb + (long)u * HW) = s4 * (cab[u] * *reinterpret_cast<const f32x4*>(xb + (long)u * HW));
+    }
+  } else {
+    const float s = sa[(long)b * HW + p];
+    for (int u = 0; u < n; ++u) yb[(long)u * HW] = s * (cab[u] * xb[(long)u * HW]);
   }
-  for (; c < C; ++c) yb[(long)c * HW] = sa * (cab[c] * xb[(long)c * HW]);
 }
 
 // ------------------------------------------------------------------------------------------------
 // CA pass 1: row means (over W) and column means (over H) of each (b,c) plane -> yin[b][c][0..H+W).
+// One workgroup per plane; the plane streams through LDS in bands of <= 8192 floats (16-B loads when W % 4
+// == 0), rows reduced by lane quads, columns accumulated in registers (W <= 1024).
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void ca_pool_kernel(const float* __restrict__ x, int H, int W, float* __restrict__ yin) {
+__global__ __launch_bounds__(256) void ca_pool_kernel(const float* __restrict__ x, int H, int W, int RB,
+                                                      float* __restrict__ yin) {
+  extern __shared__ float band[];
   const long plane = blockIdx.x;
   const float* p = x + plane * (long)H * W;
   float* o = yin + plane * (long)(H + W);
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  for (int h = wv; h < H; h += 4) {
-    float s = 0.f;
-    for (int w = lane; w < W; w += 64) s += p[(long)h * W + w];
-    s = wave_sum(s);
-    if (lane == 0) o[h] = s / (float)W;
+  const int tid = threadIdx.x;
+  float col[4] = {0.f, 0.f, 0.f, 0.f};
+  const float invW = 1.0f / (float)W;
+  for (int h0 = 0; h0 < H; h0 += RB) {
+    const int rb = (H - h0 < RB) ? H - h0 : RB;
+    const int n = rb * W;
+    const float* src = p + (long)h0 * W;
+    if ((W & 3) == 0) {
+      const float4* s4 = reinterpret_cast<const float4*>(src);
+      for (int i = tid; i < (n >> 2); i += 256) reinterpret_cast<float4*>(band)[i] = s4[i];
+    } else {
+      for (int i = tid; i < n; i += 256) band[i] = src[i];
+    }
+    __syncthreads();
+    for (int r = tid >> 2; r < rb; r += 64) {
+      float s = 0.f;
+      for (int w = tid & 3; w < W; w += 4) s += band[r * W + w];
+      s = quad_sum(s);
+      if ((tid & 3) == 0) o[h0 + r] = s * invW;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int w = tid + 256 * u;
+      if (w < W)
+        for (int r = 0; r < rb; ++r) col[u] += band[r * W + w];
+    }
+    __syncthreads();
   }
-  for (int w = tid; w < W; w += 256) {
-    float s = 0.f;
-    for (int h = 0; h < H; ++h) s += p[(long)h * W + w];
-    o[H + w] = s / (float)H;
+  const float invH = 1.0f / (float)H;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int w = tid + 256 * u;
+    if (w < W) o[H + w] = col[u] * invH;
   }
 }
 
 // CA pass 2: per position p of the concatenated (H+W) axis:
 //   t[j]   = h_sigmoid(BN(sum_c W1[j][c] yin[c][p] + b1[j]))        (conv1 + bn1 + act; BN eval, eps given)
 //   gate[c][p] = sigmoid(sum_j Wx[c][j] t[j] + bx[c]),  Wx = conv_h for p < H, conv_w otherwise.
-// grid = (ceil((H+W)/16), B); 256 threads.
+// grid = (ceil((H+W)/16), images); the 16 positions of yin, W1 (row stride C+1) and conv_h/conv_w staged in LDS.
 __global__ __launch_bounds__(256) void ca_gate_kernel(const float* __restrict__ yin, int C, int H, int W, int mip,
                                                       const float* __restrict__ w1, const float* __restrict__ b1,
                                                       const float* __restrict__ bn_w, const float* __restrict__ bn_b,
@@ -286,24 +394,37 @@ __global__ __launch_bounds__(256) void ca_gate_kernel(const float* __restrict__ 
                                                       const float* __restrict__ bh, const float* __restrict__ ww,
                                                       const float* __restrict__ bw, float* __restrict__ gate) {
   constexpr int P = 16;
-  __shared__ float t_sh[P][65];
+  extern __shared__ float sh[];
+  float* ys = sh;                              // [C][P]
+  float* w1s = ys + C * P;                     // [mip][C+1]
+  float* whs = w1s + mip * (C + 1);            // [C*mip]
+  float* wws = whs + C * mip;                  // [C*mip]
+  float* ts = wws + C * mip;                   // [P][mip+1]
   const int b = blockIdx.y;
   const int L = H + W;
   const int p0 = blockIdx.x * P;
   const int tid = threadIdx.x;
   const float* yb = yin + (long)b * C * L;
-  // t: P x mip outputs, one thread each (mip <= 64 -> P*mip <= 1024, loop)
+  for (int i = tid; i < C * P; i += 256) {
+    const int c = i / P, pp = i % P;
+    ys[i] = (p0 + pp < L) ? yb[(long)c * L + p0 + pp] : 0.f;
+  }
+  for (int i = tid; i < mip * C; i += 256) w1s[(i / C) * (C + 1) + i % C] = w1[i];
+  for (int i = tid; i < C * mip; i += 256) {
+    whs[i] = wh[i];
+    wws[i] = ww[i];
+  }
+  __syncthreads();
   for (int o = tid; o < P * mip; o += 256) {
     const int pp = o / mip, j = o % mip;
-    const int p = p0 + pp;
-    if (p >= L) continue;
+    const float* wr = w1s + j * (C + 1);
     float acc = 0.f;
-    for (int c = 0; c < C; ++c) acc += w1[(long)j * C + c] * yb[(long)c * L + p];
+    for (int c = 0; c < C; ++c) acc += wr[c] * ys[c * P + pp];
     float z = acc + b1[j];
     const float inv = 1.0f / sqrtf(bn_v[j] + bn_eps);
     z = (z - bn_m[j]) * inv * bn_w[j] + bn_b[j];
     z = fminf(fmaxf(z + 3.0f, 0.0f), 6.0f) / 6.0f;
-    t_sh[pp][j] = z;
+    ts[pp * (mip + 1) + j] = z;
   }
   __syncthreads();
   float* gb = gate + (long)b * C * L;
@@ -311,50 +432,41 @@ __global__ __launch_bounds__(256) void ca_gate_kernel(const float* __restrict__ 
     const int c = o / P, pp = o % P;
     const int p = p0 + pp;
     if (p >= L) continue;
-    const float* wx = (p < H) ? wh : ww;
+    const float* wx = ((p < H) ? whs : wws) + c * mip;
     const float bx = (p < H) ? bh[c] : bw[c];
+    const float* t = ts + pp * (mip + 1);
     float acc = 0.f;
-    for (int j = 0; j < mip; ++j) acc += wx[(long)c * mip + j] * t_sh[pp][j];
+    for (int j = 0; j < mip; ++j) acc += wx[j] * t[j];
     gb[(long)c * L + p] = sigmoidf_(acc + bx);
   }
 }
 
-// CA pass 3: y[b,c,h,w] = (x * a_w[b,c,w]) * a_h[b,c,h]; gate rows are [a_h (H) | a_w (W)].
-__global__ __launch_bounds__(256) void ca_apply_kernel(const float* __restrict__ x, float* __restrict__ y,
-                                                       const float* __restrict__ gate, int H, int W, long total) {
-  const long L = H + W;
-  if ((W & 3) == 0) {
-    const long n4 = total >> 2;
-    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
-      const long e = i << 2;
-      const long plane = e / ((long)H * W);
-      const long r = e % ((long)H * W);
-      const int h = (int)(r / W), w = (int)(r % W);
-      const float* g = gate + plane * L;
-      const float ah = g[h];
-      float4 v = reinterpret_cast<const float4*>(x)[i];
-      v.x = (v.x * g[H + w]) * ah;
-      v.y = (v.y * g[H + w + 1]) * ah;
-      v.z = (v.z * g[H + w + 2]) * ah;
-      v.w = (v.w * g[H + w + 3]) * ah;
-      reinterpret_cast<float4*>(y)[i] = v;
-    }
-  } else {
-    for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
-      const long plane = e / ((long)H * W);
-      const long r = e % ((long)H * W);
-      const int h = (int)(r / W), w = (int)(r % W);
-      const float* g = gate + plane * L;
-      y[e] = (x[e] * g[H + w]) * g[h];
-    }
-  }
+static size_t ca_gate_lds_bytes(int C, int mip) {
+  return sizeof(float) * ((size_t)C * 16 + (size_t)mip * (C + 1) + 2 * (size_t)C * mip + 16 * (size_t)(mip + 1));
 }
 
-static int grid_stride_blocks(long work_items) {
-  long b = (work_items + 255) / 256;
-  if (b > 256L * 16) b = 256L * 16;
-  if (b < 1) b = 1;
-  return (int)b;
+// CA pass 3: y[b,c,h,w] = (x * a_w[b,c,w]) * a_h[b,c,h]; gate rows are [a_h (H) | a_w (W)].
+// grid = (planes, ceil(HW / (256*V))); V = 4 when W % 4 == 0 (a float4 never straddles two rows).
+template <int V>
+__global__ __launch_bounds__(256) void ca_apply_kernel(const float* __restrict__ x, float* __restrict__ y,
+                                                       const float* __restrict__ gate, int H, int W) {
+  const long plane = blockIdx.x;
+  const long HW = (long)H * W;
+  const long e = ((long)blockIdx.y * 256 + threadIdx.x) * V;
+  if (e >= HW) return;
+  const int h = (int)(e / W), w = (int)(e - (long)h * W);
+  const float* g = gate + plane * (H + W);
+  const float ah = g[h];
+  if (V == 4) {
+    f32x4 v = *reinterpret_cast<const f32x4*>(x + plane * HW + e);
+    v.x = (v.x * g[H + w]) * ah;
+    v.y = (v.y * g[H + w + 1]) * ah;
+    v.z = (v.z * g[H + w + 2]) * ah;
+    v.w = (v.w * g[H + w + 3]) * ah;
+    *reinterpret_cast<f32x4*>(y + plane * HW + e) = v;
+  } else {
+    y[plane * HW + e] = (x[plane * HW + e] * g[H + w]) * ah;
+  }
 }
 
 }  // namespace ys
@@ -365,8 +477,10 @@ using namespace ys;
 // C ABI
 // =================================================================================================
 YS_EXPORT size_t yolosod_se_workspace(int B, int C, int H, int W) {
+  (void)H; (void)W;
   Sizer s;
-  s.take<float>((size_t)B * C);
+  s.take<float>((size_t)B * C * part_plan((long)H * W).parts);  // partial sums
+  s.take<float>((size_t)B * C);              // gates
   return s.off;
 }
 
@@ -374,34 +488,48 @@ YS_EXPORT int yolosod_se_forward(const float* x, float* y, int B, int C, int H, 
                                  const float* fc1_b, const float* fc2_w, const float* fc2_b, int hidden,
                                  void* workspace, size_t workspace_bytes, void* stream) {
   YS_CHECK_ARG(x && y && fc1_w && fc1_b && fc2_w && fc2_b, "se: null pointer");
-  YS_CHECK_ARG(B >= 0 && C > 0 && H > 0 && W > 0, "se: bad shape");
+  YS_CHECK_ARG(B >= 0 && C > 0 && C <= 16384 && H > 0 && W > 0, "se: bad shape");
   YS_CHECK_ARG(hidden > 0 && hidden <= 64, "se: hidden=%d unsupported (1..64)", hidden);
   if (B == 0) return 0;
   Carver cv(workspace, workspace_bytes);
-  float* mean = cv.take<float>((size_t)B * C);
-  YS_CHECK_ARG(mean, "se: workspace too small (%zu)", workspace_bytes);
+  float* psum = cv.take<float>((size_t)B * C * part_plan((long)H * W).parts);
+  float* gate = cv.take<float>((size_t)B * C);
+  YS_CHECK_ARG(gate, "se: workspace too small (%zu)", workspace_bytes);
   hipStream_t st = (hipStream_t)stream;
   const long HW = (long)H * W;
-  const int chunks = chunks_for_plane(HW);
   const int ipc = images_per_chunk(B, (size_t)C * HW * sizeof(float));
+  const PartPlan pp = part_plan(HW);
+  const unsigned ychunks = (unsigned)((HW + 4095) / 4096);
+  const size_t lds = sizeof(float) * (2 * (size_t)C + 128);
   for (int b0 = 0; b0 < B; b0 += ipc) {
     const int nb = (B - b0 < ipc) ? B - b0 : ipc;
     const long off = (long)b0 * C * HW;
-    hipLaunchKernelGGL((plane_stats_kernel<false>), dim3(nb * C), dim3(256), 0, st, x + off, HW, mean + (long)b0 * C,
-                       nullptr);
-    hipLaunchKernelGGL(se_apply_kernel, dim3((unsigned)(nb * C * chunks)), dim3(256), 0, st, x + off, y + off,
-                       mean + (long)b0 * C, C, HW, chunks, fc1_w, fc1_b, fc2_w, fc2_b, hidden);
+    float* ps = psum + (long)b0 * C * pp.parts;
+    hipLaunchKernelGGL((plane_part_stats_kernel<false>), dim3((unsigned)(nb * C * pp.parts)), dim3(256), 0, st,
+                       x + off, HW, pp.parts, pp.seg, ps, nullptr);
+    hipLaunchKernelGGL((channel_gate_kernel<false>), dim3(nb), dim3(256), lds, st, ps, nullptr, pp.parts, C,
+                       1.0f / (float)HW, fc1_w, fc1_b, fc2_w, fc2_b, hidden, gate + (long)b0 * C);
+    hipLaunchKernelGGL(plane_scale_kernel, dim3((unsigned)(nb * C), ychunks), dim3(256), 0, st, x + off, y + off,
+                       gate + (long)b0 * C, HW);
   }
   YS_CHECK_LAUNCH("se");
   return 0;
 }
 
+// channel groups of the CBAM per-pixel pass: 32 channels each (fixed, for batch-invariant sums); the partial
+// maps cost 2/32 of x in extra traffic.
+constexpr int kCbamGroup = 32;
+
 YS_EXPORT size_t yolosod_cbam_workspace(int B, int C, int H, int W) {
+  const long HW = (long)H * W;
+  const int ipc = B > 0 ? images_per_chunk(B, (size_t)C * HW * sizeof(float)) : 1;
+  const int G = (C + kCbamGroup - 1) / kCbamGroup;
   Sizer s;
-  s.take<float>((size_t)B * C);  // avg
-  s.take<float>((size_t)B * C);  // max
-  s.take<float>((size_t)B * C);  // ca
-  s.take<float>((size_t)B * 2 * H * W);  // [mean;max] map
+  s.take<float>((size_t)B * C * part_plan((long)H * W).parts);  // partial sums
+  s.take<float>((size_t)B * C * part_plan((long)H * W).parts);  // partial maxes
+  s.take<float>((size_t)B * C);              // ca
+  s.take<float>((size_t)ipc * G * 2 * HW);   // per-group [sum;max] maps of one chunk
+  s.take<float>((size_t)B * HW);             // sa
   return s.off;
 }
 
@@ -409,28 +537,47 @@ YS_EXPORT int yolosod_cbam_forward(const float* x, float* y, int B, int C, int H
                                    const float* fc2_w, int hidden, const float* sa_w, void* workspace,
                                    size_t workspace_bytes, void* stream) {
   YS_CHECK_ARG(x && y && fc0_w && fc2_w && sa_w, "cbam: null pointer");
-  YS_CHECK_ARG(B >= 0 && C > 0 && C <= 4096 && H > 0 && W > 0, "cbam: bad shape");
+  YS_CHECK_ARG(B >= 0 && C > 0 && C <= 16384 && H > 0 && W > 0, "cbam: bad shape");
   YS_CHECK_ARG(hidden > 0 && hidden <= 64, "cbam: hidden=%d unsupported (1..64)", hidden);
   if (B == 0) return 0;
-  Carver cv(workspace, workspace_bytes);
-  float* avg = cv.take<float>((size_t)B * C);
-  float* mx = cv.take<float>((size_t)B * C);
-  float* ca = cv.take<float>((size_t)B * C);
-  float* map = cv.take<float>((size_t)B * 2 * H * W);
-  YS_CHECK_ARG(map, "cbam: workspace too small (%zu)", workspace_bytes);
-  hipStream_t st = (hipStream_t)stream;
   const long HW = (long)H * W;
+  const int V = (HW % 4 == 0) ? 4 : 1;
+  const long pxb = (HW + 256 * V - 1) / (256 * V);
   const int ipc = images_per_chunk(B, (size_t)C * HW * sizeof(float));
+  const int G = (C + kCbamGroup - 1) / kCbamGroup;
+  Carver cv(workspace, workspace_bytes);
+  float* psum = cv.take<float>((size_t)B * C * part_plan((long)H * W).parts);
+  float* pmax = cv.take<float>((size_t)B * C * part_plan((long)H * W).parts);
+  float* ca = cv.take<float>((size_t)B * C);
+  float* mpart = cv.take<float>((size_t)ipc * G * 2 * HW);
+  float* sa = cv.take<float>((size_t)B * HW);
+  YS_CHECK_ARG(sa, "cbam: workspace too small (%zu)", workspace_bytes);
+  hipStream_t st = (hipStream_t)stream;
+  const PartPlan pp = part_plan(HW);
+  const size_t lds = sizeof(float) * (2 * (size_t)C + 128);
   for (int b0 = 0; b0 < B; b0 += ipc) {
     const int nb = (B - b0 < ipc) ? B - b0 : ipc;
     const long off = (long)b0 * C * HW;
-    hipLaunchKernelGGL((plane_stats_kernel<true>), dim3(nb * C), dim3(256), 0, st, x + off, HW,
-                       avg + (long)b0 * C, mx + (long)b0 * C);
-    dim3 g((unsigned)((HW + 255) / 256), nb);
-    hipLaunchKernelGGL(cbam_pixel_stats_kernel, g, dim3(256), 0, st, x + off, avg + (long)b0 * C, mx + (long)b0 * C,
-                       fc0_w, fc2_w, C, hidden, HW, ca + (long)b0 * C, map + (long)b0 * 2 * HW);
-    hipLaunchKernelGGL(cbam_apply_kernel, g, dim3(256), 0, st, x + off, y + off, ca + (long)b0 * C,
-                       map + (long)b0 * 2 * HW, sa_w, C, H, W);
+    float* ps = psum + (long)b0 * C * pp.parts;
+    float* pm = pmax + (long)b0 * C * pp.parts;
+    float* cab = ca + (long)b0 * C;
+    float* sab = sa + (long)b0 * HW;
+    hipLaunchKernelGGL((plane_part_stats_kernel<true>), dim3((unsigned)(nb * C * pp.parts)), dim3(256), 0, st,
+                       x + off, HW, pp.parts, pp.seg, ps, pm);
+    hipLaunchKernelGGL((channel_gate_kernel<true>), dim3(nb), dim3(256), lds, st, ps, pm, pp.parts, C,
+                       1.0f / (float)HW, fc0_w, nullptr, fc2_w, nullptr, hidden, cab);
+    dim3 gs((unsigned)pxb, G, nb);
+    if (V == 4)
+      hipLaunchKernelGGL((cbam_pixel_stats_kernel<4>), gs, dim3(256), 0, st, x + off, cab, C, kCbamGroup, HW, mpart);
+    else
+      hipLaunchKernelGGL((cbam_pixel_stats_kernel<1>), gs, dim3(256), 0, st, x + off, cab, C, kCbamGroup, HW, mpart);
+    hipLaunchKernelGGL(cbam_sa_kernel, dim3((W + 15) / 16, (H + 15) / 16, nb), dim3(256), 0, st, mpart, G, C, H, W,
+                       sa_w, sab);
+    dim3 ga((unsigned)pxb, (C + 7) / 8, nb);
+    if (V == 4)
+      hipLaunchKernelGGL((cbam_apply_kernel<4>), ga, dim3(256), 0, st, x + off, y + off, cab, sab, C, HW);
+    else
+      hipLaunchKernelGGL((cbam_apply_kernel<1>), ga, dim3(256), 0, st, x + off, y + off, cab, sab, C, HW);
   }
   YS_CHECK_LAUNCH("cbam");
   return 0;
@@ -451,8 +598,10 @@ YS_EXPORT int yolosod_ca_forward(const float* x, float* y, int B, int C, int H, 
   YS_CHECK_ARG(x && y && conv1_w && conv1_b && bn_w && bn_b && bn_mean && bn_var && convh_w && convh_b && convw_w &&
                    convw_b,
                "ca: null pointer");
-  YS_CHECK_ARG(B >= 0 && C > 0 && H > 0 && W > 0, "ca: bad shape");
+  YS_CHECK_ARG(B >= 0 && C > 0 && H > 0 && W > 0 && W <= 1024, "ca: bad shape (W <= 1024 supported)");
   YS_CHECK_ARG(mip > 0 && mip <= 64, "ca: mip=%d unsupported (1..64)", mip);
+  const size_t gate_lds = ca_gate_lds_bytes(C, mip);
+  YS_CHECK_ARG(gate_lds <= 64 * 1024, "ca: C=%d mip=%d exceed the gate kernel's LDS budget", C, mip);
   if (B == 0) return 0;
   Carver cv(workspace, workspace_bytes);
   float* yin = cv.take<float>((size_t)B * C * (H + W));
@@ -460,18 +609,27 @@ YS_EXPORT int yolosod_ca_forward(const float* x, float* y, int B, int C, int H, 
   YS_CHECK_ARG(gate, "ca: workspace too small (%zu)", workspace_bytes);
   hipStream_t st = (hipStream_t)stream;
   const long HW = (long)H * W;
+  int RB = 8192 / W;
+  if (RB < 1) RB = 1;
+  if (RB > H) RB = H;
+  const size_t pool_lds = sizeof(float) * (size_t)RB * W;
+  const int V = (W % 4 == 0) ? 4 : 1;
+  const unsigned apply_y = (unsigned)((HW + 256 * V - 1) / (256 * V));
   const int ipc = images_per_chunk(B, (size_t)C * HW * sizeof(float));
   for (int b0 = 0; b0 < B; b0 += ipc) {
     const int nb = (B - b0 < ipc) ? B - b0 : ipc;
     const long off = (long)b0 * C * HW;
     const long goff = (long)b0 * C * (H + W);
-    hipLaunchKernelGGL(ca_pool_kernel, dim3(nb * C), dim3(256), 0, st, x + off, H, W, yin + goff);
-    hipLaunchKernelGGL(ca_gate_kernel, dim3((H + W + 15) / 16, nb), dim3(256), 0, st, yin + goff, C, H, W, mip,
-                       conv1_w, conv1_b, bn_w, bn_b, bn_mean, bn_var, bn_eps, convh_w, convh_b, convw_w, convw_b,
+    hipLaunchKernelGGL(ca_pool_kernel, dim3(nb * C), dim3(256), pool_lds, st, x + off, H, W, RB, yin + goff);
+    hipLaunchKernelGGL(ca_gate_kernel, dim3((H + W + 15) / 16, nb), dim3(256), gate_lds, st, yin + goff, C, H, W,
+                       mip, conv1_w, conv1_b, bn_w, bn_b, bn_mean, bn_var, bn_eps, convh_w, convh_b, convw_w, convw_b,
                        gate + goff);
-    const long total = (long)nb * C * HW;
-    hipLaunchKernelGGL(ca_apply_kernel, dim3(grid_stride_blocks(((W & 3) == 0) ? total / 4 : total)), dim3(256), 0,
-                       st, x + off, y + off, gate + goff, H, W, total);
+    if (V == 4)
+      hipLaunchKernelGGL((ca_apply_kernel<4>), dim3(nb * C, apply_y), dim3(256), 0, st, x + off, y + off, gate + goff,
+                         H, W);
+    else
+      hipLaunchKernelGGL((ca_apply_kernel<1>), dim3(nb * C, apply_y), dim3(256), 0, st, x + off, y + off, gate + goff,
+                         H, W);
   }
   YS_CHECK_LAUNCH("ca");
   return 0;

@@ -318,6 +318,7 @@ static inline int launch_gemm(const GemmArgs& g, int batch, bool b_kc, hipStream
     }                                                                                                          \
   } while (0)
   if (narrow) YS_GEMM_LAUNCH(4, 1, 1, 2);
+  else if (g.M <= 64) YS_GEMM_LAUNCH(1, 4, 2, 2);  // 64 x 256 tiles (1x1 convs with few output channels)
   else YS_GEMM_LAUNCH(2, 2, 2, 2);
 #undef YS_GEMM_LAUNCH
   YS_CHECK_LAUNCH("gemm_f32");

@@ -399,6 +399,24 @@ YS_EXPORT int yolosod_gemm_f32(const float* A, long a_bs, int lda, const float* 
   return launch_gemm(g, batch, b_kcontig != 0, (hipStream_t)stream);
 }
 
+// 1x1 convolution (stride 1, no groups) on NCHW as a batched GEMM with the conv epilogue fused:
+// out[b*out_bs + m*HW + p] = act(sum_k W[m][k] x[b*x_bs + k*HW + p] + bias[m]) (+ res[b*res_bs + m*HW + p]).
+// out / res may be channel slices of larger concat buffers (batch strides > Cout*HW).
+YS_EXPORT int yolosod_conv1x1(const float* x, long x_bs, const float* w, const float* bias, float* out, long out_bs,
+                              const float* res, long res_bs, int B, int Cin, int Cout, long HW, int act,
+                              void* stream) {
+  YS_CHECK_ARG(x && w && out, "conv1x1: null pointer");
+  GemmArgs g{};
+  g.A = w; g.lda = Cin;
+  g.B = x; g.b_bs = x_bs; g.ldb = (int)HW;
+  g.M = Cout; g.N = (int)HW; g.K = Cin;
+  g.epi = epi_plain(out, out_bs, (int)HW);
+  g.epi.bias = bias; g.epi.bias_mode = bias ? 1 : 0;
+  g.epi.act = act;
+  g.epi.res = res; g.epi.res_bs = res_bs; g.epi.ldr = (int)HW;
+  return launch_gemm(g, B, false, (hipStream_t)stream);
+}
+
 YS_EXPORT int yolosod_layernorm(const float* x, float* y, long rows, int C, const float* w, const float* b, float eps,
                                 void* stream) {
   return launch_layernorm(x, y, rows, C, w, b, eps, (hipStream_t)stream);

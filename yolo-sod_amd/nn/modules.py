@@ -14,6 +14,7 @@ order in which they create parameters (hence seed-for-seed identical random init
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -52,12 +53,23 @@ def _act_code(act):
     return None
 
 
+# 1x1 convs as the library's fused fp32 MFMA GEMM instead of MIOpen (+ epilogue pass). Off by default: at the
+# bs=32 640x640 shapes MIOpen's 1x1 kernels were faster end to end (1526 vs 1356 images/s); kept for A/B work.
+CONV1X1_GEMM = os.environ.get("YOLOSOD_CONV1X1", "0") == "1"
+
+
 def conv_epilogue(conv: nn.Conv2d, act_code, x, out=None, res=None):
     """GPU fast path of ``act(conv(x)) (+ res)``: MIOpen conv without bias, then one HIP pass for bias +
     activation (+ shortcut), optionally written straight into a channel slice ``out`` of a concat buffer.
     Returns None when the fast path does not apply (CPU tensor, no bias, unsupported activation / shape)."""
     if x.device.type != "cuda" or conv.bias is None or act_code is None or x.dtype != torch.float32:
         return None
+    if (CONV1X1_GEMM and conv.kernel_size == (1, 1) and conv.stride == (1, 1) and conv.groups == 1 and conv.padding == (0, 0)
+            and conv.in_channels % 32 == 0 and x.stride(1) == x.shape[2] * x.shape[3] and x.stride(3) == 1
+            and x.stride(2) == x.shape[3] and (x.shape[2] * x.shape[3]) % 4 == 0 and x.stride(0) % 4 == 0):
+        # 1x1 conv = GEMM on NCHW with the epilogue fused (no MIOpen layout transposes, no extra pass)
+        return _hip.conv1x1(x, conv.weight.detach().reshape(conv.out_channels, -1), conv.bias.detach(), act_code,
+                            out=out, res=res)
     y = F.conv2d(x, conv.weight, None, conv.stride, conv.padding, conv.dilation, conv.groups)
     if (y.shape[2] * y.shape[3]) % 4:
         y = y + conv.bias.view(1, -1, 1, 1)
