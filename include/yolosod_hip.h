@@ -107,6 +107,10 @@ int yolosod_layernorm(const float* x, float* y, long rows, int C, const float* w
                       void* stream);
 int yolosod_attention(const float* qkv, float* out, long n_seq, int L, int C, int heads, void* stream);
 
+/* Test hook: 1 routes SwinBlock shapes the fused per-window kernel covers (C 64/128, heads 2/4, window <= 7x7,
+ * mlp 2C) through it (default, or env YOLOSOD_SWIN_FUSED), 0 forces the decomposed GEMM path for every shape. */
+void yolosod_debug_set_swin_fused(int on);
+
 #ifdef __cplusplus
 }
 #endif

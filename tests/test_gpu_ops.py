@@ -12,6 +12,7 @@ import torch
 import recipes
 from conftest import golden
 from oplib import build_fixture_module, tol_close
+from yolosod_amd import _hip
 from oracle import ops_ref as R
 from oracle.model_ref import OP_CLASSES
 
@@ -38,6 +39,26 @@ def test_op_matches_reference_fixture(name, cuda):
     assert ok, f"{name}: max abs err vs reference {err:.3g}"
     y64 = _oracle64(name, x)
     ok, err, ratio = tol_close(y, y64, 5e-5, 1e-4)
+    assert ok, f"{name}: vs fp64 oracle max abs err {err:.3g} (ratio {ratio:.2f})"
+
+
+@pytest.mark.parametrize("name", [n for n in recipes.OPS if n.startswith("swin_c64")])
+def test_swin_decomposed_path_matches_reference_fixture(name, cuda):
+    """The decomposed (row-stats + LN-staged GEMM + attention + GEMM) Swin path on the shapes the fused
+    per-window kernel normally takes, against the same reference fixtures."""
+    lib = _hip.load_library()
+    z = golden(f"ops_{name}")
+    m, _ = build_fixture_module(name)
+    x = torch.from_numpy(z["x"])
+    lib.yolosod_debug_set_swin_fused(0)
+    try:
+        with torch.inference_mode():
+            y = m.to(cuda)(x.to(cuda)).cpu()
+    finally:
+        lib.yolosod_debug_set_swin_fused(1)
+    ok, err, _ = tol_close(y, torch.from_numpy(z["y"]), ATOL, 0.0)
+    assert ok, f"{name}: max abs err vs reference {err:.3g}"
+    ok, err, ratio = tol_close(y, _oracle64(name, x), 5e-5, 1e-4)
     assert ok, f"{name}: vs fp64 oracle max abs err {err:.3g} (ratio {ratio:.2f})"
 
 

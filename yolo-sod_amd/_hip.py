@@ -49,6 +49,7 @@ SIGNATURES = {
     "yolosod_attention": (_i, [_vp, _vp, _l, _i, _i, _i, _vp]),
     "yolosod_bias_act": (_i, [_vp, _l, _vp, _l, _vp, _vp, _l, _i, _i, _l, _i, _vp]),
     "yolosod_conv1x1": (_i, [_vp, _l, _vp, _vp, _vp, _l, _vp, _l, _i, _i, _i, _l, _i, _vp]),
+    "yolosod_debug_set_swin_fused": (None, [_i]),
 }
 
 _LIB = None

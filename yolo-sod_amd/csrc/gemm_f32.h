@@ -2,8 +2,9 @@
 //
 //   out(b, m, n) = epilogue( sum_k A'(b, m, k) * B(b, k, n) )
 //   A(b,m,k) = A[b*a_bs + m*lda + k]       (K-contiguous)
-//   A'      = A, or LayerNorm_k(A) when ln_w != nullptr (row statistics over the full K computed in the block
-//             prologue, normalisation applied while staging the tile -> no separate LN pass over HBM)
+//   A'      = A, or LayerNorm_k(A) when ln_w != nullptr: per-row (mean, rstd) come precomputed from
+//             row_stats_kernel (one read of A); the normalisation is applied while staging the A tile, so the
+//             normalised activations never exist in HBM
 //   B_KC:  B(b,k,n) = B[b*b_bs + n*ldb + k]  (K-contiguous: nn.Linear / 1x1-conv weights, token-major acts)
 //   !B_KC: B(b,k,n) = B[b*b_bs + k*ldb + n]  (N-contiguous: NCHW activations)
 //
@@ -12,6 +13,9 @@
 // The MFMA's k index is permuted: lane half h takes k = h*16 + s (s = 0..15) of each 32-deep block, so the A and
 // K-contiguous B fragments are 16-byte ds_read_b128 along k from a [row][k] LDS image whose 36-float row stride
 // keeps each 16-lane read group conflict-free. The summation order differs from a plain k loop only by rounding.
+// Tile order is XCD-aware: workgroup i runs on XCD i % 8, so the tiles are dealt to XCDs in contiguous row-major
+// ranges and the N-tiles that share an A row-block hit the same XCD L2. The epilogue stages the accumulators
+// through LDS and stores whole rows with 16-byte coalesced stores (bias / BN / act / residual fused).
 #pragma once
 #include "common.h"
 
@@ -33,6 +37,7 @@ struct Epi {
   // window-reverse output (SwinBlock): n = global token, m = channel; out/res are NCHW [img][M][H][W]
   int swin;
   int sw_H, sw_W, sw_wh, sw_ww, sw_nWx, sw_nWin;
+  int vec;             // set by launch_gemm: 16-byte epilogue legal (alignment / strides)
 };
 
 struct GemmArgs {
@@ -43,11 +48,57 @@ struct GemmArgs {
   long b_bs;
   int ldb;
   int M, N, K;
-  const float* ln_w;  // optional LayerNorm of A rows
+  const float* ln_w;      // optional LayerNorm of A rows
   const float* ln_b;
-  float ln_eps;
+  const float* ln_stats;  // [M][2] = (mean, rstd) from row_stats_kernel, required with ln_w
+  int tiles_n, tiles;     // set by launch_gemm
   Epi epi;
 };
+
+// Per-row LayerNorm statistics (mean, 1/sqrt(var + eps)) of a K-contiguous [rows][K] matrix: one wave per row,
+// the row held in registers (K <= 1024), two passes (mean, then centred sum of squares) as torch does.
+template <int VPL>
+__global__ __launch_bounds__(256) void row_stats_kernel(const float* __restrict__ x, int ld, long rows, int K,
+                                                        float eps, float* __restrict__ stats) {
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const float4* xr = reinterpret_cast<const float4*>(x + row * ld);
+  const int K4 = K >> 2;
+  float4 v[VPL];
+  float s = 0.f;
+#pragma unroll
+  for (int u = 0; u < VPL; ++u) {
+    const int c = lane + 64 * u;
+    v[u] = (c < K4) ? xr[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+    s += (v[u].x + v[u].y) + (v[u].z + v[u].w);
+  }
+  const float mean = wave_sum(s) / (float)K;
+  float q = 0.f;
+#pragma unroll
+  for (int u = 0; u < VPL; ++u) {
+    if (lane + 64 * u < K4) {
+      const float a = v[u].x - mean, b = v[u].y - mean, c = v[u].z - mean, d = v[u].w - mean;
+      q += (a * a + b * b) + (c * c + d * d);
+    }
+  }
+  const float var = wave_sum(q) / (float)K;
+  if (lane == 0) {
+    stats[2 * row] = mean;
+    stats[2 * row + 1] = 1.0f / sqrtf(var + eps);
+  }
+}
+
+static inline int launch_row_stats(const float* x, int ld, long rows, int K, float eps, float* stats, hipStream_t st) {
+  YS_CHECK_ARG(K % 4 == 0 && K <= 1024 && ld % 4 == 0, "row_stats: K=%d ld=%d unsupported", K, ld);
+  if (rows == 0) return 0;
+  const dim3 grid((unsigned)((rows + 3) / 4));
+  if (K <= 256) hipLaunchKernelGGL((row_stats_kernel<1>), grid, dim3(256), 0, st, x, ld, rows, K, eps, stats);
+  else if (K <= 512) hipLaunchKernelGGL((row_stats_kernel<2>), grid, dim3(256), 0, st, x, ld, rows, K, eps, stats);
+  else hipLaunchKernelGGL((row_stats_kernel<4>), grid, dim3(256), 0, st, x, ld, rows, K, eps, stats);
+  YS_CHECK_LAUNCH("row_stats");
+  return 0;
+}
 
 __device__ __forceinline__ float apply_act(float v, int act) {
   if (act == 1) return siluf_(v);
@@ -75,76 +126,40 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
   constexpr int B_ELEMS = B_KC ? BN * SK : BK * SBN;
   constexpr int NA = BM * BK / 4 / 256;          // float4 per thread per A tile
   constexpr int NB = BN * BK / 4 / 256;
+  constexpr int SC = BN + 4;                     // epilogue staging row stride
+  constexpr int MAIN_ELEMS = 2 * A_ELEMS + 2 * B_ELEMS;
+  constexpr int SMEM = (MAIN_ELEMS > BM * SC ? MAIN_ELEMS : BM * SC) + (A_LN ? 2 * BM : 0);
   static_assert(WM * WN == 4, "4 waves");
-  __shared__ __attribute__((aligned(16))) float smem[2 * A_ELEMS + 2 * B_ELEMS + (A_LN ? 2 * BM : 0)];
+  __shared__ __attribute__((aligned(16))) float smem[SMEM];
   float* As = smem;
   float* Bs = smem + 2 * A_ELEMS;
-  float* s_mean = smem + 2 * A_ELEMS + 2 * B_ELEMS;
+  float* s_mean = smem + (SMEM - (A_LN ? 2 * BM : 0));
   float* s_rstd = s_mean + BM;
+
+  // XCD-aware tile order (gridDim.x = 8 * ceil(tiles / 8)); see header comment
+  const int tpx = (g.tiles + 7) >> 3;
+  const int t = (blockIdx.x & 7) * tpx + (blockIdx.x >> 3);
+  if (t >= g.tiles) return;
+  const int m0 = (t / g.tiles_n) * BM, n0 = (t % g.tiles_n) * BN;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
   const int bz = blockIdx.z;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
   const float* A = g.A + (long)bz * g.a_bs;
   const float* B = g.B + (long)bz * g.b_bs;
   const int M = g.M, N = g.N, K = g.K;
   const bool vec_b = (g.ldb & 3) == 0 && (g.b_bs & 3) == 0;
 
   if (A_LN) {
-    // Row statistics over the full K: TPR threads per row, each streaming a strided share of the row with
-    // 8 float4 loads in flight, two-pass (mean, M2) per chunk combined with Chan's formula, then across the
-    // row's threads with shuffles. Rows >= M get (0, 0).
-    constexpr int TPR = 256 / BM;  // 2 (BM=128)
-    const int r = tid / TPR, part = tid % TPR;
-    const int m = m0 + r;
-    float cnt = 0.f, mean = 0.f, m2 = 0.f;
-    if (m < M) {
-      const float4* ar = reinterpret_cast<const float4*>(A + (long)m * g.lda);
-      const int K4 = K >> 2;
-      for (int c0 = part * 8; c0 < K4; c0 += TPR * 8) {
-        float4 v[8];
-        int nv = 0;
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-          if (c0 + u < K4) { v[u] = ar[c0 + u]; nv = u + 1; }
-        float s = 0.f;
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-          if (u < nv) s += (v[u].x + v[u].y) + (v[u].z + v[u].w);
-        const float n_b = 4.0f * nv, mu_b = s / n_b;
-        float q = 0.f;
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-          if (u < nv) {
-            const float a0 = v[u].x - mu_b, a1 = v[u].y - mu_b, a2 = v[u].z - mu_b, a3 = v[u].w - mu_b;
-            q += (a0 * a0 + a1 * a1) + (a2 * a2 + a3 * a3);
-          }
-        const float n_ab = cnt + n_b, d = mu_b - mean;
-        mean += d * (n_b / n_ab);
-        m2 += q + d * d * (cnt * n_b / n_ab);
-        cnt = n_ab;
-      }
+    for (int r = tid; r < BM; r += 256) {
+      const int m = m0 + r;
+      const float2 st = (m < M) ? *reinterpret_cast<const float2*>(g.ln_stats + 2L * m) : make_float2(0.f, 0.f);
+      s_mean[r] = st.x;
+      s_rstd[r] = st.y;
     }
-#pragma unroll
-    for (int o = 1; o < TPR; o <<= 1) {
-      const float c2 = __shfl_xor(cnt, o, 64), mu2 = __shfl_xor(mean, o, 64), q2 = __shfl_xor(m2, o, 64);
-      const float n_ab = cnt + c2;
-      if (n_ab > 0.f) {
-        const float d = mu2 - mean;
-        mean += d * (c2 / n_ab);
-        m2 += q2 + d * d * (cnt * c2 / n_ab);
-      }
-      cnt = n_ab;
-    }
-    if (part == 0) {
-      s_mean[r] = mean;
-      s_rstd[r] = (m < M) ? 1.0f / sqrtf(m2 / (float)K + g.ln_eps) : 0.f;
-    }
-    __syncthreads();
   }
 
-  float4 ra[NA], rb[NB];
+  float4 ra[NA], rb[NB], lw, lb;
   auto load_tiles = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
@@ -152,6 +167,10 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
       const int r = idx >> 3, kq = (idx & 7) * 4;
       const int m = m0 + r;
       ra[i] = (m < M) ? *reinterpret_cast<const float4*>(A + (long)m * g.lda + k0 + kq) : make_float4(0, 0, 0, 0);
+    }
+    if (A_LN) {  // every A float4 of this thread sits at the same k offset (256 % 8 == 0)
+      lw = *reinterpret_cast<const float4*>(g.ln_w + k0 + (tid & 7) * 4);
+      lb = *reinterpret_cast<const float4*>(g.ln_b + k0 + (tid & 7) * 4);
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
@@ -175,7 +194,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
       }
     }
   };
-  auto store_tiles = [&](int buf, int k0) {
+  auto store_tiles = [&](int buf) {
     float* Ab = As + buf * A_ELEMS;
     float* Bb = Bs + buf * B_ELEMS;
 #pragma unroll
@@ -185,12 +204,10 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
       float4 v = ra[i];
       if (A_LN) {
         const float mu = s_mean[r], rs = s_rstd[r];
-        const float4 w = *reinterpret_cast<const float4*>(g.ln_w + k0 + kq);
-        const float4 b = *reinterpret_cast<const float4*>(g.ln_b + k0 + kq);
-        v.x = (v.x - mu) * rs * w.x + b.x;
-        v.y = (v.y - mu) * rs * w.y + b.y;
-        v.z = (v.z - mu) * rs * w.z + b.z;
-        v.w = (v.w - mu) * rs * w.w + b.w;
+        v.x = (v.x - mu) * rs * lw.x + lb.x;
+        v.y = (v.y - mu) * rs * lw.y + lb.y;
+        v.z = (v.z - mu) * rs * lw.z + lb.z;
+        v.w = (v.w - mu) * rs * lw.w + lb.w;
       }
       *reinterpret_cast<float4*>(&Ab[r * SK + kq]) = v;
     }
@@ -218,7 +235,8 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
   const int nk = K / BK;
   const int lr = lane & 31, lh = lane >> 5;
   load_tiles(0);
-  store_tiles(0, 0);
+  if (A_LN) __syncthreads();  // s_mean / s_rstd
+  store_tiles(0);
   __syncthreads();
   for (int kb = 0; kb < nk; ++kb) {
     const int buf = kb & 1;
@@ -226,18 +244,18 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
     const float* Ab = As + buf * A_ELEMS + (wm * MI * 32 + lr) * SK + lh * 16;
     const float* Bb = Bs + buf * B_ELEMS;
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
+    for (int t4 = 0; t4 < 4; ++t4) {
       float4 a[MI], b[NI];
 #pragma unroll
-      for (int i = 0; i < MI; ++i) a[i] = *reinterpret_cast<const float4*>(Ab + i * 32 * SK + 4 * t);
+      for (int i = 0; i < MI; ++i) a[i] = *reinterpret_cast<const float4*>(Ab + i * 32 * SK + 4 * t4);
       if (B_KC) {
 #pragma unroll
         for (int j = 0; j < NI; ++j)
-          b[j] = *reinterpret_cast<const float4*>(Bb + (wn * NI * 32 + j * 32 + lr) * SK + lh * 16 + 4 * t);
+          b[j] = *reinterpret_cast<const float4*>(Bb + (wn * NI * 32 + j * 32 + lr) * SK + lh * 16 + 4 * t4);
       } else {
 #pragma unroll
         for (int j = 0; j < NI; ++j) {
-          const float* col = Bb + (lh * 16 + 4 * t) * SBN + wn * NI * 32 + j * 32 + lr;
+          const float* col = Bb + (lh * 16 + 4 * t4) * SBN + wn * NI * 32 + j * 32 + lr;
           b[j] = make_float4(col[0], col[SBN], col[2 * SBN], col[3 * SBN]);
         }
       }
@@ -251,12 +269,46 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].w, b[j].w, acc[i][j], 0, 0, 0);
         }
     }
-    if (kb + 1 < nk) store_tiles(buf ^ 1, (kb + 1) * BK);
+    if (kb + 1 < nk) store_tiles(buf ^ 1);
     __syncthreads();
   }
 
-  // epilogue: C/D map of 32x32: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
   const Epi& e = g.epi;
+  if (e.vec) {
+    // stage C through LDS (the main-loop buffers are free after the last barrier), then 16-byte row stores.
+    // C/D map of 32x32: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+    float* Cs = smem;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          Cs[(wm * MI * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) * SC + wn * NI * 32 + j * 32 + lr] =
+              acc[i][j][r];
+    __syncthreads();
+    constexpr int NQ = BN / 4;
+    float* outb = e.out + (long)bz * e.out_bs;
+    const float* resb = e.res ? e.res + (long)bz * e.res_bs : nullptr;
+#pragma unroll 4
+    for (int idx = tid; idx < BM * NQ; idx += 256) {
+      const int row = idx / NQ, c4 = idx % NQ;
+      const int m = m0 + row, n = n0 + 4 * c4;
+      if (m >= M || n >= N) continue;
+      f32x4 v = *reinterpret_cast<const f32x4*>(&Cs[row * SC + 4 * c4]);
+      if (e.bias_mode == 1) v += e.bias[m];
+      else if (e.bias_mode == 2) v += *reinterpret_cast<const f32x4*>(e.bias + n);
+      if (e.bn_mode == 1) v = v * e.scale[m] + e.shift[m];
+      else if (e.bn_mode == 2)
+        v = v * *reinterpret_cast<const f32x4*>(e.scale + n) + *reinterpret_cast<const f32x4*>(e.shift + n);
+      v.x = apply_act(v.x, e.act); v.y = apply_act(v.y, e.act); v.z = apply_act(v.z, e.act); v.w = apply_act(v.w, e.act);
+      if (resb) v += *reinterpret_cast<const f32x4*>(resb + (long)m * e.ldr + n);
+      *reinterpret_cast<f32x4*>(outb + (long)m * e.ldc + n) = v;
+    }
+    return;
+  }
+
+  // scalar epilogue (window-reverse scatter of the Swin pw conv, or unaligned outputs)
 #pragma unroll
   for (int j = 0; j < NI; ++j) {
     const int n = n0 + wn * NI * 32 + j * 32 + lr;
@@ -294,21 +346,30 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
   }
 }
 
-static inline int launch_gemm(const GemmArgs& g, int batch, bool b_kc, hipStream_t st) {
+static inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+static inline int launch_gemm(const GemmArgs& g0, int batch, bool b_kc, hipStream_t st) {
+  GemmArgs g = g0;
   YS_CHECK_ARG(g.K % 32 == 0, "gemm: K=%d must be a multiple of 32", g.K);
   YS_CHECK_ARG(g.lda % 4 == 0 && (!b_kc || g.ldb % 4 == 0),
                "gemm: lda (and ldb of a K-contiguous B) must be multiples of 4");
-  YS_CHECK_ARG(((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.B & 15) == 0, "gemm: A/B must be 16-byte aligned");
-  YS_CHECK_ARG(!g.ln_w || (((uintptr_t)g.ln_w & 15) == 0 && ((uintptr_t)g.ln_b & 15) == 0),
-               "gemm: LN params must be 16-byte aligned");
+  YS_CHECK_ARG(al16(g.A) && al16(g.B), "gemm: A/B must be 16-byte aligned");
+  YS_CHECK_ARG(!g.ln_w || (al16(g.ln_w) && al16(g.ln_b) && g.ln_stats && ((uintptr_t)g.ln_stats & 7) == 0),
+               "gemm: LN params must be 16-byte aligned and come with row statistics");
   if (g.M == 0 || g.N == 0 || batch == 0) return 0;
+  const Epi& e = g.epi;
+  g.epi.vec = !e.swin && g.N % 4 == 0 && e.ldc % 4 == 0 && e.out_bs % 4 == 0 && al16(e.out) &&
+              (!e.res || (e.ldr % 4 == 0 && e.res_bs % 4 == 0 && al16(e.res))) &&
+              (e.bias_mode != 2 || al16(e.bias)) && (e.bn_mode != 2 || (al16(e.scale) && al16(e.shift)));
   const bool ln = g.ln_w != nullptr;
   // N tiles of 64 when N is not a multiple of 128 (e.g. 3C = 192) or small; 128 otherwise
   const bool narrow = (g.N % 128 != 0) && (g.N <= 256);
 #define YS_GEMM_LAUNCH(WM_, WN_, MI_, NI_)                                                                     \
   do {                                                                                                         \
     constexpr int bm = WM_ * MI_ * 32, bn = WN_ * NI_ * 32;                                                    \
-    dim3 grid((g.N + bn - 1) / bn, (g.M + bm - 1) / bm, batch);                                               \
+    g.tiles_n = (g.N + bn - 1) / bn;                                                                           \
+    g.tiles = g.tiles_n * ((g.M + bm - 1) / bm);                                                               \
+    dim3 grid((unsigned)(8 * ((g.tiles + 7) / 8)), 1, batch);                                                  \
     if (b_kc) {                                                                                                \
       if (ln) hipLaunchKernelGGL((gemm_f32_kernel<WM_, WN_, MI_, NI_, true, true>), grid, dim3(256), 0, st, g); \
       else hipLaunchKernelGGL((gemm_f32_kernel<WM_, WN_, MI_, NI_, true, false>), grid, dim3(256), 0, st, g);  \

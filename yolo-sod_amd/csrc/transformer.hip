@@ -368,13 +368,18 @@ int yolosod_swin_fused_launch(const float* x, float* y, int B, int C, int H, int
                               const float* mlp2_b, const float* pw_w, const float* bn_scale, const float* bn_shift,
                               hipStream_t st);
 
+static int g_swin_fused = -1;  // -1: from YOLOSOD_SWIN_FUSED (default on)
+
 static bool swin_fused_enabled() {
-  static int v = [] {
+  if (g_swin_fused < 0) {
     const char* e = getenv("YOLOSOD_SWIN_FUSED");
-    return e ? atoi(e) : 1;
-  }();
-  return v != 0;
+    g_swin_fused = e ? (atoi(e) != 0) : 1;
+  }
+  return g_swin_fused != 0;
 }
+
+// Test hook: route SwinBlock through the fused per-window kernel (1) or the decomposed GEMM path (0).
+YS_EXPORT void yolosod_debug_set_swin_fused(int on) { g_swin_fused = on ? 1 : 0; }
 
 // shapes the fused per-window kernel (swin_fused.hip) handles
 static bool swin_fused_ok(int C, int heads, int L, int mlp_hidden) {
@@ -434,6 +439,7 @@ YS_EXPORT size_t yolosod_swin_workspace(int B, int C, int H, int W, int window, 
   const int wide = (3 * C > mlp_hidden) ? 3 * C : mlp_hidden;
   s.take<float>((size_t)g.ntok * wide);  // QKV / MLP hidden
   s.take<float>((size_t)C * 2);          // folded BN
+  s.take<float>((size_t)g.ntok * 2);     // LayerNorm row statistics
   return s.off;
 }
 
@@ -494,7 +500,8 @@ YS_EXPORT int yolosod_swin_forward(const float* x, float* y, int B, int C, int H
   const int wide = (3 * C > mlp_hidden) ? 3 * C : mlp_hidden;
   float* Q = cv.take<float>((size_t)g.ntok * wide);
   float* bn_fold = cv.take<float>((size_t)C * 2);
-  YS_CHECK_ARG(bn_fold, "swin: workspace too small (%zu)", workspace_bytes);
+  float* lns = cv.take<float>((size_t)g.ntok * 2);
+  YS_CHECK_ARG(lns, "swin: workspace too small (%zu)", workspace_bytes);
   int rc;
 
   const size_t lds = (size_t)64 * (g.wh + 2) * (g.ww + 2) * sizeof(float);
@@ -503,9 +510,10 @@ YS_EXPORT int yolosod_swin_forward(const float* x, float* y, int B, int C, int H
                      dw_w, T, C, H, W, g.wh, g.ww, g.nWx, g.nWin);
   YS_CHECK_LAUNCH("swin_partition");
   GemmArgs ga{};
-  // QKV = LN1(T) Win^T + b_in   (LN fused into the A staging)
+  // QKV = LN1(T) Win^T + b_in   (LN applied while staging the A tiles)
+  if ((rc = launch_row_stats(T, C, g.ntok, C, ln1_eps, lns, st))) return rc;
   ga.A = T; ga.lda = C; ga.B = in_proj_w; ga.ldb = C; ga.M = (int)g.ntok; ga.N = 3 * C; ga.K = C;
-  ga.ln_w = ln1_w; ga.ln_b = ln1_b; ga.ln_eps = ln1_eps;
+  ga.ln_w = ln1_w; ga.ln_b = ln1_b; ga.ln_stats = lns;
   ga.epi = epi_plain(Q, 0, 3 * C);
   ga.epi.bias = in_proj_b; ga.epi.bias_mode = 2;
   if ((rc = launch_gemm(ga, 1, true, st))) return rc;
@@ -518,8 +526,9 @@ YS_EXPORT int yolosod_swin_forward(const float* x, float* y, int B, int C, int H
   if ((rc = launch_gemm(ga, 1, true, st))) return rc;
   // Hd = GELU(LN2(T) W1^T + b1)
   ga = GemmArgs{};
+  if ((rc = launch_row_stats(T, C, g.ntok, C, ln2_eps, lns, st))) return rc;
   ga.A = T; ga.lda = C; ga.B = mlp1_w; ga.ldb = C; ga.M = (int)g.ntok; ga.N = mlp_hidden; ga.K = C;
-  ga.ln_w = ln2_w; ga.ln_b = ln2_b; ga.ln_eps = ln2_eps;
+  ga.ln_w = ln2_w; ga.ln_b = ln2_b; ga.ln_stats = lns;
   ga.epi = epi_plain(Q, 0, mlp_hidden);
   ga.epi.bias = mlp1_b; ga.epi.bias_mode = 2; ga.epi.act = 2;
   if ((rc = launch_gemm(ga, 1, true, st))) return rc;
@@ -553,6 +562,7 @@ YS_EXPORT size_t yolosod_a2_workspace(int B, int C, int H, int W, int num_areas)
   s.take<float>((size_t)ntok * C);       // U / O
   s.take<float>((size_t)ntok * 3 * C);   // QKV
   s.take<float>((size_t)ntok * C);       // Z
+  s.take<float>((size_t)ntok * 2);       // LayerNorm row statistics
   return s.off;
 }
 
@@ -577,7 +587,8 @@ YS_EXPORT int yolosod_a2_forward(const float* x, float* y, int B, int C, int H, 
   float* U = cv.take<float>((size_t)ntok * C);
   float* Q = cv.take<float>((size_t)ntok * 3 * C);
   float* Z = cv.take<float>((size_t)ntok * C);
-  YS_CHECK_ARG(Z, "a2: workspace too small (%zu)", workspace_bytes);
+  float* lns = cv.take<float>((size_t)ntok * 2);
+  YS_CHECK_ARG(lns, "a2: workspace too small (%zu)", workspace_bytes);
   int rc;
   // XP = SiLU(Wp x + bp)  (Conv with folded BN, a2_attn.py:39): M = Cout, N = HW, batched over images
   GemmArgs ga{};
@@ -588,8 +599,9 @@ YS_EXPORT int yolosod_a2_forward(const float* x, float* y, int B, int C, int H, 
   hipLaunchKernelGGL(a2_pool_tokens_kernel, dim3(B * A), dim3(256), 0, st, XP, S, C, H, W, A);
   YS_CHECK_LAUNCH("a2_pool");
   ga = GemmArgs{};
+  if ((rc = launch_row_stats(S, C, ntok, C, ln_eps, lns, st))) return rc;
   ga.A = S; ga.lda = C; ga.B = in_proj_w; ga.ldb = C; ga.M = (int)ntok; ga.N = 3 * C; ga.K = C;
-  ga.ln_w = ln_w; ga.ln_b = ln_b; ga.ln_eps = ln_eps;
+  ga.ln_w = ln_w; ga.ln_b = ln_b; ga.ln_stats = lns;
   ga.epi = epi_plain(Q, 0, 3 * C);
   ga.epi.bias = in_proj_b; ga.epi.bias_mode = 2;
   if ((rc = launch_gemm(ga, 1, true, st))) return rc;
