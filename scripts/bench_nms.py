@@ -1,0 +1,61 @@
+"""NMS at controlled candidate loads: at random init nothing clears conf 0.25, so the bench's NMS
+line is an empty workload. Here (B=32, 4+nc=14, A=34000) predictions get exactly N candidates per image above
+conf_thres, scattered over A, boxes drawn around `clusters` centres (heavy overlap, as trained heads produce).
+Predict mode (conf 0.25, single label, max_det 300) and val mode (conf 0.001, multi-label, max_det 300).
+GPU only; parity at these sizes is tests/test_gpu_nms.py::test_nms_full_size_vs_oracle."""
+import sys
+from pathlib import Path
+
+import torch
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+import yolosod_import  # noqa: E402,F401
+from yolosod_amd.utils.ops import non_max_suppression_padded  # noqa: E402
+
+
+def make_pred(B, A, nc, n_cand, clusters, conf, seed, dev, img=640.0):
+    g = torch.Generator(device=dev).manual_seed(seed)
+    k = torch.randint(0, clusters, (B, A), generator=g, device=dev)
+    cen = torch.rand(B, clusters, 4, generator=g, device=dev)
+    cx, cy = cen[..., 0] * img, cen[..., 1] * img
+    cw, ch = 8 + cen[..., 2] * 112, 8 + cen[..., 3] * 112
+    jit = torch.randn(4, B, A, generator=g, device=dev) * 0.08
+    gat = lambda t: torch.gather(t, 1, k)  # noqa: E731
+    w, h = gat(cw), gat(ch)
+    box = torch.stack([gat(cx) + jit[0] * w, gat(cy) + jit[1] * h, w * jit[2].exp(), h * jit[3].exp()], 1)
+    # background scores below conf; n_cand anchors per image get a main-class score in (conf, 1)
+    cls = torch.rand(B, nc, A, generator=g, device=dev) * conf * 0.9
+    sel = torch.rand(B, A, generator=g, device=dev).argsort(1)[:, :n_cand]
+    main = torch.randint(0, nc, (B, n_cand), generator=g, device=dev)
+    val = conf + (1 - conf) * torch.rand(B, n_cand, generator=g, device=dev)
+    cls[torch.arange(B, device=dev)[:, None], main, sel] = val
+    return torch.cat([box, cls], 1).contiguous()
+
+
+def main():
+    dev = torch.device("cuda")
+    B, A, nc = 32, 34000, 10
+    print(f"{'mode':8s} {'cand/img':>9s} {'clusters':>8s} {'ms/call':>8s} {'kept/img':>9s}")
+    for mode, conf, kw in (("predict", 0.25, {}), ("val", 0.001, dict(multi_label=True))):
+        for n_cand in (1000, 10000, 30000):
+            for clusters in (50, 1000):
+                pred = make_pred(B, A, nc, n_cand, clusters, conf, 0, dev)
+                work = [pred.clone() for _ in range(13)]  # in-place xywh->xyxy rewrite: fresh copy per call
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                for i in range(3):
+                    non_max_suppression_padded(work[i], conf_thres=conf, iou_thres=0.7, max_det=300, **kw)
+                e0.record()
+                for i in range(3, 13):
+                    _, counts, _ = non_max_suppression_padded(work[i], conf_thres=conf, iou_thres=0.7, max_det=300,
+                                                              **kw)
+                e1.record()
+                torch.cuda.synchronize()
+                ms = e0.elapsed_time(e1) / 10
+                print(f"{mode:8s} {n_cand:9d} {clusters:8d} {ms:8.3f} {counts.float().mean().item():9.1f}",
+                      flush=True)
+
+
+if __name__ == "__main__":
+    main()

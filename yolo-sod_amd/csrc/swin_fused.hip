@@ -217,7 +217,13 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
       }
     }
   };
-  const long gw = blockIdx.x;  // one window per workgroup
+  // one window per workgroup, XCD-aware: workgroup i runs on XCD i % 8, so each XCD gets a contiguous range of
+  // windows and neighbouring windows (which share 128-B lines of x and y: a window row is only 28 B wide) meet in
+  // the same L2 instead of each XCD fetching / partially writing back the same lines.
+  const long nwin_total = (long)p.B * p.nWin;
+  const long per_xcd = (nwin_total + 7) >> 3;
+  const long gw = (long)(blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+  if (gw >= nwin_total) return;
   load_halo(gw);
   const float* w_in = p.win;
   const float* w_o = p.wo;
@@ -583,7 +589,8 @@ int yolosod_swin_fused_launch(const float* x, float* y, int B, int C, int H, int
     g_stamp_n = need;
     a.stamps = g_stamps;
   }
-  dim3 grid((unsigned)((long)B * nWin));  // one window per workgroup; 3 resident per CU (LDS 53 KB, 168 VGPRs)
+  // one window per workgroup (XCD-aware order, padded to a multiple of 8); 3 resident per CU (LDS 53 KB, 168 VGPRs)
+  dim3 grid((unsigned)(8 * (((long)B * nWin + 7) / 8)));
   const bool w7 = (wh == 7 && ww == 7);
 #define YS_SWF(CC, NHH)                                                                                  \
   if (C == CC && num_heads == NHH) {                                                                     \

@@ -248,14 +248,17 @@ static int launch_attention(const float* qkv, float* out, long n_seq, int L, int
 // =================================================================================================
 // Swin: depthwise 3x3 (pad 1, no bias) + bottom/right zero pad + window partition -> token-major T[tok][C].
 // Token order (img, wy, wx, iy, ix) as window_partition's permute(0,2,4,3,5,1) (blocks_transformer.py:43-46).
-// grid = (nWin_total, ceil(C/64)); a 64-channel slab of the (wh+2)x(ww+2) halo patch is staged in LDS.
+// grid = (8*ceil(nWin_total/8), ceil(C/64)), windows dealt to XCDs in contiguous ranges (neighbouring windows
+// share cache lines of x); a 64-channel slab of the (wh+2)x(ww+2) halo patch is staged in LDS.
 // =================================================================================================
 __global__ __launch_bounds__(256) void swin_partition_kernel(const float* __restrict__ x, const float* __restrict__ dw,
                                                              float* __restrict__ T, int C, int H, int W, int wh,
-                                                             int ww, int nWx, int nWin) {
+                                                             int ww, int nWx, int nWin, long nwin_total) {
   extern __shared__ float patch[];  // [64][(wh+2)*(ww+2)]
   const int PH = wh + 2, PW = ww + 2, PP = PH * PW;
-  const long gw = blockIdx.x;
+  const long per_xcd = (nwin_total + 7) >> 3;
+  const long gw = (long)(blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+  if (gw >= nwin_total) return;
   const int img = (int)(gw / nWin), win = (int)(gw % nWin);
   const int wy = win / nWx, wx = win % nWx;
   const int c0 = blockIdx.y * 64;
@@ -506,8 +509,8 @@ YS_EXPORT int yolosod_swin_forward(const float* x, float* y, int B, int C, int H
 
   const size_t lds = (size_t)64 * (g.wh + 2) * (g.ww + 2) * sizeof(float);
   YS_CHECK_ARG(lds <= 64 * 1024, "swin: window %dx%d too large for the partition kernel", g.wh, g.ww);
-  hipLaunchKernelGGL(swin_partition_kernel, dim3((unsigned)((long)B * g.nWin), (C + 63) / 64), dim3(256), lds, st, x,
-                     dw_w, T, C, H, W, g.wh, g.ww, g.nWx, g.nWin);
+  hipLaunchKernelGGL(swin_partition_kernel, dim3((unsigned)(8 * (((long)B * g.nWin + 7) / 8)), (C + 63) / 64),
+                     dim3(256), lds, st, x, dw_w, T, C, H, W, g.wh, g.ww, g.nWx, g.nWin, (long)B * g.nWin);
   YS_CHECK_LAUNCH("swin_partition");
   GemmArgs ga{};
   // QKV = LN1(T) Win^T + b_in   (LN applied while staging the A tiles)
