@@ -78,6 +78,16 @@ int yolosod_swin_forward(const float* x, float* y, int B, int C, int H, int W, i
 int yolosod_detect_decode(int nl, const float* const* maps, const int* heights, const int* widths,
                           const float* strides, int B, int nc, int reg_max, float* y, void* stream);
 
+/* Detect head tail fused with the decode (head.py:45-48,70 + the decode above): the last 1x1 convs
+ * of the box tower (box_w [64][c2], box_b [64]) and class tower (cls_w [nc][c3], cls_b [nc]) applied to the tower
+ * features box_feat[i] [B][c2][H_i][W_i], cls_feat[i] [B][c3][H_i][W_i] (fp32 NCHW, contiguous), then DFL /
+ * dist2bbox / sigmoid -> y [B][4+nc][A]; the [B][64+nc][H][W] raw maps are never materialised.
+ * Supports reg_max 16, c2 64, c3 64 or 128, nc <= 16. */
+int yolosod_detect_head(int nl, const float* const* box_feat, const float* const* cls_feat, int c2, int c3,
+                        const float* const* box_w, const float* const* box_b, const float* const* cls_w,
+                        const float* const* cls_b, const int* heights, const int* widths, const float* strides, int B,
+                        int nc, int reg_max, float* y, void* stream);
+
 /* non_max_suppression + torchvision.ops.nms   ultralytics/utils/ops.py:167-316 (nms call :296).
  * pred: [B, 4+nc, A] xywh (rewritten to xyxy in place when in_place); classes: device int32[n_classes] or NULL;
  * out: [B, max_det, 6] rows (x1,y1,x2,y2,conf,cls) in kept order, zero padded; counts: [B];

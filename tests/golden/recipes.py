@@ -125,3 +125,36 @@ NMS_CASES = {
     "nms_ties": (16, 2, 1500, 10, dict(conf_thres=0.25, iou_thres=0.7, tie=True)),
     "nms_iou0": (17, 1, 800, 4, dict(conf_thres=0.3, iou_thres=0.0)),
 }
+
+
+def synthetic_eval_set(seed: int, n_img: int = 24, nc: int = 6, img: float = 640.0):
+    """Synthetic ground truth + detections for the mAP harness: per image 0-14 labelled xyxy boxes; each label is
+    detected with prob 0.85 (jittered box, IoU spread over ~0.3-0.99, wrong class 10 %), plus 0-6 false positives,
+    confidences in (0.001, 1). Image 0 has labels but no detections, image 1 detections but no labels, image 2
+    neither. Returns (gt: list of (cls [m], boxes [m, 4]) float32, preds: list of [n, 6] float32)."""
+    rng = np.random.default_rng(seed)
+    gt, preds = [], []
+    for i in range(n_img):
+        m = 0 if i in (1, 2) else int(rng.integers(1, 15))
+        c = rng.integers(0, nc, m).astype(np.float32)
+        xy = rng.uniform(0, img - 40, (m, 2))
+        wh = rng.uniform(8, 160, (m, 2))
+        boxes = np.concatenate([xy, np.minimum(xy + wh, img)], 1).astype(np.float32)
+        rows = []
+        if i not in (0, 2):
+            for j in range(m):
+                if rng.uniform() < 0.85:
+                    w, h = boxes[j, 2] - boxes[j, 0], boxes[j, 3] - boxes[j, 1]
+                    s = rng.uniform(0.0, 0.25)
+                    jit = rng.normal(0, s, 4) * np.array([w, h, w, h])
+                    b = boxes[j] + jit
+                    b = np.array([min(b[0], b[2] - 1), min(b[1], b[3] - 1), max(b[2], b[0] + 1), max(b[3], b[1] + 1)])
+                    cls = c[j] if rng.uniform() > 0.1 else float(rng.integers(0, nc))
+                    rows.append([*b, rng.uniform(0.001, 1.0), cls])
+            for _ in range(int(rng.integers(0, 7))):
+                xy0 = rng.uniform(0, img - 40, 2)
+                wh0 = rng.uniform(8, 160, 2)
+                rows.append([*xy0, *(xy0 + wh0), rng.uniform(0.001, 1.0), float(rng.integers(0, nc))])
+        gt.append((c, boxes))
+        preds.append(np.array(rows, np.float32).reshape(-1, 6))
+    return gt, preds

@@ -53,3 +53,21 @@ def test_predictor_bs32_batch_invariance(gpu_model, cuda):
     out, counts, index = pred.predict_padded(x)
     assert out.shape == (32, 300, 6) and counts.shape == (32,)
     assert int(counts.min()) >= 0 and int(counts.max()) <= 300
+
+
+def test_fused_head_equals_raw_map_path(gpu_model, cuda):
+    """Detect on GPU: the fused head tail + decode kernel vs the reference-shaped path that materialises the raw
+    [B, 64+nc, H, W] maps (MIOpen 1x1 convs + HIP bias epilogue + HIP decode)."""
+    from yolosod_amd.nn.modules import Detect
+    g = torch.Generator().manual_seed(3)
+    x = torch.rand(2, 3, 640, 640, generator=g).to(cuda)
+    with torch.inference_mode():
+        y_fused = gpu_model(x)[0]
+        Detect.keep_raw = True
+        try:
+            y_raw, raw = gpu_model(x)
+        finally:
+            Detect.keep_raw = False
+    assert raw[0].shape == (2, 74, 160, 160)
+    ok, err, _ = tol_close(y_fused.cpu(), y_raw.cpu(), 1e-4, 1e-5)
+    assert ok, f"max abs err {err:.3g}"

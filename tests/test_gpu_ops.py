@@ -206,3 +206,27 @@ def test_bias_act_slice(cuda):
     ref = torch.nn.functional.silu(y.double() + b.double().view(1, -1, 1, 1)) + r.double()
     ok, err, _ = tol_close(out.cpu(), ref, 1e-5, 1e-6)
     assert ok, err
+
+
+@pytest.mark.parametrize("c3,img", [(64, 256), (128, 192), (64, 200)])
+def test_detect_head_fused_vs_oracle(c3, img, cuda):
+    """Fused last 1x1 convs + decode vs the fp64 oracle (1x1 convs then decode_ref, head.py:70,100-131)."""
+    g = torch.Generator().manual_seed(c3 + img)
+    strides, nc, B = [4.0, 8.0, 16.0, 32.0], 10, 2
+    fb, fc, wb, bb, wc, bc, maps = [], [], [], [], [], [], []
+    for s in strides:
+        h = w = int(img // s)
+        fb.append(torch.randn(B, 64, h, w, generator=g))
+        fc.append(torch.randn(B, c3, h, w, generator=g))
+        wb.append(torch.randn(64, 64, generator=g) * 0.25)
+        bb.append(torch.randn(64, generator=g))
+        wc.append(torch.randn(nc, c3, generator=g) * 0.2)
+        bc.append(torch.randn(nc, generator=g) - 2.0)
+        box = torch.einsum("ok,bkhw->bohw", wb[-1].double(), fb[-1].double()) + bb[-1].double().view(1, -1, 1, 1)
+        cls = torch.einsum("ok,bkhw->bohw", wc[-1].double(), fc[-1].double()) + bc[-1].double().view(1, -1, 1, 1)
+        maps.append(torch.cat([box, cls], 1))
+    ref = R.decode_ref(maps, strides, nc)
+    d = lambda ts: [t.to(cuda) for t in ts]  # noqa: E731
+    y = _hip.detect_head(d(fb), d(fc), d(wb), d(bb), d(wc), d(bc), strides, nc).cpu()
+    ok, err, _ = tol_close(y, ref, 5e-4, 1e-5)
+    assert ok, f"max abs err {err:.3g}"

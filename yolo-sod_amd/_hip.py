@@ -42,6 +42,7 @@ SIGNATURES = {
     "yolosod_swin_forward": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp, _vp, _vp,
                                   _f, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f, _vp, _sz, _vp]),
     "yolosod_detect_decode": (_i, [_i, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp]),
+    "yolosod_detect_head": (_i, [_i, _vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp]),
     "yolosod_nms_workspace": (_sz, [_i, _i, _i, _i]),
     "yolosod_nms": (_i, [_vp, _i, _i, _i, _f, _d, _vp, _i, _i, _i, _i, _i, _f, _i, _vp, _vp, _vp, _vp, _sz, _vp]),
     "yolosod_gemm_f32": (_i, [_vp, _l, _i, _vp, _l, _i, _i, _vp, _l, _i, _i, _i, _i, _i, _vp, _i, _i, _vp, _vp]),
@@ -261,6 +262,38 @@ def detect_decode(maps, strides, nc, reg_max=16):
     _check(_launch(("decode", (B, A), nc), lib.yolosod_detect_decode, nl, ctypes.cast(ptrs, ctypes.c_void_p), ctypes.cast(hs, ctypes.c_void_p),
                                      ctypes.cast(wsz, ctypes.c_void_p), ctypes.cast(st, ctypes.c_void_p), B, nc,
                                      reg_max, _dev(y, "y"), _stream()), "detect_decode")
+    return y
+
+
+def detect_head(box_feats, cls_feats, box_w, box_b, cls_w, cls_b, strides, nc, reg_max=16):
+    """Fused last 1x1 convs of both Detect towers + decode. box_feats[i] [B, c2, Hi, Wi], cls_feats[i]
+    [B, c3, Hi, Wi] contiguous fp32; box_w[i] [64, c2], cls_w[i] [nc, c3] -> y [B, 4+nc, A]."""
+    lib = load_library()
+    nl = len(box_feats)
+    B, c2 = box_feats[0].shape[:2]
+    c3 = cls_feats[0].shape[1]
+    for i in range(nl):
+        fb, fc = box_feats[i], cls_feats[i]
+        if (fb.shape[0] != B or fb.shape[1] != c2 or fc.shape[1] != c3 or fb.shape[2:] != fc.shape[2:]
+                or not fb.is_contiguous() or not fc.is_contiguous()):
+            raise RuntimeError(f"detect_head: level {i} features {tuple(fb.shape)} / {tuple(fc.shape)} mismatch")
+        if tuple(box_w[i].shape) != (4 * reg_max, c2) or tuple(cls_w[i].shape) != (nc, c3):
+            raise RuntimeError(f"detect_head: level {i} weights {tuple(box_w[i].shape)} / {tuple(cls_w[i].shape)}")
+    A = sum(t.shape[2] * t.shape[3] for t in box_feats)
+    y = torch.empty((B, 4 + nc, A), dtype=torch.float32, device=box_feats[0].device)
+
+    def arr(ts, what):
+        return ctypes.cast((ctypes.c_void_p * nl)(*[_dev(t, f"{what}[{i}]") for i, t in enumerate(ts)]),
+                           ctypes.c_void_p)
+
+    hs = (ctypes.c_int * nl)(*[t.shape[2] for t in box_feats])
+    wsz = (ctypes.c_int * nl)(*[t.shape[3] for t in box_feats])
+    st = (ctypes.c_float * nl)(*[float(s) for s in strides])
+    _check(_launch(("head", (B, A), (nc, c2, c3)), lib.yolosod_detect_head, nl, arr(box_feats, "box_feats"),
+                   arr(cls_feats, "cls_feats"), c2, c3, arr(box_w, "box_w"), arr(box_b, "box_b"),
+                   arr(cls_w, "cls_w"), arr(cls_b, "cls_b"), ctypes.cast(hs, ctypes.c_void_p),
+                   ctypes.cast(wsz, ctypes.c_void_p), ctypes.cast(st, ctypes.c_void_p), B, nc, reg_max,
+                   _dev(y, "y"), _stream()), "detect_head")
     return y
 
 

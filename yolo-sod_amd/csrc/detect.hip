@@ -85,6 +85,128 @@ __global__ __launch_bounds__(256) void detect_decode_kernel(DecodeArgs d) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// Fused head tail + decode: the last 1x1 convs of both towers (cv2[i][-1]: c2 -> 64 box
+// logits, cv3[i][-1]: c3 -> nc class logits, head.py:45-48,70) run as fp32 MFMA v_mfma_f32_16x16x4_f32 straight
+// into the DFL / dist2bbox / sigmoid decode, so the [B, 64+nc, H, W] raw maps never exist in HBM.
+//   A = conv weights [out][k] (held in registers for the wave's lifetime), B = tower features [k][pixel] (NCHW,
+//   loaded straight from HBM), D[out][pixel]: lane (g = lane>>4, j = lane&15) holds outputs 4g..4g+3 of pixel j.
+//   Box tile s (16 rows) is exactly side s's 16 DFL bins, so the softmax max / sum / expectation are 4 local
+//   values plus two permlane swaps (xor16, xor32). Class tile: rows 0..15 (nc <= 16).
+// Each wave owns NTS consecutive 16-pixel groups of one level of one image.
+// ------------------------------------------------------------------------------------------------
+struct HeadArgs {
+  const float* fb[4];  // box tower features  [B][C2][HW]
+  const float* fc[4];  // class tower features [B][C3][HW]
+  const float* wb[4];  // [64][C2]
+  const float* bb[4];  // [64]
+  const float* wc[4];  // [nc][C3]
+  const float* bc[4];  // [nc]
+  int hw[4], w[4], a_off[4], blk_off[5];
+  float stride[4];
+  int nl, nc, A;
+  float* y;
+};
+
+template <int C2, int C3, int NTS>
+__global__ __launch_bounds__(256) void detect_head_kernel(HeadArgs d) {
+  const int b = blockIdx.y;
+  int l = 0;
+#pragma unroll
+  for (int i = 1; i < 4; ++i)
+    if (i < d.nl && (int)blockIdx.x >= d.blk_off[i]) l = i;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int g = lane >> 4, j = lane & 15;
+  const int HW = d.hw[l];
+  const int px0 = (((int)blockIdx.x - d.blk_off[l]) * 4 + wv) * (NTS * 16);
+  if (px0 >= HW) return;  // whole wave; the kernel has no workgroup barrier
+  const int nc = d.nc;
+
+  // A operands: W[row = 16t + j][k = 4q + g]; biases of the rows this lane's accumulators hold (4g + r)
+  float wbr[4][C2 / 4], wcr[C3 / 4], bbr[4][4], bcr[4];
+  {
+    const float* wb = d.wb[l];
+    const float* wc = d.wc[l];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int q = 0; q < C2 / 4; ++q) wbr[t][q] = wb[(16 * t + j) * C2 + 4 * q + g];
+#pragma unroll
+    for (int q = 0; q < C3 / 4; ++q) wcr[q] = (j < nc) ? wc[j * C3 + 4 * q + g] : 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bbr[t][r] = d.bb[l][16 * t + 4 * g + r];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bcr[r] = (4 * g + r < nc) ? d.bc[l][4 * g + r] : 0.f;
+  }
+  const float* fbb = d.fb[l] + (long)b * C2 * HW;
+  const float* fcb = d.fc[l] + (long)b * C3 * HW;
+  const int W = d.w[l];
+  const float st = d.stride[l];
+  float* yb = d.y + (long)b * (4 + nc) * d.A + d.a_off[l];
+
+  for (int ts = 0; ts < NTS; ++ts) {
+    const int p0 = px0 + ts * 16;
+    if (p0 >= HW) break;
+    const int p = p0 + j;
+    const bool ok = p < HW;
+    float xb[C2 / 4], xc[C3 / 4];
+#pragma unroll
+    for (int q = 0; q < C2 / 4; ++q) xb[q] = ok ? fbb[(long)(4 * q + g) * HW + p] : 0.f;
+#pragma unroll
+    for (int q = 0; q < C3 / 4; ++q) xc[q] = ok ? fcb[(long)(4 * q + g) * HW + p] : 0.f;
+    f32x4 acc[5];
+#pragma unroll
+    for (int t = 0; t < 5; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < C2 / 4; ++q)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wbr[t][q], xb[q], acc[t], 0, 0, 0);
+#pragma unroll
+    for (int q = 0; q < C3 / 4; ++q) acc[4] = __builtin_amdgcn_mfma_f32_16x16x4f32(wcr[q], xc[q], acc[4], 0, 0, 0);
+
+    // DFL (block.py:79-82): softmax over the 16 bins of each side, expectation with weights 0..15
+    float dist[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = acc[s][r] + bbr[s][r];
+      float mx = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
+      mx = xor32_max(xor16_max(mx));
+      float sum = 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[r] = expf(v[r] - mx);
+        sum += v[r];
+      }
+      sum = xor32_sum(xor16_sum(sum));
+      const float inv = 1.0f / sum;
+      float e = 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) e += (float)(4 * g + r) * (v[r] * inv);
+      dist[s] = xor32_sum(xor16_sum(e));
+    }
+    if (!ok) continue;
+    const int iy = p / W, ix = p - iy * W;
+    const float ax = (float)ix + 0.5f, ay = (float)iy + 0.5f;
+    const float x1 = ax - dist[0], y1 = ay - dist[1];
+    const float x2 = ax + dist[2], y2 = ay + dist[3];
+    // dist2bbox xywh (tal.py:348-357) * stride; lane group g writes component g
+    const float out = g == 0 ? ((x1 + x2) / 2.0f) * st
+                    : g == 1 ? ((y1 + y2) / 2.0f) * st
+                    : g == 2 ? (x2 - x1) * st
+                             : (y2 - y1) * st;
+    yb[(long)g * d.A + p] = out;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int c = 4 * g + r;
+      if (c < nc) yb[(long)(4 + c) * d.A + p] = sigmoidf_(acc[4][r] + bcr[r]);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // NMS
 // ------------------------------------------------------------------------------------------------
 struct NmsArgs {
@@ -421,6 +543,51 @@ YS_EXPORT int yolosod_detect_decode(int nl, const float* const* maps, const int*
   if (B == 0 || off == 0) return 0;
   hipLaunchKernelGGL(detect_decode_kernel, dim3((off + 255) / 256, B), dim3(256), 0, (hipStream_t)stream, d);
   YS_CHECK_LAUNCH("detect_decode");
+  return 0;
+}
+
+YS_EXPORT int yolosod_detect_head(int nl, const float* const* box_feat, const float* const* cls_feat, int c2, int c3,
+                                  const float* const* box_w, const float* const* box_b, const float* const* cls_w,
+                                  const float* const* cls_b, const int* heights, const int* widths,
+                                  const float* strides, int B, int nc, int reg_max, float* y, void* stream) {
+  YS_CHECK_ARG(nl >= 1 && nl <= 4, "detect_head: nl=%d unsupported (1..4)", nl);
+  YS_CHECK_ARG(box_feat && cls_feat && box_w && box_b && cls_w && cls_b && heights && widths && strides && y,
+               "detect_head: null pointer");
+  YS_CHECK_ARG(reg_max == 16, "detect_head: reg_max=%d unsupported (16)", reg_max);
+  YS_CHECK_ARG(nc >= 1 && nc <= 16, "detect_head: nc=%d unsupported (1..16)", nc);
+  YS_CHECK_ARG(c2 == 64 && (c3 == 64 || c3 == 128), "detect_head: (c2=%d, c3=%d) unsupported ((64, 64|128))", c2, c3);
+  HeadArgs d{};
+  d.nl = nl;
+  d.nc = nc;
+  constexpr int NTS = 8;  // 16-pixel groups per wave -> 512 pixels per workgroup
+  int off = 0, blk = 0;
+  for (int i = 0; i < nl; ++i) {
+    YS_CHECK_ARG(box_feat[i] && cls_feat[i] && box_w[i] && box_b[i] && cls_w[i] && cls_b[i],
+                 "detect_head: null pointer at level %d", i);
+    d.fb[i] = box_feat[i];
+    d.fc[i] = cls_feat[i];
+    d.wb[i] = box_w[i];
+    d.bb[i] = box_b[i];
+    d.wc[i] = cls_w[i];
+    d.bc[i] = cls_b[i];
+    d.hw[i] = heights[i] * widths[i];
+    d.w[i] = widths[i];
+    d.stride[i] = strides[i];
+    d.a_off[i] = off;
+    d.blk_off[i] = blk;
+    off += d.hw[i];
+    blk += (d.hw[i] + 4 * NTS * 16 - 1) / (4 * NTS * 16);
+  }
+  d.blk_off[nl] = blk;
+  d.A = off;
+  d.y = y;
+  if (B == 0 || off == 0) return 0;
+  const dim3 grid(blk, B);
+  if (c3 == 64)
+    hipLaunchKernelGGL((detect_head_kernel<64, 64, NTS>), grid, dim3(256), 0, (hipStream_t)stream, d);
+  else
+    hipLaunchKernelGGL((detect_head_kernel<64, 128, NTS>), grid, dim3(256), 0, (hipStream_t)stream, d);
+  YS_CHECK_LAUNCH("detect_head");
   return 0;
 }
 

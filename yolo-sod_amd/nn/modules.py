@@ -437,13 +437,40 @@ class Detect(nn.Module):
                 for x in ch))
         self.dfl = DFL(self.reg_max) if self.reg_max > 1 else nn.Identity()
 
+    # Return the raw [B, 64+nc, Hi, Wi] maps as the reference does (forward's second output, head.py:70-74). When
+    # False (default), GPU inference runs the fused head tail + decode (one HIP kernel, no raw maps in HBM) and the
+    # second output is the list of tower features instead; predictors and NMS only read the first output.
+    keep_raw = False
+
     def forward(self, x):
+        if self._fused_ok(x):
+            return self._fused_forward(x)
         for i in range(self.nl):
             x[i] = self._tower(i, x[i])
         if self.training:
             return x
         y = self._inference(x)
         return y if self.export else (y, x)
+
+    def _fused_ok(self, x):
+        if self.training or self.keep_raw or self.export or x[0].device.type != "cuda":
+            return False
+        b2, b3 = self.cv2[0][-1], self.cv3[0][-1]
+        return (self.reg_max == 16 and 1 <= self.nc <= 16 and b2.in_channels == 64 and b3.in_channels in (64, 128)
+                and b2.bias is not None and b3.bias is not None and x[0].dtype == torch.float32)
+
+    def _fused_forward(self, x):
+        """cv2[i][:-1] / cv3[i][:-1] towers (PyTorch-ROCm convs + HIP epilogues), then the last 1x1 convs of both
+        towers fused with DFL / dist2bbox / sigmoid in one HIP kernel (head.py:70 + _inference :100-131)."""
+        fb, fc = [], []
+        for i in range(self.nl):
+            fb.append(self.cv2[i][:-1](x[i]).contiguous())
+            fc.append(self.cv3[i][:-1](x[i]).contiguous())
+        w = lambda c: c.weight.detach().reshape(c.out_channels, -1)  # noqa: E731
+        y = _hip.detect_head(fb, fc, [w(b[-1]) for b in self.cv2], [b[-1].bias.detach() for b in self.cv2],
+                             [w(b[-1]) for b in self.cv3], [b[-1].bias.detach() for b in self.cv3],
+                             [float(s) for s in self.stride], self.nc, self.reg_max)
+        return y, fb + fc
 
     def _tower(self, i, xi):
         """torch.cat((cv2[i](x), cv3[i](x)), 1) (head.py:70); on GPU the two final 1x1 convs write their slices of

@@ -54,6 +54,11 @@ def op_cost(key):
         B, A = shape
         nc = extra
         return B * A * ((64 + nc) + (4 + nc)) * F32, B * A * (64 * 4 + nc * 4)
+    if op == "head":  # fused last 1x1 convs of both towers + decode: reads the tower features, writes y
+        B, A = shape
+        nc, c2, c3 = extra
+        return (B * A * ((c2 + c3) + (4 + nc)) * F32 + (64 * c2 + nc * c3 + 64 + nc) * F32,
+                B * A * (2 * (64 * c2 + nc * c3) + 64 * 4 + nc * 4))
     if op == "nms":
         B, nc, A = shape
         return B * A * (4 + nc) * F32, 0
