@@ -57,3 +57,22 @@ def test_nms_full_size_vs_oracle(B, A, clusters, kw, cuda):
     for b in range(B):
         assert np.array_equal(out[b, :counts[b]], rows[b]), b
         assert np.array_equal(index[b, :counts[b]], idx[b]), b
+
+
+@pytest.mark.parametrize("B,A,clusters,kw", [
+    (2, 34000, 200, dict(conf_thres=0.25, iou_thres=0.7)),
+    (2, 34000, 3000, dict(conf_thres=0.05, iou_thres=0.45, max_det=1000)),
+    (1, 34000, 30, dict(conf_thres=0.001, iou_thres=0.7, multi_label=True, max_nms=5000)),
+])
+def test_nms_full_size_ties_vs_oracle(B, A, clusters, kw, cuda):
+    """Scores quantised to 1/16: huge tie groups straddle the prefix threshold of the top-KCAP selection and the
+    remainder path; stable (index) order among equal scores must match the reference."""
+    pred = recipes.synthetic_predictions(2000 + B + clusters, B, A, 10, n_clusters=clusters, tie_scores=True)
+    p_after, out, counts, index = _run_gpu(pred, cuda, **kw)
+    ref = pred.copy()
+    rows, idx = non_max_suppression_ref(ref, **kw)
+    assert np.array_equal(p_after, ref)
+    assert counts.tolist() == [len(r) for r in rows]
+    for b in range(B):
+        assert np.array_equal(out[b, :counts[b]], rows[b]), b
+        assert np.array_equal(index[b, :counts[b]], idx[b]), b

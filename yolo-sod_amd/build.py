@@ -18,7 +18,7 @@ INCLUDE = PKG.parent / "include"
 ARCH = os.environ.get("YOLOSOD_ARCH", "gfx950")
 
 # per-file extra flags: the decode / NMS arithmetic must not be contracted into FMAs (bit-exact NMS indices)
-EXTRA = {"detect.hip": ["-ffp-contract=off"]}
+EXTRA = {"detect.hip": ["-ffp-contract=off"], "nms.hip": ["-ffp-contract=off"]}
 COMMON = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-variable",
           "-Wno-unused-function", f"-I{INCLUDE}", f"-I{CSRC}"]
 

@@ -1,0 +1,830 @@
+// Class-wise greedy NMS on gfx950, bit-exact with the reference (compile with -ffp-contract=off).
+//
+// Reference semantics: non_max_suppression ultralytics/utils/ops.py:167-316 (xywh2xyxy :416-434) around
+// torchvision==0.20.1 ops.nms (CPU kernel: stable descending score sort, strict IoU > thr, area without +1);
+// classes are separated by offsetting boxes with cls * max_wh (ops.py:289,295).
+//
+// Design (no host sync; the per-image candidate count lives on the device):
+//   nms_prep    one thread per anchor: xywh -> xyxy (optionally in place, as the reference mutates its input),
+//               candidate class mask (score > conf, class filter, best class or multi-label).
+//   nms_count / nms_scan / nms_scatter  order-preserving compaction of the (anchor, class) candidates (= the
+//               reference's row order) over the whole GPU: per-256-anchor counts, per-image offsets, scatter of
+//               (~score bits, anchor*nc+class).
+//   nms_select  one 512-thread workgroup per image: the score order of the first <= KCAP candidates, sorted in
+//               LDS. For n <= KCAP a stable LSD radix sort of all; for n > KCAP a radix *select* first finds the
+//               key T such that the keys below T (at most KCAP of them) are exactly a prefix of the stable sorted
+//               order, and only that prefix is sorted. Writes the prefix's class-offset boxes / areas / ids.
+//   nms_mask    1024 workgroups (row block x image): the upper-triangular IoU > thr bitmask of the prefix, one
+//               64-bit word per (row, 64-column block) - the quadratic work spread over every CU.
+//   nms_resolve one workgroup per image: greedy in score order over the bitmask, 64 rows staged in LDS at a time,
+//               only alive candidates visited (bit scan); stops at max_det. Only if the prefix is exhausted before
+//               max_det boxes are kept and more candidates exist (keys >= T) does it sort that remainder and
+//               continue with the chunked in-LDS greedy (each chunk of 512 tested against the kept boxes, then
+//               its own IoU bitmask). Kept rows are written in parallel.
+#include "common.h"
+#include <math.h>
+#include <stdlib.h>
+
+namespace ys {
+
+constexpr int NMS_T = 512;  // threads per image workgroup
+constexpr int NMS_W = NMS_T / 64;
+constexpr int NMS_MAXDET = 1024;
+constexpr int KCAP = 2048;  // candidates covered by the multi-CU IoU bitmask
+constexpr int KW = KCAP / 64;
+
+struct NmsArgs {
+  float* pred;  // [B][4+nc][A]
+  int B, nc, A;
+  float conf;
+  double iou;
+  const int* classes;
+  int n_classes;
+  int agnostic, multi_label, max_det, max_nms, in_place;
+  float max_wh;
+  float4* boxes;                 // [B][A] xyxy
+  unsigned long long* amask;     // [B][A] candidate class mask
+  unsigned* keyA;                // [B][cap] compaction output (kept for the fallback)
+  unsigned* posA;
+  unsigned* keyB;                // [B][cap] scratch
+  unsigned* posB;
+  long cap;
+  float4* sbox;                  // [B][KCAP] score-ordered prefix: class-offset boxes
+  float* sarea;                  // [B][KCAP]
+  unsigned* spos;                // [B][KCAP] anchor * nc + class
+  unsigned long long* mask;      // [B][KCAP][KW]
+  int* meta;                     // [B][4]: n, neff, K (prefix length), T (prefix = keys < T)
+  int* blkcnt;                   // [B][nblk_a] candidates per 256-anchor block (prep), then exclusive offsets
+  float* out;                    // [B][max_det][6]
+  int* counts;                   // [B]
+  int* out_index;                // [B][max_det]  (anchor index)
+  unsigned long long* stamps;    // diagnostic only (YOLOSOD_NMS_STAMPS): [B][8] or nullptr
+};
+
+#define YS_NSTAMP(k) \
+  if (g.stamps && threadIdx.x == 0) g.stamps[b * 8 + (k)] = __builtin_amdgcn_s_memtime();
+
+__global__ __launch_bounds__(256) void nms_prep_kernel(NmsArgs g) {
+  const int b = blockIdx.y;
+  const int a = blockIdx.x * 256 + threadIdx.x;
+  if (a >= g.A) return;
+  float* pb = g.pred + (long)b * (4 + g.nc) * g.A + a;
+  const long As = g.A;
+  const float cx = pb[0], cy = pb[As], w = pb[2 * As], h = pb[3 * As];
+  const float hw = w / 2.0f, hh = h / 2.0f;
+  const float x1 = cx - hw, y1 = cy - hh, x2 = cx + hw, y2 = cy + hh;
+  if (g.in_place) {
+    pb[0] = x1;
+    pb[As] = y1;
+    pb[2 * As] = x2;
+    pb[3 * As] = y2;
+  }
+  g.boxes[(long)b * g.A + a] = make_float4(x1, y1, x2, y2);
+  unsigned long long mask = 0ull;
+  float best = -INFINITY;
+  int bj = 0;
+  for (int j = 0; j < g.nc; ++j) {
+    const float s = pb[(4 + j) * As];
+    if (s > best) {  // strict: first maximal index wins (torch max(dim) / amax)
+      best = s;
+      bj = j;
+    }
+    if (g.multi_label && s > g.conf) mask |= 1ull << j;
+  }
+  if (!g.multi_label) mask = (best > g.conf) ? (1ull << bj) : 0ull;
+  if (mask && g.classes) {
+    unsigned long long allow = 0ull;
+    for (int k = 0; k < g.n_classes; ++k) {
+      const int c = g.classes[k];
+      if (c >= 0 && c < 64) allow |= 1ull << c;
+    }
+    mask &= allow;
+  }
+  g.amask[(long)b * g.A + a] = mask;
+}
+
+// block-wide (256 threads) exclusive scan; returns the exclusive prefix, *total gets the block sum
+__device__ __forceinline__ int block256_exclusive_scan(int v, int* wsum4, int* total) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += t;
+  }
+  if (lane == 63) wsum4[wv] = inc;
+  __syncthreads();
+  int base = 0;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) base += (w < wv) ? wsum4[w] : 0;
+  *total = wsum4[0] + wsum4[1] + wsum4[2] + wsum4[3];
+  return base + inc - v;
+}
+
+// candidates per 256-anchor block (the compaction runs over the whole GPU: count, scan, scatter)
+__global__ __launch_bounds__(256) void nms_count_kernel(NmsArgs g) {
+  __shared__ int wsum4[4];
+  const int b = blockIdx.y;
+  const long a = (long)blockIdx.x * 256 + threadIdx.x;
+  const int c = (a < g.A) ? __popcll(g.amask[(long)b * g.A + a]) : 0;
+  int total;
+  (void)block256_exclusive_scan(c, wsum4, &total);
+  if (threadIdx.x == 0) g.blkcnt[(long)b * gridDim.x + blockIdx.x] = total;
+}
+
+// per image: exclusive scan of the block counts -> offsets; n, neff -> meta
+__global__ __launch_bounds__(256) void nms_scan_kernel(NmsArgs g, int nblk_a) {
+  __shared__ int wsum4[4];
+  __shared__ int carry;
+  const int b = blockIdx.x;
+  int* bc = g.blkcnt + (long)b * nblk_a;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (int t0 = 0; t0 < nblk_a; t0 += 256) {
+    const int i = t0 + threadIdx.x;
+    const int v = (i < nblk_a) ? bc[i] : 0;
+    int total;
+    const int ex = block256_exclusive_scan(v, wsum4, &total);
+    const int base = carry;
+    if (i < nblk_a) bc[i] = base + ex;
+    __syncthreads();
+    if (threadIdx.x == 0) carry = base + total;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const int n = carry;
+    g.meta[4 * b + 0] = n;
+    g.meta[4 * b + 1] = (n > g.max_nms) ? g.max_nms : n;
+  }
+}
+
+// ordered scatter: entry (anchor, class) in (anchor, class) order = the reference's row order
+__global__ __launch_bounds__(256) void nms_scatter_kernel(NmsArgs g) {
+  __shared__ int wsum4[4];
+  const int b = blockIdx.y;
+  const long A = g.A;
+  const long a = (long)blockIdx.x * 256 + threadIdx.x;
+  const unsigned long long m = (a < A) ? g.amask[(long)b * A + a] : 0ull;
+  int total;
+  const int ex = block256_exclusive_scan(__popcll(m), wsum4, &total);
+  if (!m) return;
+  int k = g.blkcnt[(long)b * gridDim.x + blockIdx.x] + ex;
+  const float* pb = g.pred + (long)b * (4 + g.nc) * A + a;
+  unsigned* kA = g.keyA + (long)b * g.cap;
+  unsigned* pA = g.posA + (long)b * g.cap;
+  for (int j = 0; j < g.nc; ++j)
+    if ((m >> j) & 1ull) {
+      kA[k] = ~__float_as_uint(pb[(long)(4 + j) * A]);  // ascending ~bits == descending positive score
+      pA[k] = (unsigned)(a * g.nc + j);
+      ++k;
+    }
+}
+
+__device__ __forceinline__ unsigned long long lanemask_lt() {
+  const int lane = threadIdx.x & 63;
+  return (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+}
+
+// block-wide exclusive scan of one int per thread; returns the exclusive prefix, *total gets the sum
+__device__ int block_exclusive_scan(int v, int* wsum, int* total) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += t;
+  }
+  if (lane == 63) wsum[wv] = inc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int run = 0;
+    for (int i = 0; i < NMS_W; ++i) {
+      const int t = wsum[i];
+      wsum[i] = run;
+      run += t;
+    }
+    wsum[NMS_W] = run;
+  }
+  __syncthreads();
+  const int ex = wsum[wv] + inc - v;
+  *total = wsum[NMS_W];
+  __syncthreads();
+  return ex;
+}
+
+__device__ __forceinline__ bool iou_gt(const float4 bi, float ai, const float4 bj, float aj, double thr) {
+  // torchvision CPU nms_kernel: i = the earlier (kept) box, j = the later one
+  const float xx1 = fmaxf(bi.x, bj.x), yy1 = fmaxf(bi.y, bj.y);
+  const float xx2 = fminf(bi.z, bj.z), yy2 = fminf(bi.w, bj.w);
+  const float w = fmaxf(0.0f, xx2 - xx1), h = fmaxf(0.0f, yy2 - yy1);
+  const float inter = w * h;
+  const float ovr = inter / ((ai + aj) - inter);
+  return (double)ovr > thr;
+}
+
+// hist[d] += 1 for every active lane with valid: lanes with equal digits are grouped by 8 ballots and one lane
+// per group adds the group size (no same-address atomic storms when most keys share a digit)
+__device__ __forceinline__ void hist_add_digit(unsigned* hist, unsigned d, bool valid) {
+  unsigned long long peers = __ballot(valid);
+#pragma unroll
+  for (int bt = 0; bt < 8; ++bt) {
+    const bool bit = (d >> bt) & 1u;
+    const unsigned long long bal = __ballot(bit);
+    peers &= bit ? bal : ~bal;
+  }
+  if (valid && (peers & lanemask_lt()) == 0ull) atomicAdd(&hist[d], (unsigned)__popcll(peers));
+}
+
+// exclusive scan of hist[0..256) in place by the first 256 threads of the (512-thread) block; returns nothing,
+// block-uniform (contains barriers). tmp: 4 words.
+__device__ void scan256_exclusive(unsigned* hist, unsigned* tmp) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  unsigned v = 0, inc = 0;
+  if (tid < 256) {
+    v = hist[tid];
+    inc = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned t = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += t;
+    }
+    if (lane == 63) tmp[wv] = inc;
+  }
+  __syncthreads();
+  if (tid < 256) {
+    unsigned base = 0;
+    for (int w = 0; w < wv; ++w) base += tmp[w];
+    hist[tid] = base + inc - v;
+  }
+  __syncthreads();
+}
+
+struct SortShared {
+  unsigned hist[256];
+  unsigned wcnt[NMS_W][256];
+  int flag;
+  int wsum[NMS_W + 1];
+  unsigned tmp4[4];
+};
+
+// Stable LSD radix sort (4 x 8-bit digits, ascending) of n (key, pos) pairs, ping-ponging between (ks, ps) and
+// (kd, pd); on return (ks, ps) hold the sorted pairs. Passes whose digit is uniform are skipped. Block-uniform.
+__device__ void radix_sort_pairs(unsigned*& ks, unsigned*& ps, unsigned*& kd, unsigned*& pd, int n, SortShared& sh) {
+  const int tid = threadIdx.x, wv = tid >> 6;
+  for (int pass = 0; pass < 4 && n > 1; ++pass) {
+    const int shift = pass * 8;
+    __syncthreads();  // previous pass fully done with hist / flag
+    if (tid < 256) sh.hist[tid] = 0;
+    if (tid == 0) sh.flag = 0;
+    __syncthreads();
+    for (int i0 = 0; i0 < n; i0 += NMS_T) {
+      const int i = i0 + tid;
+      hist_add_digit(sh.hist, (i < n) ? (ks[i] >> shift) & 255u : 0u, i < n);
+    }
+    __syncthreads();
+    if (tid < 256 && sh.hist[tid] == (unsigned)n) sh.flag = 1;
+    __syncthreads();
+    if (sh.flag) continue;  // every key has the same digit: the pass is the identity
+    scan256_exclusive(sh.hist, sh.tmp4);
+    for (int t0 = 0; t0 < n; t0 += NMS_T) {
+      for (int e = tid; e < NMS_W * 256; e += NMS_T) (&sh.wcnt[0][0])[e] = 0;
+      __syncthreads();
+      const int i = t0 + tid;
+      const bool valid = i < n;
+      const unsigned key = valid ? ks[i] : 0u;
+      const unsigned pos = valid ? ps[i] : 0u;
+      const unsigned d = (key >> shift) & 255u;
+      unsigned long long peers = __ballot(valid);
+#pragma unroll
+      for (int bt = 0; bt < 8; ++bt) {
+        const bool bit = (d >> bt) & 1u;
+        const unsigned long long bal = __ballot(bit);
+        peers &= bit ? bal : ~bal;
+      }
+      const unsigned long long lower = peers & lanemask_lt();
+      const int rank = __popcll(lower);
+      if (valid && lower == 0ull) sh.wcnt[wv][d] = (unsigned)__popcll(peers);
+      __syncthreads();
+      if (tid < 256) {
+        unsigned run = sh.hist[tid];
+        for (int w = 0; w < NMS_W; ++w) {
+          const unsigned c = sh.wcnt[w][tid];
+          sh.wcnt[w][tid] = run;
+          run += c;
+        }
+        sh.hist[tid] = run;
+      }
+      __syncthreads();
+      if (valid) {
+        const unsigned dst = sh.wcnt[wv][d] + rank;
+        kd[dst] = key;
+        pd[dst] = pos;
+      }
+      __syncthreads();
+    }
+    unsigned* t;
+    t = ks; ks = kd; kd = t;
+    t = ps; ps = pd; pd = t;
+  }
+  __syncthreads();
+}
+
+// Order-preserving compaction of the pairs whose key is < T (below) or >= T (!below) into (kd, pd); returns
+// the count. Block-uniform.
+__device__ int compact_by_key(const unsigned* ks, const unsigned* ps, int n, unsigned T, bool below, unsigned* kd,
+                              unsigned* pd, SortShared& sh) {
+  constexpr int CPT = 4;
+  const int tid = threadIdx.x;
+  int m = 0;
+  for (int t0 = 0; t0 < n; t0 += NMS_T * CPT) {
+    const int i0 = t0 + tid * CPT;
+    unsigned k[CPT], p[CPT];
+    int c = 0;
+#pragma unroll
+    for (int u = 0; u < CPT; ++u) {
+      const bool v = i0 + u < n;
+      k[u] = v ? ks[i0 + u] : 0u;
+      p[u] = v ? ps[i0 + u] : 0u;
+      const bool take = v && ((k[u] < T) == below);
+      c += take ? 1 : 0;
+      if (!take) k[u] = 0u, p[u] = 0xFFFFFFFFu;
+    }
+    int total;
+    const int ex = block_exclusive_scan(c, sh.wsum, &total);
+    int o = m + ex;
+#pragma unroll
+    for (int u = 0; u < CPT; ++u)
+      if (p[u] != 0xFFFFFFFFu) {
+        kd[o] = k[u];
+        pd[o] = p[u];
+        ++o;
+      }
+    m += total;
+  }
+  return m;
+}
+
+// -------------------------------------------------------------------------------------------------
+// nms_select: compaction + score order of the first <= KCAP candidates (see header)
+// -------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(NMS_T) void nms_select_kernel(NmsArgs g) {
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  __shared__ SortShared sh;
+  __shared__ unsigned sel_below, sel_prefix;
+  YS_NSTAMP(0)
+  const long A = g.A;
+  const int nc = g.nc;
+  unsigned* kA = g.keyA + (long)b * g.cap;
+  unsigned* pA = g.posA + (long)b * g.cap;
+  unsigned* kB = g.keyB + (long)b * g.cap;
+  unsigned* pB = g.posB + (long)b * g.cap;
+
+  // (a) the ordered compaction ran over the whole GPU (nms_count / nms_scan / nms_scatter)
+  const int n = g.meta[4 * b + 0];
+  YS_NSTAMP(1)
+  const int neff = (n > g.max_nms) ? g.max_nms : n;
+
+  // (b) score order of the prefix
+  unsigned *ks, *ps, *kd, *pd;
+  unsigned T = 0xFFFFFFFFu;
+  int m;
+  __shared__ unsigned lk[2][KCAP], lp[2][KCAP];  // the prefix is sorted in LDS
+  if (n <= KCAP) {
+    for (int i = tid; i < n; i += NMS_T) {
+      lk[0][i] = kA[i];
+      lp[0][i] = pA[i];
+    }
+    ks = lk[0]; ps = lp[0]; kd = lk[1]; pd = lp[1];
+    radix_sort_pairs(ks, ps, kd, pd, n, sh);
+    m = n;
+  } else {
+    // radix select, MSB first: the key T with #(key < T) <= KCAP, taking whole digit buckets while they fit
+    unsigned prefix = 0u, pmask = 0u;
+    unsigned below = 0u;
+    for (int pass = 0; pass < 4; ++pass) {
+      const int shift = 24 - 8 * pass;
+      if (tid < 256) sh.hist[tid] = 0;
+      __syncthreads();
+      for (int i = tid; i < n; i += NMS_T) {
+        const unsigned k = kA[i];
+        if ((k & pmask) == prefix) atomicAdd(&sh.hist[(k >> shift) & 255u], 1u);
+      }
+      __syncthreads();
+      if (tid == 0) {
+        unsigned run = below;
+        int d = 0;
+        for (; d < 256; ++d) {
+          if (run + sh.hist[d] > (unsigned)KCAP) break;
+          run += sh.hist[d];
+        }
+        // d < 256 always: the keys under the current prefix do not all fit (else the previous pass would
+        // have taken that whole bucket)
+        sel_below = run;
+        sel_prefix = prefix | ((unsigned)d << shift);
+      }
+      __syncthreads();
+      below = sel_below;
+      prefix = sel_prefix;
+      pmask |= 255u << shift;
+    }
+    T = prefix;  // keys < T: exactly `below` of them, a prefix of the stable ascending order
+    m = compact_by_key(kA, pA, n, T, true, lk[0], lp[0], sh);
+    __syncthreads();
+    ks = lk[0]; ps = lp[0]; kd = lk[1]; pd = lp[1];
+    radix_sort_pairs(ks, ps, kd, pd, m, sh);
+  }
+  YS_NSTAMP(2)
+  const int K = (m < neff) ? m : neff;
+  // prefix boxes with the class offset (ops.py:289,295), areas, ids
+  const float4* bx = g.boxes + (long)b * A;
+  float4* sb = g.sbox + (long)b * KCAP;
+  float* sa = g.sarea + (long)b * KCAP;
+  unsigned* sp = g.spos + (long)b * KCAP;
+  for (int i = tid; i < K; i += NMS_T) {
+    const unsigned pos = ps[i];
+    const unsigned a = pos / nc, j = pos % nc;
+    const float4 bb = bx[a];
+    const float off = g.agnostic ? 0.0f : (float)j * g.max_wh;
+    const float4 o = make_float4(bb.x + off, bb.y + off, bb.z + off, bb.w + off);
+    sb[i] = o;
+    sa[i] = (o.z - o.x) * (o.w - o.y);
+    sp[i] = pos;
+  }
+  if (tid == 0) {
+    int* mt = g.meta + 4 * b;
+    mt[2] = K;
+    mt[3] = (int)T;
+    if (g.stamps) g.stamps[b * 8 + 6] = (unsigned long long)n;
+  }
+}
+
+// -------------------------------------------------------------------------------------------------
+// nms_mask: bit q of mask[b][i][cb] set iff j = cb*64+q > i, j < K and IoU(i, j) > thr. grid = (KW, B).
+// -------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void nms_mask_kernel(NmsArgs g) {
+  const int b = blockIdx.y, rb = blockIdx.x;
+  const int K = g.meta[4 * b + 2];
+  if (rb * 64 >= K) return;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  __shared__ float4 cbx[4][64];
+  __shared__ float car[4][64];
+  const float4* sb = g.sbox + (long)b * KCAP;
+  const float* sa = g.sarea + (long)b * KCAP;
+  const int i = rb * 64 + lane;
+  const float4 bi = (i < K) ? sb[i] : make_float4(0, 0, 0, 0);
+  const float ai = (i < K) ? sa[i] : 0.f;
+  const int nblk = (K + 63) / 64;
+  unsigned long long* mrow = g.mask + ((long)b * KCAP + i) * KW;
+  for (int cb0 = rb; cb0 < nblk; cb0 += 4) {
+    const int cb = cb0 + wv;
+    const int j = cb * 64 + lane;
+    if (cb < nblk) {
+      cbx[wv][lane] = (j < K) ? sb[j] : make_float4(0, 0, 0, 0);
+      car[wv][lane] = (j < K) ? sa[j] : 0.f;
+    }
+    __syncthreads();
+    if (cb < nblk && i < K) {
+      unsigned long long bits = 0ull;
+      const int qlo = (cb == rb) ? lane + 1 : 0;
+      const int qhi = (K - cb * 64 < 64) ? K - cb * 64 : 64;
+      for (int q = qlo; q < qhi; ++q)
+        if (iou_gt(bi, ai, cbx[wv][q], car[wv][q], g.iou)) bits |= 1ull << q;
+      mrow[cb] = bits;
+    }
+    __syncthreads();
+  }
+}
+
+// -------------------------------------------------------------------------------------------------
+// nms_resolve: greedy over the prefix bitmask, then (rarely) the chunked fallback over the remainder
+// -------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(NMS_T) void nms_resolve_kernel(NmsArgs g) {
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  __shared__ unsigned long long mrows[2][64][KW];
+  __shared__ int kept_t[NMS_MAXDET];  // kept entries: < KCAP -> prefix index, else KCAP + remainder index
+  __shared__ int nkept_sh, done_sh;
+  YS_NSTAMP(3)
+  const int* mt = g.meta + 4 * b;
+  const int n = mt[0], neff = mt[1], K = mt[2];
+  const unsigned T = (unsigned)mt[3];
+  const long A = g.A;
+  const int nc = g.nc;
+  const float* pb = g.pred + (long)b * (4 + nc) * A;
+  const float4* bx = g.boxes + (long)b * A;
+  const unsigned* sp = g.spos + (long)b * KCAP;
+  float* ob = g.out + (long)b * g.max_det * 6;
+  int* oi = g.out_index + (long)b * g.max_det;
+
+  if (tid == 0) {
+    nkept_sh = 0;
+    done_sh = 0;
+  }
+  __syncthreads();
+  // (1) greedy over the prefix: lane w (< KW) of wave 0 owns removed-word w; waves 1..7 stage the next 64
+  // mask rows into the other LDS buffer meanwhile
+  {
+    const int nblk = (K + 63) / 64;
+    auto stage = [&](int rb, int buf, int t0, int nt) {
+      const unsigned long long* src = g.mask + ((long)b * KCAP + rb * 64) * KW;
+      for (int e = t0; e < 64 * KW; e += nt) {
+        const int r = e / KW, w = e % KW;
+        mrows[buf][r][w] = (rb * 64 + r < K && w >= rb && w < nblk) ? src[(long)r * KW + w] : 0ull;
+      }
+    };
+    if (nblk > 0) stage(0, 0, tid, NMS_T);
+    __syncthreads();
+    unsigned long long removed = 0ull;
+    int nkk = 0;
+    bool done = false;
+    for (int rb = 0; rb < nblk; ++rb) {
+      const int buf = rb & 1;
+      if (wv != 0) {
+        if (rb + 1 < nblk) stage(rb + 1, buf ^ 1, tid - 64, NMS_T - 64);
+      } else {
+        // lane q holds row q's bits inside this block (the diagonal word); the greedy over the block is a
+        // scalar loop (readlane), then the kept rows are OR-ed into the later words in parallel
+        const unsigned long long diag = mrows[buf][lane][rb];
+        const int rows_here = (K - rb * 64 < 64) ? K - rb * 64 : 64;
+        unsigned long long rem = __shfl(removed, rb, 64);
+        unsigned long long cand = (rows_here == 64 ? ~0ull : ((1ull << rows_here) - 1ull)) & ~rem;
+        unsigned long long keptm = 0ull;
+        while (cand) {
+          const int q = __ffsll((long long)cand) - 1;
+          keptm |= 1ull << q;
+          if (lane == 0) kept_t[nkk] = rb * 64 + q;
+          ++nkk;
+          if (nkk >= g.max_det) {
+            done = true;
+            break;
+          }
+          const unsigned lo = __builtin_amdgcn_readlane((unsigned)diag, q);
+          const unsigned hi = __builtin_amdgcn_readlane((unsigned)(diag >> 32), q);
+          rem |= ((unsigned long long)hi << 32) | lo;
+          const unsigned long long upto = (q == 63) ? ~0ull : ((2ull << q) - 1ull);
+          cand &= ~upto & ~rem;
+        }
+        if (!done && lane > rb && lane < nblk) {
+          unsigned long long acc = removed;
+          unsigned long long km = keptm;
+          while (km) {
+            const int q = __ffsll((long long)km) - 1;
+            km &= km - 1;
+            acc |= mrows[buf][q][lane];
+          }
+          removed = acc;
+        }
+        if (lane == 0) {
+          nkept_sh = nkk;
+          done_sh = done ? 1 : 0;
+        }
+      }
+      __syncthreads();
+      if (done_sh) break;
+    }
+  }
+  const int nk_prefix = nkept_sh;
+  for (int k = tid; k < nk_prefix; k += NMS_T) {
+    const unsigned p = sp[kept_t[k]];
+    const unsigned a = p / nc, j = p % nc;
+    const float4 bb = bx[a];
+    float* o = ob + (long)k * 6;
+    o[0] = bb.x; o[1] = bb.y; o[2] = bb.z; o[3] = bb.w;
+    o[4] = pb[(long)(4 + j) * A + a];
+    o[5] = (float)j;
+    oi[k] = (int)a;
+  }
+  YS_NSTAMP(4)
+
+  // (2) fallback: prefix exhausted, fewer than max_det kept, more candidates (keys >= T) within max_nms
+  if (!done_sh && K < neff) {
+    __shared__ SortShared sh;
+    __shared__ float4 kept_box[NMS_MAXDET];
+    __shared__ float kept_area[NMS_MAXDET];
+    __shared__ float4 cb[NMS_T];
+    __shared__ float ca[NMS_T];
+    __shared__ int alive[NMS_T];
+    __shared__ unsigned long long alive_w[NMS_W];
+    __shared__ unsigned long long rows[NMS_T][NMS_T / 64];
+    const float4* sb = g.sbox + (long)b * KCAP;
+    const float* sa = g.sarea + (long)b * KCAP;
+    for (int k = tid; k < nk_prefix; k += NMS_T) {
+      kept_box[k] = sb[kept_t[k]];
+      kept_area[k] = sa[kept_t[k]];
+    }
+    unsigned* kA = g.keyA + (long)b * g.cap;
+    unsigned* pA = g.posA + (long)b * g.cap;
+    unsigned* kB = g.keyB + (long)b * g.cap;
+    unsigned* pB = g.posB + (long)b * g.cap;
+    const int m = compact_by_key(kA, pA, n, T, false, kB, pB, sh);
+    __syncthreads();
+    unsigned *ks = kB, *ps = pB, *kd = kA, *pd = pA;
+    radix_sort_pairs(ks, ps, kd, pd, m, sh);
+    const int rem = (m < neff - K) ? m : neff - K;
+    for (int c0 = 0; c0 < rem; c0 += NMS_T) {
+      const int i = c0 + tid;
+      const bool valid = i < rem;
+      float4 obox = make_float4(0, 0, 0, 0);
+      float area = 0.f;
+      if (valid) {
+        const unsigned pos = ps[i];
+        const unsigned a = pos / nc, j = pos % nc;
+        const float4 bb = bx[a];
+        const float off = g.agnostic ? 0.0f : (float)j * g.max_wh;
+        obox = make_float4(bb.x + off, bb.y + off, bb.z + off, bb.w + off);
+        area = (obox.z - obox.x) * (obox.w - obox.y);
+      }
+      cb[tid] = obox;
+      ca[tid] = area;
+      const int nk = nkept_sh;
+      bool al = valid;
+      for (int k = 0; k < nk && al; ++k)
+        if (iou_gt(kept_box[k], kept_area[k], obox, area, g.iou)) al = false;
+      alive[tid] = al ? 1 : 0;
+      const unsigned long long aw = __ballot(al);
+      if (lane == 0) alive_w[wv] = aw;
+      __syncthreads();
+#pragma unroll
+      for (int wd = 0; wd < NMS_T / 64; ++wd) {
+        unsigned long long bits = 0ull;
+        if (al) {
+          for (int q = 0; q < 64; ++q) {
+            const int jj = wd * 64 + q;
+            if (jj > tid && alive[jj] && iou_gt(obox, area, cb[jj], ca[jj], g.iou)) bits |= 1ull << q;
+          }
+        }
+        rows[tid][wd] = bits;
+      }
+      __syncthreads();
+      if (wv == 0) {
+        unsigned long long removed = 0ull;
+        int nkk = nk;
+        bool done = false;
+        for (int w = 0; w < NMS_T / 64 && !done; ++w) {
+          unsigned long long cand = alive_w[w] & ~__shfl(removed, w, 64);
+          while (cand) {
+            const int q = __ffsll((long long)cand) - 1;
+            const int t = w * 64 + q;
+            if (lane == 0) {
+              kept_box[nkk] = cb[t];
+              kept_area[nkk] = ca[t];
+              kept_t[nkk] = c0 + t;  // remainder index
+            }
+            ++nkk;
+            if (nkk >= g.max_det) {
+              done = true;
+              break;
+            }
+            if (lane < NMS_T / 64) removed |= rows[t][lane];
+            const unsigned long long upto = (q == 63) ? ~0ull : ((2ull << q) - 1ull);
+            cand &= ~upto & ~__shfl(removed, w, 64);
+          }
+        }
+        if (lane == 0) {
+          nkept_sh = nkk;
+          done_sh = done ? 1 : 0;
+        }
+      }
+      __syncthreads();
+      const int nk_new = nkept_sh;
+      for (int k = nk + tid; k < nk_new; k += NMS_T) {
+        const unsigned p = ps[kept_t[k]];
+        const unsigned a = p / nc, j = p % nc;
+        const float4 bb = bx[a];
+        float* o = ob + (long)k * 6;
+        o[0] = bb.x; o[1] = bb.y; o[2] = bb.z; o[3] = bb.w;
+        o[4] = pb[(long)(4 + j) * A + a];
+        o[5] = (float)j;
+        oi[k] = (int)a;
+      }
+      if (done_sh) break;
+    }
+  }
+  __syncthreads();
+  YS_NSTAMP(5)
+  const int nk = nkept_sh;
+  for (int e = nk * 6 + tid; e < g.max_det * 6; e += NMS_T) ob[e] = 0.f;
+  for (int e = nk + tid; e < g.max_det; e += NMS_T) oi[e] = -1;
+  if (tid == 0) {
+    g.counts[b] = nk;
+    if (g.stamps) g.stamps[b * 8 + 7] = (unsigned long long)K;
+  }
+}
+
+#undef YS_NSTAMP
+
+}  // namespace ys
+
+using namespace ys;
+
+static unsigned long long* g_nms_stamps = nullptr;  // diagnostic only (YOLOSOD_NMS_STAMPS)
+static size_t g_nms_stamp_cap = 0, g_nms_stamp_n = 0;
+
+// Diagnostic: per-image phase cycles of the last NMS call (synchronous). out[b*6 + k]: 0 compaction, 1 sort /
+// select, 2 greedy over the prefix (resolve start -> prefix done, includes the mask kernel's wait), 3 fallback,
+// 4 candidates n, 5 prefix length K.
+YS_EXPORT int yolosod_debug_nms_stage_cycles(double* out, int B) {
+  if (!g_nms_stamps || (size_t)B * 8 > g_nms_stamp_n || B > 1024) return -1;
+  static unsigned long long h[8 * 1024];
+  if (hipMemcpy(h, g_nms_stamps, (size_t)B * 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  for (int b = 0; b < B; ++b) {
+    const unsigned long long* s = h + b * 8;
+    out[b * 6 + 0] = (double)(s[1] - s[0]);
+    out[b * 6 + 1] = (double)(s[2] - s[1]);
+    out[b * 6 + 2] = (double)(s[4] - s[3]);
+    out[b * 6 + 3] = (double)(s[5] - s[4]);
+    out[b * 6 + 4] = (double)s[6];
+    out[b * 6 + 5] = (double)s[7];
+  }
+  return 0;
+}
+
+static long nms_cap(int nc, int A, int multi_label) { return (long)A * (multi_label ? nc : 1); }
+
+YS_EXPORT size_t yolosod_nms_workspace(int B, int nc, int A, int multi_label) {
+  const long cap = nms_cap(nc, A, multi_label);
+  Sizer s;
+  s.take<float4>((size_t)B * A);
+  s.take<unsigned long long>((size_t)B * A);
+  for (int i = 0; i < 4; ++i) s.take<unsigned>((size_t)B * cap);
+  s.take<float4>((size_t)B * KCAP);
+  s.take<float>((size_t)B * KCAP);
+  s.take<unsigned>((size_t)B * KCAP);
+  s.take<unsigned long long>((size_t)B * KCAP * KW);
+  s.take<int>((size_t)B * 4);
+  s.take<int>((size_t)B * ((A + 255) / 256));
+  return s.off;
+}
+
+YS_EXPORT int yolosod_nms(float* pred, int B, int nc, int A, float conf_thres, double iou_thres, const int* classes,
+                          int n_classes, int agnostic, int multi_label, int max_det, int max_nms, float max_wh,
+                          int in_place, float* out, int* counts, int* out_index, void* workspace,
+                          size_t workspace_bytes, void* stream) {
+  YS_CHECK_ARG(pred && out && counts && out_index, "nms: null pointer");
+  YS_CHECK_ARG(nc >= 1 && nc <= 64, "nms: nc=%d unsupported (1..64)", nc);
+  YS_CHECK_ARG(max_det >= 1 && max_det <= NMS_MAXDET, "nms: max_det=%d unsupported (1..%d)", max_det, NMS_MAXDET);
+  YS_CHECK_ARG(max_nms >= 0, "nms: bad max_nms");
+  YS_CHECK_ARG((long)A * nc < (1L << 32), "nms: A*nc too large");
+  if (B == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  const long cap = nms_cap(nc, A, multi_label);
+  Carver cv(workspace, workspace_bytes);
+  NmsArgs g{};
+  g.pred = pred;
+  g.B = B;
+  g.nc = nc;
+  g.A = A;
+  g.conf = conf_thres;
+  g.iou = iou_thres;
+  g.classes = (n_classes > 0) ? classes : nullptr;
+  g.n_classes = n_classes;
+  g.agnostic = agnostic;
+  g.multi_label = multi_label;
+  g.max_det = max_det;
+  g.max_nms = max_nms;
+  g.in_place = in_place;
+  g.max_wh = max_wh;
+  g.boxes = cv.take<float4>((size_t)B * A);
+  g.amask = cv.take<unsigned long long>((size_t)B * A);
+  g.keyA = cv.take<unsigned>((size_t)B * cap);
+  g.posA = cv.take<unsigned>((size_t)B * cap);
+  g.keyB = cv.take<unsigned>((size_t)B * cap);
+  g.posB = cv.take<unsigned>((size_t)B * cap);
+  g.sbox = cv.take<float4>((size_t)B * KCAP);
+  g.sarea = cv.take<float>((size_t)B * KCAP);
+  g.spos = cv.take<unsigned>((size_t)B * KCAP);
+  g.mask = cv.take<unsigned long long>((size_t)B * KCAP * KW);
+  g.meta = cv.take<int>((size_t)B * 4);
+  const int nblk_a = (A + 255) / 256;
+  g.blkcnt = cv.take<int>((size_t)B * nblk_a);
+  YS_CHECK_ARG(g.blkcnt, "nms: workspace too small (%zu)", workspace_bytes);
+  g.cap = cap;
+  g.out = out;
+  g.counts = counts;
+  g.out_index = out_index;
+  g.stamps = nullptr;
+  if (getenv("YOLOSOD_NMS_STAMPS")) {
+    if ((size_t)B * 8 > g_nms_stamp_cap) {
+      if (g_nms_stamps) (void)hipFree(g_nms_stamps);
+      g_nms_stamps = nullptr;
+      if (hipMalloc((void**)&g_nms_stamps, (size_t)B * 8 * sizeof(unsigned long long)) != hipSuccess) return -1;
+      g_nms_stamp_cap = (size_t)B * 8;
+    }
+    (void)hipMemsetAsync(g_nms_stamps, 0, (size_t)B * 8 * sizeof(unsigned long long), st);
+    g_nms_stamp_n = (size_t)B * 8;
+    g.stamps = g_nms_stamps;
+  }
+  if (A > 0) {
+    hipLaunchKernelGGL(nms_prep_kernel, dim3(nblk_a, B), dim3(256), 0, st, g);
+    hipLaunchKernelGGL(nms_count_kernel, dim3(nblk_a, B), dim3(256), 0, st, g);
+  }
+  hipLaunchKernelGGL(nms_scan_kernel, dim3(B), dim3(256), 0, st, g, nblk_a);
+  if (A > 0) hipLaunchKernelGGL(nms_scatter_kernel, dim3(nblk_a, B), dim3(256), 0, st, g);
+  hipLaunchKernelGGL(nms_select_kernel, dim3(B), dim3(NMS_T), 0, st, g);
+  hipLaunchKernelGGL(nms_mask_kernel, dim3(KW, B), dim3(256), 0, st, g);
+  hipLaunchKernelGGL(nms_resolve_kernel, dim3(B), dim3(NMS_T), 0, st, g);
+  YS_CHECK_LAUNCH("nms");
+  return 0;
+}
