@@ -162,6 +162,15 @@ def main():
                 "kernel": f"{dom['op']}{tuple(dom['shape'])} (one C-ABI call = its launch sequence)",
                 "algorithmic_per_launch": dom["flops"] if bound == "mfma" else dom["bytes"]}
 
+    # path-level roofline = sum_k t_k^min / sum_k t_k^meas over every hot-path operator,
+    # t_k^min = max(bytes_k / HBM peak, flops_k / fp32 MFMA peak)
+    t_min = sum(max(o["bytes"] / (perf.PEAK_HBM_GBS * 1e9), o["flops"] / (perf.PEAK_FP32_MFMA_TFLOPS * 1e12))
+                * 1e3 * o["launches"] / args.steps for o in ops)
+    t_meas = sum(o["total_ms_per_step"] for o in ops)
+    path_roofline = {"t_min_ms": round(t_min, 4), "t_meas_ms": round(t_meas, 4),
+                     "frac": round(t_min / t_meas, 4) if t_meas else None,
+                     "definition": "sum over hot-path ops of max(bytes/8 TB/s, flops/157.3 TF/s) / measured"}
+
     total_imgs = world * bs * args.steps
     value = total_imgs / elapsed
     hip_ms = sum(o["total_ms_per_step"] for o in ops)
@@ -174,6 +183,7 @@ def main():
                                f"forward + decode + NMS(conf={args.conf}, iou=0.7)",
                    "imgsz": imgsz, "batch_per_gpu": bs, "global_batch": bs * world, "parallelism": f"dp{world}"},
         "roofline": roofline,
+        "path_roofline": path_roofline,
         "hip_ops_ms_per_step": round(hip_ms, 3),
         "hip_ops": [{k: v for k, v in o.items() if k not in ("bytes", "flops")} for o in ops],
         "cpu_baseline": None,
