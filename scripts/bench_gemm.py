@@ -15,7 +15,10 @@ SHAPES = [(56448, 768, 256), (56448, 512, 256), (56448, 256, 512), (56448, 256, 
 
 def main():
     dev = torch.device("cuda")
-    for (M, N, K) in SHAPES:
+    shapes = [tuple(int(v) for v in a.split(",")) for a in sys.argv[1:] if not a.startswith("--")] or SHAPES
+    torch_ref = "--no-torch" not in sys.argv
+    shapes = [s for s in shapes if len(s) == 3]
+    for (M, N, K) in shapes:
         A = torch.randn(M, K, device=dev)
         B = torch.randn(N, K, device=dev)
         bias = torch.randn(N, device=dev)
@@ -31,6 +34,9 @@ def main():
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / n
         tf = 2 * M * N * K / ms / 1e9
+        if not torch_ref:
+            print(f"M={M:7d} N={N:5d} K={K:5d}  {ms:8.3f} ms  {tf:7.1f} TFLOP/s", flush=True)
+            continue
         Bt = B.t()
         for _ in range(3):
             torch.mm(A, Bt)

@@ -71,3 +71,35 @@ def test_fused_head_equals_raw_map_path(gpu_model, cuda):
     assert raw[0].shape == (2, 74, 160, 160)
     ok, err, _ = tol_close(y_fused.cpu(), y_raw.cpu(), 1e-4, 1e-5)
     assert ok, f"max abs err {err:.3g}"
+
+
+def test_m_scale_model_matches_oracle(cuda):
+    """yolov12m-sod (the paper YAML with v12's m scale; BASELINE configs[4] in fp32): Swin C=128 on the
+    fused kernel, Swin C=512 and A2 C=512 on the GEMM path, Detect c3=128 on the fused head."""
+    from oracle.model_ref import build_cpu_model
+    from yolosod_amd.nn.tasks import build_model
+    gm = build_model("yolov12m-sod.yaml", seed=0, device=cuda)
+    cpu = build_cpu_model("yolov12m-sod.yaml")
+    cpu.load_state_dict({k: v.cpu() for k, v in gm.state_dict().items()})
+    g = torch.Generator().manual_seed(4)
+    x = torch.rand(1, 3, 256, 256, generator=g)
+    with torch.inference_mode():
+        y = gm(x.to(cuda))[0].cpu()
+        ref = cpu(x)[0]
+    ok, err, _ = tol_close(y, ref, ATOL, 0.0)
+    assert ok, f"max abs err {err:.3g}"
+
+
+def test_model_1280_matches_oracle(gpu_model, cuda):
+    """BASELINE configs[3] shape (1280x1280, P2 head at 320x320; Swin L28 on 2116 windows per image)."""
+    from oracle.model_ref import build_cpu_model
+    cpu = build_cpu_model()
+    cpu.load_state_dict({k: v.cpu() for k, v in gpu_model.state_dict().items()})
+    g = torch.Generator().manual_seed(5)
+    x = torch.rand(1, 3, 1280, 1280, generator=g)
+    with torch.inference_mode():
+        y = gpu_model(x.to(cuda))[0].cpu()
+        ref = cpu(x)[0]
+    assert y.shape == (1, 14, 136000)
+    ok, err, _ = tol_close(y, ref, ATOL, 0.0)
+    assert ok, f"max abs err {err:.3g}"

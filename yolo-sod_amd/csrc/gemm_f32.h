@@ -18,6 +18,7 @@
 // through LDS and stores whole rows with 16-byte coalesced stores (bias / BN / act / residual fused).
 #pragma once
 #include "common.h"
+#include <stdlib.h>
 
 namespace ys {
 
@@ -378,8 +379,13 @@ static inline int launch_gemm(const GemmArgs& g0, int batch, bool b_kc, hipStrea
       else hipLaunchKernelGGL((gemm_f32_kernel<WM_, WN_, MI_, NI_, false, false>), grid, dim3(256), 0, st, g); \
     }                                                                                                          \
   } while (0)
-  if (narrow) YS_GEMM_LAUNCH(4, 1, 1, 2);
-  else if (g.M <= 64) YS_GEMM_LAUNCH(1, 4, 2, 2);  // 64 x 256 tiles (1x1 convs with few output channels)
+  // tile choice (YOLOSOD_GEMM_TILE overrides for A/B runs: 1 = 128x64, 2 = 128x128, 3 = 64x256)
+  static const int forced = [] {
+    const char* e = getenv("YOLOSOD_GEMM_TILE");
+    return e ? atoi(e) : 0;
+  }();
+  if (forced == 1 || (!forced && narrow)) YS_GEMM_LAUNCH(4, 1, 1, 2);
+  else if (forced == 3 || (!forced && g.M <= 64)) YS_GEMM_LAUNCH(1, 4, 2, 2);  // 64 x 256 tiles
   else YS_GEMM_LAUNCH(2, 2, 2, 2);
 #undef YS_GEMM_LAUNCH
   YS_CHECK_LAUNCH("gemm_f32");
