@@ -1,8 +1,9 @@
 // Fused SwinBlock for small channel counts (C <= 128: the P2 instance L28, C = 64 in the paper model).
 //
-// One 256-thread workgroup = one 7x7 window. The window's tokens never leave LDS between the depthwise conv and
-// the final pw1x1+BN+SiLU+residual, so the per-token HBM traffic is read x (+ halo) once and write y once, against
-// ~5.5 GB of token-major scratch for the decomposed path at 640^2 bs=32.
+// One 256-thread workgroup processes one 7x7 window at a time (persistent: a strided run of windows per
+// workgroup). The window's tokens never leave LDS between the depthwise conv and the final pw1x1+BN+SiLU+residual,
+// so the per-token HBM traffic is read x (+ halo) once and write y once, against ~5.5 GB of token-major scratch
+// for the decomposed path at 640^2 bs=32.
 //
 // Stages (ultralytics/nn/modules/blocks_transformer.py):
 //   0 dw3x3 (pad 1, no bias) on the (wh+2)x(ww+2) halo patch -> T[tok][c]; tokens of the bottom/right zero pad = 0
@@ -13,20 +14,21 @@
 //   4 T += O Wo^T + bo                             (out_proj + residual, :119)
 //   5 U = LN2(T); 6 Hd = GELU(U W1^T + b1); 7 T += Hd W2^T + b2   (:122)
 //   8 y = x + SiLU(BN(Wpw T^T)) on the valid (cropped) tokens, NCHW   (window_reverse + crop :125-129, :166-171)
-// All GEMMs run on v_mfma_f32_16x16x4_f32 (exact fp32). A wave owns a slice of output columns for all 64
-// (padded) token rows; the MFMA k index is permuted (lane group g takes k in [g*K/4, (g+1)*K/4)) so operands are
-// 16-byte loads: A from LDS, weights straight from global (L2-resident, each weight element read once per
-// window). Attention computes S^T so that its accumulator registers are directly the B operand of O^T = V^T P^T
-// (keys permuted consistently), so P never touches LDS.
-// Padding rows: only 49 token rows + 1 zero row are stored; MFMA rows >= 49 read the zero row and their outputs
-// are discarded.
+// GEMMs run on v_mfma_f32_16x16x4_f32 (exact fp32). A wave owns a slice of output columns for all token rows;
+// the MFMA k index is permuted (lane group g takes k in [g*K/4, (g+1)*K/4)) so operands are 16-byte loads: A
+// from LDS, weights straight from global (L2-resident). 49 tokens = three 16-row MFMA blocks (rows 0..47) + row
+// 48 on the VALU from the weight fragments already in registers (a fourth MFMA block would be 15/16 padding:
+// this removes 25% of the MFMAs). Attention computes S^T so that its accumulator registers are directly the B
+// operand of O^T = V^T P^T (keys permuted consistently), so P never touches LDS; key 48 is a VALU rank-1 term.
 #include "common.h"
 #include <math.h>
 #include <stdlib.h>
 
 namespace ys {
 
-constexpr int SW_ROWS = 50;  // 49 tokens + zero row
+constexpr int SW_ROWS = 49;  // token rows stored per window (7x7)
+constexpr int XR = 48;       // the token row computed on the VALU (rows 0..47 = three 16-row MFMA blocks)
+constexpr int HPW = 12;      // halo patch row stride in LDS (9 used; 16-byte aligned rows)
 
 struct SwinFusedArgs {
   const float* x;
@@ -52,41 +54,66 @@ struct SwinFusedArgs {
   const float* bn_shift;
   float scale;
   int abl;  // timing ablation (debug only): 1 skip halo loads, 2 skip weight loads, 4 skip residual loads
-  unsigned long long* stamps;  // diagnostic build only: per-stage s_memtime of wave 0 ([grid][16]) or nullptr
+  unsigned long long* stamps;  // diagnostic build only: per-stage s_memtime of wave 0 ([window][16]) or nullptr
 };
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-// acc[rb][j] = A'[rows of block rb][K] . W[n][K]^T for this wave's column blocks cb = wid + 4*j (NCB % 4 == 0).
-// A: LDS [SW_ROWS][lda], row index clamped to the zero row (SW_ROWS-1). With LN, A' = (A - mean_r)*rstd_r*w + b
-// (row statistics from `stats`, LN affine parameters from LDS) is applied to the fragments as they are read, so no
-// normalised copy of the tile is stored. W: global [N][K], fragments loaded up front. MFMAs are issued
-// component-outer so 4*NJ independent accumulators separate dependent ones.
+__device__ __forceinline__ float dot4_acc(float4 a, float4 b, float acc) {
+  acc = fmaf(a.x, b.x, acc);
+  acc = fmaf(a.y, b.y, acc);
+  acc = fmaf(a.z, b.z, acc);
+  return fmaf(a.w, b.w, acc);
+}
+
+// sum over the four lane groups g = lane >> 4 (lanes l, l^16, l^32, l^48)
+__device__ __forceinline__ float group4_sum(float v) { return xor32_sum(xor16_sum(v)); }
+
+// Weight fragments of one GEMM stage for this wave: column blocks cb = wid + 4*j, lane (g, l15) holds
+// W[cb*16 + l15][g*K/4 .. (g+1)*K/4) as float4s. Loaded one stage ahead (issued before the previous stage's
+// barrier) so the L2 latency overlaps that stage instead of stalling the first MFMAs.
+template <int K, int NCB>
+struct WFrag {
+  float4 v[NCB / 4][K / 16];
+};
+
+template <int K, int NCB>
+__device__ __forceinline__ void load_wfrag(const float* __restrict__ Wg, WFrag<K, NCB>& f, int abl, int tid) {
+  const int lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l15 = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int t = 0; t < K / 16; ++t)
+#pragma unroll
+    for (int j = 0; j < NCB / 4; ++j) {
+      const float* wr = Wg + (long)((wid + 4 * j) * 16 + l15) * K + g * (K / 4);
+      f.v[j][t] = (abl & 2) ? make_float4(0.f, 0.f, 0.f, 0.f) : *reinterpret_cast<const float4*>(wr + 4 * t);
+    }
+}
+
+// acc[rb][j] = A'[rows rb*16 .. rb*16+15][K] . W[n][K]^T (rb < 3: token rows 0..47 on MFMA) and ext[j] = the same
+// for token row 48 on the VALU, for this wave's column blocks cb = wid + 4*j (NCB % 4 == 0), n = cb*16 + l15.
+// The MFMA k index is permuted: lane group g owns k in [g*K/4, (g+1)*K/4), so A and W fragments are 16-byte loads;
+// the row-48 dot products reuse the W fragments already in registers (partial over the lane's k quarter, then a
+// cross-group sum), so the fourth 16-row block - 15 of its 16 rows padding - is never issued.
+// A: LDS [SW_ROWS][lda]. With LN, A' = (A - mean_r)*rstd_r*w + b (row statistics from `stats`, LN affine params
+// from LDS), applied to the fragments as they are read. W: the stage's prefetched fragments.
 template <int K, int NCB, bool LN>
-__device__ __forceinline__ void wave_gemm_rows(const float* __restrict__ As, int lda, const float* __restrict__ Wg,
-                                               f32x4 (&acc)[4][NCB / 4], const float* stats, const float* lnw,
-                                               const float* lnb, int abl) {
+__device__ __forceinline__ void wave_gemm_rows(const float* __restrict__ As, int lda, const WFrag<K, NCB>& wf,
+                                               f32x4 (&acc)[3][NCB / 4], float (&ext)[NCB / 4], const float* stats,
+                                               const float* lnw, const float* lnb, int tid) {
   constexpr int NJ = NCB / 4;
   static_assert(NCB % 4 == 0, "column blocks must split evenly over the 4 waves");
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int lane = tid & 63;
   const int l15 = lane & 15, g = lane >> 4;
   constexpr int KQ = K / 4;  // k range per lane group
-  float4 bw[NJ][KQ / 4];
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const float* wr = Wg + (long)((wid + 4 * j) * 16 + l15) * K + g * KQ;
-#pragma unroll
-    for (int t = 0; t < KQ / 4; ++t)
-      bw[j][t] = (abl & 2) ? make_float4(0.f, 0.f, 0.f, 0.f) : *reinterpret_cast<const float4*>(wr + 4 * t);
-  }
+  const auto& bw = wf.v;
   const float* arow[4];
   float mu[4], rs[4];
 #pragma unroll
   for (int rb = 0; rb < 4; ++rb) {
-    int r = rb * 16 + l15;
-    r = r < SW_ROWS - 1 ? r : SW_ROWS - 1;
+    const int r = rb < 3 ? rb * 16 + l15 : XR;
     arow[rb] = As + r * lda + g * KQ;
     if (LN) {
       mu[rb] = stats[2 * r];
@@ -94,9 +121,11 @@ __device__ __forceinline__ void wave_gemm_rows(const float* __restrict__ As, int
     }
   }
 #pragma unroll
-  for (int rb = 0; rb < 4; ++rb)
+  for (int j = 0; j < NJ; ++j) {
+    ext[j] = 0.f;
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[rb][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int rb = 0; rb < 3; ++rb) acc[rb][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
 #pragma unroll
   for (int t = 0; t < KQ / 4; ++t) {
     float4 a[4];
@@ -116,22 +145,25 @@ __device__ __forceinline__ void wave_gemm_rows(const float* __restrict__ As, int
 #pragma unroll
     for (int c = 0; c < 4; ++c)
 #pragma unroll
-      for (int rb = 0; rb < 4; ++rb)
+      for (int rb = 0; rb < 3; ++rb)
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
           const float av = c == 0 ? a[rb].x : c == 1 ? a[rb].y : c == 2 ? a[rb].z : a[rb].w;
           const float bv = c == 0 ? bw[j][t].x : c == 1 ? bw[j][t].y : c == 2 ? bw[j][t].z : bw[j][t].w;
           acc[rb][j] = mfma4(av, bv, acc[rb][j]);
         }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) ext[j] = dot4_acc(a[3], bw[j][t], ext[j]);
   }
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) ext[j] = group4_sum(ext[j]);
 }
 
 // Row statistics (mean, rstd) of rows [0, SW_ROWS) of S[SW_ROWS][lds] over C: 4 threads per row (all rows at
 // once), each with C/4 values from float4 LDS reads, two-pass, DPP quad reductions; rows >= L get (0, 0).
 template <int C>
-__device__ __forceinline__ void lds_row_stats(const float* S, int lds, float* stats, int L, float eps) {
+__device__ __forceinline__ void lds_row_stats(const float* S, int lds, float* stats, int L, float eps, int tid) {
   constexpr int CP = C / 4;
-  const int tid = threadIdx.x;
   const int r = tid >> 2, qd = tid & 3;
   const bool valid = r < L;
   float4 v[CP / 4];
@@ -158,7 +190,10 @@ __device__ __forceinline__ void lds_row_stats(const float* S, int lds, float* st
 #define YS_STAMP(k)                                                                  \
   if (p.stamps && tid == 0) p.stamps[gw * 16 + (k)] = __builtin_amdgcn_s_memtime();
 
-template <int C, int NH, bool W7>
+// Persistent: each workgroup walks a strided sequence of windows inside its XCD's contiguous window range
+// (workgroup i runs on XCD i % 8; neighbouring windows share 128-B lines of x and y - a window row is 28 B - so
+// they meet in one L2). The next window's halo is loaded into registers during the current window's last stage.
+template <int C, int NH, bool W7, bool PERSIST>
 __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
   constexpr int HD = C / NH;
   constexpr int HID = 2 * C;
@@ -168,8 +203,10 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
   constexpr int NR = (C * 9 + 255) / 256;  // halo rows (of <= 9 floats) per thread
   static_assert(HD % 16 == 0 && HD <= 64, "head dim");
   static_assert(LH <= LQ, "MLP hidden must fit the QKV region");
-  // T: residual stream; Q: x halo patch (stage 0) -> QKV (O overwrites each wave's own query columns) -> hidden;
-  // stats: per-row (mean, rstd); lnp: LN1/LN2 affine parameters
+  static_assert(256 % C == 0 || C % 256 == 0, "depthwise channel mapping");
+  static_assert(C * 9 * HPW <= SW_ROWS * LQ, "halo patch must fit the QKV region");
+  // T: residual stream; Q: x halo patch [C][PH][HPW] (stage 0) -> QKV (O overwrites each wave's own query
+  // columns) -> MLP hidden; stats: per-row (mean, rstd); lnp: LN1/LN2 affine parameters
   __shared__ __attribute__((aligned(16))) float smem[SW_ROWS * LT + SW_ROWS * LQ + 2 * SW_ROWS + 4 * C];
   float* T = smem;
   float* Q = smem + SW_ROWS * LT;
@@ -181,17 +218,23 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
   const int wh = W7 ? 7 : p.wh, ww = W7 ? 7 : p.ww, L = W7 ? 49 : p.L;
   const int H = p.H, W = p.W;
   const long HWl = (long)H * W;
-  const int PH = wh + 2, PW = ww + 2, PP = PH * PW;
-  const long total = (long)p.B * p.nWin;
+  const int PH = wh + 2, PW = ww + 2;
 
-  // persistent: loop-invariant LN parameters (LDS) and depthwise taps (registers)
+  const long nwin_total = (long)p.B * p.nWin;
+  const long per_xcd = (nwin_total + 7) >> 3;
+  const long wpx = gridDim.x >> 3;
+  const long xbeg = (long)(blockIdx.x & 7) * per_xcd;
+  const long xend = (xbeg + per_xcd < nwin_total) ? xbeg + per_xcd : nwin_total;
+  long gw = xbeg + (blockIdx.x >> 3);
+  if (gw >= xend) return;
+
+  // loop-invariant: LN parameters (LDS), depthwise taps of this thread's channel (registers)
   for (int e = tid; e < 4 * C; e += 256) {
     const int which = e / C, c = e - which * C;
     const float* src = which == 0 ? p.ln1_w : which == 1 ? p.ln1_b : which == 2 ? p.ln2_w : p.ln2_b;
     lnp[e] = src[c];
   }
-  constexpr int TG = 256 / C;
-  const int dw_c = tid % C, dw_tg = tid / C;
+  const int dw_c = tid % C;
   float dwk[9];
 #pragma unroll
   for (int i = 0; i < 9; ++i) dwk[i] = p.dw[dw_c * 9 + i];
@@ -217,269 +260,272 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
       }
     }
   };
-  // one window per workgroup, XCD-aware: workgroup i runs on XCD i % 8, so each XCD gets a contiguous range of
-  // windows and neighbouring windows (which share 128-B lines of x and y: a window row is only 28 B wide) meet in
-  // the same L2 instead of each XCD fetching / partially writing back the same lines.
-  const long nwin_total = (long)p.B * p.nWin;
-  const long per_xcd = (nwin_total + 7) >> 3;
-  const long gw = (long)(blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
-  if (gw >= nwin_total) return;
   load_halo(gw);
-  const float* w_in = p.win;
-  const float* w_o = p.wo;
-  const float* w_1 = p.w1;
-  const float* w_2 = p.w2;
-  const float* w_pw = p.wpw;
-  const int img = (int)(gw / p.nWin), win = (int)(gw % p.nWin);
-  const int wy = win / p.nWx, wx = win % p.nWx;
-  const float* xb = p.x + (long)img * C * HWl;
-  YS_STAMP(0)
 
-  // ---- stage 0: halo patch (prefetched) -> LDS -> dw conv -> T (rows >= L and the zero row are 0) ----
+  for (;;) {
+    const long gnext = gw + wpx;
+    const bool has_next = PERSIST && gnext < xend;
+    const int img = (int)(gw / p.nWin), win = (int)(gw % p.nWin);
+    const int wy = win / p.nWx, wx = win % p.nWx;
+    const float* xb = p.x + (long)img * C * HWl;
+    // parameter pointers laundered per window: otherwise the compiler hoists every (loop-invariant) weight
+    // fragment and bias load out of the window loop and spills them
+    const float *w_in = p.win, *b_in = p.bin, *w_o = p.wo, *b_o = p.bo, *w_1 = p.w1, *b_1 = p.b1, *w_2 = p.w2,
+                *b_2 = p.b2, *w_pw = p.wpw, *bn_sc = p.bn_scale, *bn_sh = p.bn_shift;
+    asm volatile("" : "+s"(w_in), "+s"(b_in), "+s"(w_o), "+s"(b_o), "+s"(w_1), "+s"(b_1));
+    asm volatile("" : "+s"(w_2), "+s"(b_2), "+s"(w_pw), "+s"(bn_sc), "+s"(bn_sh));
+    YS_STAMP(0)
+    // QKV weight fragments: in flight during the halo store, the depthwise conv and the LN1 statistics
+    WFrag<C, 3 * C / 16> f_in;
+    load_wfrag(w_in, f_in, p.abl, tid);
+
+    // ---- stage 0: halo patch (registers) -> LDS [c][py][HPW] -> dw conv, one output row of 7 tokens per item ----
 #pragma unroll
-  for (int i = 0; i < NR; ++i) {
-    const int rr = tid + 256 * i;
-    if (rr < C * PH) {
-#pragma unroll
-      for (int px = 0; px < 9; ++px)
-        if (px < PW) Q[rr * PW + px] = hv[i][px];
-    }
-  }
-  __syncthreads();
-  YS_STAMP(1)
-  {
-    // thread -> channel c (taps in registers), tokens tok = tg, tg + TG, ...
-    const float* pcb = Q + dw_c * PP;
-    for (int tok = dw_tg; tok < SW_ROWS; tok += TG) {
-      float v = 0.f;
-      if (tok < L) {
-        const int iy = tok / ww, ix = tok - iy * ww;
-        const int hh = wy * wh + iy, wc = wx * ww + ix;
-        if (hh < H && wc < W) {
-          const float* pc = pcb + iy * PW + ix;
-          v = dwk[0] * pc[0] + dwk[1] * pc[1] + dwk[2] * pc[2] + dwk[3] * pc[PW] + dwk[4] * pc[PW + 1] +
-              dwk[5] * pc[PW + 2] + dwk[6] * pc[2 * PW] + dwk[7] * pc[2 * PW + 1] + dwk[8] * pc[2 * PW + 2];
-        }
+    for (int i = 0; i < NR; ++i) {
+      const int rr = tid + 256 * i;
+      if (rr < C * PH) {
+        float4* dst = reinterpret_cast<float4*>(Q + rr * HPW);
+        dst[0] = make_float4(hv[i][0], hv[i][1], hv[i][2], hv[i][3]);
+        dst[1] = make_float4(hv[i][4], hv[i][5], hv[i][6], hv[i][7]);
+        dst[2] = make_float4(hv[i][8], 0.f, 0.f, 0.f);
       }
-      T[tok * LT + dw_c] = v;
     }
-  }
-  __syncthreads();
-  YS_STAMP(2)
-
-  // ---- stage 1: LN1 row statistics; zero row of Q ----
-  lds_row_stats<C>(T, LT, stats, L, p.ln1_eps);
-  for (int c = tid; c < LQ; c += 256) Q[(SW_ROWS - 1) * LQ + c] = 0.f;
-  __syncthreads();
-  YS_STAMP(3)
-
-  // ---- stage 2: QKV = LN1(T) Win^T + b_in ----
-  {
-    constexpr int NCB = 3 * C / 16;
-    constexpr int NJ = NCB / 4;
-    f32x4 acc[4][NJ];
-    wave_gemm_rows<C, NCB, true>(T, LT, w_in, acc, stats, lnp, lnp + C, p.abl);
+    __syncthreads();
+    YS_STAMP(1)
+    for (int item = tid; item < C * wh; item += 256) {
+      const int iy = item / C;  // item % C == dw_c (256 % C == 0)
+      const float* hp = Q + (dw_c * PH + iy) * HPW;
+      float r[3][12];
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int n = (wid + 4 * j) * 16 + l15;
-      const float bias = p.bin[n];
+      for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
-      for (int rb = 0; rb < 4; ++rb)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = rb * 16 + g * 4 + r;
-          if (row < SW_ROWS - 1) Q[row * LQ + n] = acc[rb][j][r] + bias;
+        for (int q4 = 0; q4 < 3; ++q4) {
+          const float4 v = *reinterpret_cast<const float4*>(hp + ky * HPW + 4 * q4);
+          r[ky][4 * q4] = v.x; r[ky][4 * q4 + 1] = v.y; r[ky][4 * q4 + 2] = v.z; r[ky][4 * q4 + 3] = v.w;
         }
+      const bool rowok = wy * wh + iy < H;
+#pragma unroll
+      for (int ix = 0; ix < 7; ++ix) {
+        if (!W7 && ix >= ww) break;
+        const float v = dwk[0] * r[0][ix] + dwk[1] * r[0][ix + 1] + dwk[2] * r[0][ix + 2] + dwk[3] * r[1][ix] +
+                        dwk[4] * r[1][ix + 1] + dwk[5] * r[1][ix + 2] + dwk[6] * r[2][ix] + dwk[7] * r[2][ix + 1] +
+                        dwk[8] * r[2][ix + 2];
+        T[(iy * ww + ix) * LT + dw_c] = (rowok && wx * ww + ix < W) ? v : 0.f;
+      }
     }
-  }
-  __syncthreads();
-  YS_STAMP(4)
+    if (!W7 && L < SW_ROWS)
+      for (int e = tid; e < (SW_ROWS - L) * C; e += 256) T[(L + e / C) * LT + e % C] = 0.f;
+    __syncthreads();
+    YS_STAMP(2)
 
-  // ---- stage 3: attention, wave = query block (16 queries), all heads interleaved ----
-  // The output O[q][h*HD + d] overwrites the query columns of the wave's own rows (read only by this wave).
-  {
-    const int qb = wid;
-    int qrow = qb * 16 + l15;
-    qrow = qrow < SW_ROWS - 1 ? qrow : SW_ROWS - 1;
-    constexpr int DQ = HD / 4;  // d range per lane group
-    f32x4 st[NH][4];
+    // ---- stage 1: LN1 row statistics ----
+    lds_row_stats<C>(T, LT, stats, L, p.ln1_eps, tid);
+    __syncthreads();
+    YS_STAMP(3)
+
+    // ---- stage 2: QKV = LN1(T) Win^T + b_in ----
+    {
+      constexpr int NCB = 3 * C / 16;
+      constexpr int NJ = NCB / 4;
+      f32x4 acc[3][NJ];
+      float ext[NJ];
+      wave_gemm_rows<C, NCB, true>(T, LT, f_in, acc, ext, stats, lnp, lnp + C, tid);
 #pragma unroll
-    for (int h = 0; h < NH; ++h)
+      for (int j = 0; j < NJ; ++j) {
+        const int n = (wid + 4 * j) * 16 + l15;
+        const float bias = b_in[n];
 #pragma unroll
-      for (int kb = 0; kb < 4; ++kb) st[h][kb] = f32x4{0.f, 0.f, 0.f, 0.f};
-    int krow[4];
+        for (int rb = 0; rb < 3; ++rb)
 #pragma unroll
-    for (int kb = 0; kb < 4; ++kb) {
-      const int kr = kb * 16 + l15;
-      krow[kb] = kr < SW_ROWS - 1 ? kr : SW_ROWS - 1;
+          for (int r = 0; r < 4; ++r) Q[(rb * 16 + g * 4 + r) * LQ + n] = acc[rb][j][r] + bias;
+        if (g == 0) Q[XR * LQ + n] = ext[j] + bias;
+      }
     }
-#pragma unroll
-    for (int t = 0; t < DQ / 4; ++t) {
-      float4 qv[NH], kv[NH][4];
+    WFrag<C, C / 16> f_o;  // out-proj weights: in flight during attention
+    load_wfrag(w_o, f_o, p.abl, tid);
+    __syncthreads();
+    YS_STAMP(4)
+
+    // ---- stage 3: attention, wave = query block (16 queries), all heads interleaved ----
+    // Keys 0..47 on MFMA (S^T accumulators reused as the B operand of O^T = V^T P^T), key 48 on the VALU. The
+    // output O[q][h*HD + d] overwrites the query columns of the wave's own rows (read only by this wave).
+    {
+      const int qb = wid;
+      int qrow = qb * 16 + l15;
+      qrow = qrow < XR ? qrow : XR;
+      constexpr int DQ = HD / 4;  // d range per lane group
+      f32x4 st[NH][3];
+      float s48[NH];
 #pragma unroll
       for (int h = 0; h < NH; ++h) {
-        qv[h] = *reinterpret_cast<const float4*>(Q + qrow * LQ + h * HD + g * DQ + 4 * t);
+        s48[h] = 0.f;
 #pragma unroll
-        for (int kb = 0; kb < 4; ++kb)
-          kv[h][kb] = *reinterpret_cast<const float4*>(Q + krow[kb] * LQ + C + h * HD + g * DQ + 4 * t);
+        for (int kb = 0; kb < 3; ++kb) st[h][kb] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
 #pragma unroll
-      for (int c = 0; c < 4; ++c)
+      for (int t = 0; t < DQ / 4; ++t) {
+        float4 qv[NH], kv[NH][3], k48[NH];
 #pragma unroll
-        for (int h = 0; h < NH; ++h)
+        for (int h = 0; h < NH; ++h) {
+          qv[h] = *reinterpret_cast<const float4*>(Q + qrow * LQ + h * HD + g * DQ + 4 * t);
 #pragma unroll
-          for (int kb = 0; kb < 4; ++kb) {
-            const float kk = c == 0 ? kv[h][kb].x : c == 1 ? kv[h][kb].y : c == 2 ? kv[h][kb].z : kv[h][kb].w;
-            const float qq = c == 0 ? qv[h].x : c == 1 ? qv[h].y : c == 2 ? qv[h].z : qv[h].w;
-            st[h][kb] = mfma4(kk, qq, st[h][kb]);
+          for (int kb = 0; kb < 3; ++kb)
+            kv[h][kb] = *reinterpret_cast<const float4*>(Q + (kb * 16 + l15) * LQ + C + h * HD + g * DQ + 4 * t);
+          k48[h] = *reinterpret_cast<const float4*>(Q + XR * LQ + C + h * HD + g * DQ + 4 * t);
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+          for (int h = 0; h < NH; ++h)
+#pragma unroll
+            for (int kb = 0; kb < 3; ++kb) {
+              const float kk = c == 0 ? kv[h][kb].x : c == 1 ? kv[h][kb].y : c == 2 ? kv[h][kb].z : kv[h][kb].w;
+              const float qq = c == 0 ? qv[h].x : c == 1 ? qv[h].y : c == 2 ? qv[h].z : qv[h].w;
+              st[h][kb] = mfma4(kk, qq, st[h][kb]);
+            }
+#pragma unroll
+        for (int h = 0; h < NH; ++h) s48[h] = dot4_acc(k48[h], qv[h], s48[h]);
+      }
+      // lane holds S^T[key = kb*16 + 4g + r][q = l15] per head (+ key 48 after the group sum): softmax over keys
+      float p48[NH];
+#pragma unroll
+      for (int h = 0; h < NH; ++h) {
+        const bool k48ok = XR < L;
+        const float sv48 = k48ok ? group4_sum(s48[h]) * p.scale : -INFINITY;
+        float mx = sv48;
+#pragma unroll
+        for (int kb = 0; kb < 3; ++kb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int key = kb * 16 + 4 * g + r;
+            const float sv = (key < L) ? st[h][kb][r] * p.scale : -INFINITY;
+            st[h][kb][r] = sv;
+            mx = fmaxf(mx, sv);
           }
-    }
-    // lane holds S^T[key = kb*16 + 4g + r][q = l15] per head: softmax over keys (in-lane, then lane groups)
+        mx = xor32_max(xor16_max(mx));
+        float sum = 0.f;
 #pragma unroll
-    for (int h = 0; h < NH; ++h) {
-      float mx = -INFINITY;
+        for (int kb = 0; kb < 3; ++kb)
 #pragma unroll
-      for (int kb = 0; kb < 4; ++kb)
+          for (int r = 0; r < 4; ++r) {
+            const float e = __expf(st[h][kb][r] - mx);
+            st[h][kb][r] = e;
+            sum += e;
+          }
+        const float e48 = __expf(sv48 - mx);
+        sum += (g == 0) ? e48 : 0.f;
+        sum = group4_sum(sum);
+        const float inv = 1.0f / sum;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = kb * 16 + 4 * g + r;
-          const float sv = (key < L) ? st[h][kb][r] * p.scale : -INFINITY;
-          st[h][kb][r] = sv;
-          mx = fmaxf(mx, sv);
-        }
-      mx = xor32_max(xor16_max(mx));
-      float sum = 0.f;
+        for (int kb = 0; kb < 3; ++kb)
 #pragma unroll
-      for (int kb = 0; kb < 4; ++kb)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float e = __expf(st[h][kb][r] - mx);
-          st[h][kb][r] = e;
-          sum += e;
-        }
-      sum = xor32_sum(xor16_sum(sum));
-      const float inv = 1.0f / sum;
-#pragma unroll
-      for (int kb = 0; kb < 4; ++kb)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) st[h][kb][r] *= inv;
-    }
-    // O^T[d][q] = sum_key V[key][d] P[q][key]; MFMA (kb, r) consumes keys {kb*16 + 4g' + r}
-    f32x4 o[NH][HD / 16];
-#pragma unroll
-    for (int h = 0; h < NH; ++h)
-#pragma unroll
-      for (int db = 0; db < HD / 16; ++db) o[h][db] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int kb = 0; kb < 4; ++kb)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        int key = kb * 16 + 4 * g + r;
-        key = key < SW_ROWS - 1 ? key : SW_ROWS - 1;
-        const float* vrow = Q + key * LQ + 2 * C + l15;
-#pragma unroll
-        for (int h = 0; h < NH; ++h)
-#pragma unroll
-          for (int db = 0; db < HD / 16; ++db) o[h][db] = mfma4(vrow[h * HD + db * 16], st[h][kb][r], o[h][db]);
+          for (int r = 0; r < 4; ++r) st[h][kb][r] *= inv;
+        p48[h] = e48 * inv;
       }
-    // lane holds O^T[d = db*16 + 4g + r][q = l15] -> O[q][h*HD + d] (4 consecutive d) into the q columns
-    const int q = qb * 16 + l15;
-    if (q < L) {
+      // O^T[d][q] = sum_key V[key][d] P[q][key]; MFMA (kb, r) consumes keys {kb*16 + 4g' + r}; key 48 rank-1 update
+      f32x4 o[NH][HD / 16];
 #pragma unroll
       for (int h = 0; h < NH; ++h)
 #pragma unroll
-        for (int db = 0; db < HD / 16; ++db)
-          *reinterpret_cast<f32x4*>(Q + q * LQ + h * HD + db * 16 + 4 * g) = o[h][db];
-    }
-  }
-  __syncthreads();
-  YS_STAMP(5)
-
-  // ---- stage 4: T += O Wo^T + bo ----
-  {
-    constexpr int NCB = C / 16;
-    constexpr int NJ = NCB / 4;
-    f32x4 acc[4][NJ];
-    wave_gemm_rows<C, NCB, false>(Q, LQ, w_o, acc, nullptr, nullptr, nullptr, p.abl);
+        for (int db = 0; db < HD / 16; ++db) o[h][db] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int n = (wid + 4 * j) * 16 + l15;
-      const float bias = p.bo[n];
-#pragma unroll
-      for (int rb = 0; rb < 4; ++rb)
+      for (int kb = 0; kb < 3; ++kb)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int row = rb * 16 + g * 4 + r;
-          if (row < L) T[row * LT + n] += acc[rb][j][r] + bias;
+          const float* vrow = Q + (kb * 16 + 4 * g + r) * LQ + 2 * C + l15;
+#pragma unroll
+          for (int h = 0; h < NH; ++h)
+#pragma unroll
+            for (int db = 0; db < HD / 16; ++db) o[h][db] = mfma4(vrow[h * HD + db * 16], st[h][kb][r], o[h][db]);
         }
-    }
-  }
-  __syncthreads();
-  YS_STAMP(6)
-
-  // ---- stage 5: LN2 row statistics ----
-  lds_row_stats<C>(T, LT, stats, L, p.ln2_eps);
-  __syncthreads();
-  YS_STAMP(7)
-
-  // ---- stage 6: Hd = GELU(LN2(T) W1^T + b1) -> Q region [rows][LH] ----
-  float* Hd = Q;
-  {
-    constexpr int NCB = HID / 16;
-    constexpr int NJ = NCB / 4;
-    f32x4 acc[4][NJ];
-    wave_gemm_rows<C, NCB, true>(T, LT, w_1, acc, stats, lnp + 2 * C, lnp + 3 * C, p.abl);
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int n = (wid + 4 * j) * 16 + l15;
-      const float bias = p.b1[n];
+      for (int h = 0; h < NH; ++h)
 #pragma unroll
-      for (int rb = 0; rb < 4; ++rb)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = rb * 16 + g * 4 + r;
-          if (row < SW_ROWS - 1) Hd[row * LH + n] = gelu_fast_(acc[rb][j][r] + bias);
+        for (int db = 0; db < HD / 16; ++db) {
+          const float4 v48 = *reinterpret_cast<const float4*>(Q + XR * LQ + 2 * C + h * HD + db * 16 + 4 * g);
+          o[h][db][0] = fmaf(v48.x, p48[h], o[h][db][0]);
+          o[h][db][1] = fmaf(v48.y, p48[h], o[h][db][1]);
+          o[h][db][2] = fmaf(v48.z, p48[h], o[h][db][2]);
+          o[h][db][3] = fmaf(v48.w, p48[h], o[h][db][3]);
         }
+      // lane holds O^T[d = db*16 + 4g + r][q = l15] -> O[q][h*HD + d] (4 consecutive d) into the q columns
+      const int q = qb * 16 + l15;
+      if (q < L) {
+#pragma unroll
+        for (int h = 0; h < NH; ++h)
+#pragma unroll
+          for (int db = 0; db < HD / 16; ++db)
+            *reinterpret_cast<f32x4*>(Q + q * LQ + h * HD + db * 16 + 4 * g) = o[h][db];
+      }
     }
-    for (int c = tid; c < LH; c += 256) Hd[(SW_ROWS - 1) * LH + c] = 0.f;
-  }
-  __syncthreads();
-  YS_STAMP(8)
+    __syncthreads();
+    YS_STAMP(5)
 
-  // ---- stage 7: T += Hd W2^T + b2 ----
-  {
-    constexpr int NCB = C / 16;
-    constexpr int NJ = NCB / 4;
-    f32x4 acc[4][NJ];
-    wave_gemm_rows<HID, NCB, false>(Hd, LH, w_2, acc, nullptr, nullptr, nullptr, p.abl);
+    // ---- stage 4: T += O Wo^T + bo ----
+    {
+      constexpr int NCB = C / 16;
+      constexpr int NJ = NCB / 4;
+      f32x4 acc[3][NJ];
+      float ext[NJ];
+      wave_gemm_rows<C, C / 16, false>(Q, LQ, f_o, acc, ext, nullptr, nullptr, nullptr, tid);
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int n = (wid + 4 * j) * 16 + l15;
-      const float bias = p.b2[n];
+      for (int j = 0; j < NJ; ++j) {
+        const int n = (wid + 4 * j) * 16 + l15;
+        const float bias = b_o[n];
 #pragma unroll
-      for (int rb = 0; rb < 4; ++rb)
+        for (int rb = 0; rb < 3; ++rb)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = rb * 16 + g * 4 + r;
-          if (row < L) T[row * LT + n] += acc[rb][j][r] + bias;
-        }
+          for (int r = 0; r < 4; ++r) {
+            const int row = rb * 16 + g * 4 + r;
+            if (row < L) T[row * LT + n] += acc[rb][j][r] + bias;
+          }
+        if (g == 0 && XR < L) T[XR * LT + n] += ext[j] + bias;
+      }
     }
-  }
-  __syncthreads();
-  YS_STAMP(9)
+    WFrag<C, HID / 16> f_1;  // MLP1 weights: in flight during the LN2 statistics
+    load_wfrag(w_1, f_1, p.abl, tid);
+    __syncthreads();
+    YS_STAMP(6)
 
-  // ---- stage 8: y = x + SiLU(BN(Wpw T^T)); output tile Y^T[c][tok] (lanes over tokens) ----
-  {
-    constexpr int NCB = C / 16;
-    constexpr int CQ = C / 4;
-    float* yb = p.y + (long)img * C * HWl;
-    for (int cb = wid; cb < NCB; cb += 4) {
-      const float* wrow = w_pw + (long)(cb * 16 + l15) * C + g * CQ;
-      // residual x and BN terms first (their latency overlaps the MFMAs)
-      long pix[4];
-      float xr[4][4];
+    // ---- stage 5: LN2 row statistics ----
+    lds_row_stats<C>(T, LT, stats, L, p.ln2_eps, tid);
+    __syncthreads();
+    YS_STAMP(7)
+
+    // ---- stage 6: Hd = GELU(LN2(T) W1^T + b1) -> Q region [rows][LH] ----
+    float* Hd = Q;
+    {
+      constexpr int NCB = HID / 16;
+      constexpr int NJ = NCB / 4;
+      f32x4 acc[3][NJ];
+      float ext[NJ];
+      wave_gemm_rows<C, HID / 16, true>(T, LT, f_1, acc, ext, stats, lnp + 2 * C, lnp + 3 * C, tid);
 #pragma unroll
-      for (int tb = 0; tb < 4; ++tb) {
+      for (int j = 0; j < NJ; ++j) {
+        const int n = (wid + 4 * j) * 16 + l15;
+        const float bias = b_1[n];
+#pragma unroll
+        for (int rb = 0; rb < 3; ++rb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) Hd[(rb * 16 + g * 4 + r) * LH + n] = gelu_fast_(acc[rb][j][r] + bias);
+        if (g == 0) Hd[XR * LH + n] = gelu_fast_(ext[j] + bias);
+      }
+    }
+    WFrag<HID, C / 16> f_2;  // MLP2 weights
+    load_wfrag(w_2, f_2, p.abl, tid);
+    __syncthreads();
+    YS_STAMP(8)
+
+    // stage-8 residual x (L2-hot: this window's halo) and BN terms of this wave's first channel block, loaded
+    // here so their latency overlaps MLP2
+    const int iy48 = XR / ww, ix48 = XR - (XR / ww) * ww;
+    const long pix48 = (XR < L && wy * wh + iy48 < H && wx * ww + ix48 < W)
+                           ? (long)(wy * wh + iy48) * W + wx * ww + ix48 : -1;
+    long pix[3];
+    float xr[3][4], x48, bsc[4], bsh[4];
+    auto load_resid = [&](int cb) {
+#pragma unroll
+      for (int tb = 0; tb < 3; ++tb) {
         const int tok = tb * 16 + l15;
         const int iy = tok / ww, ix = tok - iy * ww;
         const int hh = wy * wh + iy, wc = wx * ww + ix;
@@ -488,49 +534,102 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
         for (int r = 0; r < 4; ++r)
           xr[tb][r] = (pix[tb] >= 0 && !(p.abl & 4)) ? xb[(long)(cb * 16 + 4 * g + r) * HWl + pix[tb]] : 0.f;
       }
-      float bsc[4], bsh[4];
+      x48 = (pix48 >= 0 && g == 0 && !(p.abl & 4)) ? xb[(long)(cb * 16 + l15) * HWl + pix48] : 0.f;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        bsc[r] = p.bn_scale[cb * 16 + 4 * g + r];
-        bsh[r] = p.bn_shift[cb * 16 + 4 * g + r];
+        bsc[r] = bn_sc[cb * 16 + 4 * g + r];
+        bsh[r] = bn_sh[cb * 16 + 4 * g + r];
       }
-      f32x4 acc[4];
+    };
+    load_resid(wid);
+
+    // ---- stage 7: T += Hd W2^T + b2 ----
+    {
+      constexpr int NCB = C / 16;
+      constexpr int NJ = NCB / 4;
+      f32x4 acc[3][NJ];
+      float ext[NJ];
+      wave_gemm_rows<HID, C / 16, false>(Hd, LH, f_2, acc, ext, nullptr, nullptr, nullptr, tid);
 #pragma unroll
-      for (int tb = 0; tb < 4; ++tb) acc[tb] = f32x4{0.f, 0.f, 0.f, 0.f};
-      float4 wa[CQ / 4];
+      for (int j = 0; j < NJ; ++j) {
+        const int n = (wid + 4 * j) * 16 + l15;
+        const float bias = b_2[n];
 #pragma unroll
-      for (int t = 0; t < CQ / 4; ++t) wa[t] = *reinterpret_cast<const float4*>(wrow + 4 * t);
+        for (int rb = 0; rb < 3; ++rb)
 #pragma unroll
-      for (int t = 0; t < CQ / 4; ++t) {
-        float4 bt[4];
-#pragma unroll
-        for (int tb = 0; tb < 4; ++tb) {
-          int tr = tb * 16 + l15;
-          tr = tr < SW_ROWS - 1 ? tr : SW_ROWS - 1;
-          bt[tb] = *reinterpret_cast<const float4*>(T + tr * LT + g * CQ + 4 * t);
-        }
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-#pragma unroll
-          for (int tb = 0; tb < 4; ++tb) {
-            const float av = c == 0 ? wa[t].x : c == 1 ? wa[t].y : c == 2 ? wa[t].z : wa[t].w;
-            const float bv = c == 0 ? bt[tb].x : c == 1 ? bt[tb].y : c == 2 ? bt[tb].z : bt[tb].w;
-            acc[tb] = mfma4(av, bv, acc[tb]);
+          for (int r = 0; r < 4; ++r) {
+            const int row = rb * 16 + g * 4 + r;
+            if (row < L) T[row * LT + n] += acc[rb][j][r] + bias;
           }
-      }
-      // lane holds Y^T[c = cb*16 + 4g + r][tok = tb*16 + l15]
-#pragma unroll
-      for (int tb = 0; tb < 4; ++tb) {
-        if (pix[tb] < 0) continue;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int c = cb * 16 + 4 * g + r;
-          yb[(long)c * HWl + pix[tb]] = xr[tb][r] + silu_fast_(acc[tb][r] * bsc[r] + bsh[r]);
-        }
+        if (g == 0 && XR < L) T[XR * LT + n] += ext[j] + bias;
       }
     }
+    // pw weights of this wave's first output-channel block
+    constexpr int CQ = C / 4;
+    float4 wa[CQ / 4];
+    {
+      const float* wrow = w_pw + (long)(wid * 16 + l15) * C + g * CQ;
+#pragma unroll
+      for (int t = 0; t < CQ / 4; ++t) wa[t] = *reinterpret_cast<const float4*>(wrow + 4 * t);
+    }
+    __syncthreads();
+    YS_STAMP(9)
+
+    // next window's halo: in flight during the last stage
+    if (has_next) load_halo(gnext);
+
+    // ---- stage 8: y = x + SiLU(BN(Wpw T^T)); output tile Y^T[c][tok] (lanes over tokens), token 48 on the VALU ----
+    {
+      constexpr int NCB = C / 16;
+      float* yb = p.y + (long)img * C * HWl;
+      for (int cb = wid; cb < NCB; cb += 4) {
+        const float* wrow = w_pw + (long)(cb * 16 + l15) * C + g * CQ;
+        if (cb != wid) load_resid(cb);
+        f32x4 acc[3];
+#pragma unroll
+        for (int tb = 0; tb < 3; ++tb) acc[tb] = f32x4{0.f, 0.f, 0.f, 0.f};
+        float e48 = 0.f;
+        if (cb != wid) {
+#pragma unroll
+          for (int t = 0; t < CQ / 4; ++t) wa[t] = *reinterpret_cast<const float4*>(wrow + 4 * t);
+        }
+#pragma unroll
+        for (int t = 0; t < CQ / 4; ++t) {
+          float4 bt[3];
+#pragma unroll
+          for (int tb = 0; tb < 3; ++tb)
+            bt[tb] = *reinterpret_cast<const float4*>(T + (tb * 16 + l15) * LT + g * CQ + 4 * t);
+          const float4 t48 = *reinterpret_cast<const float4*>(T + XR * LT + g * CQ + 4 * t);
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int tb = 0; tb < 3; ++tb) {
+              const float av = c == 0 ? wa[t].x : c == 1 ? wa[t].y : c == 2 ? wa[t].z : wa[t].w;
+              const float bv = c == 0 ? bt[tb].x : c == 1 ? bt[tb].y : c == 2 ? bt[tb].z : bt[tb].w;
+              acc[tb] = mfma4(av, bv, acc[tb]);
+            }
+          e48 = dot4_acc(wa[t], t48, e48);
+        }
+        e48 = group4_sum(e48);
+        // lane holds Y^T[c = cb*16 + 4g + r][tok = tb*16 + l15]
+#pragma unroll
+        for (int tb = 0; tb < 3; ++tb) {
+          if (pix[tb] < 0) continue;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int c = cb * 16 + 4 * g + r;
+            yb[(long)c * HWl + pix[tb]] = xr[tb][r] + silu_fast_(acc[tb][r] * bsc[r] + bsh[r]);
+          }
+        }
+        const int c48 = cb * 16 + l15;
+        if (g == 0 && pix48 >= 0)
+          yb[(long)c48 * HWl + pix48] = x48 + silu_fast_(e48 * bn_sc[c48] + bn_sh[c48]);
+      }
+    }
+    YS_STAMP(15)
+    if (!PERSIST || !has_next) break;
+    gw = gnext;
   }
-  YS_STAMP(15)
 }
 
 }  // namespace ys
@@ -571,7 +670,7 @@ int yolosod_swin_fused_launch(const float* x, float* y, int B, int C, int H, int
                               const float* mlp2_b, const float* pw_w, const float* bn_scale, const float* bn_shift,
                               hipStream_t st) {
   const int L = wh * ww;
-  if (L > SW_ROWS - 1 || (wh + 2) * (ww + 2) * C > SW_ROWS * (3 * C + 4) || mlp_hidden != 2 * C) return 0;
+  if (L > SW_ROWS || wh > 7 || ww > 7 || mlp_hidden != 2 * C) return 0;
   SwinFusedArgs a{x, y, B, H, W, wh, ww, nWx, nWin, L, dw_w, ln1_w, ln1_b, ln1_eps, in_proj_w, in_proj_b,
                   out_proj_w, out_proj_b, ln2_w, ln2_b, ln2_eps, mlp1_w, mlp1_b, mlp2_w, mlp2_b, pw_w,
                   bn_scale, bn_shift, 1.0f / sqrtf((float)(C / num_heads)), 0, nullptr};
@@ -589,13 +688,37 @@ int yolosod_swin_fused_launch(const float* x, float* y, int B, int C, int H, int
     g_stamp_n = need;
     a.stamps = g_stamps;
   }
-  // one window per workgroup (XCD-aware order, padded to a multiple of 8); 3 resident per CU (LDS 53 KB, 168 VGPRs)
-  dim3 grid((unsigned)(8 * (((long)B * nWin + 7) / 8)));
+  // persistent grid: (resident workgroups per CU) x CUs, a multiple of 8 (one range of windows per XCD), never
+  // more workgroups than windows; 3 resident per CU at C = 64 (LDS 52 KB)
   const bool w7 = (wh == 7 && ww == 7);
+  const long nwin = (long)B * nWin;
+  auto resident = [](const void* fn) -> long {
+    int dev = 0, cus = 256, per_cu = 1;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, 0) != hipSuccess || per_cu < 1) per_cu = 1;
+    if (const char* e = getenv("YOLOSOD_SWIN_WGS_PER_CU")) per_cu = atoi(e) > 0 ? atoi(e) : per_cu;
+    return (long)cus * per_cu;
+  };
+  auto grid_of = [&](long n) {
+    const long cap = 8 * ((nwin + 7) / 8);
+    if (n > cap) n = cap;
+    return dim3((unsigned)(8 * ((n + 7) / 8)));
+  };
+  // default: one window per workgroup (grid = windows, XCD-aware order). YOLOSOD_SWIN_PERSIST=1: persistent
+  // workgroups with the next window's halo prefetched during the last stage (A/B: the window loop makes the
+  // compiler hoist and spill per-thread addresses at 3 workgroups per CU).
+  static const bool persist = [] { const char* e = getenv("YOLOSOD_SWIN_PERSIST"); return e && atoi(e) != 0; }();
 #define YS_SWF(CC, NHH)                                                                                  \
   if (C == CC && num_heads == NHH) {                                                                     \
-    if (w7) hipLaunchKernelGGL((swin_fused_kernel<CC, NHH, true>), grid, dim3(256), 0, st, a);           \
-    else hipLaunchKernelGGL((swin_fused_kernel<CC, NHH, false>), grid, dim3(256), 0, st, a);             \
+    if (w7 && persist) {                                                                                 \
+      static const long res = resident((const void*)swin_fused_kernel<CC, NHH, true, true>);             \
+      hipLaunchKernelGGL((swin_fused_kernel<CC, NHH, true, true>), grid_of(res), dim3(256), 0, st, a);   \
+    } else if (w7) {                                                                                     \
+      hipLaunchKernelGGL((swin_fused_kernel<CC, NHH, true, false>), grid_of(nwin), dim3(256), 0, st, a); \
+    } else {                                                                                             \
+      hipLaunchKernelGGL((swin_fused_kernel<CC, NHH, false, false>), grid_of(nwin), dim3(256), 0, st, a); \
+    }                                                                                                    \
   } else
   YS_SWF(64, 2) YS_SWF(64, 4) YS_SWF(128, 2) YS_SWF(128, 4) return 0;
 #undef YS_SWF
