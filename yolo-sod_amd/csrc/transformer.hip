@@ -370,6 +370,13 @@ int yolosod_swin_fused_launch(const float* x, float* y, int B, int C, int H, int
                               const float* mlp1_w, const float* mlp1_b, int mlp_hidden, const float* mlp2_w,
                               const float* mlp2_b, const float* pw_w, const float* bn_scale, const float* bn_shift,
                               hipStream_t st);
+int yolosod_swin_wide_launch(const float* x, float* y, int B, int C, int H, int W, int num_heads, int wh, int ww,
+                             int nWx, int nWin, const float* dw_w, const float* ln1_w, const float* ln1_b,
+                             float ln1_eps, const float* in_proj_w, const float* in_proj_b, const float* out_proj_w,
+                             const float* out_proj_b, const float* ln2_w, const float* ln2_b, float ln2_eps,
+                             const float* mlp1_w, const float* mlp1_b, int mlp_hidden, const float* mlp2_w,
+                             const float* mlp2_b, const float* pw_w, const float* bn_scale, const float* bn_shift,
+                             hipStream_t st);
 
 static int g_swin_fused = -1;  // -1: from YOLOSOD_SWIN_FUSED (default on)
 
@@ -384,9 +391,16 @@ static bool swin_fused_enabled() {
 // Test hook: route SwinBlock through the fused per-window kernel (1) or the decomposed GEMM path (0).
 YS_EXPORT void yolosod_debug_set_swin_fused(int on) { g_swin_fused = on ? 1 : 0; }
 
-// shapes the fused per-window kernel (swin_fused.hip) handles
-static bool swin_fused_ok(int C, int heads, int L, int mlp_hidden) {
-  if (!swin_fused_enabled() || L > 49 || mlp_hidden != 2 * C) return false;
+static bool swin_wide_enabled() {
+  static const bool on = [] { const char* e = getenv("YOLOSOD_SWIN_WIDE"); return !e || atoi(e) != 0; }();
+  return on;
+}
+
+// shapes the fused per-window kernels handle: swin_fused.hip (C <= 128, windows of <= 49 tokens) and
+// swin_wide.hip (C = 256 with 4 heads of 64, 7x7 windows)
+static bool swin_fused_ok(int C, int heads, int wh, int ww, int mlp_hidden) {
+  if (!swin_fused_enabled() || wh * ww > 49 || mlp_hidden != 2 * C) return false;
+  if (C == 256 && heads == 4) return swin_wide_enabled() && wh == 7 && ww == 7;
   return (C == 64 && (heads == 2 || heads == 4)) || (C == 128 && (heads == 2 || heads == 4));
 }
 
@@ -459,7 +473,7 @@ __global__ void fold_bn_kernel(const float* w, const float* b, const float* m, c
 YS_EXPORT size_t yolosod_swin_workspace_v2(int B, int C, int H, int W, int num_heads, int window,
                                            int mlp_hidden) {
   SwinGeom g = swin_geom(B, H, W, window);
-  if (swin_fused_ok(C, num_heads, g.L, mlp_hidden)) {
+  if (swin_fused_ok(C, num_heads, g.wh, g.ww, mlp_hidden)) {
     Sizer s;
     s.take<float>((size_t)C * 2);
     return s.off;
@@ -484,16 +498,16 @@ YS_EXPORT int yolosod_swin_forward(const float* x, float* y, int B, int C, int H
   hipStream_t st = (hipStream_t)stream;
   SwinGeom g = swin_geom(B, H, W, window);
   YS_CHECK_ARG(g.L <= 320, "swin: window of %d tokens unsupported", g.L);
-  if (swin_fused_ok(C, num_heads, g.L, mlp_hidden)) {
+  if (swin_fused_ok(C, num_heads, g.wh, g.ww, mlp_hidden)) {
     Carver cf(workspace, workspace_bytes);
     float* fold = cf.take<float>((size_t)C * 2);
     YS_CHECK_ARG(fold, "swin: workspace too small (%zu)", workspace_bytes);
     hipLaunchKernelGGL(fold_bn_kernel, dim3((C + 255) / 256), dim3(256), 0, st, bn_w, bn_b, bn_mean, bn_var, bn_eps,
                        C, fold, fold + C);
-    const int r = yolosod_swin_fused_launch(x, y, B, C, H, W, num_heads, g.wh, g.ww, g.nWx, g.nWin, dw_w, ln1_w,
-                                            ln1_b, ln1_eps, in_proj_w, in_proj_b, out_proj_w, out_proj_b, ln2_w,
-                                            ln2_b, ln2_eps, mlp1_w, mlp1_b, mlp_hidden, mlp2_w, mlp2_b, pw_w, fold,
-                                            fold + C, st);
+    auto launch = C == 256 ? yolosod_swin_wide_launch : yolosod_swin_fused_launch;
+    const int r = launch(x, y, B, C, H, W, num_heads, g.wh, g.ww, g.nWx, g.nWin, dw_w, ln1_w, ln1_b, ln1_eps,
+                         in_proj_w, in_proj_b, out_proj_w, out_proj_b, ln2_w, ln2_b, ln2_eps, mlp1_w, mlp1_b,
+                         mlp_hidden, mlp2_w, mlp2_b, pw_w, fold, fold + C, st);
     if (r < 0) return -1;
     if (r == 1) return 0;
   }
