@@ -295,16 +295,27 @@ __global__ __launch_bounds__(256) void swin_partition_kernel(const float* __rest
 // =================================================================================================
 __global__ __launch_bounds__(256) void a2_pool_tokens_kernel(const float* __restrict__ xp, float* __restrict__ S, int C,
                                                              int H, int W, int A) {
+  // grid = (B*A, ceil(C/64)): the (64 channels x W) slab is averaged with lanes along w (row-contiguous reads),
+  // transposed through LDS and stored token-major with lanes along c (coalesced)
+  extern __shared__ float slab[];  // [64][W + 1]
   const int img = blockIdx.x / A, a = blockIdx.x % A;
+  const int c0 = blockIdx.y * 64;
+  const int nc = (C - c0 < 64) ? C - c0 : 64;
   const int r0 = (a * H) / A, r1 = ((a + 1) * H + A - 1) / A;
   const float inv = (float)(r1 - r0);
-  const float* xb = xp + (long)img * C * H * W;
-  float* Sb = S + ((long)img * A + a) * W * C;
-  for (int e = threadIdx.x; e < W * C; e += 256) {
-    const int w = e / C, c = e % C;
+  const float* xb = xp + ((long)img * C + c0) * H * W;
+  for (int e = threadIdx.x; e < nc * W; e += 256) {
+    const int c = e / W, w = e - c * W;
+    const float* src = xb + ((long)c * H + r0) * W + w;
     float s = 0.f;
-    for (int r = r0; r < r1; ++r) s += xb[((long)c * H + r) * W + w];
-    Sb[(long)w * C + c] = s / inv;
+    for (int r = 0; r < r1 - r0; ++r) s += src[(long)r * W];
+    slab[c * (W + 1) + w] = s / inv;
+  }
+  __syncthreads();
+  float* Sb = S + ((long)img * A + a) * W * C + c0;
+  for (int e = threadIdx.x; e < nc * W; e += 256) {
+    const int w = e / nc, c = e - w * nc;
+    Sb[(long)w * C + c] = slab[c * (W + 1) + w];
   }
 }
 
@@ -312,23 +323,23 @@ __global__ __launch_bounds__(256) void a2_pool_tokens_kernel(const float* __rest
 // align_corners=False (a2_attn.py:60), identity along W (same size). Upsampling commutes with the 1x1 conv.
 __global__ __launch_bounds__(256) void a2_upsample_out_kernel(const float* __restrict__ x, const float* __restrict__ T,
                                                               const float* __restrict__ bias, float* __restrict__ y,
-                                                              int C, int H, int W, int A, long total) {
+                                                              int C, int H, int W, int A) {
+  // grid = (img*C planes, ceil(H*W / 256)); the plane's A x W rows of T are tiny and L1/L2-resident
+  const long pc = blockIdx.x;  // img*C + c
+  const int c = (int)(pc % C);
+  const int e = blockIdx.y * 256 + threadIdx.x;
+  if (e >= H * W) return;
+  const int h = e / W, w = e - h * W;
   const float sc = (float)A / (float)H;
-  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
-    const int w = (int)(e % W);
-    const long t = e / W;
-    const int h = (int)(t % H);
-    const long pc = t / H;  // img*C + c
-    const int c = (int)(pc % C);
-    float src = sc * ((float)h + 0.5f) - 0.5f;
-    if (src < 0.f) src = 0.f;
-    const int y0 = (int)src;
-    const int y1 = y0 + ((y0 < A - 1) ? 1 : 0);
-    const float l1 = src - (float)y0, l0 = 1.0f - l1;
-    const float* Tp = T + pc * A * W;
-    const float u = l0 * Tp[y0 * W + w] + l1 * Tp[y1 * W + w];
-    y[e] = x[e] + siluf_(u + bias[c]);
-  }
+  float src = sc * ((float)h + 0.5f) - 0.5f;
+  if (src < 0.f) src = 0.f;
+  const int y0 = (int)src;
+  const int y1 = y0 + ((y0 < A - 1) ? 1 : 0);
+  const float l1 = src - (float)y0, l0 = 1.0f - l1;
+  const float* Tp = T + pc * A * W;
+  const float u = l0 * Tp[y0 * W + w] + l1 * Tp[y1 * W + w];
+  const long o = pc * H * W + e;
+  y[o] = x[o] + siluf_(u + bias[c]);
 }
 
 static int gs_blocks(long n) {
@@ -613,7 +624,9 @@ YS_EXPORT int yolosod_a2_forward(const float* x, float* y, int B, int C, int H, 
   ga.epi = epi_plain(XP, C * HW, (int)HW);
   ga.epi.bias = proj_b; ga.epi.bias_mode = 1; ga.epi.act = 1;
   if ((rc = launch_gemm(ga, B, false, st))) return rc;
-  hipLaunchKernelGGL(a2_pool_tokens_kernel, dim3(B * A), dim3(256), 0, st, XP, S, C, H, W, A);
+  YS_CHECK_ARG((size_t)64 * (W + 1) * sizeof(float) <= 64 * 1024, "a2: W=%d too large for the pooling kernel", W);
+  hipLaunchKernelGGL(a2_pool_tokens_kernel, dim3(B * A, (C + 63) / 64), dim3(256), (size_t)64 * (W + 1) * sizeof(float),
+                     st, XP, S, C, H, W, A);
   YS_CHECK_LAUNCH("a2_pool");
   ga = GemmArgs{};
   if ((rc = launch_row_stats(S, C, ntok, C, ln_eps, lns, st))) return rc;
@@ -634,9 +647,8 @@ YS_EXPORT int yolosod_a2_forward(const float* x, float* y, int B, int C, int H, 
   ga.A = oproj_w; ga.lda = C; ga.B = Z; ga.b_bs = (long)A * W * C; ga.ldb = C; ga.M = C; ga.N = A * W; ga.K = C;
   ga.epi = epi_plain(T, (long)C * A * W, A * W);
   if ((rc = launch_gemm(ga, B, true, st))) return rc;
-  const long total = (long)B * C * HW;
-  hipLaunchKernelGGL(a2_upsample_out_kernel, dim3(gs_blocks(total)), dim3(256), 0, st, x, T, oproj_b, y, C, H, W, A,
-                     total);
+  hipLaunchKernelGGL(a2_upsample_out_kernel, dim3((unsigned)(B * C), (unsigned)((HW + 255) / 256)), dim3(256), 0, st,
+                     x, T, oproj_b, y, C, H, W, A);
   YS_CHECK_LAUNCH("a2_upsample");
   return 0;
 }
