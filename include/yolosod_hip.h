@@ -71,6 +71,21 @@ int yolosod_swin_forward(const float* x, float* y, int B, int C, int H, int W, i
                          const float* bn_mean, const float* bn_var, float bn_eps, void* workspace,
                          size_t workspace_bytes, void* stream);
 
+/* MambaBlock (GLU fallback)        ultralytics/nn/modules/blocks_mamba.py:84-113 (Conv1x1BN, GLUBlock), :198-236
+ * (forward without mamba_ssm); arg rule nn/tasks.py:1122-1127 (MambaBlock(c, c_hidden, seq_reduction)).
+ * y = x + SiLU(BN_o(W_o . up_nearest(GLU(avg_pool_r(SiLU(BN_i(W_i . x)))))))  with
+ * GLU(p) = W_pw2 . SiLU(BN(dw3x3(sigmoid(g) * a))), [a; g] = W_pw1 . p. All BatchNorms in eval form (not folded by
+ * the reference's fuse()). x, y: [B, C, H, W]; c_hidden = ch; reduction r >= 1 (pool kernel = stride = r, floor;
+ * nearest upsample back to H x W). C and ch multiples of 32. */
+size_t yolosod_mamba_glu_workspace(int B, int C, int H, int W, int ch, int reduction);
+int yolosod_mamba_glu_forward(const float* x, float* y, int B, int C, int H, int W, int ch, int reduction,
+                              const float* in_w, const float* in_bn_w, const float* in_bn_b, const float* in_bn_mean,
+                              const float* in_bn_var, float in_bn_eps, const float* pw1_w, const float* dw_w,
+                              const float* bn_w, const float* bn_b, const float* bn_mean, const float* bn_var,
+                              float bn_eps, const float* pw2_w, const float* out_w, const float* out_bn_w,
+                              const float* out_bn_b, const float* out_bn_mean, const float* out_bn_var,
+                              float out_bn_eps, void* workspace, size_t workspace_bytes, void* stream);
+
 /* Detect._inference (decode)       ultralytics/nn/modules/head.py:100-131, DFL block.py:79-82,
  * make_anchors / dist2bbox utils/tal.py:333-357.
  * maps: host array of nl device pointers, map i = [B, 4*reg_max+nc, heights[i], widths[i]];

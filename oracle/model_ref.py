@@ -62,16 +62,25 @@ class Swin_CPU(M.SwinBlock):
                           _d(self.bn.bias), _d(self.bn.running_mean), _d(self.bn.running_var), self.bn.eps)
 
 
+class Mamba_CPU(M.MambaBlock):
+    def forward(self, x):
+        bn = lambda b: (_d(b.weight), _d(b.bias), _d(b.running_mean), _d(b.running_var), b.eps)  # noqa: E731
+        fb = self.fallback
+        return R.mamba_glu_ref(x, self.reduction, _d(self.in_proj[0].weight), bn(self.in_proj[1]),
+                               _d(fb.pw1.weight), _d(fb.dw.weight), bn(fb.bn), _d(fb.pw2.weight),
+                               _d(self.out_proj[0].weight), bn(self.out_proj[1]))
+
+
 class Detect_CPU(M.Detect):
     def _inference(self, x):
         return R.decode_ref(x, [float(s) for s in self.stride], self.nc, self.reg_max)
 
 
 REGISTRY = {"SE": SE_CPU, "SE_Block": SE_CPU, "CBAM_Block": CBAM_CPU, "CA_Block": CA_CPU, "A2_Attn": A2_CPU,
-            "SwinBlock": Swin_CPU, "Detect": Detect_CPU}
+            "SwinBlock": Swin_CPU, "MambaBlock": Mamba_CPU, "Detect": Detect_CPU}
 
 OP_CLASSES = {"SE_Block": SE_CPU, "CBAM_Block": CBAM_CPU, "CA_Block": CA_CPU, "A2_Attn": A2_CPU,
-              "SwinBlock": Swin_CPU}
+              "SwinBlock": Swin_CPU, "MambaBlock": Mamba_CPU}
 
 
 def build_cpu_model(cfg="yolov12-sod-fusion-v5-simple.yaml", seed=0, fuse=True, dtype=torch.float32):

@@ -132,6 +132,25 @@ def swin_ref(x, num_heads, window, dw_w, ln1_w, ln1_b, ln1_eps, in_w, in_b, out_
     return x + F.silu(y)
 
 
+def mamba_glu_ref(x, reduction, in_w, in_bn, pw1_w, dw_w, bn, pw2_w, out_w, out_bn):
+    """MambaBlock without mamba_ssm = GLU fallback (blocks_mamba.py:198-236, GLUBlock :94-113, Conv1x1BN :84-92).
+    *_bn = (weight, bias, running_mean, running_var, eps), eval-mode BatchNorm."""
+    B, C, H, W = x.shape
+    y = F.silu(_bn_eval(F.conv2d(x, in_w), *in_bn))                      # in_proj (:201)
+    if reduction > 1:
+        y = F.avg_pool2d(y, reduction, reduction)                         # (:204-205)
+    hid = pw1_w.shape[0] // 2
+    a, g = F.conv2d(y, pw1_w).chunk(2, dim=1)                             # GLUBlock.pw1 + split (:107)
+    z = torch.sigmoid(g) * a                                              # (:108)
+    z = F.conv2d(z, dw_w, padding=1, groups=hid)                          # dw (:109)
+    z = F.silu(_bn_eval(z, *bn))                                          # bn, act (:110-111)
+    y = F.conv2d(z, pw2_w)                                                # pw2 (:112)
+    if reduction > 1:
+        y = F.interpolate(y, size=(H, W), mode="nearest")                 # (:231-232)
+    y = F.silu(_bn_eval(F.conv2d(y, out_w), *out_bn))                     # out_proj (:235)
+    return x + y                                                          # (:236)
+
+
 def make_anchors_ref(shapes, strides, dtype=torch.float32, offset=0.5):
     """utils/tal.py:333-345: anchor (ix+0.5, iy+0.5), row-major per level, levels concatenated."""
     pts, st = [], []

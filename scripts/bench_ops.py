@@ -23,6 +23,7 @@ CASES = {
     "ca_L32": ("CA_Block", (128, 256, 32), (32, 128, 80, 80)),
     "cbam_L18": ("CBAM_Block", (256, 512, 16), (32, 256, 40, 40)),
     "se_L23": ("SE_Block", (256,), (32, 128, 80, 80)),
+    "mamba_L7": ("MambaBlock", (128, 256, 2), (32, 128, 80, 80)),  # yolov12-sod-fusion-v5 only
 }
 
 

@@ -21,7 +21,8 @@ from pathlib import Path
 sys.path.insert(0, str(Path(__file__).resolve().parent))
 from bench_ops import CASES  # noqa: E402
 
-OPKEY = {"SwinBlock": "swin", "A2_Attn": "a2", "SE_Block": "se", "CBAM_Block": "cbam", "CA_Block": "ca"}
+OPKEY = {"SwinBlock": "swin", "A2_Attn": "a2", "SE_Block": "se", "CBAM_Block": "cbam", "CA_Block": "ca",
+         "MambaBlock": "mamba"}
 CALLS = 13
 
 

@@ -33,6 +33,11 @@ OPS = {
     "swin_c64_h16x12": ("SwinBlock", (64, 2, 7), (1, 64, 16, 12)),
     "swin_c64_h20x5": ("SwinBlock", (64, 2, 7), (1, 64, 20, 5)),
     "swin_c256_h9": ("SwinBlock", (256, 4, 7), (1, 256, 9, 9)),
+    # MambaBlock(c, c_hidden, seq_reduction) (GLU fallback): fusion-v5 L7 is (128, 256, 2) at P3
+    "mamba_c128_h16": ("MambaBlock", (128, 256, 2), (1, 128, 16, 16)),
+    "mamba_c64_h15x13": ("MambaBlock", (64, 64, 2), (2, 64, 15, 13)),
+    "mamba_c32_r1": ("MambaBlock", (32, 64, 1), (2, 32, 10, 12)),
+    "mamba_c64_r3": ("MambaBlock", (64, 32, 3), (1, 64, 14, 17)),
 }
 
 

@@ -103,3 +103,25 @@ def test_model_1280_matches_oracle(gpu_model, cuda):
     assert y.shape == (1, 14, 136000)
     ok, err, _ = tol_close(y, ref, ATOL, 0.0)
     assert ok, f"max abs err {err:.3g}"
+
+
+def test_fusion_v5_model_matches_reference_and_oracle(cuda):
+    """yolov12-sod-fusion-v5: the paper graph + MambaBlock (GLU fallback, HIP yolosod_mamba_glu_forward) at P3."""
+    from oracle.model_ref import build_cpu_model
+    from yolosod_amd.nn.tasks import build_model
+    gm = build_model("yolov12-sod-fusion-v5.yaml", seed=0, device=cuda)
+    g = torch.Generator().manual_seed(0)
+    x = torch.rand(2, 3, 128, 128, generator=g)
+    with torch.inference_mode():
+        y = gm(x.to(cuda))[0].cpu()
+    ok, err, _ = tol_close(y, torch.from_numpy(golden("model_v5_out_128")["y"]), ATOL, 0.0)
+    assert ok, f"vs reference golden: max abs err {err:.3g}"
+    cpu = build_cpu_model("yolov12-sod-fusion-v5.yaml")
+    cpu.load_state_dict({k: v.cpu() for k, v in gm.state_dict().items()})
+    g = torch.Generator().manual_seed(1)
+    x = torch.rand(2, 3, 640, 640, generator=g)
+    with torch.inference_mode():
+        y = gm(x.to(cuda))[0].cpu()
+        ref = cpu(x)[0]
+    ok, err, _ = tol_close(y, ref, ATOL, 0.0)
+    assert ok, f"vs oracle at 640: max abs err {err:.3g}"

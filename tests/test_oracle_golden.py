@@ -57,7 +57,7 @@ def test_oracle_nms_matches_reference(name):
 def test_model_weights_match_reference_manifest():
     from yolosod_amd.nn.tasks import DetectionModel, state_dict_sha256
     man = json.loads((GOLDEN / "model_manifest.json").read_text())
-    for cfg in ("yolov12-sod-fusion-v5-simple", "yolov12m-sod"):
+    for cfg in ("yolov12-sod-fusion-v5-simple", "yolov12m-sod", "yolov12-sod-fusion-v5"):
         torch.manual_seed(0)
         m = DetectionModel(cfg + ".yaml")
         assert sum(p.numel() for p in m.parameters()) == man[cfg]["n_params"]
@@ -73,5 +73,17 @@ def test_oracle_model_forward_matches_reference():
     with torch.inference_mode():
         y = m(x)[0]
     ref = torch.from_numpy(golden("model_out_256")["y"])
+    ok, err, _ = tol_close(y, ref, 1e-3, 1e-6)
+    assert ok, err
+
+
+def test_oracle_fusion_v5_forward_matches_reference():
+    """yolov12-sod-fusion-v5 (MambaBlock GLU fallback at P3): seed-0 graph, reference golden."""
+    m = build_cpu_model("yolov12-sod-fusion-v5.yaml")
+    g = torch.Generator().manual_seed(0)
+    x = torch.rand(2, 3, 128, 128, generator=g)
+    with torch.inference_mode():
+        y = m(x)[0]
+    ref = torch.from_numpy(golden("model_v5_out_128")["y"])
     ok, err, _ = tol_close(y, ref, 1e-3, 1e-6)
     assert ok, err

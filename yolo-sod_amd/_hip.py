@@ -51,6 +51,9 @@ SIGNATURES = {
     "yolosod_bias_act": (_i, [_vp, _l, _vp, _l, _vp, _vp, _l, _i, _i, _l, _i, _vp]),
     "yolosod_conv1x1": (_i, [_vp, _l, _vp, _vp, _vp, _l, _vp, _l, _i, _i, _i, _l, _i, _vp]),
     "yolosod_debug_set_swin_fused": (None, [_i]),
+    "yolosod_mamba_glu_workspace": (_sz, [_i, _i, _i, _i, _i, _i]),
+    "yolosod_mamba_glu_forward": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _f, _vp, _vp,
+                                       _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp, _vp, _vp, _f, _vp, _sz, _vp]),
 }
 
 _LIB = None
@@ -241,6 +244,33 @@ def swin_forward(x, num_heads, window, dw_w, ln1_w, ln1_b, ln1_eps, in_w, in_b, 
         _p(m2_w, "mlp.2.weight", C * hid), _p(m2_b, "mlp.2.bias", C), _p(pw_w, "pw.weight", C * C),
         _p(bn_w, "bn.weight", C), _p(bn_b, "bn.bias", C), _p(bn_mean, "bn.running_mean", C),
         _p(bn_var, "bn.running_var", C), float(bn_eps), ws.data_ptr(), ws.numel(), _stream()), "swin_forward")
+    return y
+
+
+def mamba_glu_forward(x, reduction, in_w, in_bn_w, in_bn_b, in_bn_m, in_bn_v, in_eps, pw1_w, dw_w, bn_w, bn_b, bn_m,
+                      bn_v, bn_eps, pw2_w, out_w, out_bn_w, out_bn_b, out_bn_m, out_bn_v, out_eps):
+    """MambaBlock GLU fallback (blocks_mamba.py:94-113,198-236): x [B,C,H,W] -> x + out_proj(up(GLU(pool(in_proj x))))."""
+    lib = load_library()
+    B, C, H, W = x.shape
+    ch = in_w.shape[0]
+    hd = 2 * ch
+    r = int(reduction)
+    if r < 1 or H // r < 1 or W // r < 1:
+        raise RuntimeError(f"MambaBlock: seq_reduction {r} too large for {H}x{W}")
+    if C % 32 or ch % 32:
+        raise RuntimeError(f"MambaBlock: channels {C} / hidden {ch} must be multiples of 32 (MFMA GEMM K tiles)")
+    y = torch.empty_like(x)
+    ws = _workspace(lib.yolosod_mamba_glu_workspace(B, C, H, W, ch, r), x.device)
+    _check(_launch(("mamba", tuple(x.shape), (ch, r)), lib.yolosod_mamba_glu_forward,
+        _dev(x, "x"), _dev(y, "y"), B, C, H, W, ch, r, _p(in_w, "in_proj.0.weight", ch * C),
+        _p(in_bn_w, "in_proj.1.weight", ch), _p(in_bn_b, "in_proj.1.bias", ch), _p(in_bn_m, "in_proj.1.running_mean", ch),
+        _p(in_bn_v, "in_proj.1.running_var", ch), float(in_eps), _p(pw1_w, "fallback.pw1.weight", 2 * hd * ch),
+        _p(dw_w, "fallback.dw.weight", hd * 9), _p(bn_w, "fallback.bn.weight", hd), _p(bn_b, "fallback.bn.bias", hd),
+        _p(bn_m, "fallback.bn.running_mean", hd), _p(bn_v, "fallback.bn.running_var", hd), float(bn_eps),
+        _p(pw2_w, "fallback.pw2.weight", ch * hd), _p(out_w, "out_proj.0.weight", C * ch),
+        _p(out_bn_w, "out_proj.1.weight", C), _p(out_bn_b, "out_proj.1.bias", C),
+        _p(out_bn_m, "out_proj.1.running_mean", C), _p(out_bn_v, "out_proj.1.running_var", C), float(out_eps),
+        ws.data_ptr(), ws.numel(), _stream()), "mamba_glu_forward")
     return y
 
 

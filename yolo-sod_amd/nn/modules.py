@@ -25,7 +25,7 @@ from .. import _hip
 __all__ = (
     "Conv", "DWConv", "Concat", "Bottleneck", "C2f", "SPPF", "DFL", "SE", "SE_Block", "CBAM_Block",
     "ChannelAttention", "SpatialAttention", "CA_Block", "h_sigmoid", "A2_Attn", "WindowAttention", "SwinBlock",
-    "Detect",
+    "Conv1x1BN", "GLUBlock", "MambaBlock", "Detect",
 )
 
 
@@ -402,6 +402,55 @@ class SwinBlock(nn.Module):
             d(wa.attn.out_proj.bias), d(wa.norm2.weight), d(wa.norm2.bias), wa.norm2.eps, d(wa.mlp[0].weight),
             d(wa.mlp[0].bias), d(wa.mlp[2].weight), d(wa.mlp[2].bias), d(self.pw.weight), d(self.bn.weight),
             d(self.bn.bias), d(self.bn.running_mean), d(self.bn.running_var), self.bn.eps)
+
+
+class Conv1x1BN(nn.Sequential):
+    """1x1 conv (no bias) + BatchNorm + SiLU (blocks_mamba.py:84-92); not folded by fuse(), as in the reference."""
+
+    def __init__(self, c_in: int, c_out: int):
+        super().__init__(nn.Conv2d(c_in, c_out, 1, bias=False), nn.BatchNorm2d(c_out), nn.SiLU(inplace=True))
+
+
+class GLUBlock(nn.Module):
+    """GLU gated conv block, MambaBlock's fallback (blocks_mamba.py:94-113):
+    pw1 -> split (a, g) -> sigmoid(g) * a -> dw3x3 -> BN -> SiLU -> pw2."""
+
+    def __init__(self, c: int, expansion: int = 2):
+        super().__init__()
+        hidden = c * expansion
+        self.pw1 = nn.Conv2d(c, hidden * 2, 1, bias=False)
+        self.dw = nn.Conv2d(hidden, hidden, 3, padding=1, groups=hidden, bias=False)
+        self.bn = nn.BatchNorm2d(hidden)
+        self.pw2 = nn.Conv2d(hidden, c, 1, bias=False)
+        self.act = nn.SiLU(inplace=True)
+
+
+class MambaBlock(nn.Module):
+    """MambaBlock as the reference runs it without ``mamba_ssm`` (blocks_mamba.py:115-236): the GLU fallback.
+
+    y = x + out_proj(up_nearest(GLU(avg_pool_r(in_proj(x))))), in_proj / out_proj = Conv1x1BN, r = seq_reduction.
+    ``mamba_ssm`` is not part of this image (nor a dependency the reference vendors), so ``use_mamba`` is False as
+    in the reference's own fallback; parameters are created in the reference's order (in_proj, out_proj,
+    fallback). One HIP launch sequence: ``yolosod_mamba_glu_forward``."""
+
+    def __init__(self, c: int, c_hidden: int = 256, seq_reduction: int = 2):
+        super().__init__()
+        self.in_proj = Conv1x1BN(c, c_hidden)
+        self.out_proj = Conv1x1BN(c_hidden, c)
+        self.reduction = seq_reduction
+        self.use_mamba = False
+        self.fallback = GLUBlock(c_hidden, expansion=2)
+
+    def forward(self, x):
+        if _is_meta(x):
+            return torch.empty_like(x)
+        if self.training:
+            raise RuntimeError("MambaBlock: HIP path is inference-only (eval-mode BatchNorm)")
+        d = lambda t: t.detach()  # noqa: E731
+        ip, op, fb = self.in_proj, self.out_proj, self.fallback
+        bn = lambda b: (d(b.weight), d(b.bias), d(b.running_mean), d(b.running_var), b.eps)  # noqa: E731
+        return _hip.mamba_glu_forward(x, self.reduction, d(ip[0].weight), *bn(ip[1]), d(fb.pw1.weight),
+                                      d(fb.dw.weight), *bn(fb.bn), d(fb.pw2.weight), d(op[0].weight), *bn(op[1]))
 
 
 class Detect(nn.Module):

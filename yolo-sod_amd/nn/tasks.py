@@ -36,13 +36,14 @@ CFG_DIR = Path(__file__).resolve().parent.parent / "cfg"
 DEFAULT_REGISTRY = {
     "Conv": M.Conv, "DWConv": M.DWConv, "Concat": M.Concat, "Bottleneck": M.Bottleneck, "C2f": M.C2f,
     "SPPF": M.SPPF, "DFL": M.DFL, "SE": M.SE, "SE_Block": M.SE_Block, "CBAM_Block": M.CBAM_Block,
-    "CA_Block": M.CA_Block, "A2_Attn": M.A2_Attn, "SwinBlock": M.SwinBlock, "Detect": M.Detect,
+    "CA_Block": M.CA_Block, "A2_Attn": M.A2_Attn, "SwinBlock": M.SwinBlock, "MambaBlock": M.MambaBlock,
+    "Detect": M.Detect,
 }
 
 # channel-injection classes of the reference parse_model (by name)
 _SCALED_C1C2 = {"Conv", "DWConv", "Bottleneck", "C2f", "SPPF"}
 _REPEAT_INSERT = {"C2f"}
-_KEEP_CH = {"SE", "SE_Block", "SwinBlock", "CA_Block", "A2_Attn", "CBAM_Block"}
+_KEEP_CH = {"SE", "SE_Block", "SwinBlock", "CA_Block", "A2_Attn", "CBAM_Block", "MambaBlock"}
 _DETECT = {"Detect"}
 
 
@@ -115,7 +116,7 @@ def parse_model(d: dict, ch: int, verbose: bool = False, registry: dict | None =
             c2 = sum(ch[x] for x in f)
         elif name in _KEEP_CH:
             c2 = ch[f]
-            if name in {"SwinBlock", "CA_Block", "CBAM_Block"}:
+            if name in {"SwinBlock", "MambaBlock", "CA_Block", "CBAM_Block"}:
                 args = [ch[f], *args]
             elif name == "A2_Attn":
                 args = [ch[f], None, *args]

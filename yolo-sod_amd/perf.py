@@ -50,6 +50,15 @@ def op_cost(key):
         attn = tok_p * 2 * 2 * L * C
         dw = H * W * 2 * 9 * C
         return act + w, B * (dense + attn + dw)
+    if op == "mamba":  # GLU fallback: in_proj at full res, pool, pw1 (2x GLU width), dw, pw2, out_proj reduced
+        B, C, H, W = shape
+        ch, r = extra
+        hd = 2 * ch
+        hw, hwh = H * W, (H // r) * (W // r)
+        act = 2 * B * C * hw * F32
+        w = (ch * C + 2 * hd * ch + 9 * hd + ch * hd + C * ch + 4 * (ch + hd + C)) * F32
+        flops = 2 * ch * C * hw + hwh * (2 * 2 * hd * ch + 2 * 9 * hd + 2 * ch * hd + 2 * C * ch)
+        return act + w, B * flops
     if op == "decode":
         B, A = shape
         nc = extra
@@ -66,4 +75,4 @@ def op_cost(key):
 
 
 def bound_of(op):
-    return "mfma" if op in ("swin", "a2") else "hbm"
+    return "mfma" if op in ("swin", "a2", "mamba") else "hbm"
