@@ -71,6 +71,21 @@ int yolosod_swin_forward(const float* x, float* y, int B, int C, int H, int W, i
                          const float* bn_mean, const float* bn_var, float bn_eps, void* workspace,
                          size_t workspace_bytes, void* stream);
 
+/* Producer-side statistics for the channel gates (SE smallobj_modules.py:87, CBAM cbam_block.py:14-17): a conv
+ * epilogue that also writes its output's per-plane partial sums (+ maxes when pmax != NULL) in the segmentation
+ * yolosod_plane_parts returns (parts per plane, floats per part), and SE / CBAM entry points that take them instead
+ * of re-reading x (bitwise the same gate inputs up to summation order). */
+int yolosod_plane_parts(long HW, long* seg);
+int yolosod_bias_act_stats(const float* y, long y_bstride, float* out, long out_bstride, const float* bias,
+                           const float* res, long res_bstride, int B, int C, long HW, int act, int parts, long seg,
+                           float* psum, float* pmax, void* stream);
+int yolosod_se_forward_pre(const float* x, float* y, int B, int C, int H, int W, const float* fc1_w,
+                           const float* fc1_b, const float* fc2_w, const float* fc2_b, int hidden, const float* psum,
+                           void* workspace, size_t workspace_bytes, void* stream);
+int yolosod_cbam_forward_pre(const float* x, float* y, int B, int C, int H, int W, const float* fc0_w,
+                             const float* fc2_w, int hidden, const float* sa_w, const float* psum, const float* pmax,
+                             void* workspace, size_t workspace_bytes, void* stream);
+
 /* MambaBlock (GLU fallback)        ultralytics/nn/modules/blocks_mamba.py:84-113 (Conv1x1BN, GLUBlock), :198-236
  * (forward without mamba_ssm); arg rule nn/tasks.py:1122-1127 (MambaBlock(c, c_hidden, seq_reduction)).
  * y = x + SiLU(BN_o(W_o . up_nearest(GLU(avg_pool_r(SiLU(BN_i(W_i . x)))))))  with

@@ -230,3 +230,28 @@ def test_detect_head_fused_vs_oracle(c3, img, cuda):
     y = _hip.detect_head(d(fb), d(fc), d(wb), d(bb), d(wc), d(bc), strides, nc).cpu()
     ok, err, _ = tol_close(y, ref, 5e-4, 1e-5)
     assert ok, f"max abs err {err:.3g}"
+
+
+@pytest.mark.parametrize("shape", [(2, 32, 40, 40), (3, 64, 96, 120), (2, 128, 20, 20)])
+def test_producer_epilogue_stats_feed_se_and_cbam(shape, cuda):
+    """bias_act(stats=...) writes the same output as bias_act and per-plane partials that make SE / CBAM skip
+    their statistics pass; results equal the self-contained path (up to summation order)."""
+    from yolosod_amd import _hip
+    from yolosod_amd.nn import modules as M
+    g = torch.Generator().manual_seed(7)
+    y = torch.randn(shape, generator=g).to(cuda)
+    bias = torch.randn(shape[1], generator=g).to(cuda)
+    plain = _hip.bias_act(y.clone(), bias, 1)
+    with_stats = _hip.bias_act(y.clone(), bias, 1, stats="summax")
+    assert torch.equal(plain, with_stats) and with_stats._ys_plane_stats is not None
+    se = M.SE_Block(4)
+    se._maybe_build(shape[1], None)
+    cb = M.CBAM_Block(shape[1], None, 4)
+    for m in (se, cb):
+        recipes.perturb_(m, 3)
+        m.to(cuda).eval()
+        with torch.inference_mode():
+            a = m(plain)            # statistics pass over x
+            b = m(with_stats)       # partials from the producer
+        ok, err, _ = tol_close(b.cpu(), a.cpu(), 1e-6, 1e-5)
+        assert ok, (type(m).__name__, err)

@@ -49,6 +49,10 @@ SIGNATURES = {
     "yolosod_layernorm": (_i, [_vp, _vp, _l, _i, _vp, _vp, _f, _vp]),
     "yolosod_attention": (_i, [_vp, _vp, _l, _i, _i, _i, _vp]),
     "yolosod_bias_act": (_i, [_vp, _l, _vp, _l, _vp, _vp, _l, _i, _i, _l, _i, _vp]),
+    "yolosod_bias_act_stats": (_i, [_vp, _l, _vp, _l, _vp, _vp, _l, _i, _i, _l, _i, _i, _l, _vp, _vp, _vp]),
+    "yolosod_plane_parts": (_i, [_l, ctypes.POINTER(ctypes.c_long)]),
+    "yolosod_se_forward_pre": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _i, _vp, _vp, _sz, _vp]),
+    "yolosod_cbam_forward_pre": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _vp, _sz, _vp]),
     "yolosod_conv1x1": (_i, [_vp, _l, _vp, _vp, _vp, _l, _vp, _l, _i, _i, _i, _l, _i, _vp]),
     "yolosod_debug_set_swin_fused": (None, [_i]),
     "yolosod_mamba_glu_workspace": (_sz, [_i, _i, _i, _i, _i, _i]),
@@ -161,15 +165,50 @@ def _c(t: torch.Tensor) -> torch.Tensor:
 # ---------------------------------------------------------------------------------------------------------------
 # operator wrappers (parameters are passed as tensors already on the input's device)
 # ---------------------------------------------------------------------------------------------------------------
+class PlaneStats:
+    """Per-plane partial sums (+ maxes) of a tensor, emitted by its producer's epilogue (bias_act(stats=...)) in
+    the segmentation yolosod_plane_parts gives for its H*W; SE / CBAM consume them instead of re-reading it."""
+
+    __slots__ = ("psum", "pmax", "parts", "shape")
+
+    def __init__(self, psum, pmax, parts, shape):
+        self.psum, self.pmax, self.parts, self.shape = psum, pmax, parts, tuple(shape)
+
+
+_PARTS = {}
+
+
+def plane_parts(HW: int):
+    """(parts, seg) of the channel-attention statistics plan for planes of HW floats."""
+    if HW not in _PARTS:
+        seg = ctypes.c_long(0)
+        parts = load_library().yolosod_plane_parts(int(HW), ctypes.byref(seg))
+        _PARTS[HW] = (int(parts), int(seg.value))
+    return _PARTS[HW]
+
+
+def _pre_stats(x, need_max):
+    st = getattr(x, "_ys_plane_stats", None)
+    if st is None or st.shape != tuple(x.shape) or (need_max and st.pmax is None):
+        return None
+    return st
+
+
 def se_forward(x, fc1_w, fc1_b, fc2_w, fc2_b):
     lib = load_library()
     B, C, H, W = x.shape
     hid = fc1_w.shape[0]
     y = torch.empty_like(x)
     ws = _workspace(lib.yolosod_se_workspace(B, C, H, W), x.device)
-    _check(_launch(("se", tuple(x.shape), hid), lib.yolosod_se_forward, _dev(x, "x"), _dev(y, "y"), B, C, H, W, _p(fc1_w, "fc1.weight", hid * C),
-                                  _p(fc1_b, "fc1.bias", hid), _p(fc2_w, "fc2.weight", C * hid),
-                                  _p(fc2_b, "fc2.bias", C), hid, ws.data_ptr(), ws.numel(), _stream()), "se_forward")
+    pre = _pre_stats(x, False)
+    args = (_dev(x, "x"), _dev(y, "y"), B, C, H, W, _p(fc1_w, "fc1.weight", hid * C), _p(fc1_b, "fc1.bias", hid),
+            _p(fc2_w, "fc2.weight", C * hid), _p(fc2_b, "fc2.bias", C), hid)
+    if pre is not None:  # plane sums came with x from its producer's epilogue: gate + scale only
+        _check(_launch(("se", tuple(x.shape), hid), lib.yolosod_se_forward_pre, *args, pre.psum.data_ptr(),
+                       ws.data_ptr(), ws.numel(), _stream()), "se_forward_pre")
+    else:
+        _check(_launch(("se", tuple(x.shape), hid), lib.yolosod_se_forward, *args, ws.data_ptr(), ws.numel(),
+                       _stream()), "se_forward")
     return y
 
 
@@ -179,9 +218,15 @@ def cbam_forward(x, fc0_w, fc2_w, sa_w):
     hid = fc0_w.shape[0]
     y = torch.empty_like(x)
     ws = _workspace(lib.yolosod_cbam_workspace(B, C, H, W), x.device)
-    _check(_launch(("cbam", tuple(x.shape), hid), lib.yolosod_cbam_forward, _dev(x, "x"), _dev(y, "y"), B, C, H, W, _p(fc0_w, "fc.0.weight", hid * C),
-                                    _p(fc2_w, "fc.2.weight", C * hid), hid, _p(sa_w, "conv1.weight", 98),
-                                    ws.data_ptr(), ws.numel(), _stream()), "cbam_forward")
+    pre = _pre_stats(x, True)
+    args = (_dev(x, "x"), _dev(y, "y"), B, C, H, W, _p(fc0_w, "fc.0.weight", hid * C),
+            _p(fc2_w, "fc.2.weight", C * hid), hid, _p(sa_w, "conv1.weight", 98))
+    if pre is not None:
+        _check(_launch(("cbam", tuple(x.shape), hid), lib.yolosod_cbam_forward_pre, *args, pre.psum.data_ptr(),
+                       pre.pmax.data_ptr(), ws.data_ptr(), ws.numel(), _stream()), "cbam_forward_pre")
+    else:
+        _check(_launch(("cbam", tuple(x.shape), hid), lib.yolosod_cbam_forward, *args, ws.data_ptr(), ws.numel(),
+                       _stream()), "cbam_forward")
     return y
 
 
@@ -350,9 +395,11 @@ def nms(pred, conf_thres, iou_thres, classes, agnostic, multi_label, max_det, ma
     return out, counts, index
 
 
-def bias_act(y, bias, act, out=None, res=None):
+def bias_act(y, bias, act, out=None, res=None, stats=None):
     """Backbone conv epilogue: out = act(y + bias[c]) (+ res). ``out`` may be a channel slice [B, C, H, W] of a
-    larger contiguous concat buffer (batch stride > C*H*W); ``res`` likewise. In place when out is None."""
+    larger contiguous concat buffer (batch stride > C*H*W); ``res`` likewise. In place when out is None.
+    ``stats`` ("sum" / "summax"): also emit out's per-plane partial sums (+ maxes) for a following SE / CBAM,
+    attached to the returned tensor as ``_ys_plane_stats`` (PlaneStats)."""
     lib = load_library()
     B, C, H, W = y.shape
     HW = H * W
@@ -369,6 +416,16 @@ def bias_act(y, bias, act, out=None, res=None):
     yb = bstride(y, "y")
     ob = bstride(out, "out")
     rb = bstride(res, "res") if res is not None else 0
+    if stats is not None:
+        parts, seg = plane_parts(HW)
+        psum = torch.empty(B * C * parts, dtype=torch.float32, device=y.device)
+        pmax = torch.empty_like(psum) if stats == "summax" else None
+        _check(lib.yolosod_bias_act_stats(y.data_ptr(), yb, out.data_ptr(), ob, _dev(bias, "bias"),
+                                          None if res is None else res.data_ptr(), rb, B, C, HW, int(act), parts, seg,
+                                          psum.data_ptr(), None if pmax is None else pmax.data_ptr(), _stream()),
+               "bias_act_stats")
+        out._ys_plane_stats = PlaneStats(psum, pmax, parts, out.shape)
+        return out
     _check(lib.yolosod_bias_act(y.data_ptr(), yb, out.data_ptr(), ob, _dev(bias, "bias"),
                                 None if res is None else res.data_ptr(), rb, B, C, HW, int(act), _stream()),
            "bias_act")

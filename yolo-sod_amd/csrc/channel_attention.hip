@@ -484,9 +484,17 @@ YS_EXPORT size_t yolosod_se_workspace(int B, int C, int H, int W) {
   return s.off;
 }
 
-YS_EXPORT int yolosod_se_forward(const float* x, float* y, int B, int C, int H, int W, const float* fc1_w,
-                                 const float* fc1_b, const float* fc2_w, const float* fc2_b, int hidden,
-                                 void* workspace, size_t workspace_bytes, void* stream) {
+// plane segmentation of the per-plane statistics (parts per plane, floats per part) for an H*W plane, so a
+// producer epilogue (yolosod_bias_act_stats) can emit the partials the *_forward_pre entry points consume
+YS_EXPORT int yolosod_plane_parts(long HW, long* seg) {
+  const PartPlan pp = part_plan(HW);
+  if (seg) *seg = pp.seg;
+  return pp.parts;
+}
+
+static int se_forward_impl(const float* x, float* y, int B, int C, int H, int W, const float* fc1_w,
+                           const float* fc1_b, const float* fc2_w, const float* fc2_b, int hidden,
+                           const float* psum_pre, void* workspace, size_t workspace_bytes, void* stream) {
   YS_CHECK_ARG(x && y && fc1_w && fc1_b && fc2_w && fc2_b, "se: null pointer");
   YS_CHECK_ARG(B >= 0 && C > 0 && C <= 16384 && H > 0 && W > 0, "se: bad shape");
   YS_CHECK_ARG(hidden > 0 && hidden <= 64, "se: hidden=%d unsupported (1..64)", hidden);
@@ -504,9 +512,10 @@ YS_EXPORT int yolosod_se_forward(const float* x, float* y, int B, int C, int H, 
   for (int b0 = 0; b0 < B; b0 += ipc) {
     const int nb = (B - b0 < ipc) ? B - b0 : ipc;
     const long off = (long)b0 * C * HW;
-    float* ps = psum + (long)b0 * C * pp.parts;
-    hipLaunchKernelGGL((plane_part_stats_kernel<false>), dim3((unsigned)(nb * C * pp.parts)), dim3(256), 0, st,
-                       x + off, HW, pp.parts, pp.seg, ps, nullptr);
+    const float* ps = (psum_pre ? psum_pre : psum) + (long)b0 * C * pp.parts;
+    if (!psum_pre)
+      hipLaunchKernelGGL((plane_part_stats_kernel<false>), dim3((unsigned)(nb * C * pp.parts)), dim3(256), 0, st,
+                         x + off, HW, pp.parts, pp.seg, psum + (long)b0 * C * pp.parts, nullptr);
     hipLaunchKernelGGL((channel_gate_kernel<false>), dim3(nb), dim3(256), lds, st, ps, nullptr, pp.parts, C,
                        1.0f / (float)HW, fc1_w, fc1_b, fc2_w, fc2_b, hidden, gate + (long)b0 * C);
     hipLaunchKernelGGL(plane_scale_kernel, dim3((unsigned)(nb * C), ychunks), dim3(256), 0, st, x + off, y + off,
@@ -514,6 +523,23 @@ YS_EXPORT int yolosod_se_forward(const float* x, float* y, int B, int C, int H, 
   }
   YS_CHECK_LAUNCH("se");
   return 0;
+}
+
+YS_EXPORT int yolosod_se_forward(const float* x, float* y, int B, int C, int H, int W, const float* fc1_w,
+                                 const float* fc1_b, const float* fc2_w, const float* fc2_b, int hidden,
+                                 void* workspace, size_t workspace_bytes, void* stream) {
+  return se_forward_impl(x, y, B, C, H, W, fc1_w, fc1_b, fc2_w, fc2_b, hidden, nullptr, workspace, workspace_bytes,
+                         stream);
+}
+
+// As yolosod_se_forward, with x's per-plane partial sums already computed by its producer
+// (psum[B*C*parts], yolosod_plane_parts segmentation; yolosod_bias_act_stats): no statistics pass over x.
+YS_EXPORT int yolosod_se_forward_pre(const float* x, float* y, int B, int C, int H, int W, const float* fc1_w,
+                                     const float* fc1_b, const float* fc2_w, const float* fc2_b, int hidden,
+                                     const float* psum, void* workspace, size_t workspace_bytes, void* stream) {
+  YS_CHECK_ARG(psum, "se_pre: null partials");
+  return se_forward_impl(x, y, B, C, H, W, fc1_w, fc1_b, fc2_w, fc2_b, hidden, psum, workspace, workspace_bytes,
+                         stream);
 }
 
 // channel groups of the CBAM per-pixel pass: 32 channels each (fixed, for batch-invariant sums); the partial
@@ -533,9 +559,9 @@ YS_EXPORT size_t yolosod_cbam_workspace(int B, int C, int H, int W) {
   return s.off;
 }
 
-YS_EXPORT int yolosod_cbam_forward(const float* x, float* y, int B, int C, int H, int W, const float* fc0_w,
-                                   const float* fc2_w, int hidden, const float* sa_w, void* workspace,
-                                   size_t workspace_bytes, void* stream) {
+static int cbam_forward_impl(const float* x, float* y, int B, int C, int H, int W, const float* fc0_w,
+                             const float* fc2_w, int hidden, const float* sa_w, const float* psum_pre,
+                             const float* pmax_pre, void* workspace, size_t workspace_bytes, void* stream) {
   YS_CHECK_ARG(x && y && fc0_w && fc2_w && sa_w, "cbam: null pointer");
   YS_CHECK_ARG(B >= 0 && C > 0 && C <= 16384 && H > 0 && W > 0, "cbam: bad shape");
   YS_CHECK_ARG(hidden > 0 && hidden <= 64, "cbam: hidden=%d unsupported (1..64)", hidden);
@@ -558,12 +584,13 @@ YS_EXPORT int yolosod_cbam_forward(const float* x, float* y, int B, int C, int H
   for (int b0 = 0; b0 < B; b0 += ipc) {
     const int nb = (B - b0 < ipc) ? B - b0 : ipc;
     const long off = (long)b0 * C * HW;
-    float* ps = psum + (long)b0 * C * pp.parts;
-    float* pm = pmax + (long)b0 * C * pp.parts;
+    const float* ps = (psum_pre ? psum_pre : psum) + (long)b0 * C * pp.parts;
+    const float* pm = (pmax_pre ? pmax_pre : pmax) + (long)b0 * C * pp.parts;
     float* cab = ca + (long)b0 * C;
     float* sab = sa + (long)b0 * HW;
-    hipLaunchKernelGGL((plane_part_stats_kernel<true>), dim3((unsigned)(nb * C * pp.parts)), dim3(256), 0, st,
-                       x + off, HW, pp.parts, pp.seg, ps, pm);
+    if (!psum_pre)
+      hipLaunchKernelGGL((plane_part_stats_kernel<true>), dim3((unsigned)(nb * C * pp.parts)), dim3(256), 0, st,
+                         x + off, HW, pp.parts, pp.seg, psum + (long)b0 * C * pp.parts, pmax + (long)b0 * C * pp.parts);
     hipLaunchKernelGGL((channel_gate_kernel<true>), dim3(nb), dim3(256), lds, st, ps, pm, pp.parts, C,
                        1.0f / (float)HW, fc0_w, nullptr, fc2_w, nullptr, hidden, cab);
     dim3 gs((unsigned)pxb, G, nb);
@@ -581,6 +608,22 @@ YS_EXPORT int yolosod_cbam_forward(const float* x, float* y, int B, int C, int H
   }
   YS_CHECK_LAUNCH("cbam");
   return 0;
+}
+
+YS_EXPORT int yolosod_cbam_forward(const float* x, float* y, int B, int C, int H, int W, const float* fc0_w,
+                                   const float* fc2_w, int hidden, const float* sa_w, void* workspace,
+                                   size_t workspace_bytes, void* stream) {
+  return cbam_forward_impl(x, y, B, C, H, W, fc0_w, fc2_w, hidden, sa_w, nullptr, nullptr, workspace,
+                           workspace_bytes, stream);
+}
+
+// As yolosod_cbam_forward, with x's per-plane partial sums and maxes from its producer (yolosod_bias_act_stats).
+YS_EXPORT int yolosod_cbam_forward_pre(const float* x, float* y, int B, int C, int H, int W, const float* fc0_w,
+                                       const float* fc2_w, int hidden, const float* sa_w, const float* psum,
+                                       const float* pmax, void* workspace, size_t workspace_bytes, void* stream) {
+  YS_CHECK_ARG(psum && pmax, "cbam_pre: null partials");
+  return cbam_forward_impl(x, y, B, C, H, W, fc0_w, fc2_w, hidden, sa_w, psum, pmax, workspace, workspace_bytes,
+                           stream);
 }
 
 YS_EXPORT size_t yolosod_ca_workspace(int B, int C, int H, int W) {

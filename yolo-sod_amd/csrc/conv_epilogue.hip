@@ -7,6 +7,7 @@
 // (out batch stride != C*HW), so those passes and copies disappear. Same arithmetic as the reference:
 // (conv + b) rounded once, SiLU = x / (1 + exp(-x)).
 #include "common.h"
+#include <math.h>
 
 namespace ys {
 
@@ -33,9 +34,109 @@ __global__ __launch_bounds__(256) void bias_act_kernel(const float* __restrict__
   }
 }
 
+// Same epilogue, plus the per-plane partial statistics of `out` that a following SE / CBAM channel gate needs
+// (smallobj_modules.py:87 mean, cbam_block.py:14-17 mean + max): workgroup (plane, k) handles the plane segment
+// [k*seg, (k+1)*seg) - the segmentation of channel_attention.hip's part_plan - and writes psum/pmax[plane*parts + k].
+// The gate then needs no extra pass over the producer's output.
+template <int ACT, bool RES, bool MAX>
+__global__ __launch_bounds__(256) void bias_act_stats_kernel(const float* __restrict__ y, float* __restrict__ out,
+                                                             const float* __restrict__ bias,
+                                                             const float* __restrict__ res, int C, long HW,
+                                                             long y_bs, long o_bs, long r_bs, int parts, long seg,
+                                                             float* __restrict__ psum, float* __restrict__ pmax) {
+  const long plane = blockIdx.x / parts;
+  const int k = blockIdx.x % parts;
+  const long b = plane / C;
+  const int c = (int)(plane - b * C);
+  const long s0 = k * seg;
+  const long s1 = (s0 + seg < HW) ? s0 + seg : HW;
+  const float bc = bias[c];
+  const float4* y4 = reinterpret_cast<const float4*>(y + b * y_bs + (long)c * HW + s0);
+  const float4* r4 = RES ? reinterpret_cast<const float4*>(res + b * r_bs + (long)c * HW + s0) : nullptr;
+  float4* o4 = reinterpret_cast<float4*>(out + b * o_bs + (long)c * HW + s0);
+  const long n4 = (s1 - s0) >> 2;
+  const int tid = threadIdx.x;
+  float s = 0.f, m = -INFINITY;
+  for (long i0 = tid; i0 < n4; i0 += 4 * 256) {
+    float4 v[4], r[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const long i = i0 + u * 256;
+      if (i < n4) {
+        v[u] = y4[i];
+        if (RES) r[u] = r4[i];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const long i = i0 + u * 256;
+      if (i >= n4) continue;
+      float4 o = v[u];
+      o.x += bc; o.y += bc; o.z += bc; o.w += bc;
+      if (ACT == 1) {
+        o.x = siluf_(o.x); o.y = siluf_(o.y); o.z = siluf_(o.z); o.w = siluf_(o.w);
+      }
+      if (RES) {
+        o.x += r[u].x; o.y += r[u].y; o.z += r[u].z; o.w += r[u].w;
+      }
+      o4[i] = o;
+      s += (o.x + o.y) + (o.z + o.w);
+      if (MAX) m = fmaxf(m, fmaxf(fmaxf(o.x, o.y), fmaxf(o.z, o.w)));
+    }
+  }
+  __shared__ float ss[4], sm[4];
+  s = wave_sum(s);
+  if (MAX) m = wave_max(m);
+  const int w = tid >> 6;
+  if ((tid & 63) == 0) {
+    ss[w] = s;
+    sm[w] = m;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    psum[blockIdx.x] = (ss[0] + ss[1]) + (ss[2] + ss[3]);
+    if (MAX) pmax[blockIdx.x] = fmaxf(fmaxf(sm[0], sm[1]), fmaxf(sm[2], sm[3]));
+  }
+}
+
 }  // namespace ys
 
 using namespace ys;
+
+// yolosod_bias_act + per-plane partial sums (and maxes when pmax != NULL) of `out` in psum/pmax[B*C*parts], with
+// the plane segmentation (parts, seg) that yolosod_se_forward_pre / yolosod_cbam_forward_pre expect
+// (yolosod_plane_parts). Requires HW % 4 == 0 and seg % 4 == 0.
+YS_EXPORT int yolosod_bias_act_stats(const float* y, long y_bstride, float* out, long out_bstride, const float* bias,
+                                     const float* res, long res_bstride, int B, int C, long HW, int act, int parts,
+                                     long seg, float* psum, float* pmax, void* stream) {
+  YS_CHECK_ARG(y && out && bias && psum, "bias_act_stats: null pointer");
+  YS_CHECK_ARG(act == 0 || act == 1, "bias_act_stats: act=%d unsupported", act);
+  YS_CHECK_ARG(HW % 4 == 0 && seg % 4 == 0 && y_bstride % 4 == 0 && out_bstride % 4 == 0 &&
+                   (!res || res_bstride % 4 == 0),
+               "bias_act_stats: HW, seg and batch strides must be multiples of 4");
+  YS_CHECK_ARG(parts >= 1 && seg >= 1 && (long)parts * seg >= HW && (long)(parts - 1) * seg < HW,
+               "bias_act_stats: plane plan (%d x %ld) does not cover HW=%ld", parts, seg, HW);
+  YS_CHECK_ARG((((uintptr_t)y | (uintptr_t)out | (uintptr_t)(res ? res : y)) & 15) == 0,
+               "bias_act_stats: pointers must be 16-byte aligned");
+  const long blocks = (long)B * C * parts;
+  if (blocks == 0) return 0;
+  YS_CHECK_ARG(blocks < (1L << 31), "bias_act_stats: too many planes");
+  hipStream_t st = (hipStream_t)stream;
+#define YS_BAS(A_, R_, M_)                                                                                         \
+  hipLaunchKernelGGL((bias_act_stats_kernel<A_, R_, M_>), dim3((unsigned)blocks), dim3(256), 0, st, y, out, bias, res, \
+                     C, HW, y_bstride, out_bstride, res_bstride, parts, seg, psum, pmax)
+  const bool mx = pmax != nullptr;
+  if (act == 1) {
+    if (res) { if (mx) YS_BAS(1, true, true); else YS_BAS(1, true, false); }
+    else { if (mx) YS_BAS(1, false, true); else YS_BAS(1, false, false); }
+  } else {
+    if (res) { if (mx) YS_BAS(0, true, true); else YS_BAS(0, true, false); }
+    else { if (mx) YS_BAS(0, false, true); else YS_BAS(0, false, false); }
+  }
+#undef YS_BAS
+  YS_CHECK_LAUNCH("bias_act_stats");
+  return 0;
+}
 
 // out[b*out_bstride + c*HW + p] = act(y[b*y_bstride + c*HW + p] + bias[c]) + res[b*res_bstride + c*HW + p]
 // act: 0 identity, 1 SiLU. res may be NULL. In place (out == y) allowed. HW and all strides multiples of 4.

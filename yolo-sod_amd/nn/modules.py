@@ -58,9 +58,11 @@ def _act_code(act):
 CONV1X1_GEMM = os.environ.get("YOLOSOD_CONV1X1", "0") == "1"
 
 
-def conv_epilogue(conv: nn.Conv2d, act_code, x, out=None, res=None):
+def conv_epilogue(conv: nn.Conv2d, act_code, x, out=None, res=None, stats=None):
     """GPU fast path of ``act(conv(x)) (+ res)``: MIOpen conv without bias, then one HIP pass for bias +
     activation (+ shortcut), optionally written straight into a channel slice ``out`` of a concat buffer.
+    ``stats`` ("sum" / "summax"): the same pass emits the output's per-plane partial statistics for a following
+    SE / CBAM gate (``_hip.PlaneStats`` on the returned tensor).
     Returns None when the fast path does not apply (CPU tensor, no bias, unsupported activation / shape)."""
     if x.device.type != "cuda" or conv.bias is None or act_code is None or x.dtype != torch.float32:
         return None
@@ -80,7 +82,7 @@ def conv_epilogue(conv: nn.Conv2d, act_code, x, out=None, res=None):
             out.copy_(y)
             return out
         return y
-    return _hip.bias_act(y, conv.bias.detach(), act_code, out=out, res=res)
+    return _hip.bias_act(y, conv.bias.detach(), act_code, out=out, res=res, stats=stats)
 
 
 class Conv(nn.Module):
@@ -89,6 +91,8 @@ class Conv(nn.Module):
     Fused form on GPU: MIOpen conv + one HIP epilogue pass (bias + SiLU, optional shortcut / concat slice)."""
 
     default_act = nn.SiLU()
+    # set by DetectionModel when this conv's output feeds an SE ("sum") / CBAM ("summax") gate directly
+    emit_stats = None
 
     def __init__(self, c1, c2, k=1, s=1, p=None, g=1, d=1, act=True):
         super().__init__()
@@ -100,7 +104,7 @@ class Conv(nn.Module):
         return self.act(self.bn(self.conv(x)))
 
     def forward_fuse(self, x, out=None, res=None):
-        y = conv_epilogue(self.conv, _act_code(self.act), x, out, res)
+        y = conv_epilogue(self.conv, _act_code(self.act), x, out, res, self.emit_stats)
         if y is not None:
             return y
         y = self.act(self.conv(x))
