@@ -200,7 +200,7 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
   constexpr int LT = C + 4;          // T row stride (== 4 mod 64 floats: conflict-free b128 row reads)
   constexpr int LQ = 3 * C + 4;      // QKV row stride (also holds the attention output and the MLP hidden)
   constexpr int LH = HID + 4;
-  constexpr int NR = (C * 9 + 255) / 256;  // halo rows (of <= 9 floats) per thread
+  constexpr int NHL = (C * 9 + 27) / 28;  // halo loads per lane: a wave-instruction covers 7 rows x 9 columns
   static_assert(HD % 16 == 0 && HD <= 64, "head dim");
   static_assert(LH <= LQ, "MLP hidden must fit the QKV region");
   static_assert(256 % C == 0 || C % 256 == 0, "depthwise channel mapping");
@@ -239,25 +239,23 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
 #pragma unroll
   for (int i = 0; i < 9; ++i) dwk[i] = p.dw[dw_c * 9 + i];
 
-  // halo patch [C][PH][PW] of window gwin into registers, row-wise: thread -> (c, py) rows of PW floats
-  float hv[NR][9];
+  // halo patch [C][PH][PW] of window gwin into registers: lane = 9 * row + column (lane 63 idle), so one
+  // wave-instruction reads 7 row segments of 9 floats (~14 cache lines) instead of 64 rows of one float each
+  float hv[NHL];
+  const int hl_r = lane / 9, hl_px = lane - (lane / 9) * 9;
   auto load_halo = [&](long gwin) {
     const int im = (int)(gwin / p.nWin), wn = (int)(gwin % p.nWin);
     const int wy_ = wn / p.nWx, wx_ = wn % p.nWx;
     const int h0 = wy_ * wh - 1, w0 = wx_ * ww - 1;
     const float* xb_ = p.x + (long)im * C * HWl;
+    const int wc = w0 + hl_px;
+    const bool colok = hl_r < 7 && hl_px < PW && wc >= 0 && wc < W && !(p.abl & 1);
 #pragma unroll
-    for (int i = 0; i < NR; ++i) {
-      const int rr = tid + 256 * i;
+    for (int i = 0; i < NHL; ++i) {
+      const int rr = (i * 4 + wid) * 7 + hl_r;
       const int c = rr / PH, py = rr - c * PH;
       const int hh = h0 + py;
-      const bool rowok = rr < C * PH && hh >= 0 && hh < H && !(p.abl & 1);
-      const float* src = xb_ + (long)c * HWl + (long)hh * W + w0;
-#pragma unroll
-      for (int px = 0; px < 9; ++px) {
-        const int wc = w0 + px;
-        hv[i][px] = (rowok && px < PW && wc >= 0 && wc < W) ? src[px] : 0.f;
-      }
+      hv[i] = (colok && rr < C * PH && hh >= 0 && hh < H) ? xb_[(long)c * HWl + (long)hh * W + wc] : 0.f;
     }
   };
   load_halo(gw);
@@ -281,14 +279,9 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
 
     // ---- stage 0: halo patch (registers) -> LDS [c][py][HPW] -> dw conv, one output row of 7 tokens per item ----
 #pragma unroll
-    for (int i = 0; i < NR; ++i) {
-      const int rr = tid + 256 * i;
-      if (rr < C * PH) {
-        float4* dst = reinterpret_cast<float4*>(Q + rr * HPW);
-        dst[0] = make_float4(hv[i][0], hv[i][1], hv[i][2], hv[i][3]);
-        dst[1] = make_float4(hv[i][4], hv[i][5], hv[i][6], hv[i][7]);
-        dst[2] = make_float4(hv[i][8], 0.f, 0.f, 0.f);
-      }
+    for (int i = 0; i < NHL; ++i) {
+      const int rr = (i * 4 + wid) * 7 + hl_r;
+      if (hl_r < 7 && rr < C * PH) Q[rr * HPW + hl_px] = hv[i];  // columns 9..11 of a row are never read
     }
     __syncthreads();
     YS_STAMP(1)

@@ -198,24 +198,25 @@ __global__ __launch_bounds__(NT, 1) void swin_wide_kernel(Args p) {
   const float* xb = p.x + (long)img * C * HWl;
   const int h0 = wy * 7 - 1, w0 = wx * 7 - 1;
 
-  // halo of both channel halves into registers: thread -> (c, py) rows of 9 floats (1152 rows per half)
-  constexpr int NR = (HALF * 9 + NT - 1) / NT;
-  float hv[2][NR][9];
+  // halo of both channel halves into registers: lane = 9 * row + column (lane 63 idle), so a wave-instruction
+  // reads 7 row segments of 9 floats; 8 waves x 7 rows per step, 1152 rows (128 channels x 9) per half
+  constexpr int NR = (HALF * 9 + 8 * 7 - 1) / (8 * 7);
+  float hv[2][NR];
+  const int hl_r = lane / 9, hl_px = lane - (lane / 9) * 9;
+  {
+    const int wc = w0 + hl_px;
+    const bool colok = hl_r < 7 && wc >= 0 && wc < W;
 #pragma unroll
-  for (int hf = 0; hf < 2; ++hf)
+    for (int hf = 0; hf < 2; ++hf)
 #pragma unroll
-    for (int i = 0; i < NR; ++i) {
-      const int rr = tid + NT * i;
-      const int c = rr / 9, py = rr - c * 9;
-      const int hh = h0 + py;
-      const bool rowok = rr < HALF * 9 && hh >= 0 && hh < H;
-      const float* src = xb + (long)(hf * HALF + c) * HWl + (long)hh * W + w0;
-#pragma unroll
-      for (int px = 0; px < 9; ++px) {
-        const int wc = w0 + px;
-        hv[hf][i][px] = (rowok && wc >= 0 && wc < W) ? src[px] : 0.f;
+      for (int i = 0; i < NR; ++i) {
+        const int rr = (i * 8 + wid) * 7 + hl_r;
+        const int c = rr / 9, py = rr - c * 9;
+        const int hh = h0 + py;
+        hv[hf][i] = (colok && rr < HALF * 9 && hh >= 0 && hh < H)
+                        ? xb[(long)(hf * HALF + c) * HWl + (long)hh * W + wc] : 0.f;
       }
-    }
+  }
   for (int e = tid; e < 4 * C; e += NT) {
     const int which = e / C, c = e - which * C;
     const float* src = which == 0 ? p.ln1_w : which == 1 ? p.ln1_b : which == 2 ? p.ln2_w : p.ln2_b;
@@ -232,13 +233,8 @@ __global__ __launch_bounds__(NT, 1) void swin_wide_kernel(Args p) {
     if (hf) __syncthreads();  // previous half's dw reads done
 #pragma unroll
     for (int i = 0; i < NR; ++i) {
-      const int rr = tid + NT * i;
-      if (rr < HALF * 9) {
-        float4* dst = reinterpret_cast<float4*>(WK + rr * HPW);
-        dst[0] = make_float4(hv[hf][i][0], hv[hf][i][1], hv[hf][i][2], hv[hf][i][3]);
-        dst[1] = make_float4(hv[hf][i][4], hv[hf][i][5], hv[hf][i][6], hv[hf][i][7]);
-        dst[2] = make_float4(hv[hf][i][8], 0.f, 0.f, 0.f);
-      }
+      const int rr = (i * 8 + wid) * 7 + hl_r;
+      if (hl_r < 7 && rr < HALF * 9) WK[rr * HPW + hl_px] = hv[hf][i];  // columns 9..11 are never read
     }
     __syncthreads();
     for (int item = tid; item < HALF * 7; item += NT) {
