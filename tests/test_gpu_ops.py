@@ -74,6 +74,9 @@ REAL = {
     "ca_L32": ("CA_Block", (128, 256, 32), (2, 128, 80, 80)),
     "swin_L28_1280": ("SwinBlock", (64, 2, 7), (1, 64, 320, 320)),
     "a2_L12_1280": ("A2_Attn", (512, None, 8, 8), (1, 512, 40, 40)),
+    "swin_L9_1280": ("SwinBlock", (256, 4, 7), (1, 256, 80, 80)),
+    "swin_wide_pad_20x13": ("SwinBlock", (256, 4, 7), (2, 256, 20, 13)),  # bottom + right zero pad, fused wide
+    "mamba_L7": ("MambaBlock", (128, 256, 2), (1, 128, 80, 80)),          # yolov12-sod-fusion-v5 L7
 }
 
 
