@@ -96,6 +96,7 @@ struct HeadArgs {
   float stride[4];
   int nl, nc, A;
   float* y;
+  int abl;  // timing ablation (debug only, YOLOSOD_HEAD_ABL): 1 skip feature loads, 2 skip stores
 };
 
 template <int C2, int C3, int NTS>
@@ -142,10 +143,19 @@ __global__ __launch_bounds__(256) void detect_head_kernel(HeadArgs d) {
     const int p = p0 + j;
     const bool ok = p < HW;
     float xb[C2 / 4], xc[C3 / 4];
+    if (p0 + 16 <= HW && !(d.abl & 1)) {  // full group (wave-uniform): plain strided loads, no per-load selects
+      const float* pb = fbb + (long)g * HW + p;
+      const float* pc = fcb + (long)g * HW + p;
 #pragma unroll
-    for (int q = 0; q < C2 / 4; ++q) xb[q] = ok ? fbb[(long)(4 * q + g) * HW + p] : 0.f;
+      for (int q = 0; q < C2 / 4; ++q) xb[q] = pb[(long)q * 4 * HW];
 #pragma unroll
-    for (int q = 0; q < C3 / 4; ++q) xc[q] = ok ? fcb[(long)(4 * q + g) * HW + p] : 0.f;
+      for (int q = 0; q < C3 / 4; ++q) xc[q] = pc[(long)q * 4 * HW];
+    } else {
+#pragma unroll
+      for (int q = 0; q < C2 / 4; ++q) xb[q] = (ok && !(d.abl & 1)) ? fbb[(long)(4 * q + g) * HW + p] : 0.f;
+#pragma unroll
+      for (int q = 0; q < C3 / 4; ++q) xc[q] = (ok && !(d.abl & 1)) ? fcb[(long)(4 * q + g) * HW + p] : 0.f;
+    }
     f32x4 acc[5];
 #pragma unroll
     for (int t = 0; t < 5; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -156,7 +166,9 @@ __global__ __launch_bounds__(256) void detect_head_kernel(HeadArgs d) {
 #pragma unroll
     for (int q = 0; q < C3 / 4; ++q) acc[4] = __builtin_amdgcn_mfma_f32_16x16x4f32(wcr[q], xc[q], acc[4], 0, 0, 0);
 
-    // DFL (block.py:79-82): softmax over the 16 bins of each side, expectation with weights 0..15
+    // DFL (block.py:79-82): softmax over the 16 bins of each side, expectation with weights 0..15. Hardware
+    // exp2 / reciprocal (1-2 ulp): the head is VALU-issue bound (SQ counters: ~650 VALU per 16-pixel group
+    // against 80 MFMAs with the libm expf / IEEE division), and the box tolerance is 1e-3
     float dist[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
@@ -165,20 +177,18 @@ __global__ __launch_bounds__(256) void detect_head_kernel(HeadArgs d) {
       for (int r = 0; r < 4; ++r) v[r] = acc[s][r] + bbr[s][r];
       float mx = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
       mx = xor32_max(xor16_max(mx));
-      float sum = 0.f;
+      float sum = 0.f, e = 0.f;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        v[r] = expf(v[r] - mx);
+        v[r] = __expf(v[r] - mx);
         sum += v[r];
+        e += (float)(4 * g + r) * v[r];
       }
       sum = xor32_sum(xor16_sum(sum));
-      const float inv = 1.0f / sum;
-      float e = 0.f;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) e += (float)(4 * g + r) * (v[r] * inv);
-      dist[s] = xor32_sum(xor16_sum(e));
+      e = xor32_sum(xor16_sum(e));
+      dist[s] = e * __builtin_amdgcn_rcpf(sum);
     }
-    if (!ok) continue;
+    if (!ok || (d.abl & 2)) continue;
     const int iy = p / W, ix = p - iy * W;
     const float ax = (float)ix + 0.5f, ay = (float)iy + 0.5f;
     const float x1 = ax - dist[0], y1 = ay - dist[1];
@@ -265,6 +275,7 @@ YS_EXPORT int yolosod_detect_head(int nl, const float* const* box_feat, const fl
   d.blk_off[nl] = blk;
   d.A = off;
   d.y = y;
+  if (const char* e = getenv("YOLOSOD_HEAD_ABL")) d.abl = atoi(e);
   if (B == 0 || off == 0) return 0;
   const dim3 grid(blk, B);
   if (c3 == 64)
