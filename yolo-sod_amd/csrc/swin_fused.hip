@@ -159,10 +159,14 @@ __device__ __forceinline__ void wave_gemm_rows(const float* __restrict__ As, int
   for (int j = 0; j < NJ; ++j) ext[j] = group4_sum(ext[j]);
 }
 
-// Row statistics (mean, rstd) of rows [0, SW_ROWS) of S[SW_ROWS][lds] over C: 4 threads per row (all rows at
-// once), each with C/4 values from float4 LDS reads, two-pass, DPP quad reductions; rows >= L get (0, 0).
+// LayerNorm of rows [0, SW_ROWS) of S[SW_ROWS][lds] over C into U[SW_ROWS][ldu]: 4 threads per row (all rows at
+// once), each holding C/4 values in registers from float4 LDS reads, two-pass statistics with DPP quad reductions,
+// then U = (S - mean) * rstd * w + b written straight from those registers. Rows >= L (padding of a small global
+// window) get U = b. The GEMMs read U as plain A fragments: the normalisation is done once per element instead of
+// once per element per wave (all four waves read every A row).
 template <int C>
-__device__ __forceinline__ void lds_row_stats(const float* S, int lds, float* stats, int L, float eps, int tid) {
+__device__ __forceinline__ void lds_row_layernorm(const float* S, int lds, float* U, int ldu, const float* lnw,
+                                                  const float* lnb, int L, float eps, int tid) {
   constexpr int CP = C / 4;
   const int r = tid >> 2, qd = tid & 3;
   const bool valid = r < L;
@@ -181,9 +185,20 @@ __device__ __forceinline__ void lds_row_stats(const float* S, int lds, float* st
     q += (a0 * a0 + a1 * a1) + (a2 * a2 + a3 * a3);
   }
   const float var = quad_sum(q) / (float)C;
-  if (qd == 0 && r < SW_ROWS) {
-    stats[2 * r] = valid ? mean : 0.f;
-    stats[2 * r + 1] = valid ? 1.0f / sqrtf(var + eps) : 0.f;
+  const float mu = valid ? mean : 0.f;
+  const float rs = valid ? 1.0f / sqrtf(var + eps) : 0.f;
+  if (r < SW_ROWS) {
+#pragma unroll
+    for (int i = 0; i < CP / 4; ++i) {
+      const float4 w = *reinterpret_cast<const float4*>(lnw + qd * CP + 4 * i);
+      const float4 b = *reinterpret_cast<const float4*>(lnb + qd * CP + 4 * i);
+      float4 u;
+      u.x = (v[i].x - mu) * rs * w.x + b.x;
+      u.y = (v[i].y - mu) * rs * w.y + b.y;
+      u.z = (v[i].z - mu) * rs * w.z + b.z;
+      u.w = (v[i].w - mu) * rs * w.w + b.w;
+      *reinterpret_cast<float4*>(U + r * ldu + qd * CP + 4 * i) = u;
+    }
   }
 }
 
@@ -207,17 +222,20 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
   static_assert(C * 9 * HPW <= SW_ROWS * LQ, "halo patch must fit the QKV region");
   // T: residual stream; Q: x halo patch [C][PH][HPW] (stage 0) -> QKV (O overwrites each wave's own query
   // columns) -> MLP hidden; stats: per-row (mean, rstd); lnp: LN1/LN2 affine parameters
-  __shared__ __attribute__((aligned(16))) float smem[SW_ROWS * LT + SW_ROWS * LQ + 2 * SW_ROWS + 4 * C];
+  // LN2 output U2 [SW_ROWS][LT] sits after the MLP hidden [SW_ROWS][LH] in the Q region (MLP1 reads U2 and
+  // writes the hidden: disjoint); LN1 output U1 sits in the V columns of the QKV tile (QKV's epilogue waits)
+  constexpr int QREG = (SW_ROWS * LQ > SW_ROWS * (LH + LT)) ? SW_ROWS * LQ : SW_ROWS * (LH + LT);
+  __shared__ __attribute__((aligned(16))) float smem[SW_ROWS * LT + QREG + 4 * C];
   float* T = smem;
   float* Q = smem + SW_ROWS * LT;
-  float* stats = Q + SW_ROWS * LQ;
-  float* lnp = stats + 2 * SW_ROWS;  // [ln1_w | ln1_b | ln2_w | ln2_b]
+  float* lnp = Q + QREG;  // [ln1_w | ln1_b | ln2_w | ln2_b]
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int l15 = lane & 15, g = lane >> 4;
   const int wh = W7 ? 7 : p.wh, ww = W7 ? 7 : p.ww, L = W7 ? 49 : p.L;
   const int H = p.H, W = p.W;
   const long HWl = (long)H * W;
+  const int HWi = H * W;  // per-image offsets are 32-bit (launcher checks C*H*W < 2^31): cheap addressing
   const int PH = wh + 2, PW = ww + 2;
 
   const long nwin_total = (long)p.B * p.nWin;
@@ -255,7 +273,9 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
       const int rr = (i * 4 + wid) * 7 + hl_r;
       const int c = rr / PH, py = rr - c * PH;
       const int hh = h0 + py;
-      hv[i] = (colok && rr < C * PH && hh >= 0 && hh < H) ? xb_[(long)c * HWl + (long)hh * W + wc] : 0.f;
+      const bool ok = colok && rr < C * PH && hh >= 0 && hh < H;
+      const float v = xb_[ok ? c * HWi + hh * W + wc : 0];  // branch-free: out-of-window lanes read element 0
+      hv[i] = ok ? v : 0.f;
     }
   };
   load_halo(gw);
@@ -312,7 +332,7 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
     YS_STAMP(2)
 
     // ---- stage 1: LN1 row statistics ----
-    lds_row_stats<C>(T, LT, stats, L, p.ln1_eps, tid);
+    lds_row_layernorm<C>(T, LT, Q + 2 * C, LQ, lnp, lnp + C, L, p.ln1_eps, tid);
     __syncthreads();
     YS_STAMP(3)
 
@@ -322,7 +342,8 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
       constexpr int NJ = NCB / 4;
       f32x4 acc[3][NJ];
       float ext[NJ];
-      wave_gemm_rows<C, NCB, true>(T, LT, f_in, acc, ext, stats, lnp, lnp + C, tid);
+      wave_gemm_rows<C, NCB, false>(Q + 2 * C, LQ, f_in, acc, ext, nullptr, nullptr, nullptr, tid);
+      __syncthreads();  // every wave has read U1 (the V columns) before any wave writes V
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const int n = (wid + 4 * j) * 16 + l15;
@@ -481,7 +502,7 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
     YS_STAMP(6)
 
     // ---- stage 5: LN2 row statistics ----
-    lds_row_stats<C>(T, LT, stats, L, p.ln2_eps, tid);
+    lds_row_layernorm<C>(T, LT, Q + SW_ROWS * LH, LT, lnp + 2 * C, lnp + 3 * C, L, p.ln2_eps, tid);
     __syncthreads();
     YS_STAMP(7)
 
@@ -492,7 +513,7 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
       constexpr int NJ = NCB / 4;
       f32x4 acc[3][NJ];
       float ext[NJ];
-      wave_gemm_rows<C, HID / 16, true>(T, LT, f_1, acc, ext, stats, lnp + 2 * C, lnp + 3 * C, tid);
+      wave_gemm_rows<C, HID / 16, false>(Q + SW_ROWS * LH, LT, f_1, acc, ext, nullptr, nullptr, nullptr, tid);
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const int n = (wid + 4 * j) * 16 + l15;
@@ -512,9 +533,9 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
     // stage-8 residual x (L2-hot: this window's halo) and BN terms of this wave's first channel block, loaded
     // here so their latency overlaps MLP2
     const int iy48 = XR / ww, ix48 = XR - (XR / ww) * ww;
-    const long pix48 = (XR < L && wy * wh + iy48 < H && wx * ww + ix48 < W)
-                           ? (long)(wy * wh + iy48) * W + wx * ww + ix48 : -1;
-    long pix[3];
+    const int pix48 = (XR < L && wy * wh + iy48 < H && wx * ww + ix48 < W)
+                          ? (wy * wh + iy48) * W + wx * ww + ix48 : -1;
+    int pix[3];
     float xr[3][4], x48, bsc[4], bsh[4];
     auto load_resid = [&](int cb) {
 #pragma unroll
@@ -522,12 +543,20 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
         const int tok = tb * 16 + l15;
         const int iy = tok / ww, ix = tok - iy * ww;
         const int hh = wy * wh + iy, wc = wx * ww + ix;
-        pix[tb] = (tok < L && hh < H && wc < W) ? (long)hh * W + wc : -1;
+        pix[tb] = (tok < L && hh < H && wc < W) ? hh * W + wc : -1;
+        const bool ok = pix[tb] >= 0 && !(p.abl & 4);
+        const int base = (cb * 16 + 4 * g) * HWi + pix[tb];
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          xr[tb][r] = (pix[tb] >= 0 && !(p.abl & 4)) ? xb[(long)(cb * 16 + 4 * g + r) * HWl + pix[tb]] : 0.f;
+        for (int r = 0; r < 4; ++r) {  // branch-free: lanes outside the image read element 0
+          const float v = xb[ok ? base + r * HWi : 0];
+          xr[tb][r] = ok ? v : 0.f;
+        }
       }
-      x48 = (pix48 >= 0 && g == 0 && !(p.abl & 4)) ? xb[(long)(cb * 16 + l15) * HWl + pix48] : 0.f;
+      {
+        const bool ok = pix48 >= 0 && g == 0 && !(p.abl & 4);
+        const float v = xb[ok ? (cb * 16 + l15) * HWi + pix48 : 0];
+        x48 = ok ? v : 0.f;
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         bsc[r] = bn_sc[cb * 16 + 4 * g + r];
@@ -611,12 +640,12 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int c = cb * 16 + 4 * g + r;
-            yb[(long)c * HWl + pix[tb]] = xr[tb][r] + silu_fast_(acc[tb][r] * bsc[r] + bsh[r]);
+            yb[c * HWi + pix[tb]] = xr[tb][r] + silu_fast_(acc[tb][r] * bsc[r] + bsh[r]);
           }
         }
         const int c48 = cb * 16 + l15;
         if (g == 0 && pix48 >= 0)
-          yb[(long)c48 * HWl + pix48] = x48 + silu_fast_(e48 * bn_sc[c48] + bn_sh[c48]);
+          yb[c48 * HWi + pix48] = x48 + silu_fast_(e48 * bn_sc[c48] + bn_sh[c48]);
       }
     }
     YS_STAMP(15)
@@ -664,6 +693,7 @@ int yolosod_swin_fused_launch(const float* x, float* y, int B, int C, int H, int
                               hipStream_t st) {
   const int L = wh * ww;
   if (L > SW_ROWS || wh > 7 || ww > 7 || mlp_hidden != 2 * C) return 0;
+  if ((long)C * H * W >= (1L << 31)) return 0;  // per-image offsets are 32-bit in the kernel
   SwinFusedArgs a{x, y, B, H, W, wh, ww, nWx, nWin, L, dw_w, ln1_w, ln1_b, ln1_eps, in_proj_w, in_proj_b,
                   out_proj_w, out_proj_b, ln2_w, ln2_b, ln2_eps, mlp1_w, mlp1_b, mlp2_w, mlp2_b, pw_w,
                   bn_scale, bn_shift, 1.0f / sqrtf((float)(C / num_heads)), 0, nullptr};
