@@ -384,7 +384,12 @@ static inline int launch_gemm(const GemmArgs& g0, int batch, bool b_kc, hipStrea
     const char* e = getenv("YOLOSOD_GEMM_TILE");
     return e ? atoi(e) : 0;
   }();
-  if (forced == 1 || (!forced && narrow)) YS_GEMM_LAUNCH(4, 1, 1, 2);
+  // 128x64 tiles also when 128x128 would leave CUs idle (fewer tiles than CUs) or waste > 10% of a tile column
+  // on a ragged N (e.g. N = H*W = 400): more, smaller workgroups for the small A2 / MHA GEMMs
+  const long t128 = (long)((g.M + 127) / 128) * ((g.N + 127) / 128) * batch;
+  const bool ragged = (long)((g.N + 127) / 128) * 128 - g.N > g.N / 10;
+  const bool small = !narrow && g.M > 64 && (t128 < 256 || ragged);
+  if (forced == 1 || (!forced && (narrow || small))) YS_GEMM_LAUNCH(4, 1, 1, 2);
   else if (forced == 3 || (!forced && g.M <= 64)) YS_GEMM_LAUNCH(1, 4, 2, 2);  // 64 x 256 tiles
   else YS_GEMM_LAUNCH(2, 2, 2, 2);
 #undef YS_GEMM_LAUNCH

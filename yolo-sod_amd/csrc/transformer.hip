@@ -208,6 +208,109 @@ __global__ __launch_bounds__(256) void attn_f32_kernel(const float* __restrict__
   }
 }
 
+// Whole-sequence attention for head dim 64, L <= 256 (A2: L = 8 areas x W = 160 at 640^2): one workgroup per
+// (sequence, head) with one wave per 16 queries, K and V of the head staged once in LDS (rows of 68 floats:
+// conflict-free 16-B reads). S^T = K Q^T is accumulated per 16-key block so that the accumulator registers are
+// directly the B operand of O^T = V^T P^T (keys permuted consistently): P never leaves registers. Q is scaled
+// before the product (q * scaling, the MHA math path of a2_attn.py:53). grid = (heads, n_seq), 64 * ceil(L/16)
+// threads.
+template <int NKB>
+__global__ __launch_bounds__(1024) void attn_seq64_kernel(const float* __restrict__ qkv, int ld, int C,
+                                                          float* __restrict__ out, int ldo, int L, float scale) {
+  constexpr int HD = 64, LK = HD + 4;
+  extern __shared__ __attribute__((aligned(16))) float kv[];  // K [NKB*16][LK] | V [NKB*16][LK]
+  float* Ks = kv;
+  float* Vs = kv + NKB * 16 * LK;
+  const int h = blockIdx.x;
+  const long row0 = (long)blockIdx.y * L;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int l15 = lane & 15, g = lane >> 4;
+  // stage K and V (float4 rows; keys >= L zero)
+  for (int e = tid; e < NKB * 16 * (HD / 4); e += blockDim.x) {
+    const int key = e / (HD / 4), q4 = e - key * (HD / 4);
+    float4 k = make_float4(0.f, 0.f, 0.f, 0.f), v = k;
+    if (key < L) {
+      const float* src = qkv + (row0 + key) * ld + h * HD + 4 * q4;
+      k = *reinterpret_cast<const float4*>(src + C);
+      v = *reinterpret_cast<const float4*>(src + 2 * C);
+    }
+    *reinterpret_cast<float4*>(Ks + key * LK + 4 * q4) = k;
+    *reinterpret_cast<float4*>(Vs + key * LK + 4 * q4) = v;
+  }
+  // this wave's 16 queries: lane (g, l15) holds Q[q0 + l15][16g .. 16g+16) * scale (MFMA k permuted by 16g)
+  const int q = wv * 16 + l15;
+  float4 qf[4];
+  {
+    const int qr = q < L ? q : L - 1;
+    const float* src = qkv + (row0 + qr) * ld + h * HD + 16 * g;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      float4 v = *reinterpret_cast<const float4*>(src + 4 * t);
+      v.x *= scale; v.y *= scale; v.z *= scale; v.w *= scale;
+      qf[t] = v;
+    }
+  }
+  __syncthreads();
+  f32x4 st[NKB];
+#pragma unroll
+  for (int kb = 0; kb < NKB; ++kb) {
+    f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f};
+    const float* kr = Ks + (kb * 16 + l15) * LK + 16 * g;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const float4 k = *reinterpret_cast<const float4*>(kr + 4 * t);
+      a = __builtin_amdgcn_mfma_f32_16x16x4f32(k.x, qf[t].x, a, 0, 0, 0);
+      a = __builtin_amdgcn_mfma_f32_16x16x4f32(k.y, qf[t].y, a, 0, 0, 0);
+      a = __builtin_amdgcn_mfma_f32_16x16x4f32(k.z, qf[t].z, a, 0, 0, 0);
+      a = __builtin_amdgcn_mfma_f32_16x16x4f32(k.w, qf[t].w, a, 0, 0, 0);
+    }
+    st[kb] = a;
+  }
+  // lane holds S^T[key = kb*16 + 4g + r][query l15]: softmax over keys (in-lane, then the 4 lane groups)
+  float mx = -INFINITY;
+#pragma unroll
+  for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (kb * 16 + 4 * g + r >= L) st[kb][r] = -INFINITY;
+      mx = fmaxf(mx, st[kb][r]);
+    }
+  mx = xor32_max(xor16_max(mx));
+  float sum = 0.f;
+#pragma unroll
+  for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float e = expf(st[kb][r] - mx);
+      st[kb][r] = e;
+      sum += e;
+    }
+  sum = xor32_sum(xor16_sum(sum));
+  const float inv = 1.0f / sum;
+#pragma unroll
+  for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) st[kb][r] *= inv;
+  // O^T[d][q] = sum_key V[key][d] P[q][key]
+  f32x4 o[HD / 16];
+#pragma unroll
+  for (int db = 0; db < HD / 16; ++db) o[db] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float* vr = Vs + (kb * 16 + 4 * g + r) * LK + l15;
+#pragma unroll
+      for (int db = 0; db < HD / 16; ++db)
+        o[db] = __builtin_amdgcn_mfma_f32_16x16x4f32(vr[db * 16], st[kb][r], o[db], 0, 0, 0);
+    }
+  if (q < L) {
+    float* dst = out + (row0 + q) * ldo + h * HD + 4 * g;
+#pragma unroll
+    for (int db = 0; db < HD / 16; ++db) *reinterpret_cast<f32x4*>(dst + db * 16) = o[db];
+  }
+}
+
 template <int HD>
 static void launch_attn_hd(int nkb, dim3 grid, hipStream_t st, const float* qkv, int ld, int C, float* out, int ldo,
                            int L, float scale) {
@@ -232,6 +335,18 @@ static int launch_attention(const float* qkv, float* out, long n_seq, int L, int
   YS_CHECK_ARG(n_seq < 65536, "attention: too many sequences (%ld)", n_seq);
   const int nkb = (L + 15) / 16;
   const float scale = 1.0f / sqrtf((float)hd);
+  if (hd == 64 && nkb <= 16 && (3 * C) % 4 == 0 && C % 4 == 0) {  // whole-sequence kernel (A2 at 640^2: L = 160)
+    dim3 g2((unsigned)heads, (unsigned)n_seq);
+#define YS_ATTN_SEQ(N)                                                                                       \
+    if (nkb <= N) {                                                                                            \
+      const size_t lds = (size_t)2 * N * 16 * 68 * sizeof(float); /* K | V for N key blocks */                \
+      hipLaunchKernelGGL((attn_seq64_kernel<N>), g2, dim3(64 * nkb), lds, st, qkv, 3 * C, C, out, C, L, scale); \
+      YS_CHECK_LAUNCH("attention_seq");                                                                       \
+      return 0;                                                                                                \
+    }
+    YS_ATTN_SEQ(4) YS_ATTN_SEQ(8) YS_ATTN_SEQ(10) YS_ATTN_SEQ(12) YS_ATTN_SEQ(16)
+#undef YS_ATTN_SEQ
+  }
   dim3 grid((L + 63) / 64, heads, (unsigned)n_seq);
   switch (hd) {
     case 8: launch_attn_hd<8>(nkb, grid, st, qkv, 3 * C, C, out, C, L, scale); break;
