@@ -71,7 +71,8 @@ def load_library() -> ctypes.CDLL:
             raise RuntimeError(
                 f"yolosod_amd: HIP library {LIB_PATH} is missing - run __graft_entry__.build() "
                 "(or python yolo-sod_amd/build.py). There is no CPU fallback.")
-        lib = ctypes.CDLL(str(LIB_PATH))
+        path = os.environ.get("YOLOSOD_LIB_AB") or str(LIB_PATH)  # diagnostic A/B builds only
+        lib = ctypes.CDLL(path)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(lib, name)
             fn.restype = res

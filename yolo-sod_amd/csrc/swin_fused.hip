@@ -53,7 +53,7 @@ struct SwinFusedArgs {
   const float* bn_scale;
   const float* bn_shift;
   float scale;
-  int abl;  // timing ablation (debug only): 1 skip halo loads, 2 skip weight loads, 4 skip residual loads
+  int abl;  // timing ablation (debug only): 1 skip halo loads, 4 skip residual loads
   unsigned long long* stamps;  // diagnostic build only: per-stage s_memtime of wave 0 ([window][16]) or nullptr
 };
 
@@ -80,7 +80,7 @@ struct WFrag {
 };
 
 template <int K, int NCB>
-__device__ __forceinline__ void load_wfrag(const float* __restrict__ Wg, WFrag<K, NCB>& f, int abl, int tid) {
+__device__ __forceinline__ void load_wfrag(const float* __restrict__ Wg, WFrag<K, NCB>& f, int tid) {
   const int lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l15 = lane & 15, g = lane >> 4;
 #pragma unroll
@@ -88,7 +88,7 @@ __device__ __forceinline__ void load_wfrag(const float* __restrict__ Wg, WFrag<K
 #pragma unroll
     for (int j = 0; j < NCB / 4; ++j) {
       const float* wr = Wg + (long)((wid + 4 * j) * 16 + l15) * K + g * (K / 4);
-      f.v[j][t] = (abl & 2) ? make_float4(0.f, 0.f, 0.f, 0.f) : *reinterpret_cast<const float4*>(wr + 4 * t);
+      f.v[j][t] = *reinterpret_cast<const float4*>(wr + 4 * t);
     }
 }
 
@@ -177,26 +177,25 @@ __device__ __forceinline__ void lds_row_layernorm(const float* S, int lds, float
     v[i] = valid ? *reinterpret_cast<const float4*>(S + r * lds + qd * CP + 4 * i) : make_float4(0.f, 0.f, 0.f, 0.f);
     s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
   }
-  const float mean = quad_sum(s) / (float)C;
+  const float mean = quad_sum(s) * (1.0f / (float)C);  // C is a power of two: exact
   float q = 0.f;
 #pragma unroll
-  for (int i = 0; i < CP / 4; ++i) {
-    const float a0 = v[i].x - mean, a1 = v[i].y - mean, a2 = v[i].z - mean, a3 = v[i].w - mean;
-    q += (a0 * a0 + a1 * a1) + (a2 * a2 + a3 * a3);
+  for (int i = 0; i < CP / 4; ++i) {  // centred values kept for the output pass
+    v[i].x -= mean; v[i].y -= mean; v[i].z -= mean; v[i].w -= mean;
+    q += (v[i].x * v[i].x + v[i].y * v[i].y) + (v[i].z * v[i].z + v[i].w * v[i].w);
   }
-  const float var = quad_sum(q) / (float)C;
-  const float mu = valid ? mean : 0.f;
-  const float rs = valid ? 1.0f / sqrtf(var + eps) : 0.f;
+  const float var = quad_sum(q) * (1.0f / (float)C);
+  const float rs = valid ? __builtin_amdgcn_rsqf(var + eps) : 0.f;  // v_rsq_f32 (1 ulp)
   if (r < SW_ROWS) {
 #pragma unroll
     for (int i = 0; i < CP / 4; ++i) {
       const float4 w = *reinterpret_cast<const float4*>(lnw + qd * CP + 4 * i);
       const float4 b = *reinterpret_cast<const float4*>(lnb + qd * CP + 4 * i);
       float4 u;
-      u.x = (v[i].x - mu) * rs * w.x + b.x;
-      u.y = (v[i].y - mu) * rs * w.y + b.y;
-      u.z = (v[i].z - mu) * rs * w.z + b.z;
-      u.w = (v[i].w - mu) * rs * w.w + b.w;
+      u.x = v[i].x * rs * w.x + b.x;
+      u.y = v[i].y * rs * w.y + b.y;
+      u.z = v[i].z * rs * w.z + b.z;
+      u.w = v[i].w * rs * w.w + b.w;
       *reinterpret_cast<float4*>(U + r * ldu + qd * CP + 4 * i) = u;
     }
   }
@@ -219,7 +218,7 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
   static_assert(HD % 16 == 0 && HD <= 64, "head dim");
   static_assert(LH <= LQ, "MLP hidden must fit the QKV region");
   static_assert(256 % C == 0 || C % 256 == 0, "depthwise channel mapping");
-  static_assert(C * 9 * HPW <= SW_ROWS * LQ, "halo patch must fit the QKV region");
+  static_assert(3 * ((C + 2) / 3) * 9 * HPW <= SW_ROWS * LQ, "halo patch must fit the QKV region");
   // T: residual stream; Q: x halo patch [C][PH][HPW] (stage 0) -> QKV (O overwrites each wave's own query
   // columns) -> MLP hidden; stats: per-row (mean, rstd); lnp: LN1/LN2 affine parameters
   // LN2 output U2 [SW_ROWS][LT] sits after the MLP hidden [SW_ROWS][LH] in the Q region (MLP1 reads U2 and
@@ -235,7 +234,7 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
   const int wh = W7 ? 7 : p.wh, ww = W7 ? 7 : p.ww, L = W7 ? 49 : p.L;
   const int H = p.H, W = p.W;
   const long HWl = (long)H * W;
-  const int HWi = H * W;  // per-image offsets are 32-bit (launcher checks C*H*W < 2^31): cheap addressing
+  const int HWi = H * W;  // per-image offsets are 32-bit (launcher checks C*H*W < 2^30): cheap addressing
   const int PH = wh + 2, PW = ww + 2;
 
   const long nwin_total = (long)p.B * p.nWin;
@@ -258,24 +257,50 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
   for (int i = 0; i < 9; ++i) dwk[i] = p.dw[dw_c * 9 + i];
 
   // halo patch [C][PH][PW] of window gwin into registers: lane = 9 * row + column (lane 63 idle), so one
-  // wave-instruction reads 7 row segments of 9 floats (~14 cache lines) instead of 64 rows of one float each
-  float hv[NHL];
+  // wave-instruction reads 7 row segments of 9 floats (~14 cache lines) instead of 64 rows of one float each.
+  // W7 (PH = 9): row slot s = 7*wid + row < 27 is (channel 3i + s/9, patch row s%9) at step i, so a lane's offset
+  // is fixed across steps (the step advances the scalar soffset by 3 planes) and out-of-image lanes get an
+  // out-of-range voffset that the buffer load returns as 0: no per-load VALU. Slot 27 idles.
+  constexpr int NHS = (C + 2) / 3;                 // W7 steps (3 channels each)
+  constexpr int NHV = NHS > NHL ? NHS : NHL;
+  float hv[NHV];
   const int hl_r = lane / 9, hl_px = lane - (lane / 9) * 9;
+  const int hslot = 7 * wid + hl_r;                 // W7 row slot (valid < 27)
+  const int hcs = hslot / 9, hpy = hslot - (hslot / 9) * 9;
+  constexpr unsigned OOB = 0x80000000u;             // > any image's byte size (< 2^32 with the largest soffset)
   auto load_halo = [&](long gwin) {
-    const int im = (int)(gwin / p.nWin), wn = (int)(gwin % p.nWin);
-    const int wy_ = wn / p.nWx, wx_ = wn % p.nWx;
+    const int gwi = __builtin_amdgcn_readfirstlane((int)gwin);  // window counts are < 2^31 (launcher)
+    const int im = gwi / p.nWin, wn = gwi - (gwi / p.nWin) * p.nWin;
+    const int wy_ = wn / p.nWx, wx_ = wn - (wn / p.nWx) * p.nWx;
     const int h0 = wy_ * wh - 1, w0 = wx_ * ww - 1;
     const float* xb_ = p.x + (long)im * C * HWl;
     const int wc = w0 + hl_px;
     const bool colok = hl_r < 7 && hl_px < PW && wc >= 0 && wc < W && !(p.abl & 1);
+    if (W7) {
+      // descriptor from provably wave-uniform words (otherwise every load becomes a readfirstlane waterfall)
+      const unsigned long long xa = (unsigned long long)xb_;
+      const unsigned long long xu = ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(xa >> 32)) << 32) |
+                                    (unsigned)__builtin_amdgcn_readfirstlane((unsigned)xa);
+      const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)xu, (short)0, __builtin_amdgcn_readfirstlane(C * HWi * 4), 0x00020000);
+      const int hh = h0 + hpy;
+      const bool ok = colok && hslot < 27 && (unsigned)hh < (unsigned)H;
+      const unsigned voff = ok ? (unsigned)((hcs * HWi + hh * W + wc) * 4) : OOB;
+      const unsigned vlast = (3 * (NHS - 1) + hcs < C) ? voff : OOB;  // channel bound of the last step
 #pragma unroll
-    for (int i = 0; i < NHL; ++i) {
-      const int rr = (i * 4 + wid) * 7 + hl_r;
-      const int c = rr / PH, py = rr - c * PH;
-      const int hh = h0 + py;
-      const bool ok = colok && rr < C * PH && hh >= 0 && hh < H;
-      const float v = xb_[ok ? c * HWi + hh * W + wc : 0];  // branch-free: out-of-window lanes read element 0
-      hv[i] = ok ? v : 0.f;
+      for (int i = 0; i < NHS; ++i)
+        hv[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, i == NHS - 1 ? vlast : voff,
+                                                                              i * 3 * HWi * 4, 0));
+    } else {
+#pragma unroll
+      for (int i = 0; i < NHL; ++i) {
+        const int rr = (i * 4 + wid) * 7 + hl_r;
+        const int c = rr / PH, py = rr - c * PH;
+        const int hh = h0 + py;
+        const bool ok = colok && rr < C * PH && hh >= 0 && hh < H;
+        const float v = xb_[ok ? c * HWi + hh * W + wc : 0];  // branch-free: out-of-window lanes read element 0
+        hv[i] = ok ? v : 0.f;
+      }
     }
   };
   load_halo(gw);
@@ -283,25 +308,37 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
   for (;;) {
     const long gnext = gw + wpx;
     const bool has_next = PERSIST && gnext < xend;
-    const int img = (int)(gw / p.nWin), win = (int)(gw % p.nWin);
-    const int wy = win / p.nWx, wx = win % p.nWx;
+    const int gwc = __builtin_amdgcn_readfirstlane((int)gw);
+    const int img = gwc / p.nWin, win = gwc - (gwc / p.nWin) * p.nWin;
+    const int wy = win / p.nWx, wx = win - (win / p.nWx) * p.nWx;
     const float* xb = p.x + (long)img * C * HWl;
     // parameter pointers laundered per window: otherwise the compiler hoists every (loop-invariant) weight
     // fragment and bias load out of the window loop and spills them
     const float *w_in = p.win, *b_in = p.bin, *w_o = p.wo, *b_o = p.bo, *w_1 = p.w1, *b_1 = p.b1, *w_2 = p.w2,
                 *b_2 = p.b2, *w_pw = p.wpw, *bn_sc = p.bn_scale, *bn_sh = p.bn_shift;
-    asm volatile("" : "+s"(w_in), "+s"(b_in), "+s"(w_o), "+s"(b_o), "+s"(w_1), "+s"(b_1));
-    asm volatile("" : "+s"(w_2), "+s"(b_2), "+s"(w_pw), "+s"(bn_sc), "+s"(bn_sh));
+    // (persistent build only: the laundered pointers lose their global address space, so every weight load
+    // becomes a flat load that also counts in lgkmcnt and is waited for by each LDS wait)
+    if (PERSIST) {
+      asm volatile("" : "+s"(w_in), "+s"(b_in), "+s"(w_o), "+s"(b_o), "+s"(w_1), "+s"(b_1));
+      asm volatile("" : "+s"(w_2), "+s"(b_2), "+s"(w_pw), "+s"(bn_sc), "+s"(bn_sh));
+    }
     YS_STAMP(0)
     // QKV weight fragments: in flight during the halo store, the depthwise conv and the LN1 statistics
     WFrag<C, 3 * C / 16> f_in;
-    load_wfrag(w_in, f_in, p.abl, tid);
+    load_wfrag(w_in, f_in, tid);
 
     // ---- stage 0: halo patch (registers) -> LDS [c][py][HPW] -> dw conv, one output row of 7 tokens per item ----
+    if (W7) {
+      if (hl_r < 7 && hslot < 27) {  // patch row 9*(3i + hcs) + hpy = 27i + hslot; rows of channels >= C are unused
 #pragma unroll
-    for (int i = 0; i < NHL; ++i) {
-      const int rr = (i * 4 + wid) * 7 + hl_r;
-      if (hl_r < 7 && rr < C * PH) Q[rr * HPW + hl_px] = hv[i];  // columns 9..11 of a row are never read
+        for (int i = 0; i < NHS; ++i) Q[(27 * i + hslot) * HPW + hl_px] = hv[i];
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NHL; ++i) {
+        const int rr = (i * 4 + wid) * 7 + hl_r;
+        if (hl_r < 7 && rr < C * PH) Q[rr * HPW + hl_px] = hv[i];  // columns 9..11 of a row are never read
+      }
     }
     __syncthreads();
     YS_STAMP(1)
@@ -356,7 +393,7 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
       }
     }
     WFrag<C, C / 16> f_o;  // out-proj weights: in flight during attention
-    load_wfrag(w_o, f_o, p.abl, tid);
+    load_wfrag(w_o, f_o, tid);
     __syncthreads();
     YS_STAMP(4)
 
@@ -401,40 +438,39 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
         for (int h = 0; h < NH; ++h) s48[h] = dot4_acc(k48[h], qv[h], s48[h]);
       }
       // lane holds S^T[key = kb*16 + 4g + r][q = l15] per head (+ key 48 after the group sum): softmax over keys
-      float p48[NH];
+      // on the raw scores (scale > 0 commutes with the max), exp2 with scale*log2(e) folded into one FMA; the
+      // 1/sum normalisation is applied to O (per query = per lane) instead of to the 49 probabilities
+      const float c2 = p.scale * 1.44269504088896341f;
+      float p48[NH], inv[NH];
 #pragma unroll
       for (int h = 0; h < NH; ++h) {
         const bool k48ok = XR < L;
-        const float sv48 = k48ok ? group4_sum(s48[h]) * p.scale : -INFINITY;
+        const float sv48 = k48ok ? group4_sum(s48[h]) : -INFINITY;
         float mx = sv48;
 #pragma unroll
         for (int kb = 0; kb < 3; ++kb)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int key = kb * 16 + 4 * g + r;
-            const float sv = (key < L) ? st[h][kb][r] * p.scale : -INFINITY;
+            const float sv = (key < L) ? st[h][kb][r] : -INFINITY;
             st[h][kb][r] = sv;
             mx = fmaxf(mx, sv);
           }
         mx = xor32_max(xor16_max(mx));
+        const float mc = -mx * c2;
         float sum = 0.f;
 #pragma unroll
         for (int kb = 0; kb < 3; ++kb)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float e = __expf(st[h][kb][r] - mx);
+            const float e = __builtin_amdgcn_exp2f(fmaf(st[h][kb][r], c2, mc));
             st[h][kb][r] = e;
             sum += e;
           }
-        const float e48 = __expf(sv48 - mx);
+        const float e48 = __builtin_amdgcn_exp2f(fmaf(sv48, c2, mc));
         sum += (g == 0) ? e48 : 0.f;
-        sum = group4_sum(sum);
-        const float inv = 1.0f / sum;
-#pragma unroll
-        for (int kb = 0; kb < 3; ++kb)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) st[h][kb][r] *= inv;
-        p48[h] = e48 * inv;
+        inv[h] = __builtin_amdgcn_rcpf(group4_sum(sum));
+        p48[h] = e48;
       }
       // O^T[d][q] = sum_key V[key][d] P[q][key]; MFMA (kb, r) consumes keys {kb*16 + 4g' + r}; key 48 rank-1 update
       f32x4 o[NH][HD / 16];
@@ -457,10 +493,10 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
 #pragma unroll
         for (int db = 0; db < HD / 16; ++db) {
           const float4 v48 = *reinterpret_cast<const float4*>(Q + XR * LQ + 2 * C + h * HD + db * 16 + 4 * g);
-          o[h][db][0] = fmaf(v48.x, p48[h], o[h][db][0]);
-          o[h][db][1] = fmaf(v48.y, p48[h], o[h][db][1]);
-          o[h][db][2] = fmaf(v48.z, p48[h], o[h][db][2]);
-          o[h][db][3] = fmaf(v48.w, p48[h], o[h][db][3]);
+          o[h][db][0] = fmaf(v48.x, p48[h], o[h][db][0]) * inv[h];
+          o[h][db][1] = fmaf(v48.y, p48[h], o[h][db][1]) * inv[h];
+          o[h][db][2] = fmaf(v48.z, p48[h], o[h][db][2]) * inv[h];
+          o[h][db][3] = fmaf(v48.w, p48[h], o[h][db][3]) * inv[h];
         }
       // lane holds O^T[d = db*16 + 4g + r][q = l15] -> O[q][h*HD + d] (4 consecutive d) into the q columns
       const int q = qb * 16 + l15;
@@ -497,7 +533,7 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
       }
     }
     WFrag<C, HID / 16> f_1;  // MLP1 weights: in flight during the LN2 statistics
-    load_wfrag(w_1, f_1, p.abl, tid);
+    load_wfrag(w_1, f_1, tid);
     __syncthreads();
     YS_STAMP(6)
 
@@ -521,42 +557,58 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
 #pragma unroll
         for (int rb = 0; rb < 3; ++rb)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) Hd[(rb * 16 + g * 4 + r) * LH + n] = gelu_fast_(acc[rb][j][r] + bias);
+          for (int r = 0; r < 4; r += 2) {
+            const f32x2 hv2 = gelu2_fast_(f32x2{acc[rb][j][r], acc[rb][j][r + 1]} + bias);
+            Hd[(rb * 16 + g * 4 + r) * LH + n] = hv2.x;
+            Hd[(rb * 16 + g * 4 + r + 1) * LH + n] = hv2.y;
+          }
         if (g == 0) Hd[XR * LH + n] = gelu_fast_(ext[j] + bias);
       }
     }
     WFrag<HID, C / 16> f_2;  // MLP2 weights
-    load_wfrag(w_2, f_2, p.abl, tid);
+    load_wfrag(w_2, f_2, tid);
     __syncthreads();
     YS_STAMP(8)
 
     // stage-8 residual x (L2-hot: this window's halo) and BN terms of this wave's first channel block, loaded
-    // here so their latency overlaps MLP2
+    // here so their latency overlaps MLP2. Residual loads and y stores are buffer ops on per-image descriptors:
+    // a lane's voffset is fixed (its token, channel row 4g (+ l15 for token 48) of the wave's first block; out-of-
+    // image tokens get an out-of-range voffset: loads return 0, stores are dropped) and the channel
+    // ((cb - wid)*16 + r planes) goes into the scalar soffset.
     const int iy48 = XR / ww, ix48 = XR - (XR / ww) * ww;
     const int pix48 = (XR < L && wy * wh + iy48 < H && wx * ww + ix48 < W)
                           ? (wy * wh + iy48) * W + wx * ww + ix48 : -1;
-    int pix[3];
+    const unsigned long long ya = (unsigned long long)(p.y + (long)img * C * HWl);
+    const unsigned long long xa8 = (unsigned long long)xb;
+    const __amdgpu_buffer_rsrc_t rx8 = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(xa8 >> 32)) << 32) |
+                (unsigned)__builtin_amdgcn_readfirstlane((unsigned)xa8)),
+        (short)0, __builtin_amdgcn_readfirstlane(C * HWi * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t ry8 = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(ya >> 32)) << 32) |
+                (unsigned)__builtin_amdgcn_readfirstlane((unsigned)ya)),
+        (short)0, __builtin_amdgcn_readfirstlane(C * HWi * 4), 0x00020000);
+    unsigned vtok[3];  // byte offset of (channel wid*16 + 4g, token tb*16 + l15), or OOB
+#pragma unroll
+    for (int tb = 0; tb < 3; ++tb) {
+      const int tok = tb * 16 + l15;
+      const int iy = tok / ww, ix = tok - iy * ww;
+      const int hh = wy * wh + iy, wc = wx * ww + ix;
+      const bool ok = tok < L && hh < H && wc < W;
+      vtok[tb] = ok ? (unsigned)(((wid * 16 + 4 * g) * HWi + hh * W + wc) * 4) : OOB;
+    }
+    const unsigned v48 = (pix48 >= 0 && g == 0) ? (unsigned)(((wid * 16 + l15) * HWi + pix48) * 4) : OOB;
     float xr[3][4], x48, bsc[4], bsh[4];
     auto load_resid = [&](int cb) {
+      const int sb = (cb - wid) * 16 * HWi * 4;
+      const bool skip = p.abl & 4;
 #pragma unroll
-      for (int tb = 0; tb < 3; ++tb) {
-        const int tok = tb * 16 + l15;
-        const int iy = tok / ww, ix = tok - iy * ww;
-        const int hh = wy * wh + iy, wc = wx * ww + ix;
-        pix[tb] = (tok < L && hh < H && wc < W) ? hh * W + wc : -1;
-        const bool ok = pix[tb] >= 0 && !(p.abl & 4);
-        const int base = (cb * 16 + 4 * g) * HWi + pix[tb];
+      for (int tb = 0; tb < 3; ++tb)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {  // branch-free: lanes outside the image read element 0
-          const float v = xb[ok ? base + r * HWi : 0];
-          xr[tb][r] = ok ? v : 0.f;
-        }
-      }
-      {
-        const bool ok = pix48 >= 0 && g == 0 && !(p.abl & 4);
-        const float v = xb[ok ? (cb * 16 + l15) * HWi + pix48 : 0];
-        x48 = ok ? v : 0.f;
-      }
+        for (int r = 0; r < 4; ++r)
+          xr[tb][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx8, skip ? OOB : vtok[tb],
+                                                                                    sb + r * HWi * 4, 0));
+      x48 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx8, skip ? OOB : v48, sb, 0));
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         bsc[r] = bn_sc[cb * 16 + 4 * g + r];
@@ -603,7 +655,6 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
     // ---- stage 8: y = x + SiLU(BN(Wpw T^T)); output tile Y^T[c][tok] (lanes over tokens), token 48 on the VALU ----
     {
       constexpr int NCB = C / 16;
-      float* yb = p.y + (long)img * C * HWl;
       for (int cb = wid; cb < NCB; cb += 4) {
         const float* wrow = w_pw + (long)(cb * 16 + l15) * C + g * CQ;
         if (cb != wid) load_resid(cb);
@@ -634,18 +685,17 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
         }
         e48 = group4_sum(e48);
         // lane holds Y^T[c = cb*16 + 4g + r][tok = tb*16 + l15]
+        const int sb = (cb - wid) * 16 * HWi * 4;
 #pragma unroll
-        for (int tb = 0; tb < 3; ++tb) {
-          if (pix[tb] < 0) continue;
+        for (int tb = 0; tb < 3; ++tb)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int c = cb * 16 + 4 * g + r;
-            yb[c * HWi + pix[tb]] = xr[tb][r] + silu_fast_(acc[tb][r] * bsc[r] + bsh[r]);
-          }
-        }
+          for (int r = 0; r < 4; ++r)
+            __builtin_amdgcn_raw_buffer_store_b32(
+                __builtin_bit_cast(unsigned, xr[tb][r] + silu_fast_(acc[tb][r] * bsc[r] + bsh[r])), ry8, vtok[tb],
+                sb + r * HWi * 4, 0);
         const int c48 = cb * 16 + l15;
-        if (g == 0 && pix48 >= 0)
-          yb[c48 * HWi + pix48] = x48 + silu_fast_(e48 * bn_sc[c48] + bn_sh[c48]);
+        __builtin_amdgcn_raw_buffer_store_b32(
+            __builtin_bit_cast(unsigned, x48 + silu_fast_(e48 * bn_sc[c48] + bn_sh[c48])), ry8, v48, sb, 0);
       }
     }
     YS_STAMP(15)
@@ -693,7 +743,8 @@ int yolosod_swin_fused_launch(const float* x, float* y, int B, int C, int H, int
                               hipStream_t st) {
   const int L = wh * ww;
   if (L > SW_ROWS || wh > 7 || ww > 7 || mlp_hidden != 2 * C) return 0;
-  if ((long)C * H * W >= (1L << 31)) return 0;  // per-image offsets are 32-bit in the kernel
+  if ((long)C * H * W >= (1L << 30)) return 0;  // per-image byte offsets are 32-bit (buffer loads) in the kernel
+  if ((long)B * nWin >= (1L << 31)) return 0;    // window indices are 32-bit
   SwinFusedArgs a{x, y, B, H, W, wh, ww, nWx, nWin, L, dw_w, ln1_w, ln1_b, ln1_eps, in_proj_w, in_proj_b,
                   out_proj_w, out_proj_b, ln2_w, ln2_b, ln2_eps, mlp1_w, mlp1_b, mlp2_w, mlp2_b, pw_w,
                   bn_scale, bn_shift, 1.0f / sqrtf((float)(C / num_heads)), 0, nullptr};

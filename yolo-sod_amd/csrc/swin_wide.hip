@@ -444,7 +444,11 @@ __global__ __launch_bounds__(NT, 1) void swin_wide_kernel(Args p) {
 #pragma unroll
         for (int rb = 0; rb < 3; ++rb)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) WK[(rb * 16 + 4 * g + r) * LHC + nl[j]] = gelu_fast_(acc[rb][j][r] + bias);
+          for (int r = 0; r < 4; r += 2) {
+            const f32x2 hv2 = gelu2_fast_(f32x2{acc[rb][j][r], acc[rb][j][r + 1]} + bias);
+            WK[(rb * 16 + 4 * g + r) * LHC + nl[j]] = hv2.x;
+            WK[(rb * 16 + 4 * g + r + 1) * LHC + nl[j]] = hv2.y;
+          }
         if (g == 0) WK[XR * LHC + nl[j]] = gelu_fast_(e + bias);
       }
     }
