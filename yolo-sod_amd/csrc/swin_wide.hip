@@ -34,7 +34,7 @@ constexpr int LHC = 256 + 4;    // MLP hidden chunk
 constexpr int HPW = 12;         // halo row stride
 constexpr int HALF = 128;       // channels per halo half
 constexpr int WK_ELEMS = ROWS * LQ2;
-static_assert(HALF * 9 * HPW <= WK_ELEMS && ROWS * LHC <= WK_ELEMS, "work region");
+static_assert(54 * ((HALF + 5) / 6) * HPW <= WK_ELEMS && ROWS * LHC <= WK_ELEMS, "work region");
 constexpr int NT = 512;         // threads
 
 struct Args {
@@ -89,14 +89,14 @@ __device__ __forceinline__ void gemm_stream(const float* __restrict__ As, int ld
   constexpr int NCH = KQ / (4 * CK);
   const int l15 = lane & 15, g = lane >> 4;
   const float* arow[4];
-  float mu[4], rs[4];
+  float rs[4], nmr[4];  // LN: A' = (a*rs - mu*rs) * w + b, two packed FMAs per pair of elements
 #pragma unroll
   for (int rb = 0; rb < 4; ++rb) {
     const int r = rb < 3 ? rb * 16 + l15 : XR;
     arow[rb] = As + r * lda + g * KQ;
     if (LN) {
-      mu[rb] = stats[2 * r];
       rs[rb] = stats[2 * r + 1];
+      nmr[rb] = -stats[2 * r] * rs[rb];
     }
   }
   float4 wb0[NJ][CK], wb1[NJ][CK];
@@ -118,10 +118,12 @@ __device__ __forceinline__ void gemm_stream(const float* __restrict__ As, int ld
         const float4 bb = *reinterpret_cast<const float4*>(lnb + g * KQ + ko);
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb) {
-          a[rb].x = (a[rb].x - mu[rb]) * rs[rb] * w.x + bb.x;
-          a[rb].y = (a[rb].y - mu[rb]) * rs[rb] * w.y + bb.y;
-          a[rb].z = (a[rb].z - mu[rb]) * rs[rb] * w.z + bb.z;
-          a[rb].w = (a[rb].w - mu[rb]) * rs[rb] * w.w + bb.w;
+          const f32x2 r2 = {rs[rb], rs[rb]}, m2 = {nmr[rb], nmr[rb]};
+          const f32x2 lo = __builtin_elementwise_fma(
+              __builtin_elementwise_fma(f32x2{a[rb].x, a[rb].y}, r2, m2), f32x2{w.x, w.y}, f32x2{bb.x, bb.y});
+          const f32x2 hi = __builtin_elementwise_fma(
+              __builtin_elementwise_fma(f32x2{a[rb].z, a[rb].w}, r2, m2), f32x2{w.z, w.w}, f32x2{bb.z, bb.w});
+          a[rb] = make_float4(lo.x, lo.y, hi.x, hi.y);
         }
       }
 #pragma unroll
@@ -193,29 +195,39 @@ __global__ __launch_bounds__(NT, 1) void swin_wide_kernel(Args p) {
   const long per_xcd = (nwin_total + 7) >> 3;
   const long gw = (long)(blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
   if (gw >= nwin_total) return;
-  const int img = (int)(gw / p.nWin), win = (int)(gw % p.nWin);
-  const int wy = win / p.nWx, wx = win % p.nWx;
+  const int gwi = __builtin_amdgcn_readfirstlane((int)gw);  // window counts < 2^31 (launcher)
+  const int img = gwi / p.nWin, win = gwi - (gwi / p.nWin) * p.nWin;
+  const int wy = win / p.nWx, wx = win - (win / p.nWx) * p.nWx;
   const float* xb = p.x + (long)img * C * HWl;
   const int h0 = wy * 7 - 1, w0 = wx * 7 - 1;
 
   // halo of both channel halves into registers: lane = 9 * row + column (lane 63 idle), so a wave-instruction
-  // reads 7 row segments of 9 floats; 8 waves x 7 rows per step, 1152 rows (128 channels x 9) per half
-  constexpr int NR = (HALF * 9 + 8 * 7 - 1) / (8 * 7);
+  // reads 7 row segments of 9 floats. Row slot s = 7*wid + row < 54 is (channel 6i + s/9, patch row s%9) at step
+  // i: a lane's byte offset is fixed, the step and the half go into the scalar soffset, and out-of-image lanes
+  // get an out-of-range voffset (the buffer load returns 0) - no per-load VALU. Slots 54, 55 idle.
+  constexpr int NR = (HALF + 5) / 6;
+  constexpr unsigned OOB = 0x80000000u;
   float hv[2][NR];
   const int hl_r = lane / 9, hl_px = lane - (lane / 9) * 9;
+  const int hslot = 7 * wid + hl_r;
   {
-    const int wc = w0 + hl_px;
-    const bool colok = hl_r < 7 && wc >= 0 && wc < W;
+    const int hcs = hslot / 9, hpy = hslot - (hslot / 9) * 9;
+    const int wc = w0 + hl_px, hh = h0 + hpy;
+    const bool ok = hl_r < 7 && hslot < 54 && wc >= 0 && wc < W && (unsigned)hh < (unsigned)H;
+    const int HWi = H * W;
+    const unsigned voff = ok ? (unsigned)((hcs * HWi + hh * W + wc) * 4) : OOB;
+    const unsigned vlast = (6 * (NR - 1) + hcs < HALF) ? voff : OOB;
+    const unsigned long long xa = (unsigned long long)xb;
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(xa >> 32)) << 32) |
+                (unsigned)__builtin_amdgcn_readfirstlane((unsigned)xa)),
+        (short)0, __builtin_amdgcn_readfirstlane(C * HWi * 4), 0x00020000);
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf)
 #pragma unroll
-      for (int i = 0; i < NR; ++i) {
-        const int rr = (i * 8 + wid) * 7 + hl_r;
-        const int c = rr / 9, py = rr - c * 9;
-        const int hh = h0 + py;
-        hv[hf][i] = (colok && rr < HALF * 9 && hh >= 0 && hh < H)
-                        ? xb[(long)(hf * HALF + c) * HWl + (long)hh * W + wc] : 0.f;
-      }
+      for (int i = 0; i < NR; ++i)
+        hv[hf][i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                  rx, i == NR - 1 ? vlast : voff, (hf * HALF + 6 * i) * HWi * 4, 0));
   }
   for (int e = tid; e < 4 * C; e += NT) {
     const int which = e / C, c = e - which * C;
@@ -231,10 +243,9 @@ __global__ __launch_bounds__(NT, 1) void swin_wide_kernel(Args p) {
 #pragma unroll
     for (int i = 0; i < 9; ++i) dwk[i] = p.dw[(hf * HALF + dc) * 9 + i];
     if (hf) __syncthreads();  // previous half's dw reads done
+    if (hl_r < 7 && hslot < 54) {  // patch row 9*(6i + s/9) + s%9 = 54i + s; rows of channels >= HALF unused
 #pragma unroll
-    for (int i = 0; i < NR; ++i) {
-      const int rr = (i * 8 + wid) * 7 + hl_r;
-      if (hl_r < 7 && rr < HALF * 9) WK[rr * HPW + hl_px] = hv[hf][i];  // columns 9..11 are never read
+      for (int i = 0; i < NR; ++i) WK[(54 * i + hslot) * HPW + hl_px] = hv[hf][i];
     }
     __syncthreads();
     for (int item = tid; item < HALF * 7; item += NT) {
@@ -329,35 +340,29 @@ __global__ __launch_bounds__(NT, 1) void swin_wide_kernel(Args p) {
           for (int kb = 0; kb < 3; ++kb) st[kb] = mfma4(comp(kv[kb], c), comp(qv, c), st[kb]);
         s48 = dot4_acc(k48, qv, s48);
       }
-      // softmax over the 49 keys (lane: keys kb*16 + 4g + r for query l15; key 48 after the group sum)
-      const float sv48 = group4_sum(s48) * p.scale;
+      // softmax over the 49 keys (lane: keys kb*16 + 4g + r for query l15; key 48 after the group sum) on the raw
+      // scores, exp2 with scale*log2(e) folded into one FMA, 1/sum applied to O (per query = per lane)
+      const float c2 = p.scale * 1.44269504088896341f;
+      const float sv48 = group4_sum(s48);
       float mx = sv48;
 #pragma unroll
       for (int kb = 0; kb < 3; ++kb)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          st[kb][r] *= p.scale;
-          mx = fmaxf(mx, st[kb][r]);
-        }
+        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, st[kb][r]);
       mx = xor32_max(xor16_max(mx));
+      const float mc = -mx * c2;
       float sum = 0.f;
 #pragma unroll
       for (int kb = 0; kb < 3; ++kb)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float e = __expf(st[kb][r] - mx);
+          const float e = __builtin_amdgcn_exp2f(fmaf(st[kb][r], c2, mc));
           st[kb][r] = e;
           sum += e;
         }
-      const float e48 = __expf(sv48 - mx);
+      const float e48 = __builtin_amdgcn_exp2f(fmaf(sv48, c2, mc));
       sum += (g == 0) ? e48 : 0.f;
-      sum = group4_sum(sum);
-      const float inv = 1.0f / sum;
-#pragma unroll
-      for (int kb = 0; kb < 3; ++kb)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) st[kb][r] *= inv;
-      const float p48 = e48 * inv;
+      const float inv = __builtin_amdgcn_rcpf(group4_sum(sum));
       f32x4 o[HD / 16];
 #pragma unroll
       for (int db = 0; db < HD / 16; ++db) o[db] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -372,10 +377,10 @@ __global__ __launch_bounds__(NT, 1) void swin_wide_kernel(Args p) {
 #pragma unroll
       for (int db = 0; db < HD / 16; ++db) {
         const float4 v48 = *reinterpret_cast<const float4*>(WK + XR * LQ2 + vo + db * 16 + 4 * g);
-        o[db][0] = fmaf(v48.x, p48, o[db][0]);
-        o[db][1] = fmaf(v48.y, p48, o[db][1]);
-        o[db][2] = fmaf(v48.z, p48, o[db][2]);
-        o[db][3] = fmaf(v48.w, p48, o[db][3]);
+        o[db][0] = fmaf(v48.x, e48, o[db][0]) * inv;
+        o[db][1] = fmaf(v48.y, e48, o[db][1]) * inv;
+        o[db][2] = fmaf(v48.z, e48, o[db][2]) * inv;
+        o[db][3] = fmaf(v48.w, e48, o[db][3]) * inv;
       }
       const int q = qb * 16 + l15;
       if (q < ROWS) {
@@ -475,18 +480,31 @@ __global__ __launch_bounds__(NT, 1) void swin_wide_kernel(Args p) {
   __syncthreads();
 
   // ---- y = x + SiLU(BN(Wpw T^T)) on the valid tokens: D[c][tok], c = cb*16 + 4g + r, tok = tb*16 + l15 ----
+  // residual loads / y stores are buffer ops: fixed per-lane voffset (token; channel row 4g of block wid, + l15 for
+  // token 48), out-of-image tokens get an out-of-range voffset (loads return 0, stores are dropped), the channel
+  // offset ((cb - wid)*16 + r planes) goes into the scalar soffset
   {
-    long pix[3];
-    float xr[2][3][4], bsc[2][4], bsh[2][4];
-    const long pix48 = (wy * 7 + 6 < H && wx * 7 + 6 < W) ? (long)(wy * 7 + 6) * W + wx * 7 + 6 : -1;
+    const int HWi = H * W;
+    constexpr unsigned OOB = 0x80000000u;
+    auto rsrc = [&](const float* base) {
+      const unsigned long long a = (unsigned long long)base;
+      return __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(a >> 32)) << 32) |
+                  (unsigned)__builtin_amdgcn_readfirstlane((unsigned)a)),
+          (short)0, __builtin_amdgcn_readfirstlane(C * HWi * 4), 0x00020000);
+    };
+    const __amdgpu_buffer_rsrc_t rx = rsrc(xb), ry = rsrc(p.y + (long)img * C * HWl);
+    unsigned vtok[3];
 #pragma unroll
     for (int tb = 0; tb < 3; ++tb) {
       const int tok = tb * 16 + l15;
       const int iy = tok / 7, ix = tok - iy * 7;
       const int hh = wy * 7 + iy, wc = wx * 7 + ix;
-      pix[tb] = (hh < H && wc < W) ? (long)hh * W + wc : -1;
+      vtok[tb] = (hh < H && wc < W) ? (unsigned)(((wid * 16 + 4 * g) * HWi + hh * W + wc) * 4) : OOB;
     }
-    float x48[2];
+    const unsigned v48 = (wy * 7 + 6 < H && wx * 7 + 6 < W && g == 0)
+                             ? (unsigned)(((wid * 16 + l15) * HWi + (wy * 7 + 6) * W + wx * 7 + 6) * 4) : OOB;
+    float xr[2][3][4], bsc[2][4], bsh[2][4], x48[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int cb = wid + 8 * j;
@@ -496,9 +514,10 @@ __global__ __launch_bounds__(NT, 1) void swin_wide_kernel(Args p) {
         bsh[j][r] = p.bn_shift[cb * 16 + 4 * g + r];
 #pragma unroll
         for (int tb = 0; tb < 3; ++tb)
-          xr[j][tb][r] = pix[tb] >= 0 ? xb[(long)(cb * 16 + 4 * g + r) * HWl + pix[tb]] : 0.f;
+          xr[j][tb][r] = __builtin_bit_cast(
+              float, __builtin_amdgcn_raw_buffer_load_b32(rx, vtok[tb], (128 * j + r) * HWi * 4, 0));
       }
-      x48[j] = (pix48 >= 0 && g == 0) ? xb[(long)(cb * 16 + l15) * HWl + pix48] : 0.f;
+      x48[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, v48, 128 * j * HWi * 4, 0));
     }
     f32x4 acc[3][2];
     float ext[2];
@@ -511,22 +530,20 @@ __global__ __launch_bounds__(NT, 1) void swin_wide_kernel(Args p) {
       for (int rb = 0; rb < 3; ++rb) acc[rb][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
     gemm_stream<C, 2, false, true>(T, LT, wrow, acc, ext, nullptr, nullptr, nullptr, lane);
-    float* yb = p.y + (long)img * C * HWl;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int cb = wid + 8 * j;
 #pragma unroll
-      for (int tb = 0; tb < 3; ++tb) {
-        if (pix[tb] < 0) continue;
+      for (int tb = 0; tb < 3; ++tb)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int c = cb * 16 + 4 * g + r;
-          yb[(long)c * HWl + pix[tb]] = xr[j][tb][r] + silu_fast_(acc[tb][j][r] * bsc[j][r] + bsh[j][r]);
-        }
-      }
+        for (int r = 0; r < 4; ++r)
+          __builtin_amdgcn_raw_buffer_store_b32(
+              __builtin_bit_cast(unsigned, xr[j][tb][r] + silu_fast_(acc[tb][j][r] * bsc[j][r] + bsh[j][r])), ry,
+              vtok[tb], (128 * j + r) * HWi * 4, 0);
       const float e = group4_sum(ext[j]);
-      const int c48 = cb * 16 + l15;
-      if (g == 0 && pix48 >= 0) yb[(long)c48 * HWl + pix48] = x48[j] + silu_fast_(e * p.bn_scale[c48] + p.bn_shift[c48]);
+      const int c48 = (wid + 8 * j) * 16 + l15;
+      __builtin_amdgcn_raw_buffer_store_b32(
+          __builtin_bit_cast(unsigned, x48[j] + silu_fast_(e * p.bn_scale[c48] + p.bn_shift[c48])), ry, v48,
+          128 * j * HWi * 4, 0);
     }
   }
 }
@@ -546,6 +563,7 @@ int yolosod_swin_wide_launch(const float* x, float* y, int B, int C, int H, int 
                              const float* mlp2_b, const float* pw_w, const float* bn_scale, const float* bn_shift,
                              hipStream_t st) {
   if (C != wide::C || num_heads != C / wide::HD || wh != 7 || ww != 7 || mlp_hidden != 2 * C) return 0;
+  if ((long)C * H * W >= (1L << 30) || (long)B * nWin >= (1L << 31)) return 0;  // 32-bit byte offsets / indices
   if (const char* e = getenv("YOLOSOD_SWIN_WIDE"))
     if (atoi(e) == 0) return 0;
   wide::Args a{x, y, B, H, W, nWx, nWin, dw_w, ln1_w, ln1_b, ln1_eps, in_proj_w, in_proj_b, out_proj_w, out_proj_b,
