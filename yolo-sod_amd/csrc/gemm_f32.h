@@ -54,6 +54,7 @@ struct GemmArgs {
   const float* ln_stats;  // [M][2] = (mean, rstd) from row_stats_kernel, required with ln_w
   int tiles_n, tiles;     // set by launch_gemm
   Epi epi;
+  int nimg;               // set by launch_gemm: > 0 = batch folded into N (N-contiguous B, nimg columns per image)
 };
 
 // Per-row LayerNorm statistics (mean, 1/sqrt(var + eps)) of a K-contiguous [rows][K] matrix: one wave per row,
@@ -150,6 +151,21 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
   const float* B = g.B + (long)bz * g.b_bs;
   const int M = g.M, N = g.N, K = g.K;
   const bool vec_b = (g.ldb & 3) == 0 && (g.b_bs & 3) == 0;
+  // folded batch: column n -> image n / nimg, column n % nimg (a float4 never straddles images: nimg % 4 == 0);
+  // this thread's B columns are the same in every k block, so their offsets are computed once
+  long bcol[B_KC ? 1 : NB];
+  if (!B_KC) {
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int n = n0 + ((tid + 256 * i) % (BN / 4)) * 4;
+      if (g.nimg > 0) {
+        const int img = n / g.nimg;
+        bcol[i] = (long)img * g.b_bs + (n - img * g.nimg);
+      } else {
+        bcol[i] = n;
+      }
+    }
+  }
 
   if (A_LN) {
     for (int r = tid; r < BM; r += 256) {
@@ -183,7 +199,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
       } else {
         const int kl = idx / (BN / 4), nq = (idx % (BN / 4)) * 4;
         const int n = n0 + nq;
-        const float* src = B + (long)(k0 + kl) * g.ldb + n;
+        const float* src = B + (long)(k0 + kl) * g.ldb + bcol[i];
         if (n + 3 < N && vec_b) {
           rb[i] = *reinterpret_cast<const float4*>(src);
         } else {
@@ -294,8 +310,17 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
 #pragma unroll 4
     for (int idx = tid; idx < BM * NQ; idx += 256) {
       const int row = idx / NQ, c4 = idx % NQ;
-      const int m = m0 + row, n = n0 + 4 * c4;
+      const int m = m0 + row;
+      int n = n0 + 4 * c4;
       if (m >= M || n >= N) continue;
+      float* ob = outb;
+      const float* rb_ = resb;
+      if (g.nimg > 0) {  // folded batch (bias / BN per row only)
+        const int img = n / g.nimg;
+        n -= img * g.nimg;
+        ob += (long)img * e.out_bs;
+        if (rb_) rb_ += (long)img * e.res_bs;
+      }
       f32x4 v = *reinterpret_cast<const f32x4*>(&Cs[row * SC + 4 * c4]);
       if (e.bias_mode == 1) v += e.bias[m];
       else if (e.bias_mode == 2) v += *reinterpret_cast<const f32x4*>(e.bias + n);
@@ -303,8 +328,8 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
       else if (e.bn_mode == 2)
         v = v * *reinterpret_cast<const f32x4*>(e.scale + n) + *reinterpret_cast<const f32x4*>(e.shift + n);
       v.x = apply_act(v.x, e.act); v.y = apply_act(v.y, e.act); v.z = apply_act(v.z, e.act); v.w = apply_act(v.w, e.act);
-      if (resb) v += *reinterpret_cast<const f32x4*>(resb + (long)m * e.ldr + n);
-      *reinterpret_cast<f32x4*>(outb + (long)m * e.ldc + n) = v;
+      if (rb_) v += *reinterpret_cast<const f32x4*>(rb_ + (long)m * e.ldr + n);
+      *reinterpret_cast<f32x4*>(ob + (long)m * e.ldc + n) = v;
     }
     return;
   }
@@ -363,6 +388,15 @@ static inline int launch_gemm(const GemmArgs& g0, int batch, bool b_kc, hipStrea
               (!e.res || (e.ldr % 4 == 0 && e.res_bs % 4 == 0 && al16(e.res))) &&
               (e.bias_mode != 2 || al16(e.bias)) && (e.bn_mode != 2 || (al16(e.scale) && al16(e.shift)));
   const bool ln = g.ln_w != nullptr;
+  // N-contiguous B with a per-image N that is not a multiple of 128 (A2 at 640: H*W = 400): fold the batch into N so
+  // the tiles run across image boundaries instead of padding every image's last tile column
+  g.nimg = 0;
+  if (!b_kc && batch > 1 && g.a_bs == 0 && g.N % 128 != 0 && g.N % 4 == 0 && g.epi.vec && e.bias_mode != 2 && e.bn_mode != 2 &&
+      g.ldb % 4 == 0 && g.b_bs % 4 == 0 && (long)g.N * batch < (1L << 31) && !getenv("YOLOSOD_GEMM_NOFOLD")) {
+    g.nimg = g.N;
+    g.N *= batch;
+    batch = 1;
+  }
   // N tiles of 64 when N is not a multiple of 128 (e.g. 3C = 192) or small; 128 otherwise
   const bool narrow = (g.N % 128 != 0) && (g.N <= 256);
 #define YS_GEMM_LAUNCH(WM_, WN_, MI_, NI_)                                                                     \
