@@ -24,7 +24,20 @@ CASES = {
     "cbam_L18": ("CBAM_Block", (256, 512, 16), (32, 256, 40, 40)),
     "se_L23": ("SE_Block", (256,), (32, 128, 80, 80)),
     "mamba_L7": ("MambaBlock", (128, 256, 2), (32, 128, 80, 80)),  # yolov12-sod-fusion-v5 only
+    "head": ("detect_head", (64, 64, 10), (32, 0, 640, 640)),  # fused Detect tail + decode, 4 levels P2..P5
 }
+
+
+def head_case(dev, c2, c3, nc, B, S):
+    g = torch.Generator(device="cpu").manual_seed(0)
+    sizes = [S // s for s in (4, 8, 16, 32)]
+    fb = [torch.randn(B, c2, h, h, generator=g).to(dev) for h in sizes]
+    fc = [torch.randn(B, c3, h, h, generator=g).to(dev) for h in sizes]
+    bw = [(torch.randn(64, c2, generator=g) * 0.1).to(dev) for _ in sizes]
+    bb = [torch.zeros(64).to(dev) for _ in sizes]
+    cw = [(torch.randn(nc, c3, generator=g) * 0.1).to(dev) for _ in sizes]
+    cb = [torch.zeros(nc).to(dev) for _ in sizes]
+    return lambda: _hip.detect_head(fb, fc, bw, bb, cw, cb, [4.0, 8.0, 16.0, 32.0], nc)
 
 
 def main():
@@ -32,12 +45,16 @@ def main():
     dev = torch.device("cuda")
     for name in names:
         op, args, shape = CASES[name]
-        m = getattr(M, op)(*args)
-        if op == "SE_Block":
-            m._maybe_build(shape[1], None)
-        recipes.perturb_(m, 1)
-        m = m.to(dev).eval()
-        x = torch.randn(shape, device=dev)
+        if op == "detect_head":
+            fn = head_case(dev, *args, shape[0], shape[2])
+            m, x = (lambda _x: fn()), None
+        else:
+            m = getattr(M, op)(*args)
+            if op == "SE_Block":
+                m._maybe_build(shape[1], None)
+            recipes.perturb_(m, 1)
+            m = m.to(dev).eval()
+            x = torch.randn(shape, device=dev)
         with torch.inference_mode():
             for _ in range(3):
                 m(x)

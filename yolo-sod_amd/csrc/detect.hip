@@ -207,6 +207,149 @@ __global__ __launch_bounds__(256) void detect_head_kernel(HeadArgs d) {
   }
 }
 
+
+// Same head tail + decode with the conv weights in LDS instead of registers (A fragments are ds_read_b128 of 4
+// tiles' rows at once from a [q][g][j][t] image, conflict-free for the b128 lane groups) - the ~100 VGPRs that
+// held them now double-buffer the next 16-pixel group's feature loads, so the HBM latency of a group overlaps the
+// MFMAs and DFL of the previous one, at 3 waves per SIMD.
+template <int C2, int C3, int NTS>
+__global__ __launch_bounds__(256, C3 > 64 ? 2 : 3) void detect_head_lds_kernel(HeadArgs d) {
+  __shared__ __attribute__((aligned(16))) float wl[C2 * 64 + C3 * 16];
+  float* wlb = wl;            // [C2/4 q][4 g][16 j][4 t] = W_box[16t + j][4q + g]
+  float* wlc = wl + C2 * 64;  // [C3/16 qq][4 g][16 j][4 u] = W_cls[j][4(4qq + u) + g] (0 for j >= nc)
+  const int b = blockIdx.y;
+  int l = 0;
+#pragma unroll
+  for (int i = 1; i < 4; ++i)
+    if (i < d.nl && (int)blockIdx.x >= d.blk_off[i]) l = i;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int g = lane >> 4, j = lane & 15;
+  const int nc = d.nc;
+  {
+    const float* wb = d.wb[l];
+    const float* wc = d.wc[l];
+    for (int e = tid; e < C2 * 64; e += 256) {
+      const int t = e & 3, jj = (e >> 2) & 15, gg = (e >> 6) & 3, q = e >> 8;
+      wlb[e] = wb[(16 * t + jj) * C2 + 4 * q + gg];
+    }
+    for (int e = tid; e < C3 * 16; e += 256) {
+      const int u = e & 3, jj = (e >> 2) & 15, gg = (e >> 6) & 3, qq = e >> 8;
+      wlc[e] = (jj < nc) ? wc[jj * C3 + 4 * (4 * qq + u) + gg] : 0.f;
+    }
+  }
+  __syncthreads();
+  const int HW = d.hw[l];
+  const int px0 = (((int)blockIdx.x - d.blk_off[l]) * 4 + wv) * (NTS * 16);
+  if (px0 >= HW) return;  // whole wave; no barrier below
+  float bbr[4][4], bcr[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bbr[t][r] = d.bb[l][16 * t + 4 * g + r];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) bcr[r] = (4 * g + r < nc) ? d.bc[l][4 * g + r] : 0.f;
+  const float* fbb = d.fb[l] + (long)b * C2 * HW;
+  const float* fcb = d.fc[l] + (long)b * C3 * HW;
+  const int W = d.w[l];
+  const float st = d.stride[l];
+  float* yb = d.y + (long)b * (4 + nc) * d.A + d.a_off[l];
+  const float4* wb4 = reinterpret_cast<const float4*>(wlb) + g * 16 + j;
+  const float4* wc4 = reinterpret_cast<const float4*>(wlc) + g * 16 + j;
+
+  // feature loads are buffer loads on per-image descriptors: the lane's voffset is (channel g, pixel p), the
+  // channel step 4q goes into the scalar soffset (no per-load 64-bit addresses to keep live), and pixels past the
+  // level's end get an out-of-range voffset, which the hardware returns as 0
+  auto rsrc = [&](const float* base, int bytes) {
+    const unsigned long long a = (unsigned long long)base;
+    return __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(a >> 32)) << 32) |
+                (unsigned)__builtin_amdgcn_readfirstlane((unsigned)a)),
+        (short)0, __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+  };
+  const __amdgpu_buffer_rsrc_t rb = rsrc(fbb, C2 * HW * 4), rc = rsrc(fcb, C3 * HW * 4);
+  float xb[2][C2 / 4], xc[2][C3 / 4];
+  auto load_group = [&](int ts, float (&fb)[C2 / 4], float (&fcv)[C3 / 4]) {
+    const int p = px0 + ts * 16 + j;
+    const unsigned vo = (p < HW && !(d.abl & 1)) ? (unsigned)((g * HW + p) * 4) : 0x80000000u;
+#pragma unroll
+    for (int q = 0; q < C2 / 4; ++q)
+      fb[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb, vo, q * 16 * HW, 0));
+#pragma unroll
+    for (int q = 0; q < C3 / 4; ++q)
+      fcv[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rc, vo, q * 16 * HW, 0));
+  };
+  auto compute_group = [&](int ts, const float (&cb)[C2 / 4], const float (&cc)[C3 / 4]) {
+    const int p0 = px0 + ts * 16;
+    if (p0 >= HW) return;  // wave-uniform
+    const int p = p0 + j;
+    const bool ok = p < HW;
+    f32x4 acc[5];
+#pragma unroll
+    for (int t = 0; t < 5; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < C2 / 4; ++q) {
+      const float4 w4 = wb4[q * 64];
+      acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(w4.x, cb[q], acc[0], 0, 0, 0);
+      acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w4.y, cb[q], acc[1], 0, 0, 0);
+      acc[2] = __builtin_amdgcn_mfma_f32_16x16x4f32(w4.z, cb[q], acc[2], 0, 0, 0);
+      acc[3] = __builtin_amdgcn_mfma_f32_16x16x4f32(w4.w, cb[q], acc[3], 0, 0, 0);
+    }
+#pragma unroll
+    for (int qq = 0; qq < C3 / 16; ++qq) {
+      const float4 c4 = wc4[qq * 64];
+      acc[4] = __builtin_amdgcn_mfma_f32_16x16x4f32(c4.x, cc[4 * qq], acc[4], 0, 0, 0);
+      acc[4] = __builtin_amdgcn_mfma_f32_16x16x4f32(c4.y, cc[4 * qq + 1], acc[4], 0, 0, 0);
+      acc[4] = __builtin_amdgcn_mfma_f32_16x16x4f32(c4.z, cc[4 * qq + 2], acc[4], 0, 0, 0);
+      acc[4] = __builtin_amdgcn_mfma_f32_16x16x4f32(c4.w, cc[4 * qq + 3], acc[4], 0, 0, 0);
+    }
+    // DFL (block.py:79-82), as in detect_head_kernel
+    float dist[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = acc[s][r] + bbr[s][r];
+      float mx = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
+      mx = xor32_max(xor16_max(mx));
+      float sum = 0.f, e = 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[r] = __expf(v[r] - mx);
+        sum += v[r];
+        e += (float)(4 * g + r) * v[r];
+      }
+      sum = xor32_sum(xor16_sum(sum));
+      e = xor32_sum(xor16_sum(e));
+      dist[s] = e * __builtin_amdgcn_rcpf(sum);
+    }
+    if (!ok || (d.abl & 2)) return;
+    const int iy = p / W, ix = p - iy * W;
+    const float ax = (float)ix + 0.5f, ay = (float)iy + 0.5f;
+    const float x1 = ax - dist[0], y1 = ay - dist[1];
+    const float x2 = ax + dist[2], y2 = ay + dist[3];
+    const float out = g == 0 ? ((x1 + x2) / 2.0f) * st
+                    : g == 1 ? ((y1 + y2) / 2.0f) * st
+                    : g == 2 ? (x2 - x1) * st
+                             : (y2 - y1) * st;
+    yb[(long)g * d.A + p] = out;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int c = 4 * g + r;
+      if (c < nc) yb[(long)(4 + c) * d.A + p] = sigmoidf_(acc[4][r] + bcr[r]);
+    }
+  };
+  // ping-pong over group pairs (rolled: an unrolled group loop lets the scheduler hoist several groups' loads)
+  static_assert(NTS % 2 == 0, "group pairs");
+  load_group(0, xb[0], xc[0]);
+#pragma unroll 1
+  for (int ts = 0; ts < NTS; ts += 2) {
+    if (px0 + (ts + 1) * 16 < HW) load_group(ts + 1, xb[1], xc[1]);
+    compute_group(ts, xb[0], xc[0]);
+    if (ts + 2 < NTS && px0 + (ts + 2) * 16 < HW) load_group(ts + 2, xb[0], xc[0]);
+    compute_group(ts + 1, xb[1], xc[1]);
+  }
+}
+
 }  // namespace ys
 
 using namespace ys;
@@ -278,10 +421,19 @@ YS_EXPORT int yolosod_detect_head(int nl, const float* const* box_feat, const fl
   if (const char* e = getenv("YOLOSOD_HEAD_ABL")) d.abl = atoi(e);
   if (B == 0 || off == 0) return 0;
   const dim3 grid(blk, B);
-  if (c3 == 64)
-    hipLaunchKernelGGL((detect_head_kernel<64, 64, NTS>), grid, dim3(256), 0, (hipStream_t)stream, d);
-  else
-    hipLaunchKernelGGL((detect_head_kernel<64, 128, NTS>), grid, dim3(256), 0, (hipStream_t)stream, d);
+  // default: weights in LDS, feature loads double-buffered; YOLOSOD_HEAD_V1=1: weights in registers (A/B)
+  static const bool v1 = [] { const char* e = getenv("YOLOSOD_HEAD_V1"); return e && atoi(e) != 0; }();
+  if (v1) {
+    if (c3 == 64)
+      hipLaunchKernelGGL((detect_head_kernel<64, 64, NTS>), grid, dim3(256), 0, (hipStream_t)stream, d);
+    else
+      hipLaunchKernelGGL((detect_head_kernel<64, 128, NTS>), grid, dim3(256), 0, (hipStream_t)stream, d);
+  } else {
+    if (c3 == 64)
+      hipLaunchKernelGGL((detect_head_lds_kernel<64, 64, NTS>), grid, dim3(256), 0, (hipStream_t)stream, d);
+    else
+      hipLaunchKernelGGL((detect_head_lds_kernel<64, 128, NTS>), grid, dim3(256), 0, (hipStream_t)stream, d);
+  }
   YS_CHECK_LAUNCH("detect_head");
   return 0;
 }
