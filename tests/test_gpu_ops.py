@@ -235,6 +235,30 @@ def test_detect_head_fused_vs_oracle(c3, img, cuda):
     assert ok, f"max abs err {err:.3g}"
 
 
+@pytest.mark.parametrize("name", [n for n in recipes.OPS if n.startswith("a2_")])
+def test_a2_premultiplied_out_projection_matches_two_gemm_form(name, cuda):
+    """A2_Attn folds the MHA out-projection into the output conv (Wconv @ Wmha, one token GEMM); the C-ABI's
+    two-GEMM form (attention.out_proj passed separately) must give the same output and both match the reference."""
+    from yolosod_amd.nn.modules import conv_weight_bias
+    z = golden(f"ops_{name}")
+    m, _ = build_fixture_module(name)
+    m = m.to(cuda).eval()
+    x = torch.from_numpy(z["x"]).to(cuda)
+    at = m.attention
+    with torch.inference_mode():
+        y1 = m(x)
+        pw, pb = conv_weight_bias(m.proj)
+        ow, ob = conv_weight_bias(m.out_proj)
+        y2 = _hip.a2_forward(x, m.num_areas, m.num_heads, pw, pb, m.layer_norm.weight, m.layer_norm.bias,
+                             m.layer_norm.eps, at.in_proj_weight, at.in_proj_bias, at.out_proj.weight,
+                             at.out_proj.bias, ow, ob)
+    ok, err, _ = tol_close(y1.cpu(), y2.cpu(), 1e-5, 1e-5)
+    assert ok, f"premultiplied vs two-GEMM: {err:.3g}"
+    for y in (y1, y2):
+        ok, err, _ = tol_close(y.cpu(), torch.from_numpy(z["y"]), ATOL, 0.0)
+        assert ok, f"{name}: max abs err vs reference {err:.3g}"
+
+
 @pytest.mark.parametrize("shape", [(2, 32, 40, 40), (3, 64, 96, 120), (2, 128, 20, 20)])
 def test_producer_epilogue_stats_feed_se_and_cbam(shape, cuda):
     """bias_act(stats=...) writes the same output as bias_act and per-plane partials that make SE / CBAM skip

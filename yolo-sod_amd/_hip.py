@@ -248,7 +248,10 @@ def ca_forward(x, conv1_w, conv1_b, bn_w, bn_b, bn_mean, bn_var, bn_eps, convh_w
 
 
 def a2_forward(x, num_areas, num_heads, proj_w, proj_b, ln_w, ln_b, ln_eps, in_w, in_b, mo_w, mo_b, op_w, op_b):
+    """mo_w = mo_b = None: op_w / op_b are the pre-multiplied MHA-out x output-conv weights (A2_Attn._fused_out)."""
     lib = load_library()
+    if (mo_w is None) != (mo_b is None):
+        raise RuntimeError("a2_forward: attention.out_proj weight and bias must both be given or both be None")
     B, C, H, W = x.shape
     if C % num_heads:
         raise RuntimeError(f"A2_Attn: C={C} not divisible by num_heads={num_heads}")
@@ -260,8 +263,9 @@ def a2_forward(x, num_areas, num_heads, proj_w, proj_b, ln_w, ln_b, ln_eps, in_w
                                   _p(proj_w, "proj.weight", C * C), _p(proj_b, "proj.bias", C),
                                   _p(ln_w, "layer_norm.weight", C), _p(ln_b, "layer_norm.bias", C), float(ln_eps),
                                   _p(in_w, "in_proj_weight", 3 * C * C), _p(in_b, "in_proj_bias", 3 * C),
-                                  _p(mo_w, "attention.out_proj.weight", C * C),
-                                  _p(mo_b, "attention.out_proj.bias", C), _p(op_w, "out_proj.weight", C * C),
+                                  _p(mo_w, "attention.out_proj.weight", C * C) if mo_w is not None else None,
+                                  _p(mo_b, "attention.out_proj.bias", C) if mo_b is not None else None,
+                                  _p(op_w, "out_proj.weight", C * C),
                                   _p(op_b, "out_proj.bias", C), ws.data_ptr(), ws.numel(), _stream()),
            "a2_forward")
     return y

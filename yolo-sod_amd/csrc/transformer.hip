@@ -714,9 +714,10 @@ YS_EXPORT int yolosod_a2_forward(const float* x, float* y, int B, int C, int H, 
                                  float ln_eps, const float* in_proj_w, const float* in_proj_b,
                                  const float* mha_out_w, const float* mha_out_b, const float* oproj_w,
                                  const float* oproj_b, void* workspace, size_t workspace_bytes, void* stream) {
-  YS_CHECK_ARG(x && y && proj_w && proj_b && ln_w && ln_b && in_proj_w && in_proj_b && mha_out_w && mha_out_b &&
-                   oproj_w && oproj_b,
+  YS_CHECK_ARG(x && y && proj_w && proj_b && ln_w && ln_b && in_proj_w && in_proj_b && oproj_w && oproj_b &&
+                   (mha_out_w != nullptr) == (mha_out_b != nullptr),
                "a2: null pointer");
+  const bool premul = mha_out_w == nullptr;  // oproj_w / oproj_b already include the MHA out-projection
   YS_CHECK_ARG(B >= 0 && C > 0 && H > 0 && W > 0 && num_areas > 0, "a2: bad shape");
   YS_CHECK_ARG(C % 32 == 0, "a2: C must be a multiple of 32");
   if (B == 0) return 0;
@@ -751,15 +752,17 @@ YS_EXPORT int yolosod_a2_forward(const float* x, float* y, int B, int C, int H, 
   ga.epi.bias = in_proj_b; ga.epi.bias_mode = 2;
   if ((rc = launch_gemm(ga, 1, true, st))) return rc;
   if ((rc = launch_attention(Q, U, B, A * W, C, num_heads, st))) return rc;
-  ga = GemmArgs{};
-  ga.A = U; ga.lda = C; ga.B = mha_out_w; ga.ldb = C; ga.M = (int)ntok; ga.N = C; ga.K = C;
-  ga.epi = epi_plain(Z, 0, C);
-  ga.epi.bias = mha_out_b; ga.epi.bias_mode = 2;
-  if ((rc = launch_gemm(ga, 1, true, st))) return rc;
+  if (!premul) {
+    ga = GemmArgs{};
+    ga.A = U; ga.lda = C; ga.B = mha_out_w; ga.ldb = C; ga.M = (int)ntok; ga.N = C; ga.K = C;
+    ga.epi = epi_plain(Z, 0, C);
+    ga.epi.bias = mha_out_b; ga.epi.bias_mode = 2;
+    if ((rc = launch_gemm(ga, 1, true, st))) return rc;
+  }
   // T[img][n][t] = sum_c Wout[n][c] Z[img*AW + t][c]   (reuse S as T: B*C*A*W floats == ntok*C)
   float* T = S;
   ga = GemmArgs{};
-  ga.A = oproj_w; ga.lda = C; ga.B = Z; ga.b_bs = (long)A * W * C; ga.ldb = C; ga.M = C; ga.N = A * W; ga.K = C;
+  ga.A = oproj_w; ga.lda = C; ga.B = premul ? U : Z; ga.b_bs = (long)A * W * C; ga.ldb = C; ga.M = C; ga.N = A * W; ga.K = C;
   ga.epi = epi_plain(T, (long)C * A * W, A * W);
   if ((rc = launch_gemm(ga, B, true, st))) return rc;
   hipLaunchKernelGGL(a2_upsample_out_kernel, dim3((unsigned)(B * C), (unsigned)((HW + 255) / 256)), dim3(256), 0, st,

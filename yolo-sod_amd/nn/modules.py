@@ -361,12 +361,30 @@ class A2_Attn(nn.Module):
         if self.out_proj.conv.out_channels != x.shape[1]:
             raise RuntimeError("A2_Attn: HIP path implements the residual (c2 == c1) form only")
         pw, pb = conv_weight_bias(self.proj)
-        ow, ob = conv_weight_bias(self.out_proj)
         at = self.attention
+        fw, fb = self._fused_out()
         return _hip.a2_forward(x, self.num_areas, self.num_heads, pw, pb, self.layer_norm.weight.detach(),
                                self.layer_norm.bias.detach(), self.layer_norm.eps, at.in_proj_weight.detach(),
-                               at.in_proj_bias.detach(), at.out_proj.weight.detach(), at.out_proj.bias.detach(),
-                               ow, ob)
+                               at.in_proj_bias.detach(), None, None, fw, fb)
+
+    def _fused_out(self):
+        """MHA out-projection (a2_attn.py:53) and the output 1x1 conv (a2_attn.py:63) are consecutive linear maps
+        (the bilinear upsample between them commutes with the conv): folded once into Wf = Wconv @ Wmha,
+        bf = Wconv @ bmha + bconv (float64 product, like the BN fold), cached against the parameters' versions, so
+        the per-call path runs one token GEMM instead of two."""
+        at, op = self.attention, self.out_proj
+        src = [at.out_proj.weight, at.out_proj.bias, op.conv.weight]
+        src += [op.bn.weight, op.bn.bias, op.bn.running_mean, op.bn.running_var] if hasattr(op, "bn") else [op.conv.bias]
+        key = tuple((t.data_ptr(), t._version, t.device) for t in src)
+        cache = getattr(self, "_fused_cache", None)
+        if cache is None or cache[0] != key:
+            ow, ob = conv_weight_bias(op)
+            mw, mb = at.out_proj.weight.detach(), at.out_proj.bias.detach()
+            fw = (ow.double() @ mw.double()).float().contiguous()
+            fb = (ow.double() @ mb.double() + ob.double()).float().contiguous()
+            cache = (key, fw, fb)
+            self._fused_cache = cache
+        return cache[1], cache[2]
 
 
 class WindowAttention(nn.Module):
