@@ -85,6 +85,17 @@ int yolosod_se_forward_pre(const float* x, float* y, int B, int C, int H, int W,
 int yolosod_cbam_forward_pre(const float* x, float* y, int B, int C, int H, int W, const float* fc0_w,
                              const float* fc2_w, int hidden, const float* sa_w, const float* psum, const float* pmax,
                              void* workspace, size_t workspace_bytes, void* stream);
+/* CA_Block (ca_block.py:43-44): the producing conv's epilogue also writes the pooled row means (over W) and column
+ * means (over H) of its output, yin[B][C][H+W]; the CA entry point then runs the gate and the apply pass only.
+ * W % 4 == 0, W <= 1024. */
+int yolosod_bias_act_capool(const float* y, long y_bstride, float* out, long out_bstride, const float* bias,
+                            const float* res, long res_bstride, int B, int C, int H, int W, int act, float* yin,
+                            void* stream);
+int yolosod_ca_forward_pre(const float* x, float* y, int B, int C, int H, int W, const float* conv1_w,
+                           const float* conv1_b, int mip, const float* bn_w, const float* bn_b, const float* bn_mean,
+                           const float* bn_var, float bn_eps, const float* convh_w, const float* convh_b,
+                           const float* convw_w, const float* convw_b, const float* yin, void* workspace,
+                           size_t workspace_bytes, void* stream);
 
 /* MambaBlock (GLU fallback)        ultralytics/nn/modules/blocks_mamba.py:84-113 (Conv1x1BN, GLUBlock), :198-236
  * (forward without mamba_ssm); arg rule nn/tasks.py:1122-1127 (MambaBlock(c, c_hidden, seq_reduction)).

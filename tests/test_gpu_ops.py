@@ -259,6 +259,33 @@ def test_a2_premultiplied_out_projection_matches_two_gemm_form(name, cuda):
         assert ok, f"{name}: max abs err vs reference {err:.3g}"
 
 
+@pytest.mark.parametrize("shape,res", [((2, 128, 80, 80), False), ((3, 64, 20, 16), True), ((2, 32, 13, 12), False),
+                                       ((1, 16, 200, 48), True)])
+def test_producer_epilogue_pool_feeds_ca(shape, res, cuda):
+    """bias_act(stats="capool") writes the same output as bias_act plus CA's row / column means, and CA_Block run on
+    it (gate + apply only) equals the self-contained CA (up to summation order)."""
+    from yolosod_amd.nn import modules as M
+    g = torch.Generator().manual_seed(11)
+    y = torch.randn(shape, generator=g).to(cuda)
+    bias = torch.randn(shape[1], generator=g).to(cuda)
+    r = torch.randn(shape, generator=g).to(cuda) if res else None
+    plain = _hip.bias_act(y.clone(), bias, 1, res=r)
+    pooled = _hip.bias_act(y.clone(), bias, 1, res=r, stats="capool")
+    assert torch.equal(plain, pooled) and pooled._ys_ca_pool is not None
+    yin = pooled._ys_ca_pool[0].cpu().double()
+    ref = torch.cat([plain.double().mean(3), plain.double().mean(2)], 2).cpu()
+    ok, err, _ = tol_close(yin, ref, 1e-5, 1e-5)
+    assert ok, f"pooled means: {err:.3g}"
+    m = M.CA_Block(shape[1], None, 32)
+    recipes.perturb_(m, 5)
+    m.to(cuda).eval()
+    with torch.inference_mode():
+        a = m(plain)
+        b = m(pooled)
+    ok, err, _ = tol_close(b.cpu(), a.cpu(), 1e-6, 1e-5)
+    assert ok, f"CA with producer pooling vs self-contained: {err:.3g}"
+
+
 @pytest.mark.parametrize("shape", [(2, 32, 40, 40), (3, 64, 96, 120), (2, 128, 20, 20)])
 def test_producer_epilogue_stats_feed_se_and_cbam(shape, cuda):
     """bias_act(stats=...) writes the same output as bias_act and per-plane partials that make SE / CBAM skip

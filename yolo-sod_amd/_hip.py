@@ -49,6 +49,10 @@ SIGNATURES = {
     "yolosod_layernorm": (_i, [_vp, _vp, _l, _i, _vp, _vp, _f, _vp]),
     "yolosod_attention": (_i, [_vp, _vp, _l, _i, _i, _i, _vp]),
     "yolosod_bias_act": (_i, [_vp, _l, _vp, _l, _vp, _vp, _l, _i, _i, _l, _i, _vp]),
+    "yolosod_bias_act_capool": (_i, [_vp, ctypes.c_long, _vp, ctypes.c_long, _vp, _vp, ctypes.c_long, _i, _i, _i, _i,
+                                     _i, _vp, _vp]),
+    "yolosod_ca_forward_pre": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp,
+                                    _vp, _vp, ctypes.c_size_t, _vp]),
     "yolosod_bias_act_stats": (_i, [_vp, _l, _vp, _l, _vp, _vp, _l, _i, _i, _l, _i, _i, _l, _vp, _vp, _vp]),
     "yolosod_plane_parts": (_i, [_l, ctypes.POINTER(ctypes.c_long)]),
     "yolosod_se_forward_pre": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _i, _vp, _vp, _sz, _vp]),
@@ -237,13 +241,18 @@ def ca_forward(x, conv1_w, conv1_b, bn_w, bn_b, bn_mean, bn_var, bn_eps, convh_w
     mip = conv1_w.shape[0]
     y = torch.empty_like(x)
     ws = _workspace(lib.yolosod_ca_workspace(B, C, H, W), x.device)
-    _check(_launch(("ca", tuple(x.shape), mip), lib.yolosod_ca_forward, _dev(x, "x"), _dev(y, "y"), B, C, H, W, _p(conv1_w, "conv1.weight", mip * C),
-                                  _p(conv1_b, "conv1.bias", mip), mip, _p(bn_w, "bn1.weight", mip),
-                                  _p(bn_b, "bn1.bias", mip), _p(bn_mean, "bn1.running_mean", mip),
-                                  _p(bn_var, "bn1.running_var", mip), float(bn_eps),
-                                  _p(convh_w, "conv_h.weight", C * mip), _p(convh_b, "conv_h.bias", C),
-                                  _p(convw_w, "conv_w.weight", C * mip), _p(convw_b, "conv_w.bias", C),
-                                  ws.data_ptr(), ws.numel(), _stream()), "ca_forward")
+    args = (_dev(x, "x"), _dev(y, "y"), B, C, H, W, _p(conv1_w, "conv1.weight", mip * C),
+            _p(conv1_b, "conv1.bias", mip), mip, _p(bn_w, "bn1.weight", mip), _p(bn_b, "bn1.bias", mip),
+            _p(bn_mean, "bn1.running_mean", mip), _p(bn_var, "bn1.running_var", mip), float(bn_eps),
+            _p(convh_w, "conv_h.weight", C * mip), _p(convh_b, "conv_h.bias", C),
+            _p(convw_w, "conv_w.weight", C * mip), _p(convw_b, "conv_w.bias", C))
+    pre = getattr(x, "_ys_ca_pool", None)
+    if pre is not None and pre[1] == tuple(x.shape):  # row / column means came with x from its producer
+        _check(_launch(("ca", tuple(x.shape), mip), lib.yolosod_ca_forward_pre, *args, pre[0].data_ptr(),
+                       ws.data_ptr(), ws.numel(), _stream()), "ca_forward_pre")
+    else:
+        _check(_launch(("ca", tuple(x.shape), mip), lib.yolosod_ca_forward, *args, ws.data_ptr(), ws.numel(),
+                       _stream()), "ca_forward")
     return y
 
 
@@ -404,7 +413,8 @@ def bias_act(y, bias, act, out=None, res=None, stats=None):
     """Backbone conv epilogue: out = act(y + bias[c]) (+ res). ``out`` may be a channel slice [B, C, H, W] of a
     larger contiguous concat buffer (batch stride > C*H*W); ``res`` likewise. In place when out is None.
     ``stats`` ("sum" / "summax"): also emit out's per-plane partial sums (+ maxes) for a following SE / CBAM,
-    attached to the returned tensor as ``_ys_plane_stats`` (PlaneStats)."""
+    attached to the returned tensor as ``_ys_plane_stats`` (PlaneStats); "capool": the row / column means a
+    following CA_Block pools, attached as ``_ys_ca_pool`` ([B, C, H + W], shape)."""
     lib = load_library()
     B, C, H, W = y.shape
     HW = H * W
@@ -421,6 +431,16 @@ def bias_act(y, bias, act, out=None, res=None, stats=None):
     yb = bstride(y, "y")
     ob = bstride(out, "out")
     rb = bstride(res, "res") if res is not None else 0
+    if stats == "capool":  # CA_Block input: pooled row / column means of out, [B, C, H + W]
+        if W % 4 or W > 1024:
+            stats = None
+        else:
+            yin = torch.empty((B, C, H + W), dtype=torch.float32, device=y.device)
+            _check(lib.yolosod_bias_act_capool(y.data_ptr(), yb, out.data_ptr(), ob, _dev(bias, "bias"),
+                                               None if res is None else res.data_ptr(), rb, B, C, H, W, int(act),
+                                               yin.data_ptr(), _stream()), "bias_act_capool")
+            out._ys_ca_pool = (yin, tuple(out.shape))
+            return out
     if stats is not None:
         parts, seg = plane_parts(HW)
         psum = torch.empty(B * C * parts, dtype=torch.float32, device=y.device)

@@ -634,11 +634,11 @@ YS_EXPORT size_t yolosod_ca_workspace(int B, int C, int H, int W) {
   return s.off;
 }
 
-YS_EXPORT int yolosod_ca_forward(const float* x, float* y, int B, int C, int H, int W, const float* conv1_w,
-                                 const float* conv1_b, int mip, const float* bn_w, const float* bn_b,
-                                 const float* bn_mean, const float* bn_var, float bn_eps, const float* convh_w,
-                                 const float* convh_b, const float* convw_w, const float* convw_b, void* workspace,
-                                 size_t workspace_bytes, void* stream) {
+static int ca_forward_impl(const float* x, float* y, int B, int C, int H, int W, const float* conv1_w,
+                           const float* conv1_b, int mip, const float* bn_w, const float* bn_b, const float* bn_mean,
+                           const float* bn_var, float bn_eps, const float* convh_w, const float* convh_b,
+                           const float* convw_w, const float* convw_b, const float* yin_pre, void* workspace,
+                           size_t workspace_bytes, void* stream) {
   YS_CHECK_ARG(x && y && conv1_w && conv1_b && bn_w && bn_b && bn_mean && bn_var && convh_w && convh_b && convw_w &&
                    convw_b,
                "ca: null pointer");
@@ -664,8 +664,10 @@ YS_EXPORT int yolosod_ca_forward(const float* x, float* y, int B, int C, int H, 
     const int nb = (B - b0 < ipc) ? B - b0 : ipc;
     const long off = (long)b0 * C * HW;
     const long goff = (long)b0 * C * (H + W);
-    hipLaunchKernelGGL(ca_pool_kernel, dim3(nb * C), dim3(256), pool_lds, st, x + off, H, W, RB, yin + goff);
-    hipLaunchKernelGGL(ca_gate_kernel, dim3((H + W + 15) / 16, nb), dim3(256), gate_lds, st, yin + goff, C, H, W,
+    if (!yin_pre)
+      hipLaunchKernelGGL(ca_pool_kernel, dim3(nb * C), dim3(256), pool_lds, st, x + off, H, W, RB, yin + goff);
+    hipLaunchKernelGGL(ca_gate_kernel, dim3((H + W + 15) / 16, nb), dim3(256), gate_lds, st,
+                       (yin_pre ? yin_pre : yin) + goff, C, H, W,
                        mip, conv1_w, conv1_b, bn_w, bn_b, bn_mean, bn_var, bn_eps, convh_w, convh_b, convw_w, convw_b,
                        gate + goff);
     if (V == 4)
@@ -677,4 +679,25 @@ YS_EXPORT int yolosod_ca_forward(const float* x, float* y, int B, int C, int H, 
   }
   YS_CHECK_LAUNCH("ca");
   return 0;
+}
+
+YS_EXPORT int yolosod_ca_forward(const float* x, float* y, int B, int C, int H, int W, const float* conv1_w,
+                                 const float* conv1_b, int mip, const float* bn_w, const float* bn_b,
+                                 const float* bn_mean, const float* bn_var, float bn_eps, const float* convh_w,
+                                 const float* convh_b, const float* convw_w, const float* convw_b, void* workspace,
+                                 size_t workspace_bytes, void* stream) {
+  return ca_forward_impl(x, y, B, C, H, W, conv1_w, conv1_b, mip, bn_w, bn_b, bn_mean, bn_var, bn_eps, convh_w,
+                         convh_b, convw_w, convw_b, nullptr, workspace, workspace_bytes, stream);
+}
+
+// CA_Block with the pooled row / column means already computed by x's producer (yolosod_bias_act_capool):
+// gate + apply only.
+YS_EXPORT int yolosod_ca_forward_pre(const float* x, float* y, int B, int C, int H, int W, const float* conv1_w,
+                                     const float* conv1_b, int mip, const float* bn_w, const float* bn_b,
+                                     const float* bn_mean, const float* bn_var, float bn_eps, const float* convh_w,
+                                     const float* convh_b, const float* convw_w, const float* convw_b,
+                                     const float* yin, void* workspace, size_t workspace_bytes, void* stream) {
+  YS_CHECK_ARG(yin, "ca_pre: null pooled means");
+  return ca_forward_impl(x, y, B, C, H, W, conv1_w, conv1_b, mip, bn_w, bn_b, bn_mean, bn_var, bn_eps, convh_w,
+                         convh_b, convw_w, convw_b, yin, workspace, workspace_bytes, stream);
 }

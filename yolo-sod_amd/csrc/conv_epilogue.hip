@@ -99,6 +99,69 @@ __global__ __launch_bounds__(256) void bias_act_stats_kernel(const float* __rest
   }
 }
 
+// Same epilogue for a conv whose output feeds a CA_Block (ca_block.py:43-44): the pass also produces the plane's row
+// means (over W) and column means (over H) in yin[b][c][0..H+W), the input of CA's gate, so CA never runs its
+// pooling pass over the feature map. One workgroup per plane; the activated plane streams through LDS in bands of
+// <= 8192 floats (as channel_attention.hip's ca_pool_kernel): rows reduced by lane quads, columns in registers.
+template <int ACT, bool RES>
+__global__ __launch_bounds__(256) void bias_act_capool_kernel(const float* __restrict__ y, float* __restrict__ out,
+                                                              const float* __restrict__ bias,
+                                                              const float* __restrict__ res, int C, int H, int W,
+                                                              int RB, long y_bs, long o_bs, long r_bs,
+                                                              float* __restrict__ yin) {
+  extern __shared__ float band[];
+  const long plane = blockIdx.x;
+  const long b = plane / C;
+  const int c = (int)(plane - b * C);
+  const long HW = (long)H * W;
+  const float* yp = y + b * y_bs + (long)c * HW;
+  float* op = out + b * o_bs + (long)c * HW;
+  const float* rp = RES ? res + b * r_bs + (long)c * HW : nullptr;
+  float* o = yin + plane * (long)(H + W);
+  const float bc = bias[c];
+  const int tid = threadIdx.x;
+  float col[4] = {0.f, 0.f, 0.f, 0.f};
+  const float invW = 1.0f / (float)W;
+  for (int h0 = 0; h0 < H; h0 += RB) {
+    const int rb = (H - h0 < RB) ? H - h0 : RB;
+    const int n4 = (rb * W) >> 2;
+    const long base = (long)h0 * W;
+    for (int i = tid; i < n4; i += 256) {
+      float4 v = reinterpret_cast<const float4*>(yp + base)[i];
+      v.x += bc; v.y += bc; v.z += bc; v.w += bc;
+      if (ACT == 1) {
+        v.x = siluf_(v.x); v.y = siluf_(v.y); v.z = siluf_(v.z); v.w = siluf_(v.w);
+      }
+      if (RES) {
+        const float4 r = reinterpret_cast<const float4*>(rp + base)[i];
+        v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
+      }
+      reinterpret_cast<float4*>(op + base)[i] = v;
+      reinterpret_cast<float4*>(band)[i] = v;
+    }
+    __syncthreads();
+    for (int r = tid >> 2; r < rb; r += 64) {
+      float sm = 0.f;
+      for (int w = tid & 3; w < W; w += 4) sm += band[r * W + w];
+      sm = quad_sum(sm);
+      if ((tid & 3) == 0) o[h0 + r] = sm * invW;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int w = tid + 256 * u;
+      if (w < W)
+        for (int r = 0; r < rb; ++r) col[u] += band[r * W + w];
+    }
+    __syncthreads();
+  }
+  const float invH = 1.0f / (float)H;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int w = tid + 256 * u;
+    if (w < W) o[H + w] = col[u] * invH;
+  }
+}
+
 }  // namespace ys
 
 using namespace ys;
@@ -162,5 +225,36 @@ YS_EXPORT int yolosod_bias_act(const float* y, long y_bstride, float* out, long 
     else hipLaunchKernelGGL((bias_act_kernel<0, false>), dim3(blocks), dim3(256), 0, st, y, out, bias, res, C, hw4, yb, ob, rb, total4);
   }
   YS_CHECK_LAUNCH("bias_act");
+  return 0;
+}
+
+// yolosod_bias_act + the CA_Block pooling of `out` (row means over W, then column means over H, per plane) into
+// yin[B*C*(H+W)], the layout yolosod_ca_forward_pre takes. Requires W % 4 == 0, W <= 1024 and 4-aligned strides.
+YS_EXPORT int yolosod_bias_act_capool(const float* y, long y_bstride, float* out, long out_bstride, const float* bias,
+                                      const float* res, long res_bstride, int B, int C, int H, int W, int act,
+                                      float* yin, void* stream) {
+  YS_CHECK_ARG(y && out && bias && yin, "bias_act_capool: null pointer");
+  YS_CHECK_ARG(act == 0 || act == 1, "bias_act_capool: act=%d unsupported", act);
+  YS_CHECK_ARG(B >= 0 && C > 0 && H > 0 && W > 0 && W % 4 == 0 && W <= 1024,
+               "bias_act_capool: W=%d must be a multiple of 4 and <= 1024", W);
+  YS_CHECK_ARG(y_bstride % 4 == 0 && out_bstride % 4 == 0 && (!res || res_bstride % 4 == 0),
+               "bias_act_capool: batch strides must be multiples of 4");
+  YS_CHECK_ARG((((uintptr_t)y | (uintptr_t)out | (uintptr_t)(res ? res : y)) & 15) == 0,
+               "bias_act_capool: pointers must be 16-byte aligned");
+  const long planes = (long)B * C;
+  if (planes == 0) return 0;
+  YS_CHECK_ARG(planes < (1L << 31), "bias_act_capool: too many planes");
+  int RB = 8192 / W;
+  if (RB < 1) RB = 1;
+  if (RB > H) RB = H;
+  const size_t lds = sizeof(float) * (size_t)RB * W;
+  hipStream_t st = (hipStream_t)stream;
+#define YS_BAC(A_, R_)                                                                                           \
+  hipLaunchKernelGGL((bias_act_capool_kernel<A_, R_>), dim3((unsigned)planes), dim3(256), lds, st, y, out, bias, res, \
+                     C, H, W, RB, y_bstride, out_bstride, res_bstride, yin)
+  if (act == 1) { if (res) YS_BAC(1, true); else YS_BAC(1, false); }
+  else { if (res) YS_BAC(0, true); else YS_BAC(0, false); }
+#undef YS_BAC
+  YS_CHECK_LAUNCH("bias_act_capool");
   return 0;
 }

@@ -91,7 +91,7 @@ class Conv(nn.Module):
     Fused form on GPU: MIOpen conv + one HIP epilogue pass (bias + SiLU, optional shortcut / concat slice)."""
 
     default_act = nn.SiLU()
-    # set by DetectionModel when this conv's output feeds an SE ("sum") / CBAM ("summax") gate directly
+    # set by DetectionModel when this conv's output feeds an SE ("sum") / CBAM ("summax") / CA ("capool") directly
     emit_stats = None
 
     def __init__(self, c1, c2, k=1, s=1, p=None, g=1, d=1, act=True):

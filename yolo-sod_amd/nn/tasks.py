@@ -223,14 +223,15 @@ class DetectionModel(BaseModel):
         self.names = {i: f"{i}" for i in range(self.yaml["nc"])}
         self.inplace = self.yaml.get("inplace", True)
 
-        # SE / CBAM whose input is the previous layer's conv output: that conv's epilogue emits the gate's plane
-        # statistics in the same pass (no statistics re-read of the feature map; HIP path only)
+        # SE / CBAM / CA whose input is the previous layer's conv output: that conv's epilogue emits the gate's
+        # plane statistics (CA: row / column means) in the same pass (no statistics re-read; HIP path only)
         for i, m in enumerate(self.model):
-            if i and m.f == -1 and isinstance(m, (M.SE, M.CBAM_Block)):
+            if i and m.f == -1 and isinstance(m, (M.SE, M.CBAM_Block, M.CA_Block)):
                 prod = self.model[i - 1]
                 conv = prod if isinstance(prod, M.Conv) else getattr(prod, "cv2", None)
                 if isinstance(conv, M.Conv):
-                    conv.emit_stats = "summax" if isinstance(m, M.CBAM_Block) else "sum"
+                    conv.emit_stats = ("summax" if isinstance(m, M.CBAM_Block) else
+                                       "capool" if isinstance(m, M.CA_Block) else "sum")
 
         # lazy SE weights: the reference creates them during the stride probe, in forward (= layer) order,
         # after every eager module -> same RNG stream position here.
