@@ -45,20 +45,21 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(cfg_yaml, imgsz, n_images, threads):
-    """Oracle CPU model (fp32 PyTorch-CPU restatement + C NMS) on a bounded sample of the same workload."""
+def cpu_baseline(cfg_yaml, imgsz, n_images, threads, min_seconds=10.0):
+    """Oracle CPU model (fp32 PyTorch-CPU restatement + C NMS) on a bounded sample of the same workload:
+    8-image batches until at least `n_images` images and `min_seconds` of CPU work (capped at 256 images)."""
     from oracle.model_ref import build_cpu_model
     from oracle.nms import non_max_suppression_ref
     torch.set_num_threads(threads)
     m = build_cpu_model(cfg_yaml)
     g = torch.Generator().manual_seed(0)
-    x = torch.rand(n_images, 3, imgsz, imgsz, generator=g)
     with torch.inference_mode():
-        m(x[:1])  # warm-up
+        m(torch.rand(1, 3, imgsz, imgsz, generator=g))  # warm-up
         t0 = time.perf_counter()
         done = 0
-        for i in range(0, n_images, 8):
-            y = m(x[i:i + 8])[0]
+        while done < 256 and (done < n_images or time.perf_counter() - t0 < min_seconds):
+            x = torch.rand(8, 3, imgsz, imgsz, generator=g)
+            y = m(x)[0]
             non_max_suppression_ref(y.numpy().copy(), 0.25, 0.7, max_det=300)
             done += y.shape[0]
         dt = time.perf_counter() - t0
