@@ -87,3 +87,20 @@ def test_oracle_fusion_v5_forward_matches_reference():
     ref = torch.from_numpy(golden("model_v5_out_128")["y"])
     ok, err, _ = tol_close(y, ref, 1e-3, 1e-6)
     assert ok, err
+
+
+def test_concat_elision_plan_matches_plain_forward():
+    """The GPU executor's concat elision (tasks.py _predict_once_planned: producers write their Concat slice in
+    place, the Concat copies the rest) is pure data movement: bit-identical to torch.cat. Run on CPU through the
+    oracle operators (the Conv epilogue's CPU branch honours ``out=``)."""
+    m = build_cpu_model()
+    plan = m._concat_producers()
+    assert sorted(plan.values()) == [16, 21, 26, 30, 34, 37]
+    x = torch.rand(2, 3, 128, 128, generator=torch.Generator().manual_seed(3))
+    with torch.inference_mode():
+        m._fused = False
+        ref = m(x)[0]
+        got = m._predict_once_planned(x)[0]
+        m._fused = True
+    assert m._last_elided == 6
+    assert torch.equal(ref, got)

@@ -171,12 +171,90 @@ class BaseModel(nn.Module):
 
     def _predict_once(self, x):
         """tasks.py:165-192: run layers in YAML order, keeping the outputs other layers read."""
+        if x.device.type == "cuda" and getattr(self, "_fused", False):
+            return self._predict_once_planned(x)
         y = []
         for m in self.model:
             if m.f != -1:
                 x = y[m.f] if isinstance(m.f, int) else [x if j == -1 else y[j] for j in m.f]
             x = m(x)
             y.append(x if m.i in self.save else None)
+        return x
+
+    def _concat_producers(self):
+        """Concat layers whose ``-1`` input is a layer that can write its output straight into the Concat's
+        channel slice: a fused Conv (the HIP epilogue takes a batch-strided ``out``) or a nearest 2x Upsample
+        (one strided copy), read by nothing else. Returns {producer index: concat index}."""
+        plan = getattr(self, "_cplan", None)
+        if plan is not None:
+            return plan
+        plan = {}
+        for c, m in enumerate(self.model):
+            if not isinstance(m, M.Concat) or m.d != 1 or not isinstance(m.f, (list, tuple)) or -1 not in m.f:
+                continue
+            p = c - 1
+            prod = self.model[p]
+            if p in self.save or sum(1 for j in m.f if j in (-1, p)) != 1:
+                continue
+            if (isinstance(prod, M.Conv) and prod.is_fused() and prod.emit_stats is None) or (
+                    isinstance(prod, nn.Upsample) and prod.mode == "nearest" and prod.size is None
+                    and prod.scale_factor in (2, 2.0, (2, 2), (2.0, 2.0))):
+                plan[p] = c
+        self._cplan = plan
+        return plan
+
+    def _predict_once_planned(self, x):
+        """GPU fused forward with concat elision: for a planned Concat, the buffer is allocated when its ``-1``
+        producer runs (every other input is an earlier layer's saved output, so all shapes are known), the
+        producer writes its channel slice in place, and the Concat copies only the other inputs. Same values as
+        torch.cat (pure copies), one HBM round trip less for the producer's part."""
+        plan = self._concat_producers()
+        y = []
+        pend = {}  # concat index -> (buffer, channel offset of each input)
+        elided = 0
+        for m in self.model:
+            inp = x
+            if m.f != -1:
+                inp = y[m.f] if isinstance(m.f, int) else [x if j == -1 else y[j] for j in m.f]
+            c = plan.get(m.i)
+            if c is not None and isinstance(inp, torch.Tensor) and inp.dim() == 4:
+                cat = self.model[c]
+                B, _, H, W = inp.shape
+                if isinstance(m, nn.Upsample):
+                    H, W = 2 * H, 2 * W
+                    cp = inp.shape[1]
+                else:
+                    cv = m.conv
+                    cp = cv.out_channels
+                    H, W = ((n + 2 * p - d * (k - 1) - 1) // s + 1 for n, p, d, k, s in
+                            zip((H, W), cv.padding, cv.dilation, cv.kernel_size, cv.stride))
+                srcs = [None if j == -1 else y[j] for j in cat.f]
+                chans = [cp if s is None else s.shape[1] for s in srcs]
+                if all(s is None or (s.shape[0], s.shape[2], s.shape[3]) == (B, H, W) for s in srcs):
+                    buf = torch.empty((B, sum(chans), H, W), dtype=inp.dtype, device=inp.device)
+                    offs = [sum(chans[:i]) for i in range(len(chans))]
+                    k = [j for j in cat.f].index(-1)
+                    out = buf[:, offs[k]:offs[k] + cp]
+                    if isinstance(m, nn.Upsample):
+                        h, w = inp.shape[2], inp.shape[3]
+                        out.view(B, cp, h, 2, w, 2).copy_(inp[:, :, :, None, :, None].expand(B, cp, h, 2, w, 2))
+                    else:
+                        m.forward_fuse(inp, out=out)
+                    pend[c] = (buf, offs, chans)
+                    x = out
+                    y.append(None)
+                    continue
+            if m.i in pend:
+                buf, offs, chans = pend.pop(m.i)
+                elided += 1
+                for j, o, n in zip(m.f, offs, chans):
+                    if j != -1:
+                        buf[:, o:o + n].copy_(y[j])
+                x = buf
+            else:
+                x = m(inp)
+            y.append(x if m.i in self.save else None)
+        self._last_elided = elided
         return x
 
     def is_fused(self, thresh=10):
@@ -191,6 +269,8 @@ class BaseModel(nn.Module):
                     m.conv = _fuse_conv_and_bn(m.conv, m.bn)
                     delattr(m, "bn")
                     m.forward = m.forward_fuse
+        self._fused = True
+        self._cplan = None
         return self
 
 
