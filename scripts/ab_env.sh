@@ -1,0 +1,18 @@
+#!/bin/bash
+# Same-box A/B of an environment toggle on the default bench line: bash scripts/ab_env.sh TAG VAR VALUE_A VALUE_B
+# Runs A, B, A, B (no cpu_baseline) and writes gpurun_out/TAG/{a,b}{1,2}.json.
+set -o pipefail
+TAG=$1; VAR=$2; VA=$3; VB=$4
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+for i in 1 2; do
+  env "$VAR=$VA" timeout -k 10 300 python -u bench.py --no-cpu-baseline > "$OUT/a$i.json" 2> "$OUT/a$i.err" || exit 1
+  env "$VAR=$VB" timeout -k 10 300 python -u bench.py --no-cpu-baseline > "$OUT/b$i.json" 2> "$OUT/b$i.err" || exit 1
+done
+python - "$OUT" <<'PY'
+import json, sys, glob, os
+for f in sorted(glob.glob(os.path.join(sys.argv[1], "*.json"))):
+    d = json.load(open(f))
+    ops = {f"{o['op']}{o['shape'][1]}": o["avg_ms"] for o in d["hip_ops"]}
+    print(os.path.basename(f), d["value"], d["ms_per_step"], ops)
+PY

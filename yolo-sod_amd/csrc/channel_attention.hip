@@ -172,9 +172,9 @@ __global__ __launch_bounds__(256) void channel_gate_kernel(const float* __restri
 // (the 4-deep per-plane version streamed at ~4 TB/s, this shape at ~6 like cbam_apply). Scalar path otherwise.
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void plane_scale_kernel(const float* __restrict__ x, float* __restrict__ y,
-                                                          const float* __restrict__ gate, int C, long HW) {
-  const int b = blockIdx.z;
-  const int c0 = blockIdx.y * 8;
+                                                          const float* __restrict__ gate, int C, long HW, int rev) {
+  const int b = rev ? gridDim.z - 1 - blockIdx.z : blockIdx.z;
+  const int c0 = (rev ? gridDim.y - 1 - blockIdx.y : blockIdx.y) * 8;
   const int n = (C - c0 < 8) ? C - c0 : 8;
   const float* gb = gate + (long)b * C + c0;
   if ((HW & 3) == 0) {
@@ -520,7 +520,7 @@ static int se_forward_impl(const float* x, float* y, int B, int C, int H, int W,
     hipLaunchKernelGGL((channel_gate_kernel<false>), dim3(nb), dim3(256), lds, st, ps, nullptr, pp.parts, C,
                        1.0f / (float)HW, fc1_w, fc1_b, fc2_w, fc2_b, hidden, gate + (long)b0 * C);
     hipLaunchKernelGGL(plane_scale_kernel, dim3((unsigned)xchunks, (unsigned)((C + 7) / 8), (unsigned)nb), dim3(256),
-                       0, st, x + off, y + off, gate + (long)b0 * C, C, HW);
+                       0, st, x + off, y + off, gate + (long)b0 * C, C, HW, mall_reverse());
   }
   YS_CHECK_LAUNCH("se");
   return 0;

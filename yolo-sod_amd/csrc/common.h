@@ -3,6 +3,7 @@
 // passed as void*, never synchronises, and reports failures through an int return code plus
 // yolosod_last_error() (see include/yolosod_hip.h).
 #pragma once
+#include <stdlib.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stddef.h>
@@ -134,5 +135,16 @@ __device__ __forceinline__ float xor32_max(float v) {
 // fp32 MFMA fragment types
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// Streaming passes that re-read a tensor written just before (> 256 MiB MALL) walk it back to front, so the tail the
+// producer wrote last is still in the Infinity Cache when the pass starts. YOLOSOD_MALL_REVERSE=0 restores the
+// forward order (A/B). Results are identical either way (each workgroup's work and summation order is unchanged).
+static inline int mall_reverse() {
+  static const int r = [] {
+    const char* e = getenv("YOLOSOD_MALL_REVERSE");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  return r;
+}
 
 }  // namespace ys

@@ -15,8 +15,9 @@ template <int ACT, bool RES>
 __global__ __launch_bounds__(256) void bias_act_kernel(const float* __restrict__ y, float* __restrict__ out,
                                                        const float* __restrict__ bias, const float* __restrict__ res,
                                                        int C, long HW4, long y_bs4, long o_bs4, long r_bs4,
-                                                       long total4) {
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total4; i += (long)gridDim.x * 256) {
+                                                       long total4, int rev) {
+  for (long i0 = (long)blockIdx.x * 256 + threadIdx.x; i0 < total4; i0 += (long)gridDim.x * 256) {
+    const long i = rev ? total4 - 1 - i0 : i0;
     const long b = i / ((long)C * HW4);
     const long rem = i - b * (long)C * HW4;
     const int c = (int)(rem / HW4);
@@ -43,9 +44,11 @@ __global__ __launch_bounds__(256) void bias_act_stats_kernel(const float* __rest
                                                              const float* __restrict__ bias,
                                                              const float* __restrict__ res, int C, long HW,
                                                              long y_bs, long o_bs, long r_bs, int parts, long seg,
-                                                             float* __restrict__ psum, float* __restrict__ pmax) {
-  const long plane = blockIdx.x / parts;
-  const int k = blockIdx.x % parts;
+                                                             float* __restrict__ psum, float* __restrict__ pmax,
+                                                             int rev) {
+  const long bx = rev ? (long)gridDim.x - 1 - blockIdx.x : (long)blockIdx.x;
+  const long plane = bx / parts;
+  const int k = (int)(bx % parts);
   const long b = plane / C;
   const int c = (int)(plane - b * C);
   const long s0 = k * seg;
@@ -94,8 +97,8 @@ __global__ __launch_bounds__(256) void bias_act_stats_kernel(const float* __rest
   }
   __syncthreads();
   if (tid == 0) {
-    psum[blockIdx.x] = (ss[0] + ss[1]) + (ss[2] + ss[3]);
-    if (MAX) pmax[blockIdx.x] = fmaxf(fmaxf(sm[0], sm[1]), fmaxf(sm[2], sm[3]));
+    psum[bx] = (ss[0] + ss[1]) + (ss[2] + ss[3]);
+    if (MAX) pmax[bx] = fmaxf(fmaxf(sm[0], sm[1]), fmaxf(sm[2], sm[3]));
   }
 }
 
@@ -187,7 +190,7 @@ YS_EXPORT int yolosod_bias_act_stats(const float* y, long y_bstride, float* out,
   hipStream_t st = (hipStream_t)stream;
 #define YS_BAS(A_, R_, M_)                                                                                         \
   hipLaunchKernelGGL((bias_act_stats_kernel<A_, R_, M_>), dim3((unsigned)blocks), dim3(256), 0, st, y, out, bias, res, \
-                     C, HW, y_bstride, out_bstride, res_bstride, parts, seg, psum, pmax)
+                     C, HW, y_bstride, out_bstride, res_bstride, parts, seg, psum, pmax, mall_reverse())
   const bool mx = pmax != nullptr;
   if (act == 1) {
     if (res) { if (mx) YS_BAS(1, true, true); else YS_BAS(1, true, false); }
@@ -218,11 +221,11 @@ YS_EXPORT int yolosod_bias_act(const float* y, long y_bstride, float* out, long 
   hipStream_t st = (hipStream_t)stream;
   const long hw4 = HW / 4, yb = y_bstride / 4, ob = out_bstride / 4, rb = res_bstride / 4;
   if (act == 1) {
-    if (res) hipLaunchKernelGGL((bias_act_kernel<1, true>), dim3(blocks), dim3(256), 0, st, y, out, bias, res, C, hw4, yb, ob, rb, total4);
-    else hipLaunchKernelGGL((bias_act_kernel<1, false>), dim3(blocks), dim3(256), 0, st, y, out, bias, res, C, hw4, yb, ob, rb, total4);
+    if (res) hipLaunchKernelGGL((bias_act_kernel<1, true>), dim3(blocks), dim3(256), 0, st, y, out, bias, res, C, hw4, yb, ob, rb, total4, mall_reverse());
+    else hipLaunchKernelGGL((bias_act_kernel<1, false>), dim3(blocks), dim3(256), 0, st, y, out, bias, res, C, hw4, yb, ob, rb, total4, mall_reverse());
   } else {
-    if (res) hipLaunchKernelGGL((bias_act_kernel<0, true>), dim3(blocks), dim3(256), 0, st, y, out, bias, res, C, hw4, yb, ob, rb, total4);
-    else hipLaunchKernelGGL((bias_act_kernel<0, false>), dim3(blocks), dim3(256), 0, st, y, out, bias, res, C, hw4, yb, ob, rb, total4);
+    if (res) hipLaunchKernelGGL((bias_act_kernel<0, true>), dim3(blocks), dim3(256), 0, st, y, out, bias, res, C, hw4, yb, ob, rb, total4, mall_reverse());
+    else hipLaunchKernelGGL((bias_act_kernel<0, false>), dim3(blocks), dim3(256), 0, st, y, out, bias, res, C, hw4, yb, ob, rb, total4, mall_reverse());
   }
   YS_CHECK_LAUNCH("bias_act");
   return 0;
