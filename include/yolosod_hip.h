@@ -144,6 +144,13 @@ int yolosod_nms(float* pred, int B, int nc, int A, float conf_thres, double iou_
 int yolosod_bias_act(const float* y, long y_bstride, float* out, long out_bstride, const float* bias,
                      const float* res, long res_bstride, int B, int C, long HW, int act, void* stream);
 
+/* yolosod_bias_act that also stores channels [c2lo, C) of the result packed in out2 ([B, C - c2lo, HW], batch
+ * stride out2_bstride): C2f's Bottleneck chain (block.py:249-253, :343-356) reads channel slices of the concat
+ * buffer, which MIOpen would otherwise make contiguous with a copy pass per Bottleneck. */
+int yolosod_bias_act_dual(const float* y, long y_bstride, float* out, long out_bstride, const float* bias,
+                          const float* res, long res_bstride, float* out2, long out2_bstride, int c2lo, int B, int C,
+                          long HW, int act, void* stream);
+
 /* 1x1 convolution (stride 1, groups 1) of the backbone as an fp32 MFMA GEMM with the epilogue fused:
  * out[b*out_bs + m*HW + p] = act(sum_k w[m][k] x[b*x_bs + k*HW + p] + bias[m]) (+ res[...]); Cin % 32 == 0. */
 int yolosod_conv1x1(const float* x, long x_bs, const float* w, const float* bias, float* out, long out_bs,

@@ -211,6 +211,24 @@ def test_bias_act_slice(cuda):
     assert ok, err
 
 
+@pytest.mark.parametrize("c2lo,res", [(8, False), (0, True), (15, True)])
+def test_bias_act_dual_store(c2lo, res, cuda):
+    """yolosod_bias_act_dual: the slice store equals yolosod_bias_act bit for bit and out2 holds channels
+    [c2lo, C) of it packed (C2f's Bottleneck inputs)."""
+    from yolosod_amd import _hip
+    g = torch.Generator().manual_seed(c2lo)
+    y = torch.randn(3, 16, 10, 12, generator=g).to(cuda)
+    b = torch.randn(16, generator=g).to(cuda)
+    r = torch.randn(3, 16, 10, 12, generator=g).to(cuda) if res else None
+    buf = torch.zeros(3, 40, 10, 12, device=cuda)
+    out2 = torch.full((3, 16 - c2lo, 10, 12), float("nan"), device=cuda)
+    out = _hip.bias_act(y, b, 1, out=buf[:, 8:24], res=r, out2=out2, c2lo=c2lo)
+    ref = _hip.bias_act(y, b, 1, out=torch.empty_like(y), res=r)
+    assert torch.equal(out, ref)
+    assert torch.equal(out2, ref[:, c2lo:])
+    assert float(buf[:, :8].abs().max()) == 0.0 and float(buf[:, 24:].abs().max()) == 0.0
+
+
 @pytest.mark.parametrize("c3,img", [(64, 256), (128, 192), (64, 200)])
 def test_detect_head_fused_vs_oracle(c3, img, cuda):
     """Fused last 1x1 convs + decode vs the fp64 oracle (1x1 convs then decode_ref, head.py:70,100-131)."""

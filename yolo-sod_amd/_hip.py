@@ -49,6 +49,7 @@ SIGNATURES = {
     "yolosod_layernorm": (_i, [_vp, _vp, _l, _i, _vp, _vp, _f, _vp]),
     "yolosod_attention": (_i, [_vp, _vp, _l, _i, _i, _i, _vp]),
     "yolosod_bias_act": (_i, [_vp, _l, _vp, _l, _vp, _vp, _l, _i, _i, _l, _i, _vp]),
+    "yolosod_bias_act_dual": (_i, [_vp, _l, _vp, _l, _vp, _vp, _l, _vp, _l, _i, _i, _i, _l, _i, _vp]),
     "yolosod_bias_act_capool": (_i, [_vp, ctypes.c_long, _vp, ctypes.c_long, _vp, _vp, ctypes.c_long, _i, _i, _i, _i,
                                      _i, _vp, _vp]),
     "yolosod_ca_forward_pre": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp,
@@ -409,7 +410,7 @@ def nms(pred, conf_thres, iou_thres, classes, agnostic, multi_label, max_det, ma
     return out, counts, index
 
 
-def bias_act(y, bias, act, out=None, res=None, stats=None):
+def bias_act(y, bias, act, out=None, res=None, stats=None, out2=None, c2lo=0):
     """Backbone conv epilogue: out = act(y + bias[c]) (+ res). ``out`` may be a channel slice [B, C, H, W] of a
     larger contiguous concat buffer (batch stride > C*H*W); ``res`` likewise. In place when out is None.
     ``stats`` ("sum" / "summax"): also emit out's per-plane partial sums (+ maxes) for a following SE / CBAM,
@@ -420,6 +421,10 @@ def bias_act(y, bias, act, out=None, res=None, stats=None):
     HW = H * W
     if out is None:
         out = y
+    if out2 is not None and stats is not None:  # statistics variants have no dual store: copy afterwards
+        out = bias_act(y, bias, act, out=out, res=res, stats=stats)
+        out2.copy_(out[:, c2lo:])
+        return out
 
     def bstride(t, name):
         if t.device.type != "cuda" or t.dtype != torch.float32:
@@ -431,6 +436,14 @@ def bias_act(y, bias, act, out=None, res=None, stats=None):
     yb = bstride(y, "y")
     ob = bstride(out, "out")
     rb = bstride(res, "res") if res is not None else 0
+    if out2 is not None and stats is None:  # ``out2`` = packed copy of channels [c2lo, C) (next conv's input)
+        if (out2.device.type != "cuda" or out2.dtype != torch.float32 or tuple(out2.shape) != (B, C - c2lo, H, W)
+                or out2.stride(3) != 1 or out2.stride(2) != W or out2.stride(1) != HW):
+            raise RuntimeError("bias_act: out2 must be a float32 GPU tensor [B, C - c2lo, H, W] with contiguous channels")
+        _check(lib.yolosod_bias_act_dual(y.data_ptr(), yb, out.data_ptr(), ob, _dev(bias, "bias"),
+                                         None if res is None else res.data_ptr(), rb, out2.data_ptr(), out2.stride(0),
+                                         int(c2lo), B, C, HW, int(act), _stream()), "bias_act_dual")
+        return out
     if stats == "capool":  # CA_Block input: pooled row / column means of out, [B, C, H + W]
         if W % 4 or W > 1024:
             stats = None

@@ -11,11 +11,12 @@
 
 namespace ys {
 
-template <int ACT, bool RES>
+template <int ACT, bool RES, bool DUAL = false>
 __global__ __launch_bounds__(256) void bias_act_kernel(const float* __restrict__ y, float* __restrict__ out,
                                                        const float* __restrict__ bias, const float* __restrict__ res,
                                                        int C, long HW4, long y_bs4, long o_bs4, long r_bs4,
-                                                       long total4, int rev) {
+                                                       long total4, int rev, float* __restrict__ out2 = nullptr,
+                                                       int c2lo = 0, long o2_bs4 = 0) {
   for (long i0 = (long)blockIdx.x * 256 + threadIdx.x; i0 < total4; i0 += (long)gridDim.x * 256) {
     const long i = rev ? total4 - 1 - i0 : i0;
     const long b = i / ((long)C * HW4);
@@ -32,6 +33,8 @@ __global__ __launch_bounds__(256) void bias_act_kernel(const float* __restrict__
       v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
     }
     reinterpret_cast<float4*>(out)[b * o_bs4 + rem] = v;
+    // second, packed copy of channels [c2lo, C): the next conv's input without a separate .contiguous() pass
+    if (DUAL && c >= c2lo) reinterpret_cast<float4*>(out2)[b * o2_bs4 + rem - (long)c2lo * HW4] = v;
   }
 }
 
@@ -228,6 +231,39 @@ YS_EXPORT int yolosod_bias_act(const float* y, long y_bstride, float* out, long 
     else hipLaunchKernelGGL((bias_act_kernel<0, false>), dim3(blocks), dim3(256), 0, st, y, out, bias, res, C, hw4, yb, ob, rb, total4, mall_reverse());
   }
   YS_CHECK_LAUNCH("bias_act");
+  return 0;
+}
+
+// yolosod_bias_act that also writes channels [c2lo, C) of the result to out2 ([B, C - c2lo, HW], batch stride
+// out2_bstride). C2f feeds its Bottleneck chain from channel slices of the concat buffer; MIOpen needs packed
+// inputs, so without this every Bottleneck input was re-read and re-written by a copy kernel.
+YS_EXPORT int yolosod_bias_act_dual(const float* y, long y_bstride, float* out, long out_bstride, const float* bias,
+                                    const float* res, long res_bstride, float* out2, long out2_bstride, int c2lo,
+                                    int B, int C, long HW, int act, void* stream) {
+  YS_CHECK_ARG(y && out && bias && out2, "bias_act_dual: null pointer");
+  YS_CHECK_ARG(act == 0 || act == 1, "bias_act_dual: act=%d unsupported", act);
+  YS_CHECK_ARG(c2lo >= 0 && c2lo < C, "bias_act_dual: c2lo=%d outside [0, C=%d)", c2lo, C);
+  YS_CHECK_ARG(HW % 4 == 0 && y_bstride % 4 == 0 && out_bstride % 4 == 0 && out2_bstride % 4 == 0 &&
+                   (!res || res_bstride % 4 == 0),
+               "bias_act_dual: HW and batch strides must be multiples of 4");
+  YS_CHECK_ARG((((uintptr_t)y | (uintptr_t)out | (uintptr_t)out2 | (uintptr_t)(res ? res : y)) & 15) == 0,
+               "bias_act_dual: pointers must be 16-byte aligned");
+  const long total4 = (long)B * C * (HW / 4);
+  if (total4 == 0) return 0;
+  long blocks = (total4 + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipStream_t st = (hipStream_t)stream;
+  const long hw4 = HW / 4, yb = y_bstride / 4, ob = out_bstride / 4, rb = res_bstride / 4, o2 = out2_bstride / 4;
+#define YS_BAD(A_, R_)                                                                                        \
+  hipLaunchKernelGGL((bias_act_kernel<A_, R_, true>), dim3(blocks), dim3(256), 0, st, y, out, bias, res, C, hw4, \
+                     yb, ob, rb, total4, mall_reverse(), out2, c2lo, o2)
+  if (act == 1) {
+    if (res) YS_BAD(1, true); else YS_BAD(1, false);
+  } else {
+    if (res) YS_BAD(0, true); else YS_BAD(0, false);
+  }
+#undef YS_BAD
+  YS_CHECK_LAUNCH("bias_act_dual");
   return 0;
 }
 

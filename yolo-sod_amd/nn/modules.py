@@ -58,11 +58,12 @@ def _act_code(act):
 CONV1X1_GEMM = os.environ.get("YOLOSOD_CONV1X1", "0") == "1"
 
 
-def conv_epilogue(conv: nn.Conv2d, act_code, x, out=None, res=None, stats=None):
+def conv_epilogue(conv: nn.Conv2d, act_code, x, out=None, res=None, stats=None, out2=None, c2lo=0):
     """GPU fast path of ``act(conv(x)) (+ res)``: MIOpen conv without bias, then one HIP pass for bias +
     activation (+ shortcut), optionally written straight into a channel slice ``out`` of a concat buffer.
     ``stats`` ("sum" / "summax"): the same pass emits the output's per-plane partial statistics for a following
     SE / CBAM gate (``_hip.PlaneStats`` on the returned tensor).
+    ``out2``: also store channels [c2lo, C) packed there (the next conv's input; C2f's Bottleneck chain).
     Returns None when the fast path does not apply (CPU tensor, no bias, unsupported activation / shape)."""
     if x.device.type != "cuda" or conv.bias is None or act_code is None or x.dtype != torch.float32:
         return None
@@ -70,19 +71,24 @@ def conv_epilogue(conv: nn.Conv2d, act_code, x, out=None, res=None, stats=None):
             and conv.in_channels % 32 == 0 and x.stride(1) == x.shape[2] * x.shape[3] and x.stride(3) == 1
             and x.stride(2) == x.shape[3] and (x.shape[2] * x.shape[3]) % 4 == 0 and x.stride(0) % 4 == 0):
         # 1x1 conv = GEMM on NCHW with the epilogue fused (no MIOpen layout transposes, no extra pass)
-        return _hip.conv1x1(x, conv.weight.detach().reshape(conv.out_channels, -1), conv.bias.detach(), act_code,
-                            out=out, res=res)
+        y = _hip.conv1x1(x, conv.weight.detach().reshape(conv.out_channels, -1), conv.bias.detach(), act_code,
+                         out=out, res=res)
+        if out2 is not None:
+            out2.copy_(y[:, c2lo:])
+        return y
     y = F.conv2d(x, conv.weight, None, conv.stride, conv.padding, conv.dilation, conv.groups)
     if (y.shape[2] * y.shape[3]) % 4:
         y = y + conv.bias.view(1, -1, 1, 1)
         y = F.silu(y) if act_code == 1 else y
         if res is not None:
             y = y + res
+        if out2 is not None:
+            out2.copy_(y[:, c2lo:])
         if out is not None:
             out.copy_(y)
             return out
         return y
-    return _hip.bias_act(y, conv.bias.detach(), act_code, out=out, res=res, stats=stats)
+    return _hip.bias_act(y, conv.bias.detach(), act_code, out=out, res=res, stats=stats, out2=out2, c2lo=c2lo)
 
 
 class Conv(nn.Module):
@@ -103,13 +109,15 @@ class Conv(nn.Module):
     def forward(self, x):
         return self.act(self.bn(self.conv(x)))
 
-    def forward_fuse(self, x, out=None, res=None):
-        y = conv_epilogue(self.conv, _act_code(self.act), x, out, res, self.emit_stats)
+    def forward_fuse(self, x, out=None, res=None, out2=None, c2lo=0):
+        y = conv_epilogue(self.conv, _act_code(self.act), x, out, res, self.emit_stats, out2, c2lo)
         if y is not None:
             return y
         y = self.act(self.conv(x))
         if res is not None:
             y = y + res
+        if out2 is not None:
+            out2.copy_(y[:, c2lo:])
         if out is not None:
             out.copy_(y)
             return out
@@ -143,10 +151,12 @@ class Bottleneck(nn.Module):
         self.cv2 = Conv(c_, c2, k[1], 1, g=g)
         self.add = shortcut and c1 == c2
 
-    def forward(self, x, out=None):
+    def forward(self, x, out=None, out2=None):
         if self.cv2.is_fused():  # shortcut fused into cv2's epilogue, output optionally into a concat slice
-            return self.cv2.forward_fuse(self.cv1(x), out=out, res=x if self.add else None)
+            return self.cv2.forward_fuse(self.cv1(x), out=out, res=x if self.add else None, out2=out2)
         y = x + self.cv2(self.cv1(x)) if self.add else self.cv2(self.cv1(x))
+        if out2 is not None:
+            out2.copy_(y)
         if out is not None:
             out.copy_(y)
             return out
@@ -166,10 +176,15 @@ class C2f(nn.Module):
             # every branch writes its channel slice of one buffer: no torch.cat copy (block.py:249-253 semantics)
             B, _, H, W = x.shape
             n, c = len(self.m), self.c
+            # each Bottleneck's input also lands packed in `t` (dual-store epilogue): MIOpen reads packed tensors,
+            # so a channel slice of z would cost a copy pass per Bottleneck
             z = torch.empty((B, (2 + n) * c, H, W), dtype=x.dtype, device=x.device)
-            self.cv1.forward_fuse(x, out=z[:, : 2 * c])
+            t = torch.empty((B, c, H, W), dtype=x.dtype, device=x.device) if n else None
+            self.cv1.forward_fuse(x, out=z[:, : 2 * c], out2=t, c2lo=c)
             for i, m in enumerate(self.m):
-                m(z[:, (1 + i) * c:(2 + i) * c], out=z[:, (2 + i) * c:(3 + i) * c])
+                nxt = torch.empty_like(t) if i + 1 < n else None
+                m(t, out=z[:, (2 + i) * c:(3 + i) * c], out2=nxt)
+                t = nxt
             return self.cv2(z)
         y = list(self.cv1(x).chunk(2, 1))
         y.extend(m(y[-1]) for m in self.m)

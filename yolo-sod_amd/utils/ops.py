@@ -25,8 +25,20 @@ def xywh2xyxy(x: torch.Tensor) -> torch.Tensor:
     return y
 
 
+_CLIP_BOUNDS = {}
+
+
 def clip_boxes(boxes: torch.Tensor, shape):
-    """ops.py:319-338 (tensor branch)."""
+    """ops.py:319-338 (tensor branch). On the GPU the four per-column clamps (eight kernels) run as one clamp
+    against cached [0,0,0,0] / [w,h,w,h] bound tensors: min(max(v, 0), bound) per element, the same values."""
+    if boxes.device.type == "cuda" and boxes.dtype == torch.float32 and boxes.shape[-1] == 4:
+        key = (boxes.device, float(shape[0]), float(shape[1]))
+        lim = _CLIP_BOUNDS.get(key)
+        if lim is None:
+            lim = _CLIP_BOUNDS[key] = (torch.zeros(4, device=boxes.device),
+                                       torch.tensor([shape[1], shape[0], shape[1], shape[0]], dtype=torch.float32,
+                                                    device=boxes.device))
+        return boxes.clamp_(min=lim[0], max=lim[1])
     boxes[..., 0] = boxes[..., 0].clamp(0, shape[1])
     boxes[..., 1] = boxes[..., 1].clamp(0, shape[0])
     boxes[..., 2] = boxes[..., 2].clamp(0, shape[1])
