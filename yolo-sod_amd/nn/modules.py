@@ -545,13 +545,25 @@ class Detect(nn.Module):
         return (self.reg_max == 16 and 1 <= self.nc <= 16 and b2.in_channels == 64 and b3.in_channels in (64, 128)
                 and b2.bias is not None and b3.bias is not None and x[0].dtype == torch.float32)
 
+    def tower_features(self, i, xi):
+        """Level i's box / class tower features (cv2[i][:-1], cv3[i][:-1]): the inputs of the fused head kernel."""
+        return self.cv2[i][:-1](xi).contiguous(), self.cv3[i][:-1](xi).contiguous()
+
+    def forward_towers(self, feats):
+        """The fused head on tower features computed elsewhere (the executor's side stream): [(fb_i, fc_i)]."""
+        return self._head([f[0] for f in feats], [f[1] for f in feats])
+
     def _fused_forward(self, x):
         """cv2[i][:-1] / cv3[i][:-1] towers (PyTorch-ROCm convs + HIP epilogues), then the last 1x1 convs of both
         towers fused with DFL / dist2bbox / sigmoid in one HIP kernel (head.py:70 + _inference :100-131)."""
         fb, fc = [], []
         for i in range(self.nl):
-            fb.append(self.cv2[i][:-1](x[i]).contiguous())
-            fc.append(self.cv3[i][:-1](x[i]).contiguous())
+            b, c = self.tower_features(i, x[i])
+            fb.append(b)
+            fc.append(c)
+        return self._head(fb, fc)
+
+    def _head(self, fb, fc):
         w = lambda c: c.weight.detach().reshape(c.out_channels, -1)  # noqa: E731
         y = _hip.detect_head(fb, fc, [w(b[-1]) for b in self.cv2], [b[-1].bias.detach() for b in self.cv2],
                              [w(b[-1]) for b in self.cv3], [b[-1].bias.detach() for b in self.cv3],

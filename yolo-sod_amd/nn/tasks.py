@@ -20,6 +20,7 @@ import contextlib
 import copy
 import hashlib
 import math
+import os
 import re
 from pathlib import Path
 
@@ -31,6 +32,11 @@ import yaml
 from . import modules as M
 
 CFG_DIR = Path(__file__).resolve().parent.parent / "cfg"
+
+# GPU executor: run the Detect towers of each level on a side stream as soon as that level's feature map exists
+# (overlapping the rest of the neck); YOLOSOD_STREAMS=0 keeps everything on one stream (A/B)
+# (2: start them only after the last MAFN operator has been enqueued, so no hot-path op shares the GPU)
+STREAMS = int(os.environ.get("YOLOSOD_STREAMS", "1"))
 
 # name -> class; the YAML resolves module strings through this (tasks.py:995-1002)
 DEFAULT_REGISTRY = {
@@ -209,6 +215,19 @@ class BaseModel(nn.Module):
         producer writes its channel slice in place, and the Concat copies only the other inputs. Same values as
         torch.cat (pure copies), one HBM round trip less for the producer's part."""
         plan = self._concat_producers()
+        det = self.model[-1]
+        towers = lvl = main = side = None
+        if (STREAMS > 0 and isinstance(det, M.Detect) and isinstance(det.f, (list, tuple)) and len(set(det.f)) == len(det.f)
+                and det._fused_ok([x])):
+            lvl = {j: k for k, j in enumerate(det.f)}
+            towers = {}
+            ready = []  # levels whose feature map exists but whose towers wait for the last MAFN op (STREAMS == 2)
+            last_mafn = max((k for k, mm in enumerate(self.model)
+                             if isinstance(mm, (M.SE, M.CBAM_Block, M.CA_Block, M.A2_Attn, M.SwinBlock))), default=-1)
+            main = torch.cuda.current_stream(x.device)
+            side = getattr(self, "_side_stream", None)
+            if side is None or side.device != x.device:
+                side = self._side_stream = torch.cuda.Stream(device=x.device)
         y = []
         pend = {}  # concat index -> (buffer, channel offset of each input)
         elided = 0
@@ -251,8 +270,26 @@ class BaseModel(nn.Module):
                     if j != -1:
                         buf[:, o:o + n].copy_(y[j])
                 x = buf
+            elif m is det and towers is not None and len(towers) == det.nl:
+                main.wait_stream(side)  # every level's tower features are ready (and owned by main from here)
+                x = det.forward_towers([towers[k] for k in range(det.nl)])
             else:
                 x = m(inp)
+            if towers is not None and m is not det:
+                # Detect towers (PyTorch-ROCm convs + HIP epilogues) of each level on the side stream, overlapping
+                # the rest of the neck; inputs / outputs cross streams via record_stream
+                if m.i in lvl:
+                    ready.append((lvl[m.i], x))
+                if ready and (STREAMS != 2 or m.i >= last_mafn):
+                    side.wait_stream(main)
+                    for k, xk in ready:
+                        xk.record_stream(side)
+                        with torch.cuda.stream(side):
+                            fb, fc = det.tower_features(k, xk)
+                        fb.record_stream(main)
+                        fc.record_stream(main)
+                        towers[k] = (fb, fc)
+                    ready = []
             y.append(x if m.i in self.save else None)
         self._last_elided = elided
         return x
