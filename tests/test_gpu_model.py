@@ -125,3 +125,34 @@ def test_fusion_v5_model_matches_reference_and_oracle(cuda):
         ref = cpu(x)[0]
     ok, err, _ = tol_close(y, ref, ATOL, 0.0)
     assert ok, f"vs oracle at 640: max abs err {err:.3g}"
+
+
+def test_executor_streams_and_concat_elision_are_bit_identical(gpu_model, cuda):
+    """The GPU executor's side-stream Detect towers and concat elision move data and reorder launches only: the
+    output equals the plain one-stream, torch.cat forward bit for bit (tasks.py _predict_once_planned).
+    MIOpen's split-K conv solvers accumulate with atomics (run-to-run differences ~5e-5 in the backbone), so the
+    comparison runs with torch.backends.cudnn.deterministic (every HIP kernel of this library is deterministic)."""
+    from yolosod_amd.nn import tasks
+    g = torch.Generator().manual_seed(5)
+    x = torch.rand(4, 3, 320, 320, generator=g).to(cuda)
+    saved = tasks.STREAMS
+    det = torch.backends.cudnn.deterministic
+    torch.backends.cudnn.deterministic = True
+    try:
+        with torch.inference_mode():
+            tasks.STREAMS = 1
+            y_streams = gpu_model(x)[0].clone()
+            assert gpu_model._last_elided == 6
+            tasks.STREAMS = 0
+            y_one = gpu_model(x)[0].clone()
+            gpu_model._fused = False  # plain executor: torch.cat, one stream
+            try:
+                y_plain = gpu_model(x)[0].clone()
+            finally:
+                gpu_model._fused = True
+    finally:
+        tasks.STREAMS = saved
+        torch.backends.cudnn.deterministic = det
+    torch.cuda.synchronize()
+    assert torch.equal(y_streams, y_one)
+    assert torch.equal(y_one, y_plain)
