@@ -151,6 +151,13 @@ int yolosod_bias_act_dual(const float* y, long y_bstride, float* out, long out_b
                           const float* res, long res_bstride, float* out2, long out2_bstride, int c2lo, int B, int C,
                           long HW, int act, void* stream);
 
+/* Thin fused 1x1 convolution of the backbone (conv.py:37-55 after fuse(), 1x1 case): out = SiLU(W x + bias) (+ res)
+ * for Cout in {64, 128}, Cin in {64, 96, 128, 192, 256}, HW % 64 == 0; x / out / res may be channel slices (batch
+ * strides, multiples of 4); out2 (optional, NULL) = packed copy of channels [c2lo, Cout). Other shapes: error. */
+int yolosod_conv1x1_thin(const float* x, long x_bs, const float* w, const float* bias, float* out, long out_bs,
+                         const float* res, long res_bs, float* out2, long out2_bs, int c2lo, int B, int Cin, int Cout,
+                         long HW, void* stream);
+
 /* 1x1 convolution (stride 1, groups 1) of the backbone as an fp32 MFMA GEMM with the epilogue fused:
  * out[b*out_bs + m*HW + p] = act(sum_k w[m][k] x[b*x_bs + k*HW + p] + bias[m]) (+ res[...]); Cin % 32 == 0. */
 int yolosod_conv1x1(const float* x, long x_bs, const float* w, const float* bias, float* out, long out_bs,

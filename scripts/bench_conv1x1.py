@@ -53,6 +53,9 @@ def main():
             ta = timeit(lambda: _hip.bias_act(F.conv2d(x, w4), b, 1))
             ok = shape[1] % 32 == 0 and (shape[2] * shape[3]) % 4 == 0
             tb = timeit(lambda: _hip.conv1x1(x, w, b, 1)) if ok else float("nan")
+            okt = _hip.conv1x1_thin_ok(x, cout)
+            tt = timeit(lambda: _hip.conv1x1_thin(x, w, b)) if okt else float("nan")
+            print(f"   thin {tt:7.3f} ms", flush=True)
             flops = 2.0 * shape[0] * shape[2] * shape[3] * shape[1] * cout
             print(f"{str(shape):24s} -> {cout:5d}  miopen+epi {ta:7.3f} ms  gemm {tb:7.3f} ms  "
                   f"({flops / tb / 1e9 if ok else 0:6.1f} TF/s gemm)", flush=True)

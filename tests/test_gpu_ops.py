@@ -211,6 +211,34 @@ def test_bias_act_slice(cuda):
     assert ok, err
 
 
+@pytest.mark.parametrize("B,Cin,Cout,H,W,res,dual", [(2, 96, 64, 32, 40, False, False), (3, 256, 128, 16, 16, True, False),
+                                                     (2, 64, 64, 8, 24, True, True), (1, 192, 128, 40, 40, False, True),
+                                                     (2, 128, 64, 80, 80, False, False)])
+def test_conv1x1_thin(B, Cin, Cout, H, W, res, dual, cuda):
+    """yolosod_conv1x1_thin: SiLU(conv1x1(x) + b) (+ res) vs fp64, from / into channel slices, dual store."""
+    from yolosod_amd import _hip
+    g = torch.Generator().manual_seed(Cin * 7 + Cout + H)
+    x = torch.randn(B, Cin, H, W, generator=g)
+    w = torch.randn(Cout, Cin, generator=g) / Cin ** 0.5
+    b = torch.randn(Cout, generator=g)
+    r = torch.randn(B, Cout, H, W, generator=g) if res else None
+    ref = torch.nn.functional.silu(torch.nn.functional.conv2d(x.double(), w.double().view(Cout, Cin, 1, 1), b.double()))
+    if res:
+        ref = ref + r.double()
+    xin = torch.zeros(B, Cin + 4, H, W, device=cuda)
+    xin[:, 4:] = x.to(cuda)
+    buf = torch.zeros(B, Cout + 8, H, W, device=cuda)
+    c2lo = Cout // 2
+    out2 = torch.full((B, Cout - c2lo, H, W), float("nan"), device=cuda) if dual else None
+    out = _hip.conv1x1_thin(xin[:, 4:], w.to(cuda), b.to(cuda), out=buf[:, 4:4 + Cout],
+                            res=None if r is None else r.to(cuda), out2=out2, c2lo=c2lo)
+    ok, err, _ = tol_close(out.cpu(), ref, 1e-4, 1e-5)
+    assert ok, err
+    assert float(buf[:, :4].abs().max()) == 0.0 and float(buf[:, 4 + Cout:].abs().max()) == 0.0
+    if dual:
+        assert torch.equal(out2, out[:, c2lo:])
+
+
 @pytest.mark.parametrize("c2lo,res", [(8, False), (0, True), (15, True)])
 def test_bias_act_dual_store(c2lo, res, cuda):
     """yolosod_bias_act_dual: the slice store equals yolosod_bias_act bit for bit and out2 holds channels

@@ -49,6 +49,7 @@ SIGNATURES = {
     "yolosod_layernorm": (_i, [_vp, _vp, _l, _i, _vp, _vp, _f, _vp]),
     "yolosod_attention": (_i, [_vp, _vp, _l, _i, _i, _i, _vp]),
     "yolosod_bias_act": (_i, [_vp, _l, _vp, _l, _vp, _vp, _l, _i, _i, _l, _i, _vp]),
+    "yolosod_conv1x1_thin": (_i, [_vp, _l, _vp, _vp, _vp, _l, _vp, _l, _vp, _l, _i, _i, _i, _i, _l, _vp]),
     "yolosod_bias_act_dual": (_i, [_vp, _l, _vp, _l, _vp, _vp, _l, _vp, _l, _i, _i, _i, _l, _i, _vp]),
     "yolosod_bias_act_capool": (_i, [_vp, ctypes.c_long, _vp, ctypes.c_long, _vp, _vp, ctypes.c_long, _i, _i, _i, _i,
                                      _i, _vp, _vp]),
@@ -467,6 +468,47 @@ def bias_act(y, bias, act, out=None, res=None, stats=None, out2=None, c2lo=0):
     _check(lib.yolosod_bias_act(y.data_ptr(), yb, out.data_ptr(), ob, _dev(bias, "bias"),
                                 None if res is None else res.data_ptr(), rb, B, C, HW, int(act), _stream()),
            "bias_act")
+    return out
+
+
+THIN1X1_COUT = (64, 128)
+THIN1X1_CIN = (64, 96, 128, 192, 256)
+
+
+def conv1x1_thin_ok(x, cout) -> bool:
+    """Shapes the thin fused 1x1 conv kernel takes (yolosod_conv1x1_thin)."""
+    B, Cin, H, W = x.shape
+    return (x.device.type == "cuda" and x.dtype == torch.float32 and cout in THIN1X1_COUT and Cin in THIN1X1_CIN
+            and (H * W) % 64 == 0 and x.stride(3) == 1 and x.stride(2) == W and x.stride(1) == H * W
+            and x.stride(0) % 4 == 0 and x.data_ptr() % 16 == 0)
+
+
+def conv1x1_thin(x, w, bias, out=None, res=None, out2=None, c2lo=0):
+    """SiLU(1x1 conv(x) + bias) (+ res) for Cout 64 / 128 and Cin <= 256 in one HIP kernel (weights in registers,
+    x tiles in LDS, fp32 MFMA); ``x`` / ``out`` / ``res`` may be channel slices, ``out2`` = packed channels
+    [c2lo, Cout)."""
+    lib = load_library()
+    B, Cin, H, W = x.shape
+    Cout = w.shape[0]
+    HW = H * W
+    if out is None:
+        out = torch.empty((B, Cout, H, W), dtype=torch.float32, device=x.device)
+
+    def bstride(t, name, C):
+        if t.device.type != "cuda" or t.dtype != torch.float32:
+            raise RuntimeError(f"conv1x1_thin: {name} must be a float32 GPU tensor")
+        if tuple(t.shape) != (B, C, H, W) or t.stride(3) != 1 or t.stride(2) != W or t.stride(1) != HW:
+            raise RuntimeError(f"conv1x1_thin: {name} must be [B,{C},H,W] with contiguous channels")
+        return t.stride(0)
+
+    xb = bstride(x, "x", Cin)
+    ob = bstride(out, "out", Cout)
+    rb = bstride(res, "res", Cout) if res is not None else 0
+    o2 = bstride(out2, "out2", Cout - c2lo) if out2 is not None else 0
+    _check(lib.yolosod_conv1x1_thin(x.data_ptr(), xb, _dev(w.contiguous(), "weight"), _dev(bias, "bias"),
+                                    out.data_ptr(), ob, None if res is None else res.data_ptr(), rb,
+                                    None if out2 is None else out2.data_ptr(), o2, int(c2lo), B, Cin, Cout, HW,
+                                    _stream()), "conv1x1_thin")
     return out
 
 

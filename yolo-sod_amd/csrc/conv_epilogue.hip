@@ -168,6 +168,88 @@ __global__ __launch_bounds__(256) void bias_act_capool_kernel(const float* __res
   }
 }
 
+
+// Thin 1x1 convolution (stride 1, groups 1) with the epilogue fused: out = act(W x + b) (+ res), optional packed
+// second store of channels [c2lo, M). For the backbone's large-HW, small-channel 1x1 convs (Cout 64 / 128,
+// Cin <= 256) the MIOpen path (a GEMM library kernel at low arithmetic intensity + this file's epilogue pass) runs
+// far below HBM speed. Here one workgroup owns a 64-pixel column of one image at a time: the x tile [K][64] is staged
+// in LDS with float4 loads, the weights sit in registers for the workgroup's whole run of tiles (k-permuted so each
+// lane group holds a contiguous k quarter as float4s), and v_mfma_f32_16x16x4_f32 (exact fp32) produces all M
+// outputs of the 64 pixels; wave w owns output rows [w*M/4, (w+1)*M/4).
+template <int M, int K, bool RES, bool DUAL>
+__global__ __launch_bounds__(256, 2) void conv1x1_thin_kernel(const float* __restrict__ x, long x_bs,
+                                                              const float* __restrict__ w,
+                                                              const float* __restrict__ bias, float* __restrict__ out,
+                                                              long o_bs, const float* __restrict__ res, long r_bs,
+                                                              float* __restrict__ out2, long o2_bs, int c2lo, int HW,
+                                                              int ntile) {
+  constexpr int RB = M / 64;   // 16-row blocks per wave
+  constexpr int KQ = K / 4;    // k quarter per lane group
+  constexpr int XS = 68;       // LDS row stride (floats)
+  __shared__ __attribute__((aligned(16))) float xs[K * XS];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int l15 = lane & 15, g = lane >> 4;
+  const int b = blockIdx.y;
+  const float* xb = x + (long)b * x_bs;
+  float4 a[RB][KQ / 4];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb) {
+    const float* wr = w + (long)(wid * (M / 4) + rb * 16 + l15) * K + g * KQ;
+#pragma unroll
+    for (int t = 0; t < KQ / 4; ++t) a[rb][t] = *reinterpret_cast<const float4*>(wr + 4 * t);
+  }
+  float bv[RB][4];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bv[rb][r] = bias[wid * (M / 4) + rb * 16 + 4 * g + r];
+  for (int tile = blockIdx.x; tile < ntile; tile += gridDim.x) {
+    const int p0 = tile * 64;
+    __syncthreads();  // the previous tile's readers are done with xs
+#pragma unroll 4
+    for (int e = tid; e < K * 16; e += 256) {
+      const int row = e >> 4, c4 = e & 15;
+      *reinterpret_cast<float4*>(xs + row * XS + 4 * c4) =
+          *reinterpret_cast<const float4*>(xb + (long)row * HW + p0 + 4 * c4);
+    }
+    __syncthreads();
+    f32x4 acc[RB][4];
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+      for (int pb = 0; pb < 4; ++pb) acc[rb][pb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t4 = 0; t4 < KQ / 4; ++t4)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float* xr = xs + (g * KQ + 4 * t4 + c) * XS + l15;
+        float bx[4];
+#pragma unroll
+        for (int pb = 0; pb < 4; ++pb) bx[pb] = xr[16 * pb];
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) {
+          const float av = c == 0 ? a[rb][t4].x : c == 1 ? a[rb][t4].y : c == 2 ? a[rb][t4].z : a[rb][t4].w;
+#pragma unroll
+          for (int pb = 0; pb < 4; ++pb) acc[rb][pb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bx[pb], acc[rb][pb], 0, 0, 0);
+        }
+      }
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wid * (M / 4) + rb * 16 + 4 * g + r;
+#pragma unroll
+        for (int pb = 0; pb < 4; ++pb) {
+          const int p = p0 + pb * 16 + l15;
+          float v = siluf_(acc[rb][pb][r] + bv[rb][r]);
+          if (RES) v += res[(long)b * r_bs + (long)row * HW + p];
+          out[(long)b * o_bs + (long)row * HW + p] = v;
+          if (DUAL && row >= c2lo) out2[(long)b * o2_bs + (long)(row - c2lo) * HW + p] = v;
+        }
+      }
+  }
+}
+
 }  // namespace ys
 
 using namespace ys;
@@ -295,5 +377,40 @@ YS_EXPORT int yolosod_bias_act_capool(const float* y, long y_bstride, float* out
   else { if (res) YS_BAC(0, true); else YS_BAC(0, false); }
 #undef YS_BAC
   YS_CHECK_LAUNCH("bias_act_capool");
+  return 0;
+}
+
+// Thin fused 1x1 conv (+ bias + SiLU (+ res)) for Cout in {64, 128}, Cin in {64, 96, 128, 192, 256}, HW % 64 == 0,
+// 16-byte aligned pointers and 4-aligned batch strides; x / out / res / out2 may be channel slices (batch strides).
+// out2 (optional): packed copy of channels [c2lo, Cout). Returns a non-zero code (no launch) for other shapes.
+YS_EXPORT int yolosod_conv1x1_thin(const float* x, long x_bs, const float* w, const float* bias, float* out, long out_bs,
+                                   const float* res, long res_bs, float* out2, long out2_bs, int c2lo, int B, int Cin,
+                                   int Cout, long HW, void* stream) {
+  YS_CHECK_ARG(x && w && bias && out, "conv1x1_thin: null pointer");
+  YS_CHECK_ARG(HW % 64 == 0 && HW < (1L << 30), "conv1x1_thin: HW=%ld must be a multiple of 64", HW);
+  YS_CHECK_ARG(Cout == 64 || Cout == 128, "conv1x1_thin: Cout=%d unsupported", Cout);
+  YS_CHECK_ARG(x_bs % 4 == 0 && out_bs % 4 == 0 && (!res || res_bs % 4 == 0) && (!out2 || out2_bs % 4 == 0),
+               "conv1x1_thin: batch strides must be multiples of 4");
+  YS_CHECK_ARG((((uintptr_t)x | (uintptr_t)w | (uintptr_t)out) & 15) == 0, "conv1x1_thin: pointers must be 16-byte aligned");
+  YS_CHECK_ARG(!out2 || (c2lo >= 0 && c2lo < Cout), "conv1x1_thin: c2lo=%d", c2lo);
+  if (B == 0) return 0;
+  const int ntile = (int)(HW / 64);
+  const int gx = ntile < 4 ? ntile : (ntile + 3) / 4;  // ~4 tiles per workgroup: weights loaded once per run
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 grid((unsigned)gx, (unsigned)B);
+  bool ok = false;
+#define YS_THIN(M_, K_)                                                                                            \
+  if (Cout == M_ && Cin == K_) {                                                                                   \
+    ok = true;                                                                                                     \
+    if (res && out2) hipLaunchKernelGGL((conv1x1_thin_kernel<M_, K_, true, true>), grid, dim3(256), 0, st, x, x_bs, w, bias, out, out_bs, res, res_bs, out2, out2_bs, c2lo, (int)HW, ntile); \
+    else if (res) hipLaunchKernelGGL((conv1x1_thin_kernel<M_, K_, true, false>), grid, dim3(256), 0, st, x, x_bs, w, bias, out, out_bs, res, res_bs, out2, out2_bs, c2lo, (int)HW, ntile); \
+    else if (out2) hipLaunchKernelGGL((conv1x1_thin_kernel<M_, K_, false, true>), grid, dim3(256), 0, st, x, x_bs, w, bias, out, out_bs, res, res_bs, out2, out2_bs, c2lo, (int)HW, ntile); \
+    else hipLaunchKernelGGL((conv1x1_thin_kernel<M_, K_, false, false>), grid, dim3(256), 0, st, x, x_bs, w, bias, out, out_bs, res, res_bs, out2, out2_bs, c2lo, (int)HW, ntile); \
+  }
+  YS_THIN(64, 64) YS_THIN(64, 96) YS_THIN(64, 128) YS_THIN(64, 192) YS_THIN(64, 256)
+  YS_THIN(128, 64) YS_THIN(128, 96) YS_THIN(128, 128) YS_THIN(128, 192) YS_THIN(128, 256)
+#undef YS_THIN
+  YS_CHECK_ARG(ok, "conv1x1_thin: Cin=%d unsupported", Cin);
+  YS_CHECK_LAUNCH("conv1x1_thin");
   return 0;
 }
