@@ -158,6 +158,14 @@ int yolosod_conv1x1_thin(const float* x, long x_bs, const float* w, const float*
                          const float* res, long res_bs, float* out2, long out2_bs, int c2lo, int B, int Cin, int Cout,
                          long HW, void* stream);
 
+/* yolosod_conv1x1_thin (no res / out2) that also emits the output's per-plane statistics for a following SE / CBAM
+ * gate in the psum / pmax[B*Cout*parts] layout of yolosod_se_forward_pre / yolosod_cbam_forward_pre (parts =
+ * yolosod_plane_parts(HW); plane total in k = 0, 0 / -inf in k > 0); pmax may be NULL; tile_ws = 2*B*Cout*(HW/64)
+ * floats of scratch. */
+int yolosod_conv1x1_thin_stats(const float* x, long x_bs, const float* w, const float* bias, float* out, long out_bs,
+                               int B, int Cin, int Cout, long HW, int parts, float* psum, float* pmax, float* tile_ws,
+                               void* stream);
+
 /* 1x1 convolution (stride 1, groups 1) of the backbone as an fp32 MFMA GEMM with the epilogue fused:
  * out[b*out_bs + m*HW + p] = act(sum_k w[m][k] x[b*x_bs + k*HW + p] + bias[m]) (+ res[...]); Cin % 32 == 0. */
 int yolosod_conv1x1(const float* x, long x_bs, const float* w, const float* bias, float* out, long out_bs,

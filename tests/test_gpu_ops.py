@@ -355,3 +355,31 @@ def test_producer_epilogue_stats_feed_se_and_cbam(shape, cuda):
             b = m(with_stats)       # partials from the producer
         ok, err, _ = tol_close(b.cpu(), a.cpu(), 1e-6, 1e-5)
         assert ok, (type(m).__name__, err)
+
+
+@pytest.mark.parametrize("B,Cin,H,W,stats", [(2, 96, 40, 40, "summax"), (3, 64, 16, 24, "sum"), (2, 256, 8, 8, "summax")])
+def test_conv1x1_thin_stats_feed_se_and_cbam(B, Cin, H, W, stats, cuda):
+    """yolosod_conv1x1_thin_stats: same output as yolosod_conv1x1_thin and plane statistics that SE / CBAM take
+    instead of their own statistics pass (equal up to summation order)."""
+    from yolosod_amd import _hip
+    from yolosod_amd.nn import modules as M
+    g = torch.Generator().manual_seed(Cin + H)
+    x = torch.randn(B, Cin, H, W, generator=g).to(cuda)
+    w = (torch.randn(64, Cin, generator=g) / Cin ** 0.5).to(cuda)
+    b = torch.randn(64, generator=g).to(cuda)
+    plain = _hip.conv1x1_thin(x, w, b)
+    with_stats = _hip.conv1x1_thin(x, w, b, stats=stats)
+    assert torch.equal(plain, with_stats) and with_stats._ys_plane_stats is not None
+    mods = [M.CBAM_Block(64, None, 4)] if stats == "summax" else []
+    if stats == "sum":
+        se = M.SE_Block(16)
+        se._maybe_build(64, None)
+        mods.append(se)
+    for m in mods:
+        recipes.perturb_(m, 3)
+        m.to(cuda).eval()
+        with torch.inference_mode():
+            a = m(plain)
+            c = m(with_stats)
+        ok, err, _ = tol_close(c.cpu(), a.cpu(), 1e-6, 1e-5)
+        assert ok, (type(m).__name__, err)

@@ -49,6 +49,7 @@ SIGNATURES = {
     "yolosod_layernorm": (_i, [_vp, _vp, _l, _i, _vp, _vp, _f, _vp]),
     "yolosod_attention": (_i, [_vp, _vp, _l, _i, _i, _i, _vp]),
     "yolosod_bias_act": (_i, [_vp, _l, _vp, _l, _vp, _vp, _l, _i, _i, _l, _i, _vp]),
+    "yolosod_conv1x1_thin_stats": (_i, [_vp, _l, _vp, _vp, _vp, _l, _i, _i, _i, _l, _i, _vp, _vp, _vp, _vp]),
     "yolosod_conv1x1_thin": (_i, [_vp, _l, _vp, _vp, _vp, _l, _vp, _l, _vp, _l, _i, _i, _i, _i, _l, _vp]),
     "yolosod_bias_act_dual": (_i, [_vp, _l, _vp, _l, _vp, _vp, _l, _vp, _l, _i, _i, _i, _l, _i, _vp]),
     "yolosod_bias_act_capool": (_i, [_vp, ctypes.c_long, _vp, ctypes.c_long, _vp, _vp, ctypes.c_long, _i, _i, _i, _i,
@@ -483,7 +484,7 @@ def conv1x1_thin_ok(x, cout) -> bool:
             and x.stride(0) % 4 == 0 and x.data_ptr() % 16 == 0)
 
 
-def conv1x1_thin(x, w, bias, out=None, res=None, out2=None, c2lo=0):
+def conv1x1_thin(x, w, bias, out=None, res=None, out2=None, c2lo=0, stats=None):
     """SiLU(1x1 conv(x) + bias) (+ res) for Cout 64 / 128 and Cin <= 256 in one HIP kernel (weights in registers,
     x tiles in LDS, fp32 MFMA); ``x`` / ``out`` / ``res`` may be channel slices, ``out2`` = packed channels
     [c2lo, Cout)."""
@@ -505,6 +506,20 @@ def conv1x1_thin(x, w, bias, out=None, res=None, out2=None, c2lo=0):
     ob = bstride(out, "out", Cout)
     rb = bstride(res, "res", Cout) if res is not None else 0
     o2 = bstride(out2, "out2", Cout - c2lo) if out2 is not None else 0
+    if stats in ("sum", "summax") and res is None and out2 is None:
+        # the same pass also yields the following SE / CBAM gate's plane statistics (PlaneStats on the output)
+        parts, _ = plane_parts(HW)
+        psum = torch.empty(B * Cout * parts, dtype=torch.float32, device=x.device)
+        pmax = torch.empty_like(psum) if stats == "summax" else None
+        tws = torch.empty(2 * B * Cout * (HW // 64), dtype=torch.float32, device=x.device)
+        _check(lib.yolosod_conv1x1_thin_stats(x.data_ptr(), xb, _dev(w.contiguous(), "weight"), _dev(bias, "bias"),
+                                              out.data_ptr(), ob, B, Cin, Cout, HW, parts, psum.data_ptr(),
+                                              None if pmax is None else pmax.data_ptr(), tws.data_ptr(), _stream()),
+               "conv1x1_thin_stats")
+        out._ys_plane_stats = PlaneStats(psum, pmax, parts, out.shape)
+        return out
+    if stats is not None:
+        raise RuntimeError(f"conv1x1_thin: stats={stats!r} needs res=None and out2=None")
     _check(lib.yolosod_conv1x1_thin(x.data_ptr(), xb, _dev(w.contiguous(), "weight"), _dev(bias, "bias"),
                                     out.data_ptr(), ob, None if res is None else res.data_ptr(), rb,
                                     None if out2 is None else out2.data_ptr(), o2, int(c2lo), B, Cin, Cout, HW,

@@ -176,20 +176,23 @@ __global__ __launch_bounds__(256) void bias_act_capool_kernel(const float* __res
 // in LDS with float4 loads, the weights sit in registers for the workgroup's whole run of tiles (k-permuted so each
 // lane group holds a contiguous k quarter as float4s), and v_mfma_f32_16x16x4_f32 (exact fp32) produces all M
 // outputs of the 64 pixels; wave w owns output rows [w*M/4, (w+1)*M/4).
-template <int M, int K, bool RES, bool DUAL>
+// STATS: also the per-(plane, tile) sum and max of out in tsum/tmax[(b*M + row)*ntile + tile] (a following SE /
+// CBAM gate's statistics, reduced per plane by thin_stats_reduce_kernel).
+template <int M, int K, bool RES, bool DUAL, bool STATS = false>
 __global__ __launch_bounds__(256, 2) void conv1x1_thin_kernel(const float* __restrict__ x, long x_bs,
                                                               const float* __restrict__ w,
                                                               const float* __restrict__ bias, float* __restrict__ out,
                                                               long o_bs, const float* __restrict__ res, long r_bs,
                                                               float* __restrict__ out2, long o2_bs, int c2lo, int HW,
-                                                              int ntile) {
+                                                              int ntile, int rev, float* __restrict__ tsum = nullptr,
+                                                              float* __restrict__ tmax = nullptr) {
   constexpr int RB = M / 64;   // 16-row blocks per wave
   constexpr int KQ = K / 4;    // k quarter per lane group
   constexpr int XS = 68;       // LDS row stride (floats)
   __shared__ __attribute__((aligned(16))) float xs[K * XS];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int l15 = lane & 15, g = lane >> 4;
-  const int b = blockIdx.y;
+  const int b = rev ? gridDim.y - 1 - blockIdx.y : blockIdx.y;  // last images first: see mall_reverse()
   const float* xb = x + (long)b * x_bs;
   float4 a[RB][KQ / 4];
 #pragma unroll
@@ -238,6 +241,7 @@ __global__ __launch_bounds__(256, 2) void conv1x1_thin_kernel(const float* __res
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = wid * (M / 4) + rb * 16 + 4 * g + r;
+        float ts = 0.f, tm = -INFINITY;
 #pragma unroll
         for (int pb = 0; pb < 4; ++pb) {
           const int p = p0 + pb * 16 + l15;
@@ -245,8 +249,47 @@ __global__ __launch_bounds__(256, 2) void conv1x1_thin_kernel(const float* __res
           if (RES) v += res[(long)b * r_bs + (long)row * HW + p];
           out[(long)b * o_bs + (long)row * HW + p] = v;
           if (DUAL && row >= c2lo) out2[(long)b * o2_bs + (long)(row - c2lo) * HW + p] = v;
+          if (STATS) {
+            ts += v;
+            tm = fmaxf(tm, v);
+          }
+        }
+        if (STATS) {
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) {  // the 16 lanes of this lane group hold the row's 64 pixels
+            ts += __shfl_xor(ts, o, 64);
+            tm = fmaxf(tm, __shfl_xor(tm, o, 64));
+          }
+          if (l15 == 0) {
+            const long ti = ((long)b * M + row) * ntile + tile;
+            tsum[ti] = ts;
+            tmax[ti] = tm;
+          }
         }
       }
+  }
+}
+
+// Per-plane totals of the thin kernel's tile partials, in the (psum, pmax)[plane*parts + k] layout the SE / CBAM
+// *_forward_pre gates read: k = 0 holds the plane's sum / max, k > 0 hold 0 / -inf (the gate sums / maxes over k).
+// One wave per plane, fixed order: deterministic and independent of the batch size.
+__global__ __launch_bounds__(256) void thin_stats_reduce_kernel(const float* __restrict__ tsum,
+                                                                const float* __restrict__ tmax, long planes, int ntile,
+                                                                int parts, float* __restrict__ psum,
+                                                                float* __restrict__ pmax) {
+  const long plane = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (plane >= planes) return;
+  float s = 0.f, m = -INFINITY;
+  for (int t = lane; t < ntile; t += 64) {
+    s += tsum[plane * ntile + t];
+    m = fmaxf(m, tmax[plane * ntile + t]);
+  }
+  s = wave_sum(s);
+  m = wave_max(m);
+  for (int k = lane; k < parts; k += 64) {
+    psum[plane * parts + k] = k == 0 ? s : 0.f;
+    if (pmax) pmax[plane * parts + k] = k == 0 ? m : -INFINITY;
   }
 }
 
@@ -402,15 +445,53 @@ YS_EXPORT int yolosod_conv1x1_thin(const float* x, long x_bs, const float* w, co
 #define YS_THIN(M_, K_)                                                                                            \
   if (Cout == M_ && Cin == K_) {                                                                                   \
     ok = true;                                                                                                     \
-    if (res && out2) hipLaunchKernelGGL((conv1x1_thin_kernel<M_, K_, true, true>), grid, dim3(256), 0, st, x, x_bs, w, bias, out, out_bs, res, res_bs, out2, out2_bs, c2lo, (int)HW, ntile); \
-    else if (res) hipLaunchKernelGGL((conv1x1_thin_kernel<M_, K_, true, false>), grid, dim3(256), 0, st, x, x_bs, w, bias, out, out_bs, res, res_bs, out2, out2_bs, c2lo, (int)HW, ntile); \
-    else if (out2) hipLaunchKernelGGL((conv1x1_thin_kernel<M_, K_, false, true>), grid, dim3(256), 0, st, x, x_bs, w, bias, out, out_bs, res, res_bs, out2, out2_bs, c2lo, (int)HW, ntile); \
-    else hipLaunchKernelGGL((conv1x1_thin_kernel<M_, K_, false, false>), grid, dim3(256), 0, st, x, x_bs, w, bias, out, out_bs, res, res_bs, out2, out2_bs, c2lo, (int)HW, ntile); \
+    if (res && out2) hipLaunchKernelGGL((conv1x1_thin_kernel<M_, K_, true, true>), grid, dim3(256), 0, st, x, x_bs, w, bias, out, out_bs, res, res_bs, out2, out2_bs, c2lo, (int)HW, ntile, mall_reverse()); \
+    else if (res) hipLaunchKernelGGL((conv1x1_thin_kernel<M_, K_, true, false>), grid, dim3(256), 0, st, x, x_bs, w, bias, out, out_bs, res, res_bs, out2, out2_bs, c2lo, (int)HW, ntile, mall_reverse()); \
+    else if (out2) hipLaunchKernelGGL((conv1x1_thin_kernel<M_, K_, false, true>), grid, dim3(256), 0, st, x, x_bs, w, bias, out, out_bs, res, res_bs, out2, out2_bs, c2lo, (int)HW, ntile, mall_reverse()); \
+    else hipLaunchKernelGGL((conv1x1_thin_kernel<M_, K_, false, false>), grid, dim3(256), 0, st, x, x_bs, w, bias, out, out_bs, res, res_bs, out2, out2_bs, c2lo, (int)HW, ntile, mall_reverse()); \
   }
   YS_THIN(64, 64) YS_THIN(64, 96) YS_THIN(64, 128) YS_THIN(64, 192) YS_THIN(64, 256)
   YS_THIN(128, 64) YS_THIN(128, 96) YS_THIN(128, 128) YS_THIN(128, 192) YS_THIN(128, 256)
 #undef YS_THIN
   YS_CHECK_ARG(ok, "conv1x1_thin: Cin=%d unsupported", Cin);
   YS_CHECK_LAUNCH("conv1x1_thin");
+  return 0;
+}
+
+// yolosod_conv1x1_thin (no residual / second store) that also emits the output's per-plane statistics for a
+// following SE / CBAM gate in the psum / pmax[B*Cout*parts] layout of yolosod_se_forward_pre /
+// yolosod_cbam_forward_pre (parts = yolosod_plane_parts(HW)); pmax may be NULL. tile_ws: 2*B*Cout*(HW/64) floats.
+YS_EXPORT int yolosod_conv1x1_thin_stats(const float* x, long x_bs, const float* w, const float* bias, float* out,
+                                         long out_bs, int B, int Cin, int Cout, long HW, int parts, float* psum,
+                                         float* pmax, float* tile_ws, void* stream) {
+  YS_CHECK_ARG(x && w && bias && out && psum && tile_ws, "conv1x1_thin_stats: null pointer");
+  YS_CHECK_ARG(HW % 64 == 0 && HW < (1L << 30), "conv1x1_thin_stats: HW=%ld must be a multiple of 64", HW);
+  YS_CHECK_ARG(Cout == 64 || Cout == 128, "conv1x1_thin_stats: Cout=%d unsupported", Cout);
+  YS_CHECK_ARG(parts >= 1, "conv1x1_thin_stats: parts=%d", parts);
+  YS_CHECK_ARG(x_bs % 4 == 0 && out_bs % 4 == 0, "conv1x1_thin_stats: batch strides must be multiples of 4");
+  YS_CHECK_ARG((((uintptr_t)x | (uintptr_t)w | (uintptr_t)out) & 15) == 0,
+               "conv1x1_thin_stats: pointers must be 16-byte aligned");
+  if (B == 0) return 0;
+  const int ntile = (int)(HW / 64);
+  const int gx = ntile < 4 ? ntile : (ntile + 3) / 4;
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 grid((unsigned)gx, (unsigned)B);
+  float* tsum = tile_ws;
+  float* tmax = tile_ws + (long)B * Cout * ntile;
+  bool ok = false;
+#define YS_THINS(M_, K_)                                                                                          \
+  if (Cout == M_ && Cin == K_) {                                                                                  \
+    ok = true;                                                                                                    \
+    hipLaunchKernelGGL((conv1x1_thin_kernel<M_, K_, false, false, true>), grid, dim3(256), 0, st, x, x_bs, w, bias, \
+                       out, out_bs, nullptr, 0L, nullptr, 0L, 0, (int)HW, ntile, mall_reverse(), tsum, tmax);                   \
+  }
+  YS_THINS(64, 64) YS_THINS(64, 96) YS_THINS(64, 128) YS_THINS(64, 192) YS_THINS(64, 256)
+  YS_THINS(128, 64) YS_THINS(128, 96) YS_THINS(128, 128) YS_THINS(128, 192) YS_THINS(128, 256)
+#undef YS_THINS
+  YS_CHECK_ARG(ok, "conv1x1_thin_stats: Cin=%d unsupported", Cin);
+  const long planes = (long)B * Cout;
+  hipLaunchKernelGGL(thin_stats_reduce_kernel, dim3((unsigned)((planes + 3) / 4)), dim3(256), 0, st, tsum, tmax, planes,
+                     ntile, parts, psum, pmax);
+  YS_CHECK_LAUNCH("conv1x1_thin_stats");
   return 0;
 }

@@ -70,11 +70,12 @@ def conv_epilogue(conv: nn.Conv2d, act_code, x, out=None, res=None, stats=None, 
     Returns None when the fast path does not apply (CPU tensor, no bias, unsupported activation / shape)."""
     if x.device.type != "cuda" or conv.bias is None or act_code is None or x.dtype != torch.float32:
         return None
-    if (THIN1X1 and act_code == 1 and stats is None and conv.out_channels == 64 and conv.kernel_size == (1, 1) and conv.stride == (1, 1)
+    if (THIN1X1 and act_code == 1 and (stats is None or (stats in ("sum", "summax") and res is None and out2 is None))
+            and conv.out_channels == 64 and conv.kernel_size == (1, 1) and conv.stride == (1, 1)
             and conv.groups == 1 and conv.padding == (0, 0) and _hip.conv1x1_thin_ok(x, conv.out_channels)
             and (out is None or out.data_ptr() % 16 == 0) and (res is None or res.data_ptr() % 16 == 0)):
         return _hip.conv1x1_thin(x, conv.weight.detach().reshape(conv.out_channels, -1), conv.bias.detach(),
-                                 out=out, res=res, out2=out2, c2lo=c2lo)
+                                 out=out, res=res, out2=out2, c2lo=c2lo, stats=stats)
     if (CONV1X1_GEMM and conv.kernel_size == (1, 1) and conv.stride == (1, 1) and conv.groups == 1 and conv.padding == (0, 0)
             and conv.in_channels % 32 == 0 and x.stride(1) == x.shape[2] * x.shape[3] and x.stride(3) == 1
             and x.stride(2) == x.shape[3] and (x.shape[2] * x.shape[3]) % 4 == 0 and x.stride(0) % 4 == 0):
