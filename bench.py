@@ -28,7 +28,8 @@ sys.path.insert(0, str(ROOT))
 import yolosod_import  # noqa: E402,F401
 
 from yolosod_amd import _hip, perf  # noqa: E402
-from yolosod_amd.engine.predictor import DetectionPredictor, gather_detections  # noqa: E402
+from yolosod_amd.engine.predictor import (DetectionPredictor, seeded_images, shard_bounds,  # noqa: E402
+                                          sharded_predict)
 from yolosod_amd.nn.tasks import build_model  # noqa: E402
 
 METRIC = "images/sec @640×640 bs=32, 1→8 MI355X; mAP@0.5:0.95 parity vs CPU ref"
@@ -45,27 +46,169 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(cfg_yaml, imgsz, n_images, threads, min_seconds=10.0):
-    """Oracle CPU model (fp32 PyTorch-CPU restatement + C NMS) on a bounded sample of the same workload:
-    8-image batches until at least `n_images` images and `min_seconds` of CPU work (capped at 256 images)."""
+def host_cpu():
+    """(cpu model string, cores usable by this process): physical cores within the affinity mask, capped by a
+    cgroup CPU quota when one is set."""
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    allowed = len(os.sched_getaffinity(0))
+    try:
+        import psutil
+        per_core = max(1, (psutil.cpu_count() or allowed) // max(1, psutil.cpu_count(logical=False) or allowed))
+    except Exception:
+        per_core = 1
+    cores = max(1, allowed // per_core)
+    for f in ("/sys/fs/cgroup/cpu.max", "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"):
+        try:
+            q = open(f).read().split()
+            if q[0] not in ("max", "-1"):
+                period = int(q[1]) if len(q) > 1 else int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+                cores = max(1, min(cores, int(q[0]) // period))
+            break
+        except (OSError, ValueError, IndexError):
+            continue
+    return model, cores
+
+
+def _median(v):
+    v = sorted(v)
+    return v[len(v) // 2] if len(v) % 2 else 0.5 * (v[len(v) // 2 - 1] + v[len(v) // 2])
+
+
+def cpu_baseline(cfg_yaml, imgsz, warmup=2, iters=5, batch_all=8):
+    """the oracle CPU model (fp32 PyTorch-CPU restatement + C NMS, pinned to the reference
+    by tests/golden) on this host's cores. All usable physical cores on a bounded sample of the workload
+    (``batch_all`` images of the same 640x640 batch per iteration) and 1 thread on BASELINE configs[0] (one
+    640x640 image: the reference's default, OMP_NUM_THREADS=1 at ultralytics/__init__.py:8-9); ``warmup``
+    untimed + the median of ``iters`` timed iterations each. The MAFN + decode + NMS share is timed with hooks
+    on the operator modules inside the same iterations; NMS alone on loaded synthetic tensors (1k/10k/30k
+    candidates per image)."""
     from oracle.model_ref import build_cpu_model
     from oracle.nms import non_max_suppression_ref
-    torch.set_num_threads(threads)
+    from yolosod_amd.nn import modules as M
+    model_name, cores = host_cpu()
     m = build_cpu_model(cfg_yaml)
-    g = torch.Generator().manual_seed(0)
-    with torch.inference_mode():
-        m(torch.rand(1, 3, imgsz, imgsz, generator=g))  # warm-up
+    hot_t = []
+    t_in = {}
+
+    def pre(mod, inp):
+        t_in[id(mod)] = time.perf_counter()
+
+    def post(mod, inp, out):
+        hot_t.append(time.perf_counter() - t_in.pop(id(mod)))
+
+    hot = (M.SE, M.CBAM_Block, M.CA_Block, M.A2_Attn, M.SwinBlock, M.MambaBlock)
+    for mod in m.modules():
+        if isinstance(mod, hot):
+            mod.register_forward_pre_hook(pre)
+            mod.register_forward_hook(post)
+    det = m.model[-1]
+    inf = det._inference
+
+    def timed_inference(x):  # decode (Detect._inference, head.py:100-131)
         t0 = time.perf_counter()
-        done = 0
-        while done < 256 and (done < n_images or time.perf_counter() - t0 < min_seconds):
-            x = torch.rand(8, 3, imgsz, imgsz, generator=g)
-            y = m(x)[0]
-            non_max_suppression_ref(y.numpy().copy(), 0.25, 0.7, max_det=300)
-            done += y.shape[0]
-        dt = time.perf_counter() - t0
-    return {"value": round(done / dt, 3), "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"{done} images {imgsz}x{imgsz} (forward+decode+NMS, oracle fp32 CPU model, "
-                      f"torch threads={threads}), {dt:.1f}s"}
+        y = inf(x)
+        hot_t.append(time.perf_counter() - t0)
+        return y
+
+    det._inference = timed_inference
+
+    def run(threads, bs):
+        torch.set_num_threads(threads)
+        x = seeded_images(0, bs, imgsz)
+        tot, hotv = [], []
+        with torch.inference_mode():
+            for it in range(warmup + iters):
+                hot_t.clear()
+                t0 = time.perf_counter()
+                y = m(x)[0]
+                t1 = time.perf_counter()
+                non_max_suppression_ref(y.numpy().copy(), 0.25, 0.7, max_det=300)
+                t2 = time.perf_counter()
+                if it >= warmup:
+                    tot.append(t2 - t0)
+                    hotv.append(sum(hot_t) + (t2 - t1))
+        med = _median(tot)
+        return {"threads": threads, "batch": bs, "value": round(bs / med, 3), "unit": "images/s",
+                "ms_per_image": round(med / bs * 1e3, 2),
+                "mafn_decode_nms_ms_per_image": round(_median(hotv) / bs * 1e3, 2),
+                "iterations": f"{warmup} warm-up + median of {iters}"}
+
+    t_start = time.perf_counter()
+    all_cores = run(cores, batch_all)
+    one = run(1, 1)
+    # NMS alone, loaded: oracle NMS per image on the same synthetic tensors bench.py times on the GPU
+    nms = {}
+    for n_cand in NMS_LOADS:
+        pred = loaded_predictions(2, 34000, 10, n_cand, 50, 0.25, 0, torch.device("cpu")).numpy()
+        ts = []
+        for b in range(pred.shape[0]):
+            t0 = time.perf_counter()
+            non_max_suppression_ref(pred[b:b + 1].copy(), 0.25, 0.7, max_det=300)
+            ts.append(time.perf_counter() - t0)
+        nms[str(n_cand)] = round(_median(ts) * 1e3, 2)
+    det._inference = inf
+    return {"value": all_cores["value"], "unit": "images/s", "cores": cores, "kind": "port",
+            "cpu_model": model_name,
+            "sample": f"{batch_all} of the {imgsz}x{imgsz} images per iteration, forward + decode + NMS "
+                      f"(conf 0.25), oracle fp32 CPU model, torch threads={cores} (usable physical cores), "
+                      f"{warmup} warm-up + median of {iters}; total CPU wall {time.perf_counter() - t_start:.1f}s",
+            "all_cores": all_cores,
+            "single_thread_configs0": one,
+            "nms_loaded_ms_per_image": nms}
+
+
+NMS_LOADS = (1000, 10000, 30000)
+
+
+def loaded_predictions(B, A, nc, n_cand, clusters, conf, seed, dev, img=640.0):
+    """Synthetic Detect output [B, 4+nc, A] with exactly n_cand anchors per image scoring above ``conf`` (a main
+    class score in (conf, 1)), boxes (xywh) drawn around ``clusters`` centres with heavy overlap, as trained heads
+    produce. Random-init weights leave NMS empty (nothing clears conf 0.25), so NMS at load is timed on these."""
+    g = torch.Generator(device=dev).manual_seed(seed)
+    k = torch.randint(0, clusters, (B, A), generator=g, device=dev)
+    cen = torch.rand(B, clusters, 4, generator=g, device=dev)
+    cx, cy = cen[..., 0] * img, cen[..., 1] * img
+    cw, ch = 8 + cen[..., 2] * 112, 8 + cen[..., 3] * 112
+    jit = torch.randn(4, B, A, generator=g, device=dev) * 0.08
+    gat = lambda t: torch.gather(t, 1, k)  # noqa: E731
+    w, h = gat(cw), gat(ch)
+    box = torch.stack([gat(cx) + jit[0] * w, gat(cy) + jit[1] * h, w * jit[2].exp(), h * jit[3].exp()], 1)
+    cls = torch.rand(B, nc, A, generator=g, device=dev) * conf * 0.9
+    sel = torch.rand(B, A, generator=g, device=dev).argsort(1)[:, :n_cand]
+    main = torch.randint(0, nc, (B, n_cand), generator=g, device=dev)
+    val = conf + (1 - conf) * torch.rand(B, n_cand, generator=g, device=dev)
+    cls[torch.arange(B, device=dev)[:, None], main, sel] = val
+    return torch.cat([box, cls], 1).contiguous()
+
+
+def nms_loaded(dev, B=32, A=34000, nc=10, reps=10):
+    """HIP NMS (predict mode: conf 0.25, iou 0.7, max_det 300) on [B, 4+nc, A] tensors with 1k / 10k / 30k
+    candidates per image, HIP events around each call (fresh copy per call: NMS rewrites boxes in place)."""
+    from yolosod_amd.utils.ops import non_max_suppression_padded
+    res = {}
+    for n_cand in NMS_LOADS:
+        pred = loaded_predictions(B, A, nc, n_cand, 50, 0.25, 0, dev)
+        work = [pred.clone() for _ in range(reps + 3)]
+        ms = []
+        for i, w in enumerate(work):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            _, counts, _ = non_max_suppression_padded(w, 0.25, 0.7, max_det=300)
+            e1.record()
+            if i >= 3:
+                ms.append((e0, e1))
+        torch.cuda.synchronize()
+        t = sorted(a.elapsed_time(b) for a, b in ms)
+        res[str(n_cand)] = {"ms_per_call": round(t[len(t) // 2], 4), "images": B,
+                            "kept_per_image": round(float(counts.float().mean()), 1)}
+    return res
 
 
 def load_traffic():
@@ -86,7 +229,7 @@ def main():
     ap.add_argument("--config", default="n640", choices=list(CONFIGS))
     ap.add_argument("--conf", type=float, default=0.25)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-images", type=int, default=16)
+    ap.add_argument("--no-nms-load", action="store_true")
     ap.add_argument("--miopen-benchmark", action="store_true", help="torch.backends.cudnn.benchmark (MIOpen find)")
     args = ap.parse_args()
     if args.miopen_benchmark:
@@ -105,14 +248,15 @@ def main():
     cfg_yaml, imgsz, bs, label = CONFIGS[args.config]
     model = build_model(cfg_yaml, seed=0, device=dev)
     predictor = DetectionPredictor(model, conf=args.conf, iou=0.7, max_det=300)
-    g = torch.Generator().manual_seed(1000 + rank)
-    x = torch.rand(bs, 3, imgsz, imgsz, generator=g).to(dev)
+    # one global seeded batch of world * bs images (image i from seed 1000 + i); each rank holds its shard
+    n_global = world * bs
+    lo, hi = shard_bounds(n_global, rank, world)
+    x = seeded_images(lo, hi, imgsz, device=dev)
 
     def step():
-        out, counts, _ = predictor.predict_padded(x)
-        if world > 1:
-            gather_detections(out, counts)
-        return counts
+        if world > 1:  # shard -> rank-local predict -> all-gather of the padded detections (global image order)
+            return sharded_predict(predictor.predict_padded, n_global, lambda a, b: x)[1]
+        return predictor.predict_padded(x)[1]
 
     t_w = time.perf_counter()
     for _ in range(args.warmup):
@@ -143,8 +287,12 @@ def main():
         a = agg.setdefault(key, [0.0, 0])
         a[0] += ms
         a[1] += 1
-    ops = []
+    ops, backbone = [], []
     for key, (tot, n) in agg.items():
+        if key[0] not in perf.PATH_OPS:  # backbone conv kernels of this library: outside the path roofline
+            backbone.append({"op": key[0], "shape": list(key[1]), "extra": str(key[2]), "launches": n,
+                             "total_ms_per_step": round(tot / args.steps, 4)})
+            continue
         nbytes, flops = perf.op_cost(key)
         avg = tot / n
         ops.append({"op": key[0], "shape": list(key[1]), "launches": n, "avg_ms": round(avg, 4),
@@ -189,12 +337,16 @@ def main():
         "path_roofline": path_roofline,
         "hip_ops_ms_per_step": round(hip_ms, 3),
         "hip_ops": [{k: v for k, v in o.items() if k not in ("bytes", "flops")} for o in ops],
+        "backbone_hip_ms_per_step": round(sum(o["total_ms_per_step"] for o in backbone), 3),
+        "backbone_hip_ops": sorted(backbone, key=lambda o: -o["total_ms_per_step"])[:12],
+        "nms_loaded": None,
         "cpu_baseline": None,
     }
+    if not args.no_nms_load:  # after the timed region, same process: NMS at controlled candidate loads
+        result["nms_loaded"] = nms_loaded(dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = min(int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)), 16)
         try:
-            result["cpu_baseline"] = cpu_baseline(cfg_yaml, imgsz, args.cpu_images, threads)
+            result["cpu_baseline"] = cpu_baseline(cfg_yaml, imgsz)
         except Exception as e:  # report, never hide
             result["cpu_baseline"] = {"error": repr(e)}
     if world > 1:

@@ -132,8 +132,10 @@ int yolosod_detect_head(int nl, const float* const* box_feat, const float* const
 /* non_max_suppression + torchvision.ops.nms   ultralytics/utils/ops.py:167-316 (nms call :296).
  * pred: [B, 4+nc, A] xywh (rewritten to xyxy in place when in_place); classes: device int32[n_classes] or NULL;
  * out: [B, max_det, 6] rows (x1,y1,x2,y2,conf,cls) in kept order, zero padded; counts: [B];
- * out_index: [B, max_det] anchor index of each kept row (-1 padded). */
+ * out_index: [B, max_det] anchor index of each kept row (-1 padded). max_det 1..2^20 (the reference has no cap,
+ * ops.py:297); the workspace depends on max_det above 1024 (_v2), the original query covers max_det <= 1024. */
 size_t yolosod_nms_workspace(int B, int nc, int A, int multi_label);
+size_t yolosod_nms_workspace_v2(int B, int nc, int A, int multi_label, int max_det);
 int yolosod_nms(float* pred, int B, int nc, int A, float conf_thres, double iou_thres, const int* classes,
                 int n_classes, int agnostic, int multi_label, int max_det, int max_nms, float max_wh, int in_place,
                 float* out, int* counts, int* out_index, void* workspace, size_t workspace_bytes, void* stream);

@@ -54,6 +54,33 @@ def xywh2xyxy_np(x: np.ndarray) -> np.ndarray:
     return y
 
 
+def clip_boxes_ref(boxes: np.ndarray, shape) -> np.ndarray:
+    """ops.py:319-338 (numpy branch, in place): x to [0, w], y to [0, h]."""
+    boxes[..., [0, 2]] = boxes[..., [0, 2]].clip(0, shape[1])
+    boxes[..., [1, 3]] = boxes[..., [1, 3]].clip(0, shape[0])
+    return boxes
+
+
+def scale_boxes_ref(img1_shape, boxes: np.ndarray, img0_shape, ratio_pad=None, padding=True, xywh=False):
+    """ops.py:92-128 in fp32 (in place): undo letterbox gain / pad, then clip to img0_shape.
+    Called per image by DetectionPredictor.postprocess (models/yolo/detect/predict.py:39) on pred[:, :4]."""
+    if ratio_pad is None:
+        gain = min(img1_shape[0] / img0_shape[0], img1_shape[1] / img0_shape[1])
+        pad = (round((img1_shape[1] - img0_shape[1] * gain) / 2 - 0.1),
+               round((img1_shape[0] - img0_shape[0] * gain) / 2 - 0.1))
+    else:
+        gain = ratio_pad[0][0]
+        pad = ratio_pad[1]
+    if padding:
+        boxes[..., 0] -= np.float32(pad[0])
+        boxes[..., 1] -= np.float32(pad[1])
+        if not xywh:
+            boxes[..., 2] -= np.float32(pad[0])
+            boxes[..., 3] -= np.float32(pad[1])
+    boxes[..., :4] /= np.float32(gain)
+    return clip_boxes_ref(boxes, img0_shape)
+
+
 def non_max_suppression_ref(prediction: np.ndarray, conf_thres=0.25, iou_thres=0.45, classes=None, agnostic=False,
                             multi_label=False, max_det=300, nc=0, max_nms=30000, max_wh=7680, in_place=True):
     """Returns (rows: list of [n_i, 6] float32, anchors: list of [n_i] int64). Mutates ``prediction`` (B, 4+nc, A)

@@ -12,25 +12,7 @@ ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT))
 import yolosod_import  # noqa: E402,F401
 from yolosod_amd.utils.ops import non_max_suppression_padded  # noqa: E402
-
-
-def make_pred(B, A, nc, n_cand, clusters, conf, seed, dev, img=640.0):
-    g = torch.Generator(device=dev).manual_seed(seed)
-    k = torch.randint(0, clusters, (B, A), generator=g, device=dev)
-    cen = torch.rand(B, clusters, 4, generator=g, device=dev)
-    cx, cy = cen[..., 0] * img, cen[..., 1] * img
-    cw, ch = 8 + cen[..., 2] * 112, 8 + cen[..., 3] * 112
-    jit = torch.randn(4, B, A, generator=g, device=dev) * 0.08
-    gat = lambda t: torch.gather(t, 1, k)  # noqa: E731
-    w, h = gat(cw), gat(ch)
-    box = torch.stack([gat(cx) + jit[0] * w, gat(cy) + jit[1] * h, w * jit[2].exp(), h * jit[3].exp()], 1)
-    # background scores below conf; n_cand anchors per image get a main-class score in (conf, 1)
-    cls = torch.rand(B, nc, A, generator=g, device=dev) * conf * 0.9
-    sel = torch.rand(B, A, generator=g, device=dev).argsort(1)[:, :n_cand]
-    main = torch.randint(0, nc, (B, n_cand), generator=g, device=dev)
-    val = conf + (1 - conf) * torch.rand(B, n_cand, generator=g, device=dev)
-    cls[torch.arange(B, device=dev)[:, None], main, sel] = val
-    return torch.cat([box, cls], 1).contiguous()
+from bench import loaded_predictions as make_pred  # noqa: E402
 
 
 def main():

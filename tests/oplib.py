@@ -3,6 +3,7 @@ map a module to the keyword arguments of its HIP / oracle function."""
 from __future__ import annotations
 
 import json
+import os
 
 import torch
 
@@ -41,3 +42,29 @@ def tol_close(y, ref, atol, rtol):
     d = (y.double() - ref.double()).abs()
     lim = atol + rtol * ref.double().abs()
     return bool((d <= lim).all()), float(d.max()), float((d / lim).max())
+
+
+# Detect output [B, 4+nc, A]: rows 0-3 are box coordinates in pixels (north-star 1e-3 abs), rows 4.. are class
+# probabilities sigmoid(z). At random init those are ~2e-5 (max 1.26e-3), so an absolute 1e-3 says nothing about
+# them: they are compared in logit space instead, |dp| <= ZTOL * p (1 - p) + 2 ulp(p) (dp = p (1 - p) dz), which
+# is a relative bound for small p and a bound on 1 - p near saturation.
+BOX_ATOL = 1e-3
+SCORE_ZTOL = 1e-4
+
+
+def pred_close(y, ref, box_atol=BOX_ATOL, ztol=SCORE_ZTOL):
+    """(ok, message) for Detect outputs: box rows within box_atol, score rows within ztol in logit space."""
+    y, ref = y.double(), ref.double()
+    db = (y[:, :4] - ref[:, :4]).abs()
+    q = ref[:, 4:]
+    ds = (y[:, 4:] - q).abs()
+    lim = ztol * q * (1 - q) + q.abs().clamp_min(2.0 ** -126) * 2.0 ** -22
+    ratio = float((ds / lim).max())
+    zerr = float((ds / (q * (1 - q)).clamp_min(1e-300)).max())  # ~ max |dz|
+    ok = bool((db <= box_atol).all()) and ratio <= 1.0
+    msg = f"box max|err| {float(db.max()):.3g} (tol {box_atol}); score max|dz| ~{zerr:.3g} (tol {ztol})"
+    log = os.environ.get("YOLOSOD_PARITY_LOG")
+    if log:  # measured margins, for choosing / reviewing tolerances
+        with open(log, "a") as f:
+            f.write(f"{os.environ.get('PYTEST_CURRENT_TEST', '?')}: {msg}\n")
+    return ok, msg

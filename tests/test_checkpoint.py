@@ -95,3 +95,32 @@ def test_loader_executes_nothing_from_the_file(tmp_path):
     except pickle.UnpicklingError:
         pass
     assert not marker.exists()
+
+
+def test_save_checkpoint_restores_preexisting_reference_classes(tmp_path):
+    """saving registers stub classes under the reference class paths for pickle; a module already
+    imported at such a path keeps its own classes afterwards."""
+    import sys
+    import types
+    from yolosod_amd.nn.checkpoint import save_checkpoint
+    from yolosod_amd.nn.tasks import DetectionModel
+    names = ["ultralytics", "ultralytics.nn", "ultralytics.nn.modules", "ultralytics.nn.modules.conv"]
+    saved = {n: sys.modules.get(n) for n in names}
+    fake = {n: types.ModuleType(n) for n in names}
+
+    class Conv:  # stands in for the real reference class
+        pass
+
+    fake["ultralytics.nn.modules.conv"].Conv = Conv
+    sys.modules.update(fake)
+    try:
+        torch.manual_seed(0)
+        save_checkpoint(DetectionModel("yolov12-sod-fusion-v5-simple.yaml"), tmp_path / "m.pt")
+        assert sys.modules["ultralytics.nn.modules.conv"].Conv is Conv
+        assert not hasattr(sys.modules["ultralytics.nn.modules.conv"], "Concat")
+    finally:
+        for n, m in saved.items():
+            if m is None:
+                sys.modules.pop(n, None)
+            else:
+                sys.modules[n] = m

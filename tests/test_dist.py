@@ -3,12 +3,14 @@ for N > 1 (the path's single exchange step)."""
 import os
 import socket
 
+import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
 import yolosod_import  # noqa: F401  (spawned workers re-import this module before conftest runs)
+import conftest  # noqa: F401,E402  (sys.path: repo root + tests/golden for the workers)
 from yolosod_amd.engine.predictor import gather_detections, shard_bounds
 
 
@@ -62,3 +64,61 @@ def test_gather_detections_gloo(world):
     for p in procs:
         p.join(timeout=60)
     assert sorted(res) == [(r, True) for r in range(world)]
+
+
+def _pad_rows(rows, idx, D=300):
+    out = torch.zeros((len(rows), D, 6))
+    index = torch.full((len(rows), D), -1, dtype=torch.int32)
+    for i, (r, a) in enumerate(zip(rows, idx)):
+        out[i, :len(r)] = torch.from_numpy(r)
+        index[i, :len(r)] = torch.from_numpy(a.astype(np.int32))
+    return out, torch.tensor([len(r) for r in rows], dtype=torch.int32), index
+
+
+def _flow_worker(rank, world, port, n_images, q):
+    """The bench's N > 1 flow on CPU: shard_bounds -> rank-local predict (the oracle NMS on precomputed
+    predictions stands in for the GPU predictor) -> gather_detections, via engine.predictor.sharded_predict."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import recipes
+        from oracle.nms import non_max_suppression_ref
+        from yolosod_amd.engine.predictor import sharded_predict
+        preds = recipes.synthetic_predictions(11, n_images, 3000, 10, n_clusters=6)  # one global batch [n, 14, A]
+
+        def local_predict(p):
+            rows, idx = non_max_suppression_ref(p.numpy().copy(), 0.25, 0.3, max_det=300)
+            return _pad_rows(rows, idx)
+
+        g_out, g_cnt = sharded_predict(local_predict, n_images, lambda lo, hi: torch.from_numpy(preds[lo:hi].copy()))
+        rows, idx = non_max_suppression_ref(preds.copy(), 0.25, 0.3, max_det=300)  # unsharded, one process
+        ref_out, ref_cnt, _ = _pad_rows(rows, idx)
+        ok = (g_out.shape == ref_out.shape and torch.equal(g_cnt, ref_cnt) and torch.equal(g_out, ref_out)
+              and int(ref_cnt.min()) > 0 and len(set(ref_cnt.tolist())) > 1)
+        q.put((rank, bool(ok)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n_images", [8, 7])
+def test_sharded_flow_matches_single_process_gloo(n_images):
+    """World size 2: the gathered detections equal the single-process detections row for row, in global image
+    order (distinct per-image counts make a shard-order error visible); 7 images = uneven shards."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_flow_worker, args=(r, 2, port, n_images, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert sorted(res) == [(0, True), (1, True)]
+
+
+def test_seeded_images_are_slices_of_one_global_batch():
+    from yolosod_amd.engine.predictor import seeded_images
+    full = seeded_images(0, 6, 32)
+    for w in (1, 2, 3, 4):
+        parts = [seeded_images(*shard_bounds(6, r, w), 32) for r in range(w)]
+        assert torch.equal(torch.cat(parts), full)

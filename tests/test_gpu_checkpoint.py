@@ -8,6 +8,8 @@ import numpy as np
 import pytest
 import torch
 
+from oplib import pred_close
+
 pytestmark = pytest.mark.gpu
 
 
@@ -42,8 +44,8 @@ def test_checkpoint_weights_gpu_vs_oracle(ckpt_path, cuda):
     with torch.inference_mode():
         y = gm(x.to(cuda))[0]
         ref = cm(x)[0]
-    err = (y.cpu() - ref).abs()
-    assert float(err.max()) <= 1e-3, float(err.max())
+    ok, msg = pred_close(y.cpu(), ref)  # scores in logit space: these heads reach p ~ 0.99
+    assert ok, msg
     # NMS on the GPU predictions: HIP kernels vs the oracle on the same tensor
     with torch.inference_mode():
         out, counts, index = ops.non_max_suppression_padded(y.clone(), 0.25, 0.7, max_det=300)
@@ -53,3 +55,36 @@ def test_checkpoint_weights_gpu_vs_oracle(ckpt_path, cuda):
         assert n == len(rows[i]) and n > 0, (n, len(rows[i]))
         assert np.array_equal(index[i, :n].cpu().numpy(), anchors[i])
         assert np.array_equal(out[i, :n].cpu().numpy(), rows[i])
+
+
+def test_predictor_clipped_rows_match_oracle(ckpt_path, cuda):
+    """a11: DetectionPredictor.predict_padded = HIP NMS + scale_boxes/clip_boxes of the kept rows
+    (models/yolo/detect/predict.py:23-41 -> ops.py:92-128, 319-338 with the tensor input's own shape), bit-exact
+    against the oracle NMS + the oracle scale_boxes on the same predictions. The trained-like head keeps boxes at
+    the image border, so the clip is exercised (asserted)."""
+    from oracle.nms import non_max_suppression_ref, scale_boxes_ref
+    from yolosod_amd.engine.predictor import DetectionPredictor
+    from yolosod_amd.nn.checkpoint import attempt_load_one_weight
+    gm, _ = attempt_load_one_weight(ckpt_path, device=cuda)
+    x = torch.rand(2, 3, 640, 640, generator=torch.Generator().manual_seed(6)).to(cuda)
+    det = torch.backends.cudnn.deterministic
+    torch.backends.cudnn.deterministic = True  # MIOpen split-K atomics otherwise vary run to run (~5e-5)
+    try:
+        with torch.inference_mode():
+            y = gm(x)[0].cpu().numpy()
+            assert np.array_equal(gm(x)[0].cpu().numpy(), y)
+        out, counts, index = DetectionPredictor(gm, conf=0.25, iou=0.7, max_det=300).predict_padded(x)
+    finally:
+        torch.backends.cudnn.deterministic = det
+    rows, anchors = non_max_suppression_ref(y.copy(), 0.25, 0.7, max_det=300)
+    clipped = 0
+    for i in range(2):
+        n = int(counts[i])
+        assert n == len(rows[i]) and n > 0
+        r = rows[i].copy()
+        clipped += int(((r[:, :4] < 0) | (r[:, [0, 2]] > 640).any(1, keepdims=True)
+                        | (r[:, [1, 3]] > 640).any(1, keepdims=True)).any(1).sum())
+        r[:, :4] = scale_boxes_ref((640, 640), r[:, :4].copy(), (640, 640, 3))
+        assert np.array_equal(out[i, :n].cpu().numpy(), r)
+        assert np.array_equal(index[i, :n].cpu().numpy(), anchors[i])
+    assert clipped > 0, "no kept box crosses the image border: the clip is not exercised"

@@ -46,6 +46,9 @@ def test_nms_list_api(cuda):
     (4, 34000, 60, dict(conf_thres=0.001, iou_thres=0.7, multi_label=True)),
     (2, 34000, 3000, dict(conf_thres=0.05, iou_thres=0.5, max_det=1000)),
     (2, 136000, 400, dict(conf_thres=0.25, iou_thres=0.7)),
+    # max_det above the 1024 LDS kept-list (the reference has no cap, ops.py:297): workspace kept lists
+    (2, 34000, 8000, dict(conf_thres=0.05, iou_thres=0.5, max_det=4000)),
+    (1, 34000, 6000, dict(conf_thres=0.001, iou_thres=0.6, multi_label=True, max_det=3000)),
 ])
 def test_nms_full_size_vs_oracle(B, A, clusters, kw, cuda):
     pred = recipes.synthetic_predictions(1000 + B + A, B, A, 10, n_clusters=clusters)

@@ -104,3 +104,33 @@ def test_concat_elision_plan_matches_plain_forward():
         m._fused = True
     assert m._last_elided == 6
     assert torch.equal(ref, got)
+
+
+def test_oracle_model_640_matches_reference_checksums():
+    """The reference's fused fp32 forward of the seed-0 paper model on rand(2,3,640,640) (seed 0), recorded as
+    checksums in model_manifest.json (make_golden.py gen_model): total and per-row sums (rows 4.. are the class
+    probabilities, ~2e-5 each at random init, so their sums pin the class branch) and the max score."""
+    man = json.loads((GOLDEN / "model_manifest.json").read_text())["yolov12-sod-fusion-v5-simple"]["out_640"]
+    m = build_cpu_model()
+    x = torch.rand(2, 3, 640, 640, generator=torch.Generator().manual_seed(0))
+    with torch.inference_mode():
+        y = m(x)[0].double()
+    assert list(y.shape) == man["shape"]
+    rs = y.sum((0, 2))
+    ref_rs = torch.tensor(man["row_sums"], dtype=torch.float64)
+    assert torch.allclose(rs[:4], ref_rs[:4], rtol=1e-7, atol=0), (rs[:4] - ref_rs[:4]).tolist()
+    assert torch.allclose(rs[4:], ref_rs[4:], rtol=1e-7, atol=0), ((rs[4:] - ref_rs[4:]) / ref_rs[4:]).tolist()
+    assert abs(float(y.sum()) - man["sum"]) <= 1e-7 * man["sum"]
+    assert abs(float(y[:, 4:].max()) - man["max_score"]) <= 1e-6 * man["max_score"]
+
+
+def test_oracle_scale_boxes_matches_reference():
+    """scale_boxes / clip_boxes (ops.py:92-128, 319-338) restated in numpy fp32: bit-exact on the reference's
+    outputs for same-shape, letterboxed, explicit ratio_pad and xywh cases."""
+    from oracle.nms import scale_boxes_ref
+    z = golden("scale_boxes")
+    cases = json.loads(str(z["cases"]))
+    assert len(cases) == z["boxes"].shape[0]
+    for i, (s1, s0, rp, pad, xywh) in enumerate(cases):
+        got = scale_boxes_ref(s1, z["boxes"][i].copy(), s0, ratio_pad=rp, padding=pad, xywh=xywh)
+        assert np.array_equal(got, z["out"][i]), (i, np.abs(got - z["out"][i]).max())

@@ -44,6 +44,7 @@ SIGNATURES = {
     "yolosod_detect_decode": (_i, [_i, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp]),
     "yolosod_detect_head": (_i, [_i, _vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp]),
     "yolosod_nms_workspace": (_sz, [_i, _i, _i, _i]),
+    "yolosod_nms_workspace_v2": (_sz, [_i, _i, _i, _i, _i]),
     "yolosod_nms": (_i, [_vp, _i, _i, _i, _f, _d, _vp, _i, _i, _i, _i, _i, _f, _i, _vp, _vp, _vp, _vp, _sz, _vp]),
     "yolosod_gemm_f32": (_i, [_vp, _l, _i, _vp, _l, _i, _i, _vp, _l, _i, _i, _i, _i, _i, _vp, _i, _i, _vp, _vp]),
     "yolosod_layernorm": (_i, [_vp, _vp, _l, _i, _vp, _vp, _f, _vp]),
@@ -120,17 +121,21 @@ class op_timer:
         return False
 
 
-def _launch(key, fn, *args):
-    t = _TIMER
-    if t is None:
-        return fn(*args)
-    e0 = torch.cuda.Event(enable_timing=True)
-    e1 = torch.cuda.Event(enable_timing=True)
-    e0.record()
-    rc = fn(*args)
-    e1.record()
-    t.records.append((key, e0, e1))
-    return rc
+def _launch(key, dev, fn, *args):
+    """Run one C-ABI launch sequence with ``dev`` (the operands' device) as the current HIP device; the stream
+    argument inside ``args`` is that device's current stream (``_stream(dev)``). While an :class:`op_timer` is
+    active, HIP events bracket the sequence on that stream."""
+    with torch.cuda.device(dev):
+        t = _TIMER
+        if t is None:
+            return fn(*args)
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        rc = fn(*args)
+        e1.record()
+        t.records.append((key, e0, e1))
+        return rc
 
 
 def _check(rc: int, what: str) -> None:
@@ -152,14 +157,16 @@ def _dev(t: torch.Tensor, name: str) -> int:
 
 
 def _p(t: torch.Tensor, name: str, numel: int | None = None) -> int:
-    """Pointer of a (parameter) tensor, made fp32-contiguous on the caller's device if needed."""
+    """Pointer of a (parameter) tensor after checking its element count (and, via ``_dev``, that it is a
+    contiguous fp32 GPU tensor: no conversion is done here, callers pass prepared parameters)."""
     if numel is not None and t.numel() != numel:
         raise RuntimeError(f"{name}: expected {numel} elements, got {t.numel()}")
     return _dev(t, name)
 
 
-def _stream() -> int:
-    return torch.cuda.current_stream().cuda_stream
+def _stream(dev) -> int:
+    """The current stream of ``dev`` (the operands' device, not the current device: ADVICE r1)."""
+    return torch.cuda.current_stream(dev).cuda_stream
 
 
 def _workspace(nbytes: int, device) -> torch.Tensor:
@@ -212,11 +219,11 @@ def se_forward(x, fc1_w, fc1_b, fc2_w, fc2_b):
     args = (_dev(x, "x"), _dev(y, "y"), B, C, H, W, _p(fc1_w, "fc1.weight", hid * C), _p(fc1_b, "fc1.bias", hid),
             _p(fc2_w, "fc2.weight", C * hid), _p(fc2_b, "fc2.bias", C), hid)
     if pre is not None:  # plane sums came with x from its producer's epilogue: gate + scale only
-        _check(_launch(("se", tuple(x.shape), hid), lib.yolosod_se_forward_pre, *args, pre.psum.data_ptr(),
-                       ws.data_ptr(), ws.numel(), _stream()), "se_forward_pre")
+        _check(_launch(("se", tuple(x.shape), hid), x.device, lib.yolosod_se_forward_pre, *args, pre.psum.data_ptr(),
+                       ws.data_ptr(), ws.numel(), _stream(x.device)), "se_forward_pre")
     else:
-        _check(_launch(("se", tuple(x.shape), hid), lib.yolosod_se_forward, *args, ws.data_ptr(), ws.numel(),
-                       _stream()), "se_forward")
+        _check(_launch(("se", tuple(x.shape), hid), x.device, lib.yolosod_se_forward, *args, ws.data_ptr(), ws.numel(),
+                       _stream(x.device)), "se_forward")
     return y
 
 
@@ -230,11 +237,11 @@ def cbam_forward(x, fc0_w, fc2_w, sa_w):
     args = (_dev(x, "x"), _dev(y, "y"), B, C, H, W, _p(fc0_w, "fc.0.weight", hid * C),
             _p(fc2_w, "fc.2.weight", C * hid), hid, _p(sa_w, "conv1.weight", 98))
     if pre is not None:
-        _check(_launch(("cbam", tuple(x.shape), hid), lib.yolosod_cbam_forward_pre, *args, pre.psum.data_ptr(),
-                       pre.pmax.data_ptr(), ws.data_ptr(), ws.numel(), _stream()), "cbam_forward_pre")
+        _check(_launch(("cbam", tuple(x.shape), hid), x.device, lib.yolosod_cbam_forward_pre, *args, pre.psum.data_ptr(),
+                       pre.pmax.data_ptr(), ws.data_ptr(), ws.numel(), _stream(x.device)), "cbam_forward_pre")
     else:
-        _check(_launch(("cbam", tuple(x.shape), hid), lib.yolosod_cbam_forward, *args, ws.data_ptr(), ws.numel(),
-                       _stream()), "cbam_forward")
+        _check(_launch(("cbam", tuple(x.shape), hid), x.device, lib.yolosod_cbam_forward, *args, ws.data_ptr(), ws.numel(),
+                       _stream(x.device)), "cbam_forward")
     return y
 
 
@@ -251,11 +258,11 @@ def ca_forward(x, conv1_w, conv1_b, bn_w, bn_b, bn_mean, bn_var, bn_eps, convh_w
             _p(convw_w, "conv_w.weight", C * mip), _p(convw_b, "conv_w.bias", C))
     pre = getattr(x, "_ys_ca_pool", None)
     if pre is not None and pre[1] == tuple(x.shape):  # row / column means came with x from its producer
-        _check(_launch(("ca", tuple(x.shape), mip), lib.yolosod_ca_forward_pre, *args, pre[0].data_ptr(),
-                       ws.data_ptr(), ws.numel(), _stream()), "ca_forward_pre")
+        _check(_launch(("ca", tuple(x.shape), mip), x.device, lib.yolosod_ca_forward_pre, *args, pre[0].data_ptr(),
+                       ws.data_ptr(), ws.numel(), _stream(x.device)), "ca_forward_pre")
     else:
-        _check(_launch(("ca", tuple(x.shape), mip), lib.yolosod_ca_forward, *args, ws.data_ptr(), ws.numel(),
-                       _stream()), "ca_forward")
+        _check(_launch(("ca", tuple(x.shape), mip), x.device, lib.yolosod_ca_forward, *args, ws.data_ptr(), ws.numel(),
+                       _stream(x.device)), "ca_forward")
     return y
 
 
@@ -271,14 +278,14 @@ def a2_forward(x, num_areas, num_heads, proj_w, proj_b, ln_w, ln_b, ln_eps, in_w
         raise RuntimeError(f"A2_Attn: sequence length {num_areas * W} > 320 unsupported")
     y = torch.empty_like(x)
     ws = _workspace(lib.yolosod_a2_workspace(B, C, H, W, num_areas), x.device)
-    _check(_launch(("a2", tuple(x.shape), (num_areas, num_heads)), lib.yolosod_a2_forward, _dev(x, "x"), _dev(y, "y"), B, C, H, W, num_areas, num_heads,
+    _check(_launch(("a2", tuple(x.shape), (num_areas, num_heads)), x.device, lib.yolosod_a2_forward, _dev(x, "x"), _dev(y, "y"), B, C, H, W, num_areas, num_heads,
                                   _p(proj_w, "proj.weight", C * C), _p(proj_b, "proj.bias", C),
                                   _p(ln_w, "layer_norm.weight", C), _p(ln_b, "layer_norm.bias", C), float(ln_eps),
                                   _p(in_w, "in_proj_weight", 3 * C * C), _p(in_b, "in_proj_bias", 3 * C),
                                   _p(mo_w, "attention.out_proj.weight", C * C) if mo_w is not None else None,
                                   _p(mo_b, "attention.out_proj.bias", C) if mo_b is not None else None,
                                   _p(op_w, "out_proj.weight", C * C),
-                                  _p(op_b, "out_proj.bias", C), ws.data_ptr(), ws.numel(), _stream()),
+                                  _p(op_b, "out_proj.bias", C), ws.data_ptr(), ws.numel(), _stream(x.device)),
            "a2_forward")
     return y
 
@@ -296,7 +303,7 @@ def swin_forward(x, num_heads, window, dw_w, ln1_w, ln1_b, ln1_eps, in_w, in_b, 
         raise RuntimeError(f"SwinBlock: head dim {C}/{num_heads} unsupported")
     y = torch.empty_like(x)
     ws = _workspace(lib.yolosod_swin_workspace_v2(B, C, H, W, num_heads, window, hid), x.device)
-    _check(_launch(("swin", tuple(x.shape), (num_heads, window, hid)), lib.yolosod_swin_forward,
+    _check(_launch(("swin", tuple(x.shape), (num_heads, window, hid)), x.device, lib.yolosod_swin_forward,
         _dev(x, "x"), _dev(y, "y"), B, C, H, W, num_heads, window, _p(dw_w, "dw.weight", C * 9),
         _p(ln1_w, "norm1.weight", C), _p(ln1_b, "norm1.bias", C), float(ln1_eps),
         _p(in_w, "in_proj_weight", 3 * C * C), _p(in_b, "in_proj_bias", 3 * C),
@@ -305,7 +312,7 @@ def swin_forward(x, num_heads, window, dw_w, ln1_w, ln1_b, ln1_eps, in_w, in_b, 
         _p(m1_w, "mlp.0.weight", hid * C), _p(m1_b, "mlp.0.bias", hid), hid,
         _p(m2_w, "mlp.2.weight", C * hid), _p(m2_b, "mlp.2.bias", C), _p(pw_w, "pw.weight", C * C),
         _p(bn_w, "bn.weight", C), _p(bn_b, "bn.bias", C), _p(bn_mean, "bn.running_mean", C),
-        _p(bn_var, "bn.running_var", C), float(bn_eps), ws.data_ptr(), ws.numel(), _stream()), "swin_forward")
+        _p(bn_var, "bn.running_var", C), float(bn_eps), ws.data_ptr(), ws.numel(), _stream(x.device)), "swin_forward")
     return y
 
 
@@ -323,7 +330,7 @@ def mamba_glu_forward(x, reduction, in_w, in_bn_w, in_bn_b, in_bn_m, in_bn_v, in
         raise RuntimeError(f"MambaBlock: channels {C} / hidden {ch} must be multiples of 32 (MFMA GEMM K tiles)")
     y = torch.empty_like(x)
     ws = _workspace(lib.yolosod_mamba_glu_workspace(B, C, H, W, ch, r), x.device)
-    _check(_launch(("mamba", tuple(x.shape), (ch, r)), lib.yolosod_mamba_glu_forward,
+    _check(_launch(("mamba", tuple(x.shape), (ch, r)), x.device, lib.yolosod_mamba_glu_forward,
         _dev(x, "x"), _dev(y, "y"), B, C, H, W, ch, r, _p(in_w, "in_proj.0.weight", ch * C),
         _p(in_bn_w, "in_proj.1.weight", ch), _p(in_bn_b, "in_proj.1.bias", ch), _p(in_bn_m, "in_proj.1.running_mean", ch),
         _p(in_bn_v, "in_proj.1.running_var", ch), float(in_eps), _p(pw1_w, "fallback.pw1.weight", 2 * hd * ch),
@@ -332,7 +339,7 @@ def mamba_glu_forward(x, reduction, in_w, in_bn_w, in_bn_b, in_bn_m, in_bn_v, in
         _p(pw2_w, "fallback.pw2.weight", ch * hd), _p(out_w, "out_proj.0.weight", C * ch),
         _p(out_bn_w, "out_proj.1.weight", C), _p(out_bn_b, "out_proj.1.bias", C),
         _p(out_bn_m, "out_proj.1.running_mean", C), _p(out_bn_v, "out_proj.1.running_var", C), float(out_eps),
-        ws.data_ptr(), ws.numel(), _stream()), "mamba_glu_forward")
+        ws.data_ptr(), ws.numel(), _stream(x.device)), "mamba_glu_forward")
     return y
 
 
@@ -351,9 +358,9 @@ def detect_decode(maps, strides, nc, reg_max=16):
     hs = (ctypes.c_int * nl)(*[m.shape[2] for m in maps])
     wsz = (ctypes.c_int * nl)(*[m.shape[3] for m in maps])
     st = (ctypes.c_float * nl)(*[float(s) for s in strides])
-    _check(_launch(("decode", (B, A), nc), lib.yolosod_detect_decode, nl, ctypes.cast(ptrs, ctypes.c_void_p), ctypes.cast(hs, ctypes.c_void_p),
+    _check(_launch(("decode", (B, A), nc), maps[0].device, lib.yolosod_detect_decode, nl, ctypes.cast(ptrs, ctypes.c_void_p), ctypes.cast(hs, ctypes.c_void_p),
                                      ctypes.cast(wsz, ctypes.c_void_p), ctypes.cast(st, ctypes.c_void_p), B, nc,
-                                     reg_max, _dev(y, "y"), _stream()), "detect_decode")
+                                     reg_max, _dev(y, "y"), _stream(maps[0].device)), "detect_decode")
     return y
 
 
@@ -381,11 +388,11 @@ def detect_head(box_feats, cls_feats, box_w, box_b, cls_w, cls_b, strides, nc, r
     hs = (ctypes.c_int * nl)(*[t.shape[2] for t in box_feats])
     wsz = (ctypes.c_int * nl)(*[t.shape[3] for t in box_feats])
     st = (ctypes.c_float * nl)(*[float(s) for s in strides])
-    _check(_launch(("head", (B, A), (nc, c2, c3)), lib.yolosod_detect_head, nl, arr(box_feats, "box_feats"),
+    _check(_launch(("head", (B, A), (nc, c2, c3)), box_feats[0].device, lib.yolosod_detect_head, nl, arr(box_feats, "box_feats"),
                    arr(cls_feats, "cls_feats"), c2, c3, arr(box_w, "box_w"), arr(box_b, "box_b"),
                    arr(cls_w, "cls_w"), arr(cls_b, "cls_b"), ctypes.cast(hs, ctypes.c_void_p),
                    ctypes.cast(wsz, ctypes.c_void_p), ctypes.cast(st, ctypes.c_void_p), B, nc, reg_max,
-                   _dev(y, "y"), _stream()), "detect_head")
+                   _dev(y, "y"), _stream(box_feats[0].device)), "detect_head")
     return y
 
 
@@ -400,15 +407,15 @@ def nms(pred, conf_thres, iou_thres, classes, agnostic, multi_label, max_det, ma
     out = torch.empty((B, max_det, 6), dtype=torch.float32, device=dev)
     counts = torch.empty((B,), dtype=torch.int32, device=dev)
     index = torch.empty((B, max_det), dtype=torch.int32, device=dev)
-    ws = _workspace(lib.yolosod_nms_workspace(B, nc, A, int(multi_label)), dev)
+    ws = _workspace(lib.yolosod_nms_workspace_v2(B, nc, A, int(multi_label), int(max_det)), dev)
     cls_ptr, ncls = None, 0
     if classes is not None:
         ct = torch.as_tensor(classes, dtype=torch.int32, device=dev).reshape(-1).contiguous()
         cls_ptr, ncls = ct.data_ptr(), ct.numel()
-    _check(_launch(("nms", (B, nc, A), int(multi_label)), lib.yolosod_nms, _dev(pred, "prediction"), B, nc, A, float(conf_thres), float(iou_thres), cls_ptr, ncls,
+    _check(_launch(("nms", (B, nc, A), int(multi_label)), dev, lib.yolosod_nms, _dev(pred, "prediction"), B, nc, A, float(conf_thres), float(iou_thres), cls_ptr, ncls,
                            int(bool(agnostic)), int(bool(multi_label)), int(max_det), int(max_nms), float(max_wh),
                            1, out.data_ptr(), counts.data_ptr(), index.data_ptr(), ws.data_ptr(), ws.numel(),
-                           _stream()), "nms")
+                           _stream(dev)), "nms")
     return out, counts, index
 
 
@@ -442,32 +449,32 @@ def bias_act(y, bias, act, out=None, res=None, stats=None, out2=None, c2lo=0):
         if (out2.device.type != "cuda" or out2.dtype != torch.float32 or tuple(out2.shape) != (B, C - c2lo, H, W)
                 or out2.stride(3) != 1 or out2.stride(2) != W or out2.stride(1) != HW):
             raise RuntimeError("bias_act: out2 must be a float32 GPU tensor [B, C - c2lo, H, W] with contiguous channels")
-        _check(lib.yolosod_bias_act_dual(y.data_ptr(), yb, out.data_ptr(), ob, _dev(bias, "bias"),
+        _check(_launch(("bias_act", tuple(y.shape), "dual"), y.device, lib.yolosod_bias_act_dual, y.data_ptr(), yb, out.data_ptr(), ob, _dev(bias, "bias"),
                                          None if res is None else res.data_ptr(), rb, out2.data_ptr(), out2.stride(0),
-                                         int(c2lo), B, C, HW, int(act), _stream()), "bias_act_dual")
+                                         int(c2lo), B, C, HW, int(act), _stream(y.device)), "bias_act_dual")
         return out
     if stats == "capool":  # CA_Block input: pooled row / column means of out, [B, C, H + W]
         if W % 4 or W > 1024:
             stats = None
         else:
             yin = torch.empty((B, C, H + W), dtype=torch.float32, device=y.device)
-            _check(lib.yolosod_bias_act_capool(y.data_ptr(), yb, out.data_ptr(), ob, _dev(bias, "bias"),
+            _check(_launch(("bias_act", tuple(y.shape), "capool"), y.device, lib.yolosod_bias_act_capool, y.data_ptr(), yb, out.data_ptr(), ob, _dev(bias, "bias"),
                                                None if res is None else res.data_ptr(), rb, B, C, H, W, int(act),
-                                               yin.data_ptr(), _stream()), "bias_act_capool")
+                                               yin.data_ptr(), _stream(y.device)), "bias_act_capool")
             out._ys_ca_pool = (yin, tuple(out.shape))
             return out
     if stats is not None:
         parts, seg = plane_parts(HW)
         psum = torch.empty(B * C * parts, dtype=torch.float32, device=y.device)
         pmax = torch.empty_like(psum) if stats == "summax" else None
-        _check(lib.yolosod_bias_act_stats(y.data_ptr(), yb, out.data_ptr(), ob, _dev(bias, "bias"),
+        _check(_launch(("bias_act", tuple(y.shape), stats), y.device, lib.yolosod_bias_act_stats, y.data_ptr(), yb, out.data_ptr(), ob, _dev(bias, "bias"),
                                           None if res is None else res.data_ptr(), rb, B, C, HW, int(act), parts, seg,
-                                          psum.data_ptr(), None if pmax is None else pmax.data_ptr(), _stream()),
+                                          psum.data_ptr(), None if pmax is None else pmax.data_ptr(), _stream(y.device)),
                "bias_act_stats")
         out._ys_plane_stats = PlaneStats(psum, pmax, parts, out.shape)
         return out
-    _check(lib.yolosod_bias_act(y.data_ptr(), yb, out.data_ptr(), ob, _dev(bias, "bias"),
-                                None if res is None else res.data_ptr(), rb, B, C, HW, int(act), _stream()),
+    _check(_launch(("bias_act", tuple(y.shape), None), y.device, lib.yolosod_bias_act, y.data_ptr(), yb, out.data_ptr(), ob, _dev(bias, "bias"),
+                                None if res is None else res.data_ptr(), rb, B, C, HW, int(act), _stream(y.device)),
            "bias_act")
     return out
 
@@ -512,18 +519,18 @@ def conv1x1_thin(x, w, bias, out=None, res=None, out2=None, c2lo=0, stats=None):
         psum = torch.empty(B * Cout * parts, dtype=torch.float32, device=x.device)
         pmax = torch.empty_like(psum) if stats == "summax" else None
         tws = torch.empty(2 * B * Cout * (HW // 64), dtype=torch.float32, device=x.device)
-        _check(lib.yolosod_conv1x1_thin_stats(x.data_ptr(), xb, _dev(w.contiguous(), "weight"), _dev(bias, "bias"),
+        _check(_launch(("conv1x1_thin", tuple(x.shape), (Cout, stats)), x.device, lib.yolosod_conv1x1_thin_stats, x.data_ptr(), xb, _dev(w.contiguous(), "weight"), _dev(bias, "bias"),
                                               out.data_ptr(), ob, B, Cin, Cout, HW, parts, psum.data_ptr(),
-                                              None if pmax is None else pmax.data_ptr(), tws.data_ptr(), _stream()),
+                                              None if pmax is None else pmax.data_ptr(), tws.data_ptr(), _stream(x.device)),
                "conv1x1_thin_stats")
         out._ys_plane_stats = PlaneStats(psum, pmax, parts, out.shape)
         return out
     if stats is not None:
         raise RuntimeError(f"conv1x1_thin: stats={stats!r} needs res=None and out2=None")
-    _check(lib.yolosod_conv1x1_thin(x.data_ptr(), xb, _dev(w.contiguous(), "weight"), _dev(bias, "bias"),
+    _check(_launch(("conv1x1_thin", tuple(x.shape), (Cout, res is not None, out2 is not None)), x.device, lib.yolosod_conv1x1_thin, x.data_ptr(), xb, _dev(w.contiguous(), "weight"), _dev(bias, "bias"),
                                     out.data_ptr(), ob, None if res is None else res.data_ptr(), rb,
                                     None if out2 is None else out2.data_ptr(), o2, int(c2lo), B, Cin, Cout, HW,
-                                    _stream()), "conv1x1_thin")
+                                    _stream(x.device)), "conv1x1_thin")
     return out
 
 
@@ -547,9 +554,9 @@ def conv1x1(x, w, bias, act, out=None, res=None):
     xb = bstride(x, "x", Cin)
     ob = bstride(out, "out", Cout)
     rb = bstride(res, "res", Cout) if res is not None else 0
-    _check(lib.yolosod_conv1x1(x.data_ptr(), xb, _dev(w, "weight"), None if bias is None else _dev(bias, "bias"),
+    _check(_launch(("conv1x1", tuple(x.shape), Cout), x.device, lib.yolosod_conv1x1, x.data_ptr(), xb, _dev(w, "weight"), None if bias is None else _dev(bias, "bias"),
                                out.data_ptr(), ob, None if res is None else res.data_ptr(), rb, B, Cin, Cout, HW,
-                               int(act), _stream()), "conv1x1")
+                               int(act), _stream(x.device)), "conv1x1")
     return out
 
 
@@ -559,9 +566,9 @@ def gemm_f32(A, B, b_kcontig, bias=None, bias_mode=0, act=0, res=None):
     M, K = A.shape
     N = B.shape[0] if b_kcontig else B.shape[1]
     C = torch.empty((M, N), dtype=torch.float32, device=A.device)
-    _check(lib.yolosod_gemm_f32(_dev(A, "A"), 0, K, _dev(B, "B"), 0, B.shape[1], int(b_kcontig), _dev(C, "C"), 0, N,
+    _check(_launch(("gemm", (M, N, K), None), A.device, lib.yolosod_gemm_f32, _dev(A, "A"), 0, K, _dev(B, "B"), 0, B.shape[1], int(b_kcontig), _dev(C, "C"), 0, N,
                                 M, N, K, 1, None if bias is None else _dev(bias, "bias"), bias_mode, act,
-                                None if res is None else _dev(res, "res"), _stream()), "gemm_f32")
+                                None if res is None else _dev(res, "res"), _stream(A.device)), "gemm_f32")
     return C
 
 
@@ -569,13 +576,13 @@ def layernorm(x, w, b, eps):
     lib = load_library()
     rows, C = x.shape
     y = torch.empty_like(x)
-    _check(lib.yolosod_layernorm(_dev(x, "x"), _dev(y, "y"), rows, C, _dev(w, "w"), _dev(b, "b"), float(eps),
-                                 _stream()), "layernorm")
+    _check(_launch(("layernorm", (rows, C), None), x.device, lib.yolosod_layernorm, _dev(x, "x"), _dev(y, "y"), rows, C, _dev(w, "w"), _dev(b, "b"), float(eps),
+                                 _stream(x.device)), "layernorm")
     return y
 
 
 def attention(qkv, n_seq, L, C, heads):
     lib = load_library()
     out = torch.empty((n_seq * L, C), dtype=torch.float32, device=qkv.device)
-    _check(lib.yolosod_attention(_dev(qkv, "qkv"), _dev(out, "out"), n_seq, L, C, heads, _stream()), "attention")
+    _check(_launch(("attention", (n_seq, L, C), heads), qkv.device, lib.yolosod_attention, _dev(qkv, "qkv"), _dev(out, "out"), n_seq, L, C, heads, _stream(qkv.device)), "attention")
     return out

@@ -29,7 +29,8 @@ namespace ys {
 
 constexpr int NMS_T = 512;  // threads per image workgroup
 constexpr int NMS_W = NMS_T / 64;
-constexpr int NMS_MAXDET = 1024;
+constexpr int NMS_MAXDET = 1024;     // kept lists up to this length live in LDS; longer ones in the workspace
+constexpr int NMS_MAXDET_BIG = 1 << 20;
 constexpr int KCAP = 2048;  // candidates covered by the multi-CU IoU bitmask
 constexpr int KW = KCAP / 64;
 
@@ -58,6 +59,9 @@ struct NmsArgs {
   float* out;                    // [B][max_det][6]
   int* counts;                   // [B]
   int* out_index;                // [B][max_det]  (anchor index)
+  int* kept_t;                   // [B][max_det] kept entries when max_det > NMS_MAXDET (else LDS), else nullptr
+  float4* kbox;                  // [B][max_det] kept class-offset boxes (fallback), idem
+  float* karea;                  // [B][max_det]
   unsigned long long* stamps;    // diagnostic only (YOLOSOD_NMS_STAMPS): [B][8] or nullptr
 };
 
@@ -499,11 +503,16 @@ __global__ __launch_bounds__(256) void nms_mask_kernel(NmsArgs g) {
 // -------------------------------------------------------------------------------------------------
 // nms_resolve: greedy over the prefix bitmask, then (rarely) the chunked fallback over the remainder
 // -------------------------------------------------------------------------------------------------
+// BIG: max_det > NMS_MAXDET (the reference has no cap, ops.py:297): the kept lists live in the workspace instead
+// of LDS (same algorithm; only a caller asking for more than 1024 detections per image pays for global accesses)
+template <bool BIG>
 __global__ __launch_bounds__(NMS_T) void nms_resolve_kernel(NmsArgs g) {
   const int b = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   __shared__ unsigned long long mrows[2][64][KW];
-  __shared__ int kept_t[NMS_MAXDET];  // kept entries: < KCAP -> prefix index, else KCAP + remainder index
+  __shared__ int kept_t_lds[BIG ? 1 : NMS_MAXDET];
+  // kept entries: < KCAP -> prefix index, else KCAP + remainder index
+  int* kept_t = BIG ? g.kept_t + (long)b * g.max_det : kept_t_lds;
   __shared__ int nkept_sh, done_sh;
   YS_NSTAMP(3)
   const int* mt = g.meta + 4 * b;
@@ -600,8 +609,10 @@ __global__ __launch_bounds__(NMS_T) void nms_resolve_kernel(NmsArgs g) {
   // (2) fallback: prefix exhausted, fewer than max_det kept, more candidates (keys >= T) within max_nms
   if (!done_sh && K < neff) {
     __shared__ SortShared sh;
-    __shared__ float4 kept_box[NMS_MAXDET];
-    __shared__ float kept_area[NMS_MAXDET];
+    __shared__ float4 kept_box_lds[BIG ? 1 : NMS_MAXDET];
+    __shared__ float kept_area_lds[BIG ? 1 : NMS_MAXDET];
+    float4* kept_box = BIG ? g.kbox + (long)b * g.max_det : kept_box_lds;
+    float* kept_area = BIG ? g.karea + (long)b * g.max_det : kept_area_lds;
     __shared__ float4 cb[NMS_T];
     __shared__ float ca[NMS_T];
     __shared__ int alive[NMS_T];
@@ -743,7 +754,7 @@ YS_EXPORT int yolosod_debug_nms_stage_cycles(double* out, int B) {
 
 static long nms_cap(int nc, int A, int multi_label) { return (long)A * (multi_label ? nc : 1); }
 
-YS_EXPORT size_t yolosod_nms_workspace(int B, int nc, int A, int multi_label) {
+YS_EXPORT size_t yolosod_nms_workspace_v2(int B, int nc, int A, int multi_label, int max_det) {
   const long cap = nms_cap(nc, A, multi_label);
   Sizer s;
   s.take<float4>((size_t)B * A);
@@ -755,7 +766,16 @@ YS_EXPORT size_t yolosod_nms_workspace(int B, int nc, int A, int multi_label) {
   s.take<unsigned long long>((size_t)B * KCAP * KW);
   s.take<int>((size_t)B * 4);
   s.take<int>((size_t)B * ((A + 255) / 256));
+  if (max_det > NMS_MAXDET) {
+    s.take<int>((size_t)B * max_det);
+    s.take<float4>((size_t)B * max_det);
+    s.take<float>((size_t)B * max_det);
+  }
   return s.off;
+}
+
+YS_EXPORT size_t yolosod_nms_workspace(int B, int nc, int A, int multi_label) {
+  return yolosod_nms_workspace_v2(B, nc, A, multi_label, NMS_MAXDET);
 }
 
 YS_EXPORT int yolosod_nms(float* pred, int B, int nc, int A, float conf_thres, double iou_thres, const int* classes,
@@ -764,7 +784,8 @@ YS_EXPORT int yolosod_nms(float* pred, int B, int nc, int A, float conf_thres, d
                           size_t workspace_bytes, void* stream) {
   YS_CHECK_ARG(pred && out && counts && out_index, "nms: null pointer");
   YS_CHECK_ARG(nc >= 1 && nc <= 64, "nms: nc=%d unsupported (1..64)", nc);
-  YS_CHECK_ARG(max_det >= 1 && max_det <= NMS_MAXDET, "nms: max_det=%d unsupported (1..%d)", max_det, NMS_MAXDET);
+  YS_CHECK_ARG(max_det >= 1 && max_det <= NMS_MAXDET_BIG, "nms: max_det=%d unsupported (1..%d)", max_det,
+               NMS_MAXDET_BIG);
   YS_CHECK_ARG(max_nms >= 0, "nms: bad max_nms");
   YS_CHECK_ARG((long)A * nc < (1L << 32), "nms: A*nc too large");
   if (B == 0) return 0;
@@ -799,7 +820,13 @@ YS_EXPORT int yolosod_nms(float* pred, int B, int nc, int A, float conf_thres, d
   g.meta = cv.take<int>((size_t)B * 4);
   const int nblk_a = (A + 255) / 256;
   g.blkcnt = cv.take<int>((size_t)B * nblk_a);
-  YS_CHECK_ARG(g.blkcnt, "nms: workspace too small (%zu)", workspace_bytes);
+  const bool big = max_det > NMS_MAXDET;
+  if (big) {
+    g.kept_t = cv.take<int>((size_t)B * max_det);
+    g.kbox = cv.take<float4>((size_t)B * max_det);
+    g.karea = cv.take<float>((size_t)B * max_det);
+  }
+  YS_CHECK_ARG(g.blkcnt && (!big || g.karea), "nms: workspace too small (%zu)", workspace_bytes);
   g.cap = cap;
   g.out = out;
   g.counts = counts;
@@ -824,7 +851,10 @@ YS_EXPORT int yolosod_nms(float* pred, int B, int nc, int A, float conf_thres, d
   if (A > 0) hipLaunchKernelGGL(nms_scatter_kernel, dim3(nblk_a, B), dim3(256), 0, st, g);
   hipLaunchKernelGGL(nms_select_kernel, dim3(B), dim3(NMS_T), 0, st, g);
   hipLaunchKernelGGL(nms_mask_kernel, dim3(KW, B), dim3(256), 0, st, g);
-  hipLaunchKernelGGL(nms_resolve_kernel, dim3(B), dim3(NMS_T), 0, st, g);
+  if (big)
+    hipLaunchKernelGGL(nms_resolve_kernel<true>, dim3(B), dim3(NMS_T), 0, st, g);
+  else
+    hipLaunchKernelGGL(nms_resolve_kernel<false>, dim3(B), dim3(NMS_T), 0, st, g);
   YS_CHECK_LAUNCH("nms");
   return 0;
 }

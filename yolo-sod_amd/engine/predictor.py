@@ -75,3 +75,36 @@ def gather_detections(out: torch.Tensor, counts: torch.Tensor, group=None):
     dist.all_gather_into_tensor(g_out, out.contiguous(), group=group)
     dist.all_gather_into_tensor(g_cnt, counts.contiguous(), group=group)
     return g_out, g_cnt
+
+
+def sharded_predict(predict_padded, n_images: int, images, group=None):
+    """Data-parallel inference over ``n_images`` global images, one process per GPU.
+
+    ``images(lo, hi)`` returns this rank's shard (global images [lo, hi), ``shard_bounds``) - each rank
+    materialises only its own images; ``predict_padded(x) -> (out [b, D, 6], counts [b], ...)`` is the rank-local
+    path (``DetectionPredictor.predict_padded``). Shards are padded to the largest shard (count 0) so one
+    fixed-size all-gather serves uneven splits. Returns (out [n_images, D, 6], counts [n_images]) in global image
+    order on every rank."""
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    lo, hi = shard_bounds(n_images, rank, world)
+    out, counts = predict_padded(images(lo, hi))[:2]
+    smax = -(-n_images // world)
+    if out.shape[0] < smax:
+        pad = smax - out.shape[0]
+        out = torch.cat([out, out.new_zeros((pad, *out.shape[1:]))])
+        counts = torch.cat([counts, counts.new_zeros((pad,))])
+    g_out, g_cnt = gather_detections(out, counts, group)
+    if n_images % world:
+        keep = torch.cat([torch.arange(r * smax, r * smax + (b - a)) for r in range(world)
+                          for a, b in [shard_bounds(n_images, r, world)]])
+        g_out, g_cnt = g_out[keep.to(g_out.device)], g_cnt[keep.to(g_cnt.device)]
+    return g_out, g_cnt
+
+
+def seeded_images(lo: int, hi: int, imgsz: int, seed: int = 1000, device=None) -> torch.Tensor:
+    """Synthetic input batch of global images [lo, hi): image i = torch.rand(3, imgsz, imgsz) from a generator
+    seeded ``seed + i``, so every rank's shard is a slice of one global batch whatever the world size."""
+    x = torch.empty((hi - lo, 3, imgsz, imgsz))
+    for k, i in enumerate(range(lo, hi)):
+        x[k] = torch.rand(3, imgsz, imgsz, generator=torch.Generator().manual_seed(seed + i))
+    return x if device is None else x.to(device)

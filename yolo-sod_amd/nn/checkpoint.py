@@ -149,7 +149,8 @@ def attempt_load_one_weight(weight, device="cuda", fuse: bool = True, registry=N
 @contextlib.contextmanager
 def _ref_modules_registered():
     """Make the reference class paths importable for pickle's save-side lookup (stub classes only)."""
-    added = []
+    added, prior = [], []
+    absent = object()
     for q in set(REF_CLASS_PATH.values()):
         mod, _, name = q.rpartition(".")
         parts = mod.split(".")
@@ -158,10 +159,18 @@ def _ref_modules_registered():
             if pm not in sys.modules:
                 sys.modules[pm] = types.ModuleType(pm)
                 added.append(pm)
+        # a real (already imported) reference module keeps its class: remember it and put it back afterwards
+        prior.append((sys.modules[mod], name, getattr(sys.modules[mod], name, absent)))
         setattr(sys.modules[mod], name, _stub_class(q))
     try:
         yield
     finally:
+        for m, name, old in reversed(prior):
+            if old is absent:
+                with contextlib.suppress(AttributeError):
+                    delattr(m, name)
+            else:
+                setattr(m, name, old)
         for pm in added:
             sys.modules.pop(pm, None)
 

@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import math
 import os
+from collections.abc import Sequence
 
 import torch
 import torch.nn as nn
@@ -532,9 +533,10 @@ class Detect(nn.Module):
                 for x in ch))
         self.dfl = DFL(self.reg_max) if self.reg_max > 1 else nn.Identity()
 
-    # Return the raw [B, 64+nc, Hi, Wi] maps as the reference does (forward's second output, head.py:70-74). When
-    # False (default), GPU inference runs the fused head tail + decode (one HIP kernel, no raw maps in HBM) and the
-    # second output is the list of tower features instead; predictors and NMS only read the first output.
+    # GPU inference runs the fused head tail + decode (one HIP kernel; the [B, 64+nc, Hi, Wi] raw maps are never
+    # written). The second output keeps the reference's meaning (head.py:70-74: the raw maps) as a RawMaps
+    # sequence that computes them from the kept tower features on first access. keep_raw = True runs the
+    # unfused reference-shaped path instead (raw maps materialised, second output a plain list).
     keep_raw = False
 
     def forward(self, x):
@@ -577,22 +579,26 @@ class Detect(nn.Module):
         y = _hip.detect_head(fb, fc, [w(b[-1]) for b in self.cv2], [b[-1].bias.detach() for b in self.cv2],
                              [w(b[-1]) for b in self.cv3], [b[-1].bias.detach() for b in self.cv3],
                              [float(s) for s in self.stride], self.nc, self.reg_max)
-        return y, fb + fc
+        return y, RawMaps(self, fb, fc)
+
+    def raw_from_features(self, i, h2, h3):
+        """Level i's raw map torch.cat((cv2[i](x), cv3[i](x)), 1) (head.py:70) from its tower features: on GPU the
+        two final 1x1 convs write their slices of the [B, 4*reg_max+nc, H, W] map directly (bias in the HIP
+        epilogue)."""
+        b2, b3 = self.cv2[i], self.cv3[i]
+        B, _, H, W = h2.shape
+        if h2.device.type == "cuda" and (H * W) % 4 == 0 and b2[-1].bias is not None and b3[-1].bias is not None:
+            z = torch.empty((B, self.no, H, W), dtype=h2.dtype, device=h2.device)
+            conv_epilogue(b2[-1], 0, h2, out=z[:, : 4 * self.reg_max])
+            conv_epilogue(b3[-1], 0, h3, out=z[:, 4 * self.reg_max:])
+            return z
+        return torch.cat((b2[-1](h2), b3[-1](h3)), 1)
 
     def _tower(self, i, xi):
-        """torch.cat((cv2[i](x), cv3[i](x)), 1) (head.py:70); on GPU the two final 1x1 convs write their slices of
-        the [B, 4*reg_max+nc, H, W] map directly (bias in the HIP epilogue)."""
+        """torch.cat((cv2[i](x), cv3[i](x)), 1) (head.py:70)."""
         b2, b3 = self.cv2[i], self.cv3[i]
-        if xi.device.type == "cuda" and not self.training and b2[-1].bias is not None and b3[-1].bias is not None:
-            h2 = b2[:-1](xi)
-            h3 = b3[:-1](xi)
-            B, _, H, W = h2.shape
-            if (H * W) % 4 == 0:
-                z = torch.empty((B, self.no, H, W), dtype=h2.dtype, device=h2.device)
-                conv_epilogue(b2[-1], 0, h2, out=z[:, : 4 * self.reg_max])
-                conv_epilogue(b3[-1], 0, h3, out=z[:, 4 * self.reg_max:])
-                return z
-            return torch.cat((b2[-1](h2), b3[-1](h3)), 1)
+        if xi.device.type == "cuda" and not self.training:
+            return self.raw_from_features(i, b2[:-1](xi), b3[:-1](xi))
         return torch.cat((b2(xi), b3(xi)), 1)
 
     def _inference(self, x):
@@ -606,3 +612,36 @@ class Detect(nn.Module):
         for a, b, s in zip(self.cv2, self.cv3, self.stride):
             a[-1].bias.data[:] = 1.0
             b[-1].bias.data[: self.nc] = math.log(5 / self.nc / (640 / s) ** 2)
+
+
+class RawMaps(Sequence):
+    """Second output of the fused Detect forward: the reference's list of raw [B, 4*reg_max+nc, Hi, Wi] maps
+    (head.py:70-74), computed from the kept tower features on first access (``raw_from_features``) - the fused
+    kernel never writes them, and callers that only read ``preds[0]`` (NMS, ops.py:219-220) never pay for them.
+    Indexing / iteration / ``len`` / ``list(...)`` give the reference's tensors; ``features`` holds the
+    (box, class) tower features per level; ``materialize()`` returns the plain list."""
+
+    __slots__ = ("_det", "features", "_maps")
+
+    def __init__(self, det, fb, fc):
+        self._det = det
+        self.features = list(zip(fb, fc))
+        self._maps = None
+
+    def materialize(self) -> list:
+        if self._maps is None:
+            self._maps = [self._det.raw_from_features(i, b, c) for i, (b, c) in enumerate(self.features)]
+        return self._maps
+
+    def __getitem__(self, i):
+        return self.materialize()[i]
+
+    def __len__(self):
+        return len(self.features)
+
+    def __iter__(self):
+        return iter(self.materialize())
+
+    def __repr__(self):
+        state = "materialised" if self._maps is not None else "lazy"
+        return f"RawMaps({len(self)} levels, {state})"

@@ -12,6 +12,10 @@ PEAK_HBM_GBS = 8000.0
 PEAK_FP32_MFMA_TFLOPS = 157.3
 
 
+# operators of the SURVEY 8(a) path (rooflined); other keys the op_timer records are backbone conv kernels
+PATH_OPS = frozenset({"se", "cbam", "ca", "a2", "swin", "mamba", "decode", "head", "nms"})
+
+
 def swin_geom(H, W, ws=7):
     if H <= ws and W <= ws:
         return H, W, H, W

@@ -61,7 +61,12 @@ def scale_boxes(img1_shape, boxes, img0_shape, ratio_pad=None, padding=True, xyw
         if not xywh:
             boxes[..., 2] -= pad[0]
             boxes[..., 3] -= pad[1]
-    boxes[..., :4] /= gain
+    if boxes.device.type == "cuda":
+        # a Python-scalar divisor would run as a multiply by its reciprocal on the GPU (not bit-equal to the
+        # reference's CPU division): divide by a device tensor instead
+        boxes[..., :4] /= torch.full((), gain, dtype=boxes.dtype, device=boxes.device)
+    else:
+        boxes[..., :4] /= gain
     return clip_boxes(boxes, img0_shape)
 
 
