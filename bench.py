@@ -34,12 +34,14 @@ from yolosod_amd.nn.tasks import build_model  # noqa: E402
 
 METRIC = "images/sec @640×640 bs=32, 1→8 MI355X; mAP@0.5:0.95 parity vs CPU ref"
 CONFIGS = {
-    # name: (yaml, imgsz, batch per GPU, label) - BASELINE.json configs[1..4]; n640 is the metric's workload
-    "n640": ("yolov12-sod-fusion-v5-simple.yaml", 640, 32, "yolov12n-sod (paper YAML)"),
-    "n1280": ("yolov12-sod-fusion-v5-simple.yaml", 1280, 8, "yolov12n-sod (paper YAML)"),
-    # configs[4] names bf16; this build's m-scale path is fp32 end to end, so it is measured in fp32
-    "m640": ("yolov12m-sod.yaml", 640, 64, "yolov12m-sod (paper graph at v12 m scale)"),
+    # name: (yaml, imgsz, batch per GPU, label, dtype) - BASELINE.json configs[1..4]; n640 is the metric's workload
+    "n640": ("yolov12-sod-fusion-v5-simple.yaml", 640, 32, "yolov12n-sod (paper YAML)", torch.float32),
+    "n1280": ("yolov12-sod-fusion-v5-simple.yaml", 1280, 8, "yolov12n-sod (paper YAML)", torch.float32),
+    # configs[4]: bf16 model (parameters + activations bf16, fp32 accumulation; decode / NMS fp32), DESIGN.md 9
+    "m640": ("yolov12m-sod.yaml", 640, 64, "yolov12m-sod (paper graph at v12 m scale)", torch.bfloat16),
+    "m640f32": ("yolov12m-sod.yaml", 640, 64, "yolov12m-sod (paper graph at v12 m scale)", torch.float32),
 }
+DTYPE_NAME = {torch.float32: "f32", torch.bfloat16: "bf16"}
 
 
 def log(*a):
@@ -81,7 +83,7 @@ def _median(v):
     return v[len(v) // 2] if len(v) % 2 else 0.5 * (v[len(v) // 2 - 1] + v[len(v) // 2])
 
 
-def cpu_baseline(cfg_yaml, imgsz, warmup=2, iters=5, batch_all=8):
+def cpu_baseline(cfg_yaml, imgsz, warmup=2, iters=5, batch_all=8, single=True):
     """the oracle CPU model (fp32 PyTorch-CPU restatement + C NMS, pinned to the reference
     by tests/golden) on this host's cores. All usable physical cores on a bounded sample of the workload
     (``batch_all`` images of the same 640x640 batch per iteration) and 1 thread on BASELINE configs[0] (one
@@ -142,7 +144,7 @@ def cpu_baseline(cfg_yaml, imgsz, warmup=2, iters=5, batch_all=8):
 
     t_start = time.perf_counter()
     all_cores = run(cores, batch_all)
-    one = run(1, 1)
+    one = run(1, 1) if single else None
     # NMS alone, loaded: oracle NMS per image on the same synthetic tensors bench.py times on the GPU
     nms = {}
     for n_cand in NMS_LOADS:
@@ -245,13 +247,15 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    cfg_yaml, imgsz, bs, label = CONFIGS[args.config]
-    model = build_model(cfg_yaml, seed=0, device=dev)
+    cfg_yaml, imgsz, bs, label, dtype = CONFIGS[args.config]
+    dname = DTYPE_NAME[dtype]
+    model = build_model(cfg_yaml, seed=0, device=dev, dtype=dtype)
     predictor = DetectionPredictor(model, conf=args.conf, iou=0.7, max_det=300)
-    # one global seeded batch of world * bs images (image i from seed 1000 + i); each rank holds its shard
+    # one global seeded batch of world * bs images (image i from seed 1000 + i); each rank holds its shard, resident
+    # in HBM in the model's dtype before the timed region (the predictor's .to(dtype) is then a no-op)
     n_global = world * bs
     lo, hi = shard_bounds(n_global, rank, world)
-    x = seeded_images(lo, hi, imgsz, device=dev)
+    x = seeded_images(lo, hi, imgsz, device=dev).to(dtype)
 
     def step():
         if world > 1:  # shard -> rank-local predict -> all-gather of the padded detections (global image order)
@@ -295,15 +299,15 @@ def main():
             continue
         nbytes, flops = perf.op_cost(key)
         avg = tot / n
-        ops.append({"op": key[0], "shape": list(key[1]), "launches": n, "avg_ms": round(avg, 4),
-                    "total_ms_per_step": round(tot / args.steps, 4),
+        ops.append({"op": key[0], "shape": list(key[1]), "dtype": "bf16" if perf.elem_size(key) == 2 else "f32",
+                    "launches": n, "avg_ms": round(avg, 4), "total_ms_per_step": round(tot / args.steps, 4),
                     "GBps": round(nbytes / (avg * 1e-3) / 1e9, 1),
-                    "TFLOPs": round(flops / (avg * 1e-3) / 1e12, 2), "bytes": nbytes, "flops": flops})
+                    "TFLOPs": round(flops / (avg * 1e-3) / 1e12, 2), "bytes": nbytes, "flops": flops, "key": key})
     ops.sort(key=lambda o: -o["total_ms_per_step"])
     dom = ops[0]
-    bound = perf.bound_of(dom["op"])
+    bound = perf.bound_of(dom["key"])
     if bound == "mfma":
-        achieved, peak, unit = dom["TFLOPs"], perf.PEAK_FP32_MFMA_TFLOPS, "TFLOP/s"
+        achieved, peak, unit = dom["TFLOPs"], perf.peak_tflops(dom["key"]), "TFLOP/s"
     else:
         achieved, peak, unit = dom["GBps"], perf.PEAK_HBM_GBS, "GB/s"
     traffic = load_traffic()
@@ -314,13 +318,13 @@ def main():
                 "algorithmic_per_launch": dom["flops"] if bound == "mfma" else dom["bytes"]}
 
     # path-level roofline = sum_k t_k^min / sum_k t_k^meas over every hot-path operator,
-    # t_k^min = max(bytes_k / HBM peak, flops_k / fp32 MFMA peak)
-    t_min = sum(max(o["bytes"] / (perf.PEAK_HBM_GBS * 1e9), o["flops"] / (perf.PEAK_FP32_MFMA_TFLOPS * 1e12))
-                * 1e3 * o["launches"] / args.steps for o in ops)
+    # t_k^min = max(bytes_k / HBM peak, flops_k / matrix-core peak of the op's dtype)
+    t_min = sum(perf.t_min_ms(o["key"]) * o["launches"] / args.steps for o in ops)
     t_meas = sum(o["total_ms_per_step"] for o in ops)
     path_roofline = {"t_min_ms": round(t_min, 4), "t_meas_ms": round(t_meas, 4),
                      "frac": round(t_min / t_meas, 4) if t_meas else None,
-                     "definition": "sum over hot-path ops of max(bytes/8 TB/s, flops/157.3 TF/s) / measured"}
+                     "definition": "sum over hot-path ops of max(bytes/8 TB/s, flops/MFMA peak of the op dtype "
+                                   "(fp32 157.3, bf16 2516.6 TF/s)) / measured"}
 
     total_imgs = world * bs * args.steps
     value = total_imgs / elapsed
@@ -328,15 +332,15 @@ def main():
     result = {
         "metric": METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "scaling": "weak", "vs_baseline": None, "dtype": dname,
         "data": f"synthetic: torch.rand images in HBM, seed-0 random-init weights of {label}",
-        "config": {"workload": f"{label} {imgsz}x{imgsz}, {bs} images per GPU, fused fp32 "
+        "config": {"workload": f"{label} {imgsz}x{imgsz}, {bs} images per GPU, fused {dname} "
                                f"forward + decode + NMS(conf={args.conf}, iou=0.7)",
                    "imgsz": imgsz, "batch_per_gpu": bs, "global_batch": bs * world, "parallelism": f"dp{world}"},
         "roofline": roofline,
         "path_roofline": path_roofline,
         "hip_ops_ms_per_step": round(hip_ms, 3),
-        "hip_ops": [{k: v for k, v in o.items() if k not in ("bytes", "flops")} for o in ops],
+        "hip_ops": [{k: v for k, v in o.items() if k not in ("bytes", "flops", "key")} for o in ops],
         "backbone_hip_ms_per_step": round(sum(o["total_ms_per_step"] for o in backbone), 3),
         "backbone_hip_ops": sorted(backbone, key=lambda o: -o["total_ms_per_step"])[:12],
         "nms_loaded": None,
@@ -346,7 +350,10 @@ def main():
         result["nms_loaded"] = nms_loaded(dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            result["cpu_baseline"] = cpu_baseline(cfg_yaml, imgsz)
+            # m scale: ~4x the n model's CPU work per image - a smaller sample keeps the same ~10-30 s budget
+            m_scale = cfg_yaml.startswith("yolov12m")
+            result["cpu_baseline"] = cpu_baseline(cfg_yaml, imgsz, batch_all=2 if m_scale else 8,
+                                                  single=not m_scale)
         except Exception as e:  # report, never hide
             result["cpu_baseline"] = {"error": repr(e)}
     if world > 1:

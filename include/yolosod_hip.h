@@ -186,6 +186,70 @@ int yolosod_attention(const float* qkv, float* out, long n_seq, int L, int C, in
  * mlp 2C) through it (default, or env YOLOSOD_SWIN_FUSED), 0 forces the decomposed GEMM path for every shape. */
 void yolosod_debug_set_swin_fused(int on);
 
+/* ---------------------------------------------------------------------------------------------------------------
+ * bf16 model config (BASELINE configs[4]): `model.to(torch.bfloat16)` after fuse() - AutoBackend's fp16
+ * route (autobackend.py:145-156, predictor im.half()) with bfloat16. Activations (x, y, res, out2, tower features)
+ * and the GEMM weights of Swin / A2 are bf16 bit patterns (uint16_t, torch.bfloat16 layout); every other parameter,
+ * the statistics / partials and Detect's output are fp32. Arithmetic is fp32 (bf16 MFMA with fp32 accumulation for
+ * the GEMMs and attention); each stored tensor is rounded once (nearest even). Same argument meaning and workspace
+ * queries as the fp32 entry points above unless noted.
+ * ------------------------------------------------------------------------------------------------------------- */
+#include <stdint.h>
+
+/* SE (smallobj_modules.py:84-92); psum = producer partials (yolosod_bias_act_stats_bf16) or NULL. */
+int yolosod_se_forward_bf16(const uint16_t* x, uint16_t* y, int B, int C, int H, int W, const float* fc1_w,
+                            const float* fc1_b, const float* fc2_w, const float* fc2_b, int hidden, const float* psum,
+                            void* workspace, size_t workspace_bytes, void* stream);
+/* CBAM (cbam_block.py:52-55); psum / pmax both NULL or both the producer's partials. */
+int yolosod_cbam_forward_bf16(const uint16_t* x, uint16_t* y, int B, int C, int H, int W, const float* fc0_w,
+                              const float* fc2_w, int hidden, const float* sa_w, const float* psum, const float* pmax,
+                              void* workspace, size_t workspace_bytes, void* stream);
+/* CA (ca_block.py:38-59); yin = producer's pooled means (yolosod_bias_act_capool_bf16) or NULL. */
+int yolosod_ca_forward_bf16(const uint16_t* x, uint16_t* y, int B, int C, int H, int W, const float* conv1_w,
+                            const float* conv1_b, int mip, const float* bn_w, const float* bn_b, const float* bn_mean,
+                            const float* bn_var, float bn_eps, const float* convh_w, const float* convh_b,
+                            const float* convw_w, const float* convw_b, const float* yin, void* workspace,
+                            size_t workspace_bytes, void* stream);
+/* SwinBlock.forward (blocks_transformer.py:150-171): in_proj_w [3C][C], out_proj_w [C][C], mlp1_w [hid][C],
+ * mlp2_w [C][hid], pw_w [C][C] bf16; C % 64 == 0, head dim 32 / 64 / 128. */
+size_t yolosod_swin_workspace_bf16(int B, int C, int H, int W, int num_heads, int window, int mlp_hidden);
+int yolosod_swin_forward_bf16(const uint16_t* x, uint16_t* y, int B, int C, int H, int W, int num_heads, int window,
+                              const float* dw_w, const float* ln1_w, const float* ln1_b, float ln1_eps,
+                              const uint16_t* in_proj_w, const float* in_proj_b, const uint16_t* out_proj_w,
+                              const float* out_proj_b, const float* ln2_w, const float* ln2_b, float ln2_eps,
+                              const uint16_t* mlp1_w, const float* mlp1_b, int mlp_hidden, const uint16_t* mlp2_w,
+                              const float* mlp2_b, const uint16_t* pw_w, const float* bn_w, const float* bn_b,
+                              const float* bn_mean, const float* bn_var, float bn_eps, void* workspace,
+                              size_t workspace_bytes, void* stream);
+/* A2_Attn.forward (a2_attn.py:35-69), residual form, pre-multiplied output weights (oproj_w = Wconv . Wmha,
+ * oproj_b = Wconv . bmha + bconv); proj_w / in_proj_w / oproj_w bf16; head dim 32 / 64 / 128, H*W % 8 == 0. */
+size_t yolosod_a2_workspace_bf16(int B, int C, int H, int W, int num_areas);
+int yolosod_a2_forward_bf16(const uint16_t* x, uint16_t* y, int B, int C, int H, int W, int num_areas, int num_heads,
+                            const uint16_t* proj_w, const float* proj_b, const float* ln_w, const float* ln_b,
+                            float ln_eps, const uint16_t* in_proj_w, const float* in_proj_b, const uint16_t* oproj_w,
+                            const float* oproj_b, void* workspace, size_t workspace_bytes, void* stream);
+/* Detect head tail + decode (as yolosod_detect_head) on bf16 tower features; weights, biases and y fp32. */
+int yolosod_detect_head_bf16(int nl, const uint16_t* const* box_feat, const uint16_t* const* cls_feat, int c2, int c3,
+                             const float* const* box_w, const float* const* box_b, const float* const* cls_w,
+                             const float* const* cls_b, const int* heights, const int* widths, const float* strides,
+                             int B, int nc, int reg_max, float* y, void* stream);
+/* Conv epilogues on bf16 maps (yolosod_bias_act / _dual / _stats / _capool); out2 NULL = no second store. The
+ * statistics are fp32 sums / maxes / means of the stored (rounded) values. */
+int yolosod_bias_act_bf16(const uint16_t* y, long y_bstride, uint16_t* out, long out_bstride, const float* bias,
+                          const uint16_t* res, long res_bstride, uint16_t* out2, long out2_bstride, int c2lo, int B,
+                          int C, long HW, int act, void* stream);
+int yolosod_bias_act_stats_bf16(const uint16_t* y, long y_bstride, uint16_t* out, long out_bstride, const float* bias,
+                                const uint16_t* res, long res_bstride, int B, int C, long HW, int act, int parts,
+                                long seg, float* psum, float* pmax, void* stream);
+int yolosod_bias_act_capool_bf16(const uint16_t* y, long y_bstride, uint16_t* out, long out_bstride,
+                                 const float* bias, const uint16_t* res, long res_bstride, int B, int C, int H, int W,
+                                 int act, float* yin, void* stream);
+/* Test hooks: bf16 GEMM (bf16 out, fp32 accumulation; K % 64 == 0) and attention over contiguous sequences. */
+int yolosod_gemm_bf16(const uint16_t* A, long a_bs, int lda, const uint16_t* B, long b_bs, int ldb, int b_kcontig,
+                      uint16_t* C, long c_bs, int ldc, int M, int N, int K, int batch, const float* bias,
+                      int bias_mode, int act, const uint16_t* res, void* stream);
+int yolosod_attention_bf16(const uint16_t* qkv, uint16_t* out, long n_seq, int L, int C, int heads, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,230 @@
+"""GPU parity of the bf16 config (BASELINE configs[4]: yolov12m-sod in bf16).
+
+bf16 semantics (build-defined; the reference has no bf16 path): ``model.to(torch.bfloat16)`` after fuse() -
+AutoBackend's fp16 route (autobackend.py:145-156, predictor ``im.half()``) with bfloat16 - so parameters and every
+activation in HBM are bf16; each HIP operator reads bf16, accumulates in fp32 (bf16 MFMA for the Swin / A2
+GEMMs and attention, fp32 for reductions, LayerNorm, softmax, gates) and rounds once per stored tensor; Detect's
+decode and NMS stay fp32.
+
+Oracle: the fp32 restatement (oracle/) evaluated in float64 on the SAME bf16 values - parameters and inputs
+rounded to bf16 first - so the measured difference is only this build's internal bf16 roundings. Tolerances
+(stated in DESIGN.md section 9, measured margins in profiles/r02_bf16_margins.txt):
+  * single-rounding ops (SE, CBAM, CA, conv epilogues): |d| <= 2^-7 |ref| + 1e-6 max|ref| (one bf16 rounding of
+    the output is <= 2^-8 |ref|, bf16's unit roundoff; measured ratios 0.98-0.995 of 2^-8);
+  * GEMM / attention: |d| <= 2^-7 |ref| + 2^-8 max|ref| (products of bf16 values accumulated in fp32, output
+    rounded; attention also rounds P);
+  * Swin / A2 (5-7 stored bf16 intermediates): max|d| <= BF16_BLOCK_REL max|ref| and mean|d| <= 1e-2 mean|ref|
+    (measured: max 0.005-0.009, mean 0.0047-0.005).
+"""
+import numpy as np
+import pytest
+import torch
+
+import recipes
+from oplib import build_fixture_module
+from oracle.model_ref import OP_CLASSES
+
+pytestmark = pytest.mark.gpu
+BF = torch.bfloat16
+BF16_BLOCK_REL = 2.5e-2
+
+
+def _log(msg):
+    import os
+    p = os.environ.get("YOLOSOD_PARITY_LOG")
+    if p:
+        with open(p, "a") as f:
+            f.write(f"{os.environ.get('PYTEST_CURRENT_TEST', '?')}: {msg}\n")
+
+
+def _bf16_oracle(name, x):
+    m, _ = build_fixture_module(name, OP_CLASSES)
+    m = m.to(BF).double()
+    with torch.inference_mode():
+        return m(x.to(BF).double())
+
+
+def _gpu_bf16(name, x, cuda):
+    m, _ = build_fixture_module(name)
+    m = m.to(cuda).to(BF)
+    with torch.inference_mode():
+        y = m(x.to(cuda).to(BF))
+    assert y.dtype == BF
+    return y.double().cpu()
+
+
+SINGLE = [n for n in recipes.OPS if n.split("_")[0] in ("se", "cbam", "ca")]
+BLOCK = [n for n in recipes.OPS if n.startswith("swin") or n in ("a2_c128_h16", "a2_c512_h20")]
+
+
+@pytest.mark.parametrize("name", SINGLE)
+def test_bf16_channel_ops_vs_oracle(name, cuda):
+    op, args, shape = recipes.OPS[name]
+    x = recipes.make_input(name, shape)
+    y = _gpu_bf16(name, x, cuda)
+    ref = _bf16_oracle(name, x)
+    d = (y - ref).abs()
+    lim = 2.0 ** -7 * ref.abs() + 1e-6 * float(ref.abs().max())
+    _log(f"max|d| {float(d.max()):.3g} ratio {float((d / lim).max()):.3f}")
+    assert bool((d <= lim).all()), f"{name}: max|d| {float(d.max()):.3g}, worst ratio {float((d / lim).max()):.2f}"
+
+
+def _block_check(name, y, ref):
+    d = (y - ref).abs()
+    mx, mean = float(d.max()) / float(ref.abs().max()), float(d.mean()) / float(ref.abs().mean())
+    _log(f"max|d|/max|ref| {mx:.3g} mean|d|/mean|ref| {mean:.3g}")
+    assert mx <= BF16_BLOCK_REL and mean <= 1e-2, f"{name}: max rel {mx:.3g}, mean rel {mean:.3g}"
+
+
+@pytest.mark.parametrize("name", BLOCK)
+def test_bf16_transformer_ops_vs_oracle(name, cuda):
+    op, args, shape = recipes.OPS[name]
+    x = recipes.make_input(name, shape)
+    _block_check(name, _gpu_bf16(name, x, cuda), _bf16_oracle(name, x))
+
+
+# m-scale shapes of the bf16 config (one or two images)
+REAL_M = {
+    "se_L1_m": ("SE_Block", (64,), (1, 64, 320, 320)),
+    "cbam_L4_m": ("CBAM_Block", (128, 128, 16), (1, 128, 160, 160)),
+    "swin_L9_m": ("SwinBlock", (512, 4, 7), (2, 512, 40, 40)),
+    "a2_L12_m": ("A2_Attn", (512, None, 8, 8), (2, 512, 20, 20)),
+    "cbam_L18_m": ("CBAM_Block", (512, 512, 16), (2, 512, 40, 40)),
+    "se_L23_m": ("SE_Block", (256,), (2, 256, 80, 80)),
+    "swin_L28_m": ("SwinBlock", (128, 2, 7), (1, 128, 160, 160)),
+    "ca_L32_m": ("CA_Block", (256, 256, 32), (2, 256, 80, 80)),
+}
+
+
+@pytest.mark.parametrize("name", list(REAL_M))
+def test_bf16_m_scale_shapes_vs_oracle(name, cuda, monkeypatch):
+    monkeypatch.setitem(recipes.OPS, name, REAL_M[name])
+    x = recipes.make_input(name, REAL_M[name][2])
+    y = _gpu_bf16(name, x, cuda)
+    ref = _bf16_oracle(name, x)
+    if REAL_M[name][0] in ("SwinBlock", "A2_Attn"):
+        _block_check(name, y, ref)
+    else:
+        d = (y - ref).abs()
+        lim = 2.0 ** -7 * ref.abs() + 1e-6 * float(ref.abs().max())
+        _log(f"max|d| {float(d.max()):.3g} ratio {float((d / lim).max()):.3f}")
+        assert bool((d <= lim).all()), f"{name}: worst ratio {float((d / lim).max()):.2f}"
+
+
+@pytest.mark.parametrize("M_,N,K,bkc", [(300, 192, 64, True), (1000, 64, 128, True), (129, 768, 256, True),
+                                         (512, 400, 512, False), (64, 1600, 64, False), (130, 136, 64, False)])
+def test_gemm_bf16(M_, N, K, bkc, cuda):
+    from yolosod_amd import _hip
+    g = torch.Generator().manual_seed(M_ * 7 + N)
+    A = torch.randn(M_, K, generator=g).to(BF)
+    B = (torch.randn(N, K, generator=g) if bkc else torch.randn(K, N, generator=g)).to(BF)
+    bias = torch.randn(N, generator=g)
+    res = torch.randn(M_, N, generator=g).to(BF)
+    C = _hip.gemm_bf16(A.to(cuda), B.to(cuda), bkc, bias.to(cuda), 2, 1, res.to(cuda)).double().cpu()
+    Bm = B.double() if not bkc else B.double().t()
+    ref = torch.nn.functional.silu(A.double() @ Bm + bias.double()) + res.double()
+    d = (C - ref).abs()
+    lim = 2.0 ** -7 * ref.abs() + 2.0 ** -8 * float(ref.abs().max())
+    assert bool((d <= lim).all()), f"max|d| {float(d.max()):.3g}"
+
+
+@pytest.mark.parametrize("n_seq,L,C,heads", [(3, 49, 128, 2), (2, 160, 512, 8), (4, 49, 512, 4), (2, 30, 64, 2)])
+def test_attention_bf16(n_seq, L, C, heads, cuda):
+    from yolosod_amd import _hip
+    g = torch.Generator().manual_seed(L * 13 + C)
+    qkv = (torch.randn(n_seq * L, 3 * C, generator=g) * 1.5).to(BF)
+    out = _hip.attention_bf16(qkv.to(cuda), n_seq, L, C, heads).double().cpu()
+    hd = C // heads
+    q, k, v = qkv.double().view(n_seq, L, 3, heads, hd).permute(2, 0, 3, 1, 4)
+    p = torch.softmax(q @ k.transpose(-1, -2) / hd ** 0.5, -1)
+    ref = (p @ v).permute(0, 2, 1, 3).reshape(n_seq * L, C)
+    d = (out - ref).abs()
+    lim = 2.0 ** -7 * ref.abs() + 2.0 ** -8 * float(ref.abs().max())
+    assert bool((d <= lim).all()), f"max|d| {float(d.max()):.3g}"
+
+
+@pytest.mark.parametrize("stats", [None, "sum", "summax", "capool", "dual"])
+def test_bias_act_bf16(stats, cuda):
+    from yolosod_amd import _hip
+    g = torch.Generator().manual_seed(5)
+    B, C, H, W = 3, 24, 20, 16
+    y = torch.randn(B, C, H, W, generator=g).to(BF)
+    bias = torch.randn(C, generator=g)
+    res = torch.randn(B, C, H, W, generator=g).to(BF)
+    ref = (torch.nn.functional.silu(y.double() + bias.double().view(1, -1, 1, 1)) + res.double())
+    out2 = torch.empty((B, C - 8, H, W), dtype=BF, device=cuda) if stats == "dual" else None
+    o = _hip.bias_act(y.to(cuda), bias.to(cuda), 1, res=res.to(cuda), stats=None if stats == "dual" else stats,
+                      out2=out2, c2lo=8)
+    od = o.double().cpu()
+    d = (od - ref).abs()
+    assert bool((d <= 2.0 ** -7 * ref.abs() + 1e-6).all()), f"max|d| {float(d.max()):.3g}"
+    if stats == "dual":
+        assert torch.equal(out2.cpu(), o[:, 8:].cpu())
+    if stats in ("sum", "summax"):
+        st = o._ys_plane_stats
+        s = st.psum.view(B, C, st.parts).sum(-1).double().cpu()
+        assert torch.allclose(s, od.sum((2, 3)), rtol=1e-5, atol=1e-4)
+        if stats == "summax":
+            mx = st.pmax.view(B, C, st.parts).amax(-1).double().cpu()
+            assert torch.equal(mx, od.amax((2, 3)))
+    if stats == "capool":
+        yin = o._ys_ca_pool[0].double().cpu()
+        assert torch.allclose(yin[..., :H], od.mean(3), rtol=1e-5, atol=1e-5)
+        assert torch.allclose(yin[..., H:], od.mean(2), rtol=1e-5, atol=1e-5)
+
+
+# ---- whole model in bf16 vs the fp32 oracle model holding the same (bf16-rounded) weights ----
+def _model_pair(cfg, cuda):
+    from oracle.model_ref import build_cpu_model
+    from yolosod_amd.nn.tasks import build_model
+    gm = build_model(cfg, seed=0, device=cuda, dtype=BF)
+    cpu = build_cpu_model(cfg)
+    cpu.load_state_dict({k: v.float().cpu() for k, v in gm.state_dict().items()})
+    return gm, cpu.double()
+
+
+def _model_check(tag, y, ref, box_atol, ztol):
+    """Box rows within box_atol pixels; class rows within ztol in logit space."""
+    y, ref = y.double(), ref.double()
+    db = float((y[:, :4] - ref[:, :4]).abs().max())
+    z = lambda p: torch.log(p.clamp(1e-30, 1 - 1e-16)) - torch.log1p(-p.clamp(1e-30, 1 - 1e-16))  # noqa: E731
+    dz = float((z(y[:, 4:]) - z(ref[:, 4:])).abs().max())
+    _log(f"{tag}: box max|d| {db:.3g} px, logit max|dz| {dz:.3g}")
+    assert db <= box_atol and dz <= ztol, f"{tag}: box {db:.3g} (tol {box_atol}), logit {dz:.3g} (tol {ztol})"
+
+
+# Whole-model bounds, ~10x the measured differences (m 256/640: box 9.3e-4 / 9.1e-4 px, logit 1.8e-4 / 1.7e-4; n 256:
+# 1.0e-3 px, 1.1e-4). Random-init outputs are dominated by biases and anchors, so these checks
+# guard the plumbing (dtype flow, decode in fp32, NMS input); the per-op tests above, on perturbed parameters and
+# unit-scale inputs, are the numerical evidence for the bf16 kernels.
+BF16_BOX_ATOL = 1e-2   # pixels
+BF16_LOGIT_TOL = 2e-3
+
+
+@pytest.mark.parametrize("cfg,size", [("yolov12m-sod.yaml", 256), ("yolov12m-sod.yaml", 640),
+                                      ("yolov12-sod-fusion-v5-simple.yaml", 256)])
+def test_bf16_model_vs_oracle(cfg, size, cuda):
+    gm, cpu = _model_pair(cfg, cuda)
+    x = torch.rand(2 if size == 256 else 1, 3, size, size, generator=torch.Generator().manual_seed(3)).to(BF)
+    with torch.inference_mode():
+        y = gm(x.to(cuda))[0]
+        assert y.dtype == torch.float32  # decode stays fp32
+        ref = cpu(x.double())[0]
+    _model_check(f"{cfg}@{size}", y.cpu(), ref, BF16_BOX_ATOL, BF16_LOGIT_TOL)
+
+
+def test_bf16_m640_batch_predict(cuda):
+    """The bench workload (bs=64, 640x640, bf16) end to end through the predictor: fixed-shape NMS output, and
+    images 0 and 63 equal to running them alone (batch invariance of the bf16 path up to MIOpen's algorithm
+    choice per batch size)."""
+    from yolosod_amd.engine.predictor import DetectionPredictor, seeded_images
+    from yolosod_amd.nn.tasks import build_model
+    gm = build_model("yolov12m-sod.yaml", seed=0, device=cuda, dtype=BF)
+    pred = DetectionPredictor(gm, conf=0.001)
+    x = seeded_images(0, 64, 640, device=cuda)
+    out, counts, index = pred.predict_padded(x)
+    assert out.shape == (64, 300, 6) and out.dtype == torch.float32 and counts.shape == (64,)
+    with torch.inference_mode():
+        y_all = gm(x.to(BF))[0]
+        y0 = gm(x[:1].to(BF))[0]
+    _model_check("m640 bs64 img0 vs bs1", y_all[:1].cpu(), y0.cpu(), 1e-2, 4e-3)

@@ -66,6 +66,24 @@ SIGNATURES = {
     "yolosod_mamba_glu_workspace": (_sz, [_i, _i, _i, _i, _i, _i]),
     "yolosod_mamba_glu_forward": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _f, _vp, _vp,
                                        _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp, _vp, _vp, _f, _vp, _sz, _vp]),
+    # bf16 storage (the bf16 model config): activations / GEMM weights bf16, other parameters fp32
+    "yolosod_se_forward_bf16": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _i, _vp, _vp, _sz, _vp]),
+    "yolosod_cbam_forward_bf16": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "yolosod_ca_forward_bf16": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp,
+                                     _vp, _vp, _vp, _sz, _vp]),
+    "yolosod_bias_act_bf16": (_i, [_vp, _l, _vp, _l, _vp, _vp, _l, _vp, _l, _i, _i, _i, _l, _i, _vp]),
+    "yolosod_bias_act_stats_bf16": (_i, [_vp, _l, _vp, _l, _vp, _vp, _l, _i, _i, _l, _i, _i, _l, _vp, _vp, _vp]),
+    "yolosod_bias_act_capool_bf16": (_i, [_vp, _l, _vp, _l, _vp, _vp, _l, _i, _i, _i, _i, _i, _vp, _vp]),
+    "yolosod_swin_workspace_bf16": (_sz, [_i, _i, _i, _i, _i, _i, _i]),
+    "yolosod_swin_forward_bf16": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp, _vp,
+                                       _vp, _f, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f, _vp, _sz, _vp]),
+    "yolosod_a2_workspace_bf16": (_sz, [_i, _i, _i, _i, _i]),
+    "yolosod_a2_forward_bf16": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp,
+                                     _vp, _sz, _vp]),
+    "yolosod_detect_head_bf16": (_i, [_i, _vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp,
+                                      _vp]),
+    "yolosod_gemm_bf16": (_i, [_vp, _l, _i, _vp, _l, _i, _i, _vp, _l, _i, _i, _i, _i, _i, _vp, _i, _i, _vp, _vp]),
+    "yolosod_attention_bf16": (_i, [_vp, _vp, _l, _i, _i, _i, _vp]),
 }
 
 _LIB = None
@@ -144,24 +162,37 @@ def _check(rc: int, what: str) -> None:
         raise RuntimeError(f"yolosod_amd.{what} failed (rc={rc}): {msg}")
 
 
-def _dev(t: torch.Tensor, name: str) -> int:
+def _dev(t: torch.Tensor, name: str, dtype=torch.float32) -> int:
     if not isinstance(t, torch.Tensor):
         raise TypeError(f"{name}: expected a tensor")
     if t.device.type != "cuda":
         raise RuntimeError(f"{name}: HIP kernel requires a GPU tensor (got device {t.device}); no CPU fallback")
-    if t.dtype != torch.float32:
-        raise RuntimeError(f"{name}: expected float32, got {t.dtype}")
+    if t.dtype != dtype:
+        raise RuntimeError(f"{name}: expected {dtype}, got {t.dtype}")
     if not t.is_contiguous():
         raise RuntimeError(f"{name}: expected a contiguous tensor")
     return t.data_ptr()
 
 
-def _p(t: torch.Tensor, name: str, numel: int | None = None) -> int:
+def _p(t: torch.Tensor, name: str, numel: int | None = None, dtype=torch.float32) -> int:
     """Pointer of a (parameter) tensor after checking its element count (and, via ``_dev``, that it is a
-    contiguous fp32 GPU tensor: no conversion is done here, callers pass prepared parameters)."""
+    contiguous GPU tensor of ``dtype``: this only validates - callers pass prepared parameters, e.g. the modules'
+    cached fp32 / bf16 copies)."""
     if numel is not None and t.numel() != numel:
         raise RuntimeError(f"{name}: expected {numel} elements, got {t.numel()}")
-    return _dev(t, name)
+    return _dev(t, name, dtype)
+
+
+_BF16 = torch.bfloat16
+
+
+def _act_dtype(x: torch.Tensor) -> bool:
+    """True for bf16 activations (the bf16 model config), False for fp32; anything else raises."""
+    if x.dtype == torch.float32:
+        return False
+    if x.dtype == _BF16:
+        return True
+    raise RuntimeError(f"yolosod_amd: activations must be float32 or bfloat16, got {x.dtype}")
 
 
 def _stream(dev) -> int:
@@ -210,65 +241,88 @@ def _pre_stats(x, need_max):
 
 
 def se_forward(x, fc1_w, fc1_b, fc2_w, fc2_b):
+    """SE on fp32 or bf16 activations (parameters fp32)."""
     lib = load_library()
+    bf = _act_dtype(x)
     B, C, H, W = x.shape
     hid = fc1_w.shape[0]
     y = torch.empty_like(x)
     ws = _workspace(lib.yolosod_se_workspace(B, C, H, W), x.device)
     pre = _pre_stats(x, False)
-    args = (_dev(x, "x"), _dev(y, "y"), B, C, H, W, _p(fc1_w, "fc1.weight", hid * C), _p(fc1_b, "fc1.bias", hid),
-            _p(fc2_w, "fc2.weight", C * hid), _p(fc2_b, "fc2.bias", C), hid)
-    if pre is not None:  # plane sums came with x from its producer's epilogue: gate + scale only
-        _check(_launch(("se", tuple(x.shape), hid), x.device, lib.yolosod_se_forward_pre, *args, pre.psum.data_ptr(),
+    args = (_dev(x, "x", x.dtype), _dev(y, "y", x.dtype), B, C, H, W, _p(fc1_w, "fc1.weight", hid * C),
+            _p(fc1_b, "fc1.bias", hid), _p(fc2_w, "fc2.weight", C * hid), _p(fc2_b, "fc2.bias", C), hid)
+    key = ("se", tuple(x.shape), hid) + ((2,) if bf else ())
+    if bf:
+        _check(_launch(key, x.device, lib.yolosod_se_forward_bf16, *args, None if pre is None else pre.psum.data_ptr(),
+                       ws.data_ptr(), ws.numel(), _stream(x.device)), "se_forward_bf16")
+    elif pre is not None:  # plane sums came with x from its producer's epilogue: gate + scale only
+        _check(_launch(key, x.device, lib.yolosod_se_forward_pre, *args, pre.psum.data_ptr(),
                        ws.data_ptr(), ws.numel(), _stream(x.device)), "se_forward_pre")
     else:
-        _check(_launch(("se", tuple(x.shape), hid), x.device, lib.yolosod_se_forward, *args, ws.data_ptr(), ws.numel(),
+        _check(_launch(key, x.device, lib.yolosod_se_forward, *args, ws.data_ptr(), ws.numel(),
                        _stream(x.device)), "se_forward")
     return y
 
 
 def cbam_forward(x, fc0_w, fc2_w, sa_w):
+    """CBAM on fp32 or bf16 activations (parameters fp32)."""
     lib = load_library()
+    bf = _act_dtype(x)
     B, C, H, W = x.shape
     hid = fc0_w.shape[0]
     y = torch.empty_like(x)
     ws = _workspace(lib.yolosod_cbam_workspace(B, C, H, W), x.device)
     pre = _pre_stats(x, True)
-    args = (_dev(x, "x"), _dev(y, "y"), B, C, H, W, _p(fc0_w, "fc.0.weight", hid * C),
+    args = (_dev(x, "x", x.dtype), _dev(y, "y", x.dtype), B, C, H, W, _p(fc0_w, "fc.0.weight", hid * C),
             _p(fc2_w, "fc.2.weight", C * hid), hid, _p(sa_w, "conv1.weight", 98))
-    if pre is not None:
-        _check(_launch(("cbam", tuple(x.shape), hid), x.device, lib.yolosod_cbam_forward_pre, *args, pre.psum.data_ptr(),
+    key = ("cbam", tuple(x.shape), hid) + ((2,) if bf else ())
+    if bf:
+        _check(_launch(key, x.device, lib.yolosod_cbam_forward_bf16, *args,
+                       None if pre is None else pre.psum.data_ptr(), None if pre is None else pre.pmax.data_ptr(),
+                       ws.data_ptr(), ws.numel(), _stream(x.device)), "cbam_forward_bf16")
+    elif pre is not None:
+        _check(_launch(key, x.device, lib.yolosod_cbam_forward_pre, *args, pre.psum.data_ptr(),
                        pre.pmax.data_ptr(), ws.data_ptr(), ws.numel(), _stream(x.device)), "cbam_forward_pre")
     else:
-        _check(_launch(("cbam", tuple(x.shape), hid), x.device, lib.yolosod_cbam_forward, *args, ws.data_ptr(), ws.numel(),
+        _check(_launch(key, x.device, lib.yolosod_cbam_forward, *args, ws.data_ptr(), ws.numel(),
                        _stream(x.device)), "cbam_forward")
     return y
 
 
 def ca_forward(x, conv1_w, conv1_b, bn_w, bn_b, bn_mean, bn_var, bn_eps, convh_w, convh_b, convw_w, convw_b):
+    """CA on fp32 or bf16 activations (parameters fp32)."""
     lib = load_library()
+    bf = _act_dtype(x)
     B, C, H, W = x.shape
     mip = conv1_w.shape[0]
     y = torch.empty_like(x)
     ws = _workspace(lib.yolosod_ca_workspace(B, C, H, W), x.device)
-    args = (_dev(x, "x"), _dev(y, "y"), B, C, H, W, _p(conv1_w, "conv1.weight", mip * C),
+    args = (_dev(x, "x", x.dtype), _dev(y, "y", x.dtype), B, C, H, W, _p(conv1_w, "conv1.weight", mip * C),
             _p(conv1_b, "conv1.bias", mip), mip, _p(bn_w, "bn1.weight", mip), _p(bn_b, "bn1.bias", mip),
             _p(bn_mean, "bn1.running_mean", mip), _p(bn_var, "bn1.running_var", mip), float(bn_eps),
             _p(convh_w, "conv_h.weight", C * mip), _p(convh_b, "conv_h.bias", C),
             _p(convw_w, "conv_w.weight", C * mip), _p(convw_b, "conv_w.bias", C))
     pre = getattr(x, "_ys_ca_pool", None)
-    if pre is not None and pre[1] == tuple(x.shape):  # row / column means came with x from its producer
-        _check(_launch(("ca", tuple(x.shape), mip), x.device, lib.yolosod_ca_forward_pre, *args, pre[0].data_ptr(),
+    if pre is not None and pre[1] != tuple(x.shape):
+        pre = None
+    key = ("ca", tuple(x.shape), mip) + ((2,) if bf else ())
+    if bf:
+        _check(_launch(key, x.device, lib.yolosod_ca_forward_bf16, *args, None if pre is None else pre[0].data_ptr(),
+                       ws.data_ptr(), ws.numel(), _stream(x.device)), "ca_forward_bf16")
+    elif pre is not None:  # row / column means came with x from its producer
+        _check(_launch(key, x.device, lib.yolosod_ca_forward_pre, *args, pre[0].data_ptr(),
                        ws.data_ptr(), ws.numel(), _stream(x.device)), "ca_forward_pre")
     else:
-        _check(_launch(("ca", tuple(x.shape), mip), x.device, lib.yolosod_ca_forward, *args, ws.data_ptr(), ws.numel(),
+        _check(_launch(key, x.device, lib.yolosod_ca_forward, *args, ws.data_ptr(), ws.numel(),
                        _stream(x.device)), "ca_forward")
     return y
 
 
 def a2_forward(x, num_areas, num_heads, proj_w, proj_b, ln_w, ln_b, ln_eps, in_w, in_b, mo_w, mo_b, op_w, op_b):
-    """mo_w = mo_b = None: op_w / op_b are the pre-multiplied MHA-out x output-conv weights (A2_Attn._fused_out)."""
+    """mo_w = mo_b = None: op_w / op_b are the pre-multiplied MHA-out x output-conv weights (A2_Attn._fused_out).
+    bf16 activations: proj_w / in_w / op_w bf16 (pre-multiplied form only), biases and LN fp32."""
     lib = load_library()
+    bf = _act_dtype(x)
     if (mo_w is None) != (mo_b is None):
         raise RuntimeError("a2_forward: attention.out_proj weight and bias must both be given or both be None")
     B, C, H, W = x.shape
@@ -277,8 +331,22 @@ def a2_forward(x, num_areas, num_heads, proj_w, proj_b, ln_w, ln_b, ln_eps, in_w
     if num_areas * W > 320:
         raise RuntimeError(f"A2_Attn: sequence length {num_areas * W} > 320 unsupported")
     y = torch.empty_like(x)
+    key = ("a2", tuple(x.shape), (num_areas, num_heads)) + ((2,) if bf else ())
+    if bf:
+        if mo_w is not None:
+            raise RuntimeError("a2_forward: the bf16 path takes the pre-multiplied output weights only")
+        if C // num_heads not in (32, 64, 128) or C % 64:
+            raise RuntimeError(f"A2_Attn (bf16): C={C} with head dim {C // num_heads} unsupported")
+        ws = _workspace(lib.yolosod_a2_workspace_bf16(B, C, H, W, num_areas), x.device)
+        _check(_launch(key, x.device, lib.yolosod_a2_forward_bf16, _dev(x, "x", _BF16), _dev(y, "y", _BF16), B, C, H,
+                       W, num_areas, num_heads, _p(proj_w, "proj.weight", C * C, _BF16), _p(proj_b, "proj.bias", C),
+                       _p(ln_w, "layer_norm.weight", C), _p(ln_b, "layer_norm.bias", C), float(ln_eps),
+                       _p(in_w, "in_proj_weight", 3 * C * C, _BF16), _p(in_b, "in_proj_bias", 3 * C),
+                       _p(op_w, "out_proj.weight", C * C, _BF16), _p(op_b, "out_proj.bias", C), ws.data_ptr(),
+                       ws.numel(), _stream(x.device)), "a2_forward_bf16")
+        return y
     ws = _workspace(lib.yolosod_a2_workspace(B, C, H, W, num_areas), x.device)
-    _check(_launch(("a2", tuple(x.shape), (num_areas, num_heads)), x.device, lib.yolosod_a2_forward, _dev(x, "x"), _dev(y, "y"), B, C, H, W, num_areas, num_heads,
+    _check(_launch(key, x.device, lib.yolosod_a2_forward, _dev(x, "x"), _dev(y, "y"), B, C, H, W, num_areas, num_heads,
                                   _p(proj_w, "proj.weight", C * C), _p(proj_b, "proj.bias", C),
                                   _p(ln_w, "layer_norm.weight", C), _p(ln_b, "layer_norm.bias", C), float(ln_eps),
                                   _p(in_w, "in_proj_weight", 3 * C * C), _p(in_b, "in_proj_bias", 3 * C),
@@ -292,27 +360,36 @@ def a2_forward(x, num_areas, num_heads, proj_w, proj_b, ln_w, ln_b, ln_eps, in_w
 
 def swin_forward(x, num_heads, window, dw_w, ln1_w, ln1_b, ln1_eps, in_w, in_b, out_w, out_b, ln2_w, ln2_b,
                  ln2_eps, m1_w, m1_b, m2_w, m2_b, pw_w, bn_w, bn_b, bn_mean, bn_var, bn_eps):
+    """SwinBlock on fp32 or bf16 activations. bf16: the projection / MLP / pw weights (in_w, out_w, m1_w, m2_w,
+    pw_w) are bf16, every other parameter fp32."""
     lib = load_library()
+    bf = _act_dtype(x)
     B, C, H, W = x.shape
     hid = m1_w.shape[0]
     wh = H if (H <= window and W <= window) else min(window, H)
     ww = W if (H <= window and W <= window) else min(window, W)
     if wh * ww > 320:
         raise RuntimeError(f"SwinBlock: window of {wh}x{ww} tokens unsupported")
-    if C % num_heads or (C // num_heads) not in (8, 16, 32, 64, 128):
+    if C % num_heads or (C // num_heads) not in ((32, 64, 128) if bf else (8, 16, 32, 64, 128)):
         raise RuntimeError(f"SwinBlock: head dim {C}/{num_heads} unsupported")
     y = torch.empty_like(x)
-    ws = _workspace(lib.yolosod_swin_workspace_v2(B, C, H, W, num_heads, window, hid), x.device)
-    _check(_launch(("swin", tuple(x.shape), (num_heads, window, hid)), x.device, lib.yolosod_swin_forward,
-        _dev(x, "x"), _dev(y, "y"), B, C, H, W, num_heads, window, _p(dw_w, "dw.weight", C * 9),
+    gw = _BF16 if bf else torch.float32
+    if bf:
+        ws = _workspace(lib.yolosod_swin_workspace_bf16(B, C, H, W, num_heads, window, hid), x.device)
+        fn, what = lib.yolosod_swin_forward_bf16, "swin_forward_bf16"
+    else:
+        ws = _workspace(lib.yolosod_swin_workspace_v2(B, C, H, W, num_heads, window, hid), x.device)
+        fn, what = lib.yolosod_swin_forward, "swin_forward"
+    _check(_launch(("swin", tuple(x.shape), (num_heads, window, hid)) + ((2,) if bf else ()), x.device, fn,
+        _dev(x, "x", x.dtype), _dev(y, "y", x.dtype), B, C, H, W, num_heads, window, _p(dw_w, "dw.weight", C * 9),
         _p(ln1_w, "norm1.weight", C), _p(ln1_b, "norm1.bias", C), float(ln1_eps),
-        _p(in_w, "in_proj_weight", 3 * C * C), _p(in_b, "in_proj_bias", 3 * C),
-        _p(out_w, "out_proj.weight", C * C), _p(out_b, "out_proj.bias", C),
+        _p(in_w, "in_proj_weight", 3 * C * C, gw), _p(in_b, "in_proj_bias", 3 * C),
+        _p(out_w, "out_proj.weight", C * C, gw), _p(out_b, "out_proj.bias", C),
         _p(ln2_w, "norm2.weight", C), _p(ln2_b, "norm2.bias", C), float(ln2_eps),
-        _p(m1_w, "mlp.0.weight", hid * C), _p(m1_b, "mlp.0.bias", hid), hid,
-        _p(m2_w, "mlp.2.weight", C * hid), _p(m2_b, "mlp.2.bias", C), _p(pw_w, "pw.weight", C * C),
+        _p(m1_w, "mlp.0.weight", hid * C, gw), _p(m1_b, "mlp.0.bias", hid), hid,
+        _p(m2_w, "mlp.2.weight", C * hid, gw), _p(m2_b, "mlp.2.bias", C), _p(pw_w, "pw.weight", C * C, gw),
         _p(bn_w, "bn.weight", C), _p(bn_b, "bn.bias", C), _p(bn_mean, "bn.running_mean", C),
-        _p(bn_var, "bn.running_var", C), float(bn_eps), ws.data_ptr(), ws.numel(), _stream(x.device)), "swin_forward")
+        _p(bn_var, "bn.running_var", C), float(bn_eps), ws.data_ptr(), ws.numel(), _stream(x.device)), what)
     return y
 
 
@@ -366,9 +443,12 @@ def detect_decode(maps, strides, nc, reg_max=16):
 
 def detect_head(box_feats, cls_feats, box_w, box_b, cls_w, cls_b, strides, nc, reg_max=16):
     """Fused last 1x1 convs of both Detect towers + decode. box_feats[i] [B, c2, Hi, Wi], cls_feats[i]
-    [B, c3, Hi, Wi] contiguous fp32; box_w[i] [64, c2], cls_w[i] [nc, c3] -> y [B, 4+nc, A]."""
+    [B, c3, Hi, Wi] contiguous fp32 or bf16 (all levels alike); box_w[i] [64, c2], cls_w[i] [nc, c3] and biases
+    fp32 -> y [B, 4+nc, A] fp32 (the decode stays fp32 in the bf16 config)."""
     lib = load_library()
     nl = len(box_feats)
+    bf = _act_dtype(box_feats[0])
+    ft = box_feats[0].dtype
     B, c2 = box_feats[0].shape[:2]
     c3 = cls_feats[0].shape[1]
     for i in range(nl):
@@ -381,15 +461,16 @@ def detect_head(box_feats, cls_feats, box_w, box_b, cls_w, cls_b, strides, nc, r
     A = sum(t.shape[2] * t.shape[3] for t in box_feats)
     y = torch.empty((B, 4 + nc, A), dtype=torch.float32, device=box_feats[0].device)
 
-    def arr(ts, what):
-        return ctypes.cast((ctypes.c_void_p * nl)(*[_dev(t, f"{what}[{i}]") for i, t in enumerate(ts)]),
+    def arr(ts, what, dtype=torch.float32):
+        return ctypes.cast((ctypes.c_void_p * nl)(*[_dev(t, f"{what}[{i}]", dtype) for i, t in enumerate(ts)]),
                            ctypes.c_void_p)
 
     hs = (ctypes.c_int * nl)(*[t.shape[2] for t in box_feats])
     wsz = (ctypes.c_int * nl)(*[t.shape[3] for t in box_feats])
     st = (ctypes.c_float * nl)(*[float(s) for s in strides])
-    _check(_launch(("head", (B, A), (nc, c2, c3)), box_feats[0].device, lib.yolosod_detect_head, nl, arr(box_feats, "box_feats"),
-                   arr(cls_feats, "cls_feats"), c2, c3, arr(box_w, "box_w"), arr(box_b, "box_b"),
+    fn = lib.yolosod_detect_head_bf16 if bf else lib.yolosod_detect_head
+    _check(_launch(("head", (B, A), (nc, c2, c3)) + ((2,) if bf else ()), box_feats[0].device, fn, nl, arr(box_feats, "box_feats", ft),
+                   arr(cls_feats, "cls_feats", ft), c2, c3, arr(box_w, "box_w"), arr(box_b, "box_b"),
                    arr(cls_w, "cls_w"), arr(cls_b, "cls_b"), ctypes.cast(hs, ctypes.c_void_p),
                    ctypes.cast(wsz, ctypes.c_void_p), ctypes.cast(st, ctypes.c_void_p), B, nc, reg_max,
                    _dev(y, "y"), _stream(box_feats[0].device)), "detect_head")
@@ -424,8 +505,11 @@ def bias_act(y, bias, act, out=None, res=None, stats=None, out2=None, c2lo=0):
     larger contiguous concat buffer (batch stride > C*H*W); ``res`` likewise. In place when out is None.
     ``stats`` ("sum" / "summax"): also emit out's per-plane partial sums (+ maxes) for a following SE / CBAM,
     attached to the returned tensor as ``_ys_plane_stats`` (PlaneStats); "capool": the row / column means a
-    following CA_Block pools, attached as ``_ys_ca_pool`` ([B, C, H + W], shape)."""
+    following CA_Block pools, attached as ``_ys_ca_pool`` ([B, C, H + W], shape). y / out / res / out2 are fp32
+    or bf16 (all alike; bias fp32); the statistics are fp32 of the stored values."""
     lib = load_library()
+    bf = _act_dtype(y)
+    dt = y.dtype
     B, C, H, W = y.shape
     HW = H * W
     if out is None:
@@ -436,8 +520,8 @@ def bias_act(y, bias, act, out=None, res=None, stats=None, out2=None, c2lo=0):
         return out
 
     def bstride(t, name):
-        if t.device.type != "cuda" or t.dtype != torch.float32:
-            raise RuntimeError(f"bias_act: {name} must be a float32 GPU tensor")
+        if t.device.type != "cuda" or t.dtype != dt:
+            raise RuntimeError(f"bias_act: {name} must be a {dt} GPU tensor")
         if t.shape != y.shape or t.stride(3) != 1 or t.stride(2) != W or t.stride(1) != HW:
             raise RuntimeError(f"bias_act: {name} must be [B,C,H,W] with contiguous channels (got {t.stride()})")
         return t.stride(0)
@@ -445,37 +529,48 @@ def bias_act(y, bias, act, out=None, res=None, stats=None, out2=None, c2lo=0):
     yb = bstride(y, "y")
     ob = bstride(out, "out")
     rb = bstride(res, "res") if res is not None else 0
+    rp = None if res is None else res.data_ptr()
+    bp = _dev(bias, "bias")
     if out2 is not None and stats is None:  # ``out2`` = packed copy of channels [c2lo, C) (next conv's input)
-        if (out2.device.type != "cuda" or out2.dtype != torch.float32 or tuple(out2.shape) != (B, C - c2lo, H, W)
+        if (out2.device.type != "cuda" or out2.dtype != dt or tuple(out2.shape) != (B, C - c2lo, H, W)
                 or out2.stride(3) != 1 or out2.stride(2) != W or out2.stride(1) != HW):
-            raise RuntimeError("bias_act: out2 must be a float32 GPU tensor [B, C - c2lo, H, W] with contiguous channels")
-        _check(_launch(("bias_act", tuple(y.shape), "dual"), y.device, lib.yolosod_bias_act_dual, y.data_ptr(), yb, out.data_ptr(), ob, _dev(bias, "bias"),
-                                         None if res is None else res.data_ptr(), rb, out2.data_ptr(), out2.stride(0),
-                                         int(c2lo), B, C, HW, int(act), _stream(y.device)), "bias_act_dual")
+            raise RuntimeError(f"bias_act: out2 must be a {dt} GPU tensor [B, C - c2lo, H, W] with contiguous channels")
+        if bf:
+            _check(_launch(("bias_act", tuple(y.shape), "dual"), y.device, lib.yolosod_bias_act_bf16, y.data_ptr(), yb,
+                           out.data_ptr(), ob, bp, rp, rb, out2.data_ptr(), out2.stride(0), int(c2lo), B, C, HW,
+                           int(act), _stream(y.device)), "bias_act_bf16")
+        else:
+            _check(_launch(("bias_act", tuple(y.shape), "dual"), y.device, lib.yolosod_bias_act_dual, y.data_ptr(), yb,
+                           out.data_ptr(), ob, bp, rp, rb, out2.data_ptr(), out2.stride(0), int(c2lo), B, C, HW,
+                           int(act), _stream(y.device)), "bias_act_dual")
         return out
     if stats == "capool":  # CA_Block input: pooled row / column means of out, [B, C, H + W]
         if W % 4 or W > 1024:
             stats = None
         else:
             yin = torch.empty((B, C, H + W), dtype=torch.float32, device=y.device)
-            _check(_launch(("bias_act", tuple(y.shape), "capool"), y.device, lib.yolosod_bias_act_capool, y.data_ptr(), yb, out.data_ptr(), ob, _dev(bias, "bias"),
-                                               None if res is None else res.data_ptr(), rb, B, C, H, W, int(act),
-                                               yin.data_ptr(), _stream(y.device)), "bias_act_capool")
+            fn = lib.yolosod_bias_act_capool_bf16 if bf else lib.yolosod_bias_act_capool
+            _check(_launch(("bias_act", tuple(y.shape), "capool"), y.device, fn, y.data_ptr(), yb, out.data_ptr(), ob,
+                           bp, rp, rb, B, C, H, W, int(act), yin.data_ptr(), _stream(y.device)), "bias_act_capool")
             out._ys_ca_pool = (yin, tuple(out.shape))
             return out
     if stats is not None:
         parts, seg = plane_parts(HW)
         psum = torch.empty(B * C * parts, dtype=torch.float32, device=y.device)
         pmax = torch.empty_like(psum) if stats == "summax" else None
-        _check(_launch(("bias_act", tuple(y.shape), stats), y.device, lib.yolosod_bias_act_stats, y.data_ptr(), yb, out.data_ptr(), ob, _dev(bias, "bias"),
-                                          None if res is None else res.data_ptr(), rb, B, C, HW, int(act), parts, seg,
-                                          psum.data_ptr(), None if pmax is None else pmax.data_ptr(), _stream(y.device)),
-               "bias_act_stats")
+        fn = lib.yolosod_bias_act_stats_bf16 if bf else lib.yolosod_bias_act_stats
+        _check(_launch(("bias_act", tuple(y.shape), stats), y.device, fn, y.data_ptr(), yb, out.data_ptr(), ob, bp,
+                       rp, rb, B, C, HW, int(act), parts, seg, psum.data_ptr(),
+                       None if pmax is None else pmax.data_ptr(), _stream(y.device)), "bias_act_stats")
         out._ys_plane_stats = PlaneStats(psum, pmax, parts, out.shape)
         return out
-    _check(_launch(("bias_act", tuple(y.shape), None), y.device, lib.yolosod_bias_act, y.data_ptr(), yb, out.data_ptr(), ob, _dev(bias, "bias"),
-                                None if res is None else res.data_ptr(), rb, B, C, HW, int(act), _stream(y.device)),
-           "bias_act")
+    if bf:
+        _check(_launch(("bias_act", tuple(y.shape), None), y.device, lib.yolosod_bias_act_bf16, y.data_ptr(), yb,
+                       out.data_ptr(), ob, bp, rp, rb, None, 0, 0, B, C, HW, int(act), _stream(y.device)),
+               "bias_act_bf16")
+        return out
+    _check(_launch(("bias_act", tuple(y.shape), None), y.device, lib.yolosod_bias_act, y.data_ptr(), yb, out.data_ptr(),
+                   ob, bp, rp, rb, B, C, HW, int(act), _stream(y.device)), "bias_act")
     return out
 
 
@@ -585,4 +680,27 @@ def attention(qkv, n_seq, L, C, heads):
     lib = load_library()
     out = torch.empty((n_seq * L, C), dtype=torch.float32, device=qkv.device)
     _check(_launch(("attention", (n_seq, L, C), heads), qkv.device, lib.yolosod_attention, _dev(qkv, "qkv"), _dev(out, "out"), n_seq, L, C, heads, _stream(qkv.device)), "attention")
+    return out
+
+
+def gemm_bf16(A, B, b_kcontig, bias=None, bias_mode=0, act=0, res=None):
+    """Test hook: A [M,K] bf16; B [N,K] (b_kcontig) or [K,N] bf16; returns C [M,N] bf16 (fp32 accumulation)."""
+    lib = load_library()
+    M, K = A.shape
+    N = B.shape[0] if b_kcontig else B.shape[1]
+    C = torch.empty((M, N), dtype=_BF16, device=A.device)
+    _check(_launch(("gemm_bf16", (M, N, K), None), A.device, lib.yolosod_gemm_bf16, _dev(A, "A", _BF16), 0, K,
+                   _dev(B, "B", _BF16), 0, B.shape[1], int(b_kcontig), _dev(C, "C", _BF16), 0, N, M, N, K, 1,
+                   None if bias is None else _dev(bias, "bias"), bias_mode, act,
+                   None if res is None else _dev(res, "res", _BF16), _stream(A.device)), "gemm_bf16")
+    return C
+
+
+def attention_bf16(qkv, n_seq, L, C, heads):
+    """Test hook: bf16 attention over n_seq contiguous sequences of L rows of qkv [n_seq*L, 3C] -> [n_seq*L, C]."""
+    lib = load_library()
+    out = torch.empty((n_seq * L, C), dtype=_BF16, device=qkv.device)
+    _check(_launch(("attention_bf16", (n_seq, L, C), heads), qkv.device, lib.yolosod_attention_bf16,
+                   _dev(qkv, "qkv", _BF16), _dev(out, "out", _BF16), n_seq, L, C, heads, _stream(qkv.device)),
+           "attention_bf16")
     return out

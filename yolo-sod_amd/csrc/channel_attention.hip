@@ -1,12 +1,15 @@
 // Channel / spatial / coordinate attention of the Multi-Attention Fusion Neck: SE_Block, CBAM_Block, CA_Block.
 //
-// All three are HBM-bound (a few FLOPs per byte). Layout is the reference's NCHW fp32. Each op is split into
-//   (1) a reduction pass over x (per-plane sum/max split over several workgroups per plane, or row+column
-//       means), writing small partials,
-//   (2) a tiny per-image gate kernel (the SE / CBAM channel MLP, the CA conv1+BN+h_sigmoid+conv_h/w gates),
-//   (3) one streaming apply pass that reads x once and writes y once (float4, coalesced, every lane busy).
-// CBAM has one more reduction (per-pixel channel mean/max, split over channel groups) and a 16x16-tiled 7x7
-// conv for the spatial gate between (2) and (3).
+// All three are HBM-bound (a few FLOPs per byte). Layout is the reference's NCHW; storage is fp32 or bf16 (the
+// bf16 model config), arithmetic always fp32. Each op is
+//   (1) a reduction over x (per-plane sum/max split over several workgroups per plane, or row+column means) -
+//       normally emitted by x's producing conv epilogue (conv_epilogue.hip), so no extra pass over x,
+//   (2) the gate (the SE / CBAM channel MLP, the CA conv1+BN+h_sigmoid+conv_h/w gates),
+//   (3) one streaming apply pass that reads x once and writes y once (coalesced vectors, every lane busy).
+// SE recomputes its (tiny) channel MLP inside the apply workgroups: gate + scale is one launch. CBAM is two:
+// channel gate + per-pixel channel mean/max of ca*x (per 32-channel group), then the 7x7 spatial conv of each
+// workgroup's pixels (halo of the mean/max map in LDS) + apply. The older split kernels stay as the path for
+// shapes the fused ones do not take (H*W % 4 != 0, very wide rows).
 // Optionally (YOLOSOD_MALL_CHUNK_MB > 0) the host driver walks the batch in image chunks sized to stay resident
 // in the 256 MiB Infinity Cache between the passes. Measured on MI355X at the bs=32 640x640 shapes, the apply
 // pass' re-read does hit on-die (7.3 TB/s) but the extra launch boundaries and the smaller grids cost more
@@ -40,11 +43,17 @@ static int images_per_chunk(int B, size_t bytes_per_image) {
   return (int)n;
 }
 
+// fused gate-in-apply kernels (default on; YOLOSOD_FUSED_GATES=0 restores the split launches for A/B)
+static bool fused_gates() {
+  static const bool on = [] { const char* e = getenv("YOLOSOD_FUSED_GATES"); return !e || atoi(e) != 0; }();
+  return on;
+}
+
 constexpr int kMaxParts = 64;
 
-// How many workgroups reduce one plane: one per 8192 floats (32 KiB), so the big early planes (SE at 320x320,
-// CBAM at 160x160) still launch thousands of workgroups per chunk. Depends on the plane size only, never on
-// the batch, so results are bitwise independent of batch size, chunking and sharding.
+// How many workgroups reduce one plane: one per 8192 elements, so the big early planes (SE at 320x320, CBAM at
+// 160x160) still launch thousands of workgroups per chunk. Depends on the plane size only, never on the batch or
+// the storage type, so results are bitwise independent of batch size, chunking and sharding.
 struct PartPlan {
   int parts;
   long seg;
@@ -60,26 +69,26 @@ static PartPlan part_plan(long HW) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// (1) per-plane partial sum (+max): workgroup (plane, k) reduces x[plane][k*seg, (k+1)*seg) with four 16-B
+// (1) per-plane partial sum (+max): workgroup (plane, k) reduces x[plane][k*seg, (k+1)*seg) with four vector
 // loads in flight per lane; partials land in psum/pmax[plane * parts + k].
 // ------------------------------------------------------------------------------------------------
-template <bool WITH_MAX>
-__global__ __launch_bounds__(256) void plane_part_stats_kernel(const float* __restrict__ x, long HW, int parts,
+template <bool WITH_MAX, class T>
+__global__ __launch_bounds__(256) void plane_part_stats_kernel(const T* __restrict__ x, long HW, int parts,
                                                                long seg, float* __restrict__ psum,
                                                                float* __restrict__ pmax) {
   const long plane = blockIdx.x / parts;
   const int k = blockIdx.x % parts;
   const long s0 = k * seg;
   const long s1 = (s0 + seg < HW) ? s0 + seg : HW;
-  const float* p = x + plane * HW;
+  const T* p = x + plane * HW;
   float s = 0.f, m = -INFINITY;
   const int tid = threadIdx.x;
   if ((HW & 3) == 0) {
-    const float4* p4 = reinterpret_cast<const float4*>(p + s0);
+    const T* p4 = p + s0;
     const long n4 = (s1 - s0) >> 2;
     long i = tid;
     for (; i + 3 * 256 < n4; i += 4 * 256) {
-      float4 a = p4[i], b = p4[i + 256], c = p4[i + 512], d = p4[i + 768];
+      f32x4 a = ld4(p4 + 4 * i), b = ld4(p4 + 4 * (i + 256)), c = ld4(p4 + 4 * (i + 512)), d = ld4(p4 + 4 * (i + 768));
       s += ((a.x + a.y) + (a.z + a.w)) + ((b.x + b.y) + (b.z + b.w)) + ((c.x + c.y) + (c.z + c.w)) +
            ((d.x + d.y) + (d.z + d.w));
       if (WITH_MAX) {
@@ -88,13 +97,13 @@ __global__ __launch_bounds__(256) void plane_part_stats_kernel(const float* __re
       }
     }
     for (; i < n4; i += 256) {
-      float4 a = p4[i];
+      f32x4 a = ld4(p4 + 4 * i);
       s += (a.x + a.y) + (a.z + a.w);
       if (WITH_MAX) m = fmaxf(m, fmaxf(fmaxf(a.x, a.y), fmaxf(a.z, a.w)));
     }
   } else {
     for (long i = s0 + tid; i < s1; i += 256) {
-      float v = p[i];
+      float v = ld1(p + i);
       s += v;
       if (WITH_MAX) m = fmaxf(m, v);
     }
@@ -115,22 +124,19 @@ __global__ __launch_bounds__(256) void plane_part_stats_kernel(const float* __re
 }
 
 // ------------------------------------------------------------------------------------------------
-// (2) per-image channel gates. grid = images, 256 threads, dynamic LDS = (2*C + 128) floats.
+// (2) channel gates of one image, computed by one workgroup (256 threads) into LDS:
 //   SE:   gate[c] = sigmoid(W2 relu(W1 mean + b1) + b2)
 //   CBAM: gate[c] = sigmoid(W2 relu(W1 avg) + W2 relu(W1 max))     (no biases, cbam_block.py:14-17)
+// avg / mx: LDS [C] each, hsh: LDS [128]. Only channels [c0, c0 + n) of the output are produced, into out[0, n).
+// The summation orders are fixed (partials in k order, the hidden dot products as a wave reduction), so every
+// workgroup that recomputes a gate gets the same bits.
 // ------------------------------------------------------------------------------------------------
 template <bool CBAM>
-__global__ __launch_bounds__(256) void channel_gate_kernel(const float* __restrict__ psum,
-                                                           const float* __restrict__ pmax, int parts, int C,
-                                                           float inv_hw, const float* __restrict__ w1,
-                                                           const float* __restrict__ b1, const float* __restrict__ w2,
-                                                           const float* __restrict__ b2, int hid,
-                                                           float* __restrict__ gate) {
-  extern __shared__ float sh[];
-  float* avg = sh;            // [C]
-  float* mx = sh + C;         // [C]   (CBAM)
-  float* hsh = sh + 2 * C;    // [128] hidden of both branches
-  const int b = blockIdx.x;
+__device__ __forceinline__ void gate_mlp(const float* __restrict__ psum, const float* __restrict__ pmax, int parts,
+                                         int C, float inv_hw, const float* __restrict__ w1,
+                                         const float* __restrict__ b1, const float* __restrict__ w2,
+                                         const float* __restrict__ b2, int hid, int b, float* avg, float* mx,
+                                         float* hsh, int c0, int n, float* out) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   for (int c = tid; c < C; c += 256) {
     const float* ps = psum + ((long)b * C + c) * parts;
@@ -155,68 +161,116 @@ __global__ __launch_bounds__(256) void channel_gate_kernel(const float* __restri
     if (lane == 0) hsh[(j < hid ? 0 : 64) + jj] = fmaxf(CBAM ? acc : acc + b1[jj], 0.f);
   }
   __syncthreads();
-  for (int c = tid; c < C; c += 256) {
+  for (int i = tid; i < n; i += 256) {
+    const int c = c0 + i;
     float za = 0.f, zm = 0.f;
     for (int j = 0; j < hid; ++j) {
       const float wcj = w2[(long)c * hid + j];
       za += wcj * hsh[j];
       if (CBAM) zm += wcj * hsh[64 + j];
     }
-    gate[(long)b * C + c] = CBAM ? sigmoidf_(za + zm) : sigmoidf_(za + b2[c]);
+    out[i] = CBAM ? sigmoidf_(za + zm) : sigmoidf_(za + b2[c]);
   }
+  __syncthreads();
+}
+
+// per-image gates into global memory. grid = images, dynamic LDS = (2*C + 128 + C) floats.
+template <bool CBAM>
+__global__ __launch_bounds__(256) void channel_gate_kernel(const float* __restrict__ psum,
+                                                           const float* __restrict__ pmax, int parts, int C,
+                                                           float inv_hw, const float* __restrict__ w1,
+                                                           const float* __restrict__ b1, const float* __restrict__ w2,
+                                                           const float* __restrict__ b2, int hid,
+                                                           float* __restrict__ gate) {
+  extern __shared__ float sh[];
+  const int b = blockIdx.x;
+  float* g = sh + 2 * C + 128;
+  gate_mlp<CBAM>(psum, pmax, parts, C, inv_hw, w1, b1, w2, b2, hid, b, sh, sh + C, sh + 2 * C, 0, C, g);
+  for (int c = threadIdx.x; c < C; c += 256) gate[(long)b * C + c] = g[c];
 }
 
 // ------------------------------------------------------------------------------------------------
-// (3a) SE apply: y = x * gate[b][c]. float4 path: grid = (ceil(HW / 1024), ceil(C / 8), images), a lane scales
-// one float4 pixel in 8 consecutive channel planes - 8 independent 16-B loads in flight before the first store
-// (the 4-deep per-plane version streamed at ~4 TB/s, this shape at ~6 like cbam_apply). Scalar path otherwise.
+// (3a) SE apply: y = x * gate[b][c]. Vector path: grid = (ceil(HW / 1024), ceil(C / 8), images), a lane scales
+// 4 pixels in 8 consecutive channel planes - 8 independent vector loads in flight before the first store (the
+// 4-deep per-plane version streamed at ~4 TB/s, this shape at ~6 like cbam_apply). Scalar path otherwise.
+// FUSED: the workgroup computes the gates of its 8 channels itself from the plane partials (gate_mlp), so SE is
+// one launch after its producer; dynamic LDS = (2*C + 136) floats.
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void plane_scale_kernel(const float* __restrict__ x, float* __restrict__ y,
-                                                          const float* __restrict__ gate, int C, long HW, int rev) {
+template <class T, bool FUSED>
+__global__ __launch_bounds__(256) void plane_scale_kernel(const T* __restrict__ x, T* __restrict__ y,
+                                                          const float* __restrict__ gate, int C, long HW, int rev,
+                                                          const float* __restrict__ psum, int parts, float inv_hw,
+                                                          const float* __restrict__ w1, const float* __restrict__ b1,
+                                                          const float* __restrict__ w2, const float* __restrict__ b2,
+                                                          int hid) {
+  extern __shared__ float sh[];
   const int b = rev ? gridDim.z - 1 - blockIdx.z : blockIdx.z;
   const int c0 = (rev ? gridDim.y - 1 - blockIdx.y : blockIdx.y) * 8;
   const int n = (C - c0 < 8) ? C - c0 : 8;
-  const float* gb = gate + (long)b * C + c0;
+  const float* gb;
+  if (FUSED) {
+    float* g = sh + 2 * C + 128;
+    gate_mlp<false>(psum, nullptr, parts, C, inv_hw, w1, b1, w2, b2, hid, b, sh, nullptr, sh + 2 * C, c0, n, g);
+    gb = g;
+  } else {
+    gb = gate + (long)b * C + c0;
+  }
   if ((HW & 3) == 0) {
     const long p = ((long)blockIdx.x * 256 + threadIdx.x) * 4;
     if (p >= HW) return;
-    const float* xb = x + ((long)b * C + c0) * HW + p;
-    float* yb = y + ((long)b * C + c0) * HW + p;
+    const T* xb = x + ((long)b * C + c0) * HW + p;
+    T* yb = y + ((long)b * C + c0) * HW + p;
     if (n == 8) {
       f32x4 v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const f32x4*>(xb + (long)u * HW);
+      for (int u = 0; u < 8; ++u) v[u] = ld4(xb + (long)u * HW);
 #pragma unroll
-      for (int u = 0; u < 8; ++u) *reinterpret_cast<f32x4*>(yb + (long)u * HW) = v[u] * gb[u];
+      for (int u = 0; u < 8; ++u) st4(yb + (long)u * HW, v[u] * gb[u]);
     } else {
-      for (int u = 0; u < n; ++u)
-        *reinterpret_cast<f32x4*>(yb + (long)u * HW) = *reinterpret_cast<const f32x4*>(xb + (long)u * HW) * gb[u];
+      for (int u = 0; u < n; ++u) st4(yb + (long)u * HW, ld4(xb + (long)u * HW) * gb[u]);
     }
   } else {
     const long p = (long)blockIdx.x * 256 + threadIdx.x;
     if (p >= HW) return;
     for (int u = 0; u < n; ++u) {
       const long o = ((long)b * C + c0 + u) * HW + p;
-      y[o] = x[o] * gb[u];
+      st1(y + o, ld1(x + o) * gb[u]);
     }
   }
 }
 
 // ------------------------------------------------------------------------------------------------
 // CBAM pass 2: per-pixel channel sum / max of o = ca[c] * x over channel group g -> mpart[b][g][0|1][HW].
-// grid = (ceil(HW / (256*V)), G, images); V = 4 (float4 pixels) when HW % 4 == 0.
+// grid = (ceil(HW / (256*V)), G, images); V = 4 (vector pixels) when HW % 4 == 0.
+// FUSED: the workgroup first computes the channel gate of its group from the plane partials (gate_mlp; blockIdx.x
+// == 0 also stores it to ca for the apply pass), so channel gate + pixel statistics are one launch; dynamic LDS =
+// (3*C + 128) floats.
 // ------------------------------------------------------------------------------------------------
-template <int V>
-__global__ __launch_bounds__(256) void cbam_pixel_stats_kernel(const float* __restrict__ x,
-                                                               const float* __restrict__ ca, int C, int CG, long HW,
-                                                               float* __restrict__ mpart) {
+template <int V, class T, bool FUSED>
+__global__ __launch_bounds__(256) void cbam_pixel_stats_kernel(const T* __restrict__ x, float* __restrict__ ca,
+                                                               int C, int CG, long HW, float* __restrict__ mpart,
+                                                               const float* __restrict__ psum,
+                                                               const float* __restrict__ pmax, int parts,
+                                                               float inv_hw, const float* __restrict__ w1,
+                                                               const float* __restrict__ w2, int hid) {
+  extern __shared__ float sh[];
   const int b = blockIdx.z, g = blockIdx.y, G = gridDim.y;
-  const long p = ((long)blockIdx.x * 256 + threadIdx.x) * V;
-  if (p >= HW) return;
   const int c0 = g * CG;
   const int c1 = (c0 + CG < C) ? c0 + CG : C;
-  const float* xb = x + ((long)b * C) * HW + p;
-  const float* cab = ca + (long)b * C;
+  const float* cab;
+  if (FUSED) {
+    float* gs = sh + 2 * C + 128;
+    gate_mlp<true>(psum, pmax, parts, C, inv_hw, w1, nullptr, w2, nullptr, hid, b, sh, sh + C, sh + 2 * C, c0, c1 - c0,
+                   gs);
+    if (blockIdx.x == 0)
+      for (int i = threadIdx.x; i < c1 - c0; i += 256) ca[(long)b * C + c0 + i] = gs[i];
+    cab = gs - c0;
+  } else {
+    cab = ca + (long)b * C;
+  }
+  const long p = ((long)blockIdx.x * 256 + threadIdx.x) * V;
+  if (p >= HW) return;
+  const T* xb = x + ((long)b * C) * HW + p;
   float* sp = mpart + ((long)(b * G + g) * 2) * HW + p;
   if (V == 4) {
     f32x4 s = {0.f, 0.f, 0.f, 0.f}, m = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
@@ -224,7 +278,7 @@ __global__ __launch_bounds__(256) void cbam_pixel_stats_kernel(const float* __re
     for (; c + 8 <= c1; c += 8) {
       f32x4 v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const f32x4*>(xb + (long)(c + u) * HW);
+      for (int u = 0; u < 8; ++u) v[u] = ld4(xb + (long)(c + u) * HW);
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const f32x4 o = cab[c + u] * v[u];
@@ -233,7 +287,7 @@ __global__ __launch_bounds__(256) void cbam_pixel_stats_kernel(const float* __re
       }
     }
     for (; c < c1; ++c) {
-      const f32x4 o = cab[c] * *reinterpret_cast<const f32x4*>(xb + (long)c * HW);
+      const f32x4 o = cab[c] * ld4(xb + (long)c * HW);
       s += o;
       m.x = fmaxf(m.x, o.x); m.y = fmaxf(m.y, o.y); m.z = fmaxf(m.z, o.z); m.w = fmaxf(m.w, o.w);
     }
@@ -245,7 +299,7 @@ __global__ __launch_bounds__(256) void cbam_pixel_stats_kernel(const float* __re
     for (; c + 8 <= c1; c += 8) {
       float v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = xb[(long)(c + u) * HW];
+      for (int u = 0; u < 8; ++u) v[u] = ld1(xb + (long)(c + u) * HW);
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const float o = cab[c + u] * v[u];
@@ -254,7 +308,7 @@ __global__ __launch_bounds__(256) void cbam_pixel_stats_kernel(const float* __re
       }
     }
     for (; c < c1; ++c) {
-      const float o = cab[c] * xb[(long)c * HW];
+      const float o = cab[c] * ld1(xb + (long)c * HW);
       s += o;
       m = fmaxf(m, o);
     }
@@ -263,8 +317,26 @@ __global__ __launch_bounds__(256) void cbam_pixel_stats_kernel(const float* __re
   }
 }
 
-// CBAM pass 2b: sa = sigmoid(conv7x7([mean_c o ; max_c o]), zero pad 3, no bias) on 16x16 output tiles, the
-// 22x22 halo of both maps (combined over the G channel groups) staged in LDS. grid = (tiles_x, tiles_y, images).
+// mean / max over the channel groups of pixel (yy, xx), zero outside the image (conv2d's zero padding of the
+// [mean; max] map, cbam_block.py:33-37)
+__device__ __forceinline__ float2 cbam_map_at(const float* __restrict__ mp, int G, long HW, int H, int W, int yy,
+                                              int xx, float invC) {
+  float s = 0.f, m = 0.f;
+  if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
+    const float* q = mp + (long)yy * W + xx;
+    m = -INFINITY;
+    for (int g = 0; g < G; ++g) {
+      s += q[(long)(2 * g) * HW];
+      m = fmaxf(m, q[(long)(2 * g + 1) * HW]);
+    }
+    s *= invC;
+  }
+  return make_float2(s, m);
+}
+
+// CBAM pass 2b (split path): sa = sigmoid(conv7x7([mean_c o ; max_c o]), zero pad 3, no bias) on 16x16 output
+// tiles, the 22x22 halo of both maps (combined over the G channel groups) staged in LDS.
+// grid = (tiles_x, tiles_y, images).
 __global__ __launch_bounds__(256) void cbam_sa_kernel(const float* __restrict__ mpart, int G, int C, int H, int W,
                                                       const float* __restrict__ wsa, float* __restrict__ sa) {
   __shared__ float mm[2][22][23];
@@ -277,19 +349,9 @@ __global__ __launch_bounds__(256) void cbam_sa_kernel(const float* __restrict__ 
   const float invC = 1.0f / (float)C;
   for (int i = tid; i < 22 * 22; i += 256) {
     const int ty = i / 22, tx = i % 22;
-    const int yy = oy + ty, xx = ox + tx;
-    float s = 0.f, m = 0.f;
-    if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
-      const float* q = mpart + (long)b * G * 2 * HW + (long)yy * W + xx;
-      m = -INFINITY;
-      for (int g = 0; g < G; ++g) {
-        s += q[(long)(2 * g) * HW];
-        m = fmaxf(m, q[(long)(2 * g + 1) * HW]);
-      }
-      s *= invC;
-    }
-    mm[0][ty][tx] = s;
-    mm[1][ty][tx] = m;
+    const float2 v = cbam_map_at(mpart + (long)b * G * 2 * HW, G, HW, H, W, oy + ty, ox + tx, invC);
+    mm[0][ty][tx] = v.x;
+    mm[1][ty][tx] = v.y;
   }
   __syncthreads();
   const int ly = tid >> 4, lx = tid & 15;
@@ -305,9 +367,9 @@ __global__ __launch_bounds__(256) void cbam_sa_kernel(const float* __restrict__ 
   sa[(long)b * HW + (long)py * W + px] = sigmoidf_(z);
 }
 
-// CBAM pass 3: y = sa[p] * (ca[c] * x). grid = (ceil(HW / (256*V)), ceil(C / 8), images).
-template <int V>
-__global__ __launch_bounds__(256) void cbam_apply_kernel(const float* __restrict__ x, float* __restrict__ y,
+// CBAM pass 3 (split path): y = sa[p] * (ca[c] * x). grid = (ceil(HW / (256*V)), ceil(C / 8), images).
+template <int V, class T>
+__global__ __launch_bounds__(256) void cbam_apply_kernel(const T* __restrict__ x, T* __restrict__ y,
                                                          const float* __restrict__ ca, const float* __restrict__ sa,
                                                          int C, long HW) {
   const int b = blockIdx.z;
@@ -315,37 +377,101 @@ __global__ __launch_bounds__(256) void cbam_apply_kernel(const float* __restrict
   if (p >= HW) return;
   const int c0 = blockIdx.y * 8;
   const int n = (C - c0 < 8) ? C - c0 : 8;
-  const float* xb = x + ((long)b * C + c0) * HW + p;
-  float* yb = y + ((long)b * C + c0) * HW + p;
+  const T* xb = x + ((long)b * C + c0) * HW + p;
+  T* yb = y + ((long)b * C + c0) * HW + p;
   const float* cab = ca + (long)b * C + c0;
   if (V == 4) {
     const f32x4 s4 = *reinterpret_cast<const f32x4*>(sa + (long)b * HW + p);
     if (n == 8) {
       f32x4 v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const f32x4*>(xb + (long)u * HW);
+      for (int u = 0; u < 8; ++u) v[u] = ld4(xb + (long)u * HW);
 #pragma unroll
-      for (int u = 0; u < 8; ++u) *reinterpret_cast<f32x4*>(yb + (long)u * HW) = s4 * (cab[u] * v[u]);
+      for (int u = 0; u < 8; ++u) st4(yb + (long)u * HW, s4 * (cab[u] * v[u]));
     } else {
-      for (int u = 0; u < n; ++u)
-        *reinterpret_cast<f32x4*>(yb + (long)u * HW) = s4 * (cab[u] * *reinterpret_cast<const f32x4*>(xb + (long)u * HW));
+      for (int u = 0; u < n; ++u) st4(yb + (long)u * HW, s4 * (cab[u] * ld4(xb + (long)u * HW)));
     }
   } else {
     const float s = sa[(long)b * HW + p];
-    for (int u = 0; u < n; ++u) yb[(long)u * HW] = s * (cab[u] * xb[(long)u * HW]);
+    for (int u = 0; u < n; ++u) st1(yb + (long)u * HW, s * (cab[u] * ld1(xb + (long)u * HW)));
   }
+}
+
+// CBAM pass 3 (fused path): spatial gate + apply. Workgroup = 1024 consecutive pixels (4 per lane) x up to 64
+// channels of one image. The rows those pixels touch, +-3 rows of halo and 3 columns of zero padding each side, of
+// the [mean; max] map are combined from the G group partials into LDS; each lane then evaluates the 7x7 conv
+// (+ sigmoid) at its 4 pixels and streams y = sa * (ca * x) over the channels with 8 vector loads in flight.
+// grid = (ceil(HW / 1024), ceil(C / 64), images); dynamic LDS = 2 * nrows * (W + 6) floats.
+constexpr int kCbamApplyC = 64;
+template <class T>
+__global__ __launch_bounds__(256) void cbam_sa_apply_kernel(const T* __restrict__ x, T* __restrict__ y,
+                                                            const float* __restrict__ ca,
+                                                            const float* __restrict__ mpart, int G, int C, int H,
+                                                            int W, const float* __restrict__ wsa) {
+  extern __shared__ float mm[];  // [2][nrows][W + 6]
+  __shared__ float wk[98];
+  const int b = blockIdx.z;
+  const long HW = (long)H * W;
+  const int tid = threadIdx.x;
+  const long pb0 = (long)blockIdx.x * 1024;
+  const long pb1 = (pb0 + 1024 < HW) ? pb0 + 1024 : HW;
+  const int r0 = (int)(pb0 / W) - 3;
+  const int nrows = (int)((pb1 - 1) / W) + 4 - r0;
+  const int WS = W + 6;
+  if (tid < 98) wk[tid] = wsa[tid];
+  const float invC = 1.0f / (float)C;
+  const float* mp = mpart + (long)b * G * 2 * HW;
+  for (int i = tid; i < nrows * WS; i += 256) {
+    const int ry = i / WS, rx = i - ry * WS;
+    const float2 v = cbam_map_at(mp, G, HW, H, W, r0 + ry, rx - 3, invC);
+    mm[i] = v.x;
+    mm[nrows * WS + i] = v.y;
+  }
+  __syncthreads();
+  const long p = pb0 + 4L * tid;
+  if (p >= HW) return;
+  f32x4 s4;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const long pi = p + i;
+    const int py = (int)(pi / W), px = (int)(pi - (long)py * W);
+    const float* m0 = mm + (py - r0 - 3) * WS + px;  // tap (ky, kx) of map ci at m0[ci*nrows*WS + ky*WS + kx]
+    float z = 0.f;
+#pragma unroll
+    for (int ci = 0; ci < 2; ++ci)
+#pragma unroll
+      for (int ky = 0; ky < 7; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < 7; ++kx) z += wk[ci * 49 + ky * 7 + kx] * m0[ci * nrows * WS + ky * WS + kx];
+    s4[i] = sigmoidf_(z);
+  }
+  const int c0 = blockIdx.y * kCbamApplyC;
+  const int c1 = (c0 + kCbamApplyC < C) ? c0 + kCbamApplyC : C;
+  const float* cab = ca + (long)b * C;
+  const T* xb = x + (long)b * C * HW + p;
+  T* yb = y + (long)b * C * HW + p;
+  int c = c0;
+  for (; c + 8 <= c1; c += 8) {
+    f32x4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = ld4(xb + (long)(c + u) * HW);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) st4(yb + (long)(c + u) * HW, s4 * (cab[c + u] * v[u]));
+  }
+  for (; c < c1; ++c) st4(yb + (long)c * HW, s4 * (cab[c] * ld4(xb + (long)c * HW)));
 }
 
 // ------------------------------------------------------------------------------------------------
 // CA pass 1: row means (over W) and column means (over H) of each (b,c) plane -> yin[b][c][0..H+W).
-// One workgroup per plane; the plane streams through LDS in bands of <= 8192 floats (16-B loads when W % 4
+// One workgroup per plane; the plane streams through LDS in bands of <= 8192 floats (vector loads when W % 4
 // == 0), rows reduced by lane quads, columns accumulated in registers (W <= 1024).
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void ca_pool_kernel(const float* __restrict__ x, int H, int W, int RB,
+template <class T>
+__global__ __launch_bounds__(256) void ca_pool_kernel(const T* __restrict__ x, int H, int W, int RB,
                                                       float* __restrict__ yin) {
   extern __shared__ float band[];
   const long plane = blockIdx.x;
-  const float* p = x + plane * (long)H * W;
+  const T* p = x + plane * (long)H * W;
   float* o = yin + plane * (long)(H + W);
   const int tid = threadIdx.x;
   float col[4] = {0.f, 0.f, 0.f, 0.f};
@@ -353,12 +479,11 @@ __global__ __launch_bounds__(256) void ca_pool_kernel(const float* __restrict__ 
   for (int h0 = 0; h0 < H; h0 += RB) {
     const int rb = (H - h0 < RB) ? H - h0 : RB;
     const int n = rb * W;
-    const float* src = p + (long)h0 * W;
+    const T* src = p + (long)h0 * W;
     if ((W & 3) == 0) {
-      const float4* s4 = reinterpret_cast<const float4*>(src);
-      for (int i = tid; i < (n >> 2); i += 256) reinterpret_cast<float4*>(band)[i] = s4[i];
+      for (int i = tid; i < (n >> 2); i += 256) reinterpret_cast<f32x4*>(band)[i] = ld4(src + 4 * i);
     } else {
-      for (int i = tid; i < n; i += 256) band[i] = src[i];
+      for (int i = tid; i < n; i += 256) band[i] = ld1(src + i);
     }
     __syncthreads();
     for (int r = tid >> 2; r < rb; r += 64) {
@@ -447,9 +572,9 @@ static size_t ca_gate_lds_bytes(int C, int mip) {
 }
 
 // CA pass 3: y[b,c,h,w] = (x * a_w[b,c,w]) * a_h[b,c,h]; gate rows are [a_h (H) | a_w (W)].
-// grid = (planes, ceil(HW / (256*V))); V = 4 when W % 4 == 0 (a float4 never straddles two rows).
-template <int V>
-__global__ __launch_bounds__(256) void ca_apply_kernel(const float* __restrict__ x, float* __restrict__ y,
+// grid = (planes, ceil(HW / (256*V))); V = 4 when W % 4 == 0 (a vector never straddles two rows).
+template <int V, class T>
+__global__ __launch_bounds__(256) void ca_apply_kernel(const T* __restrict__ x, T* __restrict__ y,
                                                        const float* __restrict__ gate, int H, int W) {
   const long plane = blockIdx.x;
   const long HW = (long)H * W;
@@ -459,14 +584,14 @@ __global__ __launch_bounds__(256) void ca_apply_kernel(const float* __restrict__
   const float* g = gate + plane * (H + W);
   const float ah = g[h];
   if (V == 4) {
-    f32x4 v = *reinterpret_cast<const f32x4*>(x + plane * HW + e);
+    f32x4 v = ld4(x + plane * HW + e);
     v.x = (v.x * g[H + w]) * ah;
     v.y = (v.y * g[H + w + 1]) * ah;
     v.z = (v.z * g[H + w + 2]) * ah;
     v.w = (v.w * g[H + w + 3]) * ah;
-    *reinterpret_cast<f32x4*>(y + plane * HW + e) = v;
+    st4(y + plane * HW + e, v);
   } else {
-    y[plane * HW + e] = (x[plane * HW + e] * g[H + w]) * ah;
+    st1(y + plane * HW + e, (ld1(x + plane * HW + e) * g[H + w]) * ah);
   }
 }
 
@@ -485,7 +610,7 @@ YS_EXPORT size_t yolosod_se_workspace(int B, int C, int H, int W) {
   return s.off;
 }
 
-// plane segmentation of the per-plane statistics (parts per plane, floats per part) for an H*W plane, so a
+// plane segmentation of the per-plane statistics (parts per plane, elements per part) for an H*W plane, so a
 // producer epilogue (yolosod_bias_act_stats) can emit the partials the *_forward_pre entry points consume
 YS_EXPORT int yolosod_plane_parts(long HW, long* seg) {
   const PartPlan pp = part_plan(HW);
@@ -493,9 +618,10 @@ YS_EXPORT int yolosod_plane_parts(long HW, long* seg) {
   return pp.parts;
 }
 
-static int se_forward_impl(const float* x, float* y, int B, int C, int H, int W, const float* fc1_w,
-                           const float* fc1_b, const float* fc2_w, const float* fc2_b, int hidden,
-                           const float* psum_pre, void* workspace, size_t workspace_bytes, void* stream) {
+template <class T>
+static int se_forward_impl(const T* x, T* y, int B, int C, int H, int W, const float* fc1_w, const float* fc1_b,
+                           const float* fc2_w, const float* fc2_b, int hidden, const float* psum_pre, void* workspace,
+                           size_t workspace_bytes, void* stream) {
   YS_CHECK_ARG(x && y && fc1_w && fc1_b && fc2_w && fc2_b, "se: null pointer");
   YS_CHECK_ARG(B >= 0 && C > 0 && C <= 16384 && H > 0 && W > 0, "se: bad shape");
   YS_CHECK_ARG(hidden > 0 && hidden <= 64, "se: hidden=%d unsupported (1..64)", hidden);
@@ -506,21 +632,30 @@ static int se_forward_impl(const float* x, float* y, int B, int C, int H, int W,
   YS_CHECK_ARG(gate, "se: workspace too small (%zu)", workspace_bytes);
   hipStream_t st = (hipStream_t)stream;
   const long HW = (long)H * W;
-  const int ipc = images_per_chunk(B, (size_t)C * HW * sizeof(float));
+  const int ipc = images_per_chunk(B, (size_t)C * HW * sizeof(T));
   const PartPlan pp = part_plan(HW);
   const long xchunks = (HW % 4 == 0) ? (HW + 1023) / 1024 : (HW + 255) / 256;
-  const size_t lds = sizeof(float) * (2 * (size_t)C + 128);
+  const size_t lds = sizeof(float) * (3 * (size_t)C + 128);
+  const size_t lds_fused = sizeof(float) * (2 * (size_t)C + 136);
+  const bool fused = fused_gates() && lds_fused <= 64 * 1024;
+  YS_CHECK_ARG(lds <= 64 * 1024 || fused, "se: C=%d too large for the gate kernel", C);
   for (int b0 = 0; b0 < B; b0 += ipc) {
     const int nb = (B - b0 < ipc) ? B - b0 : ipc;
     const long off = (long)b0 * C * HW;
     const float* ps = (psum_pre ? psum_pre : psum) + (long)b0 * C * pp.parts;
     if (!psum_pre)
-      hipLaunchKernelGGL((plane_part_stats_kernel<false>), dim3((unsigned)(nb * C * pp.parts)), dim3(256), 0, st,
+      hipLaunchKernelGGL((plane_part_stats_kernel<false, T>), dim3((unsigned)(nb * C * pp.parts)), dim3(256), 0, st,
                          x + off, HW, pp.parts, pp.seg, psum + (long)b0 * C * pp.parts, nullptr);
-    hipLaunchKernelGGL((channel_gate_kernel<false>), dim3(nb), dim3(256), lds, st, ps, nullptr, pp.parts, C,
-                       1.0f / (float)HW, fc1_w, fc1_b, fc2_w, fc2_b, hidden, gate + (long)b0 * C);
-    hipLaunchKernelGGL(plane_scale_kernel, dim3((unsigned)xchunks, (unsigned)((C + 7) / 8), (unsigned)nb), dim3(256),
-                       0, st, x + off, y + off, gate + (long)b0 * C, C, HW, mall_reverse());
+    const dim3 grid((unsigned)xchunks, (unsigned)((C + 7) / 8), (unsigned)nb);
+    if (fused) {
+      hipLaunchKernelGGL((plane_scale_kernel<T, true>), grid, dim3(256), lds_fused, st, x + off, y + off, nullptr, C, HW,
+                         mall_reverse(), ps, pp.parts, 1.0f / (float)HW, fc1_w, fc1_b, fc2_w, fc2_b, hidden);
+    } else {
+      hipLaunchKernelGGL((channel_gate_kernel<false>), dim3(nb), dim3(256), lds, st, ps, nullptr, pp.parts, C,
+                         1.0f / (float)HW, fc1_w, fc1_b, fc2_w, fc2_b, hidden, gate + (long)b0 * C);
+      hipLaunchKernelGGL((plane_scale_kernel<T, false>), grid, dim3(256), 0, st, x + off, y + off, gate + (long)b0 * C,
+                         C, HW, mall_reverse(), nullptr, 0, 0.f, nullptr, nullptr, nullptr, nullptr, 0);
+    }
   }
   YS_CHECK_LAUNCH("se");
   return 0;
@@ -543,6 +678,14 @@ YS_EXPORT int yolosod_se_forward_pre(const float* x, float* y, int B, int C, int
                          stream);
 }
 
+// bf16 storage variants (x, y: bf16 bit patterns; parameters and partials fp32)
+YS_EXPORT int yolosod_se_forward_bf16(const bf16_t* x, bf16_t* y, int B, int C, int H, int W, const float* fc1_w,
+                                      const float* fc1_b, const float* fc2_w, const float* fc2_b, int hidden,
+                                      const float* psum, void* workspace, size_t workspace_bytes, void* stream) {
+  return se_forward_impl(x, y, B, C, H, W, fc1_w, fc1_b, fc2_w, fc2_b, hidden, psum, workspace, workspace_bytes,
+                         stream);
+}
+
 // channel groups of the CBAM per-pixel pass: 32 channels each (fixed, for batch-invariant sums); the partial
 // maps cost 2/32 of x in extra traffic.
 constexpr int kCbamGroup = 32;
@@ -560,9 +703,10 @@ YS_EXPORT size_t yolosod_cbam_workspace(int B, int C, int H, int W) {
   return s.off;
 }
 
-static int cbam_forward_impl(const float* x, float* y, int B, int C, int H, int W, const float* fc0_w,
-                             const float* fc2_w, int hidden, const float* sa_w, const float* psum_pre,
-                             const float* pmax_pre, void* workspace, size_t workspace_bytes, void* stream) {
+template <class T>
+static int cbam_forward_impl(const T* x, T* y, int B, int C, int H, int W, const float* fc0_w, const float* fc2_w,
+                             int hidden, const float* sa_w, const float* psum_pre, const float* pmax_pre,
+                             void* workspace, size_t workspace_bytes, void* stream) {
   YS_CHECK_ARG(x && y && fc0_w && fc2_w && sa_w, "cbam: null pointer");
   YS_CHECK_ARG(B >= 0 && C > 0 && C <= 16384 && H > 0 && W > 0, "cbam: bad shape");
   YS_CHECK_ARG(hidden > 0 && hidden <= 64, "cbam: hidden=%d unsupported (1..64)", hidden);
@@ -570,7 +714,7 @@ static int cbam_forward_impl(const float* x, float* y, int B, int C, int H, int 
   const long HW = (long)H * W;
   const int V = (HW % 4 == 0) ? 4 : 1;
   const long pxb = (HW + 256 * V - 1) / (256 * V);
-  const int ipc = images_per_chunk(B, (size_t)C * HW * sizeof(float));
+  const int ipc = images_per_chunk(B, (size_t)C * HW * sizeof(T));
   const int G = (C + kCbamGroup - 1) / kCbamGroup;
   Carver cv(workspace, workspace_bytes);
   float* psum = cv.take<float>((size_t)B * C * part_plan((long)H * W).parts);
@@ -581,7 +725,12 @@ static int cbam_forward_impl(const float* x, float* y, int B, int C, int H, int 
   YS_CHECK_ARG(sa, "cbam: workspace too small (%zu)", workspace_bytes);
   hipStream_t st = (hipStream_t)stream;
   const PartPlan pp = part_plan(HW);
-  const size_t lds = sizeof(float) * (2 * (size_t)C + 128);
+  const size_t lds = sizeof(float) * (3 * (size_t)C + 128);
+  // fused launches: gate + pixel statistics, then spatial gate + apply (1024-pixel workgroups, halo rows in LDS)
+  const int nrows_max = (int)((1023 + W - 1) / W) + 8;
+  const size_t lds_sa = sizeof(float) * 2 * (size_t)nrows_max * (W + 6);
+  const bool fused = fused_gates() && V == 4 && lds <= 64 * 1024 && lds_sa <= 64 * 1024;
+  YS_CHECK_ARG(lds <= 64 * 1024, "cbam: C=%d too large for the gate kernel", C);
   for (int b0 = 0; b0 < B; b0 += ipc) {
     const int nb = (B - b0 < ipc) ? B - b0 : ipc;
     const long off = (long)b0 * C * HW;
@@ -590,22 +739,32 @@ static int cbam_forward_impl(const float* x, float* y, int B, int C, int H, int 
     float* cab = ca + (long)b0 * C;
     float* sab = sa + (long)b0 * HW;
     if (!psum_pre)
-      hipLaunchKernelGGL((plane_part_stats_kernel<true>), dim3((unsigned)(nb * C * pp.parts)), dim3(256), 0, st,
+      hipLaunchKernelGGL((plane_part_stats_kernel<true, T>), dim3((unsigned)(nb * C * pp.parts)), dim3(256), 0, st,
                          x + off, HW, pp.parts, pp.seg, psum + (long)b0 * C * pp.parts, pmax + (long)b0 * C * pp.parts);
+    dim3 gs((unsigned)pxb, G, nb);
+    if (fused) {
+      hipLaunchKernelGGL((cbam_pixel_stats_kernel<4, T, true>), gs, dim3(256), lds, st, x + off, cab, C, kCbamGroup,
+                         HW, mpart, ps, pm, pp.parts, 1.0f / (float)HW, fc0_w, fc2_w, hidden);
+      dim3 ga((unsigned)((HW + 1023) / 1024), (unsigned)((C + kCbamApplyC - 1) / kCbamApplyC), nb);
+      hipLaunchKernelGGL((cbam_sa_apply_kernel<T>), ga, dim3(256), lds_sa, st, x + off, y + off, cab, mpart, G, C, H, W,
+                         sa_w);
+      continue;
+    }
     hipLaunchKernelGGL((channel_gate_kernel<true>), dim3(nb), dim3(256), lds, st, ps, pm, pp.parts, C,
                        1.0f / (float)HW, fc0_w, nullptr, fc2_w, nullptr, hidden, cab);
-    dim3 gs((unsigned)pxb, G, nb);
     if (V == 4)
-      hipLaunchKernelGGL((cbam_pixel_stats_kernel<4>), gs, dim3(256), 0, st, x + off, cab, C, kCbamGroup, HW, mpart);
+      hipLaunchKernelGGL((cbam_pixel_stats_kernel<4, T, false>), gs, dim3(256), 0, st, x + off, cab, C, kCbamGroup, HW,
+                         mpart, nullptr, nullptr, 0, 0.f, nullptr, nullptr, 0);
     else
-      hipLaunchKernelGGL((cbam_pixel_stats_kernel<1>), gs, dim3(256), 0, st, x + off, cab, C, kCbamGroup, HW, mpart);
+      hipLaunchKernelGGL((cbam_pixel_stats_kernel<1, T, false>), gs, dim3(256), 0, st, x + off, cab, C, kCbamGroup, HW,
+                         mpart, nullptr, nullptr, 0, 0.f, nullptr, nullptr, 0);
     hipLaunchKernelGGL(cbam_sa_kernel, dim3((W + 15) / 16, (H + 15) / 16, nb), dim3(256), 0, st, mpart, G, C, H, W,
                        sa_w, sab);
     dim3 ga((unsigned)pxb, (C + 7) / 8, nb);
     if (V == 4)
-      hipLaunchKernelGGL((cbam_apply_kernel<4>), ga, dim3(256), 0, st, x + off, y + off, cab, sab, C, HW);
+      hipLaunchKernelGGL((cbam_apply_kernel<4, T>), ga, dim3(256), 0, st, x + off, y + off, cab, sab, C, HW);
     else
-      hipLaunchKernelGGL((cbam_apply_kernel<1>), ga, dim3(256), 0, st, x + off, y + off, cab, sab, C, HW);
+      hipLaunchKernelGGL((cbam_apply_kernel<1, T>), ga, dim3(256), 0, st, x + off, y + off, cab, sab, C, HW);
   }
   YS_CHECK_LAUNCH("cbam");
   return 0;
@@ -614,7 +773,7 @@ static int cbam_forward_impl(const float* x, float* y, int B, int C, int H, int 
 YS_EXPORT int yolosod_cbam_forward(const float* x, float* y, int B, int C, int H, int W, const float* fc0_w,
                                    const float* fc2_w, int hidden, const float* sa_w, void* workspace,
                                    size_t workspace_bytes, void* stream) {
-  return cbam_forward_impl(x, y, B, C, H, W, fc0_w, fc2_w, hidden, sa_w, nullptr, nullptr, workspace,
+  return cbam_forward_impl(x, y, B, C, H, W, fc0_w, fc2_w, hidden, sa_w, (const float*)nullptr, nullptr, workspace,
                            workspace_bytes, stream);
 }
 
@@ -627,6 +786,15 @@ YS_EXPORT int yolosod_cbam_forward_pre(const float* x, float* y, int B, int C, i
                            stream);
 }
 
+// bf16 storage variant; psum / pmax may both be NULL (statistics pass over x) or both given (from the producer)
+YS_EXPORT int yolosod_cbam_forward_bf16(const bf16_t* x, bf16_t* y, int B, int C, int H, int W, const float* fc0_w,
+                                        const float* fc2_w, int hidden, const float* sa_w, const float* psum,
+                                        const float* pmax, void* workspace, size_t workspace_bytes, void* stream) {
+  YS_CHECK_ARG((psum == nullptr) == (pmax == nullptr), "cbam_bf16: give both partials or neither");
+  return cbam_forward_impl(x, y, B, C, H, W, fc0_w, fc2_w, hidden, sa_w, psum, pmax, workspace, workspace_bytes,
+                           stream);
+}
+
 YS_EXPORT size_t yolosod_ca_workspace(int B, int C, int H, int W) {
   Sizer s;
   s.take<float>((size_t)B * C * (H + W));  // pooled
@@ -634,11 +802,12 @@ YS_EXPORT size_t yolosod_ca_workspace(int B, int C, int H, int W) {
   return s.off;
 }
 
-static int ca_forward_impl(const float* x, float* y, int B, int C, int H, int W, const float* conv1_w,
-                           const float* conv1_b, int mip, const float* bn_w, const float* bn_b, const float* bn_mean,
-                           const float* bn_var, float bn_eps, const float* convh_w, const float* convh_b,
-                           const float* convw_w, const float* convw_b, const float* yin_pre, void* workspace,
-                           size_t workspace_bytes, void* stream) {
+template <class T>
+static int ca_forward_impl(const T* x, T* y, int B, int C, int H, int W, const float* conv1_w, const float* conv1_b,
+                           int mip, const float* bn_w, const float* bn_b, const float* bn_mean, const float* bn_var,
+                           float bn_eps, const float* convh_w, const float* convh_b, const float* convw_w,
+                           const float* convw_b, const float* yin_pre, void* workspace, size_t workspace_bytes,
+                           void* stream) {
   YS_CHECK_ARG(x && y && conv1_w && conv1_b && bn_w && bn_b && bn_mean && bn_var && convh_w && convh_b && convw_w &&
                    convw_b,
                "ca: null pointer");
@@ -659,23 +828,23 @@ static int ca_forward_impl(const float* x, float* y, int B, int C, int H, int W,
   const size_t pool_lds = sizeof(float) * (size_t)RB * W;
   const int V = (W % 4 == 0) ? 4 : 1;
   const unsigned apply_y = (unsigned)((HW + 256 * V - 1) / (256 * V));
-  const int ipc = images_per_chunk(B, (size_t)C * HW * sizeof(float));
+  const int ipc = images_per_chunk(B, (size_t)C * HW * sizeof(T));
   for (int b0 = 0; b0 < B; b0 += ipc) {
     const int nb = (B - b0 < ipc) ? B - b0 : ipc;
     const long off = (long)b0 * C * HW;
     const long goff = (long)b0 * C * (H + W);
     if (!yin_pre)
-      hipLaunchKernelGGL(ca_pool_kernel, dim3(nb * C), dim3(256), pool_lds, st, x + off, H, W, RB, yin + goff);
+      hipLaunchKernelGGL((ca_pool_kernel<T>), dim3(nb * C), dim3(256), pool_lds, st, x + off, H, W, RB, yin + goff);
     hipLaunchKernelGGL(ca_gate_kernel, dim3((H + W + 15) / 16, nb), dim3(256), gate_lds, st,
                        (yin_pre ? yin_pre : yin) + goff, C, H, W,
                        mip, conv1_w, conv1_b, bn_w, bn_b, bn_mean, bn_var, bn_eps, convh_w, convh_b, convw_w, convw_b,
                        gate + goff);
     if (V == 4)
-      hipLaunchKernelGGL((ca_apply_kernel<4>), dim3(nb * C, apply_y), dim3(256), 0, st, x + off, y + off, gate + goff,
-                         H, W);
+      hipLaunchKernelGGL((ca_apply_kernel<4, T>), dim3(nb * C, apply_y), dim3(256), 0, st, x + off, y + off,
+                         gate + goff, H, W);
     else
-      hipLaunchKernelGGL((ca_apply_kernel<1>), dim3(nb * C, apply_y), dim3(256), 0, st, x + off, y + off, gate + goff,
-                         H, W);
+      hipLaunchKernelGGL((ca_apply_kernel<1, T>), dim3(nb * C, apply_y), dim3(256), 0, st, x + off, y + off,
+                         gate + goff, H, W);
   }
   YS_CHECK_LAUNCH("ca");
   return 0;
@@ -687,7 +856,7 @@ YS_EXPORT int yolosod_ca_forward(const float* x, float* y, int B, int C, int H, 
                                  const float* convh_b, const float* convw_w, const float* convw_b, void* workspace,
                                  size_t workspace_bytes, void* stream) {
   return ca_forward_impl(x, y, B, C, H, W, conv1_w, conv1_b, mip, bn_w, bn_b, bn_mean, bn_var, bn_eps, convh_w,
-                         convh_b, convw_w, convw_b, nullptr, workspace, workspace_bytes, stream);
+                         convh_b, convw_w, convw_b, (const float*)nullptr, workspace, workspace_bytes, stream);
 }
 
 // CA_Block with the pooled row / column means already computed by x's producer (yolosod_bias_act_capool):
@@ -698,6 +867,16 @@ YS_EXPORT int yolosod_ca_forward_pre(const float* x, float* y, int B, int C, int
                                      const float* convh_b, const float* convw_w, const float* convw_b,
                                      const float* yin, void* workspace, size_t workspace_bytes, void* stream) {
   YS_CHECK_ARG(yin, "ca_pre: null pooled means");
+  return ca_forward_impl(x, y, B, C, H, W, conv1_w, conv1_b, mip, bn_w, bn_b, bn_mean, bn_var, bn_eps, convh_w,
+                         convh_b, convw_w, convw_b, yin, workspace, workspace_bytes, stream);
+}
+
+// bf16 storage variant; yin may be NULL (pooling pass over x) or the producer's pooled means
+YS_EXPORT int yolosod_ca_forward_bf16(const bf16_t* x, bf16_t* y, int B, int C, int H, int W, const float* conv1_w,
+                                      const float* conv1_b, int mip, const float* bn_w, const float* bn_b,
+                                      const float* bn_mean, const float* bn_var, float bn_eps, const float* convh_w,
+                                      const float* convh_b, const float* convw_w, const float* convw_b,
+                                      const float* yin, void* workspace, size_t workspace_bytes, void* stream) {
   return ca_forward_impl(x, y, B, C, H, W, conv1_w, conv1_b, mip, bn_w, bn_b, bn_mean, bn_var, bn_eps, convh_w,
                          convh_b, convw_w, convw_b, yin, workspace, workspace_bytes, stream);
 }

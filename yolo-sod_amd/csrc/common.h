@@ -136,6 +136,43 @@ __device__ __forceinline__ float xor32_max(float v) {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
+// ---- bf16 storage (the bf16 model config: activations in HBM as bf16, arithmetic in fp32) ------------------
+// bf16 values cross the C ABI as their 16-bit patterns (uint16_t, torch.bfloat16's layout). Widening is exact
+// (a shift); narrowing rounds to nearest even (v_cvt_pk_bf16_f32), as torch's .to(torch.bfloat16).
+typedef uint16_t bf16_t;
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float((uint32_t)v << 16); }
+__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
+  const bf16x2_t v = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(uint32_t, v);
+}
+__device__ __forceinline__ bf16_t f2bf(float a) { return (bf16_t)(pack_bf16x2(a, 0.f) & 0xffffu); }
+
+// element loads / stores of either storage type, values in fp32 registers
+__device__ __forceinline__ float ld1(const float* p) { return *p; }
+__device__ __forceinline__ float ld1(const bf16_t* p) { return bf2f(*p); }
+__device__ __forceinline__ void st1(float* p, float v) { *p = v; }
+__device__ __forceinline__ void st1(bf16_t* p, float v) { *p = f2bf(v); }
+// 4 consecutive elements (16 B for fp32, 8 B for bf16; 4-element aligned)
+__device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+__device__ __forceinline__ f32x4 ld4(const bf16_t* p) {
+  const uint2 u = *reinterpret_cast<const uint2*>(p);
+  return f32x4{__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+               __uint_as_float(u.y & 0xffff0000u)};
+}
+// the values a bf16 store of v would hold, back in fp32
+__device__ __forceinline__ f32x4 round_bf16(f32x4 v) {
+  const uint32_t a = pack_bf16x2(v.x, v.y), b = pack_bf16x2(v.z, v.w);
+  return f32x4{__uint_as_float(a << 16), __uint_as_float(a & 0xffff0000u), __uint_as_float(b << 16),
+               __uint_as_float(b & 0xffff0000u)};
+}
+__device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+__device__ __forceinline__ void st4(bf16_t* p, f32x4 v) {
+  *reinterpret_cast<uint2*>(p) = make_uint2(pack_bf16x2(v.x, v.y), pack_bf16x2(v.z, v.w));
+}
+
 // Streaming passes that re-read a tensor written just before (> 256 MiB MALL) walk it back to front, so the tail the
 // producer wrote last is still in the Infinity Cache when the pass starts. YOLOSOD_MALL_REVERSE=0 restores the
 // forward order (A/B). Results are identical either way (each workgroup's work and summation order is unchanged).

@@ -11,11 +11,11 @@
 
 namespace ys {
 
-template <int ACT, bool RES, bool DUAL = false>
-__global__ __launch_bounds__(256) void bias_act_kernel(const float* __restrict__ y, float* __restrict__ out,
-                                                       const float* __restrict__ bias, const float* __restrict__ res,
+template <int ACT, bool RES, bool DUAL = false, class T = float>
+__global__ __launch_bounds__(256) void bias_act_kernel(const T* __restrict__ y, T* __restrict__ out,
+                                                       const float* __restrict__ bias, const T* __restrict__ res,
                                                        int C, long HW4, long y_bs4, long o_bs4, long r_bs4,
-                                                       long total4, int rev, float* __restrict__ out2 = nullptr,
+                                                       long total4, int rev, T* __restrict__ out2 = nullptr,
                                                        int c2lo = 0, long o2_bs4 = 0) {
   for (long i0 = (long)blockIdx.x * 256 + threadIdx.x; i0 < total4; i0 += (long)gridDim.x * 256) {
     const long i = rev ? total4 - 1 - i0 : i0;
@@ -23,18 +23,15 @@ __global__ __launch_bounds__(256) void bias_act_kernel(const float* __restrict__
     const long rem = i - b * (long)C * HW4;
     const int c = (int)(rem / HW4);
     const float bc = bias[c];
-    float4 v = reinterpret_cast<const float4*>(y)[b * y_bs4 + rem];
-    v.x += bc; v.y += bc; v.z += bc; v.w += bc;
+    f32x4 v = ld4(y + 4 * (b * y_bs4 + rem));
+    v += bc;
     if (ACT == 1) {
       v.x = siluf_(v.x); v.y = siluf_(v.y); v.z = siluf_(v.z); v.w = siluf_(v.w);
     }
-    if (RES) {
-      const float4 r = reinterpret_cast<const float4*>(res)[b * r_bs4 + rem];
-      v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
-    }
-    reinterpret_cast<float4*>(out)[b * o_bs4 + rem] = v;
+    if (RES) v += ld4(res + 4 * (b * r_bs4 + rem));
+    st4(out + 4 * (b * o_bs4 + rem), v);
     // second, packed copy of channels [c2lo, C): the next conv's input without a separate .contiguous() pass
-    if (DUAL && c >= c2lo) reinterpret_cast<float4*>(out2)[b * o2_bs4 + rem - (long)c2lo * HW4] = v;
+    if (DUAL && c >= c2lo) st4(out2 + 4 * (b * o2_bs4 + rem - (long)c2lo * HW4), v);
   }
 }
 
@@ -42,10 +39,10 @@ __global__ __launch_bounds__(256) void bias_act_kernel(const float* __restrict__
 // (smallobj_modules.py:87 mean, cbam_block.py:14-17 mean + max): workgroup (plane, k) handles the plane segment
 // [k*seg, (k+1)*seg) - the segmentation of channel_attention.hip's part_plan - and writes psum/pmax[plane*parts + k].
 // The gate then needs no extra pass over the producer's output.
-template <int ACT, bool RES, bool MAX>
-__global__ __launch_bounds__(256) void bias_act_stats_kernel(const float* __restrict__ y, float* __restrict__ out,
+template <int ACT, bool RES, bool MAX, class T = float>
+__global__ __launch_bounds__(256) void bias_act_stats_kernel(const T* __restrict__ y, T* __restrict__ out,
                                                              const float* __restrict__ bias,
-                                                             const float* __restrict__ res, int C, long HW,
+                                                             const T* __restrict__ res, int C, long HW,
                                                              long y_bs, long o_bs, long r_bs, int parts, long seg,
                                                              float* __restrict__ psum, float* __restrict__ pmax,
                                                              int rev) {
@@ -57,35 +54,34 @@ __global__ __launch_bounds__(256) void bias_act_stats_kernel(const float* __rest
   const long s0 = k * seg;
   const long s1 = (s0 + seg < HW) ? s0 + seg : HW;
   const float bc = bias[c];
-  const float4* y4 = reinterpret_cast<const float4*>(y + b * y_bs + (long)c * HW + s0);
-  const float4* r4 = RES ? reinterpret_cast<const float4*>(res + b * r_bs + (long)c * HW + s0) : nullptr;
-  float4* o4 = reinterpret_cast<float4*>(out + b * o_bs + (long)c * HW + s0);
+  const T* y4 = y + b * y_bs + (long)c * HW + s0;
+  const T* r4 = RES ? res + b * r_bs + (long)c * HW + s0 : nullptr;
+  T* o4 = out + b * o_bs + (long)c * HW + s0;
   const long n4 = (s1 - s0) >> 2;
   const int tid = threadIdx.x;
   float s = 0.f, m = -INFINITY;
   for (long i0 = tid; i0 < n4; i0 += 4 * 256) {
-    float4 v[4], r[4];
+    f32x4 v[4], r[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const long i = i0 + u * 256;
       if (i < n4) {
-        v[u] = y4[i];
-        if (RES) r[u] = r4[i];
+        v[u] = ld4(y4 + 4 * i);
+        if (RES) r[u] = ld4(r4 + 4 * i);
       }
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const long i = i0 + u * 256;
       if (i >= n4) continue;
-      float4 o = v[u];
-      o.x += bc; o.y += bc; o.z += bc; o.w += bc;
+      f32x4 o = v[u] + bc;
       if (ACT == 1) {
         o.x = siluf_(o.x); o.y = siluf_(o.y); o.z = siluf_(o.z); o.w = siluf_(o.w);
       }
-      if (RES) {
-        o.x += r[u].x; o.y += r[u].y; o.z += r[u].z; o.w += r[u].w;
-      }
-      o4[i] = o;
+      if (RES) o += r[u];
+      st4(o4 + 4 * i, o);
+      // statistics of the stored values (bf16 storage: of the rounded values, as a consumer re-reading out sees)
+      if (sizeof(T) == 2) o = round_bf16(o);
       s += (o.x + o.y) + (o.z + o.w);
       if (MAX) m = fmaxf(m, fmaxf(fmaxf(o.x, o.y), fmaxf(o.z, o.w)));
     }
@@ -109,10 +105,10 @@ __global__ __launch_bounds__(256) void bias_act_stats_kernel(const float* __rest
 // means (over W) and column means (over H) in yin[b][c][0..H+W), the input of CA's gate, so CA never runs its
 // pooling pass over the feature map. One workgroup per plane; the activated plane streams through LDS in bands of
 // <= 8192 floats (as channel_attention.hip's ca_pool_kernel): rows reduced by lane quads, columns in registers.
-template <int ACT, bool RES>
-__global__ __launch_bounds__(256) void bias_act_capool_kernel(const float* __restrict__ y, float* __restrict__ out,
+template <int ACT, bool RES, class T = float>
+__global__ __launch_bounds__(256) void bias_act_capool_kernel(const T* __restrict__ y, T* __restrict__ out,
                                                               const float* __restrict__ bias,
-                                                              const float* __restrict__ res, int C, int H, int W,
+                                                              const T* __restrict__ res, int C, int H, int W,
                                                               int RB, long y_bs, long o_bs, long r_bs,
                                                               float* __restrict__ yin) {
   extern __shared__ float band[];
@@ -120,9 +116,9 @@ __global__ __launch_bounds__(256) void bias_act_capool_kernel(const float* __res
   const long b = plane / C;
   const int c = (int)(plane - b * C);
   const long HW = (long)H * W;
-  const float* yp = y + b * y_bs + (long)c * HW;
-  float* op = out + b * o_bs + (long)c * HW;
-  const float* rp = RES ? res + b * r_bs + (long)c * HW : nullptr;
+  const T* yp = y + b * y_bs + (long)c * HW;
+  T* op = out + b * o_bs + (long)c * HW;
+  const T* rp = RES ? res + b * r_bs + (long)c * HW : nullptr;
   float* o = yin + plane * (long)(H + W);
   const float bc = bias[c];
   const int tid = threadIdx.x;
@@ -133,17 +129,14 @@ __global__ __launch_bounds__(256) void bias_act_capool_kernel(const float* __res
     const int n4 = (rb * W) >> 2;
     const long base = (long)h0 * W;
     for (int i = tid; i < n4; i += 256) {
-      float4 v = reinterpret_cast<const float4*>(yp + base)[i];
-      v.x += bc; v.y += bc; v.z += bc; v.w += bc;
+      f32x4 v = ld4(yp + base + 4 * i) + bc;
       if (ACT == 1) {
         v.x = siluf_(v.x); v.y = siluf_(v.y); v.z = siluf_(v.z); v.w = siluf_(v.w);
       }
-      if (RES) {
-        const float4 r = reinterpret_cast<const float4*>(rp + base)[i];
-        v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
-      }
-      reinterpret_cast<float4*>(op + base)[i] = v;
-      reinterpret_cast<float4*>(band)[i] = v;
+      if (RES) v += ld4(rp + base + 4 * i);
+      st4(op + base + 4 * i, v);
+      if (sizeof(T) == 2) v = round_bf16(v);  // pool the stored (rounded) values
+      reinterpret_cast<f32x4*>(band)[i] = v;
     }
     __syncthreads();
     for (int r = tid >> 2; r < rb; r += 64) {
@@ -297,12 +290,10 @@ __global__ __launch_bounds__(256) void thin_stats_reduce_kernel(const float* __r
 
 using namespace ys;
 
-// yolosod_bias_act + per-plane partial sums (and maxes when pmax != NULL) of `out` in psum/pmax[B*C*parts], with
-// the plane segmentation (parts, seg) that yolosod_se_forward_pre / yolosod_cbam_forward_pre expect
-// (yolosod_plane_parts). Requires HW % 4 == 0 and seg % 4 == 0.
-YS_EXPORT int yolosod_bias_act_stats(const float* y, long y_bstride, float* out, long out_bstride, const float* bias,
-                                     const float* res, long res_bstride, int B, int C, long HW, int act, int parts,
-                                     long seg, float* psum, float* pmax, void* stream) {
+template <class T>
+static int bias_act_stats_impl(const T* y, long y_bstride, T* out, long out_bstride, const float* bias, const T* res,
+                               long res_bstride, int B, int C, long HW, int act, int parts, long seg, float* psum,
+                               float* pmax, void* stream) {
   YS_CHECK_ARG(y && out && bias && psum, "bias_act_stats: null pointer");
   YS_CHECK_ARG(act == 0 || act == 1, "bias_act_stats: act=%d unsupported", act);
   YS_CHECK_ARG(HW % 4 == 0 && seg % 4 == 0 && y_bstride % 4 == 0 && out_bstride % 4 == 0 &&
@@ -310,15 +301,15 @@ YS_EXPORT int yolosod_bias_act_stats(const float* y, long y_bstride, float* out,
                "bias_act_stats: HW, seg and batch strides must be multiples of 4");
   YS_CHECK_ARG(parts >= 1 && seg >= 1 && (long)parts * seg >= HW && (long)(parts - 1) * seg < HW,
                "bias_act_stats: plane plan (%d x %ld) does not cover HW=%ld", parts, seg, HW);
-  YS_CHECK_ARG((((uintptr_t)y | (uintptr_t)out | (uintptr_t)(res ? res : y)) & 15) == 0,
-               "bias_act_stats: pointers must be 16-byte aligned");
+  YS_CHECK_ARG((((uintptr_t)y | (uintptr_t)out | (uintptr_t)(res ? res : y)) & (4 * sizeof(T) - 1)) == 0,
+               "bias_act_stats: pointers must be aligned to 4 elements");
   const long blocks = (long)B * C * parts;
   if (blocks == 0) return 0;
   YS_CHECK_ARG(blocks < (1L << 31), "bias_act_stats: too many planes");
   hipStream_t st = (hipStream_t)stream;
 #define YS_BAS(A_, R_, M_)                                                                                         \
-  hipLaunchKernelGGL((bias_act_stats_kernel<A_, R_, M_>), dim3((unsigned)blocks), dim3(256), 0, st, y, out, bias, res, \
-                     C, HW, y_bstride, out_bstride, res_bstride, parts, seg, psum, pmax, mall_reverse())
+  hipLaunchKernelGGL((bias_act_stats_kernel<A_, R_, M_, T>), dim3((unsigned)blocks), dim3(256), 0, st, y, out, bias, \
+                     res, C, HW, y_bstride, out_bstride, res_bstride, parts, seg, psum, pmax, mall_reverse())
   const bool mx = pmax != nullptr;
   if (act == 1) {
     if (res) { if (mx) YS_BAS(1, true, true); else YS_BAS(1, true, false); }
@@ -332,79 +323,52 @@ YS_EXPORT int yolosod_bias_act_stats(const float* y, long y_bstride, float* out,
   return 0;
 }
 
-// out[b*out_bstride + c*HW + p] = act(y[b*y_bstride + c*HW + p] + bias[c]) + res[b*res_bstride + c*HW + p]
-// act: 0 identity, 1 SiLU. res may be NULL. In place (out == y) allowed. HW and all strides multiples of 4.
-YS_EXPORT int yolosod_bias_act(const float* y, long y_bstride, float* out, long out_bstride, const float* bias,
-                               const float* res, long res_bstride, int B, int C, long HW, int act, void* stream) {
+// out = act(y + bias[c]) (+ res), optionally also channels [c2lo, C) packed into out2 (out2 == NULL: no copy)
+template <class T>
+static int bias_act_impl(const T* y, long y_bstride, T* out, long out_bstride, const float* bias, const T* res,
+                         long res_bstride, T* out2, long out2_bstride, int c2lo, int B, int C, long HW, int act,
+                         void* stream) {
   YS_CHECK_ARG(y && out && bias, "bias_act: null pointer");
   YS_CHECK_ARG(act == 0 || act == 1, "bias_act: act=%d unsupported", act);
-  YS_CHECK_ARG(HW % 4 == 0 && y_bstride % 4 == 0 && out_bstride % 4 == 0 && (!res || res_bstride % 4 == 0),
+  YS_CHECK_ARG(!out2 || (c2lo >= 0 && c2lo < C), "bias_act_dual: c2lo=%d outside [0, C=%d)", c2lo, C);
+  YS_CHECK_ARG(HW % 4 == 0 && y_bstride % 4 == 0 && out_bstride % 4 == 0 && (!res || res_bstride % 4 == 0) &&
+                   (!out2 || out2_bstride % 4 == 0),
                "bias_act: HW and batch strides must be multiples of 4");
-  YS_CHECK_ARG((((uintptr_t)y | (uintptr_t)out | (uintptr_t)(res ? res : y)) & 15) == 0,
-               "bias_act: pointers must be 16-byte aligned");
-  const long total4 = (long)B * C * (HW / 4);
-  if (total4 == 0) return 0;
-  long blocks = (total4 + 255) / 256;
-  if (blocks > 8192) blocks = 8192;
-  hipStream_t st = (hipStream_t)stream;
-  const long hw4 = HW / 4, yb = y_bstride / 4, ob = out_bstride / 4, rb = res_bstride / 4;
-  if (act == 1) {
-    if (res) hipLaunchKernelGGL((bias_act_kernel<1, true>), dim3(blocks), dim3(256), 0, st, y, out, bias, res, C, hw4, yb, ob, rb, total4, mall_reverse());
-    else hipLaunchKernelGGL((bias_act_kernel<1, false>), dim3(blocks), dim3(256), 0, st, y, out, bias, res, C, hw4, yb, ob, rb, total4, mall_reverse());
-  } else {
-    if (res) hipLaunchKernelGGL((bias_act_kernel<0, true>), dim3(blocks), dim3(256), 0, st, y, out, bias, res, C, hw4, yb, ob, rb, total4, mall_reverse());
-    else hipLaunchKernelGGL((bias_act_kernel<0, false>), dim3(blocks), dim3(256), 0, st, y, out, bias, res, C, hw4, yb, ob, rb, total4, mall_reverse());
-  }
-  YS_CHECK_LAUNCH("bias_act");
-  return 0;
-}
-
-// yolosod_bias_act that also writes channels [c2lo, C) of the result to out2 ([B, C - c2lo, HW], batch stride
-// out2_bstride). C2f feeds its Bottleneck chain from channel slices of the concat buffer; MIOpen needs packed
-// inputs, so without this every Bottleneck input was re-read and re-written by a copy kernel.
-YS_EXPORT int yolosod_bias_act_dual(const float* y, long y_bstride, float* out, long out_bstride, const float* bias,
-                                    const float* res, long res_bstride, float* out2, long out2_bstride, int c2lo,
-                                    int B, int C, long HW, int act, void* stream) {
-  YS_CHECK_ARG(y && out && bias && out2, "bias_act_dual: null pointer");
-  YS_CHECK_ARG(act == 0 || act == 1, "bias_act_dual: act=%d unsupported", act);
-  YS_CHECK_ARG(c2lo >= 0 && c2lo < C, "bias_act_dual: c2lo=%d outside [0, C=%d)", c2lo, C);
-  YS_CHECK_ARG(HW % 4 == 0 && y_bstride % 4 == 0 && out_bstride % 4 == 0 && out2_bstride % 4 == 0 &&
-                   (!res || res_bstride % 4 == 0),
-               "bias_act_dual: HW and batch strides must be multiples of 4");
-  YS_CHECK_ARG((((uintptr_t)y | (uintptr_t)out | (uintptr_t)out2 | (uintptr_t)(res ? res : y)) & 15) == 0,
-               "bias_act_dual: pointers must be 16-byte aligned");
+  YS_CHECK_ARG((((uintptr_t)y | (uintptr_t)out | (uintptr_t)(res ? res : y) | (uintptr_t)(out2 ? out2 : y)) &
+                (4 * sizeof(T) - 1)) == 0,
+               "bias_act: pointers must be aligned to 4 elements");
   const long total4 = (long)B * C * (HW / 4);
   if (total4 == 0) return 0;
   long blocks = (total4 + 255) / 256;
   if (blocks > 8192) blocks = 8192;
   hipStream_t st = (hipStream_t)stream;
   const long hw4 = HW / 4, yb = y_bstride / 4, ob = out_bstride / 4, rb = res_bstride / 4, o2 = out2_bstride / 4;
-#define YS_BAD(A_, R_)                                                                                        \
-  hipLaunchKernelGGL((bias_act_kernel<A_, R_, true>), dim3(blocks), dim3(256), 0, st, y, out, bias, res, C, hw4, \
-                     yb, ob, rb, total4, mall_reverse(), out2, c2lo, o2)
-  if (act == 1) {
-    if (res) YS_BAD(1, true); else YS_BAD(1, false);
+#define YS_BA(A_, R_, D_)                                                                                          \
+  hipLaunchKernelGGL((bias_act_kernel<A_, R_, D_, T>), dim3(blocks), dim3(256), 0, st, y, out, bias, res, C, hw4, yb, \
+                     ob, rb, total4, mall_reverse(), out2, c2lo, o2)
+  if (out2) {
+    if (act == 1) { if (res) YS_BA(1, true, true); else YS_BA(1, false, true); }
+    else { if (res) YS_BA(0, true, true); else YS_BA(0, false, true); }
   } else {
-    if (res) YS_BAD(0, true); else YS_BAD(0, false);
+    if (act == 1) { if (res) YS_BA(1, true, false); else YS_BA(1, false, false); }
+    else { if (res) YS_BA(0, true, false); else YS_BA(0, false, false); }
   }
-#undef YS_BAD
-  YS_CHECK_LAUNCH("bias_act_dual");
+#undef YS_BA
+  YS_CHECK_LAUNCH("bias_act");
   return 0;
 }
 
-// yolosod_bias_act + the CA_Block pooling of `out` (row means over W, then column means over H, per plane) into
-// yin[B*C*(H+W)], the layout yolosod_ca_forward_pre takes. Requires W % 4 == 0, W <= 1024 and 4-aligned strides.
-YS_EXPORT int yolosod_bias_act_capool(const float* y, long y_bstride, float* out, long out_bstride, const float* bias,
-                                      const float* res, long res_bstride, int B, int C, int H, int W, int act,
-                                      float* yin, void* stream) {
+template <class T>
+static int bias_act_capool_impl(const T* y, long y_bstride, T* out, long out_bstride, const float* bias, const T* res,
+                                long res_bstride, int B, int C, int H, int W, int act, float* yin, void* stream) {
   YS_CHECK_ARG(y && out && bias && yin, "bias_act_capool: null pointer");
   YS_CHECK_ARG(act == 0 || act == 1, "bias_act_capool: act=%d unsupported", act);
   YS_CHECK_ARG(B >= 0 && C > 0 && H > 0 && W > 0 && W % 4 == 0 && W <= 1024,
                "bias_act_capool: W=%d must be a multiple of 4 and <= 1024", W);
   YS_CHECK_ARG(y_bstride % 4 == 0 && out_bstride % 4 == 0 && (!res || res_bstride % 4 == 0),
                "bias_act_capool: batch strides must be multiples of 4");
-  YS_CHECK_ARG((((uintptr_t)y | (uintptr_t)out | (uintptr_t)(res ? res : y)) & 15) == 0,
-               "bias_act_capool: pointers must be 16-byte aligned");
+  YS_CHECK_ARG((((uintptr_t)y | (uintptr_t)out | (uintptr_t)(res ? res : y)) & (4 * sizeof(T) - 1)) == 0,
+               "bias_act_capool: pointers must be aligned to 4 elements");
   const long planes = (long)B * C;
   if (planes == 0) return 0;
   YS_CHECK_ARG(planes < (1L << 31), "bias_act_capool: too many planes");
@@ -413,14 +377,73 @@ YS_EXPORT int yolosod_bias_act_capool(const float* y, long y_bstride, float* out
   if (RB > H) RB = H;
   const size_t lds = sizeof(float) * (size_t)RB * W;
   hipStream_t st = (hipStream_t)stream;
-#define YS_BAC(A_, R_)                                                                                           \
-  hipLaunchKernelGGL((bias_act_capool_kernel<A_, R_>), dim3((unsigned)planes), dim3(256), lds, st, y, out, bias, res, \
-                     C, H, W, RB, y_bstride, out_bstride, res_bstride, yin)
+#define YS_BAC(A_, R_)                                                                                               \
+  hipLaunchKernelGGL((bias_act_capool_kernel<A_, R_, T>), dim3((unsigned)planes), dim3(256), lds, st, y, out, bias, \
+                     res, C, H, W, RB, y_bstride, out_bstride, res_bstride, yin)
   if (act == 1) { if (res) YS_BAC(1, true); else YS_BAC(1, false); }
   else { if (res) YS_BAC(0, true); else YS_BAC(0, false); }
 #undef YS_BAC
   YS_CHECK_LAUNCH("bias_act_capool");
   return 0;
+}
+
+// yolosod_bias_act + per-plane partial sums (and maxes when pmax != NULL) of `out` in psum/pmax[B*C*parts], with
+// the plane segmentation (parts, seg) that yolosod_se_forward_pre / yolosod_cbam_forward_pre expect
+// (yolosod_plane_parts). Requires HW % 4 == 0 and seg % 4 == 0.
+YS_EXPORT int yolosod_bias_act_stats(const float* y, long y_bstride, float* out, long out_bstride, const float* bias,
+                                     const float* res, long res_bstride, int B, int C, long HW, int act, int parts,
+                                     long seg, float* psum, float* pmax, void* stream) {
+  return bias_act_stats_impl(y, y_bstride, out, out_bstride, bias, res, res_bstride, B, C, HW, act, parts, seg, psum,
+                             pmax, stream);
+}
+
+// out[b*out_bstride + c*HW + p] = act(y[b*y_bstride + c*HW + p] + bias[c]) + res[b*res_bstride + c*HW + p]
+// act: 0 identity, 1 SiLU. res may be NULL. In place (out == y) allowed. HW and all strides multiples of 4.
+YS_EXPORT int yolosod_bias_act(const float* y, long y_bstride, float* out, long out_bstride, const float* bias,
+                               const float* res, long res_bstride, int B, int C, long HW, int act, void* stream) {
+  return bias_act_impl(y, y_bstride, out, out_bstride, bias, res, res_bstride, (float*)nullptr, 0L, 0, B, C, HW, act,
+                       stream);
+}
+
+// yolosod_bias_act that also writes channels [c2lo, C) of the result to out2 ([B, C - c2lo, HW], batch stride
+// out2_bstride). C2f feeds its Bottleneck chain from channel slices of the concat buffer; MIOpen needs packed
+// inputs, so without this every Bottleneck input was re-read and re-written by a copy kernel.
+YS_EXPORT int yolosod_bias_act_dual(const float* y, long y_bstride, float* out, long out_bstride, const float* bias,
+                                    const float* res, long res_bstride, float* out2, long out2_bstride, int c2lo,
+                                    int B, int C, long HW, int act, void* stream) {
+  YS_CHECK_ARG(out2, "bias_act_dual: null pointer");
+  return bias_act_impl(y, y_bstride, out, out_bstride, bias, res, res_bstride, out2, out2_bstride, c2lo, B, C, HW, act,
+                       stream);
+}
+
+// yolosod_bias_act + the CA_Block pooling of `out` (row means over W, then column means over H, per plane) into
+// yin[B*C*(H+W)], the layout yolosod_ca_forward_pre takes. Requires W % 4 == 0, W <= 1024 and 4-aligned strides.
+YS_EXPORT int yolosod_bias_act_capool(const float* y, long y_bstride, float* out, long out_bstride, const float* bias,
+                                      const float* res, long res_bstride, int B, int C, int H, int W, int act,
+                                      float* yin, void* stream) {
+  return bias_act_capool_impl(y, y_bstride, out, out_bstride, bias, res, res_bstride, B, C, H, W, act, yin, stream);
+}
+
+// bf16 storage variants of the three epilogues (y / out / res / out2: bf16 bit patterns; bias, statistics fp32).
+// mode 0: plain (out2 optional, NULL = none); statistics in the *_stats / *_capool entry points. The statistics are
+// of the stored (bf16-rounded) values.
+YS_EXPORT int yolosod_bias_act_bf16(const bf16_t* y, long y_bstride, bf16_t* out, long out_bstride, const float* bias,
+                                    const bf16_t* res, long res_bstride, bf16_t* out2, long out2_bstride, int c2lo,
+                                    int B, int C, long HW, int act, void* stream) {
+  return bias_act_impl(y, y_bstride, out, out_bstride, bias, res, res_bstride, out2, out2_bstride, c2lo, B, C, HW, act,
+                       stream);
+}
+YS_EXPORT int yolosod_bias_act_stats_bf16(const bf16_t* y, long y_bstride, bf16_t* out, long out_bstride,
+                                          const float* bias, const bf16_t* res, long res_bstride, int B, int C,
+                                          long HW, int act, int parts, long seg, float* psum, float* pmax,
+                                          void* stream) {
+  return bias_act_stats_impl(y, y_bstride, out, out_bstride, bias, res, res_bstride, B, C, HW, act, parts, seg, psum,
+                             pmax, stream);
+}
+YS_EXPORT int yolosod_bias_act_capool_bf16(const bf16_t* y, long y_bstride, bf16_t* out, long out_bstride,
+                                           const float* bias, const bf16_t* res, long res_bstride, int B, int C, int H,
+                                           int W, int act, float* yin, void* stream) {
+  return bias_act_capool_impl(y, y_bstride, out, out_bstride, bias, res, res_bstride, B, C, H, W, act, yin, stream);
 }
 
 // Thin fused 1x1 conv (+ bias + SiLU (+ res)) for Cout in {64, 128}, Cin in {64, 96, 128, 192, 256}, HW % 64 == 0,

@@ -86,8 +86,8 @@ __global__ __launch_bounds__(256) void detect_decode_kernel(DecodeArgs d) {
 // Each wave owns NTS consecutive 16-pixel groups of one level of one image.
 // ------------------------------------------------------------------------------------------------
 struct HeadArgs {
-  const float* fb[4];  // box tower features  [B][C2][HW]
-  const float* fc[4];  // class tower features [B][C3][HW]
+  const void* fb[4];   // box tower features  [B][C2][HW] (fp32 or bf16, the kernel's FT)
+  const void* fc[4];   // class tower features [B][C3][HW]
   const float* wb[4];  // [64][C2]
   const float* bb[4];  // [64]
   const float* wc[4];  // [nc][C3]
@@ -96,7 +96,6 @@ struct HeadArgs {
   float stride[4];
   int nl, nc, A;
   float* y;
-  int abl;  // timing ablation (debug only, YOLOSOD_HEAD_ABL): 1 skip feature loads, 2 skip stores
 };
 
 template <int C2, int C3, int NTS>
@@ -131,8 +130,8 @@ __global__ __launch_bounds__(256) void detect_head_kernel(HeadArgs d) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) bcr[r] = (4 * g + r < nc) ? d.bc[l][4 * g + r] : 0.f;
   }
-  const float* fbb = d.fb[l] + (long)b * C2 * HW;
-  const float* fcb = d.fc[l] + (long)b * C3 * HW;
+  const float* fbb = static_cast<const float*>(d.fb[l]) + (long)b * C2 * HW;
+  const float* fcb = static_cast<const float*>(d.fc[l]) + (long)b * C3 * HW;
   const int W = d.w[l];
   const float st = d.stride[l];
   float* yb = d.y + (long)b * (4 + nc) * d.A + d.a_off[l];
@@ -143,7 +142,7 @@ __global__ __launch_bounds__(256) void detect_head_kernel(HeadArgs d) {
     const int p = p0 + j;
     const bool ok = p < HW;
     float xb[C2 / 4], xc[C3 / 4];
-    if (p0 + 16 <= HW && !(d.abl & 1)) {  // full group (wave-uniform): plain strided loads, no per-load selects
+    if (p0 + 16 <= HW) {  // full group (wave-uniform): plain strided loads, no per-load selects
       const float* pb = fbb + (long)g * HW + p;
       const float* pc = fcb + (long)g * HW + p;
 #pragma unroll
@@ -152,9 +151,9 @@ __global__ __launch_bounds__(256) void detect_head_kernel(HeadArgs d) {
       for (int q = 0; q < C3 / 4; ++q) xc[q] = pc[(long)q * 4 * HW];
     } else {
 #pragma unroll
-      for (int q = 0; q < C2 / 4; ++q) xb[q] = (ok && !(d.abl & 1)) ? fbb[(long)(4 * q + g) * HW + p] : 0.f;
+      for (int q = 0; q < C2 / 4; ++q) xb[q] = ok ? fbb[(long)(4 * q + g) * HW + p] : 0.f;
 #pragma unroll
-      for (int q = 0; q < C3 / 4; ++q) xc[q] = (ok && !(d.abl & 1)) ? fcb[(long)(4 * q + g) * HW + p] : 0.f;
+      for (int q = 0; q < C3 / 4; ++q) xc[q] = ok ? fcb[(long)(4 * q + g) * HW + p] : 0.f;
     }
     f32x4 acc[5];
 #pragma unroll
@@ -188,7 +187,7 @@ __global__ __launch_bounds__(256) void detect_head_kernel(HeadArgs d) {
       e = xor32_sum(xor16_sum(e));
       dist[s] = e * __builtin_amdgcn_rcpf(sum);
     }
-    if (!ok || (d.abl & 2)) continue;
+    if (!ok) continue;
     const int iy = p / W, ix = p - iy * W;
     const float ax = (float)ix + 0.5f, ay = (float)iy + 0.5f;
     const float x1 = ax - dist[0], y1 = ay - dist[1];
@@ -212,7 +211,7 @@ __global__ __launch_bounds__(256) void detect_head_kernel(HeadArgs d) {
 // tiles' rows at once from a [q][g][j][t] image, conflict-free for the b128 lane groups) - the ~100 VGPRs that
 // held them now double-buffer the next 16-pixel group's feature loads, so the HBM latency of a group overlaps the
 // MFMAs and DFL of the previous one, at 3 waves per SIMD.
-template <int C2, int C3, int NTS>
+template <int C2, int C3, int NTS, class FT = float>
 __global__ __launch_bounds__(256, C3 > 64 ? 2 : 3) void detect_head_lds_kernel(HeadArgs d) {
   __shared__ __attribute__((aligned(16))) float wl[C2 * 64 + C3 * 16];
   float* wlb = wl;            // [C2/4 q][4 g][16 j][4 t] = W_box[16t + j][4q + g]
@@ -248,8 +247,8 @@ __global__ __launch_bounds__(256, C3 > 64 ? 2 : 3) void detect_head_lds_kernel(H
     for (int r = 0; r < 4; ++r) bbr[t][r] = d.bb[l][16 * t + 4 * g + r];
 #pragma unroll
   for (int r = 0; r < 4; ++r) bcr[r] = (4 * g + r < nc) ? d.bc[l][4 * g + r] : 0.f;
-  const float* fbb = d.fb[l] + (long)b * C2 * HW;
-  const float* fcb = d.fc[l] + (long)b * C3 * HW;
+  const FT* fbb = static_cast<const FT*>(d.fb[l]) + (long)b * C2 * HW;
+  const FT* fcb = static_cast<const FT*>(d.fc[l]) + (long)b * C3 * HW;
   const int W = d.w[l];
   const float st = d.stride[l];
   float* yb = d.y + (long)b * (4 + nc) * d.A + d.a_off[l];
@@ -259,24 +258,30 @@ __global__ __launch_bounds__(256, C3 > 64 ? 2 : 3) void detect_head_lds_kernel(H
   // feature loads are buffer loads on per-image descriptors: the lane's voffset is (channel g, pixel p), the
   // channel step 4q goes into the scalar soffset (no per-load 64-bit addresses to keep live), and pixels past the
   // level's end get an out-of-range voffset, which the hardware returns as 0
-  auto rsrc = [&](const float* base, int bytes) {
+  auto rsrc = [&](const FT* base, int bytes) {
     const unsigned long long a = (unsigned long long)base;
     return __builtin_amdgcn_make_buffer_rsrc(
         (void*)(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(a >> 32)) << 32) |
                 (unsigned)__builtin_amdgcn_readfirstlane((unsigned)a)),
         (short)0, __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
   };
-  const __amdgpu_buffer_rsrc_t rb = rsrc(fbb, C2 * HW * 4), rc = rsrc(fcb, C3 * HW * 4);
+  constexpr int ES = (int)sizeof(FT);
+  const __amdgpu_buffer_rsrc_t rb = rsrc(fbb, C2 * HW * ES), rc = rsrc(fcb, C3 * HW * ES);
+  // one feature element: fp32 as is, bf16 widened (exact)
+  auto ldf = [&](__amdgpu_buffer_rsrc_t r, unsigned vo, int so) -> float {
+    if constexpr (sizeof(FT) == 2)
+      return __uint_as_float((unsigned)__builtin_amdgcn_raw_buffer_load_b16(r, vo, so, 0) << 16);
+    else
+      return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, so, 0));
+  };
   float xb[2][C2 / 4], xc[2][C3 / 4];
   auto load_group = [&](int ts, float (&fb)[C2 / 4], float (&fcv)[C3 / 4]) {
     const int p = px0 + ts * 16 + j;
-    const unsigned vo = (p < HW && !(d.abl & 1)) ? (unsigned)((g * HW + p) * 4) : 0x80000000u;
+    const unsigned vo = (p < HW) ? (unsigned)((g * HW + p) * ES) : 0x80000000u;
 #pragma unroll
-    for (int q = 0; q < C2 / 4; ++q)
-      fb[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb, vo, q * 16 * HW, 0));
+    for (int q = 0; q < C2 / 4; ++q) fb[q] = ldf(rb, vo, q * 4 * ES * HW);
 #pragma unroll
-    for (int q = 0; q < C3 / 4; ++q)
-      fcv[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rc, vo, q * 16 * HW, 0));
+    for (int q = 0; q < C3 / 4; ++q) fcv[q] = ldf(rc, vo, q * 4 * ES * HW);
   };
   auto compute_group = [&](int ts, const float (&cb)[C2 / 4], const float (&cc)[C3 / 4]) {
     const int p0 = px0 + ts * 16;
@@ -322,7 +327,7 @@ __global__ __launch_bounds__(256, C3 > 64 ? 2 : 3) void detect_head_lds_kernel(H
       e = xor32_sum(xor16_sum(e));
       dist[s] = e * __builtin_amdgcn_rcpf(sum);
     }
-    if (!ok || (d.abl & 2)) return;
+    if (!ok) return;
     const int iy = p / W, ix = p - iy * W;
     const float ax = (float)ix + 0.5f, ay = (float)iy + 0.5f;
     const float x1 = ax - dist[0], y1 = ay - dist[1];
@@ -383,10 +388,10 @@ YS_EXPORT int yolosod_detect_decode(int nl, const float* const* maps, const int*
   return 0;
 }
 
-YS_EXPORT int yolosod_detect_head(int nl, const float* const* box_feat, const float* const* cls_feat, int c2, int c3,
-                                  const float* const* box_w, const float* const* box_b, const float* const* cls_w,
-                                  const float* const* cls_b, const int* heights, const int* widths,
-                                  const float* strides, int B, int nc, int reg_max, float* y, void* stream) {
+static int detect_head_impl(int nl, const void* const* box_feat, const void* const* cls_feat, int c2, int c3,
+                            const float* const* box_w, const float* const* box_b, const float* const* cls_w,
+                            const float* const* cls_b, const int* heights, const int* widths, const float* strides,
+                            int B, int nc, int reg_max, float* y, bool bf16, void* stream) {
   YS_CHECK_ARG(nl >= 1 && nl <= 4, "detect_head: nl=%d unsupported (1..4)", nl);
   YS_CHECK_ARG(box_feat && cls_feat && box_w && box_b && cls_w && cls_b && heights && widths && strides && y,
                "detect_head: null pointer");
@@ -418,22 +423,42 @@ YS_EXPORT int yolosod_detect_head(int nl, const float* const* box_feat, const fl
   d.blk_off[nl] = blk;
   d.A = off;
   d.y = y;
-  if (const char* e = getenv("YOLOSOD_HEAD_ABL")) d.abl = atoi(e);
   if (B == 0 || off == 0) return 0;
   const dim3 grid(blk, B);
+  hipStream_t st = (hipStream_t)stream;
+  if (bf16) {
+    if (c3 == 64) hipLaunchKernelGGL((detect_head_lds_kernel<64, 64, NTS, bf16_t>), grid, dim3(256), 0, st, d);
+    else hipLaunchKernelGGL((detect_head_lds_kernel<64, 128, NTS, bf16_t>), grid, dim3(256), 0, st, d);
+    YS_CHECK_LAUNCH("detect_head_bf16");
+    return 0;
+  }
   // default: weights in LDS, feature loads double-buffered; YOLOSOD_HEAD_V1=1: weights in registers (A/B)
   static const bool v1 = [] { const char* e = getenv("YOLOSOD_HEAD_V1"); return e && atoi(e) != 0; }();
   if (v1) {
-    if (c3 == 64)
-      hipLaunchKernelGGL((detect_head_kernel<64, 64, NTS>), grid, dim3(256), 0, (hipStream_t)stream, d);
-    else
-      hipLaunchKernelGGL((detect_head_kernel<64, 128, NTS>), grid, dim3(256), 0, (hipStream_t)stream, d);
+    if (c3 == 64) hipLaunchKernelGGL((detect_head_kernel<64, 64, NTS>), grid, dim3(256), 0, st, d);
+    else hipLaunchKernelGGL((detect_head_kernel<64, 128, NTS>), grid, dim3(256), 0, st, d);
   } else {
-    if (c3 == 64)
-      hipLaunchKernelGGL((detect_head_lds_kernel<64, 64, NTS>), grid, dim3(256), 0, (hipStream_t)stream, d);
-    else
-      hipLaunchKernelGGL((detect_head_lds_kernel<64, 128, NTS>), grid, dim3(256), 0, (hipStream_t)stream, d);
+    if (c3 == 64) hipLaunchKernelGGL((detect_head_lds_kernel<64, 64, NTS>), grid, dim3(256), 0, st, d);
+    else hipLaunchKernelGGL((detect_head_lds_kernel<64, 128, NTS>), grid, dim3(256), 0, st, d);
   }
   YS_CHECK_LAUNCH("detect_head");
   return 0;
+}
+
+YS_EXPORT int yolosod_detect_head(int nl, const float* const* box_feat, const float* const* cls_feat, int c2, int c3,
+                                  const float* const* box_w, const float* const* box_b, const float* const* cls_w,
+                                  const float* const* cls_b, const int* heights, const int* widths,
+                                  const float* strides, int B, int nc, int reg_max, float* y, void* stream) {
+  return detect_head_impl(nl, (const void* const*)box_feat, (const void* const*)cls_feat, c2, c3, box_w, box_b, cls_w,
+                          cls_b, heights, widths, strides, B, nc, reg_max, y, false, stream);
+}
+
+// bf16 tower features (bf16 model config); weights, biases and the decode stay fp32, y is fp32
+YS_EXPORT int yolosod_detect_head_bf16(int nl, const bf16_t* const* box_feat, const bf16_t* const* cls_feat, int c2,
+                                       int c3, const float* const* box_w, const float* const* box_b,
+                                       const float* const* cls_w, const float* const* cls_b, const int* heights,
+                                       const int* widths, const float* strides, int B, int nc, int reg_max, float* y,
+                                       void* stream) {
+  return detect_head_impl(nl, (const void* const*)box_feat, (const void* const*)cls_feat, c2, c3, box_w, box_b, cls_w,
+                          cls_b, heights, widths, strides, B, nc, reg_max, y, true, stream);
 }

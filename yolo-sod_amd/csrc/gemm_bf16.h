@@ -1,0 +1,389 @@
+// bf16 MFMA GEMM for gfx950 (the bf16 model config), fp32 accumulation, fused prologue / epilogue.
+//
+//   out(b, m, n) = epilogue( sum_k A'(b, m, k) * B(b, k, n) )      out, res: bf16; bias / BN / LN params: fp32
+//   A(b,m,k) = A[b*a_bs + m*lda + k]        (K-contiguous: token-major activations or weights)
+//   A'      = A, or bf16(LayerNorm_k(A)) when ln_w != nullptr, from per-row (mean, rstd) computed once by
+//             row_stats_bf16_kernel; applied in fp32 while staging the A tile, rounded once to bf16 for the MFMA
+//   B_KC:  B(b,k,n) = B[b*b_bs + n*ldb + k]  (K-contiguous: nn.Linear / 1x1-conv weights, token-major acts)
+//   !B_KC: B(b,k,n) = B[b*b_bs + k*ldb + n]  (N-contiguous: NCHW activations; transposed while staging to LDS)
+//
+// Tiling: 4 waves, each an (MI*32)x(NI*32) block of v_mfma_f32_32x32x16_bf16 accumulators; BK = 64 (4 MFMA k-steps);
+// LDS double buffer + register prefetch of the next k block (one barrier per k block). LDS images are [row][k] with
+// a 72-element (144-byte) row stride: lane (r = l&31, h = l>>5) reads its 8 k-consecutive bf16 operand elements
+// (k = 8h .. 8h+7 of the 16-wide step) as one ds_read_b128, and the 16 rows of a read group land on distinct banks.
+// Tile order is XCD-aware (workgroup i runs on XCD i % 8: contiguous row-major tile ranges per XCD). The epilogue
+// stages the fp32 accumulators through LDS and stores 4 consecutive n per lane (8 bytes of bf16); the Swin variant
+// scatters token columns to NCHW pixels (window reverse is the identity here: tokens are in padded raster order).
+#pragma once
+#include "common.h"
+#include <stdlib.h>
+
+namespace ys {
+
+struct EpiB {
+  const float* bias;   // bias_mode 1: per-row m, 2: per-col n
+  int bias_mode;
+  const float* scale;  // folded BN:  v = v*scale + shift, bn_mode 1: per-row, 2: per-col
+  const float* shift;
+  int bn_mode;
+  int act;             // 0 none, 1 SiLU, 2 GELU(erf), 3 ReLU
+  const bf16_t* res;   // residual added after activation (same indexing as out)
+  long res_bs;
+  int ldr;
+  bf16_t* out;
+  long out_bs;
+  int ldc;
+  // Swin output: n = token of the padded raster [img][Hp][Wp], m = channel; out / res are NCHW [img][M][H][W],
+  // tokens in the padding (h >= H or w >= W) are dropped (blocks_transformer.py:125-129 crop)
+  int swin;
+  int sw_H, sw_W, sw_Hp, sw_Wp;
+  int vec;             // set by launch_gemm_bf16: 4-wide epilogue legal (alignment / strides)
+};
+
+struct GemmB {
+  const bf16_t* A;
+  long a_bs;
+  int lda;
+  const bf16_t* B;
+  long b_bs;
+  int ldb;
+  int M, N, K;
+  const float* ln_w;      // optional LayerNorm of A rows (fp32 params)
+  const float* ln_b;
+  const float* ln_stats;  // [M][2] = (mean, rstd) from row_stats_bf16_kernel, required with ln_w
+  int tiles_n, tiles;     // set by launch_gemm_bf16
+  EpiB epi;
+};
+
+// Per-row LayerNorm statistics (mean, 1/sqrt(var + eps)) of a K-contiguous bf16 [rows][K] matrix: one wave per
+// row, values widened to fp32 in registers (K <= 1024), two passes (mean, then centred sum of squares).
+template <int VPL>
+__global__ __launch_bounds__(256) void row_stats_bf16_kernel(const bf16_t* __restrict__ x, int ld, long rows, int K,
+                                                             float eps, float* __restrict__ stats) {
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const bf16_t* xr = x + row * ld;
+  const int K4 = K >> 2;
+  f32x4 v[VPL];
+  float s = 0.f;
+#pragma unroll
+  for (int u = 0; u < VPL; ++u) {
+    const int c = lane + 64 * u;
+    v[u] = (c < K4) ? ld4(xr + 4 * c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    s += (v[u].x + v[u].y) + (v[u].z + v[u].w);
+  }
+  const float mean = wave_sum(s) / (float)K;
+  float q = 0.f;
+#pragma unroll
+  for (int u = 0; u < VPL; ++u) {
+    if (lane + 64 * u < K4) {
+      const f32x4 d = v[u] - mean;
+      q += (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
+    }
+  }
+  const float var = wave_sum(q) / (float)K;
+  if (lane == 0) {
+    stats[2 * row] = mean;
+    stats[2 * row + 1] = 1.0f / sqrtf(var + eps);
+  }
+}
+
+static inline int launch_row_stats_bf16(const bf16_t* x, int ld, long rows, int K, float eps, float* stats,
+                                        hipStream_t st) {
+  YS_CHECK_ARG(K % 4 == 0 && K <= 1024 && ld % 4 == 0, "row_stats_bf16: K=%d ld=%d unsupported", K, ld);
+  if (rows == 0) return 0;
+  const dim3 grid((unsigned)((rows + 3) / 4));
+  if (K <= 256) hipLaunchKernelGGL((row_stats_bf16_kernel<1>), grid, dim3(256), 0, st, x, ld, rows, K, eps, stats);
+  else if (K <= 512) hipLaunchKernelGGL((row_stats_bf16_kernel<2>), grid, dim3(256), 0, st, x, ld, rows, K, eps, stats);
+  else hipLaunchKernelGGL((row_stats_bf16_kernel<4>), grid, dim3(256), 0, st, x, ld, rows, K, eps, stats);
+  YS_CHECK_LAUNCH("row_stats_bf16");
+  return 0;
+}
+
+__device__ __forceinline__ float act_b(float v, int act) {
+  if (act == 1) return silu_fast_(v);
+  if (act == 2) return gelu_fast_(v);
+  if (act == 3) return fmaxf(v, 0.f);
+  return v;
+}
+
+// 8 bf16 (one uint4) <-> fp32
+__device__ __forceinline__ void unpack8(uint4 u, float* f) {
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(w[i] << 16);
+    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  return make_uint4(pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3]), pack_bf16x2(f[4], f[5]), pack_bf16x2(f[6], f[7]));
+}
+
+template <int WM, int WN, int MI, int NI, bool B_KC, bool A_LN>
+__global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmB g) {
+  constexpr int BM = WM * MI * 32;
+  constexpr int BN = WN * NI * 32;
+  constexpr int BK = 64;
+  constexpr int SK = BK + 8;                  // [row][k] image stride (bf16 elements): 144 B
+  constexpr int A_ELEMS = BM * SK;
+  constexpr int B_ELEMS = BN * SK;
+  constexpr int NA = BM * BK / 8 / 256;       // 16-byte chunks per thread per A tile
+  constexpr int NB = BN * BK / 8 / 256;
+  constexpr int SC = BN + 4;                  // epilogue staging row stride (fp32)
+  constexpr int MAIN_BYTES = 2 * (A_ELEMS + B_ELEMS) * 2;
+  constexpr int STAGE_BYTES = BM * SC * 4;
+  constexpr int SMEM_BYTES = (MAIN_BYTES > STAGE_BYTES ? MAIN_BYTES : STAGE_BYTES) + (A_LN ? 8 * BM : 0);
+  static_assert(WM * WN == 4, "4 waves");
+  static_assert(NA >= 1 && NB >= 1, "tile too small");
+  __shared__ __attribute__((aligned(16))) char smem[SMEM_BYTES];
+  bf16_t* As = reinterpret_cast<bf16_t*>(smem);
+  bf16_t* Bs = As + 2 * A_ELEMS;
+  float* s_mean = reinterpret_cast<float*>(smem + SMEM_BYTES - (A_LN ? 8 * BM : 0));
+  float* s_rstd = s_mean + BM;
+
+  const int tpx = (g.tiles + 7) >> 3;
+  const int t = (blockIdx.x & 7) * tpx + (blockIdx.x >> 3);
+  if (t >= g.tiles) return;
+  const int m0 = (t / g.tiles_n) * BM, n0 = (t % g.tiles_n) * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int bz = blockIdx.z;
+  const bf16_t* A = g.A + (long)bz * g.a_bs;
+  const bf16_t* B = g.B + (long)bz * g.b_bs;
+  const int M = g.M, N = g.N, K = g.K;
+
+  if (A_LN) {
+    for (int r = tid; r < BM; r += 256) {
+      const int m = m0 + r;
+      const float2 st = (m < M) ? *reinterpret_cast<const float2*>(g.ln_stats + 2L * m) : make_float2(0.f, 0.f);
+      s_mean[r] = st.x;
+      s_rstd[r] = st.y;
+    }
+  }
+
+  uint4 ra[NA], rb[NB];
+  int cur_k0 = 0;  // k offset of the tile held in ra / rb (LN params of the A prologue)
+  auto load_tiles = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int idx = tid + 256 * i;
+      const int r = idx >> 3, kc = (idx & 7) * 8;
+      const int m = m0 + r;
+      ra[i] = make_uint4(0u, 0u, 0u, 0u);
+      if (m < M) ra[i] = *reinterpret_cast<const uint4*>(A + (long)m * g.lda + k0 + kc);
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int idx = tid + 256 * i;
+      if (B_KC) {
+        const int r = idx >> 3, kc = (idx & 7) * 8;
+        const int n = n0 + r;
+        rb[i] = make_uint4(0u, 0u, 0u, 0u);
+        if (n < N) rb[i] = *reinterpret_cast<const uint4*>(B + (long)n * g.ldb + k0 + kc);
+      } else {
+        const int kl = idx / (BN / 8), nc = (idx % (BN / 8)) * 8;
+        const int n = n0 + nc;
+        const bf16_t* src = B + (long)(k0 + kl) * g.ldb + n;
+        if (n + 7 < N) {
+          rb[i] = *reinterpret_cast<const uint4*>(src);
+        } else {
+          uint16_t e[8];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) e[q] = (n + q < N) ? src[q] : (uint16_t)0;
+          rb[i] = make_uint4(e[0] | ((uint32_t)e[1] << 16), e[2] | ((uint32_t)e[3] << 16), e[4] | ((uint32_t)e[5] << 16),
+                             e[6] | ((uint32_t)e[7] << 16));
+        }
+      }
+    }
+  };
+  auto store_tiles = [&](int buf) {
+    bf16_t* Ab = As + buf * A_ELEMS;
+    bf16_t* Bb = Bs + buf * B_ELEMS;
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int idx = tid + 256 * i;
+      const int r = idx >> 3, kc = (idx & 7) * 8;
+      uint4 v = ra[i];
+      if (A_LN) {
+        // LN params of this chunk's 8 k (L1-resident)
+        float f[8];
+        unpack8(v, f);
+        const float mu = s_mean[r], rs = s_rstd[r];
+        const float* lw = g.ln_w + cur_k0 + kc;
+        const float* lb = g.ln_b + cur_k0 + kc;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) f[q] = (f[q] - mu) * rs * lw[q] + lb[q];
+        v = pack8(f);
+      }
+      *reinterpret_cast<uint4*>(&Ab[r * SK + kc]) = v;
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int idx = tid + 256 * i;
+      if (B_KC) {
+        const int r = idx >> 3, kc = (idx & 7) * 8;
+        *reinterpret_cast<uint4*>(&Bb[r * SK + kc]) = rb[i];
+      } else {  // 8 n-consecutive values of one k row -> column k of 8 [n][k] rows
+        const int kl = idx / (BN / 8), nc = (idx % (BN / 8)) * 8;
+        const uint32_t w[4] = {rb[i].x, rb[i].y, rb[i].z, rb[i].w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          Bb[(nc + 2 * q) * SK + kl] = (bf16_t)(w[q] & 0xffffu);
+          Bb[(nc + 2 * q + 1) * SK + kl] = (bf16_t)(w[q] >> 16);
+        }
+      }
+    }
+  };
+
+  f32x16 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int nk = K / BK;
+  const int lr = lane & 31, lh = lane >> 5;
+  load_tiles(0);
+  if (A_LN) __syncthreads();  // s_mean / s_rstd
+  store_tiles(0);
+  __syncthreads();
+  for (int kb = 0; kb < nk; ++kb) {
+    const int buf = kb & 1;
+    if (kb + 1 < nk) load_tiles((kb + 1) * BK);
+    const bf16_t* Ab = As + buf * A_ELEMS + (wm * MI * 32 + lr) * SK + lh * 8;
+    const bf16_t* Bb = Bs + buf * B_ELEMS + (wn * NI * 32 + lr) * SK + lh * 8;
+#pragma unroll
+    for (int kk = 0; kk < BK / 16; ++kk) {
+      bf16x8_t a[MI], b[NI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) a[i] = *reinterpret_cast<const bf16x8_t*>(Ab + i * 32 * SK + 16 * kk);
+#pragma unroll
+      for (int j = 0; j < NI; ++j) b[j] = *reinterpret_cast<const bf16x8_t*>(Bb + j * 32 * SK + 16 * kk);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    if (kb + 1 < nk) {
+      cur_k0 = (kb + 1) * BK;
+      store_tiles(buf ^ 1);
+    }
+    __syncthreads();
+  }
+
+  const EpiB& e = g.epi;
+  // stage C through LDS (the main-loop buffers are free after the last barrier).
+  // C/D map of 32x32: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+  float* Cs = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        Cs[(wm * MI * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) * SC + wn * NI * 32 + j * 32 + lr] = acc[i][j][r];
+  __syncthreads();
+  if (e.vec) {
+    constexpr int NQ = BN / 4;
+    bf16_t* outb = e.out + (long)bz * e.out_bs;
+    const bf16_t* resb = e.res ? e.res + (long)bz * e.res_bs : nullptr;
+#pragma unroll 4
+    for (int idx = tid; idx < BM * NQ; idx += 256) {
+      const int row = idx / NQ, c4 = idx % NQ;
+      const int m = m0 + row;
+      const int n = n0 + 4 * c4;
+      if (m >= M || n >= N) continue;
+      f32x4 v = *reinterpret_cast<const f32x4*>(&Cs[row * SC + 4 * c4]);
+      if (e.bias_mode == 1) v += e.bias[m];
+      else if (e.bias_mode == 2) v += *reinterpret_cast<const f32x4*>(e.bias + n);
+      if (e.bn_mode == 1) v = v * e.scale[m] + e.shift[m];
+      else if (e.bn_mode == 2)
+        v = v * *reinterpret_cast<const f32x4*>(e.scale + n) + *reinterpret_cast<const f32x4*>(e.shift + n);
+      v.x = act_b(v.x, e.act); v.y = act_b(v.y, e.act); v.z = act_b(v.z, e.act); v.w = act_b(v.w, e.act);
+      if (resb) v += ld4(resb + (long)m * e.ldr + n);
+      st4(outb + (long)m * e.ldc + n, v);
+    }
+    return;
+  }
+  // scalar epilogue: lanes along n (Swin: consecutive raster tokens = consecutive pixels of a row), rows over m
+  for (int idx = tid; idx < BM * BN; idx += 256) {
+    const int row = idx / BN, col = idx % BN;
+    const int m = m0 + row, n = n0 + col;
+    if (m >= M || n >= N) continue;
+    float v = Cs[row * SC + col];
+    if (e.bias_mode == 1) v += e.bias[m];
+    else if (e.bias_mode == 2) v += e.bias[n];
+    if (e.bn_mode == 1) v = v * e.scale[m] + e.shift[m];
+    else if (e.bn_mode == 2) v = v * e.scale[n] + e.shift[n];
+    v = act_b(v, e.act);
+    long o, ro;
+    if (e.swin) {
+      const long per_img = (long)e.sw_Hp * e.sw_Wp;
+      const int img = (int)(n / per_img);
+      const int rr = (int)(n - img * per_img);
+      const int h = rr / e.sw_Wp, w = rr - (rr / e.sw_Wp) * e.sw_Wp;
+      if (h >= e.sw_H || w >= e.sw_W) continue;
+      o = ((long)img * M + m) * ((long)e.sw_H * e.sw_W) + (long)h * e.sw_W + w;  // out / res NCHW [img][M][H][W]
+      ro = o;
+    } else {
+      o = (long)bz * e.out_bs + (long)m * e.ldc + n;
+      ro = (long)bz * e.res_bs + (long)m * e.ldr + n;
+    }
+    if (e.res) v += bf2f(e.res[ro]);
+    e.out[o] = f2bf(v);
+  }
+}
+
+static inline bool al_b(const void* p, int bytes) { return ((uintptr_t)p & (bytes - 1)) == 0; }
+
+static inline int launch_gemm_bf16(const GemmB& g0, int batch, bool b_kc, hipStream_t st) {
+  GemmB g = g0;
+  YS_CHECK_ARG(g.K % 64 == 0, "gemm_bf16: K=%d must be a multiple of 64", g.K);
+  YS_CHECK_ARG(g.lda % 8 == 0 && g.ldb % 8 == 0 && g.a_bs % 8 == 0 && g.b_bs % 8 == 0,
+               "gemm_bf16: lda / ldb / batch strides must be multiples of 8");
+  YS_CHECK_ARG(al_b(g.A, 16) && al_b(g.B, 16), "gemm_bf16: A/B must be 16-byte aligned");
+  YS_CHECK_ARG(!g.ln_w || (g.ln_b && g.ln_stats && al_b(g.ln_stats, 8)),
+               "gemm_bf16: LN params must come with row statistics");
+  if (g.M == 0 || g.N == 0 || batch == 0) return 0;
+  const EpiB& e = g.epi;
+  g.epi.vec = !e.swin && g.N % 4 == 0 && e.ldc % 4 == 0 && e.out_bs % 4 == 0 && al_b(e.out, 8) &&
+              (!e.res || (e.ldr % 4 == 0 && e.res_bs % 4 == 0 && al_b(e.res, 8))) &&
+              (e.bias_mode != 2 || al_b(e.bias, 16)) && (e.bn_mode != 2 || (al_b(e.scale, 16) && al_b(e.shift, 16)));
+  const bool ln = g.ln_w != nullptr;
+#define YS_GEMMB_LAUNCH(WM_, WN_, MI_, NI_)                                                                     \
+  do {                                                                                                          \
+    constexpr int bm = WM_ * MI_ * 32, bn = WN_ * NI_ * 32;                                                     \
+    g.tiles_n = (g.N + bn - 1) / bn;                                                                            \
+    g.tiles = g.tiles_n * ((g.M + bm - 1) / bm);                                                                \
+    dim3 grid((unsigned)(8 * ((g.tiles + 7) / 8)), 1, batch);                                                   \
+    if (b_kc) {                                                                                                 \
+      if (ln) hipLaunchKernelGGL((gemm_bf16_kernel<WM_, WN_, MI_, NI_, true, true>), grid, dim3(256), 0, st, g); \
+      else hipLaunchKernelGGL((gemm_bf16_kernel<WM_, WN_, MI_, NI_, true, false>), grid, dim3(256), 0, st, g);  \
+    } else {                                                                                                    \
+      hipLaunchKernelGGL((gemm_bf16_kernel<WM_, WN_, MI_, NI_, false, false>), grid, dim3(256), 0, st, g);      \
+    }                                                                                                           \
+  } while (0)
+  YS_CHECK_ARG(b_kc || !ln, "gemm_bf16: LN prologue needs a K-contiguous B");
+  // 128x64 tiles when N is narrow or 128x128 would leave CUs idle; 128x128 otherwise
+  const long t128 = (long)((g.M + 127) / 128) * ((g.N + 127) / 128) * batch;
+  if (g.N <= 64 || t128 < 512) YS_GEMMB_LAUNCH(4, 1, 1, 2);
+  else YS_GEMMB_LAUNCH(2, 2, 2, 2);
+#undef YS_GEMMB_LAUNCH
+  YS_CHECK_LAUNCH("gemm_bf16");
+  return 0;
+}
+
+static inline EpiB epib_plain(bf16_t* out, long out_bs, int ldc) {
+  EpiB e{};
+  e.out = out;
+  e.out_bs = out_bs;
+  e.ldc = ldc;
+  return e;
+}
+
+}  // namespace ys

@@ -1,0 +1,523 @@
+// bf16 model config: SwinBlock and A2_Attn with bf16 activations on the bf16 matrix cores (fp32 accumulation).
+//
+//   * gemm_bf16     - gemm_bf16.h: v_mfma_f32_32x32x16_bf16, LN prologue, bias / BN / act / residual epilogue.
+//   * window_attn   - per-(sequence, head, 64 queries) attention on v_mfma_f32_16x16x32_bf16: K (row-major) and V
+//                     (transposed) of the whole sequence in LDS, one wave per 16 queries, the full score row in
+//                     registers (fp32 softmax, no rescaling), P through a per-wave LDS tile into the P.V product.
+//   * swin_tokens   - depthwise 3x3 + bottom/right zero pad -> token-major rows in padded RASTER order
+//                     [img][Hp][Wp][C]. Every Swin stage except attention is per token, so the window partition is
+//                     only an index map inside the attention kernel, and the window reverse + crop of the output
+//                     is a plain NCHW store of each token row (contiguous pixels).
+//   * a2 pool / upsample - as transformer.hip, bf16 storage.
+// Arithmetic: activations are bf16 in HBM (as `model.to(torch.bfloat16)` stores them); every reduction, LayerNorm,
+// softmax and epilogue runs in fp32 and rounds once on store. Parameters other than the GEMM weights are fp32.
+//
+// Reference semantics (fp32 originals): SwinBlock blocks_transformer.py:8-171, A2_Attn a2_attn.py:35-69.
+#include "common.h"
+#include "gemm_bf16.h"
+#include <math.h>
+#include <stdlib.h>
+
+namespace ys {
+
+// token row of (sequence, token) in the attention's qkv / out matrices
+struct TokMap {
+  int mode;  // 0: row = seq * L + t;  1: Swin window (img, wy, wx) of a padded raster [img][Hp][Wp]
+  int L, Hp, Wp, wh, ww, nWx, nWin;
+  __device__ __forceinline__ long row(long seq, int t) const {
+    if (mode == 0) return seq * L + t;
+    const long img = seq / nWin;
+    const int win = (int)(seq - img * nWin);
+    const int wy = win / nWx, wx = win - (win / nWx) * nWx;
+    const int iy = t / ww, ix = t - (t / ww) * ww;
+    return (img * Hp + wy * wh + iy) * (long)Wp + wx * ww + ix;
+  }
+};
+
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+
+// =================================================================================================
+// Attention over packed bf16 QKV rows: q at col h*HD, k at C + h*HD, v at 2C + h*HD of a row of ld = 3C;
+// out[row][h*HD + d]. grid = (ceil(L/64), heads, n_seq); 256 threads, wave w owns queries q0 + 16w .. +15.
+// MFMA 16x16x32 bf16: A/B lane l holds [row l&15][k = 8(l>>4) + j]; C/D lane l holds [row 4(l>>4) + r][col l&15].
+// S = Q K^T (fp32), softmax(S * scale) in fp32 with the row spread over the 16 lanes of a lane group, P rounded to
+// bf16 (the reference bf16 model's P), O = P V with V^T staged in LDS (operand rows = d, k = key).
+// =================================================================================================
+template <int HD, int NKB>
+__global__ __launch_bounds__(256) void window_attn_bf16_kernel(const bf16_t* __restrict__ qkv, int C,
+                                                               bf16_t* __restrict__ out, TokMap tm, float scale) {
+  constexpr int NK = NKB * 16;       // keys (padded)
+  constexpr int KS = HD + 8;         // K row stride (elements)
+  constexpr int VS = NK + 8;         // V^T row stride
+  constexpr int PS = NK + 8;         // P row stride
+  static_assert(NK % 32 == 0 && HD % 32 == 0, "k steps of 32");
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[NK * KS];
+  __shared__ __attribute__((aligned(16))) bf16_t Vt[HD * VS];
+  __shared__ __attribute__((aligned(16))) bf16_t Ps[4 * 16 * PS];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int h = blockIdx.y;
+  const long seq = blockIdx.z;
+  const int L = tm.L;
+  const int ld = 3 * C;
+  const int l15 = lane & 15, g = lane >> 4;
+
+  // stage K (row-major) and V (transposed) of the sequence; keys >= L are zero
+  for (int e = tid; e < NK * (HD / 8); e += 256) {
+    const int key = e / (HD / 8), dc = (e - key * (HD / 8)) * 8;
+    uint4 kv = make_uint4(0u, 0u, 0u, 0u), vv = kv;
+    if (key < L) {
+      const bf16_t* src = qkv + tm.row(seq, key) * ld + h * HD + dc;
+      kv = *reinterpret_cast<const uint4*>(src + C);
+      vv = *reinterpret_cast<const uint4*>(src + 2 * C);
+    }
+    *reinterpret_cast<uint4*>(&Ks[key * KS + dc]) = kv;
+    const uint32_t w[4] = {vv.x, vv.y, vv.z, vv.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      Vt[(dc + 2 * q) * VS + key] = (bf16_t)(w[q] & 0xffffu);
+      Vt[(dc + 2 * q + 1) * VS + key] = (bf16_t)(w[q] >> 16);
+    }
+  }
+  // this wave's Q fragments (rows >= L read row L-1: finite values, results dropped)
+  const int q0 = blockIdx.x * 64 + wv * 16;
+  bf16x8_t qf[HD / 32];
+  {
+    const int qr = (q0 + l15 < L) ? q0 + l15 : L - 1;
+    const bf16_t* src = qkv + tm.row(seq, qr) * ld + h * HD + 8 * g;
+#pragma unroll
+    for (int s = 0; s < HD / 32; ++s) qf[s] = *reinterpret_cast<const bf16x8_t*>(src + 32 * s);
+  }
+  __syncthreads();
+  if (q0 >= L) return;  // whole wave; no barrier below (the per-wave P tile is ordered by the wave barrier)
+
+  f32x4 sacc[NKB];
+#pragma unroll
+  for (int kb = 0; kb < NKB; ++kb) {
+    f32x4 a = {0.f, 0.f, 0.f, 0.f};
+    const bf16_t* kr = Ks + (kb * 16 + l15) * KS + 8 * g;
+#pragma unroll
+    for (int s = 0; s < HD / 32; ++s)
+      a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[s], *reinterpret_cast<const bf16x8_t*>(kr + 32 * s), a, 0, 0, 0);
+    sacc[kb] = a;
+  }
+  // softmax over keys: lane holds S[row 4g + r][key kb*16 + l15]
+  const float sl = scale * 1.44269504088896341f;  // exp(x*scale) = exp2(x*scale*log2 e)
+  float mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+  for (int kb = 0; kb < NKB; ++kb) {
+    const bool valid = kb * 16 + l15 < L;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (!valid) sacc[kb][r] = -INFINITY;
+      mx[r] = fmaxf(mx[r], sacc[kb][r]);
+    }
+  }
+  float sum[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) mx[r] = fmaxf(mx[r], __shfl_xor(mx[r], o, 64));
+    sum[r] = 0.f;
+  }
+#pragma unroll
+  for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float e = __builtin_amdgcn_exp2f((sacc[kb][r] - mx[r]) * sl);
+      sacc[kb][r] = e;
+      sum[r] += e;
+    }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) sum[r] += __shfl_xor(sum[r], o, 64);
+    sum[r] = 1.0f / sum[r];
+  }
+  bf16_t* Pw = Ps + wv * 16 * PS;
+#pragma unroll
+  for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) Pw[(4 * g + r) * PS + kb * 16 + l15] = f2bf(sacc[kb][r] * sum[r]);
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's P stores are in LDS before its reads
+  __builtin_amdgcn_wave_barrier();
+
+  f32x4 oacc[HD / 16];
+#pragma unroll
+  for (int db = 0; db < HD / 16; ++db) oacc[db] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < NK / 32; ++s) {
+    const bf16x8_t pa = *reinterpret_cast<const bf16x8_t*>(Pw + l15 * PS + 32 * s + 8 * g);
+#pragma unroll
+    for (int db = 0; db < HD / 16; ++db) {
+      const bf16x8_t vb = *reinterpret_cast<const bf16x8_t*>(Vt + (db * 16 + l15) * VS + 32 * s + 8 * g);
+      oacc[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vb, oacc[db], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int q = q0 + 4 * g + r;
+    if (q >= L) continue;
+    bf16_t* dst = out + tm.row(seq, q) * C + h * HD + l15;
+#pragma unroll
+    for (int db = 0; db < HD / 16; ++db) dst[db * 16] = f2bf(oacc[db][r]);
+  }
+}
+
+template <int HD, int N>
+constexpr size_t wattn_lds_bytes() {
+  return sizeof(bf16_t) * ((size_t)N * 16 * (HD + 8) + (size_t)HD * (N * 16 + 8) + 64 * (size_t)(N * 16 + 8));
+}
+
+template <int HD>
+static int launch_wattn_hd(int nkb, dim3 grid, hipStream_t st, const bf16_t* qkv, int C, bf16_t* out,
+                           const TokMap& tm, float scale) {
+  // key-block counts with an instance whose K / V^T / P tiles fit the 160 KiB of LDS
+#define YS_WATTN(N)                                                                                             \
+  if constexpr (wattn_lds_bytes<HD, N>() <= 160 * 1024) {                                                       \
+    if (nkb <= N) {                                                                                             \
+      hipLaunchKernelGGL((window_attn_bf16_kernel<HD, N>), grid, dim3(256), 0, st, qkv, C, out, tm, scale);     \
+      return 0;                                                                                                 \
+    }                                                                                                           \
+  }
+  YS_WATTN(4) YS_WATTN(6) YS_WATTN(8) YS_WATTN(10) YS_WATTN(12) YS_WATTN(16) YS_WATTN(20)
+#undef YS_WATTN
+  YS_CHECK_ARG(false, "attention_bf16: %d key blocks of head dim %d unsupported", nkb, HD);
+  return -1;
+}
+
+static int launch_attention_bf16(const bf16_t* qkv, bf16_t* out, long n_seq, int C, int heads, const TokMap& tm,
+                                 hipStream_t st) {
+  YS_CHECK_ARG(heads > 0 && C % heads == 0, "attention_bf16: C=%d not divisible by heads=%d", C, heads);
+  const int hd = C / heads;
+  const int L = tm.L;
+  YS_CHECK_ARG(L > 0 && L <= 320, "attention_bf16: sequence length %d unsupported (1..320)", L);
+  YS_CHECK_ARG(n_seq < 65536, "attention_bf16: too many sequences (%ld)", n_seq);
+  YS_CHECK_ARG(C % 8 == 0, "attention_bf16: C=%d must be a multiple of 8", C);
+  const int nkb = ((L + 31) / 32) * 2;  // key blocks of 16, padded to whole 32-key steps
+  const float scale = 1.0f / sqrtf((float)hd);
+  dim3 grid((L + 63) / 64, heads, (unsigned)n_seq);
+  int rc;
+  switch (hd) {
+    case 32: rc = launch_wattn_hd<32>(nkb, grid, st, qkv, C, out, tm, scale); break;
+    case 64: rc = launch_wattn_hd<64>(nkb, grid, st, qkv, C, out, tm, scale); break;
+    case 128: rc = launch_wattn_hd<128>(nkb, grid, st, qkv, C, out, tm, scale); break;
+    default: YS_CHECK_ARG(false, "attention_bf16: head dim %d unsupported (32, 64, 128)", hd);
+  }
+  if (rc) return rc;
+  YS_CHECK_LAUNCH("attention_bf16");
+  return 0;
+}
+
+// =================================================================================================
+// Swin: depthwise 3x3 (pad 1, no bias) + bottom/right zero pad -> T[(img*Hp + h)*Wp + w][C] (padded raster order).
+// grid = (B*Hp, ceil(C/CS)): one padded row of one image and a CS-channel slab; the three input rows of the slab
+// are staged in LDS (bf16, zero border), the output row is written with lanes along c (coalesced rows of T).
+// =================================================================================================
+__global__ __launch_bounds__(256) void swin_tokens_bf16_kernel(const bf16_t* __restrict__ x,
+                                                               const float* __restrict__ dw, bf16_t* __restrict__ T,
+                                                               int C, int H, int W, int Hp, int Wp, int CS) {
+  extern __shared__ bf16_t rows[];  // [CS][3][W + 2]
+  const int img = blockIdx.x / Hp, h = blockIdx.x - (blockIdx.x / Hp) * Hp;
+  const int c0 = blockIdx.y * CS;
+  const int nc = (C - c0 < CS) ? C - c0 : CS;
+  const int RW = W + 2;
+  bf16_t* Tr = T + ((long)img * Hp + h) * Wp * C + c0;
+  if (h >= H) {  // padding rows: zero tokens
+    for (int e = threadIdx.x; e < Wp * nc; e += 256) Tr[(long)(e / nc) * C + e % nc] = 0;
+    return;
+  }
+  const bf16_t* xb = x + ((long)img * C + c0) * H * W;
+  for (int e = threadIdx.x; e < nc * 3 * RW; e += 256) {
+    const int c = e / (3 * RW), r = (e / RW) % 3, px = e % RW;
+    const int hh = h - 1 + r, ww = px - 1;
+    rows[e] = (hh >= 0 && hh < H && ww >= 0 && ww < W) ? xb[((long)c * H + hh) * W + ww] : (bf16_t)0;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < Wp * nc; e += 256) {
+    const int w = e / nc, c = e - (e / nc) * nc;
+    float v = 0.f;
+    if (w < W) {
+      const bf16_t* pc = rows + c * 3 * RW + w;
+      const float* k = dw + (long)(c0 + c) * 9;
+      v = k[0] * bf2f(pc[0]) + k[1] * bf2f(pc[1]) + k[2] * bf2f(pc[2]) + k[3] * bf2f(pc[RW]) +
+          k[4] * bf2f(pc[RW + 1]) + k[5] * bf2f(pc[RW + 2]) + k[6] * bf2f(pc[2 * RW]) + k[7] * bf2f(pc[2 * RW + 1]) +
+          k[8] * bf2f(pc[2 * RW + 2]);
+    }
+    Tr[(long)w * C + c] = f2bf(v);
+  }
+}
+
+// A2: adaptive-avg-pool over rows to A areas (overlapping bins), token-major S[(img*A + a)*W + w][c] (bf16).
+__global__ __launch_bounds__(256) void a2_pool_tokens_bf16_kernel(const bf16_t* __restrict__ xp, bf16_t* __restrict__ S,
+                                                                  int C, int H, int W, int A) {
+  extern __shared__ float slab[];  // [64][W + 1]
+  const int img = blockIdx.x / A, a = blockIdx.x % A;
+  const int c0 = blockIdx.y * 64;
+  const int nc = (C - c0 < 64) ? C - c0 : 64;
+  const int r0 = (a * H) / A, r1 = ((a + 1) * H + A - 1) / A;
+  const float inv = (float)(r1 - r0);
+  const bf16_t* xb = xp + ((long)img * C + c0) * H * W;
+  for (int e = threadIdx.x; e < nc * W; e += 256) {
+    const int c = e / W, w = e - c * W;
+    const bf16_t* src = xb + ((long)c * H + r0) * W + w;
+    float s = 0.f;
+    for (int r = 0; r < r1 - r0; ++r) s += bf2f(src[(long)r * W]);
+    slab[c * (W + 1) + w] = s / inv;
+  }
+  __syncthreads();
+  bf16_t* Sb = S + ((long)img * A + a) * W * C + c0;
+  for (int e = threadIdx.x; e < nc * W; e += 256) {
+    const int w = e / nc, c = e - w * nc;
+    Sb[(long)w * C + c] = f2bf(slab[c * (W + 1) + w]);
+  }
+}
+
+// A2 tail: y = x + SiLU(up_h(T) + b), T = out conv of the area tokens laid out [img][C][A][W] (bf16).
+__global__ __launch_bounds__(256) void a2_upsample_out_bf16_kernel(const bf16_t* __restrict__ x,
+                                                                   const bf16_t* __restrict__ T,
+                                                                   const float* __restrict__ bias,
+                                                                   bf16_t* __restrict__ y, int C, int H, int W,
+                                                                   int A) {
+  const long pc = blockIdx.x;  // img*C + c
+  const int c = (int)(pc % C);
+  const int e = blockIdx.y * 256 + threadIdx.x;
+  if (e >= H * W) return;
+  const int h = e / W, w = e - h * W;
+  const float sc = (float)A / (float)H;
+  float src = sc * ((float)h + 0.5f) - 0.5f;
+  if (src < 0.f) src = 0.f;
+  const int y0 = (int)src;
+  const int y1 = y0 + ((y0 < A - 1) ? 1 : 0);
+  const float l1 = src - (float)y0, l0 = 1.0f - l1;
+  const bf16_t* Tp = T + pc * A * W;
+  const float u = l0 * bf2f(Tp[y0 * W + w]) + l1 * bf2f(Tp[y1 * W + w]);
+  const long o = pc * H * W + e;
+  y[o] = f2bf(bf2f(x[o]) + siluf_(u + bias[c]));
+}
+
+__global__ void fold_bn_bf16_kernel(const float* w, const float* b, const float* m, const float* v, float eps, int C,
+                                    float* scale, float* shift) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  const float inv = 1.0f / sqrtf(v[c] + eps);
+  const float sc = w[c] * inv;
+  scale[c] = sc;
+  shift[c] = b[c] - m[c] * sc;
+}
+
+struct SwinGeomB {
+  int wh, ww, Hp, Wp, nWx, nWin, L;
+  long ntok;  // B * Hp * Wp
+};
+static SwinGeomB swin_geom_b(int B, int H, int W, int ws) {
+  SwinGeomB g;
+  g.wh = H < ws ? H : ws;
+  g.ww = W < ws ? W : ws;
+  if (H <= ws && W <= ws) {  // single global window, no pad (blocks_transformer.py:25-28)
+    g.wh = H;
+    g.ww = W;
+  }
+  g.Hp = H + (g.wh - H % g.wh) % g.wh;
+  g.Wp = W + (g.ww - W % g.ww) % g.ww;
+  g.nWx = g.Wp / g.ww;
+  g.nWin = (g.Hp / g.wh) * g.nWx;
+  g.L = g.wh * g.ww;
+  g.ntok = (long)B * g.Hp * g.Wp;
+  return g;
+}
+
+}  // namespace ys
+
+using namespace ys;
+
+// =================================================================================================
+// C ABI (bf16 storage: activations / GEMM weights are bf16 bit patterns, other parameters fp32)
+// =================================================================================================
+YS_EXPORT int yolosod_gemm_bf16(const bf16_t* A, long a_bs, int lda, const bf16_t* B, long b_bs, int ldb,
+                                int b_kcontig, bf16_t* C, long c_bs, int ldc, int M, int N, int K, int batch,
+                                const float* bias, int bias_mode, int act, const bf16_t* res, void* stream) {
+  GemmB g{};
+  g.A = A; g.a_bs = a_bs; g.lda = lda;
+  g.B = B; g.b_bs = b_bs; g.ldb = ldb;
+  g.M = M; g.N = N; g.K = K;
+  g.epi = epib_plain(C, c_bs, ldc);
+  g.epi.bias = bias; g.epi.bias_mode = bias ? bias_mode : 0;
+  g.epi.act = act;
+  g.epi.res = res; g.epi.res_bs = c_bs; g.epi.ldr = ldc;
+  return launch_gemm_bf16(g, batch, b_kcontig != 0, (hipStream_t)stream);
+}
+
+// Test hook: attention over contiguous sequences of L rows of a [n_seq*L][3C] bf16 QKV matrix -> [n_seq*L][C].
+YS_EXPORT int yolosod_attention_bf16(const bf16_t* qkv, bf16_t* out, long n_seq, int L, int C, int heads,
+                                     void* stream) {
+  TokMap tm{};
+  tm.mode = 0;
+  tm.L = L;
+  return launch_attention_bf16(qkv, out, n_seq, C, heads, tm, (hipStream_t)stream);
+}
+
+YS_EXPORT size_t yolosod_swin_workspace_bf16(int B, int C, int H, int W, int num_heads, int window, int mlp_hidden) {
+  (void)num_heads;
+  SwinGeomB g = swin_geom_b(B, H, W, window);
+  const int wide = (3 * C > mlp_hidden) ? 3 * C : mlp_hidden;
+  Sizer s;
+  s.take<bf16_t>((size_t)g.ntok * C);     // T (residual stream)
+  s.take<bf16_t>((size_t)g.ntok * C);     // U (attention out)
+  s.take<bf16_t>((size_t)g.ntok * wide);  // QKV / MLP hidden
+  s.take<float>((size_t)C * 2);           // folded BN
+  s.take<float>((size_t)g.ntok * 2);      // LayerNorm row statistics
+  return s.off;
+}
+
+// SwinBlock.forward (blocks_transformer.py:150-171) on bf16 activations. Weights: in_proj [3C][C], out_proj [C][C],
+// mlp1 [hid][C], mlp2 [C][hid], pw [C][C] bf16; dw [C][9], LN / biases / BN fp32.
+YS_EXPORT int yolosod_swin_forward_bf16(const bf16_t* x, bf16_t* y, int B, int C, int H, int W, int num_heads,
+                                        int window, const float* dw_w, const float* ln1_w, const float* ln1_b,
+                                        float ln1_eps, const bf16_t* in_proj_w, const float* in_proj_b,
+                                        const bf16_t* out_proj_w, const float* out_proj_b, const float* ln2_w,
+                                        const float* ln2_b, float ln2_eps, const bf16_t* mlp1_w, const float* mlp1_b,
+                                        int mlp_hidden, const bf16_t* mlp2_w, const float* mlp2_b,
+                                        const bf16_t* pw_w, const float* bn_w, const float* bn_b,
+                                        const float* bn_mean, const float* bn_var, float bn_eps, void* workspace,
+                                        size_t workspace_bytes, void* stream) {
+  YS_CHECK_ARG(x && y && dw_w && ln1_w && ln1_b && in_proj_w && in_proj_b && out_proj_w && out_proj_b && ln2_w &&
+                   ln2_b && mlp1_w && mlp1_b && mlp2_w && mlp2_b && pw_w && bn_w && bn_b && bn_mean && bn_var,
+               "swin_bf16: null pointer");
+  YS_CHECK_ARG(B >= 0 && C > 0 && H > 0 && W > 0 && window > 0 && num_heads > 0, "swin_bf16: bad shape");
+  YS_CHECK_ARG(C % 64 == 0 && mlp_hidden % 64 == 0, "swin_bf16: C and mlp_hidden must be multiples of 64");
+  if (B == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  SwinGeomB g = swin_geom_b(B, H, W, window);
+  YS_CHECK_ARG(g.L <= 320, "swin_bf16: window of %d tokens unsupported", g.L);
+  YS_CHECK_ARG(g.ntok < (1L << 31), "swin_bf16: too many tokens");
+  Carver cv(workspace, workspace_bytes);
+  bf16_t* T = cv.take<bf16_t>((size_t)g.ntok * C);
+  bf16_t* U = cv.take<bf16_t>((size_t)g.ntok * C);
+  const int wide = (3 * C > mlp_hidden) ? 3 * C : mlp_hidden;
+  bf16_t* Q = cv.take<bf16_t>((size_t)g.ntok * wide);
+  float* bn_fold = cv.take<float>((size_t)C * 2);
+  float* lns = cv.take<float>((size_t)g.ntok * 2);
+  YS_CHECK_ARG(lns, "swin_bf16: workspace too small (%zu)", workspace_bytes);
+  int rc;
+  // dwconv + pad -> T (raster tokens)
+  int CS = 64;
+  while (CS > 8 && (size_t)CS * 3 * (W + 2) * sizeof(bf16_t) > 64 * 1024) CS >>= 1;
+  YS_CHECK_ARG((size_t)CS * 3 * (W + 2) * sizeof(bf16_t) <= 64 * 1024, "swin_bf16: W=%d too wide", W);
+  hipLaunchKernelGGL(swin_tokens_bf16_kernel, dim3((unsigned)(B * g.Hp), (unsigned)((C + CS - 1) / CS)), dim3(256),
+                     (size_t)CS * 3 * (W + 2) * sizeof(bf16_t), st, x, dw_w, T, C, H, W, g.Hp, g.Wp, CS);
+  YS_CHECK_LAUNCH("swin_tokens_bf16");
+  // QKV = LN1(T) Win^T + b_in
+  if ((rc = launch_row_stats_bf16(T, C, g.ntok, C, ln1_eps, lns, st))) return rc;
+  GemmB ga{};
+  ga.A = T; ga.lda = C; ga.B = in_proj_w; ga.ldb = C; ga.M = (int)g.ntok; ga.N = 3 * C; ga.K = C;
+  ga.ln_w = ln1_w; ga.ln_b = ln1_b; ga.ln_stats = lns;
+  ga.epi = epib_plain(Q, 0, 3 * C);
+  ga.epi.bias = in_proj_b; ga.epi.bias_mode = 2;
+  if ((rc = launch_gemm_bf16(ga, 1, true, st))) return rc;
+  TokMap tm{};
+  tm.mode = 1; tm.L = g.L; tm.Hp = g.Hp; tm.Wp = g.Wp; tm.wh = g.wh; tm.ww = g.ww; tm.nWx = g.nWx; tm.nWin = g.nWin;
+  if ((rc = launch_attention_bf16(Q, U, (long)B * g.nWin, C, num_heads, tm, st))) return rc;
+  // T = T + (O Wo^T + bo)
+  ga = GemmB{};
+  ga.A = U; ga.lda = C; ga.B = out_proj_w; ga.ldb = C; ga.M = (int)g.ntok; ga.N = C; ga.K = C;
+  ga.epi = epib_plain(T, 0, C);
+  ga.epi.bias = out_proj_b; ga.epi.bias_mode = 2; ga.epi.res = T; ga.epi.ldr = C;
+  if ((rc = launch_gemm_bf16(ga, 1, true, st))) return rc;
+  // Hd = GELU(LN2(T) W1^T + b1)
+  if ((rc = launch_row_stats_bf16(T, C, g.ntok, C, ln2_eps, lns, st))) return rc;
+  ga = GemmB{};
+  ga.A = T; ga.lda = C; ga.B = mlp1_w; ga.ldb = C; ga.M = (int)g.ntok; ga.N = mlp_hidden; ga.K = C;
+  ga.ln_w = ln2_w; ga.ln_b = ln2_b; ga.ln_stats = lns;
+  ga.epi = epib_plain(Q, 0, mlp_hidden);
+  ga.epi.bias = mlp1_b; ga.epi.bias_mode = 2; ga.epi.act = 2;
+  if ((rc = launch_gemm_bf16(ga, 1, true, st))) return rc;
+  // T = T + (Hd W2^T + b2)
+  ga = GemmB{};
+  ga.A = Q; ga.lda = mlp_hidden; ga.B = mlp2_w; ga.ldb = mlp_hidden; ga.M = (int)g.ntok; ga.N = C; ga.K = mlp_hidden;
+  ga.epi = epib_plain(T, 0, C);
+  ga.epi.bias = mlp2_b; ga.epi.bias_mode = 2; ga.epi.res = T; ga.epi.ldr = C;
+  if ((rc = launch_gemm_bf16(ga, 1, true, st))) return rc;
+  // y = x + SiLU(BN(pw . T)), tokens -> NCHW pixels with the crop: M = out channel, N = raster token
+  float* bn_scale = bn_fold;
+  float* bn_shift = bn_fold + C;
+  hipLaunchKernelGGL(fold_bn_bf16_kernel, dim3((C + 255) / 256), dim3(256), 0, st, bn_w, bn_b, bn_mean, bn_var, bn_eps,
+                     C, bn_scale, bn_shift);
+  ga = GemmB{};
+  ga.A = pw_w; ga.lda = C; ga.B = T; ga.ldb = C; ga.M = C; ga.N = (int)g.ntok; ga.K = C;
+  ga.epi = epib_plain(y, 0, C);
+  ga.epi.scale = bn_scale; ga.epi.shift = bn_shift; ga.epi.bn_mode = 1; ga.epi.act = 1;
+  ga.epi.res = x;
+  ga.epi.swin = 1; ga.epi.sw_H = H; ga.epi.sw_W = W; ga.epi.sw_Hp = g.Hp; ga.epi.sw_Wp = g.Wp;
+  if ((rc = launch_gemm_bf16(ga, 1, true, st))) return rc;
+  return 0;
+}
+
+YS_EXPORT size_t yolosod_a2_workspace_bf16(int B, int C, int H, int W, int num_areas) {
+  const long ntok = (long)B * num_areas * W;
+  Sizer s;
+  s.take<bf16_t>((size_t)B * C * H * W);  // proj output
+  s.take<bf16_t>((size_t)ntok * C);       // S / T
+  s.take<bf16_t>((size_t)ntok * C);       // U
+  s.take<bf16_t>((size_t)ntok * 3 * C);   // QKV
+  s.take<float>((size_t)ntok * 2);        // LayerNorm row statistics
+  return s.off;
+}
+
+// A2_Attn.forward (a2_attn.py:35-69) on bf16 activations, residual form, with the MHA out-projection folded into
+// the output conv (oproj_w = Wconv . Wmha, oproj_b = Wconv . bmha + bconv; A2_Attn._fused_out). Weights proj
+// [C][C], in_proj [3C][C], oproj [C][C] bf16; biases / LN fp32.
+YS_EXPORT int yolosod_a2_forward_bf16(const bf16_t* x, bf16_t* y, int B, int C, int H, int W, int num_areas,
+                                      int num_heads, const bf16_t* proj_w, const float* proj_b, const float* ln_w,
+                                      const float* ln_b, float ln_eps, const bf16_t* in_proj_w,
+                                      const float* in_proj_b, const bf16_t* oproj_w, const float* oproj_b,
+                                      void* workspace, size_t workspace_bytes, void* stream) {
+  YS_CHECK_ARG(x && y && proj_w && proj_b && ln_w && ln_b && in_proj_w && in_proj_b && oproj_w && oproj_b,
+               "a2_bf16: null pointer");
+  YS_CHECK_ARG(B >= 0 && C > 0 && H > 0 && W > 0 && num_areas > 0, "a2_bf16: bad shape");
+  YS_CHECK_ARG(C % 64 == 0, "a2_bf16: C must be a multiple of 64");
+  YS_CHECK_ARG(((long)H * W) % 8 == 0, "a2_bf16: H*W must be a multiple of 8");
+  if (B == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  const int A = num_areas;
+  const long HW = (long)H * W;
+  const long ntok = (long)B * A * W;
+  Carver cv(workspace, workspace_bytes);
+  bf16_t* XP = cv.take<bf16_t>((size_t)B * C * HW);
+  bf16_t* S = cv.take<bf16_t>((size_t)ntok * C);
+  bf16_t* U = cv.take<bf16_t>((size_t)ntok * C);
+  bf16_t* Q = cv.take<bf16_t>((size_t)ntok * 3 * C);
+  float* lns = cv.take<float>((size_t)ntok * 2);
+  YS_CHECK_ARG(lns, "a2_bf16: workspace too small (%zu)", workspace_bytes);
+  int rc;
+  // XP = SiLU(Wp x + bp): M = Cout, N = HW (N-contiguous B), batched over images
+  GemmB ga{};
+  ga.A = proj_w; ga.lda = C; ga.B = x; ga.b_bs = C * HW; ga.ldb = (int)HW; ga.M = C; ga.N = (int)HW; ga.K = C;
+  ga.epi = epib_plain(XP, C * HW, (int)HW);
+  ga.epi.bias = proj_b; ga.epi.bias_mode = 1; ga.epi.act = 1;
+  if ((rc = launch_gemm_bf16(ga, B, false, st))) return rc;
+  YS_CHECK_ARG((size_t)64 * (W + 1) * sizeof(float) <= 64 * 1024, "a2_bf16: W=%d too large for the pooling kernel", W);
+  hipLaunchKernelGGL(a2_pool_tokens_bf16_kernel, dim3(B * A, (C + 63) / 64), dim3(256),
+                     (size_t)64 * (W + 1) * sizeof(float), st, XP, S, C, H, W, A);
+  YS_CHECK_LAUNCH("a2_pool_bf16");
+  if ((rc = launch_row_stats_bf16(S, C, ntok, C, ln_eps, lns, st))) return rc;
+  ga = GemmB{};
+  ga.A = S; ga.lda = C; ga.B = in_proj_w; ga.ldb = C; ga.M = (int)ntok; ga.N = 3 * C; ga.K = C;
+  ga.ln_w = ln_w; ga.ln_b = ln_b; ga.ln_stats = lns;
+  ga.epi = epib_plain(Q, 0, 3 * C);
+  ga.epi.bias = in_proj_b; ga.epi.bias_mode = 2;
+  if ((rc = launch_gemm_bf16(ga, 1, true, st))) return rc;
+  TokMap tm{};
+  tm.mode = 0;
+  tm.L = A * W;
+  if ((rc = launch_attention_bf16(Q, U, B, C, num_heads, tm, st))) return rc;
+  // T[img][n][t] = sum_c Wf[n][c] U[img*AW + t][c]   (S reused as T)
+  bf16_t* T = S;
+  ga = GemmB{};
+  ga.A = oproj_w; ga.lda = C; ga.B = U; ga.b_bs = (long)A * W * C; ga.ldb = C; ga.M = C; ga.N = A * W; ga.K = C;
+  ga.epi = epib_plain(T, (long)C * A * W, A * W);
+  if ((rc = launch_gemm_bf16(ga, B, true, st))) return rc;
+  hipLaunchKernelGGL(a2_upsample_out_bf16_kernel, dim3((unsigned)(B * C), (unsigned)((HW + 255) / 256)), dim3(256), 0,
+                     st, x, T, oproj_b, y, C, H, W, A);
+  YS_CHECK_LAUNCH("a2_upsample_bf16");
+  return 0;
+}

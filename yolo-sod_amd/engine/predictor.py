@@ -36,10 +36,13 @@ class DetectionPredictor:
         self.model = model
         self.conf, self.iou, self.max_det = conf, iou, max_det
         self.classes, self.agnostic, self.multi_label = classes, agnostic_nms, multi_label
-        self.device = next(model.parameters()).device
+        p = next(model.parameters())
+        self.device, self.dtype = p.device, p.dtype
 
     def preprocess(self, im: torch.Tensor) -> torch.Tensor:
-        return im.to(self.device, non_blocking=True).float()
+        """predictor.py:123-134 tensor branch: ``.to(device)``, ``.half()`` if the model is fp16 else ``.float()`` -
+        here the model's dtype (bf16 in the bf16 config)."""
+        return im.to(self.device, non_blocking=True).to(self.dtype)
 
     @torch.inference_mode()
     def predict_padded(self, im: torch.Tensor):

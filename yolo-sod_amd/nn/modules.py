@@ -43,6 +43,34 @@ def _is_meta(x: torch.Tensor) -> bool:
     return x.device.type == "meta"
 
 
+def _cached(mod: nn.Module, tag: str, srcs, make):
+    """``make()`` cached on ``mod`` against the identity / version / dtype of the source tensors (parameter
+    conversions for the HIP operators: recomputed only when a parameter is replaced or modified in place)."""
+    # inference tensors (made under torch.inference_mode, e.g. A2's folded weights) have no version counter: they
+    # are never modified in place outside inference mode, their identity is the key
+    key = tuple((t.data_ptr(), -1 if t.is_inference() else t._version, t.dtype, t.device) for t in srcs)
+    cache = mod.__dict__.setdefault("_ys_cache", {})
+    ent = cache.get(tag)
+    if ent is None or ent[0] != key:
+        ent = cache[tag] = (key, make())
+    return ent[1]
+
+
+def _f32(mod: nn.Module, tag: str, *ts):
+    """fp32 contiguous views of parameters (the HIP operators' small parameters are fp32 in either config); in
+    the bf16 model these are cached widened copies (exact)."""
+    if all(t.dtype == torch.float32 and t.is_contiguous() for t in ts):
+        return tuple(t.detach() for t in ts)
+    return _cached(mod, tag, ts, lambda: tuple(t.detach().float().contiguous() for t in ts))
+
+
+def _as(mod: nn.Module, tag: str, dtype, *ts):
+    """Parameters as contiguous ``dtype`` tensors (GEMM weights follow the activation dtype)."""
+    if all(t.dtype == dtype and t.is_contiguous() for t in ts):
+        return tuple(t.detach() for t in ts)
+    return _cached(mod, tag, ts, lambda: tuple(t.detach().to(dtype).contiguous() for t in ts))
+
+
 # ---------------------------------------------------------------------------------------------------------------
 # host PyTorch blocks
 # ---------------------------------------------------------------------------------------------------------------
@@ -69,7 +97,8 @@ def conv_epilogue(conv: nn.Conv2d, act_code, x, out=None, res=None, stats=None, 
     SE / CBAM gate (``_hip.PlaneStats`` on the returned tensor).
     ``out2``: also store channels [c2lo, C) packed there (the next conv's input; C2f's Bottleneck chain).
     Returns None when the fast path does not apply (CPU tensor, no bias, unsupported activation / shape)."""
-    if x.device.type != "cuda" or conv.bias is None or act_code is None or x.dtype != torch.float32:
+    if x.device.type != "cuda" or conv.bias is None or act_code is None or x.dtype not in (torch.float32,
+                                                                                           torch.bfloat16):
         return None
     if (THIN1X1 and act_code == 1 and (stats is None or (stats in ("sum", "summax") and res is None and out2 is None))
             and conv.out_channels == 64 and conv.kernel_size == (1, 1) and conv.stride == (1, 1)
@@ -77,7 +106,7 @@ def conv_epilogue(conv: nn.Conv2d, act_code, x, out=None, res=None, stats=None, 
             and (out is None or out.data_ptr() % 16 == 0) and (res is None or res.data_ptr() % 16 == 0)):
         return _hip.conv1x1_thin(x, conv.weight.detach().reshape(conv.out_channels, -1), conv.bias.detach(),
                                  out=out, res=res, out2=out2, c2lo=c2lo, stats=stats)
-    if (CONV1X1_GEMM and conv.kernel_size == (1, 1) and conv.stride == (1, 1) and conv.groups == 1 and conv.padding == (0, 0)
+    if (CONV1X1_GEMM and x.dtype == torch.float32 and conv.kernel_size == (1, 1) and conv.stride == (1, 1) and conv.groups == 1 and conv.padding == (0, 0)
             and conv.in_channels % 32 == 0 and x.stride(1) == x.shape[2] * x.shape[3] and x.stride(3) == 1
             and x.stride(2) == x.shape[3] and (x.shape[2] * x.shape[3]) % 4 == 0 and x.stride(0) % 4 == 0):
         # 1x1 conv = GEMM on NCHW with the epilogue fused (no MIOpen layout transposes, no extra pass)
@@ -87,7 +116,7 @@ def conv_epilogue(conv: nn.Conv2d, act_code, x, out=None, res=None, stats=None, 
             out2.copy_(y[:, c2lo:])
         return y
     y = F.conv2d(x, conv.weight, None, conv.stride, conv.padding, conv.dilation, conv.groups)
-    if (y.shape[2] * y.shape[3]) % 4:
+    if (y.shape[2] * y.shape[3]) % 4 or y.dtype != x.dtype:
         y = y + conv.bias.view(1, -1, 1, 1)
         y = F.silu(y) if act_code == 1 else y
         if res is not None:
@@ -98,7 +127,8 @@ def conv_epilogue(conv: nn.Conv2d, act_code, x, out=None, res=None, stats=None, 
             out.copy_(y)
             return out
         return y
-    return _hip.bias_act(y, conv.bias.detach(), act_code, out=out, res=res, stats=stats, out2=out2, c2lo=c2lo)
+    (bias,) = _f32(conv, "bias", conv.bias)
+    return _hip.bias_act(y, bias, act_code, out=out, res=res, stats=stats, out2=out2, c2lo=c2lo)
 
 
 class Conv(nn.Module):
@@ -272,8 +302,8 @@ class SE(nn.Module):
             self.fc2 = nn.Conv2d(hidden, c, 1, bias=True)
             self.in_channels = c
         if device is not None and torch.device(device).type != "meta":
-            self.fc1.to(device=device, dtype=torch.float32)
-            self.fc2.to(device=device, dtype=torch.float32)
+            self.fc1.to(device=device)
+            self.fc2.to(device=device)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         b, c, h, w = x.shape
@@ -282,8 +312,7 @@ class SE(nn.Module):
                 raise RuntimeError("SE: lazy weights must be materialised before a meta shape probe")
             return torch.empty_like(x)
         self._maybe_build(c, x.device)
-        return _hip.se_forward(x, self.fc1.weight.detach(), self.fc1.bias.detach(), self.fc2.weight.detach(),
-                               self.fc2.bias.detach())
+        return _hip.se_forward(x, *_f32(self, "fc", self.fc1.weight, self.fc1.bias, self.fc2.weight, self.fc2.bias))
 
 
 SE_Block = SE
@@ -324,8 +353,8 @@ class CBAM_Block(nn.Module):
         fc = self.channel_attention.fc
         if self.spatial_attention.conv1.kernel_size != (7, 7):
             raise RuntimeError("CBAM_Block: only the 7x7 spatial kernel is implemented")
-        return _hip.cbam_forward(x, fc[0].weight.detach(), fc[2].weight.detach(),
-                                 self.spatial_attention.conv1.weight.detach())
+        return _hip.cbam_forward(x, *_f32(self, "p", fc[0].weight, fc[2].weight,
+                                          self.spatial_attention.conv1.weight))
 
 
 class h_sigmoid(nn.Module):
@@ -356,11 +385,10 @@ class CA_Block(nn.Module):
             return torch.empty_like(x)
         if self.training:
             raise RuntimeError("CA_Block: HIP path is inference-only (eval-mode BatchNorm)")
-        d = lambda t: t.detach()  # noqa: E731
-        return _hip.ca_forward(x, d(self.conv1.weight), d(self.conv1.bias), d(self.bn1.weight), d(self.bn1.bias),
-                               d(self.bn1.running_mean), d(self.bn1.running_var), self.bn1.eps,
-                               d(self.conv_h.weight), d(self.conv_h.bias), d(self.conv_w.weight),
-                               d(self.conv_w.bias))
+        p = _f32(self, "p", self.conv1.weight, self.conv1.bias, self.bn1.weight, self.bn1.bias,
+                 self.bn1.running_mean, self.bn1.running_var, self.conv_h.weight, self.conv_h.bias,
+                 self.conv_w.weight, self.conv_w.bias)
+        return _hip.ca_forward(x, *p[:6], self.bn1.eps, *p[6:])
 
 
 class A2_Attn(nn.Module):
@@ -388,9 +416,11 @@ class A2_Attn(nn.Module):
         pw, pb = conv_weight_bias(self.proj)
         at = self.attention
         fw, fb = self._fused_out()
-        return _hip.a2_forward(x, self.num_areas, self.num_heads, pw, pb, self.layer_norm.weight.detach(),
-                               self.layer_norm.bias.detach(), self.layer_norm.eps, at.in_proj_weight.detach(),
-                               at.in_proj_bias.detach(), None, None, fw, fb)
+        dt = x.dtype
+        pw, at_w, fw = _as(self, "w", dt, pw, at.in_proj_weight, fw)
+        pb, lw, lb, at_b, fb = _f32(self, "b", pb, self.layer_norm.weight, self.layer_norm.bias, at.in_proj_bias, fb)
+        return _hip.a2_forward(x, self.num_areas, self.num_heads, pw, pb, lw, lb, self.layer_norm.eps, at_w, at_b,
+                               None, None, fw, fb)
 
     def _fused_out(self):
         """MHA out-projection (a2_attn.py:53) and the output 1x1 conv (a2_attn.py:63) are consecutive linear maps
@@ -405,8 +435,8 @@ class A2_Attn(nn.Module):
         if cache is None or cache[0] != key:
             ow, ob = conv_weight_bias(op)
             mw, mb = at.out_proj.weight.detach(), at.out_proj.bias.detach()
-            fw = (ow.double() @ mw.double()).float().contiguous()
-            fb = (ow.double() @ mb.double() + ob.double()).float().contiguous()
+            fw = (ow.double() @ mw.double()).to(ow.dtype).contiguous()
+            fb = (ow.double() @ mb.double() + ob.double()).to(ow.dtype).contiguous()
             cache = (key, fw, fb)
             self._fused_cache = cache
         return cache[1], cache[2]
@@ -442,13 +472,16 @@ class SwinBlock(nn.Module):
         if self.training:
             raise RuntimeError("SwinBlock: HIP path is inference-only (eval-mode BatchNorm)")
         wa = self.window_attn
-        d = lambda t: t.detach()  # noqa: E731
+        at = wa.attn
+        in_w, out_w, m1_w, m2_w, pw_w = _as(self, "w", x.dtype, at.in_proj_weight, at.out_proj.weight,
+                                            wa.mlp[0].weight, wa.mlp[2].weight, self.pw.weight)
+        (dw, n1w, n1b, in_b, out_b, n2w, n2b, m1_b, m2_b, bnw, bnb, bnm, bnv) = _f32(
+            self, "p", self.dw.weight, wa.norm1.weight, wa.norm1.bias, at.in_proj_bias, at.out_proj.bias,
+            wa.norm2.weight, wa.norm2.bias, wa.mlp[0].bias, wa.mlp[2].bias, self.bn.weight, self.bn.bias,
+            self.bn.running_mean, self.bn.running_var)
         return _hip.swin_forward(
-            x, wa.attn.num_heads, wa.window_size, d(self.dw.weight), d(wa.norm1.weight), d(wa.norm1.bias),
-            wa.norm1.eps, d(wa.attn.in_proj_weight), d(wa.attn.in_proj_bias), d(wa.attn.out_proj.weight),
-            d(wa.attn.out_proj.bias), d(wa.norm2.weight), d(wa.norm2.bias), wa.norm2.eps, d(wa.mlp[0].weight),
-            d(wa.mlp[0].bias), d(wa.mlp[2].weight), d(wa.mlp[2].bias), d(self.pw.weight), d(self.bn.weight),
-            d(self.bn.bias), d(self.bn.running_mean), d(self.bn.running_var), self.bn.eps)
+            x, at.num_heads, wa.window_size, dw, n1w, n1b, wa.norm1.eps, in_w, in_b, out_w, out_b, n2w, n2b,
+            wa.norm2.eps, m1_w, m1_b, m2_w, m2_b, pw_w, bnw, bnb, bnm, bnv, self.bn.eps)
 
 
 class Conv1x1BN(nn.Sequential):
@@ -554,7 +587,7 @@ class Detect(nn.Module):
             return False
         b2, b3 = self.cv2[0][-1], self.cv3[0][-1]
         return (self.reg_max == 16 and 1 <= self.nc <= 16 and b2.in_channels == 64 and b3.in_channels in (64, 128)
-                and b2.bias is not None and b3.bias is not None and x[0].dtype == torch.float32)
+                and b2.bias is not None and b3.bias is not None and x[0].dtype in (torch.float32, torch.bfloat16))
 
     def tower_features(self, i, xi):
         """Level i's box / class tower features (cv2[i][:-1], cv3[i][:-1]): the inputs of the fused head kernel."""
@@ -575,10 +608,12 @@ class Detect(nn.Module):
         return self._head(fb, fc)
 
     def _head(self, fb, fc):
-        w = lambda c: c.weight.detach().reshape(c.out_channels, -1)  # noqa: E731
-        y = _hip.detect_head(fb, fc, [w(b[-1]) for b in self.cv2], [b[-1].bias.detach() for b in self.cv2],
-                             [w(b[-1]) for b in self.cv3], [b[-1].bias.detach() for b in self.cv3],
-                             [float(s) for s in self.stride], self.nc, self.reg_max)
+        nl = self.nl
+        p = _f32(self, "head", *[c[-1].weight for c in self.cv2], *[c[-1].bias for c in self.cv2],
+                 *[c[-1].weight for c in self.cv3], *[c[-1].bias for c in self.cv3])
+        w = lambda t: t.reshape(t.shape[0], -1)  # noqa: E731
+        y = _hip.detect_head(fb, fc, [w(t) for t in p[:nl]], list(p[nl:2 * nl]), [w(t) for t in p[2 * nl:3 * nl]],
+                             list(p[3 * nl:]), [float(s) for s in self.stride], self.nc, self.reg_max)
         return y, RawMaps(self, fb, fc)
 
     def raw_from_features(self, i, h2, h3):
@@ -605,7 +640,9 @@ class Detect(nn.Module):
         if x[0].device.type == "meta":
             a = sum(t.shape[2] * t.shape[3] for t in x)
             return torch.empty((x[0].shape[0], 4 + self.nc, a), device="meta")
-        return _hip.detect_decode(x, [float(s) for s in self.stride], self.nc, self.reg_max)
+        # the decode runs in fp32 in either config (fp32 anchors / decode in the bf16 model)
+        return _hip.detect_decode([t.float().contiguous() for t in x], [float(s) for s in self.stride], self.nc,
+                                  self.reg_max)
 
     def bias_init(self):
         """Detect biases (head.py:133-144)."""

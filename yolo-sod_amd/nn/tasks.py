@@ -392,10 +392,18 @@ class DetectionModel(BaseModel):
 
 
 def build_model(cfg="yolov12-sod-fusion-v5-simple.yaml", seed: int = 0, device="cuda", fuse: bool = True,
-                registry=None) -> DetectionModel:
-    """Seeded construction -> (fused) eval model on ``device`` (autobackend.py:145-156 semantics)."""
+                registry=None, dtype=torch.float32) -> DetectionModel:
+    """Seeded construction -> (fused) eval model on ``device`` (autobackend.py:145-156 semantics).
+
+    ``dtype=torch.bfloat16`` is the bf16 config: fuse in fp32, then store every parameter / buffer and every
+    activation as bf16 - AutoBackend's ``fp16`` path (``model.half()`` after ``fuse()``, autobackend.py:145-156, and
+    the predictor's ``im.half()``) with bfloat16. The HIP operators accumulate in fp32; Detect's decode and NMS stay
+    fp32."""
     torch.manual_seed(seed)
     m = DetectionModel(cfg, registry=registry)
     if fuse:
         m.fuse()
-    return m.to(device).eval()
+    m = m.to(device)
+    if dtype != torch.float32:
+        m = m.to(dtype)
+    return m.eval()

@@ -7,9 +7,20 @@ from __future__ import annotations
 
 F32 = 4
 
-# MI355X peaks (MI355X_MICROARCH.md "Chip-level parameters")
+# MI355X peaks (MI355X_MICROARCH.md "Chip-level parameters" / "Matrix cores"): dense, no sparsity
 PEAK_HBM_GBS = 8000.0
 PEAK_FP32_MFMA_TFLOPS = 157.3
+PEAK_BF16_MFMA_TFLOPS = 2516.6  # 16x the f32 MFMA rate per clock (256 CUs x 4 SIMDs x 1024 flop/clk x 2.4 GHz)
+
+
+def elem_size(key) -> int:
+    """Bytes per activation element of a recorded launch: keys of bf16 launches carry a 4th element 2."""
+    return key[3] if len(key) > 3 else F32
+
+
+def peak_tflops(key) -> float:
+    """Matrix-core peak of the arithmetic the launch runs: bf16 MFMA for bf16 activations, fp32 MFMA otherwise."""
+    return PEAK_BF16_MFMA_TFLOPS if elem_size(key) == 2 else PEAK_FP32_MFMA_TFLOPS
 
 
 # operators of the SURVEY 8(a) path (rooflined); other keys the op_timer records are backbone conv kernels
@@ -24,12 +35,18 @@ def swin_geom(H, W, ws=7):
 
 
 def op_cost(key):
-    """key = (op, shape, extra) as recorded by yolosod_amd._hip.op_timer -> (bytes, flops)."""
+    """key = (op, shape, extra[, elem bytes]) as recorded by yolosod_amd._hip.op_timer -> (bytes, flops).
+    Activations count at the launch's element size (2 for the bf16 config), parameters at 4 bytes."""
+    b, f = _op_cost(key[:3], elem_size(key))
+    return b, f
+
+
+def _op_cost(key, E):
     op, shape, extra = key
     if op in ("se", "cbam", "ca"):
         B, C, H, W = shape
         hid = extra
-        act = 2 * B * C * H * W * F32
+        act = 2 * B * C * H * W * E
         w = (2 * C * hid + C + hid) * F32
         flops = B * C * H * W * (2 if op == "se" else 6)
         return act + w, flops
@@ -37,7 +54,7 @@ def op_cost(key):
         B, C, H, W = shape
         A, heads = extra
         L = A * W
-        act = 2 * B * C * H * W * F32
+        act = 2 * B * C * H * W * E
         w = (2 * (C * C + C) + 4 * C * C + 4 * C + 2 * C) * F32
         conv = 2 * 2 * C * C * H * W  # proj + out_proj (1x1 convs on the full map)
         mha = 2 * L * C * 3 * C + 2 * L * C * C + 2 * 2 * L * L * C
@@ -48,7 +65,7 @@ def op_cost(key):
         wh, ww, Hp, Wp = swin_geom(H, W, ws)
         L = wh * ww
         tok_p = Hp * Wp
-        act = 2 * B * C * H * W * F32
+        act = 2 * B * C * H * W * E
         w = (9 * C + 4 * C * C + 3 * C + C + 2 * C * hid + hid + C + C * C + 6 * C) * F32
         dense = tok_p * (2 * C * 3 * C + 2 * C * C + 2 * 2 * C * hid) + H * W * 2 * C * C
         attn = tok_p * 2 * 2 * L * C
@@ -59,7 +76,7 @@ def op_cost(key):
         ch, r = extra
         hd = 2 * ch
         hw, hwh = H * W, (H // r) * (W // r)
-        act = 2 * B * C * hw * F32
+        act = 2 * B * C * hw * E
         w = (ch * C + 2 * hd * ch + 9 * hd + ch * hd + C * ch + 4 * (ch + hd + C)) * F32
         flops = 2 * ch * C * hw + hwh * (2 * 2 * hd * ch + 2 * 9 * hd + 2 * ch * hd + 2 * C * ch)
         return act + w, B * flops
@@ -70,7 +87,7 @@ def op_cost(key):
     if op == "head":  # fused last 1x1 convs of both towers + decode: reads the tower features, writes y
         B, A = shape
         nc, c2, c3 = extra
-        return (B * A * ((c2 + c3) + (4 + nc)) * F32 + (64 * c2 + nc * c3 + 64 + nc) * F32,
+        return (B * A * ((c2 + c3) * E + (4 + nc) * F32) + (64 * c2 + nc * c3 + 64 + nc) * F32,
                 B * A * (2 * (64 * c2 + nc * c3) + 64 * 4 + nc * 4))
     if op == "nms":
         B, nc, A = shape
@@ -78,5 +95,12 @@ def op_cost(key):
     raise KeyError(op)
 
 
-def bound_of(op):
-    return "mfma" if op in ("swin", "a2", "mamba") else "hbm"
+def bound_of(key) -> str:
+    """The roof that bounds a launch: whichever of its HBM time and matrix-core time is longer."""
+    nbytes, flops = op_cost(key)
+    return "mfma" if flops / (peak_tflops(key) * 1e12) > nbytes / (PEAK_HBM_GBS * 1e9) else "hbm"
+
+
+def t_min_ms(key) -> float:
+    nbytes, flops = op_cost(key)
+    return max(nbytes / (PEAK_HBM_GBS * 1e9), flops / (peak_tflops(key) * 1e12)) * 1e3
