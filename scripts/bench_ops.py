@@ -25,6 +25,12 @@ CASES = {
     "se_L23": ("SE_Block", (256,), (32, 128, 80, 80)),
     "mamba_L7": ("MambaBlock", (128, 256, 2), (32, 128, 80, 80)),  # yolov12-sod-fusion-v5 only
     "head": ("detect_head", (64, 64, 10), (32, 0, 640, 640)),  # fused Detect tail + decode, 4 levels P2..P5
+    # bf16 m-scale config (bs=64): run with --bf16
+    "swin_L28_m": ("SwinBlock", (128, 2, 7), (64, 128, 160, 160)),
+    "swin_L9_m": ("SwinBlock", (512, 4, 7), (64, 512, 40, 40)),
+    "a2_L12_m": ("A2_Attn", (512, None, 8, 8), (64, 512, 20, 20)),
+    "cbam_L4_m": ("CBAM_Block", (128, 128, 16), (64, 128, 160, 160)),
+    "ca_L32_m": ("CA_Block", (256, 256, 32), (64, 256, 80, 80)),
 }
 
 
@@ -41,8 +47,11 @@ def head_case(dev, c2, c3, nc, B, S):
 
 
 def main():
-    names = sys.argv[1:] or list(CASES)
+    args = sys.argv[1:]
+    bf16 = "--bf16" in args
+    names = [a for a in args if not a.startswith("--")] or list(CASES)
     dev = torch.device("cuda")
+    dt = torch.bfloat16 if bf16 else torch.float32
     for name in names:
         op, args, shape = CASES[name]
         if op == "detect_head":
@@ -53,8 +62,13 @@ def main():
             if op == "SE_Block":
                 m._maybe_build(shape[1], None)
             recipes.perturb_(m, 1)
-            m = m.to(dev).eval()
-            x = torch.randn(shape, device=dev)
+            m = m.to(dev).to(dt).eval()
+            x = torch.randn(shape, device=dev).to(dt)
+            # SE / CBAM / CA as the model runs them: x comes from a conv epilogue that also emitted the gate's
+            # statistics (bias_act stats=...), so the timed call takes the *_pre path (no statistics pass over x)
+            mode = {"SE_Block": "sum", "CBAM_Block": "summax", "CA_Block": "capool"}.get(op)
+            if mode:
+                x = _hip.bias_act(x, torch.zeros(shape[1], device=dev), 0, out=torch.empty_like(x), stats=mode)
         with torch.inference_mode():
             for _ in range(3):
                 m(x)

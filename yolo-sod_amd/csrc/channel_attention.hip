@@ -6,10 +6,12 @@
 //       normally emitted by x's producing conv epilogue (conv_epilogue.hip), so no extra pass over x,
 //   (2) the gate (the SE / CBAM channel MLP, the CA conv1+BN+h_sigmoid+conv_h/w gates),
 //   (3) one streaming apply pass that reads x once and writes y once (coalesced vectors, every lane busy).
-// SE recomputes its (tiny) channel MLP inside the apply workgroups: gate + scale is one launch. CBAM is two:
-// channel gate + per-pixel channel mean/max of ca*x (per 32-channel group), then the 7x7 spatial conv of each
-// workgroup's pixels (halo of the mean/max map in LDS) + apply. The older split kernels stay as the path for
-// shapes the fused ones do not take (H*W % 4 != 0, very wide rows).
+// SE recomputes its (tiny) channel MLP inside the apply workgroups: gate + scale is one launch. CBAM is three:
+// channel gate + per-pixel channel mean/max of ca*x (per 32-channel group) in one, the 7x7 spatial conv, the apply.
+// (A 2-launch CBAM with the spatial conv evaluated inside 1024-pixel apply workgroups - halo rows of the map in LDS,
+// first channel slab prefetched across the conv - measured slower on MI355X: L4 0.186 vs 0.132 ms, L18 0.080 vs
+// 0.053: far fewer workgroups stream the tensor, and the per-workgroup halo combine over the channel groups
+// re-reads the partial maps; it was removed.)
 // Optionally (YOLOSOD_MALL_CHUNK_MB > 0) the host driver walks the batch in image chunks sized to stay resident
 // in the 256 MiB Infinity Cache between the passes. Measured on MI355X at the bs=32 640x640 shapes, the apply
 // pass' re-read does hit on-die (7.3 TB/s) but the extra launch boundaries and the smaller grids cost more
@@ -397,70 +399,6 @@ __global__ __launch_bounds__(256) void cbam_apply_kernel(const T* __restrict__ x
   }
 }
 
-// CBAM pass 3 (fused path): spatial gate + apply. Workgroup = 1024 consecutive pixels (4 per lane) x up to 64
-// channels of one image. The rows those pixels touch, +-3 rows of halo and 3 columns of zero padding each side, of
-// the [mean; max] map are combined from the G group partials into LDS; each lane then evaluates the 7x7 conv
-// (+ sigmoid) at its 4 pixels and streams y = sa * (ca * x) over the channels with 8 vector loads in flight.
-// grid = (ceil(HW / 1024), ceil(C / 64), images); dynamic LDS = 2 * nrows * (W + 6) floats.
-constexpr int kCbamApplyC = 64;
-template <class T>
-__global__ __launch_bounds__(256) void cbam_sa_apply_kernel(const T* __restrict__ x, T* __restrict__ y,
-                                                            const float* __restrict__ ca,
-                                                            const float* __restrict__ mpart, int G, int C, int H,
-                                                            int W, const float* __restrict__ wsa) {
-  extern __shared__ float mm[];  // [2][nrows][W + 6]
-  __shared__ float wk[98];
-  const int b = blockIdx.z;
-  const long HW = (long)H * W;
-  const int tid = threadIdx.x;
-  const long pb0 = (long)blockIdx.x * 1024;
-  const long pb1 = (pb0 + 1024 < HW) ? pb0 + 1024 : HW;
-  const int r0 = (int)(pb0 / W) - 3;
-  const int nrows = (int)((pb1 - 1) / W) + 4 - r0;
-  const int WS = W + 6;
-  if (tid < 98) wk[tid] = wsa[tid];
-  const float invC = 1.0f / (float)C;
-  const float* mp = mpart + (long)b * G * 2 * HW;
-  for (int i = tid; i < nrows * WS; i += 256) {
-    const int ry = i / WS, rx = i - ry * WS;
-    const float2 v = cbam_map_at(mp, G, HW, H, W, r0 + ry, rx - 3, invC);
-    mm[i] = v.x;
-    mm[nrows * WS + i] = v.y;
-  }
-  __syncthreads();
-  const long p = pb0 + 4L * tid;
-  if (p >= HW) return;
-  f32x4 s4;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const long pi = p + i;
-    const int py = (int)(pi / W), px = (int)(pi - (long)py * W);
-    const float* m0 = mm + (py - r0 - 3) * WS + px;  // tap (ky, kx) of map ci at m0[ci*nrows*WS + ky*WS + kx]
-    float z = 0.f;
-#pragma unroll
-    for (int ci = 0; ci < 2; ++ci)
-#pragma unroll
-      for (int ky = 0; ky < 7; ++ky)
-#pragma unroll
-        for (int kx = 0; kx < 7; ++kx) z += wk[ci * 49 + ky * 7 + kx] * m0[ci * nrows * WS + ky * WS + kx];
-    s4[i] = sigmoidf_(z);
-  }
-  const int c0 = blockIdx.y * kCbamApplyC;
-  const int c1 = (c0 + kCbamApplyC < C) ? c0 + kCbamApplyC : C;
-  const float* cab = ca + (long)b * C;
-  const T* xb = x + (long)b * C * HW + p;
-  T* yb = y + (long)b * C * HW + p;
-  int c = c0;
-  for (; c + 8 <= c1; c += 8) {
-    f32x4 v[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = ld4(xb + (long)(c + u) * HW);
-#pragma unroll
-    for (int u = 0; u < 8; ++u) st4(yb + (long)(c + u) * HW, s4 * (cab[c + u] * v[u]));
-  }
-  for (; c < c1; ++c) st4(yb + (long)c * HW, s4 * (cab[c] * ld4(xb + (long)c * HW)));
-}
-
 // ------------------------------------------------------------------------------------------------
 // CA pass 1: row means (over W) and column means (over H) of each (b,c) plane -> yin[b][c][0..H+W).
 // One workgroup per plane; the plane streams through LDS in bands of <= 8192 floats (vector loads when W % 4
@@ -726,10 +664,8 @@ static int cbam_forward_impl(const T* x, T* y, int B, int C, int H, int W, const
   hipStream_t st = (hipStream_t)stream;
   const PartPlan pp = part_plan(HW);
   const size_t lds = sizeof(float) * (3 * (size_t)C + 128);
-  // fused launches: gate + pixel statistics, then spatial gate + apply (1024-pixel workgroups, halo rows in LDS)
-  const int nrows_max = (int)((1023 + W - 1) / W) + 8;
-  const size_t lds_sa = sizeof(float) * 2 * (size_t)nrows_max * (W + 6);
-  const bool fused = fused_gates() && V == 4 && lds <= 64 * 1024 && lds_sa <= 64 * 1024;
+  // fused launch: channel gate + pixel statistics
+  const bool fused = fused_gates() && V == 4 && lds <= 64 * 1024;
   YS_CHECK_ARG(lds <= 64 * 1024, "cbam: C=%d too large for the gate kernel", C);
   for (int b0 = 0; b0 < B; b0 += ipc) {
     const int nb = (B - b0 < ipc) ? B - b0 : ipc;
@@ -742,22 +678,19 @@ static int cbam_forward_impl(const T* x, T* y, int B, int C, int H, int W, const
       hipLaunchKernelGGL((plane_part_stats_kernel<true, T>), dim3((unsigned)(nb * C * pp.parts)), dim3(256), 0, st,
                          x + off, HW, pp.parts, pp.seg, psum + (long)b0 * C * pp.parts, pmax + (long)b0 * C * pp.parts);
     dim3 gs((unsigned)pxb, G, nb);
-    if (fused) {
+    if (fused) {  // channel gate computed inside the pixel-statistics workgroups
       hipLaunchKernelGGL((cbam_pixel_stats_kernel<4, T, true>), gs, dim3(256), lds, st, x + off, cab, C, kCbamGroup,
                          HW, mpart, ps, pm, pp.parts, 1.0f / (float)HW, fc0_w, fc2_w, hidden);
-      dim3 ga((unsigned)((HW + 1023) / 1024), (unsigned)((C + kCbamApplyC - 1) / kCbamApplyC), nb);
-      hipLaunchKernelGGL((cbam_sa_apply_kernel<T>), ga, dim3(256), lds_sa, st, x + off, y + off, cab, mpart, G, C, H, W,
-                         sa_w);
-      continue;
+    } else {
+      hipLaunchKernelGGL((channel_gate_kernel<true>), dim3(nb), dim3(256), lds, st, ps, pm, pp.parts, C,
+                         1.0f / (float)HW, fc0_w, nullptr, fc2_w, nullptr, hidden, cab);
+      if (V == 4)
+        hipLaunchKernelGGL((cbam_pixel_stats_kernel<4, T, false>), gs, dim3(256), 0, st, x + off, cab, C, kCbamGroup,
+                           HW, mpart, nullptr, nullptr, 0, 0.f, nullptr, nullptr, 0);
+      else
+        hipLaunchKernelGGL((cbam_pixel_stats_kernel<1, T, false>), gs, dim3(256), 0, st, x + off, cab, C, kCbamGroup,
+                           HW, mpart, nullptr, nullptr, 0, 0.f, nullptr, nullptr, 0);
     }
-    hipLaunchKernelGGL((channel_gate_kernel<true>), dim3(nb), dim3(256), lds, st, ps, pm, pp.parts, C,
-                       1.0f / (float)HW, fc0_w, nullptr, fc2_w, nullptr, hidden, cab);
-    if (V == 4)
-      hipLaunchKernelGGL((cbam_pixel_stats_kernel<4, T, false>), gs, dim3(256), 0, st, x + off, cab, C, kCbamGroup, HW,
-                         mpart, nullptr, nullptr, 0, 0.f, nullptr, nullptr, 0);
-    else
-      hipLaunchKernelGGL((cbam_pixel_stats_kernel<1, T, false>), gs, dim3(256), 0, st, x + off, cab, C, kCbamGroup, HW,
-                         mpart, nullptr, nullptr, 0, 0.f, nullptr, nullptr, 0);
     hipLaunchKernelGGL(cbam_sa_kernel, dim3((W + 15) / 16, (H + 15) / 16, nb), dim3(256), 0, st, mpart, G, C, H, W,
                        sa_w, sab);
     dim3 ga((unsigned)pxb, (C + 7) / 8, nb);

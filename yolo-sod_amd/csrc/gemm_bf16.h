@@ -108,19 +108,6 @@ __device__ __forceinline__ float act_b(float v, int act) {
   return v;
 }
 
-// 8 bf16 (one uint4) <-> fp32
-__device__ __forceinline__ void unpack8(uint4 u, float* f) {
-  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    f[2 * i] = __uint_as_float(w[i] << 16);
-    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
-  }
-}
-__device__ __forceinline__ uint4 pack8(const float* f) {
-  return make_uint4(pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3]), pack_bf16x2(f[4], f[5]), pack_bf16x2(f[6], f[7]));
-}
-
 template <int WM, int WN, int MI, int NI, bool B_KC, bool A_LN>
 __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmB g) {
   constexpr int BM = WM * MI * 32;
@@ -310,32 +297,42 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmB g) {
     }
     return;
   }
-  // scalar epilogue: lanes along n (Swin: consecutive raster tokens = consecutive pixels of a row), rows over m
-  for (int idx = tid; idx < BM * BN; idx += 256) {
-    const int row = idx / BN, col = idx % BN;
-    const int m = m0 + row, n = n0 + col;
-    if (m >= M || n >= N) continue;
+  // scalar epilogue: lanes along n (Swin: consecutive raster tokens = consecutive pixels of an output row). A
+  // thread's column is the same in every row pass (256 % BN == 0), so its output offset (token -> pixel, crop) is
+  // computed once; rows advance by the channel plane.
+  static_assert(256 % BN == 0, "column per thread");
+  const int col = tid % BN, n = n0 + col;
+  if (n >= N) return;
+  long o0, r0_, m_str, r_str;
+  if (e.swin) {
+    const long per_img = (long)e.sw_Hp * e.sw_Wp;
+    const int img = (int)(n / per_img);
+    const int rr = (int)(n - img * per_img);
+    const int h = rr / e.sw_Wp, w = rr - (rr / e.sw_Wp) * e.sw_Wp;
+    if (h >= e.sw_H || w >= e.sw_W) return;  // crop of the padded border
+    m_str = (long)e.sw_H * e.sw_W;           // out / res NCHW [img][M][H][W]
+    o0 = (long)img * M * m_str + (long)h * e.sw_W + w;
+    r0_ = o0;
+    r_str = m_str;
+  } else {
+    m_str = e.ldc;
+    r_str = e.ldr;
+    o0 = (long)bz * e.out_bs + n;
+    r0_ = (long)bz * e.res_bs + n;
+  }
+  const float bn_ = e.bias_mode == 2 ? e.bias[n] : 0.f;
+  const float sc_n = e.bn_mode == 2 ? e.scale[n] : 1.f, sh_n = e.bn_mode == 2 ? e.shift[n] : 0.f;
+  for (int row = tid / BN; row < BM; row += 256 / BN) {
+    const int m = m0 + row;
+    if (m >= M) break;
     float v = Cs[row * SC + col];
     if (e.bias_mode == 1) v += e.bias[m];
-    else if (e.bias_mode == 2) v += e.bias[n];
+    else if (e.bias_mode == 2) v += bn_;
     if (e.bn_mode == 1) v = v * e.scale[m] + e.shift[m];
-    else if (e.bn_mode == 2) v = v * e.scale[n] + e.shift[n];
+    else if (e.bn_mode == 2) v = v * sc_n + sh_n;
     v = act_b(v, e.act);
-    long o, ro;
-    if (e.swin) {
-      const long per_img = (long)e.sw_Hp * e.sw_Wp;
-      const int img = (int)(n / per_img);
-      const int rr = (int)(n - img * per_img);
-      const int h = rr / e.sw_Wp, w = rr - (rr / e.sw_Wp) * e.sw_Wp;
-      if (h >= e.sw_H || w >= e.sw_W) continue;
-      o = ((long)img * M + m) * ((long)e.sw_H * e.sw_W) + (long)h * e.sw_W + w;  // out / res NCHW [img][M][H][W]
-      ro = o;
-    } else {
-      o = (long)bz * e.out_bs + (long)m * e.ldc + n;
-      ro = (long)bz * e.res_bs + (long)m * e.ldr + n;
-    }
-    if (e.res) v += bf2f(e.res[ro]);
-    e.out[o] = f2bf(v);
+    if (e.res) v += bf2f(e.res[r0_ + (long)m * r_str]);
+    e.out[o0 + (long)m * m_str] = f2bf(v);
   }
 }
 

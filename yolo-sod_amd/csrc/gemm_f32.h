@@ -55,6 +55,7 @@ struct GemmArgs {
   int tiles_n, tiles;     // set by launch_gemm
   Epi epi;
   int nimg;               // set by launch_gemm: > 0 = batch folded into N (N-contiguous B, nimg columns per image)
+  int nmajor;             // set by launch_gemm: tiles in column-major (n-major) order
 };
 
 // Per-row LayerNorm statistics (mean, 1/sqrt(var + eps)) of a K-contiguous [rows][K] matrix: one wave per row,
@@ -142,7 +143,15 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
   const int tpx = (g.tiles + 7) >> 3;
   const int t = (blockIdx.x & 7) * tpx + (blockIdx.x >> 3);
   if (t >= g.tiles) return;
-  const int m0 = (t / g.tiles_n) * BM, n0 = (t % g.tiles_n) * BN;
+  int m0, n0;
+  if (g.nmajor) {  // all M tiles of an N column on one XCD: an N-contiguous B (NCHW activations) is read once
+    const int tiles_m = g.tiles / g.tiles_n;
+    m0 = (t % tiles_m) * BM;
+    n0 = (t / tiles_m) * BN;
+  } else {
+    m0 = (t / g.tiles_n) * BM;
+    n0 = (t % g.tiles_n) * BN;
+  }
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
@@ -391,9 +400,11 @@ static inline int launch_gemm(const GemmArgs& g0, int batch, bool b_kc, hipStrea
   // N-contiguous B with a per-image N that is not a multiple of 128 (A2 at 640: H*W = 400): fold the batch into N so
   // the tiles run across image boundaries instead of padding every image's last tile column
   g.nimg = 0;
+  g.nmajor = 0;
   if (!b_kc && batch > 1 && g.a_bs == 0 && g.N % 128 != 0 && g.N % 4 == 0 && g.epi.vec && e.bias_mode != 2 && e.bn_mode != 2 &&
       g.ldb % 4 == 0 && g.b_bs % 4 == 0 && (long)g.N * batch < (1L << 31) && !getenv("YOLOSOD_GEMM_NOFOLD")) {
     g.nimg = g.N;
+    g.nmajor = 1;
     g.N *= batch;
     batch = 1;
   }

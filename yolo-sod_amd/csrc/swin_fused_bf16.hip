@@ -1,0 +1,540 @@
+// Fused SwinBlock for the bf16 config at C = 64 / 128 (the P2 instance L28: C = 128 at the m scale), 7x7 windows.
+//
+// One 256-thread workgroup processes one window; two workgroups per CU (LDS ~73 KB at C = 128). The window's tokens
+// stay in LDS from the depthwise conv to the pw1x1 + BN + SiLU + residual store, so the per-window HBM traffic is
+// the x halo read and the y write; the GEMM weights (bf16, 288 KB at C = 128) stream from L2.
+//
+// Stages (ultralytics/nn/modules/blocks_transformer.py), activations bf16 in LDS, fp32 accumulation:
+//   0 dw3x3 (pad 1, no bias) on the 9x9 halo -> T[tok][c]; tokens of the bottom/right zero pad = 0  (:160, :31-46)
+//   1 U = LN1(T)                                   (:112)
+//   2 [Q | K] = U Win^T + b_in, V stored transposed (V^T[d][key])   (MHA in_proj, :116)
+//   3 per head: S^T = K Q^T, softmax over keys (fp32, keys >= 49 masked), O^T = V^T P^T     (:116)
+//   4 T += O Wo^T + bo                             (out_proj + residual, :119)
+//   5 U = LN2(T); 6 H = GELU(U W1^T + b1); 7 T += H W2^T + b2        (:122)
+//   8 y = x + SiLU(BN(Wpw T^T)) on the valid (cropped) tokens, NCHW  (window_reverse + crop :125-129, :166-171)
+// MFMA: v_mfma_f32_16x16x32_bf16 (lane l: A[row l&15][k = 8(l>>4)+j], B[k = 8(l>>4)+j][col l&15], D[row 4(l>>4)+r]
+// [col l&15]). GEMM tiles cover token rows 0..63 (four 16-row blocks; rows 49..63 are padding: their A rows read
+// past the 49-row buffers into the next LDS region - finite values - and their outputs are never stored).
+// Attention computes S^T so that its accumulators ARE the P^T operand of O^T = V^T P^T: for a 32-key step the B
+// fragment element j is key 4g + j of the first 16-key block (j < 4) and 16 + 4g + (j - 4) of the second, and the
+// V^T fragment is read in that key order (two 8-byte LDS reads). P is rounded to bf16 like the bf16 model's P.
+#include "common.h"
+#include <math.h>
+
+namespace ys {
+
+constexpr int SB_NR = 49;  // tokens per window
+
+struct SwinBArgs {
+  const bf16_t* x;
+  bf16_t* y;
+  int B, H, W, nWx, nWin;
+  const float* dw;
+  const float* ln1_w;
+  const float* ln1_b;
+  float ln1_eps;
+  const bf16_t* win;
+  const float* bin;
+  const bf16_t* wo;
+  const float* bo;
+  const float* ln2_w;
+  const float* ln2_b;
+  float ln2_eps;
+  const bf16_t* w1;
+  const float* b1;
+  const bf16_t* w2;
+  const float* b2;
+  const bf16_t* wpw;
+  const float* bn_scale;
+  const float* bn_shift;
+  float scale;
+};
+
+// GELU(x) = 0.5 x (1 + erf(x / sqrt 2)) for bf16 outputs: erf by Abramowitz & Stegun 7.1.25 (|error| <= 2.5e-5,
+// 100x below the 2^-8 relative rounding of the bf16 result), with x erf(x/sqrt2) = |x| erf(|x|/sqrt2) so no sign
+// fix-up is needed: GELU = 0.5 (x + |x|) - 0.5 |x| poly(t) exp(-x^2/2), t = 1 / (1 + p |x| / sqrt2)
+__device__ __forceinline__ f32x2 gelu2_bf16_(f32x2 x) {
+  const f32x2 ax = {fabsf(x.x), fabsf(x.y)};
+  const f32x2 den = __builtin_elementwise_fma(ax, f32x2{0.47047f * 0.70710678f, 0.47047f * 0.70710678f},
+                                              f32x2{1.0f, 1.0f});
+  const f32x2 t = {__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+  // 0.5 * (a1 t + a2 t^2 + a3 t^3)
+  f32x2 poly = __builtin_elementwise_fma(t, f32x2{0.5f * 0.7478556f, 0.5f * 0.7478556f},
+                                         f32x2{0.5f * -0.0958798f, 0.5f * -0.0958798f});
+  poly = __builtin_elementwise_fma(t, poly, f32x2{0.5f * 0.3480242f, 0.5f * 0.3480242f});
+  poly = poly * t;
+  const f32x2 m = ax * (ax * -0.72134752044448170f);  // -x^2/2 log2(e)
+  const f32x2 e = {__builtin_amdgcn_exp2f(m.x), __builtin_amdgcn_exp2f(m.y)};
+  const f32x2 q = (ax * poly) * e;
+  return __builtin_elementwise_fma(x + ax, f32x2{0.5f, 0.5f}, -q);
+}
+
+__device__ __forceinline__ f32x4 mfma_b(bf16x8_t a, bf16x8_t b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// weight fragments of W [N][K] (bf16, row-major) for this wave's column blocks cb = wid + 4j:
+// lane (g, l15) holds W[cb*16 + l15][32s + 8g .. +7] for every k-step s
+template <int K, int NJ>
+struct BFrag {
+  bf16x8_t v[NJ][K / 32];
+};
+
+template <int K, int NJ>
+__device__ __forceinline__ void load_bfrag(const bf16_t* __restrict__ Wg, BFrag<K, NJ>& f, int wid, int lane) {
+  const int l15 = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int s = 0; s < K / 32; ++s)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+      f.v[j][s] = *reinterpret_cast<const bf16x8_t*>(Wg + (long)((wid + 4 * j) * 16 + l15) * K + 32 * s + 8 * g);
+}
+
+// acc[rb][j] = A[rows rb*16 .. +15][0..K) . W^T for the wave's column blocks (A: LDS bf16, row stride lda)
+template <int K, int NJ>
+__device__ __forceinline__ void gemm_rows(const bf16_t* As, int lda, const BFrag<K, NJ>& f, f32x4 (&acc)[4][NJ],
+                                          int lane) {
+  const int l15 = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[rb][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < K / 32; ++s) {
+    bf16x8_t a[4];
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb)
+      a[rb] = *reinterpret_cast<const bf16x8_t*>(As + (rb * 16 + l15) * lda + 32 * s + 8 * g);
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[rb][j] = mfma_b(a[rb], f.v[j][s], acc[rb][j]);
+  }
+}
+
+// LayerNorm of rows [0, 49) of S (bf16, stride ST) into U (bf16, stride ST): 4 lanes per row (a DPP quad), each
+// holding C/4 values widened to fp32 from 16-byte reads; two-pass statistics; LN parameters from LDS
+template <int C, int ST>
+__device__ __forceinline__ void row_layernorm_b(const bf16_t* S, bf16_t* U, const float* __restrict__ lnw,
+                                                const float* __restrict__ lnb, float eps, int tid) {
+  constexpr int CP = C / 4;  // elements per lane (16 or 32)
+  const int r = tid >> 2, qd = tid & 3;
+  const bool valid = r < SB_NR;
+  float v[CP];
+#pragma unroll
+  for (int i = 0; i < CP / 8; ++i) {
+    uint4 u = make_uint4(0u, 0u, 0u, 0u);
+    if (valid) u = *reinterpret_cast<const uint4*>(S + r * ST + qd * CP + 8 * i);
+    float f[8];
+    unpack8(u, f);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[8 * i + k] = f[k];
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < CP; ++i) s += v[i];
+  const float mean = quad_sum(s) * (1.0f / (float)C);
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < CP; ++i) {
+    v[i] -= mean;
+    q += v[i] * v[i];
+  }
+  const float rs = __builtin_amdgcn_rsqf(quad_sum(q) * (1.0f / (float)C) + eps);
+  if (!valid) return;
+#pragma unroll
+  for (int i = 0; i < CP / 8; ++i) {
+    float f[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int c = qd * CP + 8 * i + k;
+      f[k] = v[8 * i + k] * rs * lnw[c] + lnb[c];
+    }
+    *reinterpret_cast<uint4*>(U + r * ST + qd * CP + 8 * i) = pack8(f);
+  }
+}
+
+template <int C, int NH>
+__global__ __launch_bounds__(256, 2) void swin_fused_bf16_kernel(SwinBArgs p) {
+  constexpr int HD = C / NH;
+  constexpr int HID = 2 * C;
+  constexpr int ST = C + 8;        // T / U / O row stride (elements)
+  constexpr int SQK = 2 * C + 8;   // [Q | K] row stride; the MLP hidden reuses the region (HID == 2C)
+  constexpr int SVT = 72;          // V^T row stride: keys 0..63 (+8)
+  static_assert(HD == 32 || HD == 64, "head dim");
+  static_assert(C == 64 || C == 128, "channels");
+  constexpr int T_OFF = 0;
+  constexpr int U_OFF = T_OFF + SB_NR * ST;
+  constexpr int QK_OFF = U_OFF + SB_NR * ST;
+  constexpr int VT_OFF = QK_OFF + SB_NR * SQK;
+  constexpr int END = VT_OFF + C * SVT;
+  static_assert(2 * C * 81 <= END - QK_OFF, "fp32 halo patch must fit the QKV region");
+  static_assert(15 * SQK <= C * SVT, "padding-row reads of the QKV region stay inside V^T");
+  // fp32 parameters staged once per workgroup: every epilogue reads LDS, so no global load sits behind a weight
+  // prefetch in the in-order vmcnt queue (a bias load after a prefetch made each stage wait for the next stage's
+  // weights)
+  constexpr int P_BIN = 0, P_BO = 3 * C, P_B1 = 4 * C, P_B2 = 6 * C, P_SC = 7 * C, P_SH = 8 * C, P_L1W = 9 * C,
+                P_L1B = 10 * C, P_L2W = 11 * C, P_L2B = 12 * C, NPAR = 13 * C;
+  __shared__ __attribute__((aligned(16))) bf16_t sm[END];
+  __shared__ __attribute__((aligned(16))) float par[NPAR];
+  bf16_t* T = sm + T_OFF;
+  bf16_t* U = sm + U_OFF;
+  bf16_t* QK = sm + QK_OFF;
+  bf16_t* Vt = sm + VT_OFF;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int l15 = lane & 15, g = lane >> 4;
+  const int H = p.H, W = p.W;
+  const long HW = (long)H * W;
+  // XCD-aware window order: workgroup i runs on XCD i % 8 and takes windows from that XCD's contiguous range, so
+  // horizontally adjacent windows (whose 7-pixel rows share 128-byte lines of x and y) meet in one L2
+  const long nwin_total = (long)p.B * p.nWin;
+  const long per_xcd = (nwin_total + 7) >> 3;
+  const long gw = (long)(blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+  if (gw >= nwin_total || (blockIdx.x >> 3) >= per_xcd) return;
+  const int img = (int)(gw / p.nWin), win = (int)(gw - (long)img * p.nWin);
+  const int wy = win / p.nWx, wx = win - (win / p.nWx) * p.nWx;
+  const bf16_t* xb = p.x + (long)img * C * HW;
+
+  // parameters -> LDS, depthwise taps -> registers, halo -> registers; then the QKV weight prefetch (last in the
+  // vmcnt queue, so the halo wait does not wait for it)
+  for (int e = tid; e < NPAR; e += 256) {
+    const int w = e / C, c = e - w * C;
+    const float* src = w < 3 ? p.bin + w * C : w == 3 ? p.bo : w < 6 ? p.b1 + (w - 4) * C : w == 6 ? p.b2
+                     : w == 7 ? p.bn_scale : w == 8 ? p.bn_shift : w == 9 ? p.ln1_w : w == 10 ? p.ln1_b
+                     : w == 11 ? p.ln2_w : p.ln2_b;
+    par[e] = src[c];
+  }
+  const int dc = tid % C;
+  float k[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) k[i] = p.dw[dc * 9 + i];
+  // halo [C][9][9]: row slot s = 7*wid + lane/9 < 27 covers (channel 3i + s/9, patch row s%9) at step i, lane%9 the
+  // column, so a lane's byte offset is fixed across the C/3 steps (the step advances the scalar offset by 3 planes)
+  // and out-of-image lanes get an out-of-range offset that the buffer load returns as 0: no per-load VALU
+  constexpr int NHS = (C + 2) / 3;
+  float hv[NHS];
+  const int hl_r = lane / 9, hl_px = lane - (lane / 9) * 9;
+  const int hslot = 7 * wid + hl_r;  // valid < 27 (lane 63 and slot 27 idle)
+  const int hcs = hslot / 9, hpy = hslot - (hslot / 9) * 9;
+  {
+    const unsigned long long xa = (unsigned long long)xb;
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(xa >> 32)) << 32) |
+                (unsigned)__builtin_amdgcn_readfirstlane((unsigned)xa)),
+        (short)0, __builtin_amdgcn_readfirstlane((int)(C * HW * 2)), 0x00020000);
+    const int hh = wy * 7 - 1 + hpy, wc = wx * 7 - 1 + hl_px;
+    const bool ok = hl_r < 7 && hslot < 27 && (unsigned)hh < (unsigned)H && (unsigned)wc < (unsigned)W;
+    const unsigned voff = ok ? (unsigned)((hcs * HW + (long)hh * W + wc) * 2) : 0x80000000u;
+#pragma unroll
+    for (int i = 0; i < NHS; ++i) {
+      const unsigned v = (3 * i + hcs < C) ? voff : 0x80000000u;
+      hv[i] = bf2f(__builtin_amdgcn_raw_buffer_load_b16(rx, v, (int)(i * 3 * HW * 2), 0));
+    }
+  }
+  constexpr int NJ_QKV = 3 * C / 64;
+  BFrag<C, NJ_QKV> f_qkv;
+  load_bfrag(p.win, f_qkv, wid, lane);
+
+  // ---- stage 0: halo -> LDS (fp32: conflict-free stride-81 reads below), depthwise conv -> T ----
+  float* halo = reinterpret_cast<float*>(sm + QK_OFF);
+  if (hl_r < 7 && hslot < 27) {
+#pragma unroll
+    for (int i = 0; i < NHS; ++i)
+      if (3 * i + hcs < C) halo[(3 * i + hcs) * 81 + hpy * 9 + hl_px] = hv[i];
+  }
+  __syncthreads();
+  {
+    const int c = dc;
+    for (int iy = tid / C; iy < 7; iy += 256 / C) {
+      const float* hp = halo + c * 81 + iy * 9;
+      float r[3][9];
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < 9; ++kx) r[ky][kx] = hp[ky * 9 + kx];
+      const bool rowok = wy * 7 + iy < H;
+#pragma unroll
+      for (int ix = 0; ix < 7; ++ix) {
+        float v = 0.f;
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+          for (int kx = 0; kx < 3; ++kx) v = fmaf(k[ky * 3 + kx], r[ky][ix + kx], v);
+        T[(iy * 7 + ix) * ST + c] = (rowok && wx * 7 + ix < W) ? f2bf(v) : (bf16_t)0;
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- stage 1: U = LN1(T) ----
+  row_layernorm_b<C, ST>(T, U, par + P_L1W, par + P_L1B, p.ln1_eps, tid);
+  __syncthreads();
+
+  // ---- stage 2: [Q | K] = U Win^T + b (rows < 49), V^T[d][key] (keys >= 49 zero) ----
+  constexpr int NJ_O = C / 64;
+  BFrag<C, NJ_O> f_o;  // out-proj weights: in flight during the QKV epilogue and attention
+  {
+    f32x4 acc[4][NJ_QKV];
+    gemm_rows<C, NJ_QKV>(U, ST, f_qkv, acc, lane);
+    load_bfrag(p.wo, f_o, wid, lane);
+#pragma unroll
+    for (int j = 0; j < NJ_QKV; ++j) {
+      const int n = (wid + 4 * j) * 16 + l15;
+      const float bias = par[P_BIN + n];
+      if (n < 2 * C) {
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = rb * 16 + 4 * g + r;
+            if (row < SB_NR) QK[row * SQK + n] = f2bf(acc[rb][j][r] + bias);
+          }
+      } else {
+        const int d = n - 2 * C;
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) {
+          const int row0 = rb * 16 + 4 * g;
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = (row0 + r < SB_NR) ? acc[rb][j][r] + bias : 0.f;
+          *reinterpret_cast<uint2*>(Vt + d * SVT + row0) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- stage 3: attention; wave = 16 queries (rows wid*16 + l15), all heads; O -> U region ----
+  {
+    const int q0 = wid * 16;
+    const int qr = (q0 + l15 < SB_NR) ? q0 + l15 : SB_NR - 1;  // padding queries read a real row (dropped)
+    const float c2 = p.scale * 1.44269504088896341f;
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+      // S^T[key][q] = sum_d K[key][d] Q[q][d]; key blocks of 16
+      bf16x8_t qf[HD / 32];
+#pragma unroll
+      for (int s = 0; s < HD / 32; ++s)
+        qf[s] = *reinterpret_cast<const bf16x8_t*>(QK + qr * SQK + h * HD + 32 * s + 8 * g);
+      f32x4 st[4];
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) {
+        st[kb] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int key = (kb * 16 + l15 < SB_NR) ? kb * 16 + l15 : SB_NR - 1;
+#pragma unroll
+        for (int s = 0; s < HD / 32; ++s)
+          st[kb] = mfma_b(*reinterpret_cast<const bf16x8_t*>(QK + key * SQK + C + h * HD + 32 * s + 8 * g), qf[s],
+                          st[kb]);
+      }
+      // lane holds S^T[key = kb*16 + 4g + r][q = l15]: softmax over keys (in lane, then over the 4 lane groups)
+      float mx = -INFINITY;
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          if (kb * 16 + 4 * g + r >= SB_NR) st[kb][r] = -INFINITY;
+          mx = fmaxf(mx, st[kb][r]);
+        }
+      mx = xor32_max(xor16_max(mx));
+      const float mc = -mx * c2;
+      float sum = 0.f;
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float e = __builtin_amdgcn_exp2f(fmaf(st[kb][r], c2, mc));
+          st[kb][r] = e;
+          sum += e;
+        }
+      const float inv = __builtin_amdgcn_rcpf(xor32_sum(xor16_sum(sum)));
+      // P^T fragments: k-step s (keys 32s..32s+31): element j = key 32s + 4g + j (j < 4), 32s + 16 + 4g + j - 4
+      bf16x8_t pf[2];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const uint32_t w0 = pack_bf16x2(st[2 * s][0] * inv, st[2 * s][1] * inv);
+        const uint32_t w1 = pack_bf16x2(st[2 * s][2] * inv, st[2 * s][3] * inv);
+        const uint32_t w2 = pack_bf16x2(st[2 * s + 1][0] * inv, st[2 * s + 1][1] * inv);
+        const uint32_t w3 = pack_bf16x2(st[2 * s + 1][2] * inv, st[2 * s + 1][3] * inv);
+        pf[s] = __builtin_bit_cast(bf16x8_t, make_uint4(w0, w1, w2, w3));
+      }
+      // O^T[d][q] = sum_key V^T[d][key] P^T[key][q]
+#pragma unroll
+      for (int db = 0; db < HD / 16; ++db) {
+        f32x4 o = {0.f, 0.f, 0.f, 0.f};
+        const bf16_t* vr = Vt + (h * HD + db * 16 + l15) * SVT + 4 * g;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const uint2 lo = *reinterpret_cast<const uint2*>(vr + 32 * s);
+          const uint2 hi = *reinterpret_cast<const uint2*>(vr + 32 * s + 16);
+          o = mfma_b(__builtin_bit_cast(bf16x8_t, make_uint4(lo.x, lo.y, hi.x, hi.y)), pf[s], o);
+        }
+        // lane holds O^T[d = db*16 + 4g + r][q = l15] -> O[q][h*HD + d .. +3]
+        if (q0 + l15 < SB_NR)
+          *reinterpret_cast<uint2*>(U + (q0 + l15) * ST + h * HD + db * 16 + 4 * g) =
+              make_uint2(pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]));
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- stage 4: T += O Wo^T + bo ----
+  constexpr int NJ_1 = HID / 64;
+  BFrag<C, NJ_1> f_1;  // MLP1 weights: in flight during out-proj and LN2
+  load_bfrag(p.w1, f_1, wid, lane);
+  {
+    f32x4 acc[4][NJ_O];
+    gemm_rows<C, NJ_O>(U, ST, f_o, acc, lane);
+#pragma unroll
+    for (int j = 0; j < NJ_O; ++j) {
+      const int n = (wid + 4 * j) * 16 + l15;
+      const float bias = par[P_BO + n];
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = rb * 16 + 4 * g + r;
+          if (row < SB_NR) T[row * ST + n] = f2bf(bf2f(T[row * ST + n]) + (acc[rb][j][r] + bias));
+        }
+    }
+  }
+  __syncthreads();
+
+  // ---- stage 5: U = LN2(T) ----
+  row_layernorm_b<C, ST>(T, U, par + P_L2W, par + P_L2B, p.ln2_eps, tid);
+  __syncthreads();
+
+  // ---- stage 6: H = GELU(U W1^T + b1) -> QK region ----
+  bf16_t* Hd = QK;
+  constexpr int NJ_2 = C / 64;
+  BFrag<HID, NJ_2> f_2;  // MLP2 weights
+  load_bfrag(p.w2, f_2, wid, lane);
+  {
+    f32x4 acc[4][NJ_1];
+    gemm_rows<C, NJ_1>(U, ST, f_1, acc, lane);
+#pragma unroll
+    for (int j = 0; j < NJ_1; ++j) {
+      const int n = (wid + 4 * j) * 16 + l15;
+      const float bias = par[P_B1 + n];
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+        for (int r = 0; r < 4; r += 2) {
+          const int row = rb * 16 + 4 * g + r;
+          const f32x2 hv = gelu2_bf16_(f32x2{acc[rb][j][r], acc[rb][j][r + 1]} + bias);
+          if (row < SB_NR) Hd[row * SQK + n] = f2bf(hv.x);
+          if (row + 1 < SB_NR) Hd[(row + 1) * SQK + n] = f2bf(hv.y);
+        }
+    }
+  }
+  __syncthreads();
+
+  // ---- stage 7: T += H W2^T + b2; the pw weights and this lane's residual pixels are loaded first (in flight
+  // during MLP2) ----
+  constexpr int NCB_PW = C / 64;  // output-channel blocks per wave
+  bf16x8_t wa[NCB_PW][C / 32];
+#pragma unroll
+  for (int j = 0; j < NCB_PW; ++j)
+#pragma unroll
+    for (int s = 0; s < C / 32; ++s)
+      wa[j][s] = *reinterpret_cast<const bf16x8_t*>(p.wpw + (long)((wid + 4 * j) * 16 + l15) * C + 32 * s + 8 * g);
+  long pix[4];  // per token block: pixel offset of token tb*16 + l15 in the image plane, or -1
+#pragma unroll
+  for (int tb = 0; tb < 4; ++tb) {
+    const int tok = tb * 16 + l15;
+    const int iy = tok / 7, ix = tok - (tok / 7) * 7;
+    const int hh = wy * 7 + iy, ww = wx * 7 + ix;
+    pix[tb] = (tok < SB_NR && hh < H && ww < W) ? (long)hh * W + ww : -1;
+  }
+  bf16_t xres[NCB_PW][4][4];
+#pragma unroll
+  for (int j = 0; j < NCB_PW; ++j)
+#pragma unroll
+    for (int tb = 0; tb < 4; ++tb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        xres[j][tb][r] = pix[tb] >= 0 ? xb[(long)((wid + 4 * j) * 16 + 4 * g + r) * HW + pix[tb]] : (bf16_t)0;
+  {
+    f32x4 acc[4][NJ_2];
+    gemm_rows<HID, NJ_2>(Hd, SQK, f_2, acc, lane);
+#pragma unroll
+    for (int j = 0; j < NJ_2; ++j) {
+      const int n = (wid + 4 * j) * 16 + l15;
+      const float bias = par[P_B2 + n];
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = rb * 16 + 4 * g + r;
+          if (row < SB_NR) T[row * ST + n] = f2bf(bf2f(T[row * ST + n]) + (acc[rb][j][r] + bias));
+        }
+    }
+  }
+  __syncthreads();
+
+  // ---- stage 8: Y^T[c][tok] = Wpw . T^T; y = x + SiLU(BN(Y)) at the window's valid pixels ----
+  {
+    bf16_t* yb = p.y + (long)img * C * HW;
+#pragma unroll
+    for (int j = 0; j < NCB_PW; ++j) {
+      const int cb = wid + 4 * j;
+      f32x4 acc[4];
+#pragma unroll
+      for (int tb = 0; tb < 4; ++tb) acc[tb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < C / 32; ++s)
+#pragma unroll
+        for (int tb = 0; tb < 4; ++tb)
+          acc[tb] = mfma_b(wa[j][s], *reinterpret_cast<const bf16x8_t*>(T + (tb * 16 + l15) * ST + 32 * s + 8 * g),
+                           acc[tb]);
+      // lane holds Y^T[c = cb*16 + 4g + r][tok = tb*16 + l15]
+#pragma unroll
+      for (int tb = 0; tb < 4; ++tb) {
+        if (pix[tb] < 0) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = cb * 16 + 4 * g + r;
+          yb[(long)c * HW + pix[tb]] =
+              f2bf(bf2f(xres[j][tb][r]) + silu_fast_(acc[tb][r] * par[P_SC + c] + par[P_SH + c]));
+        }
+      }
+    }
+  }
+}
+
+}  // namespace ys
+
+using namespace ys;
+
+// shapes the fused bf16 kernel takes: 7x7 windows, C 64 (2 heads) / 128 (2 or 4 heads), MLP hidden 2C
+bool yolosod_swin_fused_bf16_ok(int C, int num_heads, int wh, int ww, int mlp_hidden) {
+  static const bool on = [] { const char* e = getenv("YOLOSOD_SWIN_FUSED_BF16"); return !e || atoi(e) != 0; }();
+  return on && wh == 7 && ww == 7 && mlp_hidden == 2 * C &&
+         ((C == 128 && (num_heads == 2 || num_heads == 4)) || (C == 64 && num_heads == 2));
+}
+
+// returns 1 if launched, 0 if the shape is not handled (decomposed path), < 0 on error
+int yolosod_swin_fused_bf16_launch(const bf16_t* x, bf16_t* y, int B, int C, int H, int W, int num_heads, int wh,
+                                   int ww, int nWx, int nWin, const float* dw_w, const float* ln1_w, const float* ln1_b,
+                                   float ln1_eps, const bf16_t* in_proj_w, const float* in_proj_b,
+                                   const bf16_t* out_proj_w, const float* out_proj_b, const float* ln2_w,
+                                   const float* ln2_b, float ln2_eps, const bf16_t* mlp1_w, const float* mlp1_b,
+                                   int mlp_hidden, const bf16_t* mlp2_w, const float* mlp2_b, const bf16_t* pw_w,
+                                   const float* bn_scale, const float* bn_shift, hipStream_t st) {
+  if (!yolosod_swin_fused_bf16_ok(C, num_heads, wh, ww, mlp_hidden) || (long)B * nWin >= (1L << 31)) return 0;
+  SwinBArgs a{x, y, B, H, W, nWx, nWin, dw_w, ln1_w, ln1_b, ln1_eps, in_proj_w, in_proj_b, out_proj_w, out_proj_b,
+              ln2_w, ln2_b, ln2_eps, mlp1_w, mlp1_b, mlp2_w, mlp2_b, pw_w, bn_scale, bn_shift,
+              1.0f / sqrtf((float)(C / num_heads))};
+  const long nwin = (long)B * nWin;
+  const dim3 grid((unsigned)(8 * ((nwin + 7) / 8)));
+  if (C == 128 && num_heads == 2) hipLaunchKernelGGL((swin_fused_bf16_kernel<128, 2>), grid, dim3(256), 0, st, a);
+  else if (C == 128 && num_heads == 4) hipLaunchKernelGGL((swin_fused_bf16_kernel<128, 4>), grid, dim3(256), 0, st, a);
+  else if (C == 64 && num_heads == 2) hipLaunchKernelGGL((swin_fused_bf16_kernel<64, 2>), grid, dim3(256), 0, st, a);
+  else return 0;
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("swin_fused_bf16: launch failed: %s", hipGetErrorString(e));
+    return -1;
+  }
+  return 1;
+}

@@ -210,40 +210,66 @@ static int launch_attention_bf16(const bf16_t* qkv, bf16_t* out, long n_seq, int
 
 // =================================================================================================
 // Swin: depthwise 3x3 (pad 1, no bias) + bottom/right zero pad -> T[(img*Hp + h)*Wp + w][C] (padded raster order).
-// grid = (B*Hp, ceil(C/CS)): one padded row of one image and a CS-channel slab; the three input rows of the slab
-// are staged in LDS (bf16, zero border), the output row is written with lanes along c (coalesced rows of T).
+// grid = (B*Hp, ceil(C/64)): one padded row of one image and a 64-channel slab. Lane (c = tid/4, q = tid%4) computes
+// runs of 8 pixels (q, q+4, ...) of channel c from three 16-byte row loads (+ the two neighbour pixels), so the input
+// rows are read along w; the 8 results go to an LDS tile [w][64] and leave as 16-byte stores of 8 channels, so the
+// token rows are written along c. Zero tokens for h >= H and w >= W (the reference pads after the conv).
 // =================================================================================================
 __global__ __launch_bounds__(256) void swin_tokens_bf16_kernel(const bf16_t* __restrict__ x,
                                                                const float* __restrict__ dw, bf16_t* __restrict__ T,
-                                                               int C, int H, int W, int Hp, int Wp, int CS) {
-  extern __shared__ bf16_t rows[];  // [CS][3][W + 2]
+                                                               int C, int H, int W, int Hp, int Wp) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t tile[];  // [Wp][72]
+  constexpr int TS = 72;
   const int img = blockIdx.x / Hp, h = blockIdx.x - (blockIdx.x / Hp) * Hp;
-  const int c0 = blockIdx.y * CS;
-  const int nc = (C - c0 < CS) ? C - c0 : CS;
-  const int RW = W + 2;
+  const int c0 = blockIdx.y * 64;
+  const int tid = threadIdx.x;
   bf16_t* Tr = T + ((long)img * Hp + h) * Wp * C + c0;
-  if (h >= H) {  // padding rows: zero tokens
-    for (int e = threadIdx.x; e < Wp * nc; e += 256) Tr[(long)(e / nc) * C + e % nc] = 0;
-    return;
-  }
-  const bf16_t* xb = x + ((long)img * C + c0) * H * W;
-  for (int e = threadIdx.x; e < nc * 3 * RW; e += 256) {
-    const int c = e / (3 * RW), r = (e / RW) % 3, px = e % RW;
-    const int hh = h - 1 + r, ww = px - 1;
-    rows[e] = (hh >= 0 && hh < H && ww >= 0 && ww < W) ? xb[((long)c * H + hh) * W + ww] : (bf16_t)0;
+  if (h < H) {
+    const int c = tid >> 2, q = tid & 3;
+    const bool cok = c0 + c < C;
+    const bf16_t* xc = x + ((long)img * C + c0 + (cok ? c : 0)) * H * W;
+    float k[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) k[i] = cok ? dw[(long)(c0 + c) * 9 + i] : 0.f;
+    const int nruns = (W + 7) >> 3;
+    for (int run = q; run < nruns; run += 4) {
+      const int w0 = run * 8;
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = 0.f;
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        const int hh = h - 1 + r;
+        if (hh < 0 || hh >= H || !cok) continue;
+        const bf16_t* xr = xc + (long)hh * W;
+        float v[10];
+        v[0] = w0 > 0 ? bf2f(xr[w0 - 1]) : 0.f;
+        if (w0 + 8 <= W && (W & 7) == 0) {
+          float f[8];
+          unpack8(*reinterpret_cast<const uint4*>(xr + w0), f);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[1 + j] = f[j];
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[1 + j] = (w0 + j < W) ? bf2f(xr[w0 + j]) : 0.f;
+        }
+        v[9] = (w0 + 8 < W) ? bf2f(xr[w0 + 8]) : 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] += k[3 * r] * v[j] + k[3 * r + 1] * v[j + 1] + k[3 * r + 2] * v[j + 2];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (w0 + j < Wp) tile[(w0 + j) * TS + c] = (w0 + j < W) ? f2bf(o[j]) : (bf16_t)0;
+    }
+    if (tid < 64)
+      for (int w = ((W + 7) >> 3) * 8; w < Wp; ++w) tile[w * TS + tid] = 0;  // padding columns past the last run
   }
   __syncthreads();
-  for (int e = threadIdx.x; e < Wp * nc; e += 256) {
-    const int w = e / nc, c = e - (e / nc) * nc;
-    float v = 0.f;
-    if (w < W) {
-      const bf16_t* pc = rows + c * 3 * RW + w;
-      const float* k = dw + (long)(c0 + c) * 9;
-      v = k[0] * bf2f(pc[0]) + k[1] * bf2f(pc[1]) + k[2] * bf2f(pc[2]) + k[3] * bf2f(pc[RW]) +
-          k[4] * bf2f(pc[RW + 1]) + k[5] * bf2f(pc[RW + 2]) + k[6] * bf2f(pc[2 * RW]) + k[7] * bf2f(pc[2 * RW + 1]) +
-          k[8] * bf2f(pc[2 * RW + 2]);
-    }
-    Tr[(long)w * C + c] = f2bf(v);
+  const int nc8 = ((C - c0 < 64) ? C - c0 : 64) >> 3;
+  for (int e = tid; e < Wp * nc8; e += 256) {
+    const int w = e / nc8, cc = e - (e / nc8) * nc8;
+    const uint4 v = (h < H) ? *reinterpret_cast<const uint4*>(&tile[w * TS + 8 * cc]) : make_uint4(0u, 0u, 0u, 0u);
+    *reinterpret_cast<uint4*>(Tr + (long)w * C + 8 * cc) = v;
   }
 }
 
@@ -330,6 +356,15 @@ static SwinGeomB swin_geom_b(int B, int H, int W, int ws) {
 
 using namespace ys;
 
+bool yolosod_swin_fused_bf16_ok(int C, int num_heads, int wh, int ww, int mlp_hidden);
+int yolosod_swin_fused_bf16_launch(const bf16_t* x, bf16_t* y, int B, int C, int H, int W, int num_heads, int wh,
+                                   int ww, int nWx, int nWin, const float* dw_w, const float* ln1_w, const float* ln1_b,
+                                   float ln1_eps, const bf16_t* in_proj_w, const float* in_proj_b,
+                                   const bf16_t* out_proj_w, const float* out_proj_b, const float* ln2_w,
+                                   const float* ln2_b, float ln2_eps, const bf16_t* mlp1_w, const float* mlp1_b,
+                                   int mlp_hidden, const bf16_t* mlp2_w, const float* mlp2_b, const bf16_t* pw_w,
+                                   const float* bn_scale, const float* bn_shift, hipStream_t st);
+
 // =================================================================================================
 // C ABI (bf16 storage: activations / GEMM weights are bf16 bit patterns, other parameters fp32)
 // =================================================================================================
@@ -357,8 +392,12 @@ YS_EXPORT int yolosod_attention_bf16(const bf16_t* qkv, bf16_t* out, long n_seq,
 }
 
 YS_EXPORT size_t yolosod_swin_workspace_bf16(int B, int C, int H, int W, int num_heads, int window, int mlp_hidden) {
-  (void)num_heads;
   SwinGeomB g = swin_geom_b(B, H, W, window);
+  if (yolosod_swin_fused_bf16_ok(C, num_heads, g.wh, g.ww, mlp_hidden)) {  // fused per-window kernel: folded BN only
+    Sizer s;
+    s.take<float>((size_t)C * 2);
+    return s.off;
+  }
   const int wide = (3 * C > mlp_hidden) ? 3 * C : mlp_hidden;
   Sizer s;
   s.take<bf16_t>((size_t)g.ntok * C);     // T (residual stream)
@@ -390,6 +429,19 @@ YS_EXPORT int yolosod_swin_forward_bf16(const bf16_t* x, bf16_t* y, int B, int C
   SwinGeomB g = swin_geom_b(B, H, W, window);
   YS_CHECK_ARG(g.L <= 320, "swin_bf16: window of %d tokens unsupported", g.L);
   YS_CHECK_ARG(g.ntok < (1L << 31), "swin_bf16: too many tokens");
+  if (yolosod_swin_fused_bf16_ok(C, num_heads, g.wh, g.ww, mlp_hidden)) {
+    Carver cf(workspace, workspace_bytes);
+    float* fold = cf.take<float>((size_t)C * 2);
+    YS_CHECK_ARG(fold, "swin_bf16: workspace too small (%zu)", workspace_bytes);
+    hipLaunchKernelGGL(fold_bn_bf16_kernel, dim3((C + 255) / 256), dim3(256), 0, st, bn_w, bn_b, bn_mean, bn_var,
+                       bn_eps, C, fold, fold + C);
+    const int r = yolosod_swin_fused_bf16_launch(x, y, B, C, H, W, num_heads, g.wh, g.ww, g.nWx, g.nWin, dw_w, ln1_w,
+                                                 ln1_b, ln1_eps, in_proj_w, in_proj_b, out_proj_w, out_proj_b, ln2_w,
+                                                 ln2_b, ln2_eps, mlp1_w, mlp1_b, mlp_hidden, mlp2_w, mlp2_b, pw_w, fold,
+                                                 fold + C, st);
+    if (r < 0) return -1;
+    if (r == 1) return 0;
+  }
   Carver cv(workspace, workspace_bytes);
   bf16_t* T = cv.take<bf16_t>((size_t)g.ntok * C);
   bf16_t* U = cv.take<bf16_t>((size_t)g.ntok * C);
@@ -400,11 +452,10 @@ YS_EXPORT int yolosod_swin_forward_bf16(const bf16_t* x, bf16_t* y, int B, int C
   YS_CHECK_ARG(lns, "swin_bf16: workspace too small (%zu)", workspace_bytes);
   int rc;
   // dwconv + pad -> T (raster tokens)
-  int CS = 64;
-  while (CS > 8 && (size_t)CS * 3 * (W + 2) * sizeof(bf16_t) > 64 * 1024) CS >>= 1;
-  YS_CHECK_ARG((size_t)CS * 3 * (W + 2) * sizeof(bf16_t) <= 64 * 1024, "swin_bf16: W=%d too wide", W);
-  hipLaunchKernelGGL(swin_tokens_bf16_kernel, dim3((unsigned)(B * g.Hp), (unsigned)((C + CS - 1) / CS)), dim3(256),
-                     (size_t)CS * 3 * (W + 2) * sizeof(bf16_t), st, x, dw_w, T, C, H, W, g.Hp, g.Wp, CS);
+  const size_t tok_lds = (size_t)g.Wp * 72 * sizeof(bf16_t);
+  YS_CHECK_ARG(tok_lds <= 64 * 1024, "swin_bf16: W=%d too wide for the token kernel", W);
+  hipLaunchKernelGGL(swin_tokens_bf16_kernel, dim3((unsigned)(B * g.Hp), (unsigned)((C + 63) / 64)), dim3(256),
+                     tok_lds, st, x, dw_w, T, C, H, W, g.Hp, g.Wp);
   YS_CHECK_LAUNCH("swin_tokens_bf16");
   // QKV = LN1(T) Win^T + b_in
   if ((rc = launch_row_stats_bf16(T, C, g.ntok, C, ln1_eps, lns, st))) return rc;
