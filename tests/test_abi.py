@@ -63,3 +63,25 @@ def test_product_ops_refuse_cpu_tensors():
     from yolosod_amd.utils.ops import non_max_suppression
     with pytest.raises(RuntimeError, match="GPU"):
         non_max_suppression(torch.rand(1, 14, 100))
+
+
+OPS = ("se_fwd", "cbam_fwd", "ca_fwd", "a2_fwd", "swin_fwd", "detect_head_fwd", "detect_decode_fwd", "nms_batched")
+
+
+def test_torch_op_library_registers_the_kernel_families():
+    """one torch op per kernel family (csrc/torch_ops.cpp, a cpp_extension over the C ABI); Meta
+    kernels give output shapes without a GPU, and a CPU tensor reaches no kernel (no CPU implementation)."""
+    ops = _hip.ops()
+    for n in OPS:
+        assert hasattr(ops, n), n
+    m = torch.empty(2, 64, 20, 20, device="meta")
+    assert ops.se_fwd(m, m, m, m, m, None).shape == m.shape
+    assert ops.swin_fwd(m, 2, 7, *([m] * 3), 1e-5, *([m] * 6), 1e-5, *([m] * 9), 1e-3).shape == m.shape
+    feats = [torch.empty(3, 64, s, s, device="meta") for s in (16, 8, 4, 2)]
+    y = ops.detect_head_fwd(feats, feats, feats, feats, feats, feats, [4.0, 8.0, 16.0, 32.0], 10, 16)
+    assert tuple(y.shape) == (3, 14, 16 * 16 + 8 * 8 + 4 * 4 + 2 * 2)
+    out, counts, index = ops.nms_batched(torch.empty(3, 14, 100, device="meta"), 0.25, 0.7, None, False, False, 300,
+                                         30000, 7680.0)
+    assert tuple(out.shape) == (3, 300, 6) and tuple(counts.shape) == (3,) and tuple(index.shape) == (3, 300)
+    with pytest.raises((RuntimeError, NotImplementedError)):
+        ops.se_fwd(torch.zeros(1, 8, 4, 4), *[torch.zeros(1)] * 4, None)

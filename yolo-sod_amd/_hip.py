@@ -107,6 +107,26 @@ def load_library() -> ctypes.CDLL:
     return _LIB
 
 
+OPS_LIB_PATH = LIB_PATH.parent / "yolosod_torch_ops.so"
+_OPS = None
+
+
+def ops():
+    """torch.ops.yolosod (csrc/torch_ops.cpp over the C ABI): the op-registered form every hot-path wrapper below
+    dispatches through (TORCH_CHECK errors, outputs and workspaces from the caching allocator on the current
+    stream, Meta kernels for shape propagation). Raises if the extension has not been built - no fallback."""
+    global _OPS
+    if _OPS is None:
+        load_library()  # the ops library links it (RUNPATH $ORIGIN); loaded first so both share one handle
+        if not OPS_LIB_PATH.exists():
+            raise RuntimeError(f"yolosod_amd: torch-op library {OPS_LIB_PATH} is missing - run "
+                               "__graft_entry__.build() (or python yolo-sod_amd/build.py). There is no CPU fallback.")
+        if not hasattr(torch.ops.yolosod, "se_fwd"):
+            torch.ops.load_library(str(OPS_LIB_PATH))
+        _OPS = torch.ops.yolosod
+    return _OPS
+
+
 class _OpTimer:
     """Records HIP events around every C-ABI launch sequence (on the launch stream) while active."""
 
@@ -240,130 +260,63 @@ def _pre_stats(x, need_max):
     return st
 
 
+def _t(t, name):
+    """A GPU tensor argument (device / dtype / shape checks are the op's TORCH_CHECKs)."""
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name}: expected a tensor")
+    if t.device.type != "cuda":
+        raise RuntimeError(f"{name}: HIP kernel requires a GPU tensor (got device {t.device}); no CPU fallback")
+    return t
+
+
 def se_forward(x, fc1_w, fc1_b, fc2_w, fc2_b):
-    """SE on fp32 or bf16 activations (parameters fp32)."""
-    lib = load_library()
-    bf = _act_dtype(x)
-    B, C, H, W = x.shape
+    """SE on fp32 or bf16 activations (parameters fp32) -> torch.ops.yolosod.se_fwd."""
+    bf = _act_dtype(_t(x, "x"))
     hid = fc1_w.shape[0]
-    y = torch.empty_like(x)
-    ws = _workspace(lib.yolosod_se_workspace(B, C, H, W), x.device)
-    pre = _pre_stats(x, False)
-    args = (_dev(x, "x", x.dtype), _dev(y, "y", x.dtype), B, C, H, W, _p(fc1_w, "fc1.weight", hid * C),
-            _p(fc1_b, "fc1.bias", hid), _p(fc2_w, "fc2.weight", C * hid), _p(fc2_b, "fc2.bias", C), hid)
-    key = ("se", tuple(x.shape), hid) + ((2,) if bf else ())
-    if bf:
-        _check(_launch(key, x.device, lib.yolosod_se_forward_bf16, *args, None if pre is None else pre.psum.data_ptr(),
-                       ws.data_ptr(), ws.numel(), _stream(x.device)), "se_forward_bf16")
-    elif pre is not None:  # plane sums came with x from its producer's epilogue: gate + scale only
-        _check(_launch(key, x.device, lib.yolosod_se_forward_pre, *args, pre.psum.data_ptr(),
-                       ws.data_ptr(), ws.numel(), _stream(x.device)), "se_forward_pre")
-    else:
-        _check(_launch(key, x.device, lib.yolosod_se_forward, *args, ws.data_ptr(), ws.numel(),
-                       _stream(x.device)), "se_forward")
-    return y
+    pre = _pre_stats(x, False)  # plane sums that came with x from its producer's epilogue
+    return _launch(("se", tuple(x.shape), hid) + ((2,) if bf else ()), x.device, ops().se_fwd, x, fc1_w, fc1_b,
+                   fc2_w, fc2_b, None if pre is None else pre.psum)
 
 
 def cbam_forward(x, fc0_w, fc2_w, sa_w):
-    """CBAM on fp32 or bf16 activations (parameters fp32)."""
-    lib = load_library()
-    bf = _act_dtype(x)
-    B, C, H, W = x.shape
+    """CBAM on fp32 or bf16 activations (parameters fp32) -> torch.ops.yolosod.cbam_fwd."""
+    bf = _act_dtype(_t(x, "x"))
     hid = fc0_w.shape[0]
-    y = torch.empty_like(x)
-    ws = _workspace(lib.yolosod_cbam_workspace(B, C, H, W), x.device)
     pre = _pre_stats(x, True)
-    args = (_dev(x, "x", x.dtype), _dev(y, "y", x.dtype), B, C, H, W, _p(fc0_w, "fc.0.weight", hid * C),
-            _p(fc2_w, "fc.2.weight", C * hid), hid, _p(sa_w, "conv1.weight", 98))
-    key = ("cbam", tuple(x.shape), hid) + ((2,) if bf else ())
-    if bf:
-        _check(_launch(key, x.device, lib.yolosod_cbam_forward_bf16, *args,
-                       None if pre is None else pre.psum.data_ptr(), None if pre is None else pre.pmax.data_ptr(),
-                       ws.data_ptr(), ws.numel(), _stream(x.device)), "cbam_forward_bf16")
-    elif pre is not None:
-        _check(_launch(key, x.device, lib.yolosod_cbam_forward_pre, *args, pre.psum.data_ptr(),
-                       pre.pmax.data_ptr(), ws.data_ptr(), ws.numel(), _stream(x.device)), "cbam_forward_pre")
-    else:
-        _check(_launch(key, x.device, lib.yolosod_cbam_forward, *args, ws.data_ptr(), ws.numel(),
-                       _stream(x.device)), "cbam_forward")
-    return y
+    return _launch(("cbam", tuple(x.shape), hid) + ((2,) if bf else ()), x.device, ops().cbam_fwd, x, fc0_w, fc2_w,
+                   sa_w, None if pre is None else pre.psum, None if pre is None else pre.pmax)
 
 
 def ca_forward(x, conv1_w, conv1_b, bn_w, bn_b, bn_mean, bn_var, bn_eps, convh_w, convh_b, convw_w, convw_b):
-    """CA on fp32 or bf16 activations (parameters fp32)."""
-    lib = load_library()
-    bf = _act_dtype(x)
-    B, C, H, W = x.shape
+    """CA on fp32 or bf16 activations (parameters fp32) -> torch.ops.yolosod.ca_fwd."""
+    bf = _act_dtype(_t(x, "x"))
     mip = conv1_w.shape[0]
-    y = torch.empty_like(x)
-    ws = _workspace(lib.yolosod_ca_workspace(B, C, H, W), x.device)
-    args = (_dev(x, "x", x.dtype), _dev(y, "y", x.dtype), B, C, H, W, _p(conv1_w, "conv1.weight", mip * C),
-            _p(conv1_b, "conv1.bias", mip), mip, _p(bn_w, "bn1.weight", mip), _p(bn_b, "bn1.bias", mip),
-            _p(bn_mean, "bn1.running_mean", mip), _p(bn_var, "bn1.running_var", mip), float(bn_eps),
-            _p(convh_w, "conv_h.weight", C * mip), _p(convh_b, "conv_h.bias", C),
-            _p(convw_w, "conv_w.weight", C * mip), _p(convw_b, "conv_w.bias", C))
-    pre = getattr(x, "_ys_ca_pool", None)
-    if pre is not None and pre[1] != tuple(x.shape):
-        pre = None
-    key = ("ca", tuple(x.shape), mip) + ((2,) if bf else ())
-    if bf:
-        _check(_launch(key, x.device, lib.yolosod_ca_forward_bf16, *args, None if pre is None else pre[0].data_ptr(),
-                       ws.data_ptr(), ws.numel(), _stream(x.device)), "ca_forward_bf16")
-    elif pre is not None:  # row / column means came with x from its producer
-        _check(_launch(key, x.device, lib.yolosod_ca_forward_pre, *args, pre[0].data_ptr(),
-                       ws.data_ptr(), ws.numel(), _stream(x.device)), "ca_forward_pre")
-    else:
-        _check(_launch(key, x.device, lib.yolosod_ca_forward, *args, ws.data_ptr(), ws.numel(),
-                       _stream(x.device)), "ca_forward")
-    return y
+    pre = getattr(x, "_ys_ca_pool", None)  # row / column means that came with x from its producer
+    yin = pre[0] if pre is not None and pre[1] == tuple(x.shape) else None
+    return _launch(("ca", tuple(x.shape), mip) + ((2,) if bf else ()), x.device, ops().ca_fwd, x, conv1_w, conv1_b,
+                   bn_w, bn_b, bn_mean, bn_var, float(bn_eps), convh_w, convh_b, convw_w, convw_b, yin)
 
 
 def a2_forward(x, num_areas, num_heads, proj_w, proj_b, ln_w, ln_b, ln_eps, in_w, in_b, mo_w, mo_b, op_w, op_b):
-    """mo_w = mo_b = None: op_w / op_b are the pre-multiplied MHA-out x output-conv weights (A2_Attn._fused_out).
-    bf16 activations: proj_w / in_w / op_w bf16 (pre-multiplied form only), biases and LN fp32."""
-    lib = load_library()
-    bf = _act_dtype(x)
-    if (mo_w is None) != (mo_b is None):
-        raise RuntimeError("a2_forward: attention.out_proj weight and bias must both be given or both be None")
+    """A2_Attn -> torch.ops.yolosod.a2_fwd. mo_w = mo_b = None: op_w / op_b are the pre-multiplied MHA-out x
+    output-conv weights (A2_Attn._fused_out). bf16 activations: proj_w / in_w / op_w bf16 (pre-multiplied form
+    only), biases and LN fp32."""
+    bf = _act_dtype(_t(x, "x"))
     B, C, H, W = x.shape
-    if C % num_heads:
-        raise RuntimeError(f"A2_Attn: C={C} not divisible by num_heads={num_heads}")
     if num_areas * W > 320:
         raise RuntimeError(f"A2_Attn: sequence length {num_areas * W} > 320 unsupported")
-    y = torch.empty_like(x)
-    key = ("a2", tuple(x.shape), (num_areas, num_heads)) + ((2,) if bf else ())
-    if bf:
-        if mo_w is not None:
-            raise RuntimeError("a2_forward: the bf16 path takes the pre-multiplied output weights only")
-        if C // num_heads not in (32, 64, 128) or C % 64:
-            raise RuntimeError(f"A2_Attn (bf16): C={C} with head dim {C // num_heads} unsupported")
-        ws = _workspace(lib.yolosod_a2_workspace_bf16(B, C, H, W, num_areas), x.device)
-        _check(_launch(key, x.device, lib.yolosod_a2_forward_bf16, _dev(x, "x", _BF16), _dev(y, "y", _BF16), B, C, H,
-                       W, num_areas, num_heads, _p(proj_w, "proj.weight", C * C, _BF16), _p(proj_b, "proj.bias", C),
-                       _p(ln_w, "layer_norm.weight", C), _p(ln_b, "layer_norm.bias", C), float(ln_eps),
-                       _p(in_w, "in_proj_weight", 3 * C * C, _BF16), _p(in_b, "in_proj_bias", 3 * C),
-                       _p(op_w, "out_proj.weight", C * C, _BF16), _p(op_b, "out_proj.bias", C), ws.data_ptr(),
-                       ws.numel(), _stream(x.device)), "a2_forward_bf16")
-        return y
-    ws = _workspace(lib.yolosod_a2_workspace(B, C, H, W, num_areas), x.device)
-    _check(_launch(key, x.device, lib.yolosod_a2_forward, _dev(x, "x"), _dev(y, "y"), B, C, H, W, num_areas, num_heads,
-                                  _p(proj_w, "proj.weight", C * C), _p(proj_b, "proj.bias", C),
-                                  _p(ln_w, "layer_norm.weight", C), _p(ln_b, "layer_norm.bias", C), float(ln_eps),
-                                  _p(in_w, "in_proj_weight", 3 * C * C), _p(in_b, "in_proj_bias", 3 * C),
-                                  _p(mo_w, "attention.out_proj.weight", C * C) if mo_w is not None else None,
-                                  _p(mo_b, "attention.out_proj.bias", C) if mo_b is not None else None,
-                                  _p(op_w, "out_proj.weight", C * C),
-                                  _p(op_b, "out_proj.bias", C), ws.data_ptr(), ws.numel(), _stream(x.device)),
-           "a2_forward")
-    return y
+    if bf and (C // num_heads not in (32, 64, 128) or C % 64):
+        raise RuntimeError(f"A2_Attn (bf16): C={C} with head dim {C // num_heads} unsupported")
+    return _launch(("a2", tuple(x.shape), (num_areas, num_heads)) + ((2,) if bf else ()), x.device, ops().a2_fwd, x,
+                   int(num_areas), int(num_heads), proj_w, proj_b, ln_w, ln_b, float(ln_eps), in_w, in_b, mo_w, mo_b,
+                   op_w, op_b)
 
 
 def swin_forward(x, num_heads, window, dw_w, ln1_w, ln1_b, ln1_eps, in_w, in_b, out_w, out_b, ln2_w, ln2_b,
                  ln2_eps, m1_w, m1_b, m2_w, m2_b, pw_w, bn_w, bn_b, bn_mean, bn_var, bn_eps):
-    """SwinBlock on fp32 or bf16 activations. bf16: the projection / MLP / pw weights (in_w, out_w, m1_w, m2_w,
-    pw_w) are bf16, every other parameter fp32."""
-    lib = load_library()
-    bf = _act_dtype(x)
+    """SwinBlock -> torch.ops.yolosod.swin_fwd on fp32 or bf16 activations. bf16: the projection / MLP / pw weights
+    (in_w, out_w, m1_w, m2_w, pw_w) are bf16, every other parameter fp32."""
+    bf = _act_dtype(_t(x, "x"))
     B, C, H, W = x.shape
     hid = m1_w.shape[0]
     wh = H if (H <= window and W <= window) else min(window, H)
@@ -372,25 +325,10 @@ def swin_forward(x, num_heads, window, dw_w, ln1_w, ln1_b, ln1_eps, in_w, in_b, 
         raise RuntimeError(f"SwinBlock: window of {wh}x{ww} tokens unsupported")
     if C % num_heads or (C // num_heads) not in ((32, 64, 128) if bf else (8, 16, 32, 64, 128)):
         raise RuntimeError(f"SwinBlock: head dim {C}/{num_heads} unsupported")
-    y = torch.empty_like(x)
-    gw = _BF16 if bf else torch.float32
-    if bf:
-        ws = _workspace(lib.yolosod_swin_workspace_bf16(B, C, H, W, num_heads, window, hid), x.device)
-        fn, what = lib.yolosod_swin_forward_bf16, "swin_forward_bf16"
-    else:
-        ws = _workspace(lib.yolosod_swin_workspace_v2(B, C, H, W, num_heads, window, hid), x.device)
-        fn, what = lib.yolosod_swin_forward, "swin_forward"
-    _check(_launch(("swin", tuple(x.shape), (num_heads, window, hid)) + ((2,) if bf else ()), x.device, fn,
-        _dev(x, "x", x.dtype), _dev(y, "y", x.dtype), B, C, H, W, num_heads, window, _p(dw_w, "dw.weight", C * 9),
-        _p(ln1_w, "norm1.weight", C), _p(ln1_b, "norm1.bias", C), float(ln1_eps),
-        _p(in_w, "in_proj_weight", 3 * C * C, gw), _p(in_b, "in_proj_bias", 3 * C),
-        _p(out_w, "out_proj.weight", C * C, gw), _p(out_b, "out_proj.bias", C),
-        _p(ln2_w, "norm2.weight", C), _p(ln2_b, "norm2.bias", C), float(ln2_eps),
-        _p(m1_w, "mlp.0.weight", hid * C, gw), _p(m1_b, "mlp.0.bias", hid), hid,
-        _p(m2_w, "mlp.2.weight", C * hid, gw), _p(m2_b, "mlp.2.bias", C), _p(pw_w, "pw.weight", C * C, gw),
-        _p(bn_w, "bn.weight", C), _p(bn_b, "bn.bias", C), _p(bn_mean, "bn.running_mean", C),
-        _p(bn_var, "bn.running_var", C), float(bn_eps), ws.data_ptr(), ws.numel(), _stream(x.device)), what)
-    return y
+    return _launch(("swin", tuple(x.shape), (num_heads, window, hid)) + ((2,) if bf else ()), x.device, ops().swin_fwd,
+                   x, int(num_heads), int(window), dw_w, ln1_w, ln1_b, float(ln1_eps), in_w, in_b, out_w, out_b,
+                   ln2_w, ln2_b, float(ln2_eps), m1_w, m1_b, m2_w, m2_b, pw_w, bn_w, bn_b, bn_mean, bn_var,
+                   float(bn_eps))
 
 
 def mamba_glu_forward(x, reduction, in_w, in_bn_w, in_bn_b, in_bn_m, in_bn_v, in_eps, pw1_w, dw_w, bn_w, bn_b, bn_m,
@@ -421,83 +359,42 @@ def mamba_glu_forward(x, reduction, in_w, in_bn_w, in_bn_b, in_bn_m, in_bn_v, in
 
 
 def detect_decode(maps, strides, nc, reg_max=16):
-    """maps: list of [B, 4*reg_max+nc, Hi, Wi] fp32 -> y [B, 4+nc, A]."""
-    lib = load_library()
-    nl = len(maps)
-    B = maps[0].shape[0]
+    """maps: list of [B, 4*reg_max+nc, Hi, Wi] fp32 -> y [B, 4+nc, A] (torch.ops.yolosod.detect_decode_fwd)."""
     no = 4 * reg_max + nc
+    B = maps[0].shape[0]
     for i, m in enumerate(maps):
+        _t(m, f"maps[{i}]")
         if m.dim() != 4 or m.shape[0] != B or m.shape[1] != no:
             raise RuntimeError(f"detect_decode: map {i} has shape {tuple(m.shape)}, expected [B,{no},H,W]")
     A = sum(m.shape[2] * m.shape[3] for m in maps)
-    y = torch.empty((B, 4 + nc, A), dtype=torch.float32, device=maps[0].device)
-    ptrs = (ctypes.c_void_p * nl)(*[_dev(m, f"maps[{i}]") for i, m in enumerate(maps)])
-    hs = (ctypes.c_int * nl)(*[m.shape[2] for m in maps])
-    wsz = (ctypes.c_int * nl)(*[m.shape[3] for m in maps])
-    st = (ctypes.c_float * nl)(*[float(s) for s in strides])
-    _check(_launch(("decode", (B, A), nc), maps[0].device, lib.yolosod_detect_decode, nl, ctypes.cast(ptrs, ctypes.c_void_p), ctypes.cast(hs, ctypes.c_void_p),
-                                     ctypes.cast(wsz, ctypes.c_void_p), ctypes.cast(st, ctypes.c_void_p), B, nc,
-                                     reg_max, _dev(y, "y"), _stream(maps[0].device)), "detect_decode")
-    return y
+    return _launch(("decode", (B, A), nc), maps[0].device, ops().detect_decode_fwd, list(maps),
+                   [float(s) for s in strides], int(nc), int(reg_max))
 
 
 def detect_head(box_feats, cls_feats, box_w, box_b, cls_w, cls_b, strides, nc, reg_max=16):
-    """Fused last 1x1 convs of both Detect towers + decode. box_feats[i] [B, c2, Hi, Wi], cls_feats[i]
-    [B, c3, Hi, Wi] contiguous fp32 or bf16 (all levels alike); box_w[i] [64, c2], cls_w[i] [nc, c3] and biases
-    fp32 -> y [B, 4+nc, A] fp32 (the decode stays fp32 in the bf16 config)."""
-    lib = load_library()
-    nl = len(box_feats)
-    bf = _act_dtype(box_feats[0])
-    ft = box_feats[0].dtype
+    """Fused last 1x1 convs of both Detect towers + decode (torch.ops.yolosod.detect_head_fwd). box_feats[i]
+    [B, c2, Hi, Wi], cls_feats[i] [B, c3, Hi, Wi] contiguous fp32 or bf16 (all levels alike); box_w[i] [64, c2],
+    cls_w[i] [nc, c3] and biases fp32 -> y [B, 4+nc, A] fp32 (the decode stays fp32 in the bf16 config)."""
+    bf = _act_dtype(_t(box_feats[0], "box_feats[0]"))
     B, c2 = box_feats[0].shape[:2]
     c3 = cls_feats[0].shape[1]
-    for i in range(nl):
-        fb, fc = box_feats[i], cls_feats[i]
-        if (fb.shape[0] != B or fb.shape[1] != c2 or fc.shape[1] != c3 or fb.shape[2:] != fc.shape[2:]
-                or not fb.is_contiguous() or not fc.is_contiguous()):
-            raise RuntimeError(f"detect_head: level {i} features {tuple(fb.shape)} / {tuple(fc.shape)} mismatch")
-        if tuple(box_w[i].shape) != (4 * reg_max, c2) or tuple(cls_w[i].shape) != (nc, c3):
-            raise RuntimeError(f"detect_head: level {i} weights {tuple(box_w[i].shape)} / {tuple(cls_w[i].shape)}")
     A = sum(t.shape[2] * t.shape[3] for t in box_feats)
-    y = torch.empty((B, 4 + nc, A), dtype=torch.float32, device=box_feats[0].device)
-
-    def arr(ts, what, dtype=torch.float32):
-        return ctypes.cast((ctypes.c_void_p * nl)(*[_dev(t, f"{what}[{i}]", dtype) for i, t in enumerate(ts)]),
-                           ctypes.c_void_p)
-
-    hs = (ctypes.c_int * nl)(*[t.shape[2] for t in box_feats])
-    wsz = (ctypes.c_int * nl)(*[t.shape[3] for t in box_feats])
-    st = (ctypes.c_float * nl)(*[float(s) for s in strides])
-    fn = lib.yolosod_detect_head_bf16 if bf else lib.yolosod_detect_head
-    _check(_launch(("head", (B, A), (nc, c2, c3)) + ((2,) if bf else ()), box_feats[0].device, fn, nl, arr(box_feats, "box_feats", ft),
-                   arr(cls_feats, "cls_feats", ft), c2, c3, arr(box_w, "box_w"), arr(box_b, "box_b"),
-                   arr(cls_w, "cls_w"), arr(cls_b, "cls_b"), ctypes.cast(hs, ctypes.c_void_p),
-                   ctypes.cast(wsz, ctypes.c_void_p), ctypes.cast(st, ctypes.c_void_p), B, nc, reg_max,
-                   _dev(y, "y"), _stream(box_feats[0].device)), "detect_head")
-    return y
+    return _launch(("head", (B, A), (nc, c2, c3)) + ((2,) if bf else ()), box_feats[0].device, ops().detect_head_fwd,
+                   list(box_feats), list(cls_feats), list(box_w), list(box_b), list(cls_w), list(cls_b),
+                   [float(s) for s in strides], int(nc), int(reg_max))
 
 
 def nms(pred, conf_thres, iou_thres, classes, agnostic, multi_label, max_det, max_nms, max_wh, in_place):
-    """Batched NMS on pred [B, 4+nc, A] (GPU). Returns (out [B,max_det,6], counts [B] int32, index [B,max_det])."""
-    lib = load_library()
-    B, no, A = pred.shape
-    nc = no - 4
-    dev = pred.device
+    """Batched NMS on pred [B, 4+nc, A] (GPU; torch.ops.yolosod.nms_batched). Returns (out [B,max_det,6],
+    counts [B] int32, index [B,max_det] int32)."""
+    B, no, A = _t(pred, "prediction").shape
     if not in_place:
         pred = pred.clone()
-    out = torch.empty((B, max_det, 6), dtype=torch.float32, device=dev)
-    counts = torch.empty((B,), dtype=torch.int32, device=dev)
-    index = torch.empty((B, max_det), dtype=torch.int32, device=dev)
-    ws = _workspace(lib.yolosod_nms_workspace_v2(B, nc, A, int(multi_label), int(max_det)), dev)
-    cls_ptr, ncls = None, 0
+    cls = None
     if classes is not None:
-        ct = torch.as_tensor(classes, dtype=torch.int32, device=dev).reshape(-1).contiguous()
-        cls_ptr, ncls = ct.data_ptr(), ct.numel()
-    _check(_launch(("nms", (B, nc, A), int(multi_label)), dev, lib.yolosod_nms, _dev(pred, "prediction"), B, nc, A, float(conf_thres), float(iou_thres), cls_ptr, ncls,
-                           int(bool(agnostic)), int(bool(multi_label)), int(max_det), int(max_nms), float(max_wh),
-                           1, out.data_ptr(), counts.data_ptr(), index.data_ptr(), ws.data_ptr(), ws.numel(),
-                           _stream(dev)), "nms")
-    return out, counts, index
+        cls = torch.as_tensor(classes, dtype=torch.int32, device=pred.device).reshape(-1).contiguous()
+    return _launch(("nms", (B, no - 4, A), int(multi_label)), pred.device, ops().nms_batched, pred, float(conf_thres),
+                   float(iou_thres), cls, bool(agnostic), bool(multi_label), int(max_det), int(max_nms), float(max_wh))
 
 
 def bias_act(y, bias, act, out=None, res=None, stats=None, out2=None, c2lo=0):

@@ -30,6 +30,33 @@ def _hipcc() -> str:
     raise RuntimeError("hipcc not found")
 
 
+TORCH_OPS_SRC = CSRC / "torch_ops.cpp"
+TORCH_OPS_LIB = PKG / "lib" / "yolosod_torch_ops.so"
+
+
+def build_torch_ops(verbose: bool = False, force: bool = False) -> Path:
+    """torch.ops.yolosod.* (csrc/torch_ops.cpp): a torch.utils.cpp_extension library over libyolosod_hip.so, built
+    in-tree (build/torch_ops, ninja) and copied next to the HIP library (lib/, which ships to the GPU box)."""
+    import shutil
+
+    deps = [TORCH_OPS_SRC, INCLUDE / "yolosod_hip.h"]
+    if (not force and TORCH_OPS_LIB.exists()
+            and TORCH_OPS_LIB.stat().st_mtime >= max(d.stat().st_mtime for d in deps)):
+        return TORCH_OPS_LIB
+    from torch.utils import cpp_extension
+
+    bdir = OBJ / "torch_ops"
+    bdir.mkdir(parents=True, exist_ok=True)
+    so = cpp_extension.load(
+        name="yolosod_torch_ops", sources=[str(TORCH_OPS_SRC)], extra_include_paths=[str(INCLUDE), "/opt/rocm/include"],
+        extra_cflags=["-O2", "-D__HIP_PLATFORM_AMD__"],
+        extra_ldflags=[f"-L{LIB.parent}", "-lyolosod_hip", "-L/opt/rocm/lib", "-lamdhip64", "-lc10_hip", r"-Wl,-rpath,\$$ORIGIN:\$$ORIGIN/../../lib"],  # \$$: ninja + shell escape
+        build_directory=str(bdir), is_python_module=False, verbose=verbose)
+    built = bdir / "yolosod_torch_ops.so"
+    shutil.copy2(built, TORCH_OPS_LIB)
+    return TORCH_OPS_LIB
+
+
 def build(verbose: bool = False, force: bool = False) -> Path:
     srcs = sorted(CSRC.glob("*.hip"))
     headers = list(CSRC.glob("*.h")) + list(INCLUDE.glob("*.h"))
@@ -64,6 +91,7 @@ def build(verbose: bool = False, force: bool = False) -> Path:
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
+    build_torch_ops(verbose=verbose, force=force)
     return LIB
 
 

@@ -326,6 +326,11 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
     // QKV weight fragments: in flight during the halo store, the depthwise conv and the LN1 statistics
     WFrag<C, 3 * C / 16> f_in;
     load_wfrag(w_in, f_in, tid);
+    // each epilogue's biases are loaded with that stage's weight fragments: a bias load issued after the GEMM sat
+    // behind nothing but still cost an exposed L2 round trip (s_waitcnt vmcnt(0)) per stage
+    float bq[3 * C / 64];
+#pragma unroll
+    for (int j = 0; j < 3 * C / 64; ++j) bq[j] = b_in[(wid + 4 * j) * 16 + l15];
 
     // ---- stage 0: halo patch (registers) -> LDS [c][py][HPW] -> dw conv, one output row of 7 tokens per item ----
     if (W7) {
@@ -384,7 +389,7 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const int n = (wid + 4 * j) * 16 + l15;
-        const float bias = b_in[n];
+        const float bias = bq[j];
 #pragma unroll
         for (int rb = 0; rb < 3; ++rb)
 #pragma unroll
@@ -394,6 +399,9 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
     }
     WFrag<C, C / 16> f_o;  // out-proj weights: in flight during attention
     load_wfrag(w_o, f_o, tid);
+    float bo_[C / 64];
+#pragma unroll
+    for (int j = 0; j < C / 64; ++j) bo_[j] = b_o[(wid + 4 * j) * 16 + l15];
     __syncthreads();
     YS_STAMP(4)
 
@@ -521,7 +529,7 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const int n = (wid + 4 * j) * 16 + l15;
-        const float bias = b_o[n];
+        const float bias = bo_[j];
 #pragma unroll
         for (int rb = 0; rb < 3; ++rb)
 #pragma unroll
@@ -534,6 +542,9 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
     }
     WFrag<C, HID / 16> f_1;  // MLP1 weights: in flight during the LN2 statistics
     load_wfrag(w_1, f_1, tid);
+    float b1_[HID / 64];
+#pragma unroll
+    for (int j = 0; j < HID / 64; ++j) b1_[j] = b_1[(wid + 4 * j) * 16 + l15];
     __syncthreads();
     YS_STAMP(6)
 
@@ -553,7 +564,7 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const int n = (wid + 4 * j) * 16 + l15;
-        const float bias = b_1[n];
+        const float bias = b1_[j];
 #pragma unroll
         for (int rb = 0; rb < 3; ++rb)
 #pragma unroll
@@ -567,6 +578,9 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
     }
     WFrag<HID, C / 16> f_2;  // MLP2 weights
     load_wfrag(w_2, f_2, tid);
+    float b2_[C / 64];
+#pragma unroll
+    for (int j = 0; j < C / 64; ++j) b2_[j] = b_2[(wid + 4 * j) * 16 + l15];
     __syncthreads();
     YS_STAMP(8)
 
@@ -598,7 +612,7 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
       vtok[tb] = ok ? (unsigned)(((wid * 16 + 4 * g) * HWi + hh * W + wc) * 4) : OOB;
     }
     const unsigned v48 = (pix48 >= 0 && g == 0) ? (unsigned)(((wid * 16 + l15) * HWi + pix48) * 4) : OOB;
-    float xr[3][4], x48, bsc[4], bsh[4];
+    float xr[3][4], x48, bsc[4], bsh[4], sc48, sh48;
     auto load_resid = [&](int cb) {
       const int sb = (cb - wid) * 16 * HWi * 4;
       const bool skip = p.abl & 4;
@@ -614,6 +628,8 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
         bsc[r] = bn_sc[cb * 16 + 4 * g + r];
         bsh[r] = bn_sh[cb * 16 + 4 * g + r];
       }
+      sc48 = bn_sc[cb * 16 + l15];
+      sh48 = bn_sh[cb * 16 + l15];
     };
     load_resid(wid);
 
@@ -627,7 +643,7 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const int n = (wid + 4 * j) * 16 + l15;
-        const float bias = b_2[n];
+        const float bias = b2_[j];
 #pragma unroll
         for (int rb = 0; rb < 3; ++rb)
 #pragma unroll
@@ -693,9 +709,8 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
             __builtin_amdgcn_raw_buffer_store_b32(
                 __builtin_bit_cast(unsigned, xr[tb][r] + silu_fast_(acc[tb][r] * bsc[r] + bsh[r])), ry8, vtok[tb],
                 sb + r * HWi * 4, 0);
-        const int c48 = cb * 16 + l15;
         __builtin_amdgcn_raw_buffer_store_b32(
-            __builtin_bit_cast(unsigned, x48 + silu_fast_(e48 * bn_sc[c48] + bn_sh[c48])), ry8, v48, sb, 0);
+            __builtin_bit_cast(unsigned, x48 + silu_fast_(e48 * sc48 + sh48)), ry8, v48, sb, 0);
       }
     }
     YS_STAMP(15)

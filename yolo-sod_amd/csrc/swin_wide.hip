@@ -277,6 +277,9 @@ __global__ __launch_bounds__(NT, 1) void swin_wide_kernel(Args p) {
 
   // ---- attention on head pairs; out-projection partials accumulated in registers ----
   f32x4 acc_o[3][2];
+  float bo_[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) bo_[j] = p.bo[(wid + 8 * j) * 16 + l15];
   float ext_o[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
@@ -301,11 +304,14 @@ __global__ __launch_bounds__(NT, 1) void swin_wide_kernel(Args p) {
 #pragma unroll
         for (int rb = 0; rb < 3; ++rb) acc[rb][j] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
+      // biases loaded before the weight stream: after it, each one was an exposed L2 round trip
+      float bq[3];
+#pragma unroll
+      for (int j = 0; j < 3; ++j) bq[j] = p.bin[(nl[j] >> 7) * C + hp * 128 + (nl[j] & 127)];
       gemm_stream<C, 3, true, false>(T, LT, wrow, acc, ext, stats, lnp, lnp + C, lane);
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
-        const int part = nl[j] >> 7, within = nl[j] & 127;
-        const float bias = p.bin[part * C + hp * 128 + within];
+        const float bias = bq[j];
         const float e = group4_sum(ext[j]);
 #pragma unroll
         for (int rb = 0; rb < 3; ++rb)
@@ -403,7 +409,7 @@ __global__ __launch_bounds__(NT, 1) void swin_wide_kernel(Args p) {
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int n = (wid + 8 * j) * 16 + l15;
-    const float bias = p.bo[n];
+    const float bias = bo_[j];
     const float e = group4_sum(ext_o[j]);
 #pragma unroll
     for (int rb = 0; rb < 3; ++rb)
@@ -420,6 +426,9 @@ __global__ __launch_bounds__(NT, 1) void swin_wide_kernel(Args p) {
   // ---- MLP in two hidden chunks of 256; MLP2 partials accumulated in registers ----
   f32x4 acc_m[3][2];
   float ext_m[2];
+  float b2_[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) b2_[j] = p.b2[(wid + 8 * j) * 16 + l15];
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     ext_m[j] = 0.f;
@@ -441,10 +450,13 @@ __global__ __launch_bounds__(NT, 1) void swin_wide_kernel(Args p) {
 #pragma unroll
         for (int rb = 0; rb < 3; ++rb) acc[rb][j] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
+      float b1_[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b1_[j] = p.b1[ck * 256 + nl[j]];
       gemm_stream<C, 2, true, false>(T, LT, wrow, acc, ext, stats, lnp + 2 * C, lnp + 3 * C, lane);
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const float bias = p.b1[ck * 256 + nl[j]];
+        const float bias = b1_[j];
         const float e = group4_sum(ext[j]);
 #pragma unroll
         for (int rb = 0; rb < 3; ++rb)
@@ -469,7 +481,7 @@ __global__ __launch_bounds__(NT, 1) void swin_wide_kernel(Args p) {
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int n = (wid + 8 * j) * 16 + l15;
-    const float bias = p.b2[n];
+    const float bias = b2_[j];
     const float e = group4_sum(ext_m[j]);
 #pragma unroll
     for (int rb = 0; rb < 3; ++rb)
