@@ -302,7 +302,9 @@ def main():
         ops.append({"op": key[0], "shape": list(key[1]), "dtype": "bf16" if perf.elem_size(key) == 2 else "f32",
                     "launches": n, "avg_ms": round(avg, 4), "total_ms_per_step": round(tot / args.steps, 4),
                     "GBps": round(nbytes / (avg * 1e-3) / 1e9, 1),
-                    "TFLOPs": round(flops / (avg * 1e-3) / 1e12, 2), "bytes": nbytes, "flops": flops, "key": key})
+                    "TFLOPs": round(flops / (avg * 1e-3) / 1e12, 2), "bound": perf.bound_of(key),
+                    "t_min_ms": round(perf.t_min_ms(key), 4), "frac": round(perf.t_min_ms(key) / avg, 3),
+                    "bytes": nbytes, "flops": flops, "key": key})
     ops.sort(key=lambda o: -o["total_ms_per_step"])
     dom = ops[0]
     bound = perf.bound_of(dom["key"])

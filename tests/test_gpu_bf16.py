@@ -8,7 +8,7 @@ decode and NMS stay fp32.
 
 Oracle: the fp32 restatement (oracle/) evaluated in float64 on the SAME bf16 values - parameters and inputs
 rounded to bf16 first - so the measured difference is only this build's internal bf16 roundings. Tolerances
-(stated in DESIGN.md section 9, measured margins in profiles/r02_bf16_margins.txt):
+(stated in DESIGN.md section 9, measured margins in profiles/r02_parity_margins_s2.txt):
   * single-rounding ops (SE, CBAM, CA, conv epilogues): |d| <= 2^-7 |ref| + 1e-6 max|ref| (one bf16 rounding of
     the output is <= 2^-8 |ref|, bf16's unit roundoff; measured ratios 0.98-0.995 of 2^-8);
   * GEMM / attention: |d| <= 2^-7 |ref| + 2^-8 max|ref| (products of bf16 values accumulated in fp32, output
