@@ -87,7 +87,9 @@ def build(verbose: bool = False, force: bool = False) -> Path:
         raise RuntimeError(f"hipcc failed:\n{msg}")
     lib_mtime = LIB.stat().st_mtime if LIB.exists() else 0.0
     if force or procs or not LIB.exists() or any(o.stat().st_mtime > lib_mtime for o in objs):
-        cmd = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(LIB)]
+        # soname: a same-soname copy loaded first (YOLOSOD_LIB_AB) also satisfies the torch-op library's NEEDED entry
+        cmd = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-Wl,-soname,libyolosod_hip.so", *map(str, objs),
+               "-o", str(LIB)]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)

@@ -53,8 +53,6 @@ struct SwinFusedArgs {
   const float* bn_scale;
   const float* bn_shift;
   float scale;
-  int abl;  // timing ablation (debug only): 1 skip halo loads, 4 skip residual loads
-  unsigned long long* stamps;  // diagnostic build only: per-stage s_memtime of wave 0 ([window][16]) or nullptr
 };
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
@@ -92,17 +90,20 @@ __device__ __forceinline__ void load_wfrag(const float* __restrict__ Wg, WFrag<K
     }
 }
 
-// acc[rb][j] = A'[rows rb*16 .. rb*16+15][K] . W[n][K]^T (rb < 3: token rows 0..47 on MFMA) and ext[j] = the same
-// for token row 48 on the VALU, for this wave's column blocks cb = wid + 4*j (NCB % 4 == 0), n = cb*16 + l15.
+// Transposed output tiles: acc[rb][j] = (A[rows rb*16 .. +15][K] . W[n][K]^T)^T for this wave's column blocks
+// cb = wid + 4*j (NCB % 4 == 0): the W fragment is the MFMA A operand and the token rows the B operand, so lane
+// (g, l15) holds out[token rb*16 + l15][n = cb*16 + 4g .. +3] - four consecutive columns of one row, stored as one
+// 16-byte LDS write (and residual-added with one 16-byte read) instead of four 4-byte ones. The accumulators start
+// from the bias (the MFMA's C operand), so no epilogue add. ext[j] = the same for token row 48 on the VALU, column
+// n = cb*16 + l15, without bias.
 // The MFMA k index is permuted: lane group g owns k in [g*K/4, (g+1)*K/4), so A and W fragments are 16-byte loads;
 // the row-48 dot products reuse the W fragments already in registers (partial over the lane's k quarter, then a
 // cross-group sum), so the fourth 16-row block - 15 of its 16 rows padding - is never issued.
-// A: LDS [SW_ROWS][lda]. With LN, A' = (A - mean_r)*rstd_r*w + b (row statistics from `stats`, LN affine params
-// from LDS), applied to the fragments as they are read. W: the stage's prefetched fragments.
-template <int K, int NCB, bool LN>
+// A: LDS [SW_ROWS][lda]. W: the stage's prefetched fragments.
+template <int K, int NCB>
 __device__ __forceinline__ void wave_gemm_rows(const float* __restrict__ As, int lda, const WFrag<K, NCB>& wf,
-                                               f32x4 (&acc)[3][NCB / 4], float (&ext)[NCB / 4], const float* stats,
-                                               const float* lnw, const float* lnb, int tid) {
+                                               const f32x4 (&bias)[NCB / 4], f32x4 (&acc)[3][NCB / 4],
+                                               float (&ext)[NCB / 4], int tid) {
   constexpr int NJ = NCB / 4;
   static_assert(NCB % 4 == 0, "column blocks must split evenly over the 4 waves");
   const int lane = tid & 63;
@@ -110,38 +111,19 @@ __device__ __forceinline__ void wave_gemm_rows(const float* __restrict__ As, int
   constexpr int KQ = K / 4;  // k range per lane group
   const auto& bw = wf.v;
   const float* arow[4];
-  float mu[4], rs[4];
 #pragma unroll
-  for (int rb = 0; rb < 4; ++rb) {
-    const int r = rb < 3 ? rb * 16 + l15 : XR;
-    arow[rb] = As + r * lda + g * KQ;
-    if (LN) {
-      mu[rb] = stats[2 * r];
-      rs[rb] = stats[2 * r + 1];
-    }
-  }
+  for (int rb = 0; rb < 4; ++rb) arow[rb] = As + (rb < 3 ? rb * 16 + l15 : XR) * lda + g * KQ;
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     ext[j] = 0.f;
 #pragma unroll
-    for (int rb = 0; rb < 3; ++rb) acc[rb][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int rb = 0; rb < 3; ++rb) acc[rb][j] = bias[j];
   }
 #pragma unroll
   for (int t = 0; t < KQ / 4; ++t) {
     float4 a[4];
 #pragma unroll
     for (int rb = 0; rb < 4; ++rb) a[rb] = *reinterpret_cast<const float4*>(arow[rb] + 4 * t);
-    if (LN) {
-      const float4 w = *reinterpret_cast<const float4*>(lnw + g * KQ + 4 * t);
-      const float4 bb = *reinterpret_cast<const float4*>(lnb + g * KQ + 4 * t);
-#pragma unroll
-      for (int rb = 0; rb < 4; ++rb) {
-        a[rb].x = (a[rb].x - mu[rb]) * rs[rb] * w.x + bb.x;
-        a[rb].y = (a[rb].y - mu[rb]) * rs[rb] * w.y + bb.y;
-        a[rb].z = (a[rb].z - mu[rb]) * rs[rb] * w.z + bb.z;
-        a[rb].w = (a[rb].w - mu[rb]) * rs[rb] * w.w + bb.w;
-      }
-    }
 #pragma unroll
     for (int c = 0; c < 4; ++c)
 #pragma unroll
@@ -150,13 +132,26 @@ __device__ __forceinline__ void wave_gemm_rows(const float* __restrict__ As, int
         for (int j = 0; j < NJ; ++j) {
           const float av = c == 0 ? a[rb].x : c == 1 ? a[rb].y : c == 2 ? a[rb].z : a[rb].w;
           const float bv = c == 0 ? bw[j][t].x : c == 1 ? bw[j][t].y : c == 2 ? bw[j][t].z : bw[j][t].w;
-          acc[rb][j] = mfma4(av, bv, acc[rb][j]);
+          acc[rb][j] = mfma4(bv, av, acc[rb][j]);
         }
 #pragma unroll
     for (int j = 0; j < NJ; ++j) ext[j] = dot4_acc(a[3], bw[j][t], ext[j]);
   }
 #pragma unroll
   for (int j = 0; j < NJ; ++j) ext[j] = group4_sum(ext[j]);
+}
+
+// biases of this wave's column blocks: bias4[j] = b[cb*16 + 4g .. +3] (the transposed tiles' rows), b48[j] =
+// b[cb*16 + l15] (token 48's column)
+template <int NJ>
+__device__ __forceinline__ void load_bias(const float* __restrict__ b, f32x4 (&bias4)[NJ], float (&b48)[NJ],
+                                          int wid, int lane) {
+  const int l15 = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    bias4[j] = *reinterpret_cast<const f32x4*>(b + (wid + 4 * j) * 16 + 4 * g);
+    b48[j] = b[(wid + 4 * j) * 16 + l15];
+  }
 }
 
 // LayerNorm of rows [0, SW_ROWS) of S[SW_ROWS][lds] over C into U[SW_ROWS][ldu]: 4 threads per row (all rows at
@@ -200,9 +195,6 @@ __device__ __forceinline__ void lds_row_layernorm(const float* S, int lds, float
     }
   }
 }
-
-#define YS_STAMP(k)                                                                  \
-  if (p.stamps && tid == 0) p.stamps[gw * 16 + (k)] = __builtin_amdgcn_s_memtime();
 
 // Persistent: each workgroup walks a strided sequence of windows inside its XCD's contiguous window range
 // (workgroup i runs on XCD i % 8; neighbouring windows share 128-B lines of x and y - a window row is 28 B - so
@@ -275,7 +267,7 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
     const int h0 = wy_ * wh - 1, w0 = wx_ * ww - 1;
     const float* xb_ = p.x + (long)im * C * HWl;
     const int wc = w0 + hl_px;
-    const bool colok = hl_r < 7 && hl_px < PW && wc >= 0 && wc < W && !(p.abl & 1);
+    const bool colok = hl_r < 7 && hl_px < PW && wc >= 0 && wc < W;
     if (W7) {
       // descriptor from provably wave-uniform words (otherwise every load becomes a readfirstlane waterfall)
       const unsigned long long xa = (unsigned long long)xb_;
@@ -322,15 +314,14 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
       asm volatile("" : "+s"(w_in), "+s"(b_in), "+s"(w_o), "+s"(b_o), "+s"(w_1), "+s"(b_1));
       asm volatile("" : "+s"(w_2), "+s"(b_2), "+s"(w_pw), "+s"(bn_sc), "+s"(bn_sh));
     }
-    YS_STAMP(0)
     // QKV weight fragments: in flight during the halo store, the depthwise conv and the LN1 statistics
     WFrag<C, 3 * C / 16> f_in;
     load_wfrag(w_in, f_in, tid);
     // each epilogue's biases are loaded with that stage's weight fragments: a bias load issued after the GEMM sat
     // behind nothing but still cost an exposed L2 round trip (s_waitcnt vmcnt(0)) per stage
-    float bq[3 * C / 64];
-#pragma unroll
-    for (int j = 0; j < 3 * C / 64; ++j) bq[j] = b_in[(wid + 4 * j) * 16 + l15];
+    f32x4 bq[3 * C / 64];
+    float bq48[3 * C / 64];
+    load_bias(b_in, bq, bq48, wid, lane);
 
     // ---- stage 0: halo patch (registers) -> LDS [c][py][HPW] -> dw conv, one output row of 7 tokens per item ----
     if (W7) {
@@ -346,7 +337,6 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
       }
     }
     __syncthreads();
-    YS_STAMP(1)
     for (int item = tid; item < C * wh; item += 256) {
       const int iy = item / C;  // item % C == dw_c (256 % C == 0)
       const float* hp = Q + (dw_c * PH + iy) * HPW;
@@ -371,12 +361,10 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
     if (!W7 && L < SW_ROWS)
       for (int e = tid; e < (SW_ROWS - L) * C; e += 256) T[(L + e / C) * LT + e % C] = 0.f;
     __syncthreads();
-    YS_STAMP(2)
 
     // ---- stage 1: LN1 row statistics ----
     lds_row_layernorm<C>(T, LT, Q + 2 * C, LQ, lnp, lnp + C, L, p.ln1_eps, tid);
     __syncthreads();
-    YS_STAMP(3)
 
     // ---- stage 2: QKV = LN1(T) Win^T + b_in ----
     {
@@ -384,26 +372,22 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
       constexpr int NJ = NCB / 4;
       f32x4 acc[3][NJ];
       float ext[NJ];
-      wave_gemm_rows<C, NCB, false>(Q + 2 * C, LQ, f_in, acc, ext, nullptr, nullptr, nullptr, tid);
+      wave_gemm_rows<C, NCB>(Q + 2 * C, LQ, f_in, bq, acc, ext, tid);
       __syncthreads();  // every wave has read U1 (the V columns) before any wave writes V
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
-        const int n = (wid + 4 * j) * 16 + l15;
-        const float bias = bq[j];
+        const int n4 = (wid + 4 * j) * 16 + 4 * g;
 #pragma unroll
-        for (int rb = 0; rb < 3; ++rb)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) Q[(rb * 16 + g * 4 + r) * LQ + n] = acc[rb][j][r] + bias;
-        if (g == 0) Q[XR * LQ + n] = ext[j] + bias;
+        for (int rb = 0; rb < 3; ++rb) *reinterpret_cast<f32x4*>(Q + (rb * 16 + l15) * LQ + n4) = acc[rb][j];
+        if (g == 0) Q[XR * LQ + (wid + 4 * j) * 16 + l15] = ext[j] + bq48[j];
       }
     }
     WFrag<C, C / 16> f_o;  // out-proj weights: in flight during attention
     load_wfrag(w_o, f_o, tid);
-    float bo_[C / 64];
-#pragma unroll
-    for (int j = 0; j < C / 64; ++j) bo_[j] = b_o[(wid + 4 * j) * 16 + l15];
+    f32x4 bo_[C / 64];
+    float bo48[C / 64];
+    load_bias(b_o, bo_, bo48, wid, lane);
     __syncthreads();
-    YS_STAMP(4)
 
     // ---- stage 3: attention, wave = query block (16 queries), all heads interleaved ----
     // Keys 0..47 on MFMA (S^T accumulators reused as the B operand of O^T = V^T P^T), key 48 on the VALU. The
@@ -517,7 +501,6 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
       }
     }
     __syncthreads();
-    YS_STAMP(5)
 
     // ---- stage 4: T += O Wo^T + bo ----
     {
@@ -525,33 +508,28 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
       constexpr int NJ = NCB / 4;
       f32x4 acc[3][NJ];
       float ext[NJ];
-      wave_gemm_rows<C, C / 16, false>(Q, LQ, f_o, acc, ext, nullptr, nullptr, nullptr, tid);
+      wave_gemm_rows<C, C / 16>(Q, LQ, f_o, bo_, acc, ext, tid);
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
-        const int n = (wid + 4 * j) * 16 + l15;
-        const float bias = bo_[j];
+        const int n4 = (wid + 4 * j) * 16 + 4 * g;
 #pragma unroll
-        for (int rb = 0; rb < 3; ++rb)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int row = rb * 16 + g * 4 + r;
-            if (row < L) T[row * LT + n] += acc[rb][j][r] + bias;
-          }
-        if (g == 0 && XR < L) T[XR * LT + n] += ext[j] + bias;
+        for (int rb = 0; rb < 3; ++rb) {
+          f32x4* tp = reinterpret_cast<f32x4*>(T + (rb * 16 + l15) * LT + n4);
+          *tp = *tp + acc[rb][j];
+        }
+        if (g == 0 && XR < L) T[XR * LT + (wid + 4 * j) * 16 + l15] += ext[j] + bo48[j];
       }
     }
     WFrag<C, HID / 16> f_1;  // MLP1 weights: in flight during the LN2 statistics
     load_wfrag(w_1, f_1, tid);
-    float b1_[HID / 64];
-#pragma unroll
-    for (int j = 0; j < HID / 64; ++j) b1_[j] = b_1[(wid + 4 * j) * 16 + l15];
+    f32x4 b1_[HID / 64];
+    float b1_48[HID / 64];
+    load_bias(b_1, b1_, b1_48, wid, lane);
     __syncthreads();
-    YS_STAMP(6)
 
     // ---- stage 5: LN2 row statistics ----
     lds_row_layernorm<C>(T, LT, Q + SW_ROWS * LH, LT, lnp + 2 * C, lnp + 3 * C, L, p.ln2_eps, tid);
     __syncthreads();
-    YS_STAMP(7)
 
     // ---- stage 6: Hd = GELU(LN2(T) W1^T + b1) -> Q region [rows][LH] ----
     float* Hd = Q;
@@ -560,29 +538,25 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
       constexpr int NJ = NCB / 4;
       f32x4 acc[3][NJ];
       float ext[NJ];
-      wave_gemm_rows<C, HID / 16, false>(Q + SW_ROWS * LH, LT, f_1, acc, ext, nullptr, nullptr, nullptr, tid);
+      wave_gemm_rows<C, HID / 16>(Q + SW_ROWS * LH, LT, f_1, b1_, acc, ext, tid);
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
-        const int n = (wid + 4 * j) * 16 + l15;
-        const float bias = b1_[j];
+        const int n4 = (wid + 4 * j) * 16 + 4 * g;
 #pragma unroll
-        for (int rb = 0; rb < 3; ++rb)
-#pragma unroll
-          for (int r = 0; r < 4; r += 2) {
-            const f32x2 hv2 = gelu2_fast_(f32x2{acc[rb][j][r], acc[rb][j][r + 1]} + bias);
-            Hd[(rb * 16 + g * 4 + r) * LH + n] = hv2.x;
-            Hd[(rb * 16 + g * 4 + r + 1) * LH + n] = hv2.y;
-          }
-        if (g == 0) Hd[XR * LH + n] = gelu_fast_(ext[j] + bias);
+        for (int rb = 0; rb < 3; ++rb) {
+          const f32x2 lo = gelu2_fast_(f32x2{acc[rb][j][0], acc[rb][j][1]});
+          const f32x2 hi = gelu2_fast_(f32x2{acc[rb][j][2], acc[rb][j][3]});
+          *reinterpret_cast<f32x4*>(Hd + (rb * 16 + l15) * LH + n4) = f32x4{lo.x, lo.y, hi.x, hi.y};
+        }
+        if (g == 0) Hd[XR * LH + (wid + 4 * j) * 16 + l15] = gelu_fast_(ext[j] + b1_48[j]);
       }
     }
     WFrag<HID, C / 16> f_2;  // MLP2 weights
     load_wfrag(w_2, f_2, tid);
-    float b2_[C / 64];
-#pragma unroll
-    for (int j = 0; j < C / 64; ++j) b2_[j] = b_2[(wid + 4 * j) * 16 + l15];
+    f32x4 b2_[C / 64];
+    float b2_48[C / 64];
+    load_bias(b_2, b2_, b2_48, wid, lane);
     __syncthreads();
-    YS_STAMP(8)
 
     // stage-8 residual x (L2-hot: this window's halo) and BN terms of this wave's first channel block, loaded
     // here so their latency overlaps MLP2. Residual loads and y stores are buffer ops on per-image descriptors:
@@ -615,14 +589,13 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
     float xr[3][4], x48, bsc[4], bsh[4], sc48, sh48;
     auto load_resid = [&](int cb) {
       const int sb = (cb - wid) * 16 * HWi * 4;
-      const bool skip = p.abl & 4;
 #pragma unroll
       for (int tb = 0; tb < 3; ++tb)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          xr[tb][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx8, skip ? OOB : vtok[tb],
+          xr[tb][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx8, vtok[tb],
                                                                                     sb + r * HWi * 4, 0));
-      x48 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx8, skip ? OOB : v48, sb, 0));
+      x48 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx8, v48, sb, 0));
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         bsc[r] = bn_sc[cb * 16 + 4 * g + r];
@@ -639,19 +612,16 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
       constexpr int NJ = NCB / 4;
       f32x4 acc[3][NJ];
       float ext[NJ];
-      wave_gemm_rows<HID, C / 16, false>(Hd, LH, f_2, acc, ext, nullptr, nullptr, nullptr, tid);
+      wave_gemm_rows<HID, C / 16>(Hd, LH, f_2, b2_, acc, ext, tid);
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
-        const int n = (wid + 4 * j) * 16 + l15;
-        const float bias = b2_[j];
+        const int n4 = (wid + 4 * j) * 16 + 4 * g;
 #pragma unroll
-        for (int rb = 0; rb < 3; ++rb)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int row = rb * 16 + g * 4 + r;
-            if (row < L) T[row * LT + n] += acc[rb][j][r] + bias;
-          }
-        if (g == 0 && XR < L) T[XR * LT + n] += ext[j] + bias;
+        for (int rb = 0; rb < 3; ++rb) {
+          f32x4* tp = reinterpret_cast<f32x4*>(T + (rb * 16 + l15) * LT + n4);
+          *tp = *tp + acc[rb][j];
+        }
+        if (g == 0 && XR < L) T[XR * LT + (wid + 4 * j) * 16 + l15] += ext[j] + b2_48[j];
       }
     }
     // pw weights of this wave's first output-channel block
@@ -663,7 +633,6 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
       for (int t = 0; t < CQ / 4; ++t) wa[t] = *reinterpret_cast<const float4*>(wrow + 4 * t);
     }
     __syncthreads();
-    YS_STAMP(9)
 
     // next window's halo: in flight during the last stage
     if (has_next) load_halo(gnext);
@@ -713,7 +682,6 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
             __builtin_bit_cast(unsigned, x48 + silu_fast_(e48 * sc48 + sh48)), ry8, v48, sb, 0);
       }
     }
-    YS_STAMP(15)
     if (!PERSIST || !has_next) break;
     gw = gnext;
   }
@@ -722,31 +690,6 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
 }  // namespace ys
 
 using namespace ys;
-
-static unsigned long long* g_stamps = nullptr;  // diagnostic build only (YOLOSOD_SWIN_STAMPS)
-static size_t g_stamp_cap = 0, g_stamp_n = 0;
-
-// Diagnostic: average cycles between consecutive per-stage stamps of the last fused launch (synchronous).
-YS_EXPORT int yolosod_debug_swin_stage_cycles(double* out, int n) {
-  if (!g_stamps || n > 16) return -1;
-  const size_t cnt = g_stamp_n;
-  unsigned long long* h = (unsigned long long*)malloc(cnt * sizeof(unsigned long long));
-  if (hipMemcpy(h, g_stamps, cnt * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess) { free(h); return -1; }
-  for (int k = 0; k < n; ++k) out[k] = 0.0;
-  size_t blocks = cnt / 16;
-  for (size_t b = 0; b < blocks; ++b) {
-    unsigned long long* r = h + b * 16;
-    unsigned long long prev = r[0];
-    for (int k = 1; k < 16; ++k) {
-      if (!r[k]) continue;
-      if (k < n) out[k] += (double)(r[k] - prev);
-      prev = r[k];
-    }
-  }
-  for (int k = 0; k < n; ++k) out[k] /= (double)blocks;
-  free(h);
-  return 0;
-}
 
 // returns 1 if launched, 0 if the shape is not handled by the fused kernel, <0 on error
 int yolosod_swin_fused_launch(const float* x, float* y, int B, int C, int H, int W, int num_heads, int wh, int ww,
@@ -762,21 +705,7 @@ int yolosod_swin_fused_launch(const float* x, float* y, int B, int C, int H, int
   if ((long)B * nWin >= (1L << 31)) return 0;    // window indices are 32-bit
   SwinFusedArgs a{x, y, B, H, W, wh, ww, nWx, nWin, L, dw_w, ln1_w, ln1_b, ln1_eps, in_proj_w, in_proj_b,
                   out_proj_w, out_proj_b, ln2_w, ln2_b, ln2_eps, mlp1_w, mlp1_b, mlp2_w, mlp2_b, pw_w,
-                  bn_scale, bn_shift, 1.0f / sqrtf((float)(C / num_heads)), 0, nullptr};
-  if (const char* e = getenv("YOLOSOD_SWIN_ABL")) a.abl = atoi(e);
-  a.stamps = nullptr;
-  if (getenv("YOLOSOD_SWIN_STAMPS")) {
-    const size_t need = (size_t)B * nWin * 16;
-    if (need > g_stamp_cap) {
-      if (g_stamps) (void)hipFree(g_stamps);
-      g_stamps = nullptr;
-      if (hipMalloc((void**)&g_stamps, need * sizeof(unsigned long long)) != hipSuccess) return -1;
-      g_stamp_cap = need;
-    }
-    (void)hipMemsetAsync(g_stamps, 0, need * sizeof(unsigned long long), st);
-    g_stamp_n = need;
-    a.stamps = g_stamps;
-  }
+                  bn_scale, bn_shift, 1.0f / sqrtf((float)(C / num_heads))};
   // persistent grid: (resident workgroups per CU) x CUs, a multiple of 8 (one range of windows per XCD), never
   // more workgroups than windows; 3 resident per CU at C = 64 (LDS 52 KB)
   const bool w7 = (wh == 7 && ww == 7);
