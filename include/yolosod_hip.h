@@ -185,6 +185,10 @@ int yolosod_attention(const float* qkv, float* out, long n_seq, int L, int C, in
 /* Test hook: 1 routes SwinBlock shapes the fused per-window kernel covers (C 64/128, heads 2/4, window <= 7x7,
  * mlp 2C) through it (default, or env YOLOSOD_SWIN_FUSED), 0 forces the decomposed GEMM path for every shape. */
 void yolosod_debug_set_swin_fused(int on);
+/* Test hook: 1 routes C = 64 / 2-head / 7x7 SwinBlocks through the opt-in kernel that runs the projection / MLP / pw
+ * GEMMs as three-term bf16 splits on the bf16 matrix cores at fp32 accuracy (csrc/swin_x3.hip; also env
+ * YOLOSOD_SWIN_X3=1), 0 (default) keeps the fp32-MFMA fused kernel. */
+void yolosod_debug_set_swin_x3(int on);
 
 /* ---------------------------------------------------------------------------------------------------------------
  * bf16 model config (BASELINE configs[4]): `model.to(torch.bfloat16)` after fuse() - AutoBackend's fp16

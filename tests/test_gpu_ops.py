@@ -62,6 +62,26 @@ def test_swin_decomposed_path_matches_reference_fixture(name, cuda):
     assert ok, f"{name}: vs fp64 oracle max abs err {err:.3g} (ratio {ratio:.2f})"
 
 
+@pytest.mark.parametrize("name", [n for n in recipes.OPS if n.startswith("swin_c64")])
+def test_swin_bf16x3_path_matches_reference_fixture(name, cuda):
+    """The opt-in C = 64 Swin kernel that runs its projection / MLP / pw GEMMs as three-term bf16 splits on the bf16
+    matrix cores (csrc/swin_x3.hip): fp32 accuracy, held to the same tolerances as the fp32 kernels."""
+    lib = _hip.load_library()
+    z = golden(f"ops_{name}")
+    m, _ = build_fixture_module(name)
+    x = torch.from_numpy(z["x"])
+    lib.yolosod_debug_set_swin_x3(1)
+    try:
+        with torch.inference_mode():
+            y = m.to(cuda)(x.to(cuda)).cpu()
+    finally:
+        lib.yolosod_debug_set_swin_x3(0)
+    ok, err, _ = tol_close(y, torch.from_numpy(z["y"]), ATOL, 0.0)
+    assert ok, f"{name}: max abs err vs reference {err:.3g}"
+    ok, err, ratio = tol_close(y, _oracle64(name, x), 5e-5, 1e-4)
+    assert ok, f"{name}: vs fp64 oracle max abs err {err:.3g} (ratio {ratio:.2f})"
+
+
 # real-model shapes (one image; the batch dimension is exercised by the model tests)
 REAL = {
     "se_L1": ("SE_Block", (64,), (1, 32, 320, 320)),

@@ -504,6 +504,18 @@ int yolosod_swin_wide_launch(const float* x, float* y, int B, int C, int H, int 
                              const float* mlp2_b, const float* pw_w, const float* bn_scale, const float* bn_shift,
                              hipStream_t st);
 
+bool yolosod_swin_x3_ok(int C, int num_heads, int wh, int ww, int mlp_hidden);
+size_t yolosod_swin_x3_workspace(int C, int mlp_hidden);
+int yolosod_swin_x3_launch(const float* x, float* y, int B, int C, int H, int W, int num_heads, int wh, int ww,
+                           int nWx, int nWin,
+                           const float* dw_w, const float* ln1_w, const float* ln1_b, float ln1_eps,
+                           const float* in_proj_w, const float* in_proj_b, const float* out_proj_w,
+                           const float* out_proj_b, const float* ln2_w, const float* ln2_b, float ln2_eps,
+                           const float* mlp1_w, const float* mlp1_b, int mlp_hidden, const float* mlp2_w,
+                           const float* mlp2_b, const float* pw_w, const float* bn_w, const float* bn_b,
+                           const float* bn_mean, const float* bn_var, float bn_eps, void* workspace,
+                           size_t workspace_bytes, hipStream_t st);
+
 static int g_swin_fused = -1;  // -1: from YOLOSOD_SWIN_FUSED (default on)
 
 static bool swin_fused_enabled() {
@@ -602,6 +614,10 @@ YS_EXPORT size_t yolosod_swin_workspace_v2(int B, int C, int H, int W, int num_h
   if (swin_fused_ok(C, num_heads, g.wh, g.ww, mlp_hidden)) {
     Sizer s;
     s.take<float>((size_t)C * 2);
+    if (yolosod_swin_x3_ok(C, num_heads, g.wh, g.ww, mlp_hidden)) {
+      const size_t x3 = yolosod_swin_x3_workspace(C, mlp_hidden);
+      return x3 > s.off ? x3 : s.off;
+    }
     return s.off;
   }
   return yolosod_swin_workspace(B, C, H, W, window, mlp_hidden);
@@ -625,6 +641,13 @@ YS_EXPORT int yolosod_swin_forward(const float* x, float* y, int B, int C, int H
   SwinGeom g = swin_geom(B, H, W, window);
   YS_CHECK_ARG(g.L <= 320, "swin: window of %d tokens unsupported", g.L);
   if (swin_fused_ok(C, num_heads, g.wh, g.ww, mlp_hidden)) {
+    // C = 64: projection / MLP / pw GEMMs on bf16 matrix cores at fp32 accuracy (swin_x3.hip)
+    const int rx = yolosod_swin_x3_launch(x, y, B, C, H, W, num_heads, g.wh, g.ww, g.nWx, g.nWin, dw_w, ln1_w, ln1_b, ln1_eps,
+                                          in_proj_w, in_proj_b, out_proj_w, out_proj_b, ln2_w, ln2_b, ln2_eps,
+                                          mlp1_w, mlp1_b, mlp_hidden, mlp2_w, mlp2_b, pw_w, bn_w, bn_b, bn_mean,
+                                          bn_var, bn_eps, workspace, workspace_bytes, st);
+    if (rx < 0) return -1;
+    if (rx == 1) return 0;
     Carver cf(workspace, workspace_bytes);
     float* fold = cf.take<float>((size_t)C * 2);
     YS_CHECK_ARG(fold, "swin: workspace too small (%zu)", workspace_bytes);
