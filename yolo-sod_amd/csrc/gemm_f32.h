@@ -56,6 +56,7 @@ struct GemmArgs {
   Epi epi;
   int nimg;               // set by launch_gemm: > 0 = batch folded into N (N-contiguous B, nimg columns per image)
   int nmajor;             // set by launch_gemm: tiles in column-major (n-major) order
+  int bfold;              // set by launch_gemm: > 0 = batch folded into the tile index (bfold images, n-major inside)
 };
 
 // Per-row LayerNorm statistics (mean, 1/sqrt(var + eps)) of a K-contiguous [rows][K] matrix: one wave per row,
@@ -140,9 +141,15 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
   float* s_rstd = s_mean + BM;
 
   // XCD-aware tile order (gridDim.x = 8 * ceil(tiles / 8)); see header comment
-  const int tpx = (g.tiles + 7) >> 3;
-  const int t = (blockIdx.x & 7) * tpx + (blockIdx.x >> 3);
-  if (t >= g.tiles) return;
+  const int ntiles = g.bfold ? g.tiles * g.bfold : g.tiles;
+  const int tpx = (ntiles + 7) >> 3;
+  int t = (blockIdx.x & 7) * tpx + (blockIdx.x >> 3);
+  if (t >= ntiles) return;
+  int bz = blockIdx.z;
+  if (g.bfold) {  // batch in the tile index: an image's tiles are contiguous, so they share one XCD's L2
+    bz = t / g.tiles;
+    t -= bz * g.tiles;
+  }
   int m0, n0;
   if (g.nmajor) {  // all M tiles of an N column on one XCD: an N-contiguous B (NCHW activations) is read once
     const int tiles_m = g.tiles / g.tiles_n;
@@ -155,7 +162,6 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
-  const int bz = blockIdx.z;
   const float* A = g.A + (long)bz * g.a_bs;
   const float* B = g.B + (long)bz * g.b_bs;
   const int M = g.M, N = g.N, K = g.K;
@@ -401,11 +407,21 @@ static inline int launch_gemm(const GemmArgs& g0, int batch, bool b_kc, hipStrea
   // the tiles run across image boundaries instead of padding every image's last tile column
   g.nimg = 0;
   g.nmajor = 0;
+  g.bfold = 0;
   if (!b_kc && batch > 1 && g.a_bs == 0 && g.N % 128 != 0 && g.N % 4 == 0 && g.epi.vec && e.bias_mode != 2 && e.bn_mode != 2 &&
       g.ldb % 4 == 0 && g.b_bs % 4 == 0 && (long)g.N * batch < (1L << 31) && !getenv("YOLOSOD_GEMM_NOFOLD")) {
     g.nimg = g.N;
     g.nmajor = 1;
     g.N *= batch;
+    batch = 1;
+  }
+  // K-contiguous per-image B with a shared A (the A2 output GEMM: B = the image's tokens): the batch goes into the
+  // tile index and the tiles run n-major, so the M tiles reading one B column block sit on one XCD (B read once)
+  const int batch0 = batch;
+  if (b_kc && batch > 1 && g.a_bs == 0 && (long)batch * ((g.M + 63) / 64) * ((g.N + 63) / 64) < (1L << 30) &&
+      !getenv("YOLOSOD_GEMM_NOFOLD")) {
+    g.bfold = batch;
+    g.nmajor = 1;
     batch = 1;
   }
   // N tiles of 64 when N is not a multiple of 128 (e.g. 3C = 192) or small; 128 otherwise
@@ -415,7 +431,8 @@ static inline int launch_gemm(const GemmArgs& g0, int batch, bool b_kc, hipStrea
     constexpr int bm = WM_ * MI_ * 32, bn = WN_ * NI_ * 32;                                                    \
     g.tiles_n = (g.N + bn - 1) / bn;                                                                           \
     g.tiles = g.tiles_n * ((g.M + bm - 1) / bm);                                                               \
-    dim3 grid((unsigned)(8 * ((g.tiles + 7) / 8)), 1, batch);                                                  \
+    const long nt_ = (long)g.tiles * (g.bfold ? g.bfold : 1);                                                  \
+    dim3 grid((unsigned)(8 * ((nt_ + 7) / 8)), 1, batch);                                                      \
     if (b_kc) {                                                                                                \
       if (ln) hipLaunchKernelGGL((gemm_f32_kernel<WM_, WN_, MI_, NI_, true, true>), grid, dim3(256), 0, st, g); \
       else hipLaunchKernelGGL((gemm_f32_kernel<WM_, WN_, MI_, NI_, true, false>), grid, dim3(256), 0, st, g);  \
@@ -431,7 +448,7 @@ static inline int launch_gemm(const GemmArgs& g0, int batch, bool b_kc, hipStrea
   }();
   // 128x64 tiles also when 128x128 would leave CUs idle (fewer tiles than CUs) or waste > 10% of a tile column
   // on a ragged N (e.g. N = H*W = 400): more, smaller workgroups for the small A2 / MHA GEMMs
-  const long t128 = (long)((g.M + 127) / 128) * ((g.N + 127) / 128) * batch;
+  const long t128 = (long)((g.M + 127) / 128) * ((g.N + 127) / 128) * batch0;
   const bool ragged = (long)((g.N + 127) / 128) * 128 - g.N > g.N / 10;
   const bool small = !narrow && g.M > 64 && (t128 < 256 || ragged);
   if (forced == 1 || (!forced && (narrow || small))) YS_GEMM_LAUNCH(4, 1, 1, 2);
