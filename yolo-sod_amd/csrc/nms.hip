@@ -6,9 +6,10 @@
 //
 // Design (no host sync; the per-image candidate count lives on the device):
 //   nms_prep    one thread per anchor: xywh -> xyxy (optionally in place, as the reference mutates its input),
-//               candidate class mask (score > conf, class filter, best class or multi-label).
-//   nms_count / nms_scan / nms_scatter  order-preserving compaction of the (anchor, class) candidates (= the
-//               reference's row order) over the whole GPU: per-256-anchor counts, per-image offsets, scatter of
+//               candidate class mask (score > conf, class filter, best class or multi-label), and the candidate
+//               count of each 256-anchor block.
+//   nms_scatter order-preserving compaction of the (anchor, class) candidates (= the reference's row order) over
+//               the whole GPU: each block sums its image's preceding block counts for its offset and scatters
 //               (~score bits, anchor*nc+class).
 //   nms_select  one 512-thread workgroup per image: the score order of the first <= KCAP candidates, sorted in
 //               LDS. For n <= KCAP a stable LSD radix sort of all; for n > KCAP a radix *select* first finds the
@@ -68,43 +69,51 @@ struct NmsArgs {
 #define YS_NSTAMP(k) \
   if (g.stamps && threadIdx.x == 0) g.stamps[b * 8 + (k)] = __builtin_amdgcn_s_memtime();
 
+__device__ __forceinline__ int block256_exclusive_scan(int v, int* wsum4, int* total);
+
+// also the candidate count of this 256-anchor block (the ordered compaction's per-block counts)
 __global__ __launch_bounds__(256) void nms_prep_kernel(NmsArgs g) {
+  __shared__ int wsum4[4];
   const int b = blockIdx.y;
   const int a = blockIdx.x * 256 + threadIdx.x;
-  if (a >= g.A) return;
-  float* pb = g.pred + (long)b * (4 + g.nc) * g.A + a;
-  const long As = g.A;
-  const float cx = pb[0], cy = pb[As], w = pb[2 * As], h = pb[3 * As];
-  const float hw = w / 2.0f, hh = h / 2.0f;
-  const float x1 = cx - hw, y1 = cy - hh, x2 = cx + hw, y2 = cy + hh;
-  if (g.in_place) {
-    pb[0] = x1;
-    pb[As] = y1;
-    pb[2 * As] = x2;
-    pb[3 * As] = y2;
-  }
-  g.boxes[(long)b * g.A + a] = make_float4(x1, y1, x2, y2);
   unsigned long long mask = 0ull;
-  float best = -INFINITY;
-  int bj = 0;
-  for (int j = 0; j < g.nc; ++j) {
-    const float s = pb[(4 + j) * As];
-    if (s > best) {  // strict: first maximal index wins (torch max(dim) / amax)
-      best = s;
-      bj = j;
+  if (a < g.A) {
+    float* pb = g.pred + (long)b * (4 + g.nc) * g.A + a;
+    const long As = g.A;
+    const float cx = pb[0], cy = pb[As], w = pb[2 * As], h = pb[3 * As];
+    const float hw = w / 2.0f, hh = h / 2.0f;
+    const float x1 = cx - hw, y1 = cy - hh, x2 = cx + hw, y2 = cy + hh;
+    if (g.in_place) {
+      pb[0] = x1;
+      pb[As] = y1;
+      pb[2 * As] = x2;
+      pb[3 * As] = y2;
     }
-    if (g.multi_label && s > g.conf) mask |= 1ull << j;
-  }
-  if (!g.multi_label) mask = (best > g.conf) ? (1ull << bj) : 0ull;
-  if (mask && g.classes) {
-    unsigned long long allow = 0ull;
-    for (int k = 0; k < g.n_classes; ++k) {
-      const int c = g.classes[k];
-      if (c >= 0 && c < 64) allow |= 1ull << c;
+    g.boxes[(long)b * g.A + a] = make_float4(x1, y1, x2, y2);
+    float best = -INFINITY;
+    int bj = 0;
+    for (int j = 0; j < g.nc; ++j) {
+      const float s = pb[(4 + j) * As];
+      if (s > best) {  // strict: first maximal index wins (torch max(dim) / amax)
+        best = s;
+        bj = j;
+      }
+      if (g.multi_label && s > g.conf) mask |= 1ull << j;
     }
-    mask &= allow;
+    if (!g.multi_label) mask = (best > g.conf) ? (1ull << bj) : 0ull;
+    if (mask && g.classes) {
+      unsigned long long allow = 0ull;
+      for (int k = 0; k < g.n_classes; ++k) {
+        const int c = g.classes[k];
+        if (c >= 0 && c < 64) allow |= 1ull << c;
+      }
+      mask &= allow;
+    }
+    g.amask[(long)b * g.A + a] = mask;
   }
-  g.amask[(long)b * g.A + a] = mask;
+  int total;
+  (void)block256_exclusive_scan(__popcll(mask), wsum4, &total);
+  if (threadIdx.x == 0) g.blkcnt[(long)b * gridDim.x + blockIdx.x] = total;
 }
 
 // block-wide (256 threads) exclusive scan; returns the exclusive prefix, *total gets the block sum
@@ -125,54 +134,25 @@ __device__ __forceinline__ int block256_exclusive_scan(int v, int* wsum4, int* t
   return base + inc - v;
 }
 
-// candidates per 256-anchor block (the compaction runs over the whole GPU: count, scan, scatter)
-__global__ __launch_bounds__(256) void nms_count_kernel(NmsArgs g) {
-  __shared__ int wsum4[4];
-  const int b = blockIdx.y;
-  const long a = (long)blockIdx.x * 256 + threadIdx.x;
-  const int c = (a < g.A) ? __popcll(g.amask[(long)b * g.A + a]) : 0;
-  int total;
-  (void)block256_exclusive_scan(c, wsum4, &total);
-  if (threadIdx.x == 0) g.blkcnt[(long)b * gridDim.x + blockIdx.x] = total;
-}
-
-// per image: exclusive scan of the block counts -> offsets; n, neff -> meta
-__global__ __launch_bounds__(256) void nms_scan_kernel(NmsArgs g, int nblk_a) {
-  __shared__ int wsum4[4];
-  __shared__ int carry;
-  const int b = blockIdx.x;
-  int* bc = g.blkcnt + (long)b * nblk_a;
-  if (threadIdx.x == 0) carry = 0;
-  __syncthreads();
-  for (int t0 = 0; t0 < nblk_a; t0 += 256) {
-    const int i = t0 + threadIdx.x;
-    const int v = (i < nblk_a) ? bc[i] : 0;
-    int total;
-    const int ex = block256_exclusive_scan(v, wsum4, &total);
-    const int base = carry;
-    if (i < nblk_a) bc[i] = base + ex;
-    __syncthreads();
-    if (threadIdx.x == 0) carry = base + total;
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    const int n = carry;
-    g.meta[4 * b + 0] = n;
-    g.meta[4 * b + 1] = (n > g.max_nms) ? g.max_nms : n;
-  }
-}
-
-// ordered scatter: entry (anchor, class) in (anchor, class) order = the reference's row order
+// ordered scatter: entry (anchor, class) in (anchor, class) order = the reference's row order; each block sums its
+// image's preceding block counts itself (no separate scan launch)
 __global__ __launch_bounds__(256) void nms_scatter_kernel(NmsArgs g) {
   __shared__ int wsum4[4];
   const int b = blockIdx.y;
   const long A = g.A;
   const long a = (long)blockIdx.x * 256 + threadIdx.x;
   const unsigned long long m = (a < A) ? g.amask[(long)b * A + a] : 0ull;
+  // this block's output offset: the candidates of the image's preceding blocks (their counts from nms_prep)
+  const int* bc = g.blkcnt + (long)b * gridDim.x;
+  int before = 0;
+  for (int i = threadIdx.x; i < (int)blockIdx.x; i += 256) before += bc[i];
+  int base;
+  (void)block256_exclusive_scan(before, wsum4, &base);
+  __syncthreads();  // wsum4 is reused by the scan below
   int total;
   const int ex = block256_exclusive_scan(__popcll(m), wsum4, &total);
   if (!m) return;
-  int k = g.blkcnt[(long)b * gridDim.x + blockIdx.x] + ex;
+  int k = base + ex;
   const float* pb = g.pred + (long)b * (4 + g.nc) * A + a;
   unsigned* kA = g.keyA + (long)b * g.cap;
   unsigned* pA = g.posA + (long)b * g.cap;
@@ -384,8 +364,15 @@ __global__ __launch_bounds__(NMS_T) void nms_select_kernel(NmsArgs g) {
   unsigned* kB = g.keyB + (long)b * g.cap;
   unsigned* pB = g.posB + (long)b * g.cap;
 
-  // (a) the ordered compaction ran over the whole GPU (nms_count / nms_scan / nms_scatter)
-  const int n = g.meta[4 * b + 0];
+  // (a) the ordered compaction ran over the whole GPU (nms_prep counts, nms_scatter); n = the image's candidates
+  __shared__ int nsum[NMS_W + 1];
+  int n;
+  {
+    const int nblk = (int)((A + 255) / 256);
+    int v = 0;
+    for (int i = tid; i < nblk; i += NMS_T) v += g.blkcnt[(long)b * nblk + i];
+    (void)block_exclusive_scan(v, nsum, &n);
+  }
   YS_NSTAMP(1)
   const int neff = (n > g.max_nms) ? g.max_nms : n;
 
@@ -457,6 +444,8 @@ __global__ __launch_bounds__(NMS_T) void nms_select_kernel(NmsArgs g) {
   }
   if (tid == 0) {
     int* mt = g.meta + 4 * b;
+    mt[0] = n;
+    mt[1] = neff;
     mt[2] = K;
     mt[3] = (int)T;
     if (g.stamps) g.stamps[b * 8 + 6] = (unsigned long long)n;
@@ -845,10 +834,8 @@ YS_EXPORT int yolosod_nms(float* pred, int B, int nc, int A, float conf_thres, d
   }
   if (A > 0) {
     hipLaunchKernelGGL(nms_prep_kernel, dim3(nblk_a, B), dim3(256), 0, st, g);
-    hipLaunchKernelGGL(nms_count_kernel, dim3(nblk_a, B), dim3(256), 0, st, g);
+    hipLaunchKernelGGL(nms_scatter_kernel, dim3(nblk_a, B), dim3(256), 0, st, g);
   }
-  hipLaunchKernelGGL(nms_scan_kernel, dim3(B), dim3(256), 0, st, g, nblk_a);
-  if (A > 0) hipLaunchKernelGGL(nms_scatter_kernel, dim3(nblk_a, B), dim3(256), 0, st, g);
   hipLaunchKernelGGL(nms_select_kernel, dim3(B), dim3(NMS_T), 0, st, g);
   hipLaunchKernelGGL(nms_mask_kernel, dim3(KW, B), dim3(256), 0, st, g);
   if (big)
