@@ -227,14 +227,26 @@ __global__ __launch_bounds__(256, C3 > 64 ? 2 : 3) void detect_head_lds_kernel(H
   {
     const float* wb = d.wb[l];
     const float* wc = d.wc[l];
-    for (int e = tid; e < C2 * 64; e += 256) {
+    // every load first, then the LDS stores (a load-store loop waits for each load in turn)
+    static_assert((C2 * 64) % 256 == 0 && (C3 * 16) % 256 == 0, "weight image sizes");
+    constexpr int NB = C2 * 64 / 256, NCL = C3 * 16 / 256;
+    float vb[NB], vc[NCL];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int e = tid + 256 * i;
       const int t = e & 3, jj = (e >> 2) & 15, gg = (e >> 6) & 3, q = e >> 8;
-      wlb[e] = wb[(16 * t + jj) * C2 + 4 * q + gg];
+      vb[i] = wb[(16 * t + jj) * C2 + 4 * q + gg];
     }
-    for (int e = tid; e < C3 * 16; e += 256) {
+#pragma unroll
+    for (int i = 0; i < NCL; ++i) {
+      const int e = tid + 256 * i;
       const int u = e & 3, jj = (e >> 2) & 15, gg = (e >> 6) & 3, qq = e >> 8;
-      wlc[e] = (jj < nc) ? wc[jj * C3 + 4 * (4 * qq + u) + gg] : 0.f;
+      vc[i] = (jj < nc) ? wc[(jj < nc ? jj : 0) * C3 + 4 * (4 * qq + u) + gg] : 0.f;
     }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) wlb[tid + 256 * i] = vb[i];
+#pragma unroll
+    for (int i = 0; i < NCL; ++i) wlc[tid + 256 * i] = vc[i];
   }
   __syncthreads();
   const int HW = d.hw[l];

@@ -90,15 +90,15 @@ __device__ __forceinline__ void load_bfrag(const bf16_t* __restrict__ Wg, BFrag<
       f.v[j][s] = *reinterpret_cast<const bf16x8_t*>(Wg + (long)((wid + 4 * j) * 16 + l15) * K + 32 * s + 8 * g);
 }
 
-// acc[rb][j] = A[rows rb*16 .. +15][0..K) . W^T for the wave's column blocks (A: LDS bf16, row stride lda)
-template <int K, int NJ>
+// acc[rb][j] += A[rows rb*16 .. +15][0..K) . W^T for the wave's column blocks (A: LDS bf16, row stride lda; the
+// caller initialises acc, e.g. with the bias). Blocks j < NTR are transposed tiles - the weight fragment is the MFMA
+// A operand, so lane (g, l15) holds out[token rb*16 + l15][n = cb*16 + 4g .. +3]: four consecutive columns of one
+// row, one 8-byte LDS store; blocks j >= NTR hold out[token rb*16 + 4g + r][n = cb*16 + l15] (four tokens of one
+// column: the layout of V^T).
+template <int K, int NJ, int NTR>
 __device__ __forceinline__ void gemm_rows(const bf16_t* As, int lda, const BFrag<K, NJ>& f, f32x4 (&acc)[4][NJ],
                                           int lane) {
   const int l15 = lane & 15, g = lane >> 4;
-#pragma unroll
-  for (int rb = 0; rb < 4; ++rb)
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[rb][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int s = 0; s < K / 32; ++s) {
     bf16x8_t a[4];
@@ -108,8 +108,16 @@ __device__ __forceinline__ void gemm_rows(const bf16_t* As, int lda, const BFrag
 #pragma unroll
     for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) acc[rb][j] = mfma_b(a[rb], f.v[j][s], acc[rb][j]);
+      for (int j = 0; j < NJ; ++j)
+        acc[rb][j] = j < NTR ? mfma_b(f.v[j][s], a[rb], acc[rb][j]) : mfma_b(a[rb], f.v[j][s], acc[rb][j]);
   }
+}
+
+// 4 consecutive bf16 <-> fp32 (8 bytes)
+__device__ __forceinline__ uint2 pack4(f32x4 v) { return make_uint2(pack_bf16x2(v.x, v.y), pack_bf16x2(v.z, v.w)); }
+__device__ __forceinline__ f32x4 unpack4(uint2 u) {
+  return f32x4{__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+               __uint_as_float(u.y & 0xffff0000u)};
 }
 
 // LayerNorm of rows [0, 49) of S (bf16, stride ST) into U (bf16, stride ST): 4 lanes per row (a DPP quad), each
@@ -198,12 +206,22 @@ __global__ __launch_bounds__(256, 2) void swin_fused_bf16_kernel(SwinBArgs p) {
 
   // parameters -> LDS, depthwise taps -> registers, halo -> registers; then the QKV weight prefetch (last in the
   // vmcnt queue, so the halo wait does not wait for it)
-  for (int e = tid; e < NPAR; e += 256) {
-    const int w = e / C, c = e - w * C;
-    const float* src = w < 3 ? p.bin + w * C : w == 3 ? p.bo : w < 6 ? p.b1 + (w - 4) * C : w == 6 ? p.b2
-                     : w == 7 ? p.bn_scale : w == 8 ? p.bn_shift : w == 9 ? p.ln1_w : w == 10 ? p.ln1_b
-                     : w == 11 ? p.ln2_w : p.ln2_b;
-    par[e] = src[c];
+  // all loads first, then the LDS stores (a load-store loop would wait for each load in turn)
+  {
+    constexpr int NPT = (NPAR + 255) / 256;
+    float pv[NPT];
+#pragma unroll
+    for (int i = 0; i < NPT; ++i) {
+      const int e = tid + 256 * i;
+      const int w = e / C, c = e - w * C;
+      const float* src = w < 3 ? p.bin + w * C : w == 3 ? p.bo : w < 6 ? p.b1 + (w - 4) * C : w == 6 ? p.b2
+                       : w == 7 ? p.bn_scale : w == 8 ? p.bn_shift : w == 9 ? p.ln1_w : w == 10 ? p.ln1_b
+                       : w == 11 ? p.ln2_w : p.ln2_b;
+      pv[i] = e < NPAR ? src[c] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < NPT; ++i)
+      if (tid + 256 * i < NPAR) par[tid + 256 * i] = pv[i];
   }
   const int dc = tid % C;
   float k[9];
@@ -275,29 +293,34 @@ __global__ __launch_bounds__(256, 2) void swin_fused_bf16_kernel(SwinBArgs p) {
   constexpr int NJ_O = C / 64;
   BFrag<C, NJ_O> f_o;  // out-proj weights: in flight during the QKV epilogue and attention
   {
+    constexpr int NTR = 2 * C / 64;  // Q | K column blocks: transposed tiles; V blocks: V^T layout
     f32x4 acc[4][NJ_QKV];
-    gemm_rows<C, NJ_QKV>(U, ST, f_qkv, acc, lane);
+#pragma unroll
+    for (int j = 0; j < NJ_QKV; ++j) {
+      const f32x4 b = j < NTR ? *reinterpret_cast<const f32x4*>(par + P_BIN + (wid + 4 * j) * 16 + 4 * g)
+                              : f32x4{1.f, 1.f, 1.f, 1.f} * par[P_BIN + (wid + 4 * j) * 16 + l15];
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) acc[rb][j] = b;
+    }
+    gemm_rows<C, NJ_QKV, NTR>(U, ST, f_qkv, acc, lane);
     load_bfrag(p.wo, f_o, wid, lane);
 #pragma unroll
     for (int j = 0; j < NJ_QKV; ++j) {
-      const int n = (wid + 4 * j) * 16 + l15;
-      const float bias = par[P_BIN + n];
-      if (n < 2 * C) {
+      if (j < NTR) {
+        const int n4 = (wid + 4 * j) * 16 + 4 * g;
 #pragma unroll
-        for (int rb = 0; rb < 4; ++rb)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int row = rb * 16 + 4 * g + r;
-            if (row < SB_NR) QK[row * SQK + n] = f2bf(acc[rb][j][r] + bias);
-          }
+        for (int rb = 0; rb < 4; ++rb) {
+          const int row = rb * 16 + l15;
+          if (row < SB_NR) *reinterpret_cast<uint2*>(QK + row * SQK + n4) = pack4(acc[rb][j]);
+        }
       } else {
-        const int d = n - 2 * C;
+        const int d = (wid + 4 * j) * 16 + l15 - 2 * C;
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb) {
           const int row0 = rb * 16 + 4 * g;
           float v[4];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = (row0 + r < SB_NR) ? acc[rb][j][r] + bias : 0.f;
+          for (int r = 0; r < 4; ++r) v[r] = (row0 + r < SB_NR) ? acc[rb][j][r] : 0.f;
           *reinterpret_cast<uint2*>(Vt + d * SVT + row0) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
         }
       }
@@ -384,18 +407,24 @@ __global__ __launch_bounds__(256, 2) void swin_fused_bf16_kernel(SwinBArgs p) {
   load_bfrag(p.w1, f_1, wid, lane);
   {
     f32x4 acc[4][NJ_O];
-    gemm_rows<C, NJ_O>(U, ST, f_o, acc, lane);
 #pragma unroll
     for (int j = 0; j < NJ_O; ++j) {
-      const int n = (wid + 4 * j) * 16 + l15;
-      const float bias = par[P_BO + n];
+      const f32x4 b = *reinterpret_cast<const f32x4*>(par + P_BO + (wid + 4 * j) * 16 + 4 * g);
 #pragma unroll
-      for (int rb = 0; rb < 4; ++rb)
+      for (int rb = 0; rb < 4; ++rb) acc[rb][j] = b;
+    }
+    gemm_rows<C, NJ_O, NJ_O>(U, ST, f_o, acc, lane);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = rb * 16 + 4 * g + r;
-          if (row < SB_NR) T[row * ST + n] = f2bf(bf2f(T[row * ST + n]) + (acc[rb][j][r] + bias));
+    for (int j = 0; j < NJ_O; ++j) {
+      const int n4 = (wid + 4 * j) * 16 + 4 * g;
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) {
+        const int row = rb * 16 + l15;
+        if (row < SB_NR) {
+          uint2* tp = reinterpret_cast<uint2*>(T + row * ST + n4);
+          *tp = pack4(unpack4(*tp) + acc[rb][j]);
         }
+      }
     }
   }
   __syncthreads();
@@ -411,20 +440,24 @@ __global__ __launch_bounds__(256, 2) void swin_fused_bf16_kernel(SwinBArgs p) {
   load_bfrag(p.w2, f_2, wid, lane);
   {
     f32x4 acc[4][NJ_1];
-    gemm_rows<C, NJ_1>(U, ST, f_1, acc, lane);
 #pragma unroll
     for (int j = 0; j < NJ_1; ++j) {
-      const int n = (wid + 4 * j) * 16 + l15;
-      const float bias = par[P_B1 + n];
+      const f32x4 b = *reinterpret_cast<const f32x4*>(par + P_B1 + (wid + 4 * j) * 16 + 4 * g);
 #pragma unroll
-      for (int rb = 0; rb < 4; ++rb)
+      for (int rb = 0; rb < 4; ++rb) acc[rb][j] = b;
+    }
+    gemm_rows<C, NJ_1, NJ_1>(U, ST, f_1, acc, lane);
 #pragma unroll
-        for (int r = 0; r < 4; r += 2) {
-          const int row = rb * 16 + 4 * g + r;
-          const f32x2 hv = gelu2_bf16_(f32x2{acc[rb][j][r], acc[rb][j][r + 1]} + bias);
-          if (row < SB_NR) Hd[row * SQK + n] = f2bf(hv.x);
-          if (row + 1 < SB_NR) Hd[(row + 1) * SQK + n] = f2bf(hv.y);
-        }
+    for (int j = 0; j < NJ_1; ++j) {
+      const int n4 = (wid + 4 * j) * 16 + 4 * g;
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) {
+        const int row = rb * 16 + l15;
+        const f32x2 lo = gelu2_bf16_(f32x2{acc[rb][j][0], acc[rb][j][1]});
+        const f32x2 hi = gelu2_bf16_(f32x2{acc[rb][j][2], acc[rb][j][3]});
+        if (row < SB_NR)
+          *reinterpret_cast<uint2*>(Hd + row * SQK + n4) = make_uint2(pack_bf16x2(lo.x, lo.y), pack_bf16x2(hi.x, hi.y));
+      }
     }
   }
   __syncthreads();
@@ -438,13 +471,26 @@ __global__ __launch_bounds__(256, 2) void swin_fused_bf16_kernel(SwinBArgs p) {
 #pragma unroll
     for (int s = 0; s < C / 32; ++s)
       wa[j][s] = *reinterpret_cast<const bf16x8_t*>(p.wpw + (long)((wid + 4 * j) * 16 + l15) * C + 32 * s + 8 * g);
-  long pix[4];  // per token block: pixel offset of token tb*16 + l15 in the image plane, or -1
+  // residual x and the y stores: buffer ops on per-image descriptors; a lane's voffset is fixed (channel row 4g of
+  // block wid, its token) and out-of-window / cropped tokens get an out-of-range voffset (loads return 0, stores are
+  // dropped), so there is no per-element branch (a branch per load serialised them behind s_waitcnt vmcnt(0))
+  constexpr unsigned OOB = 0x80000000u;
+  const int HWi = (int)HW;
+  auto rsrc_of = [&](const bf16_t* base) {
+    const unsigned long long a = (unsigned long long)base;
+    return __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(a >> 32)) << 32) |
+                (unsigned)__builtin_amdgcn_readfirstlane((unsigned)a)),
+        (short)0, __builtin_amdgcn_readfirstlane(C * HWi * 2), 0x00020000);
+  };
+  const __amdgpu_buffer_rsrc_t rxr = rsrc_of(xb);
+  unsigned vtok[4];
 #pragma unroll
   for (int tb = 0; tb < 4; ++tb) {
     const int tok = tb * 16 + l15;
     const int iy = tok / 7, ix = tok - (tok / 7) * 7;
     const int hh = wy * 7 + iy, ww = wx * 7 + ix;
-    pix[tb] = (tok < SB_NR && hh < H && ww < W) ? (long)hh * W + ww : -1;
+    vtok[tb] = (tok < SB_NR && hh < H && ww < W) ? (unsigned)(((wid * 16 + 4 * g) * HWi + hh * W + ww) * 2) : OOB;
   }
   bf16_t xres[NCB_PW][4][4];
 #pragma unroll
@@ -453,28 +499,34 @@ __global__ __launch_bounds__(256, 2) void swin_fused_bf16_kernel(SwinBArgs p) {
     for (int tb = 0; tb < 4; ++tb)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        xres[j][tb][r] = pix[tb] >= 0 ? xb[(long)((wid + 4 * j) * 16 + 4 * g + r) * HW + pix[tb]] : (bf16_t)0;
+        xres[j][tb][r] = __builtin_amdgcn_raw_buffer_load_b16(rxr, vtok[tb], (64 * j + r) * HWi * 2, 0);
   {
     f32x4 acc[4][NJ_2];
-    gemm_rows<HID, NJ_2>(Hd, SQK, f_2, acc, lane);
 #pragma unroll
     for (int j = 0; j < NJ_2; ++j) {
-      const int n = (wid + 4 * j) * 16 + l15;
-      const float bias = par[P_B2 + n];
+      const f32x4 b = *reinterpret_cast<const f32x4*>(par + P_B2 + (wid + 4 * j) * 16 + 4 * g);
 #pragma unroll
-      for (int rb = 0; rb < 4; ++rb)
+      for (int rb = 0; rb < 4; ++rb) acc[rb][j] = b;
+    }
+    gemm_rows<HID, NJ_2, NJ_2>(Hd, SQK, f_2, acc, lane);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = rb * 16 + 4 * g + r;
-          if (row < SB_NR) T[row * ST + n] = f2bf(bf2f(T[row * ST + n]) + (acc[rb][j][r] + bias));
+    for (int j = 0; j < NJ_2; ++j) {
+      const int n4 = (wid + 4 * j) * 16 + 4 * g;
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) {
+        const int row = rb * 16 + l15;
+        if (row < SB_NR) {
+          uint2* tp = reinterpret_cast<uint2*>(T + row * ST + n4);
+          *tp = pack4(unpack4(*tp) + acc[rb][j]);
         }
+      }
     }
   }
   __syncthreads();
 
   // ---- stage 8: Y^T[c][tok] = Wpw . T^T; y = x + SiLU(BN(Y)) at the window's valid pixels ----
   {
-    bf16_t* yb = p.y + (long)img * C * HW;
+    const __amdgpu_buffer_rsrc_t ryr = rsrc_of(p.y + (long)img * C * HW);
 #pragma unroll
     for (int j = 0; j < NCB_PW; ++j) {
       const int cb = wid + 4 * j;
@@ -489,15 +541,14 @@ __global__ __launch_bounds__(256, 2) void swin_fused_bf16_kernel(SwinBArgs p) {
                            acc[tb]);
       // lane holds Y^T[c = cb*16 + 4g + r][tok = tb*16 + l15]
 #pragma unroll
-      for (int tb = 0; tb < 4; ++tb) {
-        if (pix[tb] < 0) continue;
+      for (int tb = 0; tb < 4; ++tb)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int c = cb * 16 + 4 * g + r;
-          yb[(long)c * HW + pix[tb]] =
-              f2bf(bf2f(xres[j][tb][r]) + silu_fast_(acc[tb][r] * par[P_SC + c] + par[P_SH + c]));
+          __builtin_amdgcn_raw_buffer_store_b16(
+              f2bf(bf2f(xres[j][tb][r]) + silu_fast_(acc[tb][r] * par[P_SC + c] + par[P_SH + c])), ryr, vtok[tb],
+              (64 * j + r) * HWi * 2, 0);
         }
-      }
     }
   }
 }

@@ -229,10 +229,19 @@ __global__ __launch_bounds__(NT, 1) void swin_wide_kernel(Args p) {
         hv[hf][i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
                                                   rx, i == NR - 1 ? vlast : voff, (hf * HALF + 6 * i) * HWi * 4, 0));
   }
-  for (int e = tid; e < 4 * C; e += NT) {
-    const int which = e / C, c = e - which * C;
-    const float* src = which == 0 ? p.ln1_w : which == 1 ? p.ln1_b : which == 2 ? p.ln2_w : p.ln2_b;
-    lnp[e] = src[c];
+  {
+    static_assert((4 * C) % NT == 0, "LN parameter staging");
+    constexpr int NPT = 4 * C / NT;
+    float pv[NPT];  // every load first, then the LDS stores
+#pragma unroll
+    for (int i = 0; i < NPT; ++i) {
+      const int e = tid + NT * i;
+      const int which = e / C, c = e - which * C;
+      const float* src = which == 0 ? p.ln1_w : which == 1 ? p.ln1_b : which == 2 ? p.ln2_w : p.ln2_b;
+      pv[i] = src[c];
+    }
+#pragma unroll
+    for (int i = 0; i < NPT; ++i) lnp[tid + NT * i] = pv[i];
   }
 
   // ---- depthwise 3x3 per channel half: halo -> LDS [c][py][HPW], one output row of 7 tokens per item ----
