@@ -204,9 +204,56 @@ __global__ __launch_bounds__(256, 2) void swin_fused_bf16_kernel(SwinBArgs p) {
   const int wy = win / p.nWx, wx = win - (win / p.nWx) * p.nWx;
   const bf16_t* xb = p.x + (long)img * C * HW;
 
-  // parameters -> LDS, depthwise taps -> registers, halo -> registers; then the QKV weight prefetch (last in the
-  // vmcnt queue, so the halo wait does not wait for it)
-  // all loads first, then the LDS stores (a load-store loop would wait for each load in turn)
+  // halo -> registers first, then the parameters (their LDS stores wait for the halo too: one latency, not two),
+  // the depthwise taps and the QKV weight prefetch (last in the vmcnt queue, so the halo wait does not wait for it).
+  // halo [C][9][9] -> LDS fp32 [c][py][px] (stride 81 per channel). Two load layouts (uniform branch on W):
+  //  * W % 8 == 0: 16-byte loads of 8-pixel-aligned chunks - two per (channel, patch row) cover the 9 columns at the
+  //    window's offset within the first chunk (9C/128 loads per lane instead of C/3 two-byte loads); chunks outside
+  //    the image (rows, or the chunk left of column 0 / right of W) get an out-of-range offset and load zeros;
+  //  * otherwise: row slot s = 7*wid + lane/9 < 27 covers (channel 3i + s/9, patch row s%9) at step i, lane%9 the
+  //    column, so a lane's byte offset is fixed across the C/3 steps (the step advances the scalar offset by 3
+  //    planes) and out-of-image lanes get an out-of-range offset that the buffer load returns as 0.
+  float* halo = reinterpret_cast<float*>(sm + QK_OFF);
+  const unsigned long long xa = (unsigned long long)xb;
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(xa >> 32)) << 32) |
+              (unsigned)__builtin_amdgcn_readfirstlane((unsigned)xa)),
+      (short)0, __builtin_amdgcn_readfirstlane((int)(C * HW * 2)), 0x00020000);
+  const bool chunked = (W & 7) == 0;
+  constexpr int NPAIR = 9 * C;                 // (channel, patch row) pairs
+  constexpr int NST = (NPAIR + 127) / 128;      // 128 pairs (256 lanes, 2 chunks each) per step
+  constexpr int NHS = (C + 2) / 3;
+  const int hq = tid >> 1, hch = tid & 1;
+  const int s0 = wx * 7 - 1, a0 = s0 & ~7, hoff = s0 - a0;  // first halo column, its 8-px chunk, offset in it
+  uint4 hc[NST];
+  float hv[NHS];
+  const int hl_r = lane / 9, hl_px = lane - (lane / 9) * 9;
+  const int hslot = 7 * wid + hl_r;  // valid < 27 (lane 63 and slot 27 idle)
+  const int hcs = hslot / 9, hpy = hslot - (hslot / 9) * 9;
+  if (chunked) {
+    const int col = a0 + 8 * hch;
+    const bool colok = col >= 0 && col + 8 <= W;
+#pragma unroll
+    for (int st = 0; st < NST; ++st) {
+      const int pr = st * 128 + hq;
+      const int c = pr / 9, py = pr - (pr / 9) * 9;
+      const int hh = wy * 7 - 1 + py;
+      const bool ok = pr < NPAIR && colok && (unsigned)hh < (unsigned)H;
+      const unsigned v = ok ? (unsigned)(((long)c * HW + (long)hh * W + col) * 2) : 0x80000000u;
+      const auto r = __builtin_amdgcn_raw_buffer_load_b128(rx, v, 0, 0);
+      hc[st] = make_uint4(r[0], r[1], r[2], r[3]);
+    }
+  } else {
+    const int hh = wy * 7 - 1 + hpy, wc = wx * 7 - 1 + hl_px;
+    const bool ok = hl_r < 7 && hslot < 27 && (unsigned)hh < (unsigned)H && (unsigned)wc < (unsigned)W;
+    const unsigned voff = ok ? (unsigned)((hcs * HW + (long)hh * W + wc) * 2) : 0x80000000u;
+#pragma unroll
+    for (int i = 0; i < NHS; ++i) {
+      const unsigned v = (3 * i + hcs < C) ? voff : 0x80000000u;
+      hv[i] = bf2f(__builtin_amdgcn_raw_buffer_load_b16(rx, v, (int)(i * 3 * HW * 2), 0));
+    }
+  }
+  // parameters -> LDS (every load first, then the stores), depthwise taps -> registers
   {
     constexpr int NPT = (NPAR + 255) / 256;
     float pv[NPT];
@@ -227,36 +274,25 @@ __global__ __launch_bounds__(256, 2) void swin_fused_bf16_kernel(SwinBArgs p) {
   float k[9];
 #pragma unroll
   for (int i = 0; i < 9; ++i) k[i] = p.dw[dc * 9 + i];
-  // halo [C][9][9]: row slot s = 7*wid + lane/9 < 27 covers (channel 3i + s/9, patch row s%9) at step i, lane%9 the
-  // column, so a lane's byte offset is fixed across the C/3 steps (the step advances the scalar offset by 3 planes)
-  // and out-of-image lanes get an out-of-range offset that the buffer load returns as 0: no per-load VALU
-  constexpr int NHS = (C + 2) / 3;
-  float hv[NHS];
-  const int hl_r = lane / 9, hl_px = lane - (lane / 9) * 9;
-  const int hslot = 7 * wid + hl_r;  // valid < 27 (lane 63 and slot 27 idle)
-  const int hcs = hslot / 9, hpy = hslot - (hslot / 9) * 9;
-  {
-    const unsigned long long xa = (unsigned long long)xb;
-    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(xa >> 32)) << 32) |
-                (unsigned)__builtin_amdgcn_readfirstlane((unsigned)xa)),
-        (short)0, __builtin_amdgcn_readfirstlane((int)(C * HW * 2)), 0x00020000);
-    const int hh = wy * 7 - 1 + hpy, wc = wx * 7 - 1 + hl_px;
-    const bool ok = hl_r < 7 && hslot < 27 && (unsigned)hh < (unsigned)H && (unsigned)wc < (unsigned)W;
-    const unsigned voff = ok ? (unsigned)((hcs * HW + (long)hh * W + wc) * 2) : 0x80000000u;
-#pragma unroll
-    for (int i = 0; i < NHS; ++i) {
-      const unsigned v = (3 * i + hcs < C) ? voff : 0x80000000u;
-      hv[i] = bf2f(__builtin_amdgcn_raw_buffer_load_b16(rx, v, (int)(i * 3 * HW * 2), 0));
-    }
-  }
   constexpr int NJ_QKV = 3 * C / 64;
   BFrag<C, NJ_QKV> f_qkv;
   load_bfrag(p.win, f_qkv, wid, lane);
 
   // ---- stage 0: halo -> LDS (fp32: conflict-free stride-81 reads below), depthwise conv -> T ----
-  float* halo = reinterpret_cast<float*>(sm + QK_OFF);
-  if (hl_r < 7 && hslot < 27) {
+  if (chunked) {
+    // lane (pair, chunk) holds columns 8*chunk .. +7 of the 16 from a0: halo column j = 8*chunk + e - hoff
+#pragma unroll
+    for (int st = 0; st < NST; ++st) {
+      const int pr = st * 128 + hq;
+      float f[8];
+      unpack8(hc[st], f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int j = 8 * hch + e - hoff;
+        if (pr < NPAIR && j >= 0 && j < 9) halo[pr * 9 + j] = f[e];
+      }
+    }
+  } else if (hl_r < 7 && hslot < 27) {
 #pragma unroll
     for (int i = 0; i < NHS; ++i)
       if (3 * i + hcs < C) halo[(3 * i + hcs) * 81 + hpy * 9 + hl_px] = hv[i];
