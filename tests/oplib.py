@@ -41,7 +41,13 @@ def tol_close(y, ref, atol, rtol):
     """max |y-ref| <= atol + rtol*|ref| elementwise; returns (ok, max_abs_err, worst_ratio)."""
     d = (y.double() - ref.double()).abs()
     lim = atol + rtol * ref.double().abs()
-    return bool((d <= lim).all()), float(d.max()), float((d / lim).max())
+    ok, err, ratio = bool((d <= lim).all()), float(d.max()), float((d / lim).max())
+    log = os.environ.get("YOLOSOD_PARITY_LOG")
+    if log:  # measured margins, for choosing / reviewing tolerances
+        with open(log, "a") as f:
+            f.write(f"{os.environ.get('PYTEST_CURRENT_TEST', '?')}: max|err| {err:.3g} ratio {ratio:.3f} "
+                    f"(atol {atol}, rtol {rtol})\n")
+    return ok, err, ratio
 
 
 # Detect output [B, 4+nc, A]: rows 0-3 are box coordinates in pixels (north-star 1e-3 abs), rows 4.. are class

@@ -42,40 +42,22 @@ def test_op_matches_reference_fixture(name, cuda):
     assert ok, f"{name}: vs fp64 oracle max abs err {err:.3g} (ratio {ratio:.2f})"
 
 
+@pytest.mark.parametrize("x3", [0, 1], ids=["fp32_mfma", "f16x2_mfma"])
 @pytest.mark.parametrize("name", [n for n in recipes.OPS if n.startswith("swin_c64")])
-def test_swin_decomposed_path_matches_reference_fixture(name, cuda):
-    """The decomposed (row-stats + LN-staged GEMM + attention + GEMM) Swin path on the shapes the fused
-    per-window kernel normally takes, against the same reference fixtures."""
+def test_swin_c64_kernels_match_reference_fixture(name, x3, cuda):
+    """Both C = 64 fused Swin kernels: the default one that runs every matrix product as fp16 two-term splits on
+    the fp16 matrix cores (csrc/swin_x3.hip: three exact products per fp32 product) and the exact-fp32-MFMA one
+    (csrc/swin_fused.hip, YOLOSOD_SWIN_X3=0), both held to the fp32 tolerances."""
     lib = _hip.load_library()
     z = golden(f"ops_{name}")
     m, _ = build_fixture_module(name)
     x = torch.from_numpy(z["x"])
-    lib.yolosod_debug_set_swin_fused(0)
+    lib.yolosod_debug_set_swin_x3(x3)
     try:
         with torch.inference_mode():
             y = m.to(cuda)(x.to(cuda)).cpu()
     finally:
-        lib.yolosod_debug_set_swin_fused(1)
-    ok, err, _ = tol_close(y, torch.from_numpy(z["y"]), ATOL, 0.0)
-    assert ok, f"{name}: max abs err vs reference {err:.3g}"
-    ok, err, ratio = tol_close(y, _oracle64(name, x), 5e-5, 1e-4)
-    assert ok, f"{name}: vs fp64 oracle max abs err {err:.3g} (ratio {ratio:.2f})"
-
-
-@pytest.mark.parametrize("name", [n for n in recipes.OPS if n.startswith("swin_c64")])
-def test_swin_bf16x3_path_matches_reference_fixture(name, cuda):
-    """The opt-in C = 64 Swin kernel that runs its projection / MLP / pw GEMMs as three-term bf16 splits on the bf16
-    matrix cores (csrc/swin_x3.hip): fp32 accuracy, held to the same tolerances as the fp32 kernels."""
-    lib = _hip.load_library()
-    z = golden(f"ops_{name}")
-    m, _ = build_fixture_module(name)
-    x = torch.from_numpy(z["x"])
-    lib.yolosod_debug_set_swin_x3(1)
-    try:
-        with torch.inference_mode():
-            y = m.to(cuda)(x.to(cuda)).cpu()
-    finally:
-        lib.yolosod_debug_set_swin_x3(0)
+        lib.yolosod_debug_set_swin_x3(1)
     ok, err, _ = tol_close(y, torch.from_numpy(z["y"]), ATOL, 0.0)
     assert ok, f"{name}: max abs err vs reference {err:.3g}"
     ok, err, ratio = tol_close(y, _oracle64(name, x), 5e-5, 1e-4)
@@ -112,6 +94,24 @@ def test_op_real_shapes_vs_oracle(name, cuda, monkeypatch):
     assert ok, f"{name}: max abs err {err:.3g}"
     ok, err, ratio = tol_close(y, ref, 5e-5, 1e-4)
     assert ok, f"{name}: rel check max abs err {err:.3g} ratio {ratio:.2f}"
+
+
+@pytest.mark.parametrize("name", ["swin_L28", "swin_L28_1280"])
+def test_swin_L28_exact_fp32_kernel_real_shapes(name, cuda, monkeypatch):
+    """The exact-fp32-MFMA C = 64 kernel (swin_fused.hip, YOLOSOD_SWIN_X3=0) at the real shapes (the default
+    fp16-split kernel runs them in test_op_real_shapes_vs_oracle)."""
+    lib = _hip.load_library()
+    monkeypatch.setitem(recipes.OPS, name, REAL[name])
+    m, _ = build_fixture_module(name)
+    x = recipes.make_input(name, REAL[name][2])
+    lib.yolosod_debug_set_swin_x3(0)
+    try:
+        with torch.inference_mode():
+            y = m.to(cuda)(x.to(cuda)).cpu()
+    finally:
+        lib.yolosod_debug_set_swin_x3(1)
+    ok, err, ratio = tol_close(y, _oracle64(name, x), 5e-5, 1e-4)
+    assert ok, f"{name}: max abs err {err:.3g} ratio {ratio:.2f}"
 
 
 @pytest.mark.parametrize("name,shape", [("se_c32_r64", (9, 32, 64, 64)), ("se_c64_r4_odd", (5, 64, 9, 7)),

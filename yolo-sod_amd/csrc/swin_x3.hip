@@ -1,34 +1,29 @@
-// Fused SwinBlock for C = 64 (the P2 instance L28 of the paper model) with the projection / MLP / pw GEMMs on the
-// bf16 matrix cores at fp32 accuracy.
+// Fused SwinBlock for C = 64 (the P2 instance L28 of the paper model) with every matrix product - projections,
+// MLP, pw conv and the attention - on the fp16 matrix cores at fp32 accuracy.
 //
 // Why: on gfx950 the fp32 MFMA (v_mfma_f32_16x16x4_f32, 157 TF/s) shares the SIMD with the VALU - they never
-// co-execute - and the fused fp32 kernel (swin_fused.hip) spends ~58 % of its cycles in it. The bf16 MFMA runs 16x
-// faster per instruction-cycle and beside other waves' VALU. An fp32 operand splits exactly enough into three bf16
-// terms, v = h + m + l (h = bf16(v), m = bf16(v - h), l = bf16(v - h - m), round-to-nearest-even: |v - h - m - l| <=
-// 2^-27 |v|, below fp32's own 2^-24), and a product into the six terms of order >= 2^-16,
-//   a.b ~ ah.bh + ah.bm + am.bh + ah.bl + am.bm + al.bh     (dropped: am.bl, al.bm, al.bl <= ~2^-26 |a.b|),
-// each an exact bf16 x bf16 product accumulated in fp32 by the MFMA - the same accumulation as the fp32 MFMA, with a
-// representation error below fp32 rounding. Six v_mfma_f32_16x16x32_bf16 (16 cycles each) replace eight
-// v_mfma_f32_16x16x4_f32 (32 cycles each) per 16x16x32 block: 2.7x fewer matrix cycles. Weights are split once per
+// co-execute - and the fused fp32 kernel (swin_fused.hip) spends ~58 % of its cycles in it. The fp16 MFMA runs 16x
+// faster per instruction-cycle and beside other waves' VALU. An fp32 operand splits into two fp16 terms, v = h + l
+// (h = fp16(v), l = fp16(v - h), round to nearest even; v - h is exact in fp32), with |v - h - l| <= 2^-22 |v| while
+// l stays a normal fp16 number, and a product into the three terms of order >= 2^-11,
+//   a.b ~ ah.bh + ah.bl + al.bh     (dropped: al.bl <= 2^-22 |a.b|),
+// each an exact fp16 x fp16 product accumulated in fp32 by the MFMA - the same accumulation as the fp32 MFMA, with a
+// representation error of a few fp32 ulps. Three v_mfma_f32_16x16x32_f16 (16 cycles each) replace eight
+// v_mfma_f32_16x16x4_f32 (32 cycles each) per 16x16x32 block: 5.3x fewer matrix cycles. Weights are split once per
 // call by a prep kernel (with the LayerNorm affine terms folded in: W' = W diag(gamma), b' = b + W beta, so the
-// kernel's LayerNorms only normalise); activations are split by their producer (LayerNorm, attention, GELU, the
-// last residual add) when they are written to LDS, three bf16 planes per operand.
-// The attention (S = QK^T, O = PV: ~18 % of the block's FLOPs) stays on exact fp32 MFMA with the S^T-accumulator
-// trick of swin_fused.hip.
+// kernel's LayerNorms only normalise), scaled by 64 (exact) so that the low terms of small weights stay out of
+// fp16's subnormal range; the accumulators start from 64 b and are scaled back by 1/64 (exact) in each epilogue.
+// Activations are split by their producer (LayerNorm, the QKV epilogue, attention, GELU, the last residual add) when
+// they are written to LDS, two fp16 planes per operand. fp16's range (65504) bounds the activations and 64 W.
 //
-// One 256-thread workgroup per 7x7 window, three per CU (LDS 54 KB): T (fp32 residual stream [49][68]) | X (halo
-// patch -> three bf16 planes [64][72] of U1 -> QKV fp32 [49][196] -> O planes -> U2 planes -> MLP hidden half planes
-// -> final T planes for the pw GEMM) | parameters. Each producer keeps its result in registers until every wave has
-// read X's previous content. GEMM tiles cover token rows 0..63 (four 16-row blocks; rows 49..63 are finite padding
-// whose outputs are dropped) and are transposed (the weight planes are the MFMA A operand): lane (g, l15) holds
-// out[token rb*16 + l15][n = cb*16 + 4g .. +3].
-//
-// Status: OFF by default. Numerically it matches the fp32 kernel (the model tests' errors are unchanged), but on
-// MI355X it is slower at the L28 shape (bench_ops, same box): swin_fused.hip 0.91-0.93 ms; this design at two
-// workgroups per CU (81 KB LDS, one region per operand) 0.99 ms, persistent with the next halo prefetched 1.02 ms,
-// three per CU (this layout, 15 barriers, 168 VGPRs with spills) 1.10 ms. The matrix cycles per window drop from
-// 16.9k to 10k, but the six-product chains, the operand splits (~500 VALU per wave) and the extra barriers leave
-// the window's latency higher, and the HIP compiler's schedule does not hide it at these occupancies.
+// One 256-thread workgroup per 7x7 window, three per CU (LDS 48 KB): T (fp32 residual stream [49][68]) | X (halo
+// patch -> two fp16 planes [64][72] of U1 -> K planes [49][72] + V^T planes [64][72] -> O planes -> U2 planes -> MLP
+// hidden half planes -> final T planes for the pw GEMM) | parameters. Each producer keeps its result in registers
+// until every wave has read X's previous content. GEMM tiles cover token rows 0..63 (four 16-row blocks; rows 49..63
+// are finite padding whose outputs are dropped) and are transposed (the weight planes are the MFMA A operand): lane
+// (g, l15) holds out[token rb*16 + l15][n = cb*16 + 4g .. +3]. Wave w computes the Q of its own 16 queries, which
+// stay in registers as the B operand of S^T = K Q^T; the S^T accumulators are split in registers into the P^T
+// operand of O^T = V^T P^T (keys 49..63 masked to P = 0).
 //
 // Reference semantics as swin_fused.hip (ultralytics/nn/modules/blocks_transformer.py:8-171).
 #include "common.h"
@@ -36,10 +31,15 @@
 #include <stdlib.h>
 
 namespace ys {
+typedef uint16_t h16_t;  // fp16 bit pattern
 namespace x3 {
 
+typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+constexpr float WSC = 64.0f;  // weight planes hold 64 W (exact): keeps their low terms out of fp16's subnormal range
+
+
 constexpr int NR = 49;   // tokens per 7x7 window
-constexpr int XR = 48;   // attention: token row 48 on the VALU (rows 0..47 = three 16-row fp32 MFMA blocks)
 constexpr int HPW = 12;  // halo patch row stride (9 used)
 
 struct Args {
@@ -48,22 +48,22 @@ struct Args {
   int B, H, W, nWx, nWin;
   const float* dw;     // [C][9]
   float ln1_eps, ln2_eps;
-  const bf16_t* win;   // planes [3][3C][C], LN1 affine folded
+  const h16_t* win;    // planes [2][3C][C] of 64 W, LN1 affine folded
   const float* bin;    // [3C] folded
-  const bf16_t* wo;    // [3][C][C]
+  const h16_t* wo;     // [2][C][C]
   const float* bo;
-  const bf16_t* w1;    // [3][HID][C], LN2 affine folded
+  const h16_t* w1;     // [2][HID][C], LN2 affine folded
   const float* b1;     // [HID] folded
-  const bf16_t* w2;    // [3][C][HID]
+  const h16_t* w2;     // [2][C][HID]
   const float* b2;
-  const bf16_t* wpw;   // [3][C][C]
+  const h16_t* wpw;    // [2][C][C]
   const float* bn_scale;
   const float* bn_shift;
   float scale;
 };
 
-__device__ __forceinline__ f32x4 mfma16(bf16x8_t a, bf16x8_t b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+__device__ __forceinline__ f32x4 mfma16(f16x8_t a, f16x8_t b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -76,50 +76,45 @@ __device__ __forceinline__ float dot4_acc(float4 a, float4 b, float acc) {
 }
 __device__ __forceinline__ float group4_sum(float v) { return xor32_sum(xor16_sum(v)); }
 
-// one split level of a pair: the bf16 pair nearest to r (round to nearest even); r becomes the (exact) remainder
-__device__ __forceinline__ uint32_t split_level(f32x2& r) {
-  const uint32_t h = pack_bf16x2(r.x, r.y);
-  r = r - f32x2{__uint_as_float(h << 16), __uint_as_float(h & 0xffff0000u)};  // v_pk_add_f32 (neg)
-  return h;
+// v = h + l for a pair: h = fp16(v), l = fp16(v - h) (round to nearest even; v - h is exact in fp32):
+// v_cvt_pk_f16_f32, two v_cvt_f32_f16, v_pk_add_f32, v_cvt_pk_f16_f32
+__device__ __forceinline__ void split2(f32x2 v, uint32_t& h, uint32_t& l) {
+  const f16x2_t hh = __builtin_convertvector(v, f16x2_t);
+  const f32x2 r = v - __builtin_convertvector(hh, f32x2);
+  h = __builtin_bit_cast(uint32_t, hh);
+  l = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, f16x2_t));
 }
-// v = h + m + l (bf16, round to nearest even at each step)
-__device__ __forceinline__ void split4(f32x4 v, uint2& h, uint2& m, uint2& l) {
-  f32x2 a = {v.x, v.y}, b = {v.z, v.w};
-  h.x = split_level(a);
-  h.y = split_level(b);
-  m.x = split_level(a);
-  m.y = split_level(b);
-  l.x = pack_bf16x2(a.x, a.y);
-  l.y = pack_bf16x2(b.x, b.y);
+__device__ __forceinline__ void split4(f32x4 v, uint2& h, uint2& l) {
+  split2(f32x2{v.x, v.y}, h.x, l.x);
+  split2(f32x2{v.z, v.w}, h.y, l.y);
 }
-// the three planes of 4 consecutive elements of row `row`, column `col` (a multiple of 4)
+// the two planes of 4 consecutive elements of row `row`, column `col` (a multiple of 4)
 template <int PS, int PL>
-__device__ __forceinline__ void store_planes4(bf16_t* P, int row, int col, f32x4 v) {
-  uint2 h, m, l;
-  split4(v, h, m, l);
-  bf16_t* d = P + row * PS + col;
+__device__ __forceinline__ void store_planes4(h16_t* P, int row, int col, f32x4 v) {
+  uint2 h, l;
+  split4(v, h, l);
+  h16_t* d = P + row * PS + col;
   *reinterpret_cast<uint2*>(d) = h;
-  *reinterpret_cast<uint2*>(d + PL) = m;
-  *reinterpret_cast<uint2*>(d + 2 * PL) = l;
+  *reinterpret_cast<uint2*>(d + PL) = l;
 }
 
 // Weight-plane fragments of one GEMM for this wave's column blocks cb = cb0 + 4j: lane (g, l15) holds
 // W_p[cb*16 + l15][koff + 32s + 8g .. +7] (16-byte global loads, L2-resident).
 template <int K, int NJ>
 struct WP {
-  bf16x8_t v[NJ][K / 32][3];
+  f16x8_t v[NJ][K / 32][2];
 };
 template <int K, int NJ>
-__device__ __forceinline__ void load_wp(const bf16_t* __restrict__ Wp, int N, int KT, int koff, int cb0, WP<K, NJ>& f,
+__device__ __forceinline__ void load_wp(const h16_t* __restrict__ Wp, int N, int KT, int koff, int cb0, WP<K, NJ>& f,
                                         int lane) {
   const int l15 = lane & 15, g = lane >> 4;
 #pragma unroll
-  for (int p = 0; p < 3; ++p)
+  for (int p = 0; p < 2; ++p)
 #pragma unroll
     for (int s = 0; s < K / 32; ++s)
 #pragma unroll
       for (int j = 0; j < NJ; ++j)
-        f.v[j][s][p] = *reinterpret_cast<const bf16x8_t*>(
+        f.v[j][s][p] = *reinterpret_cast<const f16x8_t*>(
             Wp + ((long)p * N + (cb0 + 4 * j) * 16 + l15) * KT + koff + 32 * s + 8 * g);
 }
 
@@ -128,16 +123,15 @@ __device__ __forceinline__ void load_wp(const bf16_t* __restrict__ Wp, int N, in
 // per (k-step, row block, column block), smallest terms first. The LDS operand reads run two (k-step, row block)
 // steps ahead of the MFMAs (at two waves per SIMD a read waited for right before its MFMAs exposes its latency).
 template <int K, int NJ, int PS, int PL>
-__device__ __forceinline__ void gemm_x3(const bf16_t* A, const WP<K, NJ>& w, f32x4 (&acc)[4][NJ], int lane) {
+__device__ __forceinline__ void gemm_x3(const h16_t* A, const WP<K, NJ>& w, f32x4 (&acc)[4][NJ], int lane) {
   const int l15 = lane & 15, g = lane >> 4;
   constexpr int NS = (K / 32) * 4;  // steps (s, rb), rb fastest
-  const bf16_t* a0 = A + l15 * PS + 8 * g;
-  bf16x8_t u[3][3];
-  auto ld = [&](int i, bf16x8_t (&v)[3]) {
-    const bf16_t* ar = a0 + (i & 3) * 16 * PS + 32 * (i >> 2);
-    v[0] = *reinterpret_cast<const bf16x8_t*>(ar);
-    v[1] = *reinterpret_cast<const bf16x8_t*>(ar + PL);
-    v[2] = *reinterpret_cast<const bf16x8_t*>(ar + 2 * PL);
+  const h16_t* a0 = A + l15 * PS + 8 * g;
+  f16x8_t u[3][2];
+  auto ld = [&](int i, f16x8_t (&v)[2]) {
+    const h16_t* ar = a0 + (i & 3) * 16 * PS + 32 * (i >> 2);
+    v[0] = *reinterpret_cast<const f16x8_t*>(ar);
+    v[1] = *reinterpret_cast<const f16x8_t*>(ar + PL);
   };
   ld(0, u[0]);
   ld(1, u[1]);
@@ -145,13 +139,10 @@ __device__ __forceinline__ void gemm_x3(const bf16_t* A, const WP<K, NJ>& w, f32
   for (int i = 0; i < NS; ++i) {
     if (i + 2 < NS) ld(i + 2, u[(i + 2) % 3]);
     const int s = i >> 2, rb = i & 3;
-    const bf16x8_t* v = u[i % 3];
+    const f16x8_t* v = u[i % 3];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       f32x4 c = acc[rb][j];
-      c = mfma16(w.v[j][s][2], v[0], c);
-      c = mfma16(w.v[j][s][1], v[1], c);
-      c = mfma16(w.v[j][s][0], v[2], c);
       c = mfma16(w.v[j][s][1], v[0], c);
       c = mfma16(w.v[j][s][0], v[1], c);
       acc[rb][j] = mfma16(w.v[j][s][0], v[0], c);
@@ -160,9 +151,9 @@ __device__ __forceinline__ void gemm_x3(const bf16_t* A, const WP<K, NJ>& w, f32
 }
 
 // LayerNorm statistics of token rows [0, 49) of T (fp32, stride LT) and the normalised rows (affine folded into the
-// next GEMM) as three bf16 planes; rows 49..63 get zeros. 4 lanes per row (a DPP quad), C/4 values each.
+// next GEMM) as two fp16 planes; rows 49..63 get zeros. 4 lanes per row (a DPP quad), C/4 values each.
 template <int C, int LT, int PS, int PL>
-__device__ __forceinline__ void ln_planes(const float* T, bf16_t* P, float eps, int tid) {
+__device__ __forceinline__ void ln_planes(const float* T, h16_t* P, float eps, int tid) {
   constexpr int CP = C / 4;
   const int r = tid >> 2, qd = tid & 3;
   const bool valid = r < NR;
@@ -183,13 +174,12 @@ __device__ __forceinline__ void ln_planes(const float* T, bf16_t* P, float eps, 
   const float rs = valid ? __builtin_amdgcn_rsqf(quad_sum(q) * (1.0f / (float)C) + eps) : 0.f;
 #pragma unroll
   for (int i = 0; i < CP / 4; i += 2) {
-    uint2 h0, m0, l0, h1, m1, l1;
-    split4(v[i] * rs, h0, m0, l0);
-    split4(v[i + 1] * rs, h1, m1, l1);
-    bf16_t* d = P + r * PS + qd * CP + 4 * i;
+    uint2 h0, l0, h1, l1;
+    split4(v[i] * rs, h0, l0);
+    split4(v[i + 1] * rs, h1, l1);
+    h16_t* d = P + r * PS + qd * CP + 4 * i;
     *reinterpret_cast<uint4*>(d) = make_uint4(h0.x, h0.y, h1.x, h1.y);
-    *reinterpret_cast<uint4*>(d + PL) = make_uint4(m0.x, m0.y, m1.x, m1.y);
-    *reinterpret_cast<uint4*>(d + 2 * PL) = make_uint4(l0.x, l0.y, l1.x, l1.y);
+    *reinterpret_cast<uint4*>(d + PL) = make_uint4(l0.x, l0.y, l1.x, l1.y);
   }
 }
 
@@ -198,17 +188,20 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
   constexpr int HD = C / NH;
   constexpr int HID = 2 * C;
   constexpr int LT = C + 4;      // T row stride (floats)
-  constexpr int LQ = 3 * C + 4;  // QKV row stride (floats)
-  constexpr int PS = C + 8;      // plane row stride (bf16)
+  constexpr int PS = C + 8;      // plane row stride (fp16)
   constexpr int PL = 64 * PS;    // plane stride
+  constexpr int PSK = C + 8;     // K plane row stride
+  constexpr int KPL = NR * PSK;  // K plane stride
+  constexpr int PSV = 72;        // V^T plane row stride (keys 0..63 + 8)
+  constexpr int VPL = C * PSV;   // V^T plane stride
   constexpr int NHS = (C + 2) / 3;
   static_assert(C == 64 && HID / 2 == C, "the plane regions are sized for C = 64 (hidden halves of 64)");
-  static_assert(HD % 16 == 0 && HD <= 64, "head dim");
+  static_assert(HD == 32, "attention operands: two 16-column blocks per head");
   constexpr int T_B = NR * LT * 4;
-  constexpr int QKV_B = NR * LQ * 4;
-  constexpr int PLN_B = 3 * PL * 2;
+  constexpr int KV_B = (2 * VPL + 2 * KPL) * 2;
+  constexpr int PLN_B = 2 * PL * 2;
   constexpr int HALO_B = 3 * NHS * 9 * HPW * 4;
-  constexpr int X_B = QKV_B > HALO_B ? (QKV_B > PLN_B ? QKV_B : PLN_B) : (HALO_B > PLN_B ? HALO_B : PLN_B);
+  constexpr int X_B = KV_B > HALO_B ? (KV_B > PLN_B ? KV_B : PLN_B) : (HALO_B > PLN_B ? HALO_B : PLN_B);
   constexpr int NPAR = 3 * C + C + HID + C + 2 * C;
   static_assert(T_B % 16 == 0 && X_B % 16 == 0, "16-byte aligned regions");
   static_assert(T_B + X_B + NPAR * 4 <= 160 * 1024 / 3, "three workgroups per CU");
@@ -216,7 +209,7 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
   float* T = reinterpret_cast<float*>(smem);
   char* X = smem + T_B;
   float* Q = reinterpret_cast<float*>(X);
-  bf16_t* P = reinterpret_cast<bf16_t*>(X);
+  h16_t* P = reinterpret_cast<h16_t*>(X);
   float* par = reinterpret_cast<float*>(smem + T_B + X_B);
   constexpr int P_BIN = 0, P_BO = 3 * C, P_B1 = 4 * C, P_B2 = 4 * C + HID, P_SC = 5 * C + HID, P_SH = 6 * C + HID;
 
@@ -268,15 +261,15 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
     else if (e < P_SC) v = p.b2[e - P_B2];
     else if (e < P_SH) v = p.bn_scale[e - P_SC];
     else v = p.bn_shift[e - P_SH];
-    par[e] = v;
+    par[e] = e < P_SC ? v * WSC : (e < P_SH ? v * (1.0f / WSC) : v);  // biases x64, BN scale /64 (exact)
   }
   const int dw_c = tid % C;
   float dwk[9];
 #pragma unroll
   for (int i = 0; i < 9; ++i) dwk[i] = p.dw[dw_c * 9 + i];
-  // QKV weight planes of column block wid (the Q block): in flight during the halo store, dw conv and LN1
+  // QKV weight planes of column block 0 (the first Q block): in flight during the halo store, dw conv and LN1
   WP<C, 1> f_q;
-  load_wp(p.win, 3 * C, C, 0, wid, f_q, lane);
+  load_wp(p.win, 3 * C, C, 0, 0, f_q, lane);
 
   // ---- halo -> X (fp32 [27i + slot][HPW]) -> dw3x3 -> T (cropped / padded tokens = 0) ----
   float* halo = Q;
@@ -311,127 +304,153 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
   ln_planes<C, LT, PS, PL>(T, P, p.ln1_eps, tid);
   __syncthreads();
 
-  // ---- QKV = U1 Win'^T + b_in': three column-block passes (one weight-plane set in flight ahead); the results stay
-  // in registers until every wave has read U1, then replace it in X as fp32 [49][LQ] ----
-  constexpr int NJ_QKV = 3 * C / 64;
-  f32x4 aq[NJ_QKV][4][1];
+  // ---- QKV = U1 Win'^T + b_in' (weight planes hold 64 W). Wave w computes Q of its own 16 query rows (four column
+  // blocks of one row block: kept in registers for the attention) and the K and V column blocks w of all 64 token
+  // rows; K and V replace U1 in X as planes after every wave has read U1 ----
+  h16_t* Vt = P;                 // V^T planes [2][C][PSV]: d rows, key columns 0..63 (keys 49..63 finite padding)
+  h16_t* Kp = P + 2 * C * PSV;   // K planes [2][NR][PSK]
+  f32x4 qa[C / 16];              // lane: 64 Q[q = 16 wid + l15][cb*16 + 4g .. +3], cb = 0..C/16-1
+  f32x4 akv[2][4][1];            // 64 K (0) / 64 V (1) of column block wid, row blocks 0..3
   {
+    const int l15_ = l15;
+    f16x8_t ua[C / 32][2];
+#pragma unroll
+    for (int s2 = 0; s2 < C / 32; ++s2) {
+      const h16_t* ar = P + (wid * 16 + l15_) * PS + 32 * s2 + 8 * g;
+      ua[s2][0] = *reinterpret_cast<const f16x8_t*>(ar);
+      ua[s2][1] = *reinterpret_cast<const f16x8_t*>(ar + PL);
+    }
     WP<C, 1> f_n;
 #pragma unroll
-    for (int j = 0; j < NJ_QKV; ++j) {
-      if (j + 1 < NJ_QKV) load_wp(p.win, 3 * C, C, 0, wid + 4 * (j + 1), f_n, lane);
-      const f32x4 b = *reinterpret_cast<const f32x4*>(par + P_BIN + (wid + 4 * j) * 16 + 4 * g);
+    for (int cq = 0; cq < C / 16; ++cq) {
+      load_wp(p.win, 3 * C, C, 0, cq + 1 < C / 16 ? cq + 1 : C / 16 + wid, f_n, lane);
+      f32x4 c = *reinterpret_cast<const f32x4*>(par + P_BIN + cq * 16 + 4 * g);
 #pragma unroll
-      for (int rb = 0; rb < 4; ++rb) aq[j][rb][0] = b;
-      gemm_x3<C, 1, PS, PL>(P, f_q, aq[j], lane);
-      if (j + 1 < NJ_QKV) f_q = f_n;
+      for (int s2 = 0; s2 < C / 32; ++s2) {
+        c = mfma16(f_q.v[0][s2][1], ua[s2][0], c);
+        c = mfma16(f_q.v[0][s2][0], ua[s2][1], c);
+        c = mfma16(f_q.v[0][s2][0], ua[s2][0], c);
+      }
+      qa[cq] = c;
+      f_q = f_n;
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      if (j == 0) load_wp(p.win, 3 * C, C, 0, 2 * C / 16 + wid, f_n, lane);
+      const f32x4 b = *reinterpret_cast<const f32x4*>(par + P_BIN + ((j + 1) * C / 16 + wid) * 16 + 4 * g);
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) akv[j][rb][0] = b;
+      gemm_x3<C, 1, PS, PL>(P, f_q, akv[j], lane);
+      if (j == 0) f_q = f_n;
     }
   }
   WP<C, 1> f_o;
   load_wp(p.wo, C, C, 0, wid, f_o, lane);  // out-proj planes: in flight during attention
-  __syncthreads();
+  __syncthreads();  // every wave has read U1
 #pragma unroll
-  for (int j = 0; j < NJ_QKV; ++j)
+  for (int rb = 0; rb < 4; ++rb) {
+    const int tok = rb * 16 + l15;
+    if (tok < NR) store_planes4<PSK, KPL>(Kp, tok, wid * 16 + 4 * g, akv[0][rb][0] * (1.0f / WSC));
+    uint2 h, l;
+    split4(akv[1][rb][0] * (1.0f / WSC), h, l);
+    h16_t* vd = Vt + (wid * 16 + 4 * g) * PSV + tok;
+    vd[0] = (h16_t)(h.x & 0xffffu);
+    vd[PSV] = (h16_t)(h.x >> 16);
+    vd[2 * PSV] = (h16_t)(h.y & 0xffffu);
+    vd[3 * PSV] = (h16_t)(h.y >> 16);
+    vd[VPL] = (h16_t)(l.x & 0xffffu);
+    vd[VPL + PSV] = (h16_t)(l.x >> 16);
+    vd[VPL + 2 * PSV] = (h16_t)(l.y & 0xffffu);
+    vd[VPL + 3 * PSV] = (h16_t)(l.y >> 16);
+  }
+  // this wave's queries as the B operand of S^T = K Q^T, per head: k slot j of lane group g is head dim
+  // 4g + j (j < 4) or 16 + 4g + j - 4 (the lane's own two Q column blocks); K is read with the same permutation
+  f16x8_t qh[NH], ql[NH];
 #pragma unroll
-    for (int rb = 0; rb < 4; ++rb)
-      if (rb < 3 || l15 == 0)
-        *reinterpret_cast<f32x4*>(Q + (rb * 16 + l15) * LQ + (wid + 4 * j) * 16 + 4 * g) = aq[j][rb][0];
-  __syncthreads();
-
-  // ---- attention (fp32 MFMA), wave = 16 queries, all heads; O stays in registers until every wave has read K / V,
-  // then replaces QKV in X as planes (rows 0..63: padding queries are copies of query 48, finite) ----
+  for (int hh = 0; hh < NH; ++hh) {
+    uint2 h0, l0, h1, l1;
+    split4(qa[2 * hh] * (1.0f / WSC), h0, l0);
+    split4(qa[2 * hh + 1] * (1.0f / WSC), h1, l1);
+    qh[hh] = __builtin_bit_cast(f16x8_t, make_uint4(h0.x, h0.y, h1.x, h1.y));
+    ql[hh] = __builtin_bit_cast(f16x8_t, make_uint4(l0.x, l0.y, l1.x, l1.y));
+  }
+  __syncthreads();  // K / V planes complete
   WP<C, 1> f_1a;
   load_wp(p.w1, HID, C, 0, wid, f_1a, lane);  // MLP1 (hidden half 0) planes
+
+  // ---- attention on fp16 two-term splits, wave = 16 queries, all heads: S^T[key][q] (keys 0..63 in four 16-row
+  // blocks; keys >= 49 masked) -> softmax over keys (raw scores, exp2, 1/sum applied to O) -> O^T = V^T P^T with
+  // the S^T accumulators as the P^T operand (MFMA step s takes key blocks 2s and 2s+1: slot j of lane group g is
+  // key 32s + 4g + j (j < 4) or 32s + 16 + 4g + j - 4) ----
   f32x4 ov[NH][HD / 16];
   {
-    const int q = wid * 16 + l15;
-    const int qrow = q < XR ? q : XR;
-    constexpr int DQ = HD / 4;
-    f32x4 st[NH][3];
-    float s48[NH];
+    f32x4 st[NH][4];
 #pragma unroll
-    for (int h = 0; h < NH; ++h) {
-      s48[h] = 0.f;
+    for (int hh = 0; hh < NH; ++hh)
 #pragma unroll
-      for (int kb = 0; kb < 3; ++kb) st[h][kb] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-#pragma unroll
-    for (int t = 0; t < DQ / 4; ++t) {
-      float4 qv[NH], kv[NH][3], k48[NH];
-#pragma unroll
-      for (int h = 0; h < NH; ++h) {
-        qv[h] = *reinterpret_cast<const float4*>(Q + qrow * LQ + h * HD + g * DQ + 4 * t);
-#pragma unroll
-        for (int kb = 0; kb < 3; ++kb)
-          kv[h][kb] = *reinterpret_cast<const float4*>(Q + (kb * 16 + l15) * LQ + C + h * HD + g * DQ + 4 * t);
-        k48[h] = *reinterpret_cast<const float4*>(Q + XR * LQ + C + h * HD + g * DQ + 4 * t);
+      for (int kb = 0; kb < 4; ++kb) {
+        const int row = kb * 16 + l15 < NR ? kb * 16 + l15 : NR - 1;
+        const h16_t* kr = Kp + row * PSK + hh * HD + 4 * g;
+        const uint2 a0 = *reinterpret_cast<const uint2*>(kr), a1 = *reinterpret_cast<const uint2*>(kr + 16);
+        const uint2 b0 = *reinterpret_cast<const uint2*>(kr + KPL), b1 = *reinterpret_cast<const uint2*>(kr + KPL + 16);
+        const f16x8_t kh = __builtin_bit_cast(f16x8_t, make_uint4(a0.x, a0.y, a1.x, a1.y));
+        const f16x8_t kl = __builtin_bit_cast(f16x8_t, make_uint4(b0.x, b0.y, b1.x, b1.y));
+        f32x4 c = mfma16(kl, qh[hh], f32x4{0.f, 0.f, 0.f, 0.f});
+        c = mfma16(kh, ql[hh], c);
+        st[hh][kb] = mfma16(kh, qh[hh], c);
       }
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-#pragma unroll
-        for (int h = 0; h < NH; ++h)
-#pragma unroll
-          for (int kb = 0; kb < 3; ++kb) {
-            const float kk = c == 0 ? kv[h][kb].x : c == 1 ? kv[h][kb].y : c == 2 ? kv[h][kb].z : kv[h][kb].w;
-            const float qq = c == 0 ? qv[h].x : c == 1 ? qv[h].y : c == 2 ? qv[h].z : qv[h].w;
-            st[h][kb] = mfma4(kk, qq, st[h][kb]);
-          }
-#pragma unroll
-      for (int h = 0; h < NH; ++h) s48[h] = dot4_acc(k48[h], qv[h], s48[h]);
-    }
-    // lane holds S^T[key = kb*16 + 4g + r][q = l15] per head (+ key 48 after the group sum): softmax over the keys
-    // on the raw scores with exp2 (scale*log2 e folded into one FMA), 1/sum applied to O
     const float c2 = p.scale * 1.44269504088896341f;
-    float p48[NH], inv[NH];
+    float inv[NH];
 #pragma unroll
-    for (int h = 0; h < NH; ++h) {
-      const float sv48 = group4_sum(s48[h]);
-      float mx = sv48;
+    for (int hh = 0; hh < NH; ++hh) {
+      float mx = -INFINITY;
 #pragma unroll
-      for (int kb = 0; kb < 3; ++kb)
+      for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, st[h][kb][r]);
+        for (int r = 0; r < 4; ++r) {
+          const float sv = (kb * 16 + 4 * g + r < NR) ? st[hh][kb][r] : -INFINITY;
+          st[hh][kb][r] = sv;
+          mx = fmaxf(mx, sv);
+        }
       mx = xor32_max(xor16_max(mx));
       const float mc = -mx * c2;
       float sum = 0.f;
 #pragma unroll
-      for (int kb = 0; kb < 3; ++kb)
+      for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float e = __builtin_amdgcn_exp2f(fmaf(st[h][kb][r], c2, mc));
-          st[h][kb][r] = e;
+          const float e = __builtin_amdgcn_exp2f(fmaf(st[hh][kb][r], c2, mc));
+          st[hh][kb][r] = e;
           sum += e;
         }
-      const float e48 = __builtin_amdgcn_exp2f(fmaf(sv48, c2, mc));
-      sum += (g == 0) ? e48 : 0.f;
-      inv[h] = __builtin_amdgcn_rcpf(group4_sum(sum));
-      p48[h] = e48;
+      inv[hh] = __builtin_amdgcn_rcpf(group4_sum(sum));
     }
-    // O^T[d][q] = sum_key V[key][d] P[q][key] (MFMA (kb, r) consumes keys kb*16 + 4g' + r), key 48 rank-1 update
 #pragma unroll
-    for (int h = 0; h < NH; ++h)
+    for (int hh = 0; hh < NH; ++hh) {
 #pragma unroll
-      for (int db = 0; db < HD / 16; ++db) ov[h][db] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int db = 0; db < HD / 16; ++db) ov[hh][db] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int kb = 0; kb < 3; ++kb)
+      for (int s2 = 0; s2 < 2; ++s2) {
+        uint2 h0, l0, h1, l1;
+        split4(st[hh][2 * s2], h0, l0);
+        split4(st[hh][2 * s2 + 1], h1, l1);
+        const f16x8_t ph = __builtin_bit_cast(f16x8_t, make_uint4(h0.x, h0.y, h1.x, h1.y));
+        const f16x8_t pl = __builtin_bit_cast(f16x8_t, make_uint4(l0.x, l0.y, l1.x, l1.y));
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float* vrow = Q + (kb * 16 + 4 * g + r) * LQ + 2 * C + l15;
-#pragma unroll
-        for (int h = 0; h < NH; ++h)
-#pragma unroll
-          for (int db = 0; db < HD / 16; ++db) ov[h][db] = mfma4(vrow[h * HD + db * 16], st[h][kb][r], ov[h][db]);
+        for (int db = 0; db < HD / 16; ++db) {
+          const h16_t* vr = Vt + (hh * HD + db * 16 + l15) * PSV + 32 * s2 + 4 * g;
+          const uint2 a0 = *reinterpret_cast<const uint2*>(vr), a1 = *reinterpret_cast<const uint2*>(vr + 16);
+          const uint2 b0 = *reinterpret_cast<const uint2*>(vr + VPL), b1 = *reinterpret_cast<const uint2*>(vr + VPL + 16);
+          const f16x8_t vh = __builtin_bit_cast(f16x8_t, make_uint4(a0.x, a0.y, a1.x, a1.y));
+          const f16x8_t vl = __builtin_bit_cast(f16x8_t, make_uint4(b0.x, b0.y, b1.x, b1.y));
+          f32x4 c = mfma16(vl, ph, ov[hh][db]);
+          c = mfma16(vh, pl, c);
+          ov[hh][db] = mfma16(vh, ph, c);
+        }
       }
 #pragma unroll
-    for (int h = 0; h < NH; ++h)
-#pragma unroll
-      for (int db = 0; db < HD / 16; ++db) {
-        const float4 v48 = *reinterpret_cast<const float4*>(Q + XR * LQ + 2 * C + h * HD + db * 16 + 4 * g);
-        ov[h][db][0] = fmaf(v48.x, p48[h], ov[h][db][0]) * inv[h];
-        ov[h][db][1] = fmaf(v48.y, p48[h], ov[h][db][1]) * inv[h];
-        ov[h][db][2] = fmaf(v48.z, p48[h], ov[h][db][2]) * inv[h];
-        ov[h][db][3] = fmaf(v48.w, p48[h], ov[h][db][3]) * inv[h];
-      }
+      for (int db = 0; db < HD / 16; ++db) ov[hh][db] *= inv[hh];
+    }
   }
   __syncthreads();
 #pragma unroll
@@ -455,7 +474,7 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
       const int tok = rb * 16 + l15;
       if (rb < 3 || l15 == 0) {
         f32x4* tp = reinterpret_cast<f32x4*>(T + tok * LT + wid * 16 + 4 * g);
-        *tp = *tp + acc[rb][0];
+        *tp = *tp + acc[rb][0] * (1.0f / WSC);
       }
     }
   }
@@ -479,8 +498,9 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
     gemm_x3<C, 1, PS, PL>(P, half == 0 ? f_1a : f_1b, acc, lane);
 #pragma unroll
     for (int rb = 0; rb < 4; ++rb) {
-      const f32x2 lo = gelu2_fast_(f32x2{acc[rb][0][0], acc[rb][0][1]});
-      const f32x2 hi = gelu2_fast_(f32x2{acc[rb][0][2], acc[rb][0][3]});
+      const f32x4 a = acc[rb][0] * (1.0f / WSC);
+      const f32x2 lo = gelu2_fast_(f32x2{a[0], a[1]});
+      const f32x2 hi = gelu2_fast_(f32x2{a[2], a[3]});
       hid[half][rb] = f32x4{lo.x, lo.y, hi.x, hi.y};
     }
   }
@@ -526,7 +546,7 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
   for (int rb = 0; rb < 4; ++rb) {
     const int tok = rb * 16 + l15;
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
-    if (tok < NR) v = *reinterpret_cast<const f32x4*>(T + tok * LT + wid * 16 + 4 * g) + acc2[rb][0];
+    if (tok < NR) v = *reinterpret_cast<const f32x4*>(T + tok * LT + wid * 16 + 4 * g) + acc2[rb][0] * (1.0f / WSC);
     store_planes4<PS, PL>(P, tok, wid * 16 + 4 * g, v);
   }
   __syncthreads();
@@ -557,7 +577,7 @@ struct PrepArgs {
   const float *bn_w, *bn_b, *bn_m, *bn_v;
   float bn_eps;
   int C, HID;
-  bf16_t *pin, *po, *p1, *p2, *ppw;
+  h16_t *pin, *po, *p1, *p2, *ppw;
   float *bin_f, *b1_f, *bn_sc, *bn_sh;
 };
 
@@ -570,7 +590,7 @@ __global__ __launch_bounds__(256) void swin_x3_prep_kernel(PrepArgs a) {
   const float* bet = nullptr;
   const float* bsrc = nullptr;
   float* bdst = nullptr;
-  bf16_t* dst;
+  h16_t* dst;
   int N, K;
   if (n < 3 * C) {
     src = a.win; gam = a.ln1_w; bet = a.ln1_b; bsrc = a.bin; bdst = a.bin_f; dst = a.pin; N = 3 * C; K = C;
@@ -599,13 +619,10 @@ __global__ __launch_bounds__(256) void swin_x3_prep_kernel(PrepArgs a) {
     const float w = row[k];
     if (bet) bacc = fmaf(w, bet[k], bacc);
     const float v = gam ? w * gam[k] : w;
-    const bf16_t h = f2bf(v);
-    const float r1 = v - bf2f(h);
-    const bf16_t m = f2bf(r1);
-    const bf16_t l = f2bf(r1 - bf2f(m));
-    dst[(long)n * K + k] = h;
-    dst[((long)N + n) * K + k] = m;
-    dst[(2L * N + n) * K + k] = l;
+    const _Float16 h = (_Float16)(v * WSC);
+    const _Float16 l = (_Float16)(v * WSC - (float)h);
+    dst[(long)n * K + k] = __builtin_bit_cast(h16_t, h);
+    dst[((long)N + n) * K + k] = __builtin_bit_cast(h16_t, l);
   }
   if (bdst) {
     bacc = wave_sum(bacc);
@@ -618,12 +635,12 @@ __global__ __launch_bounds__(256) void swin_x3_prep_kernel(PrepArgs a) {
 
 using namespace ys;
 
-// Opt-in (YOLOSOD_SWIN_X3=1, or the test hook below): measured slower than swin_fused.hip on MI355X - see the header.
+// Default for C = 64 (YOLOSOD_SWIN_X3=0 routes C = 64 SwinBlocks to the exact-fp32-MFMA kernel swin_fused.hip).
 static int g_swin_x3 = -1;
 static bool swin_x3_env() {
   if (g_swin_x3 < 0) {
     const char* e = getenv("YOLOSOD_SWIN_X3");
-    g_swin_x3 = (e && atoi(e) != 0) ? 1 : 0;
+    g_swin_x3 = (e && e[0] == '0') ? 0 : 1;
   }
   return g_swin_x3 != 0;
 }
@@ -637,11 +654,11 @@ bool yolosod_swin_x3_ok(int C, int num_heads, int wh, int ww, int mlp_hidden) {
 
 size_t yolosod_swin_x3_workspace(int C, int mlp_hidden) {
   Sizer s;
-  s.take<bf16_t>((size_t)3 * 3 * C * C);           // in_proj planes
-  s.take<bf16_t>((size_t)3 * C * C);               // out_proj
-  s.take<bf16_t>((size_t)3 * mlp_hidden * C);      // mlp1
-  s.take<bf16_t>((size_t)3 * C * mlp_hidden);      // mlp2
-  s.take<bf16_t>((size_t)3 * C * C);               // pw
+  s.take<h16_t>((size_t)2 * 3 * C * C);            // in_proj planes
+  s.take<h16_t>((size_t)2 * C * C);                // out_proj
+  s.take<h16_t>((size_t)2 * mlp_hidden * C);       // mlp1
+  s.take<h16_t>((size_t)2 * C * mlp_hidden);       // mlp2
+  s.take<h16_t>((size_t)2 * C * C);                // pw
   s.take<float>((size_t)3 * C + mlp_hidden + 2 * C);  // folded biases, BN scale / shift
   return s.off;
 }
@@ -659,11 +676,11 @@ int yolosod_swin_x3_launch(const float* x, float* y, int B, int C, int H, int W,
   if (!yolosod_swin_x3_ok(C, num_heads, wh, ww, mlp_hidden)) return 0;
   if ((long)C * H * W >= (1L << 30) || (long)B * nWin >= (1L << 31)) return 0;
   Carver cv(workspace, workspace_bytes);
-  bf16_t* pin = cv.take<bf16_t>((size_t)3 * 3 * C * C);
-  bf16_t* po = cv.take<bf16_t>((size_t)3 * C * C);
-  bf16_t* p1 = cv.take<bf16_t>((size_t)3 * mlp_hidden * C);
-  bf16_t* p2 = cv.take<bf16_t>((size_t)3 * C * mlp_hidden);
-  bf16_t* ppw = cv.take<bf16_t>((size_t)3 * C * C);
+  h16_t* pin = cv.take<h16_t>((size_t)2 * 3 * C * C);
+  h16_t* po = cv.take<h16_t>((size_t)2 * C * C);
+  h16_t* p1 = cv.take<h16_t>((size_t)2 * mlp_hidden * C);
+  h16_t* p2 = cv.take<h16_t>((size_t)2 * C * mlp_hidden);
+  h16_t* ppw = cv.take<h16_t>((size_t)2 * C * C);
   float* fb = cv.take<float>((size_t)3 * C + mlp_hidden + 2 * C);
   if (!fb) {
     set_error("swin_x3: workspace too small (%zu)", workspace_bytes);
