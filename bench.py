@@ -318,6 +318,14 @@ def main():
                 "traffic": (traffic or {}).get(f"{dom['op']}:{'x'.join(map(str, dom['shape']))}"),
                 "kernel": f"{dom['op']}{tuple(dom['shape'])} (one C-ABI call = its launch sequence)",
                 "algorithmic_per_launch": dom["flops"] if bound == "mfma" else dom["bytes"]}
+    if (dom["op"] == "swin" and perf.elem_size(dom["key"]) == 4 and dom["shape"][1] in (64, 256)
+            and os.environ.get("YOLOSOD_SWIN_X3", "1") != "0"):
+        # the fp32 Swin kernels run their matrix products as fp16 two-term splits (3 exact fp16 products per fp32
+        # product, fp32 accumulation: csrc/swin_x3.hip); `frac` stays against the fp32 MFMA peak of the dtype, this
+        # is the same rate against the fp16 matrix-core ceiling of that method
+        roofline["matrix_method"] = {"method": "fp16 two-term splits on v_mfma_f32_16x16x32_f16, 3 products per fp32 "
+                                               "product", "peak_tflops": round(perf.PEAK_BF16_MFMA_TFLOPS / 3, 1),
+                                     "frac": round(achieved / (perf.PEAK_BF16_MFMA_TFLOPS / 3), 4)}
 
     # path-level roofline = sum_k t_k^min / sum_k t_k^meas over every hot-path operator,
     # t_k^min = max(bytes_k / HBM peak, flops_k / matrix-core peak of the op's dtype)

@@ -43,11 +43,12 @@ def test_op_matches_reference_fixture(name, cuda):
 
 
 @pytest.mark.parametrize("x3", [0, 1], ids=["fp32_mfma", "f16x2_mfma"])
-@pytest.mark.parametrize("name", [n for n in recipes.OPS if n.startswith("swin_c64")])
-def test_swin_c64_kernels_match_reference_fixture(name, x3, cuda):
-    """Both C = 64 fused Swin kernels: the default one that runs every matrix product as fp16 two-term splits on
-    the fp16 matrix cores (csrc/swin_x3.hip: three exact products per fp32 product) and the exact-fp32-MFMA one
-    (csrc/swin_fused.hip, YOLOSOD_SWIN_X3=0), both held to the fp32 tolerances."""
+@pytest.mark.parametrize("name", [n for n in recipes.OPS if n.startswith("swin_c64") or n.startswith("swin_c256")])
+def test_swin_kernels_match_reference_fixture(name, x3, cuda):
+    """Both kinds of fused Swin kernel: the default ones (C = 64 and C = 256) that run every matrix product as fp16
+    two-term splits on the fp16 matrix cores (csrc/swin_x3.hip: three exact products per fp32 product) and the
+    exact-fp32-MFMA ones (csrc/swin_fused.hip, csrc/swin_wide.hip; YOLOSOD_SWIN_X3=0), all held to the fp32
+    tolerances."""
     lib = _hip.load_library()
     z = golden(f"ops_{name}")
     m, _ = build_fixture_module(name)
@@ -96,10 +97,10 @@ def test_op_real_shapes_vs_oracle(name, cuda, monkeypatch):
     assert ok, f"{name}: rel check max abs err {err:.3g} ratio {ratio:.2f}"
 
 
-@pytest.mark.parametrize("name", ["swin_L28", "swin_L28_1280"])
-def test_swin_L28_exact_fp32_kernel_real_shapes(name, cuda, monkeypatch):
-    """The exact-fp32-MFMA C = 64 kernel (swin_fused.hip, YOLOSOD_SWIN_X3=0) at the real shapes (the default
-    fp16-split kernel runs them in test_op_real_shapes_vs_oracle)."""
+@pytest.mark.parametrize("name", ["swin_L28", "swin_L28_1280", "swin_L9", "swin_wide_pad_20x13"])
+def test_swin_exact_fp32_kernels_real_shapes(name, cuda, monkeypatch):
+    """The exact-fp32-MFMA Swin kernels (swin_fused.hip, swin_wide.hip; YOLOSOD_SWIN_X3=0) at the real shapes (the
+    default fp16-split kernels run them in test_op_real_shapes_vs_oracle)."""
     lib = _hip.load_library()
     monkeypatch.setitem(recipes.OPS, name, REAL[name])
     m, _ = build_fixture_module(name)

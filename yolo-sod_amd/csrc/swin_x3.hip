@@ -569,6 +569,475 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
   }
 }
 
+// ---- C = 256 (the P4 instance L9: 4 heads of 64, MLP hidden 512) -------------------------------------------------
+// One 512-thread workgroup (8 waves, 2 per SIMD) per 7x7 window, one per CU (LDS 154 KB): T (fp32 residual stream
+// [49][260]) | U (two fp16 planes [49][264]: LN1 output, then LN2 output, then the final T for the pw GEMM) | WR
+// (work region: V^T + K planes of a head pair -> O planes of the pair -> an MLP hidden chunk's planes). The halo of
+// the depthwise conv uses U + WR. Rows >= 49 of a B operand are read clamped to row 48 (finite; their outputs are
+// dropped). Per head pair: wave (lh, qb) = (local head, 16-query block) computes its Q tile row (four column
+// blocks, kept in registers) and K / V column block w of the pair for all token rows; attention as in the C = 64
+// kernel; the out-projection's partial product over the pair's 128 input channels accumulates in registers. The
+// MLP runs in two hidden chunks of 256 (MLP2 partials in registers). Weight planes stream from L2 per wave in
+// 64-k steps with one step of lookahead.
+namespace wx {
+constexpr int C = 256;
+constexpr int HD = 64;
+constexpr int HID = 512;
+constexpr int NT = 512;
+constexpr int LT = C + 4;           // T row stride (floats)
+constexpr int PSU = C + 8;          // U / hidden-chunk plane row stride (fp16)
+constexpr int UPL = NR * PSU;       // plane stride (49 rows)
+constexpr int PSK = 128 + 8;        // K planes of a head pair [49][PSK]
+constexpr int KPL = NR * PSK;
+constexpr int PSV = 56;             // V^T planes of a head pair [128][PSV]: keys 0..55 stored; the MFMA reads keys
+constexpr int VPL = 128 * PSV;      // up to 63 (P = 0 there), i.e. into the next row / the K planes (finite)
+constexpr int PSO = 128 + 8;        // O planes of a head pair [64][PSO]
+constexpr int OPL = 64 * PSO;
+constexpr int HALF = 128;           // channels per halo half
+constexpr int NRH = (HALF + 5) / 6; // halo steps per half (6 channels per step)
+constexpr int T_B = NR * LT * 4;
+constexpr int U_B = 2 * UPL * 2;
+constexpr int KV_B = (2 * VPL + 2 * KPL) * 2;
+constexpr int O_B = 2 * OPL * 2;
+constexpr int WR_B = KV_B > O_B ? (KV_B > U_B ? KV_B : U_B) : (O_B > U_B ? O_B : U_B);
+constexpr int HALO_B = 54 * NRH * HPW * 4;
+static_assert(HALO_B <= U_B + WR_B, "halo patch");
+static_assert(T_B % 16 == 0 && U_B % 16 == 0 && WR_B % 16 == 0, "16-byte aligned regions");
+static_assert(T_B + U_B + WR_B <= 160 * 1024, "LDS");
+
+// acc[rb][j] += (B rows (rb0 + rb)*16 + l15 . W[cb[j]*16 + l15]^T)^T over k in [koff, koff + K): W = two fp16
+// planes [2][N][KT] in global memory (L2), the token rows = two LDS planes (row stride PS, plane stride PL; rows
+// clamped to 48 when CLAMP). Weight fragments of KS 32-k steps are loaded one step ahead.
+template <int K, int NJ, int NRB, int KS, int PS, int PL, bool CLAMP>
+__device__ __forceinline__ void gemm_w(const h16_t* __restrict__ Wp, int N, int KT, int koff, const int (&cb)[NJ],
+                                       const h16_t* A, int rb0, f32x4 (&acc)[NRB][NJ], int lane) {
+  const int l15 = lane & 15, g = lane >> 4;
+  constexpr int NST = K / (32 * KS);
+  static_assert(K % (32 * KS) == 0, "k steps");
+  const long pst = (long)N * KT;
+  const h16_t* wr[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) wr[j] = Wp + (long)(cb[j] * 16 + l15) * KT + koff + 8 * g;
+  const h16_t* ar[NRB];
+#pragma unroll
+  for (int rb = 0; rb < NRB; ++rb) {
+    int row = (rb0 + rb) * 16 + l15;
+    if (CLAMP) row = row < NR ? row : NR - 1;
+    ar[rb] = A + row * PS + 8 * g;
+  }
+  f16x8_t w0[KS][NJ][2], w1[KS][NJ][2];
+  auto ldw = [&](f16x8_t (&w)[KS][NJ][2], int st) {
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+          w[ks][j][p] = *reinterpret_cast<const f16x8_t*>(wr[j] + p * pst + 32 * (st * KS + ks));
+  };
+  auto mma = [&](const f16x8_t (&w)[KS][NJ][2], int st) {
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int k0 = 32 * (st * KS + ks);
+#pragma unroll
+      for (int rb = 0; rb < NRB; ++rb) {
+        const f16x8_t ah = *reinterpret_cast<const f16x8_t*>(ar[rb] + k0);
+        const f16x8_t al = *reinterpret_cast<const f16x8_t*>(ar[rb] + PL + k0);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          f32x4 c = mfma16(w[ks][j][1], ah, acc[rb][j]);
+          c = mfma16(w[ks][j][0], al, c);
+          acc[rb][j] = mfma16(w[ks][j][0], ah, c);
+        }
+      }
+    }
+  };
+  ldw(w0, 0);
+#pragma unroll 1
+  for (int st = 0; st < NST; st += 2) {
+    if (st + 1 < NST) ldw(w1, st + 1);
+    mma(w0, st);
+    if (st + 1 < NST) {
+      if (st + 2 < NST) ldw(w0, st + 2);
+      mma(w1, st + 1);
+    }
+  }
+}
+
+// LayerNorm (normalisation only; the affine is folded into the next GEMM's weights) of T rows [0, 49) into the two
+// U planes: 8 lanes per row (512 threads = 64 rows), 32 values each
+__device__ __forceinline__ void ln_planes8(const float* T, h16_t* U, float eps, int tid) {
+  const int r = tid >> 3, part = tid & 7;
+  const bool valid = r < NR;
+  f32x4 v[8];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    v[i] = valid ? *reinterpret_cast<const f32x4*>(T + r * LT + part * 32 + 4 * i) : f32x4{0.f, 0.f, 0.f, 0.f};
+    s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+  }
+  s = quad_sum(s);
+  s += __shfl_xor(s, 4, 64);
+  const float mean = s * (1.0f / (float)C);
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    v[i] -= mean;
+    q += (v[i].x * v[i].x + v[i].y * v[i].y) + (v[i].z * v[i].z + v[i].w * v[i].w);
+  }
+  q = quad_sum(q);
+  q += __shfl_xor(q, 4, 64);
+  const float rs = __builtin_amdgcn_rsqf(q * (1.0f / (float)C) + eps);
+  if (valid) {
+#pragma unroll
+    for (int i = 0; i < 8; i += 2) {
+      uint2 h0, l0, h1, l1;
+      split4(v[i] * rs, h0, l0);
+      split4(v[i + 1] * rs, h1, l1);
+      h16_t* d = U + r * PSU + part * 32 + 4 * i;
+      *reinterpret_cast<uint4*>(d) = make_uint4(h0.x, h0.y, h1.x, h1.y);
+      *reinterpret_cast<uint4*>(d + UPL) = make_uint4(l0.x, l0.y, l1.x, l1.y);
+    }
+  }
+}
+
+__device__ __forceinline__ f32x4 ld_bias4(const float* b, int n) { return *reinterpret_cast<const f32x4*>(b + n) * WSC; }
+
+__global__ __launch_bounds__(NT, 1) void swin_wx_kernel(Args p) {
+  __shared__ __attribute__((aligned(16))) char smem[T_B + U_B + WR_B];
+  float* T = reinterpret_cast<float*>(smem);
+  h16_t* UP = reinterpret_cast<h16_t*>(smem + T_B);
+  h16_t* WR = reinterpret_cast<h16_t*>(smem + T_B + U_B);
+  float* HALO = reinterpret_cast<float*>(smem + T_B);
+  h16_t* Vt = WR;              // [2][128][PSV]
+  h16_t* Kp = WR + 2 * VPL;    // [2][49][PSK]
+  h16_t* Op = WR;              // [2][64][PSO]
+  h16_t* Hp = WR;              // [2][49][PSU]
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l15 = lane & 15, g = lane >> 4;
+  const int H = p.H, W = p.W;
+  const int HWi = H * W;  // per-image offsets are 32-bit (the launcher checks C*H*W < 2^30)
+
+  const long nwin_total = (long)p.B * p.nWin;
+  const long per_xcd = (nwin_total + 7) >> 3;
+  const long gwl = (long)(blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+  if (gwl >= nwin_total || (blockIdx.x >> 3) >= per_xcd) return;
+  const int gw = __builtin_amdgcn_readfirstlane((int)gwl);
+  const int img = gw / p.nWin, win = gw - (gw / p.nWin) * p.nWin;
+  const int wy = win / p.nWx, wx_ = win - (win / p.nWx) * p.nWx;
+  auto rsrc_of = [&](const float* base) {
+    const unsigned long long a = (unsigned long long)base;
+    return __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(a >> 32)) << 32) |
+                (unsigned)__builtin_amdgcn_readfirstlane((unsigned)a)),
+        (short)0, __builtin_amdgcn_readfirstlane(C * HWi * 4), 0x00020000);
+  };
+  const __amdgpu_buffer_rsrc_t rx = rsrc_of(p.x + (long)img * C * HWi);
+  constexpr unsigned OOB = 0x80000000u;
+
+  // halo of both channel halves into registers: row slot s = 7*wid + lane/9 < 54 is (channel 6i + s/9, patch row
+  // s%9) at step i, lane%9 the column; out-of-image lanes get an out-of-range voffset (the buffer load returns 0)
+  const int hl_r = lane / 9, hl_px = lane - (lane / 9) * 9;
+  const int hslot = 7 * wid + hl_r;
+  float hv[2][NRH];
+  {
+    const int hcs = hslot / 9, hpy = hslot - (hslot / 9) * 9;
+    const int hh = wy * 7 - 1 + hpy, wc = wx_ * 7 - 1 + hl_px;
+    const bool ok = hl_r < 7 && hslot < 54 && (unsigned)hh < (unsigned)H && (unsigned)wc < (unsigned)W;
+    const unsigned voff = ok ? (unsigned)((hcs * HWi + hh * W + wc) * 4) : OOB;
+    const unsigned vlast = (6 * (NRH - 1) + hcs < HALF) ? voff : OOB;
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+      for (int i = 0; i < NRH; ++i)
+        hv[hf][i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                  rx, i == NRH - 1 ? vlast : voff, (hf * HALF + 6 * i) * HWi * 4, 0));
+  }
+  const int lh = wid >> 2, qb = wid & 3;  // attention: (local head, 16-query block)
+
+  // ---- depthwise 3x3 per channel half: halo -> LDS [c][py][HPW] -> T (cropped / padded tokens = 0) ----
+  const int dc = tid % HALF;
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf) {
+    float dwk[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) dwk[i] = p.dw[(hf * HALF + dc) * 9 + i];
+    if (hf) __syncthreads();  // previous half's dw reads done
+    if (hl_r < 7 && hslot < 54) {
+#pragma unroll
+      for (int i = 0; i < NRH; ++i) HALO[(54 * i + hslot) * HPW + hl_px] = hv[hf][i];
+    }
+    __syncthreads();
+    for (int item = tid; item < HALF * 7; item += NT) {
+      const int iy = item / HALF;  // item % HALF == dc
+      const float* hp = HALO + (dc * 9 + iy) * HPW;
+      float r[3][12];
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+        for (int q4 = 0; q4 < 3; ++q4) {
+          const float4 v = *reinterpret_cast<const float4*>(hp + ky * HPW + 4 * q4);
+          r[ky][4 * q4] = v.x; r[ky][4 * q4 + 1] = v.y; r[ky][4 * q4 + 2] = v.z; r[ky][4 * q4 + 3] = v.w;
+        }
+      const bool rowok = wy * 7 + iy < H;
+#pragma unroll
+      for (int ix = 0; ix < 7; ++ix) {
+        const float v = dwk[0] * r[0][ix] + dwk[1] * r[0][ix + 1] + dwk[2] * r[0][ix + 2] + dwk[3] * r[1][ix] +
+                        dwk[4] * r[1][ix + 1] + dwk[5] * r[1][ix + 2] + dwk[6] * r[2][ix] + dwk[7] * r[2][ix + 1] +
+                        dwk[8] * r[2][ix + 2];
+        T[(iy * 7 + ix) * LT + hf * HALF + dc] = (rowok && wx_ * 7 + ix < W) ? v : 0.f;
+      }
+    }
+  }
+  __syncthreads();
+  ln_planes8(T, UP, p.ln1_eps, tid);
+  __syncthreads();
+
+  // ---- attention on head pairs; out-projection partials (this wave's column blocks wid, wid + 8) in registers ----
+  const int cbo[2] = {wid, wid + 8};
+  f32x4 acc_o[4][2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const f32x4 b = ld_bias4(p.bo, cbo[j] * 16 + 4 * g);
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb) acc_o[rb][j] = b;
+  }
+  const float c2 = p.scale * 1.44269504088896341f;
+#pragma unroll 1
+  for (int hp = 0; hp < 2; ++hp) {
+    // Q of this wave's queries (head 2hp + lh): in_proj rows hp*128 + lh*64 + [0, 64)
+    f32x4 qa[1][4];
+    {
+      int cbq[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        cbq[t] = (hp * 128 + lh * 64) / 16 + t;
+        qa[0][t] = ld_bias4(p.bin, cbq[t] * 16 + 4 * g);
+      }
+      gemm_w<C, 4, 1, 1, PSU, UPL, true>(p.win, 3 * C, C, 0, cbq, UP, qb, qa, lane);
+    }
+    // K / V column block wid of the pair, all token rows
+    f32x4 akv[4][2];
+    {
+      const int cbkv[2] = {(C + hp * 128) / 16 + wid, (2 * C + hp * 128) / 16 + wid};
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const f32x4 b = ld_bias4(p.bin, cbkv[j] * 16 + 4 * g);
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) akv[rb][j] = b;
+      }
+      gemm_w<C, 2, 4, 2, PSU, UPL, true>(p.win, 3 * C, C, 0, cbkv, UP, 0, akv, lane);
+    }
+    __syncthreads();  // the previous pair's out-projection has read its O planes (WR)
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb) {
+      const int tok = rb * 16 + l15;
+      if (tok < NR) store_planes4<PSK, KPL>(Kp, tok, wid * 16 + 4 * g, akv[rb][0] * (1.0f / WSC));
+      if (tok < PSV) {
+        uint2 h, l;
+        split4(akv[rb][1] * (1.0f / WSC), h, l);
+        h16_t* vd = Vt + (wid * 16 + 4 * g) * PSV + tok;
+        vd[0] = (h16_t)(h.x & 0xffffu);
+        vd[PSV] = (h16_t)(h.x >> 16);
+        vd[2 * PSV] = (h16_t)(h.y & 0xffffu);
+        vd[3 * PSV] = (h16_t)(h.y >> 16);
+        vd[VPL] = (h16_t)(l.x & 0xffffu);
+        vd[VPL + PSV] = (h16_t)(l.x >> 16);
+        vd[VPL + 2 * PSV] = (h16_t)(l.y & 0xffffu);
+        vd[VPL + 3 * PSV] = (h16_t)(l.y >> 16);
+      }
+    }
+    // Q as the B operand of S^T = K Q^T, per 32-d step s: slot j of lane group g is d = 32s + 4g + j (j < 4) or
+    // 32s + 16 + 4g + j - 4 (the lane's own Q tiles 2s, 2s + 1); K is read with the same permutation
+    f16x8_t qh[2], ql[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      uint2 h0, l0, h1, l1;
+      split4(qa[0][2 * s] * (1.0f / WSC), h0, l0);
+      split4(qa[0][2 * s + 1] * (1.0f / WSC), h1, l1);
+      qh[s] = __builtin_bit_cast(f16x8_t, make_uint4(h0.x, h0.y, h1.x, h1.y));
+      ql[s] = __builtin_bit_cast(f16x8_t, make_uint4(l0.x, l0.y, l1.x, l1.y));
+    }
+    __syncthreads();  // K / V^T planes complete
+    f32x4 ov[HD / 16];
+    {
+      f32x4 st[4];
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) {
+        const int row = kb * 16 + l15 < NR ? kb * 16 + l15 : NR - 1;
+        f32x4 c = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const h16_t* kr = Kp + row * PSK + lh * HD + 32 * s + 4 * g;
+          const uint2 a0 = *reinterpret_cast<const uint2*>(kr), a1 = *reinterpret_cast<const uint2*>(kr + 16);
+          const uint2 b0 = *reinterpret_cast<const uint2*>(kr + KPL), b1 = *reinterpret_cast<const uint2*>(kr + KPL + 16);
+          const f16x8_t kh = __builtin_bit_cast(f16x8_t, make_uint4(a0.x, a0.y, a1.x, a1.y));
+          const f16x8_t kl = __builtin_bit_cast(f16x8_t, make_uint4(b0.x, b0.y, b1.x, b1.y));
+          c = mfma16(kl, qh[s], c);
+          c = mfma16(kh, ql[s], c);
+          c = mfma16(kh, qh[s], c);
+        }
+        st[kb] = c;
+      }
+      float mx = -INFINITY;
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float sv = (kb * 16 + 4 * g + r < NR) ? st[kb][r] : -INFINITY;
+          st[kb][r] = sv;
+          mx = fmaxf(mx, sv);
+        }
+      mx = xor32_max(xor16_max(mx));
+      const float mc = -mx * c2;
+      float sum = 0.f;
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float e = __builtin_amdgcn_exp2f(fmaf(st[kb][r], c2, mc));
+          st[kb][r] = e;
+          sum += e;
+        }
+      const float inv = __builtin_amdgcn_rcpf(group4_sum(sum));
+#pragma unroll
+      for (int db = 0; db < HD / 16; ++db) ov[db] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        uint2 h0, l0, h1, l1;
+        split4(st[2 * s2], h0, l0);
+        split4(st[2 * s2 + 1], h1, l1);
+        const f16x8_t ph = __builtin_bit_cast(f16x8_t, make_uint4(h0.x, h0.y, h1.x, h1.y));
+        const f16x8_t pl = __builtin_bit_cast(f16x8_t, make_uint4(l0.x, l0.y, l1.x, l1.y));
+#pragma unroll
+        for (int db = 0; db < HD / 16; ++db) {
+          const h16_t* vr = Vt + (lh * HD + db * 16 + l15) * PSV + 32 * s2 + 4 * g;
+          const uint2 a0 = *reinterpret_cast<const uint2*>(vr), a1 = *reinterpret_cast<const uint2*>(vr + 16);
+          const uint2 b0 = *reinterpret_cast<const uint2*>(vr + VPL), b1 = *reinterpret_cast<const uint2*>(vr + VPL + 16);
+          const f16x8_t vh = __builtin_bit_cast(f16x8_t, make_uint4(a0.x, a0.y, a1.x, a1.y));
+          const f16x8_t vl = __builtin_bit_cast(f16x8_t, make_uint4(b0.x, b0.y, b1.x, b1.y));
+          f32x4 c = mfma16(vl, ph, ov[db]);
+          c = mfma16(vh, pl, c);
+          ov[db] = mfma16(vh, ph, c);
+        }
+      }
+#pragma unroll
+      for (int db = 0; db < HD / 16; ++db) ov[db] *= inv;
+    }
+    __syncthreads();  // every wave has read K / V^T
+#pragma unroll
+    for (int db = 0; db < HD / 16; ++db)
+      store_planes4<PSO, OPL>(Op, qb * 16 + l15, lh * HD + db * 16 + 4 * g, ov[db]);
+    __syncthreads();
+    gemm_w<128, 2, 4, 2, PSO, OPL, false>(p.wo, C, C, hp * 128, cbo, Op, 0, acc_o, lane);
+  }
+  // T += O Wo^T + bo (this wave's column blocks; rows < 49)
+#pragma unroll
+  for (int rb = 0; rb < 4; ++rb) {
+    const int tok = rb * 16 + l15;
+    if (tok < NR) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        f32x4* tp = reinterpret_cast<f32x4*>(T + tok * LT + cbo[j] * 16 + 4 * g);
+        *tp = *tp + acc_o[rb][j] * (1.0f / WSC);
+      }
+    }
+  }
+  __syncthreads();
+  ln_planes8(T, UP, p.ln2_eps, tid);
+  __syncthreads();
+
+  // ---- MLP in two hidden chunks of 256: GELU(U2 W1c'^T + b1c') -> WR planes -> MLP2 partial in registers ----
+  f32x4 acc_m[4][2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const f32x4 b = ld_bias4(p.b2, cbo[j] * 16 + 4 * g);
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb) acc_m[rb][j] = b;
+  }
+#pragma unroll 1
+  for (int ck = 0; ck < 2; ++ck) {
+    f32x4 ah[4][2];
+    const int cb1[2] = {ck * 16 + wid, ck * 16 + wid + 8};
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const f32x4 b = ld_bias4(p.b1, cb1[j] * 16 + 4 * g);
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) ah[rb][j] = b;
+    }
+    gemm_w<C, 2, 4, 2, PSU, UPL, true>(p.w1, HID, C, 0, cb1, UP, 0, ah, lane);
+    __syncthreads();  // the previous chunk's MLP2 has read WR
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb) {
+      const int tok = rb * 16 + l15;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const f32x4 a = ah[rb][j] * (1.0f / WSC);
+        const f32x2 lo = gelu2_fast_(f32x2{a[0], a[1]});
+        const f32x2 hi = gelu2_fast_(f32x2{a[2], a[3]});
+        if (tok < NR) store_planes4<PSU, UPL>(Hp, tok, cbo[j] * 16 + 4 * g, f32x4{lo.x, lo.y, hi.x, hi.y});
+      }
+    }
+    __syncthreads();
+    gemm_w<C, 2, 4, 2, PSU, UPL, true>(p.w2, C, HID, ck * 256, cbo, Hp, 0, acc_m, lane);
+  }
+  // final T = T + MLP -> U planes (the pw GEMM's operand); every wave has read U2 (MLP1 of the last chunk)
+#pragma unroll
+  for (int rb = 0; rb < 4; ++rb) {
+    const int tok = rb * 16 + l15;
+    if (tok < NR) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(T + tok * LT + cbo[j] * 16 + 4 * g) + acc_m[rb][j] * (1.0f / WSC);
+        store_planes4<PSU, UPL>(UP, tok, cbo[j] * 16 + 4 * g, v);
+      }
+    }
+  }
+  // residual x and BN terms of this lane's outputs: in flight during the pw GEMM
+  const __amdgpu_buffer_rsrc_t ry = rsrc_of(p.y + (long)img * C * HWi);
+  unsigned vtok[4];  // byte offset of (channel wid*16 + 4g, token tb*16 + l15), or out of range
+#pragma unroll
+  for (int tb = 0; tb < 4; ++tb) {
+    const int tok = tb * 16 + l15;
+    const int iy = tok / 7, ix = tok - (tok / 7) * 7;
+    const int hh = wy * 7 + iy, wc = wx_ * 7 + ix;
+    vtok[tb] = (tok < NR && hh < H && wc < W) ? (unsigned)(((wid * 16 + 4 * g) * HWi + hh * W + wc) * 4) : OOB;
+  }
+  float xr[2][4][4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int tb = 0; tb < 4; ++tb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        xr[j][tb][r] = __builtin_bit_cast(
+            float, __builtin_amdgcn_raw_buffer_load_b32(rx, vtok[tb], (128 * j + r) * HWi * 4, 0));
+  f32x4 sc[2], sh[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    sc[j] = *reinterpret_cast<const f32x4*>(p.bn_scale + cbo[j] * 16 + 4 * g) * (1.0f / WSC);
+    sh[j] = *reinterpret_cast<const f32x4*>(p.bn_shift + cbo[j] * 16 + 4 * g);
+  }
+  __syncthreads();
+  f32x4 acc[4][2];
+#pragma unroll
+  for (int tb = 0; tb < 4; ++tb)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[tb][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  gemm_w<C, 2, 4, 2, PSU, UPL, true>(p.wpw, C, C, 0, cbo, UP, 0, acc, lane);
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int tb = 0; tb < 4; ++tb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        __builtin_amdgcn_raw_buffer_store_b32(
+            __builtin_bit_cast(unsigned, xr[j][tb][r] + silu_fast_(acc[tb][j][r] * sc[j][r] + sh[j][r])), ry,
+            vtok[tb], (128 * j + r) * HWi * 4, 0);
+}
+}  // namespace wx
+
 // Weight preparation: LN affine folds and the three-plane split, one wave per output row (lanes along k,
 // coalesced); also the BN fold of the pw conv. Rows: [0,3C) in_proj (LN1 folded) | [3C,4C) out_proj | [4C,4C+HID)
 // mlp1 (LN2 folded) | mlp2 (K = HID) | pw | C BN entries.
@@ -649,7 +1118,8 @@ static bool swin_x3_env() {
 YS_EXPORT void yolosod_debug_set_swin_x3(int on) { g_swin_x3 = on ? 1 : 0; }
 
 bool yolosod_swin_x3_ok(int C, int num_heads, int wh, int ww, int mlp_hidden) {
-  return swin_x3_env() && C == 64 && num_heads == 2 && wh == 7 && ww == 7 && mlp_hidden == 2 * C;
+  return swin_x3_env() && wh == 7 && ww == 7 && mlp_hidden == 2 * C &&
+         ((C == 64 && num_heads == 2) || (C == x3::wx::C && num_heads == C / x3::wx::HD));
 }
 
 size_t yolosod_swin_x3_workspace(int C, int mlp_hidden) {
@@ -694,7 +1164,11 @@ int yolosod_swin_x3_launch(const float* x, float* y, int B, int C, int H, int W,
   x3::Args a{x, y, B, H, W, nWx, nWin, dw_w, ln1_eps, ln2_eps, pin, fb, po, out_proj_b, p1, fb + 3 * C, p2, mlp2_b,
              ppw, fb + 3 * C + mlp_hidden, fb + 4 * C + mlp_hidden, 1.0f / sqrtf((float)(C / num_heads))};
   const long nwin = (long)B * nWin;
-  hipLaunchKernelGGL((x3::swin_x3_kernel<64, 2>), dim3((unsigned)(8 * ((nwin + 7) / 8))), dim3(256), 0, st, a);
+  if (nwin == 0) return 1;
+  if (C == 64)
+    hipLaunchKernelGGL((x3::swin_x3_kernel<64, 2>), dim3((unsigned)(8 * ((nwin + 7) / 8))), dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL(x3::wx::swin_wx_kernel, dim3((unsigned)(8 * ((nwin + 7) / 8))), dim3(x3::wx::NT), 0, st, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     set_error("swin_x3: launch failed: %s", hipGetErrorString(e));
