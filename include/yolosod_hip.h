@@ -185,10 +185,18 @@ int yolosod_attention(const float* qkv, float* out, long n_seq, int L, int C, in
 /* Test hook: 1 routes SwinBlock shapes the fused per-window kernel covers (C 64/128, heads 2/4, window <= 7x7,
  * mlp 2C) through it (default, or env YOLOSOD_SWIN_FUSED), 0 forces the decomposed GEMM path for every shape. */
 void yolosod_debug_set_swin_fused(int on);
-/* Test hook: 1 routes C = 64 / 2-head / 7x7 SwinBlocks through the opt-in kernel that runs the projection / MLP / pw
- * GEMMs as three-term bf16 splits on the bf16 matrix cores at fp32 accuracy (csrc/swin_x3.hip; also env
- * YOLOSOD_SWIN_X3=1), 0 (default) keeps the fp32-MFMA fused kernel. */
+/* Test hook: 1 (default; env YOLOSOD_SWIN_X3=0 turns it off) routes 7x7-window SwinBlocks with C = 64 / 2 heads and
+ * C = 256 / 4 heads through the kernels that run every matrix product as fp16 two-term splits on the fp16 matrix
+ * cores at fp32 accuracy (csrc/swin_x3.hip), 0 through the exact-fp32-MFMA fused kernels. */
 void yolosod_debug_set_swin_x3(int on);
+/* Test hook: 1 (default; env YOLOSOD_HEAD_X2=0 turns it off) runs the Detect head's 1x1 convs as fp16 two-term
+ * splits on the fp16 matrix cores (detect_head_x2_kernel), 0 on the exact fp32 MFMA (detect_head_lds_kernel). */
+void yolosod_debug_set_head_x2(int on);
+/* Test hooks: A2_Attn's GEMMs as fp16 two-term splits on v_mfma_f32_32x32x16_f16 (1, default; env YOLOSOD_A2_X2=0
+ * turns it off) or exact fp32 MFMA (0); yolosod_debug_set_gemm_x2(1) makes every yolosod_gemm_f32 / internal fp32 GEMM
+ * call take the split products, 0 restores the callers' choice. */
+void yolosod_debug_set_a2_x2(int on);
+void yolosod_debug_set_gemm_x2(int on);
 
 /* ---------------------------------------------------------------------------------------------------------------
  * bf16 model config (BASELINE configs[4]): `model.to(torch.bfloat16)` after fuse() - AutoBackend's fp16

@@ -133,7 +133,9 @@ def test_channel_ops_batch_invariant(name, shape, cuda):
 @pytest.mark.parametrize("M_,N,K,bkc", [(300, 192, 64, True), (1000, 64, 128, True), (129, 768, 256, True),
                                          (512, 400, 512, False), (64, 1600, 64, False), (130, 13, 32, True),
                                          (70, 150, 32, False)])
-def test_gemm_f32(M_, N, K, bkc, cuda):
+@pytest.mark.parametrize("x2", [0, 1], ids=["fp32_mfma", "f16x2_mfma"])
+def test_gemm_f32(M_, N, K, bkc, x2, cuda):
+    """Generic fp32 GEMM with the fused epilogue, on exact fp32 MFMA and as fp16 two-term split products."""
     from yolosod_amd import _hip
     g = torch.Generator().manual_seed(M_ * 7 + N)
     A = torch.randn(M_, K, generator=g)
@@ -142,7 +144,13 @@ def test_gemm_f32(M_, N, K, bkc, cuda):
     res = torch.randn(M_, N, generator=g)
     ref = (A.double() @ (B.double().t() if bkc else B.double())) + bias.double()
     ref = torch.nn.functional.silu(ref) + res.double()
-    C = _hip.gemm_f32(A.to(cuda), B.to(cuda), bkc, bias=bias.to(cuda), bias_mode=2, act=1, res=res.to(cuda)).cpu()
+    lib = _hip.load_library()
+    lib.yolosod_debug_set_gemm_x2(x2)
+    try:
+        C = _hip.gemm_f32(A.to(cuda), B.to(cuda), bkc, bias=bias.to(cuda), bias_mode=2, act=1,
+                          res=res.to(cuda)).cpu()
+    finally:
+        lib.yolosod_debug_set_gemm_x2(0)
     ok, err, _ = tol_close(C, ref, 1e-4, 1e-5)
     assert ok, err
 
@@ -278,9 +286,11 @@ def test_bias_act_dual_store(c2lo, res, cuda):
     assert float(buf[:, :8].abs().max()) == 0.0 and float(buf[:, 24:].abs().max()) == 0.0
 
 
+@pytest.mark.parametrize("x2", [1, 0], ids=["f16x2_mfma", "fp32_mfma"])
 @pytest.mark.parametrize("c3,img", [(64, 256), (128, 192), (64, 200)])
-def test_detect_head_fused_vs_oracle(c3, img, cuda):
-    """Fused last 1x1 convs + decode vs the fp64 oracle (1x1 convs then decode_ref, head.py:70,100-131)."""
+def test_detect_head_fused_vs_oracle(c3, img, x2, cuda):
+    """Fused last 1x1 convs + decode vs the fp64 oracle (1x1 convs then decode_ref, head.py:70,100-131), with the
+    convs as fp16 two-term splits on the fp16 matrix cores (default) and on the exact fp32 MFMA."""
     g = torch.Generator().manual_seed(c3 + img)
     strides, nc, B = [4.0, 8.0, 16.0, 32.0], 10, 2
     fb, fc, wb, bb, wc, bc, maps = [], [], [], [], [], [], []
@@ -297,9 +307,34 @@ def test_detect_head_fused_vs_oracle(c3, img, cuda):
         maps.append(torch.cat([box, cls], 1))
     ref = R.decode_ref(maps, strides, nc)
     d = lambda ts: [t.to(cuda) for t in ts]  # noqa: E731
-    y = _hip.detect_head(d(fb), d(fc), d(wb), d(bb), d(wc), d(bc), strides, nc).cpu()
+    lib = _hip.load_library()
+    lib.yolosod_debug_set_head_x2(x2)
+    try:
+        y = _hip.detect_head(d(fb), d(fc), d(wb), d(bb), d(wc), d(bc), strides, nc).cpu()
+    finally:
+        lib.yolosod_debug_set_head_x2(1)
     ok, err, _ = tol_close(y, ref, 5e-4, 1e-5)
     assert ok, f"max abs err {err:.3g}"
+
+
+@pytest.mark.parametrize("name", [n for n in recipes.OPS if n.startswith("a2_")])
+def test_a2_exact_fp32_gemms_match_reference_fixture(name, cuda):
+    """A2_Attn with its GEMMs on exact fp32 MFMA (YOLOSOD_A2_X2=0); the default fp16-split GEMMs run the same
+    fixtures in test_op_matches_reference_fixture."""
+    lib = _hip.load_library()
+    z = golden(f"ops_{name}")
+    m, _ = build_fixture_module(name)
+    x = torch.from_numpy(z["x"])
+    lib.yolosod_debug_set_a2_x2(0)
+    try:
+        with torch.inference_mode():
+            y = m.to(cuda)(x.to(cuda)).cpu()
+    finally:
+        lib.yolosod_debug_set_a2_x2(1)
+    ok, err, _ = tol_close(y, torch.from_numpy(z["y"]), ATOL, 0.0)
+    assert ok, f"{name}: max abs err vs reference {err:.3g}"
+    ok, err, ratio = tol_close(y, _oracle64(name, x), 5e-5, 1e-4)
+    assert ok, f"{name}: vs fp64 oracle max abs err {err:.3g} (ratio {ratio:.2f})"
 
 
 @pytest.mark.parametrize("name", [n for n in recipes.OPS if n.startswith("a2_")])

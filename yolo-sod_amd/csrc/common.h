@@ -185,6 +185,39 @@ __device__ __forceinline__ void st4(bf16_t* p, f32x4 v) {
   *reinterpret_cast<uint2*>(p) = make_uint2(pack_bf16x2(v.x, v.y), pack_bf16x2(v.z, v.w));
 }
 
+// ---- fp32-accurate products on the fp16 matrix cores ------------------------------------------------------
+// v = h + l with h = fp16(v), l = fp16(v - h) (round to nearest even; v - h is exact in fp32): |v - h - l| <= 2^-22 |v|
+// while l is a normal fp16 number. a.b ~ ah.bh + ah.bl + al.bh (three exact fp16 products, fp32 accumulation; the
+// dropped al.bl <= 2^-22 |a.b|). Used by the fp32 Swin kernels (swin_x3.hip) and the Detect head (detect.hip).
+typedef uint16_t h16_t;  // fp16 bit pattern
+typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+// a pair: v_cvt_pk_f16_f32, two v_cvt_f32_f16, v_pk_add_f32, v_cvt_pk_f16_f32
+__device__ __forceinline__ void split2(f32x2 v, uint32_t& h, uint32_t& l) {
+  const f16x2_t hh = __builtin_convertvector(v, f16x2_t);
+  const f32x2 r = v - __builtin_convertvector(hh, f32x2);
+  h = __builtin_bit_cast(uint32_t, hh);
+  l = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, f16x2_t));
+}
+__device__ __forceinline__ void split4(f32x4 v, uint2& h, uint2& l) {
+  split2(f32x2{v.x, v.y}, h.x, l.x);
+  split2(f32x2{v.z, v.w}, h.y, l.y);
+}
+// 8 values -> the hi / lo fp16 operands of one v_mfma_f32_16x16x32_f16 k slot group
+__device__ __forceinline__ void split8(f32x4 a, f32x4 b, f16x8_t& h, f16x8_t& l) {
+  uint2 h0, l0, h1, l1;
+  split4(a, h0, l0);
+  split4(b, h1, l1);
+  h = __builtin_bit_cast(f16x8_t, make_uint4(h0.x, h0.y, h1.x, h1.y));
+  l = __builtin_bit_cast(f16x8_t, make_uint4(l0.x, l0.y, l1.x, l1.y));
+}
+// c += A.B for split operands (A = (ah, al), B = (bh, bl)), smallest terms first
+__device__ __forceinline__ f32x4 mfma_f16x3(f16x8_t ah, f16x8_t al, f16x8_t bh, f16x8_t bl, f32x4 c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, c, 0, 0, 0);
+}
+
 // Streaming passes that re-read a tensor written just before (> 256 MiB MALL) walk it back to front, so the tail the
 // producer wrote last is still in the Infinity Cache when the pass starts. YOLOSOD_MALL_REVERSE=0 restores the
 // forward order (A/B). Results are identical either way (each workgroup's work and summation order is unchanged).

@@ -367,6 +367,182 @@ __global__ __launch_bounds__(256, C3 > 64 ? 2 : 3) void detect_head_lds_kernel(H
   }
 }
 
+// The same head tail + decode with the 1x1 convs as fp16 two-term splits on the fp16 matrix cores (common.h:
+// three exact products per fp32 product, fp32 accumulation): 30 v_mfma_f32_16x16x32_f16 (16 cycles, beside the other
+// waves' VALU) instead of 80 v_mfma_f32_16x16x4_f32 (32 cycles, which block the SIMD's VALU) per 16-pixel group, so
+// the DFL / decode VALU work is no longer serialised behind the matrix work. Weights: LDS planes [t][s][g][row][i]
+// of 64 W (exact scaling; rows of the box conv 16t + row, channel g + 32s + 4i - the k slots of the features a lane
+// loads), split once per workgroup; the features are split in registers per group.
+template <int C2, int C3, int NTS, class FT = float>
+__global__ __launch_bounds__(256, C3 > 64 ? 2 : 3) void detect_head_x2_kernel(HeadArgs d) {
+  static_assert(C2 == 64 && C3 % 32 == 0, "k steps of 32 channels");
+  constexpr int NBW = C2 * 64, NCW = C3 * 16;  // image elements (box: 4 t x 2 s x 4 g x 16 rows x 8; cls: C3/32 s x ...)
+  __shared__ __attribute__((aligned(16))) h16_t wl[2][NBW + NCW];
+  constexpr float WS = 64.0f;
+  const int b = blockIdx.y;
+  int l = 0;
+#pragma unroll
+  for (int i = 1; i < 4; ++i)
+    if (i < d.nl && (int)blockIdx.x >= d.blk_off[i]) l = i;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int g = lane >> 4, j = lane & 15;
+  const int nc = d.nc;
+  {
+    const float* wb = d.wb[l];
+    const float* wc = d.wc[l];
+    static_assert(NBW % 512 == 0 && NCW % 512 == 0, "weight image sizes");
+    constexpr int NB = NBW / 512, NCL = NCW / 512;  // pairs per thread
+    f32x2 vb[NB], vc[NCL];
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      const int e = 2 * (tid + 256 * u);  // element pair (i, i + 1)
+      const int i = e & 7, row = (e >> 3) & 15, gg = (e >> 7) & 3, s = (e >> 9) & 1, t = e >> 10;
+      const float* src = wb + (16 * t + row) * C2 + gg + 32 * s + 4 * i;
+      vb[u] = f32x2{src[0], src[4]} * WS;
+    }
+#pragma unroll
+    for (int u = 0; u < NCL; ++u) {
+      const int e = 2 * (tid + 256 * u);
+      const int i = e & 7, row = (e >> 3) & 15, gg = (e >> 7) & 3, s = e >> 9;
+      const float* src = wc + (row < nc ? row : 0) * C3 + gg + 32 * s + 4 * i;
+      vc[u] = row < nc ? f32x2{src[0], src[4]} * WS : f32x2{0.f, 0.f};
+    }
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      uint32_t h, lo;
+      split2(vb[u], h, lo);
+      reinterpret_cast<uint32_t*>(wl[0])[tid + 256 * u] = h;
+      reinterpret_cast<uint32_t*>(wl[1])[tid + 256 * u] = lo;
+    }
+#pragma unroll
+    for (int u = 0; u < NCL; ++u) {
+      uint32_t h, lo;
+      split2(vc[u], h, lo);
+      reinterpret_cast<uint32_t*>(wl[0] + NBW)[tid + 256 * u] = h;
+      reinterpret_cast<uint32_t*>(wl[1] + NBW)[tid + 256 * u] = lo;
+    }
+  }
+  __syncthreads();
+  const int HW = d.hw[l];
+  const int px0 = (((int)blockIdx.x - d.blk_off[l]) * 4 + wv) * (NTS * 16);
+  if (px0 >= HW) return;  // whole wave; no barrier below
+  float bbr[4][4], bcr[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bbr[t][r] = d.bb[l][16 * t + 4 * g + r];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) bcr[r] = (4 * g + r < nc) ? d.bc[l][4 * g + r] : 0.f;
+  const FT* fbb = static_cast<const FT*>(d.fb[l]) + (long)b * C2 * HW;
+  const FT* fcb = static_cast<const FT*>(d.fc[l]) + (long)b * C3 * HW;
+  const int W = d.w[l];
+  const float st = d.stride[l];
+  float* yb = d.y + (long)b * (4 + nc) * d.A + d.a_off[l];
+  // A-operand rows of this lane: (t, s) block base + (g * 16 + j) * 8 halves
+  const h16_t* wbh = wl[0] + (g * 16 + j) * 8;
+  const h16_t* wbl = wl[1] + (g * 16 + j) * 8;
+
+  auto rsrc = [&](const FT* base, int bytes) {
+    const unsigned long long a = (unsigned long long)base;
+    return __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(a >> 32)) << 32) |
+                (unsigned)__builtin_amdgcn_readfirstlane((unsigned)a)),
+        (short)0, __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+  };
+  constexpr int ES = (int)sizeof(FT);
+  const __amdgpu_buffer_rsrc_t rb = rsrc(fbb, C2 * HW * ES), rc = rsrc(fcb, C3 * HW * ES);
+  auto ldf = [&](__amdgpu_buffer_rsrc_t r, unsigned vo, int so) -> float {
+    if constexpr (sizeof(FT) == 2)
+      return __uint_as_float((unsigned)__builtin_amdgcn_raw_buffer_load_b16(r, vo, so, 0) << 16);
+    else
+      return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, so, 0));
+  };
+  // lane (g, j) loads channels g + 4q of pixel j: q = 8s + i is k slot i of lane group g in k step s
+  float xb[2][C2 / 4], xc[2][C3 / 4];
+  auto load_group = [&](int ts, float (&fb)[C2 / 4], float (&fcv)[C3 / 4]) {
+    const int p = px0 + ts * 16 + j;
+    const unsigned vo = (p < HW) ? (unsigned)((g * HW + p) * ES) : 0x80000000u;
+#pragma unroll
+    for (int q = 0; q < C2 / 4; ++q) fb[q] = ldf(rb, vo, q * 4 * ES * HW);
+#pragma unroll
+    for (int q = 0; q < C3 / 4; ++q) fcv[q] = ldf(rc, vo, q * 4 * ES * HW);
+  };
+  auto compute_group = [&](int ts, const float (&cb)[C2 / 4], const float (&cc)[C3 / 4]) {
+    const int p0 = px0 + ts * 16;
+    if (p0 >= HW) return;  // wave-uniform
+    const int p = p0 + j;
+    const bool ok = p < HW;
+    f32x4 acc[5];
+#pragma unroll
+    for (int t = 0; t < 5; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < C2 / 32; ++s) {
+      f16x8_t fh, fl;
+      split8(f32x4{cb[8 * s], cb[8 * s + 1], cb[8 * s + 2], cb[8 * s + 3]},
+             f32x4{cb[8 * s + 4], cb[8 * s + 5], cb[8 * s + 6], cb[8 * s + 7]}, fh, fl);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int o = (t * 2 + s) * 512;
+        acc[t] = mfma_f16x3(*reinterpret_cast<const f16x8_t*>(wbh + o), *reinterpret_cast<const f16x8_t*>(wbl + o),
+                            fh, fl, acc[t]);
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < C3 / 32; ++s) {
+      f16x8_t fh, fl;
+      split8(f32x4{cc[8 * s], cc[8 * s + 1], cc[8 * s + 2], cc[8 * s + 3]},
+             f32x4{cc[8 * s + 4], cc[8 * s + 5], cc[8 * s + 6], cc[8 * s + 7]}, fh, fl);
+      const int o = NBW + s * 512;
+      acc[4] = mfma_f16x3(*reinterpret_cast<const f16x8_t*>(wbh + o), *reinterpret_cast<const f16x8_t*>(wbl + o), fh,
+                          fl, acc[4]);
+    }
+    // DFL (block.py:79-82), as in detect_head_kernel
+    float dist[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = acc[s][r] * (1.0f / WS) + bbr[s][r];
+      float mx = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
+      mx = xor32_max(xor16_max(mx));
+      float sum = 0.f, e = 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[r] = __expf(v[r] - mx);
+        sum += v[r];
+        e += (float)(4 * g + r) * v[r];
+      }
+      sum = xor32_sum(xor16_sum(sum));
+      e = xor32_sum(xor16_sum(e));
+      dist[s] = e * __builtin_amdgcn_rcpf(sum);
+    }
+    if (!ok) return;
+    const int iy = p / W, ix = p - iy * W;
+    const float ax = (float)ix + 0.5f, ay = (float)iy + 0.5f;
+    const float x1 = ax - dist[0], y1 = ay - dist[1];
+    const float x2 = ax + dist[2], y2 = ay + dist[3];
+    const float out = g == 0 ? ((x1 + x2) / 2.0f) * st
+                    : g == 1 ? ((y1 + y2) / 2.0f) * st
+                    : g == 2 ? (x2 - x1) * st
+                             : (y2 - y1) * st;
+    yb[(long)g * d.A + p] = out;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int c = 4 * g + r;
+      if (c < nc) yb[(long)(4 + c) * d.A + p] = sigmoidf_(acc[4][r] * (1.0f / WS) + bcr[r]);
+    }
+  };
+  static_assert(NTS % 2 == 0, "group pairs");
+  load_group(0, xb[0], xc[0]);
+#pragma unroll 1
+  for (int ts = 0; ts < NTS; ts += 2) {
+    if (px0 + (ts + 1) * 16 < HW) load_group(ts + 1, xb[1], xc[1]);
+    compute_group(ts, xb[0], xc[0]);
+    if (ts + 2 < NTS && px0 + (ts + 2) * 16 < HW) load_group(ts + 2, xb[0], xc[0]);
+    compute_group(ts + 1, xb[1], xc[1]);
+  }
+}
+
 }  // namespace ys
 
 using namespace ys;
@@ -399,6 +575,10 @@ YS_EXPORT int yolosod_detect_decode(int nl, const float* const* maps, const int*
   YS_CHECK_LAUNCH("detect_decode");
   return 0;
 }
+
+static int g_head_x2 = -1;  // head 1x1 convs: fp16-split matrix products (1, default) or exact fp32 MFMA (0)
+// Test hook: route the Detect head through detect_head_x2_kernel (1) or detect_head_lds_kernel (0).
+YS_EXPORT void yolosod_debug_set_head_x2(int on) { g_head_x2 = on ? 1 : 0; }
 
 static int detect_head_impl(int nl, const void* const* box_feat, const void* const* cls_feat, int c2, int c3,
                             const float* const* box_w, const float* const* box_b, const float* const* cls_w,
@@ -438,15 +618,28 @@ static int detect_head_impl(int nl, const void* const* box_feat, const void* con
   if (B == 0 || off == 0) return 0;
   const dim3 grid(blk, B);
   hipStream_t st = (hipStream_t)stream;
+  if (g_head_x2 < 0) {
+    const char* e = getenv("YOLOSOD_HEAD_X2");
+    g_head_x2 = (e && e[0] == '0') ? 0 : 1;
+  }
   if (bf16) {
-    if (c3 == 64) hipLaunchKernelGGL((detect_head_lds_kernel<64, 64, NTS, bf16_t>), grid, dim3(256), 0, st, d);
-    else hipLaunchKernelGGL((detect_head_lds_kernel<64, 128, NTS, bf16_t>), grid, dim3(256), 0, st, d);
+    if (g_head_x2) {
+      if (c3 == 64) hipLaunchKernelGGL((detect_head_x2_kernel<64, 64, NTS, bf16_t>), grid, dim3(256), 0, st, d);
+      else hipLaunchKernelGGL((detect_head_x2_kernel<64, 128, NTS, bf16_t>), grid, dim3(256), 0, st, d);
+    } else {
+      if (c3 == 64) hipLaunchKernelGGL((detect_head_lds_kernel<64, 64, NTS, bf16_t>), grid, dim3(256), 0, st, d);
+      else hipLaunchKernelGGL((detect_head_lds_kernel<64, 128, NTS, bf16_t>), grid, dim3(256), 0, st, d);
+    }
     YS_CHECK_LAUNCH("detect_head_bf16");
     return 0;
   }
-  // default: weights in LDS, feature loads double-buffered; YOLOSOD_HEAD_V1=1: weights in registers (A/B)
+  // default: fp16-split matrix products (detect_head_x2_kernel); YOLOSOD_HEAD_X2=0: exact fp32 MFMA with the
+  // weights in LDS; YOLOSOD_HEAD_V1=1: exact fp32 MFMA with the weights in registers (A/B)
   static const bool v1 = [] { const char* e = getenv("YOLOSOD_HEAD_V1"); return e && atoi(e) != 0; }();
-  if (v1) {
+  if (g_head_x2 && !v1) {
+    if (c3 == 64) hipLaunchKernelGGL((detect_head_x2_kernel<64, 64, NTS>), grid, dim3(256), 0, st, d);
+    else hipLaunchKernelGGL((detect_head_x2_kernel<64, 128, NTS>), grid, dim3(256), 0, st, d);
+  } else if (v1) {
     if (c3 == 64) hipLaunchKernelGGL((detect_head_kernel<64, 64, NTS>), grid, dim3(256), 0, st, d);
     else hipLaunchKernelGGL((detect_head_kernel<64, 128, NTS>), grid, dim3(256), 0, st, d);
   } else {

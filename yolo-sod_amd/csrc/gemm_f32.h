@@ -57,6 +57,10 @@ struct GemmArgs {
   int nimg;               // set by launch_gemm: > 0 = batch folded into N (N-contiguous B, nimg columns per image)
   int nmajor;             // set by launch_gemm: tiles in column-major (n-major) order
   int bfold;              // set by launch_gemm: > 0 = batch folded into the tile index (bfold images, n-major inside)
+  int x2;                 // 1: products as fp16 two-term splits on v_mfma_f32_32x32x16_f16 (fp32 accuracy)
+  float x2_sa, x2_sb;     // x2: exact power-of-two scales of A / B at the split (a weight operand: 64, keeps its
+                          // low terms out of fp16's subnormal range); the accumulators are scaled back before the
+                          // epilogue. 0 = 1
 };
 
 // Per-row LayerNorm statistics (mean, 1/sqrt(var + eps)) of a K-contiguous [rows][K] matrix: one wave per row,
@@ -119,7 +123,11 @@ __device__ __forceinline__ float epi_value(const Epi& e, int m, int n, float v) 
   return apply_act(v, e.act);
 }
 
-template <int WM, int WN, int MI, int NI, bool B_KC, bool A_LN>
+// X2: the A tile (and a K-contiguous B tile) is split into fp16 hi / lo terms while staging: row r of the LDS image
+// holds, per 8-k group j8, 8 hi halves then 8 lo halves (72 halves = the 144 B of the fp32 image's row, so the same
+// buffers; ds_read_b128 row reads stay conflict-free). A lane (half lh) of v_mfma_f32_32x32x16_f16 step s takes k
+// group 2*lh + s. An N-contiguous B tile stays fp32 [k][n] in LDS and is split in registers after 8 strided reads.
+template <int WM, int WN, int MI, int NI, bool B_KC, bool A_LN, bool X2 = false>
 __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
   constexpr int BM = WM * MI * 32;
   constexpr int BN = WN * NI * 32;
@@ -192,6 +200,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
   }
 
   float4 ra[NA], rb[NB], lw, lb;
+  const float sa = (X2 && g.x2_sa != 0.f) ? g.x2_sa : 1.f, sb = (X2 && g.x2_sb != 0.f) ? g.x2_sb : 1.f;
   auto load_tiles = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
@@ -241,12 +250,27 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
         v.z = (v.z - mu) * rs * lw.z + lb.z;
         v.w = (v.w - mu) * rs * lw.w + lb.w;
       }
-      *reinterpret_cast<float4*>(&Ab[r * SK + kq]) = v;
+      if (X2) {
+        uint2 h, l;
+        split4(f32x4{v.x, v.y, v.z, v.w} * sa, h, l);
+        h16_t* d = reinterpret_cast<h16_t*>(Ab) + r * (2 * SK) + 16 * (kq >> 3) + (kq & 7);
+        *reinterpret_cast<uint2*>(d) = h;
+        *reinterpret_cast<uint2*>(d + 8) = l;
+      } else {
+        *reinterpret_cast<float4*>(&Ab[r * SK + kq]) = v;
+      }
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
       const int idx = tid + 256 * i;
-      if (B_KC) {
+      if (B_KC && X2) {
+        const int r = idx >> 3, kq = (idx & 7) * 4;
+        uint2 h, l;
+        split4(f32x4{rb[i].x, rb[i].y, rb[i].z, rb[i].w} * sb, h, l);
+        h16_t* d = reinterpret_cast<h16_t*>(Bb) + r * (2 * SK) + 16 * (kq >> 3) + (kq & 7);
+        *reinterpret_cast<uint2*>(d) = h;
+        *reinterpret_cast<uint2*>(d + 8) = l;
+      } else if (B_KC) {
         const int r = idx >> 3, kq = (idx & 7) * 4;
         *reinterpret_cast<float4*>(&Bb[r * SK + kq]) = rb[i];
       } else {
@@ -275,6 +299,42 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
     if (kb + 1 < nk) load_tiles((kb + 1) * BK);
     const float* Ab = As + buf * A_ELEMS + (wm * MI * 32 + lr) * SK + lh * 16;
     const float* Bb = Bs + buf * B_ELEMS;
+    if constexpr (X2) {
+      const h16_t* Ah = reinterpret_cast<const h16_t*>(As + buf * A_ELEMS) + (wm * MI * 32 + lr) * (2 * SK);
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const int ko = 16 * (2 * lh + s2);  // this lane half's k group (2*lh + s2) in the split image
+        f16x8_t ah[MI], al[MI], bh[NI], bl[NI];
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          ah[i] = *reinterpret_cast<const f16x8_t*>(Ah + i * 32 * (2 * SK) + ko);
+          al[i] = *reinterpret_cast<const f16x8_t*>(Ah + i * 32 * (2 * SK) + ko + 8);
+        }
+        if constexpr (B_KC) {
+          const h16_t* Bh = reinterpret_cast<const h16_t*>(Bb) + (wn * NI * 32 + lr) * (2 * SK);
+#pragma unroll
+          for (int j = 0; j < NI; ++j) {
+            bh[j] = *reinterpret_cast<const f16x8_t*>(Bh + j * 32 * (2 * SK) + ko);
+            bl[j] = *reinterpret_cast<const f16x8_t*>(Bh + j * 32 * (2 * SK) + ko + 8);
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < NI; ++j) {
+            const float* col = Bb + (8 * (2 * lh + s2)) * SBN + wn * NI * 32 + j * 32 + lr;
+            split8(f32x4{col[0], col[SBN], col[2 * SBN], col[3 * SBN]} * sb,
+                   f32x4{col[4 * SBN], col[5 * SBN], col[6 * SBN], col[7 * SBN]} * sb, bh[j], bl[j]);
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NI; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+          }
+      }
+    } else
 #pragma unroll
     for (int t4 = 0; t4 < 4; ++t4) {
       float4 a[MI], b[NI];
@@ -305,6 +365,13 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
     __syncthreads();
   }
 
+  if (X2 && sa * sb != 1.f) {
+    const float inv = 1.0f / (sa * sb);  // exact: powers of two
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) acc[i][j] *= inv;
+  }
   const Epi& e = g.epi;
   if (e.vec) {
     // stage C through LDS (the main-loop buffers are free after the last barrier), then 16-byte row stores.
@@ -389,6 +456,12 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
 
 static inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
+// test hook state: 1 = every gemm_f32 call takes the fp16-split products (yolosod_debug_set_gemm_x2), -1 = as asked
+inline int& gemm_x2_forced() {
+  static int v = -1;
+  return v;
+}
+
 static inline int launch_gemm(const GemmArgs& g0, int batch, bool b_kc, hipStream_t st) {
   GemmArgs g = g0;
   YS_CHECK_ARG(g.K % 32 == 0, "gemm: K=%d must be a multiple of 32", g.K);
@@ -403,6 +476,7 @@ static inline int launch_gemm(const GemmArgs& g0, int batch, bool b_kc, hipStrea
               (!e.res || (e.ldr % 4 == 0 && e.res_bs % 4 == 0 && al16(e.res))) &&
               (e.bias_mode != 2 || al16(e.bias)) && (e.bn_mode != 2 || (al16(e.scale) && al16(e.shift)));
   const bool ln = g.ln_w != nullptr;
+  const bool x2 = g.x2 != 0 || gemm_x2_forced() == 1;
   // N-contiguous B with a per-image N that is not a multiple of 128 (A2 at 640: H*W = 400): fold the batch into N so
   // the tiles run across image boundaries instead of padding every image's last tile column
   g.nimg = 0;
@@ -433,7 +507,15 @@ static inline int launch_gemm(const GemmArgs& g0, int batch, bool b_kc, hipStrea
     g.tiles = g.tiles_n * ((g.M + bm - 1) / bm);                                                               \
     const long nt_ = (long)g.tiles * (g.bfold ? g.bfold : 1);                                                  \
     dim3 grid((unsigned)(8 * ((nt_ + 7) / 8)), 1, batch);                                                      \
-    if (b_kc) {                                                                                                \
+    if (x2) {                                                                                                  \
+      if (b_kc) {                                                                                              \
+        if (ln) hipLaunchKernelGGL((gemm_f32_kernel<WM_, WN_, MI_, NI_, true, true, true>), grid, dim3(256), 0, st, g); \
+        else hipLaunchKernelGGL((gemm_f32_kernel<WM_, WN_, MI_, NI_, true, false, true>), grid, dim3(256), 0, st, g); \
+      } else {                                                                                                 \
+        if (ln) hipLaunchKernelGGL((gemm_f32_kernel<WM_, WN_, MI_, NI_, false, true, true>), grid, dim3(256), 0, st, g); \
+        else hipLaunchKernelGGL((gemm_f32_kernel<WM_, WN_, MI_, NI_, false, false, true>), grid, dim3(256), 0, st, g); \
+      }                                                                                                        \
+    } else if (b_kc) {                                                                                         \
       if (ln) hipLaunchKernelGGL((gemm_f32_kernel<WM_, WN_, MI_, NI_, true, true>), grid, dim3(256), 0, st, g); \
       else hipLaunchKernelGGL((gemm_f32_kernel<WM_, WN_, MI_, NI_, true, false>), grid, dim3(256), 0, st, g);  \
     } else {                                                                                                   \

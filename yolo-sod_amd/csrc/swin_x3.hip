@@ -31,11 +31,8 @@
 #include <stdlib.h>
 
 namespace ys {
-typedef uint16_t h16_t;  // fp16 bit pattern
 namespace x3 {
 
-typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
-typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
 constexpr float WSC = 64.0f;  // weight planes hold 64 W (exact): keeps their low terms out of fp16's subnormal range
 
 
@@ -76,18 +73,6 @@ __device__ __forceinline__ float dot4_acc(float4 a, float4 b, float acc) {
 }
 __device__ __forceinline__ float group4_sum(float v) { return xor32_sum(xor16_sum(v)); }
 
-// v = h + l for a pair: h = fp16(v), l = fp16(v - h) (round to nearest even; v - h is exact in fp32):
-// v_cvt_pk_f16_f32, two v_cvt_f32_f16, v_pk_add_f32, v_cvt_pk_f16_f32
-__device__ __forceinline__ void split2(f32x2 v, uint32_t& h, uint32_t& l) {
-  const f16x2_t hh = __builtin_convertvector(v, f16x2_t);
-  const f32x2 r = v - __builtin_convertvector(hh, f32x2);
-  h = __builtin_bit_cast(uint32_t, hh);
-  l = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, f16x2_t));
-}
-__device__ __forceinline__ void split4(f32x4 v, uint2& h, uint2& l) {
-  split2(f32x2{v.x, v.y}, h.x, l.x);
-  split2(f32x2{v.z, v.w}, h.y, l.y);
-}
 // the two planes of 4 consecutive elements of row `row`, column `col` (a multiple of 4)
 template <int PS, int PL>
 __device__ __forceinline__ void store_planes4(h16_t* P, int row, int col, f32x4 v) {

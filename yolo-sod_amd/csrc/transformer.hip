@@ -720,6 +720,20 @@ YS_EXPORT int yolosod_swin_forward(const float* x, float* y, int B, int C, int H
   return 0;
 }
 
+// A2's GEMMs (proj, QKV, output): fp16 two-term split products (default) or exact fp32 MFMA (YOLOSOD_A2_X2=0)
+static int g_a2_x2 = -1;
+static bool a2_x2() {
+  if (g_a2_x2 < 0) {
+    const char* e = getenv("YOLOSOD_A2_X2");
+    g_a2_x2 = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_a2_x2 != 0;
+}
+// Test hooks: A2 GEMMs as fp16 splits (1) or exact fp32 MFMA (0); every gemm_f32 call as fp16 splits (1) or as its
+// caller asks (0)
+YS_EXPORT void yolosod_debug_set_a2_x2(int on) { g_a2_x2 = on ? 1 : 0; }
+YS_EXPORT void yolosod_debug_set_gemm_x2(int on) { gemm_x2_forced() = on ? 1 : -1; }
+
 YS_EXPORT size_t yolosod_a2_workspace(int B, int C, int H, int W, int num_areas) {
   const long ntok = (long)B * num_areas * W;
   Sizer s;
@@ -762,6 +776,8 @@ YS_EXPORT int yolosod_a2_forward(const float* x, float* y, int B, int C, int H, 
   ga.A = proj_w; ga.lda = C; ga.B = x; ga.b_bs = C * HW; ga.ldb = (int)HW; ga.M = C; ga.N = (int)HW; ga.K = C;
   ga.epi = epi_plain(XP, C * HW, (int)HW);
   ga.epi.bias = proj_b; ga.epi.bias_mode = 1; ga.epi.act = 1;
+  const bool x2 = a2_x2();
+  ga.x2 = x2; ga.x2_sa = 64.f;
   if ((rc = launch_gemm(ga, B, false, st))) return rc;
   YS_CHECK_ARG((size_t)64 * (W + 1) * sizeof(float) <= 64 * 1024, "a2: W=%d too large for the pooling kernel", W);
   hipLaunchKernelGGL(a2_pool_tokens_kernel, dim3(B * A, (C + 63) / 64), dim3(256), (size_t)64 * (W + 1) * sizeof(float),
@@ -773,6 +789,7 @@ YS_EXPORT int yolosod_a2_forward(const float* x, float* y, int B, int C, int H, 
   ga.ln_w = ln_w; ga.ln_b = ln_b; ga.ln_stats = lns;
   ga.epi = epi_plain(Q, 0, 3 * C);
   ga.epi.bias = in_proj_b; ga.epi.bias_mode = 2;
+  ga.x2 = x2; ga.x2_sb = 64.f;
   if ((rc = launch_gemm(ga, 1, true, st))) return rc;
   if ((rc = launch_attention(Q, U, B, A * W, C, num_heads, st))) return rc;
   if (!premul) {
@@ -780,6 +797,7 @@ YS_EXPORT int yolosod_a2_forward(const float* x, float* y, int B, int C, int H, 
     ga.A = U; ga.lda = C; ga.B = mha_out_w; ga.ldb = C; ga.M = (int)ntok; ga.N = C; ga.K = C;
     ga.epi = epi_plain(Z, 0, C);
     ga.epi.bias = mha_out_b; ga.epi.bias_mode = 2;
+    ga.x2 = x2; ga.x2_sb = 64.f;
     if ((rc = launch_gemm(ga, 1, true, st))) return rc;
   }
   // T[img][n][t] = sum_c Wout[n][c] Z[img*AW + t][c]   (reuse S as T: B*C*A*W floats == ntok*C)
@@ -787,6 +805,7 @@ YS_EXPORT int yolosod_a2_forward(const float* x, float* y, int B, int C, int H, 
   ga = GemmArgs{};
   ga.A = oproj_w; ga.lda = C; ga.B = premul ? U : Z; ga.b_bs = (long)A * W * C; ga.ldb = C; ga.M = C; ga.N = A * W; ga.K = C;
   ga.epi = epi_plain(T, (long)C * A * W, A * W);
+  ga.x2 = x2; ga.x2_sa = 64.f;
   if ((rc = launch_gemm(ga, B, true, st))) return rc;
   hipLaunchKernelGGL(a2_upsample_out_kernel, dim3((unsigned)(B * C), (unsigned)((HW + 255) / 256)), dim3(256), 0, st,
                      x, T, oproj_b, y, C, H, W, A);
