@@ -469,14 +469,39 @@ __global__ __launch_bounds__(256) void ca_gate_kernel(const float* __restrict__ 
   const int p0 = blockIdx.x * P;
   const int tid = threadIdx.x;
   const float* yb = yin + (long)b * C * L;
-  for (int i = tid; i < C * P; i += 256) {
-    const int c = i / P, pp = i % P;
-    ys[i] = (p0 + pp < L) ? yb[(long)c * L + p0 + pp] : 0.f;
+  // staging: 8 loads in flight per thread before their LDS stores (a load-store loop waits for each load in turn:
+  // that alone was ~20 us of L2 round trips per workgroup)
+  constexpr int U = 8;
+  for (int i0 = 0; i0 < C * P; i0 += 256 * U) {
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + tid + 256 * u, c = i / P, pp = i % P;
+      v[u] = (i < C * P && p0 + pp < L) ? yb[(long)c * L + p0 + pp] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (i0 + tid + 256 * u < C * P) ys[i0 + tid + 256 * u] = v[u];
   }
-  for (int i = tid; i < mip * C; i += 256) w1s[(i / C) * (C + 1) + i % C] = w1[i];
-  for (int i = tid; i < C * mip; i += 256) {
-    whs[i] = wh[i];
-    wws[i] = ww[i];
+  for (int i0 = 0; i0 < mip * C; i0 += 256 * U) {
+    float v[U], a[U], c_[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + tid + 256 * u;
+      const bool ok = i < mip * C;
+      v[u] = ok ? w1[i] : 0.f;
+      a[u] = ok ? wh[i] : 0.f;
+      c_[u] = ok ? ww[i] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + tid + 256 * u;
+      if (i < mip * C) {
+        w1s[(i / C) * (C + 1) + i % C] = v[u];
+        whs[i] = a[u];
+        wws[i] = c_[u];
+      }
+    }
   }
   __syncthreads();
   for (int o = tid; o < P * mip; o += 256) {
