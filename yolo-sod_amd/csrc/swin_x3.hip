@@ -12,7 +12,8 @@
 // v_mfma_f32_16x16x4_f32 (32 cycles each) per 16x16x32 block: 5.3x fewer matrix cycles. Weights are split once per
 // call by a prep kernel (with the LayerNorm affine terms folded in: W' = W diag(gamma), b' = b + W beta, so the
 // kernel's LayerNorms only normalise), scaled by 64 (exact) so that the low terms of small weights stay out of
-// fp16's subnormal range; the accumulators start from 64 b and are scaled back by 1/64 (exact) in each epilogue.
+// fp16's subnormal range; the accumulators start from 64 b and are scaled back by 1/64 (exact) in each epilogue
+// (Q, K and V keep the factor: it folds into the softmax's exp2 scale and the 1/sum applied to O).
 // Activations are split by their producer (LayerNorm, the QKV epilogue, attention, GELU, the last residual add) when
 // they are written to LDS, two fp16 planes per operand. fp16's range (65504) bounds the activations and 64 W.
 //
@@ -335,9 +336,9 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
 #pragma unroll
   for (int rb = 0; rb < 4; ++rb) {
     const int tok = rb * 16 + l15;
-    if (tok < NR) store_planes4<PSK, KPL>(Kp, tok, wid * 16 + 4 * g, akv[0][rb][0] * (1.0f / WSC));
+    if (tok < NR) store_planes4<PSK, KPL>(Kp, tok, wid * 16 + 4 * g, akv[0][rb][0]);  // K, V, Q stay x64
     uint2 h, l;
-    split4(akv[1][rb][0] * (1.0f / WSC), h, l);
+    split4(akv[1][rb][0], h, l);
     h16_t* vd = Vt + (wid * 16 + 4 * g) * PSV + tok;
     vd[0] = (h16_t)(h.x & 0xffffu);
     vd[PSV] = (h16_t)(h.x >> 16);
@@ -354,8 +355,8 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
 #pragma unroll
   for (int hh = 0; hh < NH; ++hh) {
     uint2 h0, l0, h1, l1;
-    split4(qa[2 * hh] * (1.0f / WSC), h0, l0);
-    split4(qa[2 * hh + 1] * (1.0f / WSC), h1, l1);
+    split4(qa[2 * hh], h0, l0);
+    split4(qa[2 * hh + 1], h1, l1);
     qh[hh] = __builtin_bit_cast(f16x8_t, make_uint4(h0.x, h0.y, h1.x, h1.y));
     ql[hh] = __builtin_bit_cast(f16x8_t, make_uint4(l0.x, l0.y, l1.x, l1.y));
   }
@@ -384,7 +385,7 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
         c = mfma16(kh, ql[hh], c);
         st[hh][kb] = mfma16(kh, qh[hh], c);
       }
-    const float c2 = p.scale * 1.44269504088896341f;
+    const float c2 = p.scale * 1.44269504088896341f * (1.0f / (WSC * WSC));  // S = 4096 Q K^T
     float inv[NH];
 #pragma unroll
     for (int hh = 0; hh < NH; ++hh) {
@@ -408,7 +409,7 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
           st[hh][kb][r] = e;
           sum += e;
         }
-      inv[hh] = __builtin_amdgcn_rcpf(group4_sum(sum));
+      inv[hh] = __builtin_amdgcn_rcpf(group4_sum(sum)) * (1.0f / WSC);  // V is x64
     }
 #pragma unroll
     for (int hh = 0; hh < NH; ++hh) {
@@ -788,7 +789,7 @@ __global__ __launch_bounds__(NT, 1) void swin_wx_kernel(Args p) {
 #pragma unroll
     for (int rb = 0; rb < 4; ++rb) acc_o[rb][j] = b;
   }
-  const float c2 = p.scale * 1.44269504088896341f;
+  const float c2 = p.scale * 1.44269504088896341f * (1.0f / (WSC * WSC));  // S = 4096 Q K^T
 #pragma unroll 1
   for (int hp = 0; hp < 2; ++hp) {
     // Q of this wave's queries (head 2hp + lh): in_proj rows hp*128 + lh*64 + [0, 64)
@@ -818,10 +819,10 @@ __global__ __launch_bounds__(NT, 1) void swin_wx_kernel(Args p) {
 #pragma unroll
     for (int rb = 0; rb < 4; ++rb) {
       const int tok = rb * 16 + l15;
-      if (tok < NR) store_planes4<PSK, KPL>(Kp, tok, wid * 16 + 4 * g, akv[rb][0] * (1.0f / WSC));
+      if (tok < NR) store_planes4<PSK, KPL>(Kp, tok, wid * 16 + 4 * g, akv[rb][0]);  // K, V, Q stay x64
       if (tok < PSV) {
         uint2 h, l;
-        split4(akv[rb][1] * (1.0f / WSC), h, l);
+        split4(akv[rb][1], h, l);
         h16_t* vd = Vt + (wid * 16 + 4 * g) * PSV + tok;
         vd[0] = (h16_t)(h.x & 0xffffu);
         vd[PSV] = (h16_t)(h.x >> 16);
@@ -839,8 +840,8 @@ __global__ __launch_bounds__(NT, 1) void swin_wx_kernel(Args p) {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       uint2 h0, l0, h1, l1;
-      split4(qa[0][2 * s] * (1.0f / WSC), h0, l0);
-      split4(qa[0][2 * s + 1] * (1.0f / WSC), h1, l1);
+      split4(qa[0][2 * s], h0, l0);
+      split4(qa[0][2 * s + 1], h1, l1);
       qh[s] = __builtin_bit_cast(f16x8_t, make_uint4(h0.x, h0.y, h1.x, h1.y));
       ql[s] = __builtin_bit_cast(f16x8_t, make_uint4(l0.x, l0.y, l1.x, l1.y));
     }
@@ -885,7 +886,7 @@ __global__ __launch_bounds__(NT, 1) void swin_wx_kernel(Args p) {
           st[kb][r] = e;
           sum += e;
         }
-      const float inv = __builtin_amdgcn_rcpf(group4_sum(sum));
+      const float inv = __builtin_amdgcn_rcpf(group4_sum(sum)) * (1.0f / WSC);  // V is x64
 #pragma unroll
       for (int db = 0; db < HD / 16; ++db) ov[db] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll

@@ -419,11 +419,21 @@ __global__ __launch_bounds__(256) void a2_pool_tokens_kernel(const float* __rest
   const int r0 = (a * H) / A, r1 = ((a + 1) * H + A - 1) / A;
   const float inv = (float)(r1 - r0);
   const float* xb = xp + ((long)img * C + c0) * H * W;
+  const int nr = r1 - r0;
   for (int e = threadIdx.x; e < nc * W; e += 256) {
     const int c = e / W, w = e - c * W;
     const float* src = xb + ((long)c * H + r0) * W + w;
     float s = 0.f;
-    for (int r = 0; r < r1 - r0; ++r) s += src[(long)r * W];
+    int r = 0;
+    for (; r + 4 <= nr; r += 4) {  // the bin's rows as independent loads, summed in row order
+      const float v0 = src[(long)r * W], v1 = src[(long)(r + 1) * W], v2 = src[(long)(r + 2) * W],
+                  v3 = src[(long)(r + 3) * W];
+      s += v0;
+      s += v1;
+      s += v2;
+      s += v3;
+    }
+    for (; r < nr; ++r) s += src[(long)r * W];
     slab[c * (W + 1) + w] = s / inv;
   }
   __syncthreads();
@@ -455,6 +465,38 @@ __global__ __launch_bounds__(256) void a2_upsample_out_kernel(const float* __res
   const float u = l0 * Tp[y0 * W + w] + l1 * Tp[y1 * W + w];
   const long o = pc * H * W + e;
   y[o] = x[o] + siluf_(u + bias[c]);
+}
+
+// The same tail with 4 consecutive elements of a plane per thread (H*W % 4 == 0): 16-byte x loads and y stores.
+// grid = ceil(planes * H*W / 1024).
+__global__ __launch_bounds__(256) void a2_upsample_out4_kernel(const float* __restrict__ x, const float* __restrict__ T,
+                                                               const float* __restrict__ bias, float* __restrict__ y,
+                                                               int C, int H, int W, int A, long total4) {
+  const long i4 = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i4 >= total4) return;
+  const long HW = (long)H * W;
+  const long o = i4 * 4;
+  const long pc = o / HW;  // img*C + c (HW % 4 == 0: the 4 elements share the plane)
+  const int c = (int)(pc % C);
+  const int e0 = (int)(o - pc * HW);
+  const float sc = (float)A / (float)H;
+  const float* Tp = T + pc * A * W;
+  const float b = bias[c];
+  const f32x4 xv = *reinterpret_cast<const f32x4*>(x + o);
+  f32x4 r;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int e = e0 + k;
+    const int h = e / W, w = e - h * W;
+    float src = sc * ((float)h + 0.5f) - 0.5f;
+    if (src < 0.f) src = 0.f;
+    const int y0 = (int)src;
+    const int y1 = y0 + ((y0 < A - 1) ? 1 : 0);
+    const float l1 = src - (float)y0, l0 = 1.0f - l1;
+    const float u = l0 * Tp[y0 * W + w] + l1 * Tp[y1 * W + w];
+    r[k] = xv[k] + siluf_(u + b);
+  }
+  *reinterpret_cast<f32x4*>(y + o) = r;
 }
 
 static int gs_blocks(long n) {
@@ -807,8 +849,14 @@ YS_EXPORT int yolosod_a2_forward(const float* x, float* y, int B, int C, int H, 
   ga.epi = epi_plain(T, (long)C * A * W, A * W);
   ga.x2 = x2; ga.x2_sa = 64.f;
   if ((rc = launch_gemm(ga, B, true, st))) return rc;
-  hipLaunchKernelGGL(a2_upsample_out_kernel, dim3((unsigned)(B * C), (unsigned)((HW + 255) / 256)), dim3(256), 0, st,
-                     x, T, oproj_b, y, C, H, W, A);
+  if (HW % 4 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0) {
+    const long total4 = (long)B * C * HW / 4;
+    hipLaunchKernelGGL(a2_upsample_out4_kernel, dim3((unsigned)((total4 + 255) / 256)), dim3(256), 0, st, x, T, oproj_b,
+                       y, C, H, W, A, total4);
+  } else {
+    hipLaunchKernelGGL(a2_upsample_out_kernel, dim3((unsigned)(B * C), (unsigned)((HW + 255) / 256)), dim3(256), 0,
+                       st, x, T, oproj_b, y, C, H, W, A);
+  }
   YS_CHECK_LAUNCH("a2_upsample");
   return 0;
 }
