@@ -34,6 +34,27 @@ def test_model_matches_reference_golden(gpu_model, cuda):
     assert ok, msg
 
 
+@pytest.mark.parametrize("split", [0, 1], ids=["exact_fp32_mfma", "f16_split"])
+def test_model_matrix_methods_match_reference_golden(gpu_model, split, cuda):
+    """The whole model with the Swin / head / A2 matrix products on exact fp32 MFMA (YOLOSOD_SWIN_X3 = HEAD_X2 =
+    A2_X2 = 0) and as fp16 two-term splits (the default), each against the reference golden."""
+    from yolosod_amd import _hip
+    lib = _hip.load_library()
+    g = torch.Generator().manual_seed(0)
+    x = torch.rand(2, 3, 256, 256, generator=g)
+    hooks = (lib.yolosod_debug_set_swin_x3, lib.yolosod_debug_set_head_x2, lib.yolosod_debug_set_a2_x2)
+    for h in hooks:
+        h(split)
+    try:
+        with torch.inference_mode():
+            y = gpu_model(x.to(cuda))[0].cpu()
+    finally:
+        for h in hooks:
+            h(1)
+    ok, msg = pred_close(y, torch.from_numpy(golden("model_out_256")["y"]))
+    assert ok, msg
+
+
 def test_model_640_matches_oracle(gpu_model, cuda):
     from oracle.model_ref import build_cpu_model
     cpu = build_cpu_model()
