@@ -36,7 +36,10 @@ CFG_DIR = Path(__file__).resolve().parent.parent / "cfg"
 # GPU executor: run the Detect towers of each level on a side stream as soon as that level's feature map exists
 # (overlapping the rest of the neck); YOLOSOD_STREAMS=0 keeps everything on one stream (A/B)
 # (2: start them only after the last MAFN operator has been enqueued, so no hot-path op shares the GPU)
-STREAMS = int(os.environ.get("YOLOSOD_STREAMS", "1"))
+# Unset: 1 for fp32 models, 2 for the bf16 config (its P2 towers are large enough that overlapping them with CA only
+# moved time between the two streams: m640 1636 vs 1634 img/s same-box, CA 0.33 vs 0.12 ms on the main stream)
+_STREAMS_ENV = os.environ.get("YOLOSOD_STREAMS")
+STREAMS = int(_STREAMS_ENV) if _STREAMS_ENV is not None else 1
 
 # name -> class; the YAML resolves module strings through this (tasks.py:995-1002)
 DEFAULT_REGISTRY = {
@@ -217,7 +220,10 @@ class BaseModel(nn.Module):
         plan = self._concat_producers()
         det = self.model[-1]
         towers = lvl = main = side = None
-        if (STREAMS > 0 and isinstance(det, M.Detect) and isinstance(det.f, (list, tuple)) and len(set(det.f)) == len(det.f)
+        streams = STREAMS
+        if _STREAMS_ENV is None and x.dtype == torch.bfloat16:
+            streams = 2
+        if (streams > 0 and isinstance(det, M.Detect) and isinstance(det.f, (list, tuple)) and len(set(det.f)) == len(det.f)
                 and det._fused_ok([x])):
             lvl = {j: k for k, j in enumerate(det.f)}
             towers = {}
@@ -280,7 +286,7 @@ class BaseModel(nn.Module):
                 # the rest of the neck; inputs / outputs cross streams via record_stream
                 if m.i in lvl:
                     ready.append((lvl[m.i], x))
-                if ready and (STREAMS != 2 or m.i >= last_mafn):
+                if ready and (streams != 2 or m.i >= last_mafn):
                     side.wait_stream(main)
                     for k, xk in ready:
                         xk.record_stream(side)
