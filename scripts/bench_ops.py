@@ -62,6 +62,13 @@ def main():
             if op == "SE_Block":
                 m._maybe_build(shape[1], None)
             recipes.perturb_(m, 1)
+            if bf16:  # as build_model(dtype=bf16): fold the Conv+BN pairs in fp32, then cast
+                from yolosod_amd.nn.tasks import _fuse_conv_and_bn
+                for sub in m.modules():
+                    if isinstance(sub, M.Conv) and hasattr(sub, "bn"):
+                        sub.conv = _fuse_conv_and_bn(sub.conv, sub.bn)
+                        delattr(sub, "bn")
+                        sub.forward = sub.forward_fuse
             m = m.to(dev).to(dt).eval()
             x = torch.randn(shape, device=dev).to(dt)
             # SE / CBAM / CA as the model runs them: x comes from a conv epilogue that also emitted the gate's
