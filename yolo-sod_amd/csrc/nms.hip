@@ -92,13 +92,22 @@ __global__ __launch_bounds__(256) void nms_prep_kernel(NmsArgs g) {
     g.boxes[(long)b * g.A + a] = make_float4(x1, y1, x2, y2);
     float best = -INFINITY;
     int bj = 0;
-    for (int j = 0; j < g.nc; ++j) {
-      const float s = pb[(4 + j) * As];
-      if (s > best) {  // strict: first maximal index wins (torch max(dim) / amax)
-        best = s;
-        bj = j;
+    for (int j0 = 0; j0 < g.nc; j0 += 8) {  // 8 score loads in flight, then scanned in class order
+      float sv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) sv[u] = (j0 + u < g.nc) ? pb[(4 + j0 + u) * As] : -INFINITY;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int j = j0 + u;
+        if (j < g.nc) {
+          const float s = sv[u];
+          if (s > best) {  // strict: first maximal index wins (torch max(dim) / amax)
+            best = s;
+            bj = j;
+          }
+          if (g.multi_label && s > g.conf) mask |= 1ull << j;
+        }
       }
-      if (g.multi_label && s > g.conf) mask |= 1ull << j;
     }
     if (!g.multi_label) mask = (best > g.conf) ? (1ull << bj) : 0ull;
     if (mask && g.classes) {
