@@ -141,16 +141,31 @@ __device__ __forceinline__ void gate_mlp(const float* __restrict__ psum, const f
                                          float* hsh, int c0, int n, float* out) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   for (int c = tid; c < C; c += 256) {
+    // the plane's partials as 8-deep batches of independent loads, accumulated in k order (the same bits as a plain
+    // k loop, which waited for each load in turn: up to 64 L2 round trips before the gate could start)
     const float* ps = psum + ((long)b * C + c) * parts;
-    float s = 0.f;
-    for (int k = 0; k < parts; ++k) s += ps[k];
-    avg[c] = s * inv_hw;
-    if (CBAM) {
-      const float* pm = pmax + ((long)b * C + c) * parts;
-      float m = -INFINITY;
-      for (int k = 0; k < parts; ++k) m = fmaxf(m, pm[k]);
-      mx[c] = m;
+    const float* pm = CBAM ? pmax + ((long)b * C + c) * parts : nullptr;
+    float s = 0.f, m = -INFINITY;
+    int k = 0;
+    for (; k + 8 <= parts; k += 8) {
+      float v[8], w[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        v[u] = ps[k + u];
+        if (CBAM) w[u] = pm[k + u];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        s += v[u];
+        if (CBAM) m = fmaxf(m, w[u]);
+      }
     }
+    for (; k < parts; ++k) {
+      s += ps[k];
+      if (CBAM) m = fmaxf(m, pm[k]);
+    }
+    avg[c] = s * inv_hw;
+    if (CBAM) mx[c] = m;
   }
   __syncthreads();
   const int nh = CBAM ? 2 * hid : hid;
@@ -166,7 +181,18 @@ __device__ __forceinline__ void gate_mlp(const float* __restrict__ psum, const f
   for (int i = tid; i < n; i += 256) {
     const int c = c0 + i;
     float za = 0.f, zm = 0.f;
-    for (int j = 0; j < hid; ++j) {
+    int j = 0;
+    for (; j + 4 <= hid; j += 4) {  // 4 weight loads in flight, accumulated in j order
+      float wv4[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) wv4[u] = w2[(long)c * hid + j + u];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        za += wv4[u] * hsh[j + u];
+        if (CBAM) zm += wv4[u] * hsh[64 + j + u];
+      }
+    }
+    for (; j < hid; ++j) {
       const float wcj = w2[(long)c * hid + j];
       za += wcj * hsh[j];
       if (CBAM) zm += wcj * hsh[64 + j];
