@@ -579,6 +579,9 @@ constexpr int PSV = 56;             // V^T planes of a head pair [128][PSV]: key
 constexpr int VPL = 128 * PSV;      // up to 63 (P = 0 there), i.e. into the next row / the K planes (finite)
 constexpr int PSO = 128 + 8;        // O planes of a head pair [64][PSO]
 constexpr int OPL = 64 * PSO;
+constexpr int QWS = 40;             // staged Q weight chunk row stride (32 k + 8; conflict-free b128 row reads)
+constexpr int QPL = 128 * QWS;      // its plane stride
+constexpr int QBUF = 2 * QPL;       // its buffer stride (two planes)
 constexpr int HALF = 128;           // channels per halo half
 constexpr int NRH = (HALF + 5) / 6; // halo steps per half (6 channels per step)
 constexpr int T_B = NR * LT * 4;
@@ -588,6 +591,7 @@ constexpr int O_B = 2 * OPL * 2;
 constexpr int WR_B = KV_B > O_B ? (KV_B > U_B ? KV_B : U_B) : (O_B > U_B ? O_B : U_B);
 constexpr int HALO_B = 54 * NRH * HPW * 4;
 static_assert(HALO_B <= U_B + WR_B, "halo patch");
+static_assert(2 * QBUF * 2 <= WR_B, "staged Q weights");
 static_assert(T_B % 16 == 0 && U_B % 16 == 0 && WR_B % 16 == 0, "16-byte aligned regions");
 static_assert(T_B + U_B + WR_B <= 160 * 1024, "LDS");
 
@@ -792,16 +796,47 @@ __global__ __launch_bounds__(NT, 1) void swin_wx_kernel(Args p) {
   const float c2 = p.scale * 1.44269504088896341f * (1.0f / (WSC * WSC));  // S = 4096 Q K^T
 #pragma unroll 1
   for (int hp = 0; hp < 2; ++hp) {
-    // Q of this wave's queries (head 2hp + lh): in_proj rows hp*128 + lh*64 + [0, 64)
+    // Q of this wave's queries (head 2hp + lh): in_proj rows hp*128 + lh*64 + [0, 64). The four waves of a head
+    // need the same Q weight planes, so the pair's 128 Q rows are staged once per workgroup through WR (free until
+    // the K / V stores) in 32-k chunks, double-buffered, instead of being streamed by every wave: the weight
+    // stream from L2 (~17 B/clk per CU here) was the Q GEMM's bound, at twice the KV GEMM's time for half its MFMAs
     f32x4 qa[1][4];
     {
-      int cbq[4];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        cbq[t] = (hp * 128 + lh * 64) / 16 + t;
-        qa[0][t] = ld_bias4(p.bin, cbq[t] * 16 + 4 * g);
+      for (int t = 0; t < 4; ++t) qa[0][t] = ld_bias4(p.bin, (hp * 128 + lh * 64 + 16 * t) + 4 * g);
+      if (hp) __syncthreads();  // the previous pair's out-projection has read its O planes (WR)
+      h16_t* QW = WR;  // [2 buf][2 plane][128 rows][QWS]
+      const int qr = (tid >> 1) & 127, qpl = tid >> 8, qh = tid & 1;
+      const h16_t* qsrc = p.win + ((long)qpl * 3 * C + hp * 128 + qr) * C + 16 * qh;
+      h16_t* qdst = QW + (qpl * 128 + qr) * QWS + 16 * qh;
+      uint4 qv0 = *reinterpret_cast<const uint4*>(qsrc), qv1 = *reinterpret_cast<const uint4*>(qsrc + 8);
+      *reinterpret_cast<uint4*>(qdst) = qv0;
+      *reinterpret_cast<uint4*>(qdst + 8) = qv1;
+      __syncthreads();
+      const h16_t* ub = UP + (qb * 16 + l15 < NR ? qb * 16 + l15 : NR - 1) * PSU + 8 * g;
+#pragma unroll 1
+      for (int kc = 0; kc < C / 32; ++kc) {
+        const int buf = kc & 1;
+        if (kc + 1 < C / 32) {  // next chunk's planes: in flight during this chunk's MFMAs
+          qv0 = *reinterpret_cast<const uint4*>(qsrc + 32 * (kc + 1));
+          qv1 = *reinterpret_cast<const uint4*>(qsrc + 32 * (kc + 1) + 8);
+        }
+        const f16x8_t bh = *reinterpret_cast<const f16x8_t*>(ub + 32 * kc);
+        const f16x8_t bl = *reinterpret_cast<const f16x8_t*>(ub + UPL + 32 * kc);
+        const h16_t* wq = QW + buf * QBUF + (lh * 64 + l15) * QWS + 8 * g;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const f16x8_t ah = *reinterpret_cast<const f16x8_t*>(wq + 16 * t * QWS);
+          const f16x8_t al = *reinterpret_cast<const f16x8_t*>(wq + QPL + 16 * t * QWS);
+          qa[0][t] = mfma_f16x3(ah, al, bh, bl, qa[0][t]);
+        }
+        if (kc + 1 < C / 32) {
+          h16_t* d = qdst + (buf ^ 1) * QBUF;
+          *reinterpret_cast<uint4*>(d) = qv0;
+          *reinterpret_cast<uint4*>(d + 8) = qv1;
+        }
+        __syncthreads();
       }
-      gemm_w<C, 4, 1, 1, PSU, UPL, true>(p.win, 3 * C, C, 0, cbq, UP, qb, qa, lane);
     }
     // K / V column block wid of the pair, all token rows
     f32x4 akv[4][2];
@@ -815,7 +850,7 @@ __global__ __launch_bounds__(NT, 1) void swin_wx_kernel(Args p) {
       }
       gemm_w<C, 2, 4, 2, PSU, UPL, true>(p.win, 3 * C, C, 0, cbkv, UP, 0, akv, lane);
     }
-    __syncthreads();  // the previous pair's out-projection has read its O planes (WR)
+    __syncthreads();  // every wave has read the staged Q planes (WR)
 #pragma unroll
     for (int rb = 0; rb < 4; ++rb) {
       const int tok = rb * 16 + l15;
