@@ -179,6 +179,7 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
   constexpr int PSK = C + 8;     // K plane row stride
   constexpr int KPL = NR * PSK;  // K plane stride
   constexpr int PSV = 72;        // V^T plane row stride (keys 0..63 + 8)
+  constexpr int QWS = 40;        // staged Q weight chunk row stride (32 k + 8)
   constexpr int VPL = C * PSV;   // V^T plane stride
   constexpr int NHS = (C + 2) / 3;
   static_assert(C == 64 && HID / 2 == C, "the plane regions are sized for C = 64 (hidden halves of 64)");
@@ -191,6 +192,7 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
   constexpr int NPAR = 3 * C + C + HID + C + 2 * C;
   static_assert(T_B % 16 == 0 && X_B % 16 == 0, "16-byte aligned regions");
   static_assert(T_B + X_B + NPAR * 4 <= 160 * 1024 / 3, "three workgroups per CU");
+  static_assert(PLN_B + 2 * 64 * QWS * 2 <= X_B, "staged Q weight chunk after the U1 planes");
   __shared__ __attribute__((aligned(16))) char smem[T_B + X_B + NPAR * 4];
   float* T = reinterpret_cast<float*>(smem);
   char* X = smem + T_B;
@@ -253,9 +255,13 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
   float dwk[9];
 #pragma unroll
   for (int i = 0; i < 9; ++i) dwk[i] = p.dw[dw_c * 9 + i];
-  // QKV weight planes of column block 0 (the first Q block): in flight during the halo store, dw conv and LN1
-  WP<C, 1> f_q;
-  load_wp(p.win, 3 * C, C, 0, 0, f_q, lane);
+  // The Q weight planes (rows 0..C of in_proj) are staged once per workgroup through X in two 32-k chunks (every
+  // wave needs all of them for its own 16 queries; streamed per wave they were 4x the Q bytes from L2): this
+  // thread's 32 bytes of both chunks are in flight during the halo store, the dw conv and LN1
+  const int qr = (tid >> 1) & 63, qpl = tid >> 7, qhf = tid & 1;
+  const h16_t* qsrc = p.win + ((long)qpl * 3 * C + qr) * C + 16 * qhf;
+  const uint4 qc0a = *reinterpret_cast<const uint4*>(qsrc), qc0b = *reinterpret_cast<const uint4*>(qsrc + 8);
+  const uint4 qc1a = *reinterpret_cast<const uint4*>(qsrc + 32), qc1b = *reinterpret_cast<const uint4*>(qsrc + 40);
 
   // ---- halo -> X (fp32 [27i + slot][HPW]) -> dw3x3 -> T (cropped / padded tokens = 0) ----
   float* halo = Q;
@@ -286,8 +292,14 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
   }
   __syncthreads();
 
-  // ---- LN1 -> X planes ----
+  // ---- LN1 -> X planes; Q weight chunk 0 -> X after the U1 planes (the halo there has been read) ----
   ln_planes<C, LT, PS, PL>(T, P, p.ln1_eps, tid);
+  h16_t* QW = P + 2 * PL;  // [2 plane][64 rows][QWS]
+  h16_t* qdst = QW + (qpl * 64 + qr) * QWS + 16 * qhf;
+  *reinterpret_cast<uint4*>(qdst) = qc0a;
+  *reinterpret_cast<uint4*>(qdst + 8) = qc0b;
+  WP<C, 1> f_q;  // K weight planes of column block wid
+  load_wp(p.win, 3 * C, C, 0, C / 16 + wid, f_q, lane);
   __syncthreads();
 
   // ---- QKV = U1 Win'^T + b_in' (weight planes hold 64 W). Wave w computes Q of its own 16 query rows (four column
@@ -306,28 +318,32 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
       ua[s2][0] = *reinterpret_cast<const f16x8_t*>(ar);
       ua[s2][1] = *reinterpret_cast<const f16x8_t*>(ar + PL);
     }
-    WP<C, 1> f_n;
+    WP<C, 1> f_n;  // V weight planes of column block wid
+    load_wp(p.win, 3 * C, C, 0, 2 * C / 16 + wid, f_n, lane);
 #pragma unroll
-    for (int cq = 0; cq < C / 16; ++cq) {
-      load_wp(p.win, 3 * C, C, 0, cq + 1 < C / 16 ? cq + 1 : C / 16 + wid, f_n, lane);
-      f32x4 c = *reinterpret_cast<const f32x4*>(par + P_BIN + cq * 16 + 4 * g);
+    for (int cq = 0; cq < C / 16; ++cq) qa[cq] = *reinterpret_cast<const f32x4*>(par + P_BIN + cq * 16 + 4 * g);
+    static_assert(C == 64, "two 32-k chunks");
 #pragma unroll
-      for (int s2 = 0; s2 < C / 32; ++s2) {
-        c = mfma16(f_q.v[0][s2][1], ua[s2][0], c);
-        c = mfma16(f_q.v[0][s2][0], ua[s2][1], c);
-        c = mfma16(f_q.v[0][s2][0], ua[s2][0], c);
+    for (int s2 = 0; s2 < C / 32; ++s2) {
+      if (s2 == 1) {
+        __syncthreads();  // every wave has read chunk 0
+        *reinterpret_cast<uint4*>(qdst) = qc1a;
+        *reinterpret_cast<uint4*>(qdst + 8) = qc1b;
+        __syncthreads();
       }
-      qa[cq] = c;
-      f_q = f_n;
+      const h16_t* wq = QW + l15_ * QWS + 8 * g;
+#pragma unroll
+      for (int cq = 0; cq < C / 16; ++cq)
+        qa[cq] = mfma_f16x3(*reinterpret_cast<const f16x8_t*>(wq + cq * 16 * QWS),
+                            *reinterpret_cast<const f16x8_t*>(wq + 64 * QWS + cq * 16 * QWS), ua[s2][0], ua[s2][1],
+                            qa[cq]);
     }
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      if (j == 0) load_wp(p.win, 3 * C, C, 0, 2 * C / 16 + wid, f_n, lane);
       const f32x4 b = *reinterpret_cast<const f32x4*>(par + P_BIN + ((j + 1) * C / 16 + wid) * 16 + 4 * g);
 #pragma unroll
       for (int rb = 0; rb < 4; ++rb) akv[j][rb][0] = b;
-      gemm_x3<C, 1, PS, PL>(P, f_q, akv[j], lane);
-      if (j == 0) f_q = f_n;
+      gemm_x3<C, 1, PS, PL>(P, j == 0 ? f_q : f_n, akv[j], lane);
     }
   }
   WP<C, 1> f_o;
