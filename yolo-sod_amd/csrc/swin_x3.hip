@@ -707,6 +707,18 @@ __device__ __forceinline__ void ln_planes8(const float* T, h16_t* U, float eps, 
   }
 }
 
+#ifdef YS_DIAG_STAMPS  // diagnostic builds only (scripts/diag_wx.sh): per-stage s_memtime of wave 0 of the first 256 windows
+__device__ unsigned long long ys_wx_stamps[256 * 32];
+#define WX_STAMP(k)                                                                                                  \
+  do {                                                                                                               \
+    if (threadIdx.x == 0 && blockIdx.x < 256) ys_wx_stamps[blockIdx.x * 32 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define WX_STAMP(k) \
+  do {              \
+  } while (0)
+#endif
+
 __device__ __forceinline__ f32x4 ld_bias4(const float* b, int n) { return *reinterpret_cast<const f32x4*>(b + n) * WSC; }
 
 __global__ __launch_bounds__(NT, 1) void swin_wx_kernel(Args p) {
@@ -761,6 +773,7 @@ __global__ __launch_bounds__(NT, 1) void swin_wx_kernel(Args p) {
                                                   rx, i == NRH - 1 ? vlast : voff, (hf * HALF + 6 * i) * HWi * 4, 0));
   }
   const int lh = wid >> 2, qb = wid & 3;  // attention: (local head, 16-query block)
+  WX_STAMP(0);
 
   // ---- depthwise 3x3 per channel half: halo -> LDS [c][py][HPW] -> T (cropped / padded tokens = 0) ----
   const int dc = tid % HALF;
@@ -797,8 +810,10 @@ __global__ __launch_bounds__(NT, 1) void swin_wx_kernel(Args p) {
     }
   }
   __syncthreads();
+  WX_STAMP(1);
   ln_planes8(T, UP, p.ln1_eps, tid);
   __syncthreads();
+  WX_STAMP(2);
 
   // ---- attention on head pairs; out-projection partials (this wave's column blocks wid, wid + 8) in registers ----
   const int cbo[2] = {wid, wid + 8};
@@ -854,6 +869,7 @@ __global__ __launch_bounds__(NT, 1) void swin_wx_kernel(Args p) {
         __syncthreads();
       }
     }
+    WX_STAMP(3 + 6 * hp);
     // K / V column block wid of the pair, all token rows
     f32x4 akv[4][2];
     {
@@ -866,7 +882,9 @@ __global__ __launch_bounds__(NT, 1) void swin_wx_kernel(Args p) {
       }
       gemm_w<C, 2, 4, 2, PSU, UPL, true>(p.win, 3 * C, C, 0, cbkv, UP, 0, akv, lane);
     }
+    WX_STAMP(4 + 6 * hp);
     __syncthreads();  // every wave has read the staged Q planes (WR)
+    WX_STAMP(5 + 6 * hp);
 #pragma unroll
     for (int rb = 0; rb < 4; ++rb) {
       const int tok = rb * 16 + l15;
@@ -897,6 +915,7 @@ __global__ __launch_bounds__(NT, 1) void swin_wx_kernel(Args p) {
       ql[s] = __builtin_bit_cast(f16x8_t, make_uint4(l0.x, l0.y, l1.x, l1.y));
     }
     __syncthreads();  // K / V^T planes complete
+    WX_STAMP(6 + 6 * hp);
     f32x4 ov[HD / 16];
     {
       f32x4 st[4];
@@ -963,11 +982,13 @@ __global__ __launch_bounds__(NT, 1) void swin_wx_kernel(Args p) {
       for (int db = 0; db < HD / 16; ++db) ov[db] *= inv;
     }
     __syncthreads();  // every wave has read K / V^T
+    WX_STAMP(7 + 6 * hp);
 #pragma unroll
     for (int db = 0; db < HD / 16; ++db)
       store_planes4<PSO, OPL>(Op, qb * 16 + l15, lh * HD + db * 16 + 4 * g, ov[db]);
     __syncthreads();
     gemm_w<128, 2, 4, 2, PSO, OPL, false>(p.wo, C, C, hp * 128, cbo, Op, 0, acc_o, lane);
+    WX_STAMP(8 + 6 * hp);
   }
   // T += O Wo^T + bo (this wave's column blocks; rows < 49)
 #pragma unroll
@@ -984,6 +1005,7 @@ __global__ __launch_bounds__(NT, 1) void swin_wx_kernel(Args p) {
   __syncthreads();
   ln_planes8(T, UP, p.ln2_eps, tid);
   __syncthreads();
+  WX_STAMP(15);
 
   // ---- MLP in two hidden chunks of 256: GELU(U2 W1c'^T + b1c') -> WR planes -> MLP2 partial in registers ----
   f32x4 acc_m[4][2];
@@ -1004,6 +1026,7 @@ __global__ __launch_bounds__(NT, 1) void swin_wx_kernel(Args p) {
       for (int rb = 0; rb < 4; ++rb) ah[rb][j] = b;
     }
     gemm_w<C, 2, 4, 2, PSU, UPL, true>(p.w1, HID, C, 0, cb1, UP, 0, ah, lane);
+    WX_STAMP(16 + 3 * ck);
     __syncthreads();  // the previous chunk's MLP2 has read WR
 #pragma unroll
     for (int rb = 0; rb < 4; ++rb) {
@@ -1017,7 +1040,9 @@ __global__ __launch_bounds__(NT, 1) void swin_wx_kernel(Args p) {
       }
     }
     __syncthreads();
+    WX_STAMP(17 + 3 * ck);
     gemm_w<C, 2, 4, 2, PSU, UPL, true>(p.w2, C, HID, ck * 256, cbo, Hp, 0, acc_m, lane);
+    WX_STAMP(18 + 3 * ck);
   }
   // final T = T + MLP -> U planes (the pw GEMM's operand); every wave has read U2 (MLP1 of the last chunk)
 #pragma unroll
@@ -1057,12 +1082,14 @@ __global__ __launch_bounds__(NT, 1) void swin_wx_kernel(Args p) {
     sh[j] = *reinterpret_cast<const f32x4*>(p.bn_shift + cbo[j] * 16 + 4 * g);
   }
   __syncthreads();
+  WX_STAMP(22);
   f32x4 acc[4][2];
 #pragma unroll
   for (int tb = 0; tb < 4; ++tb)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[tb][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   gemm_w<C, 2, 4, 2, PSU, UPL, true>(p.wpw, C, C, 0, cbo, UP, 0, acc, lane);
+  WX_STAMP(23);
 #pragma unroll
   for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -1072,6 +1099,7 @@ __global__ __launch_bounds__(NT, 1) void swin_wx_kernel(Args p) {
         __builtin_amdgcn_raw_buffer_store_b32(
             __builtin_bit_cast(unsigned, xr[j][tb][r] + silu_fast_(acc[tb][j][r] * sc[j][r] + sh[j][r])), ry,
             vtok[tb], (128 * j + r) * HWi * 4, 0);
+  WX_STAMP(24);
 }
 }  // namespace wx
 
@@ -1213,3 +1241,9 @@ int yolosod_swin_x3_launch(const float* x, float* y, int B, int C, int H, int W,
   }
   return 1;
 }
+
+#ifdef YS_DIAG_STAMPS
+YS_EXPORT int yolosod_diag_wx_stamps(unsigned long long* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(x3::wx::ys_wx_stamps), sizeof(x3::wx::ys_wx_stamps)) == hipSuccess ? 0 : -1;
+}
+#endif
