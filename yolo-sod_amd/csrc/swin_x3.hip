@@ -93,7 +93,8 @@ struct WP {
 template <int K, int NJ>
 __device__ __forceinline__ void load_wp(const h16_t* __restrict__ Wp, int N, int KT, int koff, int cb0, WP<K, NJ>& f,
                                         int lane) {
-  const int l15 = lane & 15, g = lane >> 4;
+  // fragment-major planes (swin_x3_prep_kernel): the 64 lanes' fragments of one (column block, 32-k step) are 1 KB
+  // contiguous, so a wave-instruction reads 8 whole cache lines (16 half lines row-major)
 #pragma unroll
   for (int p = 0; p < 2; ++p)
 #pragma unroll
@@ -101,7 +102,7 @@ __device__ __forceinline__ void load_wp(const h16_t* __restrict__ Wp, int N, int
 #pragma unroll
       for (int j = 0; j < NJ; ++j)
         f.v[j][s][p] = *reinterpret_cast<const f16x8_t*>(
-            Wp + ((long)p * N + (cb0 + 4 * j) * 16 + l15) * KT + koff + 32 * s + 8 * g);
+            Wp + (long)p * N * KT + ((long)((cb0 + 4 * j) * (KT / 32) + koff / 32 + s) * 64 + lane) * 8);
 }
 
 // acc[rb][j] += (A[rows rb*16 .. +15][0, K) . W^T)^T: A = three LDS planes (row stride PS, plane stride PL), the
@@ -179,7 +180,6 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
   constexpr int PSK = C + 8;     // K plane row stride
   constexpr int KPL = NR * PSK;  // K plane stride
   constexpr int PSV = 72;        // V^T plane row stride (keys 0..63 + 8)
-  constexpr int QWS = 40;        // staged Q weight chunk row stride (32 k + 8)
   constexpr int VPL = C * PSV;   // V^T plane stride
   constexpr int NHS = (C + 2) / 3;
   static_assert(C == 64 && HID / 2 == C, "the plane regions are sized for C = 64 (hidden halves of 64)");
@@ -192,7 +192,7 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
   constexpr int NPAR = 3 * C + C + HID + C + 2 * C;
   static_assert(T_B % 16 == 0 && X_B % 16 == 0, "16-byte aligned regions");
   static_assert(T_B + X_B + NPAR * 4 <= 160 * 1024 / 3, "three workgroups per CU");
-  static_assert(PLN_B + 2 * 64 * QWS * 2 <= X_B, "staged Q weight chunk after the U1 planes");
+  static_assert(PLN_B + 8 * 512 * 2 <= X_B, "staged Q weight chunk after the U1 planes");
   __shared__ __attribute__((aligned(16))) char smem[T_B + X_B + NPAR * 4];
   float* T = reinterpret_cast<float*>(smem);
   char* X = smem + T_B;
@@ -258,10 +258,12 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
   // The Q weight planes (rows 0..C of in_proj) are staged once per workgroup through X in two 32-k chunks (every
   // wave needs all of them for its own 16 queries; streamed per wave they were 4x the Q bytes from L2): this
   // thread's 32 bytes of both chunks are in flight during the halo store, the dw conv and LN1
-  const int qr = (tid >> 1) & 63, qpl = tid >> 7, qhf = tid & 1;
-  const h16_t* qsrc = p.win + ((long)qpl * 3 * C + qr) * C + 16 * qhf;
+  // chunk s = the fragment blocks (plane, Q column block cq) of k step s: 8 blocks of 512 halves; thread t copies
+  // halves 16 (t & 31) .. +15 of block t >> 5
+  const int qblk = tid >> 5, qpl = qblk >> 2, qcb = qblk & 3;
+  const h16_t* qsrc = p.win + (long)qpl * 3 * C * C + (long)(qcb * (C / 32)) * 512 + 16 * (tid & 31);
   const uint4 qc0a = *reinterpret_cast<const uint4*>(qsrc), qc0b = *reinterpret_cast<const uint4*>(qsrc + 8);
-  const uint4 qc1a = *reinterpret_cast<const uint4*>(qsrc + 32), qc1b = *reinterpret_cast<const uint4*>(qsrc + 40);
+  const uint4 qc1a = *reinterpret_cast<const uint4*>(qsrc + 512), qc1b = *reinterpret_cast<const uint4*>(qsrc + 520);
 
   // ---- halo -> X (fp32 [27i + slot][HPW]) -> dw3x3 -> T (cropped / padded tokens = 0) ----
   float* halo = Q;
@@ -294,8 +296,8 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
 
   // ---- LN1 -> X planes; Q weight chunk 0 -> X after the U1 planes (the halo there has been read) ----
   ln_planes<C, LT, PS, PL>(T, P, p.ln1_eps, tid);
-  h16_t* QW = P + 2 * PL;  // [2 plane][64 rows][QWS]
-  h16_t* qdst = QW + (qpl * 64 + qr) * QWS + 16 * qhf;
+  h16_t* QW = P + 2 * PL;  // [2 plane][4 column block][64 lanes][8]
+  h16_t* qdst = QW + qblk * 512 + 16 * (tid & 31);
   *reinterpret_cast<uint4*>(qdst) = qc0a;
   *reinterpret_cast<uint4*>(qdst + 8) = qc0b;
   WP<C, 1> f_q;  // K weight planes of column block wid
@@ -331,12 +333,11 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
         *reinterpret_cast<uint4*>(qdst + 8) = qc1b;
         __syncthreads();
       }
-      const h16_t* wq = QW + l15_ * QWS + 8 * g;
+      const h16_t* wq = QW + lane * 8;
 #pragma unroll
       for (int cq = 0; cq < C / 16; ++cq)
-        qa[cq] = mfma_f16x3(*reinterpret_cast<const f16x8_t*>(wq + cq * 16 * QWS),
-                            *reinterpret_cast<const f16x8_t*>(wq + 64 * QWS + cq * 16 * QWS), ua[s2][0], ua[s2][1],
-                            qa[cq]);
+        qa[cq] = mfma_f16x3(*reinterpret_cast<const f16x8_t*>(wq + cq * 512),
+                            *reinterpret_cast<const f16x8_t*>(wq + (4 + cq) * 512), ua[s2][0], ua[s2][1], qa[cq]);
     }
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -595,9 +596,7 @@ constexpr int PSV = 56;             // V^T planes of a head pair [128][PSV]: key
 constexpr int VPL = 128 * PSV;      // up to 63 (P = 0 there), i.e. into the next row / the K planes (finite)
 constexpr int PSO = 128 + 8;        // O planes of a head pair [64][PSO]
 constexpr int OPL = 64 * PSO;
-constexpr int QWS = 40;             // staged Q weight chunk row stride (32 k + 8; conflict-free b128 row reads)
-constexpr int QPL = 128 * QWS;      // its plane stride
-constexpr int QBUF = 2 * QPL;       // its buffer stride (two planes)
+constexpr int QBUF = 2 * 8 * 512;   // staged Q weight fragments of one 32-k step (2 planes x 8 column blocks)
 constexpr int HALF = 128;           // channels per halo half
 constexpr int NRH = (HALF + 5) / 6; // halo steps per half (6 channels per step)
 constexpr int T_B = NR * LT * 4;
@@ -621,9 +620,9 @@ __device__ __forceinline__ void gemm_w(const h16_t* __restrict__ Wp, int N, int 
   constexpr int NST = K / (32 * KS);
   static_assert(K % (32 * KS) == 0, "k steps");
   const long pst = (long)N * KT;
-  const h16_t* wr[NJ];
+  const h16_t* wr[NJ];  // fragment-major planes: (column block, 32-k step) fragments are 1 KB contiguous
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) wr[j] = Wp + (long)(cb[j] * 16 + l15) * KT + koff + 8 * g;
+  for (int j = 0; j < NJ; ++j) wr[j] = Wp + ((long)(cb[j] * (KT / 32) + koff / 32) * 64 + lane) * 8;
   const h16_t* ar[NRB];
 #pragma unroll
   for (int rb = 0; rb < NRB; ++rb) {
@@ -639,7 +638,7 @@ __device__ __forceinline__ void gemm_w(const h16_t* __restrict__ Wp, int N, int 
       for (int j = 0; j < NJ; ++j)
 #pragma unroll
         for (int p = 0; p < 2; ++p)
-          w[ks][j][p] = *reinterpret_cast<const f16x8_t*>(wr[j] + p * pst + 32 * (st * KS + ks));
+          w[ks][j][p] = *reinterpret_cast<const f16x8_t*>(wr[j] + p * pst + 512 * (st * KS + ks));
   };
   auto mma = [&](const f16x8_t (&w)[KS][NJ][2], int st) {
 #pragma unroll
@@ -836,10 +835,10 @@ __global__ __launch_bounds__(NT, 1) void swin_wx_kernel(Args p) {
 #pragma unroll
       for (int t = 0; t < 4; ++t) qa[0][t] = ld_bias4(p.bin, (hp * 128 + lh * 64 + 16 * t) + 4 * g);
       if (hp) __syncthreads();  // the previous pair's out-projection has read its O planes (WR)
-      h16_t* QW = WR;  // [2 buf][2 plane][128 rows][QWS]
-      const int qr = (tid >> 1) & 127, qpl = tid >> 8, qh = tid & 1;
-      const h16_t* qsrc = p.win + ((long)qpl * 3 * C + hp * 128 + qr) * C + 16 * qh;
-      h16_t* qdst = QW + (qpl * 128 + qr) * QWS + 16 * qh;
+      h16_t* QW = WR;  // [2 buf][2 plane][8 column block][64 lanes][8]: the fragment blocks of one 32-k step
+      const int qblk = tid >> 5, qpl = qblk >> 3, qcb = qblk & 7;
+      const h16_t* qsrc = p.win + (long)qpl * 3 * C * C + (long)((hp * 8 + qcb) * (C / 32)) * 512 + 16 * (tid & 31);
+      h16_t* qdst = QW + qblk * 512 + 16 * (tid & 31);
       uint4 qv0 = *reinterpret_cast<const uint4*>(qsrc), qv1 = *reinterpret_cast<const uint4*>(qsrc + 8);
       *reinterpret_cast<uint4*>(qdst) = qv0;
       *reinterpret_cast<uint4*>(qdst + 8) = qv1;
@@ -849,16 +848,16 @@ __global__ __launch_bounds__(NT, 1) void swin_wx_kernel(Args p) {
       for (int kc = 0; kc < C / 32; ++kc) {
         const int buf = kc & 1;
         if (kc + 1 < C / 32) {  // next chunk's planes: in flight during this chunk's MFMAs
-          qv0 = *reinterpret_cast<const uint4*>(qsrc + 32 * (kc + 1));
-          qv1 = *reinterpret_cast<const uint4*>(qsrc + 32 * (kc + 1) + 8);
+          qv0 = *reinterpret_cast<const uint4*>(qsrc + 512 * (kc + 1));
+          qv1 = *reinterpret_cast<const uint4*>(qsrc + 512 * (kc + 1) + 8);
         }
         const f16x8_t bh = *reinterpret_cast<const f16x8_t*>(ub + 32 * kc);
         const f16x8_t bl = *reinterpret_cast<const f16x8_t*>(ub + UPL + 32 * kc);
-        const h16_t* wq = QW + buf * QBUF + (lh * 64 + l15) * QWS + 8 * g;
+        const h16_t* wq = QW + buf * QBUF + (lh * 4) * 512 + lane * 8;
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-          const f16x8_t ah = *reinterpret_cast<const f16x8_t*>(wq + 16 * t * QWS);
-          const f16x8_t al = *reinterpret_cast<const f16x8_t*>(wq + QPL + 16 * t * QWS);
+          const f16x8_t ah = *reinterpret_cast<const f16x8_t*>(wq + t * 512);
+          const f16x8_t al = *reinterpret_cast<const f16x8_t*>(wq + 8 * 512 + t * 512);
           qa[0][t] = mfma_f16x3(ah, al, bh, bl, qa[0][t]);
         }
         if (kc + 1 < C / 32) {
@@ -1155,8 +1154,11 @@ __global__ __launch_bounds__(256) void swin_x3_prep_kernel(PrepArgs a) {
     const float v = gam ? w * gam[k] : w;
     const _Float16 h = (_Float16)(v * WSC);
     const _Float16 l = (_Float16)(v * WSC - (float)h);
-    dst[(long)n * K + k] = __builtin_bit_cast(h16_t, h);
-    dst[((long)N + n) * K + k] = __builtin_bit_cast(h16_t, l);
+    // fragment-major: element (n, k) at ((n/16 * K/32 + k/32) * 64 + (k%32)/8 * 16 + n%16) * 8 + k%8, so the 64
+    // lanes' MFMA fragments of one (column block, 32-k step) are 1 KB contiguous
+    const long fi = ((long)((n >> 4) * (K >> 5) + (k >> 5)) * 64 + (((k & 31) >> 3) << 4) + (n & 15)) * 8 + (k & 7);
+    dst[fi] = __builtin_bit_cast(h16_t, h);
+    dst[(long)N * K + fi] = __builtin_bit_cast(h16_t, l);
   }
   if (bdst) {
     bacc = wave_sum(bacc);
