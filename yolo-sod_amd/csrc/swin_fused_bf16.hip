@@ -73,8 +73,10 @@ __device__ __forceinline__ f32x4 mfma_b(bf16x8_t a, bf16x8_t b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
-// weight fragments of W [N][K] (bf16, row-major) for this wave's column blocks cb = wid + 4j:
-// lane (g, l15) holds W[cb*16 + l15][32s + 8g .. +7] for every k-step s
+// weight fragments of W [N][K] for this wave's column blocks cb = wid + 4j: lane (g, l15) holds
+// W[cb*16 + l15][32s + 8g .. +7] for every k-step s. W is the fragment-major copy swin_wfrag_kernel writes (the 64
+// lanes' fragments of one (column block, k-step) are 1 KB contiguous, so a wave-instruction reads 8 whole cache
+// lines; row-major it read 16 half lines, and the per-window weight stream L2 -> CU bounds the GEMM stages)
 template <int K, int NJ>
 struct BFrag {
   bf16x8_t v[NJ][K / 32];
@@ -82,12 +84,11 @@ struct BFrag {
 
 template <int K, int NJ>
 __device__ __forceinline__ void load_bfrag(const bf16_t* __restrict__ Wg, BFrag<K, NJ>& f, int wid, int lane) {
-  const int l15 = lane & 15, g = lane >> 4;
 #pragma unroll
   for (int s = 0; s < K / 32; ++s)
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
-      f.v[j][s] = *reinterpret_cast<const bf16x8_t*>(Wg + (long)((wid + 4 * j) * 16 + l15) * K + 32 * s + 8 * g);
+      f.v[j][s] = *reinterpret_cast<const bf16x8_t*>(Wg + ((long)((wid + 4 * j) * (K / 32) + s) * 64 + lane) * 8);
 }
 
 // acc[rb][j] += A[rows rb*16 .. +15][0..K) . W^T for the wave's column blocks (A: LDS bf16, row stride lda; the
@@ -506,7 +507,7 @@ __global__ __launch_bounds__(256, 2) void swin_fused_bf16_kernel(SwinBArgs p) {
   for (int j = 0; j < NCB_PW; ++j)
 #pragma unroll
     for (int s = 0; s < C / 32; ++s)
-      wa[j][s] = *reinterpret_cast<const bf16x8_t*>(p.wpw + (long)((wid + 4 * j) * 16 + l15) * C + 32 * s + 8 * g);
+      wa[j][s] = *reinterpret_cast<const bf16x8_t*>(p.wpw + ((long)((wid + 4 * j) * (C / 32) + s) * 64 + lane) * 8);
   // residual x and the y stores: buffer ops on per-image descriptors; a lane's voffset is fixed (channel row 4g of
   // block wid, its token) and out-of-window / cropped tokens get an out-of-range voffset (loads return 0, stores are
   // dropped), so there is no per-element branch (a branch per load serialised them behind s_waitcnt vmcnt(0))
@@ -589,9 +590,36 @@ __global__ __launch_bounds__(256, 2) void swin_fused_bf16_kernel(SwinBArgs p) {
   }
 }
 
+// fragment-major copies of the five weight matrices: thread = one 8-element run W[n][k..k+7] (16 B in, 16 B out);
+// element (n, k) of W [N][K] lands at ((n/16 * K/32 + k/32) * 64 + (k%32)/8 * 16 + n%16) * 8 + k%8
+struct WFragArgs {
+  const bf16_t* src[5];
+  bf16_t* dst[5];
+  int N[5], K[5];
+  long end[5];  // cumulative 8-element run counts
+};
+
+__global__ void __launch_bounds__(256) swin_wfrag_kernel(WFragArgs a) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.end[4]) return;
+  int m = 0;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) m += (i >= a.end[t]) ? 1 : 0;
+  const long r = i - (m ? a.end[m - 1] : 0);
+  const int K = a.K[m], k8 = K / 8;
+  const int n = (int)(r / k8), k = (int)(r % k8) * 8;
+  const bf16x8_t v = *reinterpret_cast<const bf16x8_t*>(a.src[m] + (long)n * K + k);
+  const long o = ((long)((n >> 4) * (K / 32) + (k >> 5)) * 64 + ((k & 31) >> 3) * 16 + (n & 15)) * 8;
+  *reinterpret_cast<bf16x8_t*>(a.dst[m] + o) = v;
+}
+
 }  // namespace ys
 
 using namespace ys;
+
+size_t yolosod_swin_fused_bf16_wfrag_elems(int C, int mlp_hidden) {
+  return (size_t)5 * C * C + (size_t)2 * C * mlp_hidden;
+}
 
 // shapes the fused bf16 kernel takes: 7x7 windows, C 64 (2 heads) / 128 (2 or 4 heads), MLP hidden 2C
 bool yolosod_swin_fused_bf16_ok(int C, int num_heads, int wh, int ww, int mlp_hidden) {
@@ -607,10 +635,26 @@ int yolosod_swin_fused_bf16_launch(const bf16_t* x, bf16_t* y, int B, int C, int
                                    const bf16_t* out_proj_w, const float* out_proj_b, const float* ln2_w,
                                    const float* ln2_b, float ln2_eps, const bf16_t* mlp1_w, const float* mlp1_b,
                                    int mlp_hidden, const bf16_t* mlp2_w, const float* mlp2_b, const bf16_t* pw_w,
-                                   const float* bn_scale, const float* bn_shift, hipStream_t st) {
+                                   const float* bn_scale, const float* bn_shift, bf16_t* wfrag, hipStream_t st) {
   if (!yolosod_swin_fused_bf16_ok(C, num_heads, wh, ww, mlp_hidden) || (long)B * nWin >= (1L << 31)) return 0;
-  SwinBArgs a{x, y, B, H, W, nWx, nWin, dw_w, ln1_w, ln1_b, ln1_eps, in_proj_w, in_proj_b, out_proj_w, out_proj_b,
-              ln2_w, ln2_b, ln2_eps, mlp1_w, mlp1_b, mlp2_w, mlp2_b, pw_w, bn_scale, bn_shift,
+  // weight planes in fragment-major order (wfrag: yolosod_swin_fused_bf16_wfrag_elems(C, hid) bf16)
+  const int hid = mlp_hidden;
+  WFragArgs fa{};
+  const bf16_t* srcs[5] = {in_proj_w, out_proj_w, mlp1_w, mlp2_w, pw_w};
+  const int Ns[5] = {3 * C, C, hid, C, C}, Ks[5] = {C, C, C, hid, C};
+  long run = 0, off = 0;
+  for (int t = 0; t < 5; ++t) {
+    fa.src[t] = srcs[t];
+    fa.dst[t] = wfrag + off;
+    fa.N[t] = Ns[t];
+    fa.K[t] = Ks[t];
+    run += (long)Ns[t] * Ks[t] / 8;
+    fa.end[t] = run;
+    off += (long)Ns[t] * Ks[t];
+  }
+  hipLaunchKernelGGL(swin_wfrag_kernel, dim3((unsigned)((run + 255) / 256)), dim3(256), 0, st, fa);
+  SwinBArgs a{x, y, B, H, W, nWx, nWin, dw_w, ln1_w, ln1_b, ln1_eps, fa.dst[0], in_proj_b, fa.dst[1], out_proj_b,
+              ln2_w, ln2_b, ln2_eps, fa.dst[2], mlp1_b, fa.dst[3], mlp2_b, fa.dst[4], bn_scale, bn_shift,
               1.0f / sqrtf((float)(C / num_heads))};
   const long nwin = (long)B * nWin;
   const dim3 grid((unsigned)(8 * ((nwin + 7) / 8)));

@@ -363,7 +363,8 @@ int yolosod_swin_fused_bf16_launch(const bf16_t* x, bf16_t* y, int B, int C, int
                                    const bf16_t* out_proj_w, const float* out_proj_b, const float* ln2_w,
                                    const float* ln2_b, float ln2_eps, const bf16_t* mlp1_w, const float* mlp1_b,
                                    int mlp_hidden, const bf16_t* mlp2_w, const float* mlp2_b, const bf16_t* pw_w,
-                                   const float* bn_scale, const float* bn_shift, hipStream_t st);
+                                   const float* bn_scale, const float* bn_shift, bf16_t* wfrag, hipStream_t st);
+size_t yolosod_swin_fused_bf16_wfrag_elems(int C, int mlp_hidden);
 
 // =================================================================================================
 // C ABI (bf16 storage: activations / GEMM weights are bf16 bit patterns, other parameters fp32)
@@ -393,9 +394,11 @@ YS_EXPORT int yolosod_attention_bf16(const bf16_t* qkv, bf16_t* out, long n_seq,
 
 YS_EXPORT size_t yolosod_swin_workspace_bf16(int B, int C, int H, int W, int num_heads, int window, int mlp_hidden) {
   SwinGeomB g = swin_geom_b(B, H, W, window);
-  if (yolosod_swin_fused_bf16_ok(C, num_heads, g.wh, g.ww, mlp_hidden)) {  // fused per-window kernel: folded BN only
+  if (yolosod_swin_fused_bf16_ok(C, num_heads, g.wh, g.ww, mlp_hidden)) {
+    // fused per-window kernel: folded BN and the fragment-major weight copies
     Sizer s;
     s.take<float>((size_t)C * 2);
+    s.take<bf16_t>(yolosod_swin_fused_bf16_wfrag_elems(C, mlp_hidden));
     return s.off;
   }
   const int wide = (3 * C > mlp_hidden) ? 3 * C : mlp_hidden;
@@ -432,13 +435,14 @@ YS_EXPORT int yolosod_swin_forward_bf16(const bf16_t* x, bf16_t* y, int B, int C
   if (yolosod_swin_fused_bf16_ok(C, num_heads, g.wh, g.ww, mlp_hidden)) {
     Carver cf(workspace, workspace_bytes);
     float* fold = cf.take<float>((size_t)C * 2);
-    YS_CHECK_ARG(fold, "swin_bf16: workspace too small (%zu)", workspace_bytes);
+    bf16_t* wfrag = cf.take<bf16_t>(yolosod_swin_fused_bf16_wfrag_elems(C, mlp_hidden));
+    YS_CHECK_ARG(fold && wfrag, "swin_bf16: workspace too small (%zu)", workspace_bytes);
     hipLaunchKernelGGL(fold_bn_bf16_kernel, dim3((C + 255) / 256), dim3(256), 0, st, bn_w, bn_b, bn_mean, bn_var,
                        bn_eps, C, fold, fold + C);
     const int r = yolosod_swin_fused_bf16_launch(x, y, B, C, H, W, num_heads, g.wh, g.ww, g.nWx, g.nWin, dw_w, ln1_w,
                                                  ln1_b, ln1_eps, in_proj_w, in_proj_b, out_proj_w, out_proj_b, ln2_w,
                                                  ln2_b, ln2_eps, mlp1_w, mlp1_b, mlp_hidden, mlp2_w, mlp2_b, pw_w, fold,
-                                                 fold + C, st);
+                                                 fold + C, wfrag, st);
     if (r < 0) return -1;
     if (r == 1) return 0;
   }
