@@ -5,6 +5,8 @@ count multiply-adds as 2. These are the numerators of ``roofline.achieved`` in b
 """
 from __future__ import annotations
 
+import os
+
 F32 = 4
 
 # MI355X peaks (MI355X_MICROARCH.md "Chip-level parameters" / "Matrix cores"): dense, no sparsity
@@ -21,6 +23,24 @@ def elem_size(key) -> int:
 def peak_tflops(key) -> float:
     """Matrix-core peak of the arithmetic the launch runs: bf16 MFMA for bf16 activations, fp32 MFMA otherwise."""
     return PEAK_BF16_MFMA_TFLOPS if elem_size(key) == 2 else PEAK_FP32_MFMA_TFLOPS
+
+
+def _on(name: str) -> bool:
+    return os.environ.get(name, "1") != "0"
+
+
+def method_peak_tflops(key) -> float:
+    """Matrix-core ceiling of the METHOD an fp32 launch runs its matrix products with: the fp32 Swin (C 64 / 256),
+    A2 and head kernels compute each fp32 product as 3 fp16 MFMA products of two-term splits (csrc/swin_x3.hip,
+    gemm_f32.h X2, detect_head_x2_kernel), so their ceiling is the fp16 peak / 3; everything else keeps
+    peak_tflops. Reported beside the dtype-peak fractions, never instead of them."""
+    if elem_size(key) == 4:
+        op = key[0]
+        split = ((op == "swin" and key[1][1] in (64, 256) and _on("YOLOSOD_SWIN_X3"))
+                 or (op == "a2" and _on("YOLOSOD_A2_X2")) or (op == "head" and _on("YOLOSOD_HEAD_X2")))
+        if split:
+            return PEAK_BF16_MFMA_TFLOPS / 3
+    return peak_tflops(key)
 
 
 # operators of the SURVEY 8(a) path (rooflined); other keys the op_timer records are backbone conv kernels
@@ -101,6 +121,8 @@ def bound_of(key) -> str:
     return "mfma" if flops / (peak_tflops(key) * 1e12) > nbytes / (PEAK_HBM_GBS * 1e9) else "hbm"
 
 
-def t_min_ms(key) -> float:
+def t_min_ms(key, method: bool = False) -> float:
+    """max(HBM time, matrix time) at the dtype peak, or (method=True) at the method ceiling method_peak_tflops."""
     nbytes, flops = op_cost(key)
-    return max(nbytes / (PEAK_HBM_GBS * 1e9), flops / (peak_tflops(key) * 1e12)) * 1e3
+    peak = method_peak_tflops(key) if method else peak_tflops(key)
+    return max(nbytes / (PEAK_HBM_GBS * 1e9), flops / (peak * 1e12)) * 1e3
