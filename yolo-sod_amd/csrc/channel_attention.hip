@@ -285,6 +285,15 @@ __global__ __launch_bounds__(256) void cbam_pixel_stats_kernel(const T* __restri
   const int b = blockIdx.z, g = blockIdx.y, G = gridDim.y;
   const int c0 = g * CG;
   const int c1 = (c0 + CG < C) ? c0 + CG : C;
+  const long p = ((long)blockIdx.x * 256 + threadIdx.x) * V;
+  // the first 8 channels' loads go out before the gate MLP (they do not depend on it), so its latency chain
+  // overlaps them instead of preceding them
+  const bool pre = V == 4 && p < HW && c0 + 8 <= c1;
+  f32x4 v0[8];
+  if (pre) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v0[u] = ld4(x + ((long)b * C + c0 + u) * HW + p);
+  }
   const float* cab;
   if (FUSED) {
     float* gs = sh + 2 * C + 128;
@@ -296,13 +305,21 @@ __global__ __launch_bounds__(256) void cbam_pixel_stats_kernel(const T* __restri
   } else {
     cab = ca + (long)b * C;
   }
-  const long p = ((long)blockIdx.x * 256 + threadIdx.x) * V;
   if (p >= HW) return;
   const T* xb = x + ((long)b * C) * HW + p;
   float* sp = mpart + ((long)(b * G + g) * 2) * HW + p;
   if (V == 4) {
     f32x4 s = {0.f, 0.f, 0.f, 0.f}, m = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
     int c = c0;
+    if (pre) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const f32x4 o = cab[c + u] * v0[u];
+        s += o;
+        m.x = fmaxf(m.x, o.x); m.y = fmaxf(m.y, o.y); m.z = fmaxf(m.z, o.z); m.w = fmaxf(m.w, o.w);
+      }
+      c += 8;
+    }
     for (; c + 8 <= c1; c += 8) {
       f32x4 v[8];
 #pragma unroll
@@ -353,7 +370,21 @@ __device__ __forceinline__ float2 cbam_map_at(const float* __restrict__ mp, int 
   if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
     const float* q = mp + (long)yy * W + xx;
     m = -INFINITY;
-    for (int g = 0; g < G; ++g) {
+    int g = 0;
+    for (; g + 4 <= G; g += 4) {  // 8 independent loads in flight (the sums keep their g order)
+      float a[4], c[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a[u] = q[(long)(2 * (g + u)) * HW];
+        c[u] = q[(long)(2 * (g + u) + 1) * HW];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        s += a[u];
+        m = fmaxf(m, c[u]);
+      }
+    }
+    for (; g < G; ++g) {
       s += q[(long)(2 * g) * HW];
       m = fmaxf(m, q[(long)(2 * g + 1) * HW]);
     }
@@ -422,6 +453,76 @@ __global__ __launch_bounds__(256) void cbam_apply_kernel(const T* __restrict__ x
   } else {
     const float s = sa[(long)b * HW + p];
     for (int u = 0; u < n; ++u) st1(yb + (long)u * HW, s * (cab[u] * ld1(xb + (long)u * HW)));
+  }
+}
+
+// CBAM pass 3 with the spatial gate folded in (opt-in, YOLOSOD_CBAM_SA_APPLY=1; slower, see cbam_forward_impl): the
+// workgroup takes the same 256*V-pixel run as cbam_apply_kernel and kCbamApplyCh channels; it first combines the G group maps of the rows its run touches
+// (+/- 3 halo rows, 3 zero columns each side) into LDS, evaluates sa = sigmoid(conv7x7) for its own pixels (the
+// cbam_sa_kernel sums, same order: bit-identical), then streams its channels. One launch and one HBM round trip of
+// the sa map less than the split path; the conv is recomputed by the C / kCbamApplyCh channel blocks of a run.
+// grid = (ceil(HW / (256*V)), ceil(C / kCbamApplyCh), images); dynamic LDS = 2 * cbam_sa_rows(W, V) * (W + 6) floats.
+constexpr int kCbamApplyCh = 32;
+
+__host__ __device__ inline int cbam_sa_rows(int W, int V) { return (256 * V + W - 1) / W + 1 + 6; }
+
+template <int V, class T>
+__global__ __launch_bounds__(256) void cbam_sa_apply_kernel(const T* __restrict__ x, T* __restrict__ y,
+                                                            const float* __restrict__ ca,
+                                                            const float* __restrict__ mpart, int G, int C, int H,
+                                                            int W, const float* __restrict__ wsa) {
+  extern __shared__ float mm[];  // [2][nr][W + 6]
+  __shared__ float wk[98];
+  const int b = blockIdx.z, tid = threadIdx.x;
+  const long HW = (long)H * W;
+  const long pr0 = (long)blockIdx.x * 256 * V;
+  const long pr1 = (pr0 + 256 * V < HW) ? pr0 + 256 * V : HW;
+  const int yf = (int)(pr0 / W), yl = (int)((pr1 - 1) / W);
+  const int r0 = yf - 3, nr = yl - yf + 7, WP = W + 6;
+  if (tid < 98) wk[tid] = wsa[tid];
+  const float invC = 1.0f / (float)C;
+  const float* mp = mpart + (long)b * G * 2 * HW;
+  for (int i = tid; i < nr * WP; i += 256) {
+    const int ry = i / WP, rx = i - ry * WP;
+    const float2 v = cbam_map_at(mp, G, HW, H, W, r0 + ry, rx - 3, invC);
+    mm[i] = v.x;
+    mm[nr * WP + i] = v.y;
+  }
+  __syncthreads();
+  const long p = pr0 + (long)tid * V;
+  if (p >= HW) return;
+  float sv[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    const int py = (int)((p + v) / W), px = (int)((p + v) - (long)py * W);
+    const float* m0 = mm + (py - yf) * WP + px;
+    float z = 0.f;
+#pragma unroll
+    for (int ci = 0; ci < 2; ++ci)
+#pragma unroll
+      for (int ky = 0; ky < 7; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < 7; ++kx) z += wk[ci * 49 + ky * 7 + kx] * m0[ci * nr * WP + ky * WP + kx];
+    sv[v] = sigmoidf_(z);
+  }
+  const int c0 = blockIdx.y * kCbamApplyCh;
+  const int n = (C - c0 < kCbamApplyCh) ? C - c0 : kCbamApplyCh;
+  const T* xb = x + ((long)b * C + c0) * HW + p;
+  T* yb = y + ((long)b * C + c0) * HW + p;
+  const float* cab = ca + (long)b * C + c0;
+  if (V == 4) {
+    const f32x4 s4 = {sv[0], sv[V > 1 ? 1 : 0], sv[V > 2 ? 2 : 0], sv[V > 3 ? 3 : 0]};
+    int u0 = 0;
+    for (; u0 + 8 <= n; u0 += 8) {
+      f32x4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = ld4(xb + (long)(u0 + u) * HW);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) st4(yb + (long)(u0 + u) * HW, s4 * (cab[u0 + u] * v[u]));
+    }
+    for (; u0 < n; ++u0) st4(yb + (long)u0 * HW, s4 * (cab[u0] * ld4(xb + (long)u0 * HW)));
+  } else {
+    for (int u = 0; u < n; ++u) st1(yb + (long)u * HW, sv[0] * (cab[u] * ld1(xb + (long)u * HW)));
   }
 }
 
@@ -718,6 +819,11 @@ static int cbam_forward_impl(const T* x, T* y, int B, int C, int H, int W, const
   // fused launch: channel gate + pixel statistics
   const bool fused = fused_gates() && V == 4 && lds <= 64 * 1024;
   YS_CHECK_ARG(lds <= 64 * 1024, "cbam: C=%d too large for the gate kernel", C);
+  // spatial gate folded into the apply pass: opt-in (YOLOSOD_CBAM_SA_APPLY=1), measured slower at both CBAM shapes
+  // (L4 0.134 -> 0.187 ms, L18 0.043 -> 0.058 ms same-box: the per-run map staging and the 7x7 conv, recomputed by
+  // every channel block, cost more than the sa launch they replace)
+  static const bool sa_apply = [] { const char* e = getenv("YOLOSOD_CBAM_SA_APPLY"); return e && atoi(e) != 0; }();
+  const size_t sa_lds = sa_apply ? sizeof(float) * 2 * (size_t)cbam_sa_rows(W, V) * (W + 6) : SIZE_MAX;
   for (int b0 = 0; b0 < B; b0 += ipc) {
     const int nb = (B - b0 < ipc) ? B - b0 : ipc;
     const long off = (long)b0 * C * HW;
@@ -741,6 +847,16 @@ static int cbam_forward_impl(const T* x, T* y, int B, int C, int H, int W, const
       else
         hipLaunchKernelGGL((cbam_pixel_stats_kernel<1, T, false>), gs, dim3(256), 0, st, x + off, cab, C, kCbamGroup,
                            HW, mpart, nullptr, nullptr, 0, 0.f, nullptr, nullptr, 0);
+    }
+    if (sa_lds <= 48 * 1024) {  // spatial gate inside the apply pass
+      dim3 gf((unsigned)pxb, (C + kCbamApplyCh - 1) / kCbamApplyCh, nb);
+      if (V == 4)
+        hipLaunchKernelGGL((cbam_sa_apply_kernel<4, T>), gf, dim3(256), sa_lds, st, x + off, y + off, cab, mpart, G,
+                           C, H, W, sa_w);
+      else
+        hipLaunchKernelGGL((cbam_sa_apply_kernel<1, T>), gf, dim3(256), sa_lds, st, x + off, y + off, cab, mpart, G,
+                           C, H, W, sa_w);
+      continue;
     }
     hipLaunchKernelGGL(cbam_sa_kernel, dim3((W + 15) / 16, (H + 15) / 16, nb), dim3(256), 0, st, mpart, G, C, H, W,
                        sa_w, sab);
