@@ -109,7 +109,7 @@ __device__ __forceinline__ float act_b(float v, int act) {
 }
 
 template <int WM, int WN, int MI, int NI, bool B_KC, bool A_LN>
-__global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmB g) {
+__global__ __launch_bounds__(256, A_LN ? 2 : 3) void gemm_bf16_kernel(GemmB g) {
   constexpr int BM = WM * MI * 32;
   constexpr int BN = WN * NI * 32;
   constexpr int BK = 64;
@@ -119,14 +119,18 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmB g) {
   constexpr int NA = BM * BK / 8 / 256;       // 16-byte chunks per thread per A tile
   constexpr int NB = BN * BK / 8 / 256;
   constexpr int SC = BN + 4;                  // epilogue staging row stride (fp32)
-  constexpr int MAIN_BYTES = 2 * (A_ELEMS + B_ELEMS) * 2;
-  constexpr int STAGE_BYTES = BM * SC * 4;
+  // one LDS image of the A / B tiles (the next tile waits in registers, so a second LDS buffer bought nothing but
+  // occupancy lost) and the C staging in two row halves: 37 KB per workgroup instead of 74, 3 workgroups per CU
+  constexpr int MAIN_BYTES = (A_ELEMS + B_ELEMS) * 2;
+  constexpr int HB = BM / 2;                  // staged rows per epilogue pass
+  constexpr int STAGE_BYTES = HB * SC * 4;
   constexpr int SMEM_BYTES = (MAIN_BYTES > STAGE_BYTES ? MAIN_BYTES : STAGE_BYTES) + (A_LN ? 8 * BM : 0);
   static_assert(WM * WN == 4, "4 waves");
   static_assert(NA >= 1 && NB >= 1, "tile too small");
+  static_assert(MI * 32 <= BM / 2, "a wave's rows lie in one epilogue half");
   __shared__ __attribute__((aligned(16))) char smem[SMEM_BYTES];
   bf16_t* As = reinterpret_cast<bf16_t*>(smem);
-  bf16_t* Bs = As + 2 * A_ELEMS;
+  bf16_t* Bs = As + A_ELEMS;
   float* s_mean = reinterpret_cast<float*>(smem + SMEM_BYTES - (A_LN ? 8 * BM : 0));
   float* s_rstd = s_mean + BM;
 
@@ -186,9 +190,9 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmB g) {
       }
     }
   };
-  auto store_tiles = [&](int buf) {
-    bf16_t* Ab = As + buf * A_ELEMS;
-    bf16_t* Bb = Bs + buf * B_ELEMS;
+  auto store_tiles = [&]() {
+    bf16_t* Ab = As;
+    bf16_t* Bb = Bs;
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       const int idx = tid + 256 * i;
@@ -237,13 +241,12 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmB g) {
   const int lr = lane & 31, lh = lane >> 5;
   load_tiles(0);
   if (A_LN) __syncthreads();  // s_mean / s_rstd
-  store_tiles(0);
+  store_tiles();
   __syncthreads();
   for (int kb = 0; kb < nk; ++kb) {
-    const int buf = kb & 1;
     if (kb + 1 < nk) load_tiles((kb + 1) * BK);
-    const bf16_t* Ab = As + buf * A_ELEMS + (wm * MI * 32 + lr) * SK + lh * 8;
-    const bf16_t* Bb = Bs + buf * B_ELEMS + (wn * NI * 32 + lr) * SK + lh * 8;
+    const bf16_t* Ab = As + (wm * MI * 32 + lr) * SK + lh * 8;
+    const bf16_t* Bb = Bs + (wn * NI * 32 + lr) * SK + lh * 8;
 #pragma unroll
     for (int kk = 0; kk < BK / 16; ++kk) {
       bf16x8_t a[MI], b[NI];
@@ -256,83 +259,94 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmB g) {
 #pragma unroll
         for (int j = 0; j < NI; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
     }
+    __syncthreads();
     if (kb + 1 < nk) {
       cur_k0 = (kb + 1) * BK;
-      store_tiles(buf ^ 1);
+      store_tiles();
+      __syncthreads();
     }
-    __syncthreads();
   }
 
   const EpiB& e = g.epi;
-  // stage C through LDS (the main-loop buffers are free after the last barrier).
-  // C/D map of 32x32: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+  // stage C through LDS in two row halves (the main-loop buffer is free after the last barrier); a wave's rows lie
+  // in one half. C/D map of 32x32: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
   float* Cs = reinterpret_cast<float*>(smem);
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < NI; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r)
-        Cs[(wm * MI * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) * SC + wn * NI * 32 + j * 32 + lr] = acc[i][j][r];
-  __syncthreads();
-  if (e.vec) {
-    constexpr int NQ = BN / 4;
-    bf16_t* outb = e.out + (long)bz * e.out_bs;
-    const bf16_t* resb = e.res ? e.res + (long)bz * e.res_bs : nullptr;
-#pragma unroll 4
-    for (int idx = tid; idx < BM * NQ; idx += 256) {
-      const int row = idx / NQ, c4 = idx % NQ;
-      const int m = m0 + row;
-      const int n = n0 + 4 * c4;
-      if (m >= M || n >= N) continue;
-      f32x4 v = *reinterpret_cast<const f32x4*>(&Cs[row * SC + 4 * c4]);
-      if (e.bias_mode == 1) v += e.bias[m];
-      else if (e.bias_mode == 2) v += *reinterpret_cast<const f32x4*>(e.bias + n);
-      if (e.bn_mode == 1) v = v * e.scale[m] + e.shift[m];
-      else if (e.bn_mode == 2)
-        v = v * *reinterpret_cast<const f32x4*>(e.scale + n) + *reinterpret_cast<const f32x4*>(e.shift + n);
-      v.x = act_b(v.x, e.act); v.y = act_b(v.y, e.act); v.z = act_b(v.z, e.act); v.w = act_b(v.w, e.act);
-      if (resb) v += ld4(resb + (long)m * e.ldr + n);
-      st4(outb + (long)m * e.ldc + n, v);
-    }
-    return;
-  }
-  // scalar epilogue: lanes along n (Swin: consecutive raster tokens = consecutive pixels of an output row). A
-  // thread's column is the same in every row pass (256 % BN == 0), so its output offset (token -> pixel, crop) is
-  // computed once; rows advance by the channel plane.
+  // scalar epilogue (Swin: consecutive raster tokens = consecutive pixels of an output row): a thread's column is
+  // the same in every row pass (256 % BN == 0), so its output offset (token -> pixel, crop) is computed once; rows
+  // advance by the channel plane
   static_assert(256 % BN == 0, "column per thread");
-  const int col = tid % BN, n = n0 + col;
-  if (n >= N) return;
-  long o0, r0_, m_str, r_str;
-  if (e.swin) {
-    const long per_img = (long)e.sw_Hp * e.sw_Wp;
-    const int img = (int)(n / per_img);
-    const int rr = (int)(n - img * per_img);
-    const int h = rr / e.sw_Wp, w = rr - (rr / e.sw_Wp) * e.sw_Wp;
-    if (h >= e.sw_H || w >= e.sw_W) return;  // crop of the padded border
-    m_str = (long)e.sw_H * e.sw_W;           // out / res NCHW [img][M][H][W]
-    o0 = (long)img * M * m_str + (long)h * e.sw_W + w;
-    r0_ = o0;
-    r_str = m_str;
-  } else {
-    m_str = e.ldc;
-    r_str = e.ldr;
-    o0 = (long)bz * e.out_bs + n;
-    r0_ = (long)bz * e.res_bs + n;
+  const int col = tid % BN, ncol = n0 + col;
+  bool col_ok = ncol < N;
+  long o0 = 0, r0_ = 0, m_str = 0, r_str = 0;
+  if (!e.vec && col_ok) {
+    if (e.swin) {
+      const long per_img = (long)e.sw_Hp * e.sw_Wp;
+      const int img = (int)(ncol / per_img);
+      const int rr = (int)(ncol - img * per_img);
+      const int h = rr / e.sw_Wp, w = rr - (rr / e.sw_Wp) * e.sw_Wp;
+      col_ok = h < e.sw_H && w < e.sw_W;  // crop of the padded border
+      m_str = (long)e.sw_H * e.sw_W;      // out / res NCHW [img][M][H][W]
+      o0 = (long)img * M * m_str + (long)h * e.sw_W + w;
+      r0_ = o0;
+      r_str = m_str;
+    } else {
+      m_str = e.ldc;
+      r_str = e.ldr;
+      o0 = (long)bz * e.out_bs + ncol;
+      r0_ = (long)bz * e.res_bs + ncol;
+    }
   }
-  const float bn_ = e.bias_mode == 2 ? e.bias[n] : 0.f;
-  const float sc_n = e.bn_mode == 2 ? e.scale[n] : 1.f, sh_n = e.bn_mode == 2 ? e.shift[n] : 0.f;
-  for (int row = tid / BN; row < BM; row += 256 / BN) {
-    const int m = m0 + row;
-    if (m >= M) break;
-    float v = Cs[row * SC + col];
-    if (e.bias_mode == 1) v += e.bias[m];
-    else if (e.bias_mode == 2) v += bn_;
-    if (e.bn_mode == 1) v = v * e.scale[m] + e.shift[m];
-    else if (e.bn_mode == 2) v = v * sc_n + sh_n;
-    v = act_b(v, e.act);
-    if (e.res) v += bf2f(e.res[r0_ + (long)m * r_str]);
-    e.out[o0 + (long)m * m_str] = f2bf(v);
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf) {
+    if (hf) __syncthreads();  // the first half's epilogue has read Cs
+    if ((wm * MI * 32) / HB == hf) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            Cs[(wm * MI * 32 - hf * HB + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) * SC + wn * NI * 32 + j * 32 + lr] =
+                acc[i][j][r];
+    }
+    __syncthreads();
+    const int mh = m0 + hf * HB;
+    if (e.vec) {
+      constexpr int NQ = BN / 4;
+      bf16_t* outb = e.out + (long)bz * e.out_bs;
+      const bf16_t* resb = e.res ? e.res + (long)bz * e.res_bs : nullptr;
+#pragma unroll 4
+      for (int idx = tid; idx < HB * NQ; idx += 256) {
+        const int row = idx / NQ, c4 = idx % NQ;
+        const int m = mh + row;
+        const int n = n0 + 4 * c4;
+        if (m >= M || n >= N) continue;
+        f32x4 v = *reinterpret_cast<const f32x4*>(&Cs[row * SC + 4 * c4]);
+        if (e.bias_mode == 1) v += e.bias[m];
+        else if (e.bias_mode == 2) v += *reinterpret_cast<const f32x4*>(e.bias + n);
+        if (e.bn_mode == 1) v = v * e.scale[m] + e.shift[m];
+        else if (e.bn_mode == 2)
+          v = v * *reinterpret_cast<const f32x4*>(e.scale + n) + *reinterpret_cast<const f32x4*>(e.shift + n);
+        v.x = act_b(v.x, e.act); v.y = act_b(v.y, e.act); v.z = act_b(v.z, e.act); v.w = act_b(v.w, e.act);
+        if (resb) v += ld4(resb + (long)m * e.ldr + n);
+        st4(outb + (long)m * e.ldc + n, v);
+      }
+    } else if (col_ok) {
+      const float bn_ = e.bias_mode == 2 ? e.bias[ncol] : 0.f;
+      const float sc_n = e.bn_mode == 2 ? e.scale[ncol] : 1.f, sh_n = e.bn_mode == 2 ? e.shift[ncol] : 0.f;
+      for (int row = tid / BN; row < HB; row += 256 / BN) {
+        const int m = mh + row;
+        if (m >= M) break;
+        float v = Cs[row * SC + col];
+        if (e.bias_mode == 1) v += e.bias[m];
+        else if (e.bias_mode == 2) v += bn_;
+        if (e.bn_mode == 1) v = v * e.scale[m] + e.shift[m];
+        else if (e.bn_mode == 2) v = v * sc_n + sh_n;
+        v = act_b(v, e.act);
+        if (e.res) v += bf2f(e.res[r0_ + (long)m * r_str]);
+        e.out[o0 + (long)m * m_str] = f2bf(v);
+      }
+    }
   }
 }
 
