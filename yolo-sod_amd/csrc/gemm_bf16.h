@@ -296,8 +296,27 @@ __global__ __launch_bounds__(256, A_LN ? 2 : 3) void gemm_bf16_kernel(GemmB g) {
       r0_ = (long)bz * e.res_bs + ncol;
     }
   }
+  // residual operands of a half are loaded before its staging barrier, all at once: in the loops below each
+  // iteration's residual load was a separate HBM round trip (the out-projection / MLP2 / pw GEMMs spent as long in
+  // their epilogues as in their main loops)
+  constexpr int NQ = BN / 4;
+  constexpr int VIT = HB * NQ / 256;         // vector-epilogue iterations per half
+  constexpr int SIT = HB / (256 / BN);       // scalar-epilogue rows per thread and half
+  static_assert(HB * NQ % 256 == 0 && SIT % 8 == 0, "epilogue split");
+  const bf16_t* resb = e.res ? e.res + (long)bz * e.res_bs : nullptr;
 #pragma unroll
   for (int hf = 0; hf < 2; ++hf) {
+    const int mh = m0 + hf * HB;
+    uint2 rv[VIT];
+    if (resb && e.vec) {
+#pragma unroll
+      for (int it = 0; it < VIT; ++it) {
+        const int idx = tid + 256 * it;
+        const int m = mh + idx / NQ, n = n0 + 4 * (idx % NQ);
+        rv[it] = make_uint2(0u, 0u);
+        if (m < M && n < N) rv[it] = *reinterpret_cast<const uint2*>(resb + (long)m * e.ldr + n);
+      }
+    }
     if (hf) __syncthreads();  // the first half's epilogue has read Cs
     if ((wm * MI * 32) / HB == hf) {
 #pragma unroll
@@ -310,13 +329,11 @@ __global__ __launch_bounds__(256, A_LN ? 2 : 3) void gemm_bf16_kernel(GemmB g) {
                 acc[i][j][r];
     }
     __syncthreads();
-    const int mh = m0 + hf * HB;
     if (e.vec) {
-      constexpr int NQ = BN / 4;
       bf16_t* outb = e.out + (long)bz * e.out_bs;
-      const bf16_t* resb = e.res ? e.res + (long)bz * e.res_bs : nullptr;
-#pragma unroll 4
-      for (int idx = tid; idx < HB * NQ; idx += 256) {
+#pragma unroll
+      for (int it = 0; it < VIT; ++it) {
+        const int idx = tid + 256 * it;
         const int row = idx / NQ, c4 = idx % NQ;
         const int m = mh + row;
         const int n = n0 + 4 * c4;
@@ -328,23 +345,37 @@ __global__ __launch_bounds__(256, A_LN ? 2 : 3) void gemm_bf16_kernel(GemmB g) {
         else if (e.bn_mode == 2)
           v = v * *reinterpret_cast<const f32x4*>(e.scale + n) + *reinterpret_cast<const f32x4*>(e.shift + n);
         v.x = act_b(v.x, e.act); v.y = act_b(v.y, e.act); v.z = act_b(v.z, e.act); v.w = act_b(v.w, e.act);
-        if (resb) v += ld4(resb + (long)m * e.ldr + n);
+        if (resb)
+          v += f32x4{__uint_as_float(rv[it].x << 16), __uint_as_float(rv[it].x & 0xffff0000u),
+                     __uint_as_float(rv[it].y << 16), __uint_as_float(rv[it].y & 0xffff0000u)};
         st4(outb + (long)m * e.ldc + n, v);
       }
     } else if (col_ok) {
       const float bn_ = e.bias_mode == 2 ? e.bias[ncol] : 0.f;
       const float sc_n = e.bn_mode == 2 ? e.scale[ncol] : 1.f, sh_n = e.bn_mode == 2 ? e.shift[ncol] : 0.f;
-      for (int row = tid / BN; row < HB; row += 256 / BN) {
-        const int m = mh + row;
-        if (m >= M) break;
-        float v = Cs[row * SC + col];
-        if (e.bias_mode == 1) v += e.bias[m];
-        else if (e.bias_mode == 2) v += bn_;
-        if (e.bn_mode == 1) v = v * e.scale[m] + e.shift[m];
-        else if (e.bn_mode == 2) v = v * sc_n + sh_n;
-        v = act_b(v, e.act);
-        if (e.res) v += bf2f(e.res[r0_ + (long)m * r_str]);
-        e.out[o0 + (long)m * m_str] = f2bf(v);
+      // rows in batches of 8: the batch's residual loads go out together
+      for (int it0 = 0; it0 < SIT; it0 += 8) {
+        bf16_t r8[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int m = mh + tid / BN + (it0 + u) * (256 / BN);
+          r8[u] = (e.res && m < M) ? e.res[r0_ + (long)m * r_str] : (bf16_t)0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int row = tid / BN + (it0 + u) * (256 / BN);
+          const int m = mh + row;
+          if (m < M) {
+            float v = Cs[row * SC + col];
+            if (e.bias_mode == 1) v += e.bias[m];
+            else if (e.bias_mode == 2) v += bn_;
+            if (e.bn_mode == 1) v = v * e.scale[m] + e.shift[m];
+            else if (e.bn_mode == 2) v = v * sc_n + sh_n;
+            v = act_b(v, e.act);
+            if (e.res) v += bf2f(r8[u]);
+            e.out[o0 + (long)m * m_str] = f2bf(v);
+          }
+        }
       }
     }
   }
