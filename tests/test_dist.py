@@ -40,13 +40,16 @@ def _worker(rank, world, port, q):
         g = torch.Generator().manual_seed(rank)
         out = torch.randn(B, D, 6, generator=g)
         counts = torch.randint(0, D, (B,), generator=g, dtype=torch.int32)
-        g_out, g_cnt = gather_detections(out, counts)
+        index = torch.randint(-1, 34000, (B, D), generator=g, dtype=torch.int32)
+        g_out, g_cnt, g_idx = gather_detections(out, counts, index)
         ok = True
         for r in range(world):
             gr = torch.Generator().manual_seed(r)
             ro = torch.randn(B, D, 6, generator=gr)
             rc = torch.randint(0, D, (B,), generator=gr, dtype=torch.int32)
-            ok &= torch.equal(g_out[r * B:(r + 1) * B], ro) and torch.equal(g_cnt[r * B:(r + 1) * B], rc)
+            ri = torch.randint(-1, 34000, (B, D), generator=gr, dtype=torch.int32)
+            sl = slice(r * B, (r + 1) * B)
+            ok &= torch.equal(g_out[sl], ro) and torch.equal(g_cnt[sl], rc) and torch.equal(g_idx[sl], ri)
         q.put((rank, ok))
     finally:
         dist.destroy_process_group()
@@ -90,10 +93,12 @@ def _flow_worker(rank, world, port, n_images, q):
             rows, idx = non_max_suppression_ref(p.numpy().copy(), 0.25, 0.3, max_det=300)
             return _pad_rows(rows, idx)
 
-        g_out, g_cnt = sharded_predict(local_predict, n_images, lambda lo, hi: torch.from_numpy(preds[lo:hi].copy()))
+        g_out, g_cnt, g_idx = sharded_predict(local_predict, n_images,
+                                              lambda lo, hi: torch.from_numpy(preds[lo:hi].copy()))
         rows, idx = non_max_suppression_ref(preds.copy(), 0.25, 0.3, max_det=300)  # unsharded, one process
-        ref_out, ref_cnt, _ = _pad_rows(rows, idx)
+        ref_out, ref_cnt, ref_idx = _pad_rows(rows, idx)
         ok = (g_out.shape == ref_out.shape and torch.equal(g_cnt, ref_cnt) and torch.equal(g_out, ref_out)
+              and torch.equal(g_idx, ref_idx)  # kept anchor indices survive the exchange, in global image order
               and int(ref_cnt.min()) > 0 and len(set(ref_cnt.tolist())) > 1)
         q.put((rank, bool(ok)))
     finally:
@@ -102,8 +107,8 @@ def _flow_worker(rank, world, port, n_images, q):
 
 @pytest.mark.parametrize("n_images", [8, 7])
 def test_sharded_flow_matches_single_process_gloo(n_images):
-    """World size 2: the gathered detections equal the single-process detections row for row, in global image
-    order (distinct per-image counts make a shard-order error visible); 7 images = uneven shards."""
+    """World size 2: the gathered detections and kept anchor indices equal the single-process ones row for row, in
+    global image order (distinct per-image counts make a shard-order error visible); 7 images = uneven shards."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()

@@ -8,8 +8,8 @@ MI355X additions:
 * :meth:`DetectionPredictor.predict_padded` never syncs the host: NMS returns fixed-shape ``[B, max_det, 6]``
   rows + counts, so a batch is one stream-ordered sequence of launches (graph-capturable).
 * Data parallel inference: one process per GPU; :func:`shard_bounds` splits images across ranks (no data-path
-  collective), :func:`gather_detections` is the single exchange step - an all-gather of the padded detections and
-  counts (RCCL over xGMI with backend ``nccl``; ``gloo`` on CPU for tests).
+  collective), :func:`gather_detections` is the single exchange step - an all-gather of the padded detections,
+  counts and kept anchor indices (RCCL over xGMI with backend ``nccl``; ``gloo`` on CPU for tests).
 """
 from __future__ import annotations
 
@@ -70,38 +70,43 @@ def shard_bounds(n: int, rank: int, world: int):
     return lo, lo + base + (1 if rank < rem else 0)
 
 
-def gather_detections(out: torch.Tensor, counts: torch.Tensor, group=None):
-    """All-gather padded detections of equal-size shards: [B_local, D, 6] + [B_local] -> [world*B_local, ...]."""
+def gather_detections(out: torch.Tensor, counts: torch.Tensor, index: torch.Tensor | None = None, group=None):
+    """All-gather padded detections of equal-size shards: [B_local, D, 6] + [B_local] (+ the kept anchor indices
+    [B_local, D]) -> [world*B_local, ...] in rank order. Returns (out, counts) or (out, counts, index)."""
     world = dist.get_world_size(group)
-    g_out = torch.empty((world * out.shape[0], *out.shape[1:]), dtype=out.dtype, device=out.device)
-    g_cnt = torch.empty((world * counts.shape[0],), dtype=counts.dtype, device=counts.device)
-    dist.all_gather_into_tensor(g_out, out.contiguous(), group=group)
-    dist.all_gather_into_tensor(g_cnt, counts.contiguous(), group=group)
-    return g_out, g_cnt
+    parts = [out, counts] + ([index] if index is not None else [])
+    gathered = []
+    for t in parts:
+        g = torch.empty((world * t.shape[0], *t.shape[1:]), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(g, t.contiguous(), group=group)
+        gathered.append(g)
+    return tuple(gathered)
 
 
 def sharded_predict(predict_padded, n_images: int, images, group=None):
     """Data-parallel inference over ``n_images`` global images, one process per GPU.
 
     ``images(lo, hi)`` returns this rank's shard (global images [lo, hi), ``shard_bounds``) - each rank
-    materialises only its own images; ``predict_padded(x) -> (out [b, D, 6], counts [b], ...)`` is the rank-local
-    path (``DetectionPredictor.predict_padded``). Shards are padded to the largest shard (count 0) so one
-    fixed-size all-gather serves uneven splits. Returns (out [n_images, D, 6], counts [n_images]) in global image
-    order on every rank."""
+    materialises only its own images; ``predict_padded(x) -> (out [b, D, 6], counts [b], index [b, D])`` is the
+    rank-local path (``DetectionPredictor.predict_padded``). Shards are padded to the largest shard (count 0,
+    index -1) so one fixed-size all-gather serves uneven splits. Returns (out [n_images, D, 6], counts [n_images],
+    index [n_images, D]) in global image order on every rank: the kept anchor indices of every image
+    (``models/yolo/detect/predict.py:23-41`` per image) survive the exchange."""
     world, rank = dist.get_world_size(group), dist.get_rank(group)
     lo, hi = shard_bounds(n_images, rank, world)
-    out, counts = predict_padded(images(lo, hi))[:2]
+    out, counts, index = predict_padded(images(lo, hi))[:3]
     smax = -(-n_images // world)
     if out.shape[0] < smax:
         pad = smax - out.shape[0]
         out = torch.cat([out, out.new_zeros((pad, *out.shape[1:]))])
         counts = torch.cat([counts, counts.new_zeros((pad,))])
-    g_out, g_cnt = gather_detections(out, counts, group)
+        index = torch.cat([index, index.new_full((pad, *index.shape[1:]), -1)])
+    g_out, g_cnt, g_idx = gather_detections(out, counts, index, group)
     if n_images % world:
         keep = torch.cat([torch.arange(r * smax, r * smax + (b - a)) for r in range(world)
                           for a, b in [shard_bounds(n_images, r, world)]])
-        g_out, g_cnt = g_out[keep.to(g_out.device)], g_cnt[keep.to(g_cnt.device)]
-    return g_out, g_cnt
+        g_out, g_cnt, g_idx = (t[keep.to(t.device)] for t in (g_out, g_cnt, g_idx))
+    return g_out, g_cnt, g_idx
 
 
 def seeded_images(lo: int, hi: int, imgsz: int, seed: int = 1000, device=None) -> torch.Tensor:
