@@ -9,7 +9,10 @@ Usage: python bench.py [--gpus N --steps K --warmup W]; for N > 1 launch with
        python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 --master-port P \
               bench.py --gpus N --steps K --warmup W
 Rank 0 prints ONE JSON line (plus `roofline` of the dominant HIP operator, measured live with HIP events inside
-the timed region, and `cpu_baseline` = the oracle CPU model timed on the host cores, rank 0 at N = 1 only).
+the timed region, and `cpu_baseline` = the oracle CPU model timed on the host cores, rank 0 at N = 1 only). At N = 1
+the line also carries `configs`: BASELINE configs[3] (n1280, bs 8) and configs[4] (m640 bf16, bs 64), each timed in
+its own region of the same process with the same contract (its own ms_per_step, value, roofline, path_roofline,
+hip_ops). Roofline fractions are quoted against the ceiling of the arithmetic each kernel issues (perf.py).
 """
 from __future__ import annotations
 
@@ -223,34 +226,62 @@ def load_traffic():
     return None
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="n640", choices=list(CONFIGS))
-    ap.add_argument("--conf", type=float, default=0.25)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-nms-load", action="store_true")
-    ap.add_argument("--miopen-benchmark", action="store_true", help="torch.backends.cudnn.benchmark (MIOpen find)")
-    args = ap.parse_args()
-    if args.miopen_benchmark:
-        torch.backends.cudnn.benchmark = True
+# statistics a producing conv epilogue emits for the gate that consumes its output (nn/tasks.py): the gate's own
+# kernels then read x once; the producer's extra time over the plain epilogue of the same shape is billed to the gate
+PRODUCER_GATE = {"sum": "se", "summax": "cbam", "capool": "ca"}
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
 
-    cfg_yaml, imgsz, bs, label, dtype = CONFIGS[args.config]
+def _event_ms(fn, reps=10, warm=3):
+    ts = []
+    for i in range(reps + warm):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn()
+        e1.record()
+        if i >= warm:
+            ts.append((e0, e1))
+    torch.cuda.synchronize()
+    return _median([a.elapsed_time(b) for a, b in ts])
+
+
+def producer_extra(agg, dev, dtype):
+    """{(gate op, gate input shape): (extra ms per launch, producer description)} for every producing epilogue that
+    emitted a gate's statistics in the timed region: its stats variant and its plain variant, timed back to back
+    on fresh tensors of the same shape after the timed region (HIP events on the current stream)."""
+    out = {}
+    for key in agg:
+        op, shape, extra = key[:3]
+        if op == "bias_act" and extra in PRODUCER_GATE:
+            y = torch.randn(shape, device=dev).to(dtype)
+            bias = torch.randn(shape[1], device=dev)
+            o = torch.empty_like(y)
+            t_st = _event_ms(lambda: _hip.bias_act(y, bias, 1, out=o, stats=extra))
+            t_pl = _event_ms(lambda: _hip.bias_act(y, bias, 1, out=o))
+            gate, gshape = PRODUCER_GATE[extra], tuple(shape)
+        elif op == "conv1x1_thin" and isinstance(extra, tuple) and extra[1] in ("sum", "summax"):
+            B, Cin, H, W = shape
+            cout = extra[0]
+            x = torch.randn(shape, device=dev)
+            w = torch.randn(cout, Cin, device=dev) * 0.05
+            bias = torch.randn(cout, device=dev)
+            o = torch.empty((B, cout, H, W), device=dev)
+            t_st = _event_ms(lambda: _hip.conv1x1_thin(x, w, bias, out=o, stats=extra[1]))
+            t_pl = _event_ms(lambda: _hip.conv1x1_thin(x, w, bias, out=o))
+            gate, gshape = PRODUCER_GATE[extra[1]], (B, cout, H, W)
+        else:
+            continue
+        out[(gate, gshape)] = (max(0.0, t_st - t_pl), f"{op}{tuple(shape)} {extra}: {t_st:.4f} ms with the "
+                                                      f"statistics vs {t_pl:.4f} ms plain")
+    return out
+
+
+def measure(name, world, rank, dev, steps, warmup, conf, extra_billing=True):
+    """One config: warmup, K timed steps (barrier + synchronize on both sides, max over ranks), per-operator HIP
+    event timings -> rooflines. Returns (result dict, predictor)."""
+    cfg_yaml, imgsz, bs, label, dtype = CONFIGS[name]
     dname = DTYPE_NAME[dtype]
     model = build_model(cfg_yaml, seed=0, device=dev, dtype=dtype)
-    predictor = DetectionPredictor(model, conf=args.conf, iou=0.7, max_det=300)
+    predictor = DetectionPredictor(model, conf=conf, iou=0.7, max_det=300)
     # one global seeded batch of world * bs images (image i from seed 1000 + i); each rank holds its shard, resident
     # in HBM in the model's dtype before the timed region (the predictor's .to(dtype) is then a no-op)
     n_global = world * bs
@@ -258,22 +289,22 @@ def main():
     x = seeded_images(lo, hi, imgsz, device=dev).to(dtype)
 
     def step():
-        if world > 1:  # shard -> rank-local predict -> all-gather of the padded detections (global image order)
+        if world > 1:  # shard -> rank-local predict -> all-gather of the padded detections + kept indices
             return sharded_predict(predictor.predict_padded, n_global, lambda a, b: x)[1]
         return predictor.predict_padded(x)[1]
 
     t_w = time.perf_counter()
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
     torch.cuda.synchronize()
-    log(f"[rank {rank}] warmup {args.warmup} steps {time.perf_counter() - t_w:.2f}s")
+    log(f"[rank {rank}] {name}: warmup {warmup} steps {time.perf_counter() - t_w:.2f}s")
 
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     with _hip.op_timer() as timer:
         t0 = time.perf_counter()
-        for _ in range(args.steps):
+        for _ in range(steps):
             step()
         torch.cuda.synchronize()
         if world > 1:
@@ -291,79 +322,129 @@ def main():
         a = agg.setdefault(key, [0.0, 0])
         a[0] += ms
         a[1] += 1
+    billed = producer_extra(agg, dev, dtype) if extra_billing else {}
     ops, backbone = [], []
     for key, (tot, n) in agg.items():
         if key[0] not in perf.PATH_OPS:  # backbone conv kernels of this library: outside the path roofline
             backbone.append({"op": key[0], "shape": list(key[1]), "extra": str(key[2]), "launches": n,
-                             "total_ms_per_step": round(tot / args.steps, 4)})
+                             "total_ms_per_step": round(tot / steps, 4)})
             continue
         nbytes, flops = perf.op_cost(key)
-        avg = tot / n
-        ops.append({"op": key[0], "shape": list(key[1]), "dtype": "bf16" if perf.elem_size(key) == 2 else "f32",
-                    "launches": n, "avg_ms": round(avg, 4), "total_ms_per_step": round(tot / args.steps, 4),
-                    "GBps": round(nbytes / (avg * 1e-3) / 1e9, 1),
-                    "TFLOPs": round(flops / (avg * 1e-3) / 1e12, 2), "bound": perf.bound_of(key),
-                    "t_min_ms": round(perf.t_min_ms(key), 4), "frac": round(perf.t_min_ms(key) / avg, 3),
-                    "frac_method": round(perf.t_min_ms(key, method=True) / avg, 3),
-                    "bytes": nbytes, "flops": flops, "key": key})
+        kern = tot / n
+        ext, src = billed.get((key[0], tuple(key[1])), (0.0, None))
+        avg = kern + ext
+        bound = perf.bound_of(key)
+        tm, tm_d = perf.t_min_ms(key, method=True), perf.t_min_ms(key)
+        o = {"op": key[0], "shape": list(key[1]), "dtype": "bf16" if perf.elem_size(key) == 2 else "f32",
+             "launches": n, "avg_ms": round(avg, 4), "kernels_ms": round(kern, 4),
+             "total_ms_per_step": round(avg * n / steps, 4),
+             "GBps": round(nbytes / (avg * 1e-3) / 1e9, 1), "TFLOPs": round(flops / (avg * 1e-3) / 1e12, 2),
+             "bound": bound, "peak": perf.method_peak_tflops(key) if bound == "mfma" else perf.PEAK_HBM_GBS,
+             "t_min_ms": round(tm, 4), "frac": round(tm / avg, 3), "frac_vs_dtype_peak": round(tm_d / avg, 3),
+             "bytes": nbytes, "flops": flops, "key": key}
+        if src:
+            o["producer_extra_ms"] = round(ext, 4)
+            o["producer"] = src
+        ops.append(o)
     ops.sort(key=lambda o: -o["total_ms_per_step"])
     dom = ops[0]
-    bound = perf.bound_of(dom["key"])
+    bound = dom["bound"]
     if bound == "mfma":
-        achieved, peak, unit = dom["TFLOPs"], perf.peak_tflops(dom["key"]), "TFLOP/s"
+        achieved, peak, unit = dom["TFLOPs"], perf.method_peak_tflops(dom["key"]), "TFLOP/s"
     else:
         achieved, peak, unit = dom["GBps"], perf.PEAK_HBM_GBS, "GB/s"
     traffic = load_traffic()
-    roofline = {"bound": bound, "achieved": achieved, "peak": peak, "unit": unit,
+    roofline = {"bound": bound, "achieved": achieved, "peak": round(peak, 1), "unit": unit,
                 "frac": round(achieved / peak, 4),
                 "traffic": (traffic or {}).get(f"{dom['op']}:{'x'.join(map(str, dom['shape']))}"),
                 "kernel": f"{dom['op']}{tuple(dom['shape'])} (one C-ABI call = its launch sequence)",
-                "algorithmic_per_launch": dom["flops"] if bound == "mfma" else dom["bytes"]}
-    if (dom["op"] == "swin" and perf.elem_size(dom["key"]) == 4 and dom["shape"][1] in (64, 256)
-            and os.environ.get("YOLOSOD_SWIN_X3", "1") != "0"):
-        # the fp32 Swin kernels run their matrix products as fp16 two-term splits (3 exact fp16 products per fp32
-        # product, fp32 accumulation: csrc/swin_x3.hip); `frac` stays against the fp32 MFMA peak of the dtype, this
-        # is the same rate against the fp16 matrix-core ceiling of that method
-        roofline["matrix_method"] = {"method": "fp16 two-term splits on v_mfma_f32_16x16x32_f16, 3 products per fp32 "
-                                               "product", "peak_tflops": round(perf.PEAK_BF16_MFMA_TFLOPS / 3, 1),
-                                     "frac": round(achieved / (perf.PEAK_BF16_MFMA_TFLOPS / 3), 4)}
+                "algorithmic_per_launch": dom["flops"] if bound == "mfma" else dom["bytes"],
+                "peak_basis": ("matrix-core ceiling of the method the kernel computes with" if bound == "mfma"
+                               else "HBM3E spec")}
+    if bound == "mfma":
+        dpeak = perf.peak_tflops(dom["key"])
+        if abs(dpeak - peak) > 1e-6:
+            # the fp32 Swin / A2 / head kernels run each fp32 product as 3 exact fp16 products of two-term splits
+            # (csrc/swin_x3.hip): their roof is the fp16 peak / 3; the fp32 MFMA peak is kept as a secondary figure
+            roofline["method"] = "fp16 two-term splits on v_mfma_f32_16x16x32_f16, 3 products per fp32 product"
+        roofline["frac_vs_dtype_peak"] = round(achieved / dpeak, 4)
+        roofline["dtype_peak"] = dpeak
 
     # path-level roofline = sum_k t_k^min / sum_k t_k^meas over every hot-path operator,
-    # t_k^min = max(bytes_k / HBM peak, flops_k / matrix-core peak of the op's dtype)
-    t_min = sum(perf.t_min_ms(o["key"]) * o["launches"] / args.steps for o in ops)
+    # t_k^min = max(bytes_k / HBM peak, flops_k / matrix ceiling of the method the op computes with)
     t_meas = sum(o["total_ms_per_step"] for o in ops)
+    t_min = sum(perf.t_min_ms(o["key"], method=True) * o["launches"] / steps for o in ops)
+    t_min_d = sum(perf.t_min_ms(o["key"]) * o["launches"] / steps for o in ops)
     path_roofline = {"t_min_ms": round(t_min, 4), "t_meas_ms": round(t_meas, 4),
                      "frac": round(t_min / t_meas, 4) if t_meas else None,
-                     "definition": "sum over hot-path ops of max(bytes/8 TB/s, flops/MFMA peak of the op dtype "
-                                   "(fp32 157.3, bf16 2516.6 TF/s)) / measured"}
-    # the same sum against the ceiling of the method each op computes with (fp32 ops on fp16 two-term splits:
-    # 2516.6 / 3 TF/s), so an fp32 op running faster than the fp32 MFMA peak does not read as frac > 1 of nothing
-    t_min_m = sum(perf.t_min_ms(o["key"], method=True) * o["launches"] / args.steps for o in ops)
-    path_roofline["method"] = {"t_min_ms": round(t_min_m, 4), "frac": round(t_min_m / t_meas, 4) if t_meas else None,
-                               "definition": "as above with the split-method ceiling (perf.method_peak_tflops)"}
+                     "definition": "sum over hot-path ops of max(bytes / 8 TB/s, flops / matrix ceiling of the "
+                                   "method the op computes with: fp16 peak / 3 = 838.9 TF/s for the fp32 ops on "
+                                   "fp16 two-term splits, 2516.6 for bf16, 157.3 for exact fp32 MFMA) / measured; "
+                                   "a producing epilogue's extra time for a gate's statistics is billed to the gate",
+                     "frac_vs_dtype_peak": round(t_min_d / t_meas, 4) if t_meas else None}
+    value = world * bs * steps / elapsed
+    res = {"value": round(value, 2), "unit": "images/s", "ms_per_step": round(elapsed / steps * 1e3, 3),
+           "steps": steps, "warmup": warmup, "dtype": dname,
+           "data": f"synthetic: torch.rand images in HBM, seed-0 random-init weights of {label}",
+           "config": {"workload": f"{label} {imgsz}x{imgsz}, {bs} images per GPU, fused {dname} "
+                                  f"forward + decode + NMS(conf={conf}, iou=0.7)",
+                      "imgsz": imgsz, "batch_per_gpu": bs, "global_batch": bs * world, "parallelism": f"dp{world}"},
+           "roofline": roofline, "path_roofline": path_roofline,
+           "hip_ops_ms_per_step": round(t_meas, 3),
+           "hip_ops": [{k: v for k, v in o.items() if k not in ("bytes", "flops", "key")} for o in ops],
+           "backbone_hip_ms_per_step": round(sum(o["total_ms_per_step"] for o in backbone), 3),
+           "backbone_hip_ops": sorted(backbone, key=lambda o: -o["total_ms_per_step"])[:12]}
+    return res, predictor, cfg_yaml, imgsz
 
-    total_imgs = world * bs * args.steps
-    value = total_imgs / elapsed
-    hip_ms = sum(o["total_ms_per_step"] for o in ops)
-    result = {
-        "metric": METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": dname,
-        "data": f"synthetic: torch.rand images in HBM, seed-0 random-init weights of {label}",
-        "config": {"workload": f"{label} {imgsz}x{imgsz}, {bs} images per GPU, fused {dname} "
-                               f"forward + decode + NMS(conf={args.conf}, iou=0.7)",
-                   "imgsz": imgsz, "batch_per_gpu": bs, "global_batch": bs * world, "parallelism": f"dp{world}"},
-        "roofline": roofline,
-        "path_roofline": path_roofline,
-        "hip_ops_ms_per_step": round(hip_ms, 3),
-        "hip_ops": [{k: v for k, v in o.items() if k not in ("bytes", "flops", "key")} for o in ops],
-        "backbone_hip_ms_per_step": round(sum(o["total_ms_per_step"] for o in backbone), 3),
-        "backbone_hip_ops": sorted(backbone, key=lambda o: -o["total_ms_per_step"])[:12],
-        "nms_loaded": None,
-        "cpu_baseline": None,
-    }
+
+# BASELINE.json configs[3] / configs[4] on one GPU, timed in the same process after the headline (N = 1 only)
+EXTRA_CONFIGS = ("m640", "n1280")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="n640", choices=list(CONFIGS))
+    ap.add_argument("--conf", type=float, default=0.25)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-nms-load", action="store_true")
+    ap.add_argument("--no-extra-configs", action="store_true", help="skip the m640 / n1280 blocks (N = 1 only)")
+    ap.add_argument("--miopen-benchmark", action="store_true", help="torch.backends.cudnn.benchmark (MIOpen find)")
+    args = ap.parse_args()
+    if args.miopen_benchmark:
+        torch.backends.cudnn.benchmark = True
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    head, predictor, cfg_yaml, imgsz = measure(args.config, world, rank, dev, args.steps, args.warmup, args.conf)
+    result = {"metric": METRIC, "value": head["value"], "unit": "images/s", "n_gpus": world, "steps": args.steps,
+              "warmup": args.warmup, "ms_per_step": head["ms_per_step"], "higher_is_better": True,
+              "scaling": "weak", "vs_baseline": None}
+    result.update({k: v for k, v in head.items() if k not in result})
+    result["nms_loaded"] = None
+    result["cpu_baseline"] = None
     if not args.no_nms_load:  # after the timed region, same process: NMS at controlled candidate loads
         result["nms_loaded"] = nms_loaded(dev)
+    del predictor
+    torch.cuda.empty_cache()
+    if world == 1 and args.config == "n640" and not args.no_extra_configs:
+        # configs[3] (n1280 bs 8) and configs[4] (m640 bf16 bs 64): their own timed regions, same contract
+        result["configs"] = {}
+        for name in EXTRA_CONFIGS:
+            sub, pred, _, _ = measure(name, 1, 0, dev, args.steps, args.warmup, args.conf)
+            result["configs"][name] = sub
+            del pred
+            torch.cuda.empty_cache()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             # m scale: ~4x the n model's CPU work per image - a smaller sample keeps the same ~10-30 s budget

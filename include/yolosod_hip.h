@@ -17,6 +17,7 @@
 #ifndef YOLOSOD_HIP_H
 #define YOLOSOD_HIP_H
 #include <stddef.h>
+#include <stdint.h>
 
 #ifdef __cplusplus
 extern "C" {
@@ -197,6 +198,10 @@ void yolosod_debug_set_head_x2(int on);
  * call take the split products, 0 restores the callers' choice. */
 void yolosod_debug_set_a2_x2(int on);
 void yolosod_debug_set_gemm_x2(int on);
+/* Test hook: the fp16 two-term split of the fp32-accurate matrix kernels (common.h split2) on npair pairs of v:
+ * h[i] = the fp16 pair (fp16(v[2i]), fp16(v[2i+1])), l[i] = (fp16(v[2i] - h.lo), fp16(v[2i+1] - h.hi)), as 2 x 16-bit
+ * patterns per uint32 (low half = even element). Device pointers. */
+int yolosod_debug_split_f16(const float* v, uint32_t* h, uint32_t* l, long npair, void* stream);
 
 /* ---------------------------------------------------------------------------------------------------------------
  * bf16 model config (BASELINE configs[4]): `model.to(torch.bfloat16)` after fuse() - AutoBackend's fp16

@@ -14,3 +14,25 @@ void set_error(const char* fmt, ...) {
 
 YS_EXPORT const char* yolosod_last_error(void) { return ys::g_err; }
 YS_EXPORT int yolosod_abi_version(void) { return 1; }
+
+// Test hook for the fp16 two-term split every fp32-accurate matrix kernel uses (common.h split2): h[i] / l[i] are the
+// fp16 pairs of v[2i], v[2i+1]. Lets the tests check the split bit for bit against fp16(v), fp16(v - fp16(v)).
+namespace ys {
+__global__ void debug_split_kernel(const float* __restrict__ v, uint32_t* __restrict__ h, uint32_t* __restrict__ l,
+                                   long npair) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= npair) return;
+  uint32_t hh, ll;
+  split2(f32x2{v[2 * i], v[2 * i + 1]}, hh, ll);
+  h[i] = hh;
+  l[i] = ll;
+}
+}  // namespace ys
+
+YS_EXPORT int yolosod_debug_split_f16(const float* v, uint32_t* h, uint32_t* l, long npair, void* stream) {
+  YS_CHECK_ARG(v && h && l && npair >= 0, "yolosod_debug_split_f16: bad arguments");
+  if (npair == 0) return 0;
+  ys::debug_split_kernel<<<(unsigned)((npair + 255) / 256), 256, 0, (hipStream_t)stream>>>(v, h, l, npair);
+  YS_CHECK_LAUNCH("yolosod_debug_split_f16");
+  return 0;
+}

@@ -33,7 +33,8 @@ def method_peak_tflops(key) -> float:
     """Matrix-core ceiling of the METHOD an fp32 launch runs its matrix products with: the fp32 Swin (C 64 / 256),
     A2 and head kernels compute each fp32 product as 3 fp16 MFMA products of two-term splits (csrc/swin_x3.hip,
     gemm_f32.h X2, detect_head_x2_kernel), so their ceiling is the fp16 peak / 3; everything else keeps
-    peak_tflops. Reported beside the dtype-peak fractions, never instead of them."""
+    peak_tflops. bench.py quotes every roofline fraction against this ceiling (the roof the kernel actually runs
+    on); the fraction of the dtype's peak is reported beside it as a secondary field."""
     if elem_size(key) == 4:
         op = key[0]
         split = ((op == "swin" and key[1][1] in (64, 256) and _on("YOLOSOD_SWIN_X3"))
@@ -115,10 +116,12 @@ def _op_cost(key, E):
     raise KeyError(op)
 
 
-def bound_of(key) -> str:
-    """The roof that bounds a launch: whichever of its HBM time and matrix-core time is longer."""
+def bound_of(key, method: bool = True) -> str:
+    """The roof that bounds a launch: whichever of its HBM time and matrix-core time (at the ceiling of the method
+    the launch computes with, or at the dtype peak with method=False) is longer."""
     nbytes, flops = op_cost(key)
-    return "mfma" if flops / (peak_tflops(key) * 1e12) > nbytes / (PEAK_HBM_GBS * 1e9) else "hbm"
+    peak = method_peak_tflops(key) if method else peak_tflops(key)
+    return "mfma" if flops / (peak * 1e12) > nbytes / (PEAK_HBM_GBS * 1e9) else "hbm"
 
 
 def t_min_ms(key, method: bool = False) -> float:
