@@ -6,9 +6,12 @@ element instead of fp32's 2^-24 |v| relative error. This t
 kernels split raw activations (everything downstream of a LayerNorm is unit-scale by construction): inputs scaled
 by 1e-3, the regime SURVEY App. A.11 measures for random-init activations.
 
-Bar: the error of the split path, measured against the fp64 oracle, stays within 1e-4 of the input-dependent part
-of the output (max |ref(x) - ref(0)|, so an output dominated by biases cannot hide the error), i.e. the same
-relative accuracy the unit-scale tests hold. The exact-fp32-MFMA path's error is logged beside it."""
+Bar, against the fp64 oracle: max |y - ref| <= 1e-4 max |ref| (the relative tolerance of the unit-scale tests), and
+no accuracy lost to the split: the split path's error at most 1.5x that of the same operator on the exact fp32 MFMA
+(+1e-7), so a floor that the split adds on top of fp32 rounding would show. The input-dependent part of the output,
+max |ref(x) - ref(0)|, is logged beside them (measured: split and exact errors equal to within 10-20 % at every op,
+far below the input-dependent signal at Swin, where the LayerNorms make the matrix operands unit-scale).
+"""
 import os
 
 import pytest
@@ -39,6 +42,13 @@ def _log(msg):
             f.write(f"{os.environ.get('PYTEST_CURRENT_TEST', '?')}: {msg}\n")
 
 
+def _check(err_split, err_exact, ref_max, signal, what):
+    _log(f"{what}: split err {err_split:.3g}, exact fp32 err {err_exact:.3g}, max|ref| {ref_max:.3g}, "
+         f"input-dependent signal {signal:.3g} (split err / signal {err_split / signal:.3g})")
+    assert err_split <= RTOL * ref_max, (err_split, ref_max)
+    assert err_split <= 1.5 * err_exact + 1e-7, (err_split, err_exact)
+
+
 def _run(fn, switch, on):
     lib = _hip.load_library()
     getattr(lib, switch)(on)
@@ -64,9 +74,7 @@ def test_split_small_magnitude_ops(name, cuda, monkeypatch):
     xd = x.to(cuda)
     err_split = float((_run(lambda: md(xd), switch, 1) - ref).abs().max())
     err_exact = float((_run(lambda: md(xd), switch, 0) - ref).abs().max())
-    _log(f"x*{SCALE}: split err {err_split:.3g}, exact fp32 err {err_exact:.3g}, signal {signal:.3g}, "
-         f"split err / signal {err_split / signal:.3g}")
-    assert err_split <= RTOL * signal, (err_split, signal, err_exact)
+    _check(err_split, err_exact, float(ref.abs().max()), signal, f"x*{SCALE}")
 
 
 def test_split_small_magnitude_detect_head(cuda):
@@ -97,9 +105,7 @@ def test_split_small_magnitude_detect_head(cuda):
     fn = lambda: _hip.detect_head(d(fb), d(fc), d(wb), d(bb), d(wc), d(bc), strides, nc)  # noqa: E731
     err_split = float((_run(fn, "yolosod_debug_set_head_x2", 1) - ref).abs().max())
     err_exact = float((_run(fn, "yolosod_debug_set_head_x2", 0) - ref).abs().max())
-    _log(f"features*{SCALE}: split err {err_split:.3g}, exact fp32 err {err_exact:.3g}, signal {signal:.3g}, "
-         f"split err / signal {err_split / signal:.3g}")
-    assert err_split <= RTOL * signal, (err_split, signal, err_exact)
+    _check(err_split, err_exact, float(ref.abs().max()), signal, f"features*{SCALE}")
 
 
 def test_split_is_bitwise_fp16_pair(cuda):
