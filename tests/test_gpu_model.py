@@ -154,11 +154,13 @@ def test_fused_head_second_output_is_the_reference_raw_maps(gpu_model, cuda):
                 Detect.keep_raw = False
             assert isinstance(lazy, RawMaps) and isinstance(raw, list) and len(lazy) == len(raw) == 4
             maps = list(lazy)
+            _, lazy_out = gpu_model(x)
+        maps_out = list(lazy_out)  # first read after leaving inference_mode (the features are inference tensors)
     finally:
         torch.backends.cudnn.deterministic = det
-    for a, b in zip(maps, raw):
+    for a, b, c in zip(maps, raw, maps_out):
         assert a.shape == b.shape and a.shape[1] == 74
-        assert torch.equal(a, b)
+        assert torch.equal(a, b) and torch.equal(c, b)
 
 
 def test_m_scale_model_matches_oracle(cuda):

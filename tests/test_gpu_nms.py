@@ -79,3 +79,19 @@ def test_nms_full_size_ties_vs_oracle(B, A, clusters, kw, cuda):
     for b in range(B):
         assert np.array_equal(out[b, :counts[b]], rows[b]), b
         assert np.array_equal(index[b, :counts[b]], idx[b]), b
+
+
+def test_torch_ops_reject_wrong_sized_partials_and_devices(cuda):
+    """Public torch.ops boundary: producer partials of the wrong size raise (TORCH_CHECK) instead of being read out
+    of bounds on the GPU."""
+    from yolosod_amd import _hip
+    ops = _hip.ops()
+    x = torch.randn(2, 32, 40, 40, device=cuda)
+    w1, b1 = torch.randn(4, 32, device=cuda), torch.randn(4, device=cuda)
+    w2, b2 = torch.randn(32, 4, device=cuda), torch.randn(32, device=cuda)
+    bad = torch.zeros(7, device=cuda)
+    with pytest.raises(RuntimeError, match="psum"):
+        ops.se_fwd(x, w1, b1, w2, b2, bad)
+    sa = torch.randn(98, device=cuda)
+    with pytest.raises(RuntimeError, match="psum"):
+        ops.cbam_fwd(x, w1, w2, sa, bad, bad)

@@ -25,6 +25,13 @@ void check_rc(int rc, const char* what) {
   TORCH_CHECK(rc == 0, "yolosod_amd.", what, " failed (rc=", rc, "): ", yolosod_last_error());
 }
 
+// element count of the per-plane partials a producing epilogue emits for SE / CBAM (yolosod_plane_parts)
+int64_t partials_numel(int B, int C, int H, int W) {
+  long seg = 0;
+  const int parts = yolosod_plane_parts((long)H * W, &seg);
+  return (int64_t)B * C * parts;
+}
+
 bool act_bf16(const Tensor& x, const char* what) {
   TORCH_CHECK(x.is_cuda(), what, ": HIP kernel requires a GPU tensor (got ", x.device(), "); no CPU fallback");
   TORCH_CHECK(x.dim() == 4, what, ": expected [B, C, H, W], got ", x.sizes());
@@ -54,7 +61,7 @@ Tensor se_fwd(const Tensor& x, const Tensor& fc1_w, const Tensor& fc1_b, const T
   const int B = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3), hid = fc1_w.size(0);
   Tensor y = at::empty_like(x);
   Tensor ws = workspace(yolosod_se_workspace(B, C, H, W), x);
-  const float* ps = psum ? (const float*)par(*psum, x, "psum", -1) : nullptr;
+  const float* ps = psum ? (const float*)par(*psum, x, "psum", partials_numel(B, C, H, W)) : nullptr;
   auto st = c10::hip::getCurrentHIPStream(x.get_device());
   const float* w1 = (const float*)par(fc1_w, x, "fc1.weight", (int64_t)hid * C);
   const float* b1 = (const float*)par(fc1_b, x, "fc1.bias", hid);
@@ -86,8 +93,9 @@ Tensor cbam_fwd(const Tensor& x, const Tensor& fc0_w, const Tensor& fc2_w, const
   const float* w0 = (const float*)par(fc0_w, x, "fc.0.weight", (int64_t)hid * C);
   const float* w2 = (const float*)par(fc2_w, x, "fc.2.weight", (int64_t)C * hid);
   const float* sa = (const float*)par(sa_w, x, "conv1.weight", 98);
-  const float* ps = psum ? (const float*)par(*psum, x, "psum", -1) : nullptr;
-  const float* pm = pmax ? (const float*)par(*pmax, x, "pmax", -1) : nullptr;
+  const int64_t nparts = partials_numel(B, C, H, W);  // the producer layout the kernels read: B * C * parts
+  const float* ps = psum ? (const float*)par(*psum, x, "psum", nparts) : nullptr;
+  const float* pm = pmax ? (const float*)par(*pmax, x, "pmax", nparts) : nullptr;
   int rc;
   if (bf)
     rc = yolosod_cbam_forward_bf16((const uint16_t*)x.data_ptr(), (uint16_t*)y.data_ptr(), B, C, H, W, w0, w2, hid,
@@ -237,6 +245,8 @@ Tensor detect_head_fwd(at::TensorList box_feats, at::TensorList cls_feats, at::T
   for (int i = 0; i < nl; ++i) {
     const Tensor& b = box_feats[i];
     const Tensor& c = cls_feats[i];
+    TORCH_CHECK(b.device() == x0.device() && c.device() == x0.device(), "detect_head_fwd: level ", i,
+                " features on ", b.device(), " / ", c.device(), ", level 0 on ", x0.device());
     TORCH_CHECK(act_bf16(b, "box_feats") == bf && act_bf16(c, "cls_feats") == bf && b.size(0) == B &&
                     b.size(1) == c2 && c.size(1) == c3 && b.size(2) == c.size(2) && b.size(3) == c.size(3),
                 "detect_head_fwd: level ", i, " features ", b.sizes(), " / ", c.sizes(), " mismatch");

@@ -13,6 +13,7 @@ order in which they create parameters (hence seed-for-seed identical random init
 """
 from __future__ import annotations
 
+import contextlib
 import math
 import os
 from collections.abc import Sequence
@@ -48,7 +49,9 @@ def _cached(mod: nn.Module, tag: str, srcs, make):
     conversions for the HIP operators: recomputed only when a parameter is replaced or modified in place)."""
     # inference tensors (made under torch.inference_mode, e.g. A2's folded weights) have no version counter: they
     # are never modified in place outside inference mode, their identity is the key
-    key = tuple((t.data_ptr(), -1 if t.is_inference() else t._version, t.dtype, t.device) for t in srcs)
+    # id(t) too: a replaced parameter can land at the freed address with version 0 (load_state_dict(assign=True),
+    # new Parameters), which (data_ptr, version) alone would take for the old one
+    key = tuple((id(t), t.data_ptr(), -1 if t.is_inference() else t._version, t.dtype, t.device) for t in srcs)
     cache = mod.__dict__.setdefault("_ys_cache", {})
     ent = cache.get(tag)
     if ent is None or ent[0] != key:
@@ -667,7 +670,12 @@ class RawMaps(Sequence):
 
     def materialize(self) -> list:
         if self._maps is None:
-            self._maps = [self._det.raw_from_features(i, b, c) for i, (b, c) in enumerate(self.features)]
+            # features made under inference_mode are inference tensors: read outside that mode, an autograd-
+            # recording conv on them would fail ("Inference tensors cannot be saved for backward"), so the maps are
+            # computed under inference_mode whenever the features are inference tensors
+            inf = any(t.is_inference() for pair in self.features for t in pair)
+            with torch.inference_mode(inf) if inf else contextlib.nullcontext():
+                self._maps = [self._det.raw_from_features(i, b, c) for i, (b, c) in enumerate(self.features)]
         return self._maps
 
     def __getitem__(self, i):
