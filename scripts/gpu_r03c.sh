@@ -10,4 +10,7 @@ rc=$?
 grep -E "FAILED|ERROR|passed|failed" "$OUT/pytest.log" | tail -10
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
 bash scripts/sq_run.sh "$OUT/sq" swin_L28 swin_L9 || exit 1
+YOLOSOD_LIB_AB=ablib/lib_diag.so timeout -k 10 120 python -u scripts/diag_x3.py > "$OUT/diag_x3.txt" 2>&1 || exit 1
+YOLOSOD_LIB_AB=ablib/lib_diag.so timeout -k 10 120 python -u scripts/diag_wx.py > "$OUT/diag_wx.txt" 2>&1 || exit 1
+cat "$OUT/diag_x3.txt" "$OUT/diag_wx.txt"
 exit $rc

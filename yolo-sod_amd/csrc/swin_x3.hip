@@ -36,6 +36,18 @@ namespace x3 {
 
 constexpr float WSC = 64.0f;  // weight planes hold 64 W (exact): keeps their low terms out of fp16's subnormal range
 
+#ifdef YS_DIAG_STAMPS  // diagnostic builds only (scripts/diag_x3.sh): per-stage s_memtime of wave 0, first 256 windows
+__device__ unsigned long long ys_x3_stamps[256 * 32];
+#define X3_STAMP(k)                                                                                                  \
+  do {                                                                                                               \
+    if (threadIdx.x == 0 && blockIdx.x < 256) ys_x3_stamps[blockIdx.x * 32 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define X3_STAMP(k) \
+  do {              \
+  } while (0)
+#endif
+
 
 constexpr int NR = 49;   // tokens per 7x7 window
 constexpr int HPW = 12;  // halo patch row stride (9 used)
@@ -215,6 +227,7 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
   const int gw = __builtin_amdgcn_readfirstlane((int)gwl);
   const int img = gw / p.nWin, win = gw - (gw / p.nWin) * p.nWin;
   const int wy = win / p.nWx, wx = win - (win / p.nWx) * p.nWx;
+  X3_STAMP(0);
   auto rsrc_of = [&](const float* base) {
     const unsigned long long a = (unsigned long long)base;
     return __builtin_amdgcn_make_buffer_rsrc(
@@ -272,6 +285,7 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
     for (int i = 0; i < NHS; ++i) halo[(27 * i + hslot) * HPW + hl_px] = hv[i];
   }
   __syncthreads();
+  X3_STAMP(1);
   for (int item = tid; item < C * 7; item += 256) {
     const int iy = item / C;
     const float* hp = halo + (dw_c * 9 + iy) * HPW;
@@ -293,6 +307,7 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
     }
   }
   __syncthreads();
+  X3_STAMP(2);
 
   // ---- LN1 -> X planes; Q weight chunk 0 -> X after the U1 planes (the halo there has been read) ----
   ln_planes<C, LT, PS, PL>(T, P, p.ln1_eps, tid);
@@ -303,6 +318,7 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
   WP<C, 1> f_q;  // K weight planes of column block wid
   load_wp(p.win, 3 * C, C, 0, C / 16 + wid, f_q, lane);
   __syncthreads();
+  X3_STAMP(3);
 
   // ---- QKV = U1 Win'^T + b_in' (weight planes hold 64 W). Wave w computes Q of its own 16 query rows (four column
   // blocks of one row block: kept in registers for the attention) and the K and V column blocks w of all 64 token
@@ -329,9 +345,11 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
     for (int s2 = 0; s2 < C / 32; ++s2) {
       if (s2 == 1) {
         __syncthreads();  // every wave has read chunk 0
+        X3_STAMP(4);
         *reinterpret_cast<uint4*>(qdst) = qc1a;
         *reinterpret_cast<uint4*>(qdst + 8) = qc1b;
         __syncthreads();
+        X3_STAMP(5);
       }
       const h16_t* wq = QW + lane * 8;
 #pragma unroll
@@ -350,6 +368,7 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
   WP<C, 1> f_o;
   load_wp(p.wo, C, C, 0, wid, f_o, lane);  // out-proj planes: in flight during attention
   __syncthreads();  // every wave has read U1
+  X3_STAMP(6);
 #pragma unroll
   for (int rb = 0; rb < 4; ++rb) {
     const int tok = rb * 16 + l15;
@@ -378,6 +397,7 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
     ql[hh] = __builtin_bit_cast(f16x8_t, make_uint4(l0.x, l0.y, l1.x, l1.y));
   }
   __syncthreads();  // K / V planes complete
+  X3_STAMP(7);
   WP<C, 1> f_1a;
   load_wp(p.w1, HID, C, 0, wid, f_1a, lane);  // MLP1 (hidden half 0) planes
 
@@ -456,12 +476,14 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
     }
   }
   __syncthreads();
+  X3_STAMP(8);
 #pragma unroll
   for (int h = 0; h < NH; ++h)
 #pragma unroll
     for (int db = 0; db < HD / 16; ++db)
       store_planes4<PS, PL>(P, wid * 16 + l15, h * HD + db * 16 + 4 * g, ov[h][db]);
   __syncthreads();
+  X3_STAMP(9);
 
   // ---- T += O Wo^T + bo ----
   WP<C, 1> f_1b;
@@ -482,12 +504,14 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
     }
   }
   __syncthreads();
+  X3_STAMP(10);
 
   // ---- LN2 -> X planes ----
   ln_planes<C, LT, PS, PL>(T, P, p.ln2_eps, tid);
   WP<C, 1> f_2a;
   load_wp(p.w2, C, HID, 0, wid, f_2a, lane);  // MLP2 planes, k in [0, 64)
   __syncthreads();
+  X3_STAMP(11);
 
   // ---- MLP: both hidden halves Hh = GELU(U2 W1h'^T + b1h') into registers; then half by half as planes into X,
   // each followed by its MLP2 partial acc2 += Hh W2[:, half]^T ----
@@ -518,9 +542,11 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
     __syncthreads();  // every wave has read X (U2, then hidden half 0)
+    X3_STAMP(12 + 2 * half);
 #pragma unroll
     for (int rb = 0; rb < 4; ++rb) store_planes4<PS, PL>(P, rb * 16 + l15, wid * 16 + 4 * g, hid[half][rb]);
     __syncthreads();
+    X3_STAMP(13 + 2 * half);
     gemm_x3<C, 1, PS, PL>(P, half == 0 ? f_2a : f_2b, acc2, lane);
   }
 
@@ -545,6 +571,7 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
 
   // ---- final T = T + MLP -> X planes (rows >= 49 zero): the pw GEMM's operand ----
   __syncthreads();  // every wave has read hidden half 1
+  X3_STAMP(16);
 #pragma unroll
   for (int rb = 0; rb < 4; ++rb) {
     const int tok = rb * 16 + l15;
@@ -553,6 +580,7 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
     store_planes4<PS, PL>(P, tok, wid * 16 + 4 * g, v);
   }
   __syncthreads();
+  X3_STAMP(17);
 
   // ---- y = x + SiLU(BN(Wpw T^T)): tile Y^T[c][tok], lane holds c = wid*16 + 4g + r, token tb*16 + l15 ----
   {
@@ -569,7 +597,7 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
         __builtin_amdgcn_raw_buffer_store_b32(
             __builtin_bit_cast(unsigned, xr[tb][r] + silu_fast_(acc[tb][0][r] * sc[r] + sh[r])), ry, vtok[tb],
             r * HWi * 4, 0);
-  }
+  }  X3_STAMP(18);
 }
 
 // ---- C = 256 (the P4 instance L9: 4 heads of 64, MLP hidden 512) -------------------------------------------------
@@ -1245,6 +1273,9 @@ int yolosod_swin_x3_launch(const float* x, float* y, int B, int C, int H, int W,
 }
 
 #ifdef YS_DIAG_STAMPS
+YS_EXPORT int yolosod_diag_x3_stamps(unsigned long long* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(x3::ys_x3_stamps), sizeof(x3::ys_x3_stamps)) == hipSuccess ? 0 : -1;
+}
 YS_EXPORT int yolosod_diag_wx_stamps(unsigned long long* host) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(x3::wx::ys_wx_stamps), sizeof(x3::wx::ys_wx_stamps)) == hipSuccess ? 0 : -1;
 }
