@@ -202,6 +202,9 @@ void yolosod_debug_set_gemm_x2(int on);
  * h[i] = the fp16 pair (fp16(v[2i]), fp16(v[2i+1])), l[i] = (fp16(v[2i] - h.lo), fp16(v[2i+1] - h.hi)), as 2 x 16-bit
  * patterns per uint32 (low half = even element). Device pointers. */
 int yolosod_debug_split_f16(const float* v, uint32_t* h, uint32_t* l, long npair, void* stream);
+/* Test hook: the kernel of yolosod_gemm_bf16 / the bf16 operators' K-contiguous GEMMs without a LayerNorm prologue:
+ * 0 (default; env YOLOSOD_GEMMB_GLDS) register-staged kernel, 3 / 2 LDS-DMA staged ring of 3 / 2 buffers. */
+void yolosod_debug_set_gemmb_glds(int mode);
 
 /* ---------------------------------------------------------------------------------------------------------------
  * bf16 model config (BASELINE configs[4]): `model.to(torch.bfloat16)` after fuse() - AutoBackend's fp16

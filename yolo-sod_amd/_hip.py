@@ -68,6 +68,7 @@ SIGNATURES = {
     "yolosod_debug_set_a2_x2": (None, [_i]),
     "yolosod_debug_set_gemm_x2": (None, [_i]),
     "yolosod_debug_split_f16": (_i, [_vp, _vp, _vp, _l, _vp]),
+    "yolosod_debug_set_gemmb_glds": (None, [_i]),
     "yolosod_mamba_glu_workspace": (_sz, [_i, _i, _i, _i, _i, _i]),
     "yolosod_mamba_glu_forward": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _f, _vp, _vp,
                                        _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp, _vp, _vp, _f, _vp, _sz, _vp]),

@@ -113,8 +113,12 @@ __device__ __forceinline__ void load_wp(const h16_t* __restrict__ Wp, int N, int
     for (int s = 0; s < K / 32; ++s)
 #pragma unroll
       for (int j = 0; j < NJ; ++j)
+#ifdef YS_ABL_WLOAD
+        f.v[j][s][p] = *reinterpret_cast<const f16x8_t*>(Wp + (long)(p * 64 + lane) * 8);
+#else
         f.v[j][s][p] = *reinterpret_cast<const f16x8_t*>(
             Wp + (long)p * N * KT + ((long)((cb0 + 4 * j) * (KT / 32) + koff / 32 + s) * 64 + lane) * 8);
+#endif
 }
 
 // acc[rb][j] += (A[rows rb*16 .. +15][0, K) . W^T)^T: A = three LDS planes (row stride PS, plane stride PL), the
@@ -187,7 +191,10 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
   constexpr int HD = C / NH;
   constexpr int HID = 2 * C;
   constexpr int LT = C + 4;      // T row stride (floats)
-  constexpr int PS = C + 8;      // plane row stride (fp16)
+#ifndef YS_X3_PS_PAD  // plane row padding (fp16 elements); diagnostic builds vary it
+#define YS_X3_PS_PAD 8
+#endif
+  constexpr int PS = C + YS_X3_PS_PAD;  // plane row stride (fp16)
   constexpr int PL = 64 * PS;    // plane stride
   constexpr int PSK = C + 8;     // K plane row stride
   constexpr int KPL = NR * PSK;  // K plane stride
@@ -205,7 +212,10 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
   static_assert(T_B % 16 == 0 && X_B % 16 == 0, "16-byte aligned regions");
   static_assert(T_B + X_B + NPAR * 4 <= 160 * 1024 / 3, "three workgroups per CU");
   static_assert(PLN_B + 8 * 512 * 2 <= X_B, "staged Q weight chunk after the U1 planes");
-  __shared__ __attribute__((aligned(16))) char smem[T_B + X_B + NPAR * 4];
+#ifndef YS_X3_LDS_PAD  // diagnostic builds only: extra LDS per workgroup to measure the kernel at lower occupancy
+#define YS_X3_LDS_PAD 0
+#endif
+  __shared__ __attribute__((aligned(16))) char smem[T_B + X_B + NPAR * 4 + YS_X3_LDS_PAD];
   float* T = reinterpret_cast<float*>(smem);
   char* X = smem + T_B;
   float* Q = reinterpret_cast<float*>(X);
@@ -300,9 +310,13 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
     const bool rowok = wy * 7 + iy < H;
 #pragma unroll
     for (int ix = 0; ix < 7; ++ix) {
+#ifdef YS_ABL_DW
+      const float v = dwk[4] * r[1][ix + 1];
+#else
       const float v = dwk[0] * r[0][ix] + dwk[1] * r[0][ix + 1] + dwk[2] * r[0][ix + 2] + dwk[3] * r[1][ix] +
                       dwk[4] * r[1][ix + 1] + dwk[5] * r[1][ix + 2] + dwk[6] * r[2][ix] + dwk[7] * r[2][ix + 1] +
                       dwk[8] * r[2][ix + 2];
+#endif
       T[(iy * 7 + ix) * LT + dw_c] = (rowok && wx * 7 + ix < W) ? v : 0.f;
     }
   }
@@ -442,7 +456,11 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
       for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
+#ifdef YS_ABL_EXP
+          const float e = fmaf(st[hh][kb][r], c2, mc);
+#else
           const float e = __builtin_amdgcn_exp2f(fmaf(st[hh][kb][r], c2, mc));
+#endif
           st[hh][kb][r] = e;
           sum += e;
         }
@@ -522,12 +540,18 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
     const f32x4 b = *reinterpret_cast<const f32x4*>(par + P_B1 + (wid + 4 * half) * 16 + 4 * g);
 #pragma unroll
     for (int rb = 0; rb < 4; ++rb) acc[rb][0] = b;
+#ifndef YS_ABL_MLPMFMA
     gemm_x3<C, 1, PS, PL>(P, half == 0 ? f_1a : f_1b, acc, lane);
+#endif
 #pragma unroll
     for (int rb = 0; rb < 4; ++rb) {
       const f32x4 a = acc[rb][0] * (1.0f / WSC);
+#ifdef YS_ABL_GELU  // ablation builds only (timing sensitivity; wrong results)
+      const f32x2 lo = f32x2{a[0], a[1]}, hi = f32x2{a[2], a[3]};
+#else
       const f32x2 lo = gelu2_fast_(f32x2{a[0], a[1]});
       const f32x2 hi = gelu2_fast_(f32x2{a[2], a[3]});
+#endif
       hid[half][rb] = f32x4{lo.x, lo.y, hi.x, hi.y};
     }
   }
@@ -547,7 +571,9 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
     for (int rb = 0; rb < 4; ++rb) store_planes4<PS, PL>(P, rb * 16 + l15, wid * 16 + 4 * g, hid[half][rb]);
     __syncthreads();
     X3_STAMP(13 + 2 * half);
+#ifndef YS_ABL_MLPMFMA
     gemm_x3<C, 1, PS, PL>(P, half == 0 ? f_2a : f_2b, acc2, lane);
+#endif
   }
 
   // pw planes and this lane's residual x / BN terms: in flight during the final T update
