@@ -71,6 +71,21 @@ int yolosod_swin_forward(const float* x, float* y, int B, int C, int H, int W, i
                          const float* mlp2_b, const float* pw_w, const float* bn_w, const float* bn_b,
                          const float* bn_mean, const float* bn_var, float bn_eps, void* workspace,
                          size_t workspace_bytes, void* stream);
+/* The same forward with the parameter preparation (weight split into fp16 planes with the LayerNorm affines folded,
+ * BN fold) done once by the caller and kept across calls, for the shapes of the fp16-split kernels (7x7 windows,
+ * C = 64 / 2 heads and C = 256 / 4 heads, mlp_hidden = 2C): yolosod_swin_prep_bytes returns the block's size (0 when
+ * (C, heads, hidden) has no such kernel), yolosod_swin_prepare fills a caller-owned block from the parameters of
+ * yolosod_swin_forward (re-run it whenever a parameter changes), yolosod_swin_forward_prepared runs the block. */
+size_t yolosod_swin_prep_bytes(int C, int num_heads, int mlp_hidden);
+int yolosod_swin_prepare(int C, int num_heads, int mlp_hidden, const float* ln1_w, const float* ln1_b,
+                         const float* in_proj_w, const float* in_proj_b, const float* out_proj_w, const float* ln2_w,
+                         const float* ln2_b, const float* mlp1_w, const float* mlp1_b, const float* mlp2_w,
+                         const float* pw_w, const float* bn_w, const float* bn_b, const float* bn_mean,
+                         const float* bn_var, float bn_eps, void* prep, size_t prep_bytes, void* stream);
+int yolosod_swin_forward_prepared(const float* x, float* y, int B, int C, int H, int W, int num_heads, int window,
+                                  const float* dw_w, float ln1_eps, const float* out_proj_b, float ln2_eps,
+                                  int mlp_hidden, const float* mlp2_b, const void* prep, size_t prep_bytes,
+                                  void* stream);
 
 /* Producer-side statistics for the channel gates (SE smallobj_modules.py:87, CBAM cbam_block.py:14-17): a conv
  * epilogue that also writes its output's per-plane partial sums (+ maxes when pmax != NULL) in the segmentation

@@ -439,3 +439,38 @@ def test_conv1x1_thin_stats_feed_se_and_cbam(B, Cin, H, W, stats, cuda):
             c = m(with_stats)
         ok, err, _ = tol_close(c.cpu(), a.cpu(), 1e-6, 1e-5)
         assert ok, (type(m).__name__, err)
+
+
+@pytest.mark.parametrize("name", ["swin_L28", "swin_L9"])
+def test_swin_prepared_parameters_cached_and_refreshed(name, cuda, monkeypatch):
+    """SwinBlock caches the fp16-split kernels' weight split across calls (swin_prep / swin_fwd_prepared): the
+    prepared call is bitwise the per-call-prepared one (same kernels), it is made once, and an in-place parameter
+    update (version bump) rebuilds it."""
+    from yolosod_amd import _hip
+    monkeypatch.setitem(recipes.OPS, name, REAL[name])
+    m, _ = build_fixture_module(name)
+    m = m.to(cuda)
+    x = recipes.make_input(name, REAL[name][2]).to(cuda)
+    wa = m.window_attn
+    with torch.inference_mode():
+        y1 = m(x)
+        prep1 = m._ys_cache["x3prep"][1]
+        y2 = m(x)
+        assert m._ys_cache["x3prep"][1] is prep1  # cached, not rebuilt
+        ref = _hip.swin_forward(  # unprepared entry point: the split done inside the call
+            x, wa.attn.num_heads, wa.window_size, m.dw.weight, wa.norm1.weight, wa.norm1.bias, wa.norm1.eps,
+            wa.attn.in_proj_weight, wa.attn.in_proj_bias, wa.attn.out_proj.weight, wa.attn.out_proj.bias,
+            wa.norm2.weight, wa.norm2.bias, wa.norm2.eps, wa.mlp[0].weight, wa.mlp[0].bias, wa.mlp[2].weight,
+            wa.mlp[2].bias, m.pw.weight, m.bn.weight, m.bn.bias, m.bn.running_mean, m.bn.running_var, m.bn.eps)
+    assert torch.equal(y1, y2) and torch.equal(y1, ref)
+    with torch.no_grad():
+        wa.mlp[2].weight.mul_(1.5)
+    with torch.inference_mode():
+        y3 = m(x)
+        assert m._ys_cache["x3prep"][1] is not prep1
+        ref3 = _hip.swin_forward(
+            x, wa.attn.num_heads, wa.window_size, m.dw.weight, wa.norm1.weight, wa.norm1.bias, wa.norm1.eps,
+            wa.attn.in_proj_weight, wa.attn.in_proj_bias, wa.attn.out_proj.weight, wa.attn.out_proj.bias,
+            wa.norm2.weight, wa.norm2.bias, wa.norm2.eps, wa.mlp[0].weight, wa.mlp[0].bias, wa.mlp[2].weight,
+            wa.mlp[2].bias, m.pw.weight, m.bn.weight, m.bn.bias, m.bn.running_mean, m.bn.running_var, m.bn.eps)
+    assert torch.equal(y3, ref3) and not torch.equal(y3, y1)

@@ -69,6 +69,10 @@ SIGNATURES = {
     "yolosod_debug_set_gemm_x2": (None, [_i]),
     "yolosod_debug_split_f16": (_i, [_vp, _vp, _vp, _l, _vp]),
     "yolosod_debug_set_gemmb_glds": (None, [_i]),
+    "yolosod_swin_prep_bytes": (_sz, [_i, _i, _i]),
+    "yolosod_swin_prepare": (_i, [_i, _i, _i] + [_vp] * 15 + [_f, _vp, _sz, _vp]),
+    "yolosod_swin_forward_prepared": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _f, _vp, _f, _i, _vp, _vp, _sz,
+                                           _vp]),
     "yolosod_mamba_glu_workspace": (_sz, [_i, _i, _i, _i, _i, _i]),
     "yolosod_mamba_glu_forward": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _f, _vp, _vp,
                                        _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp, _vp, _vp, _f, _vp, _sz, _vp]),
@@ -321,9 +325,11 @@ def a2_forward(x, num_areas, num_heads, proj_w, proj_b, ln_w, ln_b, ln_eps, in_w
 
 
 def swin_forward(x, num_heads, window, dw_w, ln1_w, ln1_b, ln1_eps, in_w, in_b, out_w, out_b, ln2_w, ln2_b,
-                 ln2_eps, m1_w, m1_b, m2_w, m2_b, pw_w, bn_w, bn_b, bn_mean, bn_var, bn_eps):
+                 ln2_eps, m1_w, m1_b, m2_w, m2_b, pw_w, bn_w, bn_b, bn_mean, bn_var, bn_eps, prep=None):
     """SwinBlock -> torch.ops.yolosod.swin_fwd on fp32 or bf16 activations. bf16: the projection / MLP / pw weights
-    (in_w, out_w, m1_w, m2_w, pw_w) are bf16, every other parameter fp32."""
+    (in_w, out_w, m1_w, m2_w, pw_w) are bf16, every other parameter fp32. ``prep``: a callable returning the cached
+    prepared-parameter block (swin_prepare) - used when the shape takes the fp16-split kernels
+    (torch.ops.yolosod.swin_fwd_prepared: the weight split is not redone per call)."""
     bf = _act_dtype(_t(x, "x"))
     B, C, H, W = x.shape
     hid = m1_w.shape[0]
@@ -333,10 +339,27 @@ def swin_forward(x, num_heads, window, dw_w, ln1_w, ln1_b, ln1_eps, in_w, in_b, 
         raise RuntimeError(f"SwinBlock: window of {wh}x{ww} tokens unsupported")
     if C % num_heads or (C // num_heads) not in ((32, 64, 128) if bf else (8, 16, 32, 64, 128)):
         raise RuntimeError(f"SwinBlock: head dim {C}/{num_heads} unsupported")
-    return _launch(("swin", tuple(x.shape), (num_heads, window, hid)) + ((2,) if bf else ()), x.device, ops().swin_fwd,
-                   x, int(num_heads), int(window), dw_w, ln1_w, ln1_b, float(ln1_eps), in_w, in_b, out_w, out_b,
-                   ln2_w, ln2_b, float(ln2_eps), m1_w, m1_b, m2_w, m2_b, pw_w, bn_w, bn_b, bn_mean, bn_var,
-                   float(bn_eps))
+    key = ("swin", tuple(x.shape), (num_heads, window, hid)) + ((2,) if bf else ())
+    if prep is not None and not bf and wh == 7 and ww == 7 and swin_prep_bytes(C, num_heads, hid) > 0:
+        # the weight split / folds were made once (``prep`` = swin_prepare of these parameters): one kernel launch
+        return _launch(key, x.device, ops().swin_fwd_prepared, x, prep(), int(num_heads), int(window), dw_w,
+                       float(ln1_eps), out_b, float(ln2_eps), int(hid), m2_b)
+    return _launch(key, x.device, ops().swin_fwd, x, int(num_heads), int(window), dw_w, ln1_w, ln1_b, float(ln1_eps),
+                   in_w, in_b, out_w, out_b, ln2_w, ln2_b, float(ln2_eps), m1_w, m1_b, m2_w, m2_b, pw_w, bn_w, bn_b,
+                   bn_mean, bn_var, float(bn_eps))
+
+
+def swin_prep_bytes(C, num_heads, hid) -> int:
+    """Size of the fp16-split Swin kernels' prepared-parameter block (0: no prepared path for this shape, or the
+    split kernels are switched off - yolosod_debug_set_swin_x3 / YOLOSOD_SWIN_X3=0)."""
+    return int(load_library().yolosod_swin_prep_bytes(int(C), int(num_heads), int(hid)))
+
+
+def swin_prepare(x, num_heads, ln1_w, ln1_b, in_w, in_b, out_w, ln2_w, ln2_b, m1_w, m1_b, m2_w, pw_w, bn_w, bn_b,
+                 bn_mean, bn_var, bn_eps):
+    """The prepared-parameter block (uint8 tensor on x's device) for swin_forward(..., prep=...)."""
+    return ops().swin_prep(x, int(num_heads), ln1_w, ln1_b, in_w, in_b, out_w, ln2_w, ln2_b, m1_w, m1_b, m2_w, pw_w,
+                           bn_w, bn_b, bn_mean, bn_var, float(bn_eps))
 
 
 def mamba_glu_forward(x, reduction, in_w, in_bn_w, in_bn_b, in_bn_m, in_bn_v, in_eps, pw1_w, dw_w, bn_w, bn_b, bn_m,

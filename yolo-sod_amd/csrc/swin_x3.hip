@@ -125,7 +125,9 @@ __device__ __forceinline__ void load_wp(const h16_t* __restrict__ Wp, int N, int
 // weight planes as the MFMA A operand, so the lane holds out[token rb*16 + l15][n = cb*16 + 4g .. +3]. Six products
 // per (k-step, row block, column block), smallest terms first. The LDS operand reads run two (k-step, row block)
 // steps ahead of the MFMAs (at two waves per SIMD a read waited for right before its MFMAs exposes its latency).
-template <int K, int NJ, int PS, int PL>
+// SWAP: the token rows are the MFMA's A operand and the weight planes its B operand (the same fragments), so the
+// lane holds out[token rb*16 + 4g .. +3][n = cb*16 + l15] instead (4 consecutive tokens of one output column).
+template <int K, int NJ, int PS, int PL, bool SWAP = false>
 __device__ __forceinline__ void gemm_x3(const h16_t* A, const WP<K, NJ>& w, f32x4 (&acc)[4][NJ], int lane) {
   const int l15 = lane & 15, g = lane >> 4;
   constexpr int NS = (K / 32) * 4;  // steps (s, rb), rb fastest
@@ -138,6 +140,9 @@ __device__ __forceinline__ void gemm_x3(const h16_t* A, const WP<K, NJ>& w, f32x
   };
   ld(0, u[0]);
   ld(1, u[1]);
+#ifdef YS_X3_PRIO  // experiment: the MFMA clusters issue at raised wave priority
+  __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll
   for (int i = 0; i < NS; ++i) {
     if (i + 2 < NS) ld(i + 2, u[(i + 2) % 3]);
@@ -146,11 +151,20 @@ __device__ __forceinline__ void gemm_x3(const h16_t* A, const WP<K, NJ>& w, f32x
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       f32x4 c = acc[rb][j];
-      c = mfma16(w.v[j][s][1], v[0], c);
-      c = mfma16(w.v[j][s][0], v[1], c);
-      acc[rb][j] = mfma16(w.v[j][s][0], v[0], c);
+      if (SWAP) {
+        c = mfma16(v[0], w.v[j][s][1], c);
+        c = mfma16(v[1], w.v[j][s][0], c);
+        acc[rb][j] = mfma16(v[0], w.v[j][s][0], c);
+      } else {
+        c = mfma16(w.v[j][s][1], v[0], c);
+        c = mfma16(w.v[j][s][0], v[1], c);
+        acc[rb][j] = mfma16(w.v[j][s][0], v[0], c);
+      }
     }
   }
+#ifdef YS_X3_PRIO
+  __builtin_amdgcn_s_setprio(0);
+#endif
 }
 
 // LayerNorm statistics of token rows [0, 49) of T (fp32, stride LT) and the normalised rows (affine folded into the
@@ -296,28 +310,40 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
   }
   __syncthreads();
   X3_STAMP(1);
-  for (int item = tid; item < C * 7; item += 256) {
-    const int iy = item / C;
-    const float* hp = halo + (dw_c * 9 + iy) * HPW;
-    float r[3][12];
+  {
+    // wave w computes output rows 2w and 2w + 1 (wave 3: row 6) of channel dw_c: the four halo rows they need are
+    // read once (12 16-byte LDS reads for 14 outputs)
+    const int iy0 = 2 * wid;
+    const int nrow = iy0 + 1 < 7 ? 2 : 1;
+    const float* hp = halo + (dw_c * 9 + iy0) * HPW;
+    float r[4][12];
 #pragma unroll
-    for (int ky = 0; ky < 3; ++ky)
+    for (int ky = 0; ky < 4; ++ky) {
+      if (ky < nrow + 2) {
 #pragma unroll
-      for (int q4 = 0; q4 < 3; ++q4) {
-        const float4 v = *reinterpret_cast<const float4*>(hp + ky * HPW + 4 * q4);
-        r[ky][4 * q4] = v.x; r[ky][4 * q4 + 1] = v.y; r[ky][4 * q4 + 2] = v.z; r[ky][4 * q4 + 3] = v.w;
+        for (int q4 = 0; q4 < 3; ++q4) {
+          const float4 v = *reinterpret_cast<const float4*>(hp + ky * HPW + 4 * q4);
+          r[ky][4 * q4] = v.x; r[ky][4 * q4 + 1] = v.y; r[ky][4 * q4 + 2] = v.z; r[ky][4 * q4 + 3] = v.w;
+        }
       }
-    const bool rowok = wy * 7 + iy < H;
+    }
 #pragma unroll
-    for (int ix = 0; ix < 7; ++ix) {
+    for (int d = 0; d < 2; ++d) {
+      if (d < nrow) {
+        const int iy = iy0 + d;
+        const bool rowok = wy * 7 + iy < H;
+#pragma unroll
+        for (int ix = 0; ix < 7; ++ix) {
 #ifdef YS_ABL_DW
-      const float v = dwk[4] * r[1][ix + 1];
+          const float v = dwk[4] * r[d + 1][ix + 1];
 #else
-      const float v = dwk[0] * r[0][ix] + dwk[1] * r[0][ix + 1] + dwk[2] * r[0][ix + 2] + dwk[3] * r[1][ix] +
-                      dwk[4] * r[1][ix + 1] + dwk[5] * r[1][ix + 2] + dwk[6] * r[2][ix] + dwk[7] * r[2][ix + 1] +
-                      dwk[8] * r[2][ix + 2];
+          const float v = dwk[0] * r[d][ix] + dwk[1] * r[d][ix + 1] + dwk[2] * r[d][ix + 2] + dwk[3] * r[d + 1][ix] +
+                          dwk[4] * r[d + 1][ix + 1] + dwk[5] * r[d + 1][ix + 2] + dwk[6] * r[d + 2][ix] +
+                          dwk[7] * r[d + 2][ix + 1] + dwk[8] * r[d + 2][ix + 2];
 #endif
-      T[(iy * 7 + ix) * LT + dw_c] = (rowok && wx * 7 + ix < W) ? v : 0.f;
+          T[(iy * 7 + ix) * LT + dw_c] = (rowok && wx * 7 + ix < W) ? v : 0.f;
+        }
+      }
     }
   }
   __syncthreads();
@@ -371,12 +397,18 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
         qa[cq] = mfma_f16x3(*reinterpret_cast<const f16x8_t*>(wq + cq * 512),
                             *reinterpret_cast<const f16x8_t*>(wq + (4 + cq) * 512), ua[s2][0], ua[s2][1], qa[cq]);
     }
+    {
+      // K (token-major tile, as the attention reads it) and V (transposed tile: 4 consecutive keys of one head
+      // dim per lane, stored as V^T rows with 8-byte writes)
+      const f32x4 bk = *reinterpret_cast<const f32x4*>(par + P_BIN + (C / 16 + wid) * 16 + 4 * g);
+      const float bv = par[P_BIN + 2 * C + wid * 16 + l15];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const f32x4 b = *reinterpret_cast<const f32x4*>(par + P_BIN + ((j + 1) * C / 16 + wid) * 16 + 4 * g);
-#pragma unroll
-      for (int rb = 0; rb < 4; ++rb) akv[j][rb][0] = b;
-      gemm_x3<C, 1, PS, PL>(P, j == 0 ? f_q : f_n, akv[j], lane);
+      for (int rb = 0; rb < 4; ++rb) {
+        akv[0][rb][0] = bk;
+        akv[1][rb][0] = f32x4{bv, bv, bv, bv};
+      }
+      gemm_x3<C, 1, PS, PL>(P, f_q, akv[0], lane);
+      gemm_x3<C, 1, PS, PL, true>(P, f_n, akv[1], lane);
     }
   }
   WP<C, 1> f_o;
@@ -388,16 +420,10 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
     const int tok = rb * 16 + l15;
     if (tok < NR) store_planes4<PSK, KPL>(Kp, tok, wid * 16 + 4 * g, akv[0][rb][0]);  // K, V, Q stay x64
     uint2 h, l;
-    split4(akv[1][rb][0], h, l);
-    h16_t* vd = Vt + (wid * 16 + 4 * g) * PSV + tok;
-    vd[0] = (h16_t)(h.x & 0xffffu);
-    vd[PSV] = (h16_t)(h.x >> 16);
-    vd[2 * PSV] = (h16_t)(h.y & 0xffffu);
-    vd[3 * PSV] = (h16_t)(h.y >> 16);
-    vd[VPL] = (h16_t)(l.x & 0xffffu);
-    vd[VPL + PSV] = (h16_t)(l.x >> 16);
-    vd[VPL + 2 * PSV] = (h16_t)(l.y & 0xffffu);
-    vd[VPL + 3 * PSV] = (h16_t)(l.y >> 16);
+    split4(akv[1][rb][0], h, l);  // V^T[d = wid*16 + l15][keys rb*16 + 4g .. +3]
+    h16_t* vd = Vt + (wid * 16 + l15) * PSV + rb * 16 + 4 * g;
+    *reinterpret_cast<uint2*>(vd) = h;
+    *reinterpret_cast<uint2*>(vd + VPL) = l;
   }
   // this wave's queries as the B operand of S^T = K Q^T, per head: k slot j of lane group g is head dim
   // 4g + j (j < 4) or 16 + 4g + j - 4 (the lane's own two Q column blocks); K is read with the same permutation
@@ -1254,36 +1280,65 @@ size_t yolosod_swin_x3_workspace(int C, int mlp_hidden) {
   return s.off;
 }
 
-// returns 1 if launched, 0 if the shape is not handled, < 0 on error
-int yolosod_swin_x3_launch(const float* x, float* y, int B, int C, int H, int W, int num_heads, int wh, int ww,
-                           int nWx, int nWin,
-                           const float* dw_w, const float* ln1_w, const float* ln1_b, float ln1_eps,
-                           const float* in_proj_w, const float* in_proj_b, const float* out_proj_w,
-                           const float* out_proj_b, const float* ln2_w, const float* ln2_b, float ln2_eps,
-                           const float* mlp1_w, const float* mlp1_b, int mlp_hidden, const float* mlp2_w,
-                           const float* mlp2_b, const float* pw_w, const float* bn_w, const float* bn_b,
-                           const float* bn_mean, const float* bn_var, float bn_eps, void* workspace,
-                           size_t workspace_bytes, hipStream_t st) {
-  if (!yolosod_swin_x3_ok(C, num_heads, wh, ww, mlp_hidden)) return 0;
-  if ((long)C * H * W >= (1L << 30) || (long)B * nWin >= (1L << 31)) return 0;
-  Carver cv(workspace, workspace_bytes);
-  h16_t* pin = cv.take<h16_t>((size_t)2 * 3 * C * C);
-  h16_t* po = cv.take<h16_t>((size_t)2 * C * C);
-  h16_t* p1 = cv.take<h16_t>((size_t)2 * mlp_hidden * C);
-  h16_t* p2 = cv.take<h16_t>((size_t)2 * C * mlp_hidden);
-  h16_t* ppw = cv.take<h16_t>((size_t)2 * C * C);
+// The prepared-parameter block of the fp16-split kernels (written by swin_x3_prep_kernel): weight planes of in_proj
+// (LN1 folded), out_proj, mlp1 (LN2 folded), mlp2, pw; folded in_proj / mlp1 biases; BN scale / shift.
+struct X3Prep {
+  h16_t *pin, *po, *p1, *p2, *ppw;
+  float *bin_f, *b1_f, *bn_sc, *bn_sh;
+};
+static bool x3_carve(void* buf, size_t bytes, int C, int mlp_hidden, X3Prep& q) {
+  Carver cv(buf, bytes);
+  q.pin = cv.take<h16_t>((size_t)2 * 3 * C * C);
+  q.po = cv.take<h16_t>((size_t)2 * C * C);
+  q.p1 = cv.take<h16_t>((size_t)2 * mlp_hidden * C);
+  q.p2 = cv.take<h16_t>((size_t)2 * C * mlp_hidden);
+  q.ppw = cv.take<h16_t>((size_t)2 * C * C);
   float* fb = cv.take<float>((size_t)3 * C + mlp_hidden + 2 * C);
-  if (!fb) {
-    set_error("swin_x3: workspace too small (%zu)", workspace_bytes);
+  if (!fb) return false;
+  q.bin_f = fb;
+  q.b1_f = fb + 3 * C;
+  q.bn_sc = fb + 3 * C + mlp_hidden;
+  q.bn_sh = fb + 4 * C + mlp_hidden;
+  return true;
+}
+
+// weight split / folds into a prepared block (C, heads, mlp_hidden must satisfy yolosod_swin_x3_ok)
+int yolosod_swin_x3_prepare(int C, int mlp_hidden, const float* ln1_w, const float* ln1_b, const float* in_proj_w,
+                            const float* in_proj_b, const float* out_proj_w, const float* ln2_w, const float* ln2_b,
+                            const float* mlp1_w, const float* mlp1_b, const float* mlp2_w, const float* pw_w,
+                            const float* bn_w, const float* bn_b, const float* bn_mean, const float* bn_var,
+                            float bn_eps, void* prep, size_t prep_bytes, hipStream_t st) {
+  X3Prep q;
+  if (!x3_carve(prep, prep_bytes, C, mlp_hidden, q)) {
+    set_error("swin_x3: prepared-parameter buffer too small (%zu)", prep_bytes);
     return -1;
   }
   x3::PrepArgs pa{in_proj_w, in_proj_b, ln1_w, ln1_b, out_proj_w, mlp1_w, mlp1_b, ln2_w, ln2_b, mlp2_w, pw_w,
-                  bn_w, bn_b, bn_mean, bn_var, bn_eps, C, mlp_hidden, pin, po, p1, p2, ppw,
-                  fb, fb + 3 * C, fb + 3 * C + mlp_hidden, fb + 4 * C + mlp_hidden};
+                  bn_w, bn_b, bn_mean, bn_var, bn_eps, C, mlp_hidden, q.pin, q.po, q.p1, q.p2, q.ppw,
+                  q.bin_f, q.b1_f, q.bn_sc, q.bn_sh};
   const int rows = 3 * C + C + mlp_hidden + C + C + C;
   hipLaunchKernelGGL(x3::swin_x3_prep_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, pa);
-  x3::Args a{x, y, B, H, W, nWx, nWin, dw_w, ln1_eps, ln2_eps, pin, fb, po, out_proj_b, p1, fb + 3 * C, p2, mlp2_b,
-             ppw, fb + 3 * C + mlp_hidden, fb + 4 * C + mlp_hidden, 1.0f / sqrtf((float)(C / num_heads))};
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("swin_x3_prep: launch failed: %s", hipGetErrorString(e));
+    return -1;
+  }
+  return 0;
+}
+
+// the per-window kernel on a prepared block; returns 1 if launched, 0 if the shape is not handled, < 0 on error
+int yolosod_swin_x3_run(const float* x, float* y, int B, int C, int H, int W, int num_heads, int wh, int ww, int nWx,
+                        int nWin, const float* dw_w, float ln1_eps, const float* out_proj_b, float ln2_eps,
+                        int mlp_hidden, const float* mlp2_b, const void* prep, size_t prep_bytes, hipStream_t st) {
+  if (!yolosod_swin_x3_ok(C, num_heads, wh, ww, mlp_hidden)) return 0;
+  if ((long)C * H * W >= (1L << 30) || (long)B * nWin >= (1L << 31)) return 0;
+  X3Prep q;
+  if (!x3_carve(const_cast<void*>(prep), prep_bytes, C, mlp_hidden, q)) {
+    set_error("swin_x3: prepared-parameter buffer too small (%zu)", prep_bytes);
+    return -1;
+  }
+  x3::Args a{x, y, B, H, W, nWx, nWin, dw_w, ln1_eps, ln2_eps, q.pin, q.bin_f, q.po, out_proj_b, q.p1, q.b1_f, q.p2,
+             mlp2_b, q.ppw, q.bn_sc, q.bn_sh, 1.0f / sqrtf((float)(C / num_heads))};
   const long nwin = (long)B * nWin;
   if (nwin == 0) return 1;
   if (C == 64)
@@ -1296,6 +1351,49 @@ int yolosod_swin_x3_launch(const float* x, float* y, int B, int C, int H, int W,
     return -1;
   }
   return 1;
+}
+
+// returns 1 if launched, 0 if the shape is not handled, < 0 on error (prep into the workspace, then the kernel)
+int yolosod_swin_x3_launch(const float* x, float* y, int B, int C, int H, int W, int num_heads, int wh, int ww,
+                           int nWx, int nWin,
+                           const float* dw_w, const float* ln1_w, const float* ln1_b, float ln1_eps,
+                           const float* in_proj_w, const float* in_proj_b, const float* out_proj_w,
+                           const float* out_proj_b, const float* ln2_w, const float* ln2_b, float ln2_eps,
+                           const float* mlp1_w, const float* mlp1_b, int mlp_hidden, const float* mlp2_w,
+                           const float* mlp2_b, const float* pw_w, const float* bn_w, const float* bn_b,
+                           const float* bn_mean, const float* bn_var, float bn_eps, void* workspace,
+                           size_t workspace_bytes, hipStream_t st) {
+  if (!yolosod_swin_x3_ok(C, num_heads, wh, ww, mlp_hidden)) return 0;
+  if ((long)C * H * W >= (1L << 30) || (long)B * nWin >= (1L << 31)) return 0;
+  if (yolosod_swin_x3_prepare(C, mlp_hidden, ln1_w, ln1_b, in_proj_w, in_proj_b, out_proj_w, ln2_w, ln2_b, mlp1_w,
+                              mlp1_b, mlp2_w, pw_w, bn_w, bn_b, bn_mean, bn_var, bn_eps, workspace, workspace_bytes,
+                              st) < 0)
+    return -1;
+  return yolosod_swin_x3_run(x, y, B, C, H, W, num_heads, wh, ww, nWx, nWin, dw_w, ln1_eps, out_proj_b, ln2_eps,
+                             mlp_hidden, mlp2_b, workspace, workspace_bytes, st);
+}
+
+// ---- C ABI: the prepared-parameter path (the weight split cached by the caller across calls) -----------------------
+YS_EXPORT size_t yolosod_swin_prep_bytes(int C, int num_heads, int mlp_hidden) {
+  return yolosod_swin_x3_ok(C, num_heads, 7, 7, mlp_hidden) ? yolosod_swin_x3_workspace(C, mlp_hidden) : 0;
+}
+
+YS_EXPORT int yolosod_swin_prepare(int C, int num_heads, int mlp_hidden, const float* ln1_w, const float* ln1_b,
+                                   const float* in_proj_w, const float* in_proj_b, const float* out_proj_w,
+                                   const float* ln2_w, const float* ln2_b, const float* mlp1_w, const float* mlp1_b,
+                                   const float* mlp2_w, const float* pw_w, const float* bn_w, const float* bn_b,
+                                   const float* bn_mean, const float* bn_var, float bn_eps, void* prep,
+                                   size_t prep_bytes, void* stream) {
+  YS_CHECK_ARG(ln1_w && ln1_b && in_proj_w && in_proj_b && out_proj_w && ln2_w && ln2_b && mlp1_w && mlp1_b &&
+                   mlp2_w && pw_w && bn_w && bn_b && bn_mean && bn_var && prep,
+               "swin_prepare: null pointer");
+  YS_CHECK_ARG(yolosod_swin_x3_ok(C, num_heads, 7, 7, mlp_hidden),
+               "swin_prepare: C=%d heads=%d hidden=%d has no prepared-parameter kernel", C, num_heads, mlp_hidden);
+  return yolosod_swin_x3_prepare(C, mlp_hidden, ln1_w, ln1_b, in_proj_w, in_proj_b, out_proj_w, ln2_w, ln2_b, mlp1_w,
+                                 mlp1_b, mlp2_w, pw_w, bn_w, bn_b, bn_mean, bn_var, bn_eps, prep, prep_bytes,
+                                 (hipStream_t)stream) < 0
+             ? -1
+             : 0;
 }
 
 #ifdef YS_DIAG_STAMPS

@@ -181,6 +181,51 @@ Tensor a2_fwd(const Tensor& x, int64_t num_areas, int64_t num_heads, const Tenso
   return y;
 }
 
+// The fp16-split Swin kernels' prepared parameters (weight planes, folds) as a uint8 tensor, made once per parameter
+// version by the caller (nn/modules.SwinBlock caches it) and passed to swin_fwd_prepared.
+Tensor swin_prep(const Tensor& x, int64_t num_heads, const Tensor& ln1_w, const Tensor& ln1_b, const Tensor& in_w,
+                 const Tensor& in_b, const Tensor& out_w, const Tensor& ln2_w, const Tensor& ln2_b, const Tensor& m1_w,
+                 const Tensor& m1_b, const Tensor& m2_w, const Tensor& pw_w, const Tensor& bn_w, const Tensor& bn_b,
+                 const Tensor& bn_mean, const Tensor& bn_var, double bn_eps) {
+  TORCH_CHECK(!act_bf16(x, "swin_prep"), "swin_prep: the prepared path is the fp32 config's");
+  c10::DeviceGuard guard(x.device());
+  const int C = x.size(1), hid = m1_w.size(0);
+  const size_t bytes = yolosod_swin_prep_bytes(C, num_heads, hid);
+  TORCH_CHECK(bytes > 0, "swin_prep: C=", C, " heads=", num_heads, " hidden=", hid, " has no prepared path");
+  Tensor prep = at::empty({(int64_t)bytes}, x.options().dtype(at::kByte));
+  auto st = c10::hip::getCurrentHIPStream(x.get_device());
+  const int rc = yolosod_swin_prepare(
+      C, num_heads, hid, (const float*)par(ln1_w, x, "norm1.weight", C), (const float*)par(ln1_b, x, "norm1.bias", C),
+      (const float*)par(in_w, x, "in_proj_weight", 3LL * C * C), (const float*)par(in_b, x, "in_proj_bias", 3 * C),
+      (const float*)par(out_w, x, "out_proj.weight", (int64_t)C * C), (const float*)par(ln2_w, x, "norm2.weight", C),
+      (const float*)par(ln2_b, x, "norm2.bias", C), (const float*)par(m1_w, x, "mlp.0.weight", (int64_t)hid * C),
+      (const float*)par(m1_b, x, "mlp.0.bias", hid), (const float*)par(m2_w, x, "mlp.2.weight", (int64_t)C * hid),
+      (const float*)par(pw_w, x, "pw.weight", (int64_t)C * C), (const float*)par(bn_w, x, "bn.weight", C),
+      (const float*)par(bn_b, x, "bn.bias", C), (const float*)par(bn_mean, x, "bn.running_mean", C),
+      (const float*)par(bn_var, x, "bn.running_var", C), (float)bn_eps, prep.data_ptr(), bytes, sp(st));
+  check_rc(rc, "swin_prep");
+  return prep;
+}
+
+Tensor swin_fwd_prepared(const Tensor& x, const Tensor& prep, int64_t num_heads, int64_t window, const Tensor& dw_w,
+                         double ln1_eps, const Tensor& out_b, double ln2_eps, int64_t hid, const Tensor& m2_b) {
+  TORCH_CHECK(!act_bf16(x, "swin_fwd_prepared"), "swin_fwd_prepared: fp32 activations only");
+  c10::DeviceGuard guard(x.device());
+  const int B = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const size_t bytes = yolosod_swin_prep_bytes(C, num_heads, hid);
+  TORCH_CHECK(bytes > 0 && (size_t)prep.numel() == bytes && prep.scalar_type() == at::kByte &&
+                  prep.device() == x.device() && prep.is_contiguous(),
+              "swin_fwd_prepared: prep must be the ", bytes, "-byte block of swin_prep on ", x.device());
+  Tensor y = at::empty_like(x);
+  auto st = c10::hip::getCurrentHIPStream(x.get_device());
+  const int rc = yolosod_swin_forward_prepared(
+      (const float*)x.data_ptr(), (float*)y.data_ptr(), B, C, H, W, num_heads, window,
+      (const float*)par(dw_w, x, "dw.weight", 9LL * C), (float)ln1_eps, (const float*)par(out_b, x, "out_proj.bias", C),
+      (float)ln2_eps, hid, (const float*)par(m2_b, x, "mlp.2.bias", C), prep.data_ptr(), bytes, sp(st));
+  check_rc(rc, "swin_fwd_prepared");
+  return y;
+}
+
 Tensor swin_fwd(const Tensor& x, int64_t num_heads, int64_t window, const Tensor& dw_w, const Tensor& ln1_w,
                 const Tensor& ln1_b, double ln1_eps, const Tensor& in_w, const Tensor& in_b, const Tensor& out_w,
                 const Tensor& out_b, const Tensor& ln2_w, const Tensor& ln2_b, double ln2_eps, const Tensor& m1_w,
@@ -342,6 +387,11 @@ TORCH_LIBRARY(yolosod, m) {
         "Tensor in_w, Tensor in_b, Tensor out_w, Tensor out_b, Tensor ln2_w, Tensor ln2_b, float ln2_eps, "
         "Tensor m1_w, Tensor m1_b, Tensor m2_w, Tensor m2_b, Tensor pw_w, Tensor bn_w, Tensor bn_b, Tensor bn_mean, "
         "Tensor bn_var, float bn_eps) -> Tensor");
+  m.def("swin_prep(Tensor x, int num_heads, Tensor ln1_w, Tensor ln1_b, Tensor in_w, Tensor in_b, Tensor out_w, "
+        "Tensor ln2_w, Tensor ln2_b, Tensor m1_w, Tensor m1_b, Tensor m2_w, Tensor pw_w, Tensor bn_w, Tensor bn_b, "
+        "Tensor bn_mean, Tensor bn_var, float bn_eps) -> Tensor");
+  m.def("swin_fwd_prepared(Tensor x, Tensor prep, int num_heads, int window, Tensor dw_w, float ln1_eps, "
+        "Tensor out_b, float ln2_eps, int hid, Tensor m2_b) -> Tensor");
   m.def("detect_head_fwd(Tensor[] box_feats, Tensor[] cls_feats, Tensor[] box_w, Tensor[] box_b, Tensor[] cls_w, "
         "Tensor[] cls_b, float[] strides, int nc, int reg_max) -> Tensor");
   m.def("detect_decode_fwd(Tensor[] maps, float[] strides, int nc, int reg_max) -> Tensor");
@@ -355,6 +405,8 @@ TORCH_LIBRARY_IMPL(yolosod, CUDA, m) {
   m.impl("ca_fwd", ca_fwd);
   m.impl("a2_fwd", a2_fwd);
   m.impl("swin_fwd", swin_fwd);
+  m.impl("swin_prep", swin_prep);
+  m.impl("swin_fwd_prepared", swin_fwd_prepared);
   m.impl("detect_head_fwd", detect_head_fwd);
   m.impl("detect_decode_fwd", detect_decode_fwd);
   m.impl("nms_batched", nms_batched);
@@ -375,6 +427,8 @@ TORCH_LIBRARY_IMPL(yolosod, Meta, m) {
                         const Tensor&, const Tensor&, const Tensor&, const Tensor&, const Tensor&, const Tensor&, double,
                         const Tensor&, const Tensor&, const Tensor&, const Tensor&, const Tensor&, const Tensor&,
                         const Tensor&, const Tensor&, const Tensor&, double) { return mafn_meta(x); });
+  m.impl("swin_fwd_prepared", [](const Tensor& x, const Tensor&, int64_t, int64_t, const Tensor&, double,
+                                 const Tensor&, double, int64_t, const Tensor&) { return mafn_meta(x); });
   m.impl("detect_head_fwd", [](at::TensorList bf, at::TensorList, at::TensorList, at::TensorList, at::TensorList,
                                at::TensorList, at::ArrayRef<double>, int64_t nc, int64_t) {
     int64_t A = 0;

@@ -665,6 +665,28 @@ YS_EXPORT size_t yolosod_swin_workspace_v2(int B, int C, int H, int W, int num_h
   return yolosod_swin_workspace(B, C, H, W, window, mlp_hidden);
 }
 
+int yolosod_swin_x3_run(const float* x, float* y, int B, int C, int H, int W, int num_heads, int wh, int ww, int nWx,
+                        int nWin, const float* dw_w, float ln1_eps, const float* out_proj_b, float ln2_eps,
+                        int mlp_hidden, const float* mlp2_b, const void* prep, size_t prep_bytes, hipStream_t st);
+
+// SwinBlock.forward on a prepared-parameter block (yolosod_swin_prepare): the shapes the fp16-split kernels take
+// (7x7 windows, yolosod_swin_prep_bytes > 0); anything else is an error (use yolosod_swin_forward).
+YS_EXPORT int yolosod_swin_forward_prepared(const float* x, float* y, int B, int C, int H, int W, int num_heads,
+                                            int window, const float* dw_w, float ln1_eps, const float* out_proj_b,
+                                            float ln2_eps, int mlp_hidden, const float* mlp2_b, const void* prep,
+                                            size_t prep_bytes, void* stream) {
+  YS_CHECK_ARG(x && y && dw_w && out_proj_b && mlp2_b && prep, "swin_prepared: null pointer");
+  YS_CHECK_ARG(B >= 0 && C > 0 && H > 0 && W > 0 && window > 0, "swin_prepared: bad shape");
+  if (B == 0) return 0;
+  SwinGeom g = swin_geom(B, H, W, window);
+  const int r = yolosod_swin_x3_run(x, y, B, C, H, W, num_heads, g.wh, g.ww, g.nWx, g.nWin, dw_w, ln1_eps, out_proj_b,
+                                    ln2_eps, mlp_hidden, mlp2_b, prep, prep_bytes, (hipStream_t)stream);
+  if (r < 0) return -1;
+  YS_CHECK_ARG(r == 1, "swin_prepared: shape C=%d heads=%d window %dx%d has no prepared-parameter kernel", C,
+               num_heads, g.wh, g.ww);
+  return 0;
+}
+
 YS_EXPORT int yolosod_swin_forward(const float* x, float* y, int B, int C, int H, int W, int num_heads, int window,
                                    const float* dw_w, const float* ln1_w, const float* ln1_b, float ln1_eps,
                                    const float* in_proj_w, const float* in_proj_b, const float* out_proj_w,

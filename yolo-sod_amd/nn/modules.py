@@ -482,9 +482,16 @@ class SwinBlock(nn.Module):
             self, "p", self.dw.weight, wa.norm1.weight, wa.norm1.bias, at.in_proj_bias, at.out_proj.bias,
             wa.norm2.weight, wa.norm2.bias, wa.mlp[0].bias, wa.mlp[2].bias, self.bn.weight, self.bn.bias,
             self.bn.running_mean, self.bn.running_var)
+        srcs = (wa.norm1.weight, wa.norm1.bias, at.in_proj_weight, at.in_proj_bias, at.out_proj.weight,
+                wa.norm2.weight, wa.norm2.bias, wa.mlp[0].weight, wa.mlp[0].bias, wa.mlp[2].weight, self.pw.weight,
+                self.bn.weight, self.bn.bias, self.bn.running_mean, self.bn.running_var)
+        # the fp16-split kernels' weight split / folds, made once per parameter version (not per call)
+        prep = lambda: _cached(self, "x3prep", srcs, lambda: _hip.swin_prepare(  # noqa: E731
+            x, at.num_heads, n1w, n1b, in_w, in_b, out_w, n2w, n2b, m1_w, m1_b, m2_w, pw_w, bnw, bnb, bnm, bnv,
+            self.bn.eps))
         return _hip.swin_forward(
             x, at.num_heads, wa.window_size, dw, n1w, n1b, wa.norm1.eps, in_w, in_b, out_w, out_b, n2w, n2b,
-            wa.norm2.eps, m1_w, m1_b, m2_w, m2_b, pw_w, bnw, bnb, bnm, bnv, self.bn.eps)
+            wa.norm2.eps, m1_w, m1_b, m2_w, m2_b, pw_w, bnw, bnb, bnm, bnv, self.bn.eps, prep=prep)
 
 
 class Conv1x1BN(nn.Sequential):
