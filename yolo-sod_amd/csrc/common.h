@@ -192,17 +192,15 @@ __device__ __forceinline__ void st4(bf16_t* p, f32x4 v) {
 typedef uint16_t h16_t;  // fp16 bit pattern
 typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
 typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
-// a pair: h = v_cvt_pk_f16_f32 (round to nearest even), then each low term with one v_fma_mix{lo,hi}_f16: fma(-h, 1,
-// v) evaluates v - h exactly in fp32 (h widened from its fp16 half) and rounds it once to fp16 - the same value as
-// fp16(v - h) - writing the low / high half of l. 3 VALU per pair instead of 5 (two v_cvt_f32_f16 widenings, a
-// v_pk_add_f32 and a second v_cvt_pk_f16_f32).
+// a pair: v_cvt_pk_f16_f32, two v_cvt_f32_f16, v_pk_add_f32, v_cvt_pk_f16_f32. (A 3-instruction form with the low
+// terms from v_fma_mix{lo,hi}_f16 in inline asm was tried: the compiler does not model the hazards of an asm
+// statement, and with MFMA results as its inputs the C = 64 Swin kernel computed nondeterministic garbage under some
+// schedules; the VALU it saved was worth ~1 % of that kernel's time.)
 __device__ __forceinline__ void split2(f32x2 v, uint32_t& h, uint32_t& l) {
   const f16x2_t hh = __builtin_convertvector(v, f16x2_t);
+  const f32x2 r = v - __builtin_convertvector(hh, f32x2);
   h = __builtin_bit_cast(uint32_t, hh);
-  uint32_t r;
-  asm("v_fma_mixlo_f16 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(h), "v"(v.x));
-  asm("v_fma_mixhi_f16 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(r) : "v"(h), "v"(v.y));
-  l = r;
+  l = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, f16x2_t));
 }
 __device__ __forceinline__ void split4(f32x4 v, uint2& h, uint2& l) {
   split2(f32x2{v.x, v.y}, h.x, l.x);

@@ -310,6 +310,28 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
   }
   __syncthreads();
   X3_STAMP(1);
+#ifdef YS_OLD_DW
+  for (int item = tid; item < C * 7; item += 256) {
+    const int iy = item / C;
+    const float* hp = halo + (dw_c * 9 + iy) * HPW;
+    float r[3][12];
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+      for (int q4 = 0; q4 < 3; ++q4) {
+        const float4 v = *reinterpret_cast<const float4*>(hp + ky * HPW + 4 * q4);
+        r[ky][4 * q4] = v.x; r[ky][4 * q4 + 1] = v.y; r[ky][4 * q4 + 2] = v.z; r[ky][4 * q4 + 3] = v.w;
+      }
+    const bool rowok = wy * 7 + iy < H;
+#pragma unroll
+    for (int ix = 0; ix < 7; ++ix) {
+      const float v = dwk[0] * r[0][ix] + dwk[1] * r[0][ix + 1] + dwk[2] * r[0][ix + 2] + dwk[3] * r[1][ix] +
+                      dwk[4] * r[1][ix + 1] + dwk[5] * r[1][ix + 2] + dwk[6] * r[2][ix] + dwk[7] * r[2][ix + 1] +
+                      dwk[8] * r[2][ix + 2];
+      T[(iy * 7 + ix) * LT + dw_c] = (rowok && wx * 7 + ix < W) ? v : 0.f;
+    }
+  }
+#else
   {
     // wave w computes output rows 2w and 2w + 1 (wave 3: row 6) of channel dw_c: the four halo rows they need are
     // read once (12 16-byte LDS reads for 14 outputs)
@@ -346,6 +368,7 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
       }
     }
   }
+#endif
   __syncthreads();
   X3_STAMP(2);
 
@@ -408,7 +431,15 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
         akv[1][rb][0] = f32x4{bv, bv, bv, bv};
       }
       gemm_x3<C, 1, PS, PL>(P, f_q, akv[0], lane);
+#ifdef YS_OLD_V
+      {
+        const f32x4 b = *reinterpret_cast<const f32x4*>(par + P_BIN + (2 * C / 16 + wid) * 16 + 4 * g);
+        for (int rb = 0; rb < 4; ++rb) akv[1][rb][0] = b;
+      }
+      gemm_x3<C, 1, PS, PL>(P, f_n, akv[1], lane);
+#else
       gemm_x3<C, 1, PS, PL, true>(P, f_n, akv[1], lane);
+#endif
     }
   }
   WP<C, 1> f_o;
@@ -420,10 +451,23 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
     const int tok = rb * 16 + l15;
     if (tok < NR) store_planes4<PSK, KPL>(Kp, tok, wid * 16 + 4 * g, akv[0][rb][0]);  // K, V, Q stay x64
     uint2 h, l;
+#ifdef YS_OLD_V
+    split4(akv[1][rb][0], h, l);
+    h16_t* vd = Vt + (wid * 16 + 4 * g) * PSV + tok;
+    vd[0] = (h16_t)(h.x & 0xffffu);
+    vd[PSV] = (h16_t)(h.x >> 16);
+    vd[2 * PSV] = (h16_t)(h.y & 0xffffu);
+    vd[3 * PSV] = (h16_t)(h.y >> 16);
+    vd[VPL] = (h16_t)(l.x & 0xffffu);
+    vd[VPL + PSV] = (h16_t)(l.x >> 16);
+    vd[VPL + 2 * PSV] = (h16_t)(l.y & 0xffffu);
+    vd[VPL + 3 * PSV] = (h16_t)(l.y >> 16);
+#else
     split4(akv[1][rb][0], h, l);  // V^T[d = wid*16 + l15][keys rb*16 + 4g .. +3]
     h16_t* vd = Vt + (wid * 16 + l15) * PSV + rb * 16 + 4 * g;
     *reinterpret_cast<uint2*>(vd) = h;
     *reinterpret_cast<uint2*>(vd + VPL) = l;
+#endif
   }
   // this wave's queries as the B operand of S^T = K Q^T, per head: k slot j of lane group g is head dim
   // 4g + j (j < 4) or 16 + 4g + j - 4 (the lane's own two Q column blocks); K is read with the same permutation
