@@ -217,6 +217,12 @@ void yolosod_debug_set_gemm_x2(int on);
  * h[i] = the fp16 pair (fp16(v[2i]), fp16(v[2i+1])), l[i] = (fp16(v[2i] - h.lo), fp16(v[2i+1] - h.hi)), as 2 x 16-bit
  * patterns per uint32 (low half = even element). Device pointers. */
 int yolosod_debug_split_f16(const float* v, uint32_t* h, uint32_t* l, long npair, void* stream);
+/* Split-range guard of the fp32-accurate fp16-split kernels (Swin x3 / wx and their weight preparation, Detect head
+ * x2, the X2 GEMMs): fp16 represents |v| < 65520 only, so every split site records the largest magnitude it split and
+ * a kernel that saw one beyond 65504 (or a NaN) sets the current device's flag word. Returns 1 if set since the last
+ * reset, 0 if not, < 0 on error; synchronises `stream` first; reset != 0 clears it. A caller that sees 1 redoes the
+ * work on the exact-fp32-MFMA kernels (the yolosod_debug_set_*(0) switches; DetectionPredictor does). */
+int yolosod_split_range_flag(int reset, void* stream);
 /* Test hook: the kernel of yolosod_gemm_bf16 / the bf16 operators' K-contiguous GEMMs without a LayerNorm prologue:
  * 0 (default; env YOLOSOD_GEMMB_GLDS) register-staged kernel, 3 / 2 LDS-DMA staged ring of 3 / 2 buffers. */
 void yolosod_debug_set_gemmb_glds(int mode);

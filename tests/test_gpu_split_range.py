@@ -129,3 +129,51 @@ def test_split_is_bitwise_fp16_pair(cuda):
     fin = torch.isfinite(ref_h)
     assert torch.equal(hh.view(torch.int16)[fin], ref_h.view(torch.int16)[fin])
     assert torch.equal(ll.view(torch.int16)[fin], ref_l.view(torch.int16)[fin])
+
+
+@pytest.mark.parametrize("name", ["swin_L28", "swin_L9", "a2_L12"])
+def test_split_range_guard_flags_and_exact_fallback(name, cuda, monkeypatch):
+    """Operands beyond fp16's range set the split-range flag (instead of silent inf / NaN), and the exact-fp32 path
+    the guard falls back to stays accurate; in-range work leaves it clear."""
+    op, args, shape, _ = OPS[name]
+    monkeypatch.setitem(recipes.OPS, name, (op, args, shape))
+    m, _ = build_fixture_module(name)
+    md = m.to(cuda)
+    x = recipes.make_input(name, shape)
+    _hip.split_range_flag(reset=True)
+    with torch.inference_mode():
+        md(x.to(cuda))
+    assert not _hip.split_range_flag(reset=True)
+    big = x * 1e5  # Swin: the residual stream (the pw product's operand) ~1e5; A2: the proj GEMM's input
+    with torch.inference_mode():
+        md(big.to(cuda))
+    assert _hip.split_range_flag(reset=True)
+    ref_m, _ = build_fixture_module(name, OP_CLASSES)
+    with torch.inference_mode():
+        ref = ref_m.double()(big.double())
+        with _hip.exact_fp32_matrix():
+            y = md(big.to(cuda)).cpu().double()
+    assert float((y - ref).abs().max()) <= 1e-4 * float(ref.abs().max())
+    if not name.startswith("swin"):
+        return
+    # weights beyond range (64 W > 65504): flagged by the weight preparation
+    with torch.no_grad():
+        md.window_attn.mlp[2].weight.mul_(2e4)
+    with torch.inference_mode():
+        md(x.to(cuda))
+    assert _hip.split_range_flag(reset=True)
+
+
+def test_split_range_guard_detect_head(cuda):
+    g = torch.Generator().manual_seed(4)
+    strides, nc, B, img = [4.0, 8.0, 16.0, 32.0], 10, 1, 128
+    mk = lambda *s: torch.randn(*s, generator=g).to(cuda)  # noqa: E731
+    fb = [mk(B, 64, int(img // s), int(img // s)) for s in strides]
+    fc = [mk(B, 64, int(img // s), int(img // s)) for s in strides]
+    wb, bb = [mk(64, 64) * 0.1 for _ in strides], [mk(64) for _ in strides]
+    wc, bc = [mk(nc, 64) * 0.1 for _ in strides], [mk(nc) for _ in strides]
+    _hip.split_range_flag(reset=True)
+    _hip.detect_head(fb, fc, wb, bb, wc, bc, strides, nc)
+    assert not _hip.split_range_flag(reset=True)
+    _hip.detect_head([f * 1e5 for f in fb], fc, wb, bb, wc, bc, strides, nc)
+    assert _hip.split_range_flag(reset=True)

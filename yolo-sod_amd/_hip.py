@@ -70,6 +70,7 @@ SIGNATURES = {
     "yolosod_debug_split_f16": (_i, [_vp, _vp, _vp, _l, _vp]),
     "yolosod_debug_set_gemmb_glds": (None, [_i]),
     "yolosod_swin_prep_bytes": (_sz, [_i, _i, _i]),
+    "yolosod_split_range_flag": (_i, [_i, _vp]),
     "yolosod_swin_prepare": (_i, [_i, _i, _i] + [_vp] * 15 + [_f, _vp, _sz, _vp]),
     "yolosod_swin_forward_prepared": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _f, _vp, _f, _i, _vp, _vp, _sz,
                                            _vp]),
@@ -347,6 +348,35 @@ def swin_forward(x, num_heads, window, dw_w, ln1_w, ln1_b, ln1_eps, in_w, in_b, 
     return _launch(key, x.device, ops().swin_fwd, x, int(num_heads), int(window), dw_w, ln1_w, ln1_b, float(ln1_eps),
                    in_w, in_b, out_w, out_b, ln2_w, ln2_b, float(ln2_eps), m1_w, m1_b, m2_w, m2_b, pw_w, bn_w, bn_b,
                    bn_mean, bn_var, float(bn_eps))
+
+
+def split_range_flag(reset: bool = True, device=None) -> bool:
+    """True if a fp16-split kernel on ``device`` (default: current) saw an operand beyond fp16's range since the last
+    reset (the C-ABI's split-range guard); synchronises the device's current stream."""
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    with torch.cuda.device(dev):
+        rc = load_library().yolosod_split_range_flag(int(bool(reset)), _stream(dev))
+    if rc < 0:
+        _check(rc, "split_range_flag")
+    return rc == 1
+
+
+class exact_fp32_matrix:
+    """``with exact_fp32_matrix(): ...`` runs the fp32 model's matrix products on the exact fp32 MFMA kernels
+    (Swin swin_fused / swin_wide, Detect head LDS kernel, A2 fp32 GEMMs) instead of the fp16 two-term splits - the
+    fallback when split_range_flag() reports an operand outside fp16's range."""
+
+    def __enter__(self):
+        lib = load_library()
+        for f in ("yolosod_debug_set_swin_x3", "yolosod_debug_set_head_x2", "yolosod_debug_set_a2_x2"):
+            getattr(lib, f)(0)
+        return self
+
+    def __exit__(self, *exc):
+        lib = load_library()
+        for f in ("yolosod_debug_set_swin_x3", "yolosod_debug_set_head_x2", "yolosod_debug_set_a2_x2"):
+            getattr(lib, f)(1)
+        return False
 
 
 def swin_prep_bytes(C, num_heads, hid) -> int:

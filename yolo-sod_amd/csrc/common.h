@@ -214,6 +214,22 @@ __device__ __forceinline__ void split8(f32x4 a, f32x4 b, f16x8_t& h, f16x8_t& l)
   h = __builtin_bit_cast(f16x8_t, make_uint4(h0.x, h0.y, h1.x, h1.y));
   l = __builtin_bit_cast(f16x8_t, make_uint4(l0.x, l0.y, l1.x, l1.y));
 }
+// Split-range guard (fp16 holds |h| < 65520; beyond it h = inf and the products turn into inf / NaN): every split site
+// folds the magnitudes it splits into a per-thread running max (max3 with |.| modifiers, ~one VALU per pair) and the
+// kernel reports once at its end into a per-device flag word (range_flag_dev(); yolosod_split_range_flag reads it).
+// The flag makes a launch whose operands left the method's range visible, so the caller can redo it on the exact
+// fp32 kernels (DetectionPredictor does) instead of returning silent inf / NaN.
+__device__ __forceinline__ float range_acc(float m, f32x4 v) {
+  return fmaxf(fmaxf(m, fmaxf(fabsf(v.x), fabsf(v.y))), fmaxf(fabsf(v.z), fabsf(v.w)));
+}
+__device__ __forceinline__ float range_acc2(float m, f32x2 v) { return fmaxf(m, fmaxf(fabsf(v.x), fabsf(v.y))); }
+constexpr float SPLIT_RANGE = 65504.0f;  // largest finite fp16
+__device__ __forceinline__ void range_report(unsigned* flag, float m) {
+  if (flag && !(m <= SPLIT_RANGE)) *flag = 1u;  // NaN inputs report too
+}
+// host: the device's flag word (allocated and zeroed on first use, one per device)
+unsigned* range_flag_dev();
+
 // c += A.B for split operands (A = (ah, al), B = (bh, bl)), smallest terms first
 __device__ __forceinline__ f32x4 mfma_f16x3(f16x8_t ah, f16x8_t al, f16x8_t bh, f16x8_t bl, f32x4 c) {
   c = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, c, 0, 0, 0);

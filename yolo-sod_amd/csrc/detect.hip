@@ -96,6 +96,7 @@ struct HeadArgs {
   float stride[4];
   int nl, nc, A;
   float* y;
+  unsigned* range_flag;  // split-range guard of the x2 kernel (common.h range_report)
 };
 
 template <int C2, int C3, int NTS>
@@ -387,6 +388,7 @@ __global__ __launch_bounds__(256, C3 > 64 ? 2 : 3) void detect_head_x2_kernel(He
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int g = lane >> 4, j = lane & 15;
   const int nc = d.nc;
+  float rng = 0.f;  // largest magnitude split (64 W, features): split-range guard
   {
     const float* wb = d.wb[l];
     const float* wc = d.wc[l];
@@ -411,6 +413,7 @@ __global__ __launch_bounds__(256, C3 > 64 ? 2 : 3) void detect_head_x2_kernel(He
     for (int u = 0; u < NB; ++u) {
       uint32_t h, lo;
       split2(vb[u], h, lo);
+      rng = range_acc2(rng, vb[u]);
       reinterpret_cast<uint32_t*>(wl[0])[tid + 256 * u] = h;
       reinterpret_cast<uint32_t*>(wl[1])[tid + 256 * u] = lo;
     }
@@ -418,6 +421,7 @@ __global__ __launch_bounds__(256, C3 > 64 ? 2 : 3) void detect_head_x2_kernel(He
     for (int u = 0; u < NCL; ++u) {
       uint32_t h, lo;
       split2(vc[u], h, lo);
+      rng = range_acc2(rng, vc[u]);
       reinterpret_cast<uint32_t*>(wl[0] + NBW)[tid + 256 * u] = h;
       reinterpret_cast<uint32_t*>(wl[1] + NBW)[tid + 256 * u] = lo;
     }
@@ -478,8 +482,10 @@ __global__ __launch_bounds__(256, C3 > 64 ? 2 : 3) void detect_head_x2_kernel(He
 #pragma unroll
     for (int s = 0; s < C2 / 32; ++s) {
       f16x8_t fh, fl;
-      split8(f32x4{cb[8 * s], cb[8 * s + 1], cb[8 * s + 2], cb[8 * s + 3]},
-             f32x4{cb[8 * s + 4], cb[8 * s + 5], cb[8 * s + 6], cb[8 * s + 7]}, fh, fl);
+      const f32x4 va{cb[8 * s], cb[8 * s + 1], cb[8 * s + 2], cb[8 * s + 3]};
+      const f32x4 vb2{cb[8 * s + 4], cb[8 * s + 5], cb[8 * s + 6], cb[8 * s + 7]};
+      split8(va, vb2, fh, fl);
+      rng = range_acc(range_acc(rng, va), vb2);
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         const int o = (t * 2 + s) * 512;
@@ -490,8 +496,10 @@ __global__ __launch_bounds__(256, C3 > 64 ? 2 : 3) void detect_head_x2_kernel(He
 #pragma unroll
     for (int s = 0; s < C3 / 32; ++s) {
       f16x8_t fh, fl;
-      split8(f32x4{cc[8 * s], cc[8 * s + 1], cc[8 * s + 2], cc[8 * s + 3]},
-             f32x4{cc[8 * s + 4], cc[8 * s + 5], cc[8 * s + 6], cc[8 * s + 7]}, fh, fl);
+      const f32x4 va{cc[8 * s], cc[8 * s + 1], cc[8 * s + 2], cc[8 * s + 3]};
+      const f32x4 vb2{cc[8 * s + 4], cc[8 * s + 5], cc[8 * s + 6], cc[8 * s + 7]};
+      split8(va, vb2, fh, fl);
+      rng = range_acc(range_acc(rng, va), vb2);
       const int o = NBW + s * 512;
       acc[4] = mfma_f16x3(*reinterpret_cast<const f16x8_t*>(wbh + o), *reinterpret_cast<const f16x8_t*>(wbl + o), fh,
                           fl, acc[4]);
@@ -541,6 +549,7 @@ __global__ __launch_bounds__(256, C3 > 64 ? 2 : 3) void detect_head_x2_kernel(He
     if (ts + 2 < NTS && px0 + (ts + 2) * 16 < HW) load_group(ts + 2, xb[0], xc[0]);
     compute_group(ts + 1, xb[1], xc[1]);
   }
+  range_report(d.range_flag, rng);
 }
 
 }  // namespace ys
@@ -593,6 +602,7 @@ static int detect_head_impl(int nl, const void* const* box_feat, const void* con
   HeadArgs d{};
   d.nl = nl;
   d.nc = nc;
+  d.range_flag = range_flag_dev();
   constexpr int NTS = 8;  // 16-pixel groups per wave -> 512 pixels per workgroup
   int off = 0, blk = 0;
   for (int i = 0; i < nl; ++i) {

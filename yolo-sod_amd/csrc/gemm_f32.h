@@ -61,6 +61,7 @@ struct GemmArgs {
   float x2_sa, x2_sb;     // x2: exact power-of-two scales of A / B at the split (a weight operand: 64, keeps its
                           // low terms out of fp16's subnormal range); the accumulators are scaled back before the
                           // epilogue. 0 = 1
+  unsigned* range_flag;   // x2: split-range guard (common.h range_report); set by launch_gemm
 };
 
 // Per-row LayerNorm statistics (mean, 1/sqrt(var + eps)) of a K-contiguous [rows][K] matrix: one wave per row,
@@ -200,6 +201,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
   }
 
   float4 ra[NA], rb[NB], lw, lb;
+  float rng = 0.f;  // X2: largest magnitude split (scaled operands), split-range guard
   const float sa = (X2 && g.x2_sa != 0.f) ? g.x2_sa : 1.f, sb = (X2 && g.x2_sb != 0.f) ? g.x2_sb : 1.f;
   auto load_tiles = [&](int k0) {
 #pragma unroll
@@ -253,6 +255,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
       if (X2) {
         uint2 h, l;
         split4(f32x4{v.x, v.y, v.z, v.w} * sa, h, l);
+        rng = range_acc(rng, f32x4{v.x, v.y, v.z, v.w} * sa);
         h16_t* d = reinterpret_cast<h16_t*>(Ab) + r * (2 * SK) + 16 * (kq >> 3) + (kq & 7);
         *reinterpret_cast<uint2*>(d) = h;
         *reinterpret_cast<uint2*>(d + 8) = l;
@@ -267,6 +270,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
         const int r = idx >> 3, kq = (idx & 7) * 4;
         uint2 h, l;
         split4(f32x4{rb[i].x, rb[i].y, rb[i].z, rb[i].w} * sb, h, l);
+        rng = range_acc(rng, f32x4{rb[i].x, rb[i].y, rb[i].z, rb[i].w} * sb);
         h16_t* d = reinterpret_cast<h16_t*>(Bb) + r * (2 * SK) + 16 * (kq >> 3) + (kq & 7);
         *reinterpret_cast<uint2*>(d) = h;
         *reinterpret_cast<uint2*>(d + 8) = l;
@@ -321,8 +325,10 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
 #pragma unroll
           for (int j = 0; j < NI; ++j) {
             const float* col = Bb + (8 * (2 * lh + s2)) * SBN + wn * NI * 32 + j * 32 + lr;
-            split8(f32x4{col[0], col[SBN], col[2 * SBN], col[3 * SBN]} * sb,
-                   f32x4{col[4 * SBN], col[5 * SBN], col[6 * SBN], col[7 * SBN]} * sb, bh[j], bl[j]);
+            const f32x4 c0 = f32x4{col[0], col[SBN], col[2 * SBN], col[3 * SBN]} * sb;
+            const f32x4 c1 = f32x4{col[4 * SBN], col[5 * SBN], col[6 * SBN], col[7 * SBN]} * sb;
+            split8(c0, c1, bh[j], bl[j]);
+            rng = range_acc(range_acc(rng, c0), c1);
           }
         }
 #pragma unroll
@@ -365,6 +371,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
     __syncthreads();
   }
 
+  if (X2) range_report(g.range_flag, rng);
   if (X2 && sa * sb != 1.f) {
     const float inv = 1.0f / (sa * sb);  // exact: powers of two
 #pragma unroll
@@ -498,6 +505,7 @@ static inline int launch_gemm(const GemmArgs& g0, int batch, bool b_kc, hipStrea
     g.nmajor = 1;
     batch = 1;
   }
+  g.range_flag = x2 ? range_flag_dev() : nullptr;
   // N tiles of 64 when N is not a multiple of 128 (e.g. 3C = 192) or small; 128 otherwise
   const bool narrow = (g.N % 128 != 0) && (g.N <= 256);
 #define YS_GEMM_LAUNCH(WM_, WN_, MI_, NI_)                                                                     \

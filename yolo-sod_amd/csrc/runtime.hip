@@ -13,6 +13,40 @@ void set_error(const char* fmt, ...) {
 }  // namespace ys
 
 YS_EXPORT const char* yolosod_last_error(void) { return ys::g_err; }
+
+namespace ys {
+// the split-range flag word of each device (common.h range_report)
+unsigned* range_flag_dev() {
+  static unsigned* flags[64] = {nullptr};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (!flags[dev]) {
+    unsigned* p = nullptr;
+    if (hipMalloc(&p, sizeof(unsigned)) != hipSuccess) return nullptr;
+    if (hipMemset(p, 0, sizeof(unsigned)) != hipSuccess) return nullptr;
+    flags[dev] = p;
+  }
+  return flags[dev];
+}
+}  // namespace ys
+
+// 1 if a split kernel on the current device has seen an operand outside the fp16 range (|v| > 65504 or NaN) since
+// the last reset, else 0; < 0 on error. Waits for the work queued on `stream` (the flag's producers) first.
+YS_EXPORT int yolosod_split_range_flag(int reset, void* stream) {
+  unsigned* f = ys::range_flag_dev();
+  YS_CHECK_ARG(f, "split_range_flag: no flag word on this device");
+  unsigned v = 0;
+  if (hipMemcpyAsync(&v, f, sizeof(unsigned), hipMemcpyDeviceToHost, (hipStream_t)stream) != hipSuccess ||
+      hipStreamSynchronize((hipStream_t)stream) != hipSuccess) {
+    ys::set_error("split_range_flag: copy failed");
+    return -1;
+  }
+  if (reset && v && hipMemsetAsync(f, 0, sizeof(unsigned), (hipStream_t)stream) != hipSuccess) {
+    ys::set_error("split_range_flag: reset failed");
+    return -1;
+  }
+  return v ? 1 : 0;
+}
 YS_EXPORT int yolosod_abi_version(void) { return 1; }
 
 // Test hook for the fp16 two-term split every fp32-accurate matrix kernel uses (common.h split2): h[i] / l[i] are the

@@ -70,6 +70,7 @@ struct Args {
   const float* bn_scale;
   const float* bn_shift;
   float scale;
+  unsigned* range_flag;  // split-range guard (common.h range_report), may be null
 };
 
 __device__ __forceinline__ f32x4 mfma16(f16x8_t a, f16x8_t b, f32x4 c) {
@@ -238,6 +239,7 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
   constexpr int P_BIN = 0, P_BO = 3 * C, P_B1 = 4 * C, P_B2 = 4 * C + HID, P_SC = 5 * C + HID, P_SH = 6 * C + HID;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  float rng = 0.f;  // largest magnitude this thread splits outside a LayerNorm (split-range guard)
   const int l15 = lane & 15, g = lane >> 4;
   const int H = p.H, W = p.W;
   const int HWi = H * W;  // per-image offsets are 32-bit (the launcher checks C*H*W < 2^30)
@@ -450,6 +452,7 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
   for (int rb = 0; rb < 4; ++rb) {
     const int tok = rb * 16 + l15;
     if (tok < NR) store_planes4<PSK, KPL>(Kp, tok, wid * 16 + 4 * g, akv[0][rb][0]);  // K, V, Q stay x64
+    rng = range_acc(range_acc(rng, akv[0][rb][0]), akv[1][rb][0]);
     uint2 h, l;
 #ifdef YS_OLD_V
     split4(akv[1][rb][0], h, l);
@@ -477,6 +480,7 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
     uint2 h0, l0, h1, l1;
     split4(qa[2 * hh], h0, l0);
     split4(qa[2 * hh + 1], h1, l1);
+    rng = range_acc(range_acc(rng, qa[2 * hh]), qa[2 * hh + 1]);
     qh[hh] = __builtin_bit_cast(f16x8_t, make_uint4(h0.x, h0.y, h1.x, h1.y));
     ql[hh] = __builtin_bit_cast(f16x8_t, make_uint4(l0.x, l0.y, l1.x, l1.y));
   }
@@ -569,7 +573,10 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
   for (int h = 0; h < NH; ++h)
 #pragma unroll
     for (int db = 0; db < HD / 16; ++db)
+    {
       store_planes4<PS, PL>(P, wid * 16 + l15, h * HD + db * 16 + 4 * g, ov[h][db]);
+      rng = range_acc(rng, ov[h][db]);
+    }
   __syncthreads();
   X3_STAMP(9);
 
@@ -638,7 +645,10 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
     __syncthreads();  // every wave has read X (U2, then hidden half 0)
     X3_STAMP(12 + 2 * half);
 #pragma unroll
-    for (int rb = 0; rb < 4; ++rb) store_planes4<PS, PL>(P, rb * 16 + l15, wid * 16 + 4 * g, hid[half][rb]);
+    for (int rb = 0; rb < 4; ++rb) {
+      store_planes4<PS, PL>(P, rb * 16 + l15, wid * 16 + 4 * g, hid[half][rb]);
+      rng = range_acc(rng, hid[half][rb]);
+    }
     __syncthreads();
     X3_STAMP(13 + 2 * half);
 #ifndef YS_ABL_MLPMFMA
@@ -674,7 +684,9 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
     if (tok < NR) v = *reinterpret_cast<const f32x4*>(T + tok * LT + wid * 16 + 4 * g) + acc2[rb][0] * (1.0f / WSC);
     store_planes4<PS, PL>(P, tok, wid * 16 + 4 * g, v);
+    rng = range_acc(rng, v);
   }
+  range_report(p.range_flag, rng);
   __syncthreads();
   X3_STAMP(17);
 
@@ -859,6 +871,7 @@ __global__ __launch_bounds__(NT, 1) void swin_wx_kernel(Args p) {
   const int l15 = lane & 15, g = lane >> 4;
   const int H = p.H, W = p.W;
   const int HWi = H * W;  // per-image offsets are 32-bit (the launcher checks C*H*W < 2^30)
+  float rng = 0.f;        // largest magnitude this thread splits outside a LayerNorm (split-range guard)
 
   const long nwin_total = (long)p.B * p.nWin;
   const long per_xcd = (nwin_total + 7) >> 3;
@@ -1012,6 +1025,7 @@ __global__ __launch_bounds__(NT, 1) void swin_wx_kernel(Args p) {
     for (int rb = 0; rb < 4; ++rb) {
       const int tok = rb * 16 + l15;
       if (tok < NR) store_planes4<PSK, KPL>(Kp, tok, wid * 16 + 4 * g, akv[rb][0]);  // K, V, Q stay x64
+      rng = range_acc(range_acc(rng, akv[rb][0]), akv[rb][1]);
       if (tok < PSV) {
         uint2 h, l;
         split4(akv[rb][1], h, l);
@@ -1034,6 +1048,7 @@ __global__ __launch_bounds__(NT, 1) void swin_wx_kernel(Args p) {
       uint2 h0, l0, h1, l1;
       split4(qa[0][2 * s], h0, l0);
       split4(qa[0][2 * s + 1], h1, l1);
+      rng = range_acc(range_acc(rng, qa[0][2 * s]), qa[0][2 * s + 1]);
       qh[s] = __builtin_bit_cast(f16x8_t, make_uint4(h0.x, h0.y, h1.x, h1.y));
       ql[s] = __builtin_bit_cast(f16x8_t, make_uint4(l0.x, l0.y, l1.x, l1.y));
     }
@@ -1108,7 +1123,10 @@ __global__ __launch_bounds__(NT, 1) void swin_wx_kernel(Args p) {
     WX_STAMP(7 + 6 * hp);
 #pragma unroll
     for (int db = 0; db < HD / 16; ++db)
+    {
       store_planes4<PSO, OPL>(Op, qb * 16 + l15, lh * HD + db * 16 + 4 * g, ov[db]);
+      rng = range_acc(rng, ov[db]);
+    }
     __syncthreads();
     gemm_w<128, 2, 4, 2, PSO, OPL, false>(p.wo, C, C, hp * 128, cbo, Op, 0, acc_o, lane);
     WX_STAMP(8 + 6 * hp);
@@ -1160,6 +1178,7 @@ __global__ __launch_bounds__(NT, 1) void swin_wx_kernel(Args p) {
         const f32x2 lo = gelu2_fast_(f32x2{a[0], a[1]});
         const f32x2 hi = gelu2_fast_(f32x2{a[2], a[3]});
         if (tok < NR) store_planes4<PSU, UPL>(Hp, tok, cbo[j] * 16 + 4 * g, f32x4{lo.x, lo.y, hi.x, hi.y});
+        rng = range_acc(rng, f32x4{lo.x, lo.y, hi.x, hi.y});
       }
     }
     __syncthreads();
@@ -1176,9 +1195,11 @@ __global__ __launch_bounds__(NT, 1) void swin_wx_kernel(Args p) {
       for (int j = 0; j < 2; ++j) {
         const f32x4 v = *reinterpret_cast<const f32x4*>(T + tok * LT + cbo[j] * 16 + 4 * g) + acc_m[rb][j] * (1.0f / WSC);
         store_planes4<PSU, UPL>(UP, tok, cbo[j] * 16 + 4 * g, v);
+        rng = range_acc(rng, v);
       }
     }
   }
+  range_report(p.range_flag, rng);
   // residual x and BN terms of this lane's outputs: in flight during the pw GEMM
   const __amdgpu_buffer_rsrc_t ry = rsrc_of(p.y + (long)img * C * HWi);
   unsigned vtok[4];  // byte offset of (channel wid*16 + 4g, token tb*16 + l15), or out of range
@@ -1236,6 +1257,7 @@ struct PrepArgs {
   int C, HID;
   h16_t *pin, *po, *p1, *p2, *ppw;
   float *bin_f, *b1_f, *bn_sc, *bn_sh;
+  unsigned* range_flag;  // split-range guard: 64 W' must stay finite in fp16
 };
 
 __global__ __launch_bounds__(256) void swin_x3_prep_kernel(PrepArgs a) {
@@ -1272,12 +1294,14 @@ __global__ __launch_bounds__(256) void swin_x3_prep_kernel(PrepArgs a) {
   }
   const float* row = src + (long)n * K;
   float bacc = 0.f;
+  float wmax = 0.f;
   for (int k = lane; k < K; k += 64) {
     const float w = row[k];
     if (bet) bacc = fmaf(w, bet[k], bacc);
     const float v = gam ? w * gam[k] : w;
     const _Float16 h = (_Float16)(v * WSC);
     const _Float16 l = (_Float16)(v * WSC - (float)h);
+    wmax = fmaxf(wmax, fabsf(v * WSC));
     // fragment-major: element (n, k) at ((n/16 * K/32 + k/32) * 64 + (k%32)/8 * 16 + n%16) * 8 + k%8, so the 64
     // lanes' MFMA fragments of one (column block, 32-k step) are 1 KB contiguous
     const long fi = ((long)((n >> 4) * (K >> 5) + (k >> 5)) * 64 + (((k & 31) >> 3) << 4) + (n & 15)) * 8 + (k & 7);
@@ -1288,6 +1312,7 @@ __global__ __launch_bounds__(256) void swin_x3_prep_kernel(PrepArgs a) {
     bacc = wave_sum(bacc);
     if (lane == 0) bdst[n] = bsrc[n] + bacc;
   }
+  range_report(a.range_flag, wmax);
 }
 
 }  // namespace x3
@@ -1359,7 +1384,7 @@ int yolosod_swin_x3_prepare(int C, int mlp_hidden, const float* ln1_w, const flo
   }
   x3::PrepArgs pa{in_proj_w, in_proj_b, ln1_w, ln1_b, out_proj_w, mlp1_w, mlp1_b, ln2_w, ln2_b, mlp2_w, pw_w,
                   bn_w, bn_b, bn_mean, bn_var, bn_eps, C, mlp_hidden, q.pin, q.po, q.p1, q.p2, q.ppw,
-                  q.bin_f, q.b1_f, q.bn_sc, q.bn_sh};
+                  q.bin_f, q.b1_f, q.bn_sc, q.bn_sh, range_flag_dev()};
   const int rows = 3 * C + C + mlp_hidden + C + C + C;
   hipLaunchKernelGGL(x3::swin_x3_prep_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, pa);
   hipError_t e = hipGetLastError();
@@ -1382,7 +1407,7 @@ int yolosod_swin_x3_run(const float* x, float* y, int B, int C, int H, int W, in
     return -1;
   }
   x3::Args a{x, y, B, H, W, nWx, nWin, dw_w, ln1_eps, ln2_eps, q.pin, q.bin_f, q.po, out_proj_b, q.p1, q.b1_f, q.p2,
-             mlp2_b, q.ppw, q.bn_sc, q.bn_sh, 1.0f / sqrtf((float)(C / num_heads))};
+             mlp2_b, q.ppw, q.bn_sc, q.bn_sh, 1.0f / sqrtf((float)(C / num_heads)), range_flag_dev()};
   const long nwin = (long)B * nWin;
   if (nwin == 0) return 1;
   if (C == 64)

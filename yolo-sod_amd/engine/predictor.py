@@ -6,7 +6,9 @@ fused model -> ``postprocess`` = ``non_max_suppression`` + ``scale_boxes`` (same
 
 MI355X additions:
 * :meth:`DetectionPredictor.predict_padded` never syncs the host: NMS returns fixed-shape ``[B, max_det, 6]``
-  rows + counts, so a batch is one stream-ordered sequence of launches (graph-capturable).
+  rows + counts, so a batch is one stream-ordered sequence of launches (graph-capturable). ``__call__`` (which syncs
+  for the per-image lists anyway) also reads the split-range guard and redoes a batch whose operands left the fp16-split
+  kernels' range on the exact fp32 kernels; predict_padded callers read ``_hip.split_range_flag()`` themselves.
 * Data parallel inference: one process per GPU; :func:`shard_bounds` splits images across ranks (no data-path
   collective), :func:`gather_detections` is the single exchange step - an all-gather of the padded detections,
   counts and kept anchor indices (RCCL over xGMI with backend ``nccl``; ``gloo`` on CPU for tests).
@@ -18,6 +20,7 @@ from dataclasses import dataclass
 import torch
 import torch.distributed as dist
 
+from .. import _hip
 from ..utils import ops
 
 
@@ -58,6 +61,11 @@ class DetectionPredictor:
 
     def __call__(self, im: torch.Tensor):
         out, counts, index = self.predict_padded(im)
+        if self.dtype == torch.float32 and _hip.split_range_flag(reset=True, device=self.device):
+            # an operand left the fp16-split kernels' range (|v| > 65504): this batch again on the exact fp32 MFMA
+            with _hip.exact_fp32_matrix():
+                out, counts, index = self.predict_padded(im)
+            _hip.split_range_flag(reset=True, device=self.device)
         n = counts.cpu().tolist()
         shape = tuple(im.shape[2:])
         return [Detections(out[i, : n[i]], index[i, : n[i]], shape) for i in range(len(n))]
