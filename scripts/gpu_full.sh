@@ -14,6 +14,6 @@ grep -E "FAILED|ERROR|passed|failed" "$OUT/pytest.log" | tail -15
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
 timeout -k 10 500 python -u bench.py --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err" || { echo "bench failed"; tail -20 "$OUT/bench.err"; exit 1; }
 cut -c1-300 "$OUT/bench.json"
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-nms-load --no-extra-configs > "$OUT/bench_rocprof.json" 2> "$OUT/bench_rocprof.err" || { echo "rocprof failed"; tail -5 "$OUT/bench_rocprof.err"; exit 1; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-nms-load --no-extra-configs > "$OUT/bench_rocprof.json" 2> "$OUT/bench_rocprof.err" || { echo "rocprof failed"; tail -5 "$OUT/bench_rocprof.err"; exit 1; }
 find "$OUT/prof" -name "*kernel_stats.csv" | head -3
 exit $rc

@@ -271,7 +271,11 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
   float hv[NHS];
   {
     const int hcs = hslot / 9, hpy = hslot - (hslot / 9) * 9;
+#ifdef YS_ABL_HALO  // ablation: every window loads window (1, 1)'s halo (L2-hot)
+    const int hh = 7 - 1 + hpy, wc = 7 - 1 + hl_px;
+#else
     const int hh = wy * 7 - 1 + hpy, wc = wx * 7 - 1 + hl_px;
+#endif
     const bool ok = hl_r < 7 && hslot < 27 && (unsigned)hh < (unsigned)H && (unsigned)wc < (unsigned)W;
     const unsigned voff = ok ? (unsigned)((hcs * HWi + hh * W + wc) * 4) : OOB;
     const unsigned vlast = (3 * (NHS - 1) + hcs < C) ? voff : OOB;
