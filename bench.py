@@ -28,6 +28,11 @@ import torch.distributed as dist
 
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
+# MIOpen solver choices for the backbone / neck convs: a user find-db recorded on MI355X with MIOPEN_FIND_MODE=NORMAL
+# (every applicable solver timed; scripts/miopen_db.sh), so every run takes the same solvers instead of whatever the
+# first-call search of its box measured (round 3: one fresh box chose Winograd f3x2 over the implicit GEMM for the
+# stride-2 convs, 18.0 vs 16.4 ms per step). Set MIOPEN_USER_DB_PATH to override.
+os.environ.setdefault("MIOPEN_USER_DB_PATH", str(ROOT / "yolo-sod_amd" / "miopen_db"))
 import yolosod_import  # noqa: E402,F401
 
 from yolosod_amd import _hip, perf  # noqa: E402

@@ -365,9 +365,9 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
 #ifdef YS_ABL_DW
           const float v = dwk[4] * r[d + 1][ix + 1];
 #else
-          const float v = dwk[0] * r[d][ix] + dwk[1] * r[d][ix + 1] + dwk[2] * r[d][ix + 2] + dwk[3] * r[d + 1][ix] +
-                          dwk[4] * r[d + 1][ix + 1] + dwk[5] * r[d + 1][ix + 2] + dwk[6] * r[d + 2][ix] +
-                          dwk[7] * r[d + 2][ix + 1] + dwk[8] * r[d + 2][ix + 2];
+          float v = dwk[0] * r[d][ix];  // one FMA per tap (a plain sum of products vectorises into pk_mul + add)
+#pragma unroll
+          for (int t = 1; t < 9; ++t) v = fmaf(dwk[t], r[d + t / 3][ix + t % 3], v);
 #endif
           T[(iy * 7 + ix) * LT + dw_c] = (rowok && wx * 7 + ix < W) ? v : 0.f;
         }
