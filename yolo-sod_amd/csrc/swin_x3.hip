@@ -207,7 +207,8 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
   constexpr int HID = 2 * C;
   constexpr int LT = C + 4;      // T row stride (floats)
 #ifndef YS_X3_PS_PAD  // plane row padding (fp16 elements); diagnostic builds vary it
-#define YS_X3_PS_PAD 8
+#define YS_X3_PS_PAD 16  // PS = 80 = ten 16-byte quads: the ds_read_b128 lane groups of the GEMM operand
+                         // reads hit 16 distinct quads (PS = 72, nine quads: 28 of 64 lanes in 2-way conflicts)
 #endif
   constexpr int PS = C + YS_X3_PS_PAD;  // plane row stride (fp16)
   constexpr int PL = 64 * PS;    // plane stride
