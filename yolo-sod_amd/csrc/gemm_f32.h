@@ -135,10 +135,15 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
   constexpr int BK = 32;
   constexpr int SK = BK + 4;                     // [row][k] images
   constexpr int SBN = BN + 4;                    // [k][n] image (N-contiguous B)
-  constexpr int A_ELEMS = BM * SK;
-  constexpr int B_ELEMS = B_KC ? BN * SK : BK * SBN;
   constexpr int NA = BM * BK / 4 / 256;          // float4 per thread per A tile
   constexpr int NB = BN * BK / 4 / 256;
+  // X2 with an N-contiguous B whose tile is one 4x4 (k, n) block per thread: the block is loaded as four float4 rows,
+  // transposed in registers and split once into the same [n][k] hi / lo image as a K-contiguous B, so the MFMA loop
+  // reads whole 16-byte fragments (the [k][n] fp32 image took 8 strided reads and a split per fragment and wave)
+  constexpr bool BT = X2 && !B_KC && NB == 4 && BN / 4 * (BK / 4) == 256;
+  constexpr bool B_IMG = B_KC || BT;             // B staged as a [n][k] image
+  constexpr int A_ELEMS = BM * SK;
+  constexpr int B_ELEMS = B_IMG ? BN * SK : BK * SBN;
   constexpr int SC = BN + 4;                     // epilogue staging row stride
   constexpr int MAIN_ELEMS = 2 * A_ELEMS + 2 * B_ELEMS;
   constexpr int SMEM = (MAIN_ELEMS > BM * SC ? MAIN_ELEMS : BM * SC) + (A_LN ? 2 * BM : 0);
@@ -181,7 +186,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
   if (!B_KC) {
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
-      const int n = n0 + ((tid + 256 * i) % (BN / 4)) * 4;
+      const int n = n0 + ((BT ? tid : tid + 256 * i) % (BN / 4)) * 4;
       if (g.nimg > 0) {
         const int img = n / g.nimg;
         bcol[i] = (long)img * g.b_bs + (n - img * g.nimg);
@@ -203,29 +208,60 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
   float4 ra[NA], rb[NB], lw, lb;
   float rng = 0.f;  // X2: largest magnitude split (scaled operands), split-range guard
   const float sa = (X2 && g.x2_sa != 0.f) ? g.x2_sa : 1.f, sb = (X2 && g.x2_sb != 0.f) ? g.x2_sb : 1.f;
-  auto load_tiles = [&](int k0) {
+  // per-thread operand pointers at k = 0 (a k block adds k0 or k0 * ldb), and whether the whole tile is in range
+  // (block-uniform: the loads then need no per-lane predicates)
+  const float* pa[NA];
 #pragma unroll
-    for (int i = 0; i < NA; ++i) {
-      const int idx = tid + 256 * i;
-      const int r = idx >> 3, kq = (idx & 7) * 4;
-      const int m = m0 + r;
-      ra[i] = (m < M) ? *reinterpret_cast<const float4*>(A + (long)m * g.lda + k0 + kq) : make_float4(0, 0, 0, 0);
+  for (int i = 0; i < NA; ++i) {
+    const int idx = tid + 256 * i;
+    const int m = m0 + (idx >> 3);
+    pa[i] = A + (long)(m < M ? m : M - 1) * g.lda + (idx & 7) * 4;
+  }
+  const float* pb[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int idx = tid + 256 * i;
+    if (B_KC) {
+      const int n = n0 + (idx >> 3);
+      pb[i] = B + (long)(n < N ? n : N - 1) * g.ldb + (idx & 7) * 4;
+    } else {
+      const int kl = BT ? 4 * (tid / (BN / 4)) + i : idx / (BN / 4);
+      pb[i] = B + (long)kl * g.ldb + bcol[i];
+    }
+  }
+  const bool full_a = m0 + BM <= M;
+  const bool full_b = n0 + BN <= N && (B_KC || vec_b);
+  auto load_tiles = [&](int k0) {
+    if (full_a) {  // scalar branch: the tile's rows are all in range
+#pragma unroll
+      for (int i = 0; i < NA; ++i) ra[i] = *reinterpret_cast<const float4*>(pa[i] + k0);
+    } else {
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        const int m = m0 + ((tid + 256 * i) >> 3);
+        ra[i] = (m < M) ? *reinterpret_cast<const float4*>(pa[i] + k0) : make_float4(0, 0, 0, 0);
+      }
     }
     if (A_LN) {  // every A float4 of this thread sits at the same k offset (256 % 8 == 0)
       lw = *reinterpret_cast<const float4*>(g.ln_w + k0 + (tid & 7) * 4);
       lb = *reinterpret_cast<const float4*>(g.ln_b + k0 + (tid & 7) * 4);
     }
+    if (full_b) {
+#pragma unroll
+      for (int i = 0; i < NB; ++i)
+        rb[i] = *reinterpret_cast<const float4*>(pb[i] + (B_KC ? (long)k0 : (long)k0 * g.ldb));
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
       const int idx = tid + 256 * i;
       if (B_KC) {
-        const int r = idx >> 3, kq = (idx & 7) * 4;
-        const int n = n0 + r;
-        rb[i] = (n < N) ? *reinterpret_cast<const float4*>(B + (long)n * g.ldb + k0 + kq) : make_float4(0, 0, 0, 0);
+        const int n = n0 + (idx >> 3);
+        rb[i] = (n < N) ? *reinterpret_cast<const float4*>(pb[i] + k0) : make_float4(0, 0, 0, 0);
       } else {
-        const int kl = idx / (BN / 4), nq = (idx % (BN / 4)) * 4;
-        const int n = n0 + nq;
-        const float* src = B + (long)(k0 + kl) * g.ldb + bcol[i];
+        // BT: thread t loads rows 4 (t / (BN/4)) + i of its column quad 4 (t % (BN/4))
+        const int n = n0 + (BT ? tid : idx) % (BN / 4) * 4;
+        const float* src = pb[i] + (long)k0 * g.ldb;
         if (n + 3 < N && vec_b) {
           rb[i] = *reinterpret_cast<const float4*>(src);
         } else {
@@ -266,7 +302,23 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
       const int idx = tid + 256 * i;
-      if (B_KC && X2) {
+      if (BT) {
+        if (i == 0) {  // the whole 4x4 block: column quad 4 (tid % (BN/4)), k rows kq .. kq + 3
+          const int nq = (tid % (BN / 4)) * 4, kq = 4 * (tid / (BN / 4));
+          const f32x4 r4[4] = {f32x4{rb[0].x, rb[0].y, rb[0].z, rb[0].w}, f32x4{rb[1].x, rb[1].y, rb[1].z, rb[1].w},
+                               f32x4{rb[2].x, rb[2].y, rb[2].z, rb[2].w}, f32x4{rb[3].x, rb[3].y, rb[3].z, rb[3].w}};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const f32x4 col = f32x4{r4[0][j], r4[1][j], r4[2][j], r4[3][j]} * sb;
+            uint2 h, l;
+            split4(col, h, l);
+            rng = range_acc(rng, col);
+            h16_t* d = reinterpret_cast<h16_t*>(Bb) + (nq + j) * (2 * SK) + 16 * (kq >> 3) + (kq & 7);
+            *reinterpret_cast<uint2*>(d) = h;
+            *reinterpret_cast<uint2*>(d + 8) = l;
+          }
+        }
+      } else if (B_KC && X2) {
         const int r = idx >> 3, kq = (idx & 7) * 4;
         uint2 h, l;
         split4(f32x4{rb[i].x, rb[i].y, rb[i].z, rb[i].w} * sb, h, l);
@@ -292,7 +344,11 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
+#ifdef YS_GEMM_HALFK  // diagnostic builds only: half the k blocks (timing of the main loop vs the rest; wrong results)
+  const int nk = K / BK / 2;
+#else
   const int nk = K / BK;
+#endif
   const int lr = lane & 31, lh = lane >> 5;
   load_tiles(0);
   if (A_LN) __syncthreads();  // s_mean / s_rstd
@@ -314,7 +370,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
           ah[i] = *reinterpret_cast<const f16x8_t*>(Ah + i * 32 * (2 * SK) + ko);
           al[i] = *reinterpret_cast<const f16x8_t*>(Ah + i * 32 * (2 * SK) + ko + 8);
         }
-        if constexpr (B_KC) {
+        if constexpr (B_IMG) {
           const h16_t* Bh = reinterpret_cast<const h16_t*>(Bb) + (wn * NI * 32 + lr) * (2 * SK);
 #pragma unroll
           for (int j = 0; j < NI; ++j) {
