@@ -1,19 +1,24 @@
 #!/bin/bash
-# rocprofv3 kernel summary of scripts/bench_ops.py cases: bash scripts/prof_ops.sh TAG [--bf16] case...
+# per-kernel times (rocprofv3 kernel trace) of bench_ops cases: bash scripts/prof_ops.sh TAG [--bf16] case...
 set -o pipefail
 TAG=$1; shift
-OUT=gpurun_out/$TAG
-mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/prof" -o run -- python3 -u scripts/bench_ops.py "$@" \
-  > "$OUT/ops.txt" 2> "$OUT/ops.err" || { echo "rocprof failed"; tail -20 "$OUT/ops.err"; exit 1; }
-cat "$OUT/ops.txt"
-f=$(find "$OUT/prof" -name '*kernel_stats.csv' | head -1)
-cp "$f" "$OUT/kernel_stats.csv"
-python3 - "$OUT/kernel_stats.csv" <<'PY'
-import csv, sys
-rows = list(csv.DictReader(open(sys.argv[1])))
-rows.sort(key=lambda r: -float(r["TotalDurationNs"]))
-for r in rows[:25]:
-    print(f'{float(r["TotalDurationNs"])/1e6:9.3f} ms {int(r["Calls"]):5d} x {float(r["AverageNs"])/1e3:9.1f} us  {r["Name"][:100]}')
+OUT=gpurun_out/$TAG; mkdir -p $OUT
+timeout -k 10 180 rocprofv3 --kernel-trace --stats -f csv -d $OUT/p -o run -- python3 -u scripts/bench_ops.py "$@" > $OUT/out.txt 2>&1 || exit 1
+grep " ms " $OUT/out.txt
+python3 - $OUT/p <<'PY'
+import csv, sys, pathlib
+f = next(pathlib.Path(sys.argv[1]).rglob("*kernel_stats.csv"))
+for r in csv.DictReader(open(f)):
+    if "ys::" in r["Name"]:
+        print(f'  {int(r["Calls"]):4d} x {float(r["AverageNs"])/1e3:8.1f} us {r["Name"][:110]}')
+PY
+python3 - $OUT/p <<'PY'
+import csv, sys, pathlib
+f = next(pathlib.Path(sys.argv[1]).rglob("*kernel_trace.csv"))
+rows = sorted(csv.DictReader(open(f)), key=lambda r: int(r["Start_Timestamp"]))
+rows = [r for r in rows if "ys::" in r["Kernel_Name"]]
+print("last launch sequence:")
+for r in rows[-12:]:
+    print(f'  {(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3:8.1f} us grid {r["Grid_Size_X"]:>8s} lds {r["LDS_Block_Size"]:>6s} vgpr {r["VGPR_Count"]:>4s} {r["Kernel_Name"][:100]}')
 PY

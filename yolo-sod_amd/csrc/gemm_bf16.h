@@ -38,6 +38,7 @@ struct EpiB {
   int swin;
   int sw_H, sw_W, sw_Hp, sw_Wp;
   int vec;             // set by launch_gemm_bf16: 4-wide epilogue legal (alignment / strides)
+  int pair;            // set by launch_gemm_bf16: Swin output as token pairs (4-byte stores; W, Wp even)
 };
 
 struct GemmB {
@@ -98,6 +99,67 @@ static inline int launch_row_stats_bf16(const bf16_t* x, int ld, long rows, int 
   else if (K <= 512) hipLaunchKernelGGL((row_stats_bf16_kernel<2>), grid, dim3(256), 0, st, x, ld, rows, K, eps, stats);
   else hipLaunchKernelGGL((row_stats_bf16_kernel<4>), grid, dim3(256), 0, st, x, ld, rows, K, eps, stats);
   YS_CHECK_LAUNCH("row_stats_bf16");
+  return 0;
+}
+
+// LayerNorm of K-contiguous bf16 rows, written back as bf16 rows for a GEMM without an A prologue: the statistics
+// exactly as row_stats_bf16_kernel, then bf16(fma((x - mean) * rstd, w, b)) - the expression the LN prologue of
+// gemm_bf16_kernel evaluates. Applying it once per row instead of in every N tile's staging (QKV: 12 tiles of 128 at
+// C = 512) took the VALU of the LN off those GEMMs' main loops.
+template <int VPL>
+__global__ __launch_bounds__(256) void ln_rows_bf16_kernel(const bf16_t* __restrict__ x, int ld, long rows, int K,
+                                                           float eps, const float* __restrict__ w,
+                                                           const float* __restrict__ b, bf16_t* __restrict__ out,
+                                                           int ldo) {
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const bf16_t* xr = x + row * ld;
+  const int K4 = K >> 2;
+  f32x4 v[VPL];
+  float s = 0.f;
+#pragma unroll
+  for (int u = 0; u < VPL; ++u) {
+    const int c = lane + 64 * u;
+    v[u] = (c < K4) ? ld4(xr + 4 * c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    s += (v[u].x + v[u].y) + (v[u].z + v[u].w);
+  }
+  const float mean = wave_sum(s) / (float)K;
+  float q = 0.f;
+#pragma unroll
+  for (int u = 0; u < VPL; ++u) {
+    if (lane + 64 * u < K4) {
+      const f32x4 d = v[u] - mean;
+      q += (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
+    }
+  }
+  const float var = wave_sum(q) / (float)K;
+  const float rs = 1.0f / sqrtf(var + eps);
+#pragma unroll
+  for (int u = 0; u < VPL; ++u) {
+    const int c = lane + 64 * u;
+    if (c < K4) {
+      const f32x4 lw = *reinterpret_cast<const f32x4*>(w + 4 * c), lb = *reinterpret_cast<const f32x4*>(b + 4 * c);
+      f32x4 o;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[i] = fmaf((v[u][i] - mean) * rs, lw[i], lb[i]);
+      st4(out + row * ldo + 4 * c, o);
+    }
+  }
+}
+
+static inline int launch_ln_rows_bf16(const bf16_t* x, int ld, long rows, int K, float eps, const float* w,
+                                      const float* b, bf16_t* out, int ldo, hipStream_t st) {
+  YS_CHECK_ARG(K % 4 == 0 && K <= 1024 && ld % 4 == 0 && ldo % 4 == 0, "ln_rows_bf16: K=%d ld=%d unsupported", K, ld);
+  YS_CHECK_ARG(((uintptr_t)w | (uintptr_t)b) % 16 == 0, "ln_rows_bf16: LN params must be 16-byte aligned");
+  if (rows == 0) return 0;
+  const dim3 grid((unsigned)((rows + 3) / 4));
+#define YS_LNR(V_) hipLaunchKernelGGL((ln_rows_bf16_kernel<V_>), grid, dim3(256), 0, st, x, ld, rows, K, eps, w, b, out, ldo)
+  if (K <= 256) YS_LNR(1);
+  else if (K <= 512) YS_LNR(2);
+  else YS_LNR(4);
+#undef YS_LNR
+  YS_CHECK_LAUNCH("ln_rows_bf16");
   return 0;
 }
 
@@ -206,7 +268,7 @@ __global__ __launch_bounds__(256, A_LN ? 2 : 3) void gemm_bf16_kernel(GemmB g) {
         const float* lw = g.ln_w + cur_k0 + kc;
         const float* lb = g.ln_b + cur_k0 + kc;
 #pragma unroll
-        for (int q = 0; q < 8; ++q) f[q] = (f[q] - mu) * rs * lw[q] + lb[q];
+        for (int q = 0; q < 8; ++q) f[q] = fmaf((f[q] - mu) * rs, lw[q], lb[q]);
         v = pack8(f);
       }
       *reinterpret_cast<uint4*>(&Ab[r * SK + kc]) = v;
@@ -349,6 +411,45 @@ __global__ __launch_bounds__(256, A_LN ? 2 : 3) void gemm_bf16_kernel(GemmB g) {
           v += f32x4{__uint_as_float(rv[it].x << 16), __uint_as_float(rv[it].x & 0xffff0000u),
                      __uint_as_float(rv[it].y << 16), __uint_as_float(rv[it].y & 0xffff0000u)};
         st4(outb + (long)m * e.ldc + n, v);
+      }
+    } else if (BN == 128 && e.pair) {
+      // Swin output as token pairs: thread (rsub, pc) owns tokens n0 + 2 pc, +1 (same image row: W and Wp are even,
+      // so a pair is cropped whole or not at all) for rows rsub + 4 it - one 4-byte residual load and one 4-byte
+      // store per pair instead of two 2-byte accesses per element
+      static_assert(HB % 4 == 0, "pair epilogue: 4 rows per pass");
+      const int pc = tid & 63, rsub = tid >> 6;  // BN == 128: 64 pairs per row
+      const long tok = (long)n0 + 2 * pc;
+      const long per_img = (long)e.sw_Hp * e.sw_Wp;
+      const int img = (int)(tok / per_img);
+      const int rr = (int)(tok - img * per_img);
+      const int h = rr / e.sw_Wp, w = rr - (rr / e.sw_Wp) * e.sw_Wp;
+      if (tok < N && h < e.sw_H && w < e.sw_W) {
+        const long HWo = (long)e.sw_H * e.sw_W;
+        const long o0p = (long)img * M * HWo + (long)h * e.sw_W + w;
+        constexpr int PIT = HB / 4;
+        uint32_t rp[PIT];
+#pragma unroll
+        for (int it = 0; it < PIT; ++it) {
+          const int m = mh + rsub + 4 * it;
+          rp[it] = (e.res && m < M) ? *reinterpret_cast<const uint32_t*>(e.res + o0p + (long)m * HWo) : 0u;
+        }
+#pragma unroll
+        for (int it = 0; it < PIT; ++it) {
+          const int row = rsub + 4 * it;
+          const int m = mh + row;
+          if (m >= M) continue;
+          const float2 c2 = *reinterpret_cast<const float2*>(&Cs[row * SC + 2 * pc]);
+          float v0 = c2.x, v1 = c2.y;
+          if (e.bias_mode == 1) { v0 += e.bias[m]; v1 += e.bias[m]; }
+          if (e.bn_mode == 1) { v0 = v0 * e.scale[m] + e.shift[m]; v1 = v1 * e.scale[m] + e.shift[m]; }
+          v0 = act_b(v0, e.act);
+          v1 = act_b(v1, e.act);
+          if (e.res) {
+            v0 += __uint_as_float(rp[it] << 16);
+            v1 += __uint_as_float(rp[it] & 0xffff0000u);
+          }
+          *reinterpret_cast<uint32_t*>(e.out + o0p + (long)m * HWo) = pack_bf16x2(v0, v1);
+        }
       }
     } else if (col_ok) {
       const float bn_ = e.bias_mode == 2 ? e.bias[ncol] : 0.f;
@@ -547,6 +648,8 @@ static inline int launch_gemm_bf16(const GemmB& g0, int batch, bool b_kc, hipStr
                "gemm_bf16: LN params must come with row statistics");
   if (g.M == 0 || g.N == 0 || batch == 0) return 0;
   const EpiB& e = g.epi;
+  g.epi.pair = e.swin && e.sw_W % 2 == 0 && e.sw_Wp % 2 == 0 && e.bias_mode != 2 && e.bn_mode != 2 && al_b(e.out, 4) &&
+               (!e.res || al_b(e.res, 4));
   g.epi.vec = !e.swin && g.N % 4 == 0 && e.ldc % 4 == 0 && e.out_bs % 4 == 0 && al_b(e.out, 8) &&
               (!e.res || (e.ldr % 4 == 0 && e.res_bs % 4 == 0 && al_b(e.res, 8))) &&
               (e.bias_mode != 2 || al_b(e.bias, 16)) && (e.bn_mode != 2 || (al_b(e.scale, 16) && al_b(e.shift, 16)));

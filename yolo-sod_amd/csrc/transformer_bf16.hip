@@ -465,11 +465,10 @@ YS_EXPORT int yolosod_swin_forward_bf16(const bf16_t* x, bf16_t* y, int B, int C
   hipLaunchKernelGGL(swin_tokens_bf16_kernel, dim3((unsigned)(B * g.Hp), (unsigned)((C + 63) / 64)), dim3(256),
                      tok_lds, st, x, dw_w, T, C, H, W, g.Hp, g.Wp);
   YS_CHECK_LAUNCH("swin_tokens_bf16");
-  // QKV = LN1(T) Win^T + b_in
-  if ((rc = launch_row_stats_bf16(T, C, g.ntok, C, ln1_eps, lns, st))) return rc;
+  // QKV = LN1(T) Win^T + b_in (LN1(T) -> U once, U is free until the attention writes it)
+  if ((rc = launch_ln_rows_bf16(T, C, g.ntok, C, ln1_eps, ln1_w, ln1_b, U, C, st))) return rc;
   GemmB ga{};
-  ga.A = T; ga.lda = C; ga.B = in_proj_w; ga.ldb = C; ga.M = (int)g.ntok; ga.N = 3 * C; ga.K = C;
-  ga.ln_w = ln1_w; ga.ln_b = ln1_b; ga.ln_stats = lns;
+  ga.A = U; ga.lda = C; ga.B = in_proj_w; ga.ldb = C; ga.M = (int)g.ntok; ga.N = 3 * C; ga.K = C;
   ga.epi = epib_plain(Q, 0, 3 * C);
   ga.epi.bias = in_proj_b; ga.epi.bias_mode = 2;
   if ((rc = launch_gemm_bf16(ga, 1, true, st))) return rc;
@@ -482,11 +481,10 @@ YS_EXPORT int yolosod_swin_forward_bf16(const bf16_t* x, bf16_t* y, int B, int C
   ga.epi = epib_plain(T, 0, C);
   ga.epi.bias = out_proj_b; ga.epi.bias_mode = 2; ga.epi.res = T; ga.epi.ldr = C;
   if ((rc = launch_gemm_bf16(ga, 1, true, st))) return rc;
-  // Hd = GELU(LN2(T) W1^T + b1)
-  if ((rc = launch_row_stats_bf16(T, C, g.ntok, C, ln2_eps, lns, st))) return rc;
+  // Hd = GELU(LN2(T) W1^T + b1) (LN2(T) -> U: the out-projection has read it)
+  if ((rc = launch_ln_rows_bf16(T, C, g.ntok, C, ln2_eps, ln2_w, ln2_b, U, C, st))) return rc;
   ga = GemmB{};
-  ga.A = T; ga.lda = C; ga.B = mlp1_w; ga.ldb = C; ga.M = (int)g.ntok; ga.N = mlp_hidden; ga.K = C;
-  ga.ln_w = ln2_w; ga.ln_b = ln2_b; ga.ln_stats = lns;
+  ga.A = U; ga.lda = C; ga.B = mlp1_w; ga.ldb = C; ga.M = (int)g.ntok; ga.N = mlp_hidden; ga.K = C;
   ga.epi = epib_plain(Q, 0, mlp_hidden);
   ga.epi.bias = mlp1_b; ga.epi.bias_mode = 2; ga.epi.act = 2;
   if ((rc = launch_gemm_bf16(ga, 1, true, st))) return rc;
@@ -558,10 +556,10 @@ YS_EXPORT int yolosod_a2_forward_bf16(const bf16_t* x, bf16_t* y, int B, int C, 
   hipLaunchKernelGGL(a2_pool_tokens_bf16_kernel, dim3(B * A, (C + 63) / 64), dim3(256),
                      (size_t)64 * (W + 1) * sizeof(float), st, XP, S, C, H, W, A);
   YS_CHECK_LAUNCH("a2_pool_bf16");
-  if ((rc = launch_row_stats_bf16(S, C, ntok, C, ln_eps, lns, st))) return rc;
+  // LN(S) -> U once (U is free until the attention writes it), then the QKV GEMM without an A prologue
+  if ((rc = launch_ln_rows_bf16(S, C, ntok, C, ln_eps, ln_w, ln_b, U, C, st))) return rc;
   ga = GemmB{};
-  ga.A = S; ga.lda = C; ga.B = in_proj_w; ga.ldb = C; ga.M = (int)ntok; ga.N = 3 * C; ga.K = C;
-  ga.ln_w = ln_w; ga.ln_b = ln_b; ga.ln_stats = lns;
+  ga.A = U; ga.lda = C; ga.B = in_proj_w; ga.ldb = C; ga.M = (int)ntok; ga.N = 3 * C; ga.K = C;
   ga.epi = epib_plain(Q, 0, 3 * C);
   ga.epi.bias = in_proj_b; ga.epi.bias_mode = 2;
   if ((rc = launch_gemm_bf16(ga, 1, true, st))) return rc;
