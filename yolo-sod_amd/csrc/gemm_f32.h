@@ -109,6 +109,62 @@ static inline int launch_row_stats(const float* x, int ld, long rows, int K, flo
   return 0;
 }
 
+// LayerNorm of K-contiguous fp32 rows written out as rows (the A operand of a GEMM without an LN prologue): the
+// statistics exactly as row_stats_kernel, then fma((x - mean) * rstd, w, b). For an A operand that many N tiles stage
+// (A2's QKV GEMM: 12 tiles of 128 at C = 512) this normalises each element once instead of once per tile.
+template <int VPL>
+__global__ __launch_bounds__(256) void ln_rows_kernel(const float* __restrict__ x, int ld, long rows, int K, float eps,
+                                                      const float* __restrict__ w, const float* __restrict__ b,
+                                                      float* __restrict__ out, int ldo) {
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const float4* xr = reinterpret_cast<const float4*>(x + row * ld);
+  const int K4 = K >> 2;
+  float4 v[VPL];
+  float s = 0.f;
+#pragma unroll
+  for (int u = 0; u < VPL; ++u) {
+    const int c = lane + 64 * u;
+    v[u] = (c < K4) ? xr[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+    s += (v[u].x + v[u].y) + (v[u].z + v[u].w);
+  }
+  const float mean = wave_sum(s) / (float)K;
+  float q = 0.f;
+#pragma unroll
+  for (int u = 0; u < VPL; ++u) {
+    if (lane + 64 * u < K4) {
+      const float a = v[u].x - mean, bb = v[u].y - mean, c = v[u].z - mean, d = v[u].w - mean;
+      q += (a * a + bb * bb) + (c * c + d * d);
+    }
+  }
+  const float var = wave_sum(q) / (float)K;
+  const float rs = 1.0f / sqrtf(var + eps);
+#pragma unroll
+  for (int u = 0; u < VPL; ++u) {
+    const int c = lane + 64 * u;
+    if (c < K4) {
+      const float4 lw = reinterpret_cast<const float4*>(w)[c], lb = reinterpret_cast<const float4*>(b)[c];
+      reinterpret_cast<float4*>(out + row * ldo)[c] =
+          make_float4(fmaf((v[u].x - mean) * rs, lw.x, lb.x), fmaf((v[u].y - mean) * rs, lw.y, lb.y),
+                      fmaf((v[u].z - mean) * rs, lw.z, lb.z), fmaf((v[u].w - mean) * rs, lw.w, lb.w));
+    }
+  }
+}
+
+static inline int launch_ln_rows(const float* x, int ld, long rows, int K, float eps, const float* w, const float* b,
+                                 float* out, int ldo, hipStream_t st) {
+  YS_CHECK_ARG(K % 4 == 0 && K <= 1024 && ld % 4 == 0 && ldo % 4 == 0, "ln_rows: K=%d ld=%d unsupported", K, ld);
+  YS_CHECK_ARG(((uintptr_t)w | (uintptr_t)b | (uintptr_t)x | (uintptr_t)out) % 16 == 0, "ln_rows: 16-byte alignment");
+  if (rows == 0) return 0;
+  const dim3 grid((unsigned)((rows + 3) / 4));
+  if (K <= 256) hipLaunchKernelGGL((ln_rows_kernel<1>), grid, dim3(256), 0, st, x, ld, rows, K, eps, w, b, out, ldo);
+  else if (K <= 512) hipLaunchKernelGGL((ln_rows_kernel<2>), grid, dim3(256), 0, st, x, ld, rows, K, eps, w, b, out, ldo);
+  else hipLaunchKernelGGL((ln_rows_kernel<4>), grid, dim3(256), 0, st, x, ld, rows, K, eps, w, b, out, ldo);
+  YS_CHECK_LAUNCH("ln_rows");
+  return 0;
+}
+
 __device__ __forceinline__ float apply_act(float v, int act) {
   if (act == 1) return siluf_(v);
   if (act == 2) return geluf_(v);

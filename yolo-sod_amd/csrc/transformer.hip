@@ -740,10 +740,9 @@ YS_EXPORT int yolosod_swin_forward(const float* x, float* y, int B, int C, int H
                      dim3(256), lds, st, x, dw_w, T, C, H, W, g.wh, g.ww, g.nWx, g.nWin, (long)B * g.nWin);
   YS_CHECK_LAUNCH("swin_partition");
   GemmArgs ga{};
-  // QKV = LN1(T) Win^T + b_in   (LN applied while staging the A tiles)
-  if ((rc = launch_row_stats(T, C, g.ntok, C, ln1_eps, lns, st))) return rc;
-  ga.A = T; ga.lda = C; ga.B = in_proj_w; ga.ldb = C; ga.M = (int)g.ntok; ga.N = 3 * C; ga.K = C;
-  ga.ln_w = ln1_w; ga.ln_b = ln1_b; ga.ln_stats = lns;
+  // QKV = LN1(T) Win^T + b_in   (LN1(T) -> U once: U is free until the attention writes it)
+  if ((rc = launch_ln_rows(T, C, g.ntok, C, ln1_eps, ln1_w, ln1_b, U, C, st))) return rc;
+  ga.A = U; ga.lda = C; ga.B = in_proj_w; ga.ldb = C; ga.M = (int)g.ntok; ga.N = 3 * C; ga.K = C;
   ga.epi = epi_plain(Q, 0, 3 * C);
   ga.epi.bias = in_proj_b; ga.epi.bias_mode = 2;
   if ((rc = launch_gemm(ga, 1, true, st))) return rc;
@@ -756,9 +755,8 @@ YS_EXPORT int yolosod_swin_forward(const float* x, float* y, int B, int C, int H
   if ((rc = launch_gemm(ga, 1, true, st))) return rc;
   // Hd = GELU(LN2(T) W1^T + b1)
   ga = GemmArgs{};
-  if ((rc = launch_row_stats(T, C, g.ntok, C, ln2_eps, lns, st))) return rc;
-  ga.A = T; ga.lda = C; ga.B = mlp1_w; ga.ldb = C; ga.M = (int)g.ntok; ga.N = mlp_hidden; ga.K = C;
-  ga.ln_w = ln2_w; ga.ln_b = ln2_b; ga.ln_stats = lns;
+  if ((rc = launch_ln_rows(T, C, g.ntok, C, ln2_eps, ln2_w, ln2_b, U, C, st))) return rc;  // the out-proj has read U
+  ga.A = U; ga.lda = C; ga.B = mlp1_w; ga.ldb = C; ga.M = (int)g.ntok; ga.N = mlp_hidden; ga.K = C;
   ga.epi = epi_plain(Q, 0, mlp_hidden);
   ga.epi.bias = mlp1_b; ga.epi.bias_mode = 2; ga.epi.act = 2;
   if ((rc = launch_gemm(ga, 1, true, st))) return rc;
@@ -848,9 +846,9 @@ YS_EXPORT int yolosod_a2_forward(const float* x, float* y, int B, int C, int H, 
                      st, XP, S, C, H, W, A);
   YS_CHECK_LAUNCH("a2_pool");
   ga = GemmArgs{};
-  if ((rc = launch_row_stats(S, C, ntok, C, ln_eps, lns, st))) return rc;
-  ga.A = S; ga.lda = C; ga.B = in_proj_w; ga.ldb = C; ga.M = (int)ntok; ga.N = 3 * C; ga.K = C;
-  ga.ln_w = ln_w; ga.ln_b = ln_b; ga.ln_stats = lns;
+  // LN(S) -> U once (U is free until the attention writes it), then the QKV GEMM without an LN prologue
+  if ((rc = launch_ln_rows(S, C, ntok, C, ln_eps, ln_w, ln_b, U, C, st))) return rc;
+  ga.A = U; ga.lda = C; ga.B = in_proj_w; ga.ldb = C; ga.M = (int)ntok; ga.N = 3 * C; ga.K = C;
   ga.epi = epi_plain(Q, 0, 3 * C);
   ga.epi.bias = in_proj_b; ga.epi.bias_mode = 2;
   ga.x2 = x2; ga.x2_sb = 64.f;
