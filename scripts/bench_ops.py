@@ -18,6 +18,9 @@ CASES = {
     "swin_L28": ("SwinBlock", (64, 2, 7), (32, 64, 160, 160)),
     "swin_L9": ("SwinBlock", (256, 4, 7), (32, 256, 40, 40)),
     "a2_L12": ("A2_Attn", (512, None, 8, 8), (32, 512, 20, 20)),
+    "a2_L12_1280": ("A2_Attn", (512, None, 8, 8), (8, 512, 40, 40)),  # configs[3] (n1280, bs 8)
+    "swin_L28_1280": ("SwinBlock", (64, 2, 7), (8, 64, 320, 320)),
+    "swin_L9_1280": ("SwinBlock", (256, 4, 7), (8, 256, 80, 80)),
     "se_L1": ("SE_Block", (64,), (32, 32, 320, 320)),
     "cbam_L4": ("CBAM_Block", (64, 128, 16), (32, 64, 160, 160)),
     "ca_L32": ("CA_Block", (128, 256, 32), (32, 128, 80, 80)),
