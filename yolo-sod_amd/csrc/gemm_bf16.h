@@ -180,6 +180,8 @@ __global__ __launch_bounds__(256, A_LN ? 2 : 3) void gemm_bf16_kernel(GemmB g) {
   constexpr int B_ELEMS = BN * SK;
   constexpr int NA = BM * BK / 8 / 256;       // 16-byte chunks per thread per A tile
   constexpr int NB = BN * BK / 8 / 256;
+  // an N-contiguous B tile as one 4x8 (k, n) block per thread (BN / 8 column chunks x BK / 4 row quads = 256)
+  constexpr bool BT = !B_KC && NB == 4 && (BN / 8) * (BK / 4) == 256;
   constexpr int SC = BN + 4;                  // epilogue staging row stride (fp32)
   // one LDS image of the A / B tiles (the next tile waits in registers, so a second LDS buffer bought nothing but
   // occupancy lost) and the C staging in two row halves: 37 KB per workgroup instead of 74, 3 workgroups per CU
@@ -237,7 +239,10 @@ __global__ __launch_bounds__(256, A_LN ? 2 : 3) void gemm_bf16_kernel(GemmB g) {
         rb[i] = make_uint4(0u, 0u, 0u, 0u);
         if (n < N) rb[i] = *reinterpret_cast<const uint4*>(B + (long)n * g.ldb + k0 + kc);
       } else {
-        const int kl = idx / (BN / 8), nc = (idx % (BN / 8)) * 8;
+        // BT: thread t loads k rows 4 (t / (BN/8)) + i of its 8-column chunk (t % (BN/8)): a 4x8 (k, n) block that
+        // store_tiles writes as 8 [n][k] rows of 4 k (8-byte LDS stores instead of 32 2-byte ones)
+        const int kl = BT ? 4 * (tid / (BN / 8)) + i : idx / (BN / 8);
+        const int nc = ((BT ? tid : idx) % (BN / 8)) * 8;
         const int n = n0 + nc;
         const bf16_t* src = B + (long)(k0 + kl) * g.ldb + n;
         if (n + 7 < N) {
@@ -279,6 +284,19 @@ __global__ __launch_bounds__(256, A_LN ? 2 : 3) void gemm_bf16_kernel(GemmB g) {
       if (B_KC) {
         const int r = idx >> 3, kc = (idx & 7) * 8;
         *reinterpret_cast<uint4*>(&Bb[r * SK + kc]) = rb[i];
+      } else if (BT) {  // the thread's 4x8 block: n = nc + j gets k = kq .. kq + 3 as one 8-byte store
+        if (i == 0) {
+          const int kq = 4 * (tid / (BN / 8)), nc = (tid % (BN / 8)) * 8;
+          const uint32_t w[4][4] = {{rb[0].x, rb[0].y, rb[0].z, rb[0].w}, {rb[1].x, rb[1].y, rb[1].z, rb[1].w},
+                                    {rb[2].x, rb[2].y, rb[2].z, rb[2].w}, {rb[3].x, rb[3].y, rb[3].z, rb[3].w}};
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int sh = (j & 1) * 16;  // element j of a row: 32-bit word j / 2, half j % 2
+            const uint32_t e0 = (w[0][j >> 1] >> sh) & 0xffffu, e1 = (w[1][j >> 1] >> sh) & 0xffffu;
+            const uint32_t e2 = (w[2][j >> 1] >> sh) & 0xffffu, e3 = (w[3][j >> 1] >> sh) & 0xffffu;
+            *reinterpret_cast<uint2*>(&Bb[(nc + j) * SK + kq]) = make_uint2(e0 | (e1 << 16), e2 | (e3 << 16));
+          }
+        }
       } else {  // 8 n-consecutive values of one k row -> column k of 8 [n][k] rows
         const int kl = idx / (BN / 8), nc = (idx % (BN / 8)) * 8;
         const uint32_t w[4] = {rb[i].x, rb[i].y, rb[i].z, rb[i].w};

@@ -321,6 +321,40 @@ __global__ __launch_bounds__(256) void a2_upsample_out_bf16_kernel(const bf16_t*
   y[o] = f2bf(bf2f(x[o]) + siluf_(u + bias[c]));
 }
 
+// The same tail with 4 consecutive elements of a plane per thread (H*W % 4 == 0): 8-byte x loads and y stores (the
+// 2-byte form ran at ~1.3 TB/s). grid = ceil(planes * H*W / 1024); same arithmetic per element.
+__global__ __launch_bounds__(256) void a2_upsample_out4_bf16_kernel(const bf16_t* __restrict__ x,
+                                                                    const bf16_t* __restrict__ T,
+                                                                    const float* __restrict__ bias,
+                                                                    bf16_t* __restrict__ y, int C, int H, int W, int A,
+                                                                    long total4) {
+  const long i4 = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i4 >= total4) return;
+  const long HW = (long)H * W;
+  const long o = i4 * 4;
+  const long pc = o / HW;  // img*C + c (HW % 4 == 0: the 4 elements share the plane)
+  const int c = (int)(pc % C);
+  const int e0 = (int)(o - pc * HW);
+  const float sc = (float)A / (float)H;
+  const bf16_t* Tp = T + pc * A * W;
+  const float b = bias[c];
+  const f32x4 xv = ld4(x + o);
+  f32x4 r;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int e = e0 + k;
+    const int h = e / W, w = e - h * W;
+    float src = sc * ((float)h + 0.5f) - 0.5f;
+    if (src < 0.f) src = 0.f;
+    const int y0 = (int)src;
+    const int y1 = y0 + ((y0 < A - 1) ? 1 : 0);
+    const float l1 = src - (float)y0, l0 = 1.0f - l1;
+    const float u = l0 * bf2f(Tp[y0 * W + w]) + l1 * bf2f(Tp[y1 * W + w]);
+    r[k] = xv[k] + siluf_(u + b);
+  }
+  st4(y + o, r);
+}
+
 __global__ void fold_bn_bf16_kernel(const float* w, const float* b, const float* m, const float* v, float eps, int C,
                                     float* scale, float* shift) {
   const int c = blockIdx.x * 256 + threadIdx.x;
@@ -573,8 +607,14 @@ YS_EXPORT int yolosod_a2_forward_bf16(const bf16_t* x, bf16_t* y, int B, int C, 
   ga.A = oproj_w; ga.lda = C; ga.B = U; ga.b_bs = (long)A * W * C; ga.ldb = C; ga.M = C; ga.N = A * W; ga.K = C;
   ga.epi = epib_plain(T, (long)C * A * W, A * W);
   if ((rc = launch_gemm_bf16(ga, B, true, st))) return rc;
-  hipLaunchKernelGGL(a2_upsample_out_bf16_kernel, dim3((unsigned)(B * C), (unsigned)((HW + 255) / 256)), dim3(256), 0,
-                     st, x, T, oproj_b, y, C, H, W, A);
+  if (HW % 4 == 0 && ((uintptr_t)x & 7) == 0 && ((uintptr_t)y & 7) == 0) {
+    const long total4 = (long)B * C * HW / 4;
+    hipLaunchKernelGGL(a2_upsample_out4_bf16_kernel, dim3((unsigned)((total4 + 255) / 256)), dim3(256), 0, st, x, T,
+                       oproj_b, y, C, H, W, A, total4);
+  } else {
+    hipLaunchKernelGGL(a2_upsample_out_bf16_kernel, dim3((unsigned)(B * C), (unsigned)((HW + 255) / 256)), dim3(256), 0,
+                       st, x, T, oproj_b, y, C, H, W, A);
+  }
   YS_CHECK_LAUNCH("a2_upsample_bf16");
   return 0;
 }
