@@ -673,7 +673,13 @@ __global__ __launch_bounds__(256) void ca_apply_kernel(const T* __restrict__ x, 
   const int h = (int)(e / W), w = (int)(e - (long)h * W);
   const float* g = gate + plane * (H + W);
   const float ah = g[h];
-  if (V == 4) {
+  if (V == 8 && sizeof(T) == 2) {  // bf16 storage: 16-byte accesses (8 elements of one row: W % 8 == 0)
+    float f[8];
+    unpack8(*reinterpret_cast<const uint4*>(x + plane * HW + e), f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = (f[j] * g[H + w + j]) * ah;
+    *reinterpret_cast<uint4*>(y + plane * HW + e) = pack8(f);
+  } else if (V == 4) {
     f32x4 v = ld4(x + plane * HW + e);
     v.x = (v.x * g[H + w]) * ah;
     v.y = (v.y * g[H + w + 1]) * ah;
@@ -927,7 +933,10 @@ static int ca_forward_impl(const T* x, T* y, int B, int C, int H, int W, const f
   if (RB > H) RB = H;
   const size_t pool_lds = sizeof(float) * (size_t)RB * W;
   const int V = (W % 4 == 0) ? 4 : 1;
-  const unsigned apply_y = (unsigned)((HW + 256 * V - 1) / (256 * V));
+  // bf16: 8 elements (16 bytes) per thread in the apply pass when rows allow it (4 elements = 8-byte accesses ran at
+  // ~4 TB/s at the m640 shape)
+  const int VA = (sizeof(T) == 2 && W % 8 == 0) ? 8 : V;
+  const unsigned apply_y = (unsigned)((HW + 256 * VA - 1) / (256 * VA));
   const int ipc = images_per_chunk(B, (size_t)C * HW * sizeof(T));
   for (int b0 = 0; b0 < B; b0 += ipc) {
     const int nb = (B - b0 < ipc) ? B - b0 : ipc;
@@ -939,7 +948,10 @@ static int ca_forward_impl(const T* x, T* y, int B, int C, int H, int W, const f
                        (yin_pre ? yin_pre : yin) + goff, C, H, W,
                        mip, conv1_w, conv1_b, bn_w, bn_b, bn_mean, bn_var, bn_eps, convh_w, convh_b, convw_w, convw_b,
                        gate + goff);
-    if (V == 4)
+    if (VA == 8)
+      hipLaunchKernelGGL((ca_apply_kernel<8, T>), dim3(nb * C, apply_y), dim3(256), 0, st, x + off, y + off,
+                         gate + goff, H, W);
+    else if (V == 4)
       hipLaunchKernelGGL((ca_apply_kernel<4, T>), dim3(nb * C, apply_y), dim3(256), 0, st, x + off, y + off,
                          gate + goff, H, W);
     else
