@@ -19,8 +19,12 @@ CASES = [  # (B, C, H, W, residual, stats)
 
 def main():
     dev = torch.device("cuda")
+    bf16 = "--bf16" in sys.argv
+    dt = torch.bfloat16 if bf16 else torch.float32
     for B, C, H, W, res, stats in CASES:
-        y = torch.randn(B, C, H, W, device=dev)
+        if bf16:
+            B *= 2  # the m640 config's batch of 64
+        y = torch.randn(B, C, H, W, device=dev).to(dt)
         out = torch.empty_like(y)
         r = torch.randn_like(y) if res else None
         bias = torch.randn(C, device=dev)
@@ -35,7 +39,7 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / 20
-        nbytes = y.numel() * 4 * (3 if res else 2)
+        nbytes = y.numel() * y.element_size() * (3 if res else 2)
         print(f"bias_act {B}x{C}x{H}x{W} res={int(res)} stats={stats}: {ms * 1e3:7.1f} us  {nbytes / ms / 1e9:6.2f} TB/s",
               flush=True)
 

@@ -11,6 +11,19 @@
 
 namespace ys {
 
+// SiLU of an epilogue value: bf16 storage uses the hardware exp2 / rcp form (error ~2^-22 relative, far below the
+// bf16 rounding of the store; the libm expf + IEEE division made the bf16 passes VALU-bound), fp32 storage the
+// libm form (x / (1 + exp(-x)), the reference's arithmetic)
+template <class T>
+__device__ __forceinline__ float silu_st(float v) {
+#ifdef YS_FAST_SILU_F32  // A/B builds only: the fast form for fp32 storage too
+  return silu_fast_(v);
+#else
+  if constexpr (sizeof(T) == 2) return silu_fast_(v);
+  else return siluf_(v);
+#endif
+}
+
 template <int ACT, bool RES, bool DUAL = false, class T = float>
 __global__ __launch_bounds__(256) void bias_act_kernel(const T* __restrict__ y, T* __restrict__ out,
                                                        const float* __restrict__ bias, const T* __restrict__ res,
@@ -26,12 +39,44 @@ __global__ __launch_bounds__(256) void bias_act_kernel(const T* __restrict__ y, 
     f32x4 v = ld4(y + 4 * (b * y_bs4 + rem));
     v += bc;
     if (ACT == 1) {
-      v.x = siluf_(v.x); v.y = siluf_(v.y); v.z = siluf_(v.z); v.w = siluf_(v.w);
+      v.x = silu_st<T>(v.x); v.y = silu_st<T>(v.y); v.z = silu_st<T>(v.z); v.w = silu_st<T>(v.w);
     }
     if (RES) v += ld4(res + 4 * (b * r_bs4 + rem));
     st4(out + 4 * (b * o_bs4 + rem), v);
     // second, packed copy of channels [c2lo, C): the next conv's input without a separate .contiguous() pass
     if (DUAL && c >= c2lo) st4(out2 + 4 * (b * o2_bs4 + rem - (long)c2lo * HW4), v);
+  }
+}
+
+// bf16 storage, 8 elements (16 bytes) per access: the same grid-stride walk in 8-element units (HW % 8 == 0, batch
+// strides % 8 == 0, 16-byte aligned). With 4 elements per access (8 bytes) the bf16 epilogues ran at 2-3.3 TB/s.
+// The bf16 config's semantics: fp32 arithmetic, one rounding on store.
+template <int ACT, bool RES, bool DUAL>
+__global__ __launch_bounds__(256) void bias_act8_bf16_kernel(const bf16_t* __restrict__ y, bf16_t* __restrict__ out,
+                                                             const float* __restrict__ bias,
+                                                             const bf16_t* __restrict__ res, int C, long HW8,
+                                                             long y_bs8, long o_bs8, long r_bs8, long total8, int rev,
+                                                             bf16_t* __restrict__ out2, int c2lo, long o2_bs8) {
+  for (long i0 = (long)blockIdx.x * 256 + threadIdx.x; i0 < total8; i0 += (long)gridDim.x * 256) {
+    const long i = rev ? total8 - 1 - i0 : i0;
+    const long b = i / ((long)C * HW8);
+    const long rem = i - b * (long)C * HW8;
+    const int c = (int)(rem / HW8);
+    const float bc = bias[c];
+    float f[8];
+    unpack8(*reinterpret_cast<const uint4*>(y + 8 * (b * y_bs8 + rem)), f);
+    float r[8];
+    if (RES) unpack8(*reinterpret_cast<const uint4*>(res + 8 * (b * r_bs8 + rem)), r);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float v = f[j] + bc;
+      if (ACT == 1) v = silu_st<bf16_t>(v);
+      if (RES) v += r[j];
+      f[j] = v;
+    }
+    const uint4 o = pack8(f);
+    *reinterpret_cast<uint4*>(out + 8 * (b * o_bs8 + rem)) = o;
+    if (DUAL && c >= c2lo) *reinterpret_cast<uint4*>(out2 + 8 * (b * o2_bs8 + rem - (long)c2lo * HW8)) = o;
   }
 }
 
@@ -76,7 +121,7 @@ __global__ __launch_bounds__(256) void bias_act_stats_kernel(const T* __restrict
       if (i >= n4) continue;
       f32x4 o = v[u] + bc;
       if (ACT == 1) {
-        o.x = siluf_(o.x); o.y = siluf_(o.y); o.z = siluf_(o.z); o.w = siluf_(o.w);
+        o.x = silu_st<T>(o.x); o.y = silu_st<T>(o.y); o.z = silu_st<T>(o.z); o.w = silu_st<T>(o.w);
       }
       if (RES) o += r[u];
       st4(o4 + 4 * i, o);
@@ -131,7 +176,7 @@ __global__ __launch_bounds__(256) void bias_act_capool_kernel(const T* __restric
     for (int i = tid; i < n4; i += 256) {
       f32x4 v = ld4(yp + base + 4 * i) + bc;
       if (ACT == 1) {
-        v.x = siluf_(v.x); v.y = siluf_(v.y); v.z = siluf_(v.z); v.w = siluf_(v.w);
+        v.x = silu_st<T>(v.x); v.y = silu_st<T>(v.y); v.z = silu_st<T>(v.z); v.w = silu_st<T>(v.w);
       }
       if (RES) v += ld4(rp + base + 4 * i);
       st4(op + base + 4 * i, v);
@@ -339,9 +384,32 @@ static int bias_act_impl(const T* y, long y_bstride, T* out, long out_bstride, c
                "bias_act: pointers must be aligned to 4 elements");
   const long total4 = (long)B * C * (HW / 4);
   if (total4 == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  if constexpr (sizeof(T) == 2) {
+    if (HW % 8 == 0 && y_bstride % 8 == 0 && out_bstride % 8 == 0 && (!res || res_bstride % 8 == 0) &&
+        (!out2 || out2_bstride % 8 == 0) &&
+        (((uintptr_t)y | (uintptr_t)out | (uintptr_t)(res ? res : y) | (uintptr_t)(out2 ? out2 : y)) & 15) == 0) {
+      const long total8 = total4 / 2;
+      long b8 = (total8 + 255) / 256;
+      if (b8 > 8192) b8 = 8192;
+      const long hw8 = HW / 8, yb8 = y_bstride / 8, ob8 = out_bstride / 8, rb8 = res_bstride / 8, o28 = out2_bstride / 8;
+#define YS_BA8(A_, R_, D_)                                                                                              \
+  hipLaunchKernelGGL((bias_act8_bf16_kernel<A_, R_, D_>), dim3(b8), dim3(256), 0, st, y, out, bias, res, C, hw8, yb8, ob8, \
+                     rb8, total8, mall_reverse(), out2, c2lo, o28)
+      if (out2) {
+        if (act == 1) { if (res) YS_BA8(1, true, true); else YS_BA8(1, false, true); }
+        else { if (res) YS_BA8(0, true, true); else YS_BA8(0, false, true); }
+      } else {
+        if (act == 1) { if (res) YS_BA8(1, true, false); else YS_BA8(1, false, false); }
+        else { if (res) YS_BA8(0, true, false); else YS_BA8(0, false, false); }
+      }
+#undef YS_BA8
+      YS_CHECK_LAUNCH("bias_act8_bf16");
+      return 0;
+    }
+  }
   long blocks = (total4 + 255) / 256;
   if (blocks > 8192) blocks = 8192;
-  hipStream_t st = (hipStream_t)stream;
   const long hw4 = HW / 4, yb = y_bstride / 4, ob = out_bstride / 4, rb = res_bstride / 4, o2 = out2_bstride / 4;
 #define YS_BA(A_, R_, D_)                                                                                          \
   hipLaunchKernelGGL((bias_act_kernel<A_, R_, D_, T>), dim3(blocks), dim3(256), 0, st, y, out, bias, res, C, hw4, yb, \
