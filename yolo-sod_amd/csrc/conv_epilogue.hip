@@ -84,7 +84,8 @@ __global__ __launch_bounds__(256) void bias_act8_bf16_kernel(const bf16_t* __res
 // (smallobj_modules.py:87 mean, cbam_block.py:14-17 mean + max): workgroup (plane, k) handles the plane segment
 // [k*seg, (k+1)*seg) - the segmentation of channel_attention.hip's part_plan - and writes psum/pmax[plane*parts + k].
 // The gate then needs no extra pass over the producer's output.
-template <int ACT, bool RES, bool MAX, class T = float>
+// V8 (bf16 storage, segment and plane multiples of 8, 16-byte aligned): 8 elements per 16-byte access.
+template <int ACT, bool RES, bool MAX, class T = float, bool V8 = false>
 __global__ __launch_bounds__(256) void bias_act_stats_kernel(const T* __restrict__ y, T* __restrict__ out,
                                                              const float* __restrict__ bias,
                                                              const T* __restrict__ res, int C, long HW,
@@ -105,6 +106,41 @@ __global__ __launch_bounds__(256) void bias_act_stats_kernel(const T* __restrict
   const long n4 = (s1 - s0) >> 2;
   const int tid = threadIdx.x;
   float s = 0.f, m = -INFINITY;
+  if constexpr (V8 && sizeof(T) == 2) {
+    const long n8 = (s1 - s0) >> 3;
+    for (long i0 = tid; i0 < n8; i0 += 4 * 256) {
+      uint4 v[4], r[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const long i = i0 + u * 256;
+        if (i < n8) {
+          v[u] = *reinterpret_cast<const uint4*>(y4 + 8 * i);
+          if (RES) r[u] = *reinterpret_cast<const uint4*>(r4 + 8 * i);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const long i = i0 + u * 256;
+        if (i >= n8) continue;
+        float f[8], rr[8];
+        unpack8(v[u], f);
+        if (RES) unpack8(r[u], rr);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float o = f[j] + bc;
+          if (ACT == 1) o = silu_st<T>(o);
+          if (RES) o += rr[j];
+          f[j] = o;
+        }
+        const uint4 ob = pack8(f);
+        *reinterpret_cast<uint4*>(o4 + 8 * i) = ob;
+        unpack8(ob, f);  // statistics of the stored (rounded) values
+        s += ((f[0] + f[1]) + (f[2] + f[3])) + ((f[4] + f[5]) + (f[6] + f[7]));
+        if (MAX)
+          m = fmaxf(m, fmaxf(fmaxf(fmaxf(f[0], f[1]), fmaxf(f[2], f[3])), fmaxf(fmaxf(f[4], f[5]), fmaxf(f[6], f[7]))));
+      }
+    }
+  } else
   for (long i0 = tid; i0 < n4; i0 += 4 * 256) {
     f32x4 v[4], r[4];
 #pragma unroll
@@ -352,9 +388,20 @@ static int bias_act_stats_impl(const T* y, long y_bstride, T* out, long out_bstr
   if (blocks == 0) return 0;
   YS_CHECK_ARG(blocks < (1L << 31), "bias_act_stats: too many planes");
   hipStream_t st = (hipStream_t)stream;
+  // bf16: 8 elements per 16-byte access when the plane plan and the strides allow it
+  const bool v8 = sizeof(T) == 2 && HW % 8 == 0 && seg % 8 == 0 && y_bstride % 8 == 0 && out_bstride % 8 == 0 &&
+                  (!res || res_bstride % 8 == 0) && (((uintptr_t)y | (uintptr_t)out | (uintptr_t)(res ? res : y)) & 15) == 0;
 #define YS_BAS(A_, R_, M_)                                                                                         \
-  hipLaunchKernelGGL((bias_act_stats_kernel<A_, R_, M_, T>), dim3((unsigned)blocks), dim3(256), 0, st, y, out, bias, \
-                     res, C, HW, y_bstride, out_bstride, res_bstride, parts, seg, psum, pmax, mall_reverse())
+  do {                                                                                                             \
+    if (v8)                                                                                                        \
+      hipLaunchKernelGGL((bias_act_stats_kernel<A_, R_, M_, T, true>), dim3((unsigned)blocks), dim3(256), 0, st, y, \
+                         out, bias, res, C, HW, y_bstride, out_bstride, res_bstride, parts, seg, psum, pmax,       \
+                         mall_reverse());                                                                          \
+    else                                                                                                           \
+      hipLaunchKernelGGL((bias_act_stats_kernel<A_, R_, M_, T>), dim3((unsigned)blocks), dim3(256), 0, st, y, out,  \
+                         bias, res, C, HW, y_bstride, out_bstride, res_bstride, parts, seg, psum, pmax,            \
+                         mall_reverse());                                                                          \
+  } while (0)
   const bool mx = pmax != nullptr;
   if (act == 1) {
     if (res) { if (mx) YS_BAS(1, true, true); else YS_BAS(1, true, false); }
