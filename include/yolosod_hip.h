@@ -107,6 +107,11 @@ int yolosod_cbam_forward_pre(const float* x, float* y, int B, int C, int H, int 
 int yolosod_bias_act_capool(const float* y, long y_bstride, float* out, long out_bstride, const float* bias,
                             const float* res, long res_bstride, int B, int C, int H, int W, int act, float* yin,
                             void* stream);
+/* Nearest 2x upsample (nn.Upsample(None, 2, 'nearest') rows of the neck YAML) of x [B, C, h, w] into a channel
+ * slice of the following Concat's buffer (out batch stride in elements): the neck glue's copy, not a hot-path op.
+ * elem_bytes 4 (fp32) / 2 (bf16); w % 4 == 0 and 16-byte aligned pointers / strides. */
+int yolosod_upsample2x(const void* x, void* out, long out_bstride, int B, int C, int h, int w, int elem_bytes,
+                       void* stream);
 int yolosod_ca_forward_pre(const float* x, float* y, int B, int C, int H, int W, const float* conv1_w,
                            const float* conv1_b, int mip, const float* bn_w, const float* bn_b, const float* bn_mean,
                            const float* bn_var, float bn_eps, const float* convh_w, const float* convh_b,

@@ -50,6 +50,7 @@ SIGNATURES = {
     "yolosod_layernorm": (_i, [_vp, _vp, _l, _i, _vp, _vp, _f, _vp]),
     "yolosod_attention": (_i, [_vp, _vp, _l, _i, _i, _i, _vp]),
     "yolosod_bias_act": (_i, [_vp, _l, _vp, _l, _vp, _vp, _l, _i, _i, _l, _i, _vp]),
+    "yolosod_upsample2x": (_i, [_vp, _vp, _l, _i, _i, _i, _i, _i, _vp]),
     "yolosod_conv1x1_thin_stats": (_i, [_vp, _l, _vp, _vp, _vp, _l, _i, _i, _i, _l, _i, _vp, _vp, _vp, _vp]),
     "yolosod_conv1x1_thin": (_i, [_vp, _l, _vp, _vp, _vp, _l, _vp, _l, _vp, _l, _i, _i, _i, _i, _l, _vp]),
     "yolosod_bias_act_dual": (_i, [_vp, _l, _vp, _l, _vp, _vp, _l, _vp, _l, _i, _i, _i, _l, _i, _vp]),
@@ -530,6 +531,25 @@ def bias_act(y, bias, act, out=None, res=None, stats=None, out2=None, c2lo=0):
     _check(_launch(("bias_act", tuple(y.shape), None), y.device, lib.yolosod_bias_act, y.data_ptr(), yb, out.data_ptr(),
                    ob, bp, rp, rb, B, C, HW, int(act), _stream(y.device)), "bias_act")
     return out
+
+
+def upsample2x_into(x, out) -> bool:
+    """Nearest 2x upsample of x [B, C, h, w] (contiguous, fp32 / bf16) into ``out`` [B, C, 2h, 2w], a channel slice
+    of a Concat buffer (contiguous channels, any batch stride): the neck's ``nn.Upsample`` + ``Concat`` glue
+    (tasks._predict_once_planned). Returns False, launching nothing, when the HIP kernel's shape / alignment
+    conditions (w % 4 == 0, 16-byte aligned operands and strides) do not hold."""
+    B, C, h, w = x.shape
+    if (x.device.type != "cuda" or out.device != x.device or out.dtype != x.dtype or x.dtype not in (torch.float32, _BF16)
+            or not x.is_contiguous() or tuple(out.shape) != (B, C, 2 * h, 2 * w) or out.stride(3) != 1
+            or out.stride(2) != 2 * w or out.stride(1) != 4 * h * w):
+        return False
+    eb = x.element_size()
+    if (w % 4 or x.data_ptr() % 16 or out.data_ptr() % 16 or (out.stride(0) * eb) % 16 or (4 * h * w * eb) % 16
+            or B == 0):
+        return False
+    _check(_launch(("upsample2x", tuple(x.shape), None), x.device, load_library().yolosod_upsample2x, x.data_ptr(),
+                   out.data_ptr(), out.stride(0), B, C, h, w, eb, _stream(x.device)), "upsample2x")
+    return True
 
 
 THIN1X1_COUT = (64, 128)

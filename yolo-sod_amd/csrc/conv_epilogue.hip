@@ -367,9 +367,65 @@ __global__ __launch_bounds__(256) void thin_stats_reduce_kernel(const float* __r
   }
 }
 
+// Nearest 2x upsample (nn.Upsample(scale_factor=2, mode='nearest'), conv.py / tasks.py neck rows) straight into a
+// channel slice of the Concat buffer (batch stride ob). A thread takes 4 consecutive pixels of one input row (one 16 /
+// 8-byte load) and writes them doubled to output rows 2i and 2i + 1 (two 32 / 16-byte row chunks, 16-byte stores):
+// the strided 6-D copy PyTorch runs for it streams at ~3.3 TB/s. Pure data movement: E is the element's bit pattern
+// (uint32_t for fp32, uint16_t for bf16). Requires w % 4 == 0 and 16-byte aligned x / out / strides (host checks).
+template <class E>
+__global__ __launch_bounds__(256) void upsample2x_kernel(const E* __restrict__ x, E* __restrict__ out, long ob, int C,
+                                                         int h, int w, long quads) {
+  const int wq = w >> 2;
+  for (long q = (long)blockIdx.x * 256 + threadIdx.x; q < quads; q += (long)gridDim.x * 256) {
+    const long row = q / wq;  // (b, c, i)
+    const int j = (int)(q - row * wq) * 4;
+    const long plane = row / h;
+    const int i = (int)(row - plane * h);
+    const int b = (int)(plane / C), c = (int)(plane - (long)b * C);
+    E* o = out + (long)b * ob + ((long)c * 2 * h + 2 * i) * (2L * w) + 2 * j;
+    if (sizeof(E) == 4) {
+      const uint4 v = *reinterpret_cast<const uint4*>(x + row * w + j);
+      const uint4 lo = make_uint4(v.x, v.x, v.y, v.y), hi = make_uint4(v.z, v.z, v.w, v.w);
+      uint4* o0 = reinterpret_cast<uint4*>(o);
+      uint4* o1 = reinterpret_cast<uint4*>(o + 2L * w);
+      o0[0] = lo; o0[1] = hi; o1[0] = lo; o1[1] = hi;
+    } else {
+      const uint2 v = *reinterpret_cast<const uint2*>(x + row * w + j);
+      const uint32_t e0 = v.x & 0xffffu, e1 = v.x >> 16, e2 = v.y & 0xffffu, e3 = v.y >> 16;
+      const uint4 d = make_uint4(e0 | (e0 << 16), e1 | (e1 << 16), e2 | (e2 << 16), e3 | (e3 << 16));
+      *reinterpret_cast<uint4*>(o) = d;
+      *reinterpret_cast<uint4*>(o + 2L * w) = d;
+    }
+  }
+}
+
 }  // namespace ys
 
 using namespace ys;
+
+// x [B, C, h, w] contiguous -> out [B, C, 2h, 2w] with batch stride out_bstride (elements); elem_bytes 4 (fp32) or 2
+// (bf16). Returns 0, or a negative code when the shape / alignment is not handled (the caller keeps its copy).
+YS_EXPORT int yolosod_upsample2x(const void* x, void* out, long out_bstride, int B, int C, int h, int w, int elem_bytes,
+                                 void* stream) {
+  YS_CHECK_ARG(x && out, "upsample2x: null pointer");
+  YS_CHECK_ARG(B >= 0 && C > 0 && h > 0 && w > 0 && (elem_bytes == 4 || elem_bytes == 2), "upsample2x: bad shape");
+  YS_CHECK_ARG(w % 4 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)out & 15) == 0 &&
+                   (out_bstride * elem_bytes) % 16 == 0 && (4L * h * w * elem_bytes) % 16 == 0 &&
+                   out_bstride >= 4L * C * h * w,
+               "upsample2x: w %% 4, 16-byte alignment and a batch stride >= C*4*h*w required");
+  if (B == 0) return 0;
+  const long quads = (long)B * C * h * (w / 4);
+  const unsigned grid = (unsigned)((quads + 255) / 256 < 8192 ? (quads + 255) / 256 : 8192);
+  hipStream_t st = (hipStream_t)stream;
+  if (elem_bytes == 4)
+    hipLaunchKernelGGL(upsample2x_kernel<uint32_t>, dim3(grid), dim3(256), 0, st, (const uint32_t*)x, (uint32_t*)out,
+                       out_bstride, C, h, w, quads);
+  else
+    hipLaunchKernelGGL(upsample2x_kernel<uint16_t>, dim3(grid), dim3(256), 0, st, (const uint16_t*)x, (uint16_t*)out,
+                       out_bstride, C, h, w, quads);
+  YS_CHECK_LAUNCH("upsample2x");
+  return 0;
+}
 
 template <class T>
 static int bias_act_stats_impl(const T* y, long y_bstride, T* out, long out_bstride, const float* bias, const T* res,

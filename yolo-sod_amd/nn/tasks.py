@@ -29,6 +29,7 @@ import torch
 import torch.nn as nn
 import yaml
 
+from .. import _hip
 from . import modules as M
 
 CFG_DIR = Path(__file__).resolve().parent.parent / "cfg"
@@ -40,6 +41,9 @@ CFG_DIR = Path(__file__).resolve().parent.parent / "cfg"
 # moved time between the two streams: m640 1636 vs 1634 img/s same-box, CA 0.33 vs 0.12 ms on the main stream)
 _STREAMS_ENV = os.environ.get("YOLOSOD_STREAMS")
 STREAMS = int(_STREAMS_ENV) if _STREAMS_ENV is not None else 1
+# the neck's nearest 2x upsample into its Concat slice as one HIP pass (YOLOSOD_UPSAMPLE_HIP=0: PyTorch's strided
+# copy, for A/B)
+UPSAMPLE_HIP = os.environ.get("YOLOSOD_UPSAMPLE_HIP", "1") != "0"
 
 # name -> class; the YAML resolves module strings through this (tasks.py:995-1002)
 DEFAULT_REGISTRY = {
@@ -262,7 +266,8 @@ class BaseModel(nn.Module):
                     out = buf[:, offs[k]:offs[k] + cp]
                     if isinstance(m, nn.Upsample):
                         h, w = inp.shape[2], inp.shape[3]
-                        out.view(B, cp, h, 2, w, 2).copy_(inp[:, :, :, None, :, None].expand(B, cp, h, 2, w, 2))
+                        if not (UPSAMPLE_HIP and _hip.upsample2x_into(inp, out)):
+                            out.view(B, cp, h, 2, w, 2).copy_(inp[:, :, :, None, :, None].expand(B, cp, h, 2, w, 2))
                     else:
                         m.forward_fuse(inp, out=out)
                     pend[c] = (buf, offs, chans)
