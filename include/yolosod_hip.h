@@ -25,6 +25,10 @@ extern "C" {
 
 int yolosod_abi_version(void);
 const char* yolosod_last_error(void);
+/* Per-device state (the split-range flag word), allocated and zeroed eagerly; idempotent. Call once per device before
+ * the first launch on it (and before any stream capture): a launch on a device never initialised allocates the state
+ * itself, synchronously. Returns 0, or < 0 on error. The current device is restored. */
+int yolosod_init(int device);
 
 /* SE / SE_Block.forward            ultralytics/nn/modules/smallobj_modules.py:84-92
  * y = x * sigmoid(fc2(relu(fc1(mean_hw(x)))));  fc1: [hidden,C]+[hidden], fc2: [C,hidden]+[C]. */
@@ -75,8 +79,12 @@ int yolosod_swin_forward(const float* x, float* y, int B, int C, int H, int W, i
  * BN fold) done once by the caller and kept across calls, for the shapes of the fp16-split kernels (7x7 windows,
  * C = 64 / 2 heads and C = 256 / 4 heads, mlp_hidden = 2C): yolosod_swin_prep_bytes returns the block's size (0 when
  * (C, heads, hidden) has no such kernel), yolosod_swin_prepare fills a caller-owned block from the parameters of
- * yolosod_swin_forward (re-run it whenever a parameter changes), yolosod_swin_forward_prepared runs the block. */
+ * yolosod_swin_forward (re-run it whenever a parameter changes), yolosod_swin_forward_prepared runs the block with a
+ * caller-owned scratch of yolosod_swin_prepared_workspace bytes (C = 64: T after the attention residual, token-major,
+ * between the attention kernel and the token-tiled MLP kernel). The block also keeps the weights' split-range result,
+ * which every forward on it reports again (yolosod_split_range_flag). One image's C*H*W must stay below 2^30. */
 size_t yolosod_swin_prep_bytes(int C, int num_heads, int mlp_hidden);
+size_t yolosod_swin_prepared_workspace(int B, int C, int H, int W, int num_heads, int window, int mlp_hidden);
 int yolosod_swin_prepare(int C, int num_heads, int mlp_hidden, const float* ln1_w, const float* ln1_b,
                          const float* in_proj_w, const float* in_proj_b, const float* out_proj_w, const float* ln2_w,
                          const float* ln2_b, const float* mlp1_w, const float* mlp1_b, const float* mlp2_w,
@@ -85,7 +93,7 @@ int yolosod_swin_prepare(int C, int num_heads, int mlp_hidden, const float* ln1_
 int yolosod_swin_forward_prepared(const float* x, float* y, int B, int C, int H, int W, int num_heads, int window,
                                   const float* dw_w, float ln1_eps, const float* out_proj_b, float ln2_eps,
                                   int mlp_hidden, const float* mlp2_b, const void* prep, size_t prep_bytes,
-                                  void* stream);
+                                  void* workspace, size_t workspace_bytes, void* stream);
 
 /* Producer-side statistics for the channel gates (SE smallobj_modules.py:87, CBAM cbam_block.py:14-17): a conv
  * epilogue that also writes its output's per-plane partial sums (+ maxes when pmax != NULL) in the segmentation
@@ -209,14 +217,18 @@ void yolosod_debug_set_swin_fused(int on);
 /* Test hook: 1 (default; env YOLOSOD_SWIN_X3=0 turns it off) routes 7x7-window SwinBlocks with C = 64 / 2 heads and
  * C = 256 / 4 heads through the kernels that run every matrix product as fp16 two-term splits on the fp16 matrix
  * cores at fp32 accuracy (csrc/swin_x3.hip), 0 through the exact-fp32-MFMA fused kernels. */
-void yolosod_debug_set_swin_x3(int on);
+int yolosod_debug_set_swin_x3(int on);
+/* Test hook: 1 (env YOLOSOD_SWIN_SPLIT=1) runs the C = 64 fp16-split SwinBlock as two kernels split at the attention
+ * residual (per-window attention half, token-tiled MLP / pw half), 0 (default) as the one-kernel form.
+ * The yolosod_debug_set_* switches that return int return the previous state. */
+int yolosod_debug_set_swin_split(int on);
 /* Test hook: 1 (default; env YOLOSOD_HEAD_X2=0 turns it off) runs the Detect head's 1x1 convs as fp16 two-term
  * splits on the fp16 matrix cores (detect_head_x2_kernel), 0 on the exact fp32 MFMA (detect_head_lds_kernel). */
-void yolosod_debug_set_head_x2(int on);
+int yolosod_debug_set_head_x2(int on);
 /* Test hooks: A2_Attn's GEMMs as fp16 two-term splits on v_mfma_f32_32x32x16_f16 (1, default; env YOLOSOD_A2_X2=0
  * turns it off) or exact fp32 MFMA (0); yolosod_debug_set_gemm_x2(1) makes every yolosod_gemm_f32 / internal fp32 GEMM
  * call take the split products, 0 restores the callers' choice. */
-void yolosod_debug_set_a2_x2(int on);
+int yolosod_debug_set_a2_x2(int on);
 void yolosod_debug_set_gemm_x2(int on);
 /* Test hook: the fp16 two-term split of the fp32-accurate matrix kernels (common.h split2) on npair pairs of v:
  * h[i] = the fp16 pair (fp16(v[2i]), fp16(v[2i+1])), l[i] = (fp16(v[2i] - h.lo), fp16(v[2i+1] - h.hi)), as 2 x 16-bit

@@ -114,3 +114,70 @@ def nms_stability(y_ref: np.ndarray, y_oth: np.ndarray, conf=0.25, iou_thres=0.7
     res["stable"] = bool(m_conf > 2 * d_s and m_cls > 2 * d_s and m_order > 2 * d_s and m_out > 2 * d_s
                          and m_iou > d_iou_tol)
     return res
+
+
+def first_divergence(y_ref: np.ndarray, y_oth: np.ndarray, conf=0.25, iou_thres=0.7, max_nms=30000, max_wh=7680):
+    """The first decision at which predict-mode NMS on ``y_oth`` departs from NMS on ``y_ref`` (single label,
+    class-aware; ``ultralytics/utils/ops.py:274-297`` around torchvision's greedy NMS), or None when every decision
+    agrees - the kept anchor lists are then identical.
+
+    Both outputs are replayed side by side, stage by stage, in the order the reference takes its decisions: the
+    candidate filter (ops.py:234, 275), the best class (:274), the descending-score processing order and the
+    ``max_nms`` cut (:284-286), then the greedy IoU tests box by box (torchvision CPU nms). Everything before the
+    returned decision is identical in both runs, so it is the cause of the first difference in the kept lists. The
+    result holds the decision's margin measured on ``y_ref`` and the tolerance it is held to: twice the measured
+    perturbation of that decision's inputs (score decisions: 2 max|d score| over the image; IoU tests: 2 max|d IoU|
+    over the same-class candidate pairs + 1e-6)."""
+    s_r = np.ascontiguousarray(y_ref[4:].T)
+    s_o = np.ascontiguousarray(y_oth[4:].T)
+    tol_s = 2 * float(np.abs(s_r.astype(np.float64) - s_o).max())
+    best_r, best_o = s_r.max(1), s_o.max(1)
+    c_r, c_o = best_r > np.float32(conf), best_o > np.float32(conf)
+    if (c_r != c_o).any():
+        x = np.nonzero(c_r != c_o)[0]
+        margin = float(np.abs(best_r[x].astype(np.float64) - np.float32(conf)).max())
+        return {"kind": "conf", "anchors": x.tolist(), "margin": margin, "tol": tol_s}
+    cand = np.nonzero(c_r)[0]
+    if cand.size == 0:
+        return None
+    cls_r, cls_o = s_r[cand].argmax(1), s_o[cand].argmax(1)
+    if (cls_r != cls_o).any():
+        x = np.nonzero(cls_r != cls_o)[0]
+        top2 = np.sort(s_r[cand[x]], 1)[:, -2:].astype(np.float64)
+        return {"kind": "class", "anchors": cand[x].tolist(), "margin": float((top2[:, 1] - top2[:, 0]).max()),
+                "tol": tol_s}
+    sc_r = s_r[cand, cls_r]
+    sc_o = s_o[cand, cls_o]
+    ord_r = np.argsort(-sc_r, kind="stable")
+    ord_o = np.argsort(-sc_o, kind="stable")
+    n_proc = min(cand.size, max_nms)
+    if not np.array_equal(ord_r[:n_proc], ord_o[:n_proc]):
+        j = int(np.nonzero(ord_r[:n_proc] != ord_o[:n_proc])[0][0])
+        a, b = ord_r[j], ord_o[j]
+        return {"kind": "order", "position": j, "anchors": [int(cand[a]), int(cand[b])],
+                "margin": abs(float(sc_r[a]) - float(sc_r[b])), "tol": tol_s}
+    order = ord_r[:n_proc]
+    off = (cls_r.astype(np.float32) * np.float32(max_wh))[:, None]
+    b_r = (_xyxy(y_ref[:4, cand].T) + off).astype(np.float32)
+    b_o = (_xyxy(y_oth[:4, cand].T) + off).astype(np.float32)
+    # per class (the offsets keep classes apart): pairwise IoU of both runs and the IoU perturbation
+    ious, d_iou = {}, 0.0
+    for c in np.unique(cls_r[order]):
+        sel = order[cls_r[order] == c]
+        ir, io = _iou(b_r[sel]), _iou(b_o[sel])
+        if len(sel) > 1:
+            iu = np.triu_indices(len(sel), 1)
+            d_iou = max(d_iou, float(np.abs(ir[iu] - io[iu]).max()))
+        ious[int(c)] = (sel, ir, io, [])
+    tol_iou = 2 * d_iou + 1e-6
+    pos = {int(t): i for c in ious for i, t in enumerate(ious[c][0])}
+    for t in order:  # global processing order = per-class order interleaved by score
+        sel, ir, io, kept = ious[int(cls_r[t])]
+        i = pos[int(t)]
+        mx_r = float(ir[kept, i].max()) if kept else 0.0
+        mx_o = float(io[kept, i].max()) if kept else 0.0
+        if (mx_r > iou_thres) != (mx_o > iou_thres):
+            return {"kind": "iou", "anchors": [int(cand[t])], "margin": abs(mx_r - iou_thres), "tol": tol_iou}
+        if not (mx_r > iou_thres):
+            kept.append(i)
+    return None

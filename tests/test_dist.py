@@ -121,6 +121,64 @@ def test_sharded_flow_matches_single_process_gloo(n_images):
     assert sorted(res) == [(0, True), (1, True)]
 
 
+def test_packed_detections_roundtrip():
+    """The exchange buffer (one int32 row per image: fp32 row bits | kept indices | count) unpacks bit for bit,
+    including NaN / -0.0 / inf rows and index -1 padding."""
+    from yolosod_amd.engine.predictor import pack_detections, unpack_detections
+    g = torch.Generator().manual_seed(5)
+    out = torch.randn(3, 300, 6, generator=g)
+    out[0, 0, 0], out[1, 2, 3], out[2, 4, 5] = float("nan"), -0.0, float("inf")
+    counts = torch.tensor([0, 17, 300], dtype=torch.int32)
+    index = torch.randint(-1, 34000, (3, 300), generator=g, dtype=torch.int32)
+    p = pack_detections(out, counts, index)
+    assert p.dtype == torch.int32 and tuple(p.shape) == (3, 7 * 300 + 1) and p.is_contiguous()
+    o2, c2, i2 = unpack_detections(p, 300, True)
+    assert torch.equal(o2.view(torch.int32), out.view(torch.int32)) and torch.equal(c2, counts)
+    assert torch.equal(i2, index)
+    o3, c3 = unpack_detections(pack_detections(out, counts), 300, False)
+    assert torch.equal(o3.view(torch.int32), out.view(torch.int32)) and torch.equal(c3, counts)
+
+
+def _count_collectives_worker(rank, world, port, q):
+    """gather_detections issues exactly one collective (a single exchange latency per step)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        calls = []
+        orig = dist.all_gather_into_tensor
+
+        def counting(*a, **k):
+            calls.append(1)
+            return orig(*a, **k)
+
+        dist.all_gather_into_tensor = counting
+        try:
+            out = torch.full((2, 300, 6), float(rank))
+            g_out, g_cnt, g_idx = gather_detections(out, torch.tensor([rank, 1], dtype=torch.int32),
+                                                    torch.full((2, 300), rank, dtype=torch.int32))
+        finally:
+            dist.all_gather_into_tensor = orig
+        ok = (len(calls) == 1 and g_out.shape == (4, 300, 6) and g_cnt.tolist() == [0, 1, 1, 1]
+              and torch.equal(g_idx[:2], torch.zeros(2, 300, dtype=torch.int32))
+              and torch.equal(g_out[2:], torch.ones(2, 300, 6)))
+        q.put((rank, bool(ok)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gather_detections_is_one_collective_gloo():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_count_collectives_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=90) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert sorted(res) == [(0, True), (1, True)]
+
+
 def test_seeded_images_are_slices_of_one_global_batch():
     from yolosod_amd.engine.predictor import seeded_images
     full = seeded_images(0, 6, 32)

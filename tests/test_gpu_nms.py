@@ -95,3 +95,45 @@ def test_torch_ops_reject_wrong_sized_partials_and_devices(cuda):
     sa = torch.randn(98, device=cuda)
     with pytest.raises(RuntimeError, match="psum"):
         ops.cbam_fwd(x, w1, w2, sa, bad, bad)
+
+
+@pytest.mark.parametrize("kw", [dict(conf_thres=0.25, iou_thres=0.7), dict(conf_thres=0.001, iou_thres=0.6,
+                                                                           multi_label=True)])
+def test_nms_not_in_place_leaves_prediction_untouched(kw, cuda):
+    """in_place=False (DetectionPredictor's call: its Detect output is local) gives the same rows / indices as the
+    in-place call and leaves the prediction tensor bit-identical, without a copy."""
+    from yolosod_amd.utils.ops import non_max_suppression_padded
+    pred = recipes.synthetic_predictions(77, 4, 34000, 10, n_clusters=300)
+    p = torch.from_numpy(pred.copy()).to(cuda)
+    out, counts, index = non_max_suppression_padded(p, in_place=False, **kw)
+    assert np.array_equal(p.cpu().numpy(), pred)
+    p_after, out2, counts2, index2 = _run_gpu(pred, cuda, **kw)
+    assert torch.equal(counts.cpu(), torch.from_numpy(counts2)) and torch.equal(index.cpu(), torch.from_numpy(index2))
+    assert np.array_equal(out.cpu().numpy(), out2)
+
+
+def test_nms_empty_and_sparse_blocks(cuda):
+    """Images without candidates (random-init heads: nothing clears conf) and images whose candidates sit in a few
+    256-anchor blocks only: nms_prep stores masks / boxes for candidate blocks only and nms_scatter skips the
+    rest; results equal the oracle on a workspace filled with garbage first."""
+    from yolosod_amd.utils.ops import non_max_suppression_padded
+    g = np.random.default_rng(8)
+    B, A, nc = 6, 34000, 10
+    pred = np.zeros((B, 4 + nc, A), np.float32)
+    pred[:, 0:2] = g.uniform(0, 640, (B, 2, A))
+    pred[:, 2:4] = g.uniform(4, 90, (B, 2, A))
+    pred[:, 4:] = g.uniform(0, 0.2, (B, nc, A))  # below conf everywhere
+    for b, blocks in ((1, [0]), (3, [7, 8, 132]), (5, list(range(0, 133, 11)))):
+        for blk in blocks:
+            a = np.arange(blk * 256, min(A, blk * 256 + 256))[g.uniform(size=min(256, A - blk * 256)) < 0.3]
+            pred[b, 4 + g.integers(0, nc, a.size), a] = g.uniform(0.3, 1.0, a.size).astype(np.float32)
+    torch.empty(64 << 20, dtype=torch.uint8, device=cuda).fill_(0xA5)  # recycled by the caching allocator: garbage
+    p_after, out, counts, index = _run_gpu(pred, cuda, conf_thres=0.25, iou_thres=0.7)
+    ref = pred.copy()
+    rows, idx = non_max_suppression_ref(ref, 0.25, 0.7)
+    assert np.array_equal(p_after, ref)
+    assert counts.tolist() == [len(r) for r in rows] and counts[0] == 0 and counts[3] > 0
+    for b in range(B):
+        assert np.array_equal(out[b, :counts[b]], rows[b]), b
+        assert np.array_equal(index[b, :counts[b]], idx[b]), b
+        assert (out[b, counts[b]:] == 0).all() and (index[b, counts[b]:] == -1).all()

@@ -115,6 +115,35 @@ def test_swin_exact_fp32_kernels_real_shapes(name, cuda, monkeypatch):
     assert ok, f"{name}: max abs err {err:.3g} ratio {ratio:.2f}"
 
 
+SPLIT_SHAPES = {  # C = 64 SwinBlocks through both forms of the fp16-split kernels
+    "swin_c64_h20": None, "swin_c64_h14": None, "swin_c64_h16x12": None,
+    "swin_L28": REAL["swin_L28"],
+    "swin_c64_b3_20x13": ("SwinBlock", (64, 2, 7), (3, 64, 20, 13)),  # 260 tokens / image: tiles straddle images
+    "swin_c64_b5_9x7": ("SwinBlock", (64, 2, 7), (5, 64, 9, 7)),      # 63 tokens / image: ragged last tile
+}
+
+
+@pytest.mark.parametrize("split", [0, 1], ids=["one_kernel", "split"])
+@pytest.mark.parametrize("name", list(SPLIT_SHAPES))
+def test_swin_c64_split_and_one_kernel_forms(name, split, cuda, monkeypatch):
+    """The C = 64 block split at the attention residual (swin_x3_kernel<64, 2, true> -> token-major T1 ->
+    tok::swin_mlp_kernel, the default) and the one-kernel form (YOLOSOD_SWIN_SPLIT=0), both against the fp64 oracle
+    at the fp32 tolerances; shapes with cropped windows, several images per token tile and a ragged last tile."""
+    lib = _hip.load_library()
+    if SPLIT_SHAPES[name] is not None:
+        monkeypatch.setitem(recipes.OPS, name, SPLIT_SHAPES[name])
+    m, _ = build_fixture_module(name)
+    x = recipes.make_input(name, recipes.OPS[name][2])
+    prev = lib.yolosod_debug_set_swin_split(split)
+    try:
+        with torch.inference_mode():
+            y = m.to(cuda)(x.to(cuda)).cpu()
+    finally:
+        lib.yolosod_debug_set_swin_split(prev)
+    ok, err, ratio = tol_close(y, _oracle64(name, x), 5e-5, 1e-4)
+    assert ok, f"{name} split={split}: vs fp64 oracle max abs err {err:.3g} (ratio {ratio:.2f})"
+
+
 @pytest.mark.parametrize("name,shape", [("se_c32_r64", (9, 32, 64, 64)), ("se_c64_r4_odd", (5, 64, 9, 7)),
                                         ("cbam_c64", (9, 64, 48, 40)), ("cbam_c32_odd", (5, 32, 13, 11)),
                                         ("ca_c128", (9, 128, 24, 20)), ("ca_c64_odd", (5, 64, 9, 7))])

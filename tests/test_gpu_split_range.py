@@ -156,12 +156,41 @@ def test_split_range_guard_flags_and_exact_fallback(name, cuda, monkeypatch):
     assert float((y - ref).abs().max()) <= 1e-4 * float(ref.abs().max())
     if not name.startswith("swin"):
         return
-    # weights beyond range (64 W > 65504): flagged by the weight preparation
+    # weights beyond range (64 W > 65504): flagged by the weight preparation, and again by every later forward on the
+    # cached prepared block (the block keeps the preparation's range word)
     with torch.no_grad():
         md.window_attn.mlp[2].weight.mul_(2e4)
+    for _ in range(3):
+        with torch.inference_mode():
+            md(x.to(cuda))
+        assert _hip.split_range_flag(reset=True)
+
+
+@pytest.mark.parametrize("name", ["swin_L28", "swin_L9", "a2_L12"])
+def test_split_range_guard_flags_nan(name, cuda, monkeypatch):
+    """A NaN operand sets the flag: the running max is the NaN-propagating IEEE maximum (v_maximum3_f32)."""
+    op, args, shape, _ = OPS[name]
+    monkeypatch.setitem(recipes.OPS, name, (op, args, shape))
+    m, _ = build_fixture_module(name)
+    md = m.to(cuda)
+    x = recipes.make_input(name, shape)
+    x[0, 3, 5, 7] = float("nan")
+    _hip.split_range_flag(reset=True)
     with torch.inference_mode():
         md(x.to(cuda))
     assert _hip.split_range_flag(reset=True)
+
+
+def test_exact_fp32_matrix_restores_switches(cuda):
+    """exact_fp32_matrix() restores each split switch to its previous state instead of forcing it on."""
+    lib = _hip.load_library()
+    prev = lib.yolosod_debug_set_head_x2(0)
+    try:
+        with _hip.exact_fp32_matrix():
+            pass
+        assert lib.yolosod_debug_set_head_x2(0) == 0  # still off after the context
+    finally:
+        lib.yolosod_debug_set_head_x2(prev)
 
 
 def test_split_range_guard_detect_head(cuda):
@@ -177,3 +206,45 @@ def test_split_range_guard_detect_head(cuda):
     assert not _hip.split_range_flag(reset=True)
     _hip.detect_head([f * 1e5 for f in fb], fc, wb, bb, wc, bc, strides, nc)
     assert _hip.split_range_flag(reset=True)
+    fn = [f.clone() for f in fb]
+    fn[1][0, 5, 2, 3] = float("nan")
+    _hip.detect_head(fn, fc, wb, bb, wc, bc, strides, nc)
+    assert _hip.split_range_flag(reset=True)
+
+
+def test_sharded_predict_redoes_flagged_shard_on_exact_kernels(cuda):
+    """engine.predictor.sharded_predict (the bench's N > 1 step) reads the split-range flag after the rank-local
+    predict and redoes a flagged shard on the exact fp32 kernels before the exchange, as DetectionPredictor.__call__
+    does: with out-of-range Swin weights (64 W > 65504, flagged by the cached prepared block on every forward) its
+    detections equal the exact-fp32 run bit for bit. World size 1 over RCCL (one process, this GPU)."""
+    import socket
+
+    import torch.distributed as dist
+
+    from yolosod_amd.engine.predictor import DetectionPredictor, seeded_images, sharded_predict
+    from yolosod_amd.nn.tasks import build_model
+    m = build_model("yolov12-sod-fusion-v5-simple.yaml", seed=0, device=cuda)
+    with torch.no_grad():
+        m.model[28].window_attn.mlp[2].weight.mul_(2e4)  # the P2 SwinBlock (C = 64)
+    pred = DetectionPredictor(m, conf=0.001, iou=0.7, max_det=300)
+    x = seeded_images(0, 2, 256, device=cuda)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    det = torch.backends.cudnn.deterministic
+    torch.backends.cudnn.deterministic = True
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, device_id=cuda)
+    try:
+        _hip.split_range_flag(reset=True)
+        g_out, g_cnt, g_idx = sharded_predict(pred.predict_padded, 2, lambda lo, hi: x[lo:hi])
+        assert not _hip.split_range_flag(reset=True)  # the guard consumed (and cleared) the flag
+        with _hip.exact_fp32_matrix():
+            r_out, r_cnt, r_idx = pred.predict_padded(x)
+        _hip.split_range_flag(reset=True)
+    finally:
+        dist.destroy_process_group()
+        torch.backends.cudnn.deterministic = det
+    assert torch.isfinite(g_out).all()
+    assert torch.equal(g_cnt, r_cnt) and torch.equal(g_idx, r_idx)
+    assert torch.equal(g_out, r_out)

@@ -38,6 +38,15 @@ def scenes(seed: int, n: int, size: int) -> torch.Tensor:
     return torch.stack([scene(g, size) for _ in range(n)])
 
 
+def noisy_scenes(seed: int, n: int, size: int, sigma: float = 0.06) -> torch.Tensor:
+    """The rectangle scenes with per-pixel Gaussian noise on top (clamped to [0, 1]): no flat region is left, so no
+    two neighbouring anchors see identical receptive fields and their scores are never exactly tied in fp32 (the flat
+    scenes produce such ties, which any re-association can flip)."""
+    g = torch.Generator().manual_seed(seed)
+    x = torch.stack([scene(g, size) for _ in range(n)])
+    return (x + sigma * torch.randn(x.shape, generator=g)).clamp_(0.0, 1.0)
+
+
 def make_trained_like_checkpoint(path, cal_size: int = 320, cls_scale: float = 0.4, cls_shift: float = 2.0):
     from oracle.model_ref import REGISTRY
     from yolosod_amd.nn.checkpoint import save_checkpoint

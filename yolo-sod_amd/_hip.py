@@ -64,9 +64,9 @@ SIGNATURES = {
     "yolosod_cbam_forward_pre": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _vp, _sz, _vp]),
     "yolosod_conv1x1": (_i, [_vp, _l, _vp, _vp, _vp, _l, _vp, _l, _i, _i, _i, _l, _i, _vp]),
     "yolosod_debug_set_swin_fused": (None, [_i]),
-    "yolosod_debug_set_swin_x3": (None, [_i]),
-    "yolosod_debug_set_head_x2": (None, [_i]),
-    "yolosod_debug_set_a2_x2": (None, [_i]),
+    "yolosod_debug_set_swin_x3": (_i, [_i]),
+    "yolosod_debug_set_head_x2": (_i, [_i]),
+    "yolosod_debug_set_a2_x2": (_i, [_i]),
     "yolosod_debug_set_gemm_x2": (None, [_i]),
     "yolosod_debug_split_f16": (_i, [_vp, _vp, _vp, _l, _vp]),
     "yolosod_debug_set_gemmb_glds": (None, [_i]),
@@ -74,7 +74,10 @@ SIGNATURES = {
     "yolosod_split_range_flag": (_i, [_i, _vp]),
     "yolosod_swin_prepare": (_i, [_i, _i, _i] + [_vp] * 15 + [_f, _vp, _sz, _vp]),
     "yolosod_swin_forward_prepared": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _f, _vp, _f, _i, _vp, _vp, _sz,
-                                           _vp]),
+                                           _vp, _sz, _vp]),
+    "yolosod_swin_prepared_workspace": (_sz, [_i, _i, _i, _i, _i, _i, _i]),
+    "yolosod_init": (_i, [_i]),
+    "yolosod_debug_set_swin_split": (_i, [_i]),
     "yolosod_mamba_glu_workspace": (_sz, [_i, _i, _i, _i, _i, _i]),
     "yolosod_mamba_glu_forward": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _f, _vp, _vp,
                                        _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp, _vp, _vp, _f, _vp, _sz, _vp]),
@@ -173,10 +176,24 @@ class op_timer:
         return False
 
 
+_INIT_DEVS = set()
+
+
+def _init_device(dev) -> None:
+    """yolosod_init once per device: the library's device state (the split-range flag word) is allocated and zeroed
+    before the first launch there, never lazily inside a stream capture."""
+    idx = torch.device(dev).index
+    idx = torch.cuda.current_device() if idx is None else idx
+    if idx not in _INIT_DEVS:
+        _check(load_library().yolosod_init(int(idx)), "init")
+        _INIT_DEVS.add(idx)
+
+
 def _launch(key, dev, fn, *args):
     """Run one C-ABI launch sequence with ``dev`` (the operands' device) as the current HIP device; the stream
     argument inside ``args`` is that device's current stream (``_stream(dev)``). While an :class:`op_timer` is
     active, HIP events bracket the sequence on that stream."""
+    _init_device(dev)
     with torch.cuda.device(dev):
         t = _TIMER
         if t is None:
@@ -342,7 +359,8 @@ def swin_forward(x, num_heads, window, dw_w, ln1_w, ln1_b, ln1_eps, in_w, in_b, 
     if C % num_heads or (C // num_heads) not in ((32, 64, 128) if bf else (8, 16, 32, 64, 128)):
         raise RuntimeError(f"SwinBlock: head dim {C}/{num_heads} unsupported")
     key = ("swin", tuple(x.shape), (num_heads, window, hid)) + ((2,) if bf else ())
-    if prep is not None and not bf and wh == 7 and ww == 7 and swin_prep_bytes(C, num_heads, hid) > 0:
+    if (prep is not None and not bf and wh == 7 and ww == 7 and C * H * W < (1 << 30)
+            and swin_prep_bytes(C, num_heads, hid) > 0):
         # the weight split / folds were made once (``prep`` = swin_prepare of these parameters): one kernel launch
         return _launch(key, x.device, ops().swin_fwd_prepared, x, prep(), int(num_heads), int(window), dw_w,
                        float(ln1_eps), out_b, float(ln2_eps), int(hid), m2_b)
@@ -367,16 +385,18 @@ class exact_fp32_matrix:
     (Swin swin_fused / swin_wide, Detect head LDS kernel, A2 fp32 GEMMs) instead of the fp16 two-term splits - the
     fallback when split_range_flag() reports an operand outside fp16's range."""
 
+    _SWITCHES = ("yolosod_debug_set_swin_x3", "yolosod_debug_set_head_x2", "yolosod_debug_set_a2_x2")
+
     def __enter__(self):
         lib = load_library()
-        for f in ("yolosod_debug_set_swin_x3", "yolosod_debug_set_head_x2", "yolosod_debug_set_a2_x2"):
-            getattr(lib, f)(0)
+        # each switch returns its previous state, restored on exit (a user's YOLOSOD_*=0 or an outer setting stays)
+        self._prev = [int(getattr(lib, f)(0)) for f in self._SWITCHES]
         return self
 
     def __exit__(self, *exc):
         lib = load_library()
-        for f in ("yolosod_debug_set_swin_x3", "yolosod_debug_set_head_x2", "yolosod_debug_set_a2_x2"):
-            getattr(lib, f)(1)
+        for f, v in zip(self._SWITCHES, self._prev):
+            getattr(lib, f)(v)
         return False
 
 
@@ -448,15 +468,15 @@ def detect_head(box_feats, cls_feats, box_w, box_b, cls_w, cls_b, strides, nc, r
 
 def nms(pred, conf_thres, iou_thres, classes, agnostic, multi_label, max_det, max_nms, max_wh, in_place):
     """Batched NMS on pred [B, 4+nc, A] (GPU; torch.ops.yolosod.nms_batched). Returns (out [B,max_det,6],
-    counts [B] int32, index [B,max_det] int32)."""
+    counts [B] int32, index [B,max_det] int32). in_place: pred[:, :4] is rewritten to xyxy (the reference's
+    non_max_suppression(in_place=True)); otherwise pred is left untouched (no copy is made)."""
     B, no, A = _t(pred, "prediction").shape
-    if not in_place:
-        pred = pred.clone()
     cls = None
     if classes is not None:
         cls = torch.as_tensor(classes, dtype=torch.int32, device=pred.device).reshape(-1).contiguous()
     return _launch(("nms", (B, no - 4, A), int(multi_label)), pred.device, ops().nms_batched, pred, float(conf_thres),
-                   float(iou_thres), cls, bool(agnostic), bool(multi_label), int(max_det), int(max_nms), float(max_wh))
+                   float(iou_thres), cls, bool(agnostic), bool(multi_label), int(max_det), int(max_nms), float(max_wh),
+                   bool(in_place))
 
 
 def bias_act(y, bias, act, out=None, res=None, stats=None, out2=None, c2lo=0):

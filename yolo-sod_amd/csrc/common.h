@@ -219,10 +219,14 @@ __device__ __forceinline__ void split8(f32x4 a, f32x4 b, f16x8_t& h, f16x8_t& l)
 // kernel reports once at its end into a per-device flag word (range_flag_dev(); yolosod_split_range_flag reads it).
 // The flag makes a launch whose operands left the method's range visible, so the caller can redo it on the exact
 // fp32 kernels (DetectionPredictor does) instead of returning silent inf / NaN.
+// The running max is the IEEE 754-2019 maximum (v_maximum3_f32 on gfx950), which propagates a NaN operand: fmaxf
+// (maxNum) would return the non-NaN operand and lose it, so a NaN produced upstream (e.g. a Swin block fed to the Detect
+// head) would go unflagged. Same instruction count as the fmaxf form.
+__device__ __forceinline__ float nmax_(float a, float b) { return __builtin_elementwise_maximum(a, b); }
 __device__ __forceinline__ float range_acc(float m, f32x4 v) {
-  return fmaxf(fmaxf(m, fmaxf(fabsf(v.x), fabsf(v.y))), fmaxf(fabsf(v.z), fabsf(v.w)));
+  return nmax_(nmax_(m, nmax_(fabsf(v.x), fabsf(v.y))), nmax_(fabsf(v.z), fabsf(v.w)));
 }
-__device__ __forceinline__ float range_acc2(float m, f32x2 v) { return fmaxf(m, fmaxf(fabsf(v.x), fabsf(v.y))); }
+__device__ __forceinline__ float range_acc2(float m, f32x2 v) { return nmax_(m, nmax_(fabsf(v.x), fabsf(v.y))); }
 constexpr float SPLIT_RANGE = 65504.0f;  // largest finite fp16
 __device__ __forceinline__ void range_report(unsigned* flag, float m) {
   if (flag && !(m <= SPLIT_RANGE)) *flag = 1u;  // NaN inputs report too

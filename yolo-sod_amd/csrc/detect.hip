@@ -586,8 +586,19 @@ YS_EXPORT int yolosod_detect_decode(int nl, const float* const* maps, const int*
 }
 
 static int g_head_x2 = -1;  // head 1x1 convs: fp16-split matrix products (1, default) or exact fp32 MFMA (0)
+static bool head_x2_env() {
+  if (g_head_x2 < 0) {
+    const char* e = getenv("YOLOSOD_HEAD_X2");
+    g_head_x2 = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_head_x2 != 0;
+}
 // Test hook: route the Detect head through detect_head_x2_kernel (1) or detect_head_lds_kernel (0).
-YS_EXPORT void yolosod_debug_set_head_x2(int on) { g_head_x2 = on ? 1 : 0; }
+YS_EXPORT int yolosod_debug_set_head_x2(int on) {
+  const int prev = head_x2_env() ? 1 : 0;
+  g_head_x2 = on ? 1 : 0;
+  return prev;
+}
 
 static int detect_head_impl(int nl, const void* const* box_feat, const void* const* cls_feat, int c2, int c3,
                             const float* const* box_w, const float* const* box_b, const float* const* cls_w,
@@ -628,10 +639,7 @@ static int detect_head_impl(int nl, const void* const* box_feat, const void* con
   if (B == 0 || off == 0) return 0;
   const dim3 grid(blk, B);
   hipStream_t st = (hipStream_t)stream;
-  if (g_head_x2 < 0) {
-    const char* e = getenv("YOLOSOD_HEAD_X2");
-    g_head_x2 = (e && e[0] == '0') ? 0 : 1;
-  }
+  head_x2_env();
   if (bf16) {
     if (g_head_x2) {
       if (c3 == 64) hipLaunchKernelGGL((detect_head_x2_kernel<64, 64, NTS, bf16_t>), grid, dim3(256), 0, st, d);

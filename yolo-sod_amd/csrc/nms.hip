@@ -71,12 +71,16 @@ struct NmsArgs {
 
 __device__ __forceinline__ int block256_exclusive_scan(int v, int* wsum4, int* total);
 
-// also the candidate count of this 256-anchor block (the ordered compaction's per-block counts)
+// also the candidate count of this 256-anchor block (the ordered compaction's per-block counts). Only candidate
+// anchors' xyxy boxes are stored (every later reader indexes candidates), and the block's candidate masks only when
+// it has any (nms_scatter skips blocks whose count is 0): an image without candidates costs the read of its scores
+// plus the in-place rewrite the reference's in_place=True asks for.
 __global__ __launch_bounds__(256) void nms_prep_kernel(NmsArgs g) {
   __shared__ int wsum4[4];
   const int b = blockIdx.y;
   const int a = blockIdx.x * 256 + threadIdx.x;
   unsigned long long mask = 0ull;
+  float4 box = make_float4(0.f, 0.f, 0.f, 0.f);
   if (a < g.A) {
     float* pb = g.pred + (long)b * (4 + g.nc) * g.A + a;
     const long As = g.A;
@@ -89,7 +93,7 @@ __global__ __launch_bounds__(256) void nms_prep_kernel(NmsArgs g) {
       pb[2 * As] = x2;
       pb[3 * As] = y2;
     }
-    g.boxes[(long)b * g.A + a] = make_float4(x1, y1, x2, y2);
+    box = make_float4(x1, y1, x2, y2);
     float best = -INFINITY;
     int bj = 0;
     for (int j0 = 0; j0 < g.nc; j0 += 8) {  // 8 score loads in flight, then scanned in class order
@@ -118,11 +122,14 @@ __global__ __launch_bounds__(256) void nms_prep_kernel(NmsArgs g) {
       }
       mask &= allow;
     }
-    g.amask[(long)b * g.A + a] = mask;
   }
   int total;
   (void)block256_exclusive_scan(__popcll(mask), wsum4, &total);
   if (threadIdx.x == 0) g.blkcnt[(long)b * gridDim.x + blockIdx.x] = total;
+  if (total != 0 && a < g.A) {
+    g.amask[(long)b * g.A + a] = mask;
+    if (mask) g.boxes[(long)b * g.A + a] = box;
+  }
 }
 
 // block-wide (256 threads) exclusive scan; returns the exclusive prefix, *total gets the block sum
@@ -150,9 +157,10 @@ __global__ __launch_bounds__(256) void nms_scatter_kernel(NmsArgs g) {
   const int b = blockIdx.y;
   const long A = g.A;
   const long a = (long)blockIdx.x * 256 + threadIdx.x;
-  const unsigned long long m = (a < A) ? g.amask[(long)b * A + a] : 0ull;
   // this block's output offset: the candidates of the image's preceding blocks (their counts from nms_prep)
   const int* bc = g.blkcnt + (long)b * gridDim.x;
+  if (bc[blockIdx.x] == 0) return;  // no candidates here (nms_prep did not store this block's masks)
+  const unsigned long long m = (a < A) ? g.amask[(long)b * A + a] : 0ull;
   int before = 0;
   for (int i = threadIdx.x; i < (int)blockIdx.x; i += 256) before += bc[i];
   int base;

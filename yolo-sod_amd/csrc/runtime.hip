@@ -1,6 +1,7 @@
 // Library-wide runtime pieces of the C ABI: error reporting and version query.
 #include "common.h"
 #include <string.h>
+#include <mutex>
 
 namespace ys {
 static thread_local char g_err[1024] = {0};
@@ -15,20 +16,47 @@ void set_error(const char* fmt, ...) {
 YS_EXPORT const char* yolosod_last_error(void) { return ys::g_err; }
 
 namespace ys {
-// the split-range flag word of each device (common.h range_report)
-unsigned* range_flag_dev() {
-  static unsigned* flags[64] = {nullptr};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  if (!flags[dev]) {
+// the split-range flag word of each device (common.h range_report). yolosod_init(device) allocates and zeroes it
+// eagerly (the Python binding calls it once per device before the first launch, so no allocation or synchronous
+// memset happens inside a stream capture); a launch on a device that was never initialised allocates it here. The
+// table is guarded by a mutex, so concurrent first use from two threads allocates once.
+static std::mutex g_flag_mu;
+static unsigned* g_flags[64] = {nullptr};
+static unsigned* flag_alloc(int dev) {
+  std::lock_guard<std::mutex> lk(g_flag_mu);
+  if (!g_flags[dev]) {
     unsigned* p = nullptr;
     if (hipMalloc(&p, sizeof(unsigned)) != hipSuccess) return nullptr;
-    if (hipMemset(p, 0, sizeof(unsigned)) != hipSuccess) return nullptr;
-    flags[dev] = p;
+    if (hipMemset(p, 0, sizeof(unsigned)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+      (void)hipFree(p);
+      return nullptr;
+    }
+    g_flags[dev] = p;
   }
-  return flags[dev];
+  return g_flags[dev];
+}
+unsigned* range_flag_dev() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  unsigned* p = __atomic_load_n(&g_flags[dev], __ATOMIC_ACQUIRE);
+  return p ? p : flag_alloc(dev);
 }
 }  // namespace ys
+
+// Per-device initialisation of the library's device state (the split-range flag word); idempotent. Returns 0, or < 0
+// if the device cannot be selected or the allocation fails. The current device is restored.
+YS_EXPORT int yolosod_init(int device) {
+  int prev = 0;
+  YS_CHECK_ARG(device >= 0 && device < 64, "yolosod_init: device %d out of range", device);
+  if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(device) != hipSuccess) {
+    ys::set_error("yolosod_init: cannot select device %d", device);
+    return -1;
+  }
+  unsigned* p = ys::flag_alloc(device);
+  (void)hipSetDevice(prev);
+  YS_CHECK_ARG(p, "yolosod_init: flag allocation failed on device %d", device);
+  return 0;
+}
 
 // 1 if a split kernel on the current device has seen an operand outside the fp16 range (|v| > 65504 or NaN) since
 // the last reset, else 0; < 0 on error. Waits for the work queued on `stream` (the flag's producers) first.

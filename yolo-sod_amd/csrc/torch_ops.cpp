@@ -216,12 +216,16 @@ Tensor swin_fwd_prepared(const Tensor& x, const Tensor& prep, int64_t num_heads,
   TORCH_CHECK(bytes > 0 && (size_t)prep.numel() == bytes && prep.scalar_type() == at::kByte &&
                   prep.device() == x.device() && prep.is_contiguous(),
               "swin_fwd_prepared: prep must be the ", bytes, "-byte block of swin_prep on ", x.device());
+  TORCH_CHECK((int64_t)C * H * W < (1LL << 30), "swin_fwd_prepared: one image of ", C, "x", H, "x", W,
+              " is too large for the prepared kernels (use swin_fwd)");
   Tensor y = at::empty_like(x);
   auto st = c10::hip::getCurrentHIPStream(x.get_device());
+  Tensor ws = workspace(yolosod_swin_prepared_workspace(B, C, H, W, num_heads, window, hid), x);
   const int rc = yolosod_swin_forward_prepared(
       (const float*)x.data_ptr(), (float*)y.data_ptr(), B, C, H, W, num_heads, window,
       (const float*)par(dw_w, x, "dw.weight", 9LL * C), (float)ln1_eps, (const float*)par(out_b, x, "out_proj.bias", C),
-      (float)ln2_eps, hid, (const float*)par(m2_b, x, "mlp.2.bias", C), prep.data_ptr(), bytes, sp(st));
+      (float)ln2_eps, hid, (const float*)par(m2_b, x, "mlp.2.bias", C), prep.data_ptr(), bytes, ws.data_ptr(),
+      ws.numel(), sp(st));
   check_rc(rc, "swin_fwd_prepared");
   return y;
 }
@@ -345,7 +349,7 @@ Tensor detect_decode_fwd(at::TensorList maps, at::ArrayRef<double> strides, int6
 
 std::tuple<Tensor, Tensor, Tensor> nms_batched(const Tensor& pred, double conf_thres, double iou_thres,
                                                const c10::optional<Tensor>& classes, bool agnostic, bool multi_label,
-                                               int64_t max_det, int64_t max_nms, double max_wh) {
+                                               int64_t max_det, int64_t max_nms, double max_wh, bool in_place) {
   TORCH_CHECK(pred.is_cuda() && pred.scalar_type() == at::kFloat && pred.is_contiguous() && pred.dim() == 3,
               "nms_batched: prediction must be a contiguous float32 GPU tensor [B, 4+nc, A], got ", pred.sizes());
   c10::DeviceGuard guard(pred.device());
@@ -365,7 +369,7 @@ std::tuple<Tensor, Tensor, Tensor> nms_batched(const Tensor& pred, double conf_t
   }
   auto st = c10::hip::getCurrentHIPStream(pred.get_device());
   check_rc(yolosod_nms(pred.data_ptr<float>(), B, nc, A, (float)conf_thres, iou_thres, cls, ncls, agnostic, multi_label,
-                       max_det, max_nms, (float)max_wh, 1, out.data_ptr<float>(), counts.data_ptr<int>(),
+                       max_det, max_nms, (float)max_wh, in_place ? 1 : 0, out.data_ptr<float>(), counts.data_ptr<int>(),
                        index.data_ptr<int>(), ws.data_ptr(), ws.numel(), sp(st)),
            "nms_batched");
   return {out, counts, index};
@@ -396,7 +400,7 @@ TORCH_LIBRARY(yolosod, m) {
         "Tensor[] cls_b, float[] strides, int nc, int reg_max) -> Tensor");
   m.def("detect_decode_fwd(Tensor[] maps, float[] strides, int nc, int reg_max) -> Tensor");
   m.def("nms_batched(Tensor(a!) pred, float conf_thres, float iou_thres, Tensor? classes, bool agnostic, "
-        "bool multi_label, int max_det, int max_nms, float max_wh) -> (Tensor, Tensor, Tensor)");
+        "bool multi_label, int max_det, int max_nms, float max_wh, bool in_place=True) -> (Tensor, Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(yolosod, CUDA, m) {
@@ -441,7 +445,7 @@ TORCH_LIBRARY_IMPL(yolosod, Meta, m) {
     return at::empty({maps[0].size(0), 4 + nc, A}, maps[0].options().dtype(at::kFloat));
   });
   m.impl("nms_batched", [](const Tensor& pred, double, double, const c10::optional<Tensor>&, bool, bool,
-                           int64_t max_det, int64_t, double) {
+                           int64_t max_det, int64_t, double, bool) {
     const int64_t B = pred.size(0);
     auto f = pred.options();
     return std::make_tuple(at::empty({B, max_det, 6}, f), at::empty({B}, f.dtype(at::kInt)),

@@ -548,6 +548,7 @@ int yolosod_swin_wide_launch(const float* x, float* y, int B, int C, int H, int 
 
 bool yolosod_swin_x3_ok(int C, int num_heads, int wh, int ww, int mlp_hidden);
 size_t yolosod_swin_x3_workspace(int C, int mlp_hidden);
+size_t yolosod_swin_x3_run_workspace(int B, int C, int H, int W);
 int yolosod_swin_x3_launch(const float* x, float* y, int B, int C, int H, int W, int num_heads, int wh, int ww,
                            int nWx, int nWin,
                            const float* dw_w, const float* ln1_w, const float* ln1_b, float ln1_eps,
@@ -657,7 +658,7 @@ YS_EXPORT size_t yolosod_swin_workspace_v2(int B, int C, int H, int W, int num_h
     Sizer s;
     s.take<float>((size_t)C * 2);
     if (yolosod_swin_x3_ok(C, num_heads, g.wh, g.ww, mlp_hidden)) {
-      const size_t x3 = yolosod_swin_x3_workspace(C, mlp_hidden);
+      const size_t x3 = yolosod_swin_x3_workspace(C, mlp_hidden) + yolosod_swin_x3_run_workspace(B, C, H, W);
       return x3 > s.off ? x3 : s.off;
     }
     return s.off;
@@ -667,23 +668,44 @@ YS_EXPORT size_t yolosod_swin_workspace_v2(int B, int C, int H, int W, int num_h
 
 int yolosod_swin_x3_run(const float* x, float* y, int B, int C, int H, int W, int num_heads, int wh, int ww, int nWx,
                         int nWin, const float* dw_w, float ln1_eps, const float* out_proj_b, float ln2_eps,
-                        int mlp_hidden, const float* mlp2_b, const void* prep, size_t prep_bytes, hipStream_t st);
+                        int mlp_hidden, const float* mlp2_b, const void* prep, size_t prep_bytes, void* ws,
+                        size_t ws_bytes, hipStream_t st);
+
+// Scratch of yolosod_swin_forward_prepared for this shape (0 for shapes whose prepared kernels need none).
+YS_EXPORT size_t yolosod_swin_prepared_workspace(int B, int C, int H, int W, int num_heads, int window,
+                                                 int mlp_hidden) {
+  if (B <= 0 || C <= 0 || H <= 0 || W <= 0 || window <= 0) return 0;
+  SwinGeom g = swin_geom(B, H, W, window);
+  if (!yolosod_swin_x3_ok(C, num_heads, g.wh, g.ww, mlp_hidden)) return 0;
+  return yolosod_swin_x3_run_workspace(B, C, H, W);
+}
 
 // SwinBlock.forward on a prepared-parameter block (yolosod_swin_prepare): the shapes the fp16-split kernels take
-// (7x7 windows, yolosod_swin_prep_bytes > 0); anything else is an error (use yolosod_swin_forward).
+// (7x7 windows, yolosod_swin_prep_bytes > 0, one image's C*H*W < 2^30); anything else is an error (use
+// yolosod_swin_forward). The batch is walked in chunks of images whose window count stays below 2^31.
 YS_EXPORT int yolosod_swin_forward_prepared(const float* x, float* y, int B, int C, int H, int W, int num_heads,
                                             int window, const float* dw_w, float ln1_eps, const float* out_proj_b,
                                             float ln2_eps, int mlp_hidden, const float* mlp2_b, const void* prep,
-                                            size_t prep_bytes, void* stream) {
+                                            size_t prep_bytes, void* workspace, size_t workspace_bytes,
+                                            void* stream) {
   YS_CHECK_ARG(x && y && dw_w && out_proj_b && mlp2_b && prep, "swin_prepared: null pointer");
   YS_CHECK_ARG(B >= 0 && C > 0 && H > 0 && W > 0 && window > 0, "swin_prepared: bad shape");
   if (B == 0) return 0;
+  YS_CHECK_ARG((long)C * H * W < (1L << 30), "swin_prepared: one image of %dx%dx%d is too large for the prepared kernels",
+               C, H, W);
   SwinGeom g = swin_geom(B, H, W, window);
-  const int r = yolosod_swin_x3_run(x, y, B, C, H, W, num_heads, g.wh, g.ww, g.nWx, g.nWin, dw_w, ln1_eps, out_proj_b,
-                                    ln2_eps, mlp_hidden, mlp2_b, prep, prep_bytes, (hipStream_t)stream);
-  if (r < 0) return -1;
-  YS_CHECK_ARG(r == 1, "swin_prepared: shape C=%d heads=%d window %dx%d has no prepared-parameter kernel", C,
-               num_heads, g.wh, g.ww);
+  const long per = ((1L << 31) - 1) / (g.nWin > 0 ? g.nWin : 1);
+  const int bc = per < B ? (int)per : B;
+  const long img_el = (long)C * H * W;
+  for (int b0 = 0; b0 < B; b0 += bc) {
+    const int nb = B - b0 < bc ? B - b0 : bc;
+    const int r = yolosod_swin_x3_run(x + b0 * img_el, y + b0 * img_el, nb, C, H, W, num_heads, g.wh, g.ww, g.nWx,
+                                      g.nWin, dw_w, ln1_eps, out_proj_b, ln2_eps, mlp_hidden, mlp2_b, prep, prep_bytes,
+                                      workspace, workspace_bytes, (hipStream_t)stream);
+    if (r < 0) return -1;
+    YS_CHECK_ARG(r == 1, "swin_prepared: shape C=%d heads=%d window %dx%d has no prepared-parameter kernel", C,
+                 num_heads, g.wh, g.ww);
+  }
   return 0;
 }
 
@@ -793,7 +815,11 @@ static bool a2_x2() {
 }
 // Test hooks: A2 GEMMs as fp16 splits (1) or exact fp32 MFMA (0); every gemm_f32 call as fp16 splits (1) or as its
 // caller asks (0)
-YS_EXPORT void yolosod_debug_set_a2_x2(int on) { g_a2_x2 = on ? 1 : 0; }
+YS_EXPORT int yolosod_debug_set_a2_x2(int on) {
+  const int prev = a2_x2() ? 1 : 0;
+  g_a2_x2 = on ? 1 : 0;
+  return prev;
+}
 YS_EXPORT void yolosod_debug_set_gemm_x2(int on) { gemm_x2_forced() = on ? 1 : -1; }
 
 YS_EXPORT size_t yolosod_a2_workspace(int B, int C, int H, int W, int num_areas) {
