@@ -60,6 +60,19 @@ int yolosod_a2_forward(const float* x, float* y, int B, int C, int H, int W, int
                        const float* in_proj_w, const float* in_proj_b, const float* mha_out_w,
                        const float* mha_out_b, const float* oproj_w, const float* oproj_b, void* workspace,
                        size_t workspace_bytes, void* stream);
+/* The fused LN -> QKV -> attention kernel of the fp16-split path (csrc/a2_fused.hip; head dim 64, areas * W <= 160)
+ * takes the in_proj weights prepared once: yolosod_a2_prep_bytes (0 = the shape does not take the fused kernel),
+ * yolosod_a2_prepare (in_proj with the LayerNorm affine folded, split into fp16 planes; re-run when layer_norm /
+ * in_proj change), yolosod_a2_forward_prepared (the forward of yolosod_a2_forward with the pre-multiplied output
+ * weights, on that block; the workspace is yolosod_a2_workspace). yolosod_a2_forward prepares per call instead. */
+size_t yolosod_a2_prep_bytes(int C, int num_heads, int num_areas, int W);
+int yolosod_a2_prepare(int C, const float* ln_w, const float* ln_b, const float* in_proj_w, const float* in_proj_b,
+                       void* prep, size_t prep_bytes, void* stream);
+int yolosod_a2_forward_prepared(const float* x, float* y, int B, int C, int H, int W, int num_areas, int num_heads,
+                                const float* proj_w, const float* proj_b, const float* ln_w, const float* ln_b,
+                                float ln_eps, const float* in_proj_w, const float* in_proj_b, const float* oproj_w,
+                                const float* oproj_b, const void* prep, size_t prep_bytes, void* workspace,
+                                size_t workspace_bytes, void* stream);
 
 /* SwinBlock.forward                ultralytics/nn/modules/blocks_transformer.py:150-171 (WindowAttention
  * :100-131, window_partition :8-47, window_reverse :49-79).  dw: [C,1,3,3]; in_proj [3C,C]; mlp1 [hid,C];

@@ -76,6 +76,10 @@ SIGNATURES = {
     "yolosod_swin_forward_prepared": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _f, _vp, _f, _i, _vp, _vp, _sz,
                                            _vp, _sz, _vp]),
     "yolosod_swin_prepared_workspace": (_sz, [_i, _i, _i, _i, _i, _i, _i]),
+    "yolosod_a2_prep_bytes": (_sz, [_i, _i, _i, _i]),
+    "yolosod_a2_prepare": (_i, [_i, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "yolosod_a2_forward_prepared": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp,
+                                         _vp, _vp, _sz, _vp, _sz, _vp]),
     "yolosod_init": (_i, [_i]),
     "yolosod_debug_set_swin_split": (_i, [_i]),
     "yolosod_mamba_glu_workspace": (_sz, [_i, _i, _i, _i, _i, _i]),
@@ -328,19 +332,34 @@ def ca_forward(x, conv1_w, conv1_b, bn_w, bn_b, bn_mean, bn_var, bn_eps, convh_w
                    bn_w, bn_b, bn_mean, bn_var, float(bn_eps), convh_w, convh_b, convw_w, convw_b, yin)
 
 
-def a2_forward(x, num_areas, num_heads, proj_w, proj_b, ln_w, ln_b, ln_eps, in_w, in_b, mo_w, mo_b, op_w, op_b):
+def a2_prep_bytes(C, num_heads, num_areas, W) -> int:
+    """Size of the fused LN / QKV / attention kernel's prepared block (0: the shape does not take that kernel)."""
+    return int(load_library().yolosod_a2_prep_bytes(int(C), int(num_heads), int(num_areas), int(W)))
+
+
+def a2_prepare(x, num_areas, num_heads, ln_w, ln_b, in_w, in_b):
+    """The prepared in_proj block (uint8 tensor on x's device) for a2_forward(..., prep=...)."""
+    return ops().a2_prep(x, int(num_areas), int(num_heads), ln_w, ln_b, in_w, in_b)
+
+
+def a2_forward(x, num_areas, num_heads, proj_w, proj_b, ln_w, ln_b, ln_eps, in_w, in_b, mo_w, mo_b, op_w, op_b,
+               prep=None):
     """A2_Attn -> torch.ops.yolosod.a2_fwd. mo_w = mo_b = None: op_w / op_b are the pre-multiplied MHA-out x
     output-conv weights (A2_Attn._fused_out). bf16 activations: proj_w / in_w / op_w bf16 (pre-multiplied form
-    only), biases and LN fp32."""
+    only), biases and LN fp32. ``prep``: a callable returning the cached prepared block (a2_prepare) - used when the
+    shape takes the fused LN / QKV / attention kernel (fp32)."""
     bf = _act_dtype(_t(x, "x"))
     B, C, H, W = x.shape
     if num_areas * W > 320:
         raise RuntimeError(f"A2_Attn: sequence length {num_areas * W} > 320 unsupported")
     if bf and (C // num_heads not in (32, 64, 128) or C % 64):
         raise RuntimeError(f"A2_Attn (bf16): C={C} with head dim {C // num_heads} unsupported")
+    pblk = None
+    if prep is not None and not bf and mo_w is None and a2_prep_bytes(C, num_heads, num_areas, W) > 0:
+        pblk = prep()
     return _launch(("a2", tuple(x.shape), (num_areas, num_heads)) + ((2,) if bf else ()), x.device, ops().a2_fwd, x,
                    int(num_areas), int(num_heads), proj_w, proj_b, ln_w, ln_b, float(ln_eps), in_w, in_b, mo_w, mo_b,
-                   op_w, op_b)
+                   op_w, op_b, pblk)
 
 
 def swin_forward(x, num_heads, window, dw_w, ln1_w, ln1_b, ln1_eps, in_w, in_b, out_w, out_b, ln2_w, ln2_b,

@@ -142,10 +142,29 @@ Tensor ca_fwd(const Tensor& x, const Tensor& conv1_w, const Tensor& conv1_b, con
   return y;
 }
 
+// A2's fused LN / QKV / attention kernel's prepared in_proj weights (yolosod_a2_prepare) as a uint8 tensor, made
+// once per parameter version by the caller (nn/modules.A2_Attn caches it) and passed to a2_fwd.
+Tensor a2_prep(const Tensor& x, int64_t num_areas, int64_t num_heads, const Tensor& ln_w, const Tensor& ln_b,
+               const Tensor& in_w, const Tensor& in_b) {
+  TORCH_CHECK(!act_bf16(x, "a2_prep"), "a2_prep: the prepared path is the fp32 config's");
+  c10::DeviceGuard guard(x.device());
+  const int C = x.size(1), W = x.size(3);
+  const size_t bytes = yolosod_a2_prep_bytes(C, num_heads, num_areas, W);
+  TORCH_CHECK(bytes > 0, "a2_prep: C=", C, " heads=", num_heads, " L=", num_areas * W, " has no fused kernel");
+  Tensor prep = at::empty({(int64_t)bytes}, x.options().dtype(at::kByte));
+  auto st = c10::hip::getCurrentHIPStream(x.get_device());
+  check_rc(yolosod_a2_prepare(C, (const float*)par(ln_w, x, "layer_norm.weight", C),
+                              (const float*)par(ln_b, x, "layer_norm.bias", C),
+                              (const float*)par(in_w, x, "in_proj_weight", 3LL * C * C),
+                              (const float*)par(in_b, x, "in_proj_bias", 3 * C), prep.data_ptr(), bytes, sp(st)),
+           "a2_prep");
+  return prep;
+}
+
 Tensor a2_fwd(const Tensor& x, int64_t num_areas, int64_t num_heads, const Tensor& proj_w, const Tensor& proj_b,
               const Tensor& ln_w, const Tensor& ln_b, double ln_eps, const Tensor& in_w, const Tensor& in_b,
               const c10::optional<Tensor>& mo_w, const c10::optional<Tensor>& mo_b, const Tensor& op_w,
-              const Tensor& op_b) {
+              const Tensor& op_b, const c10::optional<Tensor>& prep) {
   const bool bf = act_bf16(x, "a2_fwd");
   c10::DeviceGuard guard(x.device());
   const int B = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
@@ -173,9 +192,20 @@ Tensor a2_fwd(const Tensor& x, int64_t num_areas, int64_t num_heads, const Tenso
     Tensor ws = workspace(yolosod_a2_workspace(B, C, H, W, num_areas), x);
     const float* mw = mo_w ? (const float*)par(*mo_w, x, "attention.out_proj.weight", (int64_t)C * C) : nullptr;
     const float* mb = mo_b ? (const float*)par(*mo_b, x, "attention.out_proj.bias", C) : nullptr;
-    rc = yolosod_a2_forward((const float*)x.data_ptr(), (float*)y.data_ptr(), B, C, H, W, num_areas, num_heads,
-                            (const float*)pw, pb, lw, lb, (float)ln_eps, (const float*)iw, ib, mw, mb,
-                            (const float*)ow, ob, ws.data_ptr(), ws.numel(), sp(st));
+    const size_t pbytes = yolosod_a2_prep_bytes(C, num_heads, num_areas, W);
+    if (prep && pbytes > 0 && !mo_w) {
+      TORCH_CHECK((size_t)prep->numel() == pbytes && prep->scalar_type() == at::kByte && prep->device() == x.device() &&
+                      prep->is_contiguous(),
+                  "a2_fwd: prep must be the ", pbytes, "-byte block of a2_prep on ", x.device());
+      rc = yolosod_a2_forward_prepared((const float*)x.data_ptr(), (float*)y.data_ptr(), B, C, H, W, num_areas,
+                                       num_heads, (const float*)pw, pb, lw, lb, (float)ln_eps, (const float*)iw, ib,
+                                       (const float*)ow, ob, prep->data_ptr(), pbytes, ws.data_ptr(), ws.numel(),
+                                       sp(st));
+    } else {
+      rc = yolosod_a2_forward((const float*)x.data_ptr(), (float*)y.data_ptr(), B, C, H, W, num_areas, num_heads,
+                              (const float*)pw, pb, lw, lb, (float)ln_eps, (const float*)iw, ib, mw, mb,
+                              (const float*)ow, ob, ws.data_ptr(), ws.numel(), sp(st));
+    }
   }
   check_rc(rc, "a2_fwd");
   return y;
@@ -386,7 +416,10 @@ TORCH_LIBRARY(yolosod, m) {
   m.def("ca_fwd(Tensor x, Tensor conv1_w, Tensor conv1_b, Tensor bn_w, Tensor bn_b, Tensor bn_mean, Tensor bn_var, "
         "float bn_eps, Tensor convh_w, Tensor convh_b, Tensor convw_w, Tensor convw_b, Tensor? yin) -> Tensor");
   m.def("a2_fwd(Tensor x, int num_areas, int num_heads, Tensor proj_w, Tensor proj_b, Tensor ln_w, Tensor ln_b, "
-        "float ln_eps, Tensor in_w, Tensor in_b, Tensor? mo_w, Tensor? mo_b, Tensor op_w, Tensor op_b) -> Tensor");
+        "float ln_eps, Tensor in_w, Tensor in_b, Tensor? mo_w, Tensor? mo_b, Tensor op_w, Tensor op_b, "
+        "Tensor? prep=None) -> Tensor");
+  m.def("a2_prep(Tensor x, int num_areas, int num_heads, Tensor ln_w, Tensor ln_b, Tensor in_w, Tensor in_b) -> "
+        "Tensor");
   m.def("swin_fwd(Tensor x, int num_heads, int window, Tensor dw_w, Tensor ln1_w, Tensor ln1_b, float ln1_eps, "
         "Tensor in_w, Tensor in_b, Tensor out_w, Tensor out_b, Tensor ln2_w, Tensor ln2_b, float ln2_eps, "
         "Tensor m1_w, Tensor m1_b, Tensor m2_w, Tensor m2_b, Tensor pw_w, Tensor bn_w, Tensor bn_b, Tensor bn_mean, "
@@ -408,6 +441,7 @@ TORCH_LIBRARY_IMPL(yolosod, CUDA, m) {
   m.impl("cbam_fwd", cbam_fwd);
   m.impl("ca_fwd", ca_fwd);
   m.impl("a2_fwd", a2_fwd);
+  m.impl("a2_prep", a2_prep);
   m.impl("swin_fwd", swin_fwd);
   m.impl("swin_prep", swin_prep);
   m.impl("swin_fwd_prepared", swin_fwd_prepared);
@@ -426,7 +460,7 @@ TORCH_LIBRARY_IMPL(yolosod, Meta, m) {
                       const c10::optional<Tensor>&) { return mafn_meta(x); });
   m.impl("a2_fwd", [](const Tensor& x, int64_t, int64_t, const Tensor&, const Tensor&, const Tensor&, const Tensor&,
                       double, const Tensor&, const Tensor&, const c10::optional<Tensor>&, const c10::optional<Tensor>&,
-                      const Tensor&, const Tensor&) { return mafn_meta(x); });
+                      const Tensor&, const Tensor&, const c10::optional<Tensor>&) { return mafn_meta(x); });
   m.impl("swin_fwd", [](const Tensor& x, int64_t, int64_t, const Tensor&, const Tensor&, const Tensor&, double,
                         const Tensor&, const Tensor&, const Tensor&, const Tensor&, const Tensor&, const Tensor&, double,
                         const Tensor&, const Tensor&, const Tensor&, const Tensor&, const Tensor&, const Tensor&,

@@ -822,23 +822,74 @@ YS_EXPORT int yolosod_debug_set_a2_x2(int on) {
 }
 YS_EXPORT void yolosod_debug_set_gemm_x2(int on) { gemm_x2_forced() = on ? 1 : -1; }
 
+bool yolosod_a2_fused_ok(int C, int num_heads, int L);
+size_t yolosod_a2_fused_prep_bytes(int C);
+int yolosod_a2_fused_prepare(int C, const float* ln_w, const float* ln_b, const float* in_w, const float* in_b,
+                             void* prep, size_t prep_bytes, hipStream_t st);
+int yolosod_a2_fused_run(const float* S, const float* stats, float* O, int B, int L, int C, int num_heads,
+                         const void* prep, size_t prep_bytes, hipStream_t st);
+
 YS_EXPORT size_t yolosod_a2_workspace(int B, int C, int H, int W, int num_areas) {
   const long ntok = (long)B * num_areas * W;
   Sizer s;
   s.take<float>((size_t)B * C * H * W);  // proj output
   s.take<float>((size_t)ntok * C);       // S
   s.take<float>((size_t)ntok * C);       // U / O
-  s.take<float>((size_t)ntok * 3 * C);   // QKV
+  s.take<float>((size_t)ntok * 3 * C);   // QKV (decomposed path)
   s.take<float>((size_t)ntok * C);       // Z
   s.take<float>((size_t)ntok * 2);       // LayerNorm row statistics
+  s.take<char>(yolosod_a2_fused_prep_bytes(C));  // per-call weight preparation of the fused LN / QKV / attention kernel
   return s.off;
 }
+
+// Size of the prepared-parameter block of the fused LN / QKV / attention kernel (0: the shape does not take it).
+YS_EXPORT size_t yolosod_a2_prep_bytes(int C, int num_heads, int num_areas, int W) {
+  return yolosod_a2_fused_ok(C, num_heads, num_areas * W) ? yolosod_a2_fused_prep_bytes(C) : 0;
+}
+
+// Weight preparation for yolosod_a2_forward_prepared: in_proj with the LayerNorm affine folded, split into fp16
+// planes; re-run whenever layer_norm / in_proj parameters change.
+YS_EXPORT int yolosod_a2_prepare(int C, const float* ln_w, const float* ln_b, const float* in_proj_w,
+                                 const float* in_proj_b, void* prep, size_t prep_bytes, void* stream) {
+  YS_CHECK_ARG(ln_w && ln_b && in_proj_w && in_proj_b && prep, "a2_prepare: null pointer");
+  YS_CHECK_ARG(C > 0 && C % 64 == 0 && C <= 1024, "a2_prepare: C=%d unsupported", C);
+  return yolosod_a2_fused_prepare(C, ln_w, ln_b, in_proj_w, in_proj_b, prep, prep_bytes, (hipStream_t)stream);
+}
+
+static int a2_forward_impl(const float* x, float* y, int B, int C, int H, int W, int num_areas, int num_heads,
+                           const float* proj_w, const float* proj_b, const float* ln_w, const float* ln_b,
+                           float ln_eps, const float* in_proj_w, const float* in_proj_b, const float* mha_out_w,
+                           const float* mha_out_b, const float* oproj_w, const float* oproj_b, const void* prep,
+                           size_t prep_bytes, void* workspace, size_t workspace_bytes, hipStream_t st);
 
 YS_EXPORT int yolosod_a2_forward(const float* x, float* y, int B, int C, int H, int W, int num_areas, int num_heads,
                                  const float* proj_w, const float* proj_b, const float* ln_w, const float* ln_b,
                                  float ln_eps, const float* in_proj_w, const float* in_proj_b,
                                  const float* mha_out_w, const float* mha_out_b, const float* oproj_w,
                                  const float* oproj_b, void* workspace, size_t workspace_bytes, void* stream) {
+  return a2_forward_impl(x, y, B, C, H, W, num_areas, num_heads, proj_w, proj_b, ln_w, ln_b, ln_eps, in_proj_w,
+                         in_proj_b, mha_out_w, mha_out_b, oproj_w, oproj_b, nullptr, 0, workspace, workspace_bytes,
+                         (hipStream_t)stream);
+}
+
+// The same forward on a prepared block (yolosod_a2_prepare of these LN / in_proj parameters) kept by the caller.
+YS_EXPORT int yolosod_a2_forward_prepared(const float* x, float* y, int B, int C, int H, int W, int num_areas,
+                                          int num_heads, const float* proj_w, const float* proj_b, const float* ln_w,
+                                          const float* ln_b, float ln_eps, const float* in_proj_w,
+                                          const float* in_proj_b, const float* oproj_w, const float* oproj_b,
+                                          const void* prep, size_t prep_bytes, void* workspace,
+                                          size_t workspace_bytes, void* stream) {
+  YS_CHECK_ARG(prep, "a2_prepared: null prepared block");
+  return a2_forward_impl(x, y, B, C, H, W, num_areas, num_heads, proj_w, proj_b, ln_w, ln_b, ln_eps, in_proj_w,
+                         in_proj_b, nullptr, nullptr, oproj_w, oproj_b, prep, prep_bytes, workspace, workspace_bytes,
+                         (hipStream_t)stream);
+}
+
+static int a2_forward_impl(const float* x, float* y, int B, int C, int H, int W, int num_areas, int num_heads,
+                           const float* proj_w, const float* proj_b, const float* ln_w, const float* ln_b,
+                           float ln_eps, const float* in_proj_w, const float* in_proj_b, const float* mha_out_w,
+                           const float* mha_out_b, const float* oproj_w, const float* oproj_b, const void* prep,
+                           size_t prep_bytes, void* workspace, size_t workspace_bytes, hipStream_t st) {
   YS_CHECK_ARG(x && y && proj_w && proj_b && ln_w && ln_b && in_proj_w && in_proj_b && oproj_w && oproj_b &&
                    (mha_out_w != nullptr) == (mha_out_b != nullptr),
                "a2: null pointer");
@@ -846,7 +897,6 @@ YS_EXPORT int yolosod_a2_forward(const float* x, float* y, int B, int C, int H, 
   YS_CHECK_ARG(B >= 0 && C > 0 && H > 0 && W > 0 && num_areas > 0, "a2: bad shape");
   YS_CHECK_ARG(C % 32 == 0, "a2: C must be a multiple of 32");
   if (B == 0) return 0;
-  hipStream_t st = (hipStream_t)stream;
   const int A = num_areas;
   const long HW = (long)H * W;
   const long ntok = (long)B * A * W;
@@ -857,7 +907,9 @@ YS_EXPORT int yolosod_a2_forward(const float* x, float* y, int B, int C, int H, 
   float* Q = cv.take<float>((size_t)ntok * 3 * C);
   float* Z = cv.take<float>((size_t)ntok * C);
   float* lns = cv.take<float>((size_t)ntok * 2);
-  YS_CHECK_ARG(lns, "a2: workspace too small (%zu)", workspace_bytes);
+  const size_t fpb = yolosod_a2_fused_prep_bytes(C);
+  char* fprep = cv.take<char>(fpb);
+  YS_CHECK_ARG(fprep, "a2: workspace too small (%zu)", workspace_bytes);
   int rc;
   // XP = SiLU(Wp x + bp)  (Conv with folded BN, a2_attn.py:39): M = Cout, N = HW, batched over images
   GemmArgs ga{};
@@ -872,14 +924,25 @@ YS_EXPORT int yolosod_a2_forward(const float* x, float* y, int B, int C, int H, 
                      st, XP, S, C, H, W, A);
   YS_CHECK_LAUNCH("a2_pool");
   ga = GemmArgs{};
-  // LN(S) -> U once (U is free until the attention writes it), then the QKV GEMM without an LN prologue
-  if ((rc = launch_ln_rows(S, C, ntok, C, ln_eps, ln_w, ln_b, U, C, st))) return rc;
-  ga.A = U; ga.lda = C; ga.B = in_proj_w; ga.ldb = C; ga.M = (int)ntok; ga.N = 3 * C; ga.K = C;
-  ga.epi = epi_plain(Q, 0, 3 * C);
-  ga.epi.bias = in_proj_b; ga.epi.bias_mode = 2;
-  ga.x2 = x2; ga.x2_sb = 64.f;
-  if ((rc = launch_gemm(ga, 1, true, st))) return rc;
-  if ((rc = launch_attention(Q, U, B, A * W, C, num_heads, st))) return rc;
+  if (x2 && yolosod_a2_fused_ok(C, num_heads, A * W)) {
+    // LN -> QKV -> attention per (image, head) in one kernel (a2_fused.hip): S + row statistics -> U
+    if (!prep) {
+      if ((rc = yolosod_a2_fused_prepare(C, ln_w, ln_b, in_proj_w, in_proj_b, fprep, fpb, st))) return rc;
+      prep = fprep;
+      prep_bytes = fpb;
+    }
+    if ((rc = launch_row_stats(S, C, ntok, C, ln_eps, lns, st))) return rc;
+    if ((rc = yolosod_a2_fused_run(S, lns, U, B, A * W, C, num_heads, prep, prep_bytes, st))) return rc;
+  } else {
+    // LN(S) -> U once (U is free until the attention writes it), then the QKV GEMM without an LN prologue
+    if ((rc = launch_ln_rows(S, C, ntok, C, ln_eps, ln_w, ln_b, U, C, st))) return rc;
+    ga.A = U; ga.lda = C; ga.B = in_proj_w; ga.ldb = C; ga.M = (int)ntok; ga.N = 3 * C; ga.K = C;
+    ga.epi = epi_plain(Q, 0, 3 * C);
+    ga.epi.bias = in_proj_b; ga.epi.bias_mode = 2;
+    ga.x2 = x2; ga.x2_sb = 64.f;
+    if ((rc = launch_gemm(ga, 1, true, st))) return rc;
+    if ((rc = launch_attention(Q, U, B, A * W, C, num_heads, st))) return rc;
+  }
   if (!premul) {
     ga = GemmArgs{};
     ga.A = U; ga.lda = C; ga.B = mha_out_w; ga.ldb = C; ga.M = (int)ntok; ga.N = C; ga.K = C;

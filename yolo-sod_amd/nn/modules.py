@@ -422,8 +422,12 @@ class A2_Attn(nn.Module):
         dt = x.dtype
         pw, at_w, fw = _as(self, "w", dt, pw, at.in_proj_weight, fw)
         pb, lw, lb, at_b, fb = _f32(self, "b", pb, self.layer_norm.weight, self.layer_norm.bias, at.in_proj_bias, fb)
+        srcs = (self.layer_norm.weight, self.layer_norm.bias, at.in_proj_weight, at.in_proj_bias)
+        # the fused LN / QKV / attention kernel's weight split with the LN affine folded, once per parameter version
+        prep = lambda: _cached(self, "a2prep", srcs, lambda: _hip.a2_prepare(  # noqa: E731
+            x, self.num_areas, self.num_heads, lw, lb, at_w, at_b))
         return _hip.a2_forward(x, self.num_areas, self.num_heads, pw, pb, lw, lb, self.layer_norm.eps, at_w, at_b,
-                               None, None, fw, fb)
+                               None, None, fw, fb, prep=prep)
 
     def _fused_out(self):
         """MHA out-projection (a2_attn.py:53) and the output 1x1 conv (a2_attn.py:63) are consecutive linear maps
