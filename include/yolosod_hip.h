@@ -61,13 +61,13 @@ int yolosod_a2_forward(const float* x, float* y, int B, int C, int H, int W, int
                        const float* mha_out_b, const float* oproj_w, const float* oproj_b, void* workspace,
                        size_t workspace_bytes, void* stream);
 /* The fused LN -> QKV -> attention kernel of the fp16-split path (csrc/a2_fused.hip; head dim 64, areas * W <= 160)
- * takes the in_proj weights prepared once: yolosod_a2_prep_bytes (0 = the shape does not take the fused kernel),
- * yolosod_a2_prepare (in_proj with the LayerNorm affine folded, split into fp16 planes; re-run when layer_norm /
- * in_proj change), yolosod_a2_forward_prepared (the forward of yolosod_a2_forward with the pre-multiplied output
+ * and the proj + SiLU + pooling kernel (H*W <= 400) take the weights prepared once: yolosod_a2_prep_bytes (0 = the
+ * shape does not take the fused kernels), yolosod_a2_prepare (in_proj with the LayerNorm affine folded and the
+ * BN-folded proj conv, split into fp16 planes; re-run when one of them changes), yolosod_a2_forward_prepared (the forward of yolosod_a2_forward with the pre-multiplied output
  * weights, on that block; the workspace is yolosod_a2_workspace). yolosod_a2_forward prepares per call instead. */
 size_t yolosod_a2_prep_bytes(int C, int num_heads, int num_areas, int W);
-int yolosod_a2_prepare(int C, const float* ln_w, const float* ln_b, const float* in_proj_w, const float* in_proj_b,
-                       void* prep, size_t prep_bytes, void* stream);
+int yolosod_a2_prepare(int C, const float* proj_w, const float* ln_w, const float* ln_b, const float* in_proj_w,
+                       const float* in_proj_b, void* prep, size_t prep_bytes, void* stream);
 int yolosod_a2_forward_prepared(const float* x, float* y, int B, int C, int H, int W, int num_areas, int num_heads,
                                 const float* proj_w, const float* proj_b, const float* ln_w, const float* ln_b,
                                 float ln_eps, const float* in_proj_w, const float* in_proj_b, const float* oproj_w,
@@ -242,6 +242,9 @@ int yolosod_debug_set_head_x2(int on);
  * turns it off) or exact fp32 MFMA (0); yolosod_debug_set_gemm_x2(1) makes every yolosod_gemm_f32 / internal fp32 GEMM
  * call take the split products, 0 restores the callers' choice. */
 int yolosod_debug_set_a2_x2(int on);
+/* Test hook: A2_Attn's split path through the fused kernels (1, default; env YOLOSOD_A2_FUSED=0 turns it off:
+ * proj + SiLU + pooling, then LN + QKV + attention, csrc/a2_fused.hip) or the decomposed GEMM path (0). */
+int yolosod_debug_set_a2_fused(int on);
 void yolosod_debug_set_gemm_x2(int on);
 /* Test hook: the fp16 two-term split of the fp32-accurate matrix kernels (common.h split2) on npair pairs of v:
  * h[i] = the fp16 pair (fp16(v[2i]), fp16(v[2i+1])), l[i] = (fp16(v[2i] - h.lo), fp16(v[2i+1] - h.hi)), as 2 x 16-bit

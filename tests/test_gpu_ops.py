@@ -144,6 +144,35 @@ def test_swin_c64_split_and_one_kernel_forms(name, split, cuda, monkeypatch):
     assert ok, f"{name} split={split}: vs fp64 oracle max abs err {err:.3g} (ratio {ratio:.2f})"
 
 
+A2_FUSED_SHAPES = {  # A2_Attn through both forms of its fp16-split path
+    "a2_c512_h20": None, "a2_c128_h16": None,
+    "a2_L12": REAL["a2_L12"],
+    "a2_b3_c256_12x8": ("A2_Attn", (256, None, 8, 4), (3, 256, 12, 8)),   # L = 64, 96 pixels, 4 heads
+    "a2_b2_c192_10x20": ("A2_Attn", (192, None, 4, 3), (2, 192, 10, 20)),  # 4 areas of 3 rows, overlapping bins
+    "a2_L12_1280": REAL["a2_L12_1280"],  # L = 320: the decomposed path in both forms
+}
+
+
+@pytest.mark.parametrize("fused", [0, 1], ids=["decomposed", "fused"])
+@pytest.mark.parametrize("name", list(A2_FUSED_SHAPES))
+def test_a2_fused_and_decomposed_forms(name, fused, cuda, monkeypatch):
+    """A2_Attn's split path as the fused kernels (a2_fused.hip: proj + SiLU + row pooling, then LN + QKV + attention
+    per (image, head); the default) and as the decomposed GEMM path (YOLOSOD_A2_FUSED=0), against the fp64 oracle."""
+    lib = _hip.load_library()
+    if A2_FUSED_SHAPES[name] is not None:
+        monkeypatch.setitem(recipes.OPS, name, A2_FUSED_SHAPES[name])
+    m, _ = build_fixture_module(name)
+    x = recipes.make_input(name, recipes.OPS[name][2])
+    prev = lib.yolosod_debug_set_a2_fused(fused)
+    try:
+        with torch.inference_mode():
+            y = m.to(cuda)(x.to(cuda)).cpu()
+    finally:
+        lib.yolosod_debug_set_a2_fused(prev)
+    ok, err, ratio = tol_close(y, _oracle64(name, x), 5e-5, 1e-4)
+    assert ok, f"{name} fused={fused}: vs fp64 oracle max abs err {err:.3g} (ratio {ratio:.2f})"
+
+
 @pytest.mark.parametrize("name,shape", [("se_c32_r64", (9, 32, 64, 64)), ("se_c64_r4_odd", (5, 64, 9, 7)),
                                         ("cbam_c64", (9, 64, 48, 40)), ("cbam_c32_odd", (5, 32, 13, 11)),
                                         ("ca_c128", (9, 128, 24, 20)), ("ca_c64_odd", (5, 64, 9, 7))])

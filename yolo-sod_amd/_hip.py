@@ -77,11 +77,12 @@ SIGNATURES = {
                                            _vp, _sz, _vp]),
     "yolosod_swin_prepared_workspace": (_sz, [_i, _i, _i, _i, _i, _i, _i]),
     "yolosod_a2_prep_bytes": (_sz, [_i, _i, _i, _i]),
-    "yolosod_a2_prepare": (_i, [_i, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "yolosod_a2_prepare": (_i, [_i, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "yolosod_a2_forward_prepared": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp,
                                          _vp, _vp, _sz, _vp, _sz, _vp]),
     "yolosod_init": (_i, [_i]),
     "yolosod_debug_set_swin_split": (_i, [_i]),
+    "yolosod_debug_set_a2_fused": (_i, [_i]),
     "yolosod_mamba_glu_workspace": (_sz, [_i, _i, _i, _i, _i, _i]),
     "yolosod_mamba_glu_forward": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _f, _vp, _vp,
                                        _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp, _vp, _vp, _f, _vp, _sz, _vp]),
@@ -337,9 +338,9 @@ def a2_prep_bytes(C, num_heads, num_areas, W) -> int:
     return int(load_library().yolosod_a2_prep_bytes(int(C), int(num_heads), int(num_areas), int(W)))
 
 
-def a2_prepare(x, num_areas, num_heads, ln_w, ln_b, in_w, in_b):
-    """The prepared in_proj block (uint8 tensor on x's device) for a2_forward(..., prep=...)."""
-    return ops().a2_prep(x, int(num_areas), int(num_heads), ln_w, ln_b, in_w, in_b)
+def a2_prepare(x, num_areas, num_heads, proj_w, ln_w, ln_b, in_w, in_b):
+    """The prepared block (proj and in_proj fp16 planes, uint8 tensor on x's device) for a2_forward(..., prep=...)."""
+    return ops().a2_prep(x, int(num_areas), int(num_heads), proj_w, ln_w, ln_b, in_w, in_b)
 
 
 def a2_forward(x, num_areas, num_heads, proj_w, proj_b, ln_w, ln_b, ln_eps, in_w, in_b, mo_w, mo_b, op_w, op_b,

@@ -7,16 +7,17 @@
 // and runs as the following token GEMM; the pooling before it is a2_pool_tokens_kernel.
 //
 // Why one kernel: the decomposed path wrote the normalised tokens, then Q/K/V [tokens][3C] (31 MB at bs 32) to HBM
-// and read them back in the attention kernel, over three launches. Here one 256-thread workgroup per (image, head)
+// and read them back in the attention kernel, over three launches. Here one 512-thread workgroup per (image, head)
 // keeps everything of its head on chip:
-//   1. K loop over the C input channels in 32-wide steps: the step's slice of the pooled tokens [L][32] is read from
-//      HBM / L2, normalised with the per-token (mean, rstd) of row_stats_kernel (the LN affine is folded into the
-//      prepared weights: W' = W diag(gamma), b' = b + W beta) and stored as two fp16 planes in LDS (double-buffered);
-//      wave w owns head-local column block w of Q, K and V (16 output dims each) for all L tokens - its weight
-//      fragments stream from L2 in the fragment-major layout of the prep kernel, one step ahead.
+//   1. K loop over the C input channels in 64-wide stages: the stage's slice of the pooled tokens [L][64] is read
+//      from HBM / L2 one stage ahead, normalised with the per-token (mean, rstd) of row_stats_kernel (the LN affine
+//      is folded into the prepared weights: W' = W diag(gamma), b' = b + W beta) and stored as two fp16 planes in
+//      LDS (double-buffered); wave w owns head-local column block w & 3 of Q, K and V (16 output dims each) for half
+//      of the tokens (w >> 2) - its weight fragments stream from L2 in the fragment-major layout of the prep kernel,
+//      one stage ahead.
 //   2. Q and K go to LDS as [token][d] planes, V as V^T [d][token] planes (computed with the operands swapped, so a
 //      lane holds 4 consecutive tokens of one dim).
-//   3. Attention: wave w takes query blocks w, w+4, w+8: S^T = K Q^T per 16-key block (the Q fragments read with the
+//   3. Attention: wave w takes query blocks w, w+8: S^T = K Q^T per 16-key block (the Q fragments read with the
 //      k permutation that makes the S^T accumulators the P^T operand of O^T = V^T P^T), softmax over keys in
 //      registers (exp2, 1/sum applied to O), O written token-major [B*L][C] at the head's 64 columns.
 // Weights are scaled by 64 (exact) at the split so their low terms stay normal fp16; Q, K, V keep the factor: it is
@@ -29,8 +30,8 @@ namespace a2f {
 
 constexpr float WSC = 64.0f;
 constexpr int HD = 64;          // head dim (the kernel's shape)
-constexpr int KS = 32;          // k step
-constexpr int PSA = KS + 8;     // activation plane row stride (halves): 5 16-byte quads, conflict-free b128 reads
+constexpr int KS = 64;          // k stage (two 32-k MFMA steps)
+constexpr int PSA = KS + 8;     // activation plane row stride (halves): 9 16-byte quads, conflict-free b128 reads
 constexpr int PSQ = HD + 8;     // Q / K plane row stride
 constexpr int MAXTB = 10;       // token blocks of 16: L <= 160
 
@@ -51,7 +52,10 @@ struct Args {
 };
 
 template <int NTB>
-__global__ __launch_bounds__(256, 1) void a2_qkv_attn_kernel(Args p) {
+__global__ __launch_bounds__(512, 1) void a2_qkv_attn_kernel(Args p) {
+  constexpr int NW = 8;                 // waves: (column block 0..3 of Q / K / V) x (token half 0..1)
+  constexpr int NT = 64 * NW;
+  constexpr int TBH = (NTB + 1) / 2;    // token blocks per half
   constexpr int NL = NTB * 16;          // padded tokens
   constexpr int APL = NL * PSA;         // activation plane (halves)
   constexpr int QPL = NL * PSQ;         // Q / K plane
@@ -70,6 +74,7 @@ __global__ __launch_bounds__(256, 1) void a2_qkv_attn_kernel(Args p) {
 
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l15 = lane & 15, g = lane >> 4;
+  const int cblk = wid & 3, tb0 = (wid >> 2) * TBH;
   const int C = p.C, L = p.L;
   const int heads = C / HD;
   // XCD-aware: the heads of one image run on one XCD (they read the same pooled tokens from its L2)
@@ -79,28 +84,28 @@ __global__ __launch_bounds__(256, 1) void a2_qkv_attn_kernel(Args p) {
   float rng = 0.f;
 
   const float* Sb = p.S + (long)img * L * C;
-  for (int t = tid; t < NL; t += 256) {
+  for (int t = tid; t < NL; t += NT) {
     const float2 v = t < L ? *reinterpret_cast<const float2*>(p.stats + 2 * ((long)img * L + t)) : make_float2(0.f, 0.f);
     st[t] = v;
   }
-  // this thread's staging items: token rows of the 32-wide k slice as float4 (NL * 8 float4 per step)
-  constexpr int NIT = (NL * 8 + 255) / 256;
-  float4 stg[NIT];
-  auto load_step = [&](int s) {
+  // staging items of one 64-wide k stage: token rows as float4 (NL * 16 per stage)
+  constexpr int NIT = (NL * 16 + NT - 1) / NT;
+  float4 sA[NIT], sB[NIT];  // stage s + 1 and s + 2 in flight (two register sets)
+  auto load_stage = [&](float4 (&stg)[NIT], int s) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < NIT; ++i) {
-      const int e = tid + 256 * i;
-      const int t = e >> 3, q = e & 7;
-      stg[i] = (e < NL * 8 && t < L) ? *reinterpret_cast<const float4*>(Sb + (long)t * C + KS * s + 4 * q)
-                                     : make_float4(0.f, 0.f, 0.f, 0.f);
+      const int e = tid + NT * i;
+      const int t = e >> 4, q = e & 15;
+      stg[i] = (e < NL * 16 && t < L) ? *reinterpret_cast<const float4*>(Sb + (long)t * C + KS * s + 4 * q)
+                                      : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   };
-  auto store_step = [&](int buf) {
+  auto store_stage = [&](const float4 (&stg)[NIT], int buf) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < NIT; ++i) {
-      const int e = tid + 256 * i;
-      if (e < NL * 8) {
-        const int t = e >> 3, q = e & 7;
+      const int e = tid + NT * i;
+      if (e < NL * 16) {
+        const int t = e >> 4, q = e & 15;
         const float2 ms = st[t];
         const float4 v = stg[i];
         const f32x4 u = f32x4{(v.x - ms.x) * ms.y, (v.y - ms.x) * ms.y, (v.z - ms.x) * ms.y, (v.w - ms.x) * ms.y};
@@ -112,102 +117,110 @@ __global__ __launch_bounds__(256, 1) void a2_qkv_attn_kernel(Args p) {
       }
     }
   };
-  // weight fragments of this wave's column block w of Q, K, V (rows h*64 + 16w + [0,16) of each third)
-  const int nsteps = C / KS;
+  // weight fragments of column block cblk of Q, K, V (rows h*64 + 16 cblk + [0,16) of each third); 32-k steps
+  const int nk32 = C / 32;
+  const int nstage = C / KS;
   const long pst = (long)3 * C * C;  // plane stride
   int nbr[3];
 #pragma unroll
-  for (int m = 0; m < 3; ++m) nbr[m] = (m * C + h * HD) / 16 + wid;
-  auto wfrag = [&](int m, int s, int pl) {
-    return *reinterpret_cast<const f16x8_t*>(p.w + pl * pst + ((long)(nbr[m] * nsteps + s) * 64 + lane) * 8);
+  for (int m = 0; m < 3; ++m) nbr[m] = (m * C + h * HD) / 16 + cblk;
+  auto wfrag = [&](int m, int s32, int pl) {
+    return *reinterpret_cast<const f16x8_t*>(p.w + pl * pst + ((long)(nbr[m] * nk32 + s32) * 64 + lane) * 8);
   };
-  f16x8_t wc[3][2], wn[3][2];
+  f16x8_t wa[3][2], wb[3][2];  // [m][plane] of two consecutive 32-k sub-steps (a rolling prefetch)
+  auto load_w = [&](f16x8_t (&w)[3][2], int s32) {
 #pragma unroll
-  for (int m = 0; m < 3; ++m) {
-    wc[m][0] = wfrag(m, 0, 0);
-    wc[m][1] = wfrag(m, 0, 1);
-  }
-  // accumulators: Q, K (lane: token tb*16 + l15, dims 16w + 4g + r) and V swapped (lane: dim 16w + l15, tokens
-  // tb*16 + 4g + r); start from 64 b'
-  f32x4 acc[3][NTB];
+    for (int m = 0; m < 3; ++m) {
+      w[m][0] = wfrag(m, s32, 0);
+      w[m][1] = wfrag(m, s32, 1);
+    }
+  };
+  load_w(wa, 0);
+  // accumulators: Q, K (lane: token tb*16 + l15, dims 16 cblk + 4g + r) and V swapped (lane: dim 16 cblk + l15,
+  // tokens tb*16 + 4g + r); start from 64 b'
+  f32x4 acc[3][TBH];
   {
-    const f32x4 bq = *reinterpret_cast<const f32x4*>(p.b + h * HD + 16 * wid + 4 * g) * WSC;
-    const f32x4 bk = *reinterpret_cast<const f32x4*>(p.b + C + h * HD + 16 * wid + 4 * g) * WSC;
-    const float bv = p.b[2 * C + h * HD + 16 * wid + l15] * WSC;
+    const f32x4 bq = *reinterpret_cast<const f32x4*>(p.b + h * HD + 16 * cblk + 4 * g) * WSC;
+    const f32x4 bk = *reinterpret_cast<const f32x4*>(p.b + C + h * HD + 16 * cblk + 4 * g) * WSC;
+    const float bv = p.b[2 * C + h * HD + 16 * cblk + l15] * WSC;
 #pragma unroll
-    for (int tb = 0; tb < NTB; ++tb) {
-      acc[0][tb] = bq;
-      acc[1][tb] = bk;
-      acc[2][tb] = f32x4{bv, bv, bv, bv};
+    for (int i = 0; i < TBH; ++i) {
+      acc[0][i] = bq;
+      acc[1][i] = bk;
+      acc[2][i] = f32x4{bv, bv, bv, bv};
     }
   }
-  load_step(0);
+  load_stage(sA, 0);
+  if (nstage > 1) load_stage(sB, 1);
   __syncthreads();  // stats in LDS
-  store_step(0);
-  for (int s = 0; s < nsteps; ++s) {
+  store_stage(sA, 0);
+  auto mma = [&](const f16x8_t (&w)[3][2], int buf, int u) __attribute__((always_inline)) {
+    const h16_t* a0 = Ab + (buf * 2) * APL + l15 * PSA + 32 * u + 8 * g;
+#pragma unroll
+    for (int i = 0; i < TBH; ++i) {
+      const int tb = tb0 + i;
+      if (tb < NTB) {
+        const f16x8_t xh = *reinterpret_cast<const f16x8_t*>(a0 + tb * 16 * PSA);
+        const f16x8_t xl = *reinterpret_cast<const f16x8_t*>(a0 + tb * 16 * PSA + APL);
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {  // Q, K: weights as the A operand (rows = dims), tokens as B
+          f32x4 c = mfma16(w[m][1], xh, acc[m][i]);
+          c = mfma16(w[m][0], xl, c);
+          acc[m][i] = mfma16(w[m][0], xh, c);
+        }
+        {  // V: tokens as the A operand, weights as B (lane: 4 consecutive tokens of one dim)
+          f32x4 c = mfma16(xh, w[2][1], acc[2][i]);
+          c = mfma16(xl, w[2][0], c);
+          acc[2][i] = mfma16(xh, w[2][0], c);
+        }
+      }
+    }
+  };
+  auto stage = [&](int s, float4 (&stored)[NIT], float4 (&next)[NIT]) __attribute__((always_inline)) {
+    // entry: stage s is in buffer s & 1, `next` holds stage s + 1's loads in flight, `stored` is free
     const int buf = s & 1;
-    if (s + 1 < nsteps) {
-      load_step(s + 1);
-#pragma unroll
-      for (int m = 0; m < 3; ++m) {
-        wn[m][0] = wfrag(m, s + 1, 0);
-        wn[m][1] = wfrag(m, s + 1, 1);
-      }
-    }
-    __syncthreads();  // step s's planes stored; every wave is done with step s - 1's buffer
-    const h16_t* a0 = Ab + (buf * 2) * APL + l15 * PSA + 8 * g;
-#pragma unroll
-    for (int tb = 0; tb < NTB; ++tb) {
-      const f16x8_t xh = *reinterpret_cast<const f16x8_t*>(a0 + tb * 16 * PSA);
-      const f16x8_t xl = *reinterpret_cast<const f16x8_t*>(a0 + tb * 16 * PSA + APL);
-#pragma unroll
-      for (int m = 0; m < 2; ++m) {  // Q, K: weights as the A operand (rows = dims), tokens as B
-        f32x4 c = mfma16(wc[m][1], xh, acc[m][tb]);
-        c = mfma16(wc[m][0], xl, c);
-        acc[m][tb] = mfma16(wc[m][0], xh, c);
-      }
-      {  // V: tokens as the A operand, weights as B (lane: 4 consecutive tokens of one dim)
-        f32x4 c = mfma16(xh, wc[2][1], acc[2][tb]);
-        c = mfma16(xl, wc[2][0], c);
-        acc[2][tb] = mfma16(xh, wc[2][0], c);
-      }
-    }
-    if (s + 1 < nsteps) {
-      store_step(buf ^ 1);
-#pragma unroll
-      for (int m = 0; m < 3; ++m) {
-        wc[m][0] = wn[m][0];
-        wc[m][1] = wn[m][1];
-      }
-    }
+    if (s + 2 < nstage) load_stage(stored, s + 2);
+    __syncthreads();  // stage s's planes stored; every wave is done with stage s - 1's buffer
+    load_w(wb, 2 * s + 1);
+    mma(wa, buf, 0);
+    if (s + 1 < nstage) load_w(wa, 2 * s + 2);
+    mma(wb, buf, 1);
+    if (s + 1 < nstage) store_stage(next, buf ^ 1);
+  };
+  for (int s = 0; s < nstage; s += 2) {
+    stage(s, sA, sB);
+    if (s + 1 < nstage) stage(s + 1, sB, sA);
   }
   __syncthreads();  // every wave is done with the activation planes (Q / K / V^T reuse the region)
   // Q, K -> [token][d] planes, V -> V^T [d][token] planes (all x64); padded tokens hold finite values
 #pragma unroll
-  for (int tb = 0; tb < NTB; ++tb) {
-    const int tok = tb * 16 + l15;
-    uint2 hh, ll;
+  for (int i = 0; i < TBH; ++i) {
+    const int tb = tb0 + i;
+    if (tb < NTB) {
+      const int tok = tb * 16 + l15;
+      uint2 hh, ll;
 #pragma unroll
-    for (int m = 0; m < 2; ++m) {
-      const f32x4 v = acc[m][tb];
-      rng = range_acc(rng, v);
-      split4(v, hh, ll);
-      h16_t* d = (m == 0 ? Qp : Kp) + tok * PSQ + 16 * wid + 4 * g;
+      for (int m = 0; m < 2; ++m) {
+        const f32x4 v = acc[m][i];
+        rng = range_acc(rng, v);
+        split4(v, hh, ll);
+        h16_t* d = (m == 0 ? Qp : Kp) + tok * PSQ + 16 * cblk + 4 * g;
+        *reinterpret_cast<uint2*>(d) = hh;
+        *reinterpret_cast<uint2*>(d + QPL) = ll;
+      }
+      rng = range_acc(rng, acc[2][i]);
+      split4(acc[2][i], hh, ll);
+      h16_t* d = Vt + (16 * cblk + l15) * PSV + tb * 16 + 4 * g;
       *reinterpret_cast<uint2*>(d) = hh;
-      *reinterpret_cast<uint2*>(d + QPL) = ll;
+      *reinterpret_cast<uint2*>(d + VPL) = ll;
     }
-    rng = range_acc(rng, acc[2][tb]);
-    split4(acc[2][tb], hh, ll);
-    h16_t* d = Vt + (16 * wid + l15) * PSV + tb * 16 + 4 * g;
-    *reinterpret_cast<uint2*>(d) = hh;
-    *reinterpret_cast<uint2*>(d + VPL) = ll;
   }
   __syncthreads();
 
   // attention: S^T[key][q] per 16-key block; slot j of lane group g in 32-d step s is head dim 32s + 4g + j (j < 4)
   // or 32s + 16 + 4g + j - 4 for both the Q (B) and K (A) fragments
   const float c2 = p.scale * 1.44269504088896341f * (1.0f / (WSC * WSC));
-  for (int qb = wid; qb < NTB; qb += 4) {
+  for (int qb = wid; qb < NTB; qb += NW) {
     f16x8_t qh[2], ql[2];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -233,6 +246,8 @@ __global__ __launch_bounds__(256, 1) void a2_qkv_attn_kernel(Args p) {
         c = mfma16(kh, qh[s], c);
       }
       sc[kb] = c;
+      // keep the scheduler from hoisting every key block's K reads ahead (register pressure at 2 waves per SIMD)
+      if (kb & 1) __builtin_amdgcn_sched_barrier(0);
     }
     float mx = -INFINITY;
 #pragma unroll
@@ -298,31 +313,206 @@ __global__ __launch_bounds__(256, 1) void a2_qkv_attn_kernel(Args p) {
   if (p.prep_flag && p.range_flag && blockIdx.x == 0 && threadIdx.x == 0 && *p.prep_flag) *p.range_flag = 1u;
 }
 
-// in_proj with the LN affine folded, split into fp16 planes (x64, fragment-major: element (n, k) of W' [3C][C] at
-// ((n/16 * C/32 + k/32) * 64 + (k%32)/8 * 16 + n%16) * 8 + k%8), folded bias b' = b + W beta; one wave per row
+// ---- proj 1x1 conv (BN folded) + SiLU + adaptive row pooling to the area tokens, one kernel ----------------------
+// a2_attn.py:39-48: x_proj = SiLU(conv1x1(x)) (Conv with folded BN), pooled = adaptive_avg_pool2d(x_proj, (A, W)),
+// seq = pooled.flatten(2).transpose(1, 2). One 512-thread workgroup per (image, 64 output channels) computes the
+// [64][H*W] tile of x_proj on fp16-split MFMA (weights = the A operand, pixels = B), keeps it in LDS and averages
+// the row bins [floor(a H / A), ceil((a + 1) H / A)) straight into the token-major S rows: x_proj never reaches HBM
+// (the decomposed path wrote and re-read it, 26 MB each way at bs 32). The x tile of each 32-channel k step is staged
+// as 4x4 (k, pixel) blocks transposed in registers into [pixel][k] fp16 planes (double-buffered).
+constexpr int PMAXHW = 400;   // pixels per image the tile holds (20x20 at 640^2)
+constexpr int PPS = 40;       // staged plane row stride (halves): 32 k + 8
+template <int NCB>            // 16-pixel column blocks per image
+__global__ __launch_bounds__(512, 1) void a2_proj_pool_kernel(const float* __restrict__ x, const h16_t* __restrict__ wp,
+                                                              const float* __restrict__ bp, float* __restrict__ S,
+                                                              int C, int H, int W, int A, unsigned* range_flag) {
+  constexpr int NPX = NCB * 16;                 // padded pixels
+  constexpr int PPL = NPX * PPS;                // plane (halves)
+  constexpr int STG_B = 2 * 2 * PPL * 2;        // two buffers x two planes
+  constexpr int HWP = NPX + 1;                  // fp32 tile row stride (odd: conflict-free per-channel reads)
+  constexpr int T_B = 64 * HWP * 4;
+  constexpr int R_B = STG_B > T_B ? STG_B : T_B;
+  constexpr int NT = 512, NW = 8;
+  constexpr int CBW = (NCB + NW - 1) / NW;      // column blocks per wave
+  static_assert(R_B <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) char smem[R_B];
+  h16_t* Pl = reinterpret_cast<h16_t*>(smem);   // [2 buf][2 plane][NPX][PPS]
+  float* Tt = reinterpret_cast<float*>(smem);   // [64][HWP] after the K loop
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l15 = lane & 15, g = lane >> 4;
+  const int HW = H * W;
+  const int ncb64 = C / 64;
+  const int nblk = gridDim.x;
+  const int wg = (nblk & 7) ? (int)blockIdx.x : (int)(blockIdx.x & 7) * (nblk >> 3) + (int)(blockIdx.x >> 3);
+  const int img = wg / ncb64, co = (wg - img * ncb64) * 64;
+  const float* xb = x + (long)img * C * HW;
+  float rng = 0.f;
+
+  // staging: (4 k x 4 pixel) blocks of the 32 x NPX step tile; 8 * NPX / 4 blocks
+  constexpr int NBLK = 8 * (NPX / 4);
+  constexpr int NIT = (NBLK + NT - 1) / NT;
+  // the x tile of step s is loaded two steps ahead (two register sets), stored split at the end of step s - 1
+  float4 sA[NIT][4], sB[NIT][4];
+  auto load_step = [&](float4 (&stg)[NIT][4], int s) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) {
+      const int e = tid + NT * i;
+      const int kq = e & 7, pq = e >> 3;  // k group fastest: the LDS stores of 8 lanes fill one 64-byte row run
+      const int k = 32 * s + 4 * kq, px = 4 * pq;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        stg[i][r] = (e < NBLK && px < HW) ? *reinterpret_cast<const float4*>(xb + (long)(k + r) * HW + px)
+                                          : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto store_step = [&](const float4 (&stg)[NIT][4], int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) {
+      const int e = tid + NT * i;
+      if (e < NBLK) {
+        const int kq = e & 7, pq = e >> 3;
+        const float4* v = stg[i];
+        // pixel 4pq + j: k 4kq .. 4kq + 3
+        const f32x4 col[4] = {f32x4{v[0].x, v[1].x, v[2].x, v[3].x}, f32x4{v[0].y, v[1].y, v[2].y, v[3].y},
+                              f32x4{v[0].z, v[1].z, v[2].z, v[3].z}, f32x4{v[0].w, v[1].w, v[2].w, v[3].w}};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          uint2 hh, ll;
+          split4(col[j], hh, ll);
+          rng = range_acc(rng, col[j]);
+          h16_t* d = Pl + (buf * 2) * PPL + (4 * pq + j) * PPS + 4 * kq;
+          *reinterpret_cast<uint2*>(d) = hh;
+          *reinterpret_cast<uint2*>(d + PPL) = ll;
+        }
+      }
+    }
+  };
+  // weight fragments (A operand): output rows co + 16 rb + l15, k = 32 s + 8g .. +7, fragment-major planes of W'
+  const int nk32 = C / 32;
+  const long pst = (long)C * C;
+  auto wfrag = [&](int rb, int s, int pl) {
+    return *reinterpret_cast<const f16x8_t*>(wp + pl * pst + ((long)(((co >> 4) + rb) * nk32 + s) * 64 + lane) * 8);
+  };
+  f32x4 acc[4][CBW];
+#pragma unroll
+  for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+    for (int j = 0; j < CBW; ++j) acc[rb][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f16x8_t wa[4][2], wb[4][2];
+#pragma unroll
+  for (int rb = 0; rb < 4; ++rb) {
+    wa[rb][0] = wfrag(rb, 0, 0);
+    wa[rb][1] = wfrag(rb, 0, 1);
+  }
+  auto step = [&](int s, float4 (&stored)[NIT][4], float4 (&next)[NIT][4]) __attribute__((always_inline)) {
+    // entry: step s's planes are stored (buffer s & 1), `next` holds step s + 1's loads in flight, `stored` is free
+    const int buf = s & 1;
+    if (s + 2 < nk32) load_step(stored, s + 2);
+    if (s + 1 < nk32) {
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) {
+        wb[rb][0] = wfrag(rb, s + 1, 0);
+        wb[rb][1] = wfrag(rb, s + 1, 1);
+      }
+    }
+    __syncthreads();  // step s's planes stored; every wave is done with step s - 1's buffer
+    const h16_t* b0 = Pl + (buf * 2) * PPL + l15 * PPS + 8 * g;
+#pragma unroll
+    for (int j = 0; j < CBW; ++j) {
+      const int cb = wid + NW * j;
+      if (cb < NCB) {
+        const f16x8_t xh = *reinterpret_cast<const f16x8_t*>(b0 + cb * 16 * PPS);
+        const f16x8_t xl = *reinterpret_cast<const f16x8_t*>(b0 + cb * 16 * PPS + PPL);
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) {
+          f32x4 c = mfma16(wa[rb][1], xh, acc[rb][j]);
+          c = mfma16(wa[rb][0], xl, c);
+          acc[rb][j] = mfma16(wa[rb][0], xh, c);
+        }
+      }
+    }
+    if (s + 1 < nk32) {
+      store_step(next, buf ^ 1);
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) {
+        wa[rb][0] = wb[rb][0];
+        wa[rb][1] = wb[rb][1];
+      }
+    }
+  };
+  load_step(sA, 0);
+  if (nk32 > 1) load_step(sB, 1);
+  store_step(sA, 0);
+  for (int s = 0; s < nk32; s += 2) {
+    step(s, sA, sB);
+    if (s + 1 < nk32) step(s + 1, sB, sA);
+  }
+  __syncthreads();  // the staging planes are free: the SiLU tile takes the region
+  // lane (g, l15) of (rb, j): channel co + 16 rb + 4g + r, pixel (wid + 8j) * 16 + l15
+#pragma unroll
+  for (int rb = 0; rb < 4; ++rb) {
+    const f32x4 bias = *reinterpret_cast<const f32x4*>(bp + co + 16 * rb + 4 * g);
+#pragma unroll
+    for (int j = 0; j < CBW; ++j) {
+      const int cb = wid + NW * j;
+      if (cb < NCB) {
+        const int px = cb * 16 + l15;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Tt[(16 * rb + 4 * g + r) * HWP + px] = siluf_(acc[rb][j][r] * (1.0f / WSC) + bias[r]);
+      }
+    }
+  }
+  __syncthreads();
+  // pooled tokens: thread (c = tid % 64) averages its channel's bins in row order (as the reference's CPU pooling)
+  const int c = tid & 63;
+  const float* trow = Tt + c * HWP;
+  float* Sb = S + (long)img * A * W * C + co + c;
+  for (int t = tid >> 6; t < A * W; t += NW) {
+    const int a = t / W, w = t - (t / W) * W;
+    const int r0 = (a * H) / A, r1 = ((a + 1) * H + A - 1) / A;
+    float sum = 0.f;
+    for (int r = r0; r < r1; ++r) sum += trow[r * W + w];
+    Sb[(long)t * C] = sum / (float)(r1 - r0);
+  }
+  range_report(range_flag, rng);
+}
+
+// Weight preparation, one wave per output row: rows [0, 3C) = in_proj with the LN affine folded (W' = W diag(gamma),
+// b' = b + W beta), rows [3C, 4C) = the proj 1x1 conv (BN folded by the caller); both split into fp16 planes (x64,
+// fragment-major: element (n, k) of [N][C] at ((n/16 * C/32 + k/32) * 64 + (k%32)/8 * 16 + n%16) * 8 + k%8)
 __global__ __launch_bounds__(256) void a2_prep_kernel(const float* __restrict__ w, const float* __restrict__ bias,
                                                       const float* __restrict__ ln_w, const float* __restrict__ ln_b,
-                                                      int C, h16_t* __restrict__ planes, float* __restrict__ bf,
+                                                      const float* __restrict__ pw, int C, h16_t* __restrict__ planes,
+                                                      float* __restrict__ bf, h16_t* __restrict__ pplanes,
                                                       unsigned* range_flag, unsigned* prep_flag) {
   const int lane = threadIdx.x & 63;
-  const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (n >= 3 * C) return;
-  const float* row = w + (long)n * C;
-  const long N = 3L * C;
+  int n = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (n >= 4 * C) return;
+  const bool proj = n >= 3 * C;
+  if (proj) n -= 3 * C;
+  const float* row = (proj ? pw : w) + (long)n * C;
+  const long N = proj ? (long)C : 3L * C;
+  h16_t* dst = proj ? pplanes : planes;
   float bacc = 0.f, wmax = 0.f;
   for (int k = lane; k < C; k += 64) {
     const float wv = row[k];
-    bacc = fmaf(wv, ln_b[k], bacc);
-    const float v = wv * ln_w[k] * WSC;
+    float v = wv * WSC;
+    if (!proj) {
+      bacc = fmaf(wv, ln_b[k], bacc);
+      v = wv * ln_w[k] * WSC;
+    }
     const _Float16 hh = (_Float16)v;
     const _Float16 ll = (_Float16)(v - (float)hh);
     wmax = nmax_(wmax, fabsf(v));
     const long fi = ((long)((n >> 4) * (C >> 5) + (k >> 5)) * 64 + (((k & 31) >> 3) << 4) + (n & 15)) * 8 + (k & 7);
-    planes[fi] = __builtin_bit_cast(h16_t, hh);
-    planes[N * C + fi] = __builtin_bit_cast(h16_t, ll);
+    dst[fi] = __builtin_bit_cast(h16_t, hh);
+    dst[N * C + fi] = __builtin_bit_cast(h16_t, ll);
   }
-  bacc = wave_sum(bacc);
-  if (lane == 0) bf[n] = bias[n] + bacc;
+  if (!proj) {
+    bacc = wave_sum(bacc);
+    if (lane == 0) bf[n] = bias[n] + bacc;
+  }
   range_report(range_flag, wmax);
   range_report(prep_flag, wmax);
 }
@@ -332,59 +522,109 @@ __global__ __launch_bounds__(256) void a2_prep_kernel(const float* __restrict__ 
 
 using namespace ys;
 
-// the fused kernel's shapes: head dim 64, C a multiple of 64 (<= 1024), L = areas * W <= 160
+// the fused kernels (default; YOLOSOD_A2_FUSED=0 runs the decomposed GEMM path on the same split products)
+static int g_a2_fused = -1;
+static bool a2_fused_env() {
+  if (g_a2_fused < 0) {
+    const char* e = getenv("YOLOSOD_A2_FUSED");
+    g_a2_fused = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_a2_fused != 0;
+}
+// Test hook: A2 through the fused kernels (1) or the decomposed path (0); returns the previous state.
+YS_EXPORT int yolosod_debug_set_a2_fused(int on) {
+  const int prev = a2_fused_env() ? 1 : 0;
+  g_a2_fused = on ? 1 : 0;
+  return prev;
+}
+
+// the LN / QKV / attention kernel's shapes: head dim 64, C a multiple of 64 (<= 1024), L = areas * W <= 160
 bool yolosod_a2_fused_ok(int C, int num_heads, int L) {
-  static const bool on = [] { const char* e = getenv("YOLOSOD_A2_FUSED"); return !(e && e[0] == '0'); }();
-  return on && num_heads > 0 && C == a2f::HD * num_heads && C <= 1024 && L >= 1 && L <= a2f::MAXTB * 16;
+  const bool on = a2_fused_env();
+  return on && num_heads > 0 && C == a2f::HD * num_heads && C % a2f::KS == 0 && C <= 1024 && L >= 1 &&
+         L <= a2f::MAXTB * 16;
 }
 
 size_t yolosod_a2_fused_prep_bytes(int C) {
   Sizer s;
-  s.take<h16_t>((size_t)2 * 3 * C * C);
-  s.take<float>((size_t)3 * C);
-  s.take<unsigned>(1);
+  s.take<h16_t>((size_t)2 * 3 * C * C);  // in_proj planes (LN folded)
+  s.take<float>((size_t)3 * C);          // folded in_proj bias
+  s.take<h16_t>((size_t)2 * C * C);      // proj planes
+  s.take<unsigned>(1);                   // the weights' split-range word
   return s.off;
 }
 
-static bool a2f_carve(void* buf, size_t bytes, int C, h16_t*& planes, float*& bf, unsigned*& pflag) {
-  Carver cv(buf, bytes);
-  planes = cv.take<h16_t>((size_t)2 * 3 * C * C);
-  bf = cv.take<float>((size_t)3 * C);
-  pflag = cv.take<unsigned>(1);
-  return pflag != nullptr;
-}
-
-int yolosod_a2_fused_prepare(int C, const float* ln_w, const float* ln_b, const float* in_w, const float* in_b,
-                             void* prep, size_t prep_bytes, hipStream_t st) {
+struct A2Prep {
   h16_t* planes;
   float* bf;
+  h16_t* pplanes;
   unsigned* pflag;
-  YS_CHECK_ARG(a2f_carve(prep, prep_bytes, C, planes, bf, pflag), "a2 prep: buffer too small (%zu)", prep_bytes);
-  if (hipMemsetAsync(pflag, 0, sizeof(unsigned), st) != hipSuccess) {
+};
+static bool a2f_carve(void* buf, size_t bytes, int C, A2Prep& q) {
+  Carver cv(buf, bytes);
+  q.planes = cv.take<h16_t>((size_t)2 * 3 * C * C);
+  q.bf = cv.take<float>((size_t)3 * C);
+  q.pplanes = cv.take<h16_t>((size_t)2 * C * C);
+  q.pflag = cv.take<unsigned>(1);
+  return q.pflag != nullptr;
+}
+
+int yolosod_a2_fused_prepare(int C, const float* proj_w, const float* ln_w, const float* ln_b, const float* in_w,
+                             const float* in_b, void* prep, size_t prep_bytes, hipStream_t st) {
+  A2Prep q;
+  YS_CHECK_ARG(a2f_carve(prep, prep_bytes, C, q), "a2 prep: buffer too small (%zu)", prep_bytes);
+  if (hipMemsetAsync(q.pflag, 0, sizeof(unsigned), st) != hipSuccess) {
     set_error("a2 prep: flag reset failed");
     return -1;
   }
-  hipLaunchKernelGGL(a2f::a2_prep_kernel, dim3((3 * C + 3) / 4), dim3(256), 0, st, in_w, in_b, ln_w, ln_b, C, planes,
-                     bf, range_flag_dev(), pflag);
+  hipLaunchKernelGGL(a2f::a2_prep_kernel, dim3((4 * C + 3) / 4), dim3(256), 0, st, in_w, in_b, ln_w, ln_b, proj_w, C,
+                     q.planes, q.bf, q.pplanes, range_flag_dev(), q.pflag);
   YS_CHECK_LAUNCH("a2_prep");
   return 0;
+}
+
+// the proj + SiLU + pooling kernel's shapes: C a multiple of 64, one image's pixels within the LDS tile
+bool yolosod_a2_proj_pool_ok(int C, int H, int W) {
+  const bool on = a2_fused_env();
+  return on && C % 64 == 0 && C <= 1024 && (long)H * W <= a2f::PMAXHW && ((long)H * W) % 4 == 0;
+}
+
+// x -> S (token-major pooled SiLU(proj x + bp)). Returns < 0 on error.
+int yolosod_a2_proj_pool_run(const float* x, const float* proj_b, float* S, int B, int C, int H, int W, int A,
+                             const void* prep, size_t prep_bytes, hipStream_t st) {
+  A2Prep q;
+  YS_CHECK_ARG(a2f_carve(const_cast<void*>(prep), prep_bytes, C, q), "a2: prepared block too small");
+  YS_CHECK_ARG(yolosod_a2_proj_pool_ok(C, H, W), "a2: proj/pool shape C=%d %dx%d not fused", C, H, W);
+  YS_CHECK_ARG(((uintptr_t)x & 15) == 0, "a2: x must be 16-byte aligned");
+  const long nwg = (long)B * (C / 64);
+  YS_CHECK_ARG(nwg < (1L << 31), "a2: too many workgroups");
+  const int ncb = (H * W + 15) / 16;
+#define YS_A2P(N)                                                                                                    \
+  if (ncb <= N) {                                                                                                     \
+    hipLaunchKernelGGL((a2f::a2_proj_pool_kernel<N>), dim3((unsigned)nwg), dim3(512), 0, st, x, q.pplanes, proj_b, S, \
+                       C, H, W, A, range_flag_dev());                                                                 \
+    YS_CHECK_LAUNCH("a2_proj_pool");                                                                                  \
+    return 0;                                                                                                         \
+  }
+  YS_A2P(4) YS_A2P(8) YS_A2P(13) YS_A2P(16) YS_A2P(25)
+#undef YS_A2P
+  YS_CHECK_ARG(false, "a2: %dx%d pixels too many for the proj/pool kernel", H, W);
+  return -1;
 }
 
 // LN -> QKV -> attention of all (image, head) pairs: S / stats -> O ([B*L][C]). Returns < 0 on error.
 int yolosod_a2_fused_run(const float* S, const float* stats, float* O, int B, int L, int C, int num_heads,
                          const void* prep, size_t prep_bytes, hipStream_t st) {
-  h16_t* planes;
-  float* bf;
-  unsigned* pflag;
-  YS_CHECK_ARG(a2f_carve(const_cast<void*>(prep), prep_bytes, C, planes, bf, pflag), "a2: prepared block too small");
+  A2Prep q;
+  YS_CHECK_ARG(a2f_carve(const_cast<void*>(prep), prep_bytes, C, q), "a2: prepared block too small");
   YS_CHECK_ARG(yolosod_a2_fused_ok(C, num_heads, L), "a2: shape C=%d heads=%d L=%d not fused", C, num_heads, L);
   const long nwg = (long)B * num_heads;
   YS_CHECK_ARG(nwg < (1L << 31), "a2: too many (image, head) pairs");
-  a2f::Args a{S, stats, planes, bf, O, L, C, 1.0f / sqrtf((float)a2f::HD), range_flag_dev(), pflag};
+  a2f::Args a{S, stats, q.planes, q.bf, O, L, C, 1.0f / sqrtf((float)a2f::HD), range_flag_dev(), q.pflag};
   const int ntb = (L + 15) / 16;
 #define YS_A2F(N)                                                                                         \
   case N:                                                                                                 \
-    hipLaunchKernelGGL((a2f::a2_qkv_attn_kernel<N>), dim3((unsigned)nwg), dim3(256), 0, st, a); \
+    hipLaunchKernelGGL((a2f::a2_qkv_attn_kernel<N>), dim3((unsigned)nwg), dim3(512), 0, st, a); \
     break;
   switch (ntb) {
     YS_A2F(1) YS_A2F(2) YS_A2F(3) YS_A2F(4) YS_A2F(5) YS_A2F(6) YS_A2F(7) YS_A2F(8) YS_A2F(9) YS_A2F(10)

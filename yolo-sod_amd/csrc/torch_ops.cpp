@@ -144,8 +144,8 @@ Tensor ca_fwd(const Tensor& x, const Tensor& conv1_w, const Tensor& conv1_b, con
 
 // A2's fused LN / QKV / attention kernel's prepared in_proj weights (yolosod_a2_prepare) as a uint8 tensor, made
 // once per parameter version by the caller (nn/modules.A2_Attn caches it) and passed to a2_fwd.
-Tensor a2_prep(const Tensor& x, int64_t num_areas, int64_t num_heads, const Tensor& ln_w, const Tensor& ln_b,
-               const Tensor& in_w, const Tensor& in_b) {
+Tensor a2_prep(const Tensor& x, int64_t num_areas, int64_t num_heads, const Tensor& proj_w, const Tensor& ln_w,
+               const Tensor& ln_b, const Tensor& in_w, const Tensor& in_b) {
   TORCH_CHECK(!act_bf16(x, "a2_prep"), "a2_prep: the prepared path is the fp32 config's");
   c10::DeviceGuard guard(x.device());
   const int C = x.size(1), W = x.size(3);
@@ -153,7 +153,8 @@ Tensor a2_prep(const Tensor& x, int64_t num_areas, int64_t num_heads, const Tens
   TORCH_CHECK(bytes > 0, "a2_prep: C=", C, " heads=", num_heads, " L=", num_areas * W, " has no fused kernel");
   Tensor prep = at::empty({(int64_t)bytes}, x.options().dtype(at::kByte));
   auto st = c10::hip::getCurrentHIPStream(x.get_device());
-  check_rc(yolosod_a2_prepare(C, (const float*)par(ln_w, x, "layer_norm.weight", C),
+  check_rc(yolosod_a2_prepare(C, (const float*)par(proj_w, x, "proj.weight", (int64_t)C * C),
+                              (const float*)par(ln_w, x, "layer_norm.weight", C),
                               (const float*)par(ln_b, x, "layer_norm.bias", C),
                               (const float*)par(in_w, x, "in_proj_weight", 3LL * C * C),
                               (const float*)par(in_b, x, "in_proj_bias", 3 * C), prep.data_ptr(), bytes, sp(st)),
@@ -418,8 +419,8 @@ TORCH_LIBRARY(yolosod, m) {
   m.def("a2_fwd(Tensor x, int num_areas, int num_heads, Tensor proj_w, Tensor proj_b, Tensor ln_w, Tensor ln_b, "
         "float ln_eps, Tensor in_w, Tensor in_b, Tensor? mo_w, Tensor? mo_b, Tensor op_w, Tensor op_b, "
         "Tensor? prep=None) -> Tensor");
-  m.def("a2_prep(Tensor x, int num_areas, int num_heads, Tensor ln_w, Tensor ln_b, Tensor in_w, Tensor in_b) -> "
-        "Tensor");
+  m.def("a2_prep(Tensor x, int num_areas, int num_heads, Tensor proj_w, Tensor ln_w, Tensor ln_b, Tensor in_w, "
+        "Tensor in_b) -> Tensor");
   m.def("swin_fwd(Tensor x, int num_heads, int window, Tensor dw_w, Tensor ln1_w, Tensor ln1_b, float ln1_eps, "
         "Tensor in_w, Tensor in_b, Tensor out_w, Tensor out_b, Tensor ln2_w, Tensor ln2_b, float ln2_eps, "
         "Tensor m1_w, Tensor m1_b, Tensor m2_w, Tensor m2_b, Tensor pw_w, Tensor bn_w, Tensor bn_b, Tensor bn_mean, "

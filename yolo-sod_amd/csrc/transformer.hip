@@ -824,10 +824,13 @@ YS_EXPORT void yolosod_debug_set_gemm_x2(int on) { gemm_x2_forced() = on ? 1 : -
 
 bool yolosod_a2_fused_ok(int C, int num_heads, int L);
 size_t yolosod_a2_fused_prep_bytes(int C);
-int yolosod_a2_fused_prepare(int C, const float* ln_w, const float* ln_b, const float* in_w, const float* in_b,
-                             void* prep, size_t prep_bytes, hipStream_t st);
+int yolosod_a2_fused_prepare(int C, const float* proj_w, const float* ln_w, const float* ln_b, const float* in_w,
+                             const float* in_b, void* prep, size_t prep_bytes, hipStream_t st);
 int yolosod_a2_fused_run(const float* S, const float* stats, float* O, int B, int L, int C, int num_heads,
                          const void* prep, size_t prep_bytes, hipStream_t st);
+bool yolosod_a2_proj_pool_ok(int C, int H, int W);
+int yolosod_a2_proj_pool_run(const float* x, const float* proj_b, float* S, int B, int C, int H, int W, int A,
+                             const void* prep, size_t prep_bytes, hipStream_t st);
 
 YS_EXPORT size_t yolosod_a2_workspace(int B, int C, int H, int W, int num_areas) {
   const long ntok = (long)B * num_areas * W;
@@ -847,13 +850,15 @@ YS_EXPORT size_t yolosod_a2_prep_bytes(int C, int num_heads, int num_areas, int 
   return yolosod_a2_fused_ok(C, num_heads, num_areas * W) ? yolosod_a2_fused_prep_bytes(C) : 0;
 }
 
-// Weight preparation for yolosod_a2_forward_prepared: in_proj with the LayerNorm affine folded, split into fp16
-// planes; re-run whenever layer_norm / in_proj parameters change.
-YS_EXPORT int yolosod_a2_prepare(int C, const float* ln_w, const float* ln_b, const float* in_proj_w,
-                                 const float* in_proj_b, void* prep, size_t prep_bytes, void* stream) {
-  YS_CHECK_ARG(ln_w && ln_b && in_proj_w && in_proj_b && prep, "a2_prepare: null pointer");
+// Weight preparation for yolosod_a2_forward_prepared: in_proj with the LayerNorm affine folded and the proj 1x1 conv
+// (BN folded, as passed to the forward), split into fp16 planes; re-run whenever one of them changes.
+YS_EXPORT int yolosod_a2_prepare(int C, const float* proj_w, const float* ln_w, const float* ln_b,
+                                 const float* in_proj_w, const float* in_proj_b, void* prep, size_t prep_bytes,
+                                 void* stream) {
+  YS_CHECK_ARG(proj_w && ln_w && ln_b && in_proj_w && in_proj_b && prep, "a2_prepare: null pointer");
   YS_CHECK_ARG(C > 0 && C % 64 == 0 && C <= 1024, "a2_prepare: C=%d unsupported", C);
-  return yolosod_a2_fused_prepare(C, ln_w, ln_b, in_proj_w, in_proj_b, prep, prep_bytes, (hipStream_t)stream);
+  return yolosod_a2_fused_prepare(C, proj_w, ln_w, ln_b, in_proj_w, in_proj_b, prep, prep_bytes,
+                                  (hipStream_t)stream);
 }
 
 static int a2_forward_impl(const float* x, float* y, int B, int C, int H, int W, int num_areas, int num_heads,
@@ -911,26 +916,32 @@ static int a2_forward_impl(const float* x, float* y, int B, int C, int H, int W,
   char* fprep = cv.take<char>(fpb);
   YS_CHECK_ARG(fprep, "a2: workspace too small (%zu)", workspace_bytes);
   int rc;
-  // XP = SiLU(Wp x + bp)  (Conv with folded BN, a2_attn.py:39): M = Cout, N = HW, batched over images
-  GemmArgs ga{};
-  ga.A = proj_w; ga.lda = C; ga.B = x; ga.b_bs = C * HW; ga.ldb = (int)HW; ga.M = C; ga.N = (int)HW; ga.K = C;
-  ga.epi = epi_plain(XP, C * HW, (int)HW);
-  ga.epi.bias = proj_b; ga.epi.bias_mode = 1; ga.epi.act = 1;
   const bool x2 = a2_x2();
-  ga.x2 = x2; ga.x2_sa = 64.f;
-  if ((rc = launch_gemm(ga, B, false, st))) return rc;
-  YS_CHECK_ARG((size_t)64 * (W + 1) * sizeof(float) <= 64 * 1024, "a2: W=%d too large for the pooling kernel", W);
-  hipLaunchKernelGGL(a2_pool_tokens_kernel, dim3(B * A, (C + 63) / 64), dim3(256), (size_t)64 * (W + 1) * sizeof(float),
-                     st, XP, S, C, H, W, A);
-  YS_CHECK_LAUNCH("a2_pool");
+  const bool fused = x2 && yolosod_a2_fused_ok(C, num_heads, A * W);
+  if (fused && !prep) {  // per-call weight preparation (callers that keep a block use yolosod_a2_forward_prepared)
+    if ((rc = yolosod_a2_fused_prepare(C, proj_w, ln_w, ln_b, in_proj_w, in_proj_b, fprep, fpb, st))) return rc;
+    prep = fprep;
+    prep_bytes = fpb;
+  }
+  GemmArgs ga{};
+  if (fused && yolosod_a2_proj_pool_ok(C, H, W) && ((uintptr_t)x & 15) == 0) {
+    // proj + SiLU + row pooling in one kernel (a2_fused.hip): x -> S; the projected map never reaches HBM
+    if ((rc = yolosod_a2_proj_pool_run(x, proj_b, S, B, C, H, W, A, prep, prep_bytes, st))) return rc;
+  } else {
+    // XP = SiLU(Wp x + bp)  (Conv with folded BN, a2_attn.py:39): M = Cout, N = HW, batched over images
+    ga.A = proj_w; ga.lda = C; ga.B = x; ga.b_bs = C * HW; ga.ldb = (int)HW; ga.M = C; ga.N = (int)HW; ga.K = C;
+    ga.epi = epi_plain(XP, C * HW, (int)HW);
+    ga.epi.bias = proj_b; ga.epi.bias_mode = 1; ga.epi.act = 1;
+    ga.x2 = x2; ga.x2_sa = 64.f;
+    if ((rc = launch_gemm(ga, B, false, st))) return rc;
+    YS_CHECK_ARG((size_t)64 * (W + 1) * sizeof(float) <= 64 * 1024, "a2: W=%d too large for the pooling kernel", W);
+    hipLaunchKernelGGL(a2_pool_tokens_kernel, dim3(B * A, (C + 63) / 64), dim3(256),
+                       (size_t)64 * (W + 1) * sizeof(float), st, XP, S, C, H, W, A);
+    YS_CHECK_LAUNCH("a2_pool");
+  }
   ga = GemmArgs{};
-  if (x2 && yolosod_a2_fused_ok(C, num_heads, A * W)) {
+  if (fused) {
     // LN -> QKV -> attention per (image, head) in one kernel (a2_fused.hip): S + row statistics -> U
-    if (!prep) {
-      if ((rc = yolosod_a2_fused_prepare(C, ln_w, ln_b, in_proj_w, in_proj_b, fprep, fpb, st))) return rc;
-      prep = fprep;
-      prep_bytes = fpb;
-    }
     if ((rc = launch_row_stats(S, C, ntok, C, ln_eps, lns, st))) return rc;
     if ((rc = yolosod_a2_fused_run(S, lns, U, B, A * W, C, num_heads, prep, prep_bytes, st))) return rc;
   } else {

@@ -422,10 +422,13 @@ class A2_Attn(nn.Module):
         dt = x.dtype
         pw, at_w, fw = _as(self, "w", dt, pw, at.in_proj_weight, fw)
         pb, lw, lb, at_b, fb = _f32(self, "b", pb, self.layer_norm.weight, self.layer_norm.bias, at.in_proj_bias, fb)
-        srcs = (self.layer_norm.weight, self.layer_norm.bias, at.in_proj_weight, at.in_proj_bias)
-        # the fused LN / QKV / attention kernel's weight split with the LN affine folded, once per parameter version
+        pr = self.proj
+        srcs = (self.layer_norm.weight, self.layer_norm.bias, at.in_proj_weight, at.in_proj_bias, pr.conv.weight)
+        srcs += ((pr.bn.weight, pr.bn.bias, pr.bn.running_mean, pr.bn.running_var) if hasattr(pr, "bn")
+                 else (pr.conv.bias,))
+        # the fused kernels' weight split (proj conv; in_proj with the LN affine folded), once per parameter version
         prep = lambda: _cached(self, "a2prep", srcs, lambda: _hip.a2_prepare(  # noqa: E731
-            x, self.num_areas, self.num_heads, lw, lb, at_w, at_b))
+            x, self.num_areas, self.num_heads, pw, lw, lb, at_w, at_b))
         return _hip.a2_forward(x, self.num_areas, self.num_heads, pw, pb, lw, lb, self.layer_norm.eps, at_w, at_b,
                                None, None, fw, fb, prep=prep)
 
