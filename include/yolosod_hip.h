@@ -256,9 +256,6 @@ int yolosod_debug_split_f16(const float* v, uint32_t* h, uint32_t* l, long npair
  * reset, 0 if not, < 0 on error; synchronises `stream` first; reset != 0 clears it. A caller that sees 1 redoes the
  * work on the exact-fp32-MFMA kernels (the yolosod_debug_set_*(0) switches; DetectionPredictor does). */
 int yolosod_split_range_flag(int reset, void* stream);
-/* Test hook: the kernel of yolosod_gemm_bf16 / the bf16 operators' K-contiguous GEMMs without a LayerNorm prologue:
- * 0 (default; env YOLOSOD_GEMMB_GLDS) register-staged kernel, 3 / 2 LDS-DMA staged ring of 3 / 2 buffers. */
-void yolosod_debug_set_gemmb_glds(int mode);
 
 /* ---------------------------------------------------------------------------------------------------------------
  * bf16 model config (BASELINE configs[4]): `model.to(torch.bfloat16)` after fuse() - AutoBackend's fp16

@@ -69,7 +69,6 @@ SIGNATURES = {
     "yolosod_debug_set_a2_x2": (_i, [_i]),
     "yolosod_debug_set_gemm_x2": (None, [_i]),
     "yolosod_debug_split_f16": (_i, [_vp, _vp, _vp, _l, _vp]),
-    "yolosod_debug_set_gemmb_glds": (None, [_i]),
     "yolosod_swin_prep_bytes": (_sz, [_i, _i, _i]),
     "yolosod_split_range_flag": (_i, [_i, _vp]),
     "yolosod_swin_prepare": (_i, [_i, _i, _i] + [_vp] * 15 + [_f, _vp, _sz, _vp]),

@@ -32,7 +32,7 @@ constexpr float WSC = 64.0f;
 constexpr int HD = 64;          // head dim (the kernel's shape)
 constexpr int KS = 64;          // k stage (two 32-k MFMA steps)
 constexpr int PSA = KS + 8;     // activation plane row stride (halves): 9 16-byte quads, conflict-free b128 reads
-constexpr int PSQ = HD + 8;     // Q / K plane row stride
+constexpr int PSQ = HD + 4;     // Q / K plane row stride (34 dwords: the 8-byte fragment reads of 16 rows hit distinct bank pairs)
 constexpr int MAXTB = 10;       // token blocks of 16: L <= 160
 
 __device__ __forceinline__ f32x4 mfma16(f16x8_t a, f16x8_t b, f32x4 c) {
@@ -59,7 +59,7 @@ __global__ __launch_bounds__(512, 1) void a2_qkv_attn_kernel(Args p) {
   constexpr int NL = NTB * 16;          // padded tokens
   constexpr int APL = NL * PSA;         // activation plane (halves)
   constexpr int QPL = NL * PSQ;         // Q / K plane
-  constexpr int PSV = NL + 8;           // V^T row stride
+  constexpr int PSV = NL + 4;           // V^T row stride (an odd multiple of 2 dwords mod 32: conflict-free 8-byte reads)
   constexpr int VPL = HD * PSV;         // V^T plane
   constexpr int A_B = 2 * 2 * APL * 2;  // two buffers x two planes
   constexpr int QKV_B = (2 * QPL * 2 + 2 * VPL) * 2;
@@ -151,7 +151,7 @@ __global__ __launch_bounds__(512, 1) void a2_qkv_attn_kernel(Args p) {
     }
   }
   load_stage(sA, 0);
-  if (nstage > 1) load_stage(sB, 1);
+  load_stage(sB, nstage > 1 ? 1 : 0);
   __syncthreads();  // stats in LDS
   store_stage(sA, 0);
   auto mma = [&](const f16x8_t (&w)[3][2], int buf, int u) __attribute__((always_inline)) {
@@ -179,11 +179,13 @@ __global__ __launch_bounds__(512, 1) void a2_qkv_attn_kernel(Args p) {
   auto stage = [&](int s, float4 (&stored)[NIT], float4 (&next)[NIT]) __attribute__((always_inline)) {
     // entry: stage s is in buffer s & 1, `next` holds stage s + 1's loads in flight, `stored` is free
     const int buf = s & 1;
-    if (s + 2 < nstage) load_stage(stored, s + 2);
+    // unconditional (clamped) loads: a register set written on some trips only becomes a phi whose copies wait
+    // for the loads in flight
+    load_stage(stored, s + 2 < nstage ? s + 2 : nstage - 1);
     __syncthreads();  // stage s's planes stored; every wave is done with stage s - 1's buffer
     load_w(wb, 2 * s + 1);
     mma(wa, buf, 0);
-    if (s + 1 < nstage) load_w(wa, 2 * s + 2);
+    load_w(wa, s + 1 < nstage ? 2 * s + 2 : 2 * s + 1);
     mma(wb, buf, 1);
     if (s + 1 < nstage) store_stage(next, buf ^ 1);
   };
@@ -408,13 +410,14 @@ __global__ __launch_bounds__(512, 1) void a2_proj_pool_kernel(const float* __res
   auto step = [&](int s, float4 (&stored)[NIT][4], float4 (&next)[NIT][4]) __attribute__((always_inline)) {
     // entry: step s's planes are stored (buffer s & 1), `next` holds step s + 1's loads in flight, `stored` is free
     const int buf = s & 1;
-    if (s + 2 < nk32) load_step(stored, s + 2);
-    if (s + 1 < nk32) {
+    // unconditional (clamped) loads: a register set written on some trips only becomes a phi whose copies wait
+    // for the loads in flight
+    load_step(stored, s + 2 < nk32 ? s + 2 : nk32 - 1);
+    const int sw = s + 1 < nk32 ? s + 1 : nk32 - 1;
 #pragma unroll
-      for (int rb = 0; rb < 4; ++rb) {
-        wb[rb][0] = wfrag(rb, s + 1, 0);
-        wb[rb][1] = wfrag(rb, s + 1, 1);
-      }
+    for (int rb = 0; rb < 4; ++rb) {
+      wb[rb][0] = wfrag(rb, sw, 0);
+      wb[rb][1] = wfrag(rb, sw, 1);
     }
     __syncthreads();  // step s's planes stored; every wave is done with step s - 1's buffer
     const h16_t* b0 = Pl + (buf * 2) * PPL + l15 * PPS + 8 * g;
@@ -432,17 +435,15 @@ __global__ __launch_bounds__(512, 1) void a2_proj_pool_kernel(const float* __res
         }
       }
     }
-    if (s + 1 < nk32) {
-      store_step(next, buf ^ 1);
+    if (s + 1 < nk32) store_step(next, buf ^ 1);
 #pragma unroll
-      for (int rb = 0; rb < 4; ++rb) {
-        wa[rb][0] = wb[rb][0];
-        wa[rb][1] = wb[rb][1];
-      }
+    for (int rb = 0; rb < 4; ++rb) {
+      wa[rb][0] = wb[rb][0];
+      wa[rb][1] = wb[rb][1];
     }
   };
   load_step(sA, 0);
-  if (nk32 > 1) load_step(sB, 1);
+  load_step(sB, nk32 > 1 ? 1 : 0);
   store_step(sA, 0);
   for (int s = 0; s < nk32; s += 2) {
     step(s, sA, sB);
@@ -459,21 +460,24 @@ __global__ __launch_bounds__(512, 1) void a2_proj_pool_kernel(const float* __res
       if (cb < NCB) {
         const int px = cb * 16 + l15;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) Tt[(16 * rb + 4 * g + r) * HWP + px] = siluf_(acc[rb][j][r] * (1.0f / WSC) + bias[r]);
+        for (int r = 0; r < 4; ++r) Tt[(16 * rb + 4 * g + r) * HWP + px] = silu_fast_(acc[rb][j][r] * (1.0f / WSC) + bias[r]);
       }
     }
   }
   __syncthreads();
-  // pooled tokens: thread (c = tid % 64) averages its channel's bins in row order (as the reference's CPU pooling)
+  // pooled tokens: thread (c = tid % 64, column group tid / 64) averages its channel's bins in row order (as the
+  // reference's CPU pooling) for the columns w = tid / 64 + 8 i of every area
   const int c = tid & 63;
   const float* trow = Tt + c * HWP;
   float* Sb = S + (long)img * A * W * C + co + c;
-  for (int t = tid >> 6; t < A * W; t += NW) {
-    const int a = t / W, w = t - (t / W) * W;
+  for (int a = 0; a < A; ++a) {
     const int r0 = (a * H) / A, r1 = ((a + 1) * H + A - 1) / A;
-    float sum = 0.f;
-    for (int r = r0; r < r1; ++r) sum += trow[r * W + w];
-    Sb[(long)t * C] = sum / (float)(r1 - r0);
+    const float cnt = (float)(r1 - r0);
+    for (int w = tid >> 6; w < W; w += NW) {
+      float sum = 0.f;
+      for (int r = r0; r < r1; ++r) sum += trow[r * W + w];
+      Sb[(long)(a * W + w) * C] = sum / cnt;
+    }
   }
   range_report(range_flag, rng);
 }

@@ -500,161 +500,7 @@ __global__ __launch_bounds__(256, A_LN ? 2 : 3) void gemm_bf16_kernel(GemmB g) {
   }
 }
 
-// ---- LDS-DMA staged GEMM (both operands K-contiguous, no LayerNorm prologue) -------------------------------------
-// 128x128x64 tiles, 4 waves of 64x64 (4x4 v_mfma_f32_16x16x32_bf16 accumulators). Tiles reach LDS by
-// global_load_lds_dwordx4 (1 KB = 8 rows of one 64-k block per wave-instruction, no VGPR staging, no ds_write), into
-// NBUF ring buffers with NBUF-1 tiles in flight across each barrier (counted vmcnt, raw s_barrier). LDS images are
-// [row][64] (128-byte rows, lane-linear as the DMA writes them); the 16-byte chunk c of row r sits at chunk
-// c ^ ((r >> 1) & 7) - the swizzle is applied to the GLOBAL source address of each lane - so the 16 lanes of every
-// ds_read_b128 group read 16 different 16-byte bank slots. The MFMA takes the B fragment as its A operand, so a
-// lane's accumulator holds 4 consecutive output columns n of one row m: epilogue loads / stores are 8 bytes wide and
-// need no LDS staging. Tile order: bijective XCD-aware map (contiguous row-major tile ranges per XCD).
-template <int NBUF>
-__global__ __launch_bounds__(256, NBUF == 2 ? 2 : 1) void gemm_bf16_glds_kernel(GemmB g) {
-  constexpr int BM = 128, BN = 128, BK = 64;
-  constexpr int TILE = BM * BK;  // elements of one operand tile
-  __shared__ __attribute__((aligned(16))) bf16_t smem[NBUF * 2 * TILE];
-
-  // bijective XCD remap: blocks b and b + 8 share an XCD; give each XCD a contiguous range of tiles
-  const int nwg = gridDim.x;
-  const int q = nwg >> 3, rr = nwg & 7, xcd = blockIdx.x & 7;
-  const int t = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (blockIdx.x >> 3);
-  if (t >= g.tiles) return;
-  const int m0 = (t / g.tiles_n) * BM, n0 = (t % g.tiles_n) * BN;
-
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
-  const int bz = blockIdx.z;
-  const bf16_t* A = g.A + (long)bz * g.a_bs;
-  const bf16_t* B = g.B + (long)bz * g.b_bs;
-  const int M = g.M, N = g.N, K = g.K;
-
-  // this lane's DMA sources: wave w fills rows [32w, 32w + 32) of both tiles, 8 rows per instruction; lane -> row
-  // 32w + 8i + (lane >> 3), physical chunk lane & 7 = logical chunk (lane & 7) ^ swz(row)
-  const bf16_t* srcA[4];
-  const bf16_t* srcB[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int row = 32 * wid + 8 * i + (lane >> 3);
-    const int chunk = (lane & 7) ^ ((row >> 1) & 7);
-    const int ma = min(m0 + row, M - 1), nb = min(n0 + row, N - 1);  // clamped rows: finite data, results dropped
-    srcA[i] = A + (long)ma * g.lda + 8 * chunk;
-    srcB[i] = B + (long)nb * g.ldb + 8 * chunk;
-  }
-  auto issue = [&](int kb) {
-    bf16_t* dA = smem + (kb % NBUF) * 2 * TILE;
-    bf16_t* dB = dA + TILE;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      __builtin_amdgcn_global_load_lds((const void*)(srcA[i] + kb * BK),
-                                       (__attribute__((address_space(3))) void*)(dA + (32 * wid + 8 * i) * BK), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(srcB[i] + kb * BK),
-                                       (__attribute__((address_space(3))) void*)(dB + (32 * wid + 8 * i) * BK), 16, 0, 0);
-    }
-  };
-
-  f32x4 acc[4][4];  // [n block j][m block i]: lane (g, r) holds out[m = .. + 16 i + r][n = .. + 16 j + 4 g .. + 3]
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int r = lane & 15, gq = lane >> 4;
-  const int sw = (r >> 1) & 7;  // swizzle of every row this lane reads (rows 16 i + r)
-  const int nk = K / BK;
-#pragma unroll
-  for (int p = 0; p < NBUF - 1; ++p)
-    if (p < nk) issue(p);
-  for (int kb = 0; kb < nk; ++kb) {
-    // tile kb has landed (this wave's DMAs: everything but the NBUF-2 younger tiles' 8 instructions each), every
-    // wave's too (barrier), and every wave has finished reading the buffer the next issue overwrites
-    if (NBUF == 3) {
-      if (kb + 1 < nk) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    if (kb + NBUF - 1 < nk) issue(kb + NBUF - 1);
-    const bf16_t* tA = smem + (kb % NBUF) * 2 * TILE + (wm * 64 + r) * BK;
-    const bf16_t* tB = smem + (kb % NBUF) * 2 * TILE + TILE + (wn * 64 + r) * BK;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int ch = ((4 * s + gq) ^ sw) * 8;
-      bf16x8_t a[4], b[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) a[i] = *reinterpret_cast<const bf16x8_t*>(tA + i * 16 * BK + ch);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const bf16x8_t*>(tB + j * 16 * BK + ch);
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[j][i], 0, 0, 0);
-    }
-  }
-
-  // epilogue straight from the accumulators: out[m][n .. n+3]
-  const EpiB& e = g.epi;
-  const bf16_t* resb = e.res ? e.res + (long)bz * e.res_bs : nullptr;
-  bf16_t* outb = e.out + (long)bz * e.out_bs;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int m = m0 + wm * 64 + 16 * i + r;
-    uint2 rv[4];
-    if (!e.swin && resb) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int n = n0 + wn * 64 + 16 * j + 4 * gq;
-        rv[j] = (m < M && n < N) ? *reinterpret_cast<const uint2*>(resb + (long)m * e.ldr + n) : make_uint2(0u, 0u);
-      }
-    }
-    const float bm_ = (e.bias_mode == 1 && m < M) ? e.bias[m] : 0.f;
-    const float sc_m = (e.bn_mode == 1 && m < M) ? e.scale[m] : 1.f, sh_m = (e.bn_mode == 1 && m < M) ? e.shift[m] : 0.f;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = n0 + wn * 64 + 16 * j + 4 * gq;
-      if (m >= M || n >= N) continue;
-      f32x4 v = acc[j][i];
-      if (e.bias_mode == 1) v += bm_;
-      else if (e.bias_mode == 2) v += *reinterpret_cast<const f32x4*>(e.bias + n);
-      if (e.bn_mode == 1) v = v * sc_m + sh_m;
-      else if (e.bn_mode == 2)
-        v = v * *reinterpret_cast<const f32x4*>(e.scale + n) + *reinterpret_cast<const f32x4*>(e.shift + n);
-      v.x = act_b(v.x, e.act); v.y = act_b(v.y, e.act); v.z = act_b(v.z, e.act); v.w = act_b(v.w, e.act);
-      if (!e.swin) {
-        if (resb)
-          v += f32x4{__uint_as_float(rv[j].x << 16), __uint_as_float(rv[j].x & 0xffff0000u),
-                     __uint_as_float(rv[j].y << 16), __uint_as_float(rv[j].y & 0xffff0000u)};
-        st4(outb + (long)m * e.ldc + n, v);
-      } else {
-        // Swin: n = token of the padded raster [img][Hp][Wp], m = channel; out / res NCHW, padding tokens cropped
-        const long per_img = (long)e.sw_Hp * e.sw_Wp;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const long tok = n + u;
-          const int img = (int)(tok / per_img);
-          const int rr2 = (int)(tok - img * per_img);
-          const int h = rr2 / e.sw_Wp, w = rr2 - (rr2 / e.sw_Wp) * e.sw_Wp;
-          if (h < e.sw_H && w < e.sw_W) {
-            const long o = ((long)img * M + m) * e.sw_H * e.sw_W + (long)h * e.sw_W + w;
-            e.out[o] = f2bf(v[u] + (e.res ? bf2f(e.res[o]) : 0.f));
-          }
-        }
-      }
-    }
-  }
-}
-
 static inline bool al_b(const void* p, int bytes) { return ((uintptr_t)p & (bytes - 1)) == 0; }
-
-// 0 (default): the register-staged kernel for every call; 3 / 2: the LDS-DMA kernel with a ring of 3 / 2 buffers for
-// the K-contiguous calls (env YOLOSOD_GEMMB_GLDS; test hook yolosod_debug_set_gemmb_glds). Measured at the L9_m shapes
-// (scripts/bench_gemm.py --bf16, random operands): register-staged 475-640 TF/s, ring of 2 410-590, ring of 3 (one
-// workgroup per CU) 270-400 - the LDS-DMA form stays opt-in until it is the faster one
-inline int& gemmb_glds_mode() {
-  static int m = [] { const char* e = getenv("YOLOSOD_GEMMB_GLDS"); return e ? atoi(e) : 0; }();
-  return m;
-}
 
 static inline int launch_gemm_bf16(const GemmB& g0, int batch, bool b_kc, hipStream_t st) {
   GemmB g = g0;
@@ -686,19 +532,6 @@ static inline int launch_gemm_bf16(const GemmB& g0, int batch, bool b_kc, hipStr
     }                                                                                                           \
   } while (0)
   YS_CHECK_ARG(b_kc || !ln, "gemm_bf16: LN prologue needs a K-contiguous B");
-  // LDS-DMA staged kernel: both operands K-contiguous, no LN prologue, 4-wide epilogue columns (YOLOSOD_GEMMB_GLDS=0:
-  // the register-staged kernel below for every call, for A/B)
-  const int glds = gemmb_glds_mode();
-  if (glds && b_kc && !ln && g.N % 4 == 0 && (e.swin || g.epi.vec) && (e.bias_mode != 2 || al_b(e.bias, 16)) &&
-      (e.bn_mode != 2 || (al_b(e.scale, 16) && al_b(e.shift, 16)))) {
-    g.tiles_n = (g.N + 127) / 128;
-    g.tiles = g.tiles_n * ((g.M + 127) / 128);
-    const dim3 grid((unsigned)g.tiles, 1, batch);
-    if (glds == 2) hipLaunchKernelGGL(gemm_bf16_glds_kernel<2>, grid, dim3(256), 0, st, g);
-    else hipLaunchKernelGGL(gemm_bf16_glds_kernel<3>, grid, dim3(256), 0, st, g);
-    YS_CHECK_LAUNCH("gemm_bf16_glds");
-    return 0;
-  }
   // 128x64 tiles when N is narrow or 128x128 would leave CUs idle; 128x128 otherwise
   const long t128 = (long)((g.M + 127) / 128) * ((g.N + 127) / 128) * batch;
   static const int force = [] { const char* e = getenv("YOLOSOD_GEMMB_TILE"); return e ? atoi(e) : 0; }();

@@ -419,7 +419,6 @@ YS_EXPORT int yolosod_gemm_bf16(const bf16_t* A, long a_bs, int lda, const bf16_
 
 // Test hook: which bf16 GEMM kernel takes the K-contiguous calls (3 / 2: LDS-DMA ring of 3 / 2 buffers, 0: register
 // staged).
-YS_EXPORT void yolosod_debug_set_gemmb_glds(int mode) { gemmb_glds_mode() = mode; }
 
 // Test hook: attention over contiguous sequences of L rows of a [n_seq*L][3C] bf16 QKV matrix -> [n_seq*L][C].
 YS_EXPORT int yolosod_attention_bf16(const bf16_t* qkv, bf16_t* out, long n_seq, int L, int C, int heads,
