@@ -231,56 +231,7 @@ def load_traffic():
     return None
 
 
-# statistics a producing conv epilogue emits for the gate that consumes its output (nn/tasks.py): the gate's own
-# kernels then read x once; the producer's extra time over the plain epilogue of the same shape is billed to the gate
-PRODUCER_GATE = {"sum": "se", "summax": "cbam", "capool": "ca"}
-
-
-def _event_ms(fn, reps=10, warm=3):
-    ts = []
-    for i in range(reps + warm):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        fn()
-        e1.record()
-        if i >= warm:
-            ts.append((e0, e1))
-    torch.cuda.synchronize()
-    return _median([a.elapsed_time(b) for a, b in ts])
-
-
-def producer_extra(agg, dev, dtype):
-    """{(gate op, gate input shape): (extra ms per launch, producer description)} for every producing epilogue that
-    emitted a gate's statistics in the timed region: its stats variant and its plain variant, timed back to back
-    on fresh tensors of the same shape after the timed region (HIP events on the current stream)."""
-    out = {}
-    for key in agg:
-        op, shape, extra = key[:3]
-        if op == "bias_act" and extra in PRODUCER_GATE:
-            y = torch.randn(shape, device=dev).to(dtype)
-            bias = torch.randn(shape[1], device=dev)
-            o = torch.empty_like(y)
-            t_st = _event_ms(lambda: _hip.bias_act(y, bias, 1, out=o, stats=extra))
-            t_pl = _event_ms(lambda: _hip.bias_act(y, bias, 1, out=o))
-            gate, gshape = PRODUCER_GATE[extra], tuple(shape)
-        elif op == "conv1x1_thin" and isinstance(extra, tuple) and extra[1] in ("sum", "summax"):
-            B, Cin, H, W = shape
-            cout = extra[0]
-            x = torch.randn(shape, device=dev)
-            w = torch.randn(cout, Cin, device=dev) * 0.05
-            bias = torch.randn(cout, device=dev)
-            o = torch.empty((B, cout, H, W), device=dev)
-            t_st = _event_ms(lambda: _hip.conv1x1_thin(x, w, bias, out=o, stats=extra[1]))
-            t_pl = _event_ms(lambda: _hip.conv1x1_thin(x, w, bias, out=o))
-            gate, gshape = PRODUCER_GATE[extra[1]], (B, cout, H, W)
-        else:
-            continue
-        out[(gate, gshape)] = (max(0.0, t_st - t_pl), f"{op}{tuple(shape)} {extra}: {t_st:.4f} ms with the "
-                                                      f"statistics vs {t_pl:.4f} ms plain")
-    return out
-
-
-def measure(name, world, rank, dev, steps, warmup, conf, extra_billing=True):
+def measure(name, world, rank, dev, steps, warmup, conf, ops_csv=None):
     """One config: warmup, K timed steps (barrier + synchronize on both sides, max over ranks), per-operator HIP
     event timings -> rooflines. Returns (result dict, predictor)."""
     cfg_yaml, imgsz, bs, label, dtype = CONFIGS[name]
@@ -321,37 +272,11 @@ def measure(name, world, rank, dev, steps, warmup, conf, extra_billing=True):
     elapsed = float(elapsed.item())
     durs = timer.durations_ms()
 
-    # per-operator live timings (HIP events on the launch stream) -> roofline of the dominant operator
-    agg = {}
-    for key, ms in durs:
-        a = agg.setdefault(key, [0.0, 0])
-        a[0] += ms
-        a[1] += 1
-    billed = producer_extra(agg, dev, dtype) if extra_billing else {}
-    ops, backbone = [], []
-    for key, (tot, n) in agg.items():
-        if key[0] not in perf.PATH_OPS:  # backbone conv kernels of this library: outside the path roofline
-            backbone.append({"op": key[0], "shape": list(key[1]), "extra": str(key[2]), "launches": n,
-                             "total_ms_per_step": round(tot / steps, 4)})
-            continue
-        nbytes, flops = perf.op_cost(key)
-        kern = tot / n
-        ext, src = billed.get((key[0], tuple(key[1])), (0.0, None))
-        avg = kern + ext
-        bound = perf.bound_of(key)
-        tm, tm_d = perf.t_min_ms(key, method=True), perf.t_min_ms(key)
-        o = {"op": key[0], "shape": list(key[1]), "dtype": "bf16" if perf.elem_size(key) == 2 else "f32",
-             "launches": n, "avg_ms": round(avg, 4), "kernels_ms": round(kern, 4),
-             "total_ms_per_step": round(avg * n / steps, 4),
-             "GBps": round(nbytes / (avg * 1e-3) / 1e9, 1), "TFLOPs": round(flops / (avg * 1e-3) / 1e12, 2),
-             "bound": bound, "peak": perf.method_peak_tflops(key) if bound == "mfma" else perf.PEAK_HBM_GBS,
-             "t_min_ms": round(tm, 4), "frac": round(tm / avg, 3), "frac_vs_dtype_peak": round(tm_d / avg, 3),
-             "bytes": nbytes, "flops": flops, "key": key}
-        if src:
-            o["producer_extra_ms"] = round(ext, 4)
-            o["producer"] = src
-        ops.append(o)
-    ops.sort(key=lambda o: -o["total_ms_per_step"])
+    # per-operator live timings (HIP events on the launch stream) -> roofline of the dominant operator; the
+    # producer billing uses the same region's launches only (perf.producer_billing)
+    if ops_csv is not None:
+        ops_csv.extend(perf.calls_to_rows(name, steps, durs))
+    ops, backbone, path_roofline = perf.summarize(durs, steps)
     dom = ops[0]
     bound = dom["bound"]
     if bound == "mfma":
@@ -375,30 +300,19 @@ def measure(name, world, rank, dev, steps, warmup, conf, extra_billing=True):
         roofline["frac_vs_dtype_peak"] = round(achieved / dpeak, 4)
         roofline["dtype_peak"] = dpeak
 
-    # path-level roofline = sum_k t_k^min / sum_k t_k^meas over every hot-path operator,
-    # t_k^min = max(bytes_k / HBM peak, flops_k / matrix ceiling of the method the op computes with)
-    t_meas = sum(o["total_ms_per_step"] for o in ops)
-    t_min = sum(perf.t_min_ms(o["key"], method=True) * o["launches"] / steps for o in ops)
-    t_min_d = sum(perf.t_min_ms(o["key"]) * o["launches"] / steps for o in ops)
-    path_roofline = {"t_min_ms": round(t_min, 4), "t_meas_ms": round(t_meas, 4),
-                     "frac": round(t_min / t_meas, 4) if t_meas else None,
-                     "definition": "sum over hot-path ops of max(bytes / 8 TB/s, flops / matrix ceiling of the "
-                                   "method the op computes with: fp16 peak / 3 = 838.9 TF/s for the fp32 ops on "
-                                   "fp16 two-term splits, 2516.6 for bf16, 157.3 for exact fp32 MFMA) / measured; "
-                                   "a producing epilogue's extra time for a gate's statistics is billed to the gate",
-                     "frac_vs_dtype_peak": round(t_min_d / t_meas, 4) if t_meas else None}
+    t_meas = path_roofline["t_meas_ms"]
     value = world * bs * steps / elapsed
     res = {"value": round(value, 2), "unit": "images/s", "ms_per_step": round(elapsed / steps * 1e3, 3),
            "steps": steps, "warmup": warmup, "dtype": dname,
            "data": f"synthetic: torch.rand images in HBM, seed-0 random-init weights of {label}",
-           "config": {"workload": f"{label} {imgsz}x{imgsz}, {bs} images per GPU, fused {dname} "
+           "config": {"name": name, "workload": f"{label} {imgsz}x{imgsz}, {bs} images per GPU, fused {dname} "
                                   f"forward + decode + NMS(conf={conf}, iou=0.7)",
                       "imgsz": imgsz, "batch_per_gpu": bs, "global_batch": bs * world, "parallelism": f"dp{world}"},
            "roofline": roofline, "path_roofline": path_roofline,
            "hip_ops_ms_per_step": round(t_meas, 3),
            "hip_ops": [{k: v for k, v in o.items() if k not in ("bytes", "flops", "key")} for o in ops],
            "backbone_hip_ms_per_step": round(sum(o["total_ms_per_step"] for o in backbone), 3),
-           "backbone_hip_ops": sorted(backbone, key=lambda o: -o["total_ms_per_step"])[:12]}
+           "backbone_hip_ops": backbone[:12]}
     return res, predictor, cfg_yaml, imgsz
 
 
@@ -417,6 +331,9 @@ def main():
     ap.add_argument("--no-nms-load", action="store_true")
     ap.add_argument("--no-extra-configs", action="store_true", help="skip the m640 / n1280 blocks (N = 1 only)")
     ap.add_argument("--miopen-benchmark", action="store_true", help="torch.backends.cudnn.benchmark (MIOpen find)")
+    ap.add_argument("--ops-csv", default=None,
+                    help="write every timed C-ABI launch (HIP event ms, rank 0) of every config to this CSV: "
+                         "scripts/roofline_from_csv.py recomputes hip_ops / producer billing / path_roofline from it")
     args = ap.parse_args()
     if args.miopen_benchmark:
         torch.backends.cudnn.benchmark = True
@@ -431,7 +348,9 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    head, predictor, cfg_yaml, imgsz = measure(args.config, world, rank, dev, args.steps, args.warmup, args.conf)
+    rows = [] if args.ops_csv and rank == 0 else None
+    head, predictor, cfg_yaml, imgsz = measure(args.config, world, rank, dev, args.steps, args.warmup, args.conf,
+                                               ops_csv=rows)
     result = {"metric": METRIC, "value": head["value"], "unit": "images/s", "n_gpus": world, "steps": args.steps,
               "warmup": args.warmup, "ms_per_step": head["ms_per_step"], "higher_is_better": True,
               "scaling": "weak", "vs_baseline": None}
@@ -446,7 +365,7 @@ def main():
         # configs[3] (n1280 bs 8) and configs[4] (m640 bf16 bs 64): their own timed regions, same contract
         result["configs"] = {}
         for name in EXTRA_CONFIGS:
-            sub, pred, _, _ = measure(name, 1, 0, dev, args.steps, args.warmup, args.conf)
+            sub, pred, _, _ = measure(name, 1, 0, dev, args.steps, args.warmup, args.conf, ops_csv=rows)
             result["configs"][name] = sub
             del pred
             torch.cuda.empty_cache()
@@ -461,6 +380,12 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    if rows is not None:
+        import csv
+        with open(args.ops_csv, "w", newline="") as f:
+            w = csv.DictWriter(f, fieldnames=perf.CSV_FIELDS)
+            w.writeheader()
+            w.writerows(rows)
     if rank == 0:
         print(json.dumps(result), flush=True)
 

@@ -1,0 +1,65 @@
+"""perf.summarize: the hip_ops / producer billing / path roofline bench.py reports, recomputed from per-launch rows
+(CPU only; the numbers are synthetic)."""
+import pytest
+
+import yolosod_import  # noqa: F401
+from yolosod_amd import perf
+
+CAP = ("bias_act", (32, 128, 80, 80), "capool")
+PLAIN = ("bias_act", (32, 128, 80, 80), None)
+PLAIN_RES = ("bias_act", (32, 128, 80, 80), "res")
+CA = ("ca", (32, 128, 80, 80), 8)
+SE_PROD = ("bias_act", (32, 32, 320, 320), "sum")
+SE = ("se", (32, 32, 320, 320), 8)
+THIN = ("conv1x1_thin", (32, 96, 160, 160), (64, "summax"))
+THIN_PLAIN = ("conv1x1_thin", (32, 96, 160, 160), (64, False, False))
+CBAM = ("cbam", (32, 64, 160, 160), 4)
+
+
+def _calls():
+    return [(CAP, 0.13), (PLAIN, 0.06), (PLAIN, 0.065), (PLAIN_RES, 0.5), (CA, 0.08),
+            (SE_PROD, 0.15), (SE, 0.17), (THIN, 0.19), (THIN_PLAIN, 0.16), (CBAM, 0.13)]
+
+
+def _by_op(ops):
+    return {(o["op"], tuple(o["shape"])): o for o in ops}
+
+
+def test_producer_billed_from_the_same_region():
+    ops, backbone, path = perf.summarize(_calls(), steps=1)
+    o = _by_op(ops)
+    # CA: in-model capool minus the mean of the in-model plain launches without a residual (the "res" one excluded)
+    assert o[("ca", CA[1])]["producer_extra_ms"] == pytest.approx(0.13 - 0.0625, abs=1e-4)
+    assert o[("ca", CA[1])]["avg_ms"] == pytest.approx(0.08 + 0.0675, abs=1e-4)
+    # CBAM on the thin conv: stats variant minus the plain variant of the same shape and Cout
+    assert o[("cbam", CBAM[1])]["producer_extra_ms"] == pytest.approx(0.03, abs=1e-4)
+    # SE: no plain variant of that shape in the region -> plain pass priced at the HBM roof (upper bound)
+    roof = 2 * 32 * 32 * 320 * 320 * 4 / 8e12 * 1e3
+    assert o[("se", SE[1])]["producer_extra_ms"] == pytest.approx(0.15 - roof, abs=1e-4)
+    assert "HBM roof" in o[("se", SE[1])]["producer"]
+    assert {b["op"] for b in backbone} == {"bias_act", "conv1x1_thin"}
+    t_meas = sum(x["total_ms_per_step"] for x in ops)
+    assert path["t_meas_ms"] == pytest.approx(t_meas, abs=1e-3)
+    assert path["frac"] == pytest.approx(path["t_min_ms"] / path["t_meas_ms"], abs=1e-3)
+
+
+def test_csv_rows_round_trip_keys_exactly():
+    calls = _calls() + [(("bias_act", (8, 64, 40, 40), "summax+res", 2), 0.02), (("cbam", (8, 64, 40, 40), 4, 2), 0.03),
+                        (("swin", (32, 64, 160, 160), (2, 7, 256)), 0.5), (("nms", (32, 10, 34000), 300), 0.03)]
+    rows = perf.calls_to_rows("n640", 10, calls)
+    assert [r["seq"] for r in rows] == list(range(len(calls)))
+    assert perf.rows_to_calls(rows) == calls
+    a = perf.summarize(calls, 10)
+    b = perf.summarize(perf.rows_to_calls(rows), 10)
+    assert [(o["op"], o["avg_ms"], o.get("producer_extra_ms")) for o in a[0]] == \
+        [(o["op"], o["avg_ms"], o.get("producer_extra_ms")) for o in b[0]]
+
+
+def test_bf16_residual_producer_pairs_with_its_plain_residual_variant():
+    prod = ("bias_act", (8, 64, 40, 40), "summax+res", 2)
+    plain = ("bias_act", (8, 64, 40, 40), "res", 2)
+    gate, gshape, pkey, nbytes = perf.producer_of(prod)
+    assert (gate, gshape, pkey) == ("cbam", (8, 64, 40, 40), plain)
+    assert nbytes == 3 * 8 * 64 * 40 * 40 * 2
+    billed = perf.producer_billing(perf.aggregate([(prod, 0.05), (plain, 0.04), (plain, 0.02)]))
+    assert billed[("cbam", (8, 64, 40, 40))][0] == pytest.approx(0.02)

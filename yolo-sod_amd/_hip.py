@@ -529,16 +529,23 @@ def bias_act(y, bias, act, out=None, res=None, stats=None, out2=None, c2lo=0):
     rb = bstride(res, "res") if res is not None else 0
     rp = None if res is None else res.data_ptr()
     bp = _dev(bias, "bias")
+    # op_timer key: extra = variant (+ "+res" with a shortcut input); bf16 launches carry the element size 2
+    tail = (2,) if bf else ()
+    rs = "" if res is None else "+res"
+
+    def key(variant):
+        return ("bias_act", tuple(y.shape), (variant + rs) if variant else (rs[1:] or None)) + tail
+
     if out2 is not None and stats is None:  # ``out2`` = packed copy of channels [c2lo, C) (next conv's input)
         if (out2.device.type != "cuda" or out2.dtype != dt or tuple(out2.shape) != (B, C - c2lo, H, W)
                 or out2.stride(3) != 1 or out2.stride(2) != W or out2.stride(1) != HW):
             raise RuntimeError(f"bias_act: out2 must be a {dt} GPU tensor [B, C - c2lo, H, W] with contiguous channels")
         if bf:
-            _check(_launch(("bias_act", tuple(y.shape), "dual"), y.device, lib.yolosod_bias_act_bf16, y.data_ptr(), yb,
+            _check(_launch(key("dual"), y.device, lib.yolosod_bias_act_bf16, y.data_ptr(), yb,
                            out.data_ptr(), ob, bp, rp, rb, out2.data_ptr(), out2.stride(0), int(c2lo), B, C, HW,
                            int(act), _stream(y.device)), "bias_act_bf16")
         else:
-            _check(_launch(("bias_act", tuple(y.shape), "dual"), y.device, lib.yolosod_bias_act_dual, y.data_ptr(), yb,
+            _check(_launch(key("dual"), y.device, lib.yolosod_bias_act_dual, y.data_ptr(), yb,
                            out.data_ptr(), ob, bp, rp, rb, out2.data_ptr(), out2.stride(0), int(c2lo), B, C, HW,
                            int(act), _stream(y.device)), "bias_act_dual")
         return out
@@ -548,7 +555,7 @@ def bias_act(y, bias, act, out=None, res=None, stats=None, out2=None, c2lo=0):
         else:
             yin = torch.empty((B, C, H + W), dtype=torch.float32, device=y.device)
             fn = lib.yolosod_bias_act_capool_bf16 if bf else lib.yolosod_bias_act_capool
-            _check(_launch(("bias_act", tuple(y.shape), "capool"), y.device, fn, y.data_ptr(), yb, out.data_ptr(), ob,
+            _check(_launch(key("capool"), y.device, fn, y.data_ptr(), yb, out.data_ptr(), ob,
                            bp, rp, rb, B, C, H, W, int(act), yin.data_ptr(), _stream(y.device)), "bias_act_capool")
             out._ys_ca_pool = (yin, tuple(out.shape))
             return out
@@ -557,17 +564,17 @@ def bias_act(y, bias, act, out=None, res=None, stats=None, out2=None, c2lo=0):
         psum = torch.empty(B * C * parts, dtype=torch.float32, device=y.device)
         pmax = torch.empty_like(psum) if stats == "summax" else None
         fn = lib.yolosod_bias_act_stats_bf16 if bf else lib.yolosod_bias_act_stats
-        _check(_launch(("bias_act", tuple(y.shape), stats), y.device, fn, y.data_ptr(), yb, out.data_ptr(), ob, bp,
+        _check(_launch(key(stats), y.device, fn, y.data_ptr(), yb, out.data_ptr(), ob, bp,
                        rp, rb, B, C, HW, int(act), parts, seg, psum.data_ptr(),
                        None if pmax is None else pmax.data_ptr(), _stream(y.device)), "bias_act_stats")
         out._ys_plane_stats = PlaneStats(psum, pmax, parts, out.shape)
         return out
     if bf:
-        _check(_launch(("bias_act", tuple(y.shape), None), y.device, lib.yolosod_bias_act_bf16, y.data_ptr(), yb,
+        _check(_launch(key(None), y.device, lib.yolosod_bias_act_bf16, y.data_ptr(), yb,
                        out.data_ptr(), ob, bp, rp, rb, None, 0, 0, B, C, HW, int(act), _stream(y.device)),
                "bias_act_bf16")
         return out
-    _check(_launch(("bias_act", tuple(y.shape), None), y.device, lib.yolosod_bias_act, y.data_ptr(), yb, out.data_ptr(),
+    _check(_launch(key(None), y.device, lib.yolosod_bias_act, y.data_ptr(), yb, out.data_ptr(),
                    ob, bp, rp, rb, B, C, HW, int(act), _stream(y.device)), "bias_act")
     return out
 

@@ -129,3 +129,134 @@ def t_min_ms(key, method: bool = False) -> float:
     nbytes, flops = op_cost(key)
     peak = method_peak_tflops(key) if method else peak_tflops(key)
     return max(nbytes / (PEAK_HBM_GBS * 1e9), flops / (peak * 1e12)) * 1e3
+
+
+# ---- hot-path summary of one timed region (bench.py, scripts/roofline_from_csv.py) --------------------------------
+
+# statistics a producing conv epilogue emits for the gate that consumes its output (nn/tasks.py): the gate's own
+# kernels then read x once; the producer's extra time over its plain variant is billed to the gate
+PRODUCER_GATE = {"sum": "se", "summax": "cbam", "capool": "ca"}
+
+
+def _numel(shape) -> int:
+    n = 1
+    for d in shape:
+        n *= d
+    return n
+
+
+def producer_of(key):
+    """For a launch key of a producing epilogue that emitted a gate's statistics: (gate op, gate input shape, key of
+    the plain variant of the same shape, HBM bytes of the plain pass); None for any other key."""
+    op, shape, extra = key[:3]
+    tail, E = tuple(key[3:]), elem_size(key)
+    if op == "bias_act" and isinstance(extra, str) and extra.split("+")[0] in PRODUCER_GATE:
+        st, res = extra.split("+")[0], extra.endswith("+res")
+        plain = ("bias_act", tuple(shape), "res" if res else None) + tail
+        return PRODUCER_GATE[st], tuple(shape), plain, _numel(shape) * E * (3 if res else 2)
+    if op == "conv1x1_thin" and isinstance(extra, tuple) and len(extra) == 2 and extra[1] in ("sum", "summax"):
+        B, cin, H, W = shape
+        cout = extra[0]
+        plain = ("conv1x1_thin", tuple(shape), (cout, False, False)) + tail
+        return PRODUCER_GATE[extra[1]], (B, cout, H, W), plain, B * H * W * (cin + cout) * E
+    return None
+
+
+def aggregate(calls):
+    """[(key, ms), ...] per launch -> {key: [total ms, launches]} in first-seen order."""
+    agg = {}
+    for key, ms in calls:
+        a = agg.setdefault(key, [0.0, 0])
+        a[0] += ms
+        a[1] += 1
+    return agg
+
+
+def producer_billing(agg):
+    """{(gate op, gate shape): (extra ms per launch, description)} from the SAME timed region: the producer's mean
+    in-model time minus the mean in-model time of its plain variant of the same shape (same element type, same
+    residual input). When the model runs no plain variant of that shape, the plain pass is priced at the HBM roof
+    (plain bytes / 8 TB/s), which bills the gate an upper bound of the producer's extra time."""
+    out = {}
+    for key, (tot, n) in agg.items():
+        p = producer_of(key)
+        if p is None:
+            continue
+        gate, gshape, plain, pbytes = p
+        t_st = tot / n
+        if plain in agg:
+            t_pl = agg[plain][0] / agg[plain][1]
+            basis = f"its in-model plain variant, {agg[plain][1]} launches"
+        else:
+            t_pl = pbytes / (PEAK_HBM_GBS * 1e9) * 1e3
+            basis = "plain pass at the HBM roof (no plain variant of this shape in the model)"
+        out[(gate, gshape)] = (max(0.0, t_st - t_pl),
+                               f"{key[0]}{tuple(key[1])} {key[2]}: {t_st:.4f} ms in-model vs {t_pl:.4f} ms ({basis})")
+    return out
+
+
+def summarize(calls, steps):
+    """Per-operator summary of one timed region's launches: (ops, backbone ops, path_roofline). ``ops`` carry the
+    cost-model fields (bytes, flops, key) beside the reported ones; avg_ms = the operator's own launch sequence + the
+    billed producer extra; path_roofline = sum_k t_k^min / sum_k t_k^meas."""
+    agg = aggregate(calls)
+    billed = producer_billing(agg)
+    ops, backbone = [], []
+    for key, (tot, n) in agg.items():
+        if key[0] not in PATH_OPS:  # backbone conv kernels of this library: outside the path roofline
+            backbone.append({"op": key[0], "shape": list(key[1]), "extra": str(key[2]), "launches": n,
+                             "total_ms_per_step": round(tot / steps, 4)})
+            continue
+        nbytes, flops = op_cost(key)
+        kern = tot / n
+        ext, src = billed.get((key[0], tuple(key[1])), (0.0, None))
+        avg = kern + ext
+        bound = bound_of(key)
+        tm, tm_d = t_min_ms(key, method=True), t_min_ms(key)
+        o = {"op": key[0], "shape": list(key[1]), "dtype": "bf16" if elem_size(key) == 2 else "f32",
+             "launches": n, "avg_ms": round(avg, 4), "kernels_ms": round(kern, 4),
+             "total_ms_per_step": round(avg * n / steps, 4),
+             "GBps": round(nbytes / (avg * 1e-3) / 1e9, 1), "TFLOPs": round(flops / (avg * 1e-3) / 1e12, 2),
+             "bound": bound, "peak": method_peak_tflops(key) if bound == "mfma" else PEAK_HBM_GBS,
+             "t_min_ms": round(tm, 4), "frac": round(tm / avg, 3), "frac_vs_dtype_peak": round(tm_d / avg, 3),
+             "bytes": nbytes, "flops": flops, "key": key}
+        if src:
+            o["producer_extra_ms"] = round(ext, 4)
+            o["producer"] = src
+        ops.append(o)
+    ops.sort(key=lambda o: -o["total_ms_per_step"])
+    t_meas = sum(o["total_ms_per_step"] for o in ops)
+    t_min = sum(t_min_ms(o["key"], method=True) * o["launches"] / steps for o in ops)
+    t_min_d = sum(t_min_ms(o["key"]) * o["launches"] / steps for o in ops)
+    path = {"t_min_ms": round(t_min, 4), "t_meas_ms": round(t_meas, 4),
+            "frac": round(t_min / t_meas, 4) if t_meas else None,
+            "definition": "sum over hot-path ops of max(bytes / 8 TB/s, flops / matrix ceiling of the method the op "
+                          "computes with: fp16 peak / 3 = 838.9 TF/s for the fp32 ops on fp16 two-term splits, 2516.6 "
+                          "for bf16, 157.3 for exact fp32 MFMA) / measured; a producing epilogue's extra time for a "
+                          "gate's statistics (in-model producer minus its in-model plain variant of the same shape) is "
+                          "billed to the gate",
+            "frac_vs_dtype_peak": round(t_min_d / t_meas, 4) if t_meas else None}
+    return ops, sorted(backbone, key=lambda o: -o["total_ms_per_step"]), path
+
+
+# ---- per-launch CSV (bench.py --ops-csv): one row per timed C-ABI launch sequence ---------------------------------
+
+CSV_FIELDS = ("config", "steps", "seq", "op", "shape", "extra", "esize", "ms")
+
+
+def calls_to_rows(config, steps, calls):
+    return [{"config": config, "steps": steps, "seq": i, "op": k[0], "shape": "x".join(map(str, k[1])),
+             "extra": repr(k[2]), "esize": k[3] if len(k) > 3 else "", "ms": f"{ms:.6f}"}
+            for i, (k, ms) in enumerate(calls)]
+
+
+def rows_to_calls(rows):
+    """CSV rows of one config -> [(key, ms)] exactly as the op_timer recorded them."""
+    import ast
+    out = []
+    for r in rows:
+        key = (r["op"], tuple(int(d) for d in r["shape"].split("x")), ast.literal_eval(r["extra"]))
+        if r["esize"] != "":
+            key = key + (int(r["esize"]),)
+        out.append((key, float(r["ms"])))
+    return out
