@@ -220,7 +220,8 @@ __global__ __launch_bounds__(256) void channel_gate_kernel(const float* __restri
 // ------------------------------------------------------------------------------------------------
 // (3a) SE apply: y = x * gate[b][c]. Vector path: grid = (ceil(HW / 1024), ceil(C / 8), images), a lane scales
 // 4 pixels in 8 consecutive channel planes - 8 independent vector loads in flight before the first store (the
-// 4-deep per-plane version streamed at ~4 TB/s, this shape at ~6 like cbam_apply). Scalar path otherwise.
+// 4-deep per-plane version streamed at ~4 TB/s, this shape at ~6 like cbam_apply), issued before the fused gate MLP.
+// Scalar path otherwise.
 // FUSED: the workgroup computes the gates of its 8 channels itself from the plane partials (gate_mlp), so SE is
 // one launch after its producer; dynamic LDS = (2*C + 136) floats.
 // ------------------------------------------------------------------------------------------------
@@ -235,6 +236,16 @@ __global__ __launch_bounds__(256) void plane_scale_kernel(const T* __restrict__ 
   const int b = rev ? gridDim.z - 1 - blockIdx.z : blockIdx.z;
   const int c0 = (rev ? gridDim.y - 1 - blockIdx.y : blockIdx.y) * 8;
   const int n = (C - c0 < 8) ? C - c0 : 8;
+  // vector path with 8 channels: the lane's 8 loads go out before the gate MLP (they do not depend on it), so its
+  // latency chain overlaps them instead of preceding them
+  const long p4 = ((long)blockIdx.x * 256 + threadIdx.x) * 4;
+  const bool pre = (HW & 3) == 0 && n == 8 && p4 < HW;
+  f32x4 v[8];
+  if (pre) {
+    const T* xb = x + ((long)b * C + c0) * HW + p4;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = ld4(xb + (long)u * HW);
+  }
   const float* gb;
   if (FUSED) {
     float* g = sh + 2 * C + 128;
@@ -249,9 +260,6 @@ __global__ __launch_bounds__(256) void plane_scale_kernel(const T* __restrict__ 
     const T* xb = x + ((long)b * C + c0) * HW + p;
     T* yb = y + ((long)b * C + c0) * HW + p;
     if (n == 8) {
-      f32x4 v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = ld4(xb + (long)u * HW);
 #pragma unroll
       for (int u = 0; u < 8; ++u) st4(yb + (long)u * HW, v[u] * gb[u]);
     } else {
@@ -359,6 +367,63 @@ __global__ __launch_bounds__(256) void cbam_pixel_stats_kernel(const T* __restri
     }
     sp[0] = s;
     sp[HW] = m;
+  }
+}
+
+// CBAM pass 2, wave-split form (V = 4 with the fused gate; default, YOLOSOD_CBAM_PS2=0 selects the form above): a
+// workgroup takes 256 pixels of one 32-channel group; wave w takes channels c0 + 8w .. +8 of the group, each lane 4
+// pixels. A lane issues all 8 of its 16-byte loads before the channel gate is computed, so the HBM stream overlaps the
+// gate's latency chain (the form above keeps 32 channels per lane, 8 of them in flight across the gate, and at
+// HW = 1600 leaves 44 % of its second pixel block idle); the 4 waves' partial sum / max meet in LDS in wave order
+// (fixed: batch-invariant). grid = (ceil(HW / 256), G, images); dynamic LDS = (3*C + 128 + 2048) floats.
+template <class T>
+__global__ __launch_bounds__(256) void cbam_pixel_stats_ws_kernel(const T* __restrict__ x, float* __restrict__ ca,
+                                                                  int C, int CG, long HW, float* __restrict__ mpart,
+                                                                  const float* __restrict__ psum,
+                                                                  const float* __restrict__ pmax, int parts,
+                                                                  float inv_hw, const float* __restrict__ w1,
+                                                                  const float* __restrict__ w2, int hid) {
+  extern __shared__ float sh[];  // avg[C] | mx[C] | hsh[128] | gate[C] | red[2][4][256]
+  const int b = blockIdx.z, g = blockIdx.y, G = gridDim.y;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int c0 = g * CG;
+  const int c1 = (c0 + CG < C) ? c0 + CG : C;
+  const int cw0 = c0 + 8 * wv;
+  const int nw = (c1 - cw0 < 8) ? (c1 - cw0 > 0 ? c1 - cw0 : 0) : 8;  // this wave's channels [cw0, cw0 + nw)
+  const long p = ((long)blockIdx.x * 64 + lane) * 4;
+  const bool pv = p < HW;
+  f32x4 v[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u)
+    v[u] = (pv && u < nw) ? ld4(x + ((long)b * C + cw0 + u) * HW + p) : f32x4{0.f, 0.f, 0.f, 0.f};
+  float* gs = sh + 2 * C + 128;
+  gate_mlp<true>(psum, pmax, parts, C, inv_hw, w1, nullptr, w2, nullptr, hid, b, sh, sh + C, sh + 2 * C, c0, c1 - c0,
+                 gs);
+  if (blockIdx.x == 0)
+    for (int i = tid; i < c1 - c0; i += 256) ca[(long)b * C + c0 + i] = gs[i];
+  f32x4 s = {0.f, 0.f, 0.f, 0.f}, m = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+  for (int u = 0; u < 8; ++u)
+    if (u < nw) {
+      const f32x4 o = gs[8 * wv + u] * v[u];
+      s += o;
+      m.x = fmaxf(m.x, o.x); m.y = fmaxf(m.y, o.y); m.z = fmaxf(m.z, o.z); m.w = fmaxf(m.w, o.w);
+    }
+  float* red = gs + C;
+  *reinterpret_cast<f32x4*>(red + wv * 256 + 4 * lane) = s;
+  *reinterpret_cast<f32x4*>(red + 1024 + wv * 256 + 4 * lane) = m;
+  __syncthreads();
+  const long px = (long)blockIdx.x * 256 + tid;
+  if (px < HW) {
+    float ss = red[tid], mm = red[1024 + tid];
+#pragma unroll
+    for (int w = 1; w < 4; ++w) {
+      ss += red[w * 256 + tid];
+      mm = fmaxf(mm, red[1024 + w * 256 + tid]);
+    }
+    float* sp = mpart + ((long)(b * G + g) * 2) * HW;
+    sp[px] = ss;
+    sp[HW + px] = mm;
   }
 }
 
@@ -691,6 +756,48 @@ __global__ __launch_bounds__(256) void ca_apply_kernel(const T* __restrict__ x, 
   }
 }
 
+// CA pass 3, one workgroup per fp32 plane (W % 4 == 0; default, YOLOSOD_CA_APPLY2=0 selects the form above): the
+// plane's gate row [a_h | a_w] is staged in LDS and the plane streams in 16-byte accesses, each thread's (up to 8 per
+// round) loads issued before the first is used; the form above keeps one load in flight per thread and ran at
+// ~3.9 TB/s on the n640 plane (80 x 80). Same expression: (x * a_w[w]) * a_h[h]. dynamic LDS = (H + W) floats.
+__global__ __launch_bounds__(256) void ca_apply_plane_kernel(const float* __restrict__ x, float* __restrict__ y,
+                                                             const float* __restrict__ gate, int H, int W) {
+  extern __shared__ float gsh[];
+  const long plane = blockIdx.x;
+  const long HW = (long)H * W;
+  const int L = H + W, tid = threadIdx.x;
+  const float* g = gate + plane * L;
+  const float* xp = x + plane * HW;
+  float* yp = y + plane * HW;
+  const long n4 = HW >> 2;
+  for (int i = tid; i < L; i += 256) gsh[i] = g[i];
+  for (long i0 = 0; i0 < n4; i0 += 8 * 256) {
+    f32x4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const long i = i0 + tid + 256 * u;
+      if (i < n4) v[u] = ld4(xp + 4 * i);
+    }
+    if (i0 == 0) __syncthreads();  // the gate row is staged (the plane's first loads are already in flight)
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const long i = i0 + tid + 256 * u;
+      if (i < n4) {
+        const long e = 4 * i;
+        const int h = (int)(e / W), w = (int)(e - (long)h * W);
+        const float ah = gsh[h];
+        const float* aw = gsh + H + w;
+        f32x4 o;
+        o.x = (v[u].x * aw[0]) * ah;
+        o.y = (v[u].y * aw[1]) * ah;
+        o.z = (v[u].z * aw[2]) * ah;
+        o.w = (v[u].w * aw[3]) * ah;
+        st4(yp + e, o);
+      }
+    }
+  }
+}
+
 }  // namespace ys
 
 using namespace ys;
@@ -830,6 +937,7 @@ static int cbam_forward_impl(const T* x, T* y, int B, int C, int H, int W, const
   // every channel block, cost more than the sa launch they replace)
   static const bool sa_apply = [] { const char* e = getenv("YOLOSOD_CBAM_SA_APPLY"); return e && atoi(e) != 0; }();
   const size_t sa_lds = sa_apply ? sizeof(float) * 2 * (size_t)cbam_sa_rows(W, V) * (W + 6) : SIZE_MAX;
+  static const bool ps2 = [] { const char* e = getenv("YOLOSOD_CBAM_PS2"); return !e || atoi(e) != 0; }();
   for (int b0 = 0; b0 < B; b0 += ipc) {
     const int nb = (B - b0 < ipc) ? B - b0 : ipc;
     const long off = (long)b0 * C * HW;
@@ -841,7 +949,12 @@ static int cbam_forward_impl(const T* x, T* y, int B, int C, int H, int W, const
       hipLaunchKernelGGL((plane_part_stats_kernel<true, T>), dim3((unsigned)(nb * C * pp.parts)), dim3(256), 0, st,
                          x + off, HW, pp.parts, pp.seg, psum + (long)b0 * C * pp.parts, pmax + (long)b0 * C * pp.parts);
     dim3 gs((unsigned)pxb, G, nb);
-    if (fused) {  // channel gate computed inside the pixel-statistics workgroups
+    if (fused && ps2) {  // channel gate inside the pixel-statistics workgroups, 8 channels per wave
+      const size_t lds2 = sizeof(float) * (3 * (size_t)C + 128 + 2048);
+      hipLaunchKernelGGL((cbam_pixel_stats_ws_kernel<T>), dim3((unsigned)((HW + 255) / 256), G, nb), dim3(256), lds2,
+                         st, x + off, cab, C, kCbamGroup, HW, mpart, ps, pm, pp.parts, 1.0f / (float)HW, fc0_w, fc2_w,
+                         hidden);
+    } else if (fused) {  // channel gate computed inside the pixel-statistics workgroups
       hipLaunchKernelGGL((cbam_pixel_stats_kernel<4, T, true>), gs, dim3(256), lds, st, x + off, cab, C, kCbamGroup,
                          HW, mpart, ps, pm, pp.parts, 1.0f / (float)HW, fc0_w, fc2_w, hidden);
     } else {
@@ -938,6 +1051,7 @@ static int ca_forward_impl(const T* x, T* y, int B, int C, int H, int W, const f
   const int VA = (sizeof(T) == 2 && W % 8 == 0) ? 8 : V;
   const unsigned apply_y = (unsigned)((HW + 256 * VA - 1) / (256 * VA));
   const int ipc = images_per_chunk(B, (size_t)C * HW * sizeof(T));
+  static const bool apply2 = [] { const char* e = getenv("YOLOSOD_CA_APPLY2"); return !e || atoi(e) != 0; }();
   for (int b0 = 0; b0 < B; b0 += ipc) {
     const int nb = (B - b0 < ipc) ? B - b0 : ipc;
     const long off = (long)b0 * C * HW;
@@ -948,7 +1062,10 @@ static int ca_forward_impl(const T* x, T* y, int B, int C, int H, int W, const f
                        (yin_pre ? yin_pre : yin) + goff, C, H, W,
                        mip, conv1_w, conv1_b, bn_w, bn_b, bn_mean, bn_var, bn_eps, convh_w, convh_b, convw_w, convw_b,
                        gate + goff);
-    if (VA == 8)
+    if (sizeof(T) == 4 && V == 4 && apply2)
+      hipLaunchKernelGGL(ca_apply_plane_kernel, dim3(nb * C), dim3(256), sizeof(float) * (size_t)(H + W), st,
+                         (const float*)(x + off), (float*)(y + off), gate + goff, H, W);
+    else if (VA == 8)
       hipLaunchKernelGGL((ca_apply_kernel<8, T>), dim3(nb * C, apply_y), dim3(256), 0, st, x + off, y + off,
                          gate + goff, H, W);
     else if (V == 4)
