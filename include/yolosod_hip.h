@@ -246,6 +246,10 @@ int yolosod_debug_set_a2_x2(int on);
  * proj + SiLU + pooling, then LN + QKV + attention, csrc/a2_fused.hip) or the decomposed GEMM path (0). */
 int yolosod_debug_set_a2_fused(int on);
 void yolosod_debug_set_gemm_x2(int on);
+/* Test hook: the bf16 decomposed SwinBlock's depthwise conv + token layout and LN1 in one pass
+ * (swin_tokens_ln_bf16_kernel, 1, default; env YOLOSOD_SWIN_TOKLN=0 turns it off) or as two kernels (0);
+ * bit-identical. Returns the previous state. */
+int yolosod_debug_set_swin_tokln(int on);
 /* Test hook: the fp16 two-term split of the fp32-accurate matrix kernels (common.h split2) on npair pairs of v:
  * h[i] = the fp16 pair (fp16(v[2i]), fp16(v[2i+1])), l[i] = (fp16(v[2i] - h.lo), fp16(v[2i+1] - h.hi)), as 2 x 16-bit
  * patterns per uint32 (low half = even element). Device pointers. */

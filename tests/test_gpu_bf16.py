@@ -111,6 +111,28 @@ def test_bf16_m_scale_shapes_vs_oracle(name, cuda, monkeypatch):
         assert bool((d <= lim).all()), f"{name}: worst ratio {float((d / lim).max()):.2f}"
 
 
+@pytest.mark.parametrize("shape", [(2, 512, 40, 40), (1, 256, 24, 16), (2, 1024, 16, 8)],
+                         ids=["L9_m", "c256_24x16", "c1024_16x8"])
+def test_swin_bf16_tokens_ln_pass_is_bit_identical(shape, cuda, monkeypatch):
+    """The decomposed bf16 SwinBlock with the depthwise conv + token layout + LN1 in one pass
+    (swin_tokens_ln_bf16_kernel) equals the two-kernel form bit for bit (same expressions, same sum order)."""
+    from yolosod_amd import _hip
+    lib = _hip.load_library()
+    name = "swin_L9_m"
+    B, C, H, W = shape
+    # C >= 256 takes the decomposed path (the fused per-window bf16 kernel covers C 64 / 128); head dim <= 128
+    monkeypatch.setitem(recipes.OPS, name, ("SwinBlock", (C, max(4, C // 128), 7), shape))
+    x = recipes.make_input(name, shape)
+    prev = lib.yolosod_debug_set_swin_tokln(1)
+    try:
+        a = _gpu_bf16(name, x, cuda)
+        lib.yolosod_debug_set_swin_tokln(0)
+        b = _gpu_bf16(name, x, cuda)
+    finally:
+        lib.yolosod_debug_set_swin_tokln(prev)
+    assert torch.equal(a, b), f"max|d| {float((a - b).abs().max()):.3g}"
+
+
 @pytest.mark.parametrize("M_,N,K,bkc", [(300, 192, 64, True), (1000, 64, 128, True), (129, 768, 256, True),
                                          (517, 200, 1024, True), (256, 1536, 512, True),
                                          (512, 400, 512, False), (64, 1600, 64, False), (130, 136, 64, False)])

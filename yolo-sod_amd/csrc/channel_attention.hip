@@ -228,6 +228,7 @@ __global__ __launch_bounds__(256) void channel_gate_kernel(const float* __restri
 template <class T, bool FUSED>
 __global__ __launch_bounds__(256) void plane_scale_kernel(const T* __restrict__ x, T* __restrict__ y,
                                                           const float* __restrict__ gate, int C, long HW, int rev,
+                                                          int se_pre,
                                                           const float* __restrict__ psum, int parts, float inv_hw,
                                                           const float* __restrict__ w1, const float* __restrict__ b1,
                                                           const float* __restrict__ w2, const float* __restrict__ b2,
@@ -239,7 +240,7 @@ __global__ __launch_bounds__(256) void plane_scale_kernel(const T* __restrict__ 
   // vector path with 8 channels: the lane's 8 loads go out before the gate MLP (they do not depend on it), so its
   // latency chain overlaps them instead of preceding them
   const long p4 = ((long)blockIdx.x * 256 + threadIdx.x) * 4;
-  const bool pre = (HW & 3) == 0 && n == 8 && p4 < HW;
+  const bool pre = se_pre && (HW & 3) == 0 && n == 8 && p4 < HW;
   f32x4 v[8];
   if (pre) {
     const T* xb = x + ((long)b * C + c0) * HW + p4;
@@ -260,6 +261,10 @@ __global__ __launch_bounds__(256) void plane_scale_kernel(const T* __restrict__ 
     const T* xb = x + ((long)b * C + c0) * HW + p;
     T* yb = y + ((long)b * C + c0) * HW + p;
     if (n == 8) {
+      if (!pre) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = ld4(xb + (long)u * HW);
+      }
 #pragma unroll
       for (int u = 0; u < 8; ++u) st4(yb + (long)u * HW, v[u] * gb[u]);
     } else {
@@ -370,7 +375,7 @@ __global__ __launch_bounds__(256) void cbam_pixel_stats_kernel(const T* __restri
   }
 }
 
-// CBAM pass 2, wave-split form (V = 4 with the fused gate; default, YOLOSOD_CBAM_PS2=0 selects the form above): a
+// CBAM pass 2, wave-split form (V = 4 with the fused gate; opt-in, YOLOSOD_CBAM_PS2=1; measured no faster): a
 // workgroup takes 256 pixels of one 32-channel group; wave w takes channels c0 + 8w .. +8 of the group, each lane 4
 // pixels. A lane issues all 8 of its 16-byte loads before the channel gate is computed, so the HBM stream overlaps the
 // gate's latency chain (the form above keeps 32 channels per lane, 8 of them in flight across the gate, and at
@@ -756,7 +761,7 @@ __global__ __launch_bounds__(256) void ca_apply_kernel(const T* __restrict__ x, 
   }
 }
 
-// CA pass 3, one workgroup per fp32 plane (W % 4 == 0; default, YOLOSOD_CA_APPLY2=0 selects the form above): the
+// CA pass 3, one workgroup per fp32 plane (W % 4 == 0; opt-in, YOLOSOD_CA_APPLY2=1, see ca_forward_impl): the
 // plane's gate row [a_h | a_w] is staged in LDS and the plane streams in 16-byte accesses, each thread's (up to 8 per
 // round) loads issued before the first is used; the form above keeps one load in flight per thread and ran at
 // ~3.9 TB/s on the n640 plane (80 x 80). Same expression: (x * a_w[w]) * a_h[h]. dynamic LDS = (H + W) floats.
@@ -842,6 +847,8 @@ static int se_forward_impl(const T* x, T* y, int B, int C, int H, int W, const f
   const size_t lds_fused = sizeof(float) * (2 * (size_t)C + 136);
   const bool fused = fused_gates() && lds_fused <= 64 * 1024;
   YS_CHECK_ARG(lds <= 64 * 1024 || fused, "se: C=%d too large for the gate kernel", C);
+  // the fused apply's 8 loads per lane issued before the gate MLP (YOLOSOD_SE_PRE=0: after it)
+  static const int se_pre = [] { const char* e = getenv("YOLOSOD_SE_PRE"); return (!e || atoi(e) != 0) ? 1 : 0; }();
   for (int b0 = 0; b0 < B; b0 += ipc) {
     const int nb = (B - b0 < ipc) ? B - b0 : ipc;
     const long off = (long)b0 * C * HW;
@@ -852,12 +859,12 @@ static int se_forward_impl(const T* x, T* y, int B, int C, int H, int W, const f
     const dim3 grid((unsigned)xchunks, (unsigned)((C + 7) / 8), (unsigned)nb);
     if (fused) {
       hipLaunchKernelGGL((plane_scale_kernel<T, true>), grid, dim3(256), lds_fused, st, x + off, y + off, nullptr, C, HW,
-                         mall_reverse(), ps, pp.parts, 1.0f / (float)HW, fc1_w, fc1_b, fc2_w, fc2_b, hidden);
+                         mall_reverse(), se_pre, ps, pp.parts, 1.0f / (float)HW, fc1_w, fc1_b, fc2_w, fc2_b, hidden);
     } else {
       hipLaunchKernelGGL((channel_gate_kernel<false>), dim3(nb), dim3(256), lds, st, ps, nullptr, pp.parts, C,
                          1.0f / (float)HW, fc1_w, fc1_b, fc2_w, fc2_b, hidden, gate + (long)b0 * C);
       hipLaunchKernelGGL((plane_scale_kernel<T, false>), grid, dim3(256), 0, st, x + off, y + off, gate + (long)b0 * C,
-                         C, HW, mall_reverse(), nullptr, 0, 0.f, nullptr, nullptr, nullptr, nullptr, 0);
+                         C, HW, mall_reverse(), 0, nullptr, 0, 0.f, nullptr, nullptr, nullptr, nullptr, 0);
     }
   }
   YS_CHECK_LAUNCH("se");
@@ -937,7 +944,8 @@ static int cbam_forward_impl(const T* x, T* y, int B, int C, int H, int W, const
   // every channel block, cost more than the sa launch they replace)
   static const bool sa_apply = [] { const char* e = getenv("YOLOSOD_CBAM_SA_APPLY"); return e && atoi(e) != 0; }();
   const size_t sa_lds = sa_apply ? sizeof(float) * 2 * (size_t)cbam_sa_rows(W, V) * (W + 6) : SIZE_MAX;
-  static const bool ps2 = [] { const char* e = getenv("YOLOSOD_CBAM_PS2"); return !e || atoi(e) != 0; }();
+  // 8 channels per wave (opt-in, YOLOSOD_CBAM_PS2=1): measured level at L18 and 3 % slower at L4 in the model
+  static const bool ps2 = [] { const char* e = getenv("YOLOSOD_CBAM_PS2"); return e && atoi(e) != 0; }();
   for (int b0 = 0; b0 < B; b0 += ipc) {
     const int nb = (B - b0 < ipc) ? B - b0 : ipc;
     const long off = (long)b0 * C * HW;
@@ -1051,7 +1059,10 @@ static int ca_forward_impl(const T* x, T* y, int B, int C, int H, int W, const f
   const int VA = (sizeof(T) == 2 && W % 8 == 0) ? 8 : V;
   const unsigned apply_y = (unsigned)((HW + 256 * VA - 1) / (256 * VA));
   const int ipc = images_per_chunk(B, (size_t)C * HW * sizeof(T));
-  static const bool apply2 = [] { const char* e = getenv("YOLOSOD_CA_APPLY2"); return !e || atoi(e) != 0; }();
+  // one workgroup per plane (opt-in, YOLOSOD_CA_APPLY2=1): faster alone (CA 0.079 -> 0.057 ms with the Detect towers
+  // on one stream) but 2x slower in the model while the towers' MIOpen convs run on the side stream (0.19-0.21 vs
+  // 0.08-0.09 ms same-box, profiles/r04_channel_ab/): its 4096 long-lived workgroups lose the CUs to the conv
+  static const bool apply2 = [] { const char* e = getenv("YOLOSOD_CA_APPLY2"); return e && atoi(e) != 0; }();
   for (int b0 = 0; b0 < B; b0 += ipc) {
     const int nb = (B - b0 < ipc) ? B - b0 : ipc;
     const long off = (long)b0 * C * HW;

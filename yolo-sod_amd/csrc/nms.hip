@@ -4,29 +4,24 @@
 // torchvision==0.20.1 ops.nms (CPU kernel: stable descending score sort, strict IoU > thr, area without +1);
 // classes are separated by offsetting boxes with cls * max_wh (ops.py:289,295).
 //
-// Design (no host sync; the per-image candidate count lives on the device). Three launches; a phase that needs every
-// workgroup of an image done runs in the image's LAST-ARRIVING workgroup (release fence + agent-scope atomic counter,
-// acquire fence; no workgroup ever waits on another, so no co-residency is assumed):
-//   nms_prep            4 anchors per thread (16-byte loads when A % 4 == 0): xywh -> xyxy (optionally in place, as
-//                       the reference mutates its input), candidate class mask (score > conf, class filter, best class
-//                       or multi-label), and the candidate count of each 1024-anchor block; zeroes the image's
-//                       arrival counters.
-//   nms_scatter_select  order-preserving compaction of the (anchor, class) candidates (= the reference's row order)
-//                       over the whole GPU: each block sums its image's preceding block counts for its offset and
-//                       scatters (~score bits, anchor*nc+class). The image's last block then selects: the score order
-//                       of the first <= KCAP candidates, sorted in LDS. For n <= KCAP a stable LSD radix sort of all;
-//                       for n > KCAP a radix *select* first finds the key T such that the keys below T (at most KCAP of
-//                       them) are exactly a prefix of the stable sorted order, and only that prefix is sorted. Writes
-//                       the prefix's class-offset boxes / areas / ids.
-//   nms_mask_resolve    (row block x image) workgroups: the upper-triangular IoU > thr bitmask of the prefix, one 64-bit
-//                       word per (row, 64-column block) - the quadratic work spread over every CU. The image's last
-//                       workgroup then resolves: greedy in score order over the bitmask, 64 rows staged in LDS at a
-//                       time, only alive candidates visited (bit scan); stops at max_det. Only if the prefix is
-//                       exhausted before max_det boxes are kept and more candidates exist (keys >= T) does it sort
-//                       that remainder and continue with the chunked in-LDS greedy (each chunk of 512 tested against
-//                       the kept boxes, then its own IoU bitmask). Kept rows are written in parallel.
-// An image without candidates costs the read of its scores and two near-empty workgroup passes (the five-launch form
-// spent ~4-5 us per launch on an empty batch).
+// Design (no host sync; the per-image candidate count lives on the device):
+//   nms_prep    one thread per anchor: xywh -> xyxy (optionally in place, as the reference mutates its input),
+//               candidate class mask (score > conf, class filter, best class or multi-label), and the candidate
+//               count of each 256-anchor block.
+//   nms_scatter order-preserving compaction of the (anchor, class) candidates (= the reference's row order) over
+//               the whole GPU: each block sums its image's preceding block counts for its offset and scatters
+//               (~score bits, anchor*nc+class).
+//   nms_select  one 512-thread workgroup per image: the score order of the first <= KCAP candidates, sorted in
+//               LDS. For n <= KCAP a stable LSD radix sort of all; for n > KCAP a radix *select* first finds the
+//               key T such that the keys below T (at most KCAP of them) are exactly a prefix of the stable sorted
+//               order, and only that prefix is sorted. Writes the prefix's class-offset boxes / areas / ids.
+//   nms_mask    1024 workgroups (row block x image): the upper-triangular IoU > thr bitmask of the prefix, one
+//               64-bit word per (row, 64-column block) - the quadratic work spread over every CU.
+//   nms_resolve one workgroup per image: greedy in score order over the bitmask, 64 rows staged in LDS at a time,
+//               only alive candidates visited (bit scan); stops at max_det. Only if the prefix is exhausted before
+//               max_det boxes are kept and more candidates exist (keys >= T) does it sort that remainder and
+//               continue with the chunked in-LDS greedy (each chunk of 512 tested against the kept boxes, then
+//               its own IoU bitmask). Kept rows are written in parallel.
 #include "common.h"
 #include <math.h>
 #include <stdlib.h>
@@ -61,9 +56,7 @@ struct NmsArgs {
   unsigned* spos;                // [B][KCAP] anchor * nc + class
   unsigned long long* mask;      // [B][KCAP][KW]
   int* meta;                     // [B][4]: n, neff, K (prefix length), T (prefix = keys < T)
-  int* blkcnt;                   // [B][nblk_a] candidates per ANB-anchor block (prep)
-  int* arrive;                   // [B][2] arrival counters of the scatter / mask workgroups (zeroed by nms_prep)
-  int vec4;                      // A % 4 == 0 and pred 16-byte aligned: 16-byte score loads in nms_prep
+  int* blkcnt;                   // [B][nblk_a] candidates per 256-anchor block (prep), then exclusive offsets
   float* out;                    // [B][max_det][6]
   int* counts;                   // [B]
   int* out_index;                // [B][max_det]  (anchor index)
@@ -78,133 +71,64 @@ struct NmsArgs {
 
 __device__ __forceinline__ int block256_exclusive_scan(int v, int* wsum4, int* total);
 
-constexpr int PA = 4;          // anchors per nms_prep thread
-constexpr int ANB = 256 * PA;  // anchors per nms_prep / nms_scatter_select block
-
-// PA consecutive values of row `row` of the image's [4+nc][A] prediction, from anchor a0 (zeros past A)
-__device__ __forceinline__ void ld_rowpa(const float* pb, long row, long A, long a0, bool v4, float (&v)[PA]) {
-  if (v4) {
-    const float4 t = *reinterpret_cast<const float4*>(pb + row * A);
-    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
-  } else {
-#pragma unroll
-    for (int u = 0; u < PA; ++u) v[u] = (a0 + u < A) ? pb[row * A + u] : 0.f;
-  }
-}
-
-// Also the candidate count of this ANB-anchor block (the ordered compaction's per-block counts). Only candidate
+// also the candidate count of this 256-anchor block (the ordered compaction's per-block counts). Only candidate
 // anchors' xyxy boxes are stored (every later reader indexes candidates), and the block's candidate masks only when
-// it has any (nms_scatter_select skips blocks whose count is 0). Every score of the thread's PA anchors is loaded
-// before the first is compared (8 classes x 16 bytes in flight per step).
+// it has any (nms_scatter skips blocks whose count is 0): an image without candidates costs the read of its scores
+// plus the in-place rewrite the reference's in_place=True asks for.
 __global__ __launch_bounds__(256) void nms_prep_kernel(NmsArgs g) {
   __shared__ int wsum4[4];
   const int b = blockIdx.y;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {  // the later launches' arrival counters (stream order publishes them)
-    g.arrive[2 * b] = 0;
-    g.arrive[2 * b + 1] = 0;
-  }
-  const long A = g.A;
-  const long a0 = (long)blockIdx.x * ANB + (long)threadIdx.x * PA;
-  unsigned long long mask[PA];
-  float4 box[PA];
-#pragma unroll
-  for (int u = 0; u < PA; ++u) {
-    mask[u] = 0ull;
-    box[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-  if (a0 < A) {
-    float* pb = g.pred + (long)b * (4 + g.nc) * A + a0;
-    const bool v4 = g.vec4 && a0 + PA <= A;
-    float cx[PA], cy[PA], w[PA], h[PA];
-    ld_rowpa(pb, 0, A, a0, v4, cx);
-    ld_rowpa(pb, 1, A, a0, v4, cy);
-    ld_rowpa(pb, 2, A, a0, v4, w);
-    ld_rowpa(pb, 3, A, a0, v4, h);
-    float best[PA];
-    int bj[PA];
-#pragma unroll
-    for (int u = 0; u < PA; ++u) {
-      best[u] = -INFINITY;
-      bj[u] = 0;
+  const int a = blockIdx.x * 256 + threadIdx.x;
+  unsigned long long mask = 0ull;
+  float4 box = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (a < g.A) {
+    float* pb = g.pred + (long)b * (4 + g.nc) * g.A + a;
+    const long As = g.A;
+    const float cx = pb[0], cy = pb[As], w = pb[2 * As], h = pb[3 * As];
+    const float hw = w / 2.0f, hh = h / 2.0f;
+    const float x1 = cx - hw, y1 = cy - hh, x2 = cx + hw, y2 = cy + hh;
+    if (g.in_place) {
+      pb[0] = x1;
+      pb[As] = y1;
+      pb[2 * As] = x2;
+      pb[3 * As] = y2;
     }
-    for (int j0 = 0; j0 < g.nc; j0 += 8) {  // 8 classes x PA anchors of scores in flight, then scanned in class order
-      float sv[8][PA];
+    box = make_float4(x1, y1, x2, y2);
+    float best = -INFINITY;
+    int bj = 0;
+    for (int j0 = 0; j0 < g.nc; j0 += 8) {  // 8 score loads in flight, then scanned in class order
+      float sv[8];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        if (j0 + q < g.nc) ld_rowpa(pb, 4 + j0 + q, A, a0, v4, sv[q]);
-        else {
+      for (int u = 0; u < 8; ++u) sv[u] = (j0 + u < g.nc) ? pb[(4 + j0 + u) * As] : -INFINITY;
 #pragma unroll
-          for (int u = 0; u < PA; ++u) sv[q][u] = -INFINITY;
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int j = j0 + q;
+      for (int u = 0; u < 8; ++u) {
+        const int j = j0 + u;
         if (j < g.nc) {
-#pragma unroll
-          for (int u = 0; u < PA; ++u) {
-            const float sc = sv[q][u];
-            if (sc > best[u]) {  // strict: first maximal index wins (torch max(dim) / amax)
-              best[u] = sc;
-              bj[u] = j;
-            }
-            if (g.multi_label && sc > g.conf) mask[u] |= 1ull << j;
+          const float s = sv[u];
+          if (s > best) {  // strict: first maximal index wins (torch max(dim) / amax)
+            best = s;
+            bj = j;
           }
+          if (g.multi_label && s > g.conf) mask |= 1ull << j;
         }
       }
     }
-    unsigned long long allow = ~0ull;
-    if (g.classes) {
-      allow = 0ull;
+    if (!g.multi_label) mask = (best > g.conf) ? (1ull << bj) : 0ull;
+    if (mask && g.classes) {
+      unsigned long long allow = 0ull;
       for (int k = 0; k < g.n_classes; ++k) {
         const int c = g.classes[k];
         if (c >= 0 && c < 64) allow |= 1ull << c;
       }
-    }
-    float x1[PA], y1[PA], x2[PA], y2[PA];
-#pragma unroll
-    for (int u = 0; u < PA; ++u) {
-      const float hw = w[u] / 2.0f, hh = h[u] / 2.0f;
-      x1[u] = cx[u] - hw;
-      y1[u] = cy[u] - hh;
-      x2[u] = cx[u] + hw;
-      y2[u] = cy[u] + hh;
-      box[u] = make_float4(x1[u], y1[u], x2[u], y2[u]);
-      if (!g.multi_label) mask[u] = (best[u] > g.conf) ? (1ull << bj[u]) : 0ull;
-      mask[u] &= allow;
-      if (a0 + u >= A) mask[u] = 0ull;
-    }
-    if (g.in_place) {
-      if (v4) {
-        *reinterpret_cast<float4*>(pb) = make_float4(x1[0], x1[1], x1[2], x1[3]);
-        *reinterpret_cast<float4*>(pb + A) = make_float4(y1[0], y1[1], y1[2], y1[3]);
-        *reinterpret_cast<float4*>(pb + 2 * A) = make_float4(x2[0], x2[1], x2[2], x2[3]);
-        *reinterpret_cast<float4*>(pb + 3 * A) = make_float4(y2[0], y2[1], y2[2], y2[3]);
-      } else {
-#pragma unroll
-        for (int u = 0; u < PA; ++u)
-          if (a0 + u < A) {
-            pb[u] = x1[u];
-            pb[A + u] = y1[u];
-            pb[2 * A + u] = x2[u];
-            pb[3 * A + u] = y2[u];
-          }
-      }
+      mask &= allow;
     }
   }
-  int cnt = 0;
-#pragma unroll
-  for (int u = 0; u < PA; ++u) cnt += __popcll(mask[u]);
   int total;
-  (void)block256_exclusive_scan(cnt, wsum4, &total);
+  (void)block256_exclusive_scan(__popcll(mask), wsum4, &total);
   if (threadIdx.x == 0) g.blkcnt[(long)b * gridDim.x + blockIdx.x] = total;
-  if (total != 0) {
-#pragma unroll
-    for (int u = 0; u < PA; ++u)
-      if (a0 + u < A) {
-        g.amask[(long)b * A + a0 + u] = mask[u];
-        if (mask[u]) g.boxes[(long)b * A + a0 + u] = box[u];
-      }
+  if (total != 0 && a < g.A) {
+    g.amask[(long)b * g.A + a] = mask;
+    if (mask) g.boxes[(long)b * g.A + a] = box;
   }
 }
 
@@ -224,6 +148,37 @@ __device__ __forceinline__ int block256_exclusive_scan(int v, int* wsum4, int* t
   for (int w = 0; w < 4; ++w) base += (w < wv) ? wsum4[w] : 0;
   *total = wsum4[0] + wsum4[1] + wsum4[2] + wsum4[3];
   return base + inc - v;
+}
+
+// ordered scatter: entry (anchor, class) in (anchor, class) order = the reference's row order; each block sums its
+// image's preceding block counts itself (no separate scan launch)
+__global__ __launch_bounds__(256) void nms_scatter_kernel(NmsArgs g) {
+  __shared__ int wsum4[4];
+  const int b = blockIdx.y;
+  const long A = g.A;
+  const long a = (long)blockIdx.x * 256 + threadIdx.x;
+  // this block's output offset: the candidates of the image's preceding blocks (their counts from nms_prep)
+  const int* bc = g.blkcnt + (long)b * gridDim.x;
+  if (bc[blockIdx.x] == 0) return;  // no candidates here (nms_prep did not store this block's masks)
+  const unsigned long long m = (a < A) ? g.amask[(long)b * A + a] : 0ull;
+  int before = 0;
+  for (int i = threadIdx.x; i < (int)blockIdx.x; i += 256) before += bc[i];
+  int base;
+  (void)block256_exclusive_scan(before, wsum4, &base);
+  __syncthreads();  // wsum4 is reused by the scan below
+  int total;
+  const int ex = block256_exclusive_scan(__popcll(m), wsum4, &total);
+  if (!m) return;
+  int k = base + ex;
+  const float* pb = g.pred + (long)b * (4 + g.nc) * A + a;
+  unsigned* kA = g.keyA + (long)b * g.cap;
+  unsigned* pA = g.posA + (long)b * g.cap;
+  for (int j = 0; j < g.nc; ++j)
+    if ((m >> j) & 1ull) {
+      kA[k] = ~__float_as_uint(pb[(long)(4 + j) * A]);  // ascending ~bits == descending positive score
+      pA[k] = (unsigned)(a * g.nc + j);
+      ++k;
+    }
 }
 
 __device__ __forceinline__ unsigned long long lanemask_lt() {
@@ -413,8 +368,8 @@ __device__ int compact_by_key(const unsigned* ks, const unsigned* ps, int n, uns
 // -------------------------------------------------------------------------------------------------
 // nms_select: compaction + score order of the first <= KCAP candidates (see header)
 // -------------------------------------------------------------------------------------------------
-// the select phase of image b (block-uniform; NMS_T threads)
-__device__ void select_image(const NmsArgs& g, const int b) {
+__global__ __launch_bounds__(NMS_T) void nms_select_kernel(NmsArgs g) {
+  const int b = blockIdx.x;
   const int tid = threadIdx.x;
   __shared__ SortShared sh;
   __shared__ unsigned sel_below, sel_prefix;
@@ -430,7 +385,7 @@ __device__ void select_image(const NmsArgs& g, const int b) {
   __shared__ int nsum[NMS_W + 1];
   int n;
   {
-    const int nblk = (int)((A + ANB - 1) / ANB);
+    const int nblk = (int)((A + 255) / 256);
     int v = 0;
     for (int i = tid; i < nblk; i += NMS_T) v += g.blkcnt[(long)b * nblk + i];
     (void)block_exclusive_scan(v, nsum, &n);
@@ -514,71 +469,16 @@ __device__ void select_image(const NmsArgs& g, const int b) {
   }
 }
 
-// A == 0: no prep / scatter blocks; the select phase alone (it finds n = 0)
-__global__ __launch_bounds__(NMS_T) void nms_select_kernel(NmsArgs g) {
-  if (threadIdx.x == 0) g.arrive[2 * blockIdx.x + 1] = 0;
-  select_image(g, blockIdx.x);
-}
-
-// Arrival of this workgroup at counter *ctr of `nblocks` workgroups: true in exactly one workgroup, the last to
-// arrive, after every other one's global writes are visible to it (release before the agent-scope atomic, acquire
-// after it). Block-uniform.
-__device__ __forceinline__ bool arrive_last(int* ctr, int nblocks, int* flag_sh) {
-  __threadfence();
-  __syncthreads();
-  if (threadIdx.x == 0) *flag_sh = (atomicAdd(ctr, 1) == nblocks - 1) ? 1 : 0;
-  __syncthreads();
-  const bool last = *flag_sh != 0;
-  if (last) __threadfence();
-  return last;
-}
-
-// ordered scatter: entry (anchor, class) in (anchor, class) order = the reference's row order; each block sums its
-// image's preceding block counts itself (no separate scan launch). Block = ANB anchors, 2 per thread. The image's
-// last block to finish runs the select phase.
-__global__ __launch_bounds__(NMS_T) void nms_scatter_select_kernel(NmsArgs g) {
-  __shared__ int wsum[NMS_W + 1];
-  __shared__ int last_sh;
-  const int b = blockIdx.y;
-  const long A = g.A;
-  const int* bc = g.blkcnt + (long)b * gridDim.x;
-  if (bc[blockIdx.x] != 0) {  // no candidates here: nms_prep did not store this block's masks
-    const long a = (long)blockIdx.x * ANB + 2 * threadIdx.x;
-    const unsigned long long m0 = (a < A) ? g.amask[(long)b * A + a] : 0ull;
-    const unsigned long long m1 = (a + 1 < A) ? g.amask[(long)b * A + a + 1] : 0ull;
-    int before = 0;
-    for (int i = threadIdx.x; i < (int)blockIdx.x; i += NMS_T) before += bc[i];
-    int base;
-    (void)block_exclusive_scan(before, wsum, &base);
-    int total;
-    const int ex = block_exclusive_scan(__popcll(m0) + __popcll(m1), wsum, &total);
-    int k = base + ex;
-    unsigned* kA = g.keyA + (long)b * g.cap;
-    unsigned* pA = g.posA + (long)b * g.cap;
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const unsigned long long m = u ? m1 : m0;
-      if (!m) continue;
-      const float* pb = g.pred + (long)b * (4 + g.nc) * A + a + u;
-      for (int j = 0; j < g.nc; ++j)
-        if ((m >> j) & 1ull) {
-          kA[k] = ~__float_as_uint(pb[(long)(4 + j) * A]);  // ascending ~bits == descending positive score
-          pA[k] = (unsigned)((a + u) * g.nc + j);
-          ++k;
-        }
-    }
-  }
-  if (!arrive_last(g.arrive + 2 * b, (int)gridDim.x, &last_sh)) return;
-  select_image(g, b);
-}
-
 // -------------------------------------------------------------------------------------------------
-// nms_mask: bit q of mask[b][i][cb] set iff j = cb*64+q > i, j < K and IoU(i, j) > thr.
+// nms_mask: bit q of mask[b][i][cb] set iff j = cb*64+q > i, j < K and IoU(i, j) > thr. grid = (KW, B).
 // -------------------------------------------------------------------------------------------------
-// row block rb of image b (K = prefix length, rb * 64 < K); cbx / car: NMS_W x 64 staging entries. Block-uniform.
-__device__ void mask_rows(const NmsArgs& g, const int b, const int rb, const int K, float4 (*cbx)[64],
-                          float (*car)[64]) {
+__global__ __launch_bounds__(256) void nms_mask_kernel(NmsArgs g) {
+  const int b = blockIdx.y, rb = blockIdx.x;
+  const int K = g.meta[4 * b + 2];
+  if (rb * 64 >= K) return;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  __shared__ float4 cbx[4][64];
+  __shared__ float car[4][64];
   const float4* sb = g.sbox + (long)b * KCAP;
   const float* sa = g.sarea + (long)b * KCAP;
   const int i = rb * 64 + lane;
@@ -586,7 +486,7 @@ __device__ void mask_rows(const NmsArgs& g, const int b, const int rb, const int
   const float ai = (i < K) ? sa[i] : 0.f;
   const int nblk = (K + 63) / 64;
   unsigned long long* mrow = g.mask + ((long)b * KCAP + i) * KW;
-  for (int cb0 = rb; cb0 < nblk; cb0 += NMS_W) {
+  for (int cb0 = rb; cb0 < nblk; cb0 += 4) {
     const int cb = cb0 + wv;
     const int j = cb * 64 + lane;
     if (cb < nblk) {
@@ -611,11 +511,11 @@ __device__ void mask_rows(const NmsArgs& g, const int b, const int rb, const int
 // -------------------------------------------------------------------------------------------------
 // BIG: max_det > NMS_MAXDET (the reference has no cap, ops.py:297): the kept lists live in the workspace instead
 // of LDS (same algorithm; only a caller asking for more than 1024 detections per image pays for global accesses)
-// ubuf: 32 KB of LDS, the staged mask rows of the prefix greedy, then the fallback's chunk bitmask. Block-uniform.
 template <bool BIG>
-__device__ void resolve_image(const NmsArgs& g, const int b, unsigned long long* ubuf) {
+__global__ __launch_bounds__(NMS_T) void nms_resolve_kernel(NmsArgs g) {
+  const int b = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  unsigned long long (*mrows)[64][KW] = reinterpret_cast<unsigned long long (*)[64][KW]>(ubuf);
+  __shared__ unsigned long long mrows[2][64][KW];
   __shared__ int kept_t_lds[BIG ? 1 : NMS_MAXDET];
   // kept entries: < KCAP -> prefix index, else KCAP + remainder index
   int* kept_t = BIG ? g.kept_t + (long)b * g.max_det : kept_t_lds;
@@ -723,7 +623,7 @@ __device__ void resolve_image(const NmsArgs& g, const int b, unsigned long long*
     __shared__ float ca[NMS_T];
     __shared__ int alive[NMS_T];
     __shared__ unsigned long long alive_w[NMS_W];
-    unsigned long long (*rows)[NMS_T / 64] = reinterpret_cast<unsigned long long (*)[NMS_T / 64]>(ubuf);
+    __shared__ unsigned long long rows[NMS_T][NMS_T / 64];
     const float4* sb = g.sbox + (long)b * KCAP;
     const float* sa = g.sarea + (long)b * KCAP;
     for (int k = tid; k < nk_prefix; k += NMS_T) {
@@ -829,23 +729,6 @@ __device__ void resolve_image(const NmsArgs& g, const int b, unsigned long long*
   }
 }
 
-// grid (KW, B): workgroup (rb, b) computes the mask rows of row block rb of image b (if rb * 64 < K); the image's last
-// workgroup to finish resolves it
-template <bool BIG>
-__global__ __launch_bounds__(NMS_T) void nms_mask_resolve_kernel(NmsArgs g) {
-  static_assert(2 * 64 * KW * 8 == NMS_T * (NMS_T / 64) * 8, "mask rows and the fallback bitmask share ubuf");
-  static_assert(NMS_W * 64 * (16 + 4) <= 2 * 64 * KW * 8, "the mask staging fits in ubuf");
-  __shared__ __attribute__((aligned(16))) unsigned long long ubuf[2 * 64 * KW];
-  __shared__ int last_sh;
-  const int b = blockIdx.y, rb = blockIdx.x;
-  const int K = g.meta[4 * b + 2];
-  if (rb * 64 < K)
-    mask_rows(g, b, rb, K, reinterpret_cast<float4 (*)[64]>(ubuf),
-              reinterpret_cast<float (*)[64]>(reinterpret_cast<char*>(ubuf) + NMS_W * 64 * 16));
-  if (!arrive_last(g.arrive + 2 * b + 1, (int)gridDim.x, &last_sh)) return;
-  resolve_image<BIG>(g, b, ubuf);
-}
-
 #undef YS_NSTAMP
 
 }  // namespace ys
@@ -888,8 +771,7 @@ YS_EXPORT size_t yolosod_nms_workspace_v2(int B, int nc, int A, int multi_label,
   s.take<unsigned>((size_t)B * KCAP);
   s.take<unsigned long long>((size_t)B * KCAP * KW);
   s.take<int>((size_t)B * 4);
-  s.take<int>((size_t)B * ((A + ANB - 1) / ANB));
-  s.take<int>((size_t)B * 2);
+  s.take<int>((size_t)B * ((A + 255) / 256));
   if (max_det > NMS_MAXDET) {
     s.take<int>((size_t)B * max_det);
     s.take<float4>((size_t)B * max_det);
@@ -942,17 +824,15 @@ YS_EXPORT int yolosod_nms(float* pred, int B, int nc, int A, float conf_thres, d
   g.spos = cv.take<unsigned>((size_t)B * KCAP);
   g.mask = cv.take<unsigned long long>((size_t)B * KCAP * KW);
   g.meta = cv.take<int>((size_t)B * 4);
-  const int nblk_a = (A + ANB - 1) / ANB;
+  const int nblk_a = (A + 255) / 256;
   g.blkcnt = cv.take<int>((size_t)B * nblk_a);
-  g.arrive = cv.take<int>((size_t)B * 2);
-  g.vec4 = (A % 4 == 0 && ((uintptr_t)pred & 15) == 0) ? 1 : 0;
   const bool big = max_det > NMS_MAXDET;
   if (big) {
     g.kept_t = cv.take<int>((size_t)B * max_det);
     g.kbox = cv.take<float4>((size_t)B * max_det);
     g.karea = cv.take<float>((size_t)B * max_det);
   }
-  YS_CHECK_ARG(g.arrive && (!big || g.karea), "nms: workspace too small (%zu)", workspace_bytes);
+  YS_CHECK_ARG(g.blkcnt && (!big || g.karea), "nms: workspace too small (%zu)", workspace_bytes);
   g.cap = cap;
   g.out = out;
   g.counts = counts;
@@ -971,14 +851,14 @@ YS_EXPORT int yolosod_nms(float* pred, int B, int nc, int A, float conf_thres, d
   }
   if (A > 0) {
     hipLaunchKernelGGL(nms_prep_kernel, dim3(nblk_a, B), dim3(256), 0, st, g);
-    hipLaunchKernelGGL(nms_scatter_select_kernel, dim3(nblk_a, B), dim3(NMS_T), 0, st, g);
-  } else {
-    hipLaunchKernelGGL(nms_select_kernel, dim3(B), dim3(NMS_T), 0, st, g);
+    hipLaunchKernelGGL(nms_scatter_kernel, dim3(nblk_a, B), dim3(256), 0, st, g);
   }
+  hipLaunchKernelGGL(nms_select_kernel, dim3(B), dim3(NMS_T), 0, st, g);
+  hipLaunchKernelGGL(nms_mask_kernel, dim3(KW, B), dim3(256), 0, st, g);
   if (big)
-    hipLaunchKernelGGL(nms_mask_resolve_kernel<true>, dim3(KW, B), dim3(NMS_T), 0, st, g);
+    hipLaunchKernelGGL(nms_resolve_kernel<true>, dim3(B), dim3(NMS_T), 0, st, g);
   else
-    hipLaunchKernelGGL(nms_mask_resolve_kernel<false>, dim3(KW, B), dim3(NMS_T), 0, st, g);
+    hipLaunchKernelGGL(nms_resolve_kernel<false>, dim3(B), dim3(NMS_T), 0, st, g);
   YS_CHECK_LAUNCH("nms");
   return 0;
 }

@@ -273,6 +273,118 @@ __global__ __launch_bounds__(256) void swin_tokens_bf16_kernel(const bf16_t* __r
   }
 }
 
+// Swin tokens + LN1 in one pass (W % 8 == 0, W <= 64, C % 64 == 0, C <= 1024): workgroup = one padded row of one
+// image with all C channels. Thread c (then c + 256, ...) computes its channel's depthwise 3x3 over the whole row from
+// three rows of W / 8 16-byte loads (the neighbour pixels come from the adjacent runs: no 2-byte loads), with the same
+// expression and order as swin_tokens_bf16_kernel, into an LDS tile [Wp][C + 8]; then wave w normalises tokens w,
+// w + 4, ... exactly as ln_rows_bf16_kernel (same lane -> channel map and sum order) and writes both the T row and the
+// U = LN1(T) row. Bit-identical to swin_tokens_bf16_kernel + ln_rows_bf16_kernel; one launch and one HBM round trip
+// of T less. dynamic LDS = Wp * (C + 8) * 2 bytes.
+template <int VPL>
+__global__ __launch_bounds__(256) void swin_tokens_ln_bf16_kernel(const bf16_t* __restrict__ x,
+                                                                  const float* __restrict__ dw, bf16_t* __restrict__ T,
+                                                                  bf16_t* __restrict__ U, int C, int H, int W, int Hp,
+                                                                  int Wp, float eps, const float* __restrict__ lw,
+                                                                  const float* __restrict__ lb) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t tile[];  // [Wp][C + 8]
+  const int TS = C + 8;
+  const int img = blockIdx.x / Hp, h = blockIdx.x - (blockIdx.x / Hp) * Hp;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int nruns = W >> 3;
+  for (int c = tid; c < C; c += 256) {
+    if (h < H) {
+      const bf16_t* xc = x + ((long)img * C + c) * H * W;
+      float k[9];
+#pragma unroll
+      for (int i = 0; i < 9; ++i) k[i] = dw[(long)c * 9 + i];
+      uint4 rows[3][8];
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        const int hh = h - 1 + r;
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          rows[r][q] = (q < nruns && hh >= 0 && hh < H) ? *reinterpret_cast<const uint4*>(xc + (long)hh * W + 8 * q)
+                                                       : make_uint4(0u, 0u, 0u, 0u);
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        if (q >= nruns) break;
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = 0.f;
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+          const int hh = h - 1 + r;
+          if (hh < 0 || hh >= H) continue;
+          float v[10], f[8];
+          unpack8(rows[r][q], f);
+          v[0] = 0.f;
+          if (q > 0) {
+            float pf[8];
+            unpack8(rows[r][q - 1], pf);
+            v[0] = pf[7];
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[1 + j] = f[j];
+          v[9] = 0.f;
+          if (q + 1 < nruns) {
+            float nf[8];
+            unpack8(rows[r][q + 1], nf);
+            v[9] = nf[0];
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] += k[3 * r] * v[j] + k[3 * r + 1] * v[j + 1] + k[3 * r + 2] * v[j + 2];
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) tile[(8 * q + j) * TS + c] = f2bf(o[j]);
+      }
+      for (int w = W; w < Wp; ++w) tile[w * TS + c] = (bf16_t)0;
+    } else {
+      for (int w = 0; w < Wp; ++w) tile[w * TS + c] = (bf16_t)0;
+    }
+  }
+  __syncthreads();
+  const int K4 = C >> 2;
+  for (int w = wv; w < Wp; w += 4) {
+    const long row = ((long)img * Hp + h) * Wp + w;
+    const bf16_t* tr = tile + w * TS;
+    f32x4 v[VPL];
+    uint2 raw[VPL];
+    float s = 0.f;
+#pragma unroll
+    for (int u = 0; u < VPL; ++u) {
+      const int c = lane + 64 * u;
+      raw[u] = (c < K4) ? *reinterpret_cast<const uint2*>(tr + 4 * c) : make_uint2(0u, 0u);
+      v[u] = f32x4{__uint_as_float(raw[u].x << 16), __uint_as_float(raw[u].x & 0xffff0000u),
+                   __uint_as_float(raw[u].y << 16), __uint_as_float(raw[u].y & 0xffff0000u)};
+      s += (v[u].x + v[u].y) + (v[u].z + v[u].w);
+    }
+    const float mean = wave_sum(s) / (float)C;
+    float q = 0.f;
+#pragma unroll
+    for (int u = 0; u < VPL; ++u) {
+      if (lane + 64 * u < K4) {
+        const f32x4 d = v[u] - mean;
+        q += (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
+      }
+    }
+    const float var = wave_sum(q) / (float)C;
+    const float rs = 1.0f / sqrtf(var + eps);
+#pragma unroll
+    for (int u = 0; u < VPL; ++u) {
+      const int c = lane + 64 * u;
+      if (c < K4) {
+        *reinterpret_cast<uint2*>(T + row * C + 4 * c) = raw[u];
+        const f32x4 w4 = *reinterpret_cast<const f32x4*>(lw + 4 * c), b4 = *reinterpret_cast<const f32x4*>(lb + 4 * c);
+        f32x4 o;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = fmaf((v[u][i] - mean) * rs, w4[i], b4[i]);
+        st4(U + row * C + 4 * c, o);
+      }
+    }
+  }
+}
+
 // A2: adaptive-avg-pool over rows to A areas (overlapping bins), token-major S[(img*A + a)*W + w][c] (bf16).
 __global__ __launch_bounds__(256) void a2_pool_tokens_bf16_kernel(const bf16_t* __restrict__ xp, bf16_t* __restrict__ S,
                                                                   int C, int H, int W, int A) {
@@ -448,6 +560,18 @@ YS_EXPORT size_t yolosod_swin_workspace_bf16(int B, int C, int H, int W, int num
   return s.off;
 }
 
+// tokens + LN1 in one pass (swin_tokens_ln_bf16_kernel; YOLOSOD_SWIN_TOKLN=0 selects the two-kernel form)
+static int& tokens_ln_mode() {
+  static int on = [] { const char* e = getenv("YOLOSOD_SWIN_TOKLN"); return (!e || atoi(e) != 0) ? 1 : 0; }();
+  return on;
+}
+static bool tokens_ln_env() { return tokens_ln_mode() != 0; }
+YS_EXPORT int yolosod_debug_set_swin_tokln(int on) {
+  const int prev = tokens_ln_mode();
+  tokens_ln_mode() = on ? 1 : 0;
+  return prev;
+}
+
 // SwinBlock.forward (blocks_transformer.py:150-171) on bf16 activations. Weights: in_proj [3C][C], out_proj [C][C],
 // mlp1 [hid][C], mlp2 [C][hid], pw [C][C] bf16; dw [C][9], LN / biases / BN fp32.
 YS_EXPORT int yolosod_swin_forward_bf16(const bf16_t* x, bf16_t* y, int B, int C, int H, int W, int num_heads,
@@ -492,14 +616,30 @@ YS_EXPORT int yolosod_swin_forward_bf16(const bf16_t* x, bf16_t* y, int B, int C
   float* lns = cv.take<float>((size_t)g.ntok * 2);
   YS_CHECK_ARG(lns, "swin_bf16: workspace too small (%zu)", workspace_bytes);
   int rc;
-  // dwconv + pad -> T (raster tokens)
-  const size_t tok_lds = (size_t)g.Wp * 72 * sizeof(bf16_t);
-  YS_CHECK_ARG(tok_lds <= 64 * 1024, "swin_bf16: W=%d too wide for the token kernel", W);
-  hipLaunchKernelGGL(swin_tokens_bf16_kernel, dim3((unsigned)(B * g.Hp), (unsigned)((C + 63) / 64)), dim3(256),
-                     tok_lds, st, x, dw_w, T, C, H, W, g.Hp, g.Wp);
-  YS_CHECK_LAUNCH("swin_tokens_bf16");
-  // QKV = LN1(T) Win^T + b_in (LN1(T) -> U once, U is free until the attention writes it)
-  if ((rc = launch_ln_rows_bf16(T, C, g.ntok, C, ln1_eps, ln1_w, ln1_b, U, C, st))) return rc;
+  // dwconv + pad -> T (raster tokens), and U = LN1(T) (U is free until the attention writes it)
+  const size_t tokln_lds = (size_t)g.Wp * (C + 8) * sizeof(bf16_t);
+  if (tokens_ln_env() && W % 8 == 0 && W <= 64 && C <= 1024 && tokln_lds <= 80 * 1024 &&
+      ((uintptr_t)ln1_w | (uintptr_t)ln1_b) % 16 == 0) {
+    const dim3 grid((unsigned)(B * g.Hp));
+    if (C <= 256)
+      hipLaunchKernelGGL((swin_tokens_ln_bf16_kernel<1>), grid, dim3(256), tokln_lds, st, x, dw_w, T, U, C, H, W,
+                         g.Hp, g.Wp, ln1_eps, ln1_w, ln1_b);
+    else if (C <= 512)
+      hipLaunchKernelGGL((swin_tokens_ln_bf16_kernel<2>), grid, dim3(256), tokln_lds, st, x, dw_w, T, U, C, H, W,
+                         g.Hp, g.Wp, ln1_eps, ln1_w, ln1_b);
+    else
+      hipLaunchKernelGGL((swin_tokens_ln_bf16_kernel<4>), grid, dim3(256), tokln_lds, st, x, dw_w, T, U, C, H, W,
+                         g.Hp, g.Wp, ln1_eps, ln1_w, ln1_b);
+    YS_CHECK_LAUNCH("swin_tokens_ln_bf16");
+  } else {
+    const size_t tok_lds = (size_t)g.Wp * 72 * sizeof(bf16_t);
+    YS_CHECK_ARG(tok_lds <= 64 * 1024, "swin_bf16: W=%d too wide for the token kernel", W);
+    hipLaunchKernelGGL(swin_tokens_bf16_kernel, dim3((unsigned)(B * g.Hp), (unsigned)((C + 63) / 64)), dim3(256),
+                       tok_lds, st, x, dw_w, T, C, H, W, g.Hp, g.Wp);
+    YS_CHECK_LAUNCH("swin_tokens_bf16");
+    // QKV = LN1(T) Win^T + b_in (LN1(T) -> U once, U is free until the attention writes it)
+    if ((rc = launch_ln_rows_bf16(T, C, g.ntok, C, ln1_eps, ln1_w, ln1_b, U, C, st))) return rc;
+  }
   GemmB ga{};
   ga.A = U; ga.lda = C; ga.B = in_proj_w; ga.ldb = C; ga.M = (int)g.ntok; ga.N = 3 * C; ga.K = C;
   ga.epi = epib_plain(Q, 0, 3 * C);
