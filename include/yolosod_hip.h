@@ -235,6 +235,9 @@ int yolosod_debug_set_swin_x3(int on);
  * residual (per-window attention half, token-tiled MLP / pw half), 0 (default) as the one-kernel form.
  * The yolosod_debug_set_* switches that return int return the previous state. */
 int yolosod_debug_set_swin_split(int on);
+/* Test hook: the C = 64 fp16-split SwinBlock kernel's activation planes as unpadded rows with XOR-swizzled 16-byte
+ * chunks (1, default; env YOLOSOD_X3_SWZ=0 turns it off) or rows padded to 80 elements (0); same results. */
+int yolosod_debug_set_x3_swz(int on);
 /* Test hook: 1 (default; env YOLOSOD_HEAD_X2=0 turns it off) runs the Detect head's 1x1 convs as fp16 two-term
  * splits on the fp16 matrix cores (detect_head_x2_kernel), 0 on the exact fp32 MFMA (detect_head_lds_kernel). */
 int yolosod_debug_set_head_x2(int on);

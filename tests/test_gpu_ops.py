@@ -144,6 +144,31 @@ def test_swin_c64_split_and_one_kernel_forms(name, split, cuda, monkeypatch):
     assert ok, f"{name} split={split}: vs fp64 oracle max abs err {err:.3g} (ratio {ratio:.2f})"
 
 
+@pytest.mark.parametrize("split", [0, 1], ids=["one_kernel", "split"])
+@pytest.mark.parametrize("name", ["swin_c64_h20", "swin_c64_b3_20x13", "swin_L28"])
+def test_swin_c64_swizzled_planes_bit_identical(name, split, cuda, monkeypatch):
+    """The C = 64 kernel's activation planes as unpadded rows with XOR-swizzled 16-byte chunks (default) and as rows
+    padded to 80 elements: a layout change only, so the outputs are bit-identical (both the one-kernel form and the
+    attention half of the split pair)."""
+    lib = _hip.load_library()
+    if SPLIT_SHAPES[name] is not None:
+        monkeypatch.setitem(recipes.OPS, name, SPLIT_SHAPES[name])
+    m, _ = build_fixture_module(name)
+    m = m.to(cuda)
+    x = recipes.make_input(name, recipes.OPS[name][2]).to(cuda)
+    prev_s = lib.yolosod_debug_set_swin_split(split)
+    prev = lib.yolosod_debug_set_x3_swz(1)
+    try:
+        with torch.inference_mode():
+            a = m(x).cpu()
+            lib.yolosod_debug_set_x3_swz(0)
+            b = m(x).cpu()
+    finally:
+        lib.yolosod_debug_set_x3_swz(prev)
+        lib.yolosod_debug_set_swin_split(prev_s)
+    assert torch.equal(a, b), f"{name}: max|d| {float((a - b).abs().max()):.3g}"
+
+
 A2_FUSED_SHAPES = {  # A2_Attn through both forms of its fp16-split path
     "a2_c512_h20": None, "a2_c128_h16": None,
     "a2_L12": REAL["a2_L12"],

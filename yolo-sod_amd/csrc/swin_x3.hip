@@ -95,12 +95,31 @@ __device__ __forceinline__ float dot4_acc(float4 a, float4 b, float acc) {
 }
 __device__ __forceinline__ float group4_sum(float v) { return xor32_sum(xor16_sum(v)); }
 
+// Element (row, col) of a [rows][PS] fp16 plane. SWZ: the 16-byte chunks of a row are XOR-swizzled by the row's low
+// three bits (chunk c -> c ^ (row & 7)) in an unpadded row (PS = 64): the GEMM operand reads (ds_read_b128, lane =
+// (row l15, chunk g)), the LN plane stores (ds_write_b128, 4 lanes per row) and the accumulator stores
+// (ds_write_b64, 16 rows x one column group) are then conflict-free / 2-way instead of 0 / 2-way / 4-way at PS = 80.
+template <int PS, bool SWZ>
+__device__ __forceinline__ int plane_off(int row, int col) {
+  if constexpr (SWZ) return row * PS + ((((col >> 3) ^ (row & 7))) << 3) + (col & 7);
+  else return row * PS + col;
+}
+// The same for planes that are only read 8 bytes at a time (the attention's K and V^T planes: ds_read_b64 and
+// ds_write_b64 of 4 elements, lane = (row l15, column group g)): 8-byte chunks swizzled by the row's low four bits,
+// which makes both the reads and the 16-row column stores conflict-free (at the padded stride 72 the stores were
+// 2-way)
+template <int PS, bool SWZ>
+__device__ __forceinline__ int plane_off8(int row, int col) {
+  if constexpr (SWZ) return row * PS + ((((col >> 2) ^ (row & 15))) << 2) + (col & 3);
+  else return row * PS + col;
+}
+
 // the two planes of 4 consecutive elements of row `row`, column `col` (a multiple of 4)
-template <int PS, int PL>
+template <int PS, int PL, bool SWZ = false, bool SWZ8 = false>
 __device__ __forceinline__ void store_planes4(h16_t* P, int row, int col, f32x4 v) {
   uint2 h, l;
   split4(v, h, l);
-  h16_t* d = P + row * PS + col;
+  h16_t* d = P + (SWZ8 ? plane_off8<PS, true>(row, col) : plane_off<PS, SWZ>(row, col));
   *reinterpret_cast<uint2*>(d) = h;
   *reinterpret_cast<uint2*>(d + PL) = l;
 }
@@ -136,14 +155,17 @@ __device__ __forceinline__ void load_wp(const h16_t* __restrict__ Wp, int N, int
 // steps ahead of the MFMAs (at two waves per SIMD a read waited for right before its MFMAs exposes its latency).
 // SWAP: the token rows are the MFMA's A operand and the weight planes its B operand (the same fragments), so the
 // lane holds out[token rb*16 + 4g .. +3][n = cb*16 + l15] instead (4 consecutive tokens of one output column).
-template <int K, int NJ, int PS, int PL, bool SWAP = false>
+template <int K, int NJ, int PS, int PL, bool SWAP = false, bool SWZ = false>
 __device__ __forceinline__ void gemm_x3(const h16_t* A, const WP<K, NJ>& w, f32x4 (&acc)[4][NJ], int lane) {
   const int l15 = lane & 15, g = lane >> 4;
   constexpr int NS = (K / 32) * 4;  // steps (s, rb), rb fastest
-  const h16_t* a0 = A + l15 * PS + 8 * g;
+  const h16_t* a0 = A + l15 * PS;
+  int coff[K / 32];  // this lane's column offset of k step s (rows l15 + 16 rb share the low row bits)
+#pragma unroll
+  for (int s = 0; s < K / 32; ++s) coff[s] = plane_off<PS, SWZ>(l15, 32 * s + 8 * g) - l15 * PS;
   f16x8_t u[3][2];
   auto ld = [&](int i, f16x8_t (&v)[2]) {
-    const h16_t* ar = a0 + (i & 3) * 16 * PS + 32 * (i >> 2);
+    const h16_t* ar = a0 + (i & 3) * 16 * PS + coff[i >> 2];
     v[0] = *reinterpret_cast<const f16x8_t*>(ar);
     v[1] = *reinterpret_cast<const f16x8_t*>(ar + PL);
   };
@@ -178,7 +200,7 @@ __device__ __forceinline__ void gemm_x3(const h16_t* A, const WP<K, NJ>& w, f32x
 
 // LayerNorm statistics of token rows [0, 49) of T (fp32, stride LT) and the normalised rows (affine folded into the
 // next GEMM) as two fp16 planes; rows 49..63 get zeros. 4 lanes per row (a DPP quad), C/4 values each.
-template <int C, int LT, int PS, int PL>
+template <int C, int LT, int PS, int PL, bool SWZ = false>
 __device__ __forceinline__ void ln_planes(const float* T, h16_t* P, float eps, int tid) {
   constexpr int CP = C / 4;
   const int r = tid >> 2, qd = tid & 3;
@@ -203,7 +225,7 @@ __device__ __forceinline__ void ln_planes(const float* T, h16_t* P, float eps, i
     uint2 h0, l0, h1, l1;
     split4(v[i] * rs, h0, l0);
     split4(v[i + 1] * rs, h1, l1);
-    h16_t* d = P + r * PS + qd * CP + 4 * i;
+    h16_t* d = P + plane_off<PS, SWZ>(r, qd * CP + 4 * i);
     *reinterpret_cast<uint4*>(d) = make_uint4(h0.x, h0.y, h1.x, h1.y);
     *reinterpret_cast<uint4*>(d + PL) = make_uint4(l0.x, l0.y, l1.x, l1.y);
   }
@@ -212,7 +234,7 @@ __device__ __forceinline__ void ln_planes(const float* T, h16_t* P, float eps, i
 // SPLIT: the attention half only (split at the attention residual): dw -> LN1 -> QKV -> attention -> out-proj + the
 // residual, stored token-major to p.t1 for the cropped tokens; the per-token half (LN2 -> MLP -> pw -> BN -> SiLU -> + x)
 // runs in swin_mlp_kernel, token-tiled, with its weights resident in LDS and no window padding.
-template <int C, int NH, bool SPLIT = false>
+template <int C, int NH, bool SPLIT = false, bool SWZ = false>
 __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
   constexpr int HD = C / NH;
   constexpr int HID = 2 * C;
@@ -221,11 +243,11 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
 #define YS_X3_PS_PAD 16  // PS = 80 = ten 16-byte quads: the ds_read_b128 lane groups of the GEMM operand
                          // reads hit 16 distinct quads (PS = 72, nine quads: 28 of 64 lanes in 2-way conflicts)
 #endif
-  constexpr int PS = C + YS_X3_PS_PAD;  // plane row stride (fp16)
+  constexpr int PS = SWZ ? C : C + YS_X3_PS_PAD;  // plane row stride (fp16); SWZ: unpadded, chunk-swizzled rows
   constexpr int PL = 64 * PS;    // plane stride
-  constexpr int PSK = C + 8;     // K plane row stride
+  constexpr int PSK = SWZ ? C : C + 8;  // K plane row stride (SWZ: unpadded, 8-byte chunks swizzled)
   constexpr int KPL = NR * PSK;  // K plane stride
-  constexpr int PSV = 72;        // V^T plane row stride (keys 0..63 + 8)
+  constexpr int PSV = SWZ ? 64 : 72;    // V^T plane row stride (keys 0..63 (+ 8))
   constexpr int VPL = C * PSV;   // V^T plane stride
   constexpr int NHS = (C + 2) / 3;
   static_assert(C == 64 && HID / 2 == C, "the plane regions are sized for C = 64 (hidden halves of 64)");
@@ -391,7 +413,7 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
   X3_STAMP(2);
 
   // ---- LN1 -> X planes; Q weight chunk 0 -> X after the U1 planes (the halo there has been read) ----
-  ln_planes<C, LT, PS, PL>(T, P, p.ln1_eps, tid);
+  ln_planes<C, LT, PS, PL, SWZ>(T, P, p.ln1_eps, tid);
   h16_t* QW = P + 2 * PL;  // [2 plane][4 column block][64 lanes][8]
   h16_t* qdst = QW + qblk * 512 + 16 * (tid & 31);
   *reinterpret_cast<uint4*>(qdst) = qc0a;
@@ -413,7 +435,7 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
     f16x8_t ua[C / 32][2];
 #pragma unroll
     for (int s2 = 0; s2 < C / 32; ++s2) {
-      const h16_t* ar = P + (wid * 16 + l15_) * PS + 32 * s2 + 8 * g;
+      const h16_t* ar = P + plane_off<PS, SWZ>(wid * 16 + l15_, 32 * s2 + 8 * g);
       ua[s2][0] = *reinterpret_cast<const f16x8_t*>(ar);
       ua[s2][1] = *reinterpret_cast<const f16x8_t*>(ar + PL);
     }
@@ -448,15 +470,16 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
         akv[0][rb][0] = bk;
         akv[1][rb][0] = f32x4{bv, bv, bv, bv};
       }
-      gemm_x3<C, 1, PS, PL>(P, f_q, akv[0], lane);
+      gemm_x3<C, 1, PS, PL, false, SWZ>(P, f_q, akv[0], lane);
 #ifdef YS_OLD_V
+    static_assert(!SWZ, "diagnostic V layout: padded planes only");
       {
         const f32x4 b = *reinterpret_cast<const f32x4*>(par + P_BIN + (2 * C / 16 + wid) * 16 + 4 * g);
         for (int rb = 0; rb < 4; ++rb) akv[1][rb][0] = b;
       }
-      gemm_x3<C, 1, PS, PL>(P, f_n, akv[1], lane);
+      gemm_x3<C, 1, PS, PL, false, SWZ>(P, f_n, akv[1], lane);
 #else
-      gemm_x3<C, 1, PS, PL, true>(P, f_n, akv[1], lane);
+      gemm_x3<C, 1, PS, PL, true, SWZ>(P, f_n, akv[1], lane);
 #endif
     }
   }
@@ -467,7 +490,7 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
 #pragma unroll
   for (int rb = 0; rb < 4; ++rb) {
     const int tok = rb * 16 + l15;
-    if (tok < NR) store_planes4<PSK, KPL>(Kp, tok, wid * 16 + 4 * g, akv[0][rb][0]);  // K, V, Q stay x64
+    if (tok < NR) store_planes4<PSK, KPL, false, SWZ>(Kp, tok, wid * 16 + 4 * g, akv[0][rb][0]);  // K, V, Q stay x64
     rng = range_acc(range_acc(rng, akv[0][rb][0]), akv[1][rb][0]);
     uint2 h, l;
 #ifdef YS_OLD_V
@@ -483,7 +506,7 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
     vd[VPL + 3 * PSV] = (h16_t)(l.y >> 16);
 #else
     split4(akv[1][rb][0], h, l);  // V^T[d = wid*16 + l15][keys rb*16 + 4g .. +3]
-    h16_t* vd = Vt + (wid * 16 + l15) * PSV + rb * 16 + 4 * g;
+    h16_t* vd = Vt + plane_off8<PSV, SWZ>(wid * 16 + l15, rb * 16 + 4 * g);
     *reinterpret_cast<uint2*>(vd) = h;
     *reinterpret_cast<uint2*>(vd + VPL) = l;
 #endif
@@ -517,9 +540,10 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb) {
         const int row = kb * 16 + l15 < NR ? kb * 16 + l15 : NR - 1;
-        const h16_t* kr = Kp + row * PSK + hh * HD + 4 * g;
-        const uint2 a0 = *reinterpret_cast<const uint2*>(kr), a1 = *reinterpret_cast<const uint2*>(kr + 16);
-        const uint2 b0 = *reinterpret_cast<const uint2*>(kr + KPL), b1 = *reinterpret_cast<const uint2*>(kr + KPL + 16);
+        const h16_t* kr0 = Kp + plane_off8<PSK, SWZ>(row, hh * HD + 4 * g);
+        const h16_t* kr1 = Kp + plane_off8<PSK, SWZ>(row, hh * HD + 4 * g + 16);
+        const uint2 a0 = *reinterpret_cast<const uint2*>(kr0), a1 = *reinterpret_cast<const uint2*>(kr1);
+        const uint2 b0 = *reinterpret_cast<const uint2*>(kr0 + KPL), b1 = *reinterpret_cast<const uint2*>(kr1 + KPL);
         const f16x8_t kh = __builtin_bit_cast(f16x8_t, make_uint4(a0.x, a0.y, a1.x, a1.y));
         const f16x8_t kl = __builtin_bit_cast(f16x8_t, make_uint4(b0.x, b0.y, b1.x, b1.y));
         f32x4 c = mfma16(kl, qh[hh], f32x4{0.f, 0.f, 0.f, 0.f});
@@ -569,9 +593,10 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
         const f16x8_t pl = __builtin_bit_cast(f16x8_t, make_uint4(l0.x, l0.y, l1.x, l1.y));
 #pragma unroll
         for (int db = 0; db < HD / 16; ++db) {
-          const h16_t* vr = Vt + (hh * HD + db * 16 + l15) * PSV + 32 * s2 + 4 * g;
-          const uint2 a0 = *reinterpret_cast<const uint2*>(vr), a1 = *reinterpret_cast<const uint2*>(vr + 16);
-          const uint2 b0 = *reinterpret_cast<const uint2*>(vr + VPL), b1 = *reinterpret_cast<const uint2*>(vr + VPL + 16);
+          const h16_t* vr0 = Vt + plane_off8<PSV, SWZ>(hh * HD + db * 16 + l15, 32 * s2 + 4 * g);
+          const h16_t* vr1 = Vt + plane_off8<PSV, SWZ>(hh * HD + db * 16 + l15, 32 * s2 + 4 * g + 16);
+          const uint2 a0 = *reinterpret_cast<const uint2*>(vr0), a1 = *reinterpret_cast<const uint2*>(vr1);
+          const uint2 b0 = *reinterpret_cast<const uint2*>(vr0 + VPL), b1 = *reinterpret_cast<const uint2*>(vr1 + VPL);
           const f16x8_t vh = __builtin_bit_cast(f16x8_t, make_uint4(a0.x, a0.y, a1.x, a1.y));
           const f16x8_t vl = __builtin_bit_cast(f16x8_t, make_uint4(b0.x, b0.y, b1.x, b1.y));
           f32x4 c = mfma16(vl, ph, ov[hh][db]);
@@ -590,7 +615,7 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
 #pragma unroll
     for (int db = 0; db < HD / 16; ++db)
     {
-      store_planes4<PS, PL>(P, wid * 16 + l15, h * HD + db * 16 + 4 * g, ov[h][db]);
+      store_planes4<PS, PL, SWZ>(P, wid * 16 + l15, h * HD + db * 16 + 4 * g, ov[h][db]);
       rng = range_acc(rng, ov[h][db]);
     }
   __syncthreads();
@@ -604,7 +629,7 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
     const f32x4 b = *reinterpret_cast<const f32x4*>(par + P_BO + wid * 16 + 4 * g);
 #pragma unroll
     for (int rb = 0; rb < 4; ++rb) acc[rb][0] = b;
-    gemm_x3<C, 1, PS, PL>(P, f_o, acc, lane);
+    gemm_x3<C, 1, PS, PL, false, SWZ>(P, f_o, acc, lane);
     if constexpr (SPLIT) {
       // T1 = T + O Wo^T + bo of this wave's column block, straight from the accumulators to the token-major buffer:
       // the 4 lane groups of a token write 64 contiguous bytes; cropped and padded tokens are not stored
@@ -635,7 +660,7 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
   X3_STAMP(10);
 
   // ---- LN2 -> X planes ----
-  ln_planes<C, LT, PS, PL>(T, P, p.ln2_eps, tid);
+  ln_planes<C, LT, PS, PL, SWZ>(T, P, p.ln2_eps, tid);
   WP<C, 1> f_2a;
   load_wp(p.w2, C, HID, 0, wid, f_2a, lane);  // MLP2 planes, k in [0, 64)
   __syncthreads();
@@ -651,7 +676,7 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
 #pragma unroll
     for (int rb = 0; rb < 4; ++rb) acc[rb][0] = b;
 #ifndef YS_ABL_MLPMFMA
-    gemm_x3<C, 1, PS, PL>(P, half == 0 ? f_1a : f_1b, acc, lane);
+    gemm_x3<C, 1, PS, PL, false, SWZ>(P, half == 0 ? f_1a : f_1b, acc, lane);
 #endif
 #pragma unroll
     for (int rb = 0; rb < 4; ++rb) {
@@ -679,13 +704,13 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
     X3_STAMP(12 + 2 * half);
 #pragma unroll
     for (int rb = 0; rb < 4; ++rb) {
-      store_planes4<PS, PL>(P, rb * 16 + l15, wid * 16 + 4 * g, hid[half][rb]);
+      store_planes4<PS, PL, SWZ>(P, rb * 16 + l15, wid * 16 + 4 * g, hid[half][rb]);
       rng = range_acc(rng, hid[half][rb]);
     }
     __syncthreads();
     X3_STAMP(13 + 2 * half);
 #ifndef YS_ABL_MLPMFMA
-    gemm_x3<C, 1, PS, PL>(P, half == 0 ? f_2a : f_2b, acc2, lane);
+    gemm_x3<C, 1, PS, PL, false, SWZ>(P, half == 0 ? f_2a : f_2b, acc2, lane);
 #endif
   }
 
@@ -716,7 +741,7 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
     const int tok = rb * 16 + l15;
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
     if (tok < NR) v = *reinterpret_cast<const f32x4*>(T + tok * LT + wid * 16 + 4 * g) + acc2[rb][0] * (1.0f / WSC);
-    store_planes4<PS, PL>(P, tok, wid * 16 + 4 * g, v);
+    store_planes4<PS, PL, SWZ>(P, tok, wid * 16 + 4 * g, v);
     rng = range_acc(rng, v);
   }
   range_report(p.range_flag, rng);
@@ -729,7 +754,7 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
     f32x4 acc[4][1];
 #pragma unroll
     for (int tb = 0; tb < 4; ++tb) acc[tb][0] = f32x4{0.f, 0.f, 0.f, 0.f};
-    gemm_x3<C, 1, PS, PL>(P, f_pw, acc, lane);
+    gemm_x3<C, 1, PS, PL, false, SWZ>(P, f_pw, acc, lane);
     const f32x4 sc = *reinterpret_cast<const f32x4*>(par + P_SC + wid * 16 + 4 * g);
     const f32x4 sh = *reinterpret_cast<const f32x4*>(par + P_SH + wid * 16 + 4 * g);
 #pragma unroll
@@ -758,13 +783,17 @@ constexpr int HD = 64;
 constexpr int HID = 512;
 constexpr int NT = 512;
 constexpr int LT = C + 4;           // T row stride (floats)
-constexpr int PSU = C + 8;          // U / hidden-chunk plane row stride (fp16)
+// U / hidden-chunk and O planes: rows padded to 272 / 144 elements with the 16-byte chunks of a row swizzled in their
+// low two index bits by row bits 2-3 (swz_row): the GEMM operand reads (ds_read_b128, lane = (row l15, chunk g) + k)
+// are then conflict-free and the swizzle stays additive in k (at 264 / 136 unswizzled they were 2-way); the accumulator
+// stores (ds_write_b64, 16 rows x one column group) stay 2-way
+constexpr int PSU = 272;            // U / hidden-chunk plane row stride (fp16)
 constexpr int UPL = NR * PSU;       // plane stride (49 rows)
 constexpr int PSK = 128 + 8;        // K planes of a head pair [49][PSK]
 constexpr int KPL = NR * PSK;
 constexpr int PSV = 56;             // V^T planes of a head pair [128][PSV]: keys 0..55 stored; the MFMA reads keys
 constexpr int VPL = 128 * PSV;      // up to 63 (P = 0 there), i.e. into the next row / the K planes (finite)
-constexpr int PSO = 128 + 8;        // O planes of a head pair [64][PSO]
+constexpr int PSO = 144;            // O planes of a head pair [64][PSO]
 constexpr int OPL = 64 * PSO;
 constexpr int QBUF = 2 * 8 * 512;   // staged Q weight fragments of one 32-k step (2 planes x 8 column blocks)
 constexpr int HALF = 128;           // channels per halo half
@@ -779,6 +808,22 @@ static_assert(HALO_B <= U_B + WR_B, "halo patch");
 static_assert(2 * QBUF * 2 <= WR_B, "staged Q weights");
 static_assert(T_B % 16 == 0 && U_B % 16 == 0 && WR_B % 16 == 0, "16-byte aligned regions");
 static_assert(T_B + U_B + WR_B <= 160 * 1024, "LDS");
+
+__device__ __forceinline__ int swz_row(int row) { return ((row >> 2) & 1) | (((row >> 3) & 1) << 1); }
+// element (row, col) of a swizzled U / hidden / O plane
+template <int PS>
+__device__ __forceinline__ int poff(int row, int col) {
+  return row * PS + ((((col >> 3) ^ swz_row(row))) << 3) + (col & 7);
+}
+// the two planes of 4 consecutive elements of row `row`, column `col` (a multiple of 4), swizzled
+template <int PS, int PL>
+__device__ __forceinline__ void store4(h16_t* P, int row, int col, f32x4 v) {
+  uint2 h, l;
+  split4(v, h, l);
+  h16_t* d = P + poff<PS>(row, col);
+  *reinterpret_cast<uint2*>(d) = h;
+  *reinterpret_cast<uint2*>(d + PL) = l;
+}
 
 // acc[rb][j] += (B rows (rb0 + rb)*16 + l15 . W[cb[j]*16 + l15]^T)^T over k in [koff, koff + K): W = two fp16
 // planes [2][N][KT] in global memory (L2), the token rows = two LDS planes (row stride PS, plane stride PL; rows
@@ -798,7 +843,7 @@ __device__ __forceinline__ void gemm_w(const h16_t* __restrict__ Wp, int N, int 
   for (int rb = 0; rb < NRB; ++rb) {
     int row = (rb0 + rb) * 16 + l15;
     if (CLAMP) row = row < NR ? row : NR - 1;
-    ar[rb] = A + row * PS + 8 * g;
+    ar[rb] = A + row * PS + 8 * (g ^ swz_row(row));  // k steps are whole 4-chunk groups: the swizzle adds
   }
   f16x8_t w0[KS][NJ][2], w1[KS][NJ][2];
   auto ldw = [&](f16x8_t (&w)[KS][NJ][2], int st) {
@@ -840,7 +885,9 @@ __device__ __forceinline__ void gemm_w(const h16_t* __restrict__ Wp, int N, int 
 }
 
 // LayerNorm (normalisation only; the affine is folded into the next GEMM's weights) of T rows [0, 49) into the two
-// U planes: 8 lanes per row (512 threads = 64 rows), 32 values each
+// U planes: 8 lanes per row (512 threads = 64 rows), 32 values each - lane `part` takes columns part*8 + 64j .. +7
+// (j = 0..3), so the 8 lanes of a row store one contiguous 128-byte run per j (with 32 contiguous columns per lane
+// the plane stores were 4-way bank conflicts)
 __device__ __forceinline__ void ln_planes8(const float* T, h16_t* U, float eps, int tid) {
   const int r = tid >> 3, part = tid & 7;
   const bool valid = r < NR;
@@ -848,7 +895,8 @@ __device__ __forceinline__ void ln_planes8(const float* T, h16_t* U, float eps, 
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    v[i] = valid ? *reinterpret_cast<const f32x4*>(T + r * LT + part * 32 + 4 * i) : f32x4{0.f, 0.f, 0.f, 0.f};
+    v[i] = valid ? *reinterpret_cast<const f32x4*>(T + r * LT + part * 8 + 64 * (i >> 1) + 4 * (i & 1))
+                 : f32x4{0.f, 0.f, 0.f, 0.f};
     s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
   }
   s = quad_sum(s);
@@ -869,7 +917,7 @@ __device__ __forceinline__ void ln_planes8(const float* T, h16_t* U, float eps, 
       uint2 h0, l0, h1, l1;
       split4(v[i] * rs, h0, l0);
       split4(v[i + 1] * rs, h1, l1);
-      h16_t* d = U + r * PSU + part * 32 + 4 * i;
+      h16_t* d = U + poff<PSU>(r, part * 8 + 64 * (i >> 1));
       *reinterpret_cast<uint4*>(d) = make_uint4(h0.x, h0.y, h1.x, h1.y);
       *reinterpret_cast<uint4*>(d + UPL) = make_uint4(l0.x, l0.y, l1.x, l1.y);
     }
@@ -1014,7 +1062,8 @@ __global__ __launch_bounds__(NT, 1) void swin_wx_kernel(Args p) {
       *reinterpret_cast<uint4*>(qdst) = qv0;
       *reinterpret_cast<uint4*>(qdst + 8) = qv1;
       __syncthreads();
-      const h16_t* ub = UP + (qb * 16 + l15 < NR ? qb * 16 + l15 : NR - 1) * PSU + 8 * g;
+      const int urow = qb * 16 + l15 < NR ? qb * 16 + l15 : NR - 1;
+      const h16_t* ub = UP + urow * PSU + 8 * (g ^ swz_row(urow));
 #pragma unroll 1
       for (int kc = 0; kc < C / 32; ++kc) {
         const int buf = kc & 1;
@@ -1158,7 +1207,7 @@ __global__ __launch_bounds__(NT, 1) void swin_wx_kernel(Args p) {
 #pragma unroll
     for (int db = 0; db < HD / 16; ++db)
     {
-      store_planes4<PSO, OPL>(Op, qb * 16 + l15, lh * HD + db * 16 + 4 * g, ov[db]);
+      store4<PSO, OPL>(Op, qb * 16 + l15, lh * HD + db * 16 + 4 * g, ov[db]);
       rng = range_acc(rng, ov[db]);
     }
     __syncthreads();
@@ -1211,7 +1260,7 @@ __global__ __launch_bounds__(NT, 1) void swin_wx_kernel(Args p) {
         const f32x4 a = ah[rb][j] * (1.0f / WSC);
         const f32x2 lo = gelu2_fast_(f32x2{a[0], a[1]});
         const f32x2 hi = gelu2_fast_(f32x2{a[2], a[3]});
-        if (tok < NR) store_planes4<PSU, UPL>(Hp, tok, cbo[j] * 16 + 4 * g, f32x4{lo.x, lo.y, hi.x, hi.y});
+        if (tok < NR) store4<PSU, UPL>(Hp, tok, cbo[j] * 16 + 4 * g, f32x4{lo.x, lo.y, hi.x, hi.y});
         rng = range_acc(rng, f32x4{lo.x, lo.y, hi.x, hi.y});
       }
     }
@@ -1228,7 +1277,7 @@ __global__ __launch_bounds__(NT, 1) void swin_wx_kernel(Args p) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const f32x4 v = *reinterpret_cast<const f32x4*>(T + tok * LT + cbo[j] * 16 + 4 * g) + acc_m[rb][j] * (1.0f / WSC);
-        store_planes4<PSU, UPL>(UP, tok, cbo[j] * 16 + 4 * g, v);
+        store4<PSU, UPL>(UP, tok, cbo[j] * 16 + 4 * g, v);
         rng = range_acc(rng, v);
       }
     }
@@ -1654,6 +1703,22 @@ YS_EXPORT int yolosod_debug_set_swin_split(int on) {
 }
 static bool x3_split(int C) { return C == x3::tok::C && swin_split_env(); }
 
+// C = 64 kernel planes: chunk-swizzled unpadded rows (1, default; env YOLOSOD_X3_SWZ=0: rows padded to 80)
+static int g_x3_swz = -1;
+static bool x3_swz_env() {
+  if (g_x3_swz < 0) {
+    const char* e = getenv("YOLOSOD_X3_SWZ");
+    g_x3_swz = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_x3_swz != 0;
+}
+// Test hook: the C = 64 kernel's plane layout, swizzled (1) or padded (0); returns the previous state.
+YS_EXPORT int yolosod_debug_set_x3_swz(int on) {
+  const int prev = x3_swz_env() ? 1 : 0;
+  g_x3_swz = on ? 1 : 0;
+  return prev;
+}
+
 // images per launch of the split pair: the token-tiled kernel addresses x / y / T1 with 32-bit buffer offsets
 static int x3_split_chunk(int C, int H, int W) {
   const long per = (long)C * H * W * 4;
@@ -1782,8 +1847,12 @@ int yolosod_swin_x3_run(const float* x, float* y, int B, int C, int H, int W, in
       ac.B = nb;
       ac.t1 = (float*)ws;
       const long nw = (long)nb * nWin;
-      hipLaunchKernelGGL((x3::swin_x3_kernel<64, 2, true>), dim3((unsigned)(8 * ((nw + 7) / 8))), dim3(256), 0, st,
-                         ac);
+      if (x3_swz_env())
+        hipLaunchKernelGGL((x3::swin_x3_kernel<64, 2, true, true>), dim3((unsigned)(8 * ((nw + 7) / 8))), dim3(256), 0,
+                           st, ac);
+      else
+        hipLaunchKernelGGL((x3::swin_x3_kernel<64, 2, true>), dim3((unsigned)(8 * ((nw + 7) / 8))), dim3(256), 0, st,
+                           ac);
       x3::tok::Args tk{(const float*)ws, ac.x, ac.y, nb, H * W, q.mfrag, q.b1_f, mlp2_b, q.bn_sc, q.bn_sh, ln2_eps,
                        flag, q.pflag};
       const long ntile = ((long)nb * H * W + 31) / 32;
@@ -1792,7 +1861,11 @@ int yolosod_swin_x3_run(const float* x, float* y, int B, int C, int H, int W, in
       hipLaunchKernelGGL(x3::tok::swin_mlp_kernel, dim3(grid), dim3(x3::tok::NT), 0, st, tk);
     }
   } else if (C == 64) {
-    hipLaunchKernelGGL((x3::swin_x3_kernel<64, 2>), dim3((unsigned)(8 * ((nwin + 7) / 8))), dim3(256), 0, st, a);
+    if (x3_swz_env())
+      hipLaunchKernelGGL((x3::swin_x3_kernel<64, 2, false, true>), dim3((unsigned)(8 * ((nwin + 7) / 8))), dim3(256), 0,
+                         st, a);
+    else
+      hipLaunchKernelGGL((x3::swin_x3_kernel<64, 2>), dim3((unsigned)(8 * ((nwin + 7) / 8))), dim3(256), 0, st, a);
   } else {
     hipLaunchKernelGGL(x3::wx::swin_wx_kernel, dim3((unsigned)(8 * ((nwin + 7) / 8))), dim3(x3::wx::NT), 0, st, a);
   }
