@@ -41,18 +41,26 @@ typedef short s16x8 __attribute__((ext_vector_type(8)));
 // out[row][h*HD + d]. grid = (ceil(L/64), heads, n_seq); 256 threads, wave w owns queries q0 + 16w .. +15.
 // MFMA 16x16x32 bf16: A/B lane l holds [row l&15][k = 8(l>>4) + j]; C/D lane l holds [row 4(l>>4) + r][col l&15].
 // S = Q K^T (fp32), softmax(S * scale) in fp32 with the row spread over the 16 lanes of a lane group, P rounded to
-// bf16 (the reference bf16 model's P), O = P V with V^T staged in LDS (operand rows = d, k = key).
+// bf16 (the reference bf16 model's P), O = P V. V is staged row-major like K (16-byte stores) and read transposed into
+// the PV B operand with ds_read_b64_tr_b16: staging V^T with 2-byte stores had 16 lanes of one key on one bank
+// (16-way conflicts; 74 % of the kernel's LDS cycles at L9_m). The 16-column blocks of the V rows with bit 3 set are
+// XOR-swapped with the other half of the row (vcol), so the two key quads a 32-lane half reads (rows 8 apart) sit on
+// disjoint banks.
 // =================================================================================================
+template <int HD>
+__device__ __forceinline__ int vcol(int row, int col) {
+  return (((col >> 4) ^ (((row >> 3) & 1) * (HD / 32))) << 4) | (col & 15);
+}
 template <int HD, int NKB>
 __global__ __launch_bounds__(256) void window_attn_bf16_kernel(const bf16_t* __restrict__ qkv, int C,
                                                                bf16_t* __restrict__ out, TokMap tm, float scale) {
   constexpr int NK = NKB * 16;       // keys (padded)
   constexpr int KS = HD + 8;         // K row stride (elements)
-  constexpr int VS = NK + 8;         // V^T row stride
+  constexpr int VS = HD + 16;        // V row stride (keys are rows)
   constexpr int PS = NK + 8;         // P row stride
   static_assert(NK % 32 == 0 && HD % 32 == 0, "k steps of 32");
   __shared__ __attribute__((aligned(16))) bf16_t Ks[NK * KS];
-  __shared__ __attribute__((aligned(16))) bf16_t Vt[HD * VS];
+  __shared__ __attribute__((aligned(16))) bf16_t Vr[NK * VS];
   __shared__ __attribute__((aligned(16))) bf16_t Ps[4 * 16 * PS];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int h = blockIdx.y;
@@ -71,12 +79,7 @@ __global__ __launch_bounds__(256) void window_attn_bf16_kernel(const bf16_t* __r
       vv = *reinterpret_cast<const uint4*>(src + 2 * C);
     }
     *reinterpret_cast<uint4*>(&Ks[key * KS + dc]) = kv;
-    const uint32_t w[4] = {vv.x, vv.y, vv.z, vv.w};
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      Vt[(dc + 2 * q) * VS + key] = (bf16_t)(w[q] & 0xffffu);
-      Vt[(dc + 2 * q + 1) * VS + key] = (bf16_t)(w[q] >> 16);
-    }
+    *reinterpret_cast<uint4*>(&Vr[key * VS + vcol<HD>(key, dc)]) = vv;
   }
   // this wave's Q fragments (rows >= L read row L-1: finite values, results dropped)
   const int q0 = blockIdx.x * 64 + wv * 16;
@@ -144,13 +147,23 @@ __global__ __launch_bounds__(256) void window_attn_bf16_kernel(const bf16_t* __r
   f32x4 oacc[HD / 16];
 #pragma unroll
   for (int db = 0; db < HD / 16; ++db) oacc[db] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // transposed V reads: lane 4q + p of lane group g supplies row (key) 32s + 8g + q (+ 4), columns db*16 + 4p .. +3;
+  // lane l15 receives column (d) db*16 + l15 of the 4 keys - the B operand's k slots 8g .. 8g + 3 (+ 4 .. 7)
+  const int tq = l15 >> 2, tp = l15 & 3;
 #pragma unroll
   for (int s = 0; s < NK / 32; ++s) {
     const bf16x8_t pa = *reinterpret_cast<const bf16x8_t*>(Pw + l15 * PS + 32 * s + 8 * g);
+    const int r0 = 32 * s + 8 * g + tq;
 #pragma unroll
     for (int db = 0; db < HD / 16; ++db) {
-      const bf16x8_t vb = *reinterpret_cast<const bf16x8_t*>(Vt + (db * 16 + l15) * VS + 32 * s + 8 * g);
-      oacc[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vb, oacc[db], 0, 0, 0);
+      typedef short s16x4 __attribute__((ext_vector_type(4)));
+      typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+      const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (lds_s16x4*)(Vr + r0 * VS + vcol<HD>(r0, db * 16 + 4 * tp)));
+      const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (lds_s16x4*)(Vr + (r0 + 4) * VS + vcol<HD>(r0 + 4, db * 16 + 4 * tp)));
+      const s16x8 v8 = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+      oacc[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, __builtin_bit_cast(bf16x8_t, v8), oacc[db], 0, 0, 0);
     }
   }
 #pragma unroll
@@ -165,7 +178,7 @@ __global__ __launch_bounds__(256) void window_attn_bf16_kernel(const bf16_t* __r
 
 template <int HD, int N>
 constexpr size_t wattn_lds_bytes() {
-  return sizeof(bf16_t) * ((size_t)N * 16 * (HD + 8) + (size_t)HD * (N * 16 + 8) + 64 * (size_t)(N * 16 + 8));
+  return sizeof(bf16_t) * ((size_t)N * 16 * (HD + 8) + (size_t)N * 16 * (HD + 16) + 64 * (size_t)(N * 16 + 8));
 }
 
 template <int HD>
