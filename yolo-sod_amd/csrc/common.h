@@ -96,6 +96,7 @@ __device__ __forceinline__ f32x2 gelu2_fast_(f32x2 x) {
 // x / (1 + e^-x) as x * rcp(1 + e^-x): v_rcp_f32 (1 ulp) instead of the 10-instruction IEEE division sequence
 // (__fdividef is a full-precision divide on this target)
 __device__ __forceinline__ float silu_fast_(float x) { return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
+__device__ __forceinline__ float sigmoid_fast_(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
 
 // wave64 reductions
 __device__ __forceinline__ float wave_sum(float v) {

@@ -537,7 +537,9 @@ __global__ __launch_bounds__(256, C3 > 64 ? 2 : 3) void detect_head_x2_kernel(He
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int c = 4 * g + r;
-      if (c < nc) yb[(long)(4 + c) * d.A + p] = sigmoidf_(acc[4][r] * (1.0f / WS) + bcr[r]);
+      // class score: sigmoid on the hardware exp2 / rcp (1-2 ulp; the libm expf + IEEE division were ~15 % of the
+      // kernel's VALU, and the split products already carry a few ulp)
+      if (c < nc) yb[(long)(4 + c) * d.A + p] = sigmoid_fast_(acc[4][r] * (1.0f / WS) + bcr[r]);
     }
   };
   static_assert(NTS % 2 == 0, "group pairs");
