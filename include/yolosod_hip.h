@@ -238,6 +238,10 @@ int yolosod_debug_set_swin_split(int on);
 /* Test hook: the C = 64 fp16-split SwinBlock kernel's activation planes as unpadded rows with XOR-swizzled 16-byte
  * chunks (1, default; env YOLOSOD_X3_SWZ=0 turns it off) or rows padded to 80 elements (0); same results. */
 int yolosod_debug_set_x3_swz(int on);
+/* Test hook: pixels per area group of the A2 proj + SiLU + pooling kernel (the launcher takes the fewest area groups
+ * whose row bands fit; 208 by default - two workgroups per CU - env YOLOSOD_A2_POOL_PX; <= 0 restores 208). Same
+ * results for every cap. Returns the previous cap. */
+int yolosod_debug_set_a2_pool_px(int px);
 /* Test hook: 1 (default; env YOLOSOD_HEAD_X2=0 turns it off) runs the Detect head's 1x1 convs as fp16 two-term
  * splits on the fp16 matrix cores (detect_head_x2_kernel), 0 on the exact fp32 MFMA (detect_head_lds_kernel). */
 int yolosod_debug_set_head_x2(int on);

@@ -198,6 +198,30 @@ def test_a2_fused_and_decomposed_forms(name, fused, cuda, monkeypatch):
     assert ok, f"{name} fused={fused}: vs fp64 oracle max abs err {err:.3g} (ratio {ratio:.2f})"
 
 
+@pytest.mark.parametrize("name", ["a2_c512_h20", "a2_L12", "a2_b3_c256_12x8", "a2_b2_c192_10x20"])
+def test_a2_proj_pool_area_groups_bit_identical(name, cuda, monkeypatch):
+    """The proj + SiLU + pooling kernel over one tile per image (cap 400 pixels) and split into area groups (cap 208,
+    the default: two groups of 10 rows at 20x20; cap 100: four groups) computes every pixel with the same k order, so
+    the outputs are bit-identical."""
+    lib = _hip.load_library()
+    if A2_FUSED_SHAPES[name] is not None:
+        monkeypatch.setitem(recipes.OPS, name, A2_FUSED_SHAPES[name])
+    m, _ = build_fixture_module(name)
+    m = m.to(cuda)
+    x = recipes.make_input(name, recipes.OPS[name][2]).to(cuda)
+    prev = lib.yolosod_debug_set_a2_pool_px(400)
+    try:
+        with torch.inference_mode():
+            ys = [m(x).cpu()]
+            for cap in (208, 100):
+                lib.yolosod_debug_set_a2_pool_px(cap)
+                ys.append(m(x).cpu())
+    finally:
+        lib.yolosod_debug_set_a2_pool_px(prev)
+    for cap, y in zip((208, 100), ys[1:]):
+        assert torch.equal(ys[0], y), f"{name} cap {cap}: max|d| {float((ys[0] - y).abs().max()):.3g}"
+
+
 @pytest.mark.parametrize("name,shape", [("se_c32_r64", (9, 32, 64, 64)), ("se_c64_r4_odd", (5, 64, 9, 7)),
                                         ("cbam_c64", (9, 64, 48, 40)), ("cbam_c32_odd", (5, 32, 13, 11)),
                                         ("ca_c128", (9, 128, 24, 20)), ("ca_c64_odd", (5, 64, 9, 7))])

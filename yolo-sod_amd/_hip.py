@@ -84,6 +84,7 @@ SIGNATURES = {
     "yolosod_debug_set_a2_fused": (_i, [_i]),
     "yolosod_debug_set_swin_tokln": (_i, [_i]),
     "yolosod_debug_set_x3_swz": (_i, [_i]),
+    "yolosod_debug_set_a2_pool_px": (_i, [_i]),
     "yolosod_mamba_glu_workspace": (_sz, [_i, _i, _i, _i, _i, _i]),
     "yolosod_mamba_glu_forward": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _f, _vp, _vp,
                                        _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp, _vp, _vp, _f, _vp, _sz, _vp]),

@@ -317,24 +317,43 @@ __global__ __launch_bounds__(512, 1) void a2_qkv_attn_kernel(Args p) {
 
 // ---- proj 1x1 conv (BN folded) + SiLU + adaptive row pooling to the area tokens, one kernel ----------------------
 // a2_attn.py:39-48: x_proj = SiLU(conv1x1(x)) (Conv with folded BN), pooled = adaptive_avg_pool2d(x_proj, (A, W)),
-// seq = pooled.flatten(2).transpose(1, 2). One 512-thread workgroup per (image, 64 output channels) computes the
-// [64][H*W] tile of x_proj on fp16-split MFMA (weights = the A operand, pixels = B), keeps it in LDS and averages
-// the row bins [floor(a H / A), ceil((a + 1) H / A)) straight into the token-major S rows: x_proj never reaches HBM
-// (the decomposed path wrote and re-read it, 26 MB each way at bs 32). The x tile of each 32-channel k step is staged
-// as 4x4 (k, pixel) blocks transposed in registers into [pixel][k] fp16 planes (double-buffered).
-constexpr int PMAXHW = 400;   // pixels per image the tile holds (20x20 at 640^2)
+// seq = pooled.flatten(2).transpose(1, 2). One 512-thread workgroup per (image, 64 output channels, area group)
+// computes the [64][pixels] tile of x_proj over the rows its areas pool on fp16-split MFMA (weights = the A operand,
+// pixels = B), keeps it in LDS and averages the row bins [floor(a H / A), ceil((a + 1) H / A)) straight into the
+// token-major S rows: x_proj never reaches HBM (the decomposed path wrote and re-read it, 26 MB each way at bs 32).
+// Area group q of G takes areas [q A / G, (q + 1) A / G) and the rows [floor(a0 H / A), ceil(a1 H / A)) they pool
+// (a row shared by two bins at a group edge is computed by both groups): at 20x20 / 8 areas two groups of 10 rows
+// halve the tile, so two workgroups share a CU and hide each other's load latency (one per CU waited on memory half
+// of its cycles): the half-tile kernel runs 4 waves (each with the column blocks and registers of a wave of the
+// one-tile kernel), so a CU holds two independent workgroups. The x tile of each 32-channel k step is staged as 4x4
+// (k, pixel) blocks transposed in registers into [pixel][k] fp16 planes (double-buffered).
+constexpr int PMAXHW = 400;   // pixels per area group the tile holds (20x20 at 640^2 in one group)
 constexpr int PPS = 40;       // staged plane row stride (halves): 32 k + 8
-template <int NCB>            // 16-pixel column blocks per image
-__global__ __launch_bounds__(512, 1) void a2_proj_pool_kernel(const float* __restrict__ x, const h16_t* __restrict__ wp,
-                                                              const float* __restrict__ bp, float* __restrict__ S,
-                                                              int C, int H, int W, int A, unsigned* range_flag) {
+struct PoolGroup {
+  int a0, a1, r0, r1;  // areas [a0, a1), rows [r0, r1)
+};
+__host__ __device__ inline PoolGroup pool_group(int q, int G, int A, int H) {
+  PoolGroup g;
+  g.a0 = (q * A) / G;
+  g.a1 = ((q + 1) * A) / G;
+  g.r0 = (g.a0 * H) / A;
+  g.r1 = (g.a1 * H + A - 1) / A;
+  return g;
+}
+template <int NCB, int NW>  // 16-pixel column blocks per area group, waves; (13, 4): two workgroups per CU
+__global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void a2_proj_pool_kernel(const float* __restrict__ x,
+                                                                              const h16_t* __restrict__ wp,
+                                                                              const float* __restrict__ bp,
+                                                                              float* __restrict__ S, int C, int H,
+                                                                              int W, int A, int G,
+                                                                              unsigned* range_flag) {
   constexpr int NPX = NCB * 16;                 // padded pixels
   constexpr int PPL = NPX * PPS;                // plane (halves)
   constexpr int STG_B = 2 * 2 * PPL * 2;        // two buffers x two planes
   constexpr int HWP = NPX + 1;                  // fp32 tile row stride (odd: conflict-free per-channel reads)
   constexpr int T_B = 64 * HWP * 4;
   constexpr int R_B = STG_B > T_B ? STG_B : T_B;
-  constexpr int NT = 512, NW = 8;
+  constexpr int NT = 64 * NW;
   constexpr int CBW = (NCB + NW - 1) / NW;      // column blocks per wave
   static_assert(R_B <= 160 * 1024, "LDS");
   __shared__ __attribute__((aligned(16))) char smem[R_B];
@@ -346,9 +365,13 @@ __global__ __launch_bounds__(512, 1) void a2_proj_pool_kernel(const float* __res
   const int HW = H * W;
   const int ncb64 = C / 64;
   const int nblk = gridDim.x;
+  // XCD-aware: consecutive wg (the channel blocks and area groups of one image) on one XCD
   const int wg = (nblk & 7) ? (int)blockIdx.x : (int)(blockIdx.x & 7) * (nblk >> 3) + (int)(blockIdx.x >> 3);
-  const int img = wg / ncb64, co = (wg - img * ncb64) * 64;
-  const float* xb = x + (long)img * C * HW;
+  const int img = wg / (ncb64 * G), rem = wg - img * ncb64 * G;
+  const int grp = rem / ncb64, co = (rem - grp * ncb64) * 64;
+  const PoolGroup pg = pool_group(grp, G, A, H);
+  const int npx = (pg.r1 - pg.r0) * W;  // the group's pixels (a multiple of 4: W % 4 == 0 when G > 1)
+  const float* xb = x + (long)img * C * HW + pg.r0 * W;
   float rng = 0.f;
 
   // staging: (4 k x 4 pixel) blocks of the 32 x NPX step tile; 8 * NPX / 4 blocks
@@ -359,13 +382,14 @@ __global__ __launch_bounds__(512, 1) void a2_proj_pool_kernel(const float* __res
   auto load_step = [&](float4 (&stg)[NIT][4], int s) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < NIT; ++i) {
+      // every load unconditional, its pixel clamped into the group: a load under a branch merges into a phi, and
+      // the merge waited for every load in flight (vmcnt(0) between the load pairs of a step). Blocks past NBLK are
+      // not stored; pixels past npx land in the tile's padding columns, whose outputs nothing reads.
       const int e = tid + NT * i;
       const int kq = e & 7, pq = e >> 3;  // k group fastest: the LDS stores of 8 lanes fill one 64-byte row run
-      const int k = 32 * s + 4 * kq, px = 4 * pq;
+      const int k = 32 * s + 4 * kq, px = min(4 * pq, npx - 4);
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        stg[i][r] = (e < NBLK && px < HW) ? *reinterpret_cast<const float4*>(xb + (long)(k + r) * HW + px)
-                                          : make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int r = 0; r < 4; ++r) stg[i][r] = *reinterpret_cast<const float4*>(xb + (long)(k + r) * HW + px);
     }
   };
   auto store_step = [&](const float4 (&stg)[NIT][4], int buf) __attribute__((always_inline)) {
@@ -411,14 +435,16 @@ __global__ __launch_bounds__(512, 1) void a2_proj_pool_kernel(const float* __res
     // entry: step s's planes are stored (buffer s & 1), `next` holds step s + 1's loads in flight, `stored` is free
     const int buf = s & 1;
     // unconditional (clamped) loads: a register set written on some trips only becomes a phi whose copies wait
-    // for the loads in flight
-    load_step(stored, s + 2 < nk32 ? s + 2 : nk32 - 1);
+    // for the loads in flight. The next step's weight fragments go out before the x tile two steps ahead: the
+    // vmcnt queue is in order, so waiting for the weights (one step of lookahead) would otherwise also wait for the
+    // x loads issued with them, and the x tile would get one step of latency, not two.
     const int sw = s + 1 < nk32 ? s + 1 : nk32 - 1;
 #pragma unroll
     for (int rb = 0; rb < 4; ++rb) {
       wb[rb][0] = wfrag(rb, sw, 0);
       wb[rb][1] = wfrag(rb, sw, 1);
     }
+    load_step(stored, s + 2 < nk32 ? s + 2 : nk32 - 1);
     __syncthreads();  // step s's planes stored; every wave is done with step s - 1's buffer
     const h16_t* b0 = Pl + (buf * 2) * PPL + l15 * PPS + 8 * g;
 #pragma unroll
@@ -466,11 +492,11 @@ __global__ __launch_bounds__(512, 1) void a2_proj_pool_kernel(const float* __res
   }
   __syncthreads();
   // pooled tokens: thread (c = tid % 64, column group tid / 64) averages its channel's bins in row order (as the
-  // reference's CPU pooling) for the columns w = tid / 64 + 8 i of every area
+  // reference's CPU pooling) for the columns w = tid / 64 + 8 i of every area of the group
   const int c = tid & 63;
-  const float* trow = Tt + c * HWP;
+  const float* trow = Tt + c * HWP - pg.r0 * W;
   float* Sb = S + (long)img * A * W * C + co + c;
-  for (int a = 0; a < A; ++a) {
+  for (int a = pg.a0; a < pg.a1; ++a) {
     const int r0 = (a * H) / A, r1 = ((a + 1) * H + A - 1) / A;
     const float cnt = (float)(r1 - r0);
     for (int w = tid >> 6; w < W; w += NW) {
@@ -587,10 +613,45 @@ int yolosod_a2_fused_prepare(int C, const float* proj_w, const float* ln_w, cons
   return 0;
 }
 
-// the proj + SiLU + pooling kernel's shapes: C a multiple of 64, one image's pixels within the LDS tile
-bool yolosod_a2_proj_pool_ok(int C, int H, int W) {
+// Area groups of the proj + SiLU + pooling kernel: the fewest groups whose row bands fit `cap` pixels (0: none fit).
+// Groups > 1 need W % 4 == 0 (16-byte aligned band starts).
+static int g_a2_pool_cap = -1;  // pixels per group the launcher aims for (YOLOSOD_A2_POOL_PX; 208: 2 workgroups / CU)
+static int a2_pool_cap() {
+  if (g_a2_pool_cap < 0) {
+    const char* e = getenv("YOLOSOD_A2_POOL_PX");
+    g_a2_pool_cap = e ? atoi(e) : 208;
+    if (g_a2_pool_cap <= 0 || g_a2_pool_cap > a2f::PMAXHW) g_a2_pool_cap = a2f::PMAXHW;
+  }
+  return g_a2_pool_cap;
+}
+static int a2_pool_groups(int H, int W, int A, int cap, int* max_px) {
+  for (int G = 1; G <= A; ++G) {
+    if (G > 1 && W % 4 != 0) break;
+    int mx = 0;
+    for (int q = 0; q < G; ++q) {
+      const a2f::PoolGroup g = a2f::pool_group(q, G, A, H);
+      const int px = (g.r1 - g.r0) * W;
+      mx = px > mx ? px : mx;
+    }
+    if (mx <= cap && mx % 4 == 0) {
+      if (max_px) *max_px = mx;
+      return G;
+    }
+  }
+  return 0;
+}
+// Test hook: pixels per area group of the proj / pool kernel (0: the default); returns the previous cap.
+YS_EXPORT int yolosod_debug_set_a2_pool_px(int px) {
+  const int prev = a2_pool_cap();
+  g_a2_pool_cap = (px <= 0 || px > a2f::PMAXHW) ? 208 : px;
+  return prev;
+}
+
+// the proj + SiLU + pooling kernel's shapes: C a multiple of 64, every area group's rows within the LDS tile
+bool yolosod_a2_proj_pool_ok(int C, int H, int W, int A) {
   const bool on = a2_fused_env();
-  return on && C % 64 == 0 && C <= 1024 && (long)H * W <= a2f::PMAXHW && ((long)H * W) % 4 == 0;
+  return on && C % 64 == 0 && C <= 1024 && A > 0 &&
+         (a2_pool_groups(H, W, A, a2_pool_cap(), nullptr) > 0 || a2_pool_groups(H, W, A, a2f::PMAXHW, nullptr) > 0);
 }
 
 // x -> S (token-major pooled SiLU(proj x + bp)). Returns < 0 on error.
@@ -598,19 +659,22 @@ int yolosod_a2_proj_pool_run(const float* x, const float* proj_b, float* S, int 
                              const void* prep, size_t prep_bytes, hipStream_t st) {
   A2Prep q;
   YS_CHECK_ARG(a2f_carve(const_cast<void*>(prep), prep_bytes, C, q), "a2: prepared block too small");
-  YS_CHECK_ARG(yolosod_a2_proj_pool_ok(C, H, W), "a2: proj/pool shape C=%d %dx%d not fused", C, H, W);
+  YS_CHECK_ARG(yolosod_a2_proj_pool_ok(C, H, W, A), "a2: proj/pool shape C=%d %dx%d A=%d not fused", C, H, W, A);
   YS_CHECK_ARG(((uintptr_t)x & 15) == 0, "a2: x must be 16-byte aligned");
-  const long nwg = (long)B * (C / 64);
+  int mx = 0;
+  int G = a2_pool_groups(H, W, A, a2_pool_cap(), &mx);
+  if (G == 0) G = a2_pool_groups(H, W, A, a2f::PMAXHW, &mx);
+  const long nwg = (long)B * (C / 64) * G;
   YS_CHECK_ARG(nwg < (1L << 31), "a2: too many workgroups");
-  const int ncb = (H * W + 15) / 16;
-#define YS_A2P(N)                                                                                                    \
+  const int ncb = (mx + 15) / 16;
+#define YS_A2P(N, NW)                                                                                                \
   if (ncb <= N) {                                                                                                     \
-    hipLaunchKernelGGL((a2f::a2_proj_pool_kernel<N>), dim3((unsigned)nwg), dim3(512), 0, st, x, q.pplanes, proj_b, S, \
-                       C, H, W, A, range_flag_dev());                                                                 \
+    hipLaunchKernelGGL((a2f::a2_proj_pool_kernel<N, NW>), dim3((unsigned)nwg), dim3(64 * NW), 0, st, x, q.pplanes,   \
+                       proj_b, S, C, H, W, A, G, range_flag_dev());                                                   \
     YS_CHECK_LAUNCH("a2_proj_pool");                                                                                  \
     return 0;                                                                                                         \
   }
-  YS_A2P(4) YS_A2P(8) YS_A2P(13) YS_A2P(16) YS_A2P(25)
+  YS_A2P(4, 4) YS_A2P(8, 4) YS_A2P(13, 4) YS_A2P(16, 8) YS_A2P(25, 8)
 #undef YS_A2P
   YS_CHECK_ARG(false, "a2: %dx%d pixels too many for the proj/pool kernel", H, W);
   return -1;

@@ -136,6 +136,7 @@ __device__ __forceinline__ float xor32_max(float v) {
 // fp32 MFMA fragment types
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 
 // ---- bf16 storage (the bf16 model config: activations in HBM as bf16, arithmetic in fp32) ------------------
 // bf16 values cross the C ABI as their 16-bit patterns (uint16_t, torch.bfloat16's layout). Widening is exact

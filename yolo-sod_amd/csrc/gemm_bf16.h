@@ -219,41 +219,35 @@ __global__ __launch_bounds__(256, A_LN ? 2 : 3) void gemm_bf16_kernel(GemmB g) {
     }
   }
 
-  uint4 ra[NA], rb[NB];
+  // rb as a native vector: a uint4 (struct) element copied global -> array -> LDS stays a memcpy through a stack
+  // array once its load is unconditional (scratch round trip per tile)
+  uint4 ra[NA];
+  u32x4_t rb[NB];
   int cur_k0 = 0;  // k offset of the tile held in ra / rb (LN params of the A prologue)
+  // Every tile load is unconditional: rows past M / N read row M-1 / N-1 and an N-contiguous chunk past N reads
+  // column 0, whose products land in output rows / columns the epilogue never stores. A load under a per-lane
+  // predicate merges into a phi whose copy waited for every load in flight (vmcnt(0) after each load of a tile).
+  // A partial N-contiguous chunk (n < N < n + 8) reads up to ldb (ldb % 8 == 0): in bounds, and its columns past N
+  // only feed unstored outputs.
   auto load_tiles = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       const int idx = tid + 256 * i;
-      const int r = idx >> 3, kc = (idx & 7) * 8;
-      const int m = m0 + r;
-      ra[i] = make_uint4(0u, 0u, 0u, 0u);
-      if (m < M) ra[i] = *reinterpret_cast<const uint4*>(A + (long)m * g.lda + k0 + kc);
+      const int m = m0 + (idx >> 3);
+      ra[i] = *reinterpret_cast<const uint4*>(A + (long)(m < M ? m : M - 1) * g.lda + k0 + (idx & 7) * 8);
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
       const int idx = tid + 256 * i;
       if (B_KC) {
-        const int r = idx >> 3, kc = (idx & 7) * 8;
-        const int n = n0 + r;
-        rb[i] = make_uint4(0u, 0u, 0u, 0u);
-        if (n < N) rb[i] = *reinterpret_cast<const uint4*>(B + (long)n * g.ldb + k0 + kc);
+        const int n = n0 + (idx >> 3);
+        rb[i] = *reinterpret_cast<const u32x4_t*>(B + (long)(n < N ? n : N - 1) * g.ldb + k0 + (idx & 7) * 8);
       } else {
         // BT: thread t loads k rows 4 (t / (BN/8)) + i of its 8-column chunk (t % (BN/8)): a 4x8 (k, n) block that
         // store_tiles writes as 8 [n][k] rows of 4 k (8-byte LDS stores instead of 32 2-byte ones)
         const int kl = BT ? 4 * (tid / (BN / 8)) + i : idx / (BN / 8);
-        const int nc = ((BT ? tid : idx) % (BN / 8)) * 8;
-        const int n = n0 + nc;
-        const bf16_t* src = B + (long)(k0 + kl) * g.ldb + n;
-        if (n + 7 < N) {
-          rb[i] = *reinterpret_cast<const uint4*>(src);
-        } else {
-          uint16_t e[8];
-#pragma unroll
-          for (int q = 0; q < 8; ++q) e[q] = (n + q < N) ? src[q] : (uint16_t)0;
-          rb[i] = make_uint4(e[0] | ((uint32_t)e[1] << 16), e[2] | ((uint32_t)e[3] << 16), e[4] | ((uint32_t)e[5] << 16),
-                             e[6] | ((uint32_t)e[7] << 16));
-        }
+        const int n = n0 + ((BT ? tid : idx) % (BN / 8)) * 8;
+        rb[i] = *reinterpret_cast<const u32x4_t*>(B + (long)(k0 + kl) * g.ldb + (n < N ? n : 0));
       }
     }
   };
@@ -283,7 +277,7 @@ __global__ __launch_bounds__(256, A_LN ? 2 : 3) void gemm_bf16_kernel(GemmB g) {
       const int idx = tid + 256 * i;
       if (B_KC) {
         const int r = idx >> 3, kc = (idx & 7) * 8;
-        *reinterpret_cast<uint4*>(&Bb[r * SK + kc]) = rb[i];
+        *reinterpret_cast<u32x4_t*>(&Bb[r * SK + kc]) = rb[i];
       } else if (BT) {  // the thread's 4x8 block: n = nc + j gets k = kq .. kq + 3 as one 8-byte store
         if (i == 0) {
           const int kq = 4 * (tid / (BN / 8)), nc = (tid % (BN / 8)) * 8;
@@ -324,7 +318,9 @@ __global__ __launch_bounds__(256, A_LN ? 2 : 3) void gemm_bf16_kernel(GemmB g) {
   store_tiles();
   __syncthreads();
   for (int kb = 0; kb < nk; ++kb) {
-    if (kb + 1 < nk) load_tiles((kb + 1) * BK);
+    load_tiles((kb + 1 < nk ? kb + 1 : kb) * BK);  // unconditional (the last trip reloads its own tile)
+    // keep the next tile's loads ahead of this tile's MFMAs (the scheduler otherwise sinks them to the barrier)
+    __builtin_amdgcn_sched_barrier(0);
     const bf16_t* Ab = As + (wm * MI * 32 + lr) * SK + lh * 8;
     const bf16_t* Bb = Bs + (wn * NI * 32 + lr) * SK + lh * 8;
 #pragma unroll
@@ -393,8 +389,8 @@ __global__ __launch_bounds__(256, A_LN ? 2 : 3) void gemm_bf16_kernel(GemmB g) {
       for (int it = 0; it < VIT; ++it) {
         const int idx = tid + 256 * it;
         const int m = mh + idx / NQ, n = n0 + 4 * (idx % NQ);
-        rv[it] = make_uint2(0u, 0u);
-        if (m < M && n < N) rv[it] = *reinterpret_cast<const uint2*>(resb + (long)m * e.ldr + n);
+        // unconditional, clamped (a predicated load's phi copy waited for the loads before it)
+        rv[it] = *reinterpret_cast<const uint2*>(resb + (long)(m < M ? m : M - 1) * e.ldr + (n < N ? n : N - 4));
       }
     }
     if (hf) __syncthreads();  // the first half's epilogue has read Cs
@@ -449,7 +445,7 @@ __global__ __launch_bounds__(256, A_LN ? 2 : 3) void gemm_bf16_kernel(GemmB g) {
 #pragma unroll
         for (int it = 0; it < PIT; ++it) {
           const int m = mh + rsub + 4 * it;
-          rp[it] = (e.res && m < M) ? *reinterpret_cast<const uint32_t*>(e.res + o0p + (long)m * HWo) : 0u;
+          rp[it] = e.res ? *reinterpret_cast<const uint32_t*>(e.res + o0p + (long)(m < M ? m : M - 1) * HWo) : 0u;
         }
 #pragma unroll
         for (int it = 0; it < PIT; ++it) {
@@ -478,7 +474,7 @@ __global__ __launch_bounds__(256, A_LN ? 2 : 3) void gemm_bf16_kernel(GemmB g) {
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           const int m = mh + tid / BN + (it0 + u) * (256 / BN);
-          r8[u] = (e.res && m < M) ? e.res[r0_ + (long)m * r_str] : (bf16_t)0;
+          r8[u] = e.res ? e.res[r0_ + (long)(m < M ? m : M - 1) * r_str] : (bf16_t)0;
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {

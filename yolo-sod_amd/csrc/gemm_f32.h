@@ -239,10 +239,12 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
   // folded batch: column n -> image n / nimg, column n % nimg (a float4 never straddles images: nimg % 4 == 0);
   // this thread's B columns are the same in every k block, so their offsets are computed once
   long bcol[B_KC ? 1 : NB];
+  int bn_[B_KC ? 1 : NB];  // unclamped first column of the thread's B quad (X2: columns past N are zeroed at the split)
   if (!B_KC) {
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
-      const int n = n0 + ((BT ? tid : tid + 256 * i) % (BN / 4)) * 4;
+      bn_[i] = n0 + ((BT ? tid : tid + 256 * i) % (BN / 4)) * 4;
+      const int n = bn_[i] < N ? bn_[i] : 0;  // a quad past N reads column 0 (in bounds; its outputs are dropped)
       if (g.nimg > 0) {
         const int img = n / g.nimg;
         bcol[i] = (long)img * g.b_bs + (n - img * g.nimg);
@@ -261,11 +263,11 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
     }
   }
 
-  float4 ra[NA], rb[NB], lw, lb;
+  // native vectors: a float4 (struct) copied global -> array -> LDS stays a memcpy through a stack array
+  f32x4 ra[NA], rb[NB], lw, lb;
   float rng = 0.f;  // X2: largest magnitude split (scaled operands), split-range guard
   const float sa = (X2 && g.x2_sa != 0.f) ? g.x2_sa : 1.f, sb = (X2 && g.x2_sb != 0.f) ? g.x2_sb : 1.f;
-  // per-thread operand pointers at k = 0 (a k block adds k0 or k0 * ldb), and whether the whole tile is in range
-  // (block-uniform: the loads then need no per-lane predicates)
+  // per-thread operand pointers at k = 0 (a k block adds k0 or k0 * ldb); rows past M / N clamped
   const float* pa[NA];
 #pragma unroll
   for (int i = 0; i < NA; ++i) {
@@ -285,48 +287,33 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
       pb[i] = B + (long)kl * g.ldb + bcol[i];
     }
   }
-  const bool full_a = m0 + BM <= M;
-  const bool full_b = n0 + BN <= N && (B_KC || vec_b);
+  // Tile loads without per-lane predicates: rows past M / N read the clamped row (pa / pb), an N-contiguous quad
+  // past N reads column 0 and a partial quad reads on to ldb (ldb % 4 == 0: in bounds); those products only reach
+  // outputs the epilogue never stores. A predicated load merges into a phi whose copy waited for every load in
+  // flight (vmcnt(0) after each load of a ragged tile).
   auto load_tiles = [&](int k0) {
-    if (full_a) {  // scalar branch: the tile's rows are all in range
 #pragma unroll
-      for (int i = 0; i < NA; ++i) ra[i] = *reinterpret_cast<const float4*>(pa[i] + k0);
-    } else {
-#pragma unroll
-      for (int i = 0; i < NA; ++i) {
-        const int m = m0 + ((tid + 256 * i) >> 3);
-        ra[i] = (m < M) ? *reinterpret_cast<const float4*>(pa[i] + k0) : make_float4(0, 0, 0, 0);
-      }
-    }
+    for (int i = 0; i < NA; ++i) ra[i] = *reinterpret_cast<const f32x4*>(pa[i] + k0);
     if (A_LN) {  // every A float4 of this thread sits at the same k offset (256 % 8 == 0)
-      lw = *reinterpret_cast<const float4*>(g.ln_w + k0 + (tid & 7) * 4);
-      lb = *reinterpret_cast<const float4*>(g.ln_b + k0 + (tid & 7) * 4);
+      lw = *reinterpret_cast<const f32x4*>(g.ln_w + k0 + (tid & 7) * 4);
+      lb = *reinterpret_cast<const f32x4*>(g.ln_b + k0 + (tid & 7) * 4);
     }
-    if (full_b) {
+    if (B_KC || vec_b) {
 #pragma unroll
       for (int i = 0; i < NB; ++i)
-        rb[i] = *reinterpret_cast<const float4*>(pb[i] + (B_KC ? (long)k0 : (long)k0 * g.ldb));
+        rb[i] = *reinterpret_cast<const f32x4*>(pb[i] + (B_KC ? (long)k0 : (long)k0 * g.ldb));
       return;
     }
+    // an N-contiguous B whose rows are not 16-byte aligned (odd H*W; off the hot path): predicated element loads
+    // (BT: thread t loads rows 4 (t / (BN/4)) + i of its column quad 4 (t % (BN/4)))
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
-      const int idx = tid + 256 * i;
-      if (B_KC) {
-        const int n = n0 + (idx >> 3);
-        rb[i] = (n < N) ? *reinterpret_cast<const float4*>(pb[i] + k0) : make_float4(0, 0, 0, 0);
-      } else {
-        // BT: thread t loads rows 4 (t / (BN/4)) + i of its column quad 4 (t % (BN/4))
-        const int n = n0 + (BT ? tid : idx) % (BN / 4) * 4;
-        const float* src = pb[i] + (long)k0 * g.ldb;
-        if (n + 3 < N && vec_b) {
-          rb[i] = *reinterpret_cast<const float4*>(src);
-        } else {
-          rb[i].x = (n < N) ? src[0] : 0.f;
-          rb[i].y = (n + 1 < N) ? src[1] : 0.f;
-          rb[i].z = (n + 2 < N) ? src[2] : 0.f;
-          rb[i].w = (n + 3 < N) ? src[3] : 0.f;
-        }
-      }
+      const int n = bn_[i];
+      const float* src = pb[i] + (long)k0 * g.ldb;
+      rb[i].x = (n < N) ? src[0] : 0.f;
+      rb[i].y = (n + 1 < N) ? src[1] : 0.f;
+      rb[i].z = (n + 2 < N) ? src[2] : 0.f;
+      rb[i].w = (n + 3 < N) ? src[3] : 0.f;
     }
   };
   auto store_tiles = [&](int buf) {
@@ -336,7 +323,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
     for (int i = 0; i < NA; ++i) {
       const int idx = tid + 256 * i;
       const int r = idx >> 3, kq = (idx & 7) * 4;
-      float4 v = ra[i];
+      f32x4 v = ra[i];
       if (A_LN) {
         const float mu = s_mean[r], rs = s_rstd[r];
         v.x = (v.x - mu) * rs * lw.x + lb.x;
@@ -352,7 +339,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
         *reinterpret_cast<uint2*>(d) = h;
         *reinterpret_cast<uint2*>(d + 8) = l;
       } else {
-        *reinterpret_cast<float4*>(&Ab[r * SK + kq]) = v;
+        *reinterpret_cast<f32x4*>(&Ab[r * SK + kq]) = v;
       }
     }
 #pragma unroll
@@ -365,7 +352,10 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
                                f32x4{rb[2].x, rb[2].y, rb[2].z, rb[2].w}, f32x4{rb[3].x, rb[3].y, rb[3].z, rb[3].w}};
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const f32x4 col = f32x4{r4[0][j], r4[1][j], r4[2][j], r4[3][j]} * sb;
+            // columns past N (read from column 0 or past the row end) are zeroed here, after the wait the split
+            // needs anyway, so the range guard sees operand values only
+            const f32x4 col = bn_[0] + j < N ? f32x4{r4[0][j], r4[1][j], r4[2][j], r4[3][j]} * sb
+                                              : f32x4{0.f, 0.f, 0.f, 0.f};
             uint2 h, l;
             split4(col, h, l);
             rng = range_acc(rng, col);
@@ -384,10 +374,15 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
         *reinterpret_cast<uint2*>(d + 8) = l;
       } else if (B_KC) {
         const int r = idx >> 3, kq = (idx & 7) * 4;
-        *reinterpret_cast<float4*>(&Bb[r * SK + kq]) = rb[i];
+        *reinterpret_cast<f32x4*>(&Bb[r * SK + kq]) = rb[i];
       } else {
         const int kl = idx / (BN / 4), nq = (idx % (BN / 4)) * 4;
-        *reinterpret_cast<float4*>(&Bb[kl * SBN + nq]) = rb[i];
+        f32x4 v = rb[i];
+        if (X2) {  // the split reads these columns from LDS: columns past N zeroed for the range guard
+          const int n = bn_[i];
+          v = f32x4{n < N ? v.x : 0.f, n + 1 < N ? v.y : 0.f, n + 2 < N ? v.z : 0.f, n + 3 < N ? v.w : 0.f};
+        }
+        *reinterpret_cast<f32x4*>(&Bb[kl * SBN + nq]) = v;
       }
     }
   };
@@ -412,7 +407,8 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
   __syncthreads();
   for (int kb = 0; kb < nk; ++kb) {
     const int buf = kb & 1;
-    if (kb + 1 < nk) load_tiles((kb + 1) * BK);
+    load_tiles((kb + 1 < nk ? kb + 1 : kb) * BK);  // unconditional (the last trip reloads its own tile)
+    __builtin_amdgcn_sched_barrier(0);  // the next tile's loads stay ahead of this tile's MFMAs
     const float* Ab = As + buf * A_ELEMS + (wm * MI * 32 + lr) * SK + lh * 16;
     const float* Bb = Bs + buf * B_ELEMS;
     if constexpr (X2) {

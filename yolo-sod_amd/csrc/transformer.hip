@@ -828,7 +828,7 @@ int yolosod_a2_fused_prepare(int C, const float* proj_w, const float* ln_w, cons
                              const float* in_b, void* prep, size_t prep_bytes, hipStream_t st);
 int yolosod_a2_fused_run(const float* S, const float* stats, float* O, int B, int L, int C, int num_heads,
                          const void* prep, size_t prep_bytes, hipStream_t st);
-bool yolosod_a2_proj_pool_ok(int C, int H, int W);
+bool yolosod_a2_proj_pool_ok(int C, int H, int W, int A);
 int yolosod_a2_proj_pool_run(const float* x, const float* proj_b, float* S, int B, int C, int H, int W, int A,
                              const void* prep, size_t prep_bytes, hipStream_t st);
 
@@ -924,7 +924,7 @@ static int a2_forward_impl(const float* x, float* y, int B, int C, int H, int W,
     prep_bytes = fpb;
   }
   GemmArgs ga{};
-  if (fused && yolosod_a2_proj_pool_ok(C, H, W) && ((uintptr_t)x & 15) == 0) {
+  if (fused && yolosod_a2_proj_pool_ok(C, H, W, A) && ((uintptr_t)x & 15) == 0) {
     // proj + SiLU + row pooling in one kernel (a2_fused.hip): x -> S; the projected map never reaches HBM
     if ((rc = yolosod_a2_proj_pool_run(x, proj_b, S, B, C, H, W, A, prep, prep_bytes, st))) return rc;
   } else {
