@@ -845,7 +845,11 @@ static int se_forward_impl(const T* x, T* y, int B, int C, int H, int W, const f
   const long xchunks = (HW % 4 == 0) ? (HW + 1023) / 1024 : (HW + 255) / 256;
   const size_t lds = sizeof(float) * (3 * (size_t)C + 128);
   const size_t lds_fused = sizeof(float) * (2 * (size_t)C + 136);
-  const bool fused = fused_gates() && lds_fused <= 64 * 1024;
+  // gate MLP fused into the apply pass for small planes; a separate gate launch for large ones, where the fused
+  // form's per-workgroup MLP (12800 workgroups at 32x32x320x320) cost more than the launch: SE L1 0.158 -> 0.150 ms,
+  // L23 0.038 fused vs 0.040 split (same box, profiles/r04_se/); YOLOSOD_SE_FUSED_MAXHW overrides the bound
+  static const long fused_max_hw = [] { const char* e = getenv("YOLOSOD_SE_FUSED_MAXHW"); return e ? atol(e) : 65536L; }();
+  const bool fused = fused_gates() && lds_fused <= 64 * 1024 && (HW < fused_max_hw || lds > 64 * 1024);
   YS_CHECK_ARG(lds <= 64 * 1024 || fused, "se: C=%d too large for the gate kernel", C);
   // the fused apply's 8 loads per lane issued before the gate MLP (YOLOSOD_SE_PRE=0: after it)
   static const int se_pre = [] { const char* e = getenv("YOLOSOD_SE_PRE"); return (!e || atoi(e) != 0) ? 1 : 0; }();
