@@ -1,0 +1,15 @@
+#!/bin/bash
+# round 4: Detect head / bf16 tokens+LN with unconditional loads: head / e2e tests, same-box A/B
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+O=gpurun_out/${TAG:-r04ah}; mkdir -p $O
+BASE=$GRAFT_REPO_ROOT/yolo-sod_amd/lib_ab/libyolosod_hip_base.so
+timeout -k 10 600 python -u -m pytest -v --timeout 300 --timeout-method thread -m gpu tests/test_gpu_ops.py tests/test_gpu_model.py tests/test_gpu_e2e.py tests/test_gpu_bf16.py -k "head or decode or e2e or tokens or swin" > $O/pytest.log 2>&1 \
+  || { grep -E "FAILED|Error" $O/pytest.log | head -20; exit 1; }
+tail -1 $O/pytest.log
+for rep in 1 2; do
+  echo "base rep $rep"; YOLOSOD_LIB_AB=$BASE timeout -k 10 120 python3 scripts/bench_ops.py head 2>&1 | grep " ms "
+  YOLOSOD_LIB_AB=$BASE timeout -k 10 120 python3 scripts/bench_ops.py --bf16 swin_L9_m swin_L28_m 2>&1 | grep " ms "
+  echo "new rep $rep"; timeout -k 10 120 python3 scripts/bench_ops.py head 2>&1 | grep " ms "
+  timeout -k 10 120 python3 scripts/bench_ops.py --bf16 swin_L9_m swin_L28_m 2>&1 | grep " ms "
+done
