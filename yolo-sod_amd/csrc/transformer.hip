@@ -484,17 +484,21 @@ __global__ __launch_bounds__(256) void a2_upsample_out4_kernel(const float* __re
   const float b = bias[c];
   const f32x4 xv = *reinterpret_cast<const f32x4*>(x + o);
   f32x4 r;
+  // one division for the quad: its pixels are consecutive (a row change is a step of h)
+  int h = e0 / W, w = e0 - h * W;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    const int e = e0 + k;
-    const int h = e / W, w = e - h * W;
+    if (k > 0 && ++w == W) {
+      w = 0;
+      ++h;
+    }
     float src = sc * ((float)h + 0.5f) - 0.5f;
     if (src < 0.f) src = 0.f;
     const int y0 = (int)src;
     const int y1 = y0 + ((y0 < A - 1) ? 1 : 0);
     const float l1 = src - (float)y0, l0 = 1.0f - l1;
     const float u = l0 * Tp[y0 * W + w] + l1 * Tp[y1 * W + w];
-    r[k] = xv[k] + siluf_(u + b);
+    r[k] = xv[k] + silu_fast_(u + b);  // hardware exp2 / rcp, as the conv epilogues (~2^-22 relative)
   }
   *reinterpret_cast<f32x4*>(y + o) = r;
 }

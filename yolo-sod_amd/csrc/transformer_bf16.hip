@@ -465,17 +465,21 @@ __global__ __launch_bounds__(256) void a2_upsample_out4_bf16_kernel(const bf16_t
   const float b = bias[c];
   const f32x4 xv = ld4(x + o);
   f32x4 r;
+  // one division for the quad: its pixels are consecutive (a row change is a step of h)
+  int h = e0 / W, w = e0 - h * W;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    const int e = e0 + k;
-    const int h = e / W, w = e - h * W;
+    if (k > 0 && ++w == W) {
+      w = 0;
+      ++h;
+    }
     float src = sc * ((float)h + 0.5f) - 0.5f;
     if (src < 0.f) src = 0.f;
     const int y0 = (int)src;
     const int y1 = y0 + ((y0 < A - 1) ? 1 : 0);
     const float l1 = src - (float)y0, l0 = 1.0f - l1;
     const float u = l0 * bf2f(Tp[y0 * W + w]) + l1 * bf2f(Tp[y1 * W + w]);
-    r[k] = xv[k] + siluf_(u + b);
+    r[k] = xv[k] + silu_fast_(u + b);  // hardware exp2 / rcp (~2^-22 relative)
   }
   st4(y + o, r);
 }
