@@ -61,8 +61,8 @@ int yolosod_a2_forward(const float* x, float* y, int B, int C, int H, int W, int
                        const float* mha_out_b, const float* oproj_w, const float* oproj_b, void* workspace,
                        size_t workspace_bytes, void* stream);
 /* The fused LN -> QKV -> attention kernel of the fp16-split path (csrc/a2_fused.hip; head dim 64, areas * W <= 160)
- * and the proj + SiLU + pooling kernel (H*W <= 400) take the weights prepared once: yolosod_a2_prep_bytes (0 = the
- * shape does not take the fused kernels), yolosod_a2_prepare (in_proj with the LayerNorm affine folded and the
+ * and the proj + SiLU + pooling kernel (area groups whose rows fit 400 pixels; any sequence length) take the weights
+ * prepared once: yolosod_a2_prep_bytes (0 = the shape takes neither fused kernel), yolosod_a2_prepare (in_proj with the LayerNorm affine folded and the
  * BN-folded proj conv, split into fp16 planes; re-run when one of them changes), yolosod_a2_forward_prepared (the forward of yolosod_a2_forward with the pre-multiplied output
  * weights, on that block; the workspace is yolosod_a2_workspace). yolosod_a2_forward prepares per call instead. */
 size_t yolosod_a2_prep_bytes(int C, int num_heads, int num_areas, int W);

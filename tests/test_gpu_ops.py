@@ -198,11 +198,12 @@ def test_a2_fused_and_decomposed_forms(name, fused, cuda, monkeypatch):
     assert ok, f"{name} fused={fused}: vs fp64 oracle max abs err {err:.3g} (ratio {ratio:.2f})"
 
 
-@pytest.mark.parametrize("name", ["a2_c512_h20", "a2_L12", "a2_b3_c256_12x8", "a2_b2_c192_10x20"])
+@pytest.mark.parametrize("name", ["a2_c512_h20", "a2_L12", "a2_b3_c256_12x8", "a2_b2_c192_10x20", "a2_L12_1280"])
 def test_a2_proj_pool_area_groups_bit_identical(name, cuda, monkeypatch):
     """The proj + SiLU + pooling kernel over one tile per image (cap 400 pixels) and split into area groups (cap 208,
     the default: two groups of 10 rows at 20x20; cap 100: four groups) computes every pixel with the same k order, so
-    the outputs are bit-identical."""
+    the outputs are bit-identical. At 40x40 (n1280, L = 320: the decomposed attention after the fused proj / pool)
+    the caps give 4 / 8 / 4 groups."""
     lib = _hip.load_library()
     if A2_FUSED_SHAPES[name] is not None:
         monkeypatch.setitem(recipes.OPS, name, A2_FUSED_SHAPES[name])

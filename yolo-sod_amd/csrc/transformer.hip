@@ -849,9 +849,13 @@ YS_EXPORT size_t yolosod_a2_workspace(int B, int C, int H, int W, int num_areas)
   return s.off;
 }
 
-// Size of the prepared-parameter block of the fused LN / QKV / attention kernel (0: the shape does not take it).
+// Size of the prepared-parameter block of the fused kernels (0: the shape takes neither). The proj + SiLU + pooling
+// kernel takes it for any sequence length (its area groups bound the tile, checked per call with H), the LN / QKV /
+// attention kernel for L = num_areas * W <= 160.
 YS_EXPORT size_t yolosod_a2_prep_bytes(int C, int num_heads, int num_areas, int W) {
-  return yolosod_a2_fused_ok(C, num_heads, num_areas * W) ? yolosod_a2_fused_prep_bytes(C) : 0;
+  const bool attn = yolosod_a2_fused_ok(C, num_heads, num_areas * W);
+  const bool pool = yolosod_a2_fused_ok(C, num_heads, 1) && num_areas > 0 && W > 0;
+  return (attn || pool) ? yolosod_a2_fused_prep_bytes(C) : 0;
 }
 
 // Weight preparation for yolosod_a2_forward_prepared: in_proj with the LayerNorm affine folded and the proj 1x1 conv
@@ -928,7 +932,8 @@ static int a2_forward_impl(const float* x, float* y, int B, int C, int H, int W,
     prep_bytes = fpb;
   }
   GemmArgs ga{};
-  if (fused && yolosod_a2_proj_pool_ok(C, H, W, A) && ((uintptr_t)x & 15) == 0) {
+  // the proj / pool kernel needs the prepared proj planes: a caller's block, or the per-call one of the fused path
+  if (x2 && prep && yolosod_a2_proj_pool_ok(C, H, W, A) && ((uintptr_t)x & 15) == 0) {
     // proj + SiLU + row pooling in one kernel (a2_fused.hip): x -> S; the projected map never reaches HBM
     if ((rc = yolosod_a2_proj_pool_run(x, proj_b, S, B, C, H, W, A, prep, prep_bytes, st))) return rc;
   } else {
