@@ -93,15 +93,46 @@ __global__ __launch_bounds__(256) void attn_f32_kernel(const float* __restrict__
   const int l15 = lane & 15, l4 = lane >> 4;
 
   // Q fragment: A[i = l&15][k = l>>4] over k-steps of 4 (scaled once, as q*scale in the MHA math path)
+  // Loads without per-lane predicates where the shape allows (HD % 4 == 0): rows past L read row L - 1 (queries past
+  // L are not stored; keys past L are masked before the softmax and meet P = 0 in P.V). A predicated load merged into
+  // a phi whose copy waited for it: every Q / K / V load of the kernel was its own round trip.
+  constexpr bool VEC = HD % 4 == 0 && HDP == HD;
   float qf[(HD + 3) / 4];
   {
     const int qrow = q0 + l15;
 #pragma unroll
     for (int s = 0; s < (HD + 3) / 4; ++s) {
       const int d = 4 * s + l4;
-      qf[s] = (qrow < L && d < HD) ? qkv[(seq_row0 + qrow) * ld + h * HD + d] * scale : 0.f;
+      if (VEC)
+        qf[s] = qkv[(seq_row0 + (qrow < L ? qrow : L - 1)) * ld + h * HD + d] * scale;
+      else
+        qf[s] = (qrow < L && d < HD) ? qkv[(seq_row0 + qrow) * ld + h * HD + d] * scale : 0.f;
     }
   }
+  // a 64-key chunk of K (off = C) or V (off = 2C) into KV, all of a thread's loads issued before its LDS stores
+  auto stage = [&](int ch, int off) {
+    if constexpr (VEC) {
+      constexpr int NE = 64 * HD / 256;
+      float v[NE];
+#pragma unroll
+      for (int i = 0; i < NE; ++i) {
+        const int e = tid + 256 * i, kr = e / HD, d = e % HD;
+        const int key = ch * 64 + kr;
+        v[i] = qkv[(seq_row0 + (key < L ? key : L - 1)) * ld + off + h * HD + d];
+      }
+#pragma unroll
+      for (int i = 0; i < NE; ++i) {
+        const int e = tid + 256 * i;
+        KV[(e / HD) * KS + e % HD] = v[i];
+      }
+    } else {
+      for (int e = tid; e < 64 * HDP; e += 256) {
+        const int kr = e / HDP, d = e % HDP;
+        const int key = ch * 64 + kr;
+        KV[kr * KS + d] = (key < L && d < HD) ? qkv[(seq_row0 + key) * ld + off + h * HD + d] : 0.f;
+      }
+    }
+  };
 
   f32x4 sacc[NKB];
 #pragma unroll
@@ -111,11 +142,7 @@ __global__ __launch_bounds__(256) void attn_f32_kernel(const float* __restrict__
 #pragma unroll
   for (int ch = 0; ch < (NKB + 3) / 4; ++ch) {
     __syncthreads();
-    for (int e = tid; e < 64 * HD; e += 256) {
-      const int kr = e / HD, d = e % HD;
-      const int key = ch * 64 + kr;
-      KV[kr * KS + d] = (key < L) ? qkv[(seq_row0 + key) * ld + C + h * HD + d] : 0.f;
-    }
+    stage(ch, C);
     __syncthreads();
 #pragma unroll
     for (int kb4 = 0; kb4 < 4; ++kb4) {
@@ -177,11 +204,7 @@ __global__ __launch_bounds__(256) void attn_f32_kernel(const float* __restrict__
 #pragma unroll
   for (int ch = 0; ch < (NKB + 3) / 4; ++ch) {
     __syncthreads();
-    for (int e = tid; e < 64 * HDP; e += 256) {
-      const int kr = e / HDP, d = e % HDP;
-      const int key = ch * 64 + kr;
-      KV[kr * KS + d] = (key < L && d < HD) ? qkv[(seq_row0 + key) * ld + 2 * C + h * HD + d] : 0.f;
-    }
+    stage(ch, 2 * C);
     __syncthreads();
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
