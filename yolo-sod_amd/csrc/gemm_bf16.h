@@ -71,7 +71,8 @@ __global__ __launch_bounds__(256) void row_stats_bf16_kernel(const bf16_t* __res
 #pragma unroll
   for (int u = 0; u < VPL; ++u) {
     const int c = lane + 64 * u;
-    v[u] = (c < K4) ? ld4(xr + 4 * c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    v[u] = ld4(xr + 4 * (c < K4 ? c : K4 - 1));  // unconditional: a predicated load waited in turn
+    if (c >= K4) v[u] = f32x4{0.f, 0.f, 0.f, 0.f};
     s += (v[u].x + v[u].y) + (v[u].z + v[u].w);
   }
   const float mean = wave_sum(s) / (float)K;
@@ -121,7 +122,8 @@ __global__ __launch_bounds__(256) void ln_rows_bf16_kernel(const bf16_t* __restr
 #pragma unroll
   for (int u = 0; u < VPL; ++u) {
     const int c = lane + 64 * u;
-    v[u] = (c < K4) ? ld4(xr + 4 * c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    v[u] = ld4(xr + 4 * (c < K4 ? c : K4 - 1));  // unconditional: a predicated load waited in turn
+    if (c >= K4) v[u] = f32x4{0.f, 0.f, 0.f, 0.f};
     s += (v[u].x + v[u].y) + (v[u].z + v[u].w);
   }
   const float mean = wave_sum(s) / (float)K;

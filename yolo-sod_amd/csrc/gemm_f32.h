@@ -79,7 +79,8 @@ __global__ __launch_bounds__(256) void row_stats_kernel(const float* __restrict_
 #pragma unroll
   for (int u = 0; u < VPL; ++u) {
     const int c = lane + 64 * u;
-    v[u] = (c < K4) ? xr[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+    v[u] = xr[c < K4 ? c : K4 - 1];  // unconditional: a predicated load waited in turn
+    if (c >= K4) v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
     s += (v[u].x + v[u].y) + (v[u].z + v[u].w);
   }
   const float mean = wave_sum(s) / (float)K;
@@ -126,7 +127,8 @@ __global__ __launch_bounds__(256) void ln_rows_kernel(const float* __restrict__ 
 #pragma unroll
   for (int u = 0; u < VPL; ++u) {
     const int c = lane + 64 * u;
-    v[u] = (c < K4) ? xr[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+    v[u] = xr[c < K4 ? c : K4 - 1];  // unconditional: a predicated load waited in turn
+    if (c >= K4) v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
     s += (v[u].x + v[u].y) + (v[u].z + v[u].w);
   }
   const float mean = wave_sum(s) / (float)K;

@@ -69,17 +69,26 @@ __global__ __launch_bounds__(256) void window_attn_bf16_kernel(const bf16_t* __r
   const int ld = 3 * C;
   const int l15 = lane & 15, g = lane >> 4;
 
-  // stage K (row-major) and V (transposed) of the sequence; keys >= L are zero
-  for (int e = tid; e < NK * (HD / 8); e += 256) {
+  // stage K and V (both row-major) of the sequence: every load of the thread first, then the LDS stores, with keys
+  // >= L reading key L - 1 (finite; their scores are masked before the softmax and meet P = 0 in P.V). A predicated
+  // load in the store loop waited for each load in turn.
+  constexpr int NE = NK * (HD / 8), NR = (NE + 255) / 256;  // 16-byte items, staging rounds
+  u32x4_t kv[NR], vv[NR];
+#pragma unroll
+  for (int i = 0; i < NR; ++i) {
+    const int e = (tid + 256 * i < NE) ? tid + 256 * i : NE - 1;  // a partial last round re-reads the last item
     const int key = e / (HD / 8), dc = (e - key * (HD / 8)) * 8;
-    uint4 kv = make_uint4(0u, 0u, 0u, 0u), vv = kv;
-    if (key < L) {
-      const bf16_t* src = qkv + tm.row(seq, key) * ld + h * HD + dc;
-      kv = *reinterpret_cast<const uint4*>(src + C);
-      vv = *reinterpret_cast<const uint4*>(src + 2 * C);
-    }
-    *reinterpret_cast<uint4*>(&Ks[key * KS + dc]) = kv;
-    *reinterpret_cast<uint4*>(&Vr[key * VS + vcol<HD>(key, dc)]) = vv;
+    const bf16_t* src = qkv + tm.row(seq, key < L ? key : L - 1) * ld + h * HD + dc;
+    kv[i] = *reinterpret_cast<const u32x4_t*>(src + C);
+    vv[i] = *reinterpret_cast<const u32x4_t*>(src + 2 * C);
+  }
+#pragma unroll
+  for (int i = 0; i < NR; ++i) {
+    const int e = tid + 256 * i;
+    if (NE % 256 != 0 && e >= NE) break;
+    const int key = e / (HD / 8), dc = (e - key * (HD / 8)) * 8;
+    *reinterpret_cast<u32x4_t*>(&Ks[key * KS + dc]) = kv[i];
+    *reinterpret_cast<u32x4_t*>(&Vr[key * VS + vcol<HD>(key, dc)]) = vv[i];
   }
   // this wave's Q fragments (rows >= L read row L-1: finite values, results dropped)
   const int q0 = blockIdx.x * 64 + wv * 16;
