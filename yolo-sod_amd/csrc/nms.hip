@@ -84,9 +84,31 @@ __global__ __launch_bounds__(256) void nms_prep_kernel(NmsArgs g) {
   if (a < g.A) {
     float* pb = g.pred + (long)b * (4 + g.nc) * g.A + a;
     const long As = g.A;
+    // up to 16 class scores loaded before the box (the in-place box stores below could alias later score loads, so
+    // the compiler kept every load behind them) and unconditionally (class index clamped; classes past nc skipped)
+    float s16[16];
+    if (g.nc <= 16) {
+#pragma unroll
+      for (int u = 0; u < 16; ++u) s16[u] = pb[(4 + (u < g.nc ? u : g.nc - 1)) * As];
+    }
     const float cx = pb[0], cy = pb[As], w = pb[2 * As], h = pb[3 * As];
     const float hw = w / 2.0f, hh = h / 2.0f;
     const float x1 = cx - hw, y1 = cy - hh, x2 = cx + hw, y2 = cy + hh;
+    float best = -INFINITY;
+    int bj = 0;
+    if (g.nc <= 16) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        if (j < g.nc) {
+          const float sc = s16[j];
+          if (sc > best) {  // strict: first maximal index wins (torch max(dim) / amax)
+            best = sc;
+            bj = j;
+          }
+          if (g.multi_label && sc > g.conf) mask |= 1ull << j;
+        }
+      }
+    }
     if (g.in_place) {
       pb[0] = x1;
       pb[As] = y1;
@@ -94,9 +116,7 @@ __global__ __launch_bounds__(256) void nms_prep_kernel(NmsArgs g) {
       pb[3 * As] = y2;
     }
     box = make_float4(x1, y1, x2, y2);
-    float best = -INFINITY;
-    int bj = 0;
-    for (int j0 = 0; j0 < g.nc; j0 += 8) {  // 8 score loads in flight, then scanned in class order
+    for (int j0 = 0; g.nc > 16 && j0 < g.nc; j0 += 8) {  // 8 score loads in flight, then scanned in class order
       float sv[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) sv[u] = (j0 + u < g.nc) ? pb[(4 + j0 + u) * As] : -INFINITY;
