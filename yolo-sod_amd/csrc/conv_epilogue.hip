@@ -215,24 +215,30 @@ __global__ __launch_bounds__(256) void bias_act_capool_kernel(const T* __restric
     const int rb = (H - h0 < RB) ? H - h0 : RB;
     const int n4 = rb * W4;  // <= 2048 = 8 per thread
     const long base = (long)h0 * W;
+    // loads unconditional (index clamped into the band), all values computed, then the predicated stores: loads
+    // under per-u predicates left the waitcnt pass exec-masked regions it merged conservatively, so each u's block
+    // began with vmcnt(0) - which on gfx950 also waits for the previous block's global store to complete
     f32x4 v[8], r[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      const int i = tid + 256 * u;
-      if (i < n4) {
-        v[u] = ld4(yp + base + 4 * i);
-        if (RES) r[u] = ld4(rp + base + 4 * i);
+      const int i = tid + 256 * u < n4 ? tid + 256 * u : n4 - 1;
+      v[u] = ld4(yp + base + 4 * i);
+      if (RES) r[u] = ld4(rp + base + 4 * i);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      f32x4 t = v[u] + bc;
+      if (ACT == 1) {
+        t.x = silu_st<T>(t.x); t.y = silu_st<T>(t.y); t.z = silu_st<T>(t.z); t.w = silu_st<T>(t.w);
       }
+      if (RES) t += r[u];
+      v[u] = t;
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int i = tid + 256 * u;
       if (i < n4) {
-        f32x4 t = v[u] + bc;
-        if (ACT == 1) {
-          t.x = silu_st<T>(t.x); t.y = silu_st<T>(t.y); t.z = silu_st<T>(t.z); t.w = silu_st<T>(t.w);
-        }
-        if (RES) t += r[u];
+        f32x4 t = v[u];
         st4(op + base + 4 * i, t);
         if (sizeof(T) == 2) t = round_bf16(t);  // pool the stored (rounded) values
         band4[i] = t;
