@@ -8,11 +8,16 @@ Weak scaling: every rank processes its own batch of 32 images; value = N * 32 * 
 Usage: python bench.py [--gpus N --steps K --warmup W]; for N > 1 launch with
        python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 --master-port P \
               bench.py --gpus N --steps K --warmup W
-Rank 0 prints ONE JSON line (plus `roofline` of the dominant HIP operator, measured live with HIP events inside
-the timed region, and `cpu_baseline` = the oracle CPU model timed on the host cores, rank 0 at N = 1 only). At N = 1
-the line also carries `configs`: BASELINE configs[3] (n1280, bs 8) and configs[4] (m640 bf16, bs 64), each timed in
-its own region of the same process with the same contract (its own ms_per_step, value, roofline, path_roofline,
-hip_ops). Roofline fractions are quoted against the ceiling of the arithmetic each kernel issues (perf.py).
+       `python bench.py --gpus N` with no WORLD_SIZE in the environment starts those N ranks itself: the parent
+       (which makes no GPU call) runs torch.distributed.run as a child process and exits with its code (the
+       reference's DDP entry does the same, ultralytics/engine/trainer.py:197-200, utils/dist.py:56-66).
+Rank 0 prints ONE compact JSON line (< 4 KB): the contract fields, `roofline` of the dominant HIP operator (measured
+live with HIP events inside the timed region), `path_roofline`, `cpu_baseline` (the oracle CPU model timed on the
+host cores, rank 0 at N = 1 only) and, at N = 1, `configs`: BASELINE configs[3] (n1280, bs 8) and configs[4] (m640
+bf16, bs 64), each timed in its own region of the same process (value, ms_per_step, roofline / path fractions).
+Every per-operator figure (hip_ops, backbone_hip_ops, the full cpu_baseline) goes to the --detail-json file, which
+scripts/roofline_from_csv.py checks against --ops-csv. Roofline fractions are quoted against the ceiling of the
+arithmetic each kernel issues (perf.py).
 """
 from __future__ import annotations
 
@@ -245,8 +250,10 @@ def measure(name, world, rank, dev, steps, warmup, conf, ops_csv=None):
     x = seeded_images(lo, hi, imgsz, device=dev).to(dtype)
 
     def step():
+        # the timed step is the same at every N: no host sync inside it. The split-range guard's flag word is read
+        # once after the timed region on every rank (split_range_flagged below), not per step
         if world > 1:  # shard -> rank-local predict -> all-gather of the padded detections + kept indices
-            return sharded_predict(predictor.predict_padded, n_global, lambda a, b: x)[1]
+            return sharded_predict(predictor.predict_padded, n_global, lambda a, b: x, split_guard=False)[1]
         return predictor.predict_padded(x)[1]
 
     t_w = time.perf_counter()
@@ -266,10 +273,12 @@ def measure(name, world, rank, dev, steps, warmup, conf, ops_csv=None):
         if world > 1:
             dist.barrier()
         t1 = time.perf_counter()
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    # one read of the split-range flag per rank after the region (fp32 configs; bf16 runs no split kernels)
+    flagged = float(dtype == torch.float32 and _hip.split_range_flag(reset=True, device=dev))
+    red = torch.tensor([t1 - t0, flagged], dtype=torch.float64, device=dev)
     if world > 1:
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-    elapsed = float(elapsed.item())
+        dist.all_reduce(red, op=dist.ReduceOp.MAX)
+    elapsed, flagged = float(red[0].item()), bool(red[1].item())
     durs = timer.durations_ms()
 
     # per-operator live timings (HIP events on the launch stream) -> roofline of the dominant operator; the
@@ -308,7 +317,7 @@ def measure(name, world, rank, dev, steps, warmup, conf, ops_csv=None):
            "config": {"name": name, "workload": f"{label} {imgsz}x{imgsz}, {bs} images per GPU, fused {dname} "
                                   f"forward + decode + NMS(conf={conf}, iou=0.7)",
                       "imgsz": imgsz, "batch_per_gpu": bs, "global_batch": bs * world, "parallelism": f"dp{world}"},
-           "roofline": roofline, "path_roofline": path_roofline,
+           "roofline": roofline, "path_roofline": path_roofline, "split_range_flagged": flagged,
            "hip_ops_ms_per_step": round(t_meas, 3),
            "hip_ops": [{k: v for k, v in o.items() if k not in ("bytes", "flops", "key")} for o in ops],
            "backbone_hip_ms_per_step": round(sum(o["total_ms_per_step"] for o in backbone), 3),
@@ -318,6 +327,74 @@ def measure(name, world, rank, dev, steps, warmup, conf, ops_csv=None):
 
 # BASELINE.json configs[3] / configs[4] on one GPU, timed in the same process after the headline (N = 1 only)
 EXTRA_CONFIGS = ("m640", "n1280")
+LINE_LIMIT = 4000  # bytes: the driver parses the last stdout line; round 4's 20 KB line did not parse
+
+
+def _op_name(o):
+    return f"{o['op']}:{'x'.join(map(str, o['shape']))}"
+
+
+def _compact_roofline(r):
+    keep = ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel", "algorithmic_per_launch",
+            "frac_vs_dtype_peak")
+    out = {k: r[k] for k in keep if k in r}
+    out["kernel"] = out.get("kernel", "").split(" (")[0]
+    return out
+
+
+def compact_line(result, detail_path=None):
+    """The one stdout JSON line from the full result: contract fields, roofline (+traffic), path_roofline, the
+    cpu_baseline summary, NMS-at-load per call, per-op ms of the headline and per extra config only value /
+    ms_per_step / roofline.frac / path_roofline.frac. Everything else stays in the detail file."""
+    head = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data", "config", "split_range_flagged", "hip_ops_ms_per_step",
+            "backbone_hip_ms_per_step")
+    line = {k: result[k] for k in head if k in result}
+    line["roofline"] = _compact_roofline(result["roofline"])
+    pr = result["path_roofline"]
+    line["path_roofline"] = {k: pr[k] for k in ("t_min_ms", "t_meas_ms", "frac", "frac_vs_dtype_peak")}
+    line["hip_ops_avg_ms"] = {_op_name(o): o["avg_ms"] for o in result.get("hip_ops", [])}
+    nl = result.get("nms_loaded")
+    line["nms_loaded_ms_per_call"] = None if nl is None else {k: v["ms_per_call"] for k, v in nl.items()}
+    cb = result.get("cpu_baseline")
+    if cb is not None and "error" not in cb:
+        one = cb.get("single_thread_configs0") or {}
+        cb = {"value": cb["value"], "unit": cb["unit"], "cores": cb["cores"], "kind": cb["kind"],
+              "sample": cb["sample"], "cpu_model": cb.get("cpu_model"),
+              "mafn_decode_nms_ms_per_image": (cb.get("all_cores") or {}).get("mafn_decode_nms_ms_per_image"),
+              "single_thread_configs0_value": one.get("value"),
+              "nms_loaded_ms_per_image": cb.get("nms_loaded_ms_per_image")}
+    line["cpu_baseline"] = cb
+    if "configs" in result:
+        line["configs"] = {n: {"value": c["value"], "ms_per_step": c["ms_per_step"], "dtype": c["dtype"],
+                               "batch_per_gpu": c["config"]["batch_per_gpu"], "imgsz": c["config"]["imgsz"],
+                               "roofline_frac": c["roofline"]["frac"], "roofline_kernel":
+                                   c["roofline"]["kernel"].split(" (")[0],
+                               "path_roofline_frac": c["path_roofline"]["frac"]}
+                           for n, c in result["configs"].items()}
+    if detail_path:
+        line["detail"] = str(detail_path)
+    txt = json.dumps(line)
+    if len(txt.encode()) > LINE_LIMIT:  # never exceed: drop the per-op map first, then the NMS / CPU extras
+        for k in ("hip_ops_avg_ms", "nms_loaded_ms_per_call"):
+            line.pop(k, None)
+            txt = json.dumps(line)
+            if len(txt.encode()) <= LINE_LIMIT:
+                break
+    return line
+
+
+def launcher_cmd(argv, gpus, port):
+    """Child command that starts ``gpus`` ranks of this script (one process per GPU, RCCL), as the driver does."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", str(Path(__file__).resolve()), *argv]
+
+
+def _free_port():
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
 
 
 def main():
@@ -334,10 +411,22 @@ def main():
     ap.add_argument("--ops-csv", default=None,
                     help="write every timed C-ABI launch (HIP event ms, rank 0) of every config to this CSV: "
                          "scripts/roofline_from_csv.py recomputes hip_ops / producer billing / path_roofline from it")
+    ap.add_argument("--detail-json", default=str(ROOT / "gpurun_out" / "bench_detail.json"),
+                    help="full result (every hip_ops / backbone_hip_ops entry, the full cpu_baseline) as one JSON "
+                         "file; '' to skip")
     args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no launcher around us: start the N ranks as a child process (this process has made no GPU call) and pass
+        # its exit code on; rank 0 of the child prints the line
+        import subprocess
+        cmd = launcher_cmd(sys.argv[1:], args.gpus, _free_port())
+        log("launching: " + " ".join(cmd))
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+        sys.exit(subprocess.run(cmd, env=env).returncode)
+
     if args.miopen_benchmark:
         torch.backends.cudnn.benchmark = True
-
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -387,7 +476,16 @@ def main():
             w.writeheader()
             w.writerows(rows)
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        detail = None
+        if args.detail_json:
+            try:
+                Path(args.detail_json).parent.mkdir(parents=True, exist_ok=True)
+                Path(args.detail_json).write_text(json.dumps(result) + "\n")
+                dp = Path(args.detail_json).resolve()
+                detail = str(dp.relative_to(ROOT)) if dp.is_relative_to(ROOT) else str(dp)
+            except OSError as e:
+                log(f"detail json not written: {e!r}")
+        print(json.dumps(compact_line(result, detail)), flush=True)
 
 
 if __name__ == "__main__":

@@ -94,9 +94,12 @@ def decode_maps(spec=DECODE):
 
 
 def synthetic_predictions(seed: int, B: int, A: int, nc: int, n_clusters: int = 40, img: float = 640.0,
-                          tie_scores: bool = False) -> np.ndarray:
+                          tie_scores: bool = False, degenerate: bool = False) -> np.ndarray:
     """(B, 4+nc, A) xywh + class scores: clustered, heavily overlapping boxes, a few classes per cluster, scores
-    spread over [0, 1) with no exact ties (unless tie_scores)."""
+    spread over [0, 1) with no exact ties (unless tie_scores). ``degenerate``: also zero-area boxes (w = 0 or h = 0:
+    two of them give IoU 0 / 0 = NaN, which torchvision's ``ovr > thr`` treats as no suppression) and exact duplicates
+    of other anchors' boxes and class scores with the main score lowered (identical boxes: IoU exactly 1; identical
+    zero-area boxes: NaN), the scores kept distinct so that every kept row names one anchor."""
     rng = np.random.default_rng(seed)
     out = np.zeros((B, 4 + nc, A), np.float32)
     for b in range(B):
@@ -116,7 +119,29 @@ def synthetic_predictions(seed: int, B: int, A: int, nc: int, n_clusters: int = 
         if tie_scores:
             s = np.round(s * 16) / 16
         out[b, 4:] = s
+        if degenerate:
+            n_dup = A // 10
+            src, dst = rng.choice(A, n_dup, replace=False), rng.choice(A, n_dup, replace=False)
+            ok = src != dst
+            src, dst = src[ok], dst[ok]
+            out[b, :, dst] = out[b, :, src]
+            out[b, 4:, dst] *= np.float32(0.97)  # same box and best class, lower (distinct) scores
+            zw = rng.choice(A, A // 7, replace=False)
+            out[b, 2, zw] = 0.0
+            zh = rng.choice(A, A // 10, replace=False)
+            out[b, 3, zh] = 0.0
+            both = dst[: len(dst) // 3]  # some duplicate pairs become identical zero-area boxes
+            out[b, 2, both] = 0.0
+            out[b, 2, src[: len(dst) // 3]] = 0.0
     return out
+
+
+def nms_case(name):
+    """(prediction, non_max_suppression kwargs) of NMS fixture ``name``."""
+    seed, B, A, nc, kw = NMS_CASES[name]
+    kw = dict(kw)
+    tie, deg = kw.pop("tie", False), kw.pop("degenerate", False)
+    return synthetic_predictions(seed, B, A, nc, tie_scores=tie, degenerate=deg), kw
 
 
 NMS_CASES = {
@@ -129,6 +154,7 @@ NMS_CASES = {
     "nms_empty": (15, 2, 500, 10, dict(conf_thres=0.999999, iou_thres=0.7)),
     "nms_ties": (16, 2, 1500, 10, dict(conf_thres=0.25, iou_thres=0.7, tie=True)),
     "nms_iou0": (17, 1, 800, 4, dict(conf_thres=0.3, iou_thres=0.0)),
+    "nms_degenerate": (18, 2, 2000, 10, dict(conf_thres=0.25, iou_thres=0.7, degenerate=True)),
 }
 
 

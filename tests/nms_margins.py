@@ -116,68 +116,132 @@ def nms_stability(y_ref: np.ndarray, y_oth: np.ndarray, conf=0.25, iou_thres=0.7
     return res
 
 
-def first_divergence(y_ref: np.ndarray, y_oth: np.ndarray, conf=0.25, iou_thres=0.7, max_nms=30000, max_wh=7680):
-    """The first decision at which predict-mode NMS on ``y_oth`` departs from NMS on ``y_ref`` (single label,
-    class-aware; ``ultralytics/utils/ops.py:274-297`` around torchvision's greedy NMS), or None when every decision
-    agrees - the kept anchor lists are then identical.
+# Bounds on the perturbation of the inputs of a decision that is allowed to flip (replay_divergences): a flip is only
+# a near-tie if the two runs' outputs for the anchors it involves agree to within the forward's own accuracy.
+SCORE_PERT_MAX = 1e-3  # north_star: outputs within 1e-3 abs of the CPU reference
+BOX_PERT_MAX = 0.25    # px: twice the reference fp32 CPU path's own worst box error vs fp64 on the trained-like model
+                       # (0.12 px, tests/test_gpu_e2e.py::test_e2e_forward_within_tolerance)
 
-    Both outputs are replayed side by side, stage by stage, in the order the reference takes its decisions: the
-    candidate filter (ops.py:234, 275), the best class (:274), the descending-score processing order and the
-    ``max_nms`` cut (:284-286), then the greedy IoU tests box by box (torchvision CPU nms). Everything before the
-    returned decision is identical in both runs, so it is the cause of the first difference in the kept lists. The
-    result holds the decision's margin measured on ``y_ref`` and the tolerance it is held to: twice the measured
-    perturbation of that decision's inputs (score decisions: 2 max|d score| over the image; IoU tests: 2 max|d IoU|
-    over the same-class candidate pairs + 1e-6)."""
+
+def _rank_before(key_a, idx_a, key_b, idx_b):
+    """True where a is processed before b in torchvision's order: descending score, stable (lower index first)."""
+    return (key_a > key_b) | ((key_a == key_b) & (idx_a < idx_b))
+
+
+def replay_divergences(y_ref: np.ndarray, y_oth: np.ndarray, conf=0.25, iou_thres=0.7, max_det=300, max_nms=30000,
+                       max_wh=7680):
+    """Replay predict-mode NMS (single label, class-aware: ``ultralytics/utils/ops.py:234-297`` around torchvision's
+    greedy CPU nms) on ``y_oth``, decision by decision, and at every decision evaluate what ``y_ref`` decides in the
+    SAME state. Where they differ the replay records the decision and adopts ``y_oth``'s choice, then keeps going, so
+    every divergent decision of the image is found (not only the first one) and the replay ends with NMS(y_oth)'s own
+    kept list (``keep``; the caller checks it against the real NMS of y_oth).
+
+    Decisions, each with its margin on y_ref and the perturbation ``pert`` of its own inputs between the two runs:
+      * conf    - candidate filter ``max_c score > conf`` (ops.py:234, 275) of one anchor;
+      * class   - best class ``argmax_c`` (ops.py:274) of one anchor: top score minus the adopted class's score;
+      * max_nms - an anchor crossing the ``max_nms`` cut (ops.py:284-286);
+      * order   - processing order of two SAME-class boxes that suppress one another in either run (different
+                  classes never interact: the max_wh class offset keeps their boxes apart, ops.py:289-295);
+      * iou     - the greedy test ``any IoU(kept, t) > thr`` of one box (torchvision: ``ovr > thr``, so an IoU of
+                  0 / 0 = NaN from two zero-area boxes never suppresses; a pair that is NaN in one run only and above
+                  the threshold in the other is recorded as kind ``nan``, never justified);
+      * out_order - output order / the ``[:max_det]`` cut (ops.py:297): a pair of kept boxes (any classes) in
+                  inverted order, the earlier one within max_det.
+    A decision is justified (``ok``) when its margin is within twice its own perturbation and the perturbation is
+    within the forward's accuracy: every score involved moved by <= SCORE_PERT_MAX, every box coordinate involved by
+    <= BOX_PERT_MAX."""
     s_r = np.ascontiguousarray(y_ref[4:].T)
     s_o = np.ascontiguousarray(y_oth[4:].T)
-    tol_s = 2 * float(np.abs(s_r.astype(np.float64) - s_o).max())
+    d_s = np.abs(s_r.astype(np.float64) - s_o)  # [A, nc]
+    d_box = np.abs(y_ref[:4].astype(np.float64) - y_oth[:4]).max(0)  # [A]
+    dec = []
+
+    def add(kind, anchors, margin, pert, score_anchors=(), box_anchors=(), **kw):
+        sp = float(d_s[list(score_anchors)].max()) if len(score_anchors) else 0.0
+        bp = float(d_box[list(box_anchors)].max()) if len(box_anchors) else 0.0
+        ok = bool(margin <= 2 * pert and sp <= SCORE_PERT_MAX and bp <= BOX_PERT_MAX and kind != "nan")
+        dec.append(dict(kind=kind, anchors=[int(a) for a in anchors], margin=float(margin), tol=float(2 * pert),
+                        score_pert=sp, box_pert=bp, ok=ok, **kw))
+
     best_r, best_o = s_r.max(1), s_o.max(1)
     c_r, c_o = best_r > np.float32(conf), best_o > np.float32(conf)
-    if (c_r != c_o).any():
-        x = np.nonzero(c_r != c_o)[0]
-        margin = float(np.abs(best_r[x].astype(np.float64) - np.float32(conf)).max())
-        return {"kind": "conf", "anchors": x.tolist(), "margin": margin, "tol": tol_s}
-    cand = np.nonzero(c_r)[0]
+    for a in np.nonzero(c_r != c_o)[0]:
+        add("conf", [a], abs(float(best_r[a]) - conf), abs(float(best_r[a]) - float(best_o[a])), score_anchors=[a])
+    cand = np.nonzero(c_o)[0]
+    res = {"decisions": dec, "keep": np.zeros(0, np.int64)}
     if cand.size == 0:
-        return None
-    cls_r, cls_o = s_r[cand].argmax(1), s_o[cand].argmax(1)
-    if (cls_r != cls_o).any():
-        x = np.nonzero(cls_r != cls_o)[0]
-        top2 = np.sort(s_r[cand[x]], 1)[:, -2:].astype(np.float64)
-        return {"kind": "class", "anchors": cand[x].tolist(), "margin": float((top2[:, 1] - top2[:, 0]).max()),
-                "tol": tol_s}
-    sc_r = s_r[cand, cls_r]
+        res["ok"] = all(d["ok"] for d in dec)
+        return res
+    cls_o = s_o[cand].argmax(1)
+    cls_r = s_r[cand].argmax(1)
+    for i in np.nonzero(cls_r != cls_o)[0]:
+        a, cr, co = cand[i], cls_r[i], cls_o[i]
+        add("class", [a], float(s_r[a, cr]) - float(s_r[a, co]), max(d_s[a, cr], d_s[a, co]), score_anchors=[a])
     sc_o = s_o[cand, cls_o]
-    ord_r = np.argsort(-sc_r, kind="stable")
-    ord_o = np.argsort(-sc_o, kind="stable")
-    n_proc = min(cand.size, max_nms)
-    if not np.array_equal(ord_r[:n_proc], ord_o[:n_proc]):
-        j = int(np.nonzero(ord_r[:n_proc] != ord_o[:n_proc])[0][0])
-        a, b = ord_r[j], ord_o[j]
-        return {"kind": "order", "position": j, "anchors": [int(cand[a]), int(cand[b])],
-                "margin": abs(float(sc_r[a]) - float(sc_r[b])), "tol": tol_s}
-    order = ord_r[:n_proc]
-    off = (cls_r.astype(np.float32) * np.float32(max_wh))[:, None]
+    sc_r = s_r[cand, cls_o]  # y_ref's score of the adopted class: the key of its processing order
+    order = np.argsort(-sc_o, kind="stable")
+    if cand.size > max_nms:
+        o_r = np.argsort(-sc_r, kind="stable")
+        top_o, top_r = set(order[:max_nms].tolist()), set(o_r[:max_nms].tolist())
+        edge = float(sc_r[o_r[max_nms - 1]])
+        for i in sorted(top_o ^ top_r):
+            add("max_nms", [cand[i]], abs(float(sc_r[i]) - edge), float(d_s[cand[i]].max()), score_anchors=[cand[i]])
+        order = order[:max_nms]
+    off = (cls_o.astype(np.float32) * np.float32(max_wh))[:, None]
     b_r = (_xyxy(y_ref[:4, cand].T) + off).astype(np.float32)
     b_o = (_xyxy(y_oth[:4, cand].T) + off).astype(np.float32)
-    # per class (the offsets keep classes apart): pairwise IoU of both runs and the IoU perturbation
-    ious, d_iou = {}, 0.0
-    for c in np.unique(cls_r[order]):
-        sel = order[cls_r[order] == c]
-        ir, io = _iou(b_r[sel]), _iou(b_o[sel])
-        if len(sel) > 1:
-            iu = np.triu_indices(len(sel), 1)
-            d_iou = max(d_iou, float(np.abs(ir[iu] - io[iu]).max()))
-        ious[int(c)] = (sel, ir, io, [])
-    tol_iou = 2 * d_iou + 1e-6
-    pos = {int(t): i for c in ious for i, t in enumerate(ious[c][0])}
-    for t in order:  # global processing order = per-class order interleaved by score
-        sel, ir, io, kept = ious[int(cls_r[t])]
-        i = pos[int(t)]
-        mx_r = float(ir[kept, i].max()) if kept else 0.0
-        mx_o = float(io[kept, i].max()) if kept else 0.0
-        if (mx_r > iou_thres) != (mx_o > iou_thres):
-            return {"kind": "iou", "anchors": [int(cand[t])], "margin": abs(mx_r - iou_thres), "tol": tol_iou}
-        if not (mx_r > iou_thres):
-            kept.append(i)
-    return None
+    keep_mask = np.zeros(len(cand), bool)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        for c in np.unique(cls_o[order]):
+            sel = order[cls_o[order] == c]  # this class, in y_oth's processing order
+            ir, io = _iou(b_r[sel]), _iou(b_o[sel])
+            kept = []
+            for t in range(len(sel)):
+                if kept:
+                    rr, ro = ir[kept, t], io[kept, t]
+                    nan_r, nan_o = np.isnan(rr), np.isnan(ro)
+                    for k in np.nonzero((nan_r != nan_o) & (np.where(nan_r, ro, rr) > iou_thres))[0]:
+                        ka, ta = cand[sel[kept[k]]], cand[sel[t]]
+                        add("nan", [ka, ta], np.inf, 0.0, box_anchors=[ka, ta])
+                    sup_r, sup_o = bool((rr > iou_thres).any()), bool((ro > iou_thres).any())
+                    # processing order of the boxes that suppress t in either run
+                    for k in np.nonzero((rr > iou_thres) | (ro > iou_thres))[0]:
+                        i, j = sel[kept[k]], sel[t]
+                        if not _rank_before(sc_r[i], cand[i], sc_r[j], cand[j]):
+                            add("order", [cand[i], cand[j]], abs(float(sc_r[i]) - float(sc_r[j])),
+                                max(abs(float(sc_r[i]) - float(sc_o[i])), abs(float(sc_r[j]) - float(sc_o[j]))),
+                                score_anchors=[cand[i], cand[j]])
+                    if sup_r != sup_o:  # (a NaN-only difference is already recorded above)
+                        flip = np.nonzero(~nan_r & ~nan_o & ((rr > iou_thres) != (ro > iou_thres)))[0]
+                        ks = [cand[sel[kept[k]]] for k in flip]
+                        if len(flip):
+                                add("iou", ks + [cand[sel[t]]], float(np.abs(rr[flip] - iou_thres).max()),
+                                float(np.abs(rr[flip] - ro[flip]).max()), box_anchors=ks + [cand[sel[t]]])
+                    if sup_o:
+                        continue
+                kept.append(t)
+            keep_mask[sel[kept]] = True
+    kept_idx = order[keep_mask[order]]  # output order: y_oth's processing order (descending score, all classes)
+    # output order / max_det cut: pairs of kept boxes whose order y_ref would invert, the earlier one within max_det
+    n = len(kept_idx)
+    if n > 1:
+        kr, ka = sc_r[kept_idx].astype(np.float64), cand[kept_idx]
+        ii, jj = np.triu_indices(n, 1)
+        m = ii < max_det
+        ii, jj = ii[m], jj[m]
+        inv = ~_rank_before(kr[ii], ka[ii], kr[jj], ka[jj])
+        if inv.any():
+            ii, jj = ii[inv], jj[inv]
+            pert_k = np.abs(kr - sc_o[kept_idx])
+            add("out_order", sorted(set(ka[ii].tolist()) | set(ka[jj].tolist())),
+                float(np.abs(kr[ii] - kr[jj]).max()), float(np.maximum(pert_k[ii], pert_k[jj]).max()),
+                score_anchors=sorted(set(ka[ii].tolist()) | set(ka[jj].tolist())), pairs=int(inv.sum()))
+    res["keep"] = cand[kept_idx[:max_det]].astype(np.int64)
+    res["ok"] = all(d["ok"] for d in dec)
+    return res
+
+
+def tie_level(d, rel=2.0 ** -21):
+    """A decision whose margin on y_ref is at the level of an fp32 rounding tie of its operands (<= 16 units in the
+    last place of a score in [0.5, 1)): the flat scenes' identical receptive fields give exact ties by construction."""
+    return d["margin"] <= rel

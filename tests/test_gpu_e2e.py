@@ -9,17 +9,20 @@ Workload: the trained-like paper model (tests/trained_like.py: BN recalibrated t
 logits in a moderate range) on two sets of 32 structured 640x640 scenes - flat rectangles (whose flat regions give
 neighbouring anchors exactly tied scores) and the same rectangles under per-pixel noise (no ties) - the bench's
 batch of 32 on the GPU and all 32 images through the oracle. Rule for the indices: every image's kept anchor indices
-must be bit-identical, in order, unless the two runs part at a decision that is a near-tie: both outputs are replayed
-through the reference's NMS side by side (tests/nms_margins.first_divergence) and the FIRST decision at which they
-differ - candidate filter, best class, processing order / max_nms cut, or a greedy IoU test; everything before it is
-identical in both runs - must have a margin on the oracle's output within twice the perturbation of that decision's
-inputs measured between the two outputs. Such an exception must also keep >= 90 % of the kept anchors in common; as
-sanity bounds at most half of the flat-scene images (exact ties by construction) and a quarter of the noisy ones may
-have one. On the noisy scenes >= 8 non-empty, decision-stable images (every
-decision's margin above twice the perturbation, tests/nms_margins.nms_stability) must be bit-exact. The GPU's indices
-always equal the oracle NMS of the GPU's own output. The mAP test scores val-mode detections of both full paths
-(production fused head, not the raw-map decode) against the same synthetic labels: |mAP50-95 difference| <= 1e-3,
-precision / recall / mAP50 within two TP flips of a class-averaged count
+must be bit-identical, in order, unless every decision at which the two runs part is a near-tie. Both outputs are
+replayed through the reference's NMS side by side (tests/nms_margins.replay_divergences): at each decision -
+candidate filter, best class, processing order of boxes that suppress one another, max_nms cut, greedy IoU test
+(NaN IoUs of zero-area boxes included), output order / max_det cut - the GPU's choice is adopted and the oracle's
+choice in the same state is recorded when it differs, so EVERY divergent decision of the image is found and the
+replay ends on the GPU's own kept list. Each divergent decision must be justified by its own perturbation: its margin
+on the oracle's output within twice the change of its own inputs between the two runs, and those inputs within the
+forward's accuracy (scores 1e-3, box coordinates 0.25 px). An image with a difference must also keep >= 90 % of its
+kept anchors in common; at most a quarter of the images of either scene kind may have a difference that is not an
+exact fp32 tie (the flat scenes' identical receptive fields give tied scores by construction; ties are counted and
+logged). On the noisy scenes >= 8 non-empty, decision-stable images (every decision's margin above twice the
+perturbation, tests/nms_margins.nms_stability) must be bit-exact. The GPU's indices always equal the oracle NMS of the
+GPU's own output. The mAP test scores val-mode detections of both full paths over all 32 images (production fused
+head, not the raw-map decode) against the same synthetic labels: every metric within 1e-3
 (``models/yolo/detect/val.py:92-102`` -> ``engine/validator.py:222-262``)."""
 import os
 
@@ -27,7 +30,7 @@ import numpy as np
 import pytest
 import torch
 
-from nms_margins import first_divergence, nms_stability
+from nms_margins import nms_stability, replay_divergences, tie_level
 from trained_like import make_trained_like_checkpoint, noisy_scenes, scenes
 
 pytestmark = pytest.mark.gpu
@@ -97,7 +100,7 @@ def test_e2e_kept_indices_gpu_vs_oracle(e2e):
     yc = y_cpu.numpy()
     _, idx_cpu = non_max_suppression_ref(yc.copy(), 0.25, 0.7, max_det=300)  # oracle forward -> oracle NMS
     _, idx_gpu_ref = non_max_suppression_ref(yg.copy(), 0.25, 0.7, max_det=300)  # oracle NMS on the GPU output
-    exact = stable_exact = kept_exact = exceptions = 0
+    exact = stable_exact = kept_exact = exceptions = ties = 0
     report = []
     for b in range(B_GPU):
         n = int(counts[b])
@@ -105,33 +108,40 @@ def test_e2e_kept_indices_gpu_vs_oracle(e2e):
         assert np.array_equal(gi, idx_gpu_ref[b])  # HIP NMS == oracle NMS on the same tensor
         st = nms_stability(yc[b], yg[b])
         assert np.array_equal(st["keep"], idx_cpu[b])  # the margin analysis replays the oracle's greedy NMS
+        rp = replay_divergences(yc[b], yg[b])
+        assert np.array_equal(rp["keep"], gi)  # the side-by-side replay ends on the GPU's own kept list
         a, c = set(gi.tolist()), set(idx_cpu[b].tolist())
         overlap = len(a & c) / max(len(a | c), 1)
         same = np.array_equal(gi, idx_cpu[b])
+        dec = rp["decisions"]
+        tie_only = bool(dec) and all(tie_level(d) for d in dec)
         line = (f"img {b}: kept {n}/{len(idx_cpu[b])} same {same} overlap {overlap:.3f} cand {st['n_cand']} "
                 f"stable {st['stable']} m_conf {st['m_conf']:.2e} m_cls {st['m_cls']:.2e} m_iou {st['m_iou']:.2e} "
                 f"m_order {st['m_order']:.2e} m_out {st['m_out']:.2e} d_score {st['d_score']:.2e} "
-                f"d_iou {st['d_iou']:.2e}")
+                f"d_iou {st['d_iou']:.2e} | {len(dec)} divergent decisions"
+                + (" (all fp32 ties)" if tie_only else "")
+                + "".join(f"; {d['kind']} {d['anchors'][:4]} margin {d['margin']:.2e} tol {d['tol']:.2e} "
+                          f"dS {d['score_pert']:.1e} dB {d['box_pert']:.1e}" + ("" if d["ok"] else " NOT JUSTIFIED")
+                          for d in dec[:6]))
+        report.append(line)
+        # every decision at which the runs part, anywhere in the image, is a near-tie of its own inputs
+        assert rp["ok"], "a divergent NMS decision is not a near-tie: " + line
         if same:
             exact += 1
             kept_exact += n
             stable_exact += int(st["stable"] and n > 0)
-            report.append(line)
             continue
-        # the kept lists differ: legitimate only if the first decision at which the two runs part is a near-tie
-        fd = first_divergence(yc[b], yg[b])
-        line += f" | first divergence {fd}"
-        report.append(line)
-        assert fd is not None, "kept lists differ but every NMS decision agrees: " + line
-        assert fd["margin"] <= fd["tol"], "first diverging decision is not a near-tie: " + line
+        assert dec, "kept lists differ but every NMS decision agrees: " + line
         assert not st["stable"], line
         assert overlap >= 0.9, line
         exceptions += 1
+        ties += int(tie_only)
+    cap = B_GPU // 4
     _log(f"{kind}: {exact}/{B_GPU} images bit-exact ({kept_exact} kept boxes), {stable_exact} of them non-empty and "
-         f"decision-stable, {exceptions} justified exceptions; " + " || ".join(report))
-    # every exception above is justified at its own first divergence; the counts are sanity bounds: the flat scenes
-    # manufacture exact score ties (identical receptive fields), the noisy ones do not
-    assert exceptions <= (B_GPU // 2 if kind == "flat" else B_GPU // 4), report
+         f"decision-stable, {exceptions} justified exceptions ({ties} of them exact fp32 ties only; "
+         f"{exceptions - ties} others against a cap of {cap}); " + " || ".join(report))
+    # the count is a sanity bound on top of the per-decision justification: differences that are not exact ties
+    assert exceptions - ties <= cap, report
     assert kept_exact >= 100, "too few kept boxes on bit-exact images for the test to mean anything"
     if kind == "noisy":
         assert stable_exact >= 8, report
@@ -142,8 +152,7 @@ def test_e2e_map_through_production_head(e2e):
     from oracle.nms import non_max_suppression_ref
     from yolosod_amd.engine.validator import VAL_NMS, DetectionEvaluator
     from yolosod_amd.utils.ops import non_max_suppression
-    kind, _, y_gpu, y_cpu, _ = e2e
-    y_gpu, y_cpu = y_gpu[FP64_IMAGES], y_cpu[FP64_IMAGES]
+    kind, _, y_gpu, y_cpu, _ = e2e  # all 32 images: one TP flip moves a class-averaged P / R by < 1e-3
     nc = y_cpu.shape[1] - 4
     rows_p, _ = non_max_suppression_ref(y_cpu.numpy().copy(), conf_thres=0.25, iou_thres=0.7)
     rng = np.random.default_rng(3)
@@ -166,13 +175,6 @@ def test_e2e_map_through_production_head(e2e):
     _log(f"{kind} mAP50-95 gpu {m_gpu['metrics/mAP50-95(B)']:.6f} cpu {m_cpu['metrics/mAP50-95(B)']:.6f}; "
          f"dets {[len(d) for d in dets_gpu]} vs {[len(r) for r in rows_cpu]}")
     assert m_cpu["metrics/mAP50-95(B)"] > 0.05, m_cpu
-    # mAP@0.5:0.95 (the north-star metric) within 1e-3. Precision / recall / mAP50 are class-averaged counts: one
-    # detection whose TP status flips at a legitimate near-tie (the val-mode NMS keeps conf >= 0.001, so the noisy
-    # scenes' index parity exceptions reach it) moves a class's recall by 1 / n_labels(class) and the mean over the labelled
-    # classes by that over their number - the bound below is two such flips
-    n_lab = np.bincount(np.concatenate([lab[0] for lab in labels]).astype(np.int64), minlength=nc)
-    present = n_lab[n_lab > 0]
-    flip = 2.0 / (len(present) * max(int(present.min()), 1))
+    # every metric within 1e-3 (mAP@0.5:0.95 is the north-star metric)
     for k in m_cpu:
-        tol = 1e-3 if k == "metrics/mAP50-95(B)" else max(1e-3, flip)
-        assert abs(m_gpu[k] - m_cpu[k]) <= tol, (k, m_gpu[k], m_cpu[k], tol)
+        assert abs(m_gpu[k] - m_cpu[k]) <= 1e-3, (k, m_gpu[k], m_cpu[k])

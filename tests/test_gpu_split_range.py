@@ -248,3 +248,23 @@ def test_sharded_predict_redoes_flagged_shard_on_exact_kernels(cuda):
     assert torch.isfinite(g_out).all()
     assert torch.equal(g_cnt, r_cnt) and torch.equal(g_idx, r_idx)
     assert torch.equal(g_out, r_out)
+
+
+def test_split_range_cached_a2_block_rereports_long_sequence(cuda):
+    """A2 with L = areas * W > 160 (the n1280 shape class) skips the fused attention kernel; the proj / pool kernel
+    re-raises the cached prepared block's range word, so out-of-range proj weights flag every forward, not only the
+    one that prepared the block."""
+    from yolosod_amd.nn.modules import A2_Attn
+    torch.manual_seed(3)
+    m = A2_Attn(64, None, 8, 1).eval().to(cuda)
+    x = torch.randn(1, 64, 40, 40, device=cuda)
+    _hip.split_range_flag(reset=True)
+    with torch.inference_mode():
+        m(x)
+    assert not _hip.split_range_flag(reset=True)
+    with torch.no_grad():
+        m.proj.conv.weight.mul_(4e4)  # 64 W beyond 65504
+    for _ in range(3):
+        with torch.inference_mode():
+            m(x)
+        assert _hip.split_range_flag(reset=True)

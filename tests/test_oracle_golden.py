@@ -41,10 +41,7 @@ def test_oracle_decode_matches_reference():
 @pytest.mark.parametrize("name", list(recipes.NMS_CASES))
 def test_oracle_nms_matches_reference(name):
     z = golden(name)
-    seed, B, A, nc, kw = recipes.NMS_CASES[name]
-    kw = dict(kw)
-    tie = kw.pop("tie", False)
-    pred = recipes.synthetic_predictions(seed, B, A, nc, tie_scores=tie)
+    pred, kw = recipes.nms_case(name)
     assert np.array_equal(pred, z["pred"])
     p = pred.copy()
     rows, idx = non_max_suppression_ref(p, **kw)

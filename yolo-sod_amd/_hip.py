@@ -357,12 +357,15 @@ def a2_forward(x, num_areas, num_heads, proj_w, proj_b, ln_w, ln_b, ln_eps, in_w
         raise RuntimeError(f"A2_Attn: sequence length {num_areas * W} > 320 unsupported")
     if bf and (C // num_heads not in (32, 64, 128) or C % 64):
         raise RuntimeError(f"A2_Attn (bf16): C={C} with head dim {C // num_heads} unsupported")
-    pblk = None
-    if prep is not None and not bf and mo_w is None and a2_prep_bytes(C, num_heads, num_areas, W) > 0:
-        pblk = prep()
-    return _launch(("a2", tuple(x.shape), (num_areas, num_heads)) + ((2,) if bf else ()), x.device, ops().a2_fwd, x,
-                   int(num_areas), int(num_heads), proj_w, proj_b, ln_w, ln_b, float(ln_eps), in_w, in_b, mo_w, mo_b,
-                   op_w, op_b, pblk)
+    use_prep = prep is not None and not bf and mo_w is None and a2_prep_bytes(C, num_heads, num_areas, W) > 0
+
+    def run():
+        # the preparation (a launch on first use of a parameter version) runs inside _launch: after the device's
+        # yolosod_init, under its device guard, and timed as part of this operator
+        return ops().a2_fwd(x, int(num_areas), int(num_heads), proj_w, proj_b, ln_w, ln_b, float(ln_eps), in_w, in_b,
+                            mo_w, mo_b, op_w, op_b, prep() if use_prep else None)
+
+    return _launch(("a2", tuple(x.shape), (num_areas, num_heads)) + ((2,) if bf else ()), x.device, run)
 
 
 def swin_forward(x, num_heads, window, dw_w, ln1_w, ln1_b, ln1_eps, in_w, in_b, out_w, out_b, ln2_w, ln2_b,
@@ -383,9 +386,11 @@ def swin_forward(x, num_heads, window, dw_w, ln1_w, ln1_b, ln1_eps, in_w, in_b, 
     key = ("swin", tuple(x.shape), (num_heads, window, hid)) + ((2,) if bf else ())
     if (prep is not None and not bf and wh == 7 and ww == 7 and C * H * W < (1 << 30)
             and swin_prep_bytes(C, num_heads, hid) > 0):
-        # the weight split / folds were made once (``prep`` = swin_prepare of these parameters): one kernel launch
-        return _launch(key, x.device, ops().swin_fwd_prepared, x, prep(), int(num_heads), int(window), dw_w,
-                       float(ln1_eps), out_b, float(ln2_eps), int(hid), m2_b)
+        # the weight split / folds were made once (``prep`` = swin_prepare of these parameters): one kernel launch;
+        # prep() runs inside _launch (device initialised, timed with the operator), as in a2_forward
+        return _launch(key, x.device, lambda: ops().swin_fwd_prepared(x, prep(), int(num_heads), int(window), dw_w,
+                                                                      float(ln1_eps), out_b, float(ln2_eps), int(hid),
+                                                                      m2_b))
     return _launch(key, x.device, ops().swin_fwd, x, int(num_heads), int(window), dw_w, ln1_w, ln1_b, float(ln1_eps),
                    in_w, in_b, out_w, out_b, ln2_w, ln2_b, float(ln2_eps), m1_w, m1_b, m2_w, m2_b, pw_w, bn_w, bn_b,
                    bn_mean, bn_var, float(bn_eps))

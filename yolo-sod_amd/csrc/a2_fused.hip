@@ -346,7 +346,8 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void a2_proj_pool_kernel(
                                                                               const float* __restrict__ bp,
                                                                               float* __restrict__ S, int C, int H,
                                                                               int W, int A, int G,
-                                                                              unsigned* range_flag) {
+                                                                              unsigned* range_flag,
+                                                                              const unsigned* prep_flag) {
   constexpr int NPX = NCB * 16;                 // padded pixels
   constexpr int PPL = NPX * PPS;                // plane (halves)
   constexpr int STG_B = 2 * 2 * PPL * 2;        // two buffers x two planes
@@ -506,6 +507,9 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void a2_proj_pool_kernel(
     }
   }
   range_report(range_flag, rng);
+  // the prepared proj planes were range-checked once, at preparation: re-raise that result on every call (the
+  // attention kernel does the same for the in_proj planes, but it does not run when L > 160)
+  if (prep_flag && range_flag && blockIdx.x == 0 && threadIdx.x == 0 && *prep_flag) *range_flag = 1u;
 }
 
 // Weight preparation, one wave per output row: rows [0, 3C) = in_proj with the LN affine folded (W' = W diag(gamma),
@@ -670,7 +674,7 @@ int yolosod_a2_proj_pool_run(const float* x, const float* proj_b, float* S, int 
 #define YS_A2P(N, NW)                                                                                                \
   if (ncb <= N) {                                                                                                     \
     hipLaunchKernelGGL((a2f::a2_proj_pool_kernel<N, NW>), dim3((unsigned)nwg), dim3(64 * NW), 0, st, x, q.pplanes,   \
-                       proj_b, S, C, H, W, A, G, range_flag_dev());                                                   \
+                       proj_b, S, C, H, W, A, G, range_flag_dev(), q.pflag);                                                 \
     YS_CHECK_LAUNCH("a2_proj_pool");                                                                                  \
     return 0;                                                                                                         \
   }

@@ -24,16 +24,18 @@ static std::mutex g_flag_mu;
 static unsigned* g_flags[64] = {nullptr};
 static unsigned* flag_alloc(int dev) {
   std::lock_guard<std::mutex> lk(g_flag_mu);
-  if (!g_flags[dev]) {
+  unsigned* cur = __atomic_load_n(&g_flags[dev], __ATOMIC_RELAXED);  // writers hold the lock
+  if (!cur) {
     unsigned* p = nullptr;
     if (hipMalloc(&p, sizeof(unsigned)) != hipSuccess) return nullptr;
     if (hipMemset(p, 0, sizeof(unsigned)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
       (void)hipFree(p);
       return nullptr;
     }
-    g_flags[dev] = p;
+    __atomic_store_n(&g_flags[dev], p, __ATOMIC_RELEASE);  // pairs with the lock-free acquire load below
+    cur = p;
   }
-  return g_flags[dev];
+  return cur;
 }
 unsigned* range_flag_dev() {
   int dev = 0;
