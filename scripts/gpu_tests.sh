@@ -1,16 +1,12 @@
 #!/bin/bash
-# GPU pytest pass only: bash scripts/gpu_tests.sh TAG [pytest -k expr] [test path]
+# Selected GPU tests: bash scripts/gpu_tests.sh TAG test_file[::name] ...  (results under gpurun_out/TAG)
 set -o pipefail
-TAG=${1:-run}
-K=${2:-}
-P=${3:-tests}
-OUT=gpurun_out/$TAG
-mkdir -p "$OUT"
+TAG=$1; shift
+OUT=gpurun_out/$TAG; mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
-if [ -n "$K" ]; then KARG=(-k "$K"); else KARG=(); fi
 export YOLOSOD_PARITY_LOG="$GRAFT_REPO_ROOT/$OUT/parity.log"
-timeout -k 10 900 python -u -m pytest $P -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider \
-  "${KARG[@]}" > "$OUT/pytest.log" 2>&1
+timeout -k 10 900 python -u -m pytest "$@" -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider \
+  > "$OUT/pytest.log" 2>&1
 rc=$?
-tail -40 "$OUT/pytest.log" | grep -E "FAILED|ERROR|passed|failed|Error" | tail -25
+grep -E "PASSED|FAILED|ERROR|passed|failed" "$OUT/pytest.log" | tail -40
 exit $rc
