@@ -252,6 +252,13 @@ int yolosod_debug_set_a2_x2(int on);
 /* Test hook: A2_Attn's split path through the fused kernels (1, default; env YOLOSOD_A2_FUSED=0 turns it off:
  * proj + SiLU + pooling, then LN + QKV + attention, csrc/a2_fused.hip) or the decomposed GEMM path (0). */
 int yolosod_debug_set_a2_fused(int on);
+/* Test hook: A2_Attn's tail as one kernel (1; env YOLOSOD_A2_OUTUP=1, default off: the folded out-projection,
+ * the bilinear upsample along H, SiLU and the residual, csrc/a2_fused.hip a2_out_up_kernel) or as the token GEMM and
+ * a separate upsample pass (0); returns the previous state. */
+int yolosod_debug_set_a2_outup(int on);
+/* Test hook: A2_Attn's proj + SiLU + pooling kernel with 128 / 256 output channels per workgroup (1, default; env
+ * YOLOSOD_A2_POOL_WIDE=0 turns it off) or with 64 (0); returns the previous state. */
+int yolosod_debug_set_a2_pool_wide(int on);
 void yolosod_debug_set_gemm_x2(int on);
 /* Test hook: the bf16 decomposed SwinBlock's depthwise conv + token layout and LN1 in one pass
  * (swin_tokens_ln_bf16_kernel, 1, default; env YOLOSOD_SWIN_TOKLN=0 turns it off) or as two kernels (0);

@@ -178,31 +178,37 @@ A2_FUSED_SHAPES = {  # A2_Attn through both forms of its fp16-split path
 }
 
 
+@pytest.mark.parametrize("outup", [0, 1], ids=["gemm_upsample", "out_up"])
 @pytest.mark.parametrize("fused", [0, 1], ids=["decomposed", "fused"])
 @pytest.mark.parametrize("name", list(A2_FUSED_SHAPES))
-def test_a2_fused_and_decomposed_forms(name, fused, cuda, monkeypatch):
+def test_a2_fused_and_decomposed_forms(name, fused, outup, cuda, monkeypatch):
     """A2_Attn's split path as the fused kernels (a2_fused.hip: proj + SiLU + row pooling, then LN + QKV + attention
-    per (image, head); the default) and as the decomposed GEMM path (YOLOSOD_A2_FUSED=0), against the fp64 oracle."""
+    per (image, head); the default) and as the decomposed GEMM path (YOLOSOD_A2_FUSED=0), each with its tail as the
+    token GEMM + upsample pass (the default) or as the fused out-projection + upsample + SiLU + residual kernel
+    (a2_out_up_kernel, YOLOSOD_A2_OUTUP=1), against the fp64 oracle."""
     lib = _hip.load_library()
     if A2_FUSED_SHAPES[name] is not None:
         monkeypatch.setitem(recipes.OPS, name, A2_FUSED_SHAPES[name])
     m, _ = build_fixture_module(name)
     x = recipes.make_input(name, recipes.OPS[name][2])
     prev = lib.yolosod_debug_set_a2_fused(fused)
+    prev_ou = lib.yolosod_debug_set_a2_outup(outup)
     try:
         with torch.inference_mode():
             y = m.to(cuda)(x.to(cuda)).cpu()
     finally:
         lib.yolosod_debug_set_a2_fused(prev)
+        lib.yolosod_debug_set_a2_outup(prev_ou)
     ok, err, ratio = tol_close(y, _oracle64(name, x), 5e-5, 1e-4)
-    assert ok, f"{name} fused={fused}: vs fp64 oracle max abs err {err:.3g} (ratio {ratio:.2f})"
+    assert ok, f"{name} fused={fused} outup={outup}: vs fp64 oracle max abs err {err:.3g} (ratio {ratio:.2f})"
 
 
 @pytest.mark.parametrize("name", ["a2_c512_h20", "a2_L12", "a2_b3_c256_12x8", "a2_b2_c192_10x20", "a2_L12_1280"])
 def test_a2_proj_pool_area_groups_bit_identical(name, cuda, monkeypatch):
-    """The proj + SiLU + pooling kernel over one tile per image (cap 400 pixels) and split into area groups (cap 208,
-    the default: two groups of 10 rows at 20x20; cap 100: four groups) computes every pixel with the same k order, so
-    the outputs are bit-identical. At 40x40 (n1280, L = 320: the decomposed attention after the fused proj / pool)
+    """The proj + SiLU + pooling kernel over one tile per image (cap 400 pixels) and split into area groups (cap 208:
+    two groups of 10 rows at 20x20; cap 100: four groups), and the wide kernel (128 / 256 output channels per
+    workgroup, the default) compute every pixel with the same k order and MFMA operand layout, so the outputs are
+    bit-identical. At 40x40 (n1280, L = 320: the decomposed attention after the fused proj / pool)
     the caps give 4 / 8 / 4 groups."""
     lib = _hip.load_library()
     if A2_FUSED_SHAPES[name] is not None:
@@ -211,15 +217,19 @@ def test_a2_proj_pool_area_groups_bit_identical(name, cuda, monkeypatch):
     m = m.to(cuda)
     x = recipes.make_input(name, recipes.OPS[name][2]).to(cuda)
     prev = lib.yolosod_debug_set_a2_pool_px(400)
+    prev_w = lib.yolosod_debug_set_a2_pool_wide(0)
     try:
         with torch.inference_mode():
             ys = [m(x).cpu()]
             for cap in (208, 100):
                 lib.yolosod_debug_set_a2_pool_px(cap)
                 ys.append(m(x).cpu())
+            lib.yolosod_debug_set_a2_pool_wide(1)  # 128 / 256 channels per workgroup, its own area groups
+            ys.append(m(x).cpu())
     finally:
         lib.yolosod_debug_set_a2_pool_px(prev)
-    for cap, y in zip((208, 100), ys[1:]):
+        lib.yolosod_debug_set_a2_pool_wide(prev_w)
+    for cap, y in zip((208, 100, "wide"), ys[1:]):
         assert torch.equal(ys[0], y), f"{name} cap {cap}: max|d| {float((ys[0] - y).abs().max()):.3g}"
 
 

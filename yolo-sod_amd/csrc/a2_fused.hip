@@ -512,6 +512,337 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void a2_proj_pool_kernel(
   if (prep_flag && range_flag && blockIdx.x == 0 && threadIdx.x == 0 && *prep_flag) *range_flag = 1u;
 }
 
+// The same proj + SiLU + pooling with NRB * 16 output channels per workgroup (128 or 256 instead of 64), 8 waves, one
+// workgroup per CU: the kernel above reads each image's x once per 64-channel block, 8 times at C = 512, and at that
+// volume (8 x 26 MB per call at n640) it ran at the rate the L2 misses are served (~4 TB/s), not at its products'.
+// Here x is read C / (16 NRB) times (twice at n640) from smaller area groups (e.g. 4 groups of 5 rows at 20x20). Wave w
+// owns row blocks [w RBW, (w + 1) RBW) and every column block of the group: the weight fragments (A) stay in
+// registers across the column blocks, the staged x planes (B) are read once per row-block pair.
+template <int NCB, int NRB>
+__global__ __launch_bounds__(512, 1) void a2_proj_pool_wide_kernel(const float* __restrict__ x,
+                                                                  const h16_t* __restrict__ wp,
+                                                                  const float* __restrict__ bp, float* __restrict__ S,
+                                                                  int C, int H, int W, int A, int G,
+                                                                  unsigned* range_flag, const unsigned* prep_flag) {
+  constexpr int NW = 8, NT = 512;
+  constexpr int CH = NRB * 16;                  // output channels per workgroup
+  constexpr int RBW = NRB / NW;                 // row blocks per wave
+  constexpr int NPX = NCB * 16;                 // padded pixels
+  constexpr int PPL = NPX * PPS;                // plane (halves)
+  constexpr int STG_B = 2 * 2 * PPL * 2;        // two buffers x two planes
+  constexpr int HWP = NPX + 1;                  // fp32 tile row stride (odd: conflict-free per-channel reads)
+  constexpr int T_B = CH * HWP * 4;
+  constexpr int R_B = STG_B > T_B ? STG_B : T_B;
+  static_assert(NRB % NW == 0, "row blocks per wave");
+  static_assert(R_B <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) char smem[R_B];
+  h16_t* Pl = reinterpret_cast<h16_t*>(smem);   // [2 buf][2 plane][NPX][PPS]
+  float* Tt = reinterpret_cast<float*>(smem);   // [CH][HWP] after the K loop
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l15 = lane & 15, g = lane >> 4;
+  const int HW = H * W;
+  const int nch = C / CH;
+  const int nblk = gridDim.x;
+  // XCD-aware: consecutive wg (the channel blocks and area groups of one image) on one XCD
+  const int wgi = (nblk & 7) ? (int)blockIdx.x : (int)(blockIdx.x & 7) * (nblk >> 3) + (int)(blockIdx.x >> 3);
+  const int img = wgi / (nch * G), rem = wgi - img * nch * G;
+  const int grp = rem / nch, co = (rem - grp * nch) * CH;
+  const PoolGroup pg = pool_group(grp, G, A, H);
+  const int npx = (pg.r1 - pg.r0) * W;  // the group's pixels (a multiple of 4: W % 4 == 0 when G > 1)
+  const float* xb = x + (long)img * C * HW + pg.r0 * W;
+  float rng = 0.f;
+
+  // staging: (4 k x 4 pixel) blocks of the 32 x NPX step tile; 8 * NPX / 4 blocks
+  constexpr int NBLK = 8 * (NPX / 4);
+  constexpr int NIT = (NBLK + NT - 1) / NT;
+  // x tiles and weight fragments of steps s + 1 .. s + D - 1 are in flight in a register ring while step s computes
+  // (D = 3 measured slower: 36 -> 42 us at n640)
+  constexpr int D = 2;
+  float4 xr[D][NIT][4];
+  auto load_step = [&](float4 (&stg)[NIT][4], int s) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) {
+      // unconditional loads, pixel clamped into the group (see a2_proj_pool_kernel)
+      const int e = tid + NT * i;
+      const int kq = e & 7, pq = e >> 3;
+      const int k = 32 * s + 4 * kq, px = min(4 * pq, npx - 4);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) stg[i][r] = *reinterpret_cast<const float4*>(xb + (long)(k + r) * HW + px);
+    }
+  };
+  auto store_step = [&](const float4 (&stg)[NIT][4], int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) {
+      const int e = tid + NT * i;
+      if (e < NBLK) {
+        const int kq = e & 7, pq = e >> 3;
+        const float4* v = stg[i];
+        const f32x4 col[4] = {f32x4{v[0].x, v[1].x, v[2].x, v[3].x}, f32x4{v[0].y, v[1].y, v[2].y, v[3].y},
+                              f32x4{v[0].z, v[1].z, v[2].z, v[3].z}, f32x4{v[0].w, v[1].w, v[2].w, v[3].w}};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          uint2 hh, ll;
+          split4(col[j], hh, ll);
+          rng = range_acc(rng, col[j]);
+          h16_t* d = Pl + (buf * 2) * PPL + (4 * pq + j) * PPS + 4 * kq;
+          *reinterpret_cast<uint2*>(d) = hh;
+          *reinterpret_cast<uint2*>(d + PPL) = ll;
+        }
+      }
+    }
+  };
+  // weight fragments (A operand): output rows co + 16 (wid RBW + rb) + l15, k = 32 s + 8g .. +7, fragment-major planes
+  const int nk32 = C / 32;
+  const long pst = (long)C * C;
+  const int rbase = (co >> 4) + wid * RBW;
+  auto wfrag = [&](int rb, int s, int pl) {
+    return *reinterpret_cast<const f16x8_t*>(wp + pl * pst + ((long)((rbase + rb) * nk32 + s) * 64 + lane) * 8);
+  };
+  f32x4 acc[RBW][NCB];
+#pragma unroll
+  for (int rb = 0; rb < RBW; ++rb)
+#pragma unroll
+    for (int j = 0; j < NCB; ++j) acc[rb][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f16x8_t wr[D][RBW][2];
+  auto load_w = [&](f16x8_t (&w)[RBW][2], int s) __attribute__((always_inline)) {
+#pragma unroll
+    for (int rb = 0; rb < RBW; ++rb) {
+      w[rb][0] = wfrag(rb, s, 0);
+      w[rb][1] = wfrag(rb, s, 1);
+    }
+  };
+  // ring slot i holds step s with s % D == i; unconditional (clamped) loads past the last step
+#pragma unroll
+  for (int i = 0; i < D; ++i) {
+    load_step(xr[i], i < nk32 ? i : nk32 - 1);
+    load_w(wr[i], i < nk32 ? i : nk32 - 1);
+  }
+  store_step(xr[0], 0);
+  for (int s0 = 0; s0 < nk32; s0 += D) {
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      const int s = s0 + i;
+      if (s < nk32) {
+        const int buf = s & 1;
+        __syncthreads();  // step s's planes stored; every wave is done with step s - 1's buffer
+        const h16_t* b0 = Pl + (buf * 2) * PPL + l15 * PPS + 8 * g;
+#pragma unroll
+        for (int j = 0; j < NCB; ++j) {
+          const f16x8_t xh = *reinterpret_cast<const f16x8_t*>(b0 + j * 16 * PPS);
+          const f16x8_t xl = *reinterpret_cast<const f16x8_t*>(b0 + j * 16 * PPS + PPL);
+#pragma unroll
+          for (int rb = 0; rb < RBW; ++rb) {
+            f32x4 c = mfma16(wr[i][rb][1], xh, acc[rb][j]);
+            c = mfma16(wr[i][rb][0], xl, c);
+            acc[rb][j] = mfma16(wr[i][rb][0], xh, c);
+          }
+        }
+        if (s + 1 < nk32) store_step(xr[(i + 1) % D], buf ^ 1);
+        const int sn = s + D < nk32 ? s + D : nk32 - 1;
+        load_step(xr[i], sn);
+        load_w(wr[i], sn);
+      }
+    }
+  }
+  __syncthreads();  // the staging planes are free: the SiLU tile takes the region
+  // lane (g, l15) of (rb, j): channel co + 16 (wid RBW + rb) + 4g + r, pixel 16 j + l15
+#pragma unroll
+  for (int rb = 0; rb < RBW; ++rb) {
+    const int cl = 16 * (wid * RBW + rb) + 4 * g;
+    const f32x4 bias = *reinterpret_cast<const f32x4*>(bp + co + cl);
+#pragma unroll
+    for (int j = 0; j < NCB; ++j) {
+      const int px = j * 16 + l15;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Tt[(cl + r) * HWP + px] = silu_fast_(acc[rb][j][r] * (1.0f / WSC) + bias[r]);
+    }
+  }
+  __syncthreads();
+  // pooled tokens: thread (c = tid % CH, column group tid / CH) averages its channel's bins in row order (as the
+  // reference's CPU pooling) for the columns w = tid / CH + (NT / CH) i of every area of the group
+  constexpr int NCG = NT / CH;  // column groups
+  const int c = tid % CH;
+  const float* trow = Tt + c * HWP - pg.r0 * W;
+  float* Sb = S + (long)img * A * W * C + co + c;
+  for (int a = pg.a0; a < pg.a1; ++a) {
+    const int r0 = (a * H) / A, r1 = ((a + 1) * H + A - 1) / A;
+    const float cnt = (float)(r1 - r0);
+    for (int w = tid / CH; w < W; w += NCG) {
+      float sum = 0.f;
+      for (int r = r0; r < r1; ++r) sum += trow[r * W + w];
+      Sb[(long)(a * W + w) * C] = sum / cnt;
+    }
+  }
+  range_report(range_flag, rng);
+  if (prep_flag && range_flag && blockIdx.x == 0 && threadIdx.x == 0 && *prep_flag) *range_flag = 1u;
+}
+
+// ---- out-projection + bilinear upsample + SiLU + residual, one kernel --------------------------------------------
+// a2_attn.py:53-67: the MHA out-projection and the output 1x1 conv (BN folded) are consecutive linear maps, folded into
+// Wf = Wconv Wmha, bf (A2_Attn._fused_out); the bilinear upsample from (A, W) to (H, W) (align_corners=False: along H
+// only, identity along W) commutes with them, so y = x + SiLU(up_H(Wf O) + bf). One 256-thread workgroup per
+// (image, column tile of wc columns, 32 output channels) computes T = Wf[32 rows] O^T over the tile's A * wc tokens on
+// fp16-split MFMA (weights = the A operand, split on the fly from fp32 x 64; tokens = B, staged per 64-k stage as two
+// fp16 planes in LDS), keeps T [64][A][wc] in LDS and streams the tile's pixels of x -> y: T never reaches HBM (the
+// decomposed path wrote it and re-read it in a separate upsample pass). Wave w: row block w & 1, token blocks
+// w >> 1, (w >> 1) + 2, ... Small workgroups (>= 512 of them, two or three per CU) let one workgroup's streaming
+// epilogue overlap another's token GEMM, whose stages wait on L2 latency.
+constexpr int OU_KS = 64;          // k stage
+constexpr int OU_PS = OU_KS + 8;   // plane row stride (halves): 9 16-byte quads, conflict-free b128 reads
+template <int NTB>  // token blocks of 16 per workgroup (tokens = A * wc <= 16 NTB)
+__global__ __launch_bounds__(256, 3) void a2_out_up_kernel(const float* __restrict__ O, const float* __restrict__ wf,
+                                                           const float* __restrict__ bf, const float* __restrict__ x,
+                                                           float* __restrict__ y, int C, int H, int W, int A, int wc,
+                                                           unsigned* range_flag) {
+  constexpr int NT = 256;
+  constexpr int CB = 32;                       // output channels per workgroup
+  constexpr int NR = NTB * 16;                 // padded tokens
+  constexpr int PL = NR * OU_PS;               // plane (halves)
+  constexpr int STG_B = 2 * PL * 2;
+  constexpr int TS = NR + 4;                   // T tile row stride (floats; a multiple of 4: 16-byte row reads)
+  constexpr int T_B = CB * TS * 4;
+  constexpr int R_B = STG_B > T_B ? STG_B : T_B;
+  constexpr int TBW = (NTB + 1) / 2;           // token blocks per wave
+  constexpr int NIT = (NR * 16 + NT - 1) / NT; // staged float4 per thread per stage
+  static_assert(R_B <= 160 * 1024 / 3, "three workgroups per CU");
+  __shared__ __attribute__((aligned(16))) char smem[R_B];
+  h16_t* Pl = reinterpret_cast<h16_t*>(smem);  // [2 plane][NR][OU_PS]
+  float* Tt = reinterpret_cast<float*>(smem);  // [CB][TS] after the K loop
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l15 = lane & 15, g = lane >> 4;
+  const int rb = wid & 1, th = wid >> 1;
+  const int ncb = C / CB, ntile = W / wc;
+  const int nblk = gridDim.x;
+  // XCD-aware: the channel blocks and column tiles of one image (which read the same tokens) run on one XCD
+  const int wgi = (nblk & 7) ? (int)blockIdx.x : (int)(blockIdx.x & 7) * (nblk >> 3) + (int)(blockIdx.x >> 3);
+  const int img = wgi / (ntile * ncb), rem = wgi - img * ntile * ncb;
+  const int tile = rem / ncb, co = (rem - tile * ncb) * CB;
+  const int w0 = tile * wc;
+  const int L = A * W, nt = A * wc;
+  float rng = 0.f;
+
+  // staged item e of a stage: token row e >> 4 (local token j = a * wc + wl), 4 k values at 4 (e & 15)
+  const float* rows[NIT];
+#pragma unroll
+  for (int i = 0; i < NIT; ++i) {
+    const int e = tid + NT * i;
+    int j = e >> 4;
+    j = j < nt ? j : nt - 1;  // padding rows read the last token (finite; their outputs are dropped)
+    const int a = j / wc, wl = j - a * wc;
+    rows[i] = O + ((long)img * L + a * W + w0 + wl) * C + 4 * (e & 15);
+  }
+  f32x4 stg[NIT];
+  auto load_stage = [&](int s) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) stg[i] = *reinterpret_cast<const f32x4*>(rows[i] + OU_KS * s);
+  };
+  auto store_stage = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) {
+      const int e = tid + NT * i;
+      if (e < NR * 16) {
+        uint2 hh, ll;
+        split4(stg[i], hh, ll);
+        rng = range_acc(rng, stg[i]);
+        h16_t* d = Pl + (e >> 4) * OU_PS + 4 * (e & 15);
+        *reinterpret_cast<uint2*>(d) = hh;
+        *reinterpret_cast<uint2*>(d + PL) = ll;
+      }
+    }
+  };
+  // weight fragment (A operand) of k step s32: Wf[co + 16 rb + l15][32 s32 + 8 g .. + 7] x 64, split
+  const float* wrow = wf + (long)(co + 16 * rb + l15) * C + 8 * g;
+  auto wfrag = [&](int s32, f16x8_t& wh, f16x8_t& wl) __attribute__((always_inline)) {
+    const f32x4 a = *reinterpret_cast<const f32x4*>(wrow + 32 * s32) * WSC;
+    const f32x4 b = *reinterpret_cast<const f32x4*>(wrow + 32 * s32 + 4) * WSC;
+    rng = range_acc(range_acc(rng, a), b);
+    split8(a, b, wh, wl);
+  };
+  f32x4 acc[TBW];
+#pragma unroll
+  for (int i = 0; i < TBW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nstage = C / OU_KS;
+  load_stage(0);
+  for (int s = 0; s < nstage; ++s) {
+    __syncthreads();  // every wave is done with the previous stage's planes
+    store_stage();
+    __syncthreads();
+    if (s + 1 < nstage) load_stage(s + 1);  // in flight during this stage's products
+#pragma unroll
+    for (int u = 0; u < OU_KS / 32; ++u) {
+      f16x8_t wh, wl;
+      wfrag(2 * s + u, wh, wl);
+      const h16_t* b0 = Pl + l15 * OU_PS + 32 * u + 8 * g;
+#pragma unroll
+      for (int i = 0; i < TBW; ++i) {
+        const int tb = th + 2 * i;
+        if (tb < NTB) {
+          const f16x8_t xh = *reinterpret_cast<const f16x8_t*>(b0 + tb * 16 * OU_PS);
+          const f16x8_t xl = *reinterpret_cast<const f16x8_t*>(b0 + tb * 16 * OU_PS + PL);
+          acc[i] = mfma_f16x3(wh, wl, xh, xl, acc[i]);
+        }
+      }
+    }
+  }
+  __syncthreads();  // the planes are free: the T tile takes the region
+  // lane (g, l15) of token block tb: T[channel 16 rb + 4 g + r][token tb * 16 + l15]
+#pragma unroll
+  for (int i = 0; i < TBW; ++i) {
+    const int tb = th + 2 * i;
+    if (tb < NTB) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Tt[(16 * rb + 4 * g + r) * TS + tb * 16 + l15] = acc[i][r] * (1.0f / WSC);
+    }
+  }
+  __syncthreads();
+  // pixel rows of the tile: thread -> (channel c, row h), its wc / 4 column quads in chunks of 5 loads in flight; the
+  // interpolation weights, bias and T rows are per row. Offsets are 32-bit from the channel block's base (the launcher
+  // checks 64 * H * W < 2^29)
+  const int nq = wc >> 2, nrow = CB * H;
+  const float sc = (float)A / (float)H, r_h = 1.0f / (float)H;
+  const int HW = H * W;
+  const float* xb = x + ((long)img * C + co) * HW + w0;
+  float* yb = y + ((long)img * C + co) * HW + w0;
+  for (int row = tid; row < nrow; row += NT) {
+    int c = (int)((float)row * r_h);  // row / H: fp32 estimate + one correction each way (exact, row < 2^22)
+    c -= (c * H > row) ? 1 : 0;
+    c += ((c + 1) * H <= row) ? 1 : 0;
+    const int h = row - c * H;
+    float src = sc * ((float)h + 0.5f) - 0.5f;
+    if (src < 0.f) src = 0.f;
+    const int y0 = (int)src;
+    const int y1 = y0 + ((y0 < A - 1) ? 1 : 0);
+    const float l1 = src - (float)y0, l0 = 1.0f - l1;
+    const float b = bf[co + c];
+    const float* t0 = Tt + c * TS + y0 * wc;
+    const float* t1 = Tt + c * TS + y1 * wc;
+    const int off = c * HW + h * W;
+    for (int q0 = 0; q0 < nq; q0 += 5) {
+      f32x4 xv[5];
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        const int q = q0 + k < nq ? q0 + k : nq - 1;  // clamped (unconditional) loads; only q < nq is stored
+        xv[k] = *reinterpret_cast<const f32x4*>(xb + off + 4 * q);
+      }
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        const int q = q0 + k;
+        if (q < nq) {
+          const f32x4 u0 = *reinterpret_cast<const f32x4*>(t0 + 4 * q);
+          const f32x4 u1 = *reinterpret_cast<const f32x4*>(t1 + 4 * q);
+          f32x4 r;
+#pragma unroll
+          for (int j2 = 0; j2 < 4; ++j2) r[j2] = xv[k][j2] + silu_fast_(l0 * u0[j2] + l1 * u1[j2] + b);
+          *reinterpret_cast<f32x4*>(yb + off + 4 * q) = r;
+        }
+      }
+    }
+  }
+  range_report(range_flag, rng);
+}
+
 // Weight preparation, one wave per output row: rows [0, 3C) = in_proj with the LN affine folded (W' = W diag(gamma),
 // b' = b + W beta), rows [3C, 4C) = the proj 1x1 conv (BN folded by the caller); both split into fp16 planes (x64,
 // fragment-major: element (n, k) of [N][C] at ((n/16 * C/32 + k/32) * 64 + (k%32)/8 * 16 + n%16) * 8 + k%8)
@@ -658,6 +989,46 @@ bool yolosod_a2_proj_pool_ok(int C, int H, int W, int A) {
          (a2_pool_groups(H, W, A, a2_pool_cap(), nullptr) > 0 || a2_pool_groups(H, W, A, a2f::PMAXHW, nullptr) > 0);
 }
 
+// The wide proj / pool kernel (default; YOLOSOD_A2_POOL_WIDE=0 keeps the 64-channel one): its (column blocks, row
+// blocks per workgroup) instances and the configuration for a shape - the first instance whose area groups fit and
+// that gives >= 256 workgroups, else the one with the most workgroups (0: none fits).
+static int g_a2_pool_wide = -1;
+static bool a2_pool_wide_env() {
+  if (g_a2_pool_wide < 0) {
+    const char* e = getenv("YOLOSOD_A2_POOL_WIDE");
+    g_a2_pool_wide = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_a2_pool_wide != 0;
+}
+// Test hook: the wide proj / pool kernel on (1) or off (0); returns the previous state.
+YS_EXPORT int yolosod_debug_set_a2_pool_wide(int on) {
+  const int prev = a2_pool_wide_env() ? 1 : 0;
+  g_a2_pool_wide = on ? 1 : 0;
+  return prev;
+}
+struct A2PoolWide {
+  int ncb, nrb, G;
+};
+static A2PoolWide a2_pool_wide_cfg(int B, int C, int H, int W, int A) {
+  static const int inst[][2] = {{7, 16}, {13, 8}, {7, 8}};
+  A2PoolWide best{0, 0, 0};
+  long best_n = 0;
+  if (!a2_pool_wide_env()) return best;
+  for (const auto& in : inst) {
+    if (C % (16 * in[1])) continue;
+    int mx = 0;
+    const int G = a2_pool_groups(H, W, A, in[0] * 16, &mx);
+    if (G == 0) continue;
+    const long n = (long)B * G * (C / (16 * in[1]));
+    if (n >= 256) return A2PoolWide{in[0], in[1], G};
+    if (n > best_n) {
+      best_n = n;
+      best = A2PoolWide{in[0], in[1], G};
+    }
+  }
+  return best;
+}
+
 // x -> S (token-major pooled SiLU(proj x + bp)). Returns < 0 on error.
 int yolosod_a2_proj_pool_run(const float* x, const float* proj_b, float* S, int B, int C, int H, int W, int A,
                              const void* prep, size_t prep_bytes, hipStream_t st) {
@@ -665,6 +1036,20 @@ int yolosod_a2_proj_pool_run(const float* x, const float* proj_b, float* S, int 
   YS_CHECK_ARG(a2f_carve(const_cast<void*>(prep), prep_bytes, C, q), "a2: prepared block too small");
   YS_CHECK_ARG(yolosod_a2_proj_pool_ok(C, H, W, A), "a2: proj/pool shape C=%d %dx%d A=%d not fused", C, H, W, A);
   YS_CHECK_ARG(((uintptr_t)x & 15) == 0, "a2: x must be 16-byte aligned");
+  const A2PoolWide wc = a2_pool_wide_cfg(B, C, H, W, A);
+  if (wc.G > 0) {
+    const long nw = (long)B * wc.G * (C / (16 * wc.nrb));
+    YS_CHECK_ARG(nw < (1L << 31), "a2: too many workgroups");
+#define YS_A2PW(N, R)                                                                                               \
+  if (wc.ncb == N && wc.nrb == R) {                                                                                 \
+    hipLaunchKernelGGL((a2f::a2_proj_pool_wide_kernel<N, R>), dim3((unsigned)nw), dim3(512), 0, st, x, q.pplanes,  \
+                       proj_b, S, C, H, W, A, wc.G, range_flag_dev(), q.pflag);                                     \
+    YS_CHECK_LAUNCH("a2_proj_pool_wide");                                                                            \
+    return 0;                                                                                                        \
+  }
+    YS_A2PW(7, 16) YS_A2PW(13, 8) YS_A2PW(7, 8)
+#undef YS_A2PW
+  }
   int mx = 0;
   int G = a2_pool_groups(H, W, A, a2_pool_cap(), &mx);
   if (G == 0) G = a2_pool_groups(H, W, A, a2f::PMAXHW, &mx);
@@ -682,6 +1067,62 @@ int yolosod_a2_proj_pool_run(const float* x, const float* proj_b, float* S, int 
 #undef YS_A2P
   YS_CHECK_ARG(false, "a2: %dx%d pixels too many for the proj/pool kernel", H, W);
   return -1;
+}
+
+// the fused out-projection + upsample kernel (opt-in, YOLOSOD_A2_OUTUP=1; measured level with the token GEMM + upsample
+// pass at n640 and slower at n1280: its token GEMM re-stages the attention output per 32-channel block and waits on L2
+// every stage)
+static int g_a2_outup = -1;
+static bool a2_outup_env() {
+  if (g_a2_outup < 0) {
+    const char* e = getenv("YOLOSOD_A2_OUTUP");
+    g_a2_outup = (e && e[0] == '1') ? 1 : 0;
+  }
+  return g_a2_outup != 0;
+}
+// Test hook: the fused out-projection + upsample kernel on (1) or off (0); returns the previous state.
+YS_EXPORT int yolosod_debug_set_a2_outup(int on) {
+  const int prev = a2_outup_env() ? 1 : 0;
+  g_a2_outup = on ? 1 : 0;
+  return prev;
+}
+// Column tile of the out / upsample kernel: W itself or a divisor of W that is a multiple of 4 (16-byte pixel quads),
+// with A * wc <= 160 tokens; the widest one that still gives >= 512 workgroups (0: the shape is not fused).
+static int a2_outup_wc(int B, int C, int W, int A) {
+  int best = 0;
+  for (int wc = W; wc >= 4; --wc) {
+    if (W % wc || wc % 4 || A * wc > 160) continue;
+    best = wc;
+    if ((long)B * (C / 32) * (W / wc) >= 512) return wc;
+  }
+  return best;
+}
+bool yolosod_a2_out_up_ok(int B, int C, int H, int W, int A) {
+  return a2_outup_env() && C % 32 == 0 && C <= 1024 && A > 0 && H > 0 && a2_outup_wc(B, C, W, A) > 0;
+}
+// O ([B*L][C], L = A*W) -> y = x + SiLU(up_H(Wf O) + bf). x / y 16-byte aligned. Returns < 0 on error.
+int yolosod_a2_out_up_run(const float* O, const float* wf, const float* bf, const float* x, float* y, int B, int C,
+                          int H, int W, int A, hipStream_t st) {
+  YS_CHECK_ARG(yolosod_a2_out_up_ok(B, C, H, W, A), "a2: out/upsample shape C=%d %dx%d A=%d not fused", C, H, W, A);
+  YS_CHECK_ARG(((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0 && ((uintptr_t)O & 15) == 0 &&
+                   ((uintptr_t)wf & 15) == 0,
+               "a2: out/upsample operands must be 16-byte aligned");
+  const int wc = a2_outup_wc(B, C, W, A);
+  const long nwg = (long)B * (C / 32) * (W / wc);
+  YS_CHECK_ARG(nwg < (1L << 31) && 64L * H * W < (1L << 29), "a2: out/upsample grid too large");
+  const int ntb = (A * wc + 15) / 16;
+#define YS_A2OU(N)                                                                                             \
+  case N:                                                                                                      \
+    hipLaunchKernelGGL((a2f::a2_out_up_kernel<N>), dim3((unsigned)nwg), dim3(256), 0, st, O, wf, bf, x, y, C, \
+                       H, W, A, wc, range_flag_dev());                                                         \
+    break;
+  switch (ntb) {
+    YS_A2OU(1) YS_A2OU(2) YS_A2OU(3) YS_A2OU(4) YS_A2OU(5) YS_A2OU(6) YS_A2OU(7) YS_A2OU(8) YS_A2OU(9) YS_A2OU(10)
+    default: YS_CHECK_ARG(false, "a2: %d tokens per tile unsupported", A * wc);
+  }
+#undef YS_A2OU
+  YS_CHECK_LAUNCH("a2_out_up");
+  return 0;
 }
 
 // LN -> QKV -> attention of all (image, head) pairs: S / stats -> O ([B*L][C]). Returns < 0 on error.

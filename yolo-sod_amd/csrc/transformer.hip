@@ -858,6 +858,9 @@ int yolosod_a2_fused_run(const float* S, const float* stats, float* O, int B, in
 bool yolosod_a2_proj_pool_ok(int C, int H, int W, int A);
 int yolosod_a2_proj_pool_run(const float* x, const float* proj_b, float* S, int B, int C, int H, int W, int A,
                              const void* prep, size_t prep_bytes, hipStream_t st);
+bool yolosod_a2_out_up_ok(int B, int C, int H, int W, int A);
+int yolosod_a2_out_up_run(const float* O, const float* wf, const float* bf, const float* x, float* y, int B, int C,
+                          int H, int W, int A, hipStream_t st);
 
 YS_EXPORT size_t yolosod_a2_workspace(int B, int C, int H, int W, int num_areas) {
   const long ntok = (long)B * num_areas * W;
@@ -993,6 +996,11 @@ static int a2_forward_impl(const float* x, float* y, int B, int C, int H, int W,
     ga.epi.bias = mha_out_b; ga.epi.bias_mode = 2;
     ga.x2 = x2; ga.x2_sb = 64.f;
     if ((rc = launch_gemm(ga, 1, true, st))) return rc;
+  }
+  if (x2 && premul && yolosod_a2_out_up_ok(B, C, H, W, A) && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0 &&
+      ((uintptr_t)oproj_w & 15) == 0) {
+    // out-projection (folded) + upsample + SiLU + residual in one kernel (a2_fused.hip): T never reaches HBM
+    return yolosod_a2_out_up_run(U, oproj_w, oproj_b, x, y, B, C, H, W, A, st);
   }
   // T[img][n][t] = sum_c Wout[n][c] Z[img*AW + t][c]   (reuse S as T: B*C*A*W floats == ntok*C)
   float* T = S;
