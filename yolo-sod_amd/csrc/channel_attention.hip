@@ -666,34 +666,37 @@ __global__ __launch_bounds__(256) void ca_gate_kernel(const float* __restrict__ 
   const int p0 = blockIdx.x * P;
   const int tid = threadIdx.x;
   const float* yb = yin + (long)b * C * L;
-  // staging: 8 loads in flight per thread before their LDS stores (a load-store loop waits for each load in turn:
-  // that alone was ~20 us of L2 round trips per workgroup)
+  // staging: every load unconditional from a clamped index, 8 in flight per thread before their LDS stores (a load
+  // under a predicate merges into a phi whose copy waits for all loads in flight: each load was its own L2 / MALL
+  // round trip)
   constexpr int U = 8;
-  for (int i0 = 0; i0 < C * P; i0 += 256 * U) {
+  const int nys = C * P, nw = mip * C;
+  for (int i0 = 0; i0 < nys; i0 += 256 * U) {
     float v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int i = i0 + tid + 256 * u, c = i / P, pp = i % P;
-      v[u] = (i < C * P && p0 + pp < L) ? yb[(long)c * L + p0 + pp] : 0.f;
+      const int i = min(i0 + tid + 256 * u, nys - 1), c = i / P, pp = i % P;
+      v[u] = yb[(long)c * L + min(p0 + pp, L - 1)];
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u)
-      if (i0 + tid + 256 * u < C * P) ys[i0 + tid + 256 * u] = v[u];
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + tid + 256 * u;
+      if (i < nys) ys[i] = (p0 + i % P < L) ? v[u] : 0.f;
+    }
   }
-  for (int i0 = 0; i0 < mip * C; i0 += 256 * U) {
+  for (int i0 = 0; i0 < nw; i0 += 256 * U) {
     float v[U], a[U], c_[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int i = i0 + tid + 256 * u;
-      const bool ok = i < mip * C;
-      v[u] = ok ? w1[i] : 0.f;
-      a[u] = ok ? wh[i] : 0.f;
-      c_[u] = ok ? ww[i] : 0.f;
+      const int i = min(i0 + tid + 256 * u, nw - 1);
+      v[u] = w1[i];
+      a[u] = wh[i];
+      c_[u] = ww[i];
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int i = i0 + tid + 256 * u;
-      if (i < mip * C) {
+      if (i < nw) {
         w1s[(i / C) * (C + 1) + i % C] = v[u];
         whs[i] = a[u];
         wws[i] = c_[u];
@@ -704,8 +707,15 @@ __global__ __launch_bounds__(256) void ca_gate_kernel(const float* __restrict__ 
   for (int o = tid; o < P * mip; o += 256) {
     const int pp = o / mip, j = o % mip;
     const float* wr = w1s + j * (C + 1);
-    float acc = 0.f;
-    for (int c = 0; c < C; ++c) acc += wr[c] * ys[c * P + pp];
+    // four independent partial sums (one dependent chain of C FMAs through LDS reads was the kernel's critical path)
+    float acc4[4] = {0.f, 0.f, 0.f, 0.f};
+    int c = 0;
+    for (; c + 4 <= C; c += 4) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc4[u] = fmaf(wr[c + u], ys[(c + u) * P + pp], acc4[u]);
+    }
+    for (; c < C; ++c) acc4[0] = fmaf(wr[c], ys[c * P + pp], acc4[0]);
+    const float acc = (acc4[0] + acc4[1]) + (acc4[2] + acc4[3]);
     float z = acc + b1[j];
     const float inv = 1.0f / sqrtf(bn_v[j] + bn_eps);
     z = (z - bn_m[j]) * inv * bn_w[j] + bn_b[j];

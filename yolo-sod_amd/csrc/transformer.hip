@@ -526,6 +526,36 @@ __global__ __launch_bounds__(256) void a2_upsample_out4_kernel(const float* __re
   *reinterpret_cast<f32x4*>(y + o) = r;
 }
 
+// The same tail when W % 4 == 0: a thread's 4 pixels are 4 columns of one row, so the two T rows it interpolates are
+// read as two 16-byte loads (the general form above loads 8 scalars, each its own L2 round trip) and the row's
+// interpolation weights are computed once. grid = ceil(planes * H*W / 1024).
+__global__ __launch_bounds__(256) void a2_upsample_out4w_kernel(const float* __restrict__ x, const float* __restrict__ T,
+                                                                const float* __restrict__ bias, float* __restrict__ y,
+                                                                int C, int H, int W, int A, long total4) {
+  const long i4 = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i4 >= total4) return;
+  const long HW = (long)H * W;
+  const long o = i4 * 4;
+  const long pc = o / HW;  // img*C + c
+  const int c = (int)(pc % C);
+  const int e0 = (int)(o - pc * HW);
+  const int h = e0 / W, w = e0 - h * W;
+  const f32x4 xv = *reinterpret_cast<const f32x4*>(x + o);
+  float src = ((float)A / (float)H) * ((float)h + 0.5f) - 0.5f;
+  if (src < 0.f) src = 0.f;
+  const int y0 = (int)src;
+  const int y1 = y0 + ((y0 < A - 1) ? 1 : 0);
+  const float l1 = src - (float)y0, l0 = 1.0f - l1;
+  const float* Tp = T + pc * A * W + w;
+  const f32x4 t0 = *reinterpret_cast<const f32x4*>(Tp + y0 * W);
+  const f32x4 t1 = *reinterpret_cast<const f32x4*>(Tp + y1 * W);
+  const float b = bias[c];
+  f32x4 r;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) r[k] = xv[k] + silu_fast_(l0 * t0[k] + l1 * t1[k] + b);
+  *reinterpret_cast<f32x4*>(y + o) = r;
+}
+
 static int gs_blocks(long n) {
   long b = (n + 255) / 256;
   if (b > 4096) b = 4096;
@@ -1009,7 +1039,11 @@ static int a2_forward_impl(const float* x, float* y, int B, int C, int H, int W,
   ga.epi = epi_plain(T, (long)C * A * W, A * W);
   ga.x2 = x2; ga.x2_sa = 64.f;
   if ((rc = launch_gemm(ga, B, true, st))) return rc;
-  if (HW % 4 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0) {
+  if (W % 4 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0) {
+    const long total4 = (long)B * C * HW / 4;
+    hipLaunchKernelGGL(a2_upsample_out4w_kernel, dim3((unsigned)((total4 + 255) / 256)), dim3(256), 0, st, x, T,
+                       oproj_b, y, C, H, W, A, total4);
+  } else if (HW % 4 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0) {
     const long total4 = (long)B * C * HW / 4;
     hipLaunchKernelGGL(a2_upsample_out4_kernel, dim3((unsigned)((total4 + 255) / 256)), dim3(256), 0, st, x, T, oproj_b,
                        y, C, H, W, A, total4);
