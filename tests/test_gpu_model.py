@@ -218,21 +218,24 @@ def test_fusion_v5_model_matches_reference_and_oracle(cuda):
 
 
 def test_executor_streams_and_concat_elision_are_bit_identical(gpu_model, cuda):
-    """The GPU executor's side-stream Detect towers and concat elision move data and reorder launches only: the
-    output equals the plain one-stream, torch.cat forward bit for bit (tasks.py _predict_once_planned).
+    """The GPU executor's side-stream Detect towers (dealt to three side streams, or all on one) and concat elision
+    move data and reorder launches only: the output equals the plain one-stream, torch.cat forward bit for bit
+    (tasks.py _predict_once_planned).
     MIOpen's split-K conv solvers accumulate with atomics (run-to-run differences ~5e-5 in the backbone), so the
     comparison runs with torch.backends.cudnn.deterministic (every HIP kernel of this library is deterministic)."""
     from yolosod_amd.nn import tasks
     g = torch.Generator().manual_seed(5)
     x = torch.rand(4, 3, 320, 320, generator=g).to(cuda)
-    saved = tasks.STREAMS
+    saved, saved_side = tasks.STREAMS, tasks.SIDE_STREAMS
     det = torch.backends.cudnn.deterministic
     torch.backends.cudnn.deterministic = True
     try:
         with torch.inference_mode():
             tasks.STREAMS = 1
-            y_streams = gpu_model(x)[0].clone()
+            y_streams = gpu_model(x)[0].clone()  # towers dealt to SIDE_STREAMS (3) side streams
             assert gpu_model._last_elided == 6
+            tasks.SIDE_STREAMS = 1
+            y_side1 = gpu_model(x)[0].clone()
             tasks.STREAMS = 0
             y_one = gpu_model(x)[0].clone()
             gpu_model._fused = False  # plain executor: torch.cat, one stream
@@ -241,8 +244,9 @@ def test_executor_streams_and_concat_elision_are_bit_identical(gpu_model, cuda):
             finally:
                 gpu_model._fused = True
     finally:
-        tasks.STREAMS = saved
+        tasks.STREAMS, tasks.SIDE_STREAMS = saved, saved_side
         torch.backends.cudnn.deterministic = det
     torch.cuda.synchronize()
+    assert torch.equal(y_streams, y_side1)
     assert torch.equal(y_streams, y_one)
     assert torch.equal(y_one, y_plain)

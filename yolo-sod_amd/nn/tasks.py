@@ -41,6 +41,11 @@ CFG_DIR = Path(__file__).resolve().parent.parent / "cfg"
 # moved time between the two streams: m640 1636 vs 1634 img/s same-box, CA 0.33 vs 0.12 ms on the main stream)
 _STREAMS_ENV = os.environ.get("YOLOSOD_STREAMS")
 STREAMS = int(_STREAMS_ENV) if _STREAMS_ENV is not None else 1
+# side streams the towers are dealt to, one tower (box or class, per level) at a time, round robin. With one side
+# stream every level's towers queued behind P2's (3.4 ms of 160x160 convs at n640): the P4 / P5 towers ran after the
+# neck had finished, one small conv at a time, and the main stream idled ~0.65 ms per step before the head. Three
+# side streams + main = the box's 4 hardware queues (GPU_MAX_HW_QUEUES); more would share queues.
+SIDE_STREAMS = max(1, int(os.environ.get("YOLOSOD_SIDE_STREAMS", "3")))
 # the neck's nearest 2x upsample into its Concat slice as one HIP pass (YOLOSOD_UPSAMPLE_HIP=0: PyTorch's strided
 # copy, for A/B)
 UPSAMPLE_HIP = os.environ.get("YOLOSOD_UPSAMPLE_HIP", "1") != "0"
@@ -235,9 +240,10 @@ class BaseModel(nn.Module):
             last_mafn = max((k for k, mm in enumerate(self.model)
                              if isinstance(mm, (M.SE, M.CBAM_Block, M.CA_Block, M.A2_Attn, M.SwinBlock))), default=-1)
             main = torch.cuda.current_stream(x.device)
-            side = getattr(self, "_side_stream", None)
-            if side is None or side.device != x.device:
-                side = self._side_stream = torch.cuda.Stream(device=x.device)
+            side = getattr(self, "_side_streams", None)
+            if side is None or len(side) != SIDE_STREAMS or side[0].device != x.device:
+                side = self._side_streams = [torch.cuda.Stream(device=x.device) for _ in range(SIDE_STREAMS)]
+            rr = 0  # next side stream (round robin over towers)
         y = []
         pend = {}  # concat index -> (buffer, channel offset of each input)
         elided = 0
@@ -282,7 +288,8 @@ class BaseModel(nn.Module):
                         buf[:, o:o + n].copy_(y[j])
                 x = buf
             elif m is det and towers is not None and len(towers) == det.nl:
-                main.wait_stream(side)  # every level's tower features are ready (and owned by main from here)
+                for sd in side:  # every level's tower features are ready (and owned by main from here)
+                    main.wait_stream(sd)
                 x = det.forward_towers([towers[k] for k in range(det.nl)])
             else:
                 x = m(inp)
@@ -292,14 +299,18 @@ class BaseModel(nn.Module):
                 if m.i in lvl:
                     ready.append((lvl[m.i], x))
                 if ready and (streams != 2 or m.i >= last_mafn):
-                    side.wait_stream(main)
                     for k, xk in ready:
-                        xk.record_stream(side)
-                        with torch.cuda.stream(side):
-                            fb, fc = det.tower_features(k, xk)
-                        fb.record_stream(main)
-                        fc.record_stream(main)
-                        towers[k] = (fb, fc)
+                        feats = []
+                        for tower in (det.cv2[k], det.cv3[k]):  # box, class tower (Detect.tower_features)
+                            sd = side[rr % len(side)]
+                            rr += 1
+                            sd.wait_stream(main)
+                            xk.record_stream(sd)
+                            with torch.cuda.stream(sd):
+                                f = tower[:-1](xk).contiguous()
+                            f.record_stream(main)
+                            feats.append(f)
+                        towers[k] = tuple(feats)
                     ready = []
             y.append(x if m.i in self.save else None)
         self._last_elided = elided
