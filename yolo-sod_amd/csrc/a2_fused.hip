@@ -406,7 +406,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void a2_proj_pool_kernel(
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           uint2 hh, ll;
-          split4(col[j], hh, ll);
+          split4x(col[j], hh, ll);  // loaded x: the 3-VALU split (common.h split2x)
           rng = range_acc(rng, col[j]);
           h16_t* d = Pl + (buf * 2) * PPL + (4 * pq + j) * PPS + 4 * kq;
           *reinterpret_cast<uint2*>(d) = hh;
@@ -583,7 +583,7 @@ __global__ __launch_bounds__(512, 1) void a2_proj_pool_wide_kernel(const float* 
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           uint2 hh, ll;
-          split4(col[j], hh, ll);
+          split4x(col[j], hh, ll);  // loaded x: the 3-VALU split (common.h split2x)
           rng = range_acc(rng, col[j]);
           h16_t* d = Pl + (buf * 2) * PPL + (4 * pq + j) * PPS + 4 * kq;
           *reinterpret_cast<uint2*>(d) = hh;

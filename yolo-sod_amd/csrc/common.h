@@ -208,6 +208,35 @@ __device__ __forceinline__ void split4(f32x4 v, uint2& h, uint2& l) {
   split2(f32x2{v.x, v.y}, h.x, l.x);
   split2(f32x2{v.z, v.w}, h.y, l.y);
 }
+// The same split for values loaded from memory (no producing arithmetic the compiler could contract into the
+// subtraction): the low terms as v_fma_mixlo_f16 / v_fma_mixhi_f16 (fma(h, -1, v) of the fp16 half h and the fp32 v,
+// rounded once to fp16), three VALU per pair instead of five, bit-identical to split2 for such values (v - h is exact
+// in fp32). The compiler forms the mixed fma only from a non-constant multiplier (a constant -1 is canonicalised to a
+// subtraction first), so -1 goes through an SGPR behind an empty asm statement, and a second empty statement keeps
+// the SLP vectoriser from fusing the pair's two fmas into one v_pk_fma_f32 (neither statement emits an instruction).
+// Not used on computed operands: there split2's `v - h` may absorb the producer's last multiply (fp-contract) and
+// keep its rounding error in the low term, which the mixed form would drop.
+__device__ __forceinline__ void split2x(f32x2 v, uint32_t& h, uint32_t& l) {
+  const f16x2_t hh = __builtin_convertvector(v, f16x2_t);
+  h = __builtin_bit_cast(uint32_t, hh);
+  float m1 = -1.0f;
+  asm("" : "+s"(m1));
+  _Float16 l0 = (_Float16)__builtin_fmaf((float)hh.x, m1, v.x);
+  asm("" : "+v"(l0));
+  const _Float16 l1 = (_Float16)__builtin_fmaf((float)hh.y, m1, v.y);
+  l = __builtin_bit_cast(uint32_t, f16x2_t{l0, l1});
+}
+__device__ __forceinline__ void split4x(f32x4 v, uint2& h, uint2& l) {
+  split2x(f32x2{v.x, v.y}, h.x, l.x);
+  split2x(f32x2{v.z, v.w}, h.y, l.y);
+}
+__device__ __forceinline__ void split8x(f32x4 a, f32x4 b, f16x8_t& h, f16x8_t& l) {
+  uint2 h0, l0, h1, l1;
+  split4x(a, h0, l0);
+  split4x(b, h1, l1);
+  h = __builtin_bit_cast(f16x8_t, make_uint4(h0.x, h0.y, h1.x, h1.y));
+  l = __builtin_bit_cast(f16x8_t, make_uint4(l0.x, l0.y, l1.x, l1.y));
+}
 // 8 values -> the hi / lo fp16 operands of one v_mfma_f32_16x16x32_f16 k slot group
 __device__ __forceinline__ void split8(f32x4 a, f32x4 b, f16x8_t& h, f16x8_t& l) {
   uint2 h0, l0, h1, l1;

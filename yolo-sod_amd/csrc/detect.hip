@@ -484,7 +484,7 @@ __global__ __launch_bounds__(256, C3 > 64 ? 2 : 3) void detect_head_x2_kernel(He
       f16x8_t fh, fl;
       const f32x4 va{cb[8 * s], cb[8 * s + 1], cb[8 * s + 2], cb[8 * s + 3]};
       const f32x4 vb2{cb[8 * s + 4], cb[8 * s + 5], cb[8 * s + 6], cb[8 * s + 7]};
-      split8(va, vb2, fh, fl);
+      split8x(va, vb2, fh, fl);  // loaded features: the 3-VALU split (common.h split2x)
       rng = range_acc(range_acc(rng, va), vb2);
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
@@ -498,7 +498,7 @@ __global__ __launch_bounds__(256, C3 > 64 ? 2 : 3) void detect_head_x2_kernel(He
       f16x8_t fh, fl;
       const f32x4 va{cc[8 * s], cc[8 * s + 1], cc[8 * s + 2], cc[8 * s + 3]};
       const f32x4 vb2{cc[8 * s + 4], cc[8 * s + 5], cc[8 * s + 6], cc[8 * s + 7]};
-      split8(va, vb2, fh, fl);
+      split8x(va, vb2, fh, fl);  // loaded features: the 3-VALU split (common.h split2x)
       rng = range_acc(range_acc(rng, va), vb2);
       const int o = NBW + s * 512;
       acc[4] = mfma_f16x3(*reinterpret_cast<const f16x8_t*>(wbh + o), *reinterpret_cast<const f16x8_t*>(wbl + o), fh,
