@@ -476,11 +476,59 @@ __global__ __launch_bounds__(256) void cbam_sa_kernel(const float* __restrict__ 
   if (tid < 98) wk[tid] = wsa[tid];
   const int oy = blockIdx.y * 16 - 3, ox = blockIdx.x * 16 - 3;
   const float invC = 1.0f / (float)C;
-  for (int i = tid; i < 22 * 22; i += 256) {
-    const int ty = i / 22, tx = i % 22;
-    const float2 v = cbam_map_at(mpart + (long)b * G * 2 * HW, G, HW, H, W, oy + ty, ox + tx, invC);
-    mm[0][ty][tx] = v.x;
-    mm[1][ty][tx] = v.y;
+  // the thread's two halo positions (484 = 256 + 228): every partial-map load unconditional from a clamped position
+  // (loads under the bounds branch merged into phis, each waiting for all loads in flight), both positions' loads in
+  // flight together; out-of-image positions take the conv's zero padding afterwards. Sums keep their g order.
+  const float* mp = mpart + (long)b * G * 2 * HW;
+  int q[2];
+  bool in[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int i = min(tid + 256 * k, 22 * 22 - 1), ty = i / 22, tx = i - (i / 22) * 22;
+    const int yy = oy + ty, xx = ox + tx;
+    in[k] = yy >= 0 && yy < H && xx >= 0 && xx < W;
+    q[k] = min(max(yy, 0), H - 1) * W + min(max(xx, 0), W - 1);
+  }
+  float sm[2] = {0.f, 0.f}, mx[2] = {-INFINITY, -INFINITY};
+  int g = 0;
+  for (; g + 4 <= G; g += 4) {
+    float a[2][4], c[2][4];
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a[k][u] = mp[(long)(2 * (g + u)) * HW + q[k]];
+        c[k][u] = mp[(long)(2 * (g + u) + 1) * HW + q[k]];
+      }
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        sm[k] += a[k][u];
+        mx[k] = fmaxf(mx[k], c[k][u]);
+      }
+  }
+  for (; g < G; ++g) {
+    float a[2], c[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      a[k] = mp[(long)(2 * g) * HW + q[k]];
+      c[k] = mp[(long)(2 * g + 1) * HW + q[k]];
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      sm[k] += a[k];
+      mx[k] = fmaxf(mx[k], c[k]);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int i = tid + 256 * k;
+    if (i < 22 * 22) {
+      const int ty = i / 22, tx = i - (i / 22) * 22;
+      mm[0][ty][tx] = in[k] ? sm[k] * invC : 0.f;
+      mm[1][ty][tx] = in[k] ? mx[k] : 0.f;
+    }
   }
   __syncthreads();
   const int ly = tid >> 4, lx = tid & 15;

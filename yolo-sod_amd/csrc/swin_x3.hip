@@ -250,17 +250,23 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
   constexpr int PSV = SWZ ? 64 : 72;    // V^T plane row stride (keys 0..63 (+ 8))
   constexpr int VPL = C * PSV;   // V^T plane stride
   constexpr int NHS = (C + 2) / 3;
+  constexpr int PSH = HID + 8;  // MLP hidden plane row stride (both halves side by side, unswizzled: 272-byte rows put
+                                // the 16 rows of an operand read on distinct bank quads)
+  constexpr int PLH = 64 * PSH;                        // hidden plane stride
+  constexpr int QW_H = 2 * (C / 16) * (C / 32) * 512;  // staged Q weight fragments: [k step][plane][column block][512]
   static_assert(C == 64 && HID / 2 == C, "the plane regions are sized for C = 64 (hidden halves of 64)");
   static_assert(HD == 32, "attention operands: two 16-column blocks per head");
   constexpr int T_B = NR * LT * 4;
   constexpr int KV_B = (2 * VPL + 2 * KPL) * 2;
-  constexpr int PLN_B = 2 * PL * 2;
+  constexpr int PLN_B = 2 * PL * 2 + QW_H * 2;  // U1 planes + all Q weight fragments
+  constexpr int HID_B = 2 * PLH * 2;            // both MLP hidden halves as planes
   constexpr int HALO_B = 3 * NHS * 9 * HPW * 4;
-  constexpr int X_B = KV_B > HALO_B ? (KV_B > PLN_B ? KV_B : PLN_B) : (HALO_B > PLN_B ? HALO_B : PLN_B);
+  constexpr int X_B0 = KV_B > HALO_B ? (KV_B > PLN_B ? KV_B : PLN_B) : (HALO_B > PLN_B ? HALO_B : PLN_B);
+  constexpr int X_B = ((X_B0 > HID_B ? X_B0 : HID_B) + 15) / 16 * 16;
   constexpr int NPAR = 3 * C + C + HID + C + 2 * C;
   static_assert(T_B % 16 == 0 && X_B % 16 == 0, "16-byte aligned regions");
   static_assert(T_B + X_B + NPAR * 4 <= 160 * 1024 / 3, "three workgroups per CU");
-  static_assert(PLN_B + 8 * 512 * 2 <= X_B, "staged Q weight chunk after the U1 planes");
+  static_assert(PLN_B <= X_B && HID_B <= X_B, "staged Q weights after the U1 planes; both hidden halves");
 #ifndef YS_X3_LDS_PAD  // diagnostic builds only: extra LDS per workgroup to measure the kernel at lower occupancy
 #define YS_X3_LDS_PAD 0
 #endif
@@ -332,9 +338,10 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
   float dwk[9];
 #pragma unroll
   for (int i = 0; i < 9; ++i) dwk[i] = p.dw[dw_c * 9 + i];
-  // The Q weight planes (rows 0..C of in_proj) are staged once per workgroup through X in two 32-k chunks (every
-  // wave needs all of them for its own 16 queries; streamed per wave they were 4x the Q bytes from L2): this
-  // thread's 32 bytes of both chunks are in flight during the halo store, the dw conv and LN1
+  // The Q weight planes (rows 0..C of in_proj) are staged once per workgroup through X, both 32-k chunks at once
+  // behind the U1 planes (every wave needs all of them for its own 16 queries; streamed per wave they were 4x the Q
+  // bytes from L2; staged one chunk at a time they cost two more barriers): this thread's 32 bytes of both chunks
+  // are in flight during the halo store, the dw conv and LN1
   // chunk s = the fragment blocks (plane, Q column block cq) of k step s: 8 blocks of 512 halves; thread t copies
   // halves 16 (t & 31) .. +15 of block t >> 5
   const int qblk = tid >> 5, qpl = qblk >> 2, qcb = qblk & 3;
@@ -414,10 +421,12 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
 
   // ---- LN1 -> X planes; Q weight chunk 0 -> X after the U1 planes (the halo there has been read) ----
   ln_planes<C, LT, PS, PL, SWZ>(T, P, p.ln1_eps, tid);
-  h16_t* QW = P + 2 * PL;  // [2 plane][4 column block][64 lanes][8]
+  h16_t* QW = P + 2 * PL;  // [2 k step][2 plane][4 column block][64 lanes][8]
   h16_t* qdst = QW + qblk * 512 + 16 * (tid & 31);
   *reinterpret_cast<uint4*>(qdst) = qc0a;
   *reinterpret_cast<uint4*>(qdst + 8) = qc0b;
+  *reinterpret_cast<uint4*>(qdst + 4096) = qc1a;
+  *reinterpret_cast<uint4*>(qdst + 4104) = qc1b;
   WP<C, 1> f_q;  // K weight planes of column block wid
   load_wp(p.win, 3 * C, C, 0, C / 16 + wid, f_q, lane);
   __syncthreads();
@@ -446,15 +455,7 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
     static_assert(C == 64, "two 32-k chunks");
 #pragma unroll
     for (int s2 = 0; s2 < C / 32; ++s2) {
-      if (s2 == 1) {
-        __syncthreads();  // every wave has read chunk 0
-        X3_STAMP(4);
-        *reinterpret_cast<uint4*>(qdst) = qc1a;
-        *reinterpret_cast<uint4*>(qdst + 8) = qc1b;
-        __syncthreads();
-        X3_STAMP(5);
-      }
-      const h16_t* wq = QW + lane * 8;
+      const h16_t* wq = QW + s2 * 4096 + lane * 8;
 #pragma unroll
       for (int cq = 0; cq < C / 16; ++cq)
         qa[cq] = mfma_f16x3(*reinterpret_cast<const f16x8_t*>(wq + cq * 512),
@@ -698,21 +699,22 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
 #pragma unroll
     for (int rb = 0; rb < 4; ++rb) acc2[rb][0] = b;
   }
+  // both hidden halves as planes side by side [64][PSH] (one store, one barrier), then MLP2 over k in [0, 128)
+  __syncthreads();  // every wave has read X (U2)
+  X3_STAMP(12);
 #pragma unroll
-  for (int half = 0; half < 2; ++half) {
-    __syncthreads();  // every wave has read X (U2, then hidden half 0)
-    X3_STAMP(12 + 2 * half);
+  for (int half = 0; half < 2; ++half)
 #pragma unroll
     for (int rb = 0; rb < 4; ++rb) {
-      store_planes4<PS, PL, SWZ>(P, rb * 16 + l15, wid * 16 + 4 * g, hid[half][rb]);
+      store_planes4<PSH, PLH>(P, rb * 16 + l15, 64 * half + wid * 16 + 4 * g, hid[half][rb]);
       rng = range_acc(rng, hid[half][rb]);
     }
-    __syncthreads();
-    X3_STAMP(13 + 2 * half);
+  __syncthreads();
+  X3_STAMP(13);
 #ifndef YS_ABL_MLPMFMA
-    gemm_x3<C, 1, PS, PL, false, SWZ>(P, half == 0 ? f_2a : f_2b, acc2, lane);
+  gemm_x3<C, 1, PSH, PLH>(P, f_2a, acc2, lane);
+  gemm_x3<C, 1, PSH, PLH>(P + 64, f_2b, acc2, lane);  // hidden columns 64..127
 #endif
-  }
 
   // pw planes and this lane's residual x / BN terms: in flight during the final T update
   WP<C, 1> f_pw;
@@ -734,7 +736,7 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
       xr[tb][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, vtok[tb], r * HWi * 4, 0));
 
   // ---- final T = T + MLP -> X planes (rows >= 49 zero): the pw GEMM's operand ----
-  __syncthreads();  // every wave has read hidden half 1
+  __syncthreads();  // every wave has read the hidden planes
   X3_STAMP(16);
 #pragma unroll
   for (int rb = 0; rb < 4; ++rb) {
