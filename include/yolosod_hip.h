@@ -195,6 +195,16 @@ int yolosod_bias_act_dual(const float* y, long y_bstride, float* out, long out_b
                           const float* res, long res_bstride, float* out2, long out2_bstride, int c2lo, int B, int C,
                           long HW, int act, void* stream);
 
+/* Detect head tower conv (ultralytics/nn/modules/head.py:43-57, conv.py:37-55): 3x3 / stride 1 /
+ * pad 1 conv with 64 outputs + folded-BN bias + SiLU, fp32 NCHW in and out, as an implicit GEMM on fp16 two-term
+ * split MFMA (csrc/conv3x3.hip). Replaces torch.nn.functional.conv2d (MIOpen) + the bias / SiLU epilogue for those
+ * convs. Cin a multiple of 32 (<= 2048). The weights [64][Cin][3][3] are prepared once per version into a caller-
+ * owned block of yolosod_conv3x3_prep_bytes(Cin) bytes (0: unsupported Cin). */
+size_t yolosod_conv3x3_prep_bytes(int cin);
+int yolosod_conv3x3_prepare(const float* w, int cin, void* prep, size_t prep_bytes, void* stream);
+int yolosod_conv3x3_silu(const float* x, float* y, int B, int cin, int H, int W, const float* bias, const void* prep,
+                         size_t prep_bytes, void* stream);
+
 /* Thin fused 1x1 convolution of the backbone (conv.py:37-55 after fuse(), 1x1 case): out = SiLU(W x + bias) (+ res)
  * for Cout in {64, 128}, Cin in {64, 96, 128, 192, 256}, HW % 64 == 0; x / out / res may be channel slices (batch
  * strides, multiples of 4); out2 (optional, NULL) = packed copy of channels [c2lo, Cout). Other shapes: error. */

@@ -63,6 +63,9 @@ SIGNATURES = {
     "yolosod_se_forward_pre": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _i, _vp, _vp, _sz, _vp]),
     "yolosod_cbam_forward_pre": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _vp, _sz, _vp]),
     "yolosod_conv1x1": (_i, [_vp, _l, _vp, _vp, _vp, _l, _vp, _l, _i, _i, _i, _l, _i, _vp]),
+    "yolosod_conv3x3_prep_bytes": (_sz, [_i]),
+    "yolosod_conv3x3_prepare": (_i, [_vp, _i, _vp, _sz, _vp]),
+    "yolosod_conv3x3_silu": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _sz, _vp]),
     "yolosod_debug_set_swin_fused": (None, [_i]),
     "yolosod_debug_set_swin_x3": (_i, [_i]),
     "yolosod_debug_set_head_x2": (_i, [_i]),
@@ -687,6 +690,45 @@ def conv1x1(x, w, bias, act, out=None, res=None):
                                out.data_ptr(), ob, None if res is None else res.data_ptr(), rb, B, Cin, Cout, HW,
                                int(act), _stream(x.device)), "conv1x1")
     return out
+
+
+def conv3x3_ok(x, conv) -> bool:
+    """Shapes the fp16-split 3x3 conv kernel takes (yolosod_conv3x3_silu): fp32 contiguous NCHW on a GPU, 3x3 /
+    stride 1 / pad 1 / dilation 1 / groups 1, 64 outputs, Cin a multiple of 32."""
+    return (x.device.type == "cuda" and x.dtype == torch.float32 and x.is_contiguous() and x.dim() == 4
+            and conv.kernel_size == (3, 3) and conv.stride == (1, 1) and conv.padding == (1, 1)
+            and conv.dilation == (1, 1) and conv.groups == 1 and conv.out_channels == 64
+            and conv.in_channels % 32 == 0 and x.shape[1] == conv.in_channels
+            and int(load_library().yolosod_conv3x3_prep_bytes(int(conv.in_channels))) > 0)
+
+
+def conv3x3_prepare(w):
+    """Prepared block (fragment-major fp16 split planes of 64 W, uint8 tensor) of a [64, Cin, 3, 3] fp32 weight."""
+    lib = load_library()
+    cin = int(w.shape[1])
+    nbytes = int(lib.yolosod_conv3x3_prep_bytes(cin))
+    blk = torch.empty(nbytes, dtype=torch.uint8, device=w.device)
+    wc = w.detach().float().contiguous()
+    _check(_launch(("conv3x3_prep", (64, cin), None), w.device, lib.yolosod_conv3x3_prepare, _dev(wc, "weight"), cin,
+                   blk.data_ptr(), nbytes, _stream(w.device)), "conv3x3_prepare")
+    return blk
+
+
+def conv3x3_silu(x, bias, prep):
+    """SiLU(conv3x3(x) + bias) with 64 outputs on the fp16 two-term split MFMA (csrc/conv3x3.hip); ``prep`` is a
+    callable returning the cached prepared block of the weights (conv3x3_prepare)."""
+    lib = load_library()
+    B, Cin, H, W = x.shape
+    y = torch.empty((B, 64, H, W), dtype=torch.float32, device=x.device)
+    b = bias.detach().float().contiguous()
+
+    def run():
+        blk = prep()
+        return lib.yolosod_conv3x3_silu(_dev(x, "x"), y.data_ptr(), B, Cin, H, W, _dev(b, "bias"), blk.data_ptr(),
+                                        blk.numel(), _stream(x.device))
+
+    _check(_launch(("conv3x3", tuple(x.shape), 64), x.device, run), "conv3x3")
+    return y
 
 
 def gemm_f32(A, B, b_kcontig, bias=None, bias_mode=0, act=0, res=None):

@@ -1,0 +1,261 @@
+// 3x3 convolution (stride 1, pad 1, 64 output channels) + folded BN bias + SiLU as an implicit GEMM on the fp16
+// matrix cores at fp32 accuracy: the Detect head's conv towers (ultralytics/nn/modules/head.py:
+// 43-57: cv2[i] = Conv(c, c2, 3), Conv(c2, c2, 3); cv3[i] = Conv(c, c3, 3), Conv(c3, c3, 3) with c2 = c3 = 64 for the
+// paper model). Each Conv is conv2d (no bias) -> BN (folded into weight / bias by fuse(), torch_utils.py:238-265) ->
+// SiLU (conv.py:37-55).
+//
+// Method (the two-term split of swin_x3.hip): v = h + l with h = fp16(v), l = fp16(v - h); a product is
+// ah.bh + ah.bl + al.bh on v_mfma_f32_16x16x32_f16 with fp32 accumulation. Weights are split once per parameter
+// version by conv3x3_prep_kernel (x 64, exact, so their low terms stay normal fp16) into fragment-major planes:
+// for tap t, 32-channel input chunk q, 16-row output block rb and plane p, the 64 lanes' A fragments (lane (g, l15):
+// output channel 16 rb + l15, input channels 32 q + 8 g .. + 7) are 1 KB contiguous.
+//
+// One 256-thread workgroup per (image, 8 x 32 output tile), all 64 output channels, two workgroups per CU: per input
+// chunk, the tile's 10 x 34 input halo (zero padding outside the image) is loaded, split and stored once as two fp16
+// planes [pixel][32] in LDS; the nine taps read their B fragments (8 channels of one halo pixel per lane) at
+// tap-shifted pixel offsets of the same planes, so every input value is split once per workgroup and reused by
+// 9 taps x 64 outputs. Wave w computes output rows 4 (w >> 1) .. + 3 (eight 16-pixel column blocks) for the output
+// row blocks 2 (w & 1), 2 (w & 1) + 1: 16 accumulator tiles from 4 weight fragments (L2, one tap ahead) and 16 pixel
+// fragments (LDS) per tap. The next chunk's halo is loaded into registers while the current chunk computes.
+#include "common.h"
+
+namespace ys {
+namespace c3 {
+
+constexpr float WSC = 64.0f;
+constexpr int TH = 8, TW = 32;              // output tile
+constexpr int HH = TH + 2, HW_ = TW + 2;    // halo tile
+constexpr int NPXH = HH * HW_;              // 340 halo pixels
+constexpr int PS = 32 + 8;                  // plane row stride (halves): 80-byte pixel rows
+constexpr int PL = NPXH * PS;               // plane (halves)
+constexpr int NQUAD = NPXH * 8;             // staged items per chunk: (4-channel quad, halo pixel)
+constexpr int NT = 256;
+constexpr int NIT = (NQUAD + NT - 1) / NT;  // 11
+
+struct Args {
+  const float* x;      // [B][Cin][H][W]
+  const h16_t* wp;     // prepared planes (fragment-major, x 64)
+  const float* bias;   // [64]
+  float* y;            // [B][64][H][W]
+  int cin, H, W, tiles_x, tiles_y;
+  unsigned* range_flag;
+  const unsigned* prep_flag;
+};
+
+__global__ __launch_bounds__(256, 2) void conv3x3_x2_kernel(Args p) {
+  __shared__ __attribute__((aligned(16))) h16_t Pl[2 * PL];
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l15 = lane & 15, g = lane >> 4;
+  const int t_lin = blockIdx.x;
+  const int tx = t_lin % p.tiles_x, ty = (t_lin / p.tiles_x) % p.tiles_y, b = t_lin / (p.tiles_x * p.tiles_y);
+  const int H = p.H, W = p.W, HWi = H * W;
+  const int x0 = tx * TW - 1, y0 = ty * TH - 1;  // halo origin
+  const int nq = p.cin >> 5;
+  const float* xb = p.x + (long)b * p.cin * HWi;
+  float rng = 0.f;
+
+  // staging item e: quad = e / NPXH (channels 4 quad .. + 3 of the chunk), halo pixel e % NPXH; consecutive threads
+  // take consecutive pixels (coalesced rows). Out-of-image pixels load a clamped in-image address (unconditional
+  // loads) and store zeros. Buffer loads: 32-bit per-lane offsets, the channel / chunk offsets in the scalar offset.
+  auto rsrc = [&](const void* base, unsigned bytes) {
+    const unsigned long long a = (unsigned long long)base;
+    return __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(a >> 32)) << 32) |
+                (unsigned)__builtin_amdgcn_readfirstlane((unsigned)a)),
+        (short)0, __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+  };
+  const __amdgpu_buffer_rsrc_t rx = rsrc(xb, (unsigned)((long)p.cin * HWi * 4));
+  const __amdgpu_buffer_rsrc_t rw = rsrc(p.wp, (unsigned)(9L * nq * 8 * 1024));
+  unsigned voff[NIT];
+  bool okp[NIT];
+#pragma unroll
+  for (int i = 0; i < NIT; ++i) {
+    const int e = min(tid + NT * i, NQUAD - 1);
+    const int quad = e / NPXH, px = e - quad * NPXH;
+    const int hy = px / HW_, hx = px - hy * HW_;
+    const int yy = y0 + hy, xx = x0 + hx;
+    okp[i] = yy >= 0 && yy < H && xx >= 0 && xx < W;
+    voff[i] = (unsigned)(((4 * quad) * HWi + min(max(yy, 0), H - 1) * W + min(max(xx, 0), W - 1)) * 4);
+  }
+  f32x4 sv[NIT];
+  auto load_chunk = [&](int q) __attribute__((always_inline)) {
+    const int sx = __builtin_amdgcn_readfirstlane(32 * q * HWi * 4);
+#pragma unroll
+    for (int i = 0; i < NIT; ++i)
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        sv[i][c] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, voff[i], sx + c * HWi * 4, 0));
+  };
+  auto store_chunk = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) {
+      const int e = tid + NT * i;
+      if (e < NQUAD) {
+        const int quad = e / NPXH, px = e - quad * NPXH;
+        const f32x4 v = okp[i] ? sv[i] : f32x4{0.f, 0.f, 0.f, 0.f};
+        uint2 hh, ll;
+        split4x(v, hh, ll);
+        rng = range_acc(rng, v);
+        h16_t* d = Pl + px * PS + 4 * quad;
+        *reinterpret_cast<uint2*>(d) = hh;
+        *reinterpret_cast<uint2*>(d + PL) = ll;
+      }
+    }
+  };
+  // this wave: output row blocks 2 rp, 2 rp + 1 (channels 32 rp ..), pixel rows 4 ph .. 4 ph + 3; B-fragment pixel of
+  // column block cb at tap (0, 0): output row 4 ph + (cb >> 1), column (cb & 1) 16 + l15
+  const int rp = wid & 1, ph = wid >> 1;
+  int bpx[8];
+#pragma unroll
+  for (int cb = 0; cb < 8; ++cb) bpx[cb] = (4 * ph + (cb >> 1)) * HW_ + (cb & 1) * 16 + l15;
+  // A fragments of (tap t, chunk q): this wave's row blocks 2 rp + r (r = 0, 1), planes 0 / 1; tap t's fragments of
+  // chunk q start at byte ((t nq + q) 8) KB, [row block][plane][lane][16 bytes]
+  auto wfrag = [&](int t, int q, int r, int pl) __attribute__((always_inline)) {
+    const int st = __builtin_amdgcn_readfirstlane(((t * nq + q) * 8) * 1024);
+    return __builtin_bit_cast(f16x8_t, __builtin_amdgcn_raw_buffer_load_b128(
+                                           rw, (unsigned)((((2 * rp + r) * 2 + pl) * 64 + lane) * 16), st, 0));
+  };
+  f32x4 acc[2][8];
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int cb = 0; cb < 8; ++cb) acc[r][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  load_chunk(0);
+  for (int q = 0; q < nq; ++q) {
+    __syncthreads();  // every wave is done with the previous chunk's planes
+    store_chunk();
+    __syncthreads();
+    // the next chunk's loads in flight during this chunk's products; unconditional (the last chunk reloads itself):
+    // loads under a branch merge into phis whose copies wait for every load in flight
+    load_chunk(q + 1 < nq ? q + 1 : q);
+    f16x8_t wa[2][2], wn[2][2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      wa[r][0] = wfrag(0, q, r, 0);
+      wa[r][1] = wfrag(0, q, r, 1);
+    }
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int tn = t + 1 < 9 ? t + 1 : t;  // one tap ahead (unconditional)
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        wn[r][0] = wfrag(tn, q, r, 0);
+        wn[r][1] = wfrag(tn, q, r, 1);
+      }
+      const int toff = (t / 3) * HW_ + (t % 3);
+#pragma unroll
+      for (int cb = 0; cb < 8; ++cb) {
+        const h16_t* src = Pl + (bpx[cb] + toff) * PS + 8 * g;
+        const f16x8_t xh = *reinterpret_cast<const f16x8_t*>(src);
+        const f16x8_t xlo = *reinterpret_cast<const f16x8_t*>(src + PL);
+#pragma unroll
+        for (int r = 0; r < 2; ++r) acc[r][cb] = mfma_f16x3(wa[r][0], wa[r][1], xh, xlo, acc[r][cb]);
+      }
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        wa[r][0] = wn[r][0];
+        wa[r][1] = wn[r][1];
+      }
+    }
+  }
+  // epilogue: lane (g, l15) of (r, cb) holds output channel 16 (2 rp + r) + 4 g + j, pixel (row 4 ph + (cb >> 1),
+  // column (cb & 1) 16 + l15) of the tile. SiLU on the hardware exp2 / rcp (~2^-22 relative, below the split
+  // products' own few-ulp error)
+  float* yb = p.y + (long)b * 64 * HWi;
+#pragma unroll
+  for (int cb = 0; cb < 8; ++cb) {
+    const int oy = ty * TH + 4 * ph + (cb >> 1), ox = tx * TW + (cb & 1) * 16 + l15;
+    if (oy < H && ox < W) {
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        const int c0 = 16 * (2 * rp + r) + 4 * g;
+        const f32x4 bv = *reinterpret_cast<const f32x4*>(p.bias + c0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) yb[(c0 + j) * HWi + oy * W + ox] = silu_fast_(acc[r][cb][j] * (1.0f / WSC) + bv[j]);
+      }
+    }
+  }
+  range_report(p.range_flag, rng);
+  if (p.prep_flag && p.range_flag && blockIdx.x == 0 && threadIdx.x == 0 && *p.prep_flag) *p.range_flag = 1u;
+}
+
+// W [64][Cin][3][3] -> fragment-major planes of 64 W (see the file comment); one thread per (output channel, input
+// channel, tap). The block's own range word records whether 64 W left fp16's range (re-reported by every launch).
+__global__ __launch_bounds__(256) void conv3x3_prep_kernel(const float* __restrict__ w, int cin, h16_t* __restrict__ wp,
+                                                           unsigned* range_flag, unsigned* prep_flag) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  const long n_all = 64L * cin * 9;
+  if (i >= n_all) return;
+  const int t = (int)(i % 9), k = (int)((i / 9) % cin), n = (int)(i / (9L * cin));
+  const float v = w[i] * WSC;
+  const _Float16 hh = (_Float16)v;
+  const _Float16 ll = (_Float16)(v - (float)hh);
+  const int nq = cin >> 5, q = k >> 5, kk = k & 31, rb = n >> 4;
+  const int ln = ((kk >> 3) << 4) + (n & 15);
+  const long base = ((long)((t * nq + q) * 4 + rb) * 2) * 512 + ln * 8 + (kk & 7);
+  wp[base] = __builtin_bit_cast(h16_t, hh);
+  wp[base + 512] = __builtin_bit_cast(h16_t, ll);
+  const float m = fabsf(v);
+  range_report(range_flag, m);
+  range_report(prep_flag, m);
+}
+
+}  // namespace c3
+}  // namespace ys
+
+using namespace ys;
+
+// 3x3 / stride 1 / pad 1 conv with 64 outputs: Cin a multiple of 32 (<= 2048)
+YS_EXPORT size_t yolosod_conv3x3_prep_bytes(int cin) {
+  if (cin <= 0 || cin % 32 || cin > 2048) return 0;
+  Sizer s;
+  s.take<h16_t>((size_t)2 * 64 * cin * 9);
+  s.take<unsigned>(1);
+  return s.off;
+}
+
+static bool conv3x3_carve(void* buf, size_t bytes, int cin, h16_t** wp, unsigned** flag) {
+  Carver cv(buf, bytes);
+  *wp = cv.take<h16_t>((size_t)2 * 64 * cin * 9);
+  *flag = cv.take<unsigned>(1);
+  return *flag != nullptr;
+}
+
+// Weight preparation (re-run whenever the weights change): w [64][cin][3][3] fp32 (BN folded) -> prep block.
+YS_EXPORT int yolosod_conv3x3_prepare(const float* w, int cin, void* prep, size_t prep_bytes, void* stream) {
+  YS_CHECK_ARG(w && prep, "conv3x3_prepare: null pointer");
+  YS_CHECK_ARG(yolosod_conv3x3_prep_bytes(cin) > 0, "conv3x3_prepare: cin=%d unsupported (multiple of 32)", cin);
+  h16_t* wp;
+  unsigned* flag;
+  YS_CHECK_ARG(conv3x3_carve(prep, prep_bytes, cin, &wp, &flag), "conv3x3_prepare: block too small (%zu)", prep_bytes);
+  hipStream_t st = (hipStream_t)stream;
+  if (hipMemsetAsync(flag, 0, sizeof(unsigned), st) != hipSuccess) {
+    set_error("conv3x3_prepare: flag reset failed");
+    return -1;
+  }
+  const long n = 64L * cin * 9;
+  hipLaunchKernelGGL(c3::conv3x3_prep_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, w, cin, wp,
+                     range_flag_dev(), flag);
+  YS_CHECK_LAUNCH("conv3x3_prep");
+  return 0;
+}
+
+// y = SiLU(conv3x3(x, W) + bias), x [B][cin][H][W] -> y [B][64][H][W] (fp32, contiguous; y must not alias x).
+YS_EXPORT int yolosod_conv3x3_silu(const float* x, float* y, int B, int cin, int H, int W, const float* bias,
+                                   const void* prep, size_t prep_bytes, void* stream) {
+  YS_CHECK_ARG(x && y && bias && prep, "conv3x3: null pointer");
+  YS_CHECK_ARG(B >= 0 && H > 0 && W > 0 && yolosod_conv3x3_prep_bytes(cin) > 0, "conv3x3: bad shape");
+  YS_CHECK_ARG((long)cin * H * W < (1L << 31) && 64L * H * W < (1L << 31), "conv3x3: plane too large");
+  YS_CHECK_ARG(((uintptr_t)bias & 15) == 0, "conv3x3: bias must be 16-byte aligned");
+  if (B == 0) return 0;
+  h16_t* wp;
+  unsigned* flag;
+  YS_CHECK_ARG(conv3x3_carve(const_cast<void*>(prep), prep_bytes, cin, &wp, &flag), "conv3x3: prepared block too small");
+  c3::Args a{x, wp, bias, y, cin, H, W, (W + c3::TW - 1) / c3::TW, (H + c3::TH - 1) / c3::TH, range_flag_dev(), flag};
+  const long nwg = (long)B * a.tiles_x * a.tiles_y;
+  YS_CHECK_ARG(nwg < (1L << 31), "conv3x3: too many tiles");
+  hipLaunchKernelGGL(c3::conv3x3_x2_kernel, dim3((unsigned)nwg), dim3(256), 0, (hipStream_t)stream, a);
+  YS_CHECK_LAUNCH("conv3x3");
+  return 0;
+}

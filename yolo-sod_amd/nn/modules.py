@@ -91,18 +91,30 @@ CONV1X1_GEMM = os.environ.get("YOLOSOD_CONV1X1", "0") == "1"
 # thin 1x1 convs (Cout 64, Cin <= 256, H*W % 64 == 0) as one fused HIP kernel instead of MIOpen + epilogue
 # (scripts/bench_conv1x1.py: 96->64 at 160^2 0.16 vs 0.38 ms; at Cout 128 the MIOpen path stays faster)
 THIN1X1 = os.environ.get("YOLOSOD_THIN1X1", "1") == "1"
+# the Detect head's 3x3 tower convs (64 outputs) as the library's fp16-split implicit-GEMM kernel (csrc/conv3x3.hip)
+# instead of MIOpen + the epilogue pass, when the launch has >= 256 tiles (8 x 32 pixels; at fewer, e.g. P5's 20 x 20
+# maps, MIOpen was faster: scripts/bench_conv3x3.py). YOLOSOD_CONV3X3=0 restores MIOpen (A/B), =force takes every
+# tower conv whatever its size (tests), =all also takes every other eligible 3x3 conv of the model (the backbone
+# stays on MIOpen by default, as north_star asks)
+CONV3X3 = os.environ.get("YOLOSOD_CONV3X3", "1")
 
 
-def conv_epilogue(conv: nn.Conv2d, act_code, x, out=None, res=None, stats=None, out2=None, c2lo=0):
+def conv_epilogue(conv: nn.Conv2d, act_code, x, out=None, res=None, stats=None, out2=None, c2lo=0, tower=False):
     """GPU fast path of ``act(conv(x)) (+ res)``: MIOpen conv without bias, then one HIP pass for bias +
     activation (+ shortcut), optionally written straight into a channel slice ``out`` of a concat buffer.
     ``stats`` ("sum" / "summax"): the same pass emits the output's per-plane partial statistics for a following
     SE / CBAM gate (``_hip.PlaneStats`` on the returned tensor).
     ``out2``: also store channels [c2lo, C) packed there (the next conv's input; C2f's Bottleneck chain).
+    ``tower``: the conv is one of the Detect head's 3x3 tower convs (the fp16-split conv kernel takes it).
     Returns None when the fast path does not apply (CPU tensor, no bias, unsupported activation / shape)."""
     if x.device.type != "cuda" or conv.bias is None or act_code is None or x.dtype not in (torch.float32,
                                                                                            torch.bfloat16):
         return None
+    if (act_code == 1 and out is None and res is None and stats is None and out2 is None and CONV3X3 != "0"
+            and (CONV3X3 == "all" or tower) and _hip.conv3x3_ok(x, conv)
+            and (CONV3X3 == "force" or x.shape[0] * -(-x.shape[2] // 8) * -(-x.shape[3] // 32) >= 256)):
+        prep = lambda: _cached(conv, "c3prep", (conv.weight,), lambda: _hip.conv3x3_prepare(conv.weight))  # noqa: E731
+        return _hip.conv3x3_silu(x, conv.bias, prep)
     if (THIN1X1 and act_code == 1 and (stats is None or (stats in ("sum", "summax") and res is None and out2 is None))
             and conv.out_channels == 64 and conv.kernel_size == (1, 1) and conv.stride == (1, 1)
             and conv.groups == 1 and conv.padding == (0, 0) and _hip.conv1x1_thin_ok(x, conv.out_channels)
@@ -142,6 +154,8 @@ class Conv(nn.Module):
     default_act = nn.SiLU()
     # set by DetectionModel when this conv's output feeds an SE ("sum") / CBAM ("summax") / CA ("capool") directly
     emit_stats = None
+    # set by Detect on its 3x3 tower convs (head.py:43-57): the fp16-split conv kernel runs them (CONV3X3)
+    tower = False
 
     def __init__(self, c1, c2, k=1, s=1, p=None, g=1, d=1, act=True):
         super().__init__()
@@ -153,7 +167,7 @@ class Conv(nn.Module):
         return self.act(self.bn(self.conv(x)))
 
     def forward_fuse(self, x, out=None, res=None, out2=None, c2lo=0):
-        y = conv_epilogue(self.conv, _act_code(self.act), x, out, res, self.emit_stats, out2, c2lo)
+        y = conv_epilogue(self.conv, _act_code(self.act), x, out, res, self.emit_stats, out2, c2lo, self.tower)
         if y is not None:
             return y
         y = self.act(self.conv(x))
@@ -582,6 +596,10 @@ class Detect(nn.Module):
                               nn.Sequential(DWConv(c3, c3, 3), Conv(c3, c3, 1)), nn.Conv2d(c3, self.nc, 1))
                 for x in ch))
         self.dfl = DFL(self.reg_max) if self.reg_max > 1 else nn.Identity()
+        for seq in (*self.cv2, *self.cv3):
+            for m in seq:
+                if isinstance(m, Conv) and m.conv.kernel_size == (3, 3) and not isinstance(m, DWConv):
+                    m.tower = True
 
     # GPU inference runs the fused head tail + decode (one HIP kernel; the [B, 64+nc, Hi, Wi] raw maps are never
     # written). The second output keeps the reference's meaning (head.py:70-74: the raw maps) as a RawMaps
