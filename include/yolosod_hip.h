@@ -269,6 +269,9 @@ int yolosod_debug_set_a2_outup(int on);
 /* Test hook: A2_Attn's proj + SiLU + pooling kernel with 128 / 256 output channels per workgroup (1, default; env
  * YOLOSOD_A2_POOL_WIDE=0 turns it off) or with 64 (0); returns the previous state. */
 int yolosod_debug_set_a2_pool_wide(int on);
+/* Timing hook: ablation variants of the 3x3 conv kernel (csrc/conv3x3.hip; WRONG results for any abl != 0 and
+ * != 16 - scripts/bench_conv3x3.py only). Returns the previous value. */
+int yolosod_debug_set_conv3x3_abl(int abl);
 void yolosod_debug_set_gemm_x2(int on);
 /* Test hook: the bf16 decomposed SwinBlock's depthwise conv + token layout and LN1 in one pass
  * (swin_tokens_ln_bf16_kernel, 1, default; env YOLOSOD_SWIN_TOKLN=0 turns it off) or as two kernels (0);

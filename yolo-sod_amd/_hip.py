@@ -87,6 +87,7 @@ SIGNATURES = {
     "yolosod_debug_set_a2_fused": (_i, [_i]),
     "yolosod_debug_set_a2_outup": (_i, [_i]),
     "yolosod_debug_set_a2_pool_wide": (_i, [_i]),
+    "yolosod_debug_set_conv3x3_abl": (_i, [_i]),
     "yolosod_debug_set_swin_tokln": (_i, [_i]),
     "yolosod_debug_set_x3_swz": (_i, [_i]),
     "yolosod_debug_set_a2_pool_px": (_i, [_i]),

@@ -7,16 +7,17 @@
 // Method (the two-term split of swin_x3.hip): v = h + l with h = fp16(v), l = fp16(v - h); a product is
 // ah.bh + ah.bl + al.bh on v_mfma_f32_16x16x32_f16 with fp32 accumulation. Weights are split once per parameter
 // version by conv3x3_prep_kernel (x 64, exact, so their low terms stay normal fp16) into fragment-major planes:
-// for tap t, 32-channel input chunk q, 16-row output block rb and plane p, the 64 lanes' A fragments (lane (g, l15):
+// for tap t, 32-channel input chunk q, 16-channel output block rb and plane p, the 64 lanes' fragments (lane (g, l15):
 // output channel 16 rb + l15, input channels 32 q + 8 g .. + 7) are 1 KB contiguous.
 //
 // One 256-thread workgroup per (image, 8 x 32 output tile), all 64 output channels, two workgroups per CU: per input
 // chunk, the tile's 10 x 34 input halo (zero padding outside the image) is loaded, split and stored once as two fp16
-// planes [pixel][32] in LDS; the nine taps read their B fragments (8 channels of one halo pixel per lane) at
+// planes [pixel][32] in LDS; the nine taps read their pixel fragments (8 channels of one halo pixel per lane) at
 // tap-shifted pixel offsets of the same planes, so every input value is split once per workgroup and reused by
-// 9 taps x 64 outputs. Wave w computes output rows 4 (w >> 1) .. + 3 (eight 16-pixel column blocks) for the output
-// row blocks 2 (w & 1), 2 (w & 1) + 1: 16 accumulator tiles from 4 weight fragments (L2, one tap ahead) and 16 pixel
-// fragments (LDS) per tap. The next chunk's halo is loaded into registers while the current chunk computes.
+// 9 taps x 64 outputs. Wave w computes output rows 4 (w >> 1) .. + 3 (eight 16-pixel blocks) for the output channel
+// blocks 2 (w & 1), 2 (w & 1) + 1: 16 accumulator tiles from 4 weight fragments (L2, one tap ahead) and 16 pixel
+// fragments (LDS) per tap. The pixels are the MFMA's A operand, so a lane's accumulators are 4 consecutive pixels of
+// one channel (16-byte stores). The next chunk's halo loads are spread over the current chunk's taps.
 #include "common.h"
 
 namespace ys {
@@ -42,6 +43,9 @@ struct Args {
   const unsigned* prep_flag;
 };
 
+// ABL (timing ablations, wrong results; yolosod_debug_set_conv3x3_abl): 1 no halo loads, 2 every weight fragment from
+// one address, 4 no MFMA (a VALU stand-in keeps the LDS reads), 8 no output stores. V4: W % 4 == 0 (16-byte stores).
+template <int ABL, bool V4>
 __global__ __launch_bounds__(256, 2) void conv3x3_x2_kernel(Args p) {
   __shared__ __attribute__((aligned(16))) h16_t Pl[2 * PL];
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -78,13 +82,18 @@ __global__ __launch_bounds__(256, 2) void conv3x3_x2_kernel(Args p) {
     voff[i] = (unsigned)(((4 * quad) * HWi + min(max(yy, 0), H - 1) * W + min(max(xx, 0), W - 1)) * 4);
   }
   f32x4 sv[NIT];
-  auto load_chunk = [&](int q) __attribute__((always_inline)) {
+  // loads k = 4 i + c in [k0, k1) of chunk q's staging (item i, channel c of its quad)
+  auto load_part = [&](int q, int k0, int k1) __attribute__((always_inline)) {
     const int sx = __builtin_amdgcn_readfirstlane(32 * q * HWi * 4);
 #pragma unroll
-    for (int i = 0; i < NIT; ++i)
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-        sv[i][c] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, voff[i], sx + c * HWi * 4, 0));
+    for (int k = 0; k < 4 * NIT; ++k)
+      if (k >= k0 && k < k1) {
+        if constexpr ((ABL & 1) != 0)
+          sv[k >> 2][k & 3] = 0.5f + (float)q;
+        else
+          sv[k >> 2][k & 3] = __builtin_bit_cast(
+              float, __builtin_amdgcn_raw_buffer_load_b32(rx, voff[k >> 2], sx + (k & 3) * HWi * 4, 0));
+      }
   };
   auto store_chunk = [&]() __attribute__((always_inline)) {
 #pragma unroll
@@ -102,16 +111,18 @@ __global__ __launch_bounds__(256, 2) void conv3x3_x2_kernel(Args p) {
       }
     }
   };
-  // this wave: output row blocks 2 rp, 2 rp + 1 (channels 32 rp ..), pixel rows 4 ph .. 4 ph + 3; B-fragment pixel of
-  // column block cb at tap (0, 0): output row 4 ph + (cb >> 1), column (cb & 1) 16 + l15
+  // this wave: output channels 32 rp .. + 31 (weight row blocks 2 rp + r), pixel rows 4 ph .. 4 ph + 3 (pixel blocks
+  // cb: row 4 ph + (cb >> 1), columns (cb & 1) 16 .. + 15). The pixels are the MFMA's A operand (lane (g, l15) of a
+  // fragment: pixel l15 of the block, channels 8 g .. + 7 of the chunk) and the weights its B operand, so the lane
+  // holds 4 consecutive pixels (4 g .. + 3) of one output channel (l15): 16-byte output stores
   const int rp = wid & 1, ph = wid >> 1;
   int bpx[8];
 #pragma unroll
   for (int cb = 0; cb < 8; ++cb) bpx[cb] = (4 * ph + (cb >> 1)) * HW_ + (cb & 1) * 16 + l15;
-  // A fragments of (tap t, chunk q): this wave's row blocks 2 rp + r (r = 0, 1), planes 0 / 1; tap t's fragments of
-  // chunk q start at byte ((t nq + q) 8) KB, [row block][plane][lane][16 bytes]
+  // weight fragments of (tap t, chunk q): row blocks 2 rp + r (r = 0, 1), planes 0 / 1; tap t's fragments of chunk q
+  // start at byte ((t nq + q) 8) KB, [row block][plane][lane][16 bytes] (the B-operand lane layout is the A one)
   auto wfrag = [&](int t, int q, int r, int pl) __attribute__((always_inline)) {
-    const int st = __builtin_amdgcn_readfirstlane(((t * nq + q) * 8) * 1024);
+    const int st = (ABL & 2) ? 0 : __builtin_amdgcn_readfirstlane(((t * nq + q) * 8) * 1024);
     return __builtin_bit_cast(f16x8_t, __builtin_amdgcn_raw_buffer_load_b128(
                                            rw, (unsigned)((((2 * rp + r) * 2 + pl) * 64 + lane) * 16), st, 0));
   };
@@ -121,20 +132,25 @@ __global__ __launch_bounds__(256, 2) void conv3x3_x2_kernel(Args p) {
 #pragma unroll
     for (int cb = 0; cb < 8; ++cb) acc[r][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  load_chunk(0);
+  load_part(0, 0, 4 * NIT);
   for (int q = 0; q < nq; ++q) {
     __syncthreads();  // every wave is done with the previous chunk's planes
     store_chunk();
     __syncthreads();
-    // the next chunk's loads in flight during this chunk's products; unconditional (the last chunk reloads itself):
-    // loads under a branch merge into phis whose copies wait for every load in flight
-    load_chunk(q + 1 < nq ? q + 1 : q);
+    // The next chunk's staging loads are spread over the nine taps, each part issued behind the next tap's weight
+    // fragments, and sched barriers keep every prefetch where it is: vmcnt counts in issue order, so a wait for a
+    // tap's weights also waits for every halo load issued before them (all 44 at once: the HBM latency at tap 0 of
+    // every chunk), and without the barriers the scheduler sinks the loads to their first use (next chunk's staging,
+    // next tap) to save registers. Unconditional: the last chunk reloads itself (loads under a branch merge into phis
+    // whose copies wait for every load in flight).
+    const int qn = q + 1 < nq ? q + 1 : q;
     f16x8_t wa[2][2], wn[2][2];
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
       wa[r][0] = wfrag(0, q, r, 0);
       wa[r][1] = wfrag(0, q, r, 1);
     }
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
       const int tn = t + 1 < 9 ? t + 1 : t;  // one tap ahead (unconditional)
@@ -143,6 +159,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_x2_kernel(Args p) {
         wn[r][0] = wfrag(tn, q, r, 0);
         wn[r][1] = wfrag(tn, q, r, 1);
       }
+      load_part(qn, 5 * t, t == 8 ? 4 * NIT : 5 * t + 5);
+      __builtin_amdgcn_sched_barrier(0);
       const int toff = (t / 3) * HW_ + (t % 3);
 #pragma unroll
       for (int cb = 0; cb < 8; ++cb) {
@@ -150,7 +168,15 @@ __global__ __launch_bounds__(256, 2) void conv3x3_x2_kernel(Args p) {
         const f16x8_t xh = *reinterpret_cast<const f16x8_t*>(src);
         const f16x8_t xlo = *reinterpret_cast<const f16x8_t*>(src + PL);
 #pragma unroll
-        for (int r = 0; r < 2; ++r) acc[r][cb] = mfma_f16x3(wa[r][0], wa[r][1], xh, xlo, acc[r][cb]);
+        for (int r = 0; r < 2; ++r) {
+          if constexpr ((ABL & 4) != 0) {
+            acc[r][cb][0] += (float)xh[0] * (float)wa[r][0][0] + (float)xlo[1] * (float)wa[r][1][1];
+          } else {  // the three split products, small terms first
+            f32x4 c = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, wa[r][1], acc[r][cb], 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(xlo, wa[r][0], c, 0, 0, 0);
+            acc[r][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, wa[r][0], c, 0, 0, 0);
+          }
+        }
       }
 #pragma unroll
       for (int r = 0; r < 2; ++r) {
@@ -159,20 +185,31 @@ __global__ __launch_bounds__(256, 2) void conv3x3_x2_kernel(Args p) {
       }
     }
   }
-  // epilogue: lane (g, l15) of (r, cb) holds output channel 16 (2 rp + r) + 4 g + j, pixel (row 4 ph + (cb >> 1),
-  // column (cb & 1) 16 + l15) of the tile. SiLU on the hardware exp2 / rcp (~2^-22 relative, below the split
+  // epilogue: lane (g, l15) of (r, cb) holds output channel 16 (2 rp + r) + l15, pixels (row 4 ph + (cb >> 1),
+  // columns (cb & 1) 16 + 4 g .. + 3) of the tile. SiLU on the hardware exp2 / rcp (~2^-22 relative, below the split
   // products' own few-ulp error)
   float* yb = p.y + (long)b * 64 * HWi;
+  float bv[2];
+#pragma unroll
+  for (int r = 0; r < 2; ++r) bv[r] = p.bias[16 * (2 * rp + r) + l15];
 #pragma unroll
   for (int cb = 0; cb < 8; ++cb) {
-    const int oy = ty * TH + 4 * ph + (cb >> 1), ox = tx * TW + (cb & 1) * 16 + l15;
-    if (oy < H && ox < W) {
+    const int oy = ty * TH + 4 * ph + (cb >> 1), ox = tx * TW + (cb & 1) * 16 + 4 * g;
+    if constexpr ((ABL & 8) != 0)
+      if (acc[0][cb][0] != -1.2345e30f) continue;
 #pragma unroll
-      for (int r = 0; r < 2; ++r) {
-        const int c0 = 16 * (2 * rp + r) + 4 * g;
-        const f32x4 bv = *reinterpret_cast<const f32x4*>(p.bias + c0);
+    for (int r = 0; r < 2; ++r) {
+      float* d = yb + (16 * (2 * rp + r) + l15) * HWi + oy * W + ox;
+      f32x4 o;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) yb[(c0 + j) * HWi + oy * W + ox] = silu_fast_(acc[r][cb][j] * (1.0f / WSC) + bv[j]);
+      for (int j = 0; j < 4; ++j) o[j] = silu_fast_(acc[r][cb][j] * (1.0f / WSC) + bv[r]);
+      if constexpr (V4) {  // W % 4 == 0: the 4 pixels are all in or all out of the image
+        // non-temporal: the tile is not read again before it has left the caches (at P2 the kernel is 13 % faster)
+        if (oy < H && ox < W) __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(d));
+      } else if (oy < H) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (ox + j < W) d[j] = o[j];
       }
     }
   }
@@ -205,6 +242,13 @@ __global__ __launch_bounds__(256) void conv3x3_prep_kernel(const float* __restri
 }  // namespace ys
 
 using namespace ys;
+
+static int g_c3_abl = 0;
+YS_EXPORT int yolosod_debug_set_conv3x3_abl(int abl) {
+  const int old = g_c3_abl;
+  g_c3_abl = abl;
+  return old;
+}
 
 // 3x3 / stride 1 / pad 1 conv with 64 outputs: Cin a multiple of 32 (<= 2048)
 YS_EXPORT size_t yolosod_conv3x3_prep_bytes(int cin) {
@@ -255,7 +299,18 @@ YS_EXPORT int yolosod_conv3x3_silu(const float* x, float* y, int B, int cin, int
   c3::Args a{x, wp, bias, y, cin, H, W, (W + c3::TW - 1) / c3::TW, (H + c3::TH - 1) / c3::TH, range_flag_dev(), flag};
   const long nwg = (long)B * a.tiles_x * a.tiles_y;
   YS_CHECK_ARG(nwg < (1L << 31), "conv3x3: too many tiles");
-  hipLaunchKernelGGL(c3::conv3x3_x2_kernel, dim3((unsigned)nwg), dim3(256), 0, (hipStream_t)stream, a);
+  const bool v4 = W % 4 == 0;
+  auto kern = v4 ? c3::conv3x3_x2_kernel<0, true> : c3::conv3x3_x2_kernel<0, false>;
+  switch (g_c3_abl) {  // timing ablations (W % 4 == 0 shapes)
+    case 1: kern = c3::conv3x3_x2_kernel<1, true>; break;
+    case 2: kern = c3::conv3x3_x2_kernel<2, true>; break;
+    case 4: kern = c3::conv3x3_x2_kernel<4, true>; break;
+    case 8: kern = c3::conv3x3_x2_kernel<8, true>; break;
+    case 12: kern = c3::conv3x3_x2_kernel<12, true>; break;
+    case 15: kern = c3::conv3x3_x2_kernel<15, true>; break;
+    default: break;
+  }
+  hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(256), 0, (hipStream_t)stream, a);
   YS_CHECK_LAUNCH("conv3x3");
   return 0;
 }
