@@ -874,13 +874,21 @@ __device__ __forceinline__ void gemm_w(const h16_t* __restrict__ Wp, int N, int 
       }
     }
   };
+  // The prefetches stay where they are (sched barriers): the scheduler otherwise sinks each step's loads to the end
+  // of the previous step, right before their first use. Unconditional (the last step reloads a step, L2-hot): a
+  // load under a branch merges into a phi whose copy waits for every load in flight.
+  static_assert(NST % 2 == 0 || NST == 1, "steps in pairs");
   ldw(w0, 0);
+  if constexpr (NST == 1) {
+    mma(w0, 0);
+  } else {
 #pragma unroll 1
-  for (int st = 0; st < NST; st += 2) {
-    if (st + 1 < NST) ldw(w1, st + 1);
-    mma(w0, st);
-    if (st + 1 < NST) {
-      if (st + 2 < NST) ldw(w0, st + 2);
+    for (int st = 0; st < NST; st += 2) {
+      ldw(w1, st + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      mma(w0, st);
+      ldw(w0, st + 2 < NST ? st + 2 : st);
+      __builtin_amdgcn_sched_barrier(0);
       mma(w1, st + 1);
     }
   }
