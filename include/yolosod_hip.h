@@ -330,6 +330,14 @@ int yolosod_a2_forward_bf16(const uint16_t* x, uint16_t* y, int B, int C, int H,
                             const uint16_t* proj_w, const float* proj_b, const float* ln_w, const float* ln_b,
                             float ln_eps, const uint16_t* in_proj_w, const float* in_proj_b, const uint16_t* oproj_w,
                             const float* oproj_b, void* workspace, size_t workspace_bytes, void* stream);
+/* Detect head tail + decode (as yolosod_detect_head) of levels [l0, l1) only, into y laid out for all nl levels
+ * (the anchor offsets and A of every level; the other levels' slices of y are not written and their feature
+ * pointers not read). bf16 != 0: bf16 tower features (uint16_t patterns). Lets a caller decode the levels whose
+ * tower convolutions are done while the last level's still run (head.py:70 per level + _inference :100-131). */
+int yolosod_detect_head_levels(int nl, int l0, int l1, const void* const* box_feat, const void* const* cls_feat, int c2,
+                               int c3, const float* const* box_w, const float* const* box_b, const float* const* cls_w,
+                               const float* const* cls_b, const int* heights, const int* widths, const float* strides,
+                               int B, int nc, int reg_max, float* y, int bf16, void* stream);
 /* Detect head tail + decode (as yolosod_detect_head) on bf16 tower features; weights, biases and y fp32. */
 int yolosod_detect_head_bf16(int nl, const uint16_t* const* box_feat, const uint16_t* const* cls_feat, int c2, int c3,
                              const float* const* box_w, const float* const* box_b, const float* const* cls_w,

@@ -435,6 +435,33 @@ def test_detect_head_fused_vs_oracle(c3, img, x2, cuda):
     assert ok, f"max abs err {err:.3g}"
 
 
+@pytest.mark.parametrize("bf16", [False, True], ids=["fp32", "bf16"])
+def test_detect_head_level_ranges_bit_identical(bf16, cuda):
+    """detect_head_into (levels [l0, l1) into y laid out for all levels, the executor's split head) over a partition
+    of the levels equals the one-launch head bit for bit, and leaves the other levels' slices of y untouched."""
+    g = torch.Generator().manual_seed(11)
+    strides, nc, B = [4.0, 8.0, 16.0, 32.0], 10, 2
+    dt = torch.bfloat16 if bf16 else torch.float32
+    fb = [torch.randn(B, 64, int(256 // s), int(256 // s), generator=g).to(cuda, dt) for s in strides]
+    fc = [torch.randn(B, 64, int(256 // s), int(256 // s), generator=g).to(cuda, dt) for s in strides]
+    wb = [(torch.randn(64, 64, generator=g) * 0.25).to(cuda) for _ in strides]
+    bb = [torch.randn(64, generator=g).to(cuda) for _ in strides]
+    wc = [(torch.randn(nc, 64, generator=g) * 0.2).to(cuda) for _ in strides]
+    bc = [(torch.randn(nc, generator=g) - 2.0).to(cuda) for _ in strides]
+    args = (fb, fc, wb, bb, wc, bc, strides, nc)
+    y1 = _hip.detect_head(*args)
+    offs = [0]
+    for t in fb:
+        offs.append(offs[-1] + t.shape[2] * t.shape[3])
+    for parts in ([(0, 3), (3, 4)], [(0, 1), (1, 2), (2, 4)]):
+        y = torch.full_like(y1, float("nan"))
+        for l0, l1 in parts[:-1]:
+            _hip.detect_head_into(y, l0, l1, *args)
+        assert torch.isnan(y[..., offs[parts[-1][0]]:]).all()  # the last range not written yet
+        _hip.detect_head_into(y, *parts[-1], *args)
+        assert torch.equal(y, y1), parts
+
+
 @pytest.mark.parametrize("name", [n for n in recipes.OPS if n.startswith("a2_")])
 def test_a2_exact_fp32_gemms_match_reference_fixture(name, cuda):
     """A2_Attn with its GEMMs on exact fp32 MFMA (YOLOSOD_A2_X2=0); the default fp16-split GEMMs run the same

@@ -110,6 +110,8 @@ SIGNATURES = {
                                      _vp, _sz, _vp]),
     "yolosod_detect_head_bf16": (_i, [_i, _vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp,
                                       _vp]),
+    "yolosod_detect_head_levels": (_i, [_i, _i, _i, _vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i,
+                                        _i, _vp, _i, _vp]),
     "yolosod_gemm_bf16": (_i, [_vp, _l, _i, _vp, _l, _i, _i, _vp, _l, _i, _i, _i, _i, _i, _vp, _i, _i, _vp, _vp]),
     "yolosod_attention_bf16": (_i, [_vp, _vp, _l, _i, _i, _i, _vp]),
 }
@@ -497,6 +499,19 @@ def detect_head(box_feats, cls_feats, box_w, box_b, cls_w, cls_b, strides, nc, r
     return _launch(("head", (B, A), (nc, c2, c3)) + ((2,) if bf else ()), box_feats[0].device, ops().detect_head_fwd,
                    list(box_feats), list(cls_feats), list(box_w), list(box_b), list(cls_w), list(cls_b),
                    [float(s) for s in strides], int(nc), int(reg_max))
+
+
+def detect_head_into(y, l0, l1, box_feats, cls_feats, box_w, box_b, cls_w, cls_b, strides, nc, reg_max=16):
+    """``detect_head`` for levels [l0, l1) only, into y [B, 4+nc, A] laid out for all levels (torch.ops.yolosod.
+    detect_head_into): the executor decodes the levels whose towers are done while the last level's still run."""
+    bf = _act_dtype(_t(box_feats[0], "box_feats[0]"))
+    B, c2 = box_feats[0].shape[:2]
+    c3 = cls_feats[0].shape[1]
+    A = sum(t.shape[2] * t.shape[3] for t in box_feats[l0:l1])
+    _launch(("head", (B, A), (nc, c2, c3)) + ((2,) if bf else ()), box_feats[0].device, ops().detect_head_into, y,
+            int(l0), int(l1), list(box_feats), list(cls_feats), list(box_w), list(box_b), list(cls_w), list(cls_b),
+            [float(s) for s in strides], int(nc), int(reg_max))
+    return y
 
 
 def nms(pred, conf_thres, iou_thres, classes, agnostic, multi_label, max_det, max_nms, max_wh, in_place):

@@ -607,40 +607,48 @@ YS_EXPORT int yolosod_debug_set_head_x2(int on) {
   return prev;
 }
 
+// levels [l0, l1) of the nl-level anchor layout (the anchor offsets and A of all nl levels; the other levels' slices
+// of y are not written and their feature pointers not read)
 static int detect_head_impl(int nl, const void* const* box_feat, const void* const* cls_feat, int c2, int c3,
                             const float* const* box_w, const float* const* box_b, const float* const* cls_w,
                             const float* const* cls_b, const int* heights, const int* widths, const float* strides,
-                            int B, int nc, int reg_max, float* y, bool bf16, void* stream) {
+                            int B, int nc, int reg_max, float* y, bool bf16, void* stream, int l0 = 0, int l1 = -1) {
+  if (l1 < 0) l1 = nl;
   YS_CHECK_ARG(nl >= 1 && nl <= 4, "detect_head: nl=%d unsupported (1..4)", nl);
+  YS_CHECK_ARG(0 <= l0 && l0 < l1 && l1 <= nl, "detect_head: level range [%d, %d) outside [0, %d)", l0, l1, nl);
   YS_CHECK_ARG(box_feat && cls_feat && box_w && box_b && cls_w && cls_b && heights && widths && strides && y,
                "detect_head: null pointer");
   YS_CHECK_ARG(reg_max == 16, "detect_head: reg_max=%d unsupported (16)", reg_max);
   YS_CHECK_ARG(nc >= 1 && nc <= 16, "detect_head: nc=%d unsupported (1..16)", nc);
   YS_CHECK_ARG(c2 == 64 && (c3 == 64 || c3 == 128), "detect_head: (c2=%d, c3=%d) unsupported ((64, 64|128))", c2, c3);
   HeadArgs d{};
-  d.nl = nl;
+  d.nl = l1 - l0;
   d.nc = nc;
   d.range_flag = range_flag_dev();
   constexpr int NTS = 8;  // 16-pixel groups per wave -> 512 pixels per workgroup
   int off = 0, blk = 0;
   for (int i = 0; i < nl; ++i) {
-    YS_CHECK_ARG(box_feat[i] && cls_feat[i] && box_w[i] && box_b[i] && cls_w[i] && cls_b[i],
-                 "detect_head: null pointer at level %d", i);
-    d.fb[i] = box_feat[i];
-    d.fc[i] = cls_feat[i];
-    d.wb[i] = box_w[i];
-    d.bb[i] = box_b[i];
-    d.wc[i] = cls_w[i];
-    d.bc[i] = cls_b[i];
-    d.hw[i] = heights[i] * widths[i];
-    d.w[i] = widths[i];
-    d.stride[i] = strides[i];
-    d.a_off[i] = off;
-    d.blk_off[i] = blk;
-    off += d.hw[i];
-    blk += (d.hw[i] + 4 * NTS * 16 - 1) / (4 * NTS * 16);
+    const int hw = heights[i] * widths[i];
+    if (i >= l0 && i < l1) {
+      const int k = i - l0;
+      YS_CHECK_ARG(box_feat[i] && cls_feat[i] && box_w[i] && box_b[i] && cls_w[i] && cls_b[i],
+                   "detect_head: null pointer at level %d", i);
+      d.fb[k] = box_feat[i];
+      d.fc[k] = cls_feat[i];
+      d.wb[k] = box_w[i];
+      d.bb[k] = box_b[i];
+      d.wc[k] = cls_w[i];
+      d.bc[k] = cls_b[i];
+      d.hw[k] = hw;
+      d.w[k] = widths[i];
+      d.stride[k] = strides[i];
+      d.a_off[k] = off;
+      d.blk_off[k] = blk;
+      blk += (hw + 4 * NTS * 16 - 1) / (4 * NTS * 16);
+    }
+    off += hw;
   }
-  d.blk_off[nl] = blk;
+  d.blk_off[l1 - l0] = blk;
   d.A = off;
   d.y = y;
   if (B == 0 || off == 0) return 0;
@@ -681,6 +689,17 @@ YS_EXPORT int yolosod_detect_head(int nl, const float* const* box_feat, const fl
                                   const float* strides, int B, int nc, int reg_max, float* y, void* stream) {
   return detect_head_impl(nl, (const void* const*)box_feat, (const void* const*)cls_feat, c2, c3, box_w, box_b, cls_w,
                           cls_b, heights, widths, strides, B, nc, reg_max, y, false, stream);
+}
+
+// levels [l0, l1) only, into y laid out for all nl levels (the executor launches the levels whose towers are done
+// while the last level's towers still run); fp32 or bf16 (bf16 != 0) tower features
+YS_EXPORT int yolosod_detect_head_levels(int nl, int l0, int l1, const void* const* box_feat, const void* const* cls_feat,
+                                         int c2, int c3, const float* const* box_w, const float* const* box_b,
+                                         const float* const* cls_w, const float* const* cls_b, const int* heights,
+                                         const int* widths, const float* strides, int B, int nc, int reg_max, float* y,
+                                         int bf16, void* stream) {
+  return detect_head_impl(nl, box_feat, cls_feat, c2, c3, box_w, box_b, cls_w, cls_b, heights, widths, strides, B, nc,
+                          reg_max, y, bf16 != 0, stream, l0, l1);
 }
 
 // bf16 tower features (bf16 model config); weights, biases and the decode stay fp32, y is fp32

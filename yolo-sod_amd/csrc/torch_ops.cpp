@@ -304,14 +304,19 @@ Tensor swin_fwd(const Tensor& x, int64_t num_heads, int64_t window, const Tensor
   return y;
 }
 
-Tensor detect_head_fwd(at::TensorList box_feats, at::TensorList cls_feats, at::TensorList box_w, at::TensorList box_b,
-                       at::TensorList cls_w, at::TensorList cls_b, at::ArrayRef<double> strides, int64_t nc,
-                       int64_t reg_max) {
+// levels [l0, l1) of the fused Detect tail + decode into y [B, 4+nc, A] (A over all levels; l1 < 0: all levels,
+// y allocated here when undefined)
+static Tensor detect_head_run(at::TensorList box_feats, at::TensorList cls_feats, at::TensorList box_w,
+                              at::TensorList box_b, at::TensorList cls_w, at::TensorList cls_b,
+                              at::ArrayRef<double> strides, int64_t nc, int64_t reg_max, Tensor y, int64_t l0,
+                              int64_t l1) {
   const int nl = box_feats.size();
   TORCH_CHECK(nl >= 1 && nl <= 4 && cls_feats.size() == (size_t)nl && box_w.size() == (size_t)nl &&
                   box_b.size() == (size_t)nl && cls_w.size() == (size_t)nl && cls_b.size() == (size_t)nl &&
                   strides.size() == (size_t)nl,
               "detect_head_fwd: 1..4 levels with one tensor of each kind per level");
+  if (l1 < 0) l1 = nl;
+  TORCH_CHECK(0 <= l0 && l0 < l1 && l1 <= nl, "detect_head: level range [", l0, ", ", l1, ") outside [0, ", nl, ")");
   const Tensor& x0 = box_feats[0];
   const bool bf = act_bf16(x0, "detect_head_fwd");
   c10::DeviceGuard guard(x0.device());
@@ -341,14 +346,28 @@ Tensor detect_head_fwd(at::TensorList box_feats, at::TensorList cls_feats, at::T
     st_[i] = (float)strides[i];
     A += (int64_t)hs[i] * wsz[i];
   }
-  Tensor y = at::empty({B, 4 + nc, A}, x0.options().dtype(at::kFloat));
+  if (!y.defined()) y = at::empty({B, 4 + nc, A}, x0.options().dtype(at::kFloat));
+  TORCH_CHECK(y.device() == x0.device() && y.scalar_type() == at::kFloat && y.is_contiguous() && y.dim() == 3 &&
+                  y.size(0) == B && y.size(1) == 4 + nc && y.size(2) == A,
+              "detect_head: y must be a contiguous fp32 [", B, ", ", 4 + nc, ", ", A, "] tensor on ", x0.device());
   auto st = c10::hip::getCurrentHIPStream(x0.get_device());
-  const int rc = bf ? yolosod_detect_head_bf16(nl, (const uint16_t* const*)fb, (const uint16_t* const*)fc, c2, c3, wb,
-                                               bb, wc, bc, hs, wsz, st_, B, nc, reg_max, y.data_ptr<float>(), sp(st))
-                    : yolosod_detect_head(nl, (const float* const*)fb, (const float* const*)fc, c2, c3, wb, bb, wc, bc,
-                                          hs, wsz, st_, B, nc, reg_max, y.data_ptr<float>(), sp(st));
+  const int rc = yolosod_detect_head_levels(nl, (int)l0, (int)l1, fb, fc, c2, c3, wb, bb, wc, bc, hs, wsz, st_, B,
+                                            nc, reg_max, y.data_ptr<float>(), bf ? 1 : 0, sp(st));
   check_rc(rc, "detect_head_fwd");
   return y;
+}
+
+Tensor detect_head_fwd(at::TensorList box_feats, at::TensorList cls_feats, at::TensorList box_w, at::TensorList box_b,
+                       at::TensorList cls_w, at::TensorList cls_b, at::ArrayRef<double> strides, int64_t nc,
+                       int64_t reg_max) {
+  return detect_head_run(box_feats, cls_feats, box_w, box_b, cls_w, cls_b, strides, nc, reg_max, Tensor(), 0, -1);
+}
+
+// levels [l0, l1) into the caller's y (the executor: the levels whose towers are done, then the last one)
+void detect_head_into(Tensor y, int64_t l0, int64_t l1, at::TensorList box_feats, at::TensorList cls_feats,
+                      at::TensorList box_w, at::TensorList box_b, at::TensorList cls_w, at::TensorList cls_b,
+                      at::ArrayRef<double> strides, int64_t nc, int64_t reg_max) {
+  detect_head_run(box_feats, cls_feats, box_w, box_b, cls_w, cls_b, strides, nc, reg_max, y, l0, l1);
 }
 
 Tensor detect_decode_fwd(at::TensorList maps, at::ArrayRef<double> strides, int64_t nc, int64_t reg_max) {
@@ -432,6 +451,8 @@ TORCH_LIBRARY(yolosod, m) {
         "Tensor out_b, float ln2_eps, int hid, Tensor m2_b) -> Tensor");
   m.def("detect_head_fwd(Tensor[] box_feats, Tensor[] cls_feats, Tensor[] box_w, Tensor[] box_b, Tensor[] cls_w, "
         "Tensor[] cls_b, float[] strides, int nc, int reg_max) -> Tensor");
+  m.def("detect_head_into(Tensor(a!) y, int l0, int l1, Tensor[] box_feats, Tensor[] cls_feats, Tensor[] box_w, "
+        "Tensor[] box_b, Tensor[] cls_w, Tensor[] cls_b, float[] strides, int nc, int reg_max) -> ()");
   m.def("detect_decode_fwd(Tensor[] maps, float[] strides, int nc, int reg_max) -> Tensor");
   m.def("nms_batched(Tensor(a!) pred, float conf_thres, float iou_thres, Tensor? classes, bool agnostic, "
         "bool multi_label, int max_det, int max_nms, float max_wh, bool in_place=True) -> (Tensor, Tensor, Tensor)");
@@ -447,6 +468,7 @@ TORCH_LIBRARY_IMPL(yolosod, CUDA, m) {
   m.impl("swin_prep", swin_prep);
   m.impl("swin_fwd_prepared", swin_fwd_prepared);
   m.impl("detect_head_fwd", detect_head_fwd);
+  m.impl("detect_head_into", detect_head_into);
   m.impl("detect_decode_fwd", detect_decode_fwd);
   m.impl("nms_batched", nms_batched);
 }

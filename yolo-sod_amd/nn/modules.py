@@ -92,11 +92,13 @@ CONV1X1_GEMM = os.environ.get("YOLOSOD_CONV1X1", "0") == "1"
 # (scripts/bench_conv1x1.py: 96->64 at 160^2 0.16 vs 0.38 ms; at Cout 128 the MIOpen path stays faster)
 THIN1X1 = os.environ.get("YOLOSOD_THIN1X1", "1") == "1"
 # the Detect head's 3x3 tower convs (64 outputs) as the library's fp16-split implicit-GEMM kernel (csrc/conv3x3.hip)
-# instead of MIOpen + the epilogue pass, when the launch has >= 256 tiles (8 x 32 pixels; at fewer, e.g. P5's 20 x 20
-# maps, MIOpen was faster: scripts/bench_conv3x3.py). YOLOSOD_CONV3X3=0 restores MIOpen (A/B), =force takes every
+# instead of MIOpen + the epilogue pass, when the launch has >= CONV3X3_MIN_TILES tiles of 8 x 32 pixels (0: every
+# tower conv; the first kernel was slower than MIOpen below 256 tiles, e.g. P5's 20 x 20 maps, the current one is
+# faster at every tower shape: scripts/bench_conv3x3.py). YOLOSOD_CONV3X3=0 restores MIOpen (A/B), =force takes every
 # tower conv whatever its size (tests), =all also takes every other eligible 3x3 conv of the model (the backbone
 # stays on MIOpen by default, as north_star asks)
 CONV3X3 = os.environ.get("YOLOSOD_CONV3X3", "1")
+CONV3X3_MIN_TILES = int(os.environ.get("YOLOSOD_CONV3X3_MIN_TILES", "0"))
 
 
 def conv_epilogue(conv: nn.Conv2d, act_code, x, out=None, res=None, stats=None, out2=None, c2lo=0, tower=False):
@@ -112,7 +114,7 @@ def conv_epilogue(conv: nn.Conv2d, act_code, x, out=None, res=None, stats=None, 
         return None
     if (act_code == 1 and out is None and res is None and stats is None and out2 is None and CONV3X3 != "0"
             and (CONV3X3 == "all" or tower) and _hip.conv3x3_ok(x, conv)
-            and (CONV3X3 == "force" or x.shape[0] * -(-x.shape[2] // 8) * -(-x.shape[3] // 32) >= 256)):
+            and (CONV3X3 == "force" or x.shape[0] * -(-x.shape[2] // 8) * -(-x.shape[3] // 32) >= CONV3X3_MIN_TILES)):
         prep = lambda: _cached(conv, "c3prep", (conv.weight,), lambda: _hip.conv3x3_prepare(conv.weight))  # noqa: E731
         return _hip.conv3x3_silu(x, conv.bias, prep)
     if (THIN1X1 and act_code == 1 and (stats is None or (stats in ("sum", "summax") and res is None and out2 is None))
@@ -628,9 +630,12 @@ class Detect(nn.Module):
         """Level i's box / class tower features (cv2[i][:-1], cv3[i][:-1]): the inputs of the fused head kernel."""
         return self.cv2[i][:-1](xi).contiguous(), self.cv3[i][:-1](xi).contiguous()
 
-    def forward_towers(self, feats):
-        """The fused head on tower features computed elsewhere (the executor's side stream): [(fb_i, fc_i)]."""
-        return self._head([f[0] for f in feats], [f[1] for f in feats])
+    def forward_towers(self, feats, wait_last=None):
+        """The fused head on tower features computed elsewhere (the executor's side streams): [(fb_i, fc_i)].
+        ``wait_last``: the levels before the last are decoded first, then ``wait_last()`` (the caller's stream
+        waits for the last level's towers) and the last level - its towers start only when the neck's last feature
+        map exists, so the other levels' decode overlaps them."""
+        return self._head([f[0] for f in feats], [f[1] for f in feats], wait_last)
 
     def _fused_forward(self, x):
         """cv2[i][:-1] / cv3[i][:-1] towers (PyTorch-ROCm convs + HIP epilogues), then the last 1x1 convs of both
@@ -642,13 +647,22 @@ class Detect(nn.Module):
             fc.append(c)
         return self._head(fb, fc)
 
-    def _head(self, fb, fc):
+    def _head(self, fb, fc, wait_last=None):
         nl = self.nl
         p = _f32(self, "head", *[c[-1].weight for c in self.cv2], *[c[-1].bias for c in self.cv2],
                  *[c[-1].weight for c in self.cv3], *[c[-1].bias for c in self.cv3])
         w = lambda t: t.reshape(t.shape[0], -1)  # noqa: E731
-        y = _hip.detect_head(fb, fc, [w(t) for t in p[:nl]], list(p[nl:2 * nl]), [w(t) for t in p[2 * nl:3 * nl]],
-                             list(p[3 * nl:]), [float(s) for s in self.stride], self.nc, self.reg_max)
+        args = (fb, fc, [w(t) for t in p[:nl]], list(p[nl:2 * nl]), [w(t) for t in p[2 * nl:3 * nl]],
+                list(p[3 * nl:]), [float(s) for s in self.stride], self.nc, self.reg_max)
+        if wait_last is None or nl < 2:
+            if wait_last is not None:
+                wait_last()
+            return _hip.detect_head(*args), RawMaps(self, fb, fc)
+        A = sum(t.shape[2] * t.shape[3] for t in fb)
+        y = torch.empty((fb[0].shape[0], 4 + self.nc, A), dtype=torch.float32, device=fb[0].device)
+        _hip.detect_head_into(y, 0, nl - 1, *args)
+        wait_last()
+        _hip.detect_head_into(y, nl - 1, nl, *args)
         return y, RawMaps(self, fb, fc)
 
     def raw_from_features(self, i, h2, h3):
