@@ -269,6 +269,30 @@ int yolosod_debug_set_a2_outup(int on);
 /* Test hook: A2_Attn's proj + SiLU + pooling kernel with 128 / 256 output channels per workgroup (1, default; env
  * YOLOSOD_A2_POOL_WIDE=0 turns it off) or with 64 (0); returns the previous state. */
 int yolosod_debug_set_a2_pool_wide(int on);
+/* The SE gate only, sigmoid(fc2(relu(fc1(mean_hw(x)))))   smallobj_modules.py:87-90, into gate [B][C], for a consumer
+ * that applies y = x * gate itself (yolosod_conv3x3s2_silu); psum: x's per-plane partial sums from its producer
+ * (yolosod_bias_act_stats) or NULL (a statistics pass over x). workspace: yolosod_se_workspace bytes. */
+int yolosod_se_gate(const float* x, int B, int C, int H, int W, const float* fc1_w, const float* fc1_b,
+                    const float* fc2_w, const float* fc2_b, int hidden, const float* psum, float* gate, void* workspace,
+                    size_t workspace_bytes, void* stream);
+/* The CBAM gates only   cbam_block.py:14-23,33-37: ca [B][C] and sa [B][H][W] (sa from the channel statistics of
+ * x * ca), for a consumer that applies y = (x * ca) * sa itself; psum / pmax from the producer or both NULL.
+ * workspace: yolosod_cbam_workspace bytes. */
+int yolosod_cbam_gates(const float* x, int B, int C, int H, int W, const float* fc0_w, const float* fc2_w, int hidden,
+                       const float* sa_w, const float* psum, const float* pmax, float* ca, float* sa, void* workspace,
+                       size_t workspace_bytes, void* stream);
+/* 3x3 / stride 2 / pad 1 conv + bias + SiLU with the producing MAFN gate applied while the input is staged
+ * (csrc/conv3x3s2.hip): y = SiLU(conv3x3_s2((x * gc) * gp, W) + bias), the consumer Conv of SE_Block L1 (gc = the SE
+ * gate, smallobj_modules.py:92) and of CBAM_Block L4 (gc = ca, gp = sa, cbam_block.py:53-54) in the paper YAML, with the
+ * gate's output never written. fp16 two-term split MFMA at fp32 accuracy; Cout 64 or 128, Cin a multiple of 32 (<= 2048),
+ * Ho = (H + 1) / 2, Wo = (W + 1) / 2 with Wo % 4 == 0; x [B][cin][H][W] (B*cin*H*W*4 < 2^32), gc [B][cin] 16-byte
+ * aligned or NULL, gp [B][H][W] or NULL, y [B][cout][Ho][Wo]. Weights prepared once per parameter version into a
+ * caller-owned block of yolosod_conv3x3s2_prep_bytes(cin, cout) bytes (0: unsupported). Replaces the gate's apply pass
+ * + torch.nn.functional.conv2d (MIOpen) + the bias / SiLU epilogue. */
+size_t yolosod_conv3x3s2_prep_bytes(int cin, int cout);
+int yolosod_conv3x3s2_prepare(const float* w, int cin, int cout, void* prep, size_t prep_bytes, void* stream);
+int yolosod_conv3x3s2_silu(const float* x, float* y, int B, int cin, int cout, int H, int W, const float* bias,
+                           const float* gc, const float* gp, const void* prep, size_t prep_bytes, void* stream);
 /* Timing hook: ablation variants of the 3x3 conv kernel (csrc/conv3x3.hip; WRONG results for any abl != 0 and
  * != 16 - scripts/bench_conv3x3.py only). Returns the previous value. */
 int yolosod_debug_set_conv3x3_abl(int abl);

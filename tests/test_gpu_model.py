@@ -226,11 +226,12 @@ def test_executor_streams_and_concat_elision_are_bit_identical(gpu_model, cuda):
     from yolosod_amd.nn import tasks
     g = torch.Generator().manual_seed(5)
     x = torch.rand(4, 3, 320, 320, generator=g).to(cuda)
-    saved, saved_side, saved_split = tasks.STREAMS, tasks.SIDE_STREAMS, tasks.HEAD_SPLIT
+    saved, saved_side, saved_split, saved_gf = tasks.STREAMS, tasks.SIDE_STREAMS, tasks.HEAD_SPLIT, tasks.GATE_FUSE
     det = torch.backends.cudnn.deterministic
     torch.backends.cudnn.deterministic = True
     try:
         with torch.inference_mode():
+            tasks.GATE_FUSE = False  # the fused gate convs change the conv arithmetic (test_gate_fusion_...)
             tasks.STREAMS = 1
             y_streams = gpu_model(x)[0].clone()  # towers dealt to SIDE_STREAMS (3) side streams, head split
             assert gpu_model._last_elided == 6
@@ -246,10 +247,37 @@ def test_executor_streams_and_concat_elision_are_bit_identical(gpu_model, cuda):
             finally:
                 gpu_model._fused = True
     finally:
-        tasks.STREAMS, tasks.SIDE_STREAMS, tasks.HEAD_SPLIT = saved, saved_side, saved_split
+        tasks.STREAMS, tasks.SIDE_STREAMS, tasks.HEAD_SPLIT, tasks.GATE_FUSE = saved, saved_side, saved_split, saved_gf
         torch.backends.cudnn.deterministic = det
     torch.cuda.synchronize()
     assert torch.equal(y_streams, y_nosplit)
     assert torch.equal(y_streams, y_side1)
     assert torch.equal(y_streams, y_one)
     assert torch.equal(y_one, y_plain)
+
+
+def test_gate_fusion_matches_the_unfused_model(gpu_model, cuda):
+    """SE L1 -> Conv L2 and CBAM L4 -> Conv L5 as gate-only launches + the stride-2 conv that applies the gate while
+    staging (tasks.py GATE_FUSE, csrc/conv3x3s2.hip): the op_timer sees the fused operators instead of the SE / CBAM
+    apply, and the model output matches the unfused executor (the gate's own apply pass, MIOpen conv) within fp32
+    accuracy, at 320 and at 640 (Cout 64 and 128, one and two input chunks)."""
+    from yolosod_amd import _hip
+    from yolosod_amd.nn import tasks
+    saved = tasks.GATE_FUSE
+    for S in (320, 640):
+        x = torch.rand(2, 3, S, S, generator=torch.Generator().manual_seed(S)).to(cuda)
+        try:
+            with torch.inference_mode():
+                tasks.GATE_FUSE = True
+                with _hip.op_timer() as t:
+                    y1 = gpu_model(x)[0].clone()
+                names = [k[0] for k, _ in t.durations_ms()]
+                keys = set(names)
+                tasks.GATE_FUSE = False
+                y0 = gpu_model(x)[0].clone()
+        finally:
+            tasks.GATE_FUSE = saved
+        assert {"se_gate", "se_conv", "cbam_gate", "cbam_conv"} <= keys, keys
+        assert names.count("se") == 1 and names.count("cbam") == 1  # SE L23 and CBAM L18 keep their apply
+        ok, e, _ = tol_close(y1.cpu().double(), y0.cpu().double(), 1e-3, 1e-4)
+        assert ok, (S, e)

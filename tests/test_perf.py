@@ -63,3 +63,23 @@ def test_bf16_residual_producer_pairs_with_its_plain_residual_variant():
     assert nbytes == 3 * 8 * 64 * 40 * 40 * 2
     billed = perf.producer_billing(perf.aggregate([(prod, 0.05), (plain, 0.04), (plain, 0.02)]))
     assert billed[("cbam", (8, 64, 40, 40))][0] == pytest.approx(0.02)
+
+
+def test_fused_gate_conv_bills_the_gate_and_the_producer():
+    """A gate fused into its consumer conv (nn/tasks.py GATE_FUSE): the gate-only launches and the producer's extra
+    time go to the fused operator "<gate>_conv", whose cost counts x read once, the conv output written once and
+    the conv FLOPs at the fp16-split ceiling."""
+    gate = ("se_gate", (32, 32, 320, 320), 8)
+    fused = ("se_conv", (32, 32, 320, 320), (64, 8))
+    calls = [(SE_PROD, 0.15), (gate, 0.005), (fused, 0.14), (SE_PROD, 0.15), (gate, 0.005), (fused, 0.14)]
+    ops, backbone, path = perf.summarize(calls, steps=2)
+    o = _by_op(ops)
+    assert ("se_gate", (32, 32, 320, 320)) not in o and [b["op"] for b in backbone] == ["bias_act"]
+    f = o[("se_conv", (32, 32, 320, 320))]
+    extra = 0.15 - 32 * 32 * 320 * 320 * 4 * 2 / 8e12 * 1e3  # producer vs its plain pass at the HBM roof
+    assert f["launches"] == 2 and f["avg_ms"] == pytest.approx(0.145 + extra, abs=1e-4)
+    nbytes, flops = perf.op_cost(fused)
+    assert nbytes >= (32 * 32 * 320 * 320 + 32 * 64 * 160 * 160) * 4
+    assert flops >= 2 * 32 * 160 * 160 * 64 * 32 * 9
+    assert perf.method_peak_tflops(fused) == pytest.approx(perf.PEAK_BF16_MFMA_TFLOPS / 3)
+    assert path["t_meas_ms"] == pytest.approx(f["avg_ms"], abs=1e-3)

@@ -88,6 +88,11 @@ SIGNATURES = {
     "yolosod_debug_set_a2_outup": (_i, [_i]),
     "yolosod_debug_set_a2_pool_wide": (_i, [_i]),
     "yolosod_debug_set_conv3x3_abl": (_i, [_i]),
+    "yolosod_se_gate": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _sz, _vp]),
+    "yolosod_cbam_gates": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "yolosod_conv3x3s2_prep_bytes": (_sz, [_i, _i]),
+    "yolosod_conv3x3s2_prepare": (_i, [_vp, _i, _i, _vp, _sz, _vp]),
+    "yolosod_conv3x3s2_silu": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _sz, _vp]),
     "yolosod_debug_set_swin_tokln": (_i, [_i]),
     "yolosod_debug_set_x3_swz": (_i, [_i]),
     "yolosod_debug_set_a2_pool_px": (_i, [_i]),
@@ -331,6 +336,39 @@ def cbam_forward(x, fc0_w, fc2_w, sa_w):
     pre = _pre_stats(x, True)
     return _launch(("cbam", tuple(x.shape), hid) + ((2,) if bf else ()), x.device, ops().cbam_fwd, x, fc0_w, fc2_w,
                    sa_w, None if pre is None else pre.psum, None if pre is None else pre.pmax)
+
+
+def se_gate(x, fc1_w, fc1_b, fc2_w, fc2_b):
+    """The SE gate only (yolosod_se_gate): [B, C] fp32, for a consumer that applies x * gate itself (the fused
+    stride-2 conv, conv3x3s2_silu). fp32 activations; x's producer statistics are used when they came with it."""
+    lib = load_library()
+    B, C, H, W = x.shape
+    hid = int(fc1_w.shape[0])
+    pre = _pre_stats(x, False)
+    gate = torch.empty((B, C), dtype=torch.float32, device=x.device)
+    ws = torch.empty(int(lib.yolosod_se_workspace(B, C, H, W)), dtype=torch.uint8, device=x.device)
+    _check(_launch(("se_gate", tuple(x.shape), hid), x.device, lib.yolosod_se_gate, _dev(x, "x"), B, C, H, W,
+                   _dev(fc1_w, "fc1_w"), _dev(fc1_b, "fc1_b"), _dev(fc2_w, "fc2_w"), _dev(fc2_b, "fc2_b"), hid,
+                   None if pre is None else _dev(pre.psum, "psum"), gate.data_ptr(), ws.data_ptr(), ws.numel(),
+                   _stream(x.device)), "se_gate")
+    return gate
+
+
+def cbam_gates(x, fc0_w, fc2_w, sa_w):
+    """The CBAM gates only (yolosod_cbam_gates): (ca [B, C], sa [B, H, W]) fp32, for a consumer that applies
+    (x * ca) * sa itself (conv3x3s2_silu). fp32 activations; x's producer statistics are used when they came with it."""
+    lib = load_library()
+    B, C, H, W = x.shape
+    hid = int(fc0_w.shape[0])
+    pre = _pre_stats(x, True)
+    ca = torch.empty((B, C), dtype=torch.float32, device=x.device)
+    sa = torch.empty((B, H, W), dtype=torch.float32, device=x.device)
+    ws = torch.empty(int(lib.yolosod_cbam_workspace(B, C, H, W)), dtype=torch.uint8, device=x.device)
+    _check(_launch(("cbam_gate", tuple(x.shape), hid), x.device, lib.yolosod_cbam_gates, _dev(x, "x"), B, C, H, W,
+                   _dev(fc0_w, "fc0_w"), _dev(fc2_w, "fc2_w"), hid, _dev(sa_w, "sa_w"),
+                   None if pre is None else _dev(pre.psum, "psum"), None if pre is None else _dev(pre.pmax, "pmax"),
+                   ca.data_ptr(), sa.data_ptr(), ws.data_ptr(), ws.numel(), _stream(x.device)), "cbam_gates")
+    return ca, sa
 
 
 def ca_forward(x, conv1_w, conv1_b, bn_w, bn_b, bn_mean, bn_var, bn_eps, convh_w, convh_b, convw_w, convw_b):
@@ -744,6 +782,60 @@ def conv3x3_silu(x, bias, prep):
                                         blk.numel(), _stream(x.device))
 
     _check(_launch(("conv3x3", tuple(x.shape), 64), x.device, run), "conv3x3")
+    return y
+
+
+def conv3x3s2_ok(x, conv) -> bool:
+    """Shapes the stride-2 fused-gate conv kernel takes (yolosod_conv3x3s2_silu): fp32 contiguous NCHW on a GPU,
+    3x3 / stride 2 / pad 1 / dilation 1 / groups 1, 64 or 128 outputs, Cin a multiple of 32, output width % 4 == 0."""
+    return (x.device.type == "cuda" and x.dtype == torch.float32 and x.is_contiguous() and x.dim() == 4
+            and conv.kernel_size == (3, 3) and conv.stride == (2, 2) and conv.padding == (1, 1)
+            and conv.dilation == (1, 1) and conv.groups == 1 and conv.out_channels in (64, 128)
+            and conv.in_channels % 32 == 0 and x.shape[1] == conv.in_channels and ((x.shape[3] + 1) // 2) % 4 == 0
+            and x.numel() * 4 < 2 ** 32
+            and int(load_library().yolosod_conv3x3s2_prep_bytes(int(conv.in_channels), int(conv.out_channels))) > 0)
+
+
+def conv3x3s2_prepare(w):
+    """Prepared block (fragment-major fp16 split planes of 64 W, uint8 tensor) of a [Cout, Cin, 3, 3] fp32 weight."""
+    lib = load_library()
+    cout, cin = int(w.shape[0]), int(w.shape[1])
+    nbytes = int(lib.yolosod_conv3x3s2_prep_bytes(cin, cout))
+    if nbytes == 0:
+        raise RuntimeError(f"conv3x3s2: (Cin={cin}, Cout={cout}) unsupported")
+    blk = torch.empty(nbytes, dtype=torch.uint8, device=w.device)
+    wc = w.detach().float().contiguous()
+    _check(_launch(("conv3x3s2_prep", (cout, cin), None), w.device, lib.yolosod_conv3x3s2_prepare, _dev(wc, "weight"),
+                   cin, cout, blk.data_ptr(), nbytes, _stream(w.device)), "conv3x3s2_prepare")
+    return blk
+
+
+def conv3x3s2_silu(x, bias, prep, cout, gate_c=None, gate_p=None, key=None):
+    """SiLU(conv3x3_stride2((x * gate_c) * gate_p) + bias) on the fp16 two-term split MFMA (csrc/conv3x3s2.hip):
+    gate_c [B, Cin] (an SE / CBAM channel gate), gate_p [B, H, W] (CBAM's spatial gate), either may be None.
+    ``prep``: a callable returning the cached prepared block (conv3x3s2_prepare); ``key``: the op_timer key (default
+    ("conv3x3s2", shape, Cout, gates))."""
+    lib = load_library()
+    B, Cin, H, W = x.shape
+    y = torch.empty((B, cout, (H + 1) // 2, (W + 1) // 2), dtype=torch.float32, device=x.device)
+    b = bias.detach().float().contiguous()
+    gc = None if gate_c is None else gate_c.float().contiguous()
+    gp = None if gate_p is None else gate_p.float().contiguous()
+    if gc is not None and (tuple(gc.shape) != (B, Cin) or gc.data_ptr() % 16):
+        raise RuntimeError(f"conv3x3s2: channel gate {tuple(gc.shape)} (16-byte aligned [{B}, {Cin}] expected)")
+    if gp is not None and gp.numel() != B * H * W:
+        raise RuntimeError(f"conv3x3s2: spatial gate of {gp.numel()} values ({B * H * W} expected)")
+
+    def run():
+        blk = prep()
+        return lib.yolosod_conv3x3s2_silu(_dev(x, "x"), y.data_ptr(), B, Cin, cout, H, W, _dev(b, "bias"),
+                                          None if gc is None else _dev(gc, "gate_c"),
+                                          None if gp is None else _dev(gp, "gate_p"), blk.data_ptr(), blk.numel(),
+                                          _stream(x.device))
+
+    if key is None:
+        key = ("conv3x3s2", tuple(x.shape), cout, (gc is not None, gp is not None))
+    _check(_launch(key, x.device, run), "conv3x3s2")
     return y
 
 

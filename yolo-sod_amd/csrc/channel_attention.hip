@@ -884,11 +884,12 @@ YS_EXPORT int yolosod_plane_parts(long HW, long* seg) {
   return pp.parts;
 }
 
+// y == nullptr: the gate only, into gate_out [B][C] (its consumer applies it: yolosod_conv3x3s2_silu)
 template <class T>
 static int se_forward_impl(const T* x, T* y, int B, int C, int H, int W, const float* fc1_w, const float* fc1_b,
                            const float* fc2_w, const float* fc2_b, int hidden, const float* psum_pre, void* workspace,
-                           size_t workspace_bytes, void* stream) {
-  YS_CHECK_ARG(x && y && fc1_w && fc1_b && fc2_w && fc2_b, "se: null pointer");
+                           size_t workspace_bytes, void* stream, float* gate_out = nullptr) {
+  YS_CHECK_ARG(x && (y || gate_out) && fc1_w && fc1_b && fc2_w && fc2_b, "se: null pointer");
   YS_CHECK_ARG(B >= 0 && C > 0 && C <= 16384 && H > 0 && W > 0, "se: bad shape");
   YS_CHECK_ARG(hidden > 0 && hidden <= 64, "se: hidden=%d unsupported (1..64)", hidden);
   if (B == 0) return 0;
@@ -907,8 +908,9 @@ static int se_forward_impl(const T* x, T* y, int B, int C, int H, int W, const f
   // form's per-workgroup MLP (12800 workgroups at 32x32x320x320) cost more than the launch: SE L1 0.158 -> 0.150 ms,
   // L23 0.038 fused vs 0.040 split (same box, profiles/r04_se/); YOLOSOD_SE_FUSED_MAXHW overrides the bound
   static const long fused_max_hw = [] { const char* e = getenv("YOLOSOD_SE_FUSED_MAXHW"); return e ? atol(e) : 65536L; }();
-  const bool fused = fused_gates() && lds_fused <= 64 * 1024 && (HW < fused_max_hw || lds > 64 * 1024);
+  const bool fused = y && fused_gates() && lds_fused <= 64 * 1024 && (HW < fused_max_hw || lds > 64 * 1024);
   YS_CHECK_ARG(lds <= 64 * 1024 || fused, "se: C=%d too large for the gate kernel", C);
+  if (!y) gate = gate_out;
   // the fused apply's 8 loads per lane issued before the gate MLP (YOLOSOD_SE_PRE=0: after it)
   static const int se_pre = [] { const char* e = getenv("YOLOSOD_SE_PRE"); return (!e || atoi(e) != 0) ? 1 : 0; }();
   for (int b0 = 0; b0 < B; b0 += ipc) {
@@ -925,8 +927,10 @@ static int se_forward_impl(const T* x, T* y, int B, int C, int H, int W, const f
     } else {
       hipLaunchKernelGGL((channel_gate_kernel<false>), dim3(nb), dim3(256), lds, st, ps, nullptr, pp.parts, C,
                          1.0f / (float)HW, fc1_w, fc1_b, fc2_w, fc2_b, hidden, gate + (long)b0 * C);
-      hipLaunchKernelGGL((plane_scale_kernel<T, false>), grid, dim3(256), 0, st, x + off, y + off, gate + (long)b0 * C,
-                         C, HW, mall_reverse(), 0, nullptr, 0, 0.f, nullptr, nullptr, nullptr, nullptr, 0);
+      if (y)
+        hipLaunchKernelGGL((plane_scale_kernel<T, false>), grid, dim3(256), 0, st, x + off, y + off,
+                           gate + (long)b0 * C, C, HW, mall_reverse(), 0, nullptr, 0, 0.f, nullptr, nullptr, nullptr,
+                           nullptr, 0);
     }
   }
   YS_CHECK_LAUNCH("se");
@@ -951,6 +955,17 @@ YS_EXPORT int yolosod_se_forward_pre(const float* x, float* y, int B, int C, int
 }
 
 // bf16 storage variants (x, y: bf16 bit patterns; parameters and partials fp32)
+// The SE gate only (sigmoid(fc2(relu(fc1(mean_hw(x))))), smallobj_modules.py:87-90) into gate [B][C], for a consumer
+// that applies it itself (yolosod_conv3x3s2_silu); psum: x's per-plane partial sums from its producer, or NULL (a
+// statistics pass over x).
+YS_EXPORT int yolosod_se_gate(const float* x, int B, int C, int H, int W, const float* fc1_w, const float* fc1_b,
+                              const float* fc2_w, const float* fc2_b, int hidden, const float* psum, float* gate,
+                              void* workspace, size_t workspace_bytes, void* stream) {
+  YS_CHECK_ARG(gate, "se_gate: null gate");
+  return se_forward_impl<float>(x, nullptr, B, C, H, W, fc1_w, fc1_b, fc2_w, fc2_b, hidden, psum, workspace,
+                                workspace_bytes, stream, gate);
+}
+
 YS_EXPORT int yolosod_se_forward_bf16(const bf16_t* x, bf16_t* y, int B, int C, int H, int W, const float* fc1_w,
                                       const float* fc1_b, const float* fc2_w, const float* fc2_b, int hidden,
                                       const float* psum, void* workspace, size_t workspace_bytes, void* stream) {
@@ -975,11 +990,13 @@ YS_EXPORT size_t yolosod_cbam_workspace(int B, int C, int H, int W) {
   return s.off;
 }
 
+// y == nullptr: the gates only, into ca_out [B][C] and sa_out [B][H][W] (the consumer applies (x * ca) * sa)
 template <class T>
 static int cbam_forward_impl(const T* x, T* y, int B, int C, int H, int W, const float* fc0_w, const float* fc2_w,
                              int hidden, const float* sa_w, const float* psum_pre, const float* pmax_pre,
-                             void* workspace, size_t workspace_bytes, void* stream) {
-  YS_CHECK_ARG(x && y && fc0_w && fc2_w && sa_w, "cbam: null pointer");
+                             void* workspace, size_t workspace_bytes, void* stream, float* ca_out = nullptr,
+                             float* sa_out = nullptr) {
+  YS_CHECK_ARG(x && (y || (ca_out && sa_out)) && fc0_w && fc2_w && sa_w, "cbam: null pointer");
   YS_CHECK_ARG(B >= 0 && C > 0 && C <= 16384 && H > 0 && W > 0, "cbam: bad shape");
   YS_CHECK_ARG(hidden > 0 && hidden <= 64, "cbam: hidden=%d unsupported (1..64)", hidden);
   if (B == 0) return 0;
@@ -995,6 +1012,10 @@ static int cbam_forward_impl(const T* x, T* y, int B, int C, int H, int W, const
   float* mpart = cv.take<float>((size_t)ipc * G * 2 * HW);
   float* sa = cv.take<float>((size_t)B * HW);
   YS_CHECK_ARG(sa, "cbam: workspace too small (%zu)", workspace_bytes);
+  if (!y) {
+    ca = ca_out;
+    sa = sa_out;
+  }
   hipStream_t st = (hipStream_t)stream;
   const PartPlan pp = part_plan(HW);
   const size_t lds = sizeof(float) * (3 * (size_t)C + 128);
@@ -1037,7 +1058,7 @@ static int cbam_forward_impl(const T* x, T* y, int B, int C, int H, int W, const
         hipLaunchKernelGGL((cbam_pixel_stats_kernel<1, T, false>), gs, dim3(256), 0, st, x + off, cab, C, kCbamGroup,
                            HW, mpart, nullptr, nullptr, 0, 0.f, nullptr, nullptr, 0);
     }
-    if (sa_lds <= 48 * 1024) {  // spatial gate inside the apply pass
+    if (y && sa_lds <= 48 * 1024) {  // spatial gate inside the apply pass
       dim3 gf((unsigned)pxb, (C + kCbamApplyCh - 1) / kCbamApplyCh, nb);
       if (V == 4)
         hipLaunchKernelGGL((cbam_sa_apply_kernel<4, T>), gf, dim3(256), sa_lds, st, x + off, y + off, cab, mpart, G,
@@ -1049,6 +1070,7 @@ static int cbam_forward_impl(const T* x, T* y, int B, int C, int H, int W, const
     }
     hipLaunchKernelGGL(cbam_sa_kernel, dim3((W + 15) / 16, (H + 15) / 16, nb), dim3(256), 0, st, mpart, G, C, H, W,
                        sa_w, sab);
+    if (!y) continue;
     dim3 ga((unsigned)pxb, (C + 7) / 8, nb);
     if (V == 4)
       hipLaunchKernelGGL((cbam_apply_kernel<4, T>), ga, dim3(256), 0, st, x + off, y + off, cab, sab, C, HW);
@@ -1073,6 +1095,18 @@ YS_EXPORT int yolosod_cbam_forward_pre(const float* x, float* y, int B, int C, i
   YS_CHECK_ARG(psum && pmax, "cbam_pre: null partials");
   return cbam_forward_impl(x, y, B, C, H, W, fc0_w, fc2_w, hidden, sa_w, psum, pmax, workspace, workspace_bytes,
                            stream);
+}
+
+// The CBAM gates only (ca = sigmoid(fc(avg) + fc(max)), sa = sigmoid(conv7x7([mean_c; max_c](x * ca))),
+// cbam_block.py:14-23,33-37) into ca [B][C] and sa [B][H][W], for a consumer that applies (x * ca) * sa itself
+// (yolosod_conv3x3s2_silu); psum / pmax: x's per-plane partials from its producer, or both NULL.
+YS_EXPORT int yolosod_cbam_gates(const float* x, int B, int C, int H, int W, const float* fc0_w, const float* fc2_w,
+                                 int hidden, const float* sa_w, const float* psum, const float* pmax, float* ca,
+                                 float* sa, void* workspace, size_t workspace_bytes, void* stream) {
+  YS_CHECK_ARG((psum == nullptr) == (pmax == nullptr), "cbam_gates: give both partials or neither");
+  YS_CHECK_ARG(ca && sa, "cbam_gates: null output");
+  return cbam_forward_impl<float>(x, nullptr, B, C, H, W, fc0_w, fc2_w, hidden, sa_w, psum, pmax, workspace,
+                                  workspace_bytes, stream, ca, sa);
 }
 
 // bf16 storage variant; psum / pmax may both be NULL (statistics pass over x) or both given (from the producer)

@@ -1,0 +1,364 @@
+// 3x3 / stride 2 / pad 1 convolution + folded BN bias + SiLU on the fp16 matrix cores at fp32 accuracy, with the
+// channel / spatial gate of the MAFN operator that produces its input applied while the input is staged: the consumer
+// of SE_Block L1 (Conv(64, 3, 2) at P1 -> P2) and of CBAM_Block L4 (Conv(256, 3, 2) at P2 -> P3) in the paper YAML
+// (cfg yolov12-sod-fusion-v5-simple.yaml rows 1-2 and 4-5). The gate's output y = x * a (SE,
+// smallobj_modules.py:92) or y = (x * ca) * sa (CBAM, cbam_block.py:53-54) is formed in registers with exactly the
+// reference's fp32 products and goes straight into the convolution (conv.py:37-55 with the BN folded by fuse(),
+// torch_utils.py:238-265): the gate's apply pass (read x, write y) and the convolution's re-read of y disappear.
+//
+// Method as conv3x3.hip: v = h + l fp16 two-term splits, products ah.bh + ah.bl + al.bh on v_mfma_f32_16x16x32_f16,
+// weights x 64 split once per parameter version into fragment-major planes (for tap t, 32-channel input chunk q,
+// 16-channel output block cb and plane p, the 64 lanes' fragments are 1 KB contiguous).
+//
+// Persistent: one 512-thread workgroup per CU (LDS 94 KB: the two fp16 planes of a 9 x 65 input halo), each looping
+// over output tiles of 4 x 32 pixels and all Cout (64 or 128) channels, tiles taken from a contiguous per-XCD range.
+// Per (tile, input chunk): the staged chunk (gated, split) in LDS; the next (tile, chunk)'s input loads are spread
+// over the current chunk's nine taps (prefetch in registers); each tap's weight fragments are loaded one tap ahead.
+// Wave w computes output channel block w % NCB for NCB of the tile's 8 pixel blocks (16 output pixels of one row);
+// the pixels are the MFMA A operand, so a lane holds 4 consecutive output pixels of one channel (16-byte stores).
+#include "common.h"
+
+namespace ys {
+namespace c3s2 {
+
+constexpr float WSC = 64.0f;
+constexpr int TH = 4, TW = 32;              // output tile
+constexpr int HR = 2 * TH + 1, HC = 2 * TW + 1;  // 9 x 65 input halo
+constexpr int NPX = HR * HC;                // 585 halo pixels
+constexpr int PS = 32 + 8;                  // plane row stride (halves): stride-2 pixel reads of 16 lanes are 160 B
+                                            // apart, which puts the ds_read_b128 lane groups on distinct bank quads
+constexpr int PL = NPX * PS;                // plane (halves)
+constexpr int NT = 512;
+constexpr int NQUAD = NPX * 8;              // staged items per chunk: (4-channel quad, halo pixel)
+constexpr int NIT = (NQUAD + NT - 1) / NT;  // 10
+constexpr int NGP = (NPX + NT - 1) / NT;    // 2 spatial-gate values per thread
+
+struct Args {
+  const float* x;      // [B][Cin][H][W]
+  const h16_t* wp;     // prepared planes (fragment-major, x 64)
+  const float* bias;   // [Cout]
+  const float* gc;     // [B][Cin] channel gate (GATE & 1), 16-byte aligned
+  const float* gp;     // [B][H][W] spatial gate (GATE & 2)
+  float* y;            // [B][Cout][Ho][Wo]
+  int B, cin, H, W, Ho, Wo, tiles_x, tiles_y, ntiles;
+  unsigned* range_flag;
+  const unsigned* prep_flag;
+};
+
+// NCB: output channel blocks of 16 (Cout = 16 NCB: 4 or 8); GATE: bit 0 channel gate, bit 1 spatial gate
+template <int NCB, int GATE>
+__global__ __launch_bounds__(NT, 1) void conv3x3s2_kernel(Args p) {
+  static_assert(NCB == 4 || NCB == 8, "Cout 64 or 128");
+  constexpr int NPB = NCB;  // pixel blocks per wave (8 waves: 8 / NCB waves per channel block, 8 blocks per tile)
+  __shared__ __attribute__((aligned(16))) h16_t Pl[2 * PL];
+  __shared__ __attribute__((aligned(16))) float gcs[32];
+  __shared__ float gps[NPX];
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l15 = lane & 15, g = lane >> 4;
+  const int H = p.H, W = p.W, HWi = H * W, nq = p.cin >> 5;
+  const int cb = wid % NCB, pb0 = (wid / NCB) * NPB;
+  float rng = 0.f;
+
+  // this workgroup's tiles: XCD x = blockIdx % 8 takes the contiguous range [x per, (x + 1) per), its j-th
+  // workgroup tiles j, j + nj, ... of it (vertically / horizontally adjacent tiles share halo lines in one L2)
+  const int nj = gridDim.x >> 3, j = blockIdx.x >> 3, xcd = blockIdx.x & 7;
+  const int per = (p.ntiles + 7) >> 3;
+  const int t_beg = xcd * per + j, t_end = min((xcd + 1) * per, p.ntiles);
+  if (t_beg >= t_end) return;
+  const int n_it = ((t_end - t_beg + nj - 1) / nj) * nq;  // (tile, chunk) iterations
+
+  auto rsrc = [&](const void* base, unsigned bytes) {
+    const unsigned long long a = (unsigned long long)base;
+    return __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(a >> 32)) << 32) |
+                (unsigned)__builtin_amdgcn_readfirstlane((unsigned)a)),
+        (short)0, __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+  };
+  const __amdgpu_buffer_rsrc_t rx = rsrc(p.x, 0xffffffffu);  // per-image base in the scalar offset (checked < 2^32)
+  const __amdgpu_buffer_rsrc_t rw = rsrc(p.wp, (unsigned)(9L * nq * NCB * 2 * 1024));
+
+  // staging item e = tid + NT i: quad = e / NPX (channels 4 quad .. + 3 of the chunk), halo pixel e % NPX
+  // (consecutive threads, consecutive pixels of a halo row); packed (quad, hy, hx)
+  int pk[NIT];
+#pragma unroll
+  for (int i = 0; i < NIT; ++i) {
+    const int e = min(tid + NT * i, NQUAD - 1);
+    const int quad = e / NPX, px = e - quad * NPX;
+    const int hy = px / HC, hx = px - hy * HC;
+    pk[i] = (quad << 16) | (hy << 8) | hx;
+  }
+  auto tile_of = [&](int it, int& b, int& ty, int& tx, int& q) __attribute__((always_inline)) {
+    const int t = t_beg + (it / nq) * nj;
+    q = it - (it / nq) * nq;
+    tx = t % p.tiles_x;
+    ty = (t / p.tiles_x) % p.tiles_y;
+    b = t / (p.tiles_x * p.tiles_y);
+  };
+  // loads of (tile, chunk) iteration `it` into sv (item i, channel c = k & 3 for k = 4 i + c in [k0, k1)); okb: bit
+  // i = item i's pixel inside the image (zero padding otherwise; the load reads a clamped in-image address)
+  f32x4 sv[NIT];
+  float gcv = 0.f, gpv[NGP];
+  unsigned okb_ld = 0;
+  auto load_part = [&](int it, int k0, int k1) __attribute__((always_inline)) {
+    int b, ty, tx, q;
+    tile_of(it, b, ty, tx, q);
+    const int iy0 = 2 * TH * ty - 1, ix0 = 2 * TW * tx - 1;
+    const unsigned sb = __builtin_amdgcn_readfirstlane((unsigned)(((long)b * p.cin + 32 * q) * HWi * 4));
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) {
+      if (4 * i + 3 < k0 || 4 * i >= k1) continue;
+      const int quad = pk[i] >> 16, hy = (pk[i] >> 8) & 255, hx = pk[i] & 255;
+      const int yy = iy0 + hy, xx = ix0 + hx;
+      if (4 * i >= k0) {  // the item's first load: its in-image bit
+        const bool ok = yy >= 0 && yy < H && xx >= 0 && xx < W;
+        okb_ld = ok ? (okb_ld | (1u << i)) : (okb_ld & ~(1u << i));
+      }
+      const unsigned vo = (unsigned)((4 * quad * HWi + min(max(yy, 0), H - 1) * W + min(max(xx, 0), W - 1)) * 4);
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (4 * i + c >= k0 && 4 * i + c < k1)
+          sv[i][c] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, vo, sb + c * HWi * 4, 0));
+    }
+  };
+  // the gates of iteration `it`: channel gate of the chunk's 32 channels (thread t < 32: channel t), spatial gate of
+  // the halo pixels (thread t: pixels t + NT k), clamped unconditional loads
+  auto load_gates = [&](int it) __attribute__((always_inline)) {
+    int b, ty, tx, q;
+    tile_of(it, b, ty, tx, q);
+    if constexpr ((GATE & 1) != 0) gcv = p.gc[b * p.cin + 32 * q + (tid & 31)];
+    if constexpr ((GATE & 2) != 0) {
+      const int iy0 = 2 * TH * ty - 1, ix0 = 2 * TW * tx - 1;
+#pragma unroll
+      for (int k = 0; k < NGP; ++k) {
+        const int px = min(tid + NT * k, NPX - 1);
+        const int hy = px / HC, hx = px - hy * HC;
+        gpv[k] = p.gp[(long)b * HWi + min(max(iy0 + hy, 0), H - 1) * W + min(max(ix0 + hx, 0), W - 1)];
+      }
+    }
+  };
+  // weight fragments of (tap t, chunk q) for this wave's channel block, planes 0 / 1
+  auto wfrag = [&](int t, int q, int pl) __attribute__((always_inline)) {
+    const int st = __builtin_amdgcn_readfirstlane((((t * nq + q) * NCB + cb) * 2 + pl) * 1024);
+    return __builtin_bit_cast(f16x8_t, __builtin_amdgcn_raw_buffer_load_b128(rw, (unsigned)(lane * 16), st, 0));
+  };
+  // pixel block pb: output row pb >> 1, columns (pb & 1) 16 .. + 15; lane's halo pixel at tap (0, 0)
+  int bpx[NPB];
+#pragma unroll
+  for (int k = 0; k < NPB; ++k) {
+    const int pb = pb0 + k;
+    bpx[k] = 2 * (pb >> 1) * HC + 2 * ((pb & 1) * 16 + l15);
+  }
+  f32x4 acc[NPB];
+#pragma unroll
+  for (int k = 0; k < NPB; ++k) acc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nw = __builtin_amdgcn_readfirstlane(p.Wo);
+  const int o_ch = 16 * cb + l15;
+  const float bo = p.bias[o_ch];  // loaded once: an epilogue load would wait behind every prefetch in flight
+
+  load_part(0, 0, 4 * NIT);
+  load_gates(0);
+  for (int it = 0; it < n_it; ++it) {
+    int b, ty, tx, q;
+    tile_of(it, b, ty, tx, q);
+    const unsigned okb = okb_ld;
+    __syncthreads();  // every wave is done with the previous chunk's planes (and gates)
+    if constexpr (GATE != 0) {
+      if constexpr ((GATE & 1) != 0)
+        if (tid < 32) gcs[tid] = gcv;
+      if constexpr ((GATE & 2) != 0) {
+#pragma unroll
+        for (int k = 0; k < NGP; ++k)
+          if (tid + NT * k < NPX) gps[tid + NT * k] = gpv[k];
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) {
+      const int e = tid + NT * i;
+      if (e < NQUAD) {
+        const int quad = pk[i] >> 16, px = e - quad * NPX;
+        f32x4 v = sv[i];
+        if constexpr ((GATE & 1) != 0) v = v * *reinterpret_cast<const f32x4*>(gcs + 4 * quad);  // x * a (SE, CBAM ca)
+        if constexpr ((GATE & 2) != 0) v = v * gps[px];  // (x * ca) * sa
+        if (!((okb >> i) & 1u)) v = f32x4{0.f, 0.f, 0.f, 0.f};
+        uint2 hh, ll;
+        split4x(v, hh, ll);
+        rng = range_acc(rng, v);
+        h16_t* d = Pl + px * PS + 4 * quad;
+        *reinterpret_cast<uint2*>(d) = hh;
+        *reinterpret_cast<uint2*>(d + PL) = ll;
+      }
+    }
+    __syncthreads();
+    // next (tile, chunk)'s loads, spread over the taps behind each tap's weight prefetch (vmcnt counts in order);
+    // the last iteration reloads itself (unconditional loads: no phis waiting on every load in flight)
+    const int itn = it + 1 < n_it ? it + 1 : it;
+    f16x8_t wa[2], wn[2];
+    wa[0] = wfrag(0, q, 0);
+    wa[1] = wfrag(0, q, 1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int tn = t + 1 < 9 ? t + 1 : t;
+      wn[0] = wfrag(tn, q, 0);
+      wn[1] = wfrag(tn, q, 1);
+      if (t < 8) load_part(itn, 5 * t, t == 7 ? 4 * NIT : 5 * t + 5);
+      else load_gates(itn);
+      __builtin_amdgcn_sched_barrier(0);
+      const int toff = (t / 3) * HC + (t % 3);
+#pragma unroll
+      for (int k = 0; k < NPB; ++k) {
+        const h16_t* src = Pl + (bpx[k] + toff) * PS + 8 * g;
+        const f16x8_t xh = *reinterpret_cast<const f16x8_t*>(src);
+        const f16x8_t xl = *reinterpret_cast<const f16x8_t*>(src + PL);
+        f32x4 c = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, wa[1], acc[k], 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(xl, wa[0], c, 0, 0, 0);
+        acc[k] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, wa[0], c, 0, 0, 0);
+      }
+      wa[0] = wn[0];
+      wa[1] = wn[1];
+    }
+    if (q == nq - 1) {
+      // epilogue: lane (g, l15) of pixel block pb holds output channel 16 cb + l15, pixels (row pb >> 1, columns
+      // (pb & 1) 16 + 4 g .. + 3); every value first, then the non-temporal 16-byte stores (Wo % 4 == 0: 4 pixels
+      // all in or all out; interleaved, each store's data registers were reused behind a full vmcnt wait)
+      float* yo = p.y + ((long)b * (16 * NCB) + o_ch) * p.Ho * nw;
+      f32x4 v[NPB];
+#pragma unroll
+      for (int k = 0; k < NPB; ++k)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) v[k][jj] = silu_fast_(acc[k][jj] * (1.0f / WSC) + bo);
+#pragma unroll
+      for (int k = 0; k < NPB; ++k) {
+        const int pb = pb0 + k;
+        const int oy = ty * TH + (pb >> 1), ox = tx * TW + (pb & 1) * 16 + 4 * g;
+        if (oy < p.Ho && ox < nw) __builtin_nontemporal_store(v[k], reinterpret_cast<f32x4*>(yo + oy * nw + ox));
+        acc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  }
+  range_report(p.range_flag, rng);
+  if (p.prep_flag && p.range_flag && blockIdx.x == 0 && threadIdx.x == 0 && *p.prep_flag) *p.range_flag = 1u;
+}
+
+// W [Cout][Cin][3][3] -> fragment-major planes of 64 W: one thread per (output channel, input channel, tap). The
+// block's own range word records whether 64 W left fp16's range (re-reported by every launch).
+__global__ __launch_bounds__(256) void conv3x3s2_prep_kernel(const float* __restrict__ w, int cin, int cout,
+                                                             h16_t* __restrict__ wp, unsigned* range_flag,
+                                                             unsigned* prep_flag) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  const long n_all = (long)cout * cin * 9;
+  if (i >= n_all) return;
+  const int t = (int)(i % 9), k = (int)((i / 9) % cin), n = (int)(i / (9L * cin));
+  const float v = w[i] * WSC;
+  const _Float16 hh = (_Float16)v;
+  const _Float16 ll = (_Float16)(v - (float)hh);
+  const int nq = cin >> 5, q = k >> 5, kk = k & 31, cbk = n >> 4, ncb = cout >> 4;
+  const int ln = ((kk >> 3) << 4) + (n & 15);
+  const long base = ((long)((t * nq + q) * ncb + cbk) * 2) * 512 + ln * 8 + (kk & 7);
+  wp[base] = __builtin_bit_cast(h16_t, hh);
+  wp[base + 512] = __builtin_bit_cast(h16_t, ll);
+  const float m = fabsf(v);
+  range_report(range_flag, m);
+  range_report(prep_flag, m);
+}
+
+}  // namespace c3s2
+}  // namespace ys
+
+using namespace ys;
+
+static int s2_cu_count() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0, c = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0)
+      c = 256;
+    n = c;
+  }
+  return n;
+}
+
+// 3x3 / stride 2 / pad 1 conv with Cout 64 or 128 and Cin a multiple of 32 (<= 2048)
+YS_EXPORT size_t yolosod_conv3x3s2_prep_bytes(int cin, int cout) {
+  if (cin <= 0 || cin % 32 || cin > 2048 || (cout != 64 && cout != 128)) return 0;
+  Sizer s;
+  s.take<h16_t>((size_t)2 * cout * cin * 9);
+  s.take<unsigned>(1);
+  return s.off;
+}
+
+static bool s2_carve(void* buf, size_t bytes, int cin, int cout, h16_t** wp, unsigned** flag) {
+  Carver cv(buf, bytes);
+  *wp = cv.take<h16_t>((size_t)2 * cout * cin * 9);
+  *flag = cv.take<unsigned>(1);
+  return *flag != nullptr;
+}
+
+// Weight preparation (re-run whenever the weights change): w [cout][cin][3][3] fp32 (BN folded) -> prep block.
+YS_EXPORT int yolosod_conv3x3s2_prepare(const float* w, int cin, int cout, void* prep, size_t prep_bytes,
+                                        void* stream) {
+  YS_CHECK_ARG(w && prep, "conv3x3s2_prepare: null pointer");
+  YS_CHECK_ARG(yolosod_conv3x3s2_prep_bytes(cin, cout) > 0, "conv3x3s2_prepare: (cin=%d, cout=%d) unsupported", cin,
+               cout);
+  h16_t* wp;
+  unsigned* flag;
+  YS_CHECK_ARG(s2_carve(prep, prep_bytes, cin, cout, &wp, &flag), "conv3x3s2_prepare: block too small (%zu)",
+               prep_bytes);
+  hipStream_t st = (hipStream_t)stream;
+  if (hipMemsetAsync(flag, 0, sizeof(unsigned), st) != hipSuccess) {
+    set_error("conv3x3s2_prepare: flag reset failed");
+    return -1;
+  }
+  const long n = (long)cout * cin * 9;
+  hipLaunchKernelGGL(c3s2::conv3x3s2_prep_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, w, cin, cout,
+                     wp, range_flag_dev(), flag);
+  YS_CHECK_LAUNCH("conv3x3s2_prep");
+  return 0;
+}
+
+// y = SiLU(conv3x3_s2((x * gc) * gp, W) + bias): x [B][cin][H][W] -> y [B][cout][Ho][Wo], Ho = (H + 1) / 2,
+// Wo = (W + 1) / 2 (Wo % 4 == 0); gc [B][cin] (16-byte aligned) and gp [B][H][W] may each be NULL (no gate).
+YS_EXPORT int yolosod_conv3x3s2_silu(const float* x, float* y, int B, int cin, int cout, int H, int W,
+                                     const float* bias, const float* gc, const float* gp, const void* prep,
+                                     size_t prep_bytes, void* stream) {
+  YS_CHECK_ARG(x && y && bias && prep, "conv3x3s2: null pointer");
+  YS_CHECK_ARG(B >= 0 && H > 0 && W > 0 && yolosod_conv3x3s2_prep_bytes(cin, cout) > 0, "conv3x3s2: bad shape");
+  const int Ho = (H + 1) / 2, Wo = (W + 1) / 2;
+  YS_CHECK_ARG(Wo % 4 == 0, "conv3x3s2: output width %d not a multiple of 4", Wo);
+  YS_CHECK_ARG((long)B * cin * H * W * 4 < (1L << 32) && (long)cin * H * W < (1L << 31),
+               "conv3x3s2: input too large for 32-bit buffer offsets");
+  YS_CHECK_ARG(!gc || ((uintptr_t)gc & 15) == 0, "conv3x3s2: channel gate must be 16-byte aligned");
+  if (B == 0) return 0;
+  h16_t* wp;
+  unsigned* flag;
+  YS_CHECK_ARG(s2_carve(const_cast<void*>(prep), prep_bytes, cin, cout, &wp, &flag),
+               "conv3x3s2: prepared block too small");
+  const int tx = (Wo + c3s2::TW - 1) / c3s2::TW, ty = (Ho + c3s2::TH - 1) / c3s2::TH;
+  const long ntiles = (long)B * tx * ty;
+  YS_CHECK_ARG(ntiles < (1L << 30), "conv3x3s2: too many tiles");
+  c3s2::Args a{x, wp, bias, gc, gp, y, B, cin, H, W, Ho, Wo, tx, ty, (int)ntiles, range_flag_dev(), flag};
+  // persistent grid: one workgroup per CU (a multiple of 8 = one per XCD slot), at most one per tile
+  long grid = s2_cu_count();
+  grid = grid < ((ntiles + 7) / 8) * 8 ? grid : ((ntiles + 7) / 8) * 8;
+  grid = (grid + 7) / 8 * 8;
+  const int gate = (gc ? 1 : 0) | (gp ? 2 : 0);
+  hipStream_t st = (hipStream_t)stream;
+#define S2_LAUNCH(NCB_, G_) \
+  hipLaunchKernelGGL((c3s2::conv3x3s2_kernel<NCB_, G_>), dim3((unsigned)grid), dim3(c3s2::NT), 0, st, a)
+  if (cout == 64) {
+    if (gate == 0) S2_LAUNCH(4, 0);
+    else if (gate == 1) S2_LAUNCH(4, 1);
+    else if (gate == 2) S2_LAUNCH(4, 2);
+    else S2_LAUNCH(4, 3);
+  } else {
+    if (gate == 0) S2_LAUNCH(8, 0);
+    else if (gate == 1) S2_LAUNCH(8, 1);
+    else if (gate == 2) S2_LAUNCH(8, 2);
+    else S2_LAUNCH(8, 3);
+  }
+#undef S2_LAUNCH
+  YS_CHECK_LAUNCH("conv3x3s2");
+  return 0;
+}

@@ -168,6 +168,18 @@ class Conv(nn.Module):
     def forward(self, x):
         return self.act(self.bn(self.conv(x)))
 
+    def gated_ok(self, x) -> bool:
+        """This (fused, SiLU) Conv can run as the stride-2 kernel with its producer's gate applied at staging."""
+        return (not hasattr(self, "bn") and self.conv.bias is not None and isinstance(self.act, nn.SiLU)
+                and _hip.conv3x3s2_ok(x, self.conv))
+
+    def forward_gated(self, x, gate_c, gate_p, key):
+        """SiLU(conv((x * gate_c) * gate_p) + b): the consumer of an SE (gate_c) / CBAM (gate_c = ca, gate_p = sa)
+        whose output is never materialised (csrc/conv3x3s2.hip); ``key``: the op_timer key of the fused operator."""
+        cv = self.conv
+        prep = lambda: _cached(cv, "c3s2prep", (cv.weight,), lambda: _hip.conv3x3s2_prepare(cv.weight))  # noqa: E731
+        return _hip.conv3x3s2_silu(x, cv.bias, prep, cv.out_channels, gate_c, gate_p, key=key)
+
     def forward_fuse(self, x, out=None, res=None, out2=None, c2lo=0):
         y = conv_epilogue(self.conv, _act_code(self.act), x, out, res, self.emit_stats, out2, c2lo, self.tower)
         if y is not None:
@@ -333,6 +345,12 @@ class SE(nn.Module):
         self._maybe_build(c, x.device)
         return _hip.se_forward(x, *_f32(self, "fc", self.fc1.weight, self.fc1.bias, self.fc2.weight, self.fc2.bias))
 
+    def gate(self, x: torch.Tensor) -> torch.Tensor:
+        """The gate a [B, C] only (smallobj_modules.py:87-90), for a consumer that applies x * a itself (the
+        executor's gate fusion: Conv.forward_gated)."""
+        self._maybe_build(x.shape[1], x.device)
+        return _hip.se_gate(x, *_f32(self, "fc", self.fc1.weight, self.fc1.bias, self.fc2.weight, self.fc2.bias))
+
 
 SE_Block = SE
 
@@ -374,6 +392,14 @@ class CBAM_Block(nn.Module):
             raise RuntimeError("CBAM_Block: only the 7x7 spatial kernel is implemented")
         return _hip.cbam_forward(x, *_f32(self, "p", fc[0].weight, fc[2].weight,
                                           self.spatial_attention.conv1.weight))
+
+    def gates(self, x):
+        """(ca [B, C], sa [B, H, W]) only (cbam_block.py:14-23,33-37), for a consumer that applies (x * ca) * sa
+        itself (Conv.forward_gated)."""
+        fc = self.channel_attention.fc
+        if self.spatial_attention.conv1.kernel_size != (7, 7):
+            raise RuntimeError("CBAM_Block: only the 7x7 spatial kernel is implemented")
+        return _hip.cbam_gates(x, *_f32(self, "p", fc[0].weight, fc[2].weight, self.spatial_attention.conv1.weight))
 
 
 class h_sigmoid(nn.Module):

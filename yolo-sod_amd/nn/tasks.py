@@ -52,6 +52,10 @@ SIDE_STREAMS = max(1, int(os.environ.get("YOLOSOD_SIDE_STREAMS", "3")))
 # P5 towers (0.151 -> 0.181 ms) and the P5 part is a 25 us launch for 400 anchors, so the hot path's own time
 # grows (path roofline 0.312 -> 0.302); default: one launch after every tower
 HEAD_SPLIT = os.environ.get("YOLOSOD_HEAD_SPLIT", "0") == "1"
+# SE / CBAM whose only reader is the next layer, a fused 3x3 / stride-2 Conv (SE L1 -> L2, CBAM L4 -> L5 in the paper
+# YAML): the gate only, then the Conv applies it while staging its input (csrc/conv3x3s2.hip) - the gate's apply pass
+# and the conv's re-read of its output disappear. YOLOSOD_GATE_FUSE=0: the operator's own apply + MIOpen (A/B)
+GATE_FUSE = os.environ.get("YOLOSOD_GATE_FUSE", "1") != "0"
 # the neck's nearest 2x upsample into its Concat slice as one HIP pass (YOLOSOD_UPSAMPLE_HIP=0: PyTorch's strided
 # copy, for A/B)
 UPSAMPLE_HIP = os.environ.get("YOLOSOD_UPSAMPLE_HIP", "1") != "0"
@@ -227,6 +231,22 @@ class BaseModel(nn.Module):
         self._cplan = plan
         return plan
 
+    def _gate_consumers(self):
+        """{gate layer index: consumer Conv} for SE / CBAM layers read only by the next layer, a fused 3x3 / stride-2
+        Conv with 64 or 128 outputs (the shapes are checked again per call: Conv.gated_ok)."""
+        plan = getattr(self, "_gplan", None)
+        if plan is not None:
+            return plan
+        plan = {}
+        for k in range(len(self.model) - 1):
+            m, nxt = self.model[k], self.model[k + 1]
+            if (isinstance(m, (M.SE, M.CBAM_Block)) and k not in self.save and isinstance(nxt, M.Conv)
+                    and not isinstance(nxt, M.DWConv) and nxt.f == -1 and nxt.conv.kernel_size == (3, 3)
+                    and nxt.conv.stride == (2, 2) and nxt.conv.groups == 1 and nxt.conv.out_channels in (64, 128)):
+                plan[k] = nxt
+        self._gplan = plan
+        return plan
+
     def _predict_once_planned(self, x):
         """GPU fused forward with concat elision: for a planned Concat, the buffer is allocated when its ``-1``
         producer runs (every other input is an earlier layer's saved output, so all shapes are known), the
@@ -254,10 +274,31 @@ class BaseModel(nn.Module):
         y = []
         pend = {}  # concat index -> (buffer, channel offset of each input)
         elided = 0
+        gplan = self._gate_consumers() if GATE_FUSE else {}
+        gated = None  # (gate input, channel gate, spatial gate, fused-op key) for the next layer
         for m in self.model:
+            if gated is not None:  # the consumer Conv of the previous layer's gate
+                xg, gc, gp, key = gated
+                gated = None
+                x = m.forward_gated(xg, gc, gp, key)
+                y.append(x if m.i in self.save else None)
+                continue
             inp = x
             if m.f != -1:
                 inp = y[m.f] if isinstance(m.f, int) else [x if j == -1 else y[j] for j in m.f]
+            cons = gplan.get(m.i)
+            if cons is not None and isinstance(inp, torch.Tensor) and cons.gated_ok(inp):
+                if isinstance(m, M.SE):
+                    gc, gp = m.gate(inp), None
+                    key = ("se_conv", tuple(inp.shape), (cons.conv.out_channels, m.fc1.out_channels))
+                else:
+                    gc, gp = m.gates(inp)
+                    key = ("cbam_conv", tuple(inp.shape),
+                           (cons.conv.out_channels, m.channel_attention.fc[0].out_channels))
+                gated = (inp, gc, gp, key)
+                x = None
+                y.append(None)
+                continue
             c = plan.get(m.i)
             if c is not None and isinstance(inp, torch.Tensor) and inp.dim() == 4:
                 cat = self.model[c]

@@ -38,14 +38,21 @@ def method_peak_tflops(key) -> float:
     if elem_size(key) == 4:
         op = key[0]
         split = ((op == "swin" and key[1][1] in (64, 256) and _on("YOLOSOD_SWIN_X3"))
-                 or (op == "a2" and _on("YOLOSOD_A2_X2")) or (op == "head" and _on("YOLOSOD_HEAD_X2")))
+                 or (op == "a2" and _on("YOLOSOD_A2_X2")) or (op == "head" and _on("YOLOSOD_HEAD_X2"))
+                 or op in FUSED_CONV)
         if split:
             return PEAK_BF16_MFMA_TFLOPS / 3
     return peak_tflops(key)
 
 
+# gate operators whose apply their consumer conv does (nn/tasks.py GATE_FUSE): the fused operator "<gate>_conv" =
+# the gate's own launches ("<gate>_gate", billed to it) + the stride-2 conv that applies the gate while staging its
+# input (csrc/conv3x3s2.hip, fp16 two-term splits); its roofline counts its real I/O (x read once, the conv output
+# written once) and the conv's FLOPs
+FUSED_CONV = {"se_conv": "se", "cbam_conv": "cbam"}
+GATE_ONLY = {"se_gate": "se_conv", "cbam_gate": "cbam_conv"}
 # operators of the SURVEY 8(a) path (rooflined); other keys the op_timer records are backbone conv kernels
-PATH_OPS = frozenset({"se", "cbam", "ca", "a2", "swin", "mamba", "decode", "head", "nms"})
+PATH_OPS = frozenset({"se", "cbam", "ca", "a2", "swin", "mamba", "decode", "head", "nms", *FUSED_CONV})
 
 
 def swin_geom(H, W, ws=7):
@@ -64,6 +71,14 @@ def op_cost(key):
 
 def _op_cost(key, E):
     op, shape, extra = key
+    if op in FUSED_CONV:  # gate (statistics from the producer, MLP, CBAM's spatial map) + gated stride-2 conv
+        B, C, H, W = shape
+        cout, hid = extra
+        Ho, Wo = (H + 1) // 2, (W + 1) // 2
+        act = B * C * H * W * E + B * cout * Ho * Wo * E + (B * H * W * F32 if op == "cbam_conv" else 0)
+        w = (cout * C * 9 + cout + 2 * C * hid + C + hid + (98 if op == "cbam_conv" else 0)) * F32
+        flops = 2 * B * Ho * Wo * cout * C * 9 + B * C * H * W * (1 if op == "se_conv" else 2)
+        return act + w, flops
     if op in ("se", "cbam", "ca"):
         B, C, H, W = shape
         hid = extra
@@ -201,15 +216,23 @@ def summarize(calls, steps):
     billed producer extra; path_roofline = sum_k t_k^min / sum_k t_k^meas."""
     agg = aggregate(calls)
     billed = producer_billing(agg)
+    # gate-only launches: billed (per launch of the fused operator) to the fused operator of the same gate shape
+    gate_ms = {}
+    for key, (tot, n) in agg.items():
+        if key[0] in GATE_ONLY:
+            k2 = (GATE_ONLY[key[0]], tuple(key[1]))
+            gate_ms[k2] = gate_ms.get(k2, 0.0) + tot
     ops, backbone = [], []
     for key, (tot, n) in agg.items():
+        if key[0] in GATE_ONLY:
+            continue
         if key[0] not in PATH_OPS:  # backbone conv kernels of this library: outside the path roofline
             backbone.append({"op": key[0], "shape": list(key[1]), "extra": str(key[2]), "launches": n,
                              "total_ms_per_step": round(tot / steps, 4)})
             continue
         nbytes, flops = op_cost(key)
-        kern = tot / n
-        ext, src = billed.get((key[0], tuple(key[1])), (0.0, None))
+        kern = tot / n + gate_ms.get((key[0], tuple(key[1])), 0.0) / n
+        ext, src = billed.get((FUSED_CONV.get(key[0], key[0]), tuple(key[1])), (0.0, None))
         avg = kern + ext
         bound = bound_of(key)
         tm, tm_d = t_min_ms(key, method=True), t_min_ms(key)
