@@ -293,6 +293,9 @@ size_t yolosod_conv3x3s2_prep_bytes(int cin, int cout);
 int yolosod_conv3x3s2_prepare(const float* w, int cin, int cout, void* prep, size_t prep_bytes, void* stream);
 int yolosod_conv3x3s2_silu(const float* x, float* y, int B, int cin, int cout, int H, int W, const float* bias,
                            const float* gc, const float* gp, const void* prep, size_t prep_bytes, void* stream);
+/* Timing hook: ablation variants of the stride-2 conv kernel at Cout 64 with a channel gate (csrc/conv3x3s2.hip; WRONG
+ * results for abl != 0 - scripts/bench_conv3x3s2.py only). Returns the previous value. */
+int yolosod_debug_set_conv3x3s2_abl(int abl);
 /* Timing hook: ablation variants of the 3x3 conv kernel (csrc/conv3x3.hip; WRONG results for any abl != 0 and
  * != 16 - scripts/bench_conv3x3.py only). Returns the previous value. */
 int yolosod_debug_set_conv3x3_abl(int abl);

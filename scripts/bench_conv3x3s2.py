@@ -29,6 +29,22 @@ def timed(fn, reps=30):
     return e0.elapsed_time(e1) / reps
 
 
+ABL = [int(a) for a in sys.argv[1].split(",")] if len(sys.argv) > 1 else []
+if ABL:  # timing ablations at the SE L1 -> L2 shape (wrong results): yolosod_debug_set_conv3x3s2_abl
+    lib = _hip.load_library()
+    (B, cin, H, W), cout, _ = SHAPES[0]
+    x = torch.randn(B, cin, H, W, device=dev)
+    w = torch.randn(cout, cin, 3, 3, device=dev) * 0.05
+    b = torch.randn(cout, device=dev) * 0.1
+    gc = torch.sigmoid(torch.randn(B, cin, device=dev))
+    prep = _hip.conv3x3s2_prepare(w)
+    for a in ABL:
+        lib.yolosod_debug_set_conv3x3s2_abl(a)
+        t = timed(lambda: _hip.conv3x3s2_silu(x, b, lambda: prep, cout, gc))
+        print(f"abl {a:2d} {t:7.3f} ms", flush=True)
+    lib.yolosod_debug_set_conv3x3s2_abl(0)
+    sys.exit(0)
+
 for shape, cout, gates in SHAPES:
     B, cin, H, W = shape
     x = torch.randn(shape, device=dev)

@@ -1,0 +1,22 @@
+"""A few launches of the SE L1 -> L2 fused stride-2 conv (for rocprofv3 --pmc passes). GPU only."""
+import sys
+from pathlib import Path
+
+import torch
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+import yolosod_import  # noqa: E402,F401
+from yolosod_amd import _hip  # noqa: E402
+
+dev = torch.device("cuda", 0)
+B, cin, H, W, cout = 32, 32, 320, 320, 64
+x = torch.randn(B, cin, H, W, device=dev)
+w = torch.randn(cout, cin, 3, 3, device=dev) * 0.05
+b = torch.randn(cout, device=dev) * 0.1
+gc = torch.sigmoid(torch.randn(B, cin, device=dev))
+prep = _hip.conv3x3s2_prepare(w)
+for _ in range(5):
+    _hip.conv3x3s2_silu(x, b, lambda: prep, cout, gc)
+torch.cuda.synchronize()
+print("ok")

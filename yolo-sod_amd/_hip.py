@@ -88,6 +88,7 @@ SIGNATURES = {
     "yolosod_debug_set_a2_outup": (_i, [_i]),
     "yolosod_debug_set_a2_pool_wide": (_i, [_i]),
     "yolosod_debug_set_conv3x3_abl": (_i, [_i]),
+    "yolosod_debug_set_conv3x3s2_abl": (_i, [_i]),
     "yolosod_se_gate": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _sz, _vp]),
     "yolosod_cbam_gates": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "yolosod_conv3x3s2_prep_bytes": (_sz, [_i, _i]),

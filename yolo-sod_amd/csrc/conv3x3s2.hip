@@ -45,8 +45,10 @@ struct Args {
   const unsigned* prep_flag;
 };
 
-// NCB: output channel blocks of 16 (Cout = 16 NCB: 4 or 8); GATE: bit 0 channel gate, bit 1 spatial gate
-template <int NCB, int GATE>
+// NCB: output channel blocks of 16 (Cout = 16 NCB: 4 or 8); GATE: bit 0 channel gate, bit 1 spatial gate.
+// ABL: timing ablations (wrong results; yolosod_debug_set_conv3x3s2_abl): 1 no input loads, 2 every weight fragment
+// from one address, 4 no MFMA (a VALU stand-in keeps the LDS reads), 8 no output stores
+template <int NCB, int GATE, int ABL = 0>
 __global__ __launch_bounds__(NT, 1) void conv3x3s2_kernel(Args p) {
   static_assert(NCB == 4 || NCB == 8, "Cout 64 or 128");
   constexpr int NPB = NCB;  // pixel blocks per wave (8 waves: 8 / NCB waves per channel block, 8 blocks per tile)
@@ -117,7 +119,8 @@ __global__ __launch_bounds__(NT, 1) void conv3x3s2_kernel(Args p) {
 #pragma unroll
       for (int c = 0; c < 4; ++c)
         if (4 * i + c >= k0 && 4 * i + c < k1)
-          sv[i][c] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, vo, sb + c * HWi * 4, 0));
+          sv[i][c] = (ABL & 1) ? 0.25f + (float)c
+                               : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, vo, sb + c * HWi * 4, 0));
     }
   };
   // the gates of iteration `it`: channel gate of the chunk's 32 channels (thread t < 32: channel t), spatial gate of
@@ -138,7 +141,7 @@ __global__ __launch_bounds__(NT, 1) void conv3x3s2_kernel(Args p) {
   };
   // weight fragments of (tap t, chunk q) for this wave's channel block, planes 0 / 1
   auto wfrag = [&](int t, int q, int pl) __attribute__((always_inline)) {
-    const int st = __builtin_amdgcn_readfirstlane((((t * nq + q) * NCB + cb) * 2 + pl) * 1024);
+    const int st = (ABL & 2) ? pl * 1024 : __builtin_amdgcn_readfirstlane((((t * nq + q) * NCB + cb) * 2 + pl) * 1024);
     return __builtin_bit_cast(f16x8_t, __builtin_amdgcn_raw_buffer_load_b128(rw, (unsigned)(lane * 16), st, 0));
   };
   // pixel block pb: output row pb >> 1, columns (pb & 1) 16 .. + 15; lane's halo pixel at tap (0, 0)
@@ -211,9 +214,13 @@ __global__ __launch_bounds__(NT, 1) void conv3x3s2_kernel(Args p) {
         const h16_t* src = Pl + (bpx[k] + toff) * PS + 8 * g;
         const f16x8_t xh = *reinterpret_cast<const f16x8_t*>(src);
         const f16x8_t xl = *reinterpret_cast<const f16x8_t*>(src + PL);
-        f32x4 c = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, wa[1], acc[k], 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(xl, wa[0], c, 0, 0, 0);
-        acc[k] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, wa[0], c, 0, 0, 0);
+        if constexpr ((ABL & 4) != 0) {
+          acc[k][0] += (float)xh[0] * (float)wa[0][0] + (float)xl[1] * (float)wa[1][1];
+        } else {
+          f32x4 c = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, wa[1], acc[k], 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(xl, wa[0], c, 0, 0, 0);
+          acc[k] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, wa[0], c, 0, 0, 0);
+        }
       }
       wa[0] = wn[0];
       wa[1] = wn[1];
@@ -232,11 +239,216 @@ __global__ __launch_bounds__(NT, 1) void conv3x3s2_kernel(Args p) {
       for (int k = 0; k < NPB; ++k) {
         const int pb = pb0 + k;
         const int oy = ty * TH + (pb >> 1), ox = tx * TW + (pb & 1) * 16 + 4 * g;
-        if (oy < p.Ho && ox < nw) __builtin_nontemporal_store(v[k], reinterpret_cast<f32x4*>(yo + oy * nw + ox));
+        if (oy < p.Ho && ox < nw && (!(ABL & 8) || v[k][0] == -1.2345e30f))
+          __builtin_nontemporal_store(v[k], reinterpret_cast<f32x4*>(yo + oy * nw + ox));
         acc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
     }
   }
+  range_report(p.range_flag, rng);
+  if (p.prep_flag && p.range_flag && blockIdx.x == 0 && threadIdx.x == 0 && *p.prep_flag) *p.range_flag = 1u;
+}
+
+// Cout 64 / Cin 32 (one input chunk: the SE L1 -> Conv L2 shape): the weights are held in registers for the kernel's
+// lifetime (wave w: output channel block w & 3, all taps, 72 VGPRs), so no load but the next tile's input is in flight
+// during the taps and all of them are issued right after the staging (no wait for a tap's weights waits behind them);
+// wave w computes output rows 2 (w >> 2), + 1 (four pixel blocks) of its 16 channels. The epilogue goes through an
+// LDS tile [row][channel][32 px (+4)] and leaves as 128-byte rows (8 lanes per row) while the next tile is staged (the
+// general kernel's 64-byte lane-group stores were store-issue bound).
+constexpr int ES = TW + 4;  // epilogue row stride (floats): 144-byte channel rows, conflict-free 16-byte writes
+// THk output rows per tile, NTk threads per workgroup (THk = 2, NTk = 256: 72 KB of LDS, two workgroups per CU whose
+// staging / compute phases interleave and whose input prefetches are both in flight)
+template <int GATE, int ABL, int THk, int NTk>
+__global__ __launch_bounds__(NTk, 512 / NTk) void conv3x3s2_rw_kernel(Args p) {
+  constexpr int HRk = 2 * THk + 1, NPXk = HRk * HC, PLk = NPXk * PS, NQUADk = NPXk * 8;
+  constexpr int NITk = (NQUADk + NTk - 1) / NTk, NGPk = (NPXk + NTk - 1) / NTk;
+  static_assert(NITk <= 32, "okb bits");
+  __shared__ __attribute__((aligned(16))) h16_t Pl[2 * PLk];
+  __shared__ __attribute__((aligned(16))) float Ep[THk * 64 * ES];
+  __shared__ __attribute__((aligned(16))) float gcs[32];
+  __shared__ float gps[(GATE & 2) ? NPXk : 1];
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l15 = lane & 15, g = lane >> 4;
+  const int H = p.H, W = p.W, HWi = H * W;
+  const int rp = wid >> 2, cb = wid & 3;  // output rows 2 rp, 2 rp + 1 of the tile; channel block cb
+  float rng = 0.f;
+
+  const int nj = gridDim.x >> 3, j = blockIdx.x >> 3, xcd = blockIdx.x & 7;
+  const int per = (p.ntiles + 7) >> 3;
+  const int t_beg = xcd * per + j, t_end = min((xcd + 1) * per, p.ntiles);
+  if (t_beg >= t_end) return;
+  const int n_it = (t_end - t_beg + nj - 1) / nj;
+
+  auto rsrc = [&](const void* base, unsigned bytes) {
+    const unsigned long long a = (unsigned long long)base;
+    return __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(a >> 32)) << 32) |
+                (unsigned)__builtin_amdgcn_readfirstlane((unsigned)a)),
+        (short)0, __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+  };
+  const __amdgpu_buffer_rsrc_t rx = rsrc(p.x, 0xffffffffu);
+  const __amdgpu_buffer_rsrc_t rw = rsrc(p.wp, (unsigned)(9L * 4 * 2 * 1024));
+
+  // this wave's weights: channel block cb, taps t, planes 0 / 1
+  f16x8_t wr[9][2];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int pl = 0; pl < 2; ++pl)
+      wr[t][pl] = __builtin_bit_cast(
+          f16x8_t, __builtin_amdgcn_raw_buffer_load_b128(rw, (unsigned)(lane * 16), ((t * 4 + cb) * 2 + pl) * 1024, 0));
+  // staging item e = tid + NTk i: quad = e / NPXk (channels 4 quad .. + 3), halo pixel e % NPXk = (hy, hx); its element
+  // offset in the image for tile origin (0, 0) and its (hy, hx)
+  int pk[NITk], el0[NITk];
+#pragma unroll
+  for (int i = 0; i < NITk; ++i) {
+    const int e = min(tid + NTk * i, NQUADk - 1);
+    const int quad = e / NPXk, px = e - quad * NPXk;
+    const int hy = px / HC, hx = px - hy * HC;
+    pk[i] = (quad << 16) | (hy << 8) | hx;
+    el0[i] = 4 * quad * HWi + hy * W + hx;
+  }
+  struct Tile {
+    int b, ty, tx;
+  };
+  auto tile_of = [&](int it) __attribute__((always_inline)) {
+    const int t = t_beg + it * nj;
+    Tile tl;
+    tl.tx = t % p.tiles_x;
+    tl.ty = (t / p.tiles_x) % p.tiles_y;
+    tl.b = t / (p.tiles_x * p.tiles_y);
+    return tl;
+  };
+  f32x4 sv[NITk];
+  float gcv = 0.f, gpv[NGPk];
+  unsigned okb_ld = 0;
+  // the tile's input: one buffer resource per image (range = the image): offsets of rows above the image are
+  // negative (huge as unsigned: out of range, the load returns 0) and every other out-of-image pixel reads some
+  // in-image value that okb masks to the zero padding - no clamping on the load path
+  auto load_tile = [&](const Tile& tl) __attribute__((always_inline)) {
+    const int iy0 = 2 * THk * tl.ty - 1, ix0 = 2 * TW * tl.tx - 1;
+    const __amdgpu_buffer_rsrc_t ri = rsrc(p.x + (long)tl.b * 32 * HWi, (unsigned)(32 * HWi * 4));
+    const int toff = iy0 * W + ix0;
+    const bool interior = iy0 >= 0 && ix0 >= 0 && iy0 + HRk <= H && ix0 + HC <= W;
+    unsigned okb = 0xffffffffu;
+    if (!interior) {
+      okb = 0;
+#pragma unroll
+      for (int i = 0; i < NITk; ++i) {
+        const int hy = (pk[i] >> 8) & 255, hx = pk[i] & 255;
+        okb |= ((unsigned)(iy0 + hy) < (unsigned)H && (unsigned)(ix0 + hx) < (unsigned)W) ? (1u << i) : 0u;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NITk; ++i) {
+      const unsigned vo = (unsigned)((el0[i] + toff) * 4);
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        sv[i][c] = (ABL & 1) ? 0.25f + (float)c
+                             : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ri, vo + c * HWi * 4, 0, 0));
+    }
+    okb_ld = okb;
+    if constexpr ((GATE & 1) != 0) gcv = p.gc[tl.b * 32 + (tid & 31)];
+    if constexpr ((GATE & 2) != 0) {
+#pragma unroll
+      for (int k = 0; k < NGPk; ++k) {
+        const int px = min(tid + NTk * k, NPXk - 1);
+        const int hy = px / HC, hx = px - hy * HC;
+        gpv[k] = p.gp[(long)tl.b * HWi + min(max(iy0 + hy, 0), H - 1) * W + min(max(ix0 + hx, 0), W - 1)];
+      }
+    }
+  };
+  int bpx[4];  // pixel block k: output row 2 rp + (k >> 1), columns (k & 1) 16 .. + 15
+#pragma unroll
+  for (int k = 0; k < 4; ++k) bpx[k] = 2 * (2 * rp + (k >> 1)) * HC + 2 * ((k & 1) * 16 + l15);
+  const int nw = __builtin_amdgcn_readfirstlane(p.Wo);
+  const float bo = p.bias[16 * cb + l15];
+  // global stores of the epilogue tile: item idx = tid + NTk m: row idx >> 9, channel (idx >> 3) & 63, pixels
+  // 4 (idx & 7) .. + 3 (8 lanes per 128-byte row)
+  auto store_tile = [&](const Tile& tl) __attribute__((always_inline)) {
+#pragma unroll
+    for (int m = 0; m < THk * 512 / NTk; ++m) {
+      const int idx = tid + NTk * m;
+      const int r = idx >> 9, ch = (idx >> 3) & 63, px4 = idx & 7;
+      const int ox = tl.tx * TW + 4 * px4, oy = tl.ty * THk + r;
+      const f32x4 v = *reinterpret_cast<const f32x4*>(Ep + (r * 64 + ch) * ES + 4 * px4);
+      if (oy < p.Ho && ox < nw && (!(ABL & 8) || v[0] == -1.2345e30f))
+        __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p.y + (((long)tl.b * 64 + ch) * p.Ho + oy) * nw + ox));
+    }
+  };
+
+  Tile cur = tile_of(0), prev = cur;
+  load_tile(cur);
+  for (int it = 0; it < n_it; ++it) {
+    const unsigned okb = okb_ld;
+    __syncthreads();  // every wave is done with the previous tile's planes, gates and epilogue tile writes
+    if constexpr (GATE != 0) {
+      if constexpr ((GATE & 1) != 0)
+        if (tid < 32) gcs[tid] = gcv;
+      if constexpr ((GATE & 2) != 0) {
+#pragma unroll
+        for (int k = 0; k < NGPk; ++k)
+          if (tid + NTk * k < NPXk) gps[tid + NTk * k] = gpv[k];
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < NITk; ++i) {
+      const int e = tid + NTk * i;
+      if (e < NQUADk) {
+        const int quad = pk[i] >> 16, px = e - quad * NPXk;
+        f32x4 v = sv[i];
+        if constexpr ((GATE & 1) != 0) v = v * *reinterpret_cast<const f32x4*>(gcs + 4 * quad);
+        if constexpr ((GATE & 2) != 0) v = v * gps[px];
+        if (!((okb >> i) & 1u)) v = f32x4{0.f, 0.f, 0.f, 0.f};
+        uint2 hh, ll;
+        split4x(v, hh, ll);
+        rng = range_acc(rng, v);
+        h16_t* d = Pl + px * PS + 4 * quad;
+        *reinterpret_cast<uint2*>(d) = hh;
+        *reinterpret_cast<uint2*>(d + PLk) = ll;
+      }
+    }
+    // the previous tile's output rows, issued after the staging's waits for this tile's input (a store ahead of
+    // them made every wait a full vmcnt(0): the store count under its bounds branch is unknown)
+    if (it > 0) store_tile(prev);
+    __syncthreads();
+    prev = cur;
+    if (it + 1 < n_it) cur = tile_of(it + 1);
+    load_tile(cur);  // the next tile's input (the last iteration reloads its own): in flight during every tap
+    __builtin_amdgcn_sched_barrier(0);
+    f32x4 acc[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int toff = (t / 3) * HC + (t % 3);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const h16_t* src = Pl + (bpx[k] + toff) * PS + 8 * g;
+        const f16x8_t xh = *reinterpret_cast<const f16x8_t*>(src);
+        const f16x8_t xl = *reinterpret_cast<const f16x8_t*>(src + PLk);
+        if constexpr ((ABL & 4) != 0) {
+          acc[k][0] += (float)xh[0] * (float)wr[t][0][0] + (float)xl[1] * (float)wr[t][1][1];
+        } else {
+          f32x4 c = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, wr[t][1], acc[k], 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(xl, wr[t][0], c, 0, 0, 0);
+          acc[k] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, wr[t][0], c, 0, 0, 0);
+        }
+      }
+    }
+    // epilogue tile: lane (g, l15) of pixel block k holds channel 16 cb + l15, pixels (k & 1) 16 + 4 g .. + 3 of
+    // row 2 rp + (k >> 1)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      f32x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = silu_fast_(acc[k][e] * (1.0f / WSC) + bo);
+      *reinterpret_cast<f32x4*>(Ep + ((2 * rp + (k >> 1)) * 64 + 16 * cb + l15) * ES + 16 * (k & 1) + 4 * g) = v;
+    }
+  }
+  __syncthreads();
+  store_tile(prev);
   range_report(p.range_flag, rng);
   if (p.prep_flag && p.range_flag && blockIdx.x == 0 && threadIdx.x == 0 && *p.prep_flag) *p.range_flag = 1u;
 }
@@ -267,6 +479,13 @@ __global__ __launch_bounds__(256) void conv3x3s2_prep_kernel(const float* __rest
 }  // namespace ys
 
 using namespace ys;
+
+static int g_s2_abl = 0;
+YS_EXPORT int yolosod_debug_set_conv3x3s2_abl(int abl) {
+  const int old = g_s2_abl;
+  g_s2_abl = abl;
+  return old;
+}
 
 static int s2_cu_count() {
   static int n = 0;
@@ -347,7 +566,57 @@ YS_EXPORT int yolosod_conv3x3s2_silu(const float* x, float* y, int B, int cin, i
   hipStream_t st = (hipStream_t)stream;
 #define S2_LAUNCH(NCB_, G_) \
   hipLaunchKernelGGL((c3s2::conv3x3s2_kernel<NCB_, G_>), dim3((unsigned)grid), dim3(c3s2::NT), 0, st, a)
-  if (cout == 64) {
+  // YOLOSOD_S2_RW: 2 (default) register-resident weights, 2-row tiles, two 256-thread workgroups per CU; 1: 4-row
+  // tiles, one 512-thread workgroup; 0: the general kernel
+  static const int rw_mode = [] { const char* e = getenv("YOLOSOD_S2_RW"); return e ? atoi(e) : 2; }();
+  if (cout == 64 && cin == 32 && rw_mode == 2 && g_s2_abl < 100) {
+    c3s2::Args a2 = a;
+    a2.tiles_y = (Ho + 1) / 2;
+    const long nt2 = (long)B * a2.tiles_y * tx;
+    a2.ntiles = (int)nt2;
+    long g2 = 2L * s2_cu_count();
+    g2 = g2 < ((nt2 + 7) / 8) * 8 ? g2 : ((nt2 + 7) / 8) * 8;
+    g2 = (g2 + 7) / 8 * 8;
+#define S2RW_LAUNCH(G_, A_) \
+  hipLaunchKernelGGL((c3s2::conv3x3s2_rw_kernel<G_, A_, 2, 256>), dim3((unsigned)g2), dim3(256), 0, st, a2)
+    if (gate == 1) {
+      switch (g_s2_abl) {
+        case 1: S2RW_LAUNCH(1, 1); break;
+        case 4: S2RW_LAUNCH(1, 4); break;
+        case 8: S2RW_LAUNCH(1, 8); break;
+        case 13: S2RW_LAUNCH(1, 13); break;
+        default: S2RW_LAUNCH(1, 0); break;
+      }
+    } else if (gate == 0) S2RW_LAUNCH(0, 0);
+    else if (gate == 2) S2RW_LAUNCH(2, 0);
+    else S2RW_LAUNCH(3, 0);
+#undef S2RW_LAUNCH
+  } else if (cout == 64 && cin == 32 && rw_mode == 1 && g_s2_abl < 100) {  // 4-row tiles, 512 threads
+#define S2RW_LAUNCH(G_, A_) \
+  hipLaunchKernelGGL((c3s2::conv3x3s2_rw_kernel<G_, A_, 4, 512>), dim3((unsigned)grid), dim3(c3s2::NT), 0, st, a)
+    if (gate == 1) {
+      switch (g_s2_abl) {
+        case 1: S2RW_LAUNCH(1, 1); break;
+        case 4: S2RW_LAUNCH(1, 4); break;
+        case 8: S2RW_LAUNCH(1, 8); break;
+        case 13: S2RW_LAUNCH(1, 13); break;
+        default: S2RW_LAUNCH(1, 0); break;
+      }
+    } else if (gate == 0) S2RW_LAUNCH(0, 0);
+    else if (gate == 2) S2RW_LAUNCH(2, 0);
+    else S2RW_LAUNCH(3, 0);
+#undef S2RW_LAUNCH
+  } else if (g_s2_abl && cout == 64 && gate == 1) {  // timing ablations of the general kernel (abl + 100)
+    switch (g_s2_abl - 100) {
+      case 1: hipLaunchKernelGGL((c3s2::conv3x3s2_kernel<4, 1, 1>), dim3((unsigned)grid), dim3(c3s2::NT), 0, st, a); break;
+      case 2: hipLaunchKernelGGL((c3s2::conv3x3s2_kernel<4, 1, 2>), dim3((unsigned)grid), dim3(c3s2::NT), 0, st, a); break;
+      case 4: hipLaunchKernelGGL((c3s2::conv3x3s2_kernel<4, 1, 4>), dim3((unsigned)grid), dim3(c3s2::NT), 0, st, a); break;
+      case 8: hipLaunchKernelGGL((c3s2::conv3x3s2_kernel<4, 1, 8>), dim3((unsigned)grid), dim3(c3s2::NT), 0, st, a); break;
+      case 12: hipLaunchKernelGGL((c3s2::conv3x3s2_kernel<4, 1, 12>), dim3((unsigned)grid), dim3(c3s2::NT), 0, st, a); break;
+      case 15: hipLaunchKernelGGL((c3s2::conv3x3s2_kernel<4, 1, 15>), dim3((unsigned)grid), dim3(c3s2::NT), 0, st, a); break;
+      default: S2_LAUNCH(4, 1); break;
+    }
+  } else if (cout == 64) {
     if (gate == 0) S2_LAUNCH(4, 0);
     else if (gate == 1) S2_LAUNCH(4, 1);
     else if (gate == 2) S2_LAUNCH(4, 2);
