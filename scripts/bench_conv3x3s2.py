@@ -12,8 +12,9 @@ import yolosod_import  # noqa: E402,F401
 from yolosod_amd import _hip  # noqa: E402
 
 dev = torch.device("cuda", 0)
-# (input shape, Cout, gates): SE L1 -> L2 and CBAM L4 -> L5 (n640), SE L1 -> L2 (m640)
-SHAPES = [((32, 32, 320, 320), 64, "c"), ((32, 64, 160, 160), 128, "cp"), ((64, 64, 320, 320), 128, "c")]
+# (input shape, Cout, gates): SE L1 -> L2 and CBAM L4 -> L5 (n640, n1280), SE L1 -> L2 (m640 shape)
+SHAPES = [((32, 32, 320, 320), 64, "c"), ((32, 64, 160, 160), 128, "cp"), ((8, 32, 640, 640), 64, "c"),
+          ((8, 64, 320, 320), 128, "cp"), ((64, 64, 320, 320), 128, "c")]
 
 
 def timed(fn, reps=30):

@@ -453,6 +453,222 @@ __global__ __launch_bounds__(NTk, 512 / NTk) void conv3x3s2_rw_kernel(Args p) {
   if (p.prep_flag && p.range_flag && blockIdx.x == 0 && threadIdx.x == 0 && *p.prep_flag) *p.range_flag = 1u;
 }
 
+// Any (Cout 64 / 128, Cin multiple of 32) with 2-row tiles and 256-thread workgroups, three per CU (LDS 54 KB): the
+// general kernel's streamed weights (one tap ahead, the next (tile, chunk)'s input spread over the taps behind them;
+// two per CU at Cout 128, whose 8 accumulator tiles per wave need more than 168 registers)
+// with the register-weight kernel's unclamped per-image buffer addressing; wave w computes channel blocks
+// CBW w .. + CBW - 1 (CBW = NCB / 4) for all four pixel blocks of the tile (rows 0, 1 x two 16-column blocks).
+template <int NCB, int GATE>
+__global__ __launch_bounds__(256, NCB == 8 ? 2 : 3) void conv3x3s2_t2_kernel(Args p) {
+  constexpr int THk = 2, NTk = 256, HRk = 2 * THk + 1, NPXk = HRk * HC, PLk = NPXk * PS, NQUADk = NPXk * 8;
+  constexpr int NITk = (NQUADk + NTk - 1) / NTk, NGPk = (NPXk + NTk - 1) / NTk, CBW = NCB / 4;
+  static_assert(NCB == 4 || NCB == 8, "Cout 64 or 128");
+  __shared__ __attribute__((aligned(16))) h16_t Pl[2 * PLk];
+  __shared__ __attribute__((aligned(16))) float gcs[32];
+  __shared__ float gps[(GATE & 2) ? NPXk : 1];
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l15 = lane & 15, g = lane >> 4;
+  const int H = p.H, W = p.W, HWi = H * W, nq = p.cin >> 5;
+  float rng = 0.f;
+
+  const int nj = gridDim.x >> 3, j = blockIdx.x >> 3, xcd = blockIdx.x & 7;
+  const int per = (p.ntiles + 7) >> 3;
+  const int t_beg = xcd * per + j, t_end = min((xcd + 1) * per, p.ntiles);
+  if (t_beg >= t_end) return;
+  const int n_it = ((t_end - t_beg + nj - 1) / nj) * nq;
+
+  auto rsrc = [&](const void* base, unsigned bytes) {
+    const unsigned long long a = (unsigned long long)base;
+    return __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(a >> 32)) << 32) |
+                (unsigned)__builtin_amdgcn_readfirstlane((unsigned)a)),
+        (short)0, __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+  };
+  const __amdgpu_buffer_rsrc_t rw = rsrc(p.wp, (unsigned)(9L * nq * NCB * 2 * 1024));
+  int pk[NITk], el0[NITk];
+#pragma unroll
+  for (int i = 0; i < NITk; ++i) {
+    const int e = min(tid + NTk * i, NQUADk - 1);
+    const int quad = e / NPXk, px = e - quad * NPXk;
+    const int hy = px / HC, hx = px - hy * HC;
+    pk[i] = (quad << 16) | (hy << 8) | hx;
+    el0[i] = 4 * quad * HWi + hy * W + hx;
+  }
+  struct It {
+    int b, ty, tx, q;
+  };
+  auto it_of = [&](int it) __attribute__((always_inline)) {
+    const int t = t_beg + (it / nq) * nj;
+    It r;
+    r.q = it - (it / nq) * nq;
+    r.tx = t % p.tiles_x;
+    r.ty = (t / p.tiles_x) % p.tiles_y;
+    r.b = t / (p.tiles_x * p.tiles_y);
+    return r;
+  };
+  f32x4 sv[NITk];
+  float gcv = 0.f, gpv[NGPk];
+  unsigned okb_ld = 0;
+  // part [k0, k1) of loads k = 4 i + c of (tile, chunk) r: per-image buffer resource (range = the chunk's planes to the
+  // image end); rows above the image are negative offsets (out of range: 0), other out-of-image pixels masked by okb
+  auto load_part = [&](const It& r, int k0, int k1) __attribute__((always_inline)) {
+    const int iy0 = 2 * THk * r.ty - 1, ix0 = 2 * TW * r.tx - 1;
+    const __amdgpu_buffer_rsrc_t ri =
+        rsrc(p.x + ((long)r.b * p.cin + 32 * r.q) * HWi, (unsigned)((p.cin - 32 * r.q) * HWi * 4));
+    const int toff = iy0 * W + ix0;
+    if (k0 == 0) {
+      const bool interior = iy0 >= 0 && ix0 >= 0 && iy0 + HRk <= H && ix0 + HC <= W;
+      unsigned okb = 0xffffffffu;
+      if (!interior) {
+        okb = 0;
+#pragma unroll
+        for (int i = 0; i < NITk; ++i) {
+          const int hy = (pk[i] >> 8) & 255, hx = pk[i] & 255;
+          okb |= ((unsigned)(iy0 + hy) < (unsigned)H && (unsigned)(ix0 + hx) < (unsigned)W) ? (1u << i) : 0u;
+        }
+      }
+      okb_ld = okb;
+    }
+#pragma unroll
+    for (int i = 0; i < NITk; ++i) {
+      if (4 * i + 3 < k0 || 4 * i >= k1) continue;
+      const unsigned vo = (unsigned)((el0[i] + toff) * 4);
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (4 * i + c >= k0 && 4 * i + c < k1)
+          sv[i][c] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ri, vo + c * HWi * 4, 0, 0));
+    }
+  };
+  auto load_gates = [&](const It& r) __attribute__((always_inline)) {
+    if constexpr ((GATE & 1) != 0) gcv = p.gc[r.b * p.cin + 32 * r.q + (tid & 31)];
+    if constexpr ((GATE & 2) != 0) {
+      const int iy0 = 2 * THk * r.ty - 1, ix0 = 2 * TW * r.tx - 1;
+#pragma unroll
+      for (int k = 0; k < NGPk; ++k) {
+        const int px = min(tid + NTk * k, NPXk - 1);
+        const int hy = px / HC, hx = px - hy * HC;
+        gpv[k] = p.gp[(long)r.b * HWi + min(max(iy0 + hy, 0), H - 1) * W + min(max(ix0 + hx, 0), W - 1)];
+      }
+    }
+  };
+  auto wfrag = [&](int t, int q, int cb, int pl) __attribute__((always_inline)) {
+    const int st = __builtin_amdgcn_readfirstlane((((t * nq + q) * NCB + cb) * 2 + pl) * 1024);
+    return __builtin_bit_cast(f16x8_t, __builtin_amdgcn_raw_buffer_load_b128(rw, (unsigned)(lane * 16), st, 0));
+  };
+  int bpx[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) bpx[k] = 2 * (k >> 1) * HC + 2 * ((k & 1) * 16 + l15);
+  f32x4 acc[4][CBW];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int u = 0; u < CBW; ++u) acc[k][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nw = __builtin_amdgcn_readfirstlane(p.Wo);
+  float bo[CBW];
+#pragma unroll
+  for (int u = 0; u < CBW; ++u) bo[u] = p.bias[16 * (CBW * wid + u) + l15];
+  constexpr int NLD = 4 * NITk;               // loads per (tile, chunk)
+  constexpr int PER_TAP = (NLD + 7) / 8;      // spread over taps 0..7
+
+  It cur = it_of(0);
+  load_part(cur, 0, NLD);
+  load_gates(cur);
+  for (int it = 0; it < n_it; ++it) {
+    const It r = cur;
+    const unsigned okb = okb_ld;
+    __syncthreads();
+    if constexpr (GATE != 0) {
+      if constexpr ((GATE & 1) != 0)
+        if (tid < 32) gcs[tid] = gcv;
+      if constexpr ((GATE & 2) != 0) {
+#pragma unroll
+        for (int k = 0; k < NGPk; ++k)
+          if (tid + NTk * k < NPXk) gps[tid + NTk * k] = gpv[k];
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < NITk; ++i) {
+      const int e = tid + NTk * i;
+      if (e < NQUADk) {
+        const int quad = pk[i] >> 16, px = e - quad * NPXk;
+        f32x4 v = sv[i];
+        if constexpr ((GATE & 1) != 0) v = v * *reinterpret_cast<const f32x4*>(gcs + 4 * quad);
+        if constexpr ((GATE & 2) != 0) v = v * gps[px];
+        if (!((okb >> i) & 1u)) v = f32x4{0.f, 0.f, 0.f, 0.f};
+        uint2 hh, ll;
+        split4x(v, hh, ll);
+        rng = range_acc(rng, v);
+        h16_t* d = Pl + px * PS + 4 * quad;
+        *reinterpret_cast<uint2*>(d) = hh;
+        *reinterpret_cast<uint2*>(d + PLk) = ll;
+      }
+    }
+    __syncthreads();
+    if (it + 1 < n_it) cur = it_of(it + 1);
+    f16x8_t wa[CBW][2], wn[CBW][2];
+#pragma unroll
+    for (int u = 0; u < CBW; ++u) {
+      wa[u][0] = wfrag(0, r.q, CBW * wid + u, 0);
+      wa[u][1] = wfrag(0, r.q, CBW * wid + u, 1);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int tn = t + 1 < 9 ? t + 1 : t;
+#pragma unroll
+      for (int u = 0; u < CBW; ++u) {
+        wn[u][0] = wfrag(tn, r.q, CBW * wid + u, 0);
+        wn[u][1] = wfrag(tn, r.q, CBW * wid + u, 1);
+      }
+      if (t < 8) load_part(cur, PER_TAP * t, min(PER_TAP * t + PER_TAP, NLD));
+      else load_gates(cur);
+      __builtin_amdgcn_sched_barrier(0);
+      const int toff = (t / 3) * HC + (t % 3);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const h16_t* src = Pl + (bpx[k] + toff) * PS + 8 * g;
+        const f16x8_t xh = *reinterpret_cast<const f16x8_t*>(src);
+        const f16x8_t xl = *reinterpret_cast<const f16x8_t*>(src + PLk);
+#pragma unroll
+        for (int u = 0; u < CBW; ++u) {
+          f32x4 c = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, wa[u][1], acc[k][u], 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(xl, wa[u][0], c, 0, 0, 0);
+          acc[k][u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, wa[u][0], c, 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < CBW; ++u) {
+        wa[u][0] = wn[u][0];
+        wa[u][1] = wn[u][1];
+      }
+    }
+    if (r.q == nq - 1) {
+      f32x4 v[4][CBW];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int u = 0; u < CBW; ++u)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[k][u][e] = silu_fast_(acc[k][u][e] * (1.0f / WSC) + bo[u]);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int oy = r.ty * THk + (k >> 1), ox = r.tx * TW + (k & 1) * 16 + 4 * g;
+#pragma unroll
+        for (int u = 0; u < CBW; ++u) {
+          const int o = 16 * (CBW * wid + u) + l15;
+          if (oy < p.Ho && ox < nw)
+            __builtin_nontemporal_store(
+                v[k][u], reinterpret_cast<f32x4*>(p.y + (((long)r.b * (16 * NCB) + o) * p.Ho + oy) * nw + ox));
+          acc[k][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+    }
+  }
+  range_report(p.range_flag, rng);
+  if (p.prep_flag && p.range_flag && blockIdx.x == 0 && threadIdx.x == 0 && *p.prep_flag) *p.range_flag = 1u;
+}
+
 // W [Cout][Cin][3][3] -> fragment-major planes of 64 W: one thread per (output channel, input channel, tap). The
 // block's own range word records whether 64 W left fp16's range (re-reported by every launch).
 __global__ __launch_bounds__(256) void conv3x3s2_prep_kernel(const float* __restrict__ w, int cin, int cout,
@@ -606,6 +822,28 @@ YS_EXPORT int yolosod_conv3x3s2_silu(const float* x, float* y, int B, int cin, i
     else if (gate == 2) S2RW_LAUNCH(2, 0);
     else S2RW_LAUNCH(3, 0);
 #undef S2RW_LAUNCH
+  } else if (rw_mode >= 1 && g_s2_abl < 100) {  // 2-row tiles, three 256-thread workgroups per CU
+    c3s2::Args a2 = a;
+    a2.tiles_y = (Ho + 1) / 2;
+    const long nt2 = (long)B * a2.tiles_y * tx;
+    a2.ntiles = (int)nt2;
+    long g2 = (cout == 64 ? 3L : 2L) * s2_cu_count();
+    g2 = g2 < ((nt2 + 7) / 8) * 8 ? g2 : ((nt2 + 7) / 8) * 8;
+    g2 = (g2 + 7) / 8 * 8;
+#define S2T2_LAUNCH(NCB_, G_) \
+  hipLaunchKernelGGL((c3s2::conv3x3s2_t2_kernel<NCB_, G_>), dim3((unsigned)g2), dim3(256), 0, st, a2)
+    if (cout == 64) {
+      if (gate == 0) S2T2_LAUNCH(4, 0);
+      else if (gate == 1) S2T2_LAUNCH(4, 1);
+      else if (gate == 2) S2T2_LAUNCH(4, 2);
+      else S2T2_LAUNCH(4, 3);
+    } else {
+      if (gate == 0) S2T2_LAUNCH(8, 0);
+      else if (gate == 1) S2T2_LAUNCH(8, 1);
+      else if (gate == 2) S2T2_LAUNCH(8, 2);
+      else S2T2_LAUNCH(8, 3);
+    }
+#undef S2T2_LAUNCH
   } else if (g_s2_abl && cout == 64 && gate == 1) {  // timing ablations of the general kernel (abl + 100)
     switch (g_s2_abl - 100) {
       case 1: hipLaunchKernelGGL((c3s2::conv3x3s2_kernel<4, 1, 1>), dim3((unsigned)grid), dim3(c3s2::NT), 0, st, a); break;
