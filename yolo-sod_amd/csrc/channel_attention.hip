@@ -508,18 +508,25 @@ __global__ __launch_bounds__(256) void cbam_sa_kernel(const float* __restrict__ 
         mx[k] = fmaxf(mx[k], c[k][u]);
       }
   }
-  for (; g < G; ++g) {
-    float a[2], c[2];
+  if (g < G) {  // the last 1..3 groups: all loads in flight at once (clamped group index), the extra ones unused (a
+               // runtime loop issued each group's loads only after the previous group's sums: C = 64, L4, has G = 2)
+    float a[2][3], c[2][3];
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      a[k] = mp[(long)(2 * g) * HW + q[k]];
-      c[k] = mp[(long)(2 * g + 1) * HW + q[k]];
-    }
+    for (int k = 0; k < 2; ++k)
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      sm[k] += a[k];
-      mx[k] = fmaxf(mx[k], c[k]);
-    }
+      for (int u = 0; u < 3; ++u) {
+        const int gu = min(g + u, G - 1);
+        a[k][u] = mp[(long)(2 * gu) * HW + q[k]];
+        c[k][u] = mp[(long)(2 * gu + 1) * HW + q[k]];
+      }
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+      for (int u = 0; u < 3; ++u)
+        if (g + u < G) {
+          sm[k] += a[k][u];
+          mx[k] = fmaxf(mx[k], c[k][u]);
+        }
   }
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
