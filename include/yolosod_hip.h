@@ -284,7 +284,8 @@ int yolosod_cbam_gates(const float* x, int B, int C, int H, int W, const float* 
 /* 3x3 / stride 2 / pad 1 conv + bias + SiLU with the producing MAFN gate applied while the input is staged
  * (csrc/conv3x3s2.hip): y = SiLU(conv3x3_s2((x * gc) * gp, W) + bias), the consumer Conv of SE_Block L1 (gc = the SE
  * gate, smallobj_modules.py:92) and of CBAM_Block L4 (gc = ca, gp = sa, cbam_block.py:53-54) in the paper YAML, with the
- * gate's output never written. fp16 two-term split MFMA at fp32 accuracy; Cout 64 or 128, Cin a multiple of 32 (<= 2048),
+ * gate's output never written. fp16 two-term split MFMA at fp32 accuracy; Cout 64 or 128 (_out: multiples of 128 up to
+ * 512 too), Cin a multiple of 32 (<= 2048),
  * Ho = (H + 1) / 2, Wo = (W + 1) / 2 with Wo % 4 == 0; x [B][cin][H][W] (B*cin*H*W*4 < 2^32), gc [B][cin] 16-byte
  * aligned or NULL, gp [B][H][W] or NULL, y [B][cout][Ho][Wo]. Weights prepared once per parameter version into a
  * caller-owned block of yolosod_conv3x3s2_prep_bytes(cin, cout) bytes (0: unsupported). Replaces the gate's apply pass
@@ -293,6 +294,12 @@ size_t yolosod_conv3x3s2_prep_bytes(int cin, int cout);
 int yolosod_conv3x3s2_prepare(const float* w, int cin, int cout, void* prep, size_t prep_bytes, void* stream);
 int yolosod_conv3x3s2_silu(const float* x, float* y, int B, int cin, int cout, int H, int W, const float* bias,
                            const float* gc, const float* gp, const void* prep, size_t prep_bytes, void* stream);
+/* The same with image b's output [cout][Ho][Wo] at y + b * y_bstride (y_bstride >= cout*Ho*Wo, a multiple of 4, y
+ * 16-byte aligned): a channel slice of a concat buffer (nn/tasks.py concat elision). Cout may also be any multiple of
+ * 128 up to 512 (the PAN neck's stride-2 convs, layers 29 / 33 / 36 of the paper YAML). */
+int yolosod_conv3x3s2_silu_out(const float* x, float* y, long y_bstride, int B, int cin, int cout, int H, int W,
+                               const float* bias, const float* gc, const float* gp, const void* prep,
+                               size_t prep_bytes, void* stream);
 /* Timing hook: ablation variants of the stride-2 conv kernel at Cout 64 with a channel gate (csrc/conv3x3s2.hip; WRONG
  * results for abl != 0 - scripts/bench_conv3x3s2.py only). Returns the previous value. */
 int yolosod_debug_set_conv3x3s2_abl(int abl);

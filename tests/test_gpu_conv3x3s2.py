@@ -76,3 +76,37 @@ def test_conv3x3s2_range_guard(cuda):
     for _ in range(2):
         _hip.conv3x3s2_silu(x, b, lambda: big, 64)
         assert _hip.split_range_flag(reset=True)
+
+
+@pytest.mark.parametrize("shape,cout", [((2, 64, 40, 40), 256), ((2, 128, 24, 24), 512), ((1, 256, 40, 40), 384)])
+def test_conv3x3s2_channel_groups_match_fp64(shape, cout, cuda):
+    """Cout a multiple of 128 above 128 (the PAN neck's stride-2 convs): work items (tile, 128-channel group)."""
+    g = torch.Generator().manual_seed(sum(shape) + cout)
+    B, cin, H, W = shape
+    x = torch.randn(shape, generator=g)
+    w = torch.randn(cout, cin, 3, 3, generator=g) * (1.0 / (3 * cin ** 0.5))
+    b = torch.randn(cout, generator=g) * 0.1
+    ref = F.silu(F.conv2d(x.double(), w.double(), b.double(), stride=2, padding=1))
+    wd = w.to(cuda)
+    y = _hip.conv3x3s2_silu(x.to(cuda), b.to(cuda), lambda: _hip.conv3x3s2_prepare(wd), cout).cpu().double()
+    miopen = F.silu(F.conv2d(x.to(cuda), wd, b.to(cuda), stride=2, padding=1)).cpu().double()
+    err, err_m = float((y - ref).abs().max()), float((miopen - ref).abs().max())
+    ok, e, _ = tol_close(y, ref, 5e-5, 1e-4)
+    assert ok, f"{shape}: max abs err {e:.3g} (MIOpen fp32 {err_m:.3g})"
+    assert err <= 8 * err_m + 1e-5, (err, err_m)
+
+
+@pytest.mark.parametrize("cin,cout", [(32, 64), (64, 128), (64, 256)])
+def test_conv3x3s2_into_concat_slice(cin, cout, cuda):
+    """out= a channel slice of a concat buffer (batch stride > Cout*Ho*Wo): bit-identical to the contiguous output, and
+    the rest of the buffer untouched."""
+    g = torch.Generator().manual_seed(cin + cout)
+    x = torch.randn(3, cin, 24, 40, generator=g).to(cuda)
+    w = (torch.randn(cout, cin, 3, 3, generator=g) * 0.05).to(cuda)
+    b = (torch.randn(cout, generator=g) * 0.1).to(cuda)
+    prep = _hip.conv3x3s2_prepare(w)
+    y = _hip.conv3x3s2_silu(x, b, lambda: prep, cout)
+    buf = torch.full((3, cout + 96, 12, 20), float("nan"), device=cuda)
+    _hip.conv3x3s2_silu(x, b, lambda: prep, cout, out=buf[:, 32:32 + cout])
+    assert torch.equal(buf[:, 32:32 + cout], y)
+    assert torch.isnan(buf[:, :32]).all() and torch.isnan(buf[:, 32 + cout:]).all()

@@ -281,3 +281,26 @@ def test_gate_fusion_matches_the_unfused_model(gpu_model, cuda):
         assert names.count("se") == 1 and names.count("cbam") == 1  # SE L23 and CBAM L18 keep their apply
         ok, e, _ = tol_close(y1.cpu().double(), y0.cpu().double(), 1e-3, 1e-4)
         assert ok, (S, e)
+
+
+def test_neck_stride2_convs_take_the_kernel(gpu_model, cuda):
+    """The neck's 3x3 / stride-2 convs (layers 29 / 33 / 36) run on the stride-2 fp16-split kernel, written into
+    their Concat slices, and the model matches the MIOpen path (YOLOSOD_S2_NECK=0) within fp32 accuracy."""
+    from yolosod_amd import _hip
+    from yolosod_amd.nn import modules as M
+    assert [i for i, m in enumerate(gpu_model.model) if getattr(m, "s2", False)] == [29, 33, 36]
+    x = torch.rand(2, 3, 640, 640, generator=torch.Generator().manual_seed(7)).to(cuda)
+    saved = M.S2_NECK
+    try:
+        with torch.inference_mode():
+            M.S2_NECK = True
+            with _hip.op_timer() as t:
+                y1 = gpu_model(x)[0].clone()
+            plain = [k for k, _ in t.durations_ms() if k[0] == "conv3x3s2" and k[3] == (False, False)]
+            M.S2_NECK = False
+            y0 = gpu_model(x)[0].clone()
+    finally:
+        M.S2_NECK = saved
+    assert sorted(k[2] for k in plain) == [128, 256, 512], plain
+    ok, e, _ = tol_close(y1.cpu().double(), y0.cpu().double(), 1e-3, 1e-4)
+    assert ok, e

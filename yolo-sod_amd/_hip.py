@@ -94,6 +94,7 @@ SIGNATURES = {
     "yolosod_conv3x3s2_prep_bytes": (_sz, [_i, _i]),
     "yolosod_conv3x3s2_prepare": (_i, [_vp, _i, _i, _vp, _sz, _vp]),
     "yolosod_conv3x3s2_silu": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "yolosod_conv3x3s2_silu_out": (_i, [_vp, _vp, _l, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _sz, _vp]),
     "yolosod_debug_set_swin_tokln": (_i, [_i]),
     "yolosod_debug_set_x3_swz": (_i, [_i]),
     "yolosod_debug_set_a2_pool_px": (_i, [_i]),
@@ -788,10 +789,12 @@ def conv3x3_silu(x, bias, prep):
 
 def conv3x3s2_ok(x, conv) -> bool:
     """Shapes the stride-2 fused-gate conv kernel takes (yolosod_conv3x3s2_silu): fp32 contiguous NCHW on a GPU,
-    3x3 / stride 2 / pad 1 / dilation 1 / groups 1, 64 or 128 outputs, Cin a multiple of 32, output width % 4 == 0."""
+    3x3 / stride 2 / pad 1 / dilation 1 / groups 1, 64 or a multiple of 128 (<= 512) outputs, Cin a multiple of 32,
+    output width % 4 == 0."""
     return (x.device.type == "cuda" and x.dtype == torch.float32 and x.is_contiguous() and x.dim() == 4
             and conv.kernel_size == (3, 3) and conv.stride == (2, 2) and conv.padding == (1, 1)
-            and conv.dilation == (1, 1) and conv.groups == 1 and conv.out_channels in (64, 128)
+            and conv.dilation == (1, 1) and conv.groups == 1
+            and (conv.out_channels == 64 or (conv.out_channels % 128 == 0 and conv.out_channels <= 512))
             and conv.in_channels % 32 == 0 and x.shape[1] == conv.in_channels and ((x.shape[3] + 1) // 2) % 4 == 0
             and x.numel() * 4 < 2 ** 32
             and int(load_library().yolosod_conv3x3s2_prep_bytes(int(conv.in_channels), int(conv.out_channels))) > 0)
@@ -811,14 +814,23 @@ def conv3x3s2_prepare(w):
     return blk
 
 
-def conv3x3s2_silu(x, bias, prep, cout, gate_c=None, gate_p=None, key=None):
+def conv3x3s2_silu(x, bias, prep, cout, gate_c=None, gate_p=None, key=None, out=None):
     """SiLU(conv3x3_stride2((x * gate_c) * gate_p) + bias) on the fp16 two-term split MFMA (csrc/conv3x3s2.hip):
     gate_c [B, Cin] (an SE / CBAM channel gate), gate_p [B, H, W] (CBAM's spatial gate), either may be None.
     ``prep``: a callable returning the cached prepared block (conv3x3s2_prepare); ``key``: the op_timer key (default
-    ("conv3x3s2", shape, Cout, gates))."""
+    ("conv3x3s2", shape, Cout, gates)); ``out``: a [B, Cout, Ho, Wo] fp32 view whose images are contiguous (e.g. a
+    channel slice of a concat buffer) to write instead of a new tensor."""
     lib = load_library()
     B, Cin, H, W = x.shape
-    y = torch.empty((B, cout, (H + 1) // 2, (W + 1) // 2), dtype=torch.float32, device=x.device)
+    Ho, Wo = (H + 1) // 2, (W + 1) // 2
+    if out is None:
+        y = torch.empty((B, cout, Ho, Wo), dtype=torch.float32, device=x.device)
+    else:
+        y = out
+        if (tuple(y.shape) != (B, cout, Ho, Wo) or y.dtype != torch.float32 or y.device != x.device
+                or y.stride()[1:] != (Ho * Wo, Wo, 1) or y.data_ptr() % 16 or y.stride(0) % 4):
+            raise RuntimeError(f"conv3x3s2: out {tuple(y.shape)} / {y.stride()} is not a [{B}, {cout}, {Ho}, {Wo}] "
+                               "fp32 view with contiguous 16-byte aligned images")
     b = bias.detach().float().contiguous()
     gc = None if gate_c is None else gate_c.float().contiguous()
     gp = None if gate_p is None else gate_p.float().contiguous()
@@ -829,10 +841,10 @@ def conv3x3s2_silu(x, bias, prep, cout, gate_c=None, gate_p=None, key=None):
 
     def run():
         blk = prep()
-        return lib.yolosod_conv3x3s2_silu(_dev(x, "x"), y.data_ptr(), B, Cin, cout, H, W, _dev(b, "bias"),
-                                          None if gc is None else _dev(gc, "gate_c"),
-                                          None if gp is None else _dev(gp, "gate_p"), blk.data_ptr(), blk.numel(),
-                                          _stream(x.device))
+        return lib.yolosod_conv3x3s2_silu_out(_dev(x, "x"), y.data_ptr(), y.stride(0), B, Cin, cout, H, W,
+                                              _dev(b, "bias"), None if gc is None else _dev(gc, "gate_c"),
+                                              None if gp is None else _dev(gp, "gate_p"), blk.data_ptr(), blk.numel(),
+                                              _stream(x.device))
 
     if key is None:
         key = ("conv3x3s2", tuple(x.shape), cout, (gc is not None, gp is not None))

@@ -39,8 +39,11 @@ struct Args {
   const float* bias;   // [Cout]
   const float* gc;     // [B][Cin] channel gate (GATE & 1), 16-byte aligned
   const float* gp;     // [B][H][W] spatial gate (GATE & 2)
-  float* y;            // [B][Cout][Ho][Wo]
+  float* y;            // image b's output at y + b ybs: [Cout][Ho][Wo] (ybs >= Cout Ho Wo: a channel slice of a
+                       // concat buffer)
+  long ybs;
   int B, cin, H, W, Ho, Wo, tiles_x, tiles_y, ntiles;
+  int ncb_all;         // channel blocks of the prepared weights (Cout / 16); the t2 kernel: ncb_all / NCB groups
   unsigned* range_flag;
   const unsigned* prep_flag;
 };
@@ -229,7 +232,7 @@ __global__ __launch_bounds__(NT, 1) void conv3x3s2_kernel(Args p) {
       // epilogue: lane (g, l15) of pixel block pb holds output channel 16 cb + l15, pixels (row pb >> 1, columns
       // (pb & 1) 16 + 4 g .. + 3); every value first, then the non-temporal 16-byte stores (Wo % 4 == 0: 4 pixels
       // all in or all out; interleaved, each store's data registers were reused behind a full vmcnt wait)
-      float* yo = p.y + ((long)b * (16 * NCB) + o_ch) * p.Ho * nw;
+      float* yo = p.y + (long)b * p.ybs + (long)o_ch * p.Ho * nw;
       f32x4 v[NPB];
 #pragma unroll
       for (int k = 0; k < NPB; ++k)
@@ -373,7 +376,7 @@ __global__ __launch_bounds__(NTk, 512 / NTk) void conv3x3s2_rw_kernel(Args p) {
       const int ox = tl.tx * TW + 4 * px4, oy = tl.ty * THk + r;
       const f32x4 v = *reinterpret_cast<const f32x4*>(Ep + (r * 64 + ch) * ES + 4 * px4);
       if (oy < p.Ho && ox < nw && (!(ABL & 8) || v[0] == -1.2345e30f))
-        __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p.y + (((long)tl.b * 64 + ch) * p.Ho + oy) * nw + ox));
+        __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p.y + (long)tl.b * p.ybs + ((long)ch * p.Ho + oy) * nw + ox));
     }
   };
 
@@ -466,14 +469,19 @@ __global__ __launch_bounds__(256, NCB == 8 ? 2 : 3) void conv3x3s2_t2_kernel(Arg
   __shared__ __attribute__((aligned(16))) h16_t Pl[2 * PLk];
   __shared__ __attribute__((aligned(16))) float gcs[32];
   __shared__ float gps[(GATE & 2) ? NPXk : 1];
+  __shared__ float bsh[512];  // the bias of every output channel (Cout <= 512): an epilogue load would wait behind
+                              // every prefetch in flight
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l15 = lane & 15, g = lane >> 4;
   const int H = p.H, W = p.W, HWi = H * W, nq = p.cin >> 5;
   float rng = 0.f;
+  for (int o = tid; o < 16 * p.ncb_all; o += 256) bsh[o] = p.bias[o];  // ordered before use by the loop's barriers
 
   const int nj = gridDim.x >> 3, j = blockIdx.x >> 3, xcd = blockIdx.x & 7;
-  const int per = (p.ntiles + 7) >> 3;
-  const int t_beg = xcd * per + j, t_end = min((xcd + 1) * per, p.ntiles);
+  const int ngrp = p.ncb_all / NCB;  // output channel groups of 16 NCB: work item = (tile, group), group fastest
+  const int nitems = p.ntiles * ngrp;
+  const int per = (nitems + 7) >> 3;
+  const int t_beg = xcd * per + j, t_end = min((xcd + 1) * per, nitems);
   if (t_beg >= t_end) return;
   const int n_it = ((t_end - t_beg + nj - 1) / nj) * nq;
 
@@ -484,7 +492,7 @@ __global__ __launch_bounds__(256, NCB == 8 ? 2 : 3) void conv3x3s2_t2_kernel(Arg
                 (unsigned)__builtin_amdgcn_readfirstlane((unsigned)a)),
         (short)0, __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
   };
-  const __amdgpu_buffer_rsrc_t rw = rsrc(p.wp, (unsigned)(9L * nq * NCB * 2 * 1024));
+  const __amdgpu_buffer_rsrc_t rw = rsrc(p.wp, (unsigned)(9L * nq * p.ncb_all * 2 * 1024));
   int pk[NITk], el0[NITk];
 #pragma unroll
   for (int i = 0; i < NITk; ++i) {
@@ -495,11 +503,13 @@ __global__ __launch_bounds__(256, NCB == 8 ? 2 : 3) void conv3x3s2_t2_kernel(Arg
     el0[i] = 4 * quad * HWi + hy * W + hx;
   }
   struct It {
-    int b, ty, tx, q;
+    int b, ty, tx, q, grp;
   };
   auto it_of = [&](int it) __attribute__((always_inline)) {
-    const int t = t_beg + (it / nq) * nj;
+    const int tg = t_beg + (it / nq) * nj;
+    const int t = tg / ngrp;
     It r;
+    r.grp = tg - t * ngrp;
     r.q = it - (it / nq) * nq;
     r.tx = t % p.tiles_x;
     r.ty = (t / p.tiles_x) % p.tiles_y;
@@ -551,8 +561,8 @@ __global__ __launch_bounds__(256, NCB == 8 ? 2 : 3) void conv3x3s2_t2_kernel(Arg
       }
     }
   };
-  auto wfrag = [&](int t, int q, int cb, int pl) __attribute__((always_inline)) {
-    const int st = __builtin_amdgcn_readfirstlane((((t * nq + q) * NCB + cb) * 2 + pl) * 1024);
+  auto wfrag = [&](int t, int q, int cb, int pl) __attribute__((always_inline)) {  // cb: over all ncb_all blocks
+    const int st = __builtin_amdgcn_readfirstlane((((t * nq + q) * p.ncb_all + cb) * 2 + pl) * 1024);
     return __builtin_bit_cast(f16x8_t, __builtin_amdgcn_raw_buffer_load_b128(rw, (unsigned)(lane * 16), st, 0));
   };
   int bpx[4];
@@ -564,9 +574,6 @@ __global__ __launch_bounds__(256, NCB == 8 ? 2 : 3) void conv3x3s2_t2_kernel(Arg
 #pragma unroll
     for (int u = 0; u < CBW; ++u) acc[k][u] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int nw = __builtin_amdgcn_readfirstlane(p.Wo);
-  float bo[CBW];
-#pragma unroll
-  for (int u = 0; u < CBW; ++u) bo[u] = p.bias[16 * (CBW * wid + u) + l15];
   constexpr int NLD = 4 * NITk;               // loads per (tile, chunk)
   constexpr int PER_TAP = (NLD + 7) / 8;      // spread over taps 0..7
 
@@ -606,11 +613,12 @@ __global__ __launch_bounds__(256, NCB == 8 ? 2 : 3) void conv3x3s2_t2_kernel(Arg
     }
     __syncthreads();
     if (it + 1 < n_it) cur = it_of(it + 1);
+    const int cb0 = r.grp * NCB + CBW * wid;  // this wave's first channel block (of all ncb_all)
     f16x8_t wa[CBW][2], wn[CBW][2];
 #pragma unroll
     for (int u = 0; u < CBW; ++u) {
-      wa[u][0] = wfrag(0, r.q, CBW * wid + u, 0);
-      wa[u][1] = wfrag(0, r.q, CBW * wid + u, 1);
+      wa[u][0] = wfrag(0, r.q, cb0 + u, 0);
+      wa[u][1] = wfrag(0, r.q, cb0 + u, 1);
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -618,8 +626,8 @@ __global__ __launch_bounds__(256, NCB == 8 ? 2 : 3) void conv3x3s2_t2_kernel(Arg
       const int tn = t + 1 < 9 ? t + 1 : t;
 #pragma unroll
       for (int u = 0; u < CBW; ++u) {
-        wn[u][0] = wfrag(tn, r.q, CBW * wid + u, 0);
-        wn[u][1] = wfrag(tn, r.q, CBW * wid + u, 1);
+        wn[u][0] = wfrag(tn, r.q, cb0 + u, 0);
+        wn[u][1] = wfrag(tn, r.q, cb0 + u, 1);
       }
       if (t < 8) load_part(cur, PER_TAP * t, min(PER_TAP * t + PER_TAP, NLD));
       else load_gates(cur);
@@ -644,6 +652,9 @@ __global__ __launch_bounds__(256, NCB == 8 ? 2 : 3) void conv3x3s2_t2_kernel(Arg
       }
     }
     if (r.q == nq - 1) {
+      float bo[CBW];
+#pragma unroll
+      for (int u = 0; u < CBW; ++u) bo[u] = bsh[16 * (cb0 + u) + l15];
       f32x4 v[4][CBW];
 #pragma unroll
       for (int k = 0; k < 4; ++k)
@@ -656,10 +667,10 @@ __global__ __launch_bounds__(256, NCB == 8 ? 2 : 3) void conv3x3s2_t2_kernel(Arg
         const int oy = r.ty * THk + (k >> 1), ox = r.tx * TW + (k & 1) * 16 + 4 * g;
 #pragma unroll
         for (int u = 0; u < CBW; ++u) {
-          const int o = 16 * (CBW * wid + u) + l15;
+          const int o = 16 * (cb0 + u) + l15;
           if (oy < p.Ho && ox < nw)
             __builtin_nontemporal_store(
-                v[k][u], reinterpret_cast<f32x4*>(p.y + (((long)r.b * (16 * NCB) + o) * p.Ho + oy) * nw + ox));
+                v[k][u], reinterpret_cast<f32x4*>(p.y + (long)r.b * p.ybs + ((long)o * p.Ho + oy) * nw + ox));
           acc[k][u] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
       }
@@ -715,9 +726,9 @@ static int s2_cu_count() {
   return n;
 }
 
-// 3x3 / stride 2 / pad 1 conv with Cout 64 or 128 and Cin a multiple of 32 (<= 2048)
+// 3x3 / stride 2 / pad 1 conv with Cout 64 or a multiple of 128 (<= 512) and Cin a multiple of 32 (<= 2048)
 YS_EXPORT size_t yolosod_conv3x3s2_prep_bytes(int cin, int cout) {
-  if (cin <= 0 || cin % 32 || cin > 2048 || (cout != 64 && cout != 128)) return 0;
+  if (cin <= 0 || cin % 32 || cin > 2048 || !(cout == 64 || (cout % 128 == 0 && cout <= 512))) return 0;
   Sizer s;
   s.take<h16_t>((size_t)2 * cout * cin * 9);
   s.take<unsigned>(1);
@@ -753,15 +764,19 @@ YS_EXPORT int yolosod_conv3x3s2_prepare(const float* w, int cin, int cout, void*
   return 0;
 }
 
-// y = SiLU(conv3x3_s2((x * gc) * gp, W) + bias): x [B][cin][H][W] -> y [B][cout][Ho][Wo], Ho = (H + 1) / 2,
-// Wo = (W + 1) / 2 (Wo % 4 == 0); gc [B][cin] (16-byte aligned) and gp [B][H][W] may each be NULL (no gate).
-YS_EXPORT int yolosod_conv3x3s2_silu(const float* x, float* y, int B, int cin, int cout, int H, int W,
-                                     const float* bias, const float* gc, const float* gp, const void* prep,
-                                     size_t prep_bytes, void* stream) {
+// y = SiLU(conv3x3_s2((x * gc) * gp, W) + bias): x [B][cin][H][W] -> image b's output [cout][Ho][Wo] at
+// y + b y_bstride (y_bstride >= cout Ho Wo: a channel slice of a concat buffer), Ho = (H + 1) / 2, Wo = (W + 1) / 2
+// (Wo % 4 == 0); gc [B][cin] (16-byte aligned) and gp [B][H][W] may each be NULL (no gate).
+YS_EXPORT int yolosod_conv3x3s2_silu_out(const float* x, float* y, long y_bstride, int B, int cin, int cout, int H,
+                                         int W, const float* bias, const float* gc, const float* gp, const void* prep,
+                                         size_t prep_bytes, void* stream) {
   YS_CHECK_ARG(x && y && bias && prep, "conv3x3s2: null pointer");
   YS_CHECK_ARG(B >= 0 && H > 0 && W > 0 && yolosod_conv3x3s2_prep_bytes(cin, cout) > 0, "conv3x3s2: bad shape");
   const int Ho = (H + 1) / 2, Wo = (W + 1) / 2;
   YS_CHECK_ARG(Wo % 4 == 0, "conv3x3s2: output width %d not a multiple of 4", Wo);
+  YS_CHECK_ARG(y_bstride >= (long)cout * Ho * Wo, "conv3x3s2: output batch stride %ld < %ld", y_bstride,
+               (long)cout * Ho * Wo);
+  YS_CHECK_ARG(((uintptr_t)y & 15) == 0 && y_bstride % 4 == 0, "conv3x3s2: output not 16-byte aligned");
   YS_CHECK_ARG((long)B * cin * H * W * 4 < (1L << 32) && (long)cin * H * W < (1L << 31),
                "conv3x3s2: input too large for 32-bit buffer offsets");
   YS_CHECK_ARG(!gc || ((uintptr_t)gc & 15) == 0, "conv3x3s2: channel gate must be 16-byte aligned");
@@ -773,7 +788,8 @@ YS_EXPORT int yolosod_conv3x3s2_silu(const float* x, float* y, int B, int cin, i
   const int tx = (Wo + c3s2::TW - 1) / c3s2::TW, ty = (Ho + c3s2::TH - 1) / c3s2::TH;
   const long ntiles = (long)B * tx * ty;
   YS_CHECK_ARG(ntiles < (1L << 30), "conv3x3s2: too many tiles");
-  c3s2::Args a{x, wp, bias, gc, gp, y, B, cin, H, W, Ho, Wo, tx, ty, (int)ntiles, range_flag_dev(), flag};
+  c3s2::Args a{x, wp, bias, gc, gp, y, y_bstride, B, cin, H, W, Ho, Wo, tx, ty, (int)ntiles, cout / 16,
+               range_flag_dev(), flag};
   // persistent grid: one workgroup per CU (a multiple of 8 = one per XCD slot), at most one per tile
   long grid = s2_cu_count();
   grid = grid < ((ntiles + 7) / 8) * 8 ? grid : ((ntiles + 7) / 8) * 8;
@@ -822,11 +838,11 @@ YS_EXPORT int yolosod_conv3x3s2_silu(const float* x, float* y, int B, int cin, i
     else if (gate == 2) S2RW_LAUNCH(2, 0);
     else S2RW_LAUNCH(3, 0);
 #undef S2RW_LAUNCH
-  } else if (rw_mode >= 1 && g_s2_abl < 100) {  // 2-row tiles, three 256-thread workgroups per CU
+  } else if ((rw_mode >= 1 && g_s2_abl < 100) || cout > 128) {  // 2-row tiles, 3 (Cout 64) / 2 workgroups per CU
     c3s2::Args a2 = a;
     a2.tiles_y = (Ho + 1) / 2;
-    const long nt2 = (long)B * a2.tiles_y * tx;
-    a2.ntiles = (int)nt2;
+    const long nt2 = (long)B * a2.tiles_y * tx * (cout == 64 ? 1 : cout / 128);  // work items: (tile, group)
+    a2.ntiles = (int)((long)B * a2.tiles_y * tx);
     long g2 = (cout == 64 ? 3L : 2L) * s2_cu_count();
     g2 = g2 < ((nt2 + 7) / 8) * 8 ? g2 : ((nt2 + 7) / 8) * 8;
     g2 = (g2 + 7) / 8 * 8;
@@ -868,4 +884,12 @@ YS_EXPORT int yolosod_conv3x3s2_silu(const float* x, float* y, int B, int cin, i
 #undef S2_LAUNCH
   YS_CHECK_LAUNCH("conv3x3s2");
   return 0;
+}
+
+// As yolosod_conv3x3s2_silu_out with a contiguous y [B][cout][Ho][Wo].
+YS_EXPORT int yolosod_conv3x3s2_silu(const float* x, float* y, int B, int cin, int cout, int H, int W,
+                                     const float* bias, const float* gc, const float* gp, const void* prep,
+                                     size_t prep_bytes, void* stream) {
+  return yolosod_conv3x3s2_silu_out(x, y, (long)cout * ((H + 1) / 2) * ((W + 1) / 2), B, cin, cout, H, W, bias, gc, gp,
+                                    prep, prep_bytes, stream);
 }

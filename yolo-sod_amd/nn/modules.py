@@ -98,16 +98,22 @@ THIN1X1 = os.environ.get("YOLOSOD_THIN1X1", "1") == "1"
 # tower conv whatever its size (tests), =all also takes every other eligible 3x3 conv of the model (the backbone
 # stays on MIOpen by default, as north_star asks)
 CONV3X3 = os.environ.get("YOLOSOD_CONV3X3", "1")
+# the PAN neck's 3x3 / stride-2 convs (layers 29 / 33 / 36 of the paper YAML: the consumers of Swin L28 and CA L32,
+# and P4 -> P5) on the stride-2 fp16-split kernel (csrc/conv3x3s2.hip), writing straight into their Concat slice,
+# instead of MIOpen's NHWC implicit GEMM with its layout transposes + the bias / SiLU pass; YOLOSOD_S2_NECK=0: MIOpen
+S2_NECK = os.environ.get("YOLOSOD_S2_NECK", "1") != "0"
 CONV3X3_MIN_TILES = int(os.environ.get("YOLOSOD_CONV3X3_MIN_TILES", "0"))
 
 
-def conv_epilogue(conv: nn.Conv2d, act_code, x, out=None, res=None, stats=None, out2=None, c2lo=0, tower=False):
+def conv_epilogue(conv: nn.Conv2d, act_code, x, out=None, res=None, stats=None, out2=None, c2lo=0, tower=False,
+                  s2=False):
     """GPU fast path of ``act(conv(x)) (+ res)``: MIOpen conv without bias, then one HIP pass for bias +
     activation (+ shortcut), optionally written straight into a channel slice ``out`` of a concat buffer.
     ``stats`` ("sum" / "summax"): the same pass emits the output's per-plane partial statistics for a following
     SE / CBAM gate (``_hip.PlaneStats`` on the returned tensor).
     ``out2``: also store channels [c2lo, C) packed there (the next conv's input; C2f's Bottleneck chain).
     ``tower``: the conv is one of the Detect head's 3x3 tower convs (the fp16-split conv kernel takes it).
+    ``s2``: the conv is one of the neck's 3x3 / stride-2 convs (the stride-2 fp16-split kernel takes it).
     Returns None when the fast path does not apply (CPU tensor, no bias, unsupported activation / shape)."""
     if x.device.type != "cuda" or conv.bias is None or act_code is None or x.dtype not in (torch.float32,
                                                                                            torch.bfloat16):
@@ -117,6 +123,10 @@ def conv_epilogue(conv: nn.Conv2d, act_code, x, out=None, res=None, stats=None, 
             and (CONV3X3 == "force" or x.shape[0] * -(-x.shape[2] // 8) * -(-x.shape[3] // 32) >= CONV3X3_MIN_TILES)):
         prep = lambda: _cached(conv, "c3prep", (conv.weight,), lambda: _hip.conv3x3_prepare(conv.weight))  # noqa: E731
         return _hip.conv3x3_silu(x, conv.bias, prep)
+    if (s2 and S2_NECK and act_code == 1 and res is None and stats is None and out2 is None
+            and _hip.conv3x3s2_ok(x, conv)):
+        prep = lambda: _cached(conv, "c3s2prep", (conv.weight,), lambda: _hip.conv3x3s2_prepare(conv.weight))  # noqa: E731
+        return _hip.conv3x3s2_silu(x, conv.bias, prep, conv.out_channels, out=out)
     if (THIN1X1 and act_code == 1 and (stats is None or (stats in ("sum", "summax") and res is None and out2 is None))
             and conv.out_channels == 64 and conv.kernel_size == (1, 1) and conv.stride == (1, 1)
             and conv.groups == 1 and conv.padding == (0, 0) and _hip.conv1x1_thin_ok(x, conv.out_channels)
@@ -158,6 +168,8 @@ class Conv(nn.Module):
     emit_stats = None
     # set by Detect on its 3x3 tower convs (head.py:43-57): the fp16-split conv kernel runs them (CONV3X3)
     tower = False
+    # set by DetectionModel on the neck's 3x3 / stride-2 convs: the stride-2 fp16-split kernel runs them (S2_NECK)
+    s2 = False
 
     def __init__(self, c1, c2, k=1, s=1, p=None, g=1, d=1, act=True):
         super().__init__()
@@ -181,7 +193,8 @@ class Conv(nn.Module):
         return _hip.conv3x3s2_silu(x, cv.bias, prep, cv.out_channels, gate_c, gate_p, key=key)
 
     def forward_fuse(self, x, out=None, res=None, out2=None, c2lo=0):
-        y = conv_epilogue(self.conv, _act_code(self.act), x, out, res, self.emit_stats, out2, c2lo, self.tower)
+        y = conv_epilogue(self.conv, _act_code(self.act), x, out, res, self.emit_stats, out2, c2lo, self.tower,
+                          self.s2)
         if y is not None:
             return y
         y = self.act(self.conv(x))

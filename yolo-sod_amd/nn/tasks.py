@@ -433,6 +433,14 @@ class DetectionModel(BaseModel):
                     conv.emit_stats = ("summax" if isinstance(m, M.CBAM_Block) else
                                        "capool" if isinstance(m, M.CA_Block) else "sum")
 
+        # the neck's 3x3 / stride-2 convs run on the stride-2 fp16-split kernel (modules.S2_NECK); the backbone's
+        # convs stay on PyTorch-ROCm (north_star), except SE L1's / CBAM L4's consumers, which apply those gates
+        n_backbone = len(self.yaml.get("backbone", []))
+        for i, m in enumerate(self.model):
+            if (i >= n_backbone and isinstance(m, M.Conv) and not isinstance(m, M.DWConv)
+                    and m.conv.kernel_size == (3, 3) and m.conv.stride == (2, 2) and m.conv.groups == 1):
+                m.s2 = True
+
         # lazy SE weights: the reference creates them during the stride probe, in forward (= layer) order,
         # after every eager module -> same RNG stream position here.
         for m in self.model:
