@@ -61,6 +61,7 @@ def test_tower_convs_take_the_kernel(cuda, monkeypatch):
     m = build_model("yolov12-sod-fusion-v5-simple.yaml", seed=0, device=cuda)
     x = torch.rand(2, 3, 256, 256, generator=torch.Generator().manual_seed(4)).to(cuda)
     monkeypatch.setattr(M, "CONV3X3", "force")  # every tower conv, whatever its tile count
+    monkeypatch.setattr(M, "S1_NECK", False)  # (the neck's Bottleneck convs: test_neck_c2f_convs_take_the_kernel)
     with torch.inference_mode():
         with _hip.op_timer() as t:
             y = m(x)[0]
@@ -68,5 +69,54 @@ def test_tower_convs_take_the_kernel(cuda, monkeypatch):
         monkeypatch.setattr(M, "CONV3X3", "0")
         y0 = m(x)[0]
     assert keys.count("conv3x3") == 16  # 4 levels x (box, class) x 2 convs
+    ok, e, _ = tol_close(y.cpu().double(), y0.cpu().double(), 1e-3, 1e-4)
+    assert ok, e
+
+
+@pytest.mark.parametrize("shape,cout", [((2, 32, 40, 48), 32), ((2, 128, 24, 24), 128), ((1, 256, 20, 20), 256),
+                                        ((2, 64, 17, 28), 64)])
+def test_conv3x3_groups_out_res_match_fp64(shape, cout, cuda):
+    """Cout 32 / multiples of 64 (output groups of 32 / 64 channels), the residual added after the activation and the
+    output written into a concat slice (the neck's C2f Bottleneck cv2: x + SiLU(conv(cv1(x))), block.py:343)."""
+    g = torch.Generator().manual_seed(sum(shape) + cout)
+    B, cin, H, W = shape
+    x = torch.randn(shape, generator=g)
+    w = torch.randn(cout, cin, 3, 3, generator=g) * (1.0 / (3 * cin ** 0.5))
+    b = torch.randn(cout, generator=g) * 0.1
+    r = torch.randn(B, cout, H, W, generator=g)
+    ref = F.silu(F.conv2d(x.double(), w.double(), b.double(), padding=1))
+    wd = w.to(cuda)
+    prep = _hip.conv3x3_prepare(wd)
+    y = _hip.conv3x3_silu(x.to(cuda), b.to(cuda), lambda: prep, cout).cpu().double()
+    miopen = F.silu(F.conv2d(x.to(cuda), wd, b.to(cuda), padding=1)).cpu().double()
+    err, err_m = float((y - ref).abs().max()), float((miopen - ref).abs().max())
+    ok, e, _ = tol_close(y, ref, 5e-5, 1e-4)
+    assert ok, f"{shape}: max abs err {e:.3g} (MIOpen fp32 {err_m:.3g})"
+    assert err <= 8 * err_m + 1e-5, (err, err_m)
+    if W % 4 == 0:  # residual + concat slice: bit-identical to the plain output + res (the add is the last op)
+        buf = torch.full((B, cout + 64, H, W), float("nan"), device=cuda)
+        out = buf[:, 32:32 + cout]
+        _hip.conv3x3_silu(x.to(cuda), b.to(cuda), lambda: prep, cout, out=out, res=r.to(cuda))
+        y0 = _hip.conv3x3_silu(x.to(cuda), b.to(cuda), lambda: prep, cout)
+        assert torch.equal(out, y0 + r.to(cuda))
+        assert torch.isnan(buf[:, :32]).all() and torch.isnan(buf[:, 32 + cout:]).all()
+
+
+def test_neck_c2f_convs_take_the_kernel(cuda, monkeypatch):
+    """The neck C2fs' Bottleneck 3x3 convs (12 at the paper scale) route to the stride-1 kernel and the model matches
+    the MIOpen path (YOLOSOD_S1_NECK=0) within fp32 accuracy."""
+    from yolosod_amd.nn import modules as M
+    from yolosod_amd.nn.tasks import build_model
+    m = build_model("yolov12-sod-fusion-v5-simple.yaml", seed=0, device=cuda)
+    x = torch.rand(2, 3, 640, 640, generator=torch.Generator().manual_seed(5)).to(cuda)  # (at 320, P5 is 10 wide)
+    with torch.inference_mode():
+        with _hip.op_timer() as t:
+            y = m(x)[0]
+        n1 = sum(1 for k, _ in t.durations_ms() if k[0] == "conv3x3")
+        monkeypatch.setattr(M, "S1_NECK", False)
+        with _hip.op_timer() as t:
+            y0 = m(x)[0]
+        n0 = sum(1 for k, _ in t.durations_ms() if k[0] == "conv3x3")  # the Detect towers only
+    assert n1 - n0 == 12, (n1, n0)
     ok, e, _ = tol_close(y.cpu().double(), y0.cpu().double(), 1e-3, 1e-4)
     assert ok, e

@@ -66,6 +66,9 @@ SIGNATURES = {
     "yolosod_conv3x3_prep_bytes": (_sz, [_i]),
     "yolosod_conv3x3_prepare": (_i, [_vp, _i, _vp, _sz, _vp]),
     "yolosod_conv3x3_silu": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _sz, _vp]),
+    "yolosod_conv3x3_prep_bytes_ex": (_sz, [_i, _i]),
+    "yolosod_conv3x3_prepare_ex": (_i, [_vp, _i, _i, _vp, _sz, _vp]),
+    "yolosod_conv3x3_silu_ex": (_i, [_vp, _vp, _l, _vp, _l, _i, _i, _i, _i, _i, _vp, _vp, _sz, _vp]),
     "yolosod_debug_set_swin_fused": (None, [_i]),
     "yolosod_debug_set_swin_x3": (_i, [_i]),
     "yolosod_debug_set_head_x2": (_i, [_i]),
@@ -749,41 +752,61 @@ def conv1x1(x, w, bias, act, out=None, res=None):
 
 
 def conv3x3_ok(x, conv) -> bool:
-    """Shapes the fp16-split 3x3 conv kernel takes (yolosod_conv3x3_silu): fp32 contiguous NCHW on a GPU, 3x3 /
-    stride 1 / pad 1 / dilation 1 / groups 1, 64 outputs, Cin a multiple of 32."""
+    """Shapes the fp16-split 3x3 conv kernel takes (yolosod_conv3x3_silu_ex): fp32 contiguous NCHW on a GPU,
+    3x3 / stride 1 / pad 1 / dilation 1 / groups 1, 32 or a multiple of 64 (<= 512) outputs, Cin a multiple of 32."""
     return (x.device.type == "cuda" and x.dtype == torch.float32 and x.is_contiguous() and x.dim() == 4
             and conv.kernel_size == (3, 3) and conv.stride == (1, 1) and conv.padding == (1, 1)
-            and conv.dilation == (1, 1) and conv.groups == 1 and conv.out_channels == 64
-            and conv.in_channels % 32 == 0 and x.shape[1] == conv.in_channels
-            and int(load_library().yolosod_conv3x3_prep_bytes(int(conv.in_channels))) > 0)
+            and conv.dilation == (1, 1) and conv.groups == 1 and x.shape[1] == conv.in_channels
+            and int(load_library().yolosod_conv3x3_prep_bytes_ex(int(conv.in_channels), int(conv.out_channels))) > 0)
 
 
 def conv3x3_prepare(w):
-    """Prepared block (fragment-major fp16 split planes of 64 W, uint8 tensor) of a [64, Cin, 3, 3] fp32 weight."""
+    """Prepared block (fragment-major fp16 split planes of 64 W, uint8 tensor) of a [Cout, Cin, 3, 3] fp32 weight."""
     lib = load_library()
-    cin = int(w.shape[1])
-    nbytes = int(lib.yolosod_conv3x3_prep_bytes(cin))
+    cout, cin = int(w.shape[0]), int(w.shape[1])
+    nbytes = int(lib.yolosod_conv3x3_prep_bytes_ex(cin, cout))
+    if nbytes == 0:
+        raise RuntimeError(f"conv3x3: (Cin={cin}, Cout={cout}) unsupported")
     blk = torch.empty(nbytes, dtype=torch.uint8, device=w.device)
     wc = w.detach().float().contiguous()
-    _check(_launch(("conv3x3_prep", (64, cin), None), w.device, lib.yolosod_conv3x3_prepare, _dev(wc, "weight"), cin,
-                   blk.data_ptr(), nbytes, _stream(w.device)), "conv3x3_prepare")
+    _check(_launch(("conv3x3_prep", (cout, cin), None), w.device, lib.yolosod_conv3x3_prepare_ex, _dev(wc, "weight"),
+                   cin, cout, blk.data_ptr(), nbytes, _stream(w.device)), "conv3x3_prepare")
     return blk
 
 
-def conv3x3_silu(x, bias, prep):
-    """SiLU(conv3x3(x) + bias) with 64 outputs on the fp16 two-term split MFMA (csrc/conv3x3.hip); ``prep`` is a
-    callable returning the cached prepared block of the weights (conv3x3_prepare)."""
+def _img_view(t, shape, name):
+    """t is a [B, C, H, W] fp32 view on the GPU whose images are contiguous (a channel slice of a concat buffer)."""
+    B, C, H, W = shape
+    if (tuple(t.shape) != tuple(shape) or t.dtype != torch.float32 or t.device.type != "cuda"
+            or t.stride()[1:] != (H * W, W, 1) or t.data_ptr() % 16 or t.stride(0) % 4):
+        raise RuntimeError(f"{name} {tuple(t.shape)} / {t.stride()} is not a [{B}, {C}, {H}, {W}] fp32 view with "
+                           "contiguous 16-byte aligned images")
+
+
+def conv3x3_silu(x, bias, prep, cout=64, out=None, res=None):
+    """SiLU(conv3x3(x) + bias) (+ res) on the fp16 two-term split MFMA (csrc/conv3x3.hip); ``prep`` is a callable
+    returning the cached prepared block of the weights (conv3x3_prepare); ``out``: a [B, Cout, H, W] view with
+    contiguous images (a concat slice) to write; ``res``: the residual added after the activation (same shape)."""
     lib = load_library()
     B, Cin, H, W = x.shape
-    y = torch.empty((B, 64, H, W), dtype=torch.float32, device=x.device)
+    if out is None:
+        y = torch.empty((B, cout, H, W), dtype=torch.float32, device=x.device)
+    else:
+        _img_view(out, (B, cout, H, W), "conv3x3: out")
+        y = out
+    if res is not None:
+        _img_view(res, (B, cout, H, W), "conv3x3: res")
     b = bias.detach().float().contiguous()
 
     def run():
         blk = prep()
-        return lib.yolosod_conv3x3_silu(_dev(x, "x"), y.data_ptr(), B, Cin, H, W, _dev(b, "bias"), blk.data_ptr(),
-                                        blk.numel(), _stream(x.device))
+        return lib.yolosod_conv3x3_silu_ex(_dev(x, "x"), y.data_ptr(), y.stride(0),
+                                           None if res is None else res.data_ptr(),
+                                           0 if res is None else res.stride(0), B, Cin, cout, H, W, _dev(b, "bias"),
+                                           blk.data_ptr(), blk.numel(), _stream(x.device))
 
-    _check(_launch(("conv3x3", tuple(x.shape), 64), x.device, run), "conv3x3")
+    _check(_launch(("conv3x3", tuple(x.shape), cout) + (("res",) if res is not None else ()), x.device, run),
+           "conv3x3")
     return y
 
 

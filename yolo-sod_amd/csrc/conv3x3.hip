@@ -36,21 +36,29 @@ constexpr int NIT = (NQUAD + NT - 1) / NT;  // 11
 struct Args {
   const float* x;      // [B][Cin][H][W]
   const h16_t* wp;     // prepared planes (fragment-major, x 64)
-  const float* bias;   // [64]
-  float* y;            // [B][64][H][W]
+  const float* bias;   // [Cout]
+  float* y;            // image b's output [Cout][H][W] at y + b ybs (a channel slice of a concat buffer when
+  long ybs;            // ybs > Cout H W)
+  const float* res;    // RES: residual added after the activation (Bottleneck shortcut), image b at res + b rbs
+  long rbs;
   int cin, H, W, tiles_x, tiles_y;
+  int ncb_all;         // 16-channel blocks of the prepared weights (Cout / 16)
   unsigned* range_flag;
   const unsigned* prep_flag;
 };
 
 // ABL (timing ablations, wrong results; yolosod_debug_set_conv3x3_abl): 1 no halo loads, 2 every weight fragment from
 // one address, 4 no MFMA (a VALU stand-in keeps the LDS reads), 8 no output stores. V4: W % 4 == 0 (16-byte stores).
-template <int ABL, bool V4>
+// CBW: 16-channel blocks per wave (2: output groups of 64 channels; 1: of 32, the neck's C2f at P2), the workgroup's
+// group = blockIdx % groups (the groups of a tile run side by side and share its input in L2). RES: + residual.
+template <int ABL, bool V4, int CBW = 2, bool RES = false>
 __global__ __launch_bounds__(256, 2) void conv3x3_x2_kernel(Args p) {
   __shared__ __attribute__((aligned(16))) h16_t Pl[2 * PL];
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l15 = lane & 15, g = lane >> 4;
-  const int t_lin = blockIdx.x;
+  const int ngrp = p.ncb_all / (2 * CBW);
+  const int grp = blockIdx.x % ngrp;
+  const int t_lin = blockIdx.x / ngrp;
   const int tx = t_lin % p.tiles_x, ty = (t_lin / p.tiles_x) % p.tiles_y, b = t_lin / (p.tiles_x * p.tiles_y);
   const int H = p.H, W = p.W, HWi = H * W;
   const int x0 = tx * TW - 1, y0 = ty * TH - 1;  // halo origin
@@ -69,7 +77,10 @@ __global__ __launch_bounds__(256, 2) void conv3x3_x2_kernel(Args p) {
         (short)0, __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
   };
   const __amdgpu_buffer_rsrc_t rx = rsrc(xb, (unsigned)((long)p.cin * HWi * 4));
-  const __amdgpu_buffer_rsrc_t rw = rsrc(p.wp, (unsigned)(9L * nq * 8 * 1024));
+  // the last chunk's "next chunk" loads go through an empty resource: out of range, they return 0 without a memory
+  // access (the loads stay unconditional) and no residual / epilogue wait queues behind a needless reload
+  const __amdgpu_buffer_rsrc_t rx0 = rsrc(xb, 0u);
+  const __amdgpu_buffer_rsrc_t rw = rsrc(p.wp, (unsigned)(9L * nq * p.ncb_all * 2 * 1024));
   unsigned voff[NIT];
   bool okp[NIT];
 #pragma unroll
@@ -83,8 +94,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3_x2_kernel(Args p) {
   }
   f32x4 sv[NIT];
   // loads k = 4 i + c in [k0, k1) of chunk q's staging (item i, channel c of its quad)
-  auto load_part = [&](int q, int k0, int k1) __attribute__((always_inline)) {
+  auto load_part = [&](int q, int k0, int k1, bool live) __attribute__((always_inline)) {
     const int sx = __builtin_amdgcn_readfirstlane(32 * q * HWi * 4);
+    const __amdgpu_buffer_rsrc_t r = live ? rx : rx0;
 #pragma unroll
     for (int k = 0; k < 4 * NIT; ++k)
       if (k >= k0 && k < k1) {
@@ -92,7 +104,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_x2_kernel(Args p) {
           sv[k >> 2][k & 3] = 0.5f + (float)q;
         else
           sv[k >> 2][k & 3] = __builtin_bit_cast(
-              float, __builtin_amdgcn_raw_buffer_load_b32(rx, voff[k >> 2], sx + (k & 3) * HWi * 4, 0));
+              float, __builtin_amdgcn_raw_buffer_load_b32(r, voff[k >> 2], sx + (k & 3) * HWi * 4, 0));
       }
   };
   auto store_chunk = [&]() __attribute__((always_inline)) {
@@ -119,20 +131,21 @@ __global__ __launch_bounds__(256, 2) void conv3x3_x2_kernel(Args p) {
   int bpx[8];
 #pragma unroll
   for (int cb = 0; cb < 8; ++cb) bpx[cb] = (4 * ph + (cb >> 1)) * HW_ + (cb & 1) * 16 + l15;
-  // weight fragments of (tap t, chunk q): row blocks 2 rp + r (r = 0, 1), planes 0 / 1; tap t's fragments of chunk q
-  // start at byte ((t nq + q) 8) KB, [row block][plane][lane][16 bytes] (the B-operand lane layout is the A one)
+  // weight fragments of (tap t, chunk q): channel blocks cbw0 + r (r < CBW), planes 0 / 1; tap t's fragments of chunk
+  // q start at byte ((t nq + q) ncb_all 2) KB, [channel block][plane][lane][16 bytes] (B-operand lane layout = A's)
+  const int cbw0 = grp * 2 * CBW + CBW * rp;
   auto wfrag = [&](int t, int q, int r, int pl) __attribute__((always_inline)) {
-    const int st = (ABL & 2) ? 0 : __builtin_amdgcn_readfirstlane(((t * nq + q) * 8) * 1024);
+    const int st = (ABL & 2) ? 0 : __builtin_amdgcn_readfirstlane(((t * nq + q) * p.ncb_all * 2) * 1024);
     return __builtin_bit_cast(f16x8_t, __builtin_amdgcn_raw_buffer_load_b128(
-                                           rw, (unsigned)((((2 * rp + r) * 2 + pl) * 64 + lane) * 16), st, 0));
+                                           rw, (unsigned)((((cbw0 + r) * 2 + pl) * 64 + lane) * 16), st, 0));
   };
-  f32x4 acc[2][8];
+  f32x4 acc[CBW][8];
 #pragma unroll
-  for (int r = 0; r < 2; ++r)
+  for (int r = 0; r < CBW; ++r)
 #pragma unroll
     for (int cb = 0; cb < 8; ++cb) acc[r][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  load_part(0, 0, 4 * NIT);
+  load_part(0, 0, 4 * NIT, true);
   for (int q = 0; q < nq; ++q) {
     __syncthreads();  // every wave is done with the previous chunk's planes
     store_chunk();
@@ -144,9 +157,10 @@ __global__ __launch_bounds__(256, 2) void conv3x3_x2_kernel(Args p) {
     // next tap) to save registers. Unconditional: the last chunk reloads itself (loads under a branch merge into phis
     // whose copies wait for every load in flight).
     const int qn = q + 1 < nq ? q + 1 : q;
-    f16x8_t wa[2][2], wn[2][2];
+    const bool nlive = q + 1 < nq;
+    f16x8_t wa[CBW][2], wn[CBW][2];
 #pragma unroll
-    for (int r = 0; r < 2; ++r) {
+    for (int r = 0; r < CBW; ++r) {
       wa[r][0] = wfrag(0, q, r, 0);
       wa[r][1] = wfrag(0, q, r, 1);
     }
@@ -155,11 +169,11 @@ __global__ __launch_bounds__(256, 2) void conv3x3_x2_kernel(Args p) {
     for (int t = 0; t < 9; ++t) {
       const int tn = t + 1 < 9 ? t + 1 : t;  // one tap ahead (unconditional)
 #pragma unroll
-      for (int r = 0; r < 2; ++r) {
+      for (int r = 0; r < CBW; ++r) {
         wn[r][0] = wfrag(tn, q, r, 0);
         wn[r][1] = wfrag(tn, q, r, 1);
       }
-      load_part(qn, 5 * t, t == 8 ? 4 * NIT : 5 * t + 5);
+      load_part(qn, 5 * t, t == 8 ? 4 * NIT : 5 * t + 5, nlive);
       __builtin_amdgcn_sched_barrier(0);
       const int toff = (t / 3) * HW_ + (t % 3);
 #pragma unroll
@@ -168,7 +182,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_x2_kernel(Args p) {
         const f16x8_t xh = *reinterpret_cast<const f16x8_t*>(src);
         const f16x8_t xlo = *reinterpret_cast<const f16x8_t*>(src + PL);
 #pragma unroll
-        for (int r = 0; r < 2; ++r) {
+        for (int r = 0; r < CBW; ++r) {
           if constexpr ((ABL & 4) != 0) {
             acc[r][cb][0] += (float)xh[0] * (float)wa[r][0][0] + (float)xlo[1] * (float)wa[r][1][1];
           } else {  // the three split products, small terms first
@@ -179,7 +193,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_x2_kernel(Args p) {
         }
       }
 #pragma unroll
-      for (int r = 0; r < 2; ++r) {
+      for (int r = 0; r < CBW; ++r) {
         wa[r][0] = wn[r][0];
         wa[r][1] = wn[r][1];
       }
@@ -188,21 +202,27 @@ __global__ __launch_bounds__(256, 2) void conv3x3_x2_kernel(Args p) {
   // epilogue: lane (g, l15) of (r, cb) holds output channel 16 (2 rp + r) + l15, pixels (row 4 ph + (cb >> 1),
   // columns (cb & 1) 16 + 4 g .. + 3) of the tile. SiLU on the hardware exp2 / rcp (~2^-22 relative, below the split
   // products' own few-ulp error)
-  float* yb = p.y + (long)b * 64 * HWi;
-  float bv[2];
+  float* yb = p.y + (long)b * p.ybs;
+  float bv[CBW];
 #pragma unroll
-  for (int r = 0; r < 2; ++r) bv[r] = p.bias[16 * (2 * rp + r) + l15];
+  for (int r = 0; r < CBW; ++r) bv[r] = p.bias[16 * (cbw0 + r) + l15];
 #pragma unroll
   for (int cb = 0; cb < 8; ++cb) {
     const int oy = ty * TH + 4 * ph + (cb >> 1), ox = tx * TW + (cb & 1) * 16 + 4 * g;
     if constexpr ((ABL & 8) != 0)
       if (acc[0][cb][0] != -1.2345e30f) continue;
 #pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      float* d = yb + (16 * (2 * rp + r) + l15) * HWi + oy * W + ox;
+    for (int r = 0; r < CBW; ++r) {
+      const long po = (long)(16 * (cbw0 + r) + l15) * HWi + oy * W + ox;
+      float* d = yb + po;
       f32x4 o;
 #pragma unroll
       for (int j = 0; j < 4; ++j) o[j] = silu_fast_(acc[r][cb][j] * (1.0f / WSC) + bv[r]);
+      if constexpr (RES) {  // act(conv + b) + x (Bottleneck shortcut, block.py:343); V4 shapes only
+#pragma clang fp contract(off)  // a separately rounded add, as x + cv2(...): no fma with SiLU's last multiply
+        static_assert(!RES || V4, "residual: W % 4 == 0");
+        if (oy < H && ox < W) o = o + *reinterpret_cast<const f32x4*>(p.res + (long)b * p.rbs + po);
+      }
       if constexpr (V4) {  // W % 4 == 0: the 4 pixels are all in or all out of the image
         // non-temporal: the tile is not read again before it has left the caches (at P2 the kernel is 13 % faster)
         if (oy < H && ox < W) __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(d));
@@ -219,18 +239,19 @@ __global__ __launch_bounds__(256, 2) void conv3x3_x2_kernel(Args p) {
 
 // W [64][Cin][3][3] -> fragment-major planes of 64 W (see the file comment); one thread per (output channel, input
 // channel, tap). The block's own range word records whether 64 W left fp16's range (re-reported by every launch).
-__global__ __launch_bounds__(256) void conv3x3_prep_kernel(const float* __restrict__ w, int cin, h16_t* __restrict__ wp,
-                                                           unsigned* range_flag, unsigned* prep_flag) {
+__global__ __launch_bounds__(256) void conv3x3_prep_kernel(const float* __restrict__ w, int cin, int cout,
+                                                           h16_t* __restrict__ wp, unsigned* range_flag,
+                                                           unsigned* prep_flag) {
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  const long n_all = 64L * cin * 9;
+  const long n_all = (long)cout * cin * 9;
   if (i >= n_all) return;
   const int t = (int)(i % 9), k = (int)((i / 9) % cin), n = (int)(i / (9L * cin));
   const float v = w[i] * WSC;
   const _Float16 hh = (_Float16)v;
   const _Float16 ll = (_Float16)(v - (float)hh);
-  const int nq = cin >> 5, q = k >> 5, kk = k & 31, rb = n >> 4;
+  const int nq = cin >> 5, q = k >> 5, kk = k & 31, rb = n >> 4, ncb = cout >> 4;
   const int ln = ((kk >> 3) << 4) + (n & 15);
-  const long base = ((long)((t * nq + q) * 4 + rb) * 2) * 512 + ln * 8 + (kk & 7);
+  const long base = ((long)((t * nq + q) * ncb + rb) * 2) * 512 + ln * 8 + (kk & 7);
   wp[base] = __builtin_bit_cast(h16_t, hh);
   wp[base + 512] = __builtin_bit_cast(h16_t, ll);
   const float m = fabsf(v);
@@ -250,67 +271,100 @@ YS_EXPORT int yolosod_debug_set_conv3x3_abl(int abl) {
   return old;
 }
 
-// 3x3 / stride 1 / pad 1 conv with 64 outputs: Cin a multiple of 32 (<= 2048)
-YS_EXPORT size_t yolosod_conv3x3_prep_bytes(int cin) {
-  if (cin <= 0 || cin % 32 || cin > 2048) return 0;
+static bool c3_cout_ok(int cout) { return cout == 32 || (cout % 64 == 0 && cout <= 512); }
+
+// 3x3 / stride 1 / pad 1 conv with Cout 32 or a multiple of 64 (<= 512): Cin a multiple of 32 (<= 2048)
+YS_EXPORT size_t yolosod_conv3x3_prep_bytes_ex(int cin, int cout) {
+  if (cin <= 0 || cin % 32 || cin > 2048 || !c3_cout_ok(cout)) return 0;
   Sizer s;
-  s.take<h16_t>((size_t)2 * 64 * cin * 9);
+  s.take<h16_t>((size_t)2 * cout * cin * 9);
   s.take<unsigned>(1);
   return s.off;
 }
+YS_EXPORT size_t yolosod_conv3x3_prep_bytes(int cin) { return yolosod_conv3x3_prep_bytes_ex(cin, 64); }
 
-static bool conv3x3_carve(void* buf, size_t bytes, int cin, h16_t** wp, unsigned** flag) {
+static bool conv3x3_carve(void* buf, size_t bytes, int cin, int cout, h16_t** wp, unsigned** flag) {
   Carver cv(buf, bytes);
-  *wp = cv.take<h16_t>((size_t)2 * 64 * cin * 9);
+  *wp = cv.take<h16_t>((size_t)2 * cout * cin * 9);
   *flag = cv.take<unsigned>(1);
   return *flag != nullptr;
 }
 
-// Weight preparation (re-run whenever the weights change): w [64][cin][3][3] fp32 (BN folded) -> prep block.
-YS_EXPORT int yolosod_conv3x3_prepare(const float* w, int cin, void* prep, size_t prep_bytes, void* stream) {
+// Weight preparation (re-run whenever the weights change): w [cout][cin][3][3] fp32 (BN folded) -> prep block.
+YS_EXPORT int yolosod_conv3x3_prepare_ex(const float* w, int cin, int cout, void* prep, size_t prep_bytes,
+                                         void* stream) {
   YS_CHECK_ARG(w && prep, "conv3x3_prepare: null pointer");
-  YS_CHECK_ARG(yolosod_conv3x3_prep_bytes(cin) > 0, "conv3x3_prepare: cin=%d unsupported (multiple of 32)", cin);
+  YS_CHECK_ARG(yolosod_conv3x3_prep_bytes_ex(cin, cout) > 0, "conv3x3_prepare: (cin=%d, cout=%d) unsupported", cin,
+               cout);
   h16_t* wp;
   unsigned* flag;
-  YS_CHECK_ARG(conv3x3_carve(prep, prep_bytes, cin, &wp, &flag), "conv3x3_prepare: block too small (%zu)", prep_bytes);
+  YS_CHECK_ARG(conv3x3_carve(prep, prep_bytes, cin, cout, &wp, &flag), "conv3x3_prepare: block too small (%zu)",
+               prep_bytes);
   hipStream_t st = (hipStream_t)stream;
   if (hipMemsetAsync(flag, 0, sizeof(unsigned), st) != hipSuccess) {
     set_error("conv3x3_prepare: flag reset failed");
     return -1;
   }
-  const long n = 64L * cin * 9;
-  hipLaunchKernelGGL(c3::conv3x3_prep_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, w, cin, wp,
+  const long n = (long)cout * cin * 9;
+  hipLaunchKernelGGL(c3::conv3x3_prep_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, w, cin, cout, wp,
                      range_flag_dev(), flag);
   YS_CHECK_LAUNCH("conv3x3_prep");
   return 0;
 }
+YS_EXPORT int yolosod_conv3x3_prepare(const float* w, int cin, void* prep, size_t prep_bytes, void* stream) {
+  return yolosod_conv3x3_prepare_ex(w, cin, 64, prep, prep_bytes, stream);
+}
 
-// y = SiLU(conv3x3(x, W) + bias), x [B][cin][H][W] -> y [B][64][H][W] (fp32, contiguous; y must not alias x).
-YS_EXPORT int yolosod_conv3x3_silu(const float* x, float* y, int B, int cin, int H, int W, const float* bias,
-                                   const void* prep, size_t prep_bytes, void* stream) {
+// y = SiLU(conv3x3(x, W) + bias) (+ res): x [B][cin][H][W] -> image b's output [cout][H][W] at y + b y_bstride
+// (y_bstride >= cout H W: a channel slice of a concat buffer); res (or NULL): image b at res + b res_bstride, added
+// after the activation (Bottleneck shortcut). y must not alias x.
+YS_EXPORT int yolosod_conv3x3_silu_ex(const float* x, float* y, long y_bstride, const float* res, long res_bstride,
+                                      int B, int cin, int cout, int H, int W, const float* bias, const void* prep,
+                                      size_t prep_bytes, void* stream) {
   YS_CHECK_ARG(x && y && bias && prep, "conv3x3: null pointer");
-  YS_CHECK_ARG(B >= 0 && H > 0 && W > 0 && yolosod_conv3x3_prep_bytes(cin) > 0, "conv3x3: bad shape");
-  YS_CHECK_ARG((long)cin * H * W < (1L << 31) && 64L * H * W < (1L << 31), "conv3x3: plane too large");
-  YS_CHECK_ARG(((uintptr_t)bias & 15) == 0, "conv3x3: bias must be 16-byte aligned");
+  YS_CHECK_ARG(B >= 0 && H > 0 && W > 0 && yolosod_conv3x3_prep_bytes_ex(cin, cout) > 0, "conv3x3: bad shape");
+  YS_CHECK_ARG((long)cin * H * W < (1L << 31) && (long)cout * H * W < (1L << 31), "conv3x3: plane too large");
+  YS_CHECK_ARG(y_bstride >= (long)cout * H * W, "conv3x3: output batch stride %ld < %ld", y_bstride,
+               (long)cout * H * W);
+  const bool v4 = W % 4 == 0;
+  YS_CHECK_ARG(!v4 || (((uintptr_t)y & 15) == 0 && y_bstride % 4 == 0), "conv3x3: output not 16-byte aligned");
+  YS_CHECK_ARG(!res || (v4 && ((uintptr_t)res & 15) == 0 && res_bstride % 4 == 0 && res_bstride >= (long)cout * H * W),
+               "conv3x3: the residual needs W %% 4 == 0 and 16-byte aligned images");
   if (B == 0) return 0;
   h16_t* wp;
   unsigned* flag;
-  YS_CHECK_ARG(conv3x3_carve(const_cast<void*>(prep), prep_bytes, cin, &wp, &flag), "conv3x3: prepared block too small");
-  c3::Args a{x, wp, bias, y, cin, H, W, (W + c3::TW - 1) / c3::TW, (H + c3::TH - 1) / c3::TH, range_flag_dev(), flag};
-  const long nwg = (long)B * a.tiles_x * a.tiles_y;
+  YS_CHECK_ARG(conv3x3_carve(const_cast<void*>(prep), prep_bytes, cin, cout, &wp, &flag),
+               "conv3x3: prepared block too small");
+  c3::Args a{x, wp, bias, y, y_bstride, res, res_bstride, cin, H, W, (W + c3::TW - 1) / c3::TW,
+             (H + c3::TH - 1) / c3::TH, cout / 16, range_flag_dev(), flag};
+  const int ngrp = cout == 32 ? 1 : cout / 64;
+  const long nwg = (long)B * a.tiles_x * a.tiles_y * ngrp;
   YS_CHECK_ARG(nwg < (1L << 31), "conv3x3: too many tiles");
-  const bool v4 = W % 4 == 0;
+  hipStream_t st = (hipStream_t)stream;
   auto kern = v4 ? c3::conv3x3_x2_kernel<0, true> : c3::conv3x3_x2_kernel<0, false>;
-  switch (g_c3_abl) {  // timing ablations (W % 4 == 0 shapes)
-    case 1: kern = c3::conv3x3_x2_kernel<1, true>; break;
-    case 2: kern = c3::conv3x3_x2_kernel<2, true>; break;
-    case 4: kern = c3::conv3x3_x2_kernel<4, true>; break;
-    case 8: kern = c3::conv3x3_x2_kernel<8, true>; break;
-    case 12: kern = c3::conv3x3_x2_kernel<12, true>; break;
-    case 15: kern = c3::conv3x3_x2_kernel<15, true>; break;
-    default: break;
+  if (cout == 32) {
+    kern = res ? c3::conv3x3_x2_kernel<0, true, 1, true>
+               : (v4 ? c3::conv3x3_x2_kernel<0, true, 1, false> : c3::conv3x3_x2_kernel<0, false, 1, false>);
+  } else if (res) {
+    kern = c3::conv3x3_x2_kernel<0, true, 2, true>;
+  } else if (cout == 64 && v4) {
+    switch (g_c3_abl) {  // timing ablations (W % 4 == 0 shapes, Cout 64)
+      case 1: kern = c3::conv3x3_x2_kernel<1, true>; break;
+      case 2: kern = c3::conv3x3_x2_kernel<2, true>; break;
+      case 4: kern = c3::conv3x3_x2_kernel<4, true>; break;
+      case 8: kern = c3::conv3x3_x2_kernel<8, true>; break;
+      case 12: kern = c3::conv3x3_x2_kernel<12, true>; break;
+      case 15: kern = c3::conv3x3_x2_kernel<15, true>; break;
+      default: break;
+    }
   }
-  hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(256), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(256), 0, st, a);
   YS_CHECK_LAUNCH("conv3x3");
   return 0;
+}
+
+// 3x3 / stride 1 / pad 1 conv with 64 outputs, contiguous y [B][64][H][W].
+YS_EXPORT int yolosod_conv3x3_silu(const float* x, float* y, int B, int cin, int H, int W, const float* bias,
+                                   const void* prep, size_t prep_bytes, void* stream) {
+  return yolosod_conv3x3_silu_ex(x, y, 64L * H * W, nullptr, 0, B, cin, 64, H, W, bias, prep, prep_bytes, stream);
 }

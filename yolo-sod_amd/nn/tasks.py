@@ -440,6 +440,11 @@ class DetectionModel(BaseModel):
             if (i >= n_backbone and isinstance(m, M.Conv) and not isinstance(m, M.DWConv)
                     and m.conv.kernel_size == (3, 3) and m.conv.stride == (2, 2) and m.conv.groups == 1):
                 m.s2 = True
+            if i >= n_backbone and isinstance(m, M.C2f):  # the neck C2fs' Bottleneck 3x3 convs (S1_NECK)
+                for bt in m.m:
+                    for cv in (bt.cv1, bt.cv2):
+                        if cv.conv.kernel_size == (3, 3) and cv.conv.stride == (1, 1) and cv.conv.groups == 1:
+                            cv.s1 = True
 
         # lazy SE weights: the reference creates them during the stride probe, in forward (= layer) order,
         # after every eager module -> same RNG stream position here.
