@@ -296,11 +296,11 @@ def test_neck_stride2_convs_take_the_kernel(gpu_model, cuda):
             M.S2_NECK = True
             with _hip.op_timer() as t:
                 y1 = gpu_model(x)[0].clone()
-            plain = [k for k, _ in t.durations_ms() if k[0] == "conv3x3s2" and k[3] == (False, False)]
+            plain = [k for k, _ in t.durations_ms() if k[0] == "conv3x3s2" and k[2][1:] == (False, False)]
             M.S2_NECK = False
             y0 = gpu_model(x)[0].clone()
     finally:
         M.S2_NECK = saved
-    assert sorted(k[2] for k in plain) == [128, 256, 512], plain
+    assert sorted(k[2][0] for k in plain) == [128, 256, 512], plain
     ok, e, _ = tol_close(y1.cpu().double(), y0.cpu().double(), 1e-3, 1e-4)
     assert ok, e

@@ -805,8 +805,7 @@ def conv3x3_silu(x, bias, prep, cout=64, out=None, res=None):
                                            0 if res is None else res.stride(0), B, Cin, cout, H, W, _dev(b, "bias"),
                                            blk.data_ptr(), blk.numel(), _stream(x.device))
 
-    _check(_launch(("conv3x3", tuple(x.shape), cout) + (("res",) if res is not None else ()), x.device, run),
-           "conv3x3")
+    _check(_launch(("conv3x3", tuple(x.shape), cout if res is None else (cout, "res")), x.device, run), "conv3x3")
     return y
 
 
@@ -841,7 +840,7 @@ def conv3x3s2_silu(x, bias, prep, cout, gate_c=None, gate_p=None, key=None, out=
     """SiLU(conv3x3_stride2((x * gate_c) * gate_p) + bias) on the fp16 two-term split MFMA (csrc/conv3x3s2.hip):
     gate_c [B, Cin] (an SE / CBAM channel gate), gate_p [B, H, W] (CBAM's spatial gate), either may be None.
     ``prep``: a callable returning the cached prepared block (conv3x3s2_prepare); ``key``: the op_timer key (default
-    ("conv3x3s2", shape, Cout, gates)); ``out``: a [B, Cout, Ho, Wo] fp32 view whose images are contiguous (e.g. a
+    ("conv3x3s2", shape, (Cout, gate_c given, gate_p given))); ``out``: a [B, Cout, Ho, Wo] fp32 view whose images are contiguous (e.g. a
     channel slice of a concat buffer) to write instead of a new tensor."""
     lib = load_library()
     B, Cin, H, W = x.shape
@@ -870,7 +869,7 @@ def conv3x3s2_silu(x, bias, prep, cout, gate_c=None, gate_p=None, key=None, out=
                                               _stream(x.device))
 
     if key is None:
-        key = ("conv3x3s2", tuple(x.shape), cout, (gc is not None, gp is not None))
+        key = ("conv3x3s2", tuple(x.shape), (cout, gc is not None, gp is not None))
     _check(_launch(key, x.device, run), "conv3x3s2")
     return y
 
