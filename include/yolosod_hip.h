@@ -300,6 +300,16 @@ int yolosod_conv3x3s2_silu(const float* x, float* y, int B, int cin, int cout, i
 int yolosod_conv3x3s2_silu_out(const float* x, float* y, long y_bstride, int B, int cin, int cout, int H, int W,
                                const float* bias, const float* gc, const float* gp, const void* prep,
                                size_t prep_bytes, void* stream);
+/* 1x1 / stride 1 conv + bias + SiLU on the fp16 two-term split MFMA at fp32 accuracy (csrc/conv1x1x2.hip): the PAN
+ * neck's wide 1x1 convs (C2f cv1 / cv2, lateral convs; conv.py:37-55, block.py:249-253). Cout a multiple of 128 (<= 1024),
+ * Cin a multiple of 32 (<= 4096, weights padded to 128), HW % 4 == 0. x image b at x + b*x_bstride ([cin][HW]); y image
+ * b at y + b*y_bstride ([cout][HW], a concat slice when the stride is larger); y2 (or NULL): channels [c2lo, cout)
+ * stored again at y2 + b*y2_bstride (C2f's first Bottleneck input). Replaces MIOpen's fp32 GEMM + the bias / SiLU pass. */
+size_t yolosod_conv1x1x2_prep_bytes(int cin, int cout);
+int yolosod_conv1x1x2_prepare(const float* w, int cin, int cout, void* prep, size_t prep_bytes, void* stream);
+int yolosod_conv1x1x2_silu(const float* x, long x_bstride, float* y, long y_bstride, float* y2, long y2_bstride,
+                           int c2lo, int B, int cin, int cout, int HW, const float* bias, const void* prep,
+                           size_t prep_bytes, void* stream);
 /* Timing hook: ablation variants of the stride-2 conv kernel at Cout 64 with a channel gate (csrc/conv3x3s2.hip; WRONG
  * results for abl != 0 - scripts/bench_conv3x3s2.py only). Returns the previous value. */
 int yolosod_debug_set_conv3x3s2_abl(int abl);

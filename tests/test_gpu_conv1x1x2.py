@@ -1,0 +1,65 @@
+"""GPU: the PAN neck's wide 1x1 convs on the fp16 two-term split kernel (csrc/conv1x1x2.hip) against the exact
+(fp64) conv + bias + SiLU of the same fp32 weights (ultralytics/nn/modules/conv.py:37-55), next to MIOpen's own fp32
+error: Cout groups of 128, Cin padded to 128 (192), pixel tails (HW not a multiple of 64), concat-slice input and
+output, C2f's dual store; and the model's routing (YOLOSOD_N1_NECK) against the MIOpen path."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oplib import tol_close
+from yolosod_amd import _hip
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("shape,cout", [((2, 256, 40, 40), 128), ((2, 192, 20, 20), 128), ((1, 768, 40, 40), 256),
+                                        ((2, 1024, 20, 20), 512), ((1, 384, 12, 12), 256), ((3, 96, 8, 8), 128)])
+def test_conv1x1x2_matches_fp64(shape, cout, cuda):
+    g = torch.Generator().manual_seed(sum(shape) + cout)
+    B, cin, H, W = shape
+    x = torch.randn(shape, generator=g)
+    w = torch.randn(cout, cin, 1, 1, generator=g) * (1.0 / cin ** 0.5)
+    b = torch.randn(cout, generator=g) * 0.1
+    ref = F.silu(F.conv2d(x.double(), w.double(), b.double()))
+    wd = w.to(cuda)
+    y = _hip.conv1x1x2_silu(x.to(cuda), b.to(cuda), lambda: _hip.conv1x1x2_prepare(wd), cout).cpu().double()
+    miopen = F.silu(F.conv2d(x.to(cuda), wd, b.to(cuda))).cpu().double()
+    err, err_m = float((y - ref).abs().max()), float((miopen - ref).abs().max())
+    ok, e, _ = tol_close(y, ref, 5e-5, 1e-4)
+    assert ok, f"{shape}: max abs err {e:.3g} (MIOpen fp32 {err_m:.3g})"
+    assert err <= 8 * err_m + 1e-5, (err, err_m)
+
+
+def test_conv1x1x2_slices_and_dual_store(cuda):
+    """Input and output as channel slices of concat buffers and the dual store of channels [c2lo, Cout): bit-identical
+    to the contiguous form, the rest of the buffers untouched."""
+    g = torch.Generator().manual_seed(9)
+    xb = torch.randn(2, 320, 16, 20, generator=g).to(cuda)
+    x = xb[:, 32:288]  # 256 channels, batch stride 320 * HW
+    w = (torch.randn(256, 256, generator=g) * 0.06).to(cuda)
+    b = (torch.randn(256, generator=g) * 0.1).to(cuda)
+    prep = _hip.conv1x1x2_prepare(w)
+    y0 = _hip.conv1x1x2_silu(x.contiguous(), b, lambda: prep, 256)
+    z = torch.full((2, 384, 16, 20), float("nan"), device=cuda)
+    t = torch.empty((2, 128, 16, 20), device=cuda)
+    _hip.conv1x1x2_silu(x, b, lambda: prep, 256, out=z[:, :256], out2=t, c2lo=128)
+    assert torch.equal(z[:, :256], y0) and torch.equal(t, y0[:, 128:])
+    assert torch.isnan(z[:, 256:]).all()
+
+
+def test_neck_wide_1x1_convs_take_the_kernel(cuda, monkeypatch):
+    """The neck's wide 1x1 convs route to the kernel (those without a gate-statistics epilogue) and the model matches
+    the MIOpen path (YOLOSOD_N1_NECK=0) within fp32 accuracy."""
+    from yolosod_amd.nn import modules as M
+    from yolosod_amd.nn.tasks import build_model
+    m = build_model("yolov12-sod-fusion-v5-simple.yaml", seed=0, device=cuda)
+    x = torch.rand(2, 3, 640, 640, generator=torch.Generator().manual_seed(6)).to(cuda)
+    with torch.inference_mode():
+        with _hip.op_timer() as t:
+            y = m(x)[0]
+        n = sum(1 for k, _ in t.durations_ms() if k[0] == "conv1x1x2")
+        monkeypatch.setattr(M, "N1_NECK", False)
+        y0 = m(x)[0]
+    assert n >= 8, n
+    ok, e, _ = tol_close(y.cpu().double(), y0.cpu().double(), 1e-3, 1e-4)
+    assert ok, e

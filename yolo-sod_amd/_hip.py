@@ -66,6 +66,9 @@ SIGNATURES = {
     "yolosod_conv3x3_prep_bytes": (_sz, [_i]),
     "yolosod_conv3x3_prepare": (_i, [_vp, _i, _vp, _sz, _vp]),
     "yolosod_conv3x3_silu": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _sz, _vp]),
+    "yolosod_conv1x1x2_prep_bytes": (_sz, [_i, _i]),
+    "yolosod_conv1x1x2_prepare": (_i, [_vp, _i, _i, _vp, _sz, _vp]),
+    "yolosod_conv1x1x2_silu": (_i, [_vp, _l, _vp, _l, _vp, _l, _i, _i, _i, _i, _i, _vp, _vp, _sz, _vp]),
     "yolosod_conv3x3_prep_bytes_ex": (_sz, [_i, _i]),
     "yolosod_conv3x3_prepare_ex": (_i, [_vp, _i, _i, _vp, _sz, _vp]),
     "yolosod_conv3x3_silu_ex": (_i, [_vp, _vp, _l, _vp, _l, _i, _i, _i, _i, _i, _vp, _vp, _sz, _vp]),
@@ -806,6 +809,60 @@ def conv3x3_silu(x, bias, prep, cout=64, out=None, res=None):
                                            blk.data_ptr(), blk.numel(), _stream(x.device))
 
     _check(_launch(("conv3x3", tuple(x.shape), cout if res is None else (cout, "res")), x.device, run), "conv3x3")
+    return y
+
+
+def _imgs_contig(t) -> bool:
+    """[B, C, H, W] whose images are contiguous (any batch stride, e.g. a channel slice of a concat buffer)."""
+    B, C, H, W = t.shape
+    return t.stride()[1:] == (H * W, W, 1) and t.stride(0) % 4 == 0 and t.data_ptr() % 16 == 0
+
+
+def conv1x1x2_ok(x, conv) -> bool:
+    """Shapes the fp16-split 1x1 conv kernel takes (yolosod_conv1x1x2_silu): fp32 on a GPU with contiguous images,
+    1x1 / stride 1 / groups 1, Cout a multiple of 128 (<= 1024), Cin a multiple of 32, H*W a multiple of 4."""
+    return (x.device.type == "cuda" and x.dtype == torch.float32 and x.dim() == 4 and _imgs_contig(x)
+            and conv.kernel_size == (1, 1) and conv.stride == (1, 1) and conv.padding == (0, 0) and conv.groups == 1
+            and x.shape[1] == conv.in_channels and (x.shape[2] * x.shape[3]) % 4 == 0
+            and int(load_library().yolosod_conv1x1x2_prep_bytes(int(conv.in_channels), int(conv.out_channels))) > 0)
+
+
+def conv1x1x2_prepare(w):
+    """Prepared block (fragment-major fp16 split planes of 64 W, Cin padded to 128) of a [Cout, Cin(, 1, 1)] weight."""
+    lib = load_library()
+    cout, cin = int(w.shape[0]), int(w.shape[1])
+    nbytes = int(lib.yolosod_conv1x1x2_prep_bytes(cin, cout))
+    if nbytes == 0:
+        raise RuntimeError(f"conv1x1x2: (Cin={cin}, Cout={cout}) unsupported")
+    blk = torch.empty(nbytes, dtype=torch.uint8, device=w.device)
+    wc = w.detach().float().reshape(cout, cin).contiguous()
+    _check(_launch(("conv1x1x2_prep", (cout, cin), None), w.device, lib.yolosod_conv1x1x2_prepare, _dev(wc, "weight"),
+                   cin, cout, blk.data_ptr(), nbytes, _stream(w.device)), "conv1x1x2_prepare")
+    return blk
+
+
+def conv1x1x2_silu(x, bias, prep, cout, out=None, out2=None, c2lo=0):
+    """SiLU(W x + bias) for a 1x1 conv on the fp16 two-term split MFMA (csrc/conv1x1x2.hip). ``x``, ``out`` may be
+    channel slices of concat buffers (contiguous images); ``out2``: channels [c2lo, Cout) stored again (packed)."""
+    lib = load_library()
+    B, Cin, H, W = x.shape
+    if out is None:
+        y = torch.empty((B, cout, H, W), dtype=torch.float32, device=x.device)
+    else:
+        _img_view(out, (B, cout, H, W), "conv1x1x2: out")
+        y = out
+    if out2 is not None:
+        _img_view(out2, (B, cout - c2lo, H, W), "conv1x1x2: out2")
+    b = bias.detach().float().contiguous()
+
+    def run():
+        blk = prep()
+        return lib.yolosod_conv1x1x2_silu(x.data_ptr(), x.stride(0), y.data_ptr(), y.stride(0),
+                                          None if out2 is None else out2.data_ptr(),
+                                          0 if out2 is None else out2.stride(0), int(c2lo), B, Cin, cout, H * W,
+                                          _dev(b, "bias"), blk.data_ptr(), blk.numel(), _stream(x.device))
+
+    _check(_launch(("conv1x1x2", tuple(x.shape), (cout, out2 is not None)), x.device, run), "conv1x1x2")
     return y
 
 

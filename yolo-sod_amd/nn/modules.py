@@ -105,11 +105,14 @@ S2_NECK = os.environ.get("YOLOSOD_S2_NECK", "1") != "0"
 # the PAN neck's C2f Bottleneck 3x3 convs (layers 17 / 22 / 27 / 31 / 35 / 38) on the fp16-split stride-1 kernel, the
 # shortcut added and the output written into the C2f concat slice in its epilogue; YOLOSOD_S1_NECK=0: MIOpen
 S1_NECK = os.environ.get("YOLOSOD_S1_NECK", "1") != "0"
+# the PAN neck's wide 1x1 convs (Cout a multiple of 128: C2f cv1 / cv2, lateral convs) on the fp16-split 1x1 kernel
+# (csrc/conv1x1x2.hip) with bias / SiLU / concat slice / C2f's dual store in its epilogue; YOLOSOD_N1_NECK=0: MIOpen
+N1_NECK = os.environ.get("YOLOSOD_N1_NECK", "1") != "0"
 CONV3X3_MIN_TILES = int(os.environ.get("YOLOSOD_CONV3X3_MIN_TILES", "0"))
 
 
 def conv_epilogue(conv: nn.Conv2d, act_code, x, out=None, res=None, stats=None, out2=None, c2lo=0, tower=False,
-                  s2=False, s1=False):
+                  s2=False, s1=False, n1=False):
     """GPU fast path of ``act(conv(x)) (+ res)``: MIOpen conv without bias, then one HIP pass for bias +
     activation (+ shortcut), optionally written straight into a channel slice ``out`` of a concat buffer.
     ``stats`` ("sum" / "summax"): the same pass emits the output's per-plane partial statistics for a following
@@ -118,6 +121,7 @@ def conv_epilogue(conv: nn.Conv2d, act_code, x, out=None, res=None, stats=None, 
     ``tower``: the conv is one of the Detect head's 3x3 tower convs (the fp16-split conv kernel takes it).
     ``s2``: the conv is one of the neck's 3x3 / stride-2 convs (the stride-2 fp16-split kernel takes it).
     ``s1``: one of the neck's C2f Bottleneck 3x3 convs (the stride-1 fp16-split kernel, with out / res).
+    ``n1``: one of the neck's wide 1x1 convs (the fp16-split 1x1 kernel, with out / out2).
     Returns None when the fast path does not apply (CPU tensor, no bias, unsupported activation / shape)."""
     if x.device.type != "cuda" or conv.bias is None or act_code is None or x.dtype not in (torch.float32,
                                                                                            torch.bfloat16):
@@ -127,6 +131,10 @@ def conv_epilogue(conv: nn.Conv2d, act_code, x, out=None, res=None, stats=None, 
             and (CONV3X3 == "force" or x.shape[0] * -(-x.shape[2] // 8) * -(-x.shape[3] // 32) >= CONV3X3_MIN_TILES)):
         prep = lambda: _cached(conv, "c3prep", (conv.weight,), lambda: _hip.conv3x3_prepare(conv.weight))  # noqa: E731
         return _hip.conv3x3_silu(x, conv.bias, prep, conv.out_channels)
+    if (n1 and N1_NECK and act_code == 1 and res is None and stats is None and _hip.conv1x1x2_ok(x, conv)
+            and (out is None or _hip._imgs_contig(out)) and (out2 is None or _hip._imgs_contig(out2))):
+        prep = lambda: _cached(conv, "c1prep", (conv.weight,), lambda: _hip.conv1x1x2_prepare(conv.weight))  # noqa: E731
+        return _hip.conv1x1x2_silu(x, conv.bias, prep, conv.out_channels, out=out, out2=out2, c2lo=c2lo)
     if (s1 and S1_NECK and act_code == 1 and stats is None and out2 is None and _hip.conv3x3_ok(x, conv)
             and x.shape[3] % 4 == 0 and (res is None or res.is_contiguous())):
         prep = lambda: _cached(conv, "c3prep", (conv.weight,), lambda: _hip.conv3x3_prepare(conv.weight))  # noqa: E731
@@ -180,6 +188,8 @@ class Conv(nn.Module):
     s2 = False
     # set by DetectionModel on the neck's C2f Bottleneck 3x3 convs: the stride-1 fp16-split kernel runs them (S1_NECK)
     s1 = False
+    # set by DetectionModel on the neck's wide 1x1 convs: the fp16-split 1x1 kernel runs them (N1_NECK)
+    n1 = False
 
     def __init__(self, c1, c2, k=1, s=1, p=None, g=1, d=1, act=True):
         super().__init__()
@@ -204,7 +214,7 @@ class Conv(nn.Module):
 
     def forward_fuse(self, x, out=None, res=None, out2=None, c2lo=0):
         y = conv_epilogue(self.conv, _act_code(self.act), x, out, res, self.emit_stats, out2, c2lo, self.tower,
-                          self.s2, self.s1)
+                          self.s2, self.s1, self.n1)
         if y is not None:
             return y
         y = self.act(self.conv(x))

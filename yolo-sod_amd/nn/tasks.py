@@ -445,6 +445,12 @@ class DetectionModel(BaseModel):
                     for cv in (bt.cv1, bt.cv2):
                         if cv.conv.kernel_size == (3, 3) and cv.conv.stride == (1, 1) and cv.conv.groups == 1:
                             cv.s1 = True
+            # the neck's wide 1x1 convs (N1_NECK): lateral Convs and the C2fs' cv1 / cv2
+            if i >= n_backbone:
+                for cv in ([m] if isinstance(m, M.Conv) and not isinstance(m, M.DWConv) else
+                           [m.cv1, m.cv2] if isinstance(m, M.C2f) else []):
+                    if cv.conv.kernel_size == (1, 1) and cv.conv.groups == 1 and cv.conv.out_channels % 128 == 0:
+                        cv.n1 = True
 
         # lazy SE weights: the reference creates them during the stride probe, in forward (= layer) order,
         # after every eager module -> same RNG stream position here.
