@@ -19,14 +19,9 @@ namespace ys {
 namespace c1 {
 
 constexpr float WSC = 64.0f;
-constexpr int NP = 64;         // pixels per tile
 constexpr int KS = 128;        // input channels per stage
 constexpr int PS = KS + 8;     // plane row stride (halves): 272-byte pixel rows
-constexpr int PL = NP * PS;    // plane (halves)
 constexpr int NT = 256;
-constexpr int NITEM = (KS / 4) * NP;  // (channel quad, pixel) items per stage
-constexpr int NIT = NITEM / NT;       // 8
-static_assert(NITEM % NT == 0, "items");
 
 struct Args {
   const float* x;      // image b at x + b xbs: [Cin][HW]
@@ -42,8 +37,14 @@ struct Args {
   const unsigned* prep_flag;
 };
 
-template <bool DUAL>
+// NP pixels per tile (64 or 128: the weights are read from L2 once per tile, 128 halves that traffic)
+template <bool DUAL, int NP>
 __global__ __launch_bounds__(NT, 2) void conv1x1_x2_kernel(Args p) {
+  constexpr int PL = NP * PS;           // plane (halves)
+  constexpr int NITEM = (KS / 4) * NP;  // (channel quad, pixel) items per stage
+  constexpr int NIT = NITEM / NT;
+  constexpr int NPB = NP / 16;          // pixel blocks
+  static_assert(NITEM % NT == 0, "items");
   __shared__ __attribute__((aligned(16))) h16_t Pl[2 * PL];
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l15 = lane & 15, g = lane >> 4;
@@ -90,11 +91,11 @@ __global__ __launch_bounds__(NT, 2) void conv1x1_x2_kernel(Args p) {
     return __builtin_bit_cast(f16x8_t, __builtin_amdgcn_raw_buffer_load_b128(
                                            rw, (unsigned)((((cb0 + u) * 2 + pl) * 64 + lane) * 16), st, 0));
   };
-  f32x4 acc[2][4];
+  f32x4 acc[2][NPB];
 #pragma unroll
   for (int u = 0; u < 2; ++u)
 #pragma unroll
-    for (int k = 0; k < 4; ++k) acc[u][k] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < NPB; ++k) acc[u][k] = f32x4{0.f, 0.f, 0.f, 0.f};
   float bo[2];  // loaded before the loop: an epilogue load would wait behind every load in flight
 #pragma unroll
   for (int u = 0; u < 2; ++u) bo[u] = p.bias[16 * (cb0 + u) + l15];
@@ -130,10 +131,10 @@ __global__ __launch_bounds__(NT, 2) void conv1x1_x2_kernel(Args p) {
         wn[u][0] = wfrag(sn, u, 0);
         wn[u][1] = wfrag(sn, u, 1);
       }
-      load_part(stn, 8 * kk, 8 * kk + 8, nlive);
+      load_part(stn, NIT * kk, NIT * kk + NIT, nlive);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
+      for (int k = 0; k < NPB; ++k) {
         const h16_t* src = Pl + (16 * k + l15) * PS + 32 * kk + 8 * g;
         const f16x8_t xh = *reinterpret_cast<const f16x8_t*>(src);
         const f16x8_t xl = *reinterpret_cast<const f16x8_t*>(src + PL);
@@ -157,7 +158,7 @@ __global__ __launch_bounds__(NT, 2) void conv1x1_x2_kernel(Args p) {
   for (int u = 0; u < 2; ++u) {
     const int o = 16 * (cb0 + u) + l15;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < NPB; ++k) {
       const int px = p0 + 16 * k + 4 * g;
       f32x4 v;
 #pragma unroll
@@ -257,13 +258,20 @@ YS_EXPORT int yolosod_conv1x1x2_silu(const float* x, long x_bstride, float* y, l
   unsigned* flag;
   YS_CHECK_ARG(c1_carve(const_cast<void*>(prep), prep_bytes, cin, cout, &wp, &flag),
                "conv1x1x2: prepared block too small");
-  const int ntile = (HW + c1::NP - 1) / c1::NP;
+  static const int np = [] { const char* e = getenv("YOLOSOD_C1_NP"); return e ? atoi(e) : 64; }();
+  const int NPx = np == 64 ? 64 : 128;
+  const int ntile = (HW + NPx - 1) / NPx;
   c1::Args a{x, x_bstride, wp, bias, y, y_bstride, y2, y2_bstride, c2lo, cin, cout, HW, ntile, range_flag_dev(), flag};
   const long nwg = (long)B * ntile * (cout / 128);
   YS_CHECK_ARG(nwg < (1L << 31), "conv1x1x2: too many tiles");
   hipStream_t st = (hipStream_t)stream;
-  if (y2) hipLaunchKernelGGL(c1::conv1x1_x2_kernel<true>, dim3((unsigned)nwg), dim3(c1::NT), 0, st, a);
-  else hipLaunchKernelGGL(c1::conv1x1_x2_kernel<false>, dim3((unsigned)nwg), dim3(c1::NT), 0, st, a);
+  if (NPx == 64) {
+    if (y2) hipLaunchKernelGGL((c1::conv1x1_x2_kernel<true, 64>), dim3((unsigned)nwg), dim3(c1::NT), 0, st, a);
+    else hipLaunchKernelGGL((c1::conv1x1_x2_kernel<false, 64>), dim3((unsigned)nwg), dim3(c1::NT), 0, st, a);
+  } else {
+    if (y2) hipLaunchKernelGGL((c1::conv1x1_x2_kernel<true, 128>), dim3((unsigned)nwg), dim3(c1::NT), 0, st, a);
+    else hipLaunchKernelGGL((c1::conv1x1_x2_kernel<false, 128>), dim3((unsigned)nwg), dim3(c1::NT), 0, st, a);
+  }
   YS_CHECK_LAUNCH("conv1x1x2");
   return 0;
 }

@@ -27,7 +27,7 @@ constexpr float WSC = 64.0f;
 constexpr int TH = 8, TW = 32;              // output tile
 constexpr int HH = TH + 2, HW_ = TW + 2;    // halo tile
 constexpr int NPXH = HH * HW_;              // 340 halo pixels
-constexpr int PS = 32 + 8;                  // plane row stride (halves): 80-byte pixel rows
+constexpr int PS = 48;                       // plane row stride (halves): 96-byte pixel rows, conflict-free ds_read_b128
 constexpr int PL = NPXH * PS;               // plane (halves)
 constexpr int NQUAD = NPXH * 8;             // staged items per chunk: (4-channel quad, halo pixel)
 constexpr int NT = 256;
@@ -45,6 +45,7 @@ struct Args {
   int ncb_all;         // 16-channel blocks of the prepared weights (Cout / 16)
   unsigned* range_flag;
   const unsigned* prep_flag;
+  int ntiles;          // persistent kernel: B tiles_y tiles_x
 };
 
 // ABL (timing ablations, wrong results; yolosod_debug_set_conv3x3_abl): 1 no halo loads, 2 every weight fragment from
@@ -237,6 +238,209 @@ __global__ __launch_bounds__(256, 2) void conv3x3_x2_kernel(Args p) {
   if (p.prep_flag && p.range_flag && blockIdx.x == 0 && threadIdx.x == 0 && *p.prep_flag) *p.range_flag = 1u;
 }
 
+// Persistent form (W % 4 == 0): the same tile, MFMA and store scheme, but each workgroup walks a contiguous range of
+// work items (tile, output group) of its XCD (neighbouring tiles share halo rows in that XCD's L2), one iteration per
+// (item, input chunk), and the next iteration's halo loads (the next tile's first chunk included) are spread over the
+// current iteration's taps, so no tile starts with an exposed HBM wait. Per-image buffer resources with unclamped
+// offsets (rows above the image are negative offsets: out of range, 0); other out-of-image pixels masked by okb.
+template <int CBW, bool RES>
+__global__ __launch_bounds__(256, 2) void conv3x3_p_kernel(Args p) {
+  __shared__ __attribute__((aligned(16))) h16_t Pl[2 * PL];
+  __shared__ float bsh[512];  // every output channel's bias: an epilogue load would wait behind the prefetches
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l15 = lane & 15, g = lane >> 4;
+  const int H = p.H, W = p.W, HWi = H * W, nq = p.cin >> 5;
+  float rng = 0.f;
+  for (int o = tid; o < 16 * p.ncb_all; o += 256) bsh[o] = p.bias[o];  // ordered before use by the loop's barriers
+
+  const int ngrp = p.ncb_all / (2 * CBW);
+  const int nj = gridDim.x >> 3, j = blockIdx.x >> 3, xcd = blockIdx.x & 7;
+  const int nitems = p.ntiles * ngrp;
+  const int per = (nitems + 7) >> 3;
+  const int t_beg = xcd * per + j, t_end = min((xcd + 1) * per, nitems);
+  if (t_beg >= t_end) return;
+  const int n_it = ((t_end - t_beg + nj - 1) / nj) * nq;
+
+  auto rsrc = [&](const void* base, unsigned bytes) {
+    const unsigned long long a = (unsigned long long)base;
+    return __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(a >> 32)) << 32) |
+                (unsigned)__builtin_amdgcn_readfirstlane((unsigned)a)),
+        (short)0, __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+  };
+  const __amdgpu_buffer_rsrc_t rw = rsrc(p.wp, (unsigned)(9L * nq * p.ncb_all * 2 * 1024));
+  int pk[NIT], el0[NIT];
+#pragma unroll
+  for (int i = 0; i < NIT; ++i) {
+    const int e = min(tid + NT * i, NQUAD - 1);
+    const int quad = e / NPXH, px = e - quad * NPXH;
+    const int hy = px / HW_, hx = px - hy * HW_;
+    pk[i] = (quad << 16) | (hy << 8) | hx;
+    el0[i] = 4 * quad * HWi + hy * W + hx;
+  }
+  struct It {
+    int b, ty, tx, q, grp;
+  };
+  auto it_of = [&](int it) __attribute__((always_inline)) {
+    const int tg = t_beg + (it / nq) * nj;
+    const int t = tg / ngrp;
+    It r;
+    r.grp = tg - t * ngrp;
+    r.q = it - (it / nq) * nq;
+    r.tx = t % p.tiles_x;
+    r.ty = (t / p.tiles_x) % p.tiles_y;
+    r.b = t / (p.tiles_x * p.tiles_y);
+    return r;
+  };
+  f32x4 sv[NIT];
+  unsigned okb_ld = 0;
+  auto load_part = [&](const It& r, int k0, int k1) __attribute__((always_inline)) {
+    const int iy0 = TH * r.ty - 1, ix0 = TW * r.tx - 1;
+    const __amdgpu_buffer_rsrc_t ri =
+        rsrc(p.x + ((long)r.b * p.cin + 32 * r.q) * HWi, (unsigned)((p.cin - 32 * r.q) * HWi * 4));
+    const int toff = iy0 * W + ix0;
+    if (k0 == 0) {
+      const bool interior = iy0 >= 0 && ix0 >= 0 && iy0 + HH <= H && ix0 + HW_ <= W;
+      unsigned okb = 0xffffffffu;
+      if (!interior) {
+        okb = 0;
+#pragma unroll
+        for (int i = 0; i < NIT; ++i) {
+          const int hy = (pk[i] >> 8) & 255, hx = pk[i] & 255;
+          okb |= ((unsigned)(iy0 + hy) < (unsigned)H && (unsigned)(ix0 + hx) < (unsigned)W) ? (1u << i) : 0u;
+        }
+      }
+      okb_ld = okb;
+    }
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) {
+      if (4 * i + 3 < k0 || 4 * i >= k1) continue;
+      const unsigned vo = (unsigned)((el0[i] + toff) * 4);
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (4 * i + c >= k0 && 4 * i + c < k1)
+          sv[i][c] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ri, vo + c * HWi * 4, 0, 0));
+    }
+  };
+  const int rp = wid & 1, ph = wid >> 1;
+  int bpx[8];
+#pragma unroll
+  for (int cb = 0; cb < 8; ++cb) bpx[cb] = (4 * ph + (cb >> 1)) * HW_ + (cb & 1) * 16 + l15;
+  auto wfrag = [&](int t, int q, int cbw, int pl) __attribute__((always_inline)) {
+    const int st = __builtin_amdgcn_readfirstlane(((t * nq + q) * p.ncb_all * 2) * 1024);
+    return __builtin_bit_cast(f16x8_t, __builtin_amdgcn_raw_buffer_load_b128(
+                                           rw, (unsigned)(((cbw * 2 + pl) * 64 + lane) * 16), st, 0));
+  };
+  f32x4 acc[CBW][8];
+#pragma unroll
+  for (int r = 0; r < CBW; ++r)
+#pragma unroll
+    for (int cb = 0; cb < 8; ++cb) acc[r][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  constexpr int NLD = 4 * NIT;             // loads per (tile, chunk): 44
+  constexpr int PER_TAP = (NLD + 8) / 9;   // spread over the nine taps
+
+  It cur = it_of(0);
+  load_part(cur, 0, NLD);
+  for (int it = 0; it < n_it; ++it) {
+    const It r = cur;
+    const unsigned okb = okb_ld;
+    __syncthreads();  // every wave is done with the previous iteration's planes
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) {
+      const int e = tid + NT * i;
+      if (e < NQUAD) {
+        const int quad = pk[i] >> 16, px = e - quad * NPXH;
+        const f32x4 v = ((okb >> i) & 1u) ? sv[i] : f32x4{0.f, 0.f, 0.f, 0.f};
+        uint2 hh, ll;
+        split4x(v, hh, ll);
+        rng = range_acc(rng, v);
+        h16_t* d = Pl + px * PS + 4 * quad;
+        *reinterpret_cast<uint2*>(d) = hh;
+        *reinterpret_cast<uint2*>(d + PL) = ll;
+      }
+    }
+    __syncthreads();
+    // the last iteration reloads itself (unconditional loads; L2-hot)
+    if (it + 1 < n_it) cur = it_of(it + 1);
+    const int cbw0 = r.grp * 2 * CBW + CBW * rp;
+    f16x8_t wa[CBW][2], wn[CBW][2];
+#pragma unroll
+    for (int u = 0; u < CBW; ++u) {
+      wa[u][0] = wfrag(0, r.q, cbw0 + u, 0);
+      wa[u][1] = wfrag(0, r.q, cbw0 + u, 1);
+    }
+    // pixel fragments one (tap, pixel block) step ahead of their MFMAs (across taps too), and group barriers that
+    // keep each step's two LDS reads ahead of the previous step's MFMAs: without them the reads sit right before
+    // their use and every block waits an LDS round trip
+    auto rd = [&](int t, int cb, f16x8_t& h, f16x8_t& l) __attribute__((always_inline)) {
+      const h16_t* src = Pl + (bpx[cb] + (t / 3) * HW_ + (t % 3)) * PS + 8 * g;
+      h = *reinterpret_cast<const f16x8_t*>(src);
+      l = *reinterpret_cast<const f16x8_t*>(src + PL);
+    };
+    f16x8_t nh, nl;
+    rd(0, 0, nh, nl);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int tn = t + 1 < 9 ? t + 1 : t;
+#pragma unroll
+      for (int u = 0; u < CBW; ++u) {
+        wn[u][0] = wfrag(tn, r.q, cbw0 + u, 0);
+        wn[u][1] = wfrag(tn, r.q, cbw0 + u, 1);
+      }
+      load_part(cur, PER_TAP * t, min(PER_TAP * t + PER_TAP, NLD));
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int cb = 0; cb < 8; ++cb) {
+        const f16x8_t xh = nh, xlo = nl;
+        if (cb < 7) rd(t, cb + 1, nh, nl);
+        else if (t < 8) rd(t + 1, 0, nh, nl);
+#pragma unroll
+        for (int u = 0; u < CBW; ++u) {
+          f32x4 c = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, wa[u][1], acc[u][cb], 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(xlo, wa[u][0], c, 0, 0, 0);
+          acc[u][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, wa[u][0], c, 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int cb = 0; cb < 8; ++cb) {
+        if (cb < 7 || t < 8) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS read
+        __builtin_amdgcn_sched_group_barrier(0x008, 3 * CBW, 0);                 // MFMA
+      }
+#pragma unroll
+      for (int u = 0; u < CBW; ++u) {
+        wa[u][0] = wn[u][0];
+        wa[u][1] = wn[u][1];
+      }
+    }
+    if (r.q == nq - 1) {
+      float* yb = p.y + (long)r.b * p.ybs;
+      float bv[CBW];
+#pragma unroll
+      for (int u = 0; u < CBW; ++u) bv[u] = bsh[16 * (cbw0 + u) + l15];
+#pragma unroll
+      for (int cb = 0; cb < 8; ++cb) {
+        const int oy = r.ty * TH + 4 * ph + (cb >> 1), ox = r.tx * TW + (cb & 1) * 16 + 4 * g;
+#pragma unroll
+        for (int u = 0; u < CBW; ++u) {
+          const long po = (long)(16 * (cbw0 + u) + l15) * HWi + oy * W + ox;
+          f32x4 o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = silu_fast_(acc[u][cb][e] * (1.0f / WSC) + bv[u]);
+          if constexpr (RES) {
+#pragma clang fp contract(off)  // a separately rounded add, as x + cv2(...): no fma with SiLU's last multiply
+            if (oy < H && ox < W) o = o + *reinterpret_cast<const f32x4*>(p.res + (long)r.b * p.rbs + po);
+          }
+          if (oy < H && ox < W) __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(yb + po));
+          acc[u][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+    }
+  }
+  range_report(p.range_flag, rng);
+  if (p.prep_flag && p.range_flag && blockIdx.x == 0 && threadIdx.x == 0 && *p.prep_flag) *p.range_flag = 1u;
+}
+
 // W [64][Cin][3][3] -> fragment-major planes of 64 W (see the file comment); one thread per (output channel, input
 // channel, tap). The block's own range word records whether 64 W left fp16's range (re-reported by every launch).
 __global__ __launch_bounds__(256) void conv3x3_prep_kernel(const float* __restrict__ w, int cin, int cout,
@@ -269,6 +473,18 @@ YS_EXPORT int yolosod_debug_set_conv3x3_abl(int abl) {
   const int old = g_c3_abl;
   g_c3_abl = abl;
   return old;
+}
+
+static int c3_cu_count() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0, c = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0)
+      c = 256;
+    n = c;
+  }
+  return n;
 }
 
 static bool c3_cout_ok(int cout) { return cout == 32 || (cout % 64 == 0 && cout <= 512); }
@@ -341,6 +557,19 @@ YS_EXPORT int yolosod_conv3x3_silu_ex(const float* x, float* y, long y_bstride, 
   const long nwg = (long)B * a.tiles_x * a.tiles_y * ngrp;
   YS_CHECK_ARG(nwg < (1L << 31), "conv3x3: too many tiles");
   hipStream_t st = (hipStream_t)stream;
+  // YOLOSOD_C3_PERSIST (default 1): the persistent kernel for W % 4 == 0 (two workgroups per CU)
+  static const int persist = [] { const char* e = getenv("YOLOSOD_C3_PERSIST"); return e ? atoi(e) : 1; }();
+  if (persist && v4 && g_c3_abl == 0 && (long)B * cin * H * W * 4 < (1L << 32)) {
+    a.ntiles = (int)((long)B * a.tiles_x * a.tiles_y);
+    long grid = 2L * c3_cu_count();
+    grid = grid < ((nwg + 7) / 8) * 8 ? grid : ((nwg + 7) / 8) * 8;
+    grid = (grid + 7) / 8 * 8;
+    auto pk = cout == 32 ? (res ? c3::conv3x3_p_kernel<1, true> : c3::conv3x3_p_kernel<1, false>)
+                         : (res ? c3::conv3x3_p_kernel<2, true> : c3::conv3x3_p_kernel<2, false>);
+    hipLaunchKernelGGL(pk, dim3((unsigned)grid), dim3(256), 0, st, a);
+    YS_CHECK_LAUNCH("conv3x3");
+    return 0;
+  }
   auto kern = v4 ? c3::conv3x3_x2_kernel<0, true> : c3::conv3x3_x2_kernel<0, false>;
   if (cout == 32) {
     kern = res ? c3::conv3x3_x2_kernel<0, true, 1, true>
