@@ -122,6 +122,9 @@ def _free_port():
 
 
 class _Timer:
+    def __init__(self, select=None):
+        self.select = select
+
     def __enter__(self):
         return self
 

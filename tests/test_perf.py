@@ -83,3 +83,20 @@ def test_fused_gate_conv_bills_the_gate_and_the_producer():
     assert flops >= 2 * 32 * 160 * 160 * 64 * 32 * 9
     assert perf.method_peak_tflops(fused) == pytest.approx(perf.PEAK_BF16_MFMA_TFLOPS / 3)
     assert path["t_meas_ms"] == pytest.approx(f["avg_ms"], abs=1e-3)
+
+
+def test_path_select_times_the_path_its_producers_and_their_plain_variants_only():
+    """bench.py's timed region brackets only these launches with HIP events (perf.PathSelect)."""
+    sel = perf.PathSelect()
+    plain = ("bias_act", (32, 128, 80, 80), None)
+    assert not sel(plain)  # before its producer was seen: a plain backbone epilogue
+    assert sel(("swin", (32, 64, 160, 160), (2, 7, 128)))
+    assert sel(("se_gate", (32, 32, 320, 320), 4))
+    assert sel(("cbam_conv", (32, 64, 160, 160), (128, 4)))
+    assert sel(("bias_act", (32, 128, 80, 80), "sum"))  # producer of the SE L23 statistics
+    assert sel(plain)  # now the plain variant it is billed against
+    assert sel(("conv1x1_thin", (32, 96, 160, 160), (64, "summax")))
+    assert sel(("conv1x1_thin", (32, 96, 160, 160), (64, False, False)))
+    for key in (("conv3x3", (32, 64, 160, 160), 64), ("conv3x3s2", (32, 64, 160, 160), (128, False, False)),
+                ("conv1x1x2", (32, 192, 80, 80), (128, True)), ("bias_act", (32, 64, 80, 80), None)):
+        assert not sel(key), key

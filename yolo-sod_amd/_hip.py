@@ -173,10 +173,13 @@ def ops():
 
 
 class _OpTimer:
-    """Records HIP events around every C-ABI launch sequence (on the launch stream) while active."""
+    """Records HIP events around every C-ABI launch sequence (on the launch stream) while active; with ``select``,
+    only around the launches whose key it accepts (an event pair is a timestamped barrier on the stream: timing every
+    launch of a step costs the step a few per cent)."""
 
-    def __init__(self):
+    def __init__(self, select=None):
         self.records = []
+        self.select = select
 
     def durations_ms(self):
         torch.cuda.synchronize()
@@ -190,11 +193,15 @@ _TIMER: _OpTimer | None = None
 
 
 class op_timer:
-    """``with op_timer() as t: ...`` -> ``t.durations_ms()`` = [((op, shape, extra), ms), ...] per launch."""
+    """``with op_timer() as t: ...`` -> ``t.durations_ms()`` = [((op, shape, extra), ms), ...] per launch;
+    ``op_timer(select)``: only the launches whose key ``select(key)`` accepts are timed."""
+
+    def __init__(self, select=None):
+        self.select = select
 
     def __enter__(self):
         global _TIMER
-        self.t = _OpTimer()
+        self.t = _OpTimer(self.select)
         _TIMER = self.t
         return self.t
 
@@ -224,7 +231,7 @@ def _launch(key, dev, fn, *args):
     _init_device(dev)
     with torch.cuda.device(dev):
         t = _TIMER
-        if t is None:
+        if t is None or (t.select is not None and not t.select(key)):
             return fn(*args)
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)

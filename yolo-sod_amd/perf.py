@@ -177,6 +177,25 @@ def producer_of(key):
     return None
 
 
+class PathSelect:
+    """``op_timer`` filter for bench.py's timed region: the hot-path operators, their gate-only launches, the producing
+    epilogues that emit a gate's statistics and the plain variants those are billed against (collected while the
+    filter sees the producers: run one untimed-region step through it first); everything else - the backbone's,
+    the neck's and the Detect towers' convolutions and epilogues - runs without HIP events."""
+
+    def __init__(self):
+        self.plain = set()
+
+    def __call__(self, key):
+        if key[0] in PATH_OPS or key[0] in GATE_ONLY:
+            return True
+        p = producer_of(key)
+        if p is not None:
+            self.plain.add(p[2])
+            return True
+        return key in self.plain
+
+
 def aggregate(calls):
     """[(key, ms), ...] per launch -> {key: [total ms, launches]} in first-seen order."""
     agg = {}
