@@ -212,6 +212,12 @@ int yolosod_conv1x1_thin(const float* x, long x_bs, const float* w, const float*
                          const float* res, long res_bs, float* out2, long out2_bs, int c2lo, int B, int Cin, int Cout,
                          long HW, void* stream);
 
+/* yolosod_conv1x1_thin (no res) over a virtual concat [x; x2]: channels [0, k1) from x, [k1, Cin) from x2 (any split);
+ * bit-identical to the materialised concat. */
+int yolosod_conv1x1_thin_cat(const float* x, long x_bs, const float* x2, long x2_bs, int k1, const float* w,
+                             const float* bias, float* out, long out_bs, float* out2, long out2_bs, int c2lo, int B,
+                             int Cin, int Cout, long HW, void* stream);
+
 /* yolosod_conv1x1_thin (no res / out2) that also emits the output's per-plane statistics for a following SE / CBAM
  * gate in the psum / pmax[B*Cout*parts] layout of yolosod_se_forward_pre / yolosod_cbam_forward_pre (parts =
  * yolosod_plane_parts(HW); plane total in k = 0, 0 / -inf in k > 0); pmax may be NULL; tile_ws = 2*B*Cout*(HW/64)
@@ -310,6 +316,12 @@ int yolosod_conv1x1x2_prepare(const float* w, int cin, int cout, void* prep, siz
 int yolosod_conv1x1x2_silu(const float* x, long x_bstride, float* y, long y_bstride, float* y2, long y2_bstride,
                            int c2lo, int B, int cin, int cout, int HW, const float* bias, const void* prep,
                            size_t prep_bytes, void* stream);
+/* The same over a virtual concat [x; x2] (block.py:249-253: the C2f cv1 after a neck Concat): channels [0, k1) from x
+ * (image b at x + b*x_bstride), [k1, cin) from x2 (image b at x2 + b*x2_bstride), k1 a multiple of 128; x2 NULL:
+ * yolosod_conv1x1x2_silu. Bit-identical to the materialised concat. */
+int yolosod_conv1x1x2_silu_cat(const float* x, long x_bstride, const float* x2, long x2_bstride, int k1, float* y,
+                               long y_bstride, float* y2, long y2_bstride, int c2lo, int B, int cin, int cout, int HW,
+                               const float* bias, const void* prep, size_t prep_bytes, void* stream);
 /* Timing hook: ablation variants of the stride-2 conv kernel at Cout 64 with a channel gate (csrc/conv3x3s2.hip; WRONG
  * results for abl != 0 - scripts/bench_conv3x3s2.py only). Returns the previous value. */
 int yolosod_debug_set_conv3x3s2_abl(int abl);

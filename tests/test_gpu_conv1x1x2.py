@@ -63,3 +63,63 @@ def test_neck_wide_1x1_convs_take_the_kernel(cuda, monkeypatch):
     assert n >= 8, n
     ok, e, _ = tol_close(y.cpu().double(), y0.cpu().double(), 1e-3, 1e-4)
     assert ok, e
+
+
+@pytest.mark.parametrize("shape,k1,cout", [((2, 256, 16, 20), 128, 128), ((1, 512, 20, 20), 256, 256),
+                                           ((2, 384, 8, 8), 128, 256), ((1, 1024, 10, 10), 512, 512)])
+def test_conv1x1x2_virtual_concat_bit_identical(shape, k1, cout, cuda):
+    """A CatView (two parts read in place, the second from a channel slice) gives the materialised concat's output
+    bit for bit, dual store included."""
+    g = torch.Generator().manual_seed(k1 + cout)
+    B, cin, H, W = shape
+    a = torch.randn(B, k1, H, W, generator=g).to(cuda)
+    bb = torch.randn(B, cin - k1 + 64, H, W, generator=g).to(cuda)[:, 32:32 + cin - k1]  # a slice: batch stride
+    w = (torch.randn(cout, cin, generator=g) * (1.0 / cin ** 0.5)).to(cuda)
+    b = (torch.randn(cout, generator=g) * 0.1).to(cuda)
+    prep = _hip.conv1x1x2_prepare(w)
+    y0 = _hip.conv1x1x2_silu(torch.cat([a, bb], 1), b, lambda: prep, cout)
+    cv = _hip.CatView([a, bb])
+    assert _hip.conv1x1x2_ok(cv, torch.nn.Conv2d(cin, cout, 1))
+    y = _hip.conv1x1x2_silu(cv, b, lambda: prep, cout)
+    assert torch.equal(y, y0)
+    t = torch.empty((B, cout // 2, H, W), device=cuda)
+    _hip.conv1x1x2_silu(cv, b, lambda: prep, cout, out2=t, c2lo=cout // 2)
+    assert torch.equal(t, y0[:, cout // 2:])
+
+
+@pytest.mark.parametrize("k1,cin", [(64, 128), (32, 96), (128, 256)])
+def test_conv1x1_thin_virtual_concat_bit_identical(k1, cin, cuda):
+    """The thin 1x1 kernel over a CatView (any split) = over the materialised concat, bit for bit."""
+    g = torch.Generator().manual_seed(cin + k1)
+    a = torch.randn(2, k1, 32, 32, generator=g).to(cuda)
+    bb = torch.randn(2, cin - k1, 32, 32, generator=g).to(cuda)
+    w = (torch.randn(64, cin, generator=g) * (1.0 / cin ** 0.5)).to(cuda)
+    b = (torch.randn(64, generator=g) * 0.1).to(cuda)
+    y0 = _hip.conv1x1_thin(torch.cat([a, bb], 1), w, b)
+    cv = _hip.CatView([a, bb])
+    assert _hip.conv1x1_thin_ok(cv, 64)
+    assert torch.equal(_hip.conv1x1_thin(cv, w, b), y0)
+    t = torch.empty((2, 32, 32, 32), device=cuda)
+    _hip.conv1x1_thin(cv, w, b, out2=t, c2lo=32)
+    assert torch.equal(t, y0[:, 32:])
+
+
+def test_model_neck_concats_as_virtual_concats_bit_identical(cuda, monkeypatch):
+    """The executor hands the neck Concats to their C2f as CatViews (tasks.CATVIEW): every neck Concat does (the skip
+    inputs are never copied) and the model output is bit-identical to the concat-buffer form."""
+    from yolosod_amd.nn import tasks as T
+    m = T.build_model("yolov12-sod-fusion-v5-simple.yaml", seed=0, device=cuda)
+    x = torch.rand(2, 3, 640, 640, generator=torch.Generator().manual_seed(8)).to(cuda)
+    torch.backends.cudnn.deterministic = True
+    try:
+        with torch.inference_mode():
+            monkeypatch.setattr(T, "CATVIEW", True)
+            with _hip.op_timer() as t:
+                y = m(x)[0]
+            cats = sum(1 for k, _ in t.durations_ms() if k[0] in ("conv1x1x2", "conv1x1_thin") and "cat" in k[2])
+            monkeypatch.setattr(T, "CATVIEW", False)
+            y0 = m(x)[0]
+    finally:
+        torch.backends.cudnn.deterministic = False
+    assert cats == 6, cats
+    assert torch.equal(y, y0), float((y - y0).abs().max())

@@ -69,6 +69,9 @@ SIGNATURES = {
     "yolosod_conv1x1x2_prep_bytes": (_sz, [_i, _i]),
     "yolosod_conv1x1x2_prepare": (_i, [_vp, _i, _i, _vp, _sz, _vp]),
     "yolosod_conv1x1x2_silu": (_i, [_vp, _l, _vp, _l, _vp, _l, _i, _i, _i, _i, _i, _vp, _vp, _sz, _vp]),
+    "yolosod_conv1x1x2_silu_cat": (_i, [_vp, _l, _vp, _l, _i, _vp, _l, _vp, _l, _i, _i, _i, _i, _i, _vp, _vp, _sz,
+                                        _vp]),
+    "yolosod_conv1x1_thin_cat": (_i, [_vp, _l, _vp, _l, _i, _vp, _vp, _vp, _l, _vp, _l, _i, _i, _i, _i, _l, _vp]),
     "yolosod_conv3x3_prep_bytes_ex": (_sz, [_i, _i]),
     "yolosod_conv3x3_prepare_ex": (_i, [_vp, _i, _i, _vp, _sz, _vp]),
     "yolosod_conv3x3_silu_ex": (_i, [_vp, _vp, _l, _vp, _l, _i, _i, _i, _i, _i, _vp, _vp, _sz, _vp]),
@@ -685,7 +688,11 @@ THIN1X1_CIN = (64, 96, 128, 192, 256)
 
 
 def conv1x1_thin_ok(x, cout) -> bool:
-    """Shapes the thin fused 1x1 conv kernel takes (yolosod_conv1x1_thin)."""
+    """Shapes the thin fused 1x1 conv kernel takes (yolosod_conv1x1_thin; a CatView: yolosod_conv1x1_thin_cat)."""
+    if isinstance(x, CatView):  # any split; both parts fp32 on the GPU with contiguous images
+        B, Cin, H, W = x.shape
+        return (x.device.type == "cuda" and x.dtype == torch.float32 and cout in THIN1X1_COUT and Cin in THIN1X1_CIN
+                and (H * W) % 64 == 0 and all(_imgs_contig(t) for t in x.parts))
     B, Cin, H, W = x.shape
     return (x.device.type == "cuda" and x.dtype == torch.float32 and cout in THIN1X1_COUT and Cin in THIN1X1_CIN
             and (H * W) % 64 == 0 and x.stride(3) == 1 and x.stride(2) == W and x.stride(1) == H * W
@@ -710,6 +717,19 @@ def conv1x1_thin(x, w, bias, out=None, res=None, out2=None, c2lo=0, stats=None):
             raise RuntimeError(f"conv1x1_thin: {name} must be [B,{C},H,W] with contiguous channels")
         return t.stride(0)
 
+    if isinstance(x, CatView):  # a virtual concat: both parts read in place (no residual / statistics)
+        if res is not None or stats is not None:
+            raise RuntimeError("conv1x1_thin: a CatView input takes no res / stats")
+        x0, x1 = x.parts
+        k1 = int(x0.shape[1])
+        ob = bstride(out, "out", Cout)
+        o2 = bstride(out2, "out2", Cout - c2lo) if out2 is not None else 0
+        _check(_launch(("conv1x1_thin", tuple(x.shape), (Cout, False, out2 is not None, "cat")), x.device,
+                       lib.yolosod_conv1x1_thin_cat, x0.data_ptr(), bstride(x0, "x", k1), x1.data_ptr(),
+                       bstride(x1, "x2", Cin - k1), k1, _dev(w.contiguous(), "weight"), _dev(bias, "bias"),
+                       out.data_ptr(), ob, None if out2 is None else out2.data_ptr(), o2, int(c2lo), B, Cin, Cout, HW,
+                       _stream(x.device)), "conv1x1_thin_cat")
+        return out
     xb = bstride(x, "x", Cin)
     ob = bstride(out, "out", Cout)
     rb = bstride(res, "res", Cout) if res is not None else 0
@@ -819,6 +839,27 @@ def conv3x3_silu(x, bias, prep, cout=64, out=None, res=None):
     return y
 
 
+class CatView:
+    """A two-part channel concat left unmaterialised: [B, C0 + C1, H, W] as its parts. A neck Concat whose only reader
+    is the next C2f's cv1 (a 1x1 conv) hands this over, and the 1x1 kernels read both parts in place
+    (yolosod_conv1x1x2_silu_cat / yolosod_conv1x1_thin_cat) instead of a materialised concat (block.py:249-253,
+    conv.py:336-340: the conv of a concat = the sum of the convs of its parts over their channel ranges)."""
+
+    def __init__(self, parts):
+        a, b = parts
+        if a.shape[0] != b.shape[0] or a.shape[2:] != b.shape[2:] or a.dtype != b.dtype or a.device != b.device:
+            raise ValueError("CatView: parts must agree in batch, spatial size, dtype and device")
+        self.parts = (a, b)
+        self.shape = torch.Size((a.shape[0], a.shape[1] + b.shape[1], a.shape[2], a.shape[3]))
+        self.device, self.dtype = a.device, a.dtype
+
+    def dim(self):
+        return 4
+
+    def materialize(self):
+        return torch.cat(self.parts, 1)
+
+
 def _imgs_contig(t) -> bool:
     """[B, C, H, W] whose images are contiguous (any batch stride, e.g. a channel slice of a concat buffer)."""
     B, C, H, W = t.shape
@@ -828,7 +869,12 @@ def _imgs_contig(t) -> bool:
 def conv1x1x2_ok(x, conv) -> bool:
     """Shapes the fp16-split 1x1 conv kernel takes (yolosod_conv1x1x2_silu): fp32 on a GPU with contiguous images,
     1x1 / stride 1 / groups 1, Cout a multiple of 128 (<= 1024), Cin a multiple of 32, H*W a multiple of 4."""
-    return (x.device.type == "cuda" and x.dtype == torch.float32 and x.dim() == 4 and _imgs_contig(x)
+    if isinstance(x, CatView):  # both parts in place: the split on a 128-channel stage boundary
+        if not (all(_imgs_contig(t) for t in x.parts) and x.parts[0].shape[1] % 128 == 0):
+            return False
+    elif not (x.dim() == 4 and _imgs_contig(x)):
+        return False
+    return (x.device.type == "cuda" and x.dtype == torch.float32
             and conv.kernel_size == (1, 1) and conv.stride == (1, 1) and conv.padding == (0, 0) and conv.groups == 1
             and x.shape[1] == conv.in_channels and (x.shape[2] * x.shape[3]) % 4 == 0
             and int(load_library().yolosod_conv1x1x2_prep_bytes(int(conv.in_channels), int(conv.out_channels))) > 0)
@@ -862,14 +908,18 @@ def conv1x1x2_silu(x, bias, prep, cout, out=None, out2=None, c2lo=0):
         _img_view(out2, (B, cout - c2lo, H, W), "conv1x1x2: out2")
     b = bias.detach().float().contiguous()
 
+    x0, x1 = x.parts if isinstance(x, CatView) else (x, None)
+
     def run():
         blk = prep()
-        return lib.yolosod_conv1x1x2_silu(x.data_ptr(), x.stride(0), y.data_ptr(), y.stride(0),
-                                          None if out2 is None else out2.data_ptr(),
-                                          0 if out2 is None else out2.stride(0), int(c2lo), B, Cin, cout, H * W,
-                                          _dev(b, "bias"), blk.data_ptr(), blk.numel(), _stream(x.device))
+        return lib.yolosod_conv1x1x2_silu_cat(x0.data_ptr(), x0.stride(0), None if x1 is None else x1.data_ptr(),
+                                              0 if x1 is None else x1.stride(0), int(x0.shape[1]), y.data_ptr(),
+                                              y.stride(0), None if out2 is None else out2.data_ptr(),
+                                              0 if out2 is None else out2.stride(0), int(c2lo), B, Cin, cout, H * W,
+                                              _dev(b, "bias"), blk.data_ptr(), blk.numel(), _stream(x.device))
 
-    _check(_launch(("conv1x1x2", tuple(x.shape), (cout, out2 is not None)), x.device, run), "conv1x1x2")
+    extra = (cout, out2 is not None) + (("cat",) if x1 is not None else ())
+    _check(_launch(("conv1x1x2", tuple(x.shape), extra), x.device, run), "conv1x1x2")
     return y
 
 

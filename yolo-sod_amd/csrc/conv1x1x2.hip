@@ -35,6 +35,9 @@ struct Args {
   int c2lo, cin, cout, HW, ntile;
   unsigned* range_flag;
   const unsigned* prep_flag;
+  const float* x2;     // optional second input (a virtual concat): channels [k1, Cin) at x2 + b x2bs ([Cin - k1][HW])
+  long x2bs;
+  int k1;              // channels taken from x (Cin when x2 is NULL; else a multiple of KS)
 };
 
 // NP pixels per tile (64 or 128: the weights are read from L2 once per tile, 128 halves that traffic)
@@ -60,7 +63,10 @@ __global__ __launch_bounds__(NT, 2) void conv1x1_x2_kernel(Args p) {
                 (unsigned)__builtin_amdgcn_readfirstlane((unsigned)a)),
         (short)0, __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
   };
-  const __amdgpu_buffer_rsrc_t rx = rsrc(p.x + (long)b * p.xbs, (unsigned)((long)p.cin * HW * 4));
+  const __amdgpu_buffer_rsrc_t rx = rsrc(p.x + (long)b * p.xbs, (unsigned)((long)p.k1 * HW * 4));
+  // the second part of a virtual concat (stages from k1 / KS on); without one, an alias of rx that no stage selects
+  const __amdgpu_buffer_rsrc_t rx2 =
+      p.x2 ? rsrc(p.x2 + (long)b * p.x2bs, (unsigned)((long)(p.cin - p.k1) * HW * 4)) : rx;
   const __amdgpu_buffer_rsrc_t rx0 = rsrc(p.x, 0u);  // empty: the last stage's "next stage" loads return 0 at once
   const __amdgpu_buffer_rsrc_t rw = rsrc(p.wp, (unsigned)((long)nks * (p.cout >> 4) * 2 * 1024));
 
@@ -76,8 +82,9 @@ __global__ __launch_bounds__(NT, 2) void conv1x1_x2_kernel(Args p) {
   // the stage / channel offset is in the per-lane offset, so the buffer range check covers it: channels past Cin
   // (the last stage of a Cin that is not a multiple of KS) read 0, as do the padded weights they meet
   auto load_part = [&](int st, int k0, int k1, bool live) __attribute__((always_inline)) {
-    const unsigned sx = (unsigned)(KS * st * HW * 4);
-    const __amdgpu_buffer_rsrc_t r = live ? rx : rx0;
+    const bool second = KS * st >= p.k1;  // stage-uniform
+    const unsigned sx = (unsigned)((second ? KS * st - p.k1 : KS * st) * HW * 4);
+    const __amdgpu_buffer_rsrc_t r = live ? (second ? rx2 : rx) : rx0;
 #pragma unroll
     for (int k = 0; k < 4 * NIT; ++k)
       if (k >= k0 && k < k1)
@@ -240,14 +247,20 @@ YS_EXPORT int yolosod_conv1x1x2_prepare(const float* w, int cin, int cout, void*
   return 0;
 }
 
-// y = SiLU(W x + bias): x image b at x + b x_bstride ([cin][HW]), y image b at y + b y_bstride ([cout][HW]); y2 (or
-// NULL): channels [c2lo, cout) stored again at y2 + b y2_bstride. HW % 4 == 0; 16-byte aligned images.
-YS_EXPORT int yolosod_conv1x1x2_silu(const float* x, long x_bstride, float* y, long y_bstride, float* y2,
-                                     long y2_bstride, int c2lo, int B, int cin, int cout, int HW, const float* bias,
-                                     const void* prep, size_t prep_bytes, void* stream) {
+// y = SiLU(W [x; x2] + bias): x image b at x + b x_bstride ([k1][HW]), x2 (or NULL) image b at x2 + b x2_bstride
+// ([cin - k1][HW]: the second part of a virtual concat, k1 a multiple of 128), y image b at y + b y_bstride
+// ([cout][HW]); y2 (or NULL): channels [c2lo, cout) stored again at y2 + b y2_bstride. HW % 4 == 0; 16-byte aligned
+// images.
+YS_EXPORT int yolosod_conv1x1x2_silu_cat(const float* x, long x_bstride, const float* x2, long x2_bstride, int k1,
+                                         float* y, long y_bstride, float* y2, long y2_bstride, int c2lo, int B, int cin,
+                                         int cout, int HW, const float* bias, const void* prep, size_t prep_bytes,
+                                         void* stream) {
   YS_CHECK_ARG(x && y && bias && prep, "conv1x1x2: null pointer");
+  if (!x2) k1 = cin;
+  YS_CHECK_ARG(k1 > 0 && k1 <= cin && (!x2 || (k1 % c1::KS == 0 && k1 < cin && x2_bstride >= (long)(cin - k1) * HW)),
+               "conv1x1x2: concat split k1=%d (Cin %d) must be a multiple of %d", k1, cin, c1::KS);
   YS_CHECK_ARG(B >= 0 && HW > 0 && HW % 4 == 0 && yolosod_conv1x1x2_prep_bytes(cin, cout) > 0, "conv1x1x2: bad shape");
-  YS_CHECK_ARG(x_bstride >= (long)cin * HW && y_bstride >= (long)cout * HW, "conv1x1x2: batch strides too small");
+  YS_CHECK_ARG(x_bstride >= (long)k1 * HW && y_bstride >= (long)cout * HW, "conv1x1x2: batch strides too small");
   YS_CHECK_ARG((long)c1_pad(cin) * HW * 4 < (1L << 32), "conv1x1x2: image too large for 32-bit buffer offsets");
   YS_CHECK_ARG((((uintptr_t)y | (uintptr_t)(y2 ? y2 : y)) & 15) == 0 && y_bstride % 4 == 0 && y2_bstride % 4 == 0,
                "conv1x1x2: outputs must be 16-byte aligned");
@@ -261,7 +274,8 @@ YS_EXPORT int yolosod_conv1x1x2_silu(const float* x, long x_bstride, float* y, l
   static const int np = [] { const char* e = getenv("YOLOSOD_C1_NP"); return e ? atoi(e) : 64; }();
   const int NPx = np == 64 ? 64 : 128;
   const int ntile = (HW + NPx - 1) / NPx;
-  c1::Args a{x, x_bstride, wp, bias, y, y_bstride, y2, y2_bstride, c2lo, cin, cout, HW, ntile, range_flag_dev(), flag};
+  c1::Args a{x, x_bstride, wp, bias, y, y_bstride, y2, y2_bstride, c2lo, cin, cout, HW, ntile, range_flag_dev(), flag,
+             x2, x2_bstride, k1};
   const long nwg = (long)B * ntile * (cout / 128);
   YS_CHECK_ARG(nwg < (1L << 31), "conv1x1x2: too many tiles");
   hipStream_t st = (hipStream_t)stream;
@@ -274,4 +288,12 @@ YS_EXPORT int yolosod_conv1x1x2_silu(const float* x, long x_bstride, float* y, l
   }
   YS_CHECK_LAUNCH("conv1x1x2");
   return 0;
+}
+
+// y = SiLU(W x + bias) for one input tensor (yolosod_conv1x1x2_silu_cat without a second part)
+YS_EXPORT int yolosod_conv1x1x2_silu(const float* x, long x_bstride, float* y, long y_bstride, float* y2,
+                                     long y2_bstride, int c2lo, int B, int cin, int cout, int HW, const float* bias,
+                                     const void* prep, size_t prep_bytes, void* stream) {
+  return yolosod_conv1x1x2_silu_cat(x, x_bstride, nullptr, 0, cin, y, y_bstride, y2, y2_bstride, c2lo, B, cin, cout, HW,
+                                    bias, prep, prep_bytes, stream);
 }

@@ -283,7 +283,9 @@ __global__ __launch_bounds__(256, 2) void conv1x1_thin_kernel(const float* __res
                                                               long o_bs, const float* __restrict__ res, long r_bs,
                                                               float* __restrict__ out2, long o2_bs, int c2lo, int HW,
                                                               int ntile, int rev, float* __restrict__ tsum = nullptr,
-                                                              float* __restrict__ tmax = nullptr) {
+                                                              float* __restrict__ tmax = nullptr,
+                                                              const float* __restrict__ x2 = nullptr, long x2_bs = 0,
+                                                              int k1 = K) {
   constexpr int RB = M / 64;   // 16-row blocks per wave
   constexpr int KQ = K / 4;    // k quarter per lane group
   constexpr int XS = 68;       // LDS row stride (floats)
@@ -292,6 +294,8 @@ __global__ __launch_bounds__(256, 2) void conv1x1_thin_kernel(const float* __res
   const int l15 = lane & 15, g = lane >> 4;
   const int b = rev ? gridDim.y - 1 - blockIdx.y : blockIdx.y;  // last images first: see mall_reverse()
   const float* xb = x + (long)b * x_bs;
+  // a virtual concat: channels [k1, K) come from x2 (image b at x2 + b x2_bs)
+  const float* xb2 = x2 ? x2 + (long)b * x2_bs - (long)k1 * HW : xb;
   float4 a[RB][KQ / 4];
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb) {
@@ -311,7 +315,7 @@ __global__ __launch_bounds__(256, 2) void conv1x1_thin_kernel(const float* __res
     for (int e = tid; e < K * 16; e += 256) {
       const int row = e >> 4, c4 = e & 15;
       *reinterpret_cast<float4*>(xs + row * XS + 4 * c4) =
-          *reinterpret_cast<const float4*>(xb + (long)row * HW + p0 + 4 * c4);
+          *reinterpret_cast<const float4*>((row < k1 ? xb : xb2) + (long)row * HW + p0 + 4 * c4);
     }
     __syncthreads();
     f32x4 acc[RB][4];
@@ -673,6 +677,44 @@ YS_EXPORT int yolosod_conv1x1_thin(const float* x, long x_bs, const float* w, co
 #undef YS_THIN
   YS_CHECK_ARG(ok, "conv1x1_thin: Cin=%d unsupported", Cin);
   YS_CHECK_LAUNCH("conv1x1_thin");
+  return 0;
+}
+
+// yolosod_conv1x1_thin over a virtual concat [x; x2] (channels [0, k1) from x, [k1, Cin) from x2), no residual /
+// statistics: the C2f cv1 after a neck Concat reads both parts in place instead of a materialised concat.
+YS_EXPORT int yolosod_conv1x1_thin_cat(const float* x, long x_bs, const float* x2, long x2_bs, int k1, const float* w,
+                                       const float* bias, float* out, long out_bs, float* out2, long out2_bs, int c2lo,
+                                       int B, int Cin, int Cout, long HW, void* stream) {
+  YS_CHECK_ARG(x && x2 && w && bias && out, "conv1x1_thin_cat: null pointer");
+  YS_CHECK_ARG(k1 > 0 && k1 < Cin, "conv1x1_thin_cat: k1=%d (Cin %d)", k1, Cin);
+  YS_CHECK_ARG(HW % 64 == 0 && HW < (1L << 30), "conv1x1_thin_cat: HW=%ld must be a multiple of 64", HW);
+  YS_CHECK_ARG(Cout == 64 || Cout == 128, "conv1x1_thin_cat: Cout=%d unsupported", Cout);
+  YS_CHECK_ARG(x_bs % 4 == 0 && x2_bs % 4 == 0 && out_bs % 4 == 0 && (!out2 || out2_bs % 4 == 0),
+               "conv1x1_thin_cat: batch strides must be multiples of 4");
+  YS_CHECK_ARG((((uintptr_t)x | (uintptr_t)x2 | (uintptr_t)w | (uintptr_t)out) & 15) == 0,
+               "conv1x1_thin_cat: pointers must be 16-byte aligned");
+  YS_CHECK_ARG(!out2 || (c2lo >= 0 && c2lo < Cout), "conv1x1_thin_cat: c2lo=%d", c2lo);
+  if (B == 0) return 0;
+  const int ntile = (int)(HW / 64);
+  const int gx = ntile < 4 ? ntile : (ntile + 3) / 4;
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 grid((unsigned)gx, (unsigned)B);
+  bool ok = false;
+#define YS_THINC(M_, K_)                                                                                          \
+  if (Cout == M_ && Cin == K_) {                                                                                  \
+    ok = true;                                                                                                    \
+    if (out2) hipLaunchKernelGGL((conv1x1_thin_kernel<M_, K_, false, true>), grid, dim3(256), 0, st, x, x_bs, w,    \
+                                 bias, out, out_bs, nullptr, 0L, out2, out2_bs, c2lo, (int)HW, ntile, mall_reverse(), \
+                                 nullptr, nullptr, x2, x2_bs, k1);                                                 \
+    else hipLaunchKernelGGL((conv1x1_thin_kernel<M_, K_, false, false>), grid, dim3(256), 0, st, x, x_bs, w, bias,  \
+                            out, out_bs, nullptr, 0L, nullptr, 0L, 0, (int)HW, ntile, mall_reverse(), nullptr, nullptr, \
+                            x2, x2_bs, k1);                                                                        \
+  }
+  YS_THINC(64, 64) YS_THINC(64, 96) YS_THINC(64, 128) YS_THINC(64, 192) YS_THINC(64, 256)
+  YS_THINC(128, 64) YS_THINC(128, 96) YS_THINC(128, 128) YS_THINC(128, 192) YS_THINC(128, 256)
+#undef YS_THINC
+  YS_CHECK_ARG(ok, "conv1x1_thin_cat: Cin=%d unsupported", Cin);
+  YS_CHECK_LAUNCH("conv1x1_thin_cat");
   return 0;
 }
 

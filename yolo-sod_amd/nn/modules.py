@@ -126,6 +126,18 @@ def conv_epilogue(conv: nn.Conv2d, act_code, x, out=None, res=None, stats=None, 
     if x.device.type != "cuda" or conv.bias is None or act_code is None or x.dtype not in (torch.float32,
                                                                                            torch.bfloat16):
         return None
+    if isinstance(x, _hip.CatView):  # a virtual concat: a 1x1 kernel reads both parts in place, else materialise
+        if act_code == 1 and res is None and stats is None and conv.kernel_size == (1, 1):
+            if n1 and N1_NECK and _hip.conv1x1x2_ok(x, conv) and (out is None or _hip._imgs_contig(out)) and (
+                    out2 is None or _hip._imgs_contig(out2)):
+                prep = lambda: _cached(conv, "c1prep", (conv.weight,), lambda: _hip.conv1x1x2_prepare(conv.weight))  # noqa: E731
+                return _hip.conv1x1x2_silu(x, conv.bias, prep, conv.out_channels, out=out, out2=out2, c2lo=c2lo)
+            if (THIN1X1 and conv.out_channels == 64 and conv.stride == (1, 1) and conv.groups == 1
+                    and conv.padding == (0, 0) and _hip.conv1x1_thin_ok(x, conv.out_channels)
+                    and (out is None or out.data_ptr() % 16 == 0)):
+                return _hip.conv1x1_thin(x, conv.weight.detach().reshape(conv.out_channels, -1), conv.bias.detach(),
+                                         out=out, out2=out2, c2lo=c2lo)
+        x = x.materialize()
     if (act_code == 1 and out is None and res is None and stats is None and out2 is None and CONV3X3 != "0"
             and (CONV3X3 == "all" or tower) and _hip.conv3x3_ok(x, conv)
             and (CONV3X3 == "force" or x.shape[0] * -(-x.shape[2] // 8) * -(-x.shape[3] // 32) >= CONV3X3_MIN_TILES)):
@@ -174,6 +186,22 @@ def conv_epilogue(conv: nn.Conv2d, act_code, x, out=None, res=None, stats=None, 
     return _hip.bias_act(y, bias, act_code, out=out, res=res, stats=stats, out2=out2, c2lo=c2lo)
 
 
+def catview_route(cv, c0, c1, H, W, dtype) -> bool:
+    """Whether the fused Conv ``cv`` (a C2f cv1 after a two-input Concat of c0 + c1 channels) reads the concat as a
+    ``_hip.CatView`` in place: the wide 1x1 kernel (n1 convs, the split on a 128-channel stage) or the thin 1x1 kernel
+    (64 outputs). The executor decides with this before the Concat's producers run (YOLOSOD_CATVIEW)."""
+    conv = cv.conv
+    if (dtype != torch.float32 or not cv.is_fused() or conv.bias is None or _act_code(cv.act) != 1
+            or cv.emit_stats is not None or conv.kernel_size != (1, 1) or conv.stride != (1, 1) or conv.groups != 1
+            or conv.padding != (0, 0) or conv.in_channels != c0 + c1):
+        return False
+    if cv.n1 and N1_NECK and c0 % 128 == 0 and c1 % 32 == 0 and (H * W) % 4 == 0 and int(
+            _hip.load_library().yolosod_conv1x1x2_prep_bytes(c0 + c1, conv.out_channels)) > 0:
+        return True
+    return (THIN1X1 and conv.out_channels == 64 and c0 + c1 in _hip.THIN1X1_CIN and (H * W) % 64 == 0
+            and c0 % 4 == 0 and c1 % 4 == 0)
+
+
 class Conv(nn.Module):
     """Conv2d(no bias) + BatchNorm2d + SiLU; after ``fuse()`` the BN is folded into the conv (conv.py:37-55).
 
@@ -217,6 +245,8 @@ class Conv(nn.Module):
                           self.s2, self.s1, self.n1)
         if y is not None:
             return y
+        if isinstance(x, _hip.CatView):
+            x = x.materialize()
         y = self.act(self.conv(x))
         if res is not None:
             y = y + res
@@ -276,6 +306,8 @@ class C2f(nn.Module):
         self.m = nn.ModuleList(Bottleneck(self.c, self.c, shortcut, g, k=((3, 3), (3, 3)), e=1.0) for _ in range(n))
 
     def forward(self, x):
+        if isinstance(x, _hip.CatView) and not (x.device.type == "cuda" and self.cv1.is_fused()):
+            x = x.materialize()
         if x.device.type == "cuda" and self.cv1.is_fused():
             # every branch writes its channel slice of one buffer: no torch.cat copy (block.py:249-253 semantics)
             B, _, H, W = x.shape

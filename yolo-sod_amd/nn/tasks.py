@@ -59,6 +59,10 @@ GATE_FUSE = os.environ.get("YOLOSOD_GATE_FUSE", "1") != "0"
 # the neck's nearest 2x upsample into its Concat slice as one HIP pass (YOLOSOD_UPSAMPLE_HIP=0: PyTorch's strided
 # copy, for A/B)
 UPSAMPLE_HIP = os.environ.get("YOLOSOD_UPSAMPLE_HIP", "1") != "0"
+# a neck Concat read only by the next C2f's cv1 (a 1x1 conv whose kernel reads both parts in place) is handed over as
+# a _hip.CatView instead of a buffer: the skip input (an earlier layer's saved output) is not copied at all, the -1
+# producer writes its own tensor (YOLOSOD_CATVIEW=0: the concat buffer with the producer's slice written in place)
+CATVIEW = os.environ.get("YOLOSOD_CATVIEW", "1") != "0"
 
 # name -> class; the YAML resolves module strings through this (tasks.py:995-1002)
 DEFAULT_REGISTRY = {
@@ -273,6 +277,7 @@ class BaseModel(nn.Module):
             rr = 0  # next side stream (round robin over towers)
         y = []
         pend = {}  # concat index -> (buffer, channel offset of each input)
+        cvpend = {}  # concat index -> True: handed to the next C2f as a CatView
         elided = 0
         gplan = self._gate_consumers() if GATE_FUSE else {}
         gated = None  # (gate input, channel gate, spatial gate, fused-op key) for the next layer
@@ -313,6 +318,20 @@ class BaseModel(nn.Module):
                             zip((H, W), cv.padding, cv.dilation, cv.kernel_size, cv.stride))
                 srcs = [None if j == -1 else y[j] for j in cat.f]
                 chans = [cp if s is None else s.shape[1] for s in srcs]
+                nxt = self.model[c + 1] if c + 1 < len(self.model) else None
+                if (CATVIEW and len(srcs) == 2 and c not in self.save and isinstance(nxt, M.C2f) and nxt.f == -1
+                        and all(s is None or (s.shape[0], s.shape[2], s.shape[3]) == (B, H, W) for s in srcs)
+                        and M.catview_route(nxt.cv1, chans[0], chans[1], H, W, inp.dtype)):
+                    # the Concat becomes a CatView of its inputs: the producer writes its own tensor
+                    if isinstance(m, nn.Upsample):
+                        x = torch.empty((B, cp, H, W), dtype=inp.dtype, device=inp.device)
+                        if not (UPSAMPLE_HIP and _hip.upsample2x_into(inp, x)):
+                            x = m(inp)
+                    else:
+                        x = m(inp)
+                    cvpend[c] = True
+                    y.append(None)
+                    continue
                 if all(s is None or (s.shape[0], s.shape[2], s.shape[3]) == (B, H, W) for s in srcs):
                     buf = torch.empty((B, sum(chans), H, W), dtype=inp.dtype, device=inp.device)
                     offs = [sum(chans[:i]) for i in range(len(chans))]
@@ -328,7 +347,10 @@ class BaseModel(nn.Module):
                     x = out
                     y.append(None)
                     continue
-            if m.i in pend:
+            if cvpend.pop(m.i, False):
+                x = _hip.CatView([x if j == -1 else y[j] for j in m.f])
+                elided += 1
+            elif m.i in pend:
                 buf, offs, chans = pend.pop(m.i)
                 elided += 1
                 for j, o, n in zip(m.f, offs, chans):
