@@ -204,6 +204,17 @@ size_t yolosod_conv3x3_prep_bytes(int cin);
 int yolosod_conv3x3_prepare(const float* w, int cin, void* prep, size_t prep_bytes, void* stream);
 int yolosod_conv3x3_silu(const float* x, float* y, int B, int cin, int H, int W, const float* bias, const void* prep,
                          size_t prep_bytes, void* stream);
+/* General form (the neck's C2f Bottleneck convs too): Cout 32 or a multiple of 64 (<= 512); the output image b at
+ * y + b*y_bstride (a concat slice), res (or NULL) added after the activation (Bottleneck shortcut); _xs: the input image
+ * b at x + b*x_bstride (a channel slice, e.g. of the C2f's own buffer); _ex: contiguous x. */
+size_t yolosod_conv3x3_prep_bytes_ex(int cin, int cout);
+int yolosod_conv3x3_prepare_ex(const float* w, int cin, int cout, void* prep, size_t prep_bytes, void* stream);
+int yolosod_conv3x3_silu_ex(const float* x, float* y, long y_bstride, const float* res, long res_bstride, int B,
+                            int cin, int cout, int H, int W, const float* bias, const void* prep, size_t prep_bytes,
+                            void* stream);
+int yolosod_conv3x3_silu_xs(const float* x, long x_bstride, float* y, long y_bstride, const float* res, long res_bstride,
+                            int B, int cin, int cout, int H, int W, const float* bias, const void* prep,
+                            size_t prep_bytes, void* stream);
 
 /* Thin fused 1x1 convolution of the backbone (conv.py:37-55 after fuse(), 1x1 case): out = SiLU(W x + bias) (+ res)
  * for Cout in {64, 128}, Cin in {64, 96, 128, 192, 256}, HW % 64 == 0; x / out / res may be channel slices (batch
@@ -211,6 +222,11 @@ int yolosod_conv3x3_silu(const float* x, float* y, int B, int cin, int H, int W,
 int yolosod_conv1x1_thin(const float* x, long x_bs, const float* w, const float* bias, float* out, long out_bs,
                          const float* res, long res_bs, float* out2, long out2_bs, int c2lo, int B, int Cin, int Cout,
                          long HW, void* stream);
+
+/* SPPF's pooling pyramid (block.py SPPF: three chained MaxPool2d(5, 1, 2) + torch.cat) in one pass over the concat
+ * buffer z [B][4C][H][W] (image b at z + b*z_bstride, images contiguous): channels [C, 4C) <- the 5 / 9 / 13-window max
+ * pools (clipped to the image; = the chained pools) of channels [0, C), which cv1 wrote. H*W <= 4096. */
+int yolosod_sppf_pool(float* z, long z_bstride, int B, int C, int H, int W, void* stream);
 
 /* yolosod_conv1x1_thin (no res) over a virtual concat [x; x2]: channels [0, k1) from x, [k1, Cin) from x2 (any split);
  * bit-identical to the materialised concat. */

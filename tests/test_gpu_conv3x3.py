@@ -120,3 +120,39 @@ def test_neck_c2f_convs_take_the_kernel(cuda, monkeypatch):
     assert n1 - n0 == 12, (n1, n0)
     ok, e, _ = tol_close(y.cpu().double(), y0.cpu().double(), 1e-3, 1e-4)
     assert ok, e
+
+
+@pytest.mark.parametrize("cout,res", [(64, False), (32, True), (128, True)])
+def test_conv3x3_slice_input_bit_identical(cout, res, cuda):
+    """The input as a channel slice of a wider buffer (yolosod_conv3x3_silu_xs: the neck C2f's Bottleneck reading its
+    input inside the C2f buffer), residual a slice too: bit-identical to the packed input."""
+    g = torch.Generator().manual_seed(cout + res)
+    cin = cout if res else 64
+    buf = torch.randn(2, cin + 96, 24, 40, generator=g).to(cuda)
+    x = buf[:, 32:32 + cin]
+    w = (torch.randn(cout, cin, 3, 3, generator=g) * 0.05).to(cuda)
+    b = (torch.randn(cout, generator=g) * 0.1).to(cuda)
+    prep = _hip.conv3x3_prepare(w)
+    r = x if res else None
+    y0 = _hip.conv3x3_silu(x.contiguous(), b, lambda: prep, cout, res=None if r is None else r.contiguous())
+    y = _hip.conv3x3_silu(x, b, lambda: prep, cout, res=r)
+    assert torch.equal(y, y0)
+
+
+def test_model_neck_c2f_slices_bit_identical(cuda, monkeypatch):
+    """The neck C2fs' Bottlenecks reading their inputs as slices of the C2f buffer (modules.C2F_SLICES) give the
+    dual-store form's output bit for bit."""
+    from yolosod_amd.nn import modules as M
+    from yolosod_amd.nn.tasks import build_model
+    m = build_model("yolov12-sod-fusion-v5-simple.yaml", seed=0, device=cuda)
+    x = torch.rand(2, 3, 640, 640, generator=torch.Generator().manual_seed(12)).to(cuda)
+    torch.backends.cudnn.deterministic = True
+    try:
+        with torch.inference_mode():
+            monkeypatch.setattr(M, "C2F_SLICES", True)
+            y = m(x)[0]
+            monkeypatch.setattr(M, "C2F_SLICES", False)
+            y0 = m(x)[0]
+    finally:
+        torch.backends.cudnn.deterministic = False
+    assert torch.equal(y, y0), float((y - y0).abs().max())

@@ -619,3 +619,21 @@ def test_swin_prepared_parameters_cached_and_refreshed(name, cuda, monkeypatch):
             wa.norm2.weight, wa.norm2.bias, wa.norm2.eps, wa.mlp[0].weight, wa.mlp[0].bias, wa.mlp[2].weight,
             wa.mlp[2].bias, m.pw.weight, m.bn.weight, m.bn.bias, m.bn.running_mean, m.bn.running_var, m.bn.eps)
     assert torch.equal(y3, ref3) and not torch.equal(y3, y1)
+
+
+@pytest.mark.parametrize("shape", [(2, 16, 20, 20), (1, 8, 7, 13), (3, 4, 40, 40), (1, 2, 1, 5), (2, 3, 64, 64)])
+def test_sppf_pool_matches_chained_max_pools(shape, cuda):
+    """yolosod_sppf_pool = three chained F.max_pool2d(5, 1, 2) (block.py SPPF) bit for bit, into a batch-strided
+    concat buffer; channels [0, C) untouched."""
+    import torch.nn.functional as F
+    B, C, H, W = shape
+    g = torch.Generator().manual_seed(B * 1000 + C * 10 + H)
+    big = torch.randn(B, 4 * C + 3, H, W, generator=g).to(cuda)
+    z = big[:, 3:]
+    y0 = z[:, :C].clone()
+    _hip.sppf_pool(z, C)
+    p1 = F.max_pool2d(y0, 5, 1, 2)
+    p2 = F.max_pool2d(p1, 5, 1, 2)
+    p3 = F.max_pool2d(p2, 5, 1, 2)
+    assert torch.equal(z[:, :C], y0)
+    assert torch.equal(z[:, C:2 * C], p1) and torch.equal(z[:, 2 * C:3 * C], p2) and torch.equal(z[:, 3 * C:], p3)

@@ -71,10 +71,12 @@ SIGNATURES = {
     "yolosod_conv1x1x2_silu": (_i, [_vp, _l, _vp, _l, _vp, _l, _i, _i, _i, _i, _i, _vp, _vp, _sz, _vp]),
     "yolosod_conv1x1x2_silu_cat": (_i, [_vp, _l, _vp, _l, _i, _vp, _l, _vp, _l, _i, _i, _i, _i, _i, _vp, _vp, _sz,
                                         _vp]),
+    "yolosod_sppf_pool": (_i, [_vp, _l, _i, _i, _i, _i, _vp]),
     "yolosod_conv1x1_thin_cat": (_i, [_vp, _l, _vp, _l, _i, _vp, _vp, _vp, _l, _vp, _l, _i, _i, _i, _i, _l, _vp]),
     "yolosod_conv3x3_prep_bytes_ex": (_sz, [_i, _i]),
     "yolosod_conv3x3_prepare_ex": (_i, [_vp, _i, _i, _vp, _sz, _vp]),
     "yolosod_conv3x3_silu_ex": (_i, [_vp, _vp, _l, _vp, _l, _i, _i, _i, _i, _i, _vp, _vp, _sz, _vp]),
+    "yolosod_conv3x3_silu_xs": (_i, [_vp, _l, _vp, _l, _vp, _l, _i, _i, _i, _i, _i, _vp, _vp, _sz, _vp]),
     "yolosod_debug_set_swin_fused": (None, [_i]),
     "yolosod_debug_set_swin_x3": (_i, [_i]),
     "yolosod_debug_set_head_x2": (_i, [_i]),
@@ -782,9 +784,10 @@ def conv1x1(x, w, bias, act, out=None, res=None):
 
 
 def conv3x3_ok(x, conv) -> bool:
-    """Shapes the fp16-split 3x3 conv kernel takes (yolosod_conv3x3_silu_ex): fp32 contiguous NCHW on a GPU,
-    3x3 / stride 1 / pad 1 / dilation 1 / groups 1, 32 or a multiple of 64 (<= 512) outputs, Cin a multiple of 32."""
-    return (x.device.type == "cuda" and x.dtype == torch.float32 and x.is_contiguous() and x.dim() == 4
+    """Shapes the fp16-split 3x3 conv kernel takes (yolosod_conv3x3_silu_xs): fp32 NCHW on a GPU with contiguous
+    images (any batch stride: a channel slice), 3x3 / stride 1 / pad 1 / dilation 1 / groups 1, 32 or a multiple of
+    64 (<= 512) outputs, Cin a multiple of 32."""
+    return (x.device.type == "cuda" and x.dtype == torch.float32 and x.dim() == 4 and _imgs_contig(x)
             and conv.kernel_size == (3, 3) and conv.stride == (1, 1) and conv.padding == (1, 1)
             and conv.dilation == (1, 1) and conv.groups == 1 and x.shape[1] == conv.in_channels
             and int(load_library().yolosod_conv3x3_prep_bytes_ex(int(conv.in_channels), int(conv.out_channels))) > 0)
@@ -830,7 +833,8 @@ def conv3x3_silu(x, bias, prep, cout=64, out=None, res=None):
 
     def run():
         blk = prep()
-        return lib.yolosod_conv3x3_silu_ex(_dev(x, "x"), y.data_ptr(), y.stride(0),
+        _img_view(x, (B, Cin, H, W), "conv3x3: x")
+        return lib.yolosod_conv3x3_silu_xs(x.data_ptr(), x.stride(0), y.data_ptr(), y.stride(0),
                                            None if res is None else res.data_ptr(),
                                            0 if res is None else res.stride(0), B, Cin, cout, H, W, _dev(b, "bias"),
                                            blk.data_ptr(), blk.numel(), _stream(x.device))
@@ -858,6 +862,19 @@ class CatView:
 
     def materialize(self):
         return torch.cat(self.parts, 1)
+
+
+def sppf_pool(z, c):
+    """SPPF's pooling pyramid in place (yolosod_sppf_pool): z [B, 4c, H, W] fp32 with contiguous images (any batch
+    stride); channels [c, 4c) <- the one-, two- and three-fold 5x5 / stride-1 / pad-2 max pools of channels [0, c)."""
+    B, C4, H, W = z.shape
+    if (C4 != 4 * c or z.dtype != torch.float32 or z.device.type != "cuda"
+            or z.stride()[1:] != (H * W, W, 1)):  # scalar accesses: no alignment needed
+        raise RuntimeError("sppf_pool: z must be a [B, 4c, H, W] fp32 GPU tensor with contiguous images")
+    lib = load_library()
+    _check(_launch(("sppf_pool", (B, c, H, W), None), z.device, lib.yolosod_sppf_pool, z.data_ptr(), z.stride(0), B,
+                   int(c), H, W, _stream(z.device)), "sppf_pool")
+    return z
 
 
 def _imgs_contig(t) -> bool:

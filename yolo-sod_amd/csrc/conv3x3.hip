@@ -46,6 +46,7 @@ struct Args {
   unsigned* range_flag;
   const unsigned* prep_flag;
   int ntiles;          // persistent kernel: B tiles_y tiles_x
+  long xbs;            // image b of x at x + b xbs (>= cin H W: x may be a channel slice of a concat buffer)
 };
 
 // ABL (timing ablations, wrong results; yolosod_debug_set_conv3x3_abl): 1 no halo loads, 2 every weight fragment from
@@ -64,7 +65,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_x2_kernel(Args p) {
   const int H = p.H, W = p.W, HWi = H * W;
   const int x0 = tx * TW - 1, y0 = ty * TH - 1;  // halo origin
   const int nq = p.cin >> 5;
-  const float* xb = p.x + (long)b * p.cin * HWi;
+  const float* xb = p.x + (long)b * p.xbs;
   float rng = 0.f;
 
   // staging item e: quad = e / NPXH (channels 4 quad .. + 3 of the chunk), halo pixel e % NPXH; consecutive threads
@@ -297,7 +298,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_p_kernel(Args p) {
   auto load_part = [&](const It& r, int k0, int k1) __attribute__((always_inline)) {
     const int iy0 = TH * r.ty - 1, ix0 = TW * r.tx - 1;
     const __amdgpu_buffer_rsrc_t ri =
-        rsrc(p.x + ((long)r.b * p.cin + 32 * r.q) * HWi, (unsigned)((p.cin - 32 * r.q) * HWi * 4));
+        rsrc(p.x + (long)r.b * p.xbs + (long)32 * r.q * HWi, (unsigned)((p.cin - 32 * r.q) * HWi * 4));
     const int toff = iy0 * W + ix0;
     if (k0 == 0) {
       const bool interior = iy0 >= 0 && ix0 >= 0 && iy0 + HH <= H && ix0 + HW_ <= W;
@@ -531,13 +532,14 @@ YS_EXPORT int yolosod_conv3x3_prepare(const float* w, int cin, void* prep, size_
   return yolosod_conv3x3_prepare_ex(w, cin, 64, prep, prep_bytes, stream);
 }
 
-// y = SiLU(conv3x3(x, W) + bias) (+ res): x [B][cin][H][W] -> image b's output [cout][H][W] at y + b y_bstride
+// y = SiLU(conv3x3(x, W) + bias) (+ res): x image b at x + b x_bstride ([cin][H][W]) -> image b's output [cout][H][W] at y + b y_bstride
 // (y_bstride >= cout H W: a channel slice of a concat buffer); res (or NULL): image b at res + b res_bstride, added
 // after the activation (Bottleneck shortcut). y must not alias x.
-YS_EXPORT int yolosod_conv3x3_silu_ex(const float* x, float* y, long y_bstride, const float* res, long res_bstride,
-                                      int B, int cin, int cout, int H, int W, const float* bias, const void* prep,
-                                      size_t prep_bytes, void* stream) {
+YS_EXPORT int yolosod_conv3x3_silu_xs(const float* x, long x_bstride, float* y, long y_bstride, const float* res,
+                                      long res_bstride, int B, int cin, int cout, int H, int W, const float* bias,
+                                      const void* prep, size_t prep_bytes, void* stream) {
   YS_CHECK_ARG(x && y && bias && prep, "conv3x3: null pointer");
+  YS_CHECK_ARG(x_bstride >= (long)cin * H * W, "conv3x3: input batch stride %ld < %ld", x_bstride, (long)cin * H * W);
   YS_CHECK_ARG(B >= 0 && H > 0 && W > 0 && yolosod_conv3x3_prep_bytes_ex(cin, cout) > 0, "conv3x3: bad shape");
   YS_CHECK_ARG((long)cin * H * W < (1L << 31) && (long)cout * H * W < (1L << 31), "conv3x3: plane too large");
   YS_CHECK_ARG(y_bstride >= (long)cout * H * W, "conv3x3: output batch stride %ld < %ld", y_bstride,
@@ -552,14 +554,14 @@ YS_EXPORT int yolosod_conv3x3_silu_ex(const float* x, float* y, long y_bstride, 
   YS_CHECK_ARG(conv3x3_carve(const_cast<void*>(prep), prep_bytes, cin, cout, &wp, &flag),
                "conv3x3: prepared block too small");
   c3::Args a{x, wp, bias, y, y_bstride, res, res_bstride, cin, H, W, (W + c3::TW - 1) / c3::TW,
-             (H + c3::TH - 1) / c3::TH, cout / 16, range_flag_dev(), flag};
+             (H + c3::TH - 1) / c3::TH, cout / 16, range_flag_dev(), flag, 0, x_bstride};
   const int ngrp = cout == 32 ? 1 : cout / 64;
   const long nwg = (long)B * a.tiles_x * a.tiles_y * ngrp;
   YS_CHECK_ARG(nwg < (1L << 31), "conv3x3: too many tiles");
   hipStream_t st = (hipStream_t)stream;
   // YOLOSOD_C3_PERSIST (default 1): the persistent kernel for W % 4 == 0 (two workgroups per CU)
   static const int persist = [] { const char* e = getenv("YOLOSOD_C3_PERSIST"); return e ? atoi(e) : 1; }();
-  if (persist && v4 && g_c3_abl == 0 && (long)B * cin * H * W * 4 < (1L << 32)) {
+  if (persist && v4 && g_c3_abl == 0) {
     a.ntiles = (int)((long)B * a.tiles_x * a.tiles_y);
     long grid = 2L * c3_cu_count();
     grid = grid < ((nwg + 7) / 8) * 8 ? grid : ((nwg + 7) / 8) * 8;
@@ -590,6 +592,14 @@ YS_EXPORT int yolosod_conv3x3_silu_ex(const float* x, float* y, long y_bstride, 
   hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(256), 0, st, a);
   YS_CHECK_LAUNCH("conv3x3");
   return 0;
+}
+
+// As yolosod_conv3x3_silu_xs with a contiguous x [B][cin][H][W].
+YS_EXPORT int yolosod_conv3x3_silu_ex(const float* x, float* y, long y_bstride, const float* res, long res_bstride,
+                                      int B, int cin, int cout, int H, int W, const float* bias, const void* prep,
+                                      size_t prep_bytes, void* stream) {
+  return yolosod_conv3x3_silu_xs(x, (long)cin * H * W, y, y_bstride, res, res_bstride, B, cin, cout, H, W, bias, prep,
+                                 prep_bytes, stream);
 }
 
 // 3x3 / stride 1 / pad 1 conv with 64 outputs, contiguous y [B][64][H][W].

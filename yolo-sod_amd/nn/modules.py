@@ -109,6 +109,11 @@ S1_NECK = os.environ.get("YOLOSOD_S1_NECK", "1") != "0"
 # (csrc/conv1x1x2.hip) with bias / SiLU / concat slice / C2f's dual store in its epilogue; YOLOSOD_N1_NECK=0: MIOpen
 N1_NECK = os.environ.get("YOLOSOD_N1_NECK", "1") != "0"
 CONV3X3_MIN_TILES = int(os.environ.get("YOLOSOD_CONV3X3_MIN_TILES", "0"))
+# the neck C2fs' Bottlenecks (stride-1 fp16-split kernel) read their inputs as slices of the C2f buffer instead of
+# packed copies written by a second store (YOLOSOD_C2F_SLICES=0: the dual-store form)
+C2F_SLICES = os.environ.get("YOLOSOD_C2F_SLICES", "1") != "0"
+# SPPF's three chained max pools + concat as one HIP pass into the buffer cv1 writes (csrc/sppf.hip); 0: PyTorch
+SPPF_HIP = os.environ.get("YOLOSOD_SPPF_HIP", "1") != "0"
 
 
 def conv_epilogue(conv: nn.Conv2d, act_code, x, out=None, res=None, stats=None, out2=None, c2lo=0, tower=False,
@@ -148,7 +153,7 @@ def conv_epilogue(conv: nn.Conv2d, act_code, x, out=None, res=None, stats=None, 
         prep = lambda: _cached(conv, "c1prep", (conv.weight,), lambda: _hip.conv1x1x2_prepare(conv.weight))  # noqa: E731
         return _hip.conv1x1x2_silu(x, conv.bias, prep, conv.out_channels, out=out, out2=out2, c2lo=c2lo)
     if (s1 and S1_NECK and act_code == 1 and stats is None and out2 is None and _hip.conv3x3_ok(x, conv)
-            and x.shape[3] % 4 == 0 and (res is None or res.is_contiguous())):
+            and x.shape[3] % 4 == 0 and (res is None or _hip._imgs_contig(res))):
         prep = lambda: _cached(conv, "c3prep", (conv.weight,), lambda: _hip.conv3x3_prepare(conv.weight))  # noqa: E731
         return _hip.conv3x3_silu(x, conv.bias, prep, conv.out_channels, out=out, res=res)
     if (s2 and S2_NECK and act_code == 1 and res is None and stats is None and out2 is None
@@ -315,6 +320,14 @@ class C2f(nn.Module):
             # each Bottleneck's input also lands packed in `t` (dual-store epilogue): MIOpen reads packed tensors,
             # so a channel slice of z would cost a copy pass per Bottleneck
             z = torch.empty((B, (2 + n) * c, H, W), dtype=x.dtype, device=x.device)
+            if (n and S1_NECK and C2F_SLICES and x.dtype == torch.float32 and W % 4 == 0
+                    and all(m.cv1.s1 and m.cv2.s1 and m.cv1.conv.kernel_size == (3, 3) for m in self.m)):
+                # the Bottlenecks run on the stride-1 fp16-split kernel, which reads channel slices: each one reads
+                # its input in place from z (no packed second store)
+                self.cv1.forward_fuse(x, out=z[:, : 2 * c])
+                for i, m in enumerate(self.m):
+                    m(z[:, (1 + i) * c:(2 + i) * c], out=z[:, (2 + i) * c:(3 + i) * c])
+                return self.cv2(z)
             t = torch.empty((B, c, H, W), dtype=x.dtype, device=x.device) if n else None
             self.cv1.forward_fuse(x, out=z[:, : 2 * c], out2=t, c2lo=c)
             for i, m in enumerate(self.m):
@@ -336,6 +349,17 @@ class SPPF(nn.Module):
         self.m = nn.MaxPool2d(kernel_size=k, stride=1, padding=k // 2)
 
     def forward(self, x):
+        mp = self.m
+        if (SPPF_HIP and x.device.type == "cuda" and x.dtype == torch.float32 and self.cv1.is_fused()
+                and mp.kernel_size == 5 and mp.stride in (1, (1, 1)) and mp.padding == 2 and mp.dilation == 1
+                and not mp.ceil_mode and x.shape[2] * x.shape[3] <= 4096):
+            # cv1 writes channels [0, c) of the concat buffer, one HIP pass writes the three pools (csrc/sppf.hip)
+            B, _, H, W = x.shape
+            c = self.cv1.conv.out_channels
+            z = torch.empty((B, 4 * c, H, W), dtype=x.dtype, device=x.device)
+            self.cv1.forward_fuse(x, out=z[:, :c])
+            _hip.sppf_pool(z, c)
+            return self.cv2(z)
         y = [self.cv1(x)]
         y.extend(self.m(y[-1]) for _ in range(3))
         return self.cv2(torch.cat(y, 1))
