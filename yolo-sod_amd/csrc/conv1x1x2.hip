@@ -63,11 +63,11 @@ __global__ __launch_bounds__(NT, 2) void conv1x1_x2_kernel(Args p) {
                 (unsigned)__builtin_amdgcn_readfirstlane((unsigned)a)),
         (short)0, __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
   };
-  const __amdgpu_buffer_rsrc_t rx = rsrc(p.x + (long)b * p.xbs, (unsigned)((long)p.k1 * HW * 4));
-  // the second part of a virtual concat (stages from k1 / KS on); without one, an alias of rx that no stage selects
-  const __amdgpu_buffer_rsrc_t rx2 =
-      p.x2 ? rsrc(p.x2 + (long)b * p.x2bs, (unsigned)((long)(p.cin - p.k1) * HW * 4)) : rx;
-  const __amdgpu_buffer_rsrc_t rx0 = rsrc(p.x, 0u);  // empty: the last stage's "next stage" loads return 0 at once
+  // the part of a virtual concat a stage reads (stages from k1 / KS on: x2) as a buffer resource built from scalars
+  // per stage (a select between two resource values is lowered to VGPRs, and every load then runs a waterfall loop)
+  const float* xb1 = p.x + (long)b * p.xbs;
+  const float* xb2 = p.x2 ? p.x2 + (long)b * p.x2bs : xb1;
+  const unsigned nb1 = (unsigned)((long)p.k1 * HW * 4), nb2 = (unsigned)((long)(p.cin - p.k1) * HW * 4);
   const __amdgpu_buffer_rsrc_t rw = rsrc(p.wp, (unsigned)((long)nks * (p.cout >> 4) * 2 * 1024));
 
   // staging item e = tid + NT i: channel quad e / NP (channels 4 quad .. + 3 of the stage), pixel e % NP (clamped
@@ -84,7 +84,8 @@ __global__ __launch_bounds__(NT, 2) void conv1x1_x2_kernel(Args p) {
   auto load_part = [&](int st, int k0, int k1, bool live) __attribute__((always_inline)) {
     const bool second = KS * st >= p.k1;  // stage-uniform
     const unsigned sx = (unsigned)((second ? KS * st - p.k1 : KS * st) * HW * 4);
-    const __amdgpu_buffer_rsrc_t r = live ? (second ? rx2 : rx) : rx0;
+    // !live: an empty range (the last stage's "next stage" loads return 0 at once)
+    const __amdgpu_buffer_rsrc_t r = rsrc(second ? xb2 : xb1, live ? (second ? nb2 : nb1) : 0u);
 #pragma unroll
     for (int k = 0; k < 4 * NIT; ++k)
       if (k >= k0 && k < k1)
