@@ -123,3 +123,23 @@ def test_model_neck_concats_as_virtual_concats_bit_identical(cuda, monkeypatch):
         torch.backends.cudnn.deterministic = False
     assert cats == 6, cats
     assert torch.equal(y, y0), float((y - y0).abs().max())
+
+
+@pytest.mark.parametrize("shape", [(2, 128, 40, 40), (2, 96, 20, 24), (1, 256, 16, 16)])
+def test_conv1x1x2_cout64_matches_fp64(shape, cuda):
+    """The 64-channel-group form (the neck's Cout-64 1x1 convs) against fp64, and its dual store bit-identical."""
+    g = torch.Generator().manual_seed(sum(shape))
+    B, cin, H, W = shape
+    x = torch.randn(shape, generator=g)
+    w = torch.randn(64, cin, 1, 1, generator=g) * (1.0 / cin ** 0.5)
+    b = torch.randn(64, generator=g) * 0.1
+    ref = F.silu(F.conv2d(x.double(), w.double(), b.double()))
+    wd = w.to(cuda)
+    prep = _hip.conv1x1x2_prepare(wd)
+    y = _hip.conv1x1x2_silu(x.to(cuda), b.to(cuda), lambda: prep, 64)
+    miopen = F.silu(F.conv2d(x.to(cuda), wd, b.to(cuda))).cpu().double()
+    err, err_m = float((y.cpu().double() - ref).abs().max()), float((miopen - ref).abs().max())
+    assert err <= 8 * err_m + 1e-5, (err, err_m)
+    t = torch.empty((B, 32, H, W), device=cuda)
+    _hip.conv1x1x2_silu(x.to(cuda), b.to(cuda), lambda: prep, 64, out2=t, c2lo=32)
+    assert torch.equal(t, y[:, 32:])

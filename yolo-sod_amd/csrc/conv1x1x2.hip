@@ -41,7 +41,8 @@ struct Args {
 };
 
 // NP pixels per tile (64 or 128: the weights are read from L2 once per tile, 128 halves that traffic)
-template <bool DUAL, int NP>
+// CPW: 16-channel output blocks per wave (2: workgroups of 128 output channels; 1: of 64, for Cout 64)
+template <bool DUAL, int NP, int CPW = 2>
 __global__ __launch_bounds__(NT, 2) void conv1x1_x2_kernel(Args p) {
   constexpr int PL = NP * PS;           // plane (halves)
   constexpr int NITEM = (KS / 4) * NP;  // (channel quad, pixel) items per stage
@@ -51,7 +52,7 @@ __global__ __launch_bounds__(NT, 2) void conv1x1_x2_kernel(Args p) {
   __shared__ __attribute__((aligned(16))) h16_t Pl[2 * PL];
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l15 = lane & 15, g = lane >> 4;
-  const int ngrp = p.cout >> 7;
+  const int ngrp = p.cout / (64 * CPW);
   const int grp = blockIdx.x % ngrp, tile = (blockIdx.x / ngrp) % p.ntile, b = blockIdx.x / (ngrp * p.ntile);
   const int HW = p.HW, p0 = tile * NP, nst = (p.cin + KS - 1) / KS, nks = nst * (KS / 32);  // weights padded to KS
   float rng = 0.f;
@@ -93,20 +94,20 @@ __global__ __launch_bounds__(NT, 2) void conv1x1_x2_kernel(Args p) {
             float, __builtin_amdgcn_raw_buffer_load_b32(r, voff[k >> 2] + sx + (unsigned)((k & 3) * HW * 4), 0, 0));
   };
   // weight fragments of k step s (global), channel blocks cb0 + u, planes 0 / 1
-  const int cb0 = grp * 8 + 2 * wid;
+  const int cb0 = grp * 4 * CPW + CPW * wid;
   auto wfrag = [&](int s, int u, int pl) __attribute__((always_inline)) {
     const int st = __builtin_amdgcn_readfirstlane((s * (p.cout >> 4) * 2) * 1024);
     return __builtin_bit_cast(f16x8_t, __builtin_amdgcn_raw_buffer_load_b128(
                                            rw, (unsigned)((((cb0 + u) * 2 + pl) * 64 + lane) * 16), st, 0));
   };
-  f32x4 acc[2][NPB];
+  f32x4 acc[CPW][NPB];
 #pragma unroll
-  for (int u = 0; u < 2; ++u)
+  for (int u = 0; u < CPW; ++u)
 #pragma unroll
     for (int k = 0; k < NPB; ++k) acc[u][k] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float bo[2];  // loaded before the loop: an epilogue load would wait behind every load in flight
+  float bo[CPW];  // loaded before the loop: an epilogue load would wait behind every load in flight
 #pragma unroll
-  for (int u = 0; u < 2; ++u) bo[u] = p.bias[16 * (cb0 + u) + l15];
+  for (int u = 0; u < CPW; ++u) bo[u] = p.bias[16 * (cb0 + u) + l15];
 
   load_part(0, 0, 4 * NIT, true);
   for (int st = 0; st < nst; ++st) {
@@ -124,9 +125,9 @@ __global__ __launch_bounds__(NT, 2) void conv1x1_x2_kernel(Args p) {
     __syncthreads();
     const bool nlive = st + 1 < nst;
     const int stn = nlive ? st + 1 : st;
-    f16x8_t wa[2][2], wn[2][2];
+    f16x8_t wa[CPW][2], wn[CPW][2];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < CPW; ++u) {
       wa[u][0] = wfrag(4 * st, u, 0);
       wa[u][1] = wfrag(4 * st, u, 1);
     }
@@ -135,7 +136,7 @@ __global__ __launch_bounds__(NT, 2) void conv1x1_x2_kernel(Args p) {
     for (int kk = 0; kk < KS / 32; ++kk) {
       const int sn = kk + 1 < KS / 32 ? 4 * st + kk + 1 : 4 * st + kk;  // one k step ahead (unconditional)
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
+      for (int u = 0; u < CPW; ++u) {
         wn[u][0] = wfrag(sn, u, 0);
         wn[u][1] = wfrag(sn, u, 1);
       }
@@ -147,14 +148,14 @@ __global__ __launch_bounds__(NT, 2) void conv1x1_x2_kernel(Args p) {
         const f16x8_t xh = *reinterpret_cast<const f16x8_t*>(src);
         const f16x8_t xl = *reinterpret_cast<const f16x8_t*>(src + PL);
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
+        for (int u = 0; u < CPW; ++u) {
           f32x4 c = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, wa[u][1], acc[u][k], 0, 0, 0);
           c = __builtin_amdgcn_mfma_f32_16x16x32_f16(xl, wa[u][0], c, 0, 0, 0);
           acc[u][k] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, wa[u][0], c, 0, 0, 0);
         }
       }
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
+      for (int u = 0; u < CPW; ++u) {
         wa[u][0] = wn[u][0];
         wa[u][1] = wn[u][1];
       }
@@ -163,7 +164,7 @@ __global__ __launch_bounds__(NT, 2) void conv1x1_x2_kernel(Args p) {
   // epilogue: lane (g, l15) of (u, pixel block k) holds channel 16 (cb0 + u) + l15, pixels 16 k + 4 g .. + 3
   float* yb = p.y + (long)b * p.ybs;
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
+  for (int u = 0; u < CPW; ++u) {
     const int o = 16 * (cb0 + u) + l15;
 #pragma unroll
     for (int k = 0; k < NPB; ++k) {
@@ -210,9 +211,9 @@ using namespace ys;
 
 static int c1_pad(int cin) { return (cin + c1::KS - 1) / c1::KS * c1::KS; }
 
-// Cout a multiple of 128 (<= 1024), Cin a multiple of 32 (<= 4096; the weights are padded to a multiple of 128)
+// Cout 64 or a multiple of 128 (<= 1024), Cin a multiple of 32 (<= 4096; the weights are padded to a multiple of 128)
 YS_EXPORT size_t yolosod_conv1x1x2_prep_bytes(int cin, int cout) {
-  if (cin <= 0 || cin % 32 || cin > 4096 || cout <= 0 || cout % 128 || cout > 1024) return 0;
+  if (cin <= 0 || cin % 32 || cin > 4096 || cout <= 0 || (cout != 64 && cout % 128) || cout > 1024) return 0;
   Sizer s;
   s.take<h16_t>((size_t)2 * cout * c1_pad(cin));
   s.take<unsigned>(1);
@@ -277,10 +278,13 @@ YS_EXPORT int yolosod_conv1x1x2_silu_cat(const float* x, long x_bstride, const f
   const int ntile = (HW + NPx - 1) / NPx;
   c1::Args a{x, x_bstride, wp, bias, y, y_bstride, y2, y2_bstride, c2lo, cin, cout, HW, ntile, range_flag_dev(), flag,
              x2, x2_bstride, k1};
-  const long nwg = (long)B * ntile * (cout / 128);
+  const long nwg = (long)B * ntile * (cout == 64 ? 1 : cout / 128);
   YS_CHECK_ARG(nwg < (1L << 31), "conv1x1x2: too many tiles");
   hipStream_t st = (hipStream_t)stream;
-  if (NPx == 64) {
+  if (cout == 64) {  // one 64-channel group: a 16-channel block per wave
+    if (y2) hipLaunchKernelGGL((c1::conv1x1_x2_kernel<true, 64, 1>), dim3((unsigned)nwg), dim3(c1::NT), 0, st, a);
+    else hipLaunchKernelGGL((c1::conv1x1_x2_kernel<false, 64, 1>), dim3((unsigned)nwg), dim3(c1::NT), 0, st, a);
+  } else if (NPx == 64) {
     if (y2) hipLaunchKernelGGL((c1::conv1x1_x2_kernel<true, 64>), dim3((unsigned)nwg), dim3(c1::NT), 0, st, a);
     else hipLaunchKernelGGL((c1::conv1x1_x2_kernel<false, 64>), dim3((unsigned)nwg), dim3(c1::NT), 0, st, a);
   } else {
