@@ -44,8 +44,10 @@ STREAMS = int(_STREAMS_ENV) if _STREAMS_ENV is not None else 1
 # side streams the towers are dealt to, one tower (box or class, per level) at a time, round robin. With one side
 # stream every level's towers queued behind P2's (3.4 ms of 160x160 convs at n640): the P4 / P5 towers ran after the
 # neck had finished, one small conv at a time, and the main stream idled ~0.65 ms per step before the head. Three
-# side streams + main = the box's 4 hardware queues (GPU_MAX_HW_QUEUES); more would share queues.
-SIDE_STREAMS = max(1, int(os.environ.get("YOLOSOD_SIDE_STREAMS", "3")))
+# side streams + main = the box's 4 hardware queues (GPU_MAX_HW_QUEUES); more would share queues. With the tower
+# convs on the persistent fp16-split kernel two side streams are as fast (same box 3285 -> 3300 img/s, 2 x 2 runs,
+# profiles/r05/streams/): the default is 2.
+SIDE_STREAMS = max(1, int(os.environ.get("YOLOSOD_SIDE_STREAMS", "2")))
 # YOLOSOD_HEAD_SPLIT=1 (opt-in): the head's decode split at the last level - levels 0..nl-2 decoded once their towers
 # are done, while the last level's towers (which can only start when the neck's last feature map exists) still run
 # on the side streams. Same-box n640: 2273 vs 2258 img/s (+0.7 %), but the first part then shares the GPU with the
