@@ -32,14 +32,16 @@ def _xyxy(b):
 
 def _iou(b):
     """Pairwise IoU of xyxy boxes [n, 4] exactly as the oracle's torchvision restatement computes it: fp32 areas
-    (no +1), fp32 clamped intersection, fp32 ratio (returned as float64 for the margins)."""
+    (no +1), fp32 clamped intersection, fp32 ratio (returned as float64 for the margins). Two zero-area boxes give
+    0 / 0 = NaN, as in torchvision (its ``ovr > thr`` is then false: a NaN IoU never suppresses)."""
     b = b.astype(np.float32)
     area = (b[:, 2] - b[:, 0]) * (b[:, 3] - b[:, 1])
     lt = np.maximum(b[:, None, :2], b[None, :, :2])
     rb = np.minimum(b[:, None, 2:], b[None, :, 2:])
     wh = np.maximum(rb - lt, np.float32(0))
     inter = wh[..., 0] * wh[..., 1]
-    return (inter / ((area[:, None] + area[None, :]) - inter)).astype(np.float64)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        return (inter / ((area[:, None] + area[None, :]) - inter)).astype(np.float64)
 
 
 def nms_stability(y_ref: np.ndarray, y_oth: np.ndarray, conf=0.25, iou_thres=0.7, max_det=300, max_nms=30000,
@@ -57,7 +59,8 @@ def nms_stability(y_ref: np.ndarray, y_oth: np.ndarray, conf=0.25, iou_thres=0.7
     cand = np.nonzero(best > np.float32(conf))[0]
     res = {"d_score": d_s, "m_conf": m_conf, "n_cand": int(cand.size)}
     if cand.size == 0:
-        res.update(m_cls=np.inf, m_iou=np.inf, m_order=np.inf, m_out=np.inf, d_iou=0.0, keep=np.zeros(0, np.int64))
+        res.update(m_cls=np.inf, m_iou=np.inf, m_order=np.inf, m_out=np.inf, d_iou=0.0, nan_pairs=0,
+                   keep=np.zeros(0, np.int64))
         res["stable"] = m_conf > 2 * d_s
         return res
     sc = s_r[cand]
@@ -78,6 +81,7 @@ def nms_stability(y_ref: np.ndarray, y_oth: np.ndarray, conf=0.25, iou_thres=0.7
     order = np.argsort(-score, kind="stable")  # torchvision: descending score, stable
     # per class (the class offset max_wh keeps different classes apart), greedy with margins
     m_iou, m_order, d_iou = np.inf, np.inf, 0.0
+    nan_pairs = 0  # same-class pairs whose IoU is NaN (0 / 0) in one run only: such a pair has no margin
     keep_mask = np.zeros(len(cand), bool)
     for c in np.unique(cls):
         sel = order[cls[order] == c]  # this class, in processing order
@@ -85,10 +89,17 @@ def nms_stability(y_ref: np.ndarray, y_oth: np.ndarray, conf=0.25, iou_thres=0.7
         n = len(sel)
         if n > 1:
             iu = np.triu_indices(n, 1)
-            d_iou = max(d_iou, float(np.abs(ir[iu] - io[iu]).max()))
+            a_r, a_o = ir[iu], io[iu]
+            nr, no = np.isnan(a_r), np.isnan(a_o)
+            nan_pairs += int((nr != no).sum())
+            both = ~nr & ~no  # NaN in both runs: neither suppresses (ovr > thr is false), the same decision
+            if both.any():
+                d_iou = max(d_iou, float(np.abs(a_r[both] - a_o[both]).max()))
         kept = []
         for t in range(n):
-            mx = float(ir[kept, t].max()) if kept else 0.0
+            col = ir[kept, t]
+            col = col[~np.isnan(col)]  # torchvision's ovr > thr: a NaN IoU never suppresses
+            mx = float(col.max()) if col.size else 0.0
             m_iou = min(m_iou, abs(mx - iou_thres))
             if not (mx > iou_thres):
                 kept.append(t)
@@ -111,8 +122,9 @@ def nms_stability(y_ref: np.ndarray, y_oth: np.ndarray, conf=0.25, iou_thres=0.7
     m_out = min(m_out, cut)
     res.update(m_cls=m_cls, m_iou=m_iou, m_order=m_order, m_out=m_out, d_iou=d_iou,
                keep=cand[kept_idx[:max_det]].astype(np.int64))
+    res["nan_pairs"] = nan_pairs
     res["stable"] = bool(m_conf > 2 * d_s and m_cls > 2 * d_s and m_order > 2 * d_s and m_out > 2 * d_s
-                         and m_iou > d_iou_tol)
+                         and m_iou > d_iou_tol and nan_pairs == 0)
     return res
 
 

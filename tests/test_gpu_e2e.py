@@ -141,7 +141,10 @@ def test_e2e_kept_indices_gpu_vs_oracle(e2e):
          f"decision-stable, {exceptions} justified exceptions ({ties} of them exact fp32 ties only; "
          f"{exceptions - ties} others against a cap of {cap}); " + " || ".join(report))
     # the count is a sanity bound on top of the per-decision justification: differences that are not exact ties
-    assert exceptions - ties <= cap, report
+    headroom = (f"{kind}: {exceptions - ties} non-tie exceptions against a cap of {cap} (headroom "
+                f"{cap - (exceptions - ties)}), {ties} tie-only, {exact}/{B_GPU} bit-exact")
+    _log(headroom)
+    assert exceptions - ties <= cap, headroom + " || " + " || ".join(report)
     assert kept_exact >= 100, "too few kept boxes on bit-exact images for the test to mean anything"
     if kind == "noisy":
         assert stable_exact >= 8, report

@@ -2,6 +2,8 @@
 greedy NMS exactly (same kept anchors, same order), flags perturbations that flip a decision, and the side-by-side
 replay (replay_divergences) finds EVERY divergent decision of an image, each with its own perturbation, while ending
 on the second run's own NMS result."""
+import warnings
+
 import numpy as np
 import pytest
 
@@ -177,6 +179,15 @@ def test_replay_nan_iou_of_zero_area_boxes():
     assert "nan" in {d["kind"] for d in r["decisions"]} and not r["ok"]
     assert np.array_equal(r["keep"], _nms(oth))
     assert c == int(s[y].argmax())
+    # the margin analysis: a pair NaN in one run only has no margin, so the image is not decision-stable (min(inf,
+    # nan) used to fold it away as stable), and no RuntimeWarning escapes
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        st = nms_stability(pred, oth)
+        same = nms_stability(pred, pred.copy())
+    assert st["nan_pairs"] >= 1 and not st["stable"]
+    assert same["nan_pairs"] == 0 and np.isfinite(same["m_iou"])
+    assert np.array_equal(same["keep"], keep)
 
 
 @pytest.mark.parametrize("case", ["nms_degenerate", "nms_ties", "nms_predict"])
