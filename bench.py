@@ -260,8 +260,9 @@ def measure(name, world, rank, dev, steps, warmup, conf, ops_csv=None, time_all=
     # every launch); the last warmup step runs through the filter so that it knows the plain variants to time
     select = None if time_all else perf.PathSelect()
     t_w = time.perf_counter()
-    for i in range(warmup):
-        if i == warmup - 1 and select is not None:
+    # with --warmup 0 one untimed primer step still runs through the filter (it learns the plain variants there)
+    for i in range(max(warmup, 1 if select is not None else 0)):
+        if i == max(warmup, 1) - 1 and select is not None:
             with _hip.op_timer(select):
                 step()
         else:
@@ -269,23 +270,34 @@ def measure(name, world, rank, dev, steps, warmup, conf, ops_csv=None, time_all=
     torch.cuda.synchronize()
     log(f"[rank {rank}] {name}: warmup {warmup} steps {time.perf_counter() - t_w:.2f}s")
 
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    with _hip.op_timer(select) as timer:
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            step()
-        torch.cuda.synchronize()
+    def timed():
         if world > 1:
             dist.barrier()
-        t1 = time.perf_counter()
-    # one read of the split-range flag per rank after the region (fp32 configs; bf16 runs no split kernels)
-    flagged = float(dtype == torch.float32 and _hip.split_range_flag(reset=True, device=dev))
-    red = torch.tensor([t1 - t0, flagged], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(red, op=dist.ReduceOp.MAX)
-    elapsed, flagged = float(red[0].item()), bool(red[1].item())
+        torch.cuda.synchronize()
+        with _hip.op_timer(select) as timer:
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                step()
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            t1 = time.perf_counter()
+        # one read of the split-range flag per rank after the region (fp32 configs; bf16 runs no split kernels)
+        flagged = float(dtype == torch.float32 and _hip.split_range_flag(reset=True, device=dev))
+        red = torch.tensor([t1 - t0, flagged], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(red, op=dist.ReduceOp.MAX)
+        return float(red[0].item()), bool(red[1].item()), timer
+
+    elapsed, flagged, timer = timed()
+    redone = False
+    if flagged:
+        # an operand left the fp16-split kernels' range inside the region: the predictor would redo such a batch on
+        # the exact fp32 kernels, so the line reports the region timed that way instead of the flagged steps
+        log(f"[rank {rank}] {name}: split-range flag set in the timed region; re-timing on the exact fp32 kernels")
+        with _hip.exact_fp32_matrix():
+            elapsed, _, timer = timed()
+        redone = True
     durs = timer.durations_ms()
 
     # per-operator live timings (HIP events on the launch stream) -> roofline of the dominant operator; the
@@ -325,6 +337,7 @@ def measure(name, world, rank, dev, steps, warmup, conf, ops_csv=None, time_all=
                                   f"forward + decode + NMS(conf={conf}, iou=0.7)",
                       "imgsz": imgsz, "batch_per_gpu": bs, "global_batch": bs * world, "parallelism": f"dp{world}"},
            "roofline": roofline, "path_roofline": path_roofline, "split_range_flagged": flagged,
+           "split_range_redone_exact": redone,
            "hip_ops_ms_per_step": round(t_meas, 3),
            "hip_ops": [{k: v for k, v in o.items() if k not in ("bytes", "flops", "key")} for o in ops],
            "backbone_hip_ms_per_step": round(sum(o["total_ms_per_step"] for o in backbone), 3),

@@ -167,12 +167,24 @@ def _measure_worker(rank, world, port, q):
         b.sharded_predict = sharded
         b._hip.op_timer = _Timer
         b._hip.split_range_flag = lambda reset=False, device=None: reads.append(1) or (rank == 1)
+        exact = []
+
+        class Exact:
+            def __enter__(self):
+                exact.append(len(steps))
+
+            def __exit__(self, *a):
+                return False
+
+        b._hip.exact_fp32_matrix = Exact
         torch.cuda.synchronize = lambda *a, **k: None
         res, _, _, _ = b.measure("tiny", world, rank, torch.device("cpu"), steps=4, warmup=2, conf=0.25)
-        ok = (len(reads) == 1 and steps == [0] * 6 and guards == [False] * 6
-              and res["split_range_flagged"] is True  # max over ranks: rank 1 flagged
+        # warmup 2 + 4 timed steps with no flag read inside; the flag (max over ranks: rank 1 flagged) is read once
+        # after the region, and the flagged region is timed again on the exact kernels (4 more steps, one more read)
+        ok = (len(reads) == 2 and steps == [0] * 6 + [1] * 4 and guards == [False] * 10 and exact == [6]
+              and res["split_range_flagged"] is True and res["split_range_redone_exact"] is True
               and res["config"]["global_batch"] == 4 and res["value"] > 0)
-        q.put((rank, bool(ok), (len(reads), steps, guards, res.get("split_range_flagged"))))
+        q.put((rank, bool(ok), (len(reads), steps, guards, exact, res.get("split_range_flagged"))))
     finally:
         dist.destroy_process_group()
 

@@ -268,3 +268,47 @@ def test_split_range_cached_a2_block_rereports_long_sequence(cuda):
         with torch.inference_mode():
             m(x)
         assert _hip.split_range_flag(reset=True)
+
+
+def _conv_target(m, which):
+    """The first fused Conv of the model that the executor routes to an fp16-split conv kernel of kind ``which``:
+    a Detect tower 3x3 (conv3x3), a neck C2f Bottleneck 3x3 (conv3x3, s1), a neck stride-2 3x3 (conv3x3s2, s2), a
+    neck wide 1x1 (conv1x1x2, n1), or the SE / CBAM gate's consumer (gate-fused conv3x3s2)."""
+    from yolosod_amd.nn import modules as M
+    if which == "gate":
+        plan = m._gate_consumers()
+        return plan[min(plan)]
+    return next(c for c in m.modules() if isinstance(c, M.Conv) and getattr(c, which))
+
+
+@pytest.mark.parametrize("which", ["tower", "s1", "s2", "n1", "gate"])
+def test_predictor_guard_recovers_out_of_range_conv_weights(which, cuda):
+    """the fp16-split conv kernels report into the split-range flag, and the predictor's fallback
+    (exact_fp32_matrix) must route them away too - to MIOpen + the exact epilogues - or the redone batch would run the
+    same kernels and return inf / NaN. Weights of one conv scaled past fp16's range (64 W > 65504, flagged by the
+    cached weight preparation on every forward): the guarded predict is finite and equals the exact run bit for bit."""
+    from yolosod_amd.engine.predictor import DetectionPredictor, seeded_images
+    from yolosod_amd.nn.tasks import build_model
+    m = build_model("yolov12-sod-fusion-v5-simple.yaml", seed=0, device=cuda)
+    pred = DetectionPredictor(m, conf=0.001, iou=0.7, max_det=300)
+    conv = _conv_target(pred.model, which)
+    with torch.no_grad():
+        conv.conv.weight.mul_(4e4)
+    x = seeded_images(0, 2, 256, device=cuda)
+    det = torch.backends.cudnn.deterministic
+    torch.backends.cudnn.deterministic = True
+    try:
+        _hip.split_range_flag(reset=True)
+        with torch.inference_mode():
+            pred.predict_padded(x)
+        assert _hip.split_range_flag(reset=True), which  # the split conv kernel saw its weights out of range
+        with torch.inference_mode():
+            g_out, g_cnt, g_idx = pred.predict_padded_guarded(x)
+        assert not _hip.split_range_flag(reset=True)  # the guard consumed (and cleared) the flag
+        with torch.inference_mode(), _hip.exact_fp32_matrix():
+            r_out, r_cnt, r_idx = pred.predict_padded(x)
+        assert not _hip.split_range_flag(reset=True), which  # nothing on the exact path splits
+    finally:
+        torch.backends.cudnn.deterministic = det
+    assert torch.isfinite(g_out).all()
+    assert torch.equal(g_cnt, r_cnt) and torch.equal(g_idx, r_idx) and torch.equal(g_out, r_out)

@@ -473,23 +473,38 @@ def split_range_flag(reset: bool = True, device=None) -> bool:
     return rc == 1
 
 
+_split_convs_off = 0  # > 0 inside exact_fp32_matrix(): the fp16-split convolution kernels are bypassed
+
+
+def split_convs_enabled() -> bool:
+    """Whether the executor may route convolutions to the fp16-split conv kernels (conv3x3 / conv3x3s2 / conv1x1x2:
+    Detect towers, the gate-fused SE / CBAM consumers, the neck); false inside exact_fp32_matrix(), where they run on
+    MIOpen (+ the exact-fp32 epilogue / thin 1x1 kernels) instead."""
+    return _split_convs_off == 0
+
+
 class exact_fp32_matrix:
     """``with exact_fp32_matrix(): ...`` runs the fp32 model's matrix products on the exact fp32 MFMA kernels
-    (Swin swin_fused / swin_wide, Detect head LDS kernel, A2 fp32 GEMMs) instead of the fp16 two-term splits - the
-    fallback when split_range_flag() reports an operand outside fp16's range."""
+    (Swin swin_fused / swin_wide, Detect head LDS kernel, A2 fp32 GEMMs) instead of the fp16 two-term splits, and its
+    convolutions on MIOpen instead of the fp16-split conv kernels (split_convs_enabled) - the fallback when
+    split_range_flag() reports an operand outside fp16's range."""
 
     _SWITCHES = ("yolosod_debug_set_swin_x3", "yolosod_debug_set_head_x2", "yolosod_debug_set_a2_x2")
 
     def __enter__(self):
+        global _split_convs_off
         lib = load_library()
         # each switch returns its previous state, restored on exit (a user's YOLOSOD_*=0 or an outer setting stays)
         self._prev = [int(getattr(lib, f)(0)) for f in self._SWITCHES]
+        _split_convs_off += 1
         return self
 
     def __exit__(self, *exc):
+        global _split_convs_off
         lib = load_library()
         for f, v in zip(self._SWITCHES, self._prev):
             getattr(lib, f)(v)
+        _split_convs_off -= 1
         return False
 
 

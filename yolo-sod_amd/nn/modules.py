@@ -51,12 +51,41 @@ def _cached(mod: nn.Module, tag: str, srcs, make):
     # are never modified in place outside inference mode, their identity is the key
     # id(t) too: a replaced parameter can land at the freed address with version 0 (load_state_dict(assign=True),
     # new Parameters), which (data_ptr, version) alone would take for the old one
+    # A cached device tensor is allocated on the stream that first made it (main or a Detect tower's side stream) and
+    # may later be read on another: each use from a different stream records that stream on it, so that the caching
+    # allocator does not hand the block out again (after a parameter replacement) while such a launch still reads it.
     key = tuple((id(t), t.data_ptr(), -1 if t.is_inference() else t._version, t.dtype, t.device) for t in srcs)
     cache = mod.__dict__.setdefault("_ys_cache", {})
     ent = cache.get(tag)
     if ent is None or ent[0] != key:
-        ent = cache[tag] = (key, make())
+        val = make()
+        dev = _cuda_device(val)
+        ent = cache[tag] = (key, val, torch.cuda.current_stream(dev) if dev is not None else None)
+    elif ent[2] is not None:
+        cur = torch.cuda.current_stream(ent[2].device)
+        if cur != ent[2]:
+            _record_stream(ent[1], cur)
     return ent[1]
+
+
+def _cuda_device(v):
+    if isinstance(v, torch.Tensor):
+        return v.device if v.is_cuda else None
+    if isinstance(v, (tuple, list)):
+        for t in v:
+            d = _cuda_device(t)
+            if d is not None:
+                return d
+    return None
+
+
+def _record_stream(v, stream):
+    if isinstance(v, torch.Tensor):
+        if v.is_cuda:
+            v.record_stream(stream)
+    elif isinstance(v, (tuple, list)):
+        for t in v:
+            _record_stream(t, stream)
 
 
 def _f32(mod: nn.Module, tag: str, *ts):
@@ -131,9 +160,10 @@ def conv_epilogue(conv: nn.Conv2d, act_code, x, out=None, res=None, stats=None, 
     if x.device.type != "cuda" or conv.bias is None or act_code is None or x.dtype not in (torch.float32,
                                                                                            torch.bfloat16):
         return None
+    split = _hip.split_convs_enabled()  # false inside _hip.exact_fp32_matrix(): no fp16-split conv kernel
     if isinstance(x, _hip.CatView):  # a virtual concat: a 1x1 kernel reads both parts in place, else materialise
         if act_code == 1 and res is None and stats is None and conv.kernel_size == (1, 1):
-            if n1 and N1_NECK and _hip.conv1x1x2_ok(x, conv) and (out is None or _hip._imgs_contig(out)) and (
+            if split and n1 and N1_NECK and _hip.conv1x1x2_ok(x, conv) and (out is None or _hip._imgs_contig(out)) and (
                     out2 is None or _hip._imgs_contig(out2)):
                 prep = lambda: _cached(conv, "c1prep", (conv.weight,), lambda: _hip.conv1x1x2_prepare(conv.weight))  # noqa: E731
                 return _hip.conv1x1x2_silu(x, conv.bias, prep, conv.out_channels, out=out, out2=out2, c2lo=c2lo)
@@ -143,20 +173,20 @@ def conv_epilogue(conv: nn.Conv2d, act_code, x, out=None, res=None, stats=None, 
                 return _hip.conv1x1_thin(x, conv.weight.detach().reshape(conv.out_channels, -1), conv.bias.detach(),
                                          out=out, out2=out2, c2lo=c2lo)
         x = x.materialize()
-    if (act_code == 1 and out is None and res is None and stats is None and out2 is None and CONV3X3 != "0"
+    if (split and act_code == 1 and out is None and res is None and stats is None and out2 is None and CONV3X3 != "0"
             and (CONV3X3 == "all" or tower) and _hip.conv3x3_ok(x, conv)
             and (CONV3X3 == "force" or x.shape[0] * -(-x.shape[2] // 8) * -(-x.shape[3] // 32) >= CONV3X3_MIN_TILES)):
         prep = lambda: _cached(conv, "c3prep", (conv.weight,), lambda: _hip.conv3x3_prepare(conv.weight))  # noqa: E731
         return _hip.conv3x3_silu(x, conv.bias, prep, conv.out_channels)
-    if (n1 and N1_NECK and act_code == 1 and res is None and stats is None and _hip.conv1x1x2_ok(x, conv)
+    if (split and n1 and N1_NECK and act_code == 1 and res is None and stats is None and _hip.conv1x1x2_ok(x, conv)
             and (out is None or _hip._imgs_contig(out)) and (out2 is None or _hip._imgs_contig(out2))):
         prep = lambda: _cached(conv, "c1prep", (conv.weight,), lambda: _hip.conv1x1x2_prepare(conv.weight))  # noqa: E731
         return _hip.conv1x1x2_silu(x, conv.bias, prep, conv.out_channels, out=out, out2=out2, c2lo=c2lo)
-    if (s1 and S1_NECK and act_code == 1 and stats is None and out2 is None and _hip.conv3x3_ok(x, conv)
+    if (split and s1 and S1_NECK and act_code == 1 and stats is None and out2 is None and _hip.conv3x3_ok(x, conv)
             and x.shape[3] % 4 == 0 and (res is None or _hip._imgs_contig(res))):
         prep = lambda: _cached(conv, "c3prep", (conv.weight,), lambda: _hip.conv3x3_prepare(conv.weight))  # noqa: E731
         return _hip.conv3x3_silu(x, conv.bias, prep, conv.out_channels, out=out, res=res)
-    if (s2 and S2_NECK and act_code == 1 and res is None and stats is None and out2 is None
+    if (split and s2 and S2_NECK and act_code == 1 and res is None and stats is None and out2 is None
             and _hip.conv3x3s2_ok(x, conv)):
         prep = lambda: _cached(conv, "c3s2prep", (conv.weight,), lambda: _hip.conv3x3s2_prepare(conv.weight))  # noqa: E731
         return _hip.conv3x3s2_silu(x, conv.bias, prep, conv.out_channels, out=out)
@@ -200,7 +230,7 @@ def catview_route(cv, c0, c1, H, W, dtype) -> bool:
             or cv.emit_stats is not None or conv.kernel_size != (1, 1) or conv.stride != (1, 1) or conv.groups != 1
             or conv.padding != (0, 0) or conv.in_channels != c0 + c1):
         return False
-    if cv.n1 and N1_NECK and c0 % 128 == 0 and c1 % 32 == 0 and (H * W) % 4 == 0 and int(
+    if cv.n1 and N1_NECK and _hip.split_convs_enabled() and c0 % 128 == 0 and c1 % 32 == 0 and (H * W) % 4 == 0 and int(
             _hip.load_library().yolosod_conv1x1x2_prep_bytes(c0 + c1, conv.out_channels)) > 0:
         return True
     return (THIN1X1 and conv.out_channels == 64 and c0 + c1 in _hip.THIN1X1_CIN and (H * W) % 64 == 0
@@ -236,7 +266,7 @@ class Conv(nn.Module):
     def gated_ok(self, x) -> bool:
         """This (fused, SiLU) Conv can run as the stride-2 kernel with its producer's gate applied at staging."""
         return (not hasattr(self, "bn") and self.conv.bias is not None and isinstance(self.act, nn.SiLU)
-                and _hip.conv3x3s2_ok(x, self.conv))
+                and _hip.split_convs_enabled() and _hip.conv3x3s2_ok(x, self.conv))
 
     def forward_gated(self, x, gate_c, gate_p, key):
         """SiLU(conv((x * gate_c) * gate_p) + b): the consumer of an SE (gate_c) / CBAM (gate_c = ca, gate_p = sa)
@@ -320,7 +350,7 @@ class C2f(nn.Module):
             # each Bottleneck's input also lands packed in `t` (dual-store epilogue): MIOpen reads packed tensors,
             # so a channel slice of z would cost a copy pass per Bottleneck
             z = torch.empty((B, (2 + n) * c, H, W), dtype=x.dtype, device=x.device)
-            if (n and S1_NECK and C2F_SLICES and x.dtype == torch.float32 and W % 4 == 0
+            if (n and S1_NECK and C2F_SLICES and _hip.split_convs_enabled() and x.dtype == torch.float32 and W % 4 == 0
                     and all(m.cv1.s1 and m.cv2.s1 and m.cv1.conv.kernel_size == (3, 3) for m in self.m)):
                 # the Bottlenecks run on the stride-1 fp16-split kernel, which reads channel slices: each one reads
                 # its input in place from z (no packed second store)

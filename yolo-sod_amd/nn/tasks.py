@@ -244,9 +244,15 @@ class BaseModel(nn.Module):
         if plan is not None:
             return plan
         plan = {}
+        # a consumer that writes into a planned Concat slice or feeds a Detect level keeps its own path: the gated
+        # form returns early, before the concat-plan and tower bookkeeping of the executor
+        det = self.model[-1]
+        busy = set(self._concat_producers()) | (set(det.f) if isinstance(det, M.Detect) and isinstance(
+            det.f, (list, tuple)) else set())
         for k in range(len(self.model) - 1):
             m, nxt = self.model[k], self.model[k + 1]
-            if (isinstance(m, (M.SE, M.CBAM_Block)) and k not in self.save and isinstance(nxt, M.Conv)
+            if (isinstance(m, (M.SE, M.CBAM_Block)) and k not in self.save and k + 1 not in busy
+                    and isinstance(nxt, M.Conv)
                     and not isinstance(nxt, M.DWConv) and nxt.f == -1 and nxt.conv.kernel_size == (3, 3)
                     and nxt.conv.stride == (2, 2) and nxt.conv.groups == 1 and nxt.conv.out_channels in (64, 128)):
                 plan[k] = nxt
