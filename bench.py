@@ -373,6 +373,9 @@ def compact_line(result, detail_path=None):
     line["roofline"] = _compact_roofline(result["roofline"])
     pr = result["path_roofline"]
     line["path_roofline"] = {k: pr[k] for k in ("t_min_ms", "t_meas_ms", "frac", "frac_vs_dtype_peak")}
+    if "mafn" in pr:  # SURVEY 8(d)'s fixed path: MAFN + decode + NMS only (perf.mafn_path)
+        line["mafn_path"] = {k: pr["mafn"][k] for k in ("t_hbm_floor_ms", "t_min_ms", "t_meas_ms", "frac",
+                                                         "frac_vs_hbm_floor")}
     line["hip_ops_avg_ms"] = {_op_name(o): o["avg_ms"] for o in result.get("hip_ops", [])}
     nl = result.get("nms_loaded")
     line["nms_loaded_ms_per_call"] = None if nl is None else {k: v["ms_per_call"] for k, v in nl.items()}
@@ -390,7 +393,8 @@ def compact_line(result, detail_path=None):
                                "batch_per_gpu": c["config"]["batch_per_gpu"], "imgsz": c["config"]["imgsz"],
                                "roofline_frac": c["roofline"]["frac"], "roofline_kernel":
                                    c["roofline"]["kernel"].split(" (")[0],
-                               "path_roofline_frac": c["path_roofline"]["frac"]}
+                               "path_roofline_frac": c["path_roofline"]["frac"],
+                               "mafn_path_frac": (c["path_roofline"].get("mafn") or {}).get("frac")}
                            for n, c in result["configs"].items()}
     if detail_path:
         line["detail"] = str(detail_path)

@@ -49,6 +49,12 @@ def check(line, ops, path, label):
         if abs(line["path_roofline"][k] - path[k]) > 2e-4:
             print(f"{label}: path_roofline.{k}: line {line['path_roofline'][k]} vs CSV {path[k]}")
             bad += 1
+    mp = line["path_roofline"].get("mafn")
+    if mp is not None:
+        for k in ("t_min_ms", "t_meas_ms", "frac", "t_hbm_floor_ms"):
+            if abs(mp[k] - path["mafn"][k]) > 2e-4:
+                print(f"{label}: mafn_path.{k}: line {mp[k]} vs CSV {path['mafn'][k]}")
+                bad += 1
     return bad
 
 
@@ -56,6 +62,9 @@ def main():
     res = recompute(sys.argv[1])
     for cfg, (ops, path) in res.items():
         print(f"{cfg}: path_roofline {path['frac']} (t_min {path['t_min_ms']} / t_meas {path['t_meas_ms']} ms)")
+        mp = path["mafn"]
+        print(f"{cfg}: mafn_path {mp['frac']} (t_min {mp['t_min_ms']} / t_meas {mp['t_meas_ms']} ms), HBM floor "
+              f"{mp['t_hbm_floor_ms']} ms -> {mp['frac_vs_hbm_floor']}; {'; '.join(mp['instances'])}")
         for o in ops:
             ex = f"  producer_extra {o['producer_extra_ms']:.4f}  [{o['producer']}]" if "producer_extra_ms" in o else ""
             print(f"  {o['op']:5s} {str(o['shape']):22s} x{o['launches']:3d} avg {o['avg_ms']:.4f} ms "

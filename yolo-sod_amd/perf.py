@@ -278,7 +278,61 @@ def summarize(calls, steps):
                           "gate's statistics (in-model producer minus its in-model plain variant of the same shape) is "
                           "billed to the gate",
             "frac_vs_dtype_peak": round(t_min_d / t_meas, 4) if t_meas else None}
+    path["mafn"] = mafn_path(ops, steps)
     return ops, sorted(backbone, key=lambda o: -o["total_ms_per_step"]), path
+
+
+# ---- the MAFN + decode + NMS path exactly as SURVEY 8(d) defines it -------------------------------------------------
+
+def _split_fused(key):
+    """A gate-fused operator (se_conv / cbam_conv) -> (8(d) key of its gate instance, the consumer conv's own t_min in
+    ms): the conv reads the gated input once and writes its output once, its FLOPs at the fp16-split ceiling."""
+    op, shape, extra = key[:3]
+    B, C, H, W = shape
+    cout, hid = extra
+    E = elem_size(key)
+    Ho, Wo = (H + 1) // 2, (W + 1) // 2
+    conv_b = (B * C * H * W + B * cout * Ho * Wo) * E + (cout * C * 9 + cout) * F32
+    conv_f = 2 * B * Ho * Wo * cout * C * 9
+    t_conv = max(conv_b / (PEAK_HBM_GBS * 1e9), conv_f / (PEAK_BF16_MFMA_TFLOPS / 3 * 1e12)) * 1e3
+    return (FUSED_CONV[op], tuple(shape), hid) + tuple(key[3:]), t_conv
+
+
+def mafn_path(ops, steps):
+    """SURVEY 8(d)'s path, a fixed definition: the MAFN instances (SE / CBAM / CA / A2 / Swin / Mamba: input read once,
+    output written once, weights once), the decode (A (74 + 14) floats per image: the fused Detect head is billed at the
+    decode's bytes, its measured time includes the towers' last 1x1 convs) and the NMS scan (A 14 floats per image).
+    t_min per instance = max(bytes / 8 TB/s, FLOPs / the matrix ceiling of the method it computes with); t_meas = its
+    measured time. SE L1 / CBAM L4 run inside their consumer stride-2 conv (gate fusion): the instance is billed at its
+    8(d) bytes, its measured time = the fused operator's time minus the conv's own t_min (so an upper bound on the
+    gate's time) and the conv's FLOPs are not counted. ``frac_vs_hbm_floor`` = the 8(d) HBM floor (all bytes at 8 TB/s;
+    0.352 ms for n640 bs 32) / t_meas."""
+    t_min = t_meas = 0.0
+    nbytes = 0
+    parts = []
+    for o in ops:
+        key, n = o["key"], o["launches"]
+        if key[0] in FUSED_CONV:
+            k8, t_conv = _split_fused(key)
+            meas = max(o["avg_ms"] - t_conv, 0.0)
+        elif key[0] == "head":
+            B, A = key[1]
+            nc = key[2][0]
+            k8, meas = ("decode", (B, A), nc) + tuple(key[3:]), o["avg_ms"]
+        else:
+            k8, meas = key, o["avg_ms"]
+        b, _ = op_cost(k8)
+        tm = t_min_ms(k8, method=True)
+        nbytes += b * n / steps
+        t_min += tm * n / steps
+        t_meas += meas * n / steps
+        parts.append(f"{k8[0]}{tuple(k8[1])}: {meas:.4f} ms")
+    floor = nbytes / (PEAK_HBM_GBS * 1e9) * 1e3
+    return {"bytes_per_step": int(nbytes), "t_hbm_floor_ms": round(floor, 4), "t_min_ms": round(t_min, 4),
+            "t_meas_ms": round(t_meas, 4), "frac": round(t_min / t_meas, 4) if t_meas else None,
+            "frac_vs_hbm_floor": round(floor / t_meas, 4) if t_meas else None,
+            "definition": "SURVEY 8(d): MAFN instances + decode + NMS scan; gate-fused SE/CBAM billed without their "
+                          "consumer conv (its t_min subtracted, its FLOPs excluded)", "instances": parts}
 
 
 # ---- per-launch CSV (bench.py --ops-csv): one row per timed C-ABI launch sequence ---------------------------------
