@@ -100,3 +100,26 @@ def test_path_select_times_the_path_its_producers_and_their_plain_variants_only(
     for key in (("conv3x3", (32, 64, 160, 160), 64), ("conv3x3s2", (32, 64, 160, 160), (128, False, False)),
                 ("conv1x1x2", (32, 192, 80, 80), (128, True)), ("bias_act", (32, 64, 80, 80), None)):
         assert not sel(key), key
+
+
+def test_mafn_path_is_survey_8d_definition():
+    """perf.mafn_path: the MAFN instances + decode + NMS scan of SURVEY 8(d), whatever the executor fuses. Synthetic
+    region of the n640 paper model (bs 32, one launch each): its HBM floor is 8(d)'s 2.812 GB at 8 TB/s = 0.352 ms;
+    the gate-fused SE L1 / CBAM L4 are billed at their 8(d) bytes with the consumer conv's t_min taken off their
+    measured time and its FLOPs excluded; the Detect head is billed as the decode."""
+    B, nc = 32, 10
+    calls = [(("se_conv", (B, 32, 320, 320), (64, 4)), 0.25), (("cbam_conv", (B, 64, 160, 160), (128, 4)), 0.2),
+             (("swin", (B, 256, 40, 40), (4, 7, 512)), 0.36), (("a2", (B, 512, 20, 20), (8, 8)), 0.12),
+             (("cbam", (B, 256, 40, 40), 16), 0.05), (("se", (B, 128, 80, 80), 8), 0.04),
+             (("swin", (B, 64, 160, 160), (2, 7, 128)), 0.45), (("ca", (B, 128, 80, 80), 8), 0.05),
+             (("head", (B, 34000), (nc, 64, 64)), 0.15), (("nms", (B, nc, 34000), None), 0.035)]
+    ops, _, path = perf.summarize(calls, 1)
+    mp = path["mafn"]
+    assert abs(mp["t_hbm_floor_ms"] - 0.352) < 2e-3, mp
+    assert len(mp["instances"]) == 10
+    se8 = perf.t_min_ms(("se", (B, 32, 320, 320), 4), method=True)
+    _, t_conv = perf._split_fused(("se_conv", (B, 32, 320, 320), (64, 4)))
+    assert 0 < t_conv < 0.25 and se8 < 0.25 - t_conv
+    assert abs(mp["t_meas_ms"] - (sum(ms for _, ms in calls) - t_conv
+                                  - perf._split_fused(("cbam_conv", (B, 64, 160, 160), (128, 4)))[1])) < 1e-3
+    assert mp["frac_vs_hbm_floor"] == round(mp["t_hbm_floor_ms"] / mp["t_meas_ms"], 4)
