@@ -257,21 +257,15 @@ int yolosod_layernorm(const float* x, float* y, long rows, int C, const float* w
 int yolosod_attention(const float* qkv, float* out, long n_seq, int L, int C, int heads, void* stream);
 
 /* Test hook: 1 routes SwinBlock shapes the fused per-window kernel covers (C 64/128, heads 2/4, window <= 7x7,
- * mlp 2C) through it (default, or env YOLOSOD_SWIN_FUSED), 0 forces the decomposed GEMM path for every shape. */
+ * mlp 2C) through it (default), 0 forces the decomposed GEMM path for every shape. */
 void yolosod_debug_set_swin_fused(int on);
 /* Test hook: 1 (default; env YOLOSOD_SWIN_X3=0 turns it off) routes 7x7-window SwinBlocks with C = 64 / 2 heads and
  * C = 256 / 4 heads through the kernels that run every matrix product as fp16 two-term splits on the fp16 matrix
  * cores at fp32 accuracy (csrc/swin_x3.hip), 0 through the exact-fp32-MFMA fused kernels. */
 int yolosod_debug_set_swin_x3(int on);
-/* Test hook: 1 (env YOLOSOD_SWIN_SPLIT=1) runs the C = 64 fp16-split SwinBlock as two kernels split at the attention
- * residual (per-window attention half, token-tiled MLP / pw half), 0 (default) as the one-kernel form.
- * The yolosod_debug_set_* switches that return int return the previous state. */
-int yolosod_debug_set_swin_split(int on);
-/* Test hook: the C = 64 fp16-split SwinBlock kernel's activation planes as unpadded rows with XOR-swizzled 16-byte
- * chunks (1, default; env YOLOSOD_X3_SWZ=0 turns it off) or rows padded to 80 elements (0); same results. */
-int yolosod_debug_set_x3_swz(int on);
+/* The yolosod_debug_set_* switches that return int return the previous state. */
 /* Test hook: pixels per area group of the A2 proj + SiLU + pooling kernel (the launcher takes the fewest area groups
- * whose row bands fit; 208 by default - two workgroups per CU - env YOLOSOD_A2_POOL_PX; <= 0 restores 208). Same
+ * whose row bands fit; 208 by default - two workgroups per CU; <= 0 restores 208). Same
  * results for every cap. Returns the previous cap. */
 int yolosod_debug_set_a2_pool_px(int px);
 /* Test hook: 1 (default; env YOLOSOD_HEAD_X2=0 turns it off) runs the Detect head's 1x1 convs as fp16 two-term
@@ -281,15 +275,11 @@ int yolosod_debug_set_head_x2(int on);
  * turns it off) or exact fp32 MFMA (0); yolosod_debug_set_gemm_x2(1) makes every yolosod_gemm_f32 / internal fp32 GEMM
  * call take the split products, 0 restores the callers' choice. */
 int yolosod_debug_set_a2_x2(int on);
-/* Test hook: A2_Attn's split path through the fused kernels (1, default; env YOLOSOD_A2_FUSED=0 turns it off:
+/* Test hook: A2_Attn's split path through the fused kernels (1, default:
  * proj + SiLU + pooling, then LN + QKV + attention, csrc/a2_fused.hip) or the decomposed GEMM path (0). */
 int yolosod_debug_set_a2_fused(int on);
-/* Test hook: A2_Attn's tail as one kernel (1; env YOLOSOD_A2_OUTUP=1, default off: the folded out-projection,
- * the bilinear upsample along H, SiLU and the residual, csrc/a2_fused.hip a2_out_up_kernel) or as the token GEMM and
- * a separate upsample pass (0); returns the previous state. */
-int yolosod_debug_set_a2_outup(int on);
-/* Test hook: A2_Attn's proj + SiLU + pooling kernel with 128 / 256 output channels per workgroup (1, default; env
- * YOLOSOD_A2_POOL_WIDE=0 turns it off) or with 64 (0); returns the previous state. */
+/* Test hook: A2_Attn's proj + SiLU + pooling kernel with 128 / 256 output channels per workgroup (1, default)
+ * or with 64 (0); returns the previous state. */
 int yolosod_debug_set_a2_pool_wide(int on);
 /* The SE gate only, sigmoid(fc2(relu(fc1(mean_hw(x)))))   smallobj_modules.py:87-90, into gate [B][C], for a consumer
  * that applies y = x * gate itself (yolosod_conv3x3s2_silu); psum: x's per-plane partial sums from its producer
@@ -346,7 +336,7 @@ int yolosod_debug_set_conv3x3s2_abl(int abl);
 int yolosod_debug_set_conv3x3_abl(int abl);
 void yolosod_debug_set_gemm_x2(int on);
 /* Test hook: the bf16 decomposed SwinBlock's depthwise conv + token layout and LN1 in one pass
- * (swin_tokens_ln_bf16_kernel, 1, default; env YOLOSOD_SWIN_TOKLN=0 turns it off) or as two kernels (0);
+ * (swin_tokens_ln_bf16_kernel, 1, default) or as two kernels (0);
  * bit-identical. Returns the previous state. */
 int yolosod_debug_set_swin_tokln(int on);
 /* Test hook: the fp16 two-term split of the fp32-accurate matrix kernels (common.h split2) on npair pairs of v:

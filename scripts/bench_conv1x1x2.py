@@ -1,6 +1,5 @@
 """Times the fp16-split 1x1 kernel (yolosod_conv1x1x2_silu) on the neck's n1 conv shapes of the n640 model at bs=32
-(MIOpen conv + HIP bias/SiLU beside it). GPU only; one line per distinct (shape, Cout). YOLOSOD_C1_NP picks the
-pixel-tile width (64 / 128) for the whole process."""
+(MIOpen conv + HIP bias/SiLU beside it). GPU only; one line per distinct (shape, Cout)."""
 import sys
 from pathlib import Path
 

@@ -1,5 +1,5 @@
 """A few launches of the P2 Detect tower conv (32 x 64 x 160 x 160 -> 64) on the stride-1 fp16-split kernel, for
-rocprofv3 --pmc passes (YOLOSOD_C3_PERSIST picks the form). GPU only."""
+rocprofv3 --pmc passes. GPU only."""
 import sys
 from pathlib import Path
 

@@ -60,7 +60,7 @@ def test_tower_convs_take_the_kernel(cuda, monkeypatch):
     from yolosod_amd.nn.tasks import build_model
     m = build_model("yolov12-sod-fusion-v5-simple.yaml", seed=0, device=cuda)
     x = torch.rand(2, 3, 256, 256, generator=torch.Generator().manual_seed(4)).to(cuda)
-    monkeypatch.setattr(M, "CONV3X3", "force")  # every tower conv, whatever its tile count
+    monkeypatch.setattr(M, "CONV3X3", "1")  # the tower convs on the fp16-split kernel (the default)
     monkeypatch.setattr(M, "S1_NECK", False)  # (the neck's Bottleneck convs: test_neck_c2f_convs_take_the_kernel)
     with torch.inference_mode():
         with _hip.op_timer() as t:

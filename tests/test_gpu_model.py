@@ -226,17 +226,15 @@ def test_executor_streams_and_concat_elision_are_bit_identical(gpu_model, cuda):
     from yolosod_amd.nn import tasks
     g = torch.Generator().manual_seed(5)
     x = torch.rand(4, 3, 320, 320, generator=g).to(cuda)
-    saved, saved_side, saved_split, saved_gf = tasks.STREAMS, tasks.SIDE_STREAMS, tasks.HEAD_SPLIT, tasks.GATE_FUSE
+    saved, saved_side, saved_gf = tasks.STREAMS, tasks.SIDE_STREAMS, tasks.GATE_FUSE
     det = torch.backends.cudnn.deterministic
     torch.backends.cudnn.deterministic = True
     try:
         with torch.inference_mode():
             tasks.GATE_FUSE = False  # the fused gate convs change the conv arithmetic (test_gate_fusion_...)
             tasks.STREAMS = 1
-            y_streams = gpu_model(x)[0].clone()  # towers dealt to SIDE_STREAMS (3) side streams, head split
+            y_streams = gpu_model(x)[0].clone()  # towers dealt to SIDE_STREAMS side streams
             assert gpu_model._last_elided == 6
-            tasks.HEAD_SPLIT = False
-            y_nosplit = gpu_model(x)[0].clone()  # one head launch after every tower
             tasks.SIDE_STREAMS = 1
             y_side1 = gpu_model(x)[0].clone()
             tasks.STREAMS = 0
@@ -247,10 +245,9 @@ def test_executor_streams_and_concat_elision_are_bit_identical(gpu_model, cuda):
             finally:
                 gpu_model._fused = True
     finally:
-        tasks.STREAMS, tasks.SIDE_STREAMS, tasks.HEAD_SPLIT, tasks.GATE_FUSE = saved, saved_side, saved_split, saved_gf
+        tasks.STREAMS, tasks.SIDE_STREAMS, tasks.GATE_FUSE = saved, saved_side, saved_gf
         torch.backends.cudnn.deterministic = det
     torch.cuda.synchronize()
-    assert torch.equal(y_streams, y_nosplit)
     assert torch.equal(y_streams, y_side1)
     assert torch.equal(y_streams, y_one)
     assert torch.equal(y_one, y_plain)

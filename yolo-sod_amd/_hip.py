@@ -94,9 +94,7 @@ SIGNATURES = {
     "yolosod_a2_forward_prepared": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp,
                                          _vp, _vp, _sz, _vp, _sz, _vp]),
     "yolosod_init": (_i, [_i]),
-    "yolosod_debug_set_swin_split": (_i, [_i]),
     "yolosod_debug_set_a2_fused": (_i, [_i]),
-    "yolosod_debug_set_a2_outup": (_i, [_i]),
     "yolosod_debug_set_a2_pool_wide": (_i, [_i]),
     "yolosod_debug_set_conv3x3_abl": (_i, [_i]),
     "yolosod_debug_set_conv3x3s2_abl": (_i, [_i]),
@@ -107,7 +105,6 @@ SIGNATURES = {
     "yolosod_conv3x3s2_silu": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _sz, _vp]),
     "yolosod_conv3x3s2_silu_out": (_i, [_vp, _vp, _l, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _sz, _vp]),
     "yolosod_debug_set_swin_tokln": (_i, [_i]),
-    "yolosod_debug_set_x3_swz": (_i, [_i]),
     "yolosod_debug_set_a2_pool_px": (_i, [_i]),
     "yolosod_mamba_glu_workspace": (_sz, [_i, _i, _i, _i, _i, _i]),
     "yolosod_mamba_glu_forward": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _f, _vp, _vp,

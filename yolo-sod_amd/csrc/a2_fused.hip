@@ -678,171 +678,6 @@ __global__ __launch_bounds__(512, 1) void a2_proj_pool_wide_kernel(const float* 
   if (prep_flag && range_flag && blockIdx.x == 0 && threadIdx.x == 0 && *prep_flag) *range_flag = 1u;
 }
 
-// ---- out-projection + bilinear upsample + SiLU + residual, one kernel --------------------------------------------
-// a2_attn.py:53-67: the MHA out-projection and the output 1x1 conv (BN folded) are consecutive linear maps, folded into
-// Wf = Wconv Wmha, bf (A2_Attn._fused_out); the bilinear upsample from (A, W) to (H, W) (align_corners=False: along H
-// only, identity along W) commutes with them, so y = x + SiLU(up_H(Wf O) + bf). One 256-thread workgroup per
-// (image, column tile of wc columns, 32 output channels) computes T = Wf[32 rows] O^T over the tile's A * wc tokens on
-// fp16-split MFMA (weights = the A operand, split on the fly from fp32 x 64; tokens = B, staged per 64-k stage as two
-// fp16 planes in LDS), keeps T [64][A][wc] in LDS and streams the tile's pixels of x -> y: T never reaches HBM (the
-// decomposed path wrote it and re-read it in a separate upsample pass). Wave w: row block w & 1, token blocks
-// w >> 1, (w >> 1) + 2, ... Small workgroups (>= 512 of them, two or three per CU) let one workgroup's streaming
-// epilogue overlap another's token GEMM, whose stages wait on L2 latency.
-constexpr int OU_KS = 64;          // k stage
-constexpr int OU_PS = OU_KS + 8;   // plane row stride (halves): 9 16-byte quads, conflict-free b128 reads
-template <int NTB>  // token blocks of 16 per workgroup (tokens = A * wc <= 16 NTB)
-__global__ __launch_bounds__(256, 3) void a2_out_up_kernel(const float* __restrict__ O, const float* __restrict__ wf,
-                                                           const float* __restrict__ bf, const float* __restrict__ x,
-                                                           float* __restrict__ y, int C, int H, int W, int A, int wc,
-                                                           unsigned* range_flag) {
-  constexpr int NT = 256;
-  constexpr int CB = 32;                       // output channels per workgroup
-  constexpr int NR = NTB * 16;                 // padded tokens
-  constexpr int PL = NR * OU_PS;               // plane (halves)
-  constexpr int STG_B = 2 * PL * 2;
-  constexpr int TS = NR + 4;                   // T tile row stride (floats; a multiple of 4: 16-byte row reads)
-  constexpr int T_B = CB * TS * 4;
-  constexpr int R_B = STG_B > T_B ? STG_B : T_B;
-  constexpr int TBW = (NTB + 1) / 2;           // token blocks per wave
-  constexpr int NIT = (NR * 16 + NT - 1) / NT; // staged float4 per thread per stage
-  static_assert(R_B <= 160 * 1024 / 3, "three workgroups per CU");
-  __shared__ __attribute__((aligned(16))) char smem[R_B];
-  h16_t* Pl = reinterpret_cast<h16_t*>(smem);  // [2 plane][NR][OU_PS]
-  float* Tt = reinterpret_cast<float*>(smem);  // [CB][TS] after the K loop
-
-  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int l15 = lane & 15, g = lane >> 4;
-  const int rb = wid & 1, th = wid >> 1;
-  const int ncb = C / CB, ntile = W / wc;
-  const int nblk = gridDim.x;
-  // XCD-aware: the channel blocks and column tiles of one image (which read the same tokens) run on one XCD
-  const int wgi = (nblk & 7) ? (int)blockIdx.x : (int)(blockIdx.x & 7) * (nblk >> 3) + (int)(blockIdx.x >> 3);
-  const int img = wgi / (ntile * ncb), rem = wgi - img * ntile * ncb;
-  const int tile = rem / ncb, co = (rem - tile * ncb) * CB;
-  const int w0 = tile * wc;
-  const int L = A * W, nt = A * wc;
-  float rng = 0.f;
-
-  // staged item e of a stage: token row e >> 4 (local token j = a * wc + wl), 4 k values at 4 (e & 15)
-  const float* rows[NIT];
-#pragma unroll
-  for (int i = 0; i < NIT; ++i) {
-    const int e = tid + NT * i;
-    int j = e >> 4;
-    j = j < nt ? j : nt - 1;  // padding rows read the last token (finite; their outputs are dropped)
-    const int a = j / wc, wl = j - a * wc;
-    rows[i] = O + ((long)img * L + a * W + w0 + wl) * C + 4 * (e & 15);
-  }
-  f32x4 stg[NIT];
-  auto load_stage = [&](int s) __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < NIT; ++i) stg[i] = *reinterpret_cast<const f32x4*>(rows[i] + OU_KS * s);
-  };
-  auto store_stage = [&]() __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < NIT; ++i) {
-      const int e = tid + NT * i;
-      if (e < NR * 16) {
-        uint2 hh, ll;
-        split4(stg[i], hh, ll);
-        rng = range_acc(rng, stg[i]);
-        h16_t* d = Pl + (e >> 4) * OU_PS + 4 * (e & 15);
-        *reinterpret_cast<uint2*>(d) = hh;
-        *reinterpret_cast<uint2*>(d + PL) = ll;
-      }
-    }
-  };
-  // weight fragment (A operand) of k step s32: Wf[co + 16 rb + l15][32 s32 + 8 g .. + 7] x 64, split
-  const float* wrow = wf + (long)(co + 16 * rb + l15) * C + 8 * g;
-  auto wfrag = [&](int s32, f16x8_t& wh, f16x8_t& wl) __attribute__((always_inline)) {
-    const f32x4 a = *reinterpret_cast<const f32x4*>(wrow + 32 * s32) * WSC;
-    const f32x4 b = *reinterpret_cast<const f32x4*>(wrow + 32 * s32 + 4) * WSC;
-    rng = range_acc(range_acc(rng, a), b);
-    split8(a, b, wh, wl);
-  };
-  f32x4 acc[TBW];
-#pragma unroll
-  for (int i = 0; i < TBW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int nstage = C / OU_KS;
-  load_stage(0);
-  for (int s = 0; s < nstage; ++s) {
-    __syncthreads();  // every wave is done with the previous stage's planes
-    store_stage();
-    __syncthreads();
-    if (s + 1 < nstage) load_stage(s + 1);  // in flight during this stage's products
-#pragma unroll
-    for (int u = 0; u < OU_KS / 32; ++u) {
-      f16x8_t wh, wl;
-      wfrag(2 * s + u, wh, wl);
-      const h16_t* b0 = Pl + l15 * OU_PS + 32 * u + 8 * g;
-#pragma unroll
-      for (int i = 0; i < TBW; ++i) {
-        const int tb = th + 2 * i;
-        if (tb < NTB) {
-          const f16x8_t xh = *reinterpret_cast<const f16x8_t*>(b0 + tb * 16 * OU_PS);
-          const f16x8_t xl = *reinterpret_cast<const f16x8_t*>(b0 + tb * 16 * OU_PS + PL);
-          acc[i] = mfma_f16x3(wh, wl, xh, xl, acc[i]);
-        }
-      }
-    }
-  }
-  __syncthreads();  // the planes are free: the T tile takes the region
-  // lane (g, l15) of token block tb: T[channel 16 rb + 4 g + r][token tb * 16 + l15]
-#pragma unroll
-  for (int i = 0; i < TBW; ++i) {
-    const int tb = th + 2 * i;
-    if (tb < NTB) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) Tt[(16 * rb + 4 * g + r) * TS + tb * 16 + l15] = acc[i][r] * (1.0f / WSC);
-    }
-  }
-  __syncthreads();
-  // pixel rows of the tile: thread -> (channel c, row h), its wc / 4 column quads in chunks of 5 loads in flight; the
-  // interpolation weights, bias and T rows are per row. Offsets are 32-bit from the channel block's base (the launcher
-  // checks 64 * H * W < 2^29)
-  const int nq = wc >> 2, nrow = CB * H;
-  const float sc = (float)A / (float)H, r_h = 1.0f / (float)H;
-  const int HW = H * W;
-  const float* xb = x + ((long)img * C + co) * HW + w0;
-  float* yb = y + ((long)img * C + co) * HW + w0;
-  for (int row = tid; row < nrow; row += NT) {
-    int c = (int)((float)row * r_h);  // row / H: fp32 estimate + one correction each way (exact, row < 2^22)
-    c -= (c * H > row) ? 1 : 0;
-    c += ((c + 1) * H <= row) ? 1 : 0;
-    const int h = row - c * H;
-    float src = sc * ((float)h + 0.5f) - 0.5f;
-    if (src < 0.f) src = 0.f;
-    const int y0 = (int)src;
-    const int y1 = y0 + ((y0 < A - 1) ? 1 : 0);
-    const float l1 = src - (float)y0, l0 = 1.0f - l1;
-    const float b = bf[co + c];
-    const float* t0 = Tt + c * TS + y0 * wc;
-    const float* t1 = Tt + c * TS + y1 * wc;
-    const int off = c * HW + h * W;
-    for (int q0 = 0; q0 < nq; q0 += 5) {
-      f32x4 xv[5];
-#pragma unroll
-      for (int k = 0; k < 5; ++k) {
-        const int q = q0 + k < nq ? q0 + k : nq - 1;  // clamped (unconditional) loads; only q < nq is stored
-        xv[k] = *reinterpret_cast<const f32x4*>(xb + off + 4 * q);
-      }
-#pragma unroll
-      for (int k = 0; k < 5; ++k) {
-        const int q = q0 + k;
-        if (q < nq) {
-          const f32x4 u0 = *reinterpret_cast<const f32x4*>(t0 + 4 * q);
-          const f32x4 u1 = *reinterpret_cast<const f32x4*>(t1 + 4 * q);
-          f32x4 r;
-#pragma unroll
-          for (int j2 = 0; j2 < 4; ++j2) r[j2] = xv[k][j2] + silu_fast_(l0 * u0[j2] + l1 * u1[j2] + b);
-          *reinterpret_cast<f32x4*>(yb + off + 4 * q) = r;
-        }
-      }
-    }
-  }
-  range_report(range_flag, rng);
-}
-
 // Weight preparation, one wave per output row: rows [0, 3C) = in_proj with the LN affine folded (W' = W diag(gamma),
 // b' = b + W beta), rows [3C, 4C) = the proj 1x1 conv (BN folded by the caller); both split into fp16 planes (x64,
 // fragment-major: element (n, k) of [N][C] at ((n/16 * C/32 + k/32) * 64 + (k%32)/8 * 16 + n%16) * 8 + k%8)
@@ -887,15 +722,9 @@ __global__ __launch_bounds__(256) void a2_prep_kernel(const float* __restrict__ 
 
 using namespace ys;
 
-// the fused kernels (default; YOLOSOD_A2_FUSED=0 runs the decomposed GEMM path on the same split products)
-static int g_a2_fused = -1;
-static bool a2_fused_env() {
-  if (g_a2_fused < 0) {
-    const char* e = getenv("YOLOSOD_A2_FUSED");
-    g_a2_fused = (e && e[0] == '0') ? 0 : 1;
-  }
-  return g_a2_fused != 0;
-}
+// the fused kernels (default; the test hook below runs the decomposed GEMM path on the same split products)
+static int g_a2_fused = 1;
+static bool a2_fused_env() { return g_a2_fused != 0; }
 // Test hook: A2 through the fused kernels (1) or the decomposed path (0); returns the previous state.
 YS_EXPORT int yolosod_debug_set_a2_fused(int on) {
   const int prev = a2_fused_env() ? 1 : 0;
@@ -950,15 +779,8 @@ int yolosod_a2_fused_prepare(int C, const float* proj_w, const float* ln_w, cons
 
 // Area groups of the proj + SiLU + pooling kernel: the fewest groups whose row bands fit `cap` pixels (0: none fit).
 // Groups > 1 need W % 4 == 0 (16-byte aligned band starts).
-static int g_a2_pool_cap = -1;  // pixels per group the launcher aims for (YOLOSOD_A2_POOL_PX; 208: 2 workgroups / CU)
-static int a2_pool_cap() {
-  if (g_a2_pool_cap < 0) {
-    const char* e = getenv("YOLOSOD_A2_POOL_PX");
-    g_a2_pool_cap = e ? atoi(e) : 208;
-    if (g_a2_pool_cap <= 0 || g_a2_pool_cap > a2f::PMAXHW) g_a2_pool_cap = a2f::PMAXHW;
-  }
-  return g_a2_pool_cap;
-}
+static int g_a2_pool_cap = 208;  // pixels per group the launcher aims for (208: 2 workgroups / CU)
+static int a2_pool_cap() { return g_a2_pool_cap; }
 static int a2_pool_groups(int H, int W, int A, int cap, int* max_px) {
   for (int G = 1; G <= A; ++G) {
     if (G > 1 && W % 4 != 0) break;
@@ -989,17 +811,11 @@ bool yolosod_a2_proj_pool_ok(int C, int H, int W, int A) {
          (a2_pool_groups(H, W, A, a2_pool_cap(), nullptr) > 0 || a2_pool_groups(H, W, A, a2f::PMAXHW, nullptr) > 0);
 }
 
-// The wide proj / pool kernel (default; YOLOSOD_A2_POOL_WIDE=0 keeps the 64-channel one): its (column blocks, row
+// The wide proj / pool kernel (default; the test hook keeps the 64-channel one): its (column blocks, row
 // blocks per workgroup) instances and the configuration for a shape - the first instance whose area groups fit and
 // that gives >= 256 workgroups, else the one with the most workgroups (0: none fits).
-static int g_a2_pool_wide = -1;
-static bool a2_pool_wide_env() {
-  if (g_a2_pool_wide < 0) {
-    const char* e = getenv("YOLOSOD_A2_POOL_WIDE");
-    g_a2_pool_wide = (e && e[0] == '0') ? 0 : 1;
-  }
-  return g_a2_pool_wide != 0;
-}
+static int g_a2_pool_wide = 1;
+static bool a2_pool_wide_env() { return g_a2_pool_wide != 0; }
 // Test hook: the wide proj / pool kernel on (1) or off (0); returns the previous state.
 YS_EXPORT int yolosod_debug_set_a2_pool_wide(int on) {
   const int prev = a2_pool_wide_env() ? 1 : 0;
@@ -1067,62 +883,6 @@ int yolosod_a2_proj_pool_run(const float* x, const float* proj_b, float* S, int 
 #undef YS_A2P
   YS_CHECK_ARG(false, "a2: %dx%d pixels too many for the proj/pool kernel", H, W);
   return -1;
-}
-
-// the fused out-projection + upsample kernel (opt-in, YOLOSOD_A2_OUTUP=1; measured level with the token GEMM + upsample
-// pass at n640 and slower at n1280: its token GEMM re-stages the attention output per 32-channel block and waits on L2
-// every stage)
-static int g_a2_outup = -1;
-static bool a2_outup_env() {
-  if (g_a2_outup < 0) {
-    const char* e = getenv("YOLOSOD_A2_OUTUP");
-    g_a2_outup = (e && e[0] == '1') ? 1 : 0;
-  }
-  return g_a2_outup != 0;
-}
-// Test hook: the fused out-projection + upsample kernel on (1) or off (0); returns the previous state.
-YS_EXPORT int yolosod_debug_set_a2_outup(int on) {
-  const int prev = a2_outup_env() ? 1 : 0;
-  g_a2_outup = on ? 1 : 0;
-  return prev;
-}
-// Column tile of the out / upsample kernel: W itself or a divisor of W that is a multiple of 4 (16-byte pixel quads),
-// with A * wc <= 160 tokens; the widest one that still gives >= 512 workgroups (0: the shape is not fused).
-static int a2_outup_wc(int B, int C, int W, int A) {
-  int best = 0;
-  for (int wc = W; wc >= 4; --wc) {
-    if (W % wc || wc % 4 || A * wc > 160) continue;
-    best = wc;
-    if ((long)B * (C / 32) * (W / wc) >= 512) return wc;
-  }
-  return best;
-}
-bool yolosod_a2_out_up_ok(int B, int C, int H, int W, int A) {
-  return a2_outup_env() && C % 32 == 0 && C <= 1024 && A > 0 && H > 0 && a2_outup_wc(B, C, W, A) > 0;
-}
-// O ([B*L][C], L = A*W) -> y = x + SiLU(up_H(Wf O) + bf). x / y 16-byte aligned. Returns < 0 on error.
-int yolosod_a2_out_up_run(const float* O, const float* wf, const float* bf, const float* x, float* y, int B, int C,
-                          int H, int W, int A, hipStream_t st) {
-  YS_CHECK_ARG(yolosod_a2_out_up_ok(B, C, H, W, A), "a2: out/upsample shape C=%d %dx%d A=%d not fused", C, H, W, A);
-  YS_CHECK_ARG(((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0 && ((uintptr_t)O & 15) == 0 &&
-                   ((uintptr_t)wf & 15) == 0,
-               "a2: out/upsample operands must be 16-byte aligned");
-  const int wc = a2_outup_wc(B, C, W, A);
-  const long nwg = (long)B * (C / 32) * (W / wc);
-  YS_CHECK_ARG(nwg < (1L << 31) && 64L * H * W < (1L << 29), "a2: out/upsample grid too large");
-  const int ntb = (A * wc + 15) / 16;
-#define YS_A2OU(N)                                                                                             \
-  case N:                                                                                                      \
-    hipLaunchKernelGGL((a2f::a2_out_up_kernel<N>), dim3((unsigned)nwg), dim3(256), 0, st, O, wf, bf, x, y, C, \
-                       H, W, A, wc, range_flag_dev());                                                         \
-    break;
-  switch (ntb) {
-    YS_A2OU(1) YS_A2OU(2) YS_A2OU(3) YS_A2OU(4) YS_A2OU(5) YS_A2OU(6) YS_A2OU(7) YS_A2OU(8) YS_A2OU(9) YS_A2OU(10)
-    default: YS_CHECK_ARG(false, "a2: %d tokens per tile unsupported", A * wc);
-  }
-#undef YS_A2OU
-  YS_CHECK_LAUNCH("a2_out_up");
-  return 0;
 }
 
 // LN -> QKV -> attention of all (image, head) pairs: S / stats -> O ([B*L][C]). Returns < 0 on error.

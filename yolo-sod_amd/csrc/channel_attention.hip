@@ -12,10 +12,10 @@
 // first channel slab prefetched across the conv - measured slower on MI355X: L4 0.186 vs 0.132 ms, L18 0.080 vs
 // 0.053: far fewer workgroups stream the tensor, and the per-workgroup halo combine over the channel groups
 // re-reads the partial maps; it was removed.)
-// Optionally (YOLOSOD_MALL_CHUNK_MB > 0) the host driver walks the batch in image chunks sized to stay resident
-// in the 256 MiB Infinity Cache between the passes. Measured on MI355X at the bs=32 640x640 shapes, the apply
-// pass' re-read does hit on-die (7.3 TB/s) but the extra launch boundaries and the smaller grids cost more
-// (SE L1 0.269 vs 0.243 ms, CBAM L4 0.199 vs 0.163, CA L32 0.090 vs 0.073), so the default is one chunk.
+// (Walking the batch in image chunks sized to stay resident in the 256 MiB Infinity Cache between the passes was
+// measured on MI355X at the bs=32 640x640 shapes: the apply pass' re-read does hit on-die (7.3 TB/s) but the extra
+// launch boundaries and the smaller grids cost more - SE L1 0.269 vs 0.243 ms, CBAM L4 0.199 vs 0.163, CA L32 0.090
+// vs 0.073 - so every pass covers the whole batch.)
 //
 // Reference semantics (file:line in quitedob/yolo-sod):
 //   SE     ultralytics/nn/modules/smallobj_modules.py:84-92  (x * sigmoid(fc2(relu(fc1(mean_hw x)))))
@@ -26,30 +26,6 @@
 #include <math.h>
 
 namespace ys {
-
-static size_t mall_chunk_bytes() {
-  static size_t v = [] {
-    const char* e = getenv("YOLOSOD_MALL_CHUNK_MB");
-    long mb = e ? atol(e) : 0;
-    return (size_t)(mb < 0 ? 0 : mb) << 20;
-  }();
-  return v;
-}
-
-static int images_per_chunk(int B, size_t bytes_per_image) {
-  size_t cap = mall_chunk_bytes();
-  if (cap == 0 || bytes_per_image == 0) return B;
-  size_t n = cap / bytes_per_image;
-  if (n < 1) n = 1;
-  if ((int)n > B) n = B;
-  return (int)n;
-}
-
-// fused gate-in-apply kernels (default on; YOLOSOD_FUSED_GATES=0 restores the split launches for A/B)
-static bool fused_gates() {
-  static const bool on = [] { const char* e = getenv("YOLOSOD_FUSED_GATES"); return !e || atoi(e) != 0; }();
-  return on;
-}
 
 constexpr int kMaxParts = 64;
 
@@ -375,63 +351,6 @@ __global__ __launch_bounds__(256) void cbam_pixel_stats_kernel(const T* __restri
   }
 }
 
-// CBAM pass 2, wave-split form (V = 4 with the fused gate; opt-in, YOLOSOD_CBAM_PS2=1; measured no faster): a
-// workgroup takes 256 pixels of one 32-channel group; wave w takes channels c0 + 8w .. +8 of the group, each lane 4
-// pixels. A lane issues all 8 of its 16-byte loads before the channel gate is computed, so the HBM stream overlaps the
-// gate's latency chain (the form above keeps 32 channels per lane, 8 of them in flight across the gate, and at
-// HW = 1600 leaves 44 % of its second pixel block idle); the 4 waves' partial sum / max meet in LDS in wave order
-// (fixed: batch-invariant). grid = (ceil(HW / 256), G, images); dynamic LDS = (3*C + 128 + 2048) floats.
-template <class T>
-__global__ __launch_bounds__(256) void cbam_pixel_stats_ws_kernel(const T* __restrict__ x, float* __restrict__ ca,
-                                                                  int C, int CG, long HW, float* __restrict__ mpart,
-                                                                  const float* __restrict__ psum,
-                                                                  const float* __restrict__ pmax, int parts,
-                                                                  float inv_hw, const float* __restrict__ w1,
-                                                                  const float* __restrict__ w2, int hid) {
-  extern __shared__ float sh[];  // avg[C] | mx[C] | hsh[128] | gate[C] | red[2][4][256]
-  const int b = blockIdx.z, g = blockIdx.y, G = gridDim.y;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int c0 = g * CG;
-  const int c1 = (c0 + CG < C) ? c0 + CG : C;
-  const int cw0 = c0 + 8 * wv;
-  const int nw = (c1 - cw0 < 8) ? (c1 - cw0 > 0 ? c1 - cw0 : 0) : 8;  // this wave's channels [cw0, cw0 + nw)
-  const long p = ((long)blockIdx.x * 64 + lane) * 4;
-  const bool pv = p < HW;
-  f32x4 v[8];
-#pragma unroll
-  for (int u = 0; u < 8; ++u)
-    v[u] = (pv && u < nw) ? ld4(x + ((long)b * C + cw0 + u) * HW + p) : f32x4{0.f, 0.f, 0.f, 0.f};
-  float* gs = sh + 2 * C + 128;
-  gate_mlp<true>(psum, pmax, parts, C, inv_hw, w1, nullptr, w2, nullptr, hid, b, sh, sh + C, sh + 2 * C, c0, c1 - c0,
-                 gs);
-  if (blockIdx.x == 0)
-    for (int i = tid; i < c1 - c0; i += 256) ca[(long)b * C + c0 + i] = gs[i];
-  f32x4 s = {0.f, 0.f, 0.f, 0.f}, m = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-#pragma unroll
-  for (int u = 0; u < 8; ++u)
-    if (u < nw) {
-      const f32x4 o = gs[8 * wv + u] * v[u];
-      s += o;
-      m.x = fmaxf(m.x, o.x); m.y = fmaxf(m.y, o.y); m.z = fmaxf(m.z, o.z); m.w = fmaxf(m.w, o.w);
-    }
-  float* red = gs + C;
-  *reinterpret_cast<f32x4*>(red + wv * 256 + 4 * lane) = s;
-  *reinterpret_cast<f32x4*>(red + 1024 + wv * 256 + 4 * lane) = m;
-  __syncthreads();
-  const long px = (long)blockIdx.x * 256 + tid;
-  if (px < HW) {
-    float ss = red[tid], mm = red[1024 + tid];
-#pragma unroll
-    for (int w = 1; w < 4; ++w) {
-      ss += red[w * 256 + tid];
-      mm = fmaxf(mm, red[1024 + w * 256 + tid]);
-    }
-    float* sp = mpart + ((long)(b * G + g) * 2) * HW;
-    sp[px] = ss;
-    sp[HW + px] = mm;
-  }
-}
-
 // mean / max over the channel groups of pixel (yy, xx), zero outside the image (conv2d's zero padding of the
 // [mean; max] map, cbam_block.py:33-37)
 __device__ __forceinline__ float2 cbam_map_at(const float* __restrict__ mp, int G, long HW, int H, int W, int yy,
@@ -581,81 +500,6 @@ __global__ __launch_bounds__(256) void cbam_apply_kernel(const T* __restrict__ x
   }
 }
 
-// CBAM pass 3 with the spatial gate folded in (opt-in, YOLOSOD_CBAM_SA_APPLY=1; slower, see cbam_forward_impl): the
-// workgroup takes the same 256*V-pixel run as cbam_apply_kernel and kCbamApplyCh channels; it first combines the G group maps of the rows its run touches
-// (+/- 3 halo rows, 3 zero columns each side) into LDS, evaluates sa = sigmoid(conv7x7) for its own pixels (the
-// cbam_sa_kernel sums, same order: bit-identical), then streams its channels. One launch and one HBM round trip of
-// the sa map less than the split path; the conv is recomputed by the C / kCbamApplyCh channel blocks of a run.
-// grid = (ceil(HW / (256*V)), ceil(C / kCbamApplyCh), images); dynamic LDS = 2 * cbam_sa_rows(W, V) * (W + 6) floats.
-constexpr int kCbamApplyCh = 32;
-
-__host__ __device__ inline int cbam_sa_rows(int W, int V) { return (256 * V + W - 1) / W + 1 + 6; }
-
-template <int V, class T>
-__global__ __launch_bounds__(256) void cbam_sa_apply_kernel(const T* __restrict__ x, T* __restrict__ y,
-                                                            const float* __restrict__ ca,
-                                                            const float* __restrict__ mpart, int G, int C, int H,
-                                                            int W, const float* __restrict__ wsa) {
-  extern __shared__ float mm[];  // [2][nr][W + 6]
-  __shared__ float wk[98];
-  const int b = blockIdx.z, tid = threadIdx.x;
-  const long HW = (long)H * W;
-  const long pr0 = (long)blockIdx.x * 256 * V;
-  const long pr1 = (pr0 + 256 * V < HW) ? pr0 + 256 * V : HW;
-  const int yf = (int)(pr0 / W), yl = (int)((pr1 - 1) / W);
-  const int r0 = yf - 3, nr = yl - yf + 7, WP = W + 6;
-  if (tid < 98) wk[tid] = wsa[tid];
-  const float invC = 1.0f / (float)C;
-  const float* mp = mpart + (long)b * G * 2 * HW;
-  for (int i = tid; i < nr * WP; i += 256) {
-    const int ry = i / WP, rx = i - ry * WP;
-    const float2 v = cbam_map_at(mp, G, HW, H, W, r0 + ry, rx - 3, invC);
-    mm[i] = v.x;
-    mm[nr * WP + i] = v.y;
-  }
-  __syncthreads();
-  const long p = pr0 + (long)tid * V;
-  if (p >= HW) return;
-  float sv[V];
-#pragma unroll
-  for (int v = 0; v < V; ++v) {
-    const int py = (int)((p + v) / W), px = (int)((p + v) - (long)py * W);
-    const float* m0 = mm + (py - yf) * WP + px;
-    float z = 0.f;
-#pragma unroll
-    for (int ci = 0; ci < 2; ++ci)
-#pragma unroll
-      for (int ky = 0; ky < 7; ++ky)
-#pragma unroll
-        for (int kx = 0; kx < 7; ++kx) z += wk[ci * 49 + ky * 7 + kx] * m0[ci * nr * WP + ky * WP + kx];
-    sv[v] = sigmoidf_(z);
-  }
-  const int c0 = blockIdx.y * kCbamApplyCh;
-  const int n = (C - c0 < kCbamApplyCh) ? C - c0 : kCbamApplyCh;
-  const T* xb = x + ((long)b * C + c0) * HW + p;
-  T* yb = y + ((long)b * C + c0) * HW + p;
-  const float* cab = ca + (long)b * C + c0;
-  if (V == 4) {
-    const f32x4 s4 = {sv[0], sv[V > 1 ? 1 : 0], sv[V > 2 ? 2 : 0], sv[V > 3 ? 3 : 0]};
-    int u0 = 0;
-    for (; u0 + 8 <= n; u0 += 8) {
-      f32x4 v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = ld4(xb + (long)(u0 + u) * HW);
-#pragma unroll
-      for (int u = 0; u < 8; ++u) st4(yb + (long)(u0 + u) * HW, s4 * (cab[u0 + u] * v[u]));
-    }
-    for (; u0 < n; ++u0) st4(yb + (long)u0 * HW, s4 * (cab[u0] * ld4(xb + (long)u0 * HW)));
-  } else {
-    for (int u = 0; u < n; ++u) st1(yb + (long)u * HW, sv[0] * (cab[u] * ld1(xb + (long)u * HW)));
-  }
-}
-
-// ------------------------------------------------------------------------------------------------
-// CA pass 1: row means (over W) and column means (over H) of each (b,c) plane -> yin[b][c][0..H+W).
-// One workgroup per plane; the plane streams through LDS in bands of <= 8192 floats (vector loads when W % 4
-// == 0), rows reduced by lane quads, columns accumulated in registers (W <= 1024).
-// ------------------------------------------------------------------------------------------------
 template <class T>
 __global__ __launch_bounds__(256) void ca_pool_kernel(const T* __restrict__ x, int H, int W, int RB,
                                                       float* __restrict__ yin) {
@@ -826,48 +670,6 @@ __global__ __launch_bounds__(256) void ca_apply_kernel(const T* __restrict__ x, 
   }
 }
 
-// CA pass 3, one workgroup per fp32 plane (W % 4 == 0; opt-in, YOLOSOD_CA_APPLY2=1, see ca_forward_impl): the
-// plane's gate row [a_h | a_w] is staged in LDS and the plane streams in 16-byte accesses, each thread's (up to 8 per
-// round) loads issued before the first is used; the form above keeps one load in flight per thread and ran at
-// ~3.9 TB/s on the n640 plane (80 x 80). Same expression: (x * a_w[w]) * a_h[h]. dynamic LDS = (H + W) floats.
-__global__ __launch_bounds__(256) void ca_apply_plane_kernel(const float* __restrict__ x, float* __restrict__ y,
-                                                             const float* __restrict__ gate, int H, int W) {
-  extern __shared__ float gsh[];
-  const long plane = blockIdx.x;
-  const long HW = (long)H * W;
-  const int L = H + W, tid = threadIdx.x;
-  const float* g = gate + plane * L;
-  const float* xp = x + plane * HW;
-  float* yp = y + plane * HW;
-  const long n4 = HW >> 2;
-  for (int i = tid; i < L; i += 256) gsh[i] = g[i];
-  for (long i0 = 0; i0 < n4; i0 += 8 * 256) {
-    f32x4 v[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const long i = i0 + tid + 256 * u;
-      if (i < n4) v[u] = ld4(xp + 4 * i);
-    }
-    if (i0 == 0) __syncthreads();  // the gate row is staged (the plane's first loads are already in flight)
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const long i = i0 + tid + 256 * u;
-      if (i < n4) {
-        const long e = 4 * i;
-        const int h = (int)(e / W), w = (int)(e - (long)h * W);
-        const float ah = gsh[h];
-        const float* aw = gsh + H + w;
-        f32x4 o;
-        o.x = (v[u].x * aw[0]) * ah;
-        o.y = (v[u].y * aw[1]) * ah;
-        o.z = (v[u].z * aw[2]) * ah;
-        o.w = (v[u].w * aw[3]) * ah;
-        st4(yp + e, o);
-      }
-    }
-  }
-}
-
 }  // namespace ys
 
 using namespace ys;
@@ -906,39 +708,32 @@ static int se_forward_impl(const T* x, T* y, int B, int C, int H, int W, const f
   YS_CHECK_ARG(gate, "se: workspace too small (%zu)", workspace_bytes);
   hipStream_t st = (hipStream_t)stream;
   const long HW = (long)H * W;
-  const int ipc = images_per_chunk(B, (size_t)C * HW * sizeof(T));
   const PartPlan pp = part_plan(HW);
   const long xchunks = (HW % 4 == 0) ? (HW + 1023) / 1024 : (HW + 255) / 256;
   const size_t lds = sizeof(float) * (3 * (size_t)C + 128);
   const size_t lds_fused = sizeof(float) * (2 * (size_t)C + 136);
   // gate MLP fused into the apply pass for small planes; a separate gate launch for large ones, where the fused
   // form's per-workgroup MLP (12800 workgroups at 32x32x320x320) cost more than the launch: SE L1 0.158 -> 0.150 ms,
-  // L23 0.038 fused vs 0.040 split (same box, profiles/r04_se/); YOLOSOD_SE_FUSED_MAXHW overrides the bound
-  static const long fused_max_hw = [] { const char* e = getenv("YOLOSOD_SE_FUSED_MAXHW"); return e ? atol(e) : 65536L; }();
-  const bool fused = y && fused_gates() && lds_fused <= 64 * 1024 && (HW < fused_max_hw || lds > 64 * 1024);
+  // L23 0.038 fused vs 0.040 split (same box, profiles/r04_se/)
+  constexpr long fused_max_hw = 65536;
+  const bool fused = y && lds_fused <= 64 * 1024 && (HW < fused_max_hw || lds > 64 * 1024);
   YS_CHECK_ARG(lds <= 64 * 1024 || fused, "se: C=%d too large for the gate kernel", C);
   if (!y) gate = gate_out;
-  // the fused apply's 8 loads per lane issued before the gate MLP (YOLOSOD_SE_PRE=0: after it)
-  static const int se_pre = [] { const char* e = getenv("YOLOSOD_SE_PRE"); return (!e || atoi(e) != 0) ? 1 : 0; }();
-  for (int b0 = 0; b0 < B; b0 += ipc) {
-    const int nb = (B - b0 < ipc) ? B - b0 : ipc;
-    const long off = (long)b0 * C * HW;
-    const float* ps = (psum_pre ? psum_pre : psum) + (long)b0 * C * pp.parts;
-    if (!psum_pre)
-      hipLaunchKernelGGL((plane_part_stats_kernel<false, T>), dim3((unsigned)(nb * C * pp.parts)), dim3(256), 0, st,
-                         x + off, HW, pp.parts, pp.seg, psum + (long)b0 * C * pp.parts, nullptr);
-    const dim3 grid((unsigned)xchunks, (unsigned)((C + 7) / 8), (unsigned)nb);
-    if (fused) {
-      hipLaunchKernelGGL((plane_scale_kernel<T, true>), grid, dim3(256), lds_fused, st, x + off, y + off, nullptr, C, HW,
-                         mall_reverse(), se_pre, ps, pp.parts, 1.0f / (float)HW, fc1_w, fc1_b, fc2_w, fc2_b, hidden);
-    } else {
-      hipLaunchKernelGGL((channel_gate_kernel<false>), dim3(nb), dim3(256), lds, st, ps, nullptr, pp.parts, C,
-                         1.0f / (float)HW, fc1_w, fc1_b, fc2_w, fc2_b, hidden, gate + (long)b0 * C);
-      if (y)
-        hipLaunchKernelGGL((plane_scale_kernel<T, false>), grid, dim3(256), 0, st, x + off, y + off,
-                           gate + (long)b0 * C, C, HW, mall_reverse(), 0, nullptr, 0, 0.f, nullptr, nullptr, nullptr,
-                           nullptr, 0);
-    }
+  // the fused apply issues its 8 loads per lane before the gate MLP (pre = 1)
+  const float* ps = psum_pre ? psum_pre : psum;
+  if (!psum_pre)
+    hipLaunchKernelGGL((plane_part_stats_kernel<false, T>), dim3((unsigned)(B * C * pp.parts)), dim3(256), 0, st, x,
+                       HW, pp.parts, pp.seg, psum, nullptr);
+  const dim3 grid((unsigned)xchunks, (unsigned)((C + 7) / 8), (unsigned)B);
+  if (fused) {
+    hipLaunchKernelGGL((plane_scale_kernel<T, true>), grid, dim3(256), lds_fused, st, x, y, nullptr, C, HW,
+                       mall_reverse(), 1, ps, pp.parts, 1.0f / (float)HW, fc1_w, fc1_b, fc2_w, fc2_b, hidden);
+  } else {
+    hipLaunchKernelGGL((channel_gate_kernel<false>), dim3(B), dim3(256), lds, st, ps, nullptr, pp.parts, C,
+                       1.0f / (float)HW, fc1_w, fc1_b, fc2_w, fc2_b, hidden, gate);
+    if (y)
+      hipLaunchKernelGGL((plane_scale_kernel<T, false>), grid, dim3(256), 0, st, x, y, gate, C, HW, mall_reverse(), 0,
+                         nullptr, 0, 0.f, nullptr, nullptr, nullptr, nullptr, 0);
   }
   YS_CHECK_LAUNCH("se");
   return 0;
@@ -986,13 +781,12 @@ constexpr int kCbamGroup = 32;
 
 YS_EXPORT size_t yolosod_cbam_workspace(int B, int C, int H, int W) {
   const long HW = (long)H * W;
-  const int ipc = B > 0 ? images_per_chunk(B, (size_t)C * HW * sizeof(float)) : 1;
   const int G = (C + kCbamGroup - 1) / kCbamGroup;
   Sizer s;
   s.take<float>((size_t)B * C * part_plan((long)H * W).parts);  // partial sums
   s.take<float>((size_t)B * C * part_plan((long)H * W).parts);  // partial maxes
   s.take<float>((size_t)B * C);              // ca
-  s.take<float>((size_t)ipc * G * 2 * HW);   // per-group [sum;max] maps of one chunk
+  s.take<float>((size_t)B * G * 2 * HW);     // per-group [sum;max] maps
   s.take<float>((size_t)B * HW);             // sa
   return s.off;
 }
@@ -1010,13 +804,12 @@ static int cbam_forward_impl(const T* x, T* y, int B, int C, int H, int W, const
   const long HW = (long)H * W;
   const int V = (HW % 4 == 0) ? 4 : 1;
   const long pxb = (HW + 256 * V - 1) / (256 * V);
-  const int ipc = images_per_chunk(B, (size_t)C * HW * sizeof(T));
   const int G = (C + kCbamGroup - 1) / kCbamGroup;
   Carver cv(workspace, workspace_bytes);
   float* psum = cv.take<float>((size_t)B * C * part_plan((long)H * W).parts);
   float* pmax = cv.take<float>((size_t)B * C * part_plan((long)H * W).parts);
   float* ca = cv.take<float>((size_t)B * C);
-  float* mpart = cv.take<float>((size_t)ipc * G * 2 * HW);
+  float* mpart = cv.take<float>((size_t)B * G * 2 * HW);
   float* sa = cv.take<float>((size_t)B * HW);
   YS_CHECK_ARG(sa, "cbam: workspace too small (%zu)", workspace_bytes);
   if (!y) {
@@ -1027,62 +820,39 @@ static int cbam_forward_impl(const T* x, T* y, int B, int C, int H, int W, const
   const PartPlan pp = part_plan(HW);
   const size_t lds = sizeof(float) * (3 * (size_t)C + 128);
   // fused launch: channel gate + pixel statistics
-  const bool fused = fused_gates() && V == 4 && lds <= 64 * 1024;
+  const bool fused = V == 4 && lds <= 64 * 1024;
   YS_CHECK_ARG(lds <= 64 * 1024, "cbam: C=%d too large for the gate kernel", C);
-  // spatial gate folded into the apply pass: opt-in (YOLOSOD_CBAM_SA_APPLY=1), measured slower at both CBAM shapes
-  // (L4 0.134 -> 0.187 ms, L18 0.043 -> 0.058 ms same-box: the per-run map staging and the 7x7 conv, recomputed by
-  // every channel block, cost more than the sa launch they replace)
-  static const bool sa_apply = [] { const char* e = getenv("YOLOSOD_CBAM_SA_APPLY"); return e && atoi(e) != 0; }();
-  const size_t sa_lds = sa_apply ? sizeof(float) * 2 * (size_t)cbam_sa_rows(W, V) * (W + 6) : SIZE_MAX;
-  // 8 channels per wave (opt-in, YOLOSOD_CBAM_PS2=1): measured level at L18 and 3 % slower at L4 in the model
-  static const bool ps2 = [] { const char* e = getenv("YOLOSOD_CBAM_PS2"); return e && atoi(e) != 0; }();
-  for (int b0 = 0; b0 < B; b0 += ipc) {
-    const int nb = (B - b0 < ipc) ? B - b0 : ipc;
-    const long off = (long)b0 * C * HW;
-    const float* ps = (psum_pre ? psum_pre : psum) + (long)b0 * C * pp.parts;
-    const float* pm = (pmax_pre ? pmax_pre : pmax) + (long)b0 * C * pp.parts;
-    float* cab = ca + (long)b0 * C;
-    float* sab = sa + (long)b0 * HW;
-    if (!psum_pre)
-      hipLaunchKernelGGL((plane_part_stats_kernel<true, T>), dim3((unsigned)(nb * C * pp.parts)), dim3(256), 0, st,
-                         x + off, HW, pp.parts, pp.seg, psum + (long)b0 * C * pp.parts, pmax + (long)b0 * C * pp.parts);
-    dim3 gs((unsigned)pxb, G, nb);
-    if (fused && ps2) {  // channel gate inside the pixel-statistics workgroups, 8 channels per wave
-      const size_t lds2 = sizeof(float) * (3 * (size_t)C + 128 + 2048);
-      hipLaunchKernelGGL((cbam_pixel_stats_ws_kernel<T>), dim3((unsigned)((HW + 255) / 256), G, nb), dim3(256), lds2,
-                         st, x + off, cab, C, kCbamGroup, HW, mpart, ps, pm, pp.parts, 1.0f / (float)HW, fc0_w, fc2_w,
-                         hidden);
-    } else if (fused) {  // channel gate computed inside the pixel-statistics workgroups
-      hipLaunchKernelGGL((cbam_pixel_stats_kernel<4, T, true>), gs, dim3(256), lds, st, x + off, cab, C, kCbamGroup,
-                         HW, mpart, ps, pm, pp.parts, 1.0f / (float)HW, fc0_w, fc2_w, hidden);
-    } else {
-      hipLaunchKernelGGL((channel_gate_kernel<true>), dim3(nb), dim3(256), lds, st, ps, pm, pp.parts, C,
-                         1.0f / (float)HW, fc0_w, nullptr, fc2_w, nullptr, hidden, cab);
-      if (V == 4)
-        hipLaunchKernelGGL((cbam_pixel_stats_kernel<4, T, false>), gs, dim3(256), 0, st, x + off, cab, C, kCbamGroup,
-                           HW, mpart, nullptr, nullptr, 0, 0.f, nullptr, nullptr, 0);
-      else
-        hipLaunchKernelGGL((cbam_pixel_stats_kernel<1, T, false>), gs, dim3(256), 0, st, x + off, cab, C, kCbamGroup,
-                           HW, mpart, nullptr, nullptr, 0, 0.f, nullptr, nullptr, 0);
-    }
-    if (y && sa_lds <= 48 * 1024) {  // spatial gate inside the apply pass
-      dim3 gf((unsigned)pxb, (C + kCbamApplyCh - 1) / kCbamApplyCh, nb);
-      if (V == 4)
-        hipLaunchKernelGGL((cbam_sa_apply_kernel<4, T>), gf, dim3(256), sa_lds, st, x + off, y + off, cab, mpart, G,
-                           C, H, W, sa_w);
-      else
-        hipLaunchKernelGGL((cbam_sa_apply_kernel<1, T>), gf, dim3(256), sa_lds, st, x + off, y + off, cab, mpart, G,
-                           C, H, W, sa_w);
-      continue;
-    }
-    hipLaunchKernelGGL(cbam_sa_kernel, dim3((W + 15) / 16, (H + 15) / 16, nb), dim3(256), 0, st, mpart, G, C, H, W,
-                       sa_w, sab);
-    if (!y) continue;
-    dim3 ga((unsigned)pxb, (C + 7) / 8, nb);
+  // (Folding the 7x7 spatial conv into the apply pass measured slower at both CBAM shapes - L4 0.134 -> 0.187 ms,
+  // L18 0.043 -> 0.058 ms same-box: the per-run map staging and the conv, recomputed by every channel block, cost
+  // more than the sa launch they replace - and so did a pixel-statistics pass with 8 channels per wave: level at
+  // L18, 3 % slower at L4.)
+  const float* ps = psum_pre ? psum_pre : psum;
+  const float* pm = pmax_pre ? pmax_pre : pmax;
+  if (!psum_pre)
+    hipLaunchKernelGGL((plane_part_stats_kernel<true, T>), dim3((unsigned)(B * C * pp.parts)), dim3(256), 0, st, x, HW,
+                       pp.parts, pp.seg, psum, pmax);
+  dim3 gs((unsigned)pxb, G, B);
+  if (fused) {  // channel gate computed inside the pixel-statistics workgroups
+    hipLaunchKernelGGL((cbam_pixel_stats_kernel<4, T, true>), gs, dim3(256), lds, st, x, ca, C, kCbamGroup, HW, mpart,
+                       ps, pm, pp.parts, 1.0f / (float)HW, fc0_w, fc2_w, hidden);
+  } else {
+    hipLaunchKernelGGL((channel_gate_kernel<true>), dim3(B), dim3(256), lds, st, ps, pm, pp.parts, C, 1.0f / (float)HW,
+                       fc0_w, nullptr, fc2_w, nullptr, hidden, ca);
     if (V == 4)
-      hipLaunchKernelGGL((cbam_apply_kernel<4, T>), ga, dim3(256), 0, st, x + off, y + off, cab, sab, C, HW);
+      hipLaunchKernelGGL((cbam_pixel_stats_kernel<4, T, false>), gs, dim3(256), 0, st, x, ca, C, kCbamGroup, HW, mpart,
+                         nullptr, nullptr, 0, 0.f, nullptr, nullptr, 0);
     else
-      hipLaunchKernelGGL((cbam_apply_kernel<1, T>), ga, dim3(256), 0, st, x + off, y + off, cab, sab, C, HW);
+      hipLaunchKernelGGL((cbam_pixel_stats_kernel<1, T, false>), gs, dim3(256), 0, st, x, ca, C, kCbamGroup, HW, mpart,
+                         nullptr, nullptr, 0, 0.f, nullptr, nullptr, 0);
+  }
+  hipLaunchKernelGGL(cbam_sa_kernel, dim3((W + 15) / 16, (H + 15) / 16, B), dim3(256), 0, st, mpart, G, C, H, W, sa_w,
+                     sa);
+  if (y) {
+    dim3 ga((unsigned)pxb, (C + 7) / 8, B);
+    if (V == 4)
+      hipLaunchKernelGGL((cbam_apply_kernel<4, T>), ga, dim3(256), 0, st, x, y, ca, sa, C, HW);
+    else
+      hipLaunchKernelGGL((cbam_apply_kernel<1, T>), ga, dim3(256), 0, st, x, y, ca, sa, C, HW);
   }
   YS_CHECK_LAUNCH("cbam");
   return 0;
@@ -1161,34 +931,19 @@ static int ca_forward_impl(const T* x, T* y, int B, int C, int H, int W, const f
   // ~4 TB/s at the m640 shape)
   const int VA = (sizeof(T) == 2 && W % 8 == 0) ? 8 : V;
   const unsigned apply_y = (unsigned)((HW + 256 * VA - 1) / (256 * VA));
-  const int ipc = images_per_chunk(B, (size_t)C * HW * sizeof(T));
-  // one workgroup per plane (opt-in, YOLOSOD_CA_APPLY2=1): faster alone (CA 0.079 -> 0.057 ms with the Detect towers
-  // on one stream) but 2x slower in the model while the towers' MIOpen convs run on the side stream (0.19-0.21 vs
-  // 0.08-0.09 ms same-box, profiles/r04_channel_ab/): its 4096 long-lived workgroups lose the CUs to the conv
-  static const bool apply2 = [] { const char* e = getenv("YOLOSOD_CA_APPLY2"); return e && atoi(e) != 0; }();
-  for (int b0 = 0; b0 < B; b0 += ipc) {
-    const int nb = (B - b0 < ipc) ? B - b0 : ipc;
-    const long off = (long)b0 * C * HW;
-    const long goff = (long)b0 * C * (H + W);
-    if (!yin_pre)
-      hipLaunchKernelGGL((ca_pool_kernel<T>), dim3(nb * C), dim3(256), pool_lds, st, x + off, H, W, RB, yin + goff);
-    hipLaunchKernelGGL(ca_gate_kernel, dim3((H + W + 15) / 16, nb), dim3(256), gate_lds, st,
-                       (yin_pre ? yin_pre : yin) + goff, C, H, W,
-                       mip, conv1_w, conv1_b, bn_w, bn_b, bn_mean, bn_var, bn_eps, convh_w, convh_b, convw_w, convw_b,
-                       gate + goff);
-    if (sizeof(T) == 4 && V == 4 && apply2)
-      hipLaunchKernelGGL(ca_apply_plane_kernel, dim3(nb * C), dim3(256), sizeof(float) * (size_t)(H + W), st,
-                         (const float*)(x + off), (float*)(y + off), gate + goff, H, W);
-    else if (VA == 8)
-      hipLaunchKernelGGL((ca_apply_kernel<8, T>), dim3(nb * C, apply_y), dim3(256), 0, st, x + off, y + off,
-                         gate + goff, H, W);
-    else if (V == 4)
-      hipLaunchKernelGGL((ca_apply_kernel<4, T>), dim3(nb * C, apply_y), dim3(256), 0, st, x + off, y + off,
-                         gate + goff, H, W);
-    else
-      hipLaunchKernelGGL((ca_apply_kernel<1, T>), dim3(nb * C, apply_y), dim3(256), 0, st, x + off, y + off,
-                         gate + goff, H, W);
-  }
+  // (An apply pass with one workgroup per plane ran faster alone - 0.079 -> 0.057 ms - but 2x slower in the model
+  // beside the Detect towers' side-stream convs: its 4096 long-lived workgroups lost the CUs; profiles/r04_channel_ab/)
+  if (!yin_pre)
+    hipLaunchKernelGGL((ca_pool_kernel<T>), dim3(B * C), dim3(256), pool_lds, st, x, H, W, RB, yin);
+  hipLaunchKernelGGL(ca_gate_kernel, dim3((H + W + 15) / 16, B), dim3(256), gate_lds, st, yin_pre ? yin_pre : yin, C,
+                     H, W, mip, conv1_w, conv1_b, bn_w, bn_b, bn_mean, bn_var, bn_eps, convh_w, convh_b, convw_w,
+                     convw_b, gate);
+  if (VA == 8)
+    hipLaunchKernelGGL((ca_apply_kernel<8, T>), dim3(B * C, apply_y), dim3(256), 0, st, x, y, gate, H, W);
+  else if (V == 4)
+    hipLaunchKernelGGL((ca_apply_kernel<4, T>), dim3(B * C, apply_y), dim3(256), 0, st, x, y, gate, H, W);
+  else
+    hipLaunchKernelGGL((ca_apply_kernel<1, T>), dim3(B * C, apply_y), dim3(256), 0, st, x, y, gate, H, W);
   YS_CHECK_LAUNCH("ca");
   return 0;
 }

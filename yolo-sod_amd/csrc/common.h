@@ -273,14 +273,8 @@ __device__ __forceinline__ f32x4 mfma_f16x3(f16x8_t ah, f16x8_t al, f16x8_t bh, 
 }
 
 // Streaming passes that re-read a tensor written just before (> 256 MiB MALL) walk it back to front, so the tail the
-// producer wrote last is still in the Infinity Cache when the pass starts. YOLOSOD_MALL_REVERSE=0 restores the
-// forward order (A/B). Results are identical either way (each workgroup's work and summation order is unchanged).
-static inline int mall_reverse() {
-  static const int r = [] {
-    const char* e = getenv("YOLOSOD_MALL_REVERSE");
-    return (e && e[0] == '0') ? 0 : 1;
-  }();
-  return r;
-}
+// producer wrote last is still in the Infinity Cache when the pass starts (SE L1 0.195 -> 0.18 ms same-box). Results
+// are identical either way (each workgroup's work and summation order is unchanged).
+static inline int mall_reverse() { return 1; }
 
 }  // namespace ys

@@ -273,8 +273,7 @@ YS_EXPORT int yolosod_conv1x1x2_silu_cat(const float* x, long x_bstride, const f
   unsigned* flag;
   YS_CHECK_ARG(c1_carve(const_cast<void*>(prep), prep_bytes, cin, cout, &wp, &flag),
                "conv1x1x2: prepared block too small");
-  static const int np = [] { const char* e = getenv("YOLOSOD_C1_NP"); return e ? atoi(e) : 64; }();
-  const int NPx = np == 64 ? 64 : 128;
+  constexpr int NPx = 64;  // pixels per tile (128-pixel tiles measured slower on four of five neck shapes)
   const int ntile = (HW + NPx - 1) / NPx;
   c1::Args a{x, x_bstride, wp, bias, y, y_bstride, y2, y2_bstride, c2lo, cin, cout, HW, ntile, range_flag_dev(), flag,
              x2, x2_bstride, k1};
@@ -284,12 +283,9 @@ YS_EXPORT int yolosod_conv1x1x2_silu_cat(const float* x, long x_bstride, const f
   if (cout == 64) {  // one 64-channel group: a 16-channel block per wave
     if (y2) hipLaunchKernelGGL((c1::conv1x1_x2_kernel<true, 64, 1>), dim3((unsigned)nwg), dim3(c1::NT), 0, st, a);
     else hipLaunchKernelGGL((c1::conv1x1_x2_kernel<false, 64, 1>), dim3((unsigned)nwg), dim3(c1::NT), 0, st, a);
-  } else if (NPx == 64) {
-    if (y2) hipLaunchKernelGGL((c1::conv1x1_x2_kernel<true, 64>), dim3((unsigned)nwg), dim3(c1::NT), 0, st, a);
-    else hipLaunchKernelGGL((c1::conv1x1_x2_kernel<false, 64>), dim3((unsigned)nwg), dim3(c1::NT), 0, st, a);
   } else {
-    if (y2) hipLaunchKernelGGL((c1::conv1x1_x2_kernel<true, 128>), dim3((unsigned)nwg), dim3(c1::NT), 0, st, a);
-    else hipLaunchKernelGGL((c1::conv1x1_x2_kernel<false, 128>), dim3((unsigned)nwg), dim3(c1::NT), 0, st, a);
+    if (y2) hipLaunchKernelGGL((c1::conv1x1_x2_kernel<true, NPx>), dim3((unsigned)nwg), dim3(c1::NT), 0, st, a);
+    else hipLaunchKernelGGL((c1::conv1x1_x2_kernel<false, NPx>), dim3((unsigned)nwg), dim3(c1::NT), 0, st, a);
   }
   YS_CHECK_LAUNCH("conv1x1x2");
   return 0;

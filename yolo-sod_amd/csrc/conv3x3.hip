@@ -559,9 +559,8 @@ YS_EXPORT int yolosod_conv3x3_silu_xs(const float* x, long x_bstride, float* y, 
   const long nwg = (long)B * a.tiles_x * a.tiles_y * ngrp;
   YS_CHECK_ARG(nwg < (1L << 31), "conv3x3: too many tiles");
   hipStream_t st = (hipStream_t)stream;
-  // YOLOSOD_C3_PERSIST (default 1): the persistent kernel for W % 4 == 0 (two workgroups per CU)
-  static const int persist = [] { const char* e = getenv("YOLOSOD_C3_PERSIST"); return e ? atoi(e) : 1; }();
-  if (persist && v4 && g_c3_abl == 0) {
+  // the persistent kernel for W % 4 == 0 (two workgroups per CU); the one-tile-per-workgroup kernel otherwise
+  if (v4 && g_c3_abl == 0) {
     a.ntiles = (int)((long)B * a.tiles_x * a.tiles_y);
     long grid = 2L * c3_cu_count();
     grid = grid < ((nwg + 7) / 8) * 8 ? grid : ((nwg + 7) / 8) * 8;

@@ -798,10 +798,9 @@ YS_EXPORT int yolosod_conv3x3s2_silu_out(const float* x, float* y, long y_bstrid
   hipStream_t st = (hipStream_t)stream;
 #define S2_LAUNCH(NCB_, G_) \
   hipLaunchKernelGGL((c3s2::conv3x3s2_kernel<NCB_, G_>), dim3((unsigned)grid), dim3(c3s2::NT), 0, st, a)
-  // YOLOSOD_S2_RW: 2 (default) register-resident weights, 2-row tiles, two 256-thread workgroups per CU; 1: 4-row
-  // tiles, one 512-thread workgroup; 0: the general kernel
-  static const int rw_mode = [] { const char* e = getenv("YOLOSOD_S2_RW"); return e ? atoi(e) : 2; }();
-  if (cout == 64 && cin == 32 && rw_mode == 2 && g_s2_abl < 100) {
+  // Cout 64 / Cin 32 (the gated L2 conv): register-resident weights, 2-row tiles, two 256-thread workgroups per CU
+  // (4-row tiles in one 512-thread workgroup measured slower); other shapes: 2-row tiles of the general kernel
+  if (cout == 64 && cin == 32 && g_s2_abl < 100) {
     c3s2::Args a2 = a;
     a2.tiles_y = (Ho + 1) / 2;
     const long nt2 = (long)B * a2.tiles_y * tx;
@@ -823,22 +822,7 @@ YS_EXPORT int yolosod_conv3x3s2_silu_out(const float* x, float* y, long y_bstrid
     else if (gate == 2) S2RW_LAUNCH(2, 0);
     else S2RW_LAUNCH(3, 0);
 #undef S2RW_LAUNCH
-  } else if (cout == 64 && cin == 32 && rw_mode == 1 && g_s2_abl < 100) {  // 4-row tiles, 512 threads
-#define S2RW_LAUNCH(G_, A_) \
-  hipLaunchKernelGGL((c3s2::conv3x3s2_rw_kernel<G_, A_, 4, 512>), dim3((unsigned)grid), dim3(c3s2::NT), 0, st, a)
-    if (gate == 1) {
-      switch (g_s2_abl) {
-        case 1: S2RW_LAUNCH(1, 1); break;
-        case 4: S2RW_LAUNCH(1, 4); break;
-        case 8: S2RW_LAUNCH(1, 8); break;
-        case 13: S2RW_LAUNCH(1, 13); break;
-        default: S2RW_LAUNCH(1, 0); break;
-      }
-    } else if (gate == 0) S2RW_LAUNCH(0, 0);
-    else if (gate == 2) S2RW_LAUNCH(2, 0);
-    else S2RW_LAUNCH(3, 0);
-#undef S2RW_LAUNCH
-  } else if ((rw_mode >= 1 && g_s2_abl < 100) || cout > 128) {  // 2-row tiles, 3 (Cout 64) / 2 workgroups per CU
+  } else if (g_s2_abl < 100 || cout > 128) {  // 2-row tiles, 3 (Cout 64) / 2 workgroups per CU
     c3s2::Args a2 = a;
     a2.tiles_y = (Ho + 1) / 2;
     const long nt2 = (long)B * a2.tiles_y * tx * (cout == 64 ? 1 : cout / 128);  // work items: (tile, group)

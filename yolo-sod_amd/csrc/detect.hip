@@ -77,10 +77,11 @@ __global__ __launch_bounds__(256) void detect_decode_kernel(DecodeArgs d) {
 
 // ------------------------------------------------------------------------------------------------
 // Fused head tail + decode: the last 1x1 convs of both towers (cv2[i][-1]: c2 -> 64 box
-// logits, cv3[i][-1]: c3 -> nc class logits, head.py:45-48,70) run as fp32 MFMA v_mfma_f32_16x16x4_f32 straight
-// into the DFL / dist2bbox / sigmoid decode, so the [B, 64+nc, H, W] raw maps never exist in HBM.
-//   A = conv weights [out][k] (held in registers for the wave's lifetime), B = tower features [k][pixel] (NCHW,
-//   loaded straight from HBM), D[out][pixel]: lane (g = lane>>4, j = lane&15) holds outputs 4g..4g+3 of pixel j.
+// logits, cv3[i][-1]: c3 -> nc class logits, head.py:45-48,70) run on MFMA straight into the DFL / dist2bbox /
+// sigmoid decode, so the [B, 64+nc, H, W] raw maps never exist in HBM (detect_head_x2_kernel: fp16 two-term splits,
+// the default; detect_head_lds_kernel: exact fp32 MFMA, the split-range fallback).
+//   A = conv weights [out][k], B = tower features [k][pixel] (NCHW, loaded straight from HBM), D[out][pixel]:
+//   lane (g = lane>>4, j = lane&15) holds outputs 4g..4g+3 of pixel j.
 //   Box tile s (16 rows) is exactly side s's 16 DFL bins, so the softmax max / sum / expectation are 4 local
 //   values plus two permlane swaps (xor16, xor32). Class tile: rows 0..15 (nc <= 16).
 // Each wave owns NTS consecutive 16-pixel groups of one level of one image.
@@ -99,116 +100,7 @@ struct HeadArgs {
   unsigned* range_flag;  // split-range guard of the x2 kernel (common.h range_report)
 };
 
-template <int C2, int C3, int NTS>
-__global__ __launch_bounds__(256) void detect_head_kernel(HeadArgs d) {
-  const int b = blockIdx.y;
-  int l = 0;
-#pragma unroll
-  for (int i = 1; i < 4; ++i)
-    if (i < d.nl && (int)blockIdx.x >= d.blk_off[i]) l = i;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int g = lane >> 4, j = lane & 15;
-  const int HW = d.hw[l];
-  const int px0 = (((int)blockIdx.x - d.blk_off[l]) * 4 + wv) * (NTS * 16);
-  if (px0 >= HW) return;  // whole wave; the kernel has no workgroup barrier
-  const int nc = d.nc;
-
-  // A operands: W[row = 16t + j][k = 4q + g]; biases of the rows this lane's accumulators hold (4g + r)
-  float wbr[4][C2 / 4], wcr[C3 / 4], bbr[4][4], bcr[4];
-  {
-    const float* wb = d.wb[l];
-    const float* wc = d.wc[l];
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int q = 0; q < C2 / 4; ++q) wbr[t][q] = wb[(16 * t + j) * C2 + 4 * q + g];
-#pragma unroll
-    for (int q = 0; q < C3 / 4; ++q) wcr[q] = (j < nc) ? wc[j * C3 + 4 * q + g] : 0.f;
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) bbr[t][r] = d.bb[l][16 * t + 4 * g + r];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) bcr[r] = (4 * g + r < nc) ? d.bc[l][4 * g + r] : 0.f;
-  }
-  const float* fbb = static_cast<const float*>(d.fb[l]) + (long)b * C2 * HW;
-  const float* fcb = static_cast<const float*>(d.fc[l]) + (long)b * C3 * HW;
-  const int W = d.w[l];
-  const float st = d.stride[l];
-  float* yb = d.y + (long)b * (4 + nc) * d.A + d.a_off[l];
-
-  for (int ts = 0; ts < NTS; ++ts) {
-    const int p0 = px0 + ts * 16;
-    if (p0 >= HW) break;
-    const int p = p0 + j;
-    const bool ok = p < HW;
-    float xb[C2 / 4], xc[C3 / 4];
-    if (p0 + 16 <= HW) {  // full group (wave-uniform): plain strided loads, no per-load selects
-      const float* pb = fbb + (long)g * HW + p;
-      const float* pc = fcb + (long)g * HW + p;
-#pragma unroll
-      for (int q = 0; q < C2 / 4; ++q) xb[q] = pb[(long)q * 4 * HW];
-#pragma unroll
-      for (int q = 0; q < C3 / 4; ++q) xc[q] = pc[(long)q * 4 * HW];
-    } else {
-#pragma unroll
-      for (int q = 0; q < C2 / 4; ++q) xb[q] = ok ? fbb[(long)(4 * q + g) * HW + p] : 0.f;
-#pragma unroll
-      for (int q = 0; q < C3 / 4; ++q) xc[q] = ok ? fcb[(long)(4 * q + g) * HW + p] : 0.f;
-    }
-    f32x4 acc[5];
-#pragma unroll
-    for (int t = 0; t < 5; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int q = 0; q < C2 / 4; ++q)
-#pragma unroll
-      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wbr[t][q], xb[q], acc[t], 0, 0, 0);
-#pragma unroll
-    for (int q = 0; q < C3 / 4; ++q) acc[4] = __builtin_amdgcn_mfma_f32_16x16x4f32(wcr[q], xc[q], acc[4], 0, 0, 0);
-
-    // DFL (block.py:79-82): softmax over the 16 bins of each side, expectation with weights 0..15. Hardware
-    // exp2 / reciprocal (1-2 ulp): the head is VALU-issue bound (SQ counters: ~650 VALU per 16-pixel group
-    // against 80 MFMAs with the libm expf / IEEE division), and the box tolerance is 1e-3
-    float dist[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      float v[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = acc[s][r] + bbr[s][r];
-      float mx = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
-      mx = xor32_max(xor16_max(mx));
-      float sum = 0.f, e = 0.f;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        v[r] = __expf(v[r] - mx);
-        sum += v[r];
-        e += (float)(4 * g + r) * v[r];
-      }
-      sum = xor32_sum(xor16_sum(sum));
-      e = xor32_sum(xor16_sum(e));
-      dist[s] = e * __builtin_amdgcn_rcpf(sum);
-    }
-    if (!ok) continue;
-    const int iy = p / W, ix = p - iy * W;
-    const float ax = (float)ix + 0.5f, ay = (float)iy + 0.5f;
-    const float x1 = ax - dist[0], y1 = ay - dist[1];
-    const float x2 = ax + dist[2], y2 = ay + dist[3];
-    // dist2bbox xywh (tal.py:348-357) * stride; lane group g writes component g
-    const float out = g == 0 ? ((x1 + x2) / 2.0f) * st
-                    : g == 1 ? ((y1 + y2) / 2.0f) * st
-                    : g == 2 ? (x2 - x1) * st
-                             : (y2 - y1) * st;
-    yb[(long)g * d.A + p] = out;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int c = 4 * g + r;
-      if (c < nc) yb[(long)(4 + c) * d.A + p] = sigmoidf_(acc[4][r] + bcr[r]);
-    }
-  }
-}
-
-
-// Same head tail + decode with the conv weights in LDS instead of registers (A fragments are ds_read_b128 of 4
+// The head tail + decode on exact fp32 MFMA (the split-range fallback), the conv weights in LDS (A fragments are ds_read_b128 of 4
 // tiles' rows at once from a [q][g][j][t] image, conflict-free for the b128 lane groups) - the ~100 VGPRs that
 // held them now double-buffer the next 16-pixel group's feature loads, so the HBM latency of a group overlaps the
 // MFMAs and DFL of the previous one, at 3 waves per SIMD.
@@ -320,7 +212,7 @@ __global__ __launch_bounds__(256, C3 > 64 ? 2 : 3) void detect_head_lds_kernel(H
       acc[4] = __builtin_amdgcn_mfma_f32_16x16x4f32(c4.z, cc[4 * qq + 2], acc[4], 0, 0, 0);
       acc[4] = __builtin_amdgcn_mfma_f32_16x16x4f32(c4.w, cc[4 * qq + 3], acc[4], 0, 0, 0);
     }
-    // DFL (block.py:79-82), as in detect_head_kernel
+    // DFL (block.py:79-82)
     float dist[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
@@ -504,7 +396,7 @@ __global__ __launch_bounds__(256, C3 > 64 ? 2 : 3) void detect_head_x2_kernel(He
       acc[4] = mfma_f16x3(*reinterpret_cast<const f16x8_t*>(wbh + o), *reinterpret_cast<const f16x8_t*>(wbl + o), fh,
                           fl, acc[4]);
     }
-    // DFL (block.py:79-82), as in detect_head_kernel
+    // DFL (block.py:79-82)
     float dist[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
@@ -666,15 +558,11 @@ static int detect_head_impl(int nl, const void* const* box_feat, const void* con
     YS_CHECK_LAUNCH("detect_head_bf16");
     return 0;
   }
-  // default: fp16-split matrix products (detect_head_x2_kernel); YOLOSOD_HEAD_X2=0: exact fp32 MFMA with the
-  // weights in LDS; YOLOSOD_HEAD_V1=1: exact fp32 MFMA with the weights in registers (A/B)
-  static const bool v1 = [] { const char* e = getenv("YOLOSOD_HEAD_V1"); return e && atoi(e) != 0; }();
-  if (g_head_x2 && !v1) {
+  // default: fp16-split matrix products (detect_head_x2_kernel); YOLOSOD_HEAD_X2=0 (the split-range fallback):
+  // exact fp32 MFMA with the weights in LDS
+  if (g_head_x2) {
     if (c3 == 64) hipLaunchKernelGGL((detect_head_x2_kernel<64, 64, NTS>), grid, dim3(256), 0, st, d);
     else hipLaunchKernelGGL((detect_head_x2_kernel<64, 128, NTS>), grid, dim3(256), 0, st, d);
-  } else if (v1) {
-    if (c3 == 64) hipLaunchKernelGGL((detect_head_kernel<64, 64, NTS>), grid, dim3(256), 0, st, d);
-    else hipLaunchKernelGGL((detect_head_kernel<64, 128, NTS>), grid, dim3(256), 0, st, d);
   } else {
     if (c3 == 64) hipLaunchKernelGGL((detect_head_lds_kernel<64, 64, NTS>), grid, dim3(256), 0, st, d);
     else hipLaunchKernelGGL((detect_head_lds_kernel<64, 128, NTS>), grid, dim3(256), 0, st, d);

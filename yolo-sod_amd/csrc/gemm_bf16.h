@@ -532,7 +532,7 @@ static inline int launch_gemm_bf16(const GemmB& g0, int batch, bool b_kc, hipStr
   YS_CHECK_ARG(b_kc || !ln, "gemm_bf16: LN prologue needs a K-contiguous B");
   // 128x64 tiles when N is narrow or 128x128 would leave CUs idle; 128x128 otherwise
   const long t128 = (long)((g.M + 127) / 128) * ((g.N + 127) / 128) * batch;
-  static const int force = [] { const char* e = getenv("YOLOSOD_GEMMB_TILE"); return e ? atoi(e) : 0; }();
+  constexpr int force = 0;  // A/B builds: 1 = 128x64 everywhere, 2 = 128x128 everywhere
   if (force == 1 || (force != 2 && (g.N <= 64 || t128 < 512))) YS_GEMMB_LAUNCH(4, 1, 1, 2);
   else YS_GEMMB_LAUNCH(2, 2, 2, 2);
 #undef YS_GEMMB_LAUNCH

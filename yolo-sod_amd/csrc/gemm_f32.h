@@ -600,7 +600,7 @@ static inline int launch_gemm(const GemmArgs& g0, int batch, bool b_kc, hipStrea
   g.nmajor = 0;
   g.bfold = 0;
   if (!b_kc && batch > 1 && g.a_bs == 0 && g.N % 128 != 0 && g.N % 4 == 0 && g.epi.vec && e.bias_mode != 2 && e.bn_mode != 2 &&
-      g.ldb % 4 == 0 && g.b_bs % 4 == 0 && (long)g.N * batch < (1L << 31) && !getenv("YOLOSOD_GEMM_NOFOLD")) {
+      g.ldb % 4 == 0 && g.b_bs % 4 == 0 && (long)g.N * batch < (1L << 31)) {
     g.nimg = g.N;
     g.nmajor = 1;
     g.N *= batch;
@@ -609,8 +609,7 @@ static inline int launch_gemm(const GemmArgs& g0, int batch, bool b_kc, hipStrea
   // K-contiguous per-image B with a shared A (the A2 output GEMM: B = the image's tokens): the batch goes into the
   // tile index and the tiles run n-major, so the M tiles reading one B column block sit on one XCD (B read once)
   const int batch0 = batch;
-  if (b_kc && batch > 1 && g.a_bs == 0 && (long)batch * ((g.M + 63) / 64) * ((g.N + 63) / 64) < (1L << 30) &&
-      !getenv("YOLOSOD_GEMM_NOFOLD")) {
+  if (b_kc && batch > 1 && g.a_bs == 0 && (long)batch * ((g.M + 63) / 64) * ((g.N + 63) / 64) < (1L << 30)) {
     g.bfold = batch;
     g.nmajor = 1;
     batch = 1;
@@ -641,11 +640,7 @@ static inline int launch_gemm(const GemmArgs& g0, int batch, bool b_kc, hipStrea
       else hipLaunchKernelGGL((gemm_f32_kernel<WM_, WN_, MI_, NI_, false, false>), grid, dim3(256), 0, st, g); \
     }                                                                                                          \
   } while (0)
-  // tile choice (YOLOSOD_GEMM_TILE overrides for A/B runs: 1 = 128x64, 2 = 128x128, 3 = 64x256)
-  static const int forced = [] {
-    const char* e = getenv("YOLOSOD_GEMM_TILE");
-    return e ? atoi(e) : 0;
-  }();
+  constexpr int forced = 0;  // tile choice (A/B builds: 1 = 128x64, 2 = 128x128, 3 = 64x256)
   // 128x64 tiles also when 128x128 would leave CUs idle (fewer tiles than CUs) or waste > 10% of a tile column
   // on a ragged N (e.g. N = H*W = 400): more, smaller workgroups for the small A2 / MHA GEMMs
   const long t128 = (long)((g.M + 127) / 128) * ((g.N + 127) / 128) * batch0;

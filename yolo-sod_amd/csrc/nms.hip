@@ -63,11 +63,8 @@ struct NmsArgs {
   int* kept_t;                   // [B][max_det] kept entries when max_det > NMS_MAXDET (else LDS), else nullptr
   float4* kbox;                  // [B][max_det] kept class-offset boxes (fallback), idem
   float* karea;                  // [B][max_det]
-  unsigned long long* stamps;    // diagnostic only (YOLOSOD_NMS_STAMPS): [B][8] or nullptr
 };
 
-#define YS_NSTAMP(k) \
-  if (g.stamps && threadIdx.x == 0) g.stamps[b * 8 + (k)] = __builtin_amdgcn_s_memtime();
 
 __device__ __forceinline__ int block256_exclusive_scan(int v, int* wsum4, int* total);
 
@@ -393,7 +390,6 @@ __global__ __launch_bounds__(NMS_T) void nms_select_kernel(NmsArgs g) {
   const int tid = threadIdx.x;
   __shared__ SortShared sh;
   __shared__ unsigned sel_below, sel_prefix;
-  YS_NSTAMP(0)
   const long A = g.A;
   const int nc = g.nc;
   unsigned* kA = g.keyA + (long)b * g.cap;
@@ -410,7 +406,6 @@ __global__ __launch_bounds__(NMS_T) void nms_select_kernel(NmsArgs g) {
     for (int i = tid; i < nblk; i += NMS_T) v += g.blkcnt[(long)b * nblk + i];
     (void)block_exclusive_scan(v, nsum, &n);
   }
-  YS_NSTAMP(1)
   const int neff = (n > g.max_nms) ? g.max_nms : n;
 
   // (b) score order of the prefix
@@ -462,7 +457,6 @@ __global__ __launch_bounds__(NMS_T) void nms_select_kernel(NmsArgs g) {
     ks = lk[0]; ps = lp[0]; kd = lk[1]; pd = lp[1];
     radix_sort_pairs(ks, ps, kd, pd, m, sh);
   }
-  YS_NSTAMP(2)
   const int K = (m < neff) ? m : neff;
   // prefix boxes with the class offset (ops.py:289,295), areas, ids
   const float4* bx = g.boxes + (long)b * A;
@@ -485,7 +479,6 @@ __global__ __launch_bounds__(NMS_T) void nms_select_kernel(NmsArgs g) {
     mt[1] = neff;
     mt[2] = K;
     mt[3] = (int)T;
-    if (g.stamps) g.stamps[b * 8 + 6] = (unsigned long long)n;
   }
 }
 
@@ -540,7 +533,6 @@ __global__ __launch_bounds__(NMS_T) void nms_resolve_kernel(NmsArgs g) {
   // kept entries: < KCAP -> prefix index, else KCAP + remainder index
   int* kept_t = BIG ? g.kept_t + (long)b * g.max_det : kept_t_lds;
   __shared__ int nkept_sh, done_sh;
-  YS_NSTAMP(3)
   const int* mt = g.meta + 4 * b;
   const int n = mt[0], neff = mt[1], K = mt[2];
   const unsigned T = (unsigned)mt[3];
@@ -630,7 +622,6 @@ __global__ __launch_bounds__(NMS_T) void nms_resolve_kernel(NmsArgs g) {
     o[5] = (float)j;
     oi[k] = (int)a;
   }
-  YS_NSTAMP(4)
 
   // (2) fallback: prefix exhausted, fewer than max_det kept, more candidates (keys >= T) within max_nms
   if (!done_sh && K < neff) {
@@ -739,44 +730,19 @@ __global__ __launch_bounds__(NMS_T) void nms_resolve_kernel(NmsArgs g) {
     }
   }
   __syncthreads();
-  YS_NSTAMP(5)
   const int nk = nkept_sh;
   for (int e = nk * 6 + tid; e < g.max_det * 6; e += NMS_T) ob[e] = 0.f;
   for (int e = nk + tid; e < g.max_det; e += NMS_T) oi[e] = -1;
   if (tid == 0) {
     g.counts[b] = nk;
-    if (g.stamps) g.stamps[b * 8 + 7] = (unsigned long long)K;
   }
 }
 
-#undef YS_NSTAMP
 
 }  // namespace ys
 
 using namespace ys;
 
-static unsigned long long* g_nms_stamps = nullptr;  // diagnostic only (YOLOSOD_NMS_STAMPS)
-static size_t g_nms_stamp_cap = 0, g_nms_stamp_n = 0;
-
-// Diagnostic: per-image phase cycles of the last NMS call (synchronous). out[b*6 + k]: 0 compaction, 1 sort /
-// select, 2 greedy over the prefix (resolve start -> prefix done, includes the mask kernel's wait), 3 fallback,
-// 4 candidates n, 5 prefix length K.
-YS_EXPORT int yolosod_debug_nms_stage_cycles(double* out, int B) {
-  if (!g_nms_stamps || (size_t)B * 8 > g_nms_stamp_n || B > 1024) return -1;
-  static unsigned long long h[8 * 1024];
-  if (hipMemcpy(h, g_nms_stamps, (size_t)B * 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
-    return -1;
-  for (int b = 0; b < B; ++b) {
-    const unsigned long long* s = h + b * 8;
-    out[b * 6 + 0] = (double)(s[1] - s[0]);
-    out[b * 6 + 1] = (double)(s[2] - s[1]);
-    out[b * 6 + 2] = (double)(s[4] - s[3]);
-    out[b * 6 + 3] = (double)(s[5] - s[4]);
-    out[b * 6 + 4] = (double)s[6];
-    out[b * 6 + 5] = (double)s[7];
-  }
-  return 0;
-}
 
 static long nms_cap(int nc, int A, int multi_label) { return (long)A * (multi_label ? nc : 1); }
 
@@ -857,18 +823,6 @@ YS_EXPORT int yolosod_nms(float* pred, int B, int nc, int A, float conf_thres, d
   g.out = out;
   g.counts = counts;
   g.out_index = out_index;
-  g.stamps = nullptr;
-  if (getenv("YOLOSOD_NMS_STAMPS")) {
-    if ((size_t)B * 8 > g_nms_stamp_cap) {
-      if (g_nms_stamps) (void)hipFree(g_nms_stamps);
-      g_nms_stamps = nullptr;
-      if (hipMalloc((void**)&g_nms_stamps, (size_t)B * 8 * sizeof(unsigned long long)) != hipSuccess) return -1;
-      g_nms_stamp_cap = (size_t)B * 8;
-    }
-    (void)hipMemsetAsync(g_nms_stamps, 0, (size_t)B * 8 * sizeof(unsigned long long), st);
-    g_nms_stamp_n = (size_t)B * 8;
-    g.stamps = g_nms_stamps;
-  }
   if (A > 0) {
     hipLaunchKernelGGL(nms_prep_kernel, dim3(nblk_a, B), dim3(256), 0, st, g);
     hipLaunchKernelGGL(nms_scatter_kernel, dim3(nblk_a, B), dim3(256), 0, st, g);

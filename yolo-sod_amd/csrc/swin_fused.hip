@@ -1,7 +1,6 @@
 // Fused SwinBlock for small channel counts (C <= 128: the P2 instance L28, C = 64 in the paper model).
 //
-// One 256-thread workgroup processes one 7x7 window at a time (persistent: a strided run of windows per
-// workgroup). The window's tokens never leave LDS between the depthwise conv and the final pw1x1+BN+SiLU+residual,
+// One 256-thread workgroup processes one 7x7 window. The window's tokens never leave LDS between the depthwise conv and the final pw1x1+BN+SiLU+residual,
 // so the per-token HBM traffic is read x (+ halo) once and write y once, against ~5.5 GB of token-major scratch
 // for the decomposed path at 640^2 bs=32.
 //
@@ -196,10 +195,9 @@ __device__ __forceinline__ void lds_row_layernorm(const float* S, int lds, float
   }
 }
 
-// Persistent: each workgroup walks a strided sequence of windows inside its XCD's contiguous window range
-// (workgroup i runs on XCD i % 8; neighbouring windows share 128-B lines of x and y - a window row is 28 B - so
-// they meet in one L2). The next window's halo is loaded into registers during the current window's last stage.
-template <int C, int NH, bool W7, bool PERSIST>
+// Workgroup i runs on XCD i % 8 and takes its window from that XCD's contiguous window range (neighbouring windows
+// share 128-B lines of x and y - a window row is 28 B - so they meet in one L2).
+template <int C, int NH, bool W7>
 __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
   constexpr int HD = C / NH;
   constexpr int HID = 2 * C;
@@ -231,7 +229,6 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
 
   const long nwin_total = (long)p.B * p.nWin;
   const long per_xcd = (nwin_total + 7) >> 3;
-  const long wpx = gridDim.x >> 3;
   const long xbeg = (long)(blockIdx.x & 7) * per_xcd;
   const long xend = (xbeg + per_xcd < nwin_total) ? xbeg + per_xcd : nwin_total;
   long gw = xbeg + (blockIdx.x >> 3);
@@ -298,8 +295,6 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
   load_halo(gw);
 
   for (;;) {
-    const long gnext = gw + wpx;
-    const bool has_next = PERSIST && gnext < xend;
     const int gwc = __builtin_amdgcn_readfirstlane((int)gw);
     const int img = gwc / p.nWin, win = gwc - (gwc / p.nWin) * p.nWin;
     const int wy = win / p.nWx, wx = win - (win / p.nWx) * p.nWx;
@@ -308,12 +303,6 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
     // fragment and bias load out of the window loop and spills them
     const float *w_in = p.win, *b_in = p.bin, *w_o = p.wo, *b_o = p.bo, *w_1 = p.w1, *b_1 = p.b1, *w_2 = p.w2,
                 *b_2 = p.b2, *w_pw = p.wpw, *bn_sc = p.bn_scale, *bn_sh = p.bn_shift;
-    // (persistent build only: the laundered pointers lose their global address space, so every weight load
-    // becomes a flat load that also counts in lgkmcnt and is waited for by each LDS wait)
-    if (PERSIST) {
-      asm volatile("" : "+s"(w_in), "+s"(b_in), "+s"(w_o), "+s"(b_o), "+s"(w_1), "+s"(b_1));
-      asm volatile("" : "+s"(w_2), "+s"(b_2), "+s"(w_pw), "+s"(bn_sc), "+s"(bn_sh));
-    }
     // QKV weight fragments: in flight during the halo store, the depthwise conv and the LN1 statistics
     WFrag<C, 3 * C / 16> f_in;
     load_wfrag(w_in, f_in, tid);
@@ -635,7 +624,6 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
     __syncthreads();
 
     // next window's halo: in flight during the last stage
-    if (has_next) load_halo(gnext);
 
     // ---- stage 8: y = x + SiLU(BN(Wpw T^T)); output tile Y^T[c][tok] (lanes over tokens), token 48 on the VALU ----
     {
@@ -682,8 +670,7 @@ __global__ __launch_bounds__(256, 3) void swin_fused_kernel(SwinFusedArgs p) {
             __builtin_bit_cast(unsigned, x48 + silu_fast_(e48 * sc48 + sh48)), ry8, v48, sb, 0);
       }
     }
-    if (!PERSIST || !has_next) break;
-    gw = gnext;
+    break;  // one window per workgroup
   }
 }
 
@@ -706,36 +693,19 @@ int yolosod_swin_fused_launch(const float* x, float* y, int B, int C, int H, int
   SwinFusedArgs a{x, y, B, H, W, wh, ww, nWx, nWin, L, dw_w, ln1_w, ln1_b, ln1_eps, in_proj_w, in_proj_b,
                   out_proj_w, out_proj_b, ln2_w, ln2_b, ln2_eps, mlp1_w, mlp1_b, mlp2_w, mlp2_b, pw_w,
                   bn_scale, bn_shift, 1.0f / sqrtf((float)(C / num_heads))};
-  // persistent grid: (resident workgroups per CU) x CUs, a multiple of 8 (one range of windows per XCD), never
-  // more workgroups than windows; 3 resident per CU at C = 64 (LDS 52 KB)
   const bool w7 = (wh == 7 && ww == 7);
   const long nwin = (long)B * nWin;
-  auto resident = [](const void* fn) -> long {
-    int dev = 0, cus = 256, per_cu = 1;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, 0) != hipSuccess || per_cu < 1) per_cu = 1;
-    if (const char* e = getenv("YOLOSOD_SWIN_WGS_PER_CU")) per_cu = atoi(e) > 0 ? atoi(e) : per_cu;
-    return (long)cus * per_cu;
-  };
   auto grid_of = [&](long n) {
     const long cap = 8 * ((nwin + 7) / 8);
     if (n > cap) n = cap;
     return dim3((unsigned)(8 * ((n + 7) / 8)));
   };
-  // default: one window per workgroup (grid = windows, XCD-aware order). YOLOSOD_SWIN_PERSIST=1: persistent
-  // workgroups with the next window's halo prefetched during the last stage (A/B: the window loop makes the
-  // compiler hoist and spill per-thread addresses at 3 workgroups per CU).
-  static const bool persist = [] { const char* e = getenv("YOLOSOD_SWIN_PERSIST"); return e && atoi(e) != 0; }();
 #define YS_SWF(CC, NHH)                                                                                  \
   if (C == CC && num_heads == NHH) {                                                                     \
-    if (w7 && persist) {                                                                                 \
-      static const long res = resident((const void*)swin_fused_kernel<CC, NHH, true, true>);             \
-      hipLaunchKernelGGL((swin_fused_kernel<CC, NHH, true, true>), grid_of(res), dim3(256), 0, st, a);   \
-    } else if (w7) {                                                                                     \
-      hipLaunchKernelGGL((swin_fused_kernel<CC, NHH, true, false>), grid_of(nwin), dim3(256), 0, st, a); \
+    if (w7) {                                                                                            \
+      hipLaunchKernelGGL((swin_fused_kernel<CC, NHH, true>), grid_of(nwin), dim3(256), 0, st, a);        \
     } else {                                                                                             \
-      hipLaunchKernelGGL((swin_fused_kernel<CC, NHH, false, false>), grid_of(nwin), dim3(256), 0, st, a); \
+      hipLaunchKernelGGL((swin_fused_kernel<CC, NHH, false>), grid_of(nwin), dim3(256), 0, st, a);       \
     }                                                                                                    \
   } else
   YS_SWF(64, 2) YS_SWF(64, 4) YS_SWF(128, 2) YS_SWF(128, 4) return 0;

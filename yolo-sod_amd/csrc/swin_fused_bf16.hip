@@ -623,8 +623,7 @@ size_t yolosod_swin_fused_bf16_wfrag_elems(int C, int mlp_hidden) {
 
 // shapes the fused bf16 kernel takes: 7x7 windows, C 64 (2 heads) / 128 (2 or 4 heads), MLP hidden 2C
 bool yolosod_swin_fused_bf16_ok(int C, int num_heads, int wh, int ww, int mlp_hidden) {
-  static const bool on = [] { const char* e = getenv("YOLOSOD_SWIN_FUSED_BF16"); return !e || atoi(e) != 0; }();
-  return on && wh == 7 && ww == 7 && mlp_hidden == 2 * C &&
+  return wh == 7 && ww == 7 && mlp_hidden == 2 * C &&
          ((C == 128 && (num_heads == 2 || num_heads == 4)) || (C == 64 && num_heads == 2));
 }
 

@@ -585,8 +585,6 @@ int yolosod_swin_wide_launch(const float* x, float* y, int B, int C, int H, int 
                              hipStream_t st) {
   if (C != wide::C || num_heads != C / wide::HD || wh != 7 || ww != 7 || mlp_hidden != 2 * C) return 0;
   if ((long)C * H * W >= (1L << 30) || (long)B * nWin >= (1L << 31)) return 0;  // 32-bit byte offsets / indices
-  if (const char* e = getenv("YOLOSOD_SWIN_WIDE"))
-    if (atoi(e) == 0) return 0;
   wide::Args a{x, y, B, H, W, nWx, nWin, dw_w, ln1_w, ln1_b, ln1_eps, in_proj_w, in_proj_b, out_proj_w, out_proj_b,
                ln2_w, ln2_b, ln2_eps, mlp1_w, mlp1_b, mlp2_w, mlp2_b, pw_w, bn_scale, bn_shift,
                1.0f / sqrtf((float)wide::HD)};

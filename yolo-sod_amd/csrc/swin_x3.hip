@@ -72,7 +72,6 @@ struct Args {
   float scale;
   unsigned* range_flag;  // split-range guard (common.h range_report), may be null
   const unsigned* prep_flag;  // the prepared block's own range word (swin_x3_prep_kernel), reported on every launch
-  float* t1;  // split variant: T after the attention residual, token-major [B*H*W][C] (cropped tokens only)
 };
 
 // The weight preparation's range result is kept in the prepared block and re-reported by every launch that uses the
@@ -141,12 +140,8 @@ __device__ __forceinline__ void load_wp(const h16_t* __restrict__ Wp, int N, int
     for (int s = 0; s < K / 32; ++s)
 #pragma unroll
       for (int j = 0; j < NJ; ++j)
-#ifdef YS_ABL_WLOAD
-        f.v[j][s][p] = *reinterpret_cast<const f16x8_t*>(Wp + (long)(p * 64 + lane) * 8);
-#else
         f.v[j][s][p] = *reinterpret_cast<const f16x8_t*>(
             Wp + (long)p * N * KT + ((long)((cb0 + 4 * j) * (KT / 32) + koff / 32 + s) * 64 + lane) * 8);
-#endif
 }
 
 // acc[rb][j] += (A[rows rb*16 .. +15][0, K) . W^T)^T: A = three LDS planes (row stride PS, plane stride PL), the
@@ -171,9 +166,6 @@ __device__ __forceinline__ void gemm_x3(const h16_t* A, const WP<K, NJ>& w, f32x
   };
   ld(0, u[0]);
   ld(1, u[1]);
-#ifdef YS_X3_PRIO  // experiment: the MFMA clusters issue at raised wave priority
-  __builtin_amdgcn_s_setprio(1);
-#endif
 #pragma unroll
   for (int i = 0; i < NS; ++i) {
     if (i + 2 < NS) ld(i + 2, u[(i + 2) % 3]);
@@ -193,9 +185,6 @@ __device__ __forceinline__ void gemm_x3(const h16_t* A, const WP<K, NJ>& w, f32x
       }
     }
   }
-#ifdef YS_X3_PRIO
-  __builtin_amdgcn_s_setprio(0);
-#endif
 }
 
 // LayerNorm statistics of token rows [0, 49) of T (fp32, stride LT) and the normalised rows (affine folded into the
@@ -231,23 +220,17 @@ __device__ __forceinline__ void ln_planes(const float* T, h16_t* P, float eps, i
   }
 }
 
-// SPLIT: the attention half only (split at the attention residual): dw -> LN1 -> QKV -> attention -> out-proj + the
-// residual, stored token-major to p.t1 for the cropped tokens; the per-token half (LN2 -> MLP -> pw -> BN -> SiLU -> + x)
-// runs in swin_mlp_kernel, token-tiled, with its weights resident in LDS and no window padding.
-template <int C, int NH, bool SPLIT = false, bool SWZ = false>
+template <int C, int NH>
 __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
+  constexpr bool SWZ = true;  // unpadded plane rows with XOR-swizzled chunks (plane_off / plane_off8)
   constexpr int HD = C / NH;
   constexpr int HID = 2 * C;
   constexpr int LT = C + 4;      // T row stride (floats)
-#ifndef YS_X3_PS_PAD  // plane row padding (fp16 elements); diagnostic builds vary it
-#define YS_X3_PS_PAD 16  // PS = 80 = ten 16-byte quads: the ds_read_b128 lane groups of the GEMM operand
-                         // reads hit 16 distinct quads (PS = 72, nine quads: 28 of 64 lanes in 2-way conflicts)
-#endif
-  constexpr int PS = SWZ ? C : C + YS_X3_PS_PAD;  // plane row stride (fp16); SWZ: unpadded, chunk-swizzled rows
+  constexpr int PS = C;          // plane row stride (fp16): unpadded, chunk-swizzled rows
   constexpr int PL = 64 * PS;    // plane stride
-  constexpr int PSK = SWZ ? C : C + 8;  // K plane row stride (SWZ: unpadded, 8-byte chunks swizzled)
+  constexpr int PSK = C;         // K plane row stride: unpadded, 8-byte chunks swizzled
   constexpr int KPL = NR * PSK;  // K plane stride
-  constexpr int PSV = SWZ ? 64 : 72;    // V^T plane row stride (keys 0..63 (+ 8))
+  constexpr int PSV = 64;        // V^T plane row stride (keys 0..63)
   constexpr int VPL = C * PSV;   // V^T plane stride
   constexpr int NHS = (C + 2) / 3;
   constexpr int PSH = HID + 8;  // MLP hidden plane row stride (both halves side by side, unswizzled: 272-byte rows put
@@ -267,10 +250,7 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
   static_assert(T_B % 16 == 0 && X_B % 16 == 0, "16-byte aligned regions");
   static_assert(T_B + X_B + NPAR * 4 <= 160 * 1024 / 3, "three workgroups per CU");
   static_assert(PLN_B <= X_B && HID_B <= X_B, "staged Q weights after the U1 planes; both hidden halves");
-#ifndef YS_X3_LDS_PAD  // diagnostic builds only: extra LDS per workgroup to measure the kernel at lower occupancy
-#define YS_X3_LDS_PAD 0
-#endif
-  __shared__ __attribute__((aligned(16))) char smem[T_B + X_B + NPAR * 4 + YS_X3_LDS_PAD];
+  __shared__ __attribute__((aligned(16))) char smem[T_B + X_B + NPAR * 4];
   float* T = reinterpret_cast<float*>(smem);
   char* X = smem + T_B;
   float* Q = reinterpret_cast<float*>(X);
@@ -311,11 +291,7 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
   float hv[NHS];
   {
     const int hcs = hslot / 9, hpy = hslot - (hslot / 9) * 9;
-#ifdef YS_ABL_HALO  // ablation: every window loads window (1, 1)'s halo (L2-hot)
-    const int hh = 7 - 1 + hpy, wc = 7 - 1 + hl_px;
-#else
     const int hh = wy * 7 - 1 + hpy, wc = wx * 7 - 1 + hl_px;
-#endif
     const bool ok = hl_r < 7 && hslot < 27 && (unsigned)hh < (unsigned)H && (unsigned)wc < (unsigned)W;
     const unsigned voff = ok ? (unsigned)((hcs * HWi + hh * W + wc) * 4) : OOB;
     const unsigned vlast = (3 * (NHS - 1) + hcs < C) ? voff : OOB;
@@ -357,28 +333,6 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
   }
   __syncthreads();
   X3_STAMP(1);
-#ifdef YS_OLD_DW
-  for (int item = tid; item < C * 7; item += 256) {
-    const int iy = item / C;
-    const float* hp = halo + (dw_c * 9 + iy) * HPW;
-    float r[3][12];
-#pragma unroll
-    for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-      for (int q4 = 0; q4 < 3; ++q4) {
-        const float4 v = *reinterpret_cast<const float4*>(hp + ky * HPW + 4 * q4);
-        r[ky][4 * q4] = v.x; r[ky][4 * q4 + 1] = v.y; r[ky][4 * q4 + 2] = v.z; r[ky][4 * q4 + 3] = v.w;
-      }
-    const bool rowok = wy * 7 + iy < H;
-#pragma unroll
-    for (int ix = 0; ix < 7; ++ix) {
-      const float v = dwk[0] * r[0][ix] + dwk[1] * r[0][ix + 1] + dwk[2] * r[0][ix + 2] + dwk[3] * r[1][ix] +
-                      dwk[4] * r[1][ix + 1] + dwk[5] * r[1][ix + 2] + dwk[6] * r[2][ix] + dwk[7] * r[2][ix + 1] +
-                      dwk[8] * r[2][ix + 2];
-      T[(iy * 7 + ix) * LT + dw_c] = (rowok && wx * 7 + ix < W) ? v : 0.f;
-    }
-  }
-#else
   {
     // wave w computes output rows 2w and 2w + 1 (wave 3: row 6) of channel dw_c: the four halo rows they need are
     // read once (12 16-byte LDS reads for 14 outputs)
@@ -403,19 +357,14 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
         const bool rowok = wy * 7 + iy < H;
 #pragma unroll
         for (int ix = 0; ix < 7; ++ix) {
-#ifdef YS_ABL_DW
-          const float v = dwk[4] * r[d + 1][ix + 1];
-#else
           float v = dwk[0] * r[d][ix];  // one FMA per tap (a plain sum of products vectorises into pk_mul + add)
 #pragma unroll
           for (int t = 1; t < 9; ++t) v = fmaf(dwk[t], r[d + t / 3][ix + t % 3], v);
-#endif
           T[(iy * 7 + ix) * LT + dw_c] = (rowok && wx * 7 + ix < W) ? v : 0.f;
         }
       }
     }
   }
-#endif
   __syncthreads();
   X3_STAMP(2);
 
@@ -472,16 +421,7 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
         akv[1][rb][0] = f32x4{bv, bv, bv, bv};
       }
       gemm_x3<C, 1, PS, PL, false, SWZ>(P, f_q, akv[0], lane);
-#ifdef YS_OLD_V
-    static_assert(!SWZ, "diagnostic V layout: padded planes only");
-      {
-        const f32x4 b = *reinterpret_cast<const f32x4*>(par + P_BIN + (2 * C / 16 + wid) * 16 + 4 * g);
-        for (int rb = 0; rb < 4; ++rb) akv[1][rb][0] = b;
-      }
-      gemm_x3<C, 1, PS, PL, false, SWZ>(P, f_n, akv[1], lane);
-#else
       gemm_x3<C, 1, PS, PL, true, SWZ>(P, f_n, akv[1], lane);
-#endif
     }
   }
   WP<C, 1> f_o;
@@ -494,23 +434,10 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
     if (tok < NR) store_planes4<PSK, KPL, false, SWZ>(Kp, tok, wid * 16 + 4 * g, akv[0][rb][0]);  // K, V, Q stay x64
     rng = range_acc(range_acc(rng, akv[0][rb][0]), akv[1][rb][0]);
     uint2 h, l;
-#ifdef YS_OLD_V
-    split4(akv[1][rb][0], h, l);
-    h16_t* vd = Vt + (wid * 16 + 4 * g) * PSV + tok;
-    vd[0] = (h16_t)(h.x & 0xffffu);
-    vd[PSV] = (h16_t)(h.x >> 16);
-    vd[2 * PSV] = (h16_t)(h.y & 0xffffu);
-    vd[3 * PSV] = (h16_t)(h.y >> 16);
-    vd[VPL] = (h16_t)(l.x & 0xffffu);
-    vd[VPL + PSV] = (h16_t)(l.x >> 16);
-    vd[VPL + 2 * PSV] = (h16_t)(l.y & 0xffffu);
-    vd[VPL + 3 * PSV] = (h16_t)(l.y >> 16);
-#else
     split4(akv[1][rb][0], h, l);  // V^T[d = wid*16 + l15][keys rb*16 + 4g .. +3]
     h16_t* vd = Vt + plane_off8<PSV, SWZ>(wid * 16 + l15, rb * 16 + 4 * g);
     *reinterpret_cast<uint2*>(vd) = h;
     *reinterpret_cast<uint2*>(vd + VPL) = l;
-#endif
   }
   // this wave's queries as the B operand of S^T = K Q^T, per head: k slot j of lane group g is head dim
   // 4g + j (j < 4) or 16 + 4g + j - 4 (the lane's own two Q column blocks); K is read with the same permutation
@@ -527,7 +454,7 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
   __syncthreads();  // K / V planes complete
   X3_STAMP(7);
   WP<C, 1> f_1a;
-  if constexpr (!SPLIT) load_wp(p.w1, HID, C, 0, wid, f_1a, lane);  // MLP1 (hidden half 0) planes
+  load_wp(p.w1, HID, C, 0, wid, f_1a, lane);  // MLP1 (hidden half 0) planes
 
   // ---- attention on fp16 two-term splits, wave = 16 queries, all heads: S^T[key][q] (keys 0..63 in four 16-row
   // blocks; keys >= 49 masked) -> softmax over keys (raw scores, exp2, 1/sum applied to O) -> O^T = V^T P^T with
@@ -571,11 +498,7 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
       for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-#ifdef YS_ABL_EXP
-          const float e = fmaf(st[hh][kb][r], c2, mc);
-#else
           const float e = __builtin_amdgcn_exp2f(fmaf(st[hh][kb][r], c2, mc));
-#endif
           st[hh][kb][r] = e;
           sum += e;
         }
@@ -624,30 +547,13 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
 
   // ---- T += O Wo^T + bo ----
   WP<C, 1> f_1b;
-  if constexpr (!SPLIT) load_wp(p.w1, HID, C, 0, wid + 4, f_1b, lane);  // MLP1 (hidden half 1) planes
+  load_wp(p.w1, HID, C, 0, wid + 4, f_1b, lane);  // MLP1 (hidden half 1) planes
   {
     f32x4 acc[4][1];
     const f32x4 b = *reinterpret_cast<const f32x4*>(par + P_BO + wid * 16 + 4 * g);
 #pragma unroll
     for (int rb = 0; rb < 4; ++rb) acc[rb][0] = b;
     gemm_x3<C, 1, PS, PL, false, SWZ>(P, f_o, acc, lane);
-    if constexpr (SPLIT) {
-      // T1 = T + O Wo^T + bo of this wave's column block, straight from the accumulators to the token-major buffer:
-      // the 4 lane groups of a token write 64 contiguous bytes; cropped and padded tokens are not stored
-#pragma unroll
-      for (int rb = 0; rb < 4; ++rb) {
-        const int tok = rb * 16 + l15;
-        const int iy = tok / 7, ix = tok - (tok / 7) * 7;
-        const int hh = wy * 7 + iy, wc = wx * 7 + ix;
-        if (tok < NR && hh < H && wc < W) {
-          const f32x4 v = *reinterpret_cast<const f32x4*>(T + tok * LT + wid * 16 + 4 * g) + acc[rb][0] * (1.0f / WSC);
-          *reinterpret_cast<f32x4*>(p.t1 + ((long)img * HWi + hh * W + wc) * C + wid * 16 + 4 * g) = v;
-        }
-      }
-      range_report(p.range_flag, rng);
-      prep_report(p.prep_flag, p.range_flag);
-      return;
-    }
 #pragma unroll
     for (int rb = 0; rb < 4; ++rb) {
       const int tok = rb * 16 + l15;
@@ -676,18 +582,12 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
     const f32x4 b = *reinterpret_cast<const f32x4*>(par + P_B1 + (wid + 4 * half) * 16 + 4 * g);
 #pragma unroll
     for (int rb = 0; rb < 4; ++rb) acc[rb][0] = b;
-#ifndef YS_ABL_MLPMFMA
     gemm_x3<C, 1, PS, PL, false, SWZ>(P, half == 0 ? f_1a : f_1b, acc, lane);
-#endif
 #pragma unroll
     for (int rb = 0; rb < 4; ++rb) {
       const f32x4 a = acc[rb][0] * (1.0f / WSC);
-#ifdef YS_ABL_GELU  // ablation builds only (timing sensitivity; wrong results)
-      const f32x2 lo = f32x2{a[0], a[1]}, hi = f32x2{a[2], a[3]};
-#else
       const f32x2 lo = gelu2_fast_(f32x2{a[0], a[1]});
       const f32x2 hi = gelu2_fast_(f32x2{a[2], a[3]});
-#endif
       hid[half][rb] = f32x4{lo.x, lo.y, hi.x, hi.y};
     }
   }
@@ -711,10 +611,8 @@ __global__ __launch_bounds__(256, 3) void swin_x3_kernel(Args p) {
     }
   __syncthreads();
   X3_STAMP(13);
-#ifndef YS_ABL_MLPMFMA
   gemm_x3<C, 1, PSH, PLH>(P, f_2a, acc2, lane);
   gemm_x3<C, 1, PSH, PLH>(P + 64, f_2b, acc2, lane);  // hidden columns 64..127
-#endif
 
   // pw planes and this lane's residual x / BN terms: in flight during the final T update
   WP<C, 1> f_pw;
@@ -1341,255 +1239,10 @@ __global__ __launch_bounds__(NT, 1) void swin_wx_kernel(Args p) {
 }
 }  // namespace wx
 
-// k-permuted fragment-major weight layout of the token-tiled kernel: the A-operand fragment of (16-row block n/16,
-// 32-k step k/32) is 64 lanes x 8 halves contiguous, and slot j of lane group g holds input channel
-// 32s + 4g + j (j < 4) or 32s + 16 + 4g + j - 4 - the order in which a 16x16 output tile sits in the lanes (lane
-// (g, l15): rows 4g .. 4g + 3 of the block, column l15), so one GEMM's accumulators are the next GEMM's B operand as
-// they stand (two 16-row output blocks per 32-k step)
-__device__ __forceinline__ long frag_perm_index(int n, int k, int K) {
-  const int kk = k & 31, gq = (kk & 15) >> 2, j = ((kk >> 4) << 2) | (kk & 3);
-  return ((long)((n >> 4) * (K >> 5) + (k >> 5)) * 64 + (gq << 4) + (n & 15)) * 8 + j;
-}
-
-// ---- the per-token half of the C = 64 block, token-tiled (the block split at the attention residual) --------------
-// After the attention residual every step is per token - LN2, MLP, residual (blocks_transformer.py:122-129), then
-// window_reverse / crop and pw 1x1, BN, SiLU, + x (:160-171) - and the padded tokens are cropped, so this half needs no
-// window structure and no 49 -> 64 row padding. One 512-thread workgroup per CU holds the 80 KB of weight planes (W1'
-// with the LN2 affine folded, W2, Wpw; x64, fp16 two-term splits, k-permuted) resident in LDS; each wave runs 32-token
-// tiles (two 16-token MFMA column blocks) through LN2 -> MLP1 -> GELU -> MLP2 (+ residual) -> pw -> BN -> SiLU -> + x
-// in registers, with no barrier after the weight load: the weights are the MFMA A operand and the tokens the B
-// operand, so each GEMM's output tile is the next one's B operand (frag_perm_index). LN2's statistics are the sum
-// over the four lane groups of a token (permlane swaps). The next tile's T1 loads are in flight while a tile computes.
-namespace tok {
-constexpr int C = 64, HID = 128;
-constexpr int NW = 8, NT = 64 * NW;
-constexpr int W1_OFF = 0, W2_OFF = 2 * HID * C, WP_OFF = W2_OFF + 2 * C * HID, WALL = WP_OFF + 2 * C * C;  // halves
-constexpr int P_B1 = 0, P_B2 = HID, P_SC = HID + C, P_SH = HID + 2 * C, NPAR = HID + 3 * C;
-constexpr unsigned OOB = 0x80000000u;
-
-struct Args {
-  const float* t1;  // [ntok][C] token-major: T after the attention residual (swin_x3_kernel<64, 2, true>)
-  const float* x;   // [B][C][HW]
-  float* y;         // [B][C][HW]
-  int B, HW;        // B * HW * C * 4 < 2^31 (the launcher chunks the batch)
-  const h16_t* wfrag;  // WALL halves: planes of W1' | W2 | Wpw in frag_perm_index order (x64)
-  const float* b1f;    // [HID], LN2 folded
-  const float* b2;     // [C]
-  const float* bn_sc;  // [C] folded BN
-  const float* bn_sh;
-  float ln2_eps;
-  unsigned* range_flag;
-  const unsigned* prep_flag;
-};
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, unsigned bytes) {
-  const unsigned long long a = (unsigned long long)base;
-  return __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(a >> 32)) << 32) |
-              (unsigned)__builtin_amdgcn_readfirstlane((unsigned)a)),
-      (short)0, __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
-}
-
-struct TileT {
-  f32x4 t[2][4];   // T1[token tb*16 + l15][cb*16 + 4g .. +3]
-  unsigned vx[2];  // byte offset of (img, channel 4g, pix) of token tb*16 + l15 in x / y, or OOB
-};
-
-// T1 of the 32 tokens of `tile` (tokens past ntok read as 0 and are not stored)
-__device__ __forceinline__ void load_tile(int tile, int ntok, int HW, __amdgpu_buffer_rsrc_t rt, int l15, int g,
-                                          TileT& in) {
-  const int p0 = tile * 32;
-  const int img0 = __builtin_amdgcn_readfirstlane(p0 / HW);
-#pragma unroll
-  for (int tb = 0; tb < 2; ++tb) {
-    const int pt = p0 + tb * 16 + l15;
-    int img = img0, pix = pt - img0 * HW;
-    while (pix >= HW) {  // a tile spans several images when HW < 32
-      pix -= HW;
-      ++img;
-    }
-    const bool ok = pt < ntok;
-#ifdef YS_ABL_TOKT1  // ablation builds only: every tile reads tile 0's T1 (L2-hot)
-    const unsigned vt = ok ? (unsigned)(tb * 16 + l15) * (C * 4) + 16 * g : OOB;
-#else
-    const unsigned vt = ok ? (unsigned)pt * (C * 4) + 16 * g : OOB;
-#endif
-    in.vx[tb] = ok ? (unsigned)(((img * C + 4 * g) * HW + pix) * 4) : OOB;
-#pragma unroll
-    for (int cb = 0; cb < 4; ++cb)
-      in.t[tb][cb] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rt, vt, cb * 64, 0));
-  }
-}
-
-__device__ __forceinline__ void mlp_tile(const TileT& in, const f16x8_t* wf, const float* par, float eps, int HW,
-                                         __amdgpu_buffer_rsrc_t rx, __amdgpu_buffer_rsrc_t ry, int g, float& rng) {
-  // compiler-only fence (no instruction): the weight fragments are re-read from LDS in every tile instead of being
-  // hoisted out of the tile loop as 320 loop-invariant registers
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);
-  // residual x of this tile's outputs (needed last: in flight through the whole tile)
-  float xr[2][16];
-#pragma unroll
-  for (int tb = 0; tb < 2; ++tb)
-#pragma unroll
-    for (int c = 0; c < 16; ++c)
-#ifdef YS_ABL_TOKMEM  // ablation builds only (timing; wrong results): no x loads, no y stores
-      xr[tb][c] = 0.f;
-#else
-      xr[tb][c] = __builtin_bit_cast(
-          float, __builtin_amdgcn_raw_buffer_load_b32(rx, in.vx[tb], ((c >> 2) * 16 + (c & 3)) * HW * 4, 0));
-#endif
-  // LN2 (normalisation only; the affine is folded into W1') as the B operand of MLP1, k step s = column blocks 2s, 2s+1
-  f16x8_t uh[2][2], ul[2][2];
-#pragma unroll
-  for (int tb = 0; tb < 2; ++tb) {
-    const f32x4* v = in.t[tb];
-    float s = 0.f;
-#pragma unroll
-    for (int cb = 0; cb < 4; ++cb) s += (v[cb].x + v[cb].y) + (v[cb].z + v[cb].w);
-    const float mean = xor32_sum(xor16_sum(s)) * (1.0f / (float)C);
-    f32x4 d[4];
-    float q = 0.f;
-#pragma unroll
-    for (int cb = 0; cb < 4; ++cb) {
-      d[cb] = v[cb] - mean;
-      q += (d[cb].x * d[cb].x + d[cb].y * d[cb].y) + (d[cb].z * d[cb].z + d[cb].w * d[cb].w);
-    }
-    const float rs = __builtin_amdgcn_rsqf(xor32_sum(xor16_sum(q)) * (1.0f / (float)C) + eps);
-    split8(d[0] * rs, d[1] * rs, uh[tb][0], ul[tb][0]);
-    split8(d[2] * rs, d[3] * rs, uh[tb][1], ul[tb][1]);
-  }
-  // MLP: hidden column blocks in pairs (one 32-k step of MLP2 each): MLP1 (+ b1') -> GELU -> split -> MLP2 partial
-  f32x4 acc2[2][4];
-#pragma unroll
-  for (int nb = 0; nb < 4; ++nb) {
-    const f32x4 b = *reinterpret_cast<const f32x4*>(par + P_B2 + nb * 16 + 4 * g);
-    acc2[0][nb] = b;
-    acc2[1][nb] = b;
-  }
-#pragma unroll
-  for (int s2 = 0; s2 < HID / 32; ++s2) {
-    f32x4 h[2][2];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int nb = 2 * s2 + q;
-      const f32x4 b = *reinterpret_cast<const f32x4*>(par + P_B1 + nb * 16 + 4 * g);
-      h[0][q] = b;
-      h[1][q] = b;
-#pragma unroll
-      for (int s = 0; s < C / 32; ++s) {
-        const int f = (W1_OFF / 512) + nb * (C / 32) + s;
-        const f16x8_t whi = wf[f * 64], wlo = wf[(f + HID * C / 512) * 64];
-#pragma unroll
-        for (int tb = 0; tb < 2; ++tb) h[tb][q] = mfma_f16x3(whi, wlo, uh[tb][s], ul[tb][s], h[tb][q]);
-      }
-    }
-    f16x8_t gh[2], gl[2];
-#pragma unroll
-    for (int tb = 0; tb < 2; ++tb) {
-      f32x4 gv[2];
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const f32x4 a = h[tb][q] * (1.0f / WSC);
-        const f32x2 lo = gelu2_fast_(f32x2{a[0], a[1]});
-        const f32x2 hi = gelu2_fast_(f32x2{a[2], a[3]});
-        gv[q] = f32x4{lo.x, lo.y, hi.x, hi.y};
-      }
-      rng = range_acc(range_acc(rng, gv[0]), gv[1]);
-      split8(gv[0], gv[1], gh[tb], gl[tb]);
-    }
-#pragma unroll
-    for (int nb = 0; nb < 4; ++nb) {
-      const int f = (W2_OFF / 512) + nb * (HID / 32) + s2;
-      const f16x8_t whi = wf[f * 64], wlo = wf[(f + C * HID / 512) * 64];
-#pragma unroll
-      for (int tb = 0; tb < 2; ++tb) acc2[tb][nb] = mfma_f16x3(whi, wlo, gh[tb], gl[tb], acc2[tb][nb]);
-    }
-  }
-  // T2 = T1 + MLP as the pw GEMM's B operand
-  f16x8_t th[2][2], tl[2][2];
-#pragma unroll
-  for (int tb = 0; tb < 2; ++tb) {
-    f32x4 t2[4];
-#pragma unroll
-    for (int nb = 0; nb < 4; ++nb) {
-      t2[nb] = in.t[tb][nb] + acc2[tb][nb] * (1.0f / WSC);
-      rng = range_acc(rng, t2[nb]);
-    }
-    split8(t2[0], t2[1], th[tb][0], tl[tb][0]);
-    split8(t2[2], t2[3], th[tb][1], tl[tb][1]);
-  }
-  // y = x + SiLU(BN(Wpw T2)): lane (g, l15) holds channels nb*16 + 4g + r of token l15 (16 lanes = 64 contiguous bytes)
-#pragma unroll
-  for (int nb = 0; nb < 4; ++nb) {
-    f32x4 o[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-    for (int s = 0; s < C / 32; ++s) {
-      const int f = (WP_OFF / 512) + nb * (C / 32) + s;
-      const f16x8_t whi = wf[f * 64], wlo = wf[(f + C * C / 512) * 64];
-#pragma unroll
-      for (int tb = 0; tb < 2; ++tb) o[tb] = mfma_f16x3(whi, wlo, th[tb][s], tl[tb][s], o[tb]);
-    }
-    const f32x4 sc = *reinterpret_cast<const f32x4*>(par + P_SC + nb * 16 + 4 * g);
-    const f32x4 sh = *reinterpret_cast<const f32x4*>(par + P_SH + nb * 16 + 4 * g);
-#pragma unroll
-    for (int tb = 0; tb < 2; ++tb)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float out = xr[tb][4 * nb + r] + silu_fast_(o[tb][r] * sc[r] + sh[r]);
-#ifdef YS_ABL_TOKMEM
-        if (out == 1234.5f)  // keeps the arithmetic alive; (practically) never stores
-#endif
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, out), ry, in.vx[tb], (nb * 16 + r) * HW * 4,
-                                              0);
-      }
-  }
-}
-
-__global__ __launch_bounds__(NT, 1) void swin_mlp_kernel(Args p) {
-  __shared__ __attribute__((aligned(16))) h16_t wsh[WALL];
-  __shared__ __attribute__((aligned(16))) float par[NPAR];
-  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int l15 = lane & 15, g = lane >> 4;
-  const int HW = p.HW;
-  const int ntok = p.B * HW;
-  const int ntile = (ntok + 31) >> 5;
-  const __amdgpu_buffer_rsrc_t rt = rsrc(p.t1, (unsigned)ntok * C * 4);
-  const __amdgpu_buffer_rsrc_t rx = rsrc(p.x, (unsigned)ntok * C * 4);
-  const __amdgpu_buffer_rsrc_t ry = rsrc(p.y, (unsigned)ntok * C * 4);
-  const int stride = gridDim.x * NW;
-  int tile = blockIdx.x * NW + wid;
-  TileT ta, tb_;
-  if (tile < ntile) load_tile(tile, ntok, HW, rt, l15, g, ta);  // in flight during the weight staging
-  for (int i = tid; i < WALL / 8; i += NT) reinterpret_cast<uint4*>(wsh)[i] = reinterpret_cast<const uint4*>(p.wfrag)[i];
-  for (int i = tid; i < NPAR; i += NT) {
-    float v;
-    if (i < P_B2) v = p.b1f[i] * WSC;  // biases x64 (the accumulators hold 64 x), BN scale / 64 (exact)
-    else if (i < P_SC) v = p.b2[i - P_B2] * WSC;
-    else if (i < P_SH) v = p.bn_sc[i - P_SC] * (1.0f / WSC);
-    else v = p.bn_sh[i - P_SH];
-    par[i] = v;
-  }
-  __syncthreads();
-  const f16x8_t* wf = reinterpret_cast<const f16x8_t*>(wsh) + lane;  // fragment f: wf[64 f]
-  float rng = 0.f;
-  while (tile < ntile) {  // two tiles per trip: the register sets alternate without copies
-    if (tile + stride < ntile) load_tile(tile + stride, ntok, HW, rt, l15, g, tb_);
-    mlp_tile(ta, wf, par, p.ln2_eps, HW, rx, ry, g, rng);
-    tile += stride;
-    if (tile >= ntile) break;
-    if (tile + stride < ntile) load_tile(tile + stride, ntok, HW, rt, l15, g, ta);
-    mlp_tile(tb_, wf, par, p.ln2_eps, HW, rx, ry, g, rng);
-    tile += stride;
-  }
-  range_report(p.range_flag, rng);
-  prep_report(p.prep_flag, p.range_flag);
-}
-}  // namespace tok
 
 // Weight preparation: LN affine folds and the three-plane split, one wave per output row (lanes along k,
 // coalesced); also the BN fold of the pw conv. Rows: [0,3C) in_proj (LN1 folded) | [3C,4C) out_proj | [4C,4C+HID)
-// mlp1 (LN2 folded) | mlp2 (K = HID) | pw | C BN entries. With `mfrag`, the mlp1 / mlp2 / pw planes are also written
-// in the token-tiled kernel's k-permuted order (frag_perm_index) as one contiguous block W1' | W2 | Wpw.
+// mlp1 (LN2 folded) | mlp2 (K = HID) | pw | C BN entries.
 struct PrepArgs {
   const float *win, *bin, *ln1_w, *ln1_b, *wo, *w1, *b1, *ln2_w, *ln2_b, *w2, *wpw;
   const float *bn_w, *bn_b, *bn_m, *bn_v;
@@ -1597,7 +1250,6 @@ struct PrepArgs {
   int C, HID;
   h16_t *pin, *po, *p1, *p2, *ppw;
   float *bin_f, *b1_f, *bn_sc, *bn_sh;
-  h16_t* mfrag;          // may be null
   unsigned* range_flag;  // split-range guard: 64 W' must stay finite in fp16
   unsigned* prep_flag;   // the same result kept in the prepared block (zeroed before the launch)
 };
@@ -1612,7 +1264,6 @@ __global__ __launch_bounds__(256) void swin_x3_prep_kernel(PrepArgs a) {
   const float* bsrc = nullptr;
   float* bdst = nullptr;
   h16_t* dst;
-  h16_t* mdst = nullptr;  // the k-permuted copy (token-tiled kernel), mlp1 / mlp2 / pw only
   int N, K;
   if (n < 3 * C) {
     src = a.win; gam = a.ln1_w; bet = a.ln1_b; bsrc = a.bin; bdst = a.bin_f; dst = a.pin; N = 3 * C; K = C;
@@ -1620,13 +1271,10 @@ __global__ __launch_bounds__(256) void swin_x3_prep_kernel(PrepArgs a) {
     src = a.wo; dst = a.po; N = C; K = C;
   } else if ((n -= C) < HID) {
     src = a.w1; gam = a.ln2_w; bet = a.ln2_b; bsrc = a.b1; bdst = a.b1_f; dst = a.p1; N = HID; K = C;
-    mdst = a.mfrag;
   } else if ((n -= HID) < C) {
     src = a.w2; dst = a.p2; N = C; K = HID;
-    mdst = a.mfrag ? a.mfrag + 2 * HID * C : nullptr;
   } else if ((n -= C) < C) {
     src = a.wpw; dst = a.ppw; N = C; K = C;
-    mdst = a.mfrag ? a.mfrag + 4 * HID * C : nullptr;
   } else if ((n -= C) < C) {
     if (lane == 0) {
       const float inv = 1.0f / sqrtf(a.bn_v[n] + a.bn_eps);
@@ -1653,11 +1301,6 @@ __global__ __launch_bounds__(256) void swin_x3_prep_kernel(PrepArgs a) {
     const long fi = ((long)((n >> 4) * (K >> 5) + (k >> 5)) * 64 + (((k & 31) >> 3) << 4) + (n & 15)) * 8 + (k & 7);
     dst[fi] = __builtin_bit_cast(h16_t, h);
     dst[(long)N * K + fi] = __builtin_bit_cast(h16_t, l);
-    if (mdst) {
-      const long fp = frag_perm_index(n, k, K);
-      mdst[fp] = __builtin_bit_cast(h16_t, h);
-      mdst[(long)N * K + fp] = __builtin_bit_cast(h16_t, l);
-    }
   }
   if (bdst) {
     bacc = wave_sum(bacc);
@@ -1694,48 +1337,6 @@ bool yolosod_swin_x3_ok(int C, int num_heads, int wh, int ww, int mlp_hidden) {
          ((C == 64 && num_heads == 2) || (C == x3::wx::C && num_heads == C / x3::wx::HD));
 }
 
-// C = 64 blocks split at the attention residual (opt-in, YOLOSOD_SWIN_SPLIT=1; measured slower than the one-kernel
-// swin_x3_kernel): swin_x3_kernel<64, 2, true> (attention half, per window) +
-// tok::swin_mlp_kernel (per-token half, token-tiled)
-static int g_swin_split = -1;
-static bool swin_split_env() {
-  if (g_swin_split < 0) {
-    const char* e = getenv("YOLOSOD_SWIN_SPLIT");
-    g_swin_split = (e && e[0] == '1') ? 1 : 0;
-  }
-  return g_swin_split != 0;
-}
-// Test hook: C = 64 fp16-split SwinBlocks as the split pair (1) or the one-kernel form (0); returns the previous state.
-YS_EXPORT int yolosod_debug_set_swin_split(int on) {
-  const int prev = swin_split_env() ? 1 : 0;
-  g_swin_split = on ? 1 : 0;
-  return prev;
-}
-static bool x3_split(int C) { return C == x3::tok::C && swin_split_env(); }
-
-// C = 64 kernel planes: chunk-swizzled unpadded rows (1, default; env YOLOSOD_X3_SWZ=0: rows padded to 80)
-static int g_x3_swz = -1;
-static bool x3_swz_env() {
-  if (g_x3_swz < 0) {
-    const char* e = getenv("YOLOSOD_X3_SWZ");
-    g_x3_swz = (e && e[0] == '0') ? 0 : 1;
-  }
-  return g_x3_swz != 0;
-}
-// Test hook: the C = 64 kernel's plane layout, swizzled (1) or padded (0); returns the previous state.
-YS_EXPORT int yolosod_debug_set_x3_swz(int on) {
-  const int prev = x3_swz_env() ? 1 : 0;
-  g_x3_swz = on ? 1 : 0;
-  return prev;
-}
-
-// images per launch of the split pair: the token-tiled kernel addresses x / y / T1 with 32-bit buffer offsets
-static int x3_split_chunk(int C, int H, int W) {
-  const long per = (long)C * H * W * 4;
-  const long n = ((1L << 31) - 1) / (per > 0 ? per : 1);
-  return n < 1 ? 1 : (n > (1L << 30) ? (1 << 30) : (int)n);
-}
-
 size_t yolosod_swin_x3_workspace(int C, int mlp_hidden) {
   Sizer s;
   s.take<h16_t>((size_t)2 * 3 * C * C);            // in_proj planes
@@ -1744,25 +1345,19 @@ size_t yolosod_swin_x3_workspace(int C, int mlp_hidden) {
   s.take<h16_t>((size_t)2 * C * mlp_hidden);       // mlp2
   s.take<h16_t>((size_t)2 * C * C);                // pw
   s.take<float>((size_t)3 * C + mlp_hidden + 2 * C);  // folded biases, BN scale / shift
-  s.take<h16_t>((size_t)2 * (2 * mlp_hidden * C + C * C));  // mlp1 | mlp2 | pw, k-permuted (token-tiled kernel)
   s.take<unsigned>(1);                             // the weights' split-range result
   return s.off;
 }
 
-// scratch of one run on a prepared block: T after the attention residual for one chunk of images (split path only)
-size_t yolosod_swin_x3_run_workspace(int B, int C, int H, int W) {
-  if (!x3_split(C) || B <= 0) return 0;
-  const int bc = x3_split_chunk(C, H, W);
-  return (size_t)(B < bc ? B : bc) * H * W * C * sizeof(float);
-}
+// scratch of one run on a prepared block: none (every fp16-split Swin kernel is one launch)
+size_t yolosod_swin_x3_run_workspace(int B, int C, int H, int W) { return 0; }
 
 // The prepared-parameter block of the fp16-split kernels (written by swin_x3_prep_kernel): weight planes of in_proj
-// (LN1 folded), out_proj, mlp1 (LN2 folded), mlp2, pw; folded in_proj / mlp1 biases; BN scale / shift; the k-permuted
-// mlp1 / mlp2 / pw planes of the token-tiled kernel; the weights' split-range word.
+// (LN1 folded), out_proj, mlp1 (LN2 folded), mlp2, pw; folded in_proj / mlp1 biases; BN scale / shift; the weights'
+// split-range word.
 struct X3Prep {
   h16_t *pin, *po, *p1, *p2, *ppw;
   float *bin_f, *b1_f, *bn_sc, *bn_sh;
-  h16_t* mfrag;
   unsigned* pflag;
 };
 static bool x3_carve(void* buf, size_t bytes, int C, int mlp_hidden, X3Prep& q) {
@@ -1773,9 +1368,8 @@ static bool x3_carve(void* buf, size_t bytes, int C, int mlp_hidden, X3Prep& q) 
   q.p2 = cv.take<h16_t>((size_t)2 * C * mlp_hidden);
   q.ppw = cv.take<h16_t>((size_t)2 * C * C);
   float* fb = cv.take<float>((size_t)3 * C + mlp_hidden + 2 * C);
-  q.mfrag = cv.take<h16_t>((size_t)2 * (2 * mlp_hidden * C + C * C));
   q.pflag = cv.take<unsigned>(1);
-  if (!fb || !q.mfrag || !q.pflag) return false;
+  if (!fb || !q.pflag) return false;
   q.bin_f = fb;
   q.b1_f = fb + 3 * C;
   q.bn_sc = fb + 3 * C + mlp_hidden;
@@ -1800,7 +1394,7 @@ int yolosod_swin_x3_prepare(int C, int mlp_hidden, const float* ln1_w, const flo
   }
   x3::PrepArgs pa{in_proj_w, in_proj_b, ln1_w, ln1_b, out_proj_w, mlp1_w, mlp1_b, ln2_w, ln2_b, mlp2_w, pw_w,
                   bn_w, bn_b, bn_mean, bn_var, bn_eps, C, mlp_hidden, q.pin, q.po, q.p1, q.p2, q.ppw,
-                  q.bin_f, q.b1_f, q.bn_sc, q.bn_sh, q.mfrag, range_flag_dev(), q.pflag};
+                  q.bin_f, q.b1_f, q.bn_sc, q.bn_sh, range_flag_dev(), q.pflag};
   const int rows = 3 * C + C + mlp_hidden + C + C + C;
   hipLaunchKernelGGL(x3::swin_x3_prep_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, pa);
   hipError_t e = hipGetLastError();
@@ -1809,18 +1403,6 @@ int yolosod_swin_x3_prepare(int C, int mlp_hidden, const float* ln1_w, const flo
     return -1;
   }
   return 0;
-}
-
-static int cu_count() {
-  static int n[64] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-  if (!n[dev]) {
-    int c = 0;
-    if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) c = 256;
-    n[dev] = c;
-  }
-  return n[dev];
 }
 
 // the kernels on a prepared block; returns 1 if launched, 0 if the shape is not handled, < 0 on error. `ws` is the
@@ -1838,44 +1420,11 @@ int yolosod_swin_x3_run(const float* x, float* y, int B, int C, int H, int W, in
   }
   unsigned* flag = range_flag_dev();
   x3::Args a{x, y, B, H, W, nWx, nWin, dw_w, ln1_eps, ln2_eps, q.pin, q.bin_f, q.po, out_proj_b, q.p1, q.b1_f, q.p2,
-             mlp2_b, q.ppw, q.bn_sc, q.bn_sh, 1.0f / sqrtf((float)(C / num_heads)), flag, q.pflag, nullptr};
+             mlp2_b, q.ppw, q.bn_sc, q.bn_sh, 1.0f / sqrtf((float)(C / num_heads)), flag, q.pflag};
   const long nwin = (long)B * nWin;
   if (nwin == 0) return 1;
-  if (x3_split(C)) {
-    const size_t need = yolosod_swin_x3_run_workspace(B, C, H, W);
-    if (!ws || ws_bytes < need) {
-      set_error("swin_x3: split-path scratch too small (%zu < %zu)", ws_bytes, need);
-      return -1;
-    }
-    const int bc = x3_split_chunk(C, H, W);
-    const long img_el = (long)C * H * W;
-    for (int b0 = 0; b0 < B; b0 += bc) {
-      const int nb = B - b0 < bc ? B - b0 : bc;
-      x3::Args ac = a;
-      ac.x = x + b0 * img_el;
-      ac.y = y + b0 * img_el;
-      ac.B = nb;
-      ac.t1 = (float*)ws;
-      const long nw = (long)nb * nWin;
-      if (x3_swz_env())
-        hipLaunchKernelGGL((x3::swin_x3_kernel<64, 2, true, true>), dim3((unsigned)(8 * ((nw + 7) / 8))), dim3(256), 0,
-                           st, ac);
-      else
-        hipLaunchKernelGGL((x3::swin_x3_kernel<64, 2, true>), dim3((unsigned)(8 * ((nw + 7) / 8))), dim3(256), 0, st,
-                           ac);
-      x3::tok::Args tk{(const float*)ws, ac.x, ac.y, nb, H * W, q.mfrag, q.b1_f, mlp2_b, q.bn_sc, q.bn_sh, ln2_eps,
-                       flag, q.pflag};
-      const long ntile = ((long)nb * H * W + 31) / 32;
-      const long want = (ntile + x3::tok::NW - 1) / x3::tok::NW;
-      const int grid = (int)(want < cu_count() ? want : cu_count());
-      hipLaunchKernelGGL(x3::tok::swin_mlp_kernel, dim3(grid), dim3(x3::tok::NT), 0, st, tk);
-    }
-  } else if (C == 64) {
-    if (x3_swz_env())
-      hipLaunchKernelGGL((x3::swin_x3_kernel<64, 2, false, true>), dim3((unsigned)(8 * ((nwin + 7) / 8))), dim3(256), 0,
-                         st, a);
-    else
-      hipLaunchKernelGGL((x3::swin_x3_kernel<64, 2>), dim3((unsigned)(8 * ((nwin + 7) / 8))), dim3(256), 0, st, a);
+  if (C == 64) {
+    hipLaunchKernelGGL((x3::swin_x3_kernel<64, 2>), dim3((unsigned)(8 * ((nwin + 7) / 8))), dim3(256), 0, st, a);
   } else {
     hipLaunchKernelGGL(x3::wx::swin_wx_kernel, dim3((unsigned)(8 * ((nwin + 7) / 8))), dim3(x3::wx::NT), 0, st, a);
   }

@@ -586,9 +586,9 @@ YS_EXPORT size_t yolosod_swin_workspace_bf16(int B, int C, int H, int W, int num
   return s.off;
 }
 
-// tokens + LN1 in one pass (swin_tokens_ln_bf16_kernel; YOLOSOD_SWIN_TOKLN=0 selects the two-kernel form)
+// tokens + LN1 in one pass (swin_tokens_ln_bf16_kernel; the test hook selects the two-kernel form)
 static int& tokens_ln_mode() {
-  static int on = [] { const char* e = getenv("YOLOSOD_SWIN_TOKLN"); return (!e || atoi(e) != 0) ? 1 : 0; }();
+  static int on = 1;
   return on;
 }
 static bool tokens_ln_env() { return tokens_ln_mode() != 0; }

@@ -114,18 +114,13 @@ def _act_code(act):
     return None
 
 
-# 1x1 convs as the library's fused fp32 MFMA GEMM instead of MIOpen (+ epilogue pass). Off by default: at the
-# bs=32 640x640 shapes MIOpen's 1x1 kernels were faster end to end (1526 vs 1356 images/s); kept for A/B work.
-CONV1X1_GEMM = os.environ.get("YOLOSOD_CONV1X1", "0") == "1"
 # thin 1x1 convs (Cout 64, Cin <= 256, H*W % 64 == 0) as one fused HIP kernel instead of MIOpen + epilogue
 # (scripts/bench_conv1x1.py: 96->64 at 160^2 0.16 vs 0.38 ms; at Cout 128 the MIOpen path stays faster)
 THIN1X1 = os.environ.get("YOLOSOD_THIN1X1", "1") == "1"
 # the Detect head's 3x3 tower convs (64 outputs) as the library's fp16-split implicit-GEMM kernel (csrc/conv3x3.hip)
-# instead of MIOpen + the epilogue pass, when the launch has >= CONV3X3_MIN_TILES tiles of 8 x 32 pixels (0: every
-# tower conv; the first kernel was slower than MIOpen below 256 tiles, e.g. P5's 20 x 20 maps, the current one is
-# faster at every tower shape: scripts/bench_conv3x3.py). YOLOSOD_CONV3X3=0 restores MIOpen (A/B), =force takes every
-# tower conv whatever its size (tests), =all also takes every other eligible 3x3 conv of the model (the backbone
-# stays on MIOpen by default, as north_star asks)
+# instead of MIOpen + the epilogue pass (faster at every tower shape, P5's 20 x 20 maps included:
+# scripts/bench_conv3x3.py). YOLOSOD_CONV3X3=0 restores MIOpen (A/B), =all also takes every other eligible 3x3 conv of
+# the model (the backbone stays on MIOpen by default, as north_star asks)
 CONV3X3 = os.environ.get("YOLOSOD_CONV3X3", "1")
 # the PAN neck's 3x3 / stride-2 convs (layers 29 / 33 / 36 of the paper YAML: the consumers of Swin L28 and CA L32,
 # and P4 -> P5) on the stride-2 fp16-split kernel (csrc/conv3x3s2.hip), writing straight into their Concat slice,
@@ -137,7 +132,6 @@ S1_NECK = os.environ.get("YOLOSOD_S1_NECK", "1") != "0"
 # the PAN neck's wide 1x1 convs (Cout a multiple of 128: C2f cv1 / cv2, lateral convs) on the fp16-split 1x1 kernel
 # (csrc/conv1x1x2.hip) with bias / SiLU / concat slice / C2f's dual store in its epilogue; YOLOSOD_N1_NECK=0: MIOpen
 N1_NECK = os.environ.get("YOLOSOD_N1_NECK", "1") != "0"
-CONV3X3_MIN_TILES = int(os.environ.get("YOLOSOD_CONV3X3_MIN_TILES", "0"))
 # the neck C2fs' Bottlenecks (stride-1 fp16-split kernel) read their inputs as slices of the C2f buffer instead of
 # packed copies written by a second store (YOLOSOD_C2F_SLICES=0: the dual-store form)
 C2F_SLICES = os.environ.get("YOLOSOD_C2F_SLICES", "1") != "0"
@@ -174,8 +168,7 @@ def conv_epilogue(conv: nn.Conv2d, act_code, x, out=None, res=None, stats=None, 
                                          out=out, out2=out2, c2lo=c2lo)
         x = x.materialize()
     if (split and act_code == 1 and out is None and res is None and stats is None and out2 is None and CONV3X3 != "0"
-            and (CONV3X3 == "all" or tower) and _hip.conv3x3_ok(x, conv)
-            and (CONV3X3 == "force" or x.shape[0] * -(-x.shape[2] // 8) * -(-x.shape[3] // 32) >= CONV3X3_MIN_TILES)):
+            and (CONV3X3 == "all" or tower) and _hip.conv3x3_ok(x, conv)):
         prep = lambda: _cached(conv, "c3prep", (conv.weight,), lambda: _hip.conv3x3_prepare(conv.weight))  # noqa: E731
         return _hip.conv3x3_silu(x, conv.bias, prep, conv.out_channels)
     if (split and n1 and N1_NECK and act_code == 1 and res is None and stats is None and _hip.conv1x1x2_ok(x, conv)
@@ -196,15 +189,6 @@ def conv_epilogue(conv: nn.Conv2d, act_code, x, out=None, res=None, stats=None, 
             and (out is None or out.data_ptr() % 16 == 0) and (res is None or res.data_ptr() % 16 == 0)):
         return _hip.conv1x1_thin(x, conv.weight.detach().reshape(conv.out_channels, -1), conv.bias.detach(),
                                  out=out, res=res, out2=out2, c2lo=c2lo, stats=stats)
-    if (CONV1X1_GEMM and x.dtype == torch.float32 and conv.kernel_size == (1, 1) and conv.stride == (1, 1) and conv.groups == 1 and conv.padding == (0, 0)
-            and conv.in_channels % 32 == 0 and x.stride(1) == x.shape[2] * x.shape[3] and x.stride(3) == 1
-            and x.stride(2) == x.shape[3] and (x.shape[2] * x.shape[3]) % 4 == 0 and x.stride(0) % 4 == 0):
-        # 1x1 conv = GEMM on NCHW with the epilogue fused (no MIOpen layout transposes, no extra pass)
-        y = _hip.conv1x1(x, conv.weight.detach().reshape(conv.out_channels, -1), conv.bias.detach(), act_code,
-                         out=out, res=res)
-        if out2 is not None:
-            out2.copy_(y[:, c2lo:])
-        return y
     y = F.conv2d(x, conv.weight, None, conv.stride, conv.padding, conv.dilation, conv.groups)
     if (y.shape[2] * y.shape[3]) % 4 or y.dtype != x.dtype:
         y = y + conv.bias.view(1, -1, 1, 1)

@@ -48,12 +48,6 @@ STREAMS = int(_STREAMS_ENV) if _STREAMS_ENV is not None else 1
 # convs on the persistent fp16-split kernel two side streams are as fast (same box 3285 -> 3300 img/s, 2 x 2 runs,
 # profiles/r05/streams/): the default is 2.
 SIDE_STREAMS = max(1, int(os.environ.get("YOLOSOD_SIDE_STREAMS", "2")))
-# YOLOSOD_HEAD_SPLIT=1 (opt-in): the head's decode split at the last level - levels 0..nl-2 decoded once their towers
-# are done, while the last level's towers (which can only start when the neck's last feature map exists) still run
-# on the side streams. Same-box n640: 2273 vs 2258 img/s (+0.7 %), but the first part then shares the GPU with the
-# P5 towers (0.151 -> 0.181 ms) and the P5 part is a 25 us launch for 400 anchors, so the hot path's own time
-# grows (path roofline 0.312 -> 0.302); default: one launch after every tower
-HEAD_SPLIT = os.environ.get("YOLOSOD_HEAD_SPLIT", "0") == "1"
 # SE / CBAM whose only reader is the next layer, a fused 3x3 / stride-2 Conv (SE L1 -> L2, CBAM L4 -> L5 in the paper
 # YAML): the gate only, then the Conv applies it while staging its input (csrc/conv3x3s2.hip) - the gate's apply pass
 # and the conv's re-read of its output disappear. YOLOSOD_GATE_FUSE=0: the operator's own apply + MIOpen (A/B)
@@ -274,7 +268,6 @@ class BaseModel(nn.Module):
                 and det._fused_ok([x])):
             lvl = {j: k for k, j in enumerate(det.f)}
             towers = {}
-            tower_ev = {}  # level -> events recorded on its towers' side streams after them
             ready = []  # levels whose feature map exists but whose towers wait for the last MAFN op (STREAMS == 2)
             last_mafn = max((k for k, mm in enumerate(self.model)
                              if isinstance(mm, (M.SE, M.CBAM_Block, M.CA_Block, M.A2_Attn, M.SwinBlock))), default=-1)
@@ -367,17 +360,9 @@ class BaseModel(nn.Module):
                 x = buf
             elif m is det and towers is not None and len(towers) == det.nl:
                 feats = [towers[k] for k in range(det.nl)]
-                if HEAD_SPLIT and det.nl > 1:
-                    for k in range(det.nl - 1):
-                        for ev in tower_ev[k]:
-                            main.wait_event(ev)
-                    x = det.forward_towers(feats, lambda: [main.wait_event(ev) for ev in tower_ev[det.nl - 1]])
-                    for sd in side:  # every side stream's work is done before main goes on (as without the split)
-                        main.wait_stream(sd)
-                else:
-                    for sd in side:  # every level's tower features are ready (and owned by main from here)
-                        main.wait_stream(sd)
-                    x = det.forward_towers(feats)
+                for sd in side:  # every level's tower features are ready (and owned by main from here)
+                    main.wait_stream(sd)
+                x = det.forward_towers(feats)
             else:
                 x = m(inp)
             if towers is not None and m is not det:
@@ -388,7 +373,6 @@ class BaseModel(nn.Module):
                 if ready and (streams != 2 or m.i >= last_mafn):
                     for k, xk in ready:
                         feats = []
-                        tower_ev[k] = []
                         for tower in (det.cv2[k], det.cv3[k]):  # box, class tower (Detect.tower_features)
                             sd = side[rr % len(side)]
                             rr += 1
@@ -398,9 +382,6 @@ class BaseModel(nn.Module):
                                 f = tower[:-1](xk).contiguous()
                             f.record_stream(main)
                             feats.append(f)
-                            ev = torch.cuda.Event()
-                            ev.record(sd)
-                            tower_ev[k].append(ev)
                         towers[k] = tuple(feats)
                     ready = []
             y.append(x if m.i in self.save else None)
