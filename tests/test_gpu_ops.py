@@ -601,3 +601,24 @@ def test_sppf_pool_matches_chained_max_pools(shape, cuda):
     p3 = F.max_pool2d(p2, 5, 1, 2)
     assert torch.equal(z[:, :C], y0)
     assert torch.equal(z[:, C:2 * C], p1) and torch.equal(z[:, 2 * C:3 * C], p2) and torch.equal(z[:, 3 * C:], p3)
+
+
+def test_sppf_pool_propagates_nan(cuda):
+    """A NaN activation reaches every pooled output whose window holds it, as in the chained F.max_pool2d (ADVICE r05:
+    fmaxf would mask it)."""
+    import torch.nn.functional as F
+    g = torch.Generator().manual_seed(7)
+    z = torch.randn(2, 4 * 5, 20, 20, generator=g)
+    z[0, 1, 3, 4] = float("nan")
+    z[1, 4, 19, 0] = float("nan")
+    z[1, 2, 10, 10] = float("inf")
+    z = z.to(cuda)
+    y0 = z[:, :5].clone()
+    _hip.sppf_pool(z, 5)
+    p1 = F.max_pool2d(y0, 5, 1, 2)
+    p2 = F.max_pool2d(p1, 5, 1, 2)
+    p3 = F.max_pool2d(p2, 5, 1, 2)
+    for k, p in enumerate((p1, p2, p3), 1):
+        out = z[:, k * 5:(k + 1) * 5]
+        assert torch.equal(torch.isnan(out), torch.isnan(p)) and bool(torch.isnan(p).any())
+        assert torch.equal(torch.nan_to_num(out, nan=0.0), torch.nan_to_num(p, nan=0.0))

@@ -12,6 +12,9 @@ namespace ys {
 
 constexpr int SPPF_MAX_HW = 64 * 64;  // a plane and its three row-maximum planes in LDS (64 KB at the maximum)
 
+// NaN-propagating max, as max_pool2d's (a NaN anywhere in a window makes that output NaN; fmaxf would drop it)
+__device__ __forceinline__ float nan_max(float m, float v) { return (v > m || v != v) ? v : m; }
+
 // one 256-thread workgroup per (channel, image) plane: the plane is read once into LDS; row maxima of radius 2 / 4 / 6
 // (each extends the previous one), then column maxima of the same radius over them
 __global__ __launch_bounds__(256) void sppf_pool_kernel(float* __restrict__ z, long zbs, int C, int H, int W) {
@@ -28,18 +31,18 @@ __global__ __launch_bounds__(256) void sppf_pool_kernel(float* __restrict__ z, l
     float m = -INFINITY;
 #pragma unroll
     for (int d = -2; d <= 2; ++d)
-      if (x + d >= 0 && x + d < W) m = fmaxf(m, row[x + d]);
+      if (x + d >= 0 && x + d < W) m = nan_max(m, row[x + d]);
     rm[i] = m;
 #pragma unroll
     for (int d = 3; d <= 4; ++d) {
-      if (x - d >= 0) m = fmaxf(m, row[x - d]);
-      if (x + d < W) m = fmaxf(m, row[x + d]);
+      if (x - d >= 0) m = nan_max(m, row[x - d]);
+      if (x + d < W) m = nan_max(m, row[x + d]);
     }
     rm[HW + i] = m;
 #pragma unroll
     for (int d = 5; d <= 6; ++d) {
-      if (x - d >= 0) m = fmaxf(m, row[x - d]);
-      if (x + d < W) m = fmaxf(m, row[x + d]);
+      if (x - d >= 0) m = nan_max(m, row[x - d]);
+      if (x + d < W) m = nan_max(m, row[x + d]);
     }
     rm[2 * HW + i] = m;
   }
@@ -53,7 +56,7 @@ __global__ __launch_bounds__(256) void sppf_pool_kernel(float* __restrict__ z, l
       const float* col = rm + k * HW + x;
       float m = -INFINITY;
       const int y0 = y - r < 0 ? 0 : y - r, y1 = y + r >= H ? H - 1 : y + r;
-      for (int yy = y0; yy <= y1; ++yy) m = fmaxf(m, col[yy * W]);
+      for (int yy = y0; yy <= y1; ++yy) m = nan_max(m, col[yy * W]);
       dst[(long)(k + 1) * C * HW + i] = m;
     }
   }
