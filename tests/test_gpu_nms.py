@@ -81,6 +81,37 @@ def test_nms_full_size_ties_vs_oracle(B, A, clusters, kw, cuda):
         assert np.array_equal(index[b, :counts[b]], idx[b]), b
 
 
+@pytest.mark.parametrize("mode", ["all_equal", "low_byte", "low_byte_multi"])
+def test_nms_prefix_select_shared_key_digits(mode, cuda):
+    """The top-KCAP select skips the key digits all candidates share: 5000 candidates per image whose scores are all
+    equal (nothing below the threshold key: everything goes through the remainder path) or differ only in the lowest
+    mantissa byte (the select runs its last digit pass only); multi-label takes the global-memory select (n > the
+    register path's capacity)."""
+    B, A, nc = 2, 34000, 10
+    pred = recipes.synthetic_predictions(4242, B, A, nc, n_clusters=300)
+    rng = np.random.default_rng(5)
+    pred[:, 4:] = 0.0
+    multi = mode == "low_byte_multi"
+    for b in range(B):
+        sel = rng.choice(A, 5000, replace=False)
+        for j in (range(nc) if multi else (0,)):
+            cls = (sel + j) % nc
+            if mode == "all_equal":
+                pred[b, 4 + cls, sel] = 0.5
+            else:
+                bits = np.float32(0.5).view(np.uint32) + rng.integers(0, 256, sel.size).astype(np.uint32)
+                pred[b, 4 + cls, sel] = bits.view(np.float32)
+    kw = dict(conf_thres=0.25, iou_thres=0.6, max_det=300, multi_label=multi)
+    p_after, out, counts, index = _run_gpu(pred, cuda, **kw)
+    ref = pred.copy()
+    rows, idx = non_max_suppression_ref(ref, **kw)
+    assert np.array_equal(p_after, ref)
+    assert counts.tolist() == [len(r) for r in rows]
+    for b in range(B):
+        assert np.array_equal(out[b, :counts[b]], rows[b]), b
+        assert np.array_equal(index[b, :counts[b]], idx[b]), b
+
+
 def test_torch_ops_reject_wrong_sized_partials_and_devices(cuda):
     """Public torch.ops boundary: producer partials of the wrong size raise (TORCH_CHECK) instead of being read out
     of bounds on the GPU."""

@@ -34,6 +34,16 @@ constexpr int NMS_MAXDET = 1024;     // kept lists up to this length live in LDS
 constexpr int NMS_MAXDET_BIG = 1 << 20;
 constexpr int KCAP = 2048;  // candidates covered by the multi-CU IoU bitmask
 constexpr int KW = KCAP / 64;
+static_assert(KW == 32, "nms_resolve maps one 32-word mask row onto 32 threads");
+constexpr int RK = 72;      // keys per thread nms_select holds in registers: n <= NMS_T * RK (A = 34000 single-label)
+
+#ifdef YS_DIAG_STAMPS  // diagnostic builds only (scripts/diag_nms.sh): s_memtime of thread 0 at phase boundaries
+__device__ unsigned long long g_nms_stamps[32 * 16];
+#define YS_NSTAMP(k) \
+  if (threadIdx.x == 0 && blockIdx.x < 32) g_nms_stamps[blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memtime();
+#else
+#define YS_NSTAMP(k) ;  // a statement in both builds (never the body of an if)
+#endif
 
 struct NmsArgs {
   float* pred;  // [B][4+nc][A]
@@ -240,18 +250,41 @@ __device__ __forceinline__ bool iou_gt(const float4 bi, float ai, const float4 b
   return (double)ovr > thr;
 }
 
-// hist[d] += 1 for every active lane with valid: lanes with equal digits are grouped by 8 ballots and one lane
-// per group adds the group size (no same-address atomic storms when most keys share a digit)
-__device__ __forceinline__ void hist_add_digit(unsigned* hist, unsigned d, bool valid) {
-  unsigned long long peers = __ballot(valid);
-#pragma unroll
-  for (int bt = 0; bt < 8; ++bt) {
-    const bool bit = (d >> bt) & 1u;
-    const unsigned long long bal = __ballot(bit);
-    peers &= bit ? bal : ~bal;
+// iou_gt with the division skipped where it cannot matter: inter is >= 0 or NaN (w, h >= 0), and with inter not
+// > 0 the ratio is +-0 or NaN, which is > thr for no thr >= 0 (the reference asserts 0 <= iou_thres). all_pairs
+// (thr < 0) keeps every division. Same operations in the same order as iou_gt where it divides: bit-identical.
+__device__ __forceinline__ bool iou_gt_sparse(const float4 bi, float ai, const float4 bj, float aj, double thr,
+                                              bool all_pairs) {
+  const float xx1 = fmaxf(bi.x, bj.x), yy1 = fmaxf(bi.y, bj.y);
+  const float xx2 = fminf(bi.z, bj.z), yy2 = fminf(bi.w, bj.w);
+  const float w = fmaxf(0.0f, xx2 - xx1), h = fmaxf(0.0f, yy2 - yy1);
+  const float inter = w * h;
+  bool hit = false;
+  // divergent branch: a wave divides only if one of its pairs overlaps (a cheaper xx2 > xx1 && yy2 > yy1 pre-test
+  // in front of w, h and inter measured 24 % slower: one more divergent branch per pair)
+  if (inter > 0.0f || all_pairs) {
+    const float ovr = inter / ((ai + aj) - inter);
+    hit = (double)ovr > thr;
   }
-  if (valid && (peers & lanemask_lt()) == 0ull) atomicAdd(&hist[d], (unsigned)__popcll(peers));
+  return hit;
 }
+
+// hist[d] += 1 for every lane with valid (wave-uniform call)
+__device__ __forceinline__ void hist_add_digit(unsigned* hist, unsigned d, bool valid) {
+  const unsigned long long act = __ballot(valid);
+  if (act == 0ull) return;
+  // common case (score keys share their top digits): every valid lane has the leader's digit, one atomic
+  const int leader = __builtin_amdgcn_readfirstlane(__ffsll((long long)act) - 1);
+  const unsigned dl = __builtin_amdgcn_readlane(d, leader);
+  if (__ballot(valid && d != dl) == 0ull) {
+    if ((int)(threadIdx.x & 63) == leader) atomicAdd(&hist[dl], (unsigned)__popcll(act));
+    return;
+  }
+  // mixed digits: plain per-lane atomics (the LDS serialises only lanes that share an address; grouping equal
+  // digits by 8 ballots first cost more VALU work than the conflicts it avoids)
+  if (valid) atomicAdd(&hist[d], 1u);
+}
+
 
 // exclusive scan of hist[0..256) in place by the first 256 threads of the (512-thread) block; returns nothing,
 // block-uniform (contains barriers). tmp: 4 words.
@@ -397,6 +430,7 @@ __global__ __launch_bounds__(NMS_T) void nms_select_kernel(NmsArgs g) {
   unsigned* kB = g.keyB + (long)b * g.cap;
   unsigned* pB = g.posB + (long)b * g.cap;
 
+  YS_NSTAMP(0)
   // (a) the ordered compaction ran over the whole GPU (nms_prep counts, nms_scatter); n = the image's candidates
   __shared__ int nsum[NMS_W + 1];
   int n;
@@ -407,6 +441,7 @@ __global__ __launch_bounds__(NMS_T) void nms_select_kernel(NmsArgs g) {
     (void)block_exclusive_scan(v, nsum, &n);
   }
   const int neff = (n > g.max_nms) ? g.max_nms : n;
+  YS_NSTAMP(1)
 
   // (b) score order of the prefix
   unsigned *ks, *ps, *kd, *pd;
@@ -421,6 +456,114 @@ __global__ __launch_bounds__(NMS_T) void nms_select_kernel(NmsArgs g) {
     ks = lk[0]; ps = lp[0]; kd = lk[1]; pd = lp[1];
     radix_sort_pairs(ks, ps, kd, pd, n, sh);
     m = n;
+  } else if (n <= NMS_T * RK) {
+    // the same radix select with the keys held in registers (thread t: keys [t RK, t RK + RK)): one read of the
+    // keys instead of one per pass, and a single ordered compaction
+    const int base = tid * RK;
+    unsigned kr[RK];
+    // every load unconditional (a clamped address; entries past n masked afterwards), so all of a thread's loads
+    // are in flight together (loads under a bounds branch were merged into phis that each waited for the memory)
+    if ((reinterpret_cast<uintptr_t>(kA) & 15u) == 0) {
+      // 16-byte loads; a chunk starting past n reads the last aligned chunk before n (inside the image's keys or,
+      // for the chunk ending past n, at most 3 entries beyond them: still workspace)
+      const int last = (n - 1) & ~3;
+#pragma unroll
+      for (int v = 0; v < RK / 4; ++v) {
+        const int i = base + 4 * v;
+        const uint4 q = *reinterpret_cast<const uint4*>(kA + (i < n ? i : last));
+        kr[4 * v] = q.x; kr[4 * v + 1] = q.y; kr[4 * v + 2] = q.z; kr[4 * v + 3] = q.w;
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < RK; ++u) kr[u] = kA[min(base + u, n - 1)];
+    }
+#pragma unroll
+    for (int u = 0; u < RK; ++u)
+      if (base + u >= n) kr[u] = 0xFFFFFFFFu;
+    // digits above the highest bit in which two keys differ are common to all keys: their passes would find one
+    // bucket holding all n (> KCAP) keys and only extend the prefix, so the select starts below them (the same T)
+    // Entries past n hold 0xFFFFFFFF, the largest key: counted in the histograms they only add to the top bucket,
+    // which never moves the crossing digit (n > KCAP valid keys cross at or below it), and `key < T` never takes
+    // them; so no per-entry validity test is needed below (72 of them kept live spilled the SGPRs). kmax excludes
+    // them, unless a valid key is 0xFFFFFFFF itself (a score of +0 with conf < 0): then no digit is skipped.
+    unsigned kmin = 0xFFFFFFFFu, kmax = 0u;
+    int nff = 0;
+#pragma unroll
+    for (int u = 0; u < RK; ++u) {
+      kmin = min(kmin, kr[u]);
+      if (kr[u] != 0xFFFFFFFFu) kmax = max(kmax, kr[u]);
+      nff += (kr[u] == 0xFFFFFFFFu) ? 1 : 0;
+    }
+    if (nff > RK - max(0, min(RK, n - base))) kmax = 0xFFFFFFFFu;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      kmin = min(kmin, (unsigned)__shfl_xor((int)kmin, o, 64));
+      kmax = max(kmax, (unsigned)__shfl_xor((int)kmax, o, 64));
+    }
+    __shared__ unsigned kminmax[2];
+    if (tid == 0) {
+      kminmax[0] = 0xFFFFFFFFu;
+      kminmax[1] = 0u;
+    }
+    __syncthreads();
+    if ((tid & 63) == 0) {
+      atomicMin(&kminmax[0], kmin);
+      atomicMax(&kminmax[1], kmax);
+    }
+    __syncthreads();
+    kmin = kminmax[0];
+    kmax = kminmax[1];
+    const unsigned diff = kmin ^ kmax;
+    unsigned prefix = kmin, below = 0u;  // all keys equal: none is below T = that key
+    YS_NSTAMP(2)
+    if (diff != 0u) {
+      const int top = ((31 - __clz(diff)) / 8) * 8;  // shift of the digit holding the highest differing bit
+      unsigned pmask = (top == 24) ? 0u : (0xFFFFFFFFu << (top + 8));
+      prefix = kmin & pmask;
+      for (int shift = top; shift >= 0; shift -= 8) {
+        if (tid < 256) sh.hist[tid] = 0;
+        __syncthreads();
+        // plain LDS atomics (below the common digits the keys' digits are spread; a skewed pass only costs LDS
+        // conflicts, while hist_add_digit's uniformity test cost more than the atomics over 72 keys per thread)
+#pragma unroll
+        for (int u = 0; u < RK; ++u)
+          if ((kr[u] & pmask) == prefix) atomicAdd(&sh.hist[(kr[u] >> shift) & 255u], 1u);
+        __syncthreads();
+        const unsigned h = (tid < 256) ? sh.hist[tid] : 0u;
+        scan256_exclusive(sh.hist, sh.tmp4);
+        if (tid < 256) {
+          const unsigned run = below + sh.hist[tid];
+          if (run <= (unsigned)KCAP && run + h > (unsigned)KCAP) {
+            sel_below = run;
+            sel_prefix = prefix | ((unsigned)tid << shift);
+          }
+        }
+        __syncthreads();
+        below = sel_below;
+        prefix = sel_prefix;
+        pmask |= 255u << shift;
+        __syncthreads();
+      }
+    }
+    T = prefix;
+    YS_NSTAMP(3)
+    int c = 0;
+#pragma unroll
+    for (int u = 0; u < RK; ++u) c += (kr[u] < T) ? 1 : 0;
+    int o = block_exclusive_scan(c, sh.wsum, &m);
+#pragma unroll
+    for (int u = 0; u < RK; ++u)
+      if (kr[u] < T) {
+        lk[0][o] = kr[u];
+        lp[0][o] = (unsigned)(base + u);  // index into the compaction; its position is gathered below
+        ++o;
+      }
+    __syncthreads();
+    for (int i = tid; i < m; i += NMS_T) lp[0][i] = pA[lp[0][i]];
+    __syncthreads();
+    YS_NSTAMP(4)
+    ks = lk[0]; ps = lp[0]; kd = lk[1]; pd = lp[1];
+    radix_sort_pairs(ks, ps, kd, pd, m, sh);
   } else {
     // radix select, MSB first: the key T with #(key < T) <= KCAP, taking whole digit buckets while they fit
     unsigned prefix = 0u, pmask = 0u;
@@ -429,27 +572,39 @@ __global__ __launch_bounds__(NMS_T) void nms_select_kernel(NmsArgs g) {
       const int shift = 24 - 8 * pass;
       if (tid < 256) sh.hist[tid] = 0;
       __syncthreads();
-      for (int i = tid; i < n; i += NMS_T) {
-        const unsigned k = kA[i];
-        if ((k & pmask) == prefix) atomicAdd(&sh.hist[(k >> shift) & 255u], 1u);
+      // 8 key loads in flight per thread; equal digits grouped per wave (the top digits of score keys are nearly
+      // all equal: one LDS atomic per wave and digit, not one per key)
+      for (int i0 = 0; i0 < n; i0 += NMS_T * 8) {
+        unsigned kk[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int i = i0 + u * NMS_T + tid;
+          kk[u] = (i < n) ? kA[i] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int i = i0 + u * NMS_T + tid;
+          hist_add_digit(sh.hist, (kk[u] >> shift) & 255u, i < n && (kk[u] & pmask) == prefix);
+        }
       }
       __syncthreads();
-      if (tid == 0) {
-        unsigned run = below;
-        int d = 0;
-        for (; d < 256; ++d) {
-          if (run + sh.hist[d] > (unsigned)KCAP) break;
-          run += sh.hist[d];
+      // the digit d where the running count crosses KCAP: below + excl[d] <= KCAP < below + excl[d] + hist[d]
+      // (unique; it exists because the keys under the current prefix do not all fit, else the previous pass
+      // would have taken that whole bucket)
+      const unsigned h = (tid < 256) ? sh.hist[tid] : 0u;
+      scan256_exclusive(sh.hist, sh.tmp4);
+      if (tid < 256) {
+        const unsigned run = below + sh.hist[tid];
+        if (run <= (unsigned)KCAP && run + h > (unsigned)KCAP) {
+          sel_below = run;
+          sel_prefix = prefix | ((unsigned)tid << shift);
         }
-        // d < 256 always: the keys under the current prefix do not all fit (else the previous pass would
-        // have taken that whole bucket)
-        sel_below = run;
-        sel_prefix = prefix | ((unsigned)d << shift);
       }
       __syncthreads();
       below = sel_below;
       prefix = sel_prefix;
       pmask |= 255u << shift;
+      __syncthreads();  // sel_* and hist are rewritten by the next pass
     }
     T = prefix;  // keys < T: exactly `below` of them, a prefix of the stable ascending order
     m = compact_by_key(kA, pA, n, T, true, lk[0], lp[0], sh);
@@ -457,7 +612,16 @@ __global__ __launch_bounds__(NMS_T) void nms_select_kernel(NmsArgs g) {
     ks = lk[0]; ps = lp[0]; kd = lk[1]; pd = lp[1];
     radix_sort_pairs(ks, ps, kd, pd, m, sh);
   }
+  YS_NSTAMP(5)
   const int K = (m < neff) ? m : neff;
+#ifdef YS_DIAG_STAMPS
+  if (tid == 0 && b < 32) {
+    g_nms_stamps[b * 16 + 11] = (unsigned)n;
+    g_nms_stamps[b * 16 + 12] = (unsigned)m;
+    g_nms_stamps[b * 16 + 13] = (unsigned)K;
+    g_nms_stamps[b * 16 + 14] = T;
+  }
+#endif
   // prefix boxes with the class offset (ops.py:289,295), areas, ids
   const float4* bx = g.boxes + (long)b * A;
   float4* sb = g.sbox + (long)b * KCAP;
@@ -480,6 +644,7 @@ __global__ __launch_bounds__(NMS_T) void nms_select_kernel(NmsArgs g) {
     mt[2] = K;
     mt[3] = (int)T;
   }
+  YS_NSTAMP(6)
 }
 
 // -------------------------------------------------------------------------------------------------
@@ -487,9 +652,10 @@ __global__ __launch_bounds__(NMS_T) void nms_select_kernel(NmsArgs g) {
 // -------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void nms_mask_kernel(NmsArgs g) {
   const int b = blockIdx.y, rb = blockIdx.x;
-  const int K = g.meta[4 * b + 2];
+  const int K = __builtin_amdgcn_readfirstlane(g.meta[4 * b + 2]);
   if (rb * 64 >= K) return;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: the column reads broadcast
   __shared__ float4 cbx[4][64];
   __shared__ float car[4][64];
   const float4* sb = g.sbox + (long)b * KCAP;
@@ -498,6 +664,8 @@ __global__ __launch_bounds__(256) void nms_mask_kernel(NmsArgs g) {
   const float4 bi = (i < K) ? sb[i] : make_float4(0, 0, 0, 0);
   const float ai = (i < K) ? sa[i] : 0.f;
   const int nblk = (K + 63) / 64;
+  const double thr = g.iou;
+  const bool all_pairs = !(thr >= 0.0);
   unsigned long long* mrow = g.mask + ((long)b * KCAP + i) * KW;
   for (int cb0 = rb; cb0 < nblk; cb0 += 4) {
     const int cb = cb0 + wv;
@@ -507,13 +675,28 @@ __global__ __launch_bounds__(256) void nms_mask_kernel(NmsArgs g) {
       car[wv][lane] = (j < K) ? sa[j] : 0.f;
     }
     __syncthreads();
-    if (cb < nblk && i < K) {
-      unsigned long long bits = 0ull;
-      const int qlo = (cb == rb) ? lane + 1 : 0;
+    if (cb < nblk) {
+      // every lane walks the same columns (uniform LDS addresses: broadcast reads, unrolled so several are in
+      // flight); the diagonal block keeps only columns q > lane
       const int qhi = (K - cb * 64 < 64) ? K - cb * 64 : 64;
-      for (int q = qlo; q < qhi; ++q)
-        if (iou_gt(bi, ai, cbx[wv][q], car[wv][q], g.iou)) bits |= 1ull << q;
-      mrow[cb] = bits;
+      const float4* cx = cbx[wv];
+      const float* ca = car[wv];
+      unsigned long long bits = 0ull;
+      for (int q0 = 0; q0 < qhi; q0 += 8) {  // 8 columns' reads issued before the first test (q0 + 8 <= 64)
+        float4 bj[8];
+        float aj[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          bj[u] = cx[q0 + u];
+          aj[u] = ca[q0 + u];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (iou_gt_sparse(bi, ai, bj[u], aj[u], thr, all_pairs)) bits |= 1ull << (q0 + u);
+      }
+      if (qhi < 64) bits &= (1ull << qhi) - 1ull;  // columns past K
+      if (cb == rb) bits &= (lane == 63) ? 0ull : (~0ull << (lane + 1));
+      if (i < K) mrow[cb] = bits;
     }
     __syncthreads();
   }
@@ -527,15 +710,18 @@ __global__ __launch_bounds__(256) void nms_mask_kernel(NmsArgs g) {
 template <bool BIG>
 __global__ __launch_bounds__(NMS_T) void nms_resolve_kernel(NmsArgs g) {
   const int b = blockIdx.x;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: the wave-0 branch below stays scalar
   __shared__ unsigned long long mrows[2][64][KW];
   __shared__ int kept_t_lds[BIG ? 1 : NMS_MAXDET];
   // kept entries: < KCAP -> prefix index, else KCAP + remainder index
   int* kept_t = BIG ? g.kept_t + (long)b * g.max_det : kept_t_lds;
   __shared__ int nkept_sh, done_sh;
   const int* mt = g.meta + 4 * b;
-  const int n = mt[0], neff = mt[1], K = mt[2];
-  const unsigned T = (unsigned)mt[3];
+  // wave-uniform by construction; readfirstlane tells the compiler so (the greedy below must stay a scalar loop)
+  const int n = __builtin_amdgcn_readfirstlane(mt[0]), neff = __builtin_amdgcn_readfirstlane(mt[1]);
+  const int K = __builtin_amdgcn_readfirstlane(mt[2]);
+  const unsigned T = (unsigned)__builtin_amdgcn_readfirstlane(mt[3]);
   const long A = g.A;
   const int nc = g.nc;
   const float* pb = g.pred + (long)b * (4 + nc) * A;
@@ -544,43 +730,67 @@ __global__ __launch_bounds__(NMS_T) void nms_resolve_kernel(NmsArgs g) {
   float* ob = g.out + (long)b * g.max_det * 6;
   int* oi = g.out_index + (long)b * g.max_det;
 
+  YS_NSTAMP(8)
   if (tid == 0) {
     nkept_sh = 0;
     done_sh = 0;
   }
   __syncthreads();
-  // (1) greedy over the prefix: lane w (< KW) of wave 0 owns removed-word w; waves 1..7 stage the next 64
-  // mask rows into the other LDS buffer meanwhile
+  // (1) greedy over the prefix, 64 rows (one block) at a time. Per block: wave 0 runs the greedy over the block's
+  // diagonal word (a scalar loop, readlane), while waves 1..7 store the next block's mask rows into the other LDS
+  // buffer and issue the loads of the block after it (in flight across the barriers: one block of prefetch in
+  // registers, one in LDS); then all 8 waves OR the kept rows into the removed words of the later blocks.
   {
     const int nblk = (K + 63) / 64;
-    auto stage = [&](int rb, int buf, int t0, int nt) {
+    __shared__ unsigned long long rem_w[KW];  // removed bits of each 64-column word
+    __shared__ unsigned long long keptm_sh;
+    constexpr int SPT = (64 * KW + (NMS_T - 64) - 1) / (NMS_T - 64);  // mask words per helper thread and block
+    const int ht = tid - 64;                                           // helper thread index (waves 1..7)
+    unsigned long long v[SPT];
+    auto load_block = [&](int rb) {
       const unsigned long long* src = g.mask + ((long)b * KCAP + rb * 64) * KW;
-      for (int e = t0; e < 64 * KW; e += nt) {
-        const int r = e / KW, w = e % KW;
-        mrows[buf][r][w] = (rb * 64 + r < K && w >= rb && w < nblk) ? src[(long)r * KW + w] : 0ull;
+#pragma unroll
+      for (int u = 0; u < SPT; ++u) {
+        const int e = ht + u * (NMS_T - 64), r = e / KW, w = e % KW;
+        v[u] = (e < 64 * KW && rb * 64 + r < K && w >= rb && w < nblk) ? src[(long)r * KW + w] : 0ull;
       }
     };
-    if (nblk > 0) stage(0, 0, tid, NMS_T);
+    auto store_block = [&](int buf) {
+#pragma unroll
+      for (int u = 0; u < SPT; ++u) {
+        const int e = ht + u * (NMS_T - 64);
+        if (e < 64 * KW) mrows[buf][e / KW][e % KW] = v[u];
+      }
+    };
+    if (tid < KW) rem_w[tid] = 0ull;
+    if (wv != 0 && nblk > 0) {
+      load_block(0);
+      store_block(0);
+      if (nblk > 1) load_block(1);
+    }
     __syncthreads();
-    unsigned long long removed = 0ull;
     int nkk = 0;
-    bool done = false;
     for (int rb = 0; rb < nblk; ++rb) {
       const int buf = rb & 1;
       if (wv != 0) {
-        if (rb + 1 < nblk) stage(rb + 1, buf ^ 1, tid - 64, NMS_T - 64);
+        if (rb + 1 < nblk) store_block(buf ^ 1);
+        if (rb + 2 < nblk) load_block(rb + 2);
       } else {
-        // lane q holds row q's bits inside this block (the diagonal word); the greedy over the block is a
-        // scalar loop (readlane), then the kept rows are OR-ed into the later words in parallel
+        // lane q holds row q's bits inside this block (the diagonal word); the greedy is a scalar loop (cand, rem,
+        // keptm in SGPRs: the removed word is read back from LDS through readfirstlane so that the compiler knows
+        // it is wave-uniform; a VGPR loop condition made it a divergent VALU loop, ~5x slower)
         const unsigned long long diag = mrows[buf][lane][rb];
         const int rows_here = (K - rb * 64 < 64) ? K - rb * 64 : 64;
-        unsigned long long rem = __shfl(removed, rb, 64);
+        const unsigned long long remv = rem_w[rb];
+        unsigned long long rem = ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(remv >> 32)) << 32) |
+                                 (unsigned)__builtin_amdgcn_readfirstlane((unsigned)remv);
         unsigned long long cand = (rows_here == 64 ? ~0ull : ((1ull << rows_here) - 1ull)) & ~rem;
         unsigned long long keptm = 0ull;
+        const int nk0 = nkk;
+        bool done = false;
         while (cand) {
-          const int q = __ffsll((long long)cand) - 1;
+          const int q = __builtin_ctzll(cand);
           keptm |= 1ull << q;
-          if (lane == 0) kept_t[nkk] = rb * 64 + q;
           ++nkk;
           if (nkk >= g.max_det) {
             done = true;
@@ -592,26 +802,35 @@ __global__ __launch_bounds__(NMS_T) void nms_resolve_kernel(NmsArgs g) {
           const unsigned long long upto = (q == 63) ? ~0ull : ((2ull << q) - 1ull);
           cand &= ~upto & ~rem;
         }
-        if (!done && lane > rb && lane < nblk) {
-          unsigned long long acc = removed;
-          unsigned long long km = keptm;
-          while (km) {
-            const int q = __ffsll((long long)km) - 1;
-            km &= km - 1;
-            acc |= mrows[buf][q][lane];
-          }
-          removed = acc;
-        }
+        // the block's kept rows, in order, written by their own lanes
+        if ((keptm >> lane) & 1ull) kept_t[nk0 + __popcll(keptm & lanemask_lt())] = rb * 64 + lane;
         if (lane == 0) {
+          keptm_sh = keptm;
           nkept_sh = nkk;
           done_sh = done ? 1 : 0;
         }
       }
       __syncthreads();
       if (done_sh) break;
+      // kept rows of this block into the later words: thread (word w, group gq) ORs the kept rows whose rank
+      // among this block's kept rows is gq mod 16
+      {
+        const int w = tid & 31, gq = tid >> 5;
+        if (w > rb && w < nblk) {
+          unsigned long long km = keptm_sh, acc = 0ull;
+          for (int k = 0; km; ++k) {
+            const int q = __ffsll((long long)km) - 1;
+            km &= km - 1;
+            if ((k & 15) == gq) acc |= mrows[buf][q][w];
+          }
+          if (acc) atomicOr(&rem_w[w], acc);
+        }
+      }
+      __syncthreads();
     }
   }
   const int nk_prefix = nkept_sh;
+  YS_NSTAMP(9)
   for (int k = tid; k < nk_prefix; k += NMS_T) {
     const unsigned p = sp[kept_t[k]];
     const unsigned a = p / nc, j = p % nc;
@@ -736,12 +955,19 @@ __global__ __launch_bounds__(NMS_T) void nms_resolve_kernel(NmsArgs g) {
   if (tid == 0) {
     g.counts[b] = nk;
   }
+  YS_NSTAMP(10)
 }
 
 
 }  // namespace ys
 
 using namespace ys;
+
+#ifdef YS_DIAG_STAMPS
+YS_EXPORT int yolosod_diag_nms_stamps(unsigned long long* host) {  // [32][16] of the last call
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_nms_stamps), sizeof(g_nms_stamps)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 
 static long nms_cap(int nc, int A, int multi_label) { return (long)A * (multi_label ? nc : 1); }
