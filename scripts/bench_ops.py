@@ -34,6 +34,13 @@ CASES = {
     "a2_L12_m": ("A2_Attn", (512, None, 8, 8), (64, 512, 20, 20)),
     "cbam_L4_m": ("CBAM_Block", (128, 128, 16), (64, 128, 160, 160)),
     "ca_L32_m": ("CA_Block", (256, 256, 32), (64, 256, 80, 80)),
+    # the gate-fused operators as the model runs them (GATE_FUSE): the gate kernels, then the consumer stride-2 conv
+    # applying it while staging its input (se_conv: SE L1 -> Conv L2; cbam_conv: CBAM L4 -> Conv L5)
+    "se_conv_L1": ("gated_se", (64, 64), (32, 32, 320, 320)),
+    "cbam_conv_L4": ("gated_cbam", (64, 128, 16), (32, 64, 160, 160)),
+    # NMS (predict mode) on [32, 14, 34000] with 0 / 30k candidates per image (synthetic, bench.loaded_predictions)
+    "nms_empty": ("nms", (0,), (32, 14, 34000)),
+    "nms_30k": ("nms", (30000,), (32, 14, 34000)),
 }
 
 
@@ -49,6 +56,43 @@ def head_case(dev, c2, c3, nc, B, S):
     return lambda: _hip.detect_head(fb, fc, bw, bb, cw, cb, [4.0, 8.0, 16.0, 32.0], nc)
 
 
+def gated_case(dev, op, args, shape):
+    """gate + gated consumer conv (Conv.forward_gated) on x that carries its producer's statistics"""
+    from yolosod_amd.nn.tasks import _fuse_conv_and_bn
+    B, C, H, W = shape
+    se = op == "gated_se"
+    gate = M.SE_Block(args[0]) if se else M.CBAM_Block(C, None, args[2])
+    if se:
+        gate._maybe_build(C, None)
+    cout = args[1]
+    cons = M.Conv(C, cout, 3, 2)
+    recipes.perturb_(gate, 1)
+    recipes.perturb_(cons, 1)
+    cons.conv = _fuse_conv_and_bn(cons.conv, cons.bn)
+    delattr(cons, "bn")
+    gate, cons = gate.to(dev).eval(), cons.to(dev).eval()
+    x = torch.randn(shape, device=dev)
+    x = _hip.bias_act(x, torch.zeros(C, device=dev), 0, out=torch.empty_like(x), stats="sum" if se else "summax")
+    if se:
+        key = ("se_conv", tuple(x.shape), (cout, gate.fc1.out_channels))
+    else:
+        key = ("cbam_conv", tuple(x.shape), (cout, gate.channel_attention.fc[0].out_channels))
+
+    def fn():
+        gc, gp = (gate.gate(x), None) if se else gate.gates(x)
+        return cons.forward_gated(x, gc, gp, key)
+    return fn, key
+
+
+def nms_case(dev, n_cand, shape):
+    from bench import loaded_predictions
+    from yolosod_amd.utils.ops import non_max_suppression_padded
+    B, no, A = shape
+    pred = loaded_predictions(B, A, no - 4, n_cand, 50, 0.25, 0, dev)
+    # in place: the repeated xywh -> xyxy rewrite changes the boxes, not the candidate set or the traffic
+    return lambda: non_max_suppression_padded(pred, 0.25, 0.7, max_det=300)
+
+
 def main():
     args = sys.argv[1:]
     bf16 = "--bf16" in args
@@ -59,6 +103,12 @@ def main():
         op, args, shape = CASES[name]
         if op == "detect_head":
             fn = head_case(dev, *args, shape[0], shape[2])
+            m, x = (lambda _x: fn()), None
+        elif op in ("gated_se", "gated_cbam"):
+            fn, fused_key = gated_case(dev, op, args, shape)
+            m, x = (lambda _x: fn()), None
+        elif op == "nms":
+            fn = nms_case(dev, args[0], shape)
             m, x = (lambda _x: fn()), None
         else:
             m = getattr(M, op)(*args)
@@ -89,6 +139,8 @@ def main():
             d = t.durations_ms()
         key = d[0][0]
         ms = sum(v for _, v in d) / len(d)
+        if op in ("gated_se", "gated_cbam"):  # the gate and the conv are separate timed launches: both per call
+            key, ms = fused_key, sum(v for _, v in d) / 10
         b, f = perf.op_cost(key)
         print(f"{name:10s} {ms:8.3f} ms  {b / ms / 1e6:8.1f} GB/s  {f / ms / 1e9:7.2f} TFLOP/s", flush=True)
 

@@ -7,9 +7,10 @@ OUT=${1:?outdir}; shift
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 for c in "$@"; do
-  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/${c}_f" -o f -- python3 scripts/bench_ops.py "$c" \
+  bf=""; case "$c" in *_m) bf="--bf16";; esac  # the bf16 config's cases
+  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/${c}_f" -o f -- python3 scripts/bench_ops.py "$c" $bf \
     > "$OUT/${c}_f.txt" 2>&1 || { echo "FETCH pass failed for $c"; tail -5 "$OUT/${c}_f.txt"; exit 1; }
-  timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/${c}_w" -o w -- python3 scripts/bench_ops.py "$c" \
+  timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/${c}_w" -o w -- python3 scripts/bench_ops.py "$c" $bf \
     > "$OUT/${c}_w.txt" 2>&1 || { echo "WRITE pass failed for $c"; tail -5 "$OUT/${c}_w.txt"; exit 1; }
   grep -h "ms " "$OUT/${c}_f.txt" | tail -1
 done

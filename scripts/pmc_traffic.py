@@ -22,7 +22,7 @@ sys.path.insert(0, str(Path(__file__).resolve().parent))
 from bench_ops import CASES  # noqa: E402
 
 OPKEY = {"SwinBlock": "swin", "A2_Attn": "a2", "SE_Block": "se", "CBAM_Block": "cbam", "CA_Block": "ca",
-         "MambaBlock": "mamba", "detect_head": "head"}
+         "MambaBlock": "mamba", "detect_head": "head", "gated_se": "se_conv", "gated_cbam": "cbam_conv", "nms": "nms"}
 CALLS = 13
 
 
@@ -53,7 +53,10 @@ def main():
             continue
         per_call = (2.0 * f + w) * 1024.0 / CALLS
         key_shape = shape if cls != "detect_head" else (shape[0], 34000 * (shape[2] // 640) ** 2)
-        out[f"{OPKEY[cls]}:{'x'.join(map(str, key_shape))}"] = round(per_call)
+        if cls == "nms":  # key shape (B, nc, A); the bench's NMS (random init) is the empty one
+            key_shape = (shape[0], shape[1] - 4, shape[2])
+        if cls != "nms" or case == "nms_empty":
+            out[f"{OPKEY[cls]}:{'x'.join(map(str, key_shape))}"] = round(per_call)
         out[f"_detail:{case}"] = {"read_bytes_per_call": round(2.0 * f * 1024.0 / CALLS),
                                   "write_bytes_per_call": round(w * 1024.0 / CALLS)}
     json.dump(out, sys.stdout, indent=1, sort_keys=True)
