@@ -382,92 +382,94 @@ __device__ __forceinline__ float2 cbam_map_at(const float* __restrict__ mp, int 
   return make_float2(s, m);
 }
 
-// CBAM pass 2b (split path): sa = sigmoid(conv7x7([mean_c o ; max_c o]), zero pad 3, no bias) on 16x16 output
-// tiles, the 22x22 halo of both maps (combined over the G channel groups) staged in LDS.
+// CBAM pass 2b (split path): sa = sigmoid(conv7x7([mean_c o ; max_c o]), zero pad 3, no bias) on 16-wide x 64-tall
+// output tiles, the 22 x 70 halo of both maps (combined over the G channel groups) staged in LDS. Each thread
+// computes 4 vertically adjacent outputs, so each staged value is read from LDS once per 4 outputs (140 reads for
+// 392 FMAs; the weights are scalar loads; 16x16 tiles with one output per thread read 196 LDS values - weights
+// included - per 98 FMAs, and needed two rounds of workgroups). Per output the products accumulate in the same (map, ky, kx) order as before.
 // grid = (tiles_x, tiles_y, images).
+constexpr int kSaTW = 16, kSaTH = 64;
 __global__ __launch_bounds__(256) void cbam_sa_kernel(const float* __restrict__ mpart, int G, int C, int H, int W,
                                                       const float* __restrict__ wsa, float* __restrict__ sa) {
-  __shared__ float mm[2][22][23];
-  __shared__ float wk[98];
+  constexpr int HX = kSaTW + 6, HY = kSaTH + 6, NPOS = HX * HY, PT = (NPOS + 255) / 256;
+  __shared__ float mm[2][HY][HX + 1];
   const int b = blockIdx.z;
   const long HW = (long)H * W;
   const int tid = threadIdx.x;
-  if (tid < 98) wk[tid] = wsa[tid];
-  const int oy = blockIdx.y * 16 - 3, ox = blockIdx.x * 16 - 3;
+  const int oy = blockIdx.y * kSaTH - 3, ox = blockIdx.x * kSaTW - 3;
   const float invC = 1.0f / (float)C;
-  // the thread's two halo positions (484 = 256 + 228): every partial-map load unconditional from a clamped position
-  // (loads under the bounds branch merged into phis, each waiting for all loads in flight), both positions' loads in
-  // flight together; out-of-image positions take the conv's zero padding afterwards. Sums keep their g order.
+  // the thread's halo positions: every partial-map load unconditional from a clamped position (loads under a
+  // bounds branch were merged into phis that each waited for all loads in flight), all positions' loads of up to
+  // 4 groups in flight together; out-of-image positions take the conv's zero padding afterwards. Sums keep their
+  // g order.
   const float* mp = mpart + (long)b * G * 2 * HW;
-  int q[2];
-  bool in[2];
+  int q[PT];
+  bool in[PT];
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int i = min(tid + 256 * k, 22 * 22 - 1), ty = i / 22, tx = i - (i / 22) * 22;
+  for (int k = 0; k < PT; ++k) {
+    const int i = min(tid + 256 * k, NPOS - 1), ty = i / HX, tx = i - (i / HX) * HX;
     const int yy = oy + ty, xx = ox + tx;
     in[k] = yy >= 0 && yy < H && xx >= 0 && xx < W;
     q[k] = min(max(yy, 0), H - 1) * W + min(max(xx, 0), W - 1);
   }
-  float sm[2] = {0.f, 0.f}, mx[2] = {-INFINITY, -INFINITY};
-  int g = 0;
-  for (; g + 4 <= G; g += 4) {
-    float a[2][4], c[2][4];
+  float sm[PT], mx[PT];
 #pragma unroll
-    for (int k = 0; k < 2; ++k)
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        a[k][u] = mp[(long)(2 * (g + u)) * HW + q[k]];
-        c[k][u] = mp[(long)(2 * (g + u) + 1) * HW + q[k]];
-      }
-#pragma unroll
-    for (int k = 0; k < 2; ++k)
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        sm[k] += a[k][u];
-        mx[k] = fmaxf(mx[k], c[k][u]);
-      }
+  for (int k = 0; k < PT; ++k) {
+    sm[k] = 0.f;
+    mx[k] = -INFINITY;
   }
-  if (g < G) {  // the last 1..3 groups: all loads in flight at once (clamped group index), the extra ones unused (a
-               // runtime loop issued each group's loads only after the previous group's sums: C = 64, L4, has G = 2)
-    float a[2][3], c[2][3];
+  for (int g0 = 0; g0 < G; g0 += 4) {
+    float a[PT][4], c[PT][4];
 #pragma unroll
-    for (int k = 0; k < 2; ++k)
+    for (int k = 0; k < PT; ++k)
 #pragma unroll
-      for (int u = 0; u < 3; ++u) {
-        const int gu = min(g + u, G - 1);
+      for (int u = 0; u < 4; ++u) {
+        const int gu = min(g0 + u, G - 1);
         a[k][u] = mp[(long)(2 * gu) * HW + q[k]];
         c[k][u] = mp[(long)(2 * gu + 1) * HW + q[k]];
       }
 #pragma unroll
-    for (int k = 0; k < 2; ++k)
+    for (int k = 0; k < PT; ++k)
 #pragma unroll
-      for (int u = 0; u < 3; ++u)
-        if (g + u < G) {
+      for (int u = 0; u < 4; ++u)
+        if (g0 + u < G) {
           sm[k] += a[k][u];
           mx[k] = fmaxf(mx[k], c[k][u]);
         }
   }
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
+  for (int k = 0; k < PT; ++k) {
     const int i = tid + 256 * k;
-    if (i < 22 * 22) {
-      const int ty = i / 22, tx = i - (i / 22) * 22;
+    if (i < NPOS) {
+      const int ty = i / HX, tx = i - (i / HX) * HX;
       mm[0][ty][tx] = in[k] ? sm[k] * invC : 0.f;
       mm[1][ty][tx] = in[k] ? mx[k] : 0.f;
     }
   }
   __syncthreads();
-  const int ly = tid >> 4, lx = tid & 15;
-  const int py = blockIdx.y * 16 + ly, px = blockIdx.x * 16 + lx;
-  if (py >= H || px >= W) return;
-  float z = 0.f;
+  const int lx = tid & 15, ly = (tid >> 4) * 4;
+  float z[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int ci = 0; ci < 2; ++ci)
 #pragma unroll
-    for (int ky = 0; ky < 7; ++ky)
+    for (int r = 0; r < 10; ++r) {
+      float v[7];
 #pragma unroll
-      for (int kx = 0; kx < 7; ++kx) z += wk[ci * 49 + ky * 7 + kx] * mm[ci][ly + ky][lx + kx];
-  sa[(long)b * HW + (long)py * W + px] = sigmoidf_(z);
+      for (int kx = 0; kx < 7; ++kx) v[kx] = mm[ci][ly + r][lx + kx];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int ky = r - j;
+        if (ky >= 0 && ky < 7)
+#pragma unroll
+          for (int kx = 0; kx < 7; ++kx) z[j] += wsa[ci * 49 + ky * 7 + kx] * v[kx];  // uniform: scalar loads
+      }
+    }
+  const int px = blockIdx.x * kSaTW + lx;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int py = blockIdx.y * kSaTH + ly + j;
+    if (py < H && px < W) sa[(long)b * HW + (long)py * W + px] = sigmoidf_(z[j]);
+  }
 }
 
 // CBAM pass 3 (split path): y = sa[p] * (ca[c] * x). grid = (ceil(HW / (256*V)), ceil(C / 8), images).
@@ -845,7 +847,7 @@ static int cbam_forward_impl(const T* x, T* y, int B, int C, int H, int W, const
       hipLaunchKernelGGL((cbam_pixel_stats_kernel<1, T, false>), gs, dim3(256), 0, st, x, ca, C, kCbamGroup, HW, mpart,
                          nullptr, nullptr, 0, 0.f, nullptr, nullptr, 0);
   }
-  hipLaunchKernelGGL(cbam_sa_kernel, dim3((W + 15) / 16, (H + 15) / 16, B), dim3(256), 0, st, mpart, G, C, H, W, sa_w,
+  hipLaunchKernelGGL(cbam_sa_kernel, dim3((W + kSaTW - 1) / kSaTW, (H + kSaTH - 1) / kSaTH, B), dim3(256), 0, st, mpart, G, C, H, W, sa_w,
                      sa);
   if (y) {
     dim3 ga((unsigned)pxb, (C + 7) / 8, B);
