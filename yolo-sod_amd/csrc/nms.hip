@@ -650,56 +650,60 @@ __global__ __launch_bounds__(NMS_T) void nms_select_kernel(NmsArgs g) {
 // -------------------------------------------------------------------------------------------------
 // nms_mask: bit q of mask[b][i][cb] set iff j = cb*64+q > i, j < K and IoU(i, j) > thr. grid = (KW, B).
 // -------------------------------------------------------------------------------------------------
+// One wave per (row block rb, column block cb >= rb) pair: task t of image b enumerates the pairs column-major
+// (t = cb (cb + 1) / 2 + rb), so the pairs of the image's nblk blocks are tasks [0, nblk (nblk + 1) / 2) and later
+// tasks exit at once. Every wave has the same work (the per-row-block workgroups of round 5 gave the rb = 0 workgroup
+// 32 column blocks and the rb = 31 one a single one); the waves share no data, so there is no workgroup barrier.
+// grid = (KW (KW + 1) / 8, B).
 __global__ __launch_bounds__(256) void nms_mask_kernel(NmsArgs g) {
-  const int b = blockIdx.y, rb = blockIdx.x;
+  const int b = blockIdx.y;
   const int K = __builtin_amdgcn_readfirstlane(g.meta[4 * b + 2]);
-  if (rb * 64 >= K) return;
+  const int nblk = (K + 63) / 64;
   const int lane = threadIdx.x & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: the column reads broadcast
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int t = (int)blockIdx.x * 4 + wv;
+  if (t >= nblk * (nblk + 1) / 2) return;  // whole wave
+  int cb = (int)((sqrtf(8.0f * (float)t + 1.0f) - 1.0f) * 0.5f);
+  if (cb * (cb + 1) / 2 > t) --cb;  // float rounding guards (t < 528)
+  if ((cb + 1) * (cb + 2) / 2 <= t) ++cb;
+  const int rb = t - cb * (cb + 1) / 2;
   __shared__ float4 cbx[4][64];
   __shared__ float car[4][64];
   const float4* sb = g.sbox + (long)b * KCAP;
   const float* sa = g.sarea + (long)b * KCAP;
   const int i = rb * 64 + lane;
+  const int j = cb * 64 + lane;
   const float4 bi = (i < K) ? sb[i] : make_float4(0, 0, 0, 0);
   const float ai = (i < K) ? sa[i] : 0.f;
-  const int nblk = (K + 63) / 64;
+  // the wave's own LDS slice: written and read back by the same wave (in-order LDS), no barrier
+  cbx[wv][lane] = (j < K) ? sb[j] : make_float4(0, 0, 0, 0);
+  car[wv][lane] = (j < K) ? sa[j] : 0.f;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   const double thr = g.iou;
   const bool all_pairs = !(thr >= 0.0);
-  unsigned long long* mrow = g.mask + ((long)b * KCAP + i) * KW;
-  for (int cb0 = rb; cb0 < nblk; cb0 += 4) {
-    const int cb = cb0 + wv;
-    const int j = cb * 64 + lane;
-    if (cb < nblk) {
-      cbx[wv][lane] = (j < K) ? sb[j] : make_float4(0, 0, 0, 0);
-      car[wv][lane] = (j < K) ? sa[j] : 0.f;
-    }
-    __syncthreads();
-    if (cb < nblk) {
-      // every lane walks the same columns (uniform LDS addresses: broadcast reads, unrolled so several are in
-      // flight); the diagonal block keeps only columns q > lane
-      const int qhi = (K - cb * 64 < 64) ? K - cb * 64 : 64;
-      const float4* cx = cbx[wv];
-      const float* ca = car[wv];
-      unsigned long long bits = 0ull;
-      for (int q0 = 0; q0 < qhi; q0 += 8) {  // 8 columns' reads issued before the first test (q0 + 8 <= 64)
-        float4 bj[8];
-        float aj[8];
+  // every lane walks the same columns (uniform LDS addresses: broadcast reads, 8 in flight); the diagonal block
+  // keeps only columns q > lane
+  const int qhi = (K - cb * 64 < 64) ? K - cb * 64 : 64;
+  const float4* cx = cbx[wv];
+  const float* ca = car[wv];
+  unsigned long long bits = 0ull;
+  for (int q0 = 0; q0 < qhi; q0 += 8) {
+    float4 bj[8];
+    float aj[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          bj[u] = cx[q0 + u];
-          aj[u] = ca[q0 + u];
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-          if (iou_gt_sparse(bi, ai, bj[u], aj[u], thr, all_pairs)) bits |= 1ull << (q0 + u);
-      }
-      if (qhi < 64) bits &= (1ull << qhi) - 1ull;  // columns past K
-      if (cb == rb) bits &= (lane == 63) ? 0ull : (~0ull << (lane + 1));
-      if (i < K) mrow[cb] = bits;
+    for (int u = 0; u < 8; ++u) {
+      bj[u] = cx[q0 + u];
+      aj[u] = ca[q0 + u];
     }
-    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (iou_gt_sparse(bi, ai, bj[u], aj[u], thr, all_pairs)) bits |= 1ull << (q0 + u);
   }
+  if (qhi < 64) bits &= (1ull << qhi) - 1ull;  // columns past K
+  if (cb == rb) bits &= (lane == 63) ? 0ull : (~0ull << (lane + 1));
+  if (i < K) g.mask[((long)b * KCAP + i) * KW + cb] = bits;
 }
 
 // -------------------------------------------------------------------------------------------------
@@ -1054,7 +1058,7 @@ YS_EXPORT int yolosod_nms(float* pred, int B, int nc, int A, float conf_thres, d
     hipLaunchKernelGGL(nms_scatter_kernel, dim3(nblk_a, B), dim3(256), 0, st, g);
   }
   hipLaunchKernelGGL(nms_select_kernel, dim3(B), dim3(NMS_T), 0, st, g);
-  hipLaunchKernelGGL(nms_mask_kernel, dim3(KW, B), dim3(256), 0, st, g);
+  hipLaunchKernelGGL(nms_mask_kernel, dim3(KW * (KW + 1) / 8, B), dim3(256), 0, st, g);
   if (big)
     hipLaunchKernelGGL(nms_resolve_kernel<true>, dim3(B), dim3(NMS_T), 0, st, g);
   else
