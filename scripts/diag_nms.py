@@ -21,14 +21,14 @@ RES = ["prefix greedy", "rows out + fallback + pad"]
 def main():
     dev = torch.device("cuda")
     lib = _hip.load_library()
-    buf = (ctypes.c_ulonglong * (32 * 16))()
+    buf = (ctypes.c_ulonglong * (32 * 24))()
     for n in [int(a) for a in sys.argv[1:]] or [1000, 10000, 30000]:
         pred = loaded_predictions(32, 34000, 10, n, 50, 0.25, 0, dev)
         for _ in range(3):
             non_max_suppression_padded(pred.clone(), 0.25, 0.7, max_det=300)
         torch.cuda.synchronize()
         assert lib.yolosod_diag_nms_stamps(buf) == 0
-        a = np.frombuffer(buf, dtype=np.uint64).reshape(32, 16).astype(np.int64)
+        a = np.frombuffer(buf, dtype=np.uint64).reshape(32, 24).astype(np.int64)
         out = [f"n={n}:"]
         for i, name in enumerate(SEL):
             d = a[:, i + 1] - a[:, i]
@@ -37,6 +37,8 @@ def main():
         for i, name in enumerate(RES):
             d = a[:, 9 + i] - a[:, 8 + i]
             out.append(f"| {name} {np.median(d) / 1e3:.1f}k")
+        ps = [f"{np.median(a[:, 16 + d] - a[:, 2]) / 1e3:.1f}k" for d in (2, 1, 0) if np.median(a[:, 16 + d]) > 0]
+        out.append(f"| pass ends after key loads (digit 23:16, 15:8, 7:0): {' '.join(ps)}")
         out.append(f"| image 0: n {a[0, 11]} m {a[0, 12]} K {a[0, 13]} T {a[0, 14]:#x}")
         print(" ".join(out), "(kcycles of s_memtime)", flush=True)
 

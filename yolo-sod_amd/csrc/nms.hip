@@ -38,9 +38,9 @@ static_assert(KW == 32, "nms_resolve maps one 32-word mask row onto 32 threads")
 constexpr int RK = 72;      // keys per thread nms_select holds in registers: n <= NMS_T * RK (A = 34000 single-label)
 
 #ifdef YS_DIAG_STAMPS  // diagnostic builds only (scripts/diag_nms.sh): s_memtime of thread 0 at phase boundaries
-__device__ unsigned long long g_nms_stamps[32 * 16];
+__device__ unsigned long long g_nms_stamps[32 * 24];
 #define YS_NSTAMP(k) \
-  if (threadIdx.x == 0 && blockIdx.x < 32) g_nms_stamps[blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0 && blockIdx.x < 32) g_nms_stamps[blockIdx.x * 24 + (k)] = __builtin_amdgcn_s_memtime();
 #else
 #define YS_NSTAMP(k) ;  // a statement in both builds (never the body of an if)
 #endif
@@ -457,29 +457,20 @@ __global__ __launch_bounds__(NMS_T) void nms_select_kernel(NmsArgs g) {
     radix_sort_pairs(ks, ps, kd, pd, n, sh);
     m = n;
   } else if (n <= NMS_T * RK) {
-    // the same radix select with the keys held in registers (thread t: keys [t RK, t RK + RK)): one read of the
-    // keys instead of one per pass, and a single ordered compaction
-    const int base = tid * RK;
+    // the same radix select with the keys held in registers: one read of the keys instead of one per pass, and a
+    // single ordered compaction. Wave w holds keys [w RK 64, (w + 1) RK 64), lane l the keys w RK 64 + 64 u + l:
+    // each load instruction reads 64 consecutive keys (thread-contiguous runs of 72 keys made every 16-byte load
+    // touch 64 cache lines: 17 us of key loads at 30k candidates)
+    const int lane = tid & 63, wv = tid >> 6;
+    const int wbase = wv * RK * 64;
     unsigned kr[RK];
-    // every load unconditional (a clamped address; entries past n masked afterwards), so all of a thread's loads
+    // every load unconditional (a clamped index; entries past n masked afterwards), so all of a thread's loads
     // are in flight together (loads under a bounds branch were merged into phis that each waited for the memory)
-    if ((reinterpret_cast<uintptr_t>(kA) & 15u) == 0) {
-      // 16-byte loads; a chunk starting past n reads the last aligned chunk before n (inside the image's keys or,
-      // for the chunk ending past n, at most 3 entries beyond them: still workspace)
-      const int last = (n - 1) & ~3;
 #pragma unroll
-      for (int v = 0; v < RK / 4; ++v) {
-        const int i = base + 4 * v;
-        const uint4 q = *reinterpret_cast<const uint4*>(kA + (i < n ? i : last));
-        kr[4 * v] = q.x; kr[4 * v + 1] = q.y; kr[4 * v + 2] = q.z; kr[4 * v + 3] = q.w;
-      }
-    } else {
-#pragma unroll
-      for (int u = 0; u < RK; ++u) kr[u] = kA[min(base + u, n - 1)];
-    }
+    for (int u = 0; u < RK; ++u) kr[u] = kA[min(wbase + 64 * u + lane, n - 1)];
 #pragma unroll
     for (int u = 0; u < RK; ++u)
-      if (base + u >= n) kr[u] = 0xFFFFFFFFu;
+      if (wbase + 64 * u + lane >= n) kr[u] = 0xFFFFFFFFu;
     // digits above the highest bit in which two keys differ are common to all keys: their passes would find one
     // bucket holding all n (> KCAP) keys and only extend the prefix, so the select starts below them (the same T)
     // Entries past n hold 0xFFFFFFFF, the largest key: counted in the histograms they only add to the top bucket,
@@ -494,7 +485,7 @@ __global__ __launch_bounds__(NMS_T) void nms_select_kernel(NmsArgs g) {
       if (kr[u] != 0xFFFFFFFFu) kmax = max(kmax, kr[u]);
       nff += (kr[u] == 0xFFFFFFFFu) ? 1 : 0;
     }
-    if (nff > RK - max(0, min(RK, n - base))) kmax = 0xFFFFFFFFu;
+    if (nff > RK - max(0, min(RK, (n - wbase - lane + 63) / 64))) kmax = 0xFFFFFFFFu;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
       kmin = min(kmin, (unsigned)__shfl_xor((int)kmin, o, 64));
@@ -543,21 +534,36 @@ __global__ __launch_bounds__(NMS_T) void nms_select_kernel(NmsArgs g) {
         prefix = sel_prefix;
         pmask |= 255u << shift;
         __syncthreads();
+        YS_NSTAMP(16 + shift / 8)
       }
     }
     T = prefix;
     YS_NSTAMP(3)
-    int c = 0;
+    // ordered compaction of the keys < T: wave order is (u, lane), the waves' ranges follow each other
+    int wt = 0;
 #pragma unroll
-    for (int u = 0; u < RK; ++u) c += (kr[u] < T) ? 1 : 0;
-    int o = block_exclusive_scan(c, sh.wsum, &m);
+    for (int u = 0; u < RK; ++u) wt += __popcll(__ballot(kr[u] < T));
+    __shared__ int wtot[NMS_W];
+    if (lane == 0) wtot[wv] = wt;
+    __syncthreads();
+    int o = 0;
+    m = 0;
 #pragma unroll
-    for (int u = 0; u < RK; ++u)
-      if (kr[u] < T) {
-        lk[0][o] = kr[u];
-        lp[0][o] = (unsigned)(base + u);  // index into the compaction; its position is gathered below
-        ++o;
+    for (int w = 0; w < NMS_W; ++w) {
+      o += (w < wv) ? wtot[w] : 0;
+      m += wtot[w];
+    }
+#pragma unroll
+    for (int u = 0; u < RK; ++u) {
+      const bool take = kr[u] < T;
+      const unsigned long long bal = __ballot(take);
+      if (take) {
+        const int idx = o + __popcll(bal & lanemask_lt());
+        lk[0][idx] = kr[u];
+        lp[0][idx] = (unsigned)(wbase + 64 * u + lane);  // index into the compaction; its position is gathered below
       }
+      o += __popcll(bal);
+    }
     __syncthreads();
     for (int i = tid; i < m; i += NMS_T) lp[0][i] = pA[lp[0][i]];
     __syncthreads();
@@ -616,10 +622,10 @@ __global__ __launch_bounds__(NMS_T) void nms_select_kernel(NmsArgs g) {
   const int K = (m < neff) ? m : neff;
 #ifdef YS_DIAG_STAMPS
   if (tid == 0 && b < 32) {
-    g_nms_stamps[b * 16 + 11] = (unsigned)n;
-    g_nms_stamps[b * 16 + 12] = (unsigned)m;
-    g_nms_stamps[b * 16 + 13] = (unsigned)K;
-    g_nms_stamps[b * 16 + 14] = T;
+    g_nms_stamps[b * 24 + 11] = (unsigned)n;
+    g_nms_stamps[b * 24 + 12] = (unsigned)m;
+    g_nms_stamps[b * 24 + 13] = (unsigned)K;
+    g_nms_stamps[b * 24 + 14] = T;
   }
 #endif
   // prefix boxes with the class offset (ops.py:289,295), areas, ids
@@ -968,7 +974,7 @@ __global__ __launch_bounds__(NMS_T) void nms_resolve_kernel(NmsArgs g) {
 using namespace ys;
 
 #ifdef YS_DIAG_STAMPS
-YS_EXPORT int yolosod_diag_nms_stamps(unsigned long long* host) {  // [32][16] of the last call
+YS_EXPORT int yolosod_diag_nms_stamps(unsigned long long* host) {  // [32][24] of the last call
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_nms_stamps), sizeof(g_nms_stamps)) == hipSuccess ? 0 : -1;
 }
 #endif
