@@ -511,16 +511,23 @@ __global__ __launch_bounds__(NMS_T) void nms_select_kernel(NmsArgs g) {
       const int top = ((31 - __clz(diff)) / 8) * 8;  // shift of the digit holding the highest differing bit
       unsigned pmask = (top == 24) ? 0u : (0xFFFFFFFFu << (top + 8));
       prefix = kmin & pmask;
+      // 32 replicas of the histogram, replica r in LDS bank r: lane l adds into replica l & 31, so the 32 lanes an
+      // LDS atomic serves per cycle never share a bank. (One shared histogram: random digits over 256 bins put ~5
+      // lanes in one bank and each ds_add took ~100 cycles - 56k cycles for the first pass at 30k keys.)
+      __shared__ unsigned hrep[256 * 32];
       for (int shift = top; shift >= 0; shift -= 8) {
-        if (tid < 256) sh.hist[tid] = 0;
+        for (int e = tid; e < 256 * 32; e += NMS_T) hrep[e] = 0;
         __syncthreads();
-        // plain LDS atomics (below the common digits the keys' digits are spread; a skewed pass only costs LDS
-        // conflicts, while hist_add_digit's uniformity test cost more than the atomics over 72 keys per thread)
 #pragma unroll
         for (int u = 0; u < RK; ++u)
-          if ((kr[u] & pmask) == prefix) atomicAdd(&sh.hist[(kr[u] >> shift) & 255u], 1u);
+          if ((kr[u] & pmask) == prefix) atomicAdd(&hrep[(((kr[u] >> shift) & 255u) << 5) | (lane & 31)], 1u);
         __syncthreads();
-        const unsigned h = (tid < 256) ? sh.hist[tid] : 0u;
+        unsigned h = 0u;
+        if (tid < 256) {
+#pragma unroll
+          for (int r = 0; r < 32; ++r) h += hrep[(tid << 5) | ((r + tid) & 31)];  // rotated: conflict-free reads
+          sh.hist[tid] = h;
+        }
         scan256_exclusive(sh.hist, sh.tmp4);
         if (tid < 256) {
           const unsigned run = below + sh.hist[tid];
