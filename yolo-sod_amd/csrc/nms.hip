@@ -14,9 +14,10 @@
 //   nms_select  one 512-thread workgroup per image: the score order of the first <= KCAP candidates, sorted in
 //               LDS. For n <= KCAP a stable LSD radix sort of all; for n > KCAP a radix *select* first finds the
 //               key T such that the keys below T (at most KCAP of them) are exactly a prefix of the stable sorted
-//               order, and only that prefix is sorted. Writes the prefix's class-offset boxes / areas / ids.
-//   nms_mask    1024 workgroups (row block x image): the upper-triangular IoU > thr bitmask of the prefix, one
-//               64-bit word per (row, 64-column block) - the quadratic work spread over every CU.
+//               order (keys held in registers for n <= 36864, common digits skipped, bank-replicated histograms),
+//               and only that prefix is sorted. Writes the prefix's class-offset boxes / areas / ids.
+//   nms_mask    one wave per (row block, column block) pair of the upper triangle (528 equal tasks per image): the
+//               IoU > thr bitmask of the prefix, one 64-bit word per (row, 64-column block).
 //   nms_resolve one workgroup per image: greedy in score order over the bitmask, 64 rows staged in LDS at a time,
 //               only alive candidates visited (bit scan); stops at max_det. Only if the prefix is exhausted before
 //               max_det boxes are kept and more candidates exist (keys >= T) does it sort that remainder and
