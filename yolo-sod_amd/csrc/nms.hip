@@ -830,16 +830,18 @@ __global__ __launch_bounds__(NMS_T) void nms_resolve_kernel(NmsArgs g) {
       }
       __syncthreads();
       if (done_sh) break;
-      // kept rows of this block into the later words: thread (word w, group gq) ORs the kept rows whose rank
-      // among this block's kept rows is gq mod 16
+      // kept rows of this block into the later words: thread (word w, group gq) ORs the kept rows among rows gq,
+      // gq + 16, gq + 32, gq + 48 (four bit tests; walking every kept row of the block and taking every 16th cost up
+      // to 64 iterations per thread and block)
       {
         const int w = tid & 31, gq = tid >> 5;
         if (w > rb && w < nblk) {
-          unsigned long long km = keptm_sh, acc = 0ull;
-          for (int k = 0; km; ++k) {
-            const int q = __ffsll((long long)km) - 1;
-            km &= km - 1;
-            if ((k & 15) == gq) acc |= mrows[buf][q][w];
+          const unsigned long long km = keptm_sh;
+          unsigned long long acc = 0ull;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int q = gq + 16 * r;
+            if ((km >> q) & 1ull) acc |= mrows[buf][q][w];
           }
           if (acc) atomicOr(&rem_w[w], acc);
         }
