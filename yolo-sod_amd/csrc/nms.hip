@@ -51,6 +51,7 @@ struct NmsArgs {
   int B, nc, A;
   float conf;
   double iou;
+  float iou_f;     // the largest float <= iou: for a float ratio r, (double)r > iou <=> r > iou_f (no f64 compare)
   const int* classes;
   int n_classes;
   int agnostic, multi_label, max_det, max_nms, in_place;
@@ -241,20 +242,22 @@ __device__ int block_exclusive_scan(int v, int* wsum, int* total) {
   return ex;
 }
 
-__device__ __forceinline__ bool iou_gt(const float4 bi, float ai, const float4 bj, float aj, double thr) {
+// thr_f: the largest float <= the double threshold (NmsArgs::iou_f), so `ovr > thr_f` is exactly the reference's
+// `(double)ovr > thr` for every float ovr (NaN included) without an f64 conversion and compare
+__device__ __forceinline__ bool iou_gt(const float4 bi, float ai, const float4 bj, float aj, float thr_f) {
   // torchvision CPU nms_kernel: i = the earlier (kept) box, j = the later one
   const float xx1 = fmaxf(bi.x, bj.x), yy1 = fmaxf(bi.y, bj.y);
   const float xx2 = fminf(bi.z, bj.z), yy2 = fminf(bi.w, bj.w);
   const float w = fmaxf(0.0f, xx2 - xx1), h = fmaxf(0.0f, yy2 - yy1);
   const float inter = w * h;
   const float ovr = inter / ((ai + aj) - inter);
-  return (double)ovr > thr;
+  return ovr > thr_f;
 }
 
 // iou_gt with the division skipped where it cannot matter: inter is >= 0 or NaN (w, h >= 0), and with inter not
 // > 0 the ratio is +-0 or NaN, which is > thr for no thr >= 0 (the reference asserts 0 <= iou_thres). all_pairs
 // (thr < 0) keeps every division. Same operations in the same order as iou_gt where it divides: bit-identical.
-__device__ __forceinline__ bool iou_gt_sparse(const float4 bi, float ai, const float4 bj, float aj, double thr,
+__device__ __forceinline__ bool iou_gt_sparse(const float4 bi, float ai, const float4 bj, float aj, float thr_f,
                                               bool all_pairs) {
   const float xx1 = fmaxf(bi.x, bj.x), yy1 = fmaxf(bi.y, bj.y);
   const float xx2 = fminf(bi.z, bj.z), yy2 = fminf(bi.w, bj.w);
@@ -265,7 +268,7 @@ __device__ __forceinline__ bool iou_gt_sparse(const float4 bi, float ai, const f
   // in front of w, h and inter measured 24 % slower: one more divergent branch per pair)
   if (inter > 0.0f || all_pairs) {
     const float ovr = inter / ((ai + aj) - inter);
-    hit = (double)ovr > thr;
+    hit = ovr > thr_f;
   }
   return hit;
 }
@@ -695,8 +698,8 @@ __global__ __launch_bounds__(256) void nms_mask_kernel(NmsArgs g) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  const double thr = g.iou;
-  const bool all_pairs = !(thr >= 0.0);
+  const float thr_f = g.iou_f;
+  const bool all_pairs = !(g.iou >= 0.0);
   // every lane walks the same columns (uniform LDS addresses: broadcast reads, 8 in flight); the diagonal block
   // keeps only columns q > lane
   const int qhi = (K - cb * 64 < 64) ? K - cb * 64 : 64;
@@ -713,7 +716,7 @@ __global__ __launch_bounds__(256) void nms_mask_kernel(NmsArgs g) {
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u)
-      if (iou_gt_sparse(bi, ai, bj[u], aj[u], thr, all_pairs)) bits |= 1ull << (q0 + u);
+      if (iou_gt_sparse(bi, ai, bj[u], aj[u], thr_f, all_pairs)) bits |= 1ull << (q0 + u);
   }
   if (qhi < 64) bits &= (1ull << qhi) - 1ull;  // columns past K
   if (cb == rb) bits &= (lane == 63) ? 0ull : (~0ull << (lane + 1));
@@ -907,7 +910,7 @@ __global__ __launch_bounds__(NMS_T) void nms_resolve_kernel(NmsArgs g) {
       const int nk = nkept_sh;
       bool al = valid;
       for (int k = 0; k < nk && al; ++k)
-        if (iou_gt(kept_box[k], kept_area[k], obox, area, g.iou)) al = false;
+        if (iou_gt(kept_box[k], kept_area[k], obox, area, g.iou_f)) al = false;
       alive[tid] = al ? 1 : 0;
       const unsigned long long aw = __ballot(al);
       if (lane == 0) alive_w[wv] = aw;
@@ -918,7 +921,7 @@ __global__ __launch_bounds__(NMS_T) void nms_resolve_kernel(NmsArgs g) {
         if (al) {
           for (int q = 0; q < 64; ++q) {
             const int jj = wd * 64 + q;
-            if (jj > tid && alive[jj] && iou_gt(obox, area, cb[jj], ca[jj], g.iou)) bits |= 1ull << q;
+            if (jj > tid && alive[jj] && iou_gt(obox, area, cb[jj], ca[jj], g.iou_f)) bits |= 1ull << q;
           }
         }
         rows[tid][wd] = bits;
@@ -1037,6 +1040,11 @@ YS_EXPORT int yolosod_nms(float* pred, int B, int nc, int A, float conf_thres, d
   g.A = A;
   g.conf = conf_thres;
   g.iou = iou_thres;
+  {  // round toward -inf: the largest float <= iou_thres (NaN stays NaN: every comparison false, as in double)
+    float t = (float)iou_thres;
+    if ((double)t > iou_thres) t = nextafterf(t, -INFINITY);
+    g.iou_f = t;
+  }
   g.classes = (n_classes > 0) ? classes : nullptr;
   g.n_classes = n_classes;
   g.agnostic = agnostic;
