@@ -797,32 +797,41 @@ __global__ __launch_bounds__(NMS_T) void nms_resolve_kernel(NmsArgs g) {
         if (rb + 1 < nblk) store_block(buf ^ 1);
         if (rb + 2 < nblk) load_block(rb + 2);
       } else {
-        // lane q holds row q's bits inside this block (the diagonal word); the greedy is a scalar loop (cand, rem,
-        // keptm in SGPRs: the removed word is read back from LDS through readfirstlane so that the compiler knows
-        // it is wave-uniform; a VGPR loop condition made it a divergent VALU loop, ~5x slower)
+        // lane q holds row q's bits inside this block (the diagonal word). The block's greedy is the fixed point of
+        // kept = cand & ~OR_{j in kept} diag[j]: diag[j] only has bits above j, so the rows whose suppression
+        // chain is at most t long are settled after t rounds, and the fixed point is unique (= the sequential
+        // greedy). Each round is one wave-wide 64-bit OR; a few rounds replace a scalar loop of ~190 cycles per
+        // kept row (one wave issuing alone, readlane -> SALU dependencies). cand / kept / rem stay wave-uniform
+        // (readfirstlane), so the loop is scalar control flow.
         const unsigned long long diag = mrows[buf][lane][rb];
         const int rows_here = (K - rb * 64 < 64) ? K - rb * 64 : 64;
         const unsigned long long remv = rem_w[rb];
-        unsigned long long rem = ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(remv >> 32)) << 32) |
-                                 (unsigned)__builtin_amdgcn_readfirstlane((unsigned)remv);
-        unsigned long long cand = (rows_here == 64 ? ~0ull : ((1ull << rows_here) - 1ull)) & ~rem;
-        unsigned long long keptm = 0ull;
+        const unsigned long long rem =
+            ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(remv >> 32)) << 32) |
+            (unsigned)__builtin_amdgcn_readfirstlane((unsigned)remv);
+        const unsigned long long cand = (rows_here == 64 ? ~0ull : ((1ull << rows_here) - 1ull)) & ~rem;
+        unsigned long long keptm = cand;
+        for (int it = 0; it < 64; ++it) {
+          unsigned lo = ((keptm >> lane) & 1ull) ? (unsigned)diag : 0u;
+          unsigned hi = ((keptm >> lane) & 1ull) ? (unsigned)(diag >> 32) : 0u;
+#pragma unroll
+          for (int o = 1; o < 64; o <<= 1) {
+            lo |= (unsigned)__shfl_xor((int)lo, o, 64);
+            hi |= (unsigned)__shfl_xor((int)hi, o, 64);
+          }
+          const unsigned long long sup = ((unsigned long long)__builtin_amdgcn_readfirstlane(hi) << 32) |
+                                         (unsigned)__builtin_amdgcn_readfirstlane(lo);
+          const unsigned long long nk = cand & ~sup;
+          if (nk == keptm) break;
+          keptm = nk;
+        }
         const int nk0 = nkk;
         bool done = false;
-        while (cand) {
-          const int q = __builtin_ctzll(cand);
-          keptm |= 1ull << q;
-          ++nkk;
-          if (nkk >= g.max_det) {
-            done = true;
-            break;
-          }
-          const unsigned lo = __builtin_amdgcn_readlane((unsigned)diag, q);
-          const unsigned hi = __builtin_amdgcn_readlane((unsigned)(diag >> 32), q);
-          rem |= ((unsigned long long)hi << 32) | lo;
-          const unsigned long long upto = (q == 63) ? ~0ull : ((2ull << q) - 1ull);
-          cand &= ~upto & ~rem;
+        if (nkk + __popcll(keptm) >= g.max_det) {  // max_det reached inside this block: its first rows only
+          while (nkk + __popcll(keptm) > g.max_det) keptm &= ~(1ull << (63 - __builtin_clzll(keptm)));
+          done = true;
         }
+        nkk += __popcll(keptm);
         // the block's kept rows, in order, written by their own lanes
         if ((keptm >> lane) & 1ull) kept_t[nk0 + __popcll(keptm & lanemask_lt())] = rb * 64 + lane;
         if (lane == 0) {
