@@ -384,6 +384,74 @@ __device__ void radix_sort_pairs(unsigned*& ks, unsigned*& ps, unsigned*& kd, un
   __syncthreads();
 }
 
+// Stable LSD radix sort of n <= KCAP (key, pos) pairs in LDS, as radix_sort_pairs but one counting step per digit
+// pass: wave w owns pairs [256 w, 256 w + 256) (four rounds of 64 lanes, in index order), ranks each round's keys by
+// matching digits (8 ballots) on top of its running per-digit counts, and one prefix over the 8 waves per digit
+// (wave order = index order) gives every pair its destination. radix_sort_pairs works in 512-pair chunks, each with
+// its own four barriers and an 8-step serial prefix per digit (~32k cycles for 2048 pairs). Block-uniform.
+__device__ void radix_sort_lds(unsigned*& ks, unsigned*& ps, unsigned*& kd, unsigned*& pd, int n, SortShared& sh) {
+  static_assert(KCAP == NMS_W * 256, "one 256-pair range per wave");
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  for (int pass = 0; pass < 4 && n > 1; ++pass) {
+    const int shift = pass * 8;
+    for (int e = tid; e < NMS_W * 256; e += NMS_T) (&sh.wcnt[0][0])[e] = 0;
+    __syncthreads();
+    unsigned key[4], pos[4], dg[4];
+    int lr[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = wv * 256 + r * 64 + lane;
+      const bool valid = i < n;
+      key[r] = valid ? ks[i] : 0u;
+      pos[r] = valid ? ps[i] : 0u;
+      const unsigned d = (key[r] >> shift) & 255u;
+      dg[r] = d;
+      unsigned long long peers = __ballot(valid);
+#pragma unroll
+      for (int bt = 0; bt < 8; ++bt) {
+        const bool bit = (d >> bt) & 1u;
+        const unsigned long long bal = __ballot(bit);
+        peers &= bit ? bal : ~bal;
+      }
+      const unsigned long long lower = peers & lanemask_lt();
+      lr[r] = valid ? (int)sh.wcnt[wv][d] + __popcll(lower) : 0;  // the wave's earlier rounds + earlier lanes
+      // same-wave LDS accesses complete in order: every lane's read above precedes the leader's update
+      if (valid && lower == 0ull) sh.wcnt[wv][d] += (unsigned)__popcll(peers);
+    }
+    __syncthreads();
+    if (tid < 256) {  // per digit: exclusive offsets over the waves (index order), total into hist
+      unsigned run = 0;
+#pragma unroll
+      for (int w = 0; w < NMS_W; ++w) {
+        const unsigned c = sh.wcnt[w][tid];
+        sh.wcnt[w][tid] = run;
+        run += c;
+      }
+      sh.hist[tid] = run;
+    }
+    if (tid == 0) sh.flag = 0;
+    __syncthreads();
+    if (tid < 256 && sh.hist[tid] == (unsigned)n) sh.flag = 1;
+    __syncthreads();
+    if (sh.flag) continue;  // every key has the same digit: the pass is the identity
+    scan256_exclusive(sh.hist, sh.tmp4);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = wv * 256 + r * 64 + lane;
+      if (i < n) {
+        const unsigned dst = sh.hist[dg[r]] + sh.wcnt[wv][dg[r]] + (unsigned)lr[r];
+        kd[dst] = key[r];
+        pd[dst] = pos[r];
+      }
+    }
+    __syncthreads();
+    unsigned* t;
+    t = ks; ks = kd; kd = t;
+    t = ps; ps = pd; pd = t;
+  }
+  __syncthreads();
+}
+
 // Order-preserving compaction of the pairs whose key is < T (below) or >= T (!below) into (kd, pd); returns
 // the count. Block-uniform.
 __device__ int compact_by_key(const unsigned* ks, const unsigned* ps, int n, unsigned T, bool below, unsigned* kd,
@@ -458,7 +526,7 @@ __global__ __launch_bounds__(NMS_T) void nms_select_kernel(NmsArgs g) {
       lp[0][i] = pA[i];
     }
     ks = lk[0]; ps = lp[0]; kd = lk[1]; pd = lp[1];
-    radix_sort_pairs(ks, ps, kd, pd, n, sh);
+    radix_sort_lds(ks, ps, kd, pd, n, sh);
     m = n;
   } else if (n <= NMS_T * RK) {
     // the same radix select with the keys held in registers: one read of the keys instead of one per pass, and a
@@ -580,7 +648,7 @@ __global__ __launch_bounds__(NMS_T) void nms_select_kernel(NmsArgs g) {
     __syncthreads();
     YS_NSTAMP(4)
     ks = lk[0]; ps = lp[0]; kd = lk[1]; pd = lp[1];
-    radix_sort_pairs(ks, ps, kd, pd, m, sh);
+    radix_sort_lds(ks, ps, kd, pd, m, sh);
   } else {
     // radix select, MSB first: the key T with #(key < T) <= KCAP, taking whole digit buckets while they fit
     unsigned prefix = 0u, pmask = 0u;
@@ -627,7 +695,7 @@ __global__ __launch_bounds__(NMS_T) void nms_select_kernel(NmsArgs g) {
     m = compact_by_key(kA, pA, n, T, true, lk[0], lp[0], sh);
     __syncthreads();
     ks = lk[0]; ps = lp[0]; kd = lk[1]; pd = lp[1];
-    radix_sort_pairs(ks, ps, kd, pd, m, sh);
+    radix_sort_lds(ks, ps, kd, pd, m, sh);
   }
   YS_NSTAMP(5)
   const int K = (m < neff) ? m : neff;
