@@ -93,16 +93,14 @@ __global__ __launch_bounds__(256) void nms_prep_kernel(NmsArgs g) {
   if (a < g.A) {
     float* pb = g.pred + (long)b * (4 + g.nc) * g.A + a;
     const long As = g.A;
-    // up to 16 class scores loaded before the box (the in-place box stores below could alias later score loads, so
-    // the compiler kept every load behind them) and unconditionally (class index clamped; classes past nc skipped)
+    // the class scores first (up to 16 loaded unconditionally, class index clamped; classes past nc skipped), then
+    // the box: every anchor's when the reference's in-place xyxy rewrite is asked for, else only a candidate's (the
+    // predictor's call: an empty image reads its scores only, 10 of the 14 rows)
     float s16[16];
     if (g.nc <= 16) {
 #pragma unroll
       for (int u = 0; u < 16; ++u) s16[u] = pb[(4 + (u < g.nc ? u : g.nc - 1)) * As];
     }
-    const float cx = pb[0], cy = pb[As], w = pb[2 * As], h = pb[3 * As];
-    const float hw = w / 2.0f, hh = h / 2.0f;
-    const float x1 = cx - hw, y1 = cy - hh, x2 = cx + hw, y2 = cy + hh;
     float best = -INFINITY;
     int bj = 0;
     if (g.nc <= 16) {
@@ -118,13 +116,6 @@ __global__ __launch_bounds__(256) void nms_prep_kernel(NmsArgs g) {
         }
       }
     }
-    if (g.in_place) {
-      pb[0] = x1;
-      pb[As] = y1;
-      pb[2 * As] = x2;
-      pb[3 * As] = y2;
-    }
-    box = make_float4(x1, y1, x2, y2);
     for (int j0 = 0; g.nc > 16 && j0 < g.nc; j0 += 8) {  // 8 score loads in flight, then scanned in class order
       float sv[8];
 #pragma unroll
@@ -150,6 +141,18 @@ __global__ __launch_bounds__(256) void nms_prep_kernel(NmsArgs g) {
         if (c >= 0 && c < 64) allow |= 1ull << c;
       }
       mask &= allow;
+    }
+    if (g.in_place || mask) {
+      const float cx = pb[0], cy = pb[As], w = pb[2 * As], h = pb[3 * As];
+      const float hw = w / 2.0f, hh = h / 2.0f;
+      const float x1 = cx - hw, y1 = cy - hh, x2 = cx + hw, y2 = cy + hh;
+      if (g.in_place) {
+        pb[0] = x1;
+        pb[As] = y1;
+        pb[2 * As] = x2;
+        pb[3 * As] = y2;
+      }
+      box = make_float4(x1, y1, x2, y2);
     }
   }
   int total;
