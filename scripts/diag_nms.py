@@ -18,12 +18,20 @@ SEL = ["count scan", "to key loads", "radix select (regs)", "compaction + pos ga
 RES = ["prefix greedy", "rows out + fallback + pad"]
 
 
+CLUSTERS = 50
+
+
 def main():
+    global CLUSTERS
+    if "--clusters" in sys.argv:
+        k = sys.argv.index("--clusters")
+        CLUSTERS = int(sys.argv[k + 1])
+        del sys.argv[k:k + 2]
     dev = torch.device("cuda")
     lib = _hip.load_library()
     buf = (ctypes.c_ulonglong * (32 * 24))()
     for n in [int(a) for a in sys.argv[1:]] or [1000, 10000, 30000]:
-        pred = loaded_predictions(32, 34000, 10, n, 50, 0.25, 0, dev)
+        pred = loaded_predictions(32, 34000, 10, n, CLUSTERS, 0.25, 0, dev)
         for _ in range(3):
             non_max_suppression_padded(pred.clone(), 0.25, 0.7, max_det=300)
         torch.cuda.synchronize()
@@ -39,6 +47,9 @@ def main():
             out.append(f"| {name} {np.median(d) / 1e3:.1f}k")
         ps = [f"{np.median(a[:, 16 + d] - a[:, 2]) / 1e3:.1f}k" for d in (2, 1, 0) if np.median(a[:, 16 + d]) > 0]
         out.append(f"| pass ends after key loads (digit 23:16, 15:8, 7:0): {' '.join(ps)}")
+        out.append(f"| fallback rem {np.median(a[:, 19]):.0f} chunks {np.median(a[:, 23]):.0f}: kept-test "
+                   f"{np.median(a[:, 20]) / 1e3:.1f}k, chunk mask {np.median(a[:, 21]) / 1e3:.1f}k, greedy "
+                   f"{np.median(a[:, 22]) / 1e3:.1f}k")
         out.append(f"| image 0: n {a[0, 11]} m {a[0, 12]} K {a[0, 13]} T {a[0, 14]:#x}")
         print(" ".join(out), "(kcycles of s_memtime)", flush=True)
 

@@ -970,8 +970,31 @@ __global__ __launch_bounds__(NMS_T) void nms_resolve_kernel(NmsArgs g) {
     const int m = compact_by_key(kA, pA, n, T, false, kB, pB, sh);
     __syncthreads();
     unsigned *ks = kB, *ps = pB, *kd = kA, *pd = pA;
-    radix_sort_pairs(ks, ps, kd, pd, m, sh);
+    __shared__ unsigned rk[2][KCAP], rp[2][KCAP];
+    if (m <= KCAP) {  // a remainder of up to 2048 candidates is sorted in LDS (the global-memory sort: ~0.3 ms)
+      for (int i = tid; i < m; i += NMS_T) {
+        rk[0][i] = kB[i];
+        rp[0][i] = pB[i];
+      }
+      __syncthreads();
+      ks = rk[0]; ps = rp[0]; kd = rk[1]; pd = rp[1];
+      radix_sort_lds(ks, ps, kd, pd, m, sh);
+    } else {
+      radix_sort_pairs(ks, ps, kd, pd, m, sh);
+    }
     const int rem = (m < neff - K) ? m : neff - K;
+#ifdef YS_DIAG_STAMPS
+    unsigned long long f_t0 = __builtin_amdgcn_s_memtime(), f_t1, f_keep = 0, f_mask = 0, f_greedy = 0, f_out = 0;
+    int f_chunks = 0;
+    if (threadIdx.x == 0 && blockIdx.x < 32) g_nms_stamps[blockIdx.x * 24 + 19] = (unsigned long long)rem;
+#define YS_FACC(acc) f_t1 = __builtin_amdgcn_s_memtime(); acc += f_t1 - f_t0; f_t0 = f_t1;
+#else
+#define YS_FACC(acc)
+#endif
+#ifdef YS_DIAG_STAMPS
+    YS_FACC(f_out)
+    f_out = 0;
+#endif
     for (int c0 = 0; c0 < rem; c0 += NMS_T) {
       const int i = c0 + tid;
       const bool valid = i < rem;
@@ -988,25 +1011,57 @@ __global__ __launch_bounds__(NMS_T) void nms_resolve_kernel(NmsArgs g) {
       cb[tid] = obox;
       ca[tid] = area;
       const int nk = nkept_sh;
+      const bool all_pairs = !(g.iou >= 0.0);
+      // against the kept list: 8 kept boxes read per step (uniform LDS addresses, all in flight), the wave leaves
+      // the loop once none of its candidates is alive (a per-lane exit made every LDS read wait on its own)
       bool al = valid;
-      for (int k = 0; k < nk && al; ++k)
-        if (iou_gt(kept_box[k], kept_area[k], obox, area, g.iou_f)) al = false;
+      for (int k0 = 0; k0 < nk; k0 += 8) {
+        if (__ballot(al) == 0ull) break;
+        float4 kb[8];
+        float ka[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int k = (k0 + u < nk) ? k0 + u : nk - 1;
+          kb[u] = kept_box[k];
+          ka[u] = kept_area[k];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (k0 + u < nk && iou_gt_sparse(kb[u], ka[u], obox, area, g.iou_f, all_pairs)) al = false;
+      }
       alive[tid] = al ? 1 : 0;
       const unsigned long long aw = __ballot(al);
       if (lane == 0) alive_w[wv] = aw;
       __syncthreads();
+      YS_FACC(f_keep)
+      // the chunk's own IoU bits: only words at or after the wave's own (later candidates) and only words with an
+      // alive candidate (the others stay 0: the greedy reads bits of alive candidates only)
 #pragma unroll
       for (int wd = 0; wd < NMS_T / 64; ++wd) {
         unsigned long long bits = 0ull;
-        if (al) {
-          for (int q = 0; q < 64; ++q) {
-            const int jj = wd * 64 + q;
-            if (jj > tid && alive[jj] && iou_gt(obox, area, cb[jj], ca[jj], g.iou_f)) bits |= 1ull << q;
+        const unsigned long long awd = alive_w[wd];
+        if (wd >= wv && awd != 0ull && __ballot(al) != 0ull) {
+          for (int q0 = 0; q0 < 64; q0 += 8) {  // 8 candidates' reads in flight (uniform addresses)
+            float4 jb[8];
+            float ja[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+              jb[u] = cb[wd * 64 + q0 + u];
+              ja[u] = ca[wd * 64 + q0 + u];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+              const int q = q0 + u, jj = wd * 64 + q;
+              if (al && jj > tid && ((awd >> q) & 1ull) &&
+                  iou_gt_sparse(obox, area, jb[u], ja[u], g.iou_f, all_pairs))
+                bits |= 1ull << q;
+            }
           }
         }
         rows[tid][wd] = bits;
       }
       __syncthreads();
+      YS_FACC(f_mask)
       if (wv == 0) {
         unsigned long long removed = 0ull;
         int nkk = nk;
@@ -1037,6 +1092,7 @@ __global__ __launch_bounds__(NMS_T) void nms_resolve_kernel(NmsArgs g) {
         }
       }
       __syncthreads();
+      YS_FACC(f_greedy)
       const int nk_new = nkept_sh;
       for (int k = nk + tid; k < nk_new; k += NMS_T) {
         const unsigned p = ps[kept_t[k]];
@@ -1048,8 +1104,21 @@ __global__ __launch_bounds__(NMS_T) void nms_resolve_kernel(NmsArgs g) {
         o[5] = (float)j;
         oi[k] = (int)a;
       }
+      YS_FACC(f_out)
+#ifdef YS_DIAG_STAMPS
+      ++f_chunks;
+#endif
       if (done_sh) break;
     }
+#ifdef YS_DIAG_STAMPS
+    if (threadIdx.x == 0 && blockIdx.x < 32) {
+      g_nms_stamps[blockIdx.x * 24 + 20] = f_keep;
+      g_nms_stamps[blockIdx.x * 24 + 21] = f_mask;
+      g_nms_stamps[blockIdx.x * 24 + 22] = f_greedy;
+      g_nms_stamps[blockIdx.x * 24 + 23] = f_chunks;
+    }
+#endif
+#undef YS_FACC
   }
   __syncthreads();
   const int nk = nkept_sh;
