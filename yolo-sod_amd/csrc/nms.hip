@@ -325,10 +325,53 @@ struct SortShared {
   unsigned tmp4[4];
 };
 
+// One stable scatter of n (key, pos) pairs by the 8-bit digit at `shift` from (ks, ps) to (kd, pd), 512 pairs per
+// step; sh.hist holds the digit's exclusive prefix on entry (the digit's end offsets on return). Block-uniform.
+__device__ void radix_scatter(const unsigned* ks, const unsigned* ps, unsigned* kd, unsigned* pd, int n, int shift,
+                              SortShared& sh) {
+  const int tid = threadIdx.x, wv = tid >> 6;
+  for (int t0 = 0; t0 < n; t0 += NMS_T) {
+    for (int e = tid; e < NMS_W * 256; e += NMS_T) (&sh.wcnt[0][0])[e] = 0;
+    __syncthreads();
+    const int i = t0 + tid;
+    const bool valid = i < n;
+    const unsigned key = valid ? ks[i] : 0u;
+    const unsigned pos = valid ? ps[i] : 0u;
+    const unsigned d = (key >> shift) & 255u;
+    unsigned long long peers = __ballot(valid);
+#pragma unroll
+    for (int bt = 0; bt < 8; ++bt) {
+      const bool bit = (d >> bt) & 1u;
+      const unsigned long long bal = __ballot(bit);
+      peers &= bit ? bal : ~bal;
+    }
+    const unsigned long long lower = peers & lanemask_lt();
+    const int rank = __popcll(lower);
+    if (valid && lower == 0ull) sh.wcnt[wv][d] = (unsigned)__popcll(peers);
+    __syncthreads();
+    if (tid < 256) {
+      unsigned run = sh.hist[tid];
+      for (int w = 0; w < NMS_W; ++w) {
+        const unsigned c = sh.wcnt[w][tid];
+        sh.wcnt[w][tid] = run;
+        run += c;
+      }
+      sh.hist[tid] = run;
+    }
+    __syncthreads();
+    if (valid) {
+      const unsigned dst = sh.wcnt[wv][d] + rank;
+      kd[dst] = key;
+      pd[dst] = pos;
+    }
+    __syncthreads();
+  }
+}
+
 // Stable LSD radix sort (4 x 8-bit digits, ascending) of n (key, pos) pairs, ping-ponging between (ks, ps) and
 // (kd, pd); on return (ks, ps) hold the sorted pairs. Passes whose digit is uniform are skipped. Block-uniform.
-__device__ void radix_sort_pairs(unsigned*& ks, unsigned*& ps, unsigned*& kd, unsigned*& pd, int n, SortShared& sh) {
-  const int tid = threadIdx.x, wv = tid >> 6;
+__device__ __forceinline__ void radix_sort_pairs(unsigned*& ks, unsigned*& ps, unsigned*& kd, unsigned*& pd, int n, SortShared& sh) {
+  const int tid = threadIdx.x;
   for (int pass = 0; pass < 4 && n > 1; ++pass) {
     const int shift = pass * 8;
     __syncthreads();  // previous pass fully done with hist / flag
@@ -344,42 +387,7 @@ __device__ void radix_sort_pairs(unsigned*& ks, unsigned*& ps, unsigned*& kd, un
     __syncthreads();
     if (sh.flag) continue;  // every key has the same digit: the pass is the identity
     scan256_exclusive(sh.hist, sh.tmp4);
-    for (int t0 = 0; t0 < n; t0 += NMS_T) {
-      for (int e = tid; e < NMS_W * 256; e += NMS_T) (&sh.wcnt[0][0])[e] = 0;
-      __syncthreads();
-      const int i = t0 + tid;
-      const bool valid = i < n;
-      const unsigned key = valid ? ks[i] : 0u;
-      const unsigned pos = valid ? ps[i] : 0u;
-      const unsigned d = (key >> shift) & 255u;
-      unsigned long long peers = __ballot(valid);
-#pragma unroll
-      for (int bt = 0; bt < 8; ++bt) {
-        const bool bit = (d >> bt) & 1u;
-        const unsigned long long bal = __ballot(bit);
-        peers &= bit ? bal : ~bal;
-      }
-      const unsigned long long lower = peers & lanemask_lt();
-      const int rank = __popcll(lower);
-      if (valid && lower == 0ull) sh.wcnt[wv][d] = (unsigned)__popcll(peers);
-      __syncthreads();
-      if (tid < 256) {
-        unsigned run = sh.hist[tid];
-        for (int w = 0; w < NMS_W; ++w) {
-          const unsigned c = sh.wcnt[w][tid];
-          sh.wcnt[w][tid] = run;
-          run += c;
-        }
-        sh.hist[tid] = run;
-      }
-      __syncthreads();
-      if (valid) {
-        const unsigned dst = sh.wcnt[wv][d] + rank;
-        kd[dst] = key;
-        pd[dst] = pos;
-      }
-      __syncthreads();
-    }
+    radix_scatter(ks, ps, kd, pd, n, shift, sh);
     unsigned* t;
     t = ks; ks = kd; kd = t;
     t = ps; ps = pd; pd = t;
@@ -392,7 +400,7 @@ __device__ void radix_sort_pairs(unsigned*& ks, unsigned*& ps, unsigned*& kd, un
 // matching digits (8 ballots) on top of its running per-digit counts, and one prefix over the 8 waves per digit
 // (wave order = index order) gives every pair its destination. radix_sort_pairs works in 512-pair chunks, each with
 // its own four barriers and an 8-step serial prefix per digit (~32k cycles for 2048 pairs). Block-uniform.
-__device__ void radix_sort_lds(unsigned*& ks, unsigned*& ps, unsigned*& kd, unsigned*& pd, int n, SortShared& sh) {
+__device__ __forceinline__ void radix_sort_lds(unsigned*& ks, unsigned*& ps, unsigned*& kd, unsigned*& pd, int n, SortShared& sh) {
   static_assert(KCAP == NMS_W * 256, "one 256-pair range per wave");
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   for (int pass = 0; pass < 4 && n > 1; ++pass) {
@@ -457,8 +465,9 @@ __device__ void radix_sort_lds(unsigned*& ks, unsigned*& ps, unsigned*& kd, unsi
 
 // Order-preserving compaction of the pairs whose key is < T (below) or >= T (!below) into (kd, pd); returns
 // the count. Block-uniform.
-__device__ int compact_by_key(const unsigned* ks, const unsigned* ps, int n, unsigned T, bool below, unsigned* kd,
-                              unsigned* pd, SortShared& sh) {
+__device__ int compact_range(const unsigned* ks, const unsigned* ps, int n, unsigned lo, unsigned long long hi,
+                             unsigned* kd, unsigned* pd, SortShared& sh) {
+  // order-preserving compaction of the pairs with lo <= key < hi (hi up to 2^32)
   constexpr int CPT = 4;
   const int tid = threadIdx.x;
   int m = 0;
@@ -471,7 +480,7 @@ __device__ int compact_by_key(const unsigned* ks, const unsigned* ps, int n, uns
       const bool v = i0 + u < n;
       k[u] = v ? ks[i0 + u] : 0u;
       p[u] = v ? ps[i0 + u] : 0u;
-      const bool take = v && ((k[u] < T) == below);
+      const bool take = v && k[u] >= lo && (unsigned long long)k[u] < hi;
       c += take ? 1 : 0;
       if (!take) k[u] = 0u, p[u] = 0xFFFFFFFFu;
     }
@@ -488,6 +497,11 @@ __device__ int compact_by_key(const unsigned* ks, const unsigned* ps, int n, uns
     m += total;
   }
   return m;
+}
+
+__device__ int compact_by_key(const unsigned* ks, const unsigned* ps, int n, unsigned T, bool below, unsigned* kd,
+                              unsigned* pd, SortShared& sh) {
+  return below ? compact_range(ks, ps, n, 0u, T, kd, pd, sh) : compact_range(ks, ps, n, T, 1ull << 32, kd, pd, sh);
 }
 
 // -------------------------------------------------------------------------------------------------
@@ -969,24 +983,11 @@ __global__ __launch_bounds__(NMS_T) void nms_resolve_kernel(NmsArgs g) {
     unsigned* pB = g.posB + (long)b * g.cap;
     const int m = compact_by_key(kA, pA, n, T, false, kB, pB, sh);
     __syncthreads();
-    unsigned *ks = kB, *ps = pB, *kd = kA, *pd = pA;
-    __shared__ unsigned rk[2][KCAP], rp[2][KCAP];
-    if (m <= KCAP) {  // a remainder of up to 2048 candidates is sorted in LDS (the global-memory sort: ~0.3 ms)
-      for (int i = tid; i < m; i += NMS_T) {
-        rk[0][i] = kB[i];
-        rp[0][i] = pB[i];
-      }
-      __syncthreads();
-      ks = rk[0]; ps = rp[0]; kd = rk[1]; pd = rp[1];
-      radix_sort_lds(ks, ps, kd, pd, m, sh);
-    } else {
-      radix_sort_pairs(ks, ps, kd, pd, m, sh);
-    }
-    const int rem = (m < neff - K) ? m : neff - K;
+    const int cap_total = (m < neff - K) ? m : neff - K;  // max_nms
 #ifdef YS_DIAG_STAMPS
     unsigned long long f_t0 = __builtin_amdgcn_s_memtime(), f_t1, f_keep = 0, f_mask = 0, f_greedy = 0, f_out = 0;
     int f_chunks = 0;
-    if (threadIdx.x == 0 && blockIdx.x < 32) g_nms_stamps[blockIdx.x * 24 + 19] = (unsigned long long)rem;
+    if (threadIdx.x == 0 && blockIdx.x < 32) g_nms_stamps[blockIdx.x * 24 + 19] = (unsigned long long)cap_total;
 #define YS_FACC(acc) f_t1 = __builtin_amdgcn_s_memtime(); acc += f_t1 - f_t0; f_t0 = f_t1;
 #else
 #define YS_FACC(acc)
@@ -995,120 +996,214 @@ __global__ __launch_bounds__(NMS_T) void nms_resolve_kernel(NmsArgs g) {
     YS_FACC(f_out)
     f_out = 0;
 #endif
-    for (int c0 = 0; c0 < rem; c0 += NMS_T) {
-      const int i = c0 + tid;
-      const bool valid = i < rem;
-      float4 obox = make_float4(0, 0, 0, 0);
-      float area = 0.f;
-      if (valid) {
-        const unsigned pos = ps[i];
-        const unsigned a = pos / nc, j = pos % nc;
-        const float4 bb = bx[a];
-        const float off = g.agnostic ? 0.0f : (float)j * g.max_wh;
-        obox = make_float4(bb.x + off, bb.y + off, bb.z + off, bb.w + off);
-        area = (obox.z - obox.x) * (obox.w - obox.y);
-      }
-      cb[tid] = obox;
-      ca[tid] = area;
-      const int nk = nkept_sh;
-      const bool all_pairs = !(g.iou >= 0.0);
-      // against the kept list: 8 kept boxes read per step (uniform LDS addresses, all in flight), the wave leaves
-      // the loop once none of its candidates is alive (a per-lane exit made every LDS read wait on its own)
-      bool al = valid;
-      for (int k0 = 0; k0 < nk; k0 += 8) {
-        if (__ballot(al) == 0ull) break;
-        float4 kb[8];
-        float ka[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int k = (k0 + u < nk) ? k0 + u : nk - 1;
-          kb[u] = kept_box[k];
-          ka[u] = kept_area[k];
+    // the remainder's candidates [0, cnt) in score order (positions ps_r): chunks of 512 against the kept list, then
+    // their own IoU bits and greedy; stops at max_det
+    auto run_chunks = [&](const unsigned* ps_r, int cnt) __attribute__((always_inline)) {
+      for (int c0 = 0; c0 < cnt; c0 += NMS_T) {
+        const int i = c0 + tid;
+        const bool valid = i < cnt;
+        float4 obox = make_float4(0, 0, 0, 0);
+        float area = 0.f;
+        if (valid) {
+          const unsigned pos = ps_r[i];
+          const unsigned a = pos / nc, j = pos % nc;
+          const float4 bb = bx[a];
+          const float off = g.agnostic ? 0.0f : (float)j * g.max_wh;
+          obox = make_float4(bb.x + off, bb.y + off, bb.z + off, bb.w + off);
+          area = (obox.z - obox.x) * (obox.w - obox.y);
         }
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-          if (k0 + u < nk && iou_gt_sparse(kb[u], ka[u], obox, area, g.iou_f, all_pairs)) al = false;
-      }
-      alive[tid] = al ? 1 : 0;
-      const unsigned long long aw = __ballot(al);
-      if (lane == 0) alive_w[wv] = aw;
-      __syncthreads();
-      YS_FACC(f_keep)
-      // the chunk's own IoU bits: only words at or after the wave's own (later candidates) and only words with an
-      // alive candidate (the others stay 0: the greedy reads bits of alive candidates only)
-#pragma unroll
-      for (int wd = 0; wd < NMS_T / 64; ++wd) {
-        unsigned long long bits = 0ull;
-        const unsigned long long awd = alive_w[wd];
-        if (wd >= wv && awd != 0ull && __ballot(al) != 0ull) {
-          for (int q0 = 0; q0 < 64; q0 += 8) {  // 8 candidates' reads in flight (uniform addresses)
-            float4 jb[8];
-            float ja[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-              jb[u] = cb[wd * 64 + q0 + u];
-              ja[u] = ca[wd * 64 + q0 + u];
-            }
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-              const int q = q0 + u, jj = wd * 64 + q;
-              if (al && jj > tid && ((awd >> q) & 1ull) &&
-                  iou_gt_sparse(obox, area, jb[u], ja[u], g.iou_f, all_pairs))
-                bits |= 1ull << q;
+        cb[tid] = obox;
+        ca[tid] = area;
+        const int nk = nkept_sh;
+        const bool all_pairs = !(g.iou >= 0.0);
+        // against the kept list: 8 kept boxes read per step (uniform LDS addresses, all in flight), the wave leaves
+        // the loop once none of its candidates is alive (a per-lane exit made every LDS read wait on its own)
+        bool al = valid;
+        for (int k0 = 0; k0 < nk; k0 += 8) {
+          if (__ballot(al) == 0ull) break;
+          float4 kb[8];
+          float ka[8];
+  #pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const int k = (k0 + u < nk) ? k0 + u : nk - 1;
+            kb[u] = kept_box[k];
+            ka[u] = kept_area[k];
+          }
+  #pragma unroll
+          for (int u = 0; u < 8; ++u)
+            if (k0 + u < nk && iou_gt_sparse(kb[u], ka[u], obox, area, g.iou_f, all_pairs)) al = false;
+        }
+        alive[tid] = al ? 1 : 0;
+        const unsigned long long aw = __ballot(al);
+        if (lane == 0) alive_w[wv] = aw;
+        __syncthreads();
+        YS_FACC(f_keep)
+        // the chunk's own IoU bits: only words at or after the wave's own (later candidates) and only words with an
+        // alive candidate (the others stay 0: the greedy reads bits of alive candidates only)
+  #pragma unroll
+        for (int wd = 0; wd < NMS_T / 64; ++wd) {
+          unsigned long long bits = 0ull;
+          const unsigned long long awd = alive_w[wd];
+          if (wd >= wv && awd != 0ull && __ballot(al) != 0ull) {
+            for (int q0 = 0; q0 < 64; q0 += 8) {  // 8 candidates' reads in flight (uniform addresses)
+              float4 jb[8];
+              float ja[8];
+  #pragma unroll
+              for (int u = 0; u < 8; ++u) {
+                jb[u] = cb[wd * 64 + q0 + u];
+                ja[u] = ca[wd * 64 + q0 + u];
+              }
+  #pragma unroll
+              for (int u = 0; u < 8; ++u) {
+                const int q = q0 + u, jj = wd * 64 + q;
+                if (al && jj > tid && ((awd >> q) & 1ull) &&
+                    iou_gt_sparse(obox, area, jb[u], ja[u], g.iou_f, all_pairs))
+                  bits |= 1ull << q;
+              }
             }
           }
+          rows[tid][wd] = bits;
         }
-        rows[tid][wd] = bits;
-      }
-      __syncthreads();
-      YS_FACC(f_mask)
-      if (wv == 0) {
-        unsigned long long removed = 0ull;
-        int nkk = nk;
-        bool done = false;
-        for (int w = 0; w < NMS_T / 64 && !done; ++w) {
-          unsigned long long cand = alive_w[w] & ~__shfl(removed, w, 64);
-          while (cand) {
-            const int q = __ffsll((long long)cand) - 1;
-            const int t = w * 64 + q;
-            if (lane == 0) {
-              kept_box[nkk] = cb[t];
-              kept_area[nkk] = ca[t];
-              kept_t[nkk] = c0 + t;  // remainder index
+        __syncthreads();
+        YS_FACC(f_mask)
+        if (wv == 0) {
+          unsigned long long removed = 0ull;
+          int nkk = nk;
+          bool done = false;
+          for (int w = 0; w < NMS_T / 64 && !done; ++w) {
+            unsigned long long cand = alive_w[w] & ~__shfl(removed, w, 64);
+            while (cand) {
+              const int q = __ffsll((long long)cand) - 1;
+              const int t = w * 64 + q;
+              if (lane == 0) {
+                kept_box[nkk] = cb[t];
+                kept_area[nkk] = ca[t];
+                kept_t[nkk] = c0 + t;  // remainder index
+              }
+              ++nkk;
+              if (nkk >= g.max_det) {
+                done = true;
+                break;
+              }
+              if (lane < NMS_T / 64) removed |= rows[t][lane];
+              const unsigned long long upto = (q == 63) ? ~0ull : ((2ull << q) - 1ull);
+              cand &= ~upto & ~__shfl(removed, w, 64);
             }
-            ++nkk;
-            if (nkk >= g.max_det) {
-              done = true;
-              break;
-            }
-            if (lane < NMS_T / 64) removed |= rows[t][lane];
-            const unsigned long long upto = (q == 63) ? ~0ull : ((2ull << q) - 1ull);
-            cand &= ~upto & ~__shfl(removed, w, 64);
+          }
+          if (lane == 0) {
+            nkept_sh = nkk;
+            done_sh = done ? 1 : 0;
           }
         }
-        if (lane == 0) {
-          nkept_sh = nkk;
-          done_sh = done ? 1 : 0;
+        __syncthreads();
+        YS_FACC(f_greedy)
+        const int nk_new = nkept_sh;
+        for (int k = nk + tid; k < nk_new; k += NMS_T) {
+          const unsigned p = ps_r[kept_t[k]];
+          const unsigned a = p / nc, j = p % nc;
+          const float4 bb = bx[a];
+          float* o = ob + (long)k * 6;
+          o[0] = bb.x; o[1] = bb.y; o[2] = bb.z; o[3] = bb.w;
+          o[4] = pb[(long)(4 + j) * A + a];
+          o[5] = (float)j;
+          oi[k] = (int)a;
         }
+        YS_FACC(f_out)
+  #ifdef YS_DIAG_STAMPS
+        ++f_chunks;
+  #endif
+        if (done_sh) break;
+      }
+    };
+    // The remainder is consumed in rounds of at most KCAP candidates (a greedy that reaches max_det early reads
+    // only the first rounds; sorting the whole remainder in global memory cost ~0.34 ms at 28k keys): buckets of the
+    // 8 key bits from the highest one in which the remainder keys differ (one stable scatter pass puts them in bucket order), as many
+    // whole buckets per round as fit, each round copied into LDS and sorted there. A single bucket above KCAP (e.g.
+    // equal scores) sorts everything from that bucket on in global memory.
+    __shared__ unsigned rk[2][KCAP], rp[2][KCAP];
+    __shared__ unsigned rmin, rmax;
+    __shared__ unsigned rbase[256];
+    __shared__ int rnd_d2;
+    if (m <= KCAP) {
+      for (int i = tid; i < m; i += NMS_T) {
+        rk[0][i] = kB[i];
+        rp[0][i] = pB[i];
       }
       __syncthreads();
-      YS_FACC(f_greedy)
-      const int nk_new = nkept_sh;
-      for (int k = nk + tid; k < nk_new; k += NMS_T) {
-        const unsigned p = ps[kept_t[k]];
-        const unsigned a = p / nc, j = p % nc;
-        const float4 bb = bx[a];
-        float* o = ob + (long)k * 6;
-        o[0] = bb.x; o[1] = bb.y; o[2] = bb.z; o[3] = bb.w;
-        o[4] = pb[(long)(4 + j) * A + a];
-        o[5] = (float)j;
-        oi[k] = (int)a;
+      unsigned *ks = rk[0], *ps = rp[0], *kd = rk[1], *pd = rp[1];
+      radix_sort_lds(ks, ps, kd, pd, m, sh);
+      run_chunks(ps, cap_total);
+    } else {
+      if (tid == 0) {
+        rmin = 0xFFFFFFFFu;
+        rmax = 0u;
       }
-      YS_FACC(f_out)
-#ifdef YS_DIAG_STAMPS
-      ++f_chunks;
-#endif
-      if (done_sh) break;
+      __syncthreads();
+      unsigned kmn = 0xFFFFFFFFu, kmx = 0u;
+      for (int i = tid; i < m; i += NMS_T) {
+        const unsigned k = kB[i];
+        kmn = min(kmn, k);
+        kmx = max(kmx, k);
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        kmn = min(kmn, (unsigned)__shfl_xor((int)kmn, o, 64));
+        kmx = max(kmx, (unsigned)__shfl_xor((int)kmx, o, 64));
+      }
+      if (lane == 0) {
+        atomicMin(&rmin, kmn);
+        atomicMax(&rmax, kmx);
+      }
+      if (tid < 256) sh.hist[tid] = 0;
+      __syncthreads();
+      const unsigned diffk = rmin ^ rmax;
+      const int shiftB = diffk ? max(31 - __clz(diffk) - 7, 0) : 0;  // the 8 bits from the highest differing one
+      for (int i0 = 0; i0 < m; i0 += NMS_T) {
+        const int i = i0 + tid;
+        hist_add_digit(sh.hist, (i < m) ? (kB[i] >> shiftB) & 255u : 0u, i < m);
+      }
+      __syncthreads();
+      scan256_exclusive(sh.hist, sh.tmp4);
+      if (tid < 256) rbase[tid] = sh.hist[tid];  // keys in buckets < d (the sorts below reuse sh.hist)
+      radix_scatter(kB, pB, kA, pA, m, shiftB, sh);  // bucket d = [rbase[d], rbase[d + 1]) of (kA, pA)
+      __syncthreads();
+      int d = 0, processed = 0;
+      bool full = false;
+      while (processed < cap_total && !done_sh) {
+        if (tid == 0) rnd_d2 = d;
+        __syncthreads();
+        if (tid < 256 && tid + 1 > d) {  // candidate end t = tid + 1 in (d, 256]
+          const int t = tid + 1;
+          const unsigned et = (t < 256) ? rbase[t] : (unsigned)m;
+          if (et - rbase[d] <= (unsigned)KCAP) atomicMax(&rnd_d2, t);
+        }
+        __syncthreads();
+        const int d2 = rnd_d2;
+        if (d2 == d) {
+          full = true;
+          break;
+        }
+        const int s0 = (int)rbase[d];
+        const int cnt = ((d2 < 256) ? (int)rbase[d2] : m) - s0;
+        for (int i = tid; i < cnt; i += NMS_T) {
+          rk[0][i] = kA[s0 + i];
+          rp[0][i] = pA[s0 + i];
+        }
+        __syncthreads();
+        unsigned *ks = rk[0], *ps = rp[0], *kd = rk[1], *pd = rp[1];
+        radix_sort_lds(ks, ps, kd, pd, cnt, sh);
+        run_chunks(ps, min(cnt, cap_total - processed));
+        __syncthreads();
+        processed += cnt;
+        d = d2;
+      }
+      if (full && processed < cap_total && !done_sh) {
+        const int s0 = (int)rbase[d];
+        const int cnt = m - s0;
+        unsigned *ks = kA + s0, *ps = pA + s0, *kd = kB + s0, *pd = pB + s0;
+        radix_sort_pairs(ks, ps, kd, pd, cnt, sh);
+        run_chunks(ps, min(cnt, cap_total - processed));
+      }
     }
 #ifdef YS_DIAG_STAMPS
     if (threadIdx.x == 0 && blockIdx.x < 32) {
