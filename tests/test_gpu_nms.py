@@ -81,6 +81,32 @@ def test_nms_full_size_ties_vs_oracle(B, A, clusters, kw, cuda):
         assert np.array_equal(index[b, :counts[b]], idx[b]), b
 
 
+@pytest.mark.parametrize("kw", [
+    dict(conf_thres=0.25, iou_thres=0.7),
+    dict(conf_thres=0.25, iou_thres=0.45, multi_label=True, max_det=600),
+])
+def test_nms_remainder_class_lists_out_of_band(kw, cuda):
+    """Three clusters (the remainder path past the 2048-row prefix), 40 % of the boxes moved across x = max_wh (7680)
+    and 10 % to negative x: boxes outside their class's x band overlap boxes of the next class in the reference's
+    offset space (cross-class suppression), which any class-partitioned shortcut of the remainder's kept-list test
+    would have to handle. Must equal the all-pairs reference."""
+    B, A = 2, 34000
+    pred = recipes.synthetic_predictions(3131, B, A, 10, n_clusters=3)
+    rng = np.random.default_rng(9)
+    for b in range(B):
+        u = rng.uniform(0, 1, A)
+        pred[b, 0, u < 0.4] += 7680.0 - 320.0
+        pred[b, 0, (u >= 0.4) & (u < 0.5)] -= 640.0
+    p_after, out, counts, index = _run_gpu(pred, cuda, **kw)
+    ref = pred.copy()
+    rows, idx = non_max_suppression_ref(ref, **kw)
+    assert np.array_equal(p_after, ref)
+    assert counts.tolist() == [len(r) for r in rows]
+    for b in range(B):
+        assert np.array_equal(out[b, :counts[b]], rows[b]), b
+        assert np.array_equal(index[b, :counts[b]], idx[b]), b
+
+
 @pytest.mark.parametrize("mode", ["all_equal", "low_byte", "low_byte_multi"])
 def test_nms_prefix_select_shared_key_digits(mode, cuda):
     """The top-KCAP select skips the key digits all candidates share: 5000 candidates per image whose scores are all
